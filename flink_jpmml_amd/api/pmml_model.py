@@ -1,0 +1,199 @@
+"""``PmmlModel``: the model handle user UDFs receive (`S/api/PmmlModel.scala:43-176`).
+
+Per-record API (reference parity)::
+
+    prediction = model.predict(DenseVector(1, 1, 1, 1), replace_nan=None)   # Prediction(Score(3.0))
+
+runs ``validate → prepare → evaluate → extract`` under a Try and never raises for a bad record
+(`S/api/PmmlModel.scala:109-119`). The per-record path evaluates on the host in float64 — it is
+the semantic reference.
+
+Batch API (the MI355X path)::
+
+    scores, valid = model.predict_batch(X, device="cuda")     # X: [rows, active fields]
+
+prepares and scores a whole micro-batch with the HIP kernels; ``valid[i] == False`` is exactly
+the case where ``predict`` would return ``EmptyScore``.
+"""
+
+from __future__ import annotations
+
+import math
+from typing import Any, Dict, List, Optional, Sequence
+
+import numpy as np
+
+from ..domain.prediction import Prediction, Score, EmptyScore
+from .converter import PmmlInput, vector_conversion
+from .evaluator import EMPTY_EVALUATOR, Evaluator
+from .exceptions import InputValidationException, JPMMLExtractionException
+from .pipeline import FieldValue, Pipeline
+from .reader import ModelReader
+from .vectors import Vector, as_vector, pack_vectors
+
+
+class PmmlModel(Pipeline):
+    def __init__(self, evaluator: Evaluator):
+        self.evaluator = evaluator
+
+    # ------------------------------------------------------------------ factories
+    @staticmethod
+    def from_reader(reader: ModelReader) -> "PmmlModel":
+        """Read + parse + build the evaluator (`S/api/PmmlModel.scala:53-58`). Errors propagate;
+        operators wrap them into :class:`ModelLoadingException`."""
+        from ..runtime.compiled import CompiledPmml
+
+        text = reader.build_distributed_path()
+        return PmmlModel(Evaluator.apply(CompiledPmml.from_string(text, source=reader.source_path)))
+
+    @staticmethod
+    def from_path(path: str) -> "PmmlModel":
+        return PmmlModel.from_reader(ModelReader(path))
+
+    @staticmethod
+    def from_string(text: str) -> "PmmlModel":
+        from ..runtime.compiled import CompiledPmml
+
+        return PmmlModel(Evaluator.apply(CompiledPmml.from_string(text)))
+
+    @staticmethod
+    def empty() -> "PmmlModel":
+        return PmmlModel(EMPTY_EVALUATOR)
+
+    fromReader = from_reader  # noqa: N815
+
+    # ------------------------------------------------------------------ properties
+    @property
+    def compiled(self):
+        return self.evaluator.model
+
+    @property
+    def model_name(self) -> Optional[str]:
+        return self.evaluator.model.model_name
+
+    modelName = model_name  # noqa: N815
+
+    @property
+    def active_fields(self) -> List[str]:
+        return list(self.evaluator.model.active_fields)
+
+    @property
+    def is_empty(self) -> bool:
+        return self.evaluator is EMPTY_EVALUATOR
+
+    # ------------------------------------------------------------------ per-record pipeline
+    def predict(self, input_vector: Any, replace_nan: Optional[float] = None) -> Prediction:
+        def run() -> float:
+            validated = self.validate_input(input_vector)
+            prepared = self.prepare_input(validated, replace_nan)
+            result = self.evaluate_input(prepared)
+            return self.extract_target(result)
+
+        return Prediction.extract_prediction(run)
+
+    def validate_input(self, v: Any) -> PmmlInput:
+        """Size check against the active fields, then vector → map (`S/api/PmmlModel.scala:127-134`)."""
+        model = self.evaluator.model
+        vec: Vector = as_vector(v)
+        size = len(model.active_fields)
+        if vec.size != size:
+            raise InputValidationException(f"input vector {vec!r} size {vec.size} is not conform to model size {size}")
+        return vector_conversion(vec, self.evaluator)
+
+    def prepare_input(self, input_map: PmmlInput, replace_nan: Optional[float] = None) -> Dict[str, FieldValue]:
+        """Per-field preparation (`S/api/PmmlModel.scala:143-152`): absent values take
+        ``replace_nan`` (if given) else PMML missing-value handling."""
+        compiled = self.evaluator.model
+        schema = compiled.schema
+        out: Dict[str, FieldValue] = {}
+        for name in compiled.active_fields:
+            raw = input_map.get(name)
+            if raw is None and replace_nan is not None:
+                raw = replace_nan
+            try:
+                enc = schema.prepare_value(name, raw, compiled.mining_fields.get(name))
+                df = schema.data_fields.get(name)
+                fv = FieldValue(schema.decode(name, enc), enc, df.data_type if df else None, df.optype if df else None)
+                outcome: Any = fv
+            except Exception as e:  # noqa: BLE001 - any failure becomes InputPreparationException
+                outcome = e
+            k, fv = self.prepare_and_emit(outcome, name)
+            out[k] = fv
+        return out
+
+    def evaluate_input(self, prepared: Dict[str, FieldValue]) -> Dict[str, Any]:
+        """Evaluate one prepared record; returns ``{target fields..., output fields...}`` decoded."""
+        compiled = self.evaluator.model
+        row = np.array([[prepared[name].encoded if name in prepared else math.nan
+                         for name in compiled.active_fields]], dtype=np.float64)
+        res, outs = compiled.evaluate_prepared(row)
+        result: Dict[str, Any] = {}
+        labels = res.label_strings()
+        for tf in compiled.target_fields:
+            if not res.valid[0]:
+                result[tf] = None
+            elif res.kind == "regression":
+                result[tf] = float(res.value[0])
+            else:
+                result[tf] = labels[0]
+        for k, v in outs.items():
+            result[k] = compiled.schema.decode(k, float(v[0]))
+        return result
+
+    def extract_target(self, evaluation_result: Dict[str, Any]) -> float:
+        """First named target → double, else :class:`JPMMLExtractionException`
+        (`S/api/PmmlModel.scala:167-174`)."""
+        targets = self.extract_target_fields(evaluation_result)
+        if targets:
+            v = self.extract_target_value(targets[0][1])
+            if v is not None:
+                return v
+        raise JPMMLExtractionException("Target value is null.")
+
+    def outputs_of(self, evaluation_result: Dict[str, Any]) -> Dict[str, Any]:
+        return dict(self.extract_output_fields(evaluation_result))
+
+    def predict_with_outputs(self, input_vector: Any, replace_nan: Optional[float] = None) -> Prediction:
+        """Like :meth:`predict` but also returns the PMML ``<Output>`` fields in
+        ``Prediction.outputs`` (the reference extracts and drops them)."""
+        try:
+            validated = self.validate_input(input_vector)
+            prepared = self.prepare_input(validated, replace_nan)
+            result = self.evaluate_input(prepared)
+            target = self.extract_target(result)
+        except Exception as e:  # noqa: BLE001
+            return Prediction.on_failed_prediction(e)
+        return Prediction(Score(target), self.outputs_of(result))
+
+    # Scala-style aliases
+    validateInput = validate_input  # noqa: N815
+    prepareInput = prepare_input  # noqa: N815
+    evaluateInput = evaluate_input  # noqa: N815
+    extractTarget = extract_target  # noqa: N815
+
+    # ------------------------------------------------------------------ batch API
+    def predict_batch(self, X: Any, replace_nan: Optional[float] = None, device: Any = None, **opts):
+        """Score a ``[rows, active_fields]`` matrix (numpy or torch; NaN = missing) or a sequence
+        of vectors. Returns ``(scores, valid)``; numpy on host, torch tensors on device."""
+        compiled = self.evaluator.model
+        if isinstance(X, (list, tuple)) and X and isinstance(as_vector(X[0]), Vector) and not np.isscalar(X[0]):
+            return self.predict_vectors(X, replace_nan, device, **opts)
+        return compiled.score_matrix(X, replace_nan=replace_nan, device=device, **opts)
+
+    def predict_vectors(self, vectors: Sequence[Any], replace_nan: Optional[float] = None, device: Any = None,
+                        **opts) -> List[Prediction]:
+        """Batch version of :meth:`predict` over vector objects → list of :class:`Prediction`."""
+        compiled = self.evaluator.model
+        width = len(compiled.active_fields)
+        vs = [as_vector(v) for v in vectors]
+        ok_size = np.array([v.size == width for v in vs], dtype=bool)
+        X = pack_vectors([v if o else np.full(width, np.nan) for v, o in zip(vs, ok_size)], width)
+        scores, valid = compiled.score_matrix(X, replace_nan=replace_nan, device=device, **opts)
+        if not isinstance(scores, np.ndarray):
+            scores = scores.detach().cpu().numpy()
+            valid = valid.detach().cpu().numpy()
+        valid = np.asarray(valid, dtype=bool) & ok_size
+        return [Prediction(Score(float(s))) if v else Prediction(EmptyScore) for s, v in zip(scores, valid)]
+
+    def __repr__(self) -> str:
+        return f"PmmlModel({self.evaluator!r})"

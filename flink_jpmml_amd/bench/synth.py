@@ -1,0 +1,310 @@
+"""Synthetic PMML model + data generators for the benchmark configs of ``BASELINE.json``.
+
+No network, no checkpoints: every model is random-initialised with the *structure* of the named
+exporter and written as a PMML document, then loaded back through the normal parser, so the
+benchmark measures the real load → compile → score path.
+
+* :func:`gbdt_pmml` — XGBoost-style (JPMML-XGBoost layout) gradient-boosted trees:
+  ``MiningModel(sum)`` of binary ``TreeModel``s with ``defaultChild`` missing routing, float
+  fields, base score in ``Targets/@rescaleConstant``; ``objective="binary"`` adds the
+  ``modelChain`` → ``RegressionModel(logit)`` calibrator (config 5).
+* :func:`random_forest_pmml` — scikit-learn-style ``majorityVote`` forest (config 3).
+* :func:`iris_logistic_pmml` — multinomial logistic regression on Iris (config 1).
+* :func:`mlp_pmml` — 3-layer ``NeuralNetwork`` (config 4).
+* :func:`svm_pmml` — RBF ``SupportVectorMachineModel``.
+* :func:`stream_matrix` — the synthetic record stream (fp32, optional missing values).
+"""
+
+from __future__ import annotations
+
+import io
+from typing import List, Optional, Tuple
+
+import numpy as np
+
+NS = "http://www.dmg.org/PMML-4_4"
+
+
+def _header(out: io.StringIO, desc: str) -> None:
+    out.write(f'<?xml version="1.0" encoding="UTF-8"?>\n<PMML version="4.4" xmlns="{NS}">\n')
+    out.write(f' <Header description="{desc}"><Application name="flink_jpmml_amd.bench.synth" version="1"/></Header>\n')
+
+
+def _fnum(x: float) -> str:
+    return repr(float(np.float32(x)))
+
+
+class _TreeGen:
+    def __init__(self, rng: np.random.Generator, n_features: int, depth: int, p_split: float,
+                 thresholds: np.ndarray):
+        self.rng = rng
+        self.F = n_features
+        self.depth = depth
+        self.p_split = p_split
+        self.thr = thresholds
+        self.next_id = 0
+
+    def nid(self) -> int:
+        self.next_id += 1
+        return self.next_id
+
+    def write(self, out: io.StringIO, depth: int, pred: str, leaf_fn, indent: str, force_split: bool = False) -> None:
+        my = self.nid()
+        split = depth < self.depth and (force_split or self.rng.random() < self.p_split)
+        if not split:
+            out.write(f'{indent}<Node id="{my}" score="{leaf_fn()}">{pred}</Node>\n')
+            return
+        f = int(self.rng.integers(self.F))
+        t = _fnum(self.thr[f, int(self.rng.integers(self.thr.shape[1]))])
+        left_id = self.next_id + 1  # ids are assigned depth-first: the left child is next
+        go_left = bool(self.rng.random() < 0.5)
+        # write children into a buffer first to learn the right child's id
+        buf = io.StringIO()
+        self.write(buf, depth + 1, f'<SimplePredicate field="f{f}" operator="lessThan" value="{t}"/>', leaf_fn,
+                   indent + " ")
+        right_id = self.next_id + 1
+        self.write(buf, depth + 1, f'<SimplePredicate field="f{f}" operator="greaterOrEqual" value="{t}"/>', leaf_fn,
+                   indent + " ")
+        dflt = left_id if go_left else right_id
+        out.write(f'{indent}<Node id="{my}" defaultChild="{dflt}">{pred}\n')
+        out.write(buf.getvalue())
+        out.write(f'{indent}</Node>\n')
+
+
+def _data_dictionary(out: io.StringIO, F: int, target: str, target_type: str = "double",
+                     categories: Optional[List[str]] = None) -> None:
+    out.write(f' <DataDictionary numberOfFields="{F + 1}">\n')
+    for j in range(F):
+        out.write(f'  <DataField name="f{j}" optype="continuous" dataType="float"/>\n')
+    if categories is None:
+        out.write(f'  <DataField name="{target}" optype="continuous" dataType="{target_type}"/>\n')
+    else:
+        out.write(f'  <DataField name="{target}" optype="categorical" dataType="{target_type}">\n')
+        for c in categories:
+            out.write(f'   <Value value="{c}"/>\n')
+        out.write('  </DataField>\n')
+    out.write(' </DataDictionary>\n')
+
+
+def _mining_schema(out: io.StringIO, F: int, target: Optional[str], indent: str = "  ") -> None:
+    out.write(f'{indent}<MiningSchema>\n')
+    if target is not None:
+        out.write(f'{indent} <MiningField name="{target}" usageType="target"/>\n')
+    for j in range(F):
+        out.write(f'{indent} <MiningField name="f{j}"/>\n')
+    out.write(f'{indent}</MiningSchema>\n')
+
+
+def gbdt_pmml(n_trees: int = 1000, depth: int = 6, n_features: int = 32, seed: int = 0,
+              objective: str = "regression", p_split: float = 0.9, learning_rate: float = 0.1,
+              base_score: float = 0.5) -> str:
+    """XGBoost-style GBDT PMML (regression or binary:logistic chain)."""
+    rng = np.random.default_rng(seed)
+    thresholds = np.sort(rng.standard_normal((n_features, 64)).astype(np.float32), axis=1)
+    out = io.StringIO()
+    _header(out, f"synthetic GBDT {n_trees} trees depth {depth} ({objective})")
+    binary = objective == "binary"
+    _data_dictionary(out, n_features, "y", "integer" if binary else "double", ["0", "1"] if binary else None)
+
+    def leaf() -> str:
+        return _fnum(learning_rate * rng.standard_normal())
+
+    def trees_model(indent: str, target_in_schema: bool, rescale: float) -> None:
+        out.write(f'{indent}<MiningModel functionName="regression">\n')
+        _mining_schema(out, n_features, None if not target_in_schema else "y", indent + " ")
+        if binary:
+            out.write(f'{indent} <Output><OutputField name="xgbValue" optype="continuous" dataType="float" '
+                      f'isFinalResult="false"/></Output>\n')
+        out.write(f'{indent} <Targets><Target rescaleConstant="{_fnum(rescale)}"/></Targets>\n')
+        out.write(f'{indent} <Segmentation multipleModelMethod="sum">\n')
+        for t in range(n_trees):
+            g = _TreeGen(rng, n_features, depth, p_split, thresholds)
+            out.write(f'{indent}  <Segment id="{t + 1}"><True/>\n')
+            out.write(f'{indent}   <TreeModel functionName="regression" missingValueStrategy="defaultChild" '
+                      f'noTrueChildStrategy="returnLastPrediction" splitCharacteristic="binarySplit">\n')
+            _mining_schema(out, n_features, None, indent + "    ")
+            g.write(out, 0, "<True/>", leaf, indent + "    ", force_split=True)
+            out.write(f'{indent}   </TreeModel>\n{indent}  </Segment>\n')
+        out.write(f'{indent} </Segmentation>\n{indent}</MiningModel>\n')
+
+    if not binary:
+        out.write(' <MiningModel functionName="regression" algorithmName="XGBoost (GBTree)">\n')
+        _mining_schema(out, n_features, "y", "  ")
+        out.write(f'  <Targets><Target field="y" rescaleConstant="{_fnum(base_score)}"/></Targets>\n')
+        out.write('  <Segmentation multipleModelMethod="sum">\n')
+        for t in range(n_trees):
+            g = _TreeGen(rng, n_features, depth, p_split, thresholds)
+            out.write(f'   <Segment id="{t + 1}"><True/>\n')
+            out.write('    <TreeModel functionName="regression" missingValueStrategy="defaultChild" '
+                      'noTrueChildStrategy="returnLastPrediction" splitCharacteristic="binarySplit">\n')
+            _mining_schema(out, n_features, None, "     ")
+            g.write(out, 0, "<True/>", leaf, "     ", force_split=True)
+            out.write('    </TreeModel>\n   </Segment>\n')
+        out.write('  </Segmentation>\n </MiningModel>\n</PMML>\n')
+        return out.getvalue()
+    out.write(' <MiningModel functionName="classification" algorithmName="XGBoost (GBTree)">\n')
+    _mining_schema(out, n_features, "y", "  ")
+    out.write('  <Segmentation multipleModelMethod="modelChain">\n')
+    out.write('   <Segment id="1"><True/>\n')
+    trees_model("    ", False, float(np.log(base_score / (1 - base_score))))
+    out.write('   </Segment>\n   <Segment id="2"><True/>\n')
+    out.write('    <RegressionModel functionName="classification" normalizationMethod="logit">\n')
+    out.write('     <MiningSchema><MiningField name="y" usageType="target"/>'
+              '<MiningField name="xgbValue"/></MiningSchema>\n')
+    out.write('     <RegressionTable intercept="0.0" targetCategory="1">'
+              '<NumericPredictor name="xgbValue" coefficient="1.0"/></RegressionTable>\n')
+    out.write('     <RegressionTable intercept="0.0" targetCategory="0"/>\n')
+    out.write('    </RegressionModel>\n   </Segment>\n  </Segmentation>\n </MiningModel>\n</PMML>\n')
+    return out.getvalue()
+
+
+def random_forest_pmml(n_trees: int = 500, depth: int = 8, n_features: int = 32, n_classes: int = 3,
+                       seed: int = 0, p_split: float = 0.85) -> str:
+    """scikit-learn-style majority-vote random forest (classification trees, ``none`` missing
+    strategy with a ``True`` second child)."""
+    rng = np.random.default_rng(seed)
+    thresholds = np.sort(rng.standard_normal((n_features, 64)).astype(np.float32), axis=1)
+    cats = [str(c) for c in range(n_classes)]
+    out = io.StringIO()
+    _header(out, f"synthetic random forest {n_trees} trees depth {depth}")
+    _data_dictionary(out, n_features, "y", "integer", cats)
+    out.write(' <MiningModel functionName="classification" algorithmName="sklearn RandomForest">\n')
+    _mining_schema(out, n_features, "y", "  ")
+    out.write('  <Segmentation multipleModelMethod="majorityVote">\n')
+    for t in range(n_trees):
+        g = _TreeGen(rng, n_features, depth, p_split, thresholds)
+        out.write(f'   <Segment id="{t + 1}"><True/>\n')
+        out.write('    <TreeModel functionName="classification" missingValueStrategy="defaultChild" '
+                  'splitCharacteristic="binarySplit">\n')
+        _mining_schema(out, n_features, "y", "     ")
+        g.write(out, 0, "<True/>", lambda: cats[int(rng.integers(n_classes))], "     ", force_split=True)
+        out.write('    </TreeModel>\n   </Segment>\n')
+    out.write('  </Segmentation>\n </MiningModel>\n</PMML>\n')
+    return out.getvalue()
+
+
+def iris_logistic_pmml() -> str:
+    """Multinomial logistic regression on the four Iris features (softmax over 3 tables)."""
+    fields = ["sepal_length", "sepal_width", "petal_length", "petal_width"]
+    coefs = {
+        "Iris-setosa": (9.85, [-0.42, 0.97, -2.52, -1.08]),
+        "Iris-versicolor": (2.24, [0.53, -0.32, -0.21, -0.94]),
+        "Iris-virginica": (-12.09, [-0.11, -0.65, 2.73, 2.02]),
+    }
+    out = io.StringIO()
+    _header(out, "Iris multinomial logistic regression")
+    out.write(' <DataDictionary numberOfFields="5">\n')
+    for f in fields:
+        out.write(f'  <DataField name="{f}" optype="continuous" dataType="double"/>\n')
+    out.write('  <DataField name="species" optype="categorical" dataType="string">\n')
+    for c in coefs:
+        out.write(f'   <Value value="{c}"/>\n')
+    out.write('  </DataField>\n </DataDictionary>\n')
+    out.write(' <RegressionModel functionName="classification" normalizationMethod="softmax" modelName="iris_lr">\n')
+    out.write('  <MiningSchema><MiningField name="species" usageType="target"/>')
+    for f in fields:
+        out.write(f'<MiningField name="{f}"/>')
+    out.write('</MiningSchema>\n')
+    out.write('  <Output>')
+    for c in coefs:
+        out.write(f'<OutputField name="probability({c})" optype="continuous" dataType="double" '
+                  f'feature="probability" value="{c}"/>')
+    out.write('</Output>\n')
+    for c, (b, w) in coefs.items():
+        out.write(f'  <RegressionTable intercept="{b}" targetCategory="{c}">')
+        for f, x in zip(fields, w):
+            out.write(f'<NumericPredictor name="{f}" coefficient="{x}"/>')
+        out.write('</RegressionTable>\n')
+    out.write(' </RegressionModel>\n</PMML>\n')
+    return out.getvalue()
+
+
+def mlp_pmml(n_features: int = 64, hidden: Tuple[int, ...] = (256, 256), n_out: int = 1, seed: int = 0,
+             activation: str = "rectifier", classification: bool = False) -> str:
+    """3-layer NeuralNetwork (``hidden`` layers + output layer), NormContinuous inputs."""
+    rng = np.random.default_rng(seed)
+    out = io.StringIO()
+    _header(out, f"synthetic MLP {n_features}-{'-'.join(map(str, hidden))}-{n_out}")
+    cats = [str(c) for c in range(n_out)] if classification else None
+    _data_dictionary(out, n_features, "y", "integer" if classification else "double", cats)
+    fn = "classification" if classification else "regression"
+    out.write(f' <NeuralNetwork functionName="{fn}" activationFunction="{activation}">\n')
+    _mining_schema(out, n_features, "y", "  ")
+    out.write('  <NeuralInputs>\n')
+    for j in range(n_features):
+        mu, sd = rng.standard_normal() * 0.1, 1.0 + 0.1 * rng.random()
+        out.write(f'   <NeuralInput id="i{j}"><DerivedField optype="continuous" dataType="double">'
+                  f'<NormContinuous field="f{j}"><LinearNorm orig="{mu - sd:.6f}" norm="-1"/>'
+                  f'<LinearNorm orig="{mu + sd:.6f}" norm="1"/></NormContinuous></DerivedField></NeuralInput>\n')
+    out.write('  </NeuralInputs>\n')
+    prev = [f"i{j}" for j in range(n_features)]
+    dims = list(hidden) + [n_out]
+    for li, width in enumerate(dims):
+        last = li == len(dims) - 1
+        attrs = ""
+        if last:
+            attrs = ' activationFunction="identity"' + (' normalizationMethod="softmax"' if classification else "")
+        out.write(f'  <NeuralLayer{attrs}>\n')
+        scale = 1.0 / np.sqrt(len(prev))
+        W = rng.standard_normal((width, len(prev))) * scale
+        b = rng.standard_normal(width) * 0.05
+        ids = []
+        for k in range(width):
+            nid = f"n{li}_{k}"
+            ids.append(nid)
+            out.write(f'   <Neuron id="{nid}" bias="{b[k]:.7g}">')
+            out.write("".join(f'<Con from="{p}" weight="{W[k, j]:.7g}"/>' for j, p in enumerate(prev)))
+            out.write('</Neuron>\n')
+        out.write('  </NeuralLayer>\n')
+        prev = ids
+    out.write('  <NeuralOutputs>\n')
+    for k, nid in enumerate(prev):
+        if classification:
+            ex = f'<NormDiscrete field="y" value="{k}"/>'
+        else:
+            ex = '<FieldRef field="y"/>'
+        out.write(f'   <NeuralOutput outputNeuron="{nid}"><DerivedField optype="continuous" dataType="double">'
+                  f'{ex}</DerivedField></NeuralOutput>\n')
+    out.write('  </NeuralOutputs>\n </NeuralNetwork>\n</PMML>\n')
+    return out.getvalue()
+
+
+def svm_pmml(n_features: int = 16, n_sv: int = 256, seed: int = 0, kernel: str = "radialBasis",
+             classification: bool = True, gamma: float = 0.05) -> str:
+    rng = np.random.default_rng(seed)
+    out = io.StringIO()
+    _header(out, f"synthetic SVM {kernel} {n_sv} support vectors")
+    cats = ["neg", "pos"] if classification else None
+    _data_dictionary(out, n_features, "y", "string" if classification else "double", cats)
+    fn = "classification" if classification else "regression"
+    out.write(f' <SupportVectorMachineModel functionName="{fn}" svmRepresentation="SupportVectors">\n')
+    _mining_schema(out, n_features, "y", "  ")
+    ktag = {"radialBasis": f'<RadialBasisKernelType gamma="{gamma}"/>', "linear": '<LinearKernelType/>',
+            "polynomial": f'<PolynomialKernelType gamma="{gamma}" coef0="1" degree="3"/>',
+            "sigmoid": f'<SigmoidKernelType gamma="{gamma}" coef0="0.5"/>'}[kernel]
+    out.write(f'  {ktag}\n  <VectorDictionary numberOfVectors="{n_sv}">\n   <VectorFields numberOfFields="{n_features}">')
+    out.write("".join(f'<FieldRef field="f{j}"/>' for j in range(n_features)))
+    out.write('</VectorFields>\n')
+    S = rng.standard_normal((n_sv, n_features))
+    for i in range(n_sv):
+        out.write(f'   <VectorInstance id="sv{i}"><Array n="{n_features}" type="real">'
+                  + " ".join(f"{v:.6g}" for v in S[i]) + '</Array></VectorInstance>\n')
+    out.write('  </VectorDictionary>\n')
+    tc = ' targetCategory="neg" alternateTargetCategory="pos"' if classification else ""
+    out.write(f'  <SupportVectorMachine{tc}>\n   <SupportVectors numberOfSupportVectors="{n_sv}">')
+    out.write("".join(f'<SupportVector vectorId="sv{i}"/>' for i in range(n_sv)))
+    out.write('</SupportVectors>\n')
+    alpha = rng.standard_normal(n_sv) * 0.5
+    out.write(f'   <Coefficients numberOfCoefficients="{n_sv}" absoluteValue="{rng.standard_normal() * 0.1:.6g}">')
+    out.write("".join(f'<Coefficient value="{a:.6g}"/>' for a in alpha))
+    out.write('</Coefficients>\n  </SupportVectorMachine>\n </SupportVectorMachineModel>\n</PMML>\n')
+    return out.getvalue()
+
+
+def stream_matrix(n_rows: int, n_features: int, seed: int = 0, missing_rate: float = 0.0) -> np.ndarray:
+    """Synthetic fp32 record batch ``[rows, features]`` (standard normal; NaN = missing)."""
+    rng = np.random.default_rng(seed)
+    X = rng.standard_normal((n_rows, n_features), dtype=np.float32)
+    if missing_rate > 0:
+        X[rng.random((n_rows, n_features)) < missing_rate] = np.nan
+    return X

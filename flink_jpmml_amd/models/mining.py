@@ -1,0 +1,220 @@
+"""MiningModel (ensembles / model chains): GBDT, random forests, calibrated chains.
+
+``Segmentation/@multipleModelMethod``:
+
+* regression: ``sum``, ``average``, ``weightedAverage``, ``median``, ``weightedMedian``, ``max``,
+  ``min``;
+* classification: ``majorityVote``, ``weightedMajorityVote``, ``average``, ``weightedAverage``,
+  ``max``, ``median``;
+* any: ``selectFirst`` (first segment whose predicate is TRUE), ``modelChain`` (segments run in
+  order, each one's ``<Output>`` fields feed the next; the last applicable segment is the result).
+
+``missingPredictionTreatment``: ``returnMissing``/``continue`` make the aggregate missing when a
+segment yields no prediction; ``skipSegment`` ignores such segments.
+"""
+
+from __future__ import annotations
+
+from typing import List
+
+import numpy as np
+
+from ..api.exceptions import UnsupportedFeatureException
+from ..pmml import ir
+from ..pmml.fields import NAN, Columns, FieldSchema, eval_predicate
+from .base import ModelEvaluator, ModelResult
+
+
+class MiningEvaluator(ModelEvaluator):
+    def __init__(self, model: ir.MiningModel, schema: FieldSchema):
+        super().__init__(model, schema)
+        from .registry import make_evaluator  # circular
+
+        self.mm = model
+        self.method = model.multiple_model_method
+        self.segments = model.segments
+        self.sub = [make_evaluator(s.model, schema) for s in model.segments]
+        self.weights = np.array([s.weight for s in model.segments], dtype=np.float64)
+        if self.kind == "classification":
+            cats = self.classification_categories()
+            seen = set(cats)
+            for ev in self.sub:
+                for c in getattr(ev, "categories", None) or []:
+                    if c not in seen:
+                        cats.append(c)
+                        seen.add(c)
+            self.categories = cats
+        else:
+            self.categories = None
+
+    def _evaluate(self, cols: Columns) -> ModelResult:
+        n = cols.n
+        method = self.method
+        results: List[ModelResult] = []
+        applies: List[np.ndarray] = []
+        chain = method == "modelChain"
+        for seg, ev in zip(self.segments, self.sub):
+            t, _u = eval_predicate(seg.predicate, cols)
+            if method == "selectFirst" and results:
+                taken = np.zeros(n, dtype=bool)
+                for a in applies:
+                    taken |= a
+                if taken.all():
+                    break
+            r = ev.evaluate(cols)
+            if chain or ev.model.output:
+                outs = ev.compute_outputs(cols, r)
+                # rows the segment does not apply to must not see its outputs
+                if not t.all():
+                    for k, v in outs.items():
+                        cols.set(k, np.where(t, v, NAN))
+            results.append(r)
+            applies.append(t)
+        if not results:
+            return ModelResult(self.kind, np.full(n, NAN), np.zeros(n, dtype=bool), categories=self.categories)
+        if method in ("modelChain", "selectFirst"):
+            return self._select(results, applies, last=(method == "modelChain"))
+        if self.kind == "classification":
+            return self._classify(results, applies)
+        return self._regress(results, applies)
+
+    # ------------------------------------------------------------------ selection
+    def _select(self, results: List[ModelResult], applies: List[np.ndarray], last: bool) -> ModelResult:
+        n = results[0].n
+        chosen = np.full(n, -1)
+        order = range(len(results) - 1, -1, -1) if last else range(len(results))
+        for i in order:
+            chosen = np.where((chosen < 0) & applies[i], i, chosen)
+        final = results[-1] if last else results[0]
+        kind = final.kind
+        value = np.full(n, NAN)
+        valid = np.zeros(n, dtype=bool)
+        cats = final.categories if kind == "classification" else None
+        probs = np.full((n, len(cats)), NAN) if cats is not None and final.probs is not None else None
+        ent = [None] * n
+        for i, r in enumerate(results):
+            m = chosen == i
+            if not m.any():
+                continue
+            if kind == "classification" and r.kind == "classification" and r.categories != cats:
+                # remap to the final segment's category order
+                remap = np.array([cats.index(c) if c in cats else -1 for c in r.categories], dtype=np.float64)
+                v = np.where(r.valid, remap[np.where(r.valid, r.value, 0).astype(int)], NAN)
+                value[m] = v[m]
+            else:
+                value[m] = r.value[m]
+            valid[m] = r.valid[m]
+            if probs is not None and r.probs is not None and r.probs.shape[1] == probs.shape[1]:
+                probs[m] = r.probs[m]
+            el = r.extra.get("entity_labels")
+            if el is not None:
+                for j in np.nonzero(m)[0]:
+                    ent[j] = el[j]
+        res = ModelResult(kind, value, valid & ~np.isnan(value), categories=cats, probs=probs,
+                          entity_ids=final.entity_ids, affinity=None)
+        if kind == "clustering":
+            res.affinity = final.affinity
+        res.extra["entity_labels"] = ent
+        return res
+
+    # ------------------------------------------------------------------ regression
+    def _regress(self, results: List[ModelResult], applies: List[np.ndarray]) -> ModelResult:
+        V = np.stack([np.where(r.valid, r.value, NAN) for r in results], axis=1)
+        A = np.stack(applies, axis=1)
+        W = np.broadcast_to(self.weights[None, :], V.shape)
+        miss = np.isnan(V) & A
+        skip = self.mm.missing_prediction_treatment == "skipSegment"
+        use = A & ~np.isnan(V)
+        method = self.method
+        with np.errstate(invalid="ignore", divide="ignore"):
+            Vz = np.where(use, V, 0.0)
+            if method == "sum":
+                out = np.sum(Vz, axis=1)
+            elif method == "average":
+                out = np.sum(Vz, axis=1) / np.sum(use, axis=1)
+            elif method == "weightedAverage":
+                out = np.sum(Vz * W, axis=1) / np.sum(np.where(use, W, 0.0), axis=1)
+            elif method in ("max", "min"):
+                fill = -np.inf if method == "max" else np.inf
+                Vf = np.where(use, V, fill)
+                out = Vf.max(axis=1) if method == "max" else Vf.min(axis=1)
+            elif method == "median":
+                out = np.nanmedian(np.where(use, V, NAN), axis=1)
+            elif method == "weightedMedian":
+                out = _weighted_median(V, W, use)
+            else:
+                raise UnsupportedFeatureException(f"multipleModelMethod {method!r} for regression")
+        valid = np.any(use, axis=1)
+        if not skip:
+            valid &= ~np.any(miss, axis=1)
+        out = np.where(valid, out, NAN)
+        return ModelResult("regression", out, valid & np.isfinite(out))
+
+    # ------------------------------------------------------------------ classification
+    def _classify(self, results: List[ModelResult], applies: List[np.ndarray]) -> ModelResult:
+        cats = self.categories
+        C = len(cats)
+        n = results[0].n
+        method = self.method
+        acc = np.zeros((n, C))
+        wsum = np.zeros(n)
+        anymiss = np.zeros(n, dtype=bool)
+        count = np.zeros(n)
+        for r, a, w in zip(results, applies, self.weights):
+            use = a & r.valid
+            anymiss |= a & ~r.valid
+            if r.kind != "classification":
+                raise UnsupportedFeatureException("classification ensemble over non-classification segments")
+            idx_map = np.array([cats.index(c) for c in r.categories])
+            if method in ("majorityVote", "weightedMajorityVote"):
+                lab = idx_map[np.where(use, r.value, 0).astype(int)]
+                ww = w if method == "weightedMajorityVote" else 1.0
+                np.add.at(acc, (np.nonzero(use)[0], lab[use]), ww)
+                wsum += np.where(use, ww, 0.0)
+            else:
+                P = np.zeros((n, C))
+                P[:, idx_map] = np.nan_to_num(r.probs) if r.probs is not None else 0.0
+                if method in ("average", "weightedAverage"):
+                    ww = w if method == "weightedAverage" else 1.0
+                    acc += np.where(use[:, None], P * ww, 0.0)
+                    wsum += np.where(use, ww, 0.0)
+                elif method == "max":
+                    acc = np.where(use[:, None], np.maximum(acc, P), acc)
+                elif method == "median":
+                    acc += 0  # handled below
+                else:
+                    raise UnsupportedFeatureException(f"multipleModelMethod {method!r} for classification")
+            count += use
+        if method == "median":
+            stack = []
+            for r, a in zip(results, applies):
+                idx_map = np.array([cats.index(c) for c in r.categories])
+                P = np.full((n, C), NAN)
+                P[:, idx_map] = r.probs
+                P[~(a & r.valid)] = NAN
+                stack.append(P)
+            acc = np.nanmedian(np.stack(stack, axis=0), axis=0)
+        with np.errstate(invalid="ignore", divide="ignore"):
+            if method in ("majorityVote", "weightedMajorityVote", "average", "weightedAverage"):
+                probs = acc / wsum[:, None]
+            else:
+                probs = acc
+        valid = count > 0
+        if self.mm.missing_prediction_treatment != "skipSegment":
+            valid &= ~anymiss
+        lab = np.argmax(np.nan_to_num(probs, nan=-1.0), axis=1).astype(np.float64)
+        return ModelResult("classification", np.where(valid, lab, NAN), valid, categories=cats,
+                           probs=np.where(valid[:, None], probs, NAN))
+
+
+def _weighted_median(V: np.ndarray, W: np.ndarray, use: np.ndarray) -> np.ndarray:
+    out = np.full(V.shape[0], NAN)
+    for i in range(V.shape[0]):
+        v = V[i, use[i]]
+        w = W[i, use[i]]
+        if v.size == 0:
+            continue
+        o = np.argsort(v, kind="stable")
+        cw = np.cumsum(w[o])
+        out[i] = v[o][np.searchsorted(cw, 0.5 * cw[-1])]
+    return out

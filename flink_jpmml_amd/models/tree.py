@@ -1,0 +1,291 @@
+"""TreeModel: host oracle (general predicates) + binary-split lowering for the GPU.
+
+Oracle semantics (PMML 4.x TreeModel): children are tried in document order, the first child
+whose predicate is TRUE is followed. A predicate that is UNKNOWN (missing input) is handled by
+``missingValueStrategy``:
+
+* ``none`` — UNKNOWN counts as FALSE;
+* ``lastPrediction`` — stop and return the current node's score;
+* ``nullPrediction`` — no prediction (→ ``EmptyScore``);
+* ``defaultChild`` — continue at the node's ``defaultChild``.
+
+When no child is TRUE, ``noTrueChildStrategy`` decides: ``returnNullPrediction`` (default) or
+``returnLastPrediction``.
+
+The oracle walks the tree breadth-first over *row subsets* with numpy, so a whole batch is
+evaluated with O(nodes) vector operations.
+
+:func:`lower_binary_tree` recognises the binary split form emitted by XGBoost / LightGBM /
+scikit-learn exporters (two children: ``field OP threshold`` and its complement or ``True``) and
+produces the (feature, threshold, op, default-direction, leaf) arrays of
+:mod:`flink_jpmml_amd.runtime.plans` for the HIP traversal kernel.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+
+from ..api.exceptions import UnsupportedFeatureException
+from ..pmml import ir
+from ..pmml.fields import NAN, Columns, FieldSchema, eval_predicate
+from .base import ModelEvaluator, ModelResult
+
+
+class _RowView:
+    __slots__ = ("cols", "rows", "n", "schema")
+
+    def __init__(self, cols: Columns, rows: np.ndarray):
+        self.cols = cols
+        self.rows = rows
+        self.n = int(len(rows))
+        self.schema = cols.schema
+
+    def get(self, name: str) -> np.ndarray:
+        return self.cols.get(name)[self.rows]
+
+
+class TreeEvaluator(ModelEvaluator):
+    def __init__(self, model: ir.TreeModel, schema: FieldSchema):
+        super().__init__(model, schema)
+        self.tree = model
+        if model.missing_value_strategy in ("weightedConfidence", "aggregateNodes"):
+            raise UnsupportedFeatureException(f"missingValueStrategy {model.missing_value_strategy!r}")
+        self.nodes: List[ir.Node] = []
+        self._index: Dict[int, int] = {}
+        stack = [model.root]
+        while stack:
+            nd = stack.pop()
+            self._index[id(nd)] = len(self.nodes)
+            self.nodes.append(nd)
+            stack.extend(reversed(nd.children))
+        if self.kind == "classification":
+            cats = self.classification_categories()
+            seen = set(cats)
+            for nd in self.nodes:
+                for s in [nd.score] + [d.value for d in nd.distributions]:
+                    if s is not None and s not in seen:
+                        cats.append(s)
+                        seen.add(s)
+            self.categories = cats
+            C = len(cats)
+            self.node_probs = np.zeros((len(self.nodes), C))
+            self.node_label = np.full(len(self.nodes), NAN)
+            for i, nd in enumerate(self.nodes):
+                if nd.score is not None:
+                    self.node_label[i] = cats.index(nd.score)
+                if nd.distributions:
+                    tot = sum(d.record_count for d in nd.distributions)
+                    for d in nd.distributions:
+                        p = d.probability if d.probability is not None else (d.record_count / tot if tot else 0.0)
+                        self.node_probs[i, cats.index(d.value)] = p
+                elif nd.score is not None:
+                    self.node_probs[i, cats.index(nd.score)] = 1.0
+        else:
+            self.categories = None
+            self.node_value = np.array([_num(nd.score) for nd in self.nodes], dtype=np.float64)
+
+    def leaf_index(self, cols: Columns) -> np.ndarray:
+        """Index (into ``self.nodes``) of the scoring node per row; -1 = null prediction."""
+        n = cols.n
+        out = np.full(n, -1, dtype=np.int64)
+        strat = self.tree.missing_value_strategy
+        no_true = self.tree.no_true_child_strategy
+        work: List[Tuple[ir.Node, np.ndarray]] = [(self.tree.root, np.arange(n))]
+        # the root's own predicate (normally True) selects the rows that reach it
+        root_t, _ = eval_predicate(self.tree.root.predicate, cols)
+        work = [(self.tree.root, np.nonzero(root_t)[0])]
+        while work:
+            node, rows = work.pop()
+            if rows.size == 0:
+                continue
+            me = self._index[id(node)]
+            if not node.children:
+                out[rows] = me
+                continue
+            remaining = rows
+            by_id = {c.id: c for c in node.children}
+            for child in node.children:
+                if remaining.size == 0:
+                    break
+                view = _RowView(cols, remaining)
+                t, u = eval_predicate(child.predicate, view)
+                if u.any() and strat != "none":
+                    urows = remaining[u]
+                    if strat == "lastPrediction":
+                        out[urows] = me
+                    elif strat == "defaultChild":
+                        dc = by_id.get(node.default_child)
+                        if dc is not None:
+                            work.append((dc, urows))
+                    # nullPrediction: stays -1
+                    keep = ~u
+                    t = t[keep]
+                    remaining = remaining[keep]
+                if t.any():
+                    work.append((child, remaining[t]))
+                    remaining = remaining[~t]
+            if remaining.size and no_true == "returnLastPrediction":
+                out[remaining] = me
+        return out
+
+    def _evaluate(self, cols: Columns) -> ModelResult:
+        leaf = self.leaf_index(cols)
+        ok = leaf >= 0
+        safe = np.where(ok, leaf, 0)
+        ids = [nd.id for nd in self.nodes]
+        ent = [ids[i] if o else None for i, o in zip(safe, ok)]
+        if self.kind == "classification":
+            lab = np.where(ok, self.node_label[safe], NAN)
+            ok = ok & ~np.isnan(lab)
+            probs = np.where(ok[:, None], self.node_probs[safe], NAN)
+            res = ModelResult("classification", np.where(ok, lab, NAN), ok, categories=self.categories, probs=probs)
+        else:
+            val = np.where(ok, self.node_value[safe], NAN)
+            ok = ok & ~np.isnan(val)
+            res = ModelResult("regression", val, ok)
+        res.extra["entity_labels"] = ent
+        res.extra["leaf"] = leaf
+        return res
+
+
+def _num(s: Optional[str]) -> float:
+    if s is None:
+        return NAN
+    try:
+        return float(s)
+    except ValueError:
+        return NAN
+
+
+# --------------------------------------------------------------------------- lowering
+
+# comparison opcodes understood by the HIP kernel: go LEFT when  x OP threshold
+OP_LT, OP_LE, OP_GT, OP_GE = 0, 1, 2, 3
+_OPS = {"lessThan": OP_LT, "lessOrEqual": OP_LE, "greaterThan": OP_GT, "greaterOrEqual": OP_GE}
+_NEG = {"lessThan": "greaterOrEqual", "lessOrEqual": "greaterThan", "greaterThan": "lessOrEqual",
+        "greaterOrEqual": "lessThan"}
+
+
+@dataclass
+class BinaryTree:
+    """Pointer-form binary tree: arrays indexed by node id (0 = root)."""
+
+    feature: np.ndarray  # int32, -1 for leaves
+    threshold: np.ndarray  # float64
+    op: np.ndarray  # int8, go-left condition
+    default_left: np.ndarray  # bool: where a missing value goes
+    left: np.ndarray  # int32
+    right: np.ndarray  # int32
+    leaf_value: np.ndarray  # float64 (regression) / class index (classification)
+    leaf_probs: Optional[np.ndarray]  # [nodes, C] or None
+    depth: int
+
+
+class NotBinary(Exception):
+    pass
+
+
+def lower_binary_tree(ev: TreeEvaluator, field_index: Dict[str, int]) -> BinaryTree:
+    """Lower a TreeModel into pointer-form binary arrays, or raise :class:`NotBinary`.
+
+    Accepted node shapes (all exporters we know of use one of them):
+
+    * two children ``[x OP t, True]`` or ``[x OP t, x NEG(OP) t]``;
+    * missing values: ``defaultChild`` strategy (per-node default), ``none`` strategy with a
+      ``True`` second child (missing → right), or ``lastPrediction``/``nullPrediction`` are *not*
+      lowered (they need per-node early exit) and raise :class:`NotBinary`.
+    """
+    tm = ev.tree
+    strat = tm.missing_value_strategy
+    if strat not in ("none", "defaultChild"):
+        raise NotBinary(f"missingValueStrategy {strat}")
+    if not isinstance(tm.root.predicate, ir.TruePredicate):
+        raise NotBinary("root predicate is not True")
+    feats: List[int] = []
+    thr: List[float] = []
+    ops: List[int] = []
+    dleft: List[bool] = []
+    lefts: List[int] = []
+    rights: List[int] = []
+    leafv: List[float] = []
+    leafp: List[np.ndarray] = []
+    classification = ev.kind == "classification"
+
+    def new_node() -> int:
+        feats.append(-1)
+        thr.append(0.0)
+        ops.append(0)
+        dleft.append(False)
+        lefts.append(-1)
+        rights.append(-1)
+        leafv.append(NAN)
+        if classification:
+            leafp.append(np.zeros(len(ev.categories)))
+        return len(feats) - 1
+
+    max_depth = 0
+    stack = [(tm.root, new_node(), 0)]
+    while stack:
+        node, k, depth = stack.pop()
+        max_depth = max(max_depth, depth)
+        i = ev._index[id(node)]
+        if not node.children:
+            if classification:
+                leafv[k] = ev.node_label[i]
+                leafp[k] = ev.node_probs[i]
+            else:
+                leafv[k] = ev.node_value[i]
+            if np.isnan(leafv[k]):
+                raise NotBinary("leaf without score")
+            continue
+        if len(node.children) != 2:
+            raise NotBinary("node does not have exactly two children")
+        a, b = node.children
+        pa, pb = a.predicate, b.predicate
+        if not isinstance(pa, ir.SimplePredicate) or pa.operator not in _OPS:
+            raise NotBinary("first child predicate is not a numeric comparison")
+        if pa.field not in field_index or ev.schema.is_string(pa.field):
+            raise NotBinary("split on a non-input or string field")
+        if isinstance(pb, ir.TruePredicate):
+            pass
+        elif isinstance(pb, ir.SimplePredicate) and pb.field == pa.field and pb.operator == _NEG[pa.operator] \
+                and pb.value == pa.value:
+            pass
+        else:
+            raise NotBinary("second child is not the complement of the first")
+        # missing-value direction
+        if strat == "defaultChild":
+            if node.default_child is None:
+                raise NotBinary("defaultChild strategy without defaultChild attribute")
+            go_left = node.default_child == a.id
+            if not go_left and node.default_child != b.id:
+                raise NotBinary("defaultChild does not name a child")
+        else:
+            # 'none': UNKNOWN counts as FALSE -> a missing value fails the first predicate; the
+            # second child is taken only if it is True (a complement predicate is also UNKNOWN
+            # -> no true child -> noTrueChildStrategy, which we cannot lower)
+            if not isinstance(pb, ir.TruePredicate):
+                raise NotBinary("missing value with complement predicate needs noTrueChild handling")
+            go_left = False
+        feats[k] = field_index[pa.field]
+        thr[k] = float(pa.value)
+        ops[k] = _OPS[pa.operator]
+        dleft[k] = go_left
+        la, lb = new_node(), new_node()
+        lefts[k], rights[k] = la, lb
+        stack.append((a, la, depth + 1))
+        stack.append((b, lb, depth + 1))
+    return BinaryTree(
+        feature=np.array(feats, dtype=np.int32),
+        threshold=np.array(thr, dtype=np.float64),
+        op=np.array(ops, dtype=np.int8),
+        default_left=np.array(dleft, dtype=bool),
+        left=np.array(lefts, dtype=np.int32),
+        right=np.array(rights, dtype=np.int32),
+        leaf_value=np.array(leafv, dtype=np.float64),
+        leaf_probs=np.stack(leafp) if classification else None,
+        depth=max_depth,
+    )

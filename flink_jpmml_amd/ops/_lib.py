@@ -1,0 +1,221 @@
+"""Build + load of the native HIP kernel library (``_pmml_kernels.so``) and its C ABI.
+
+The kernels are plain HIP C++ compiled by ``hipcc --offload-arch=gfx950`` into one shared object
+with ``extern "C"`` launchers that take a raw ``hipStream_t`` and a POD argument struct. Python
+calls them through :mod:`ctypes` with ``torch`` tensor device pointers — no PyTorch C++ headers in
+the build (a full rebuild takes seconds), one HIP runtime in the process (the ``.so`` binds to the
+``libamdhip64.so.7`` that ``torch`` already loaded, matched by SONAME).
+
+On a machine with a GPU a missing / unloadable library is an error (:class:`KernelLibraryError`),
+never a silent fallback.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import glob
+import logging
+import os
+import shutil
+import subprocess
+import threading
+from typing import List, Optional
+
+logger = logging.getLogger(__name__)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+LIB_PATH = os.path.join(HERE, "_pmml_kernels.so")
+ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0] or "gfx950"
+
+
+class KernelLibraryError(RuntimeError):
+    pass
+
+
+def sources() -> List[str]:
+    return sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+
+
+def _headers() -> List[str]:
+    return sorted(glob.glob(os.path.join(CSRC, "*.h")))
+
+
+def is_stale() -> bool:
+    if not os.path.exists(LIB_PATH):
+        return True
+    t = os.path.getmtime(LIB_PATH)
+    return any(os.path.getmtime(p) > t for p in sources() + _headers())
+
+
+def hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if cand and os.path.exists(cand):
+            return cand
+    raise KernelLibraryError("hipcc not found (set HIPCC or install ROCm)")
+
+
+def build(force: bool = False, verbose: bool = False, jobs: int = 4) -> str:
+    """Compile every ``csrc/*.hip`` for gfx950 and link ``_pmml_kernels.so`` (in-tree)."""
+    if not force and not is_stale():
+        return LIB_PATH
+    cc = hipcc()
+    objdir = os.path.join(HERE, "_build")
+    os.makedirs(objdir, exist_ok=True)
+    flags = ["-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
+             "-ffp-contract=fast", "-munsafe-fp-atomics"]
+    procs = []
+    objs = []
+    for src in sources():
+        obj = os.path.join(objdir, os.path.basename(src).replace(".hip", ".o"))
+        objs.append(obj)
+        cmd = [cc, *flags, "-c", src, "-o", obj]
+        if verbose:
+            logger.info("%s", " ".join(cmd))
+        procs.append((src, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
+        if len([p for p in procs if p[1].poll() is None]) >= jobs:
+            procs[0][1].wait()
+    for src, p in procs:
+        out, _ = p.communicate()
+        if p.returncode != 0:
+            raise KernelLibraryError(f"hipcc failed on {os.path.basename(src)}:\n{out.decode(errors='replace')}")
+    tmp = LIB_PATH + ".tmp"
+    cmd = [cc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", tmp]
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+    if r.returncode != 0:
+        raise KernelLibraryError(f"link failed:\n{r.stdout.decode(errors='replace')}")
+    os.replace(tmp, LIB_PATH)
+    return LIB_PATH
+
+
+# --------------------------------------------------------------------------- ctypes ABI
+
+c_void_p = ctypes.c_void_p
+c_int = ctypes.c_int
+c_float = ctypes.c_float
+
+
+class FieldPrep(ctypes.Structure):
+    _fields_ = [("flags", ctypes.c_uint32), ("lo", c_float), ("hi", c_float), ("missing_repl", c_float),
+                ("invalid_repl", c_float), ("out_lo", c_float), ("out_hi", c_float), ("pad", c_float)]
+
+
+class Epilogue(ctypes.Structure):
+    _fields_ = [("mode", c_int), ("n_classes", c_int), ("a", c_float), ("b", c_float), ("thr", c_float),
+                ("has_table", c_int), ("table", c_void_p), ("write_probs", c_int), ("link", c_int)]
+
+
+class TreeArgs(ctypes.Structure):
+    _fields_ = [("X", c_void_p), ("n_rows", c_int), ("n_feat", c_int), ("ldx", c_int), ("pad0", c_int),
+                ("prep", c_void_p), ("row_valid_in", c_void_p), ("blob", c_void_p), ("roots", c_void_p),
+                ("leaves", c_void_p), ("tree_slot", c_void_p), ("n_trees", c_int), ("rec_words", c_int),
+                ("chunk_trees", c_int), ("P", c_int), ("C", c_int), ("trees_per_split", c_int),
+                ("general", c_int), ("pad1", c_int), ("epi", Epilogue), ("score", c_void_p),
+                ("valid", c_void_p), ("probs", c_void_p), ("partial", c_void_p)]
+
+
+class ClusterArgs(ctypes.Structure):
+    _fields_ = [("X", c_void_p), ("n_rows", c_int), ("n_feat", c_int), ("ldx", c_int), ("K", c_int),
+                ("prep", c_void_p), ("centers", c_void_p), ("weights", c_void_p), ("scales", c_void_p),
+                ("qweights", c_void_p), ("cfun", c_void_p), ("table", c_void_p), ("metric", c_int),
+                ("similarity", c_int), ("p", c_float), ("pad", c_int), ("score", c_void_p), ("valid", c_void_p),
+                ("label", c_void_p), ("affinity", c_void_p)]
+
+
+class LinearArgs(ctypes.Structure):
+    _fields_ = [("X", c_void_p), ("n_rows", c_int), ("n_feat", c_int), ("ldx", c_int), ("K", c_int),
+                ("prep", c_void_p), ("W", c_void_p), ("bias", c_void_p), ("simplemax", c_int), ("pad", c_int),
+                ("epi", Epilogue), ("score", c_void_p), ("valid", c_void_p), ("probs", c_void_p)]
+
+
+class MlpArgs(ctypes.Structure):
+    _fields_ = [("X", c_void_p), ("n_rows", c_int), ("n_feat", c_int), ("ldx", c_int), ("n_layers", c_int),
+                ("prep", c_void_p), ("in_scale", c_void_p), ("in_shift", c_void_p), ("weights", c_void_p),
+                ("biases", c_void_p), ("dims", c_void_p), ("acts", c_void_p), ("out_scale", c_float),
+                ("out_shift", c_float), ("final_norm", c_int), ("pad", c_int), ("epi", Epilogue),
+                ("score", c_void_p), ("valid", c_void_p), ("probs", c_void_p)]
+
+
+class SvmArgs(ctypes.Structure):
+    _fields_ = [("X", c_void_p), ("n_rows", c_int), ("n_feat", c_int), ("ldx", c_int), ("n_sv", c_int),
+                ("prep", c_void_p), ("sv", c_void_p), ("sv_norm", c_void_p), ("coef", c_void_p),
+                ("intercept", c_void_p), ("n_machines", c_int), ("kernel", c_int), ("gamma", c_float),
+                ("coef0", c_float), ("degree", c_float), ("pad", c_int), ("decision", c_void_p),
+                ("valid", c_void_p)]
+
+
+_ABI = {
+    "pmml_tree_args_size": TreeArgs,
+    "pmml_cluster_args_size": ClusterArgs,
+    "pmml_linear_args_size": LinearArgs,
+    "pmml_mlp_args_size": MlpArgs,
+    "pmml_svm_args_size": SvmArgs,
+}
+
+_lib: Optional[ctypes.CDLL] = None
+_lock = threading.Lock()
+
+
+def load(auto_build: bool = True) -> ctypes.CDLL:
+    """Load (building first if stale and ``hipcc`` is available) and ABI-check the library."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        import torch  # noqa: F401  -- bind to torch's HIP runtime before dlopen
+
+        if auto_build and is_stale():
+            try:
+                build()
+            except KernelLibraryError:
+                if not os.path.exists(LIB_PATH):
+                    raise
+                logger.warning("kernel sources newer than %s but rebuild failed; using the existing library",
+                               LIB_PATH)
+        if not os.path.exists(LIB_PATH):
+            raise KernelLibraryError(f"{LIB_PATH} missing: run `python -c 'import __graft_entry__ as g; g.build()'`")
+        try:
+            lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        except OSError as e:
+            raise KernelLibraryError(f"cannot load {LIB_PATH}: {e}") from e
+        for fn, struct in _ABI.items():
+            f = getattr(lib, fn, None)
+            if f is None:
+                continue
+            f.restype = c_int
+            got = f()
+            if got != ctypes.sizeof(struct):
+                raise KernelLibraryError(f"ABI mismatch: {fn}={got}, ctypes sizeof={ctypes.sizeof(struct)}")
+        for name in ("pmml_tree_launch", "pmml_cluster_launch", "pmml_linear_launch", "pmml_mlp_launch",
+                     "pmml_svm_launch"):
+            f = getattr(lib, name, None)
+            if f is not None:
+                f.restype = c_int
+        lib.pmml_tree_launch.argtypes = [c_void_p, ctypes.POINTER(TreeArgs), c_int, c_int, c_int, c_int]
+        lib.pmml_cluster_launch.argtypes = [c_void_p, ctypes.POINTER(ClusterArgs)]
+        lib.pmml_linear_launch.argtypes = [c_void_p, ctypes.POINTER(LinearArgs)]
+        if hasattr(lib, "pmml_mlp_launch"):
+            lib.pmml_mlp_launch.argtypes = [c_void_p, ctypes.POINTER(MlpArgs), c_int]
+        if hasattr(lib, "pmml_svm_launch"):
+            lib.pmml_svm_launch.argtypes = [c_void_p, ctypes.POINTER(SvmArgs)]
+        _lib = lib
+        return lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise KernelLibraryError(f"{what} failed with code {rc}")
+
+
+def ptr(t) -> Optional[int]:
+    """Device pointer of a tensor (None → NULL)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_handle(stream=None) -> int:
+    import torch
+
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream

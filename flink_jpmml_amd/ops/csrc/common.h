@@ -1,0 +1,127 @@
+// Shared device helpers for the PMML scoring kernels (gfx950 / CDNA4, wave64).
+//
+// Every kernel consumes a row-major [rows, F] fp32 feature matrix (NaN = missing) that arrives
+// straight from the host ingest buffer, and applies the MiningField / DataField preparation
+// (missing replacement, validity interval + invalidValueTreatment, outliers) *while staging the
+// tile into LDS* — there is no separate "prepare" pass over HBM.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define PMML_API extern "C" __attribute__((visibility("default")))
+
+// FieldPrep.flags bits
+enum : uint32_t {
+  FP_HAS_MISSING_REPL = 1u << 0,   // NaN -> missing_repl
+  FP_HAS_INTERVAL = 1u << 1,       // validity interval [lo, hi] (closure bits below)
+  FP_LO_OPEN = 1u << 2,
+  FP_HI_OPEN = 1u << 3,
+  FP_INVALID_RETURN = 1u << 4,     // invalid -> whole row invalid (returnInvalid)
+  FP_INVALID_AS_MISSING = 1u << 5, // invalid -> NaN (then missing replacement)
+  FP_INVALID_AS_VALUE = 1u << 6,   // invalid -> invalid_repl
+  FP_OUTLIER_AS_MISSING = 1u << 7, // x < out_lo | x > out_hi -> NaN
+  FP_OUTLIER_AS_EXTREME = 1u << 8, // clamp to [out_lo, out_hi]
+  FP_INTEGER = 1u << 9,            // non-integral value is invalid
+  FP_CODE_RANGE = 1u << 10,        // categorical codes: valid iff 0 <= x < hi (string vocabularies)
+  FP_ROW_INVALID = 1u << 11,       // field definition rejects every value (e.g. Interval on categorical)
+};
+
+struct FieldPrep {
+  uint32_t flags;
+  float lo, hi;          // validity interval (or code range in hi)
+  float missing_repl;
+  float invalid_repl;
+  float out_lo, out_hi;  // outlier bounds
+  float pad;
+};
+static_assert(sizeof(FieldPrep) == 32, "FieldPrep must stay 32 bytes (host mirror in ops/_lib.py)");
+
+// Prepare one raw value. Sets *bad when the row must be rejected (returnInvalid).
+__device__ __forceinline__ float prep_value(float x, const FieldPrep& p, bool* bad) {
+  const uint32_t fl = p.flags;
+  if (fl == 0u) return x;
+  if (fl & FP_ROW_INVALID) { *bad = true; return x; }
+  bool miss = (x != x);
+  if (!miss) {
+    bool invalid = false;
+    if (fl & FP_HAS_INTERVAL) {
+      bool lo_ok = (fl & FP_LO_OPEN) ? (x > p.lo) : (x >= p.lo);
+      bool hi_ok = (fl & FP_HI_OPEN) ? (x < p.hi) : (x <= p.hi);
+      invalid = !(lo_ok && hi_ok);
+    }
+    if (fl & FP_CODE_RANGE) invalid = invalid || !(x >= 0.f && x < p.hi);
+    if (fl & FP_INTEGER) invalid = invalid || (floorf(x) != x);
+    if (invalid) {
+      if (fl & FP_INVALID_RETURN) *bad = true;
+      else if (fl & FP_INVALID_AS_MISSING) miss = true;
+      else if (fl & FP_INVALID_AS_VALUE) x = p.invalid_repl;
+    } else {
+      if (fl & FP_OUTLIER_AS_MISSING) miss = (x < p.out_lo) || (x > p.out_hi);
+      else if (fl & FP_OUTLIER_AS_EXTREME) x = fminf(fmaxf(x, p.out_lo), p.out_hi);
+    }
+  }
+  if (miss) x = (fl & FP_HAS_MISSING_REPL) ? p.missing_repl : __builtin_nanf("");
+  return x;
+}
+
+__device__ __forceinline__ float fast_sigmoid(float z) { return 1.0f / (1.0f + __expf(-z)); }
+
+// Epilogue modes shared by the model kernels.
+enum : int {
+  EPI_AFFINE = 0,       // score = link(a * acc0 + b)
+  EPI_LOGISTIC2 = 1,    // p0 = link(a * acc0 + b), p1 = 1 - p0; label = p0 >= thr ? 0 : 1
+  EPI_ARGMAX = 2,       // label = argmax_c acc_c (ties -> lowest c); probs = acc * a
+  EPI_SOFTMAX = 3,      // probs = softmax(acc); label = argmax
+};
+
+struct Epilogue {
+  int mode;
+  int n_classes;        // accumulator slots C
+  float a, b;           // affine
+  float thr;            // EPI_LOGISTIC2 threshold
+  int has_table;        // score = table[label] (class label parsed as double), NaN -> invalid
+  const float* table;   // [C]
+  int write_probs;      // also write probs[row, C]
+  int link;             // LINK_* applied after the affine map (EPI_AFFINE, EPI_LOGISTIC2)
+};
+
+enum : int { LINK_NONE = 0, LINK_LOGIT = 1, LINK_EXP = 2, LINK_PROBIT = 3, LINK_CLOGLOG = 4, LINK_LOGLOG = 5,
+             LINK_CAUCHIT = 6 };
+
+__device__ __forceinline__ float apply_link(int link, float y) {
+  switch (link) {
+    case LINK_LOGIT: return 1.0f / (1.0f + expf(-y));
+    case LINK_EXP: return expf(y);
+    case LINK_PROBIT: return 0.5f * erfcf(-y * 0.70710678118654752f);
+    case LINK_CLOGLOG: return 1.0f - expf(-expf(y));
+    case LINK_LOGLOG: return expf(-expf(-y));
+    case LINK_CAUCHIT: return 0.5f + atanf(y) * 0.31830988618379067f;
+    default: return y;
+  }
+}
+
+// Stage TB rows x F features of a row-major [n_rows, ldx] matrix into LDS as [F][TB] (lane-major,
+// so lane r reading feature f hits bank (f*TB + r) % 64 — conflict free for any mix of features),
+// applying the field preparation and flagging rejected rows in bad[TB]. Ends with a barrier.
+template <int TB>
+__device__ __forceinline__ void stage_rows_T(const float* __restrict__ X, int n_rows, int F, int ldx,
+                                             const FieldPrep* __restrict__ prep, float* __restrict__ feat,
+                                             int* __restrict__ bad, int row0) {
+  bad[threadIdx.x] = 0;
+  __syncthreads();
+  const int total = TB * F;
+  for (int e = threadIdx.x; e < total; e += TB) {
+    const int r = e / F;
+    const int f = e - r * F;
+    const int row = row0 + r;
+    float x = __builtin_nanf("");
+    bool b = false;
+    if (row < n_rows) {
+      x = X[(size_t)row * ldx + f];
+      if (prep) x = prep_value(x, prep[f], &b);
+    }
+    feat[f * TB + r] = x;
+    if (b) bad[r] = 1;
+  }
+  __syncthreads();
+}

@@ -1,0 +1,50 @@
+// Fused per-row epilogue: ensemble/linear accumulators -> PMML target value (+ probabilities).
+#pragma once
+#include "common.h"
+
+// acc: C accumulator values of this row (registers or LDS, read through the accessor).
+template <typename Acc>
+__device__ __forceinline__ void apply_epilogue(const Epilogue& e, Acc acc, bool row_ok, int row, int n_rows,
+                                               float* __restrict__ score, uint8_t* __restrict__ valid,
+                                               float* __restrict__ probs) {
+  float s = __builtin_nanf("");
+  bool ok = row_ok;
+  int label = 0;
+  if (e.mode == EPI_AFFINE) {
+    s = apply_link(e.link, fmaf(e.a, acc(0), e.b));
+    ok = ok && (s == s);
+    if (e.write_probs && probs) probs[row] = s;
+  } else if (e.mode == EPI_LOGISTIC2) {
+    float p0 = apply_link(e.link, fmaf(e.a, acc(0), e.b));
+    label = (p0 >= e.thr) ? 0 : 1;
+    if (e.write_probs && probs) {
+      probs[(size_t)row * 2 + 0] = p0;
+      probs[(size_t)row * 2 + 1] = 1.0f - p0;
+    }
+    ok = ok && (p0 == p0);
+  } else {
+    const int C = e.n_classes;
+    float best = -__builtin_inff();
+    float mx = -__builtin_inff();
+    for (int c = 0; c < C; ++c) mx = fmaxf(mx, acc(c));
+    float denom = 0.f;
+    if (e.mode == EPI_SOFTMAX) {
+      for (int c = 0; c < C; ++c) denom += __expf(acc(c) - mx);
+    }
+    for (int c = 0; c < C; ++c) {
+      float v = acc(c);
+      if (v > best) { best = v; label = c; }
+      if (e.write_probs && probs) {
+        float pv = (e.mode == EPI_SOFTMAX) ? __expf(v - mx) / denom : v * e.a;
+        probs[(size_t)row * C + c] = pv;
+      }
+    }
+    ok = ok && (best == best) && (best > -__builtin_inff());
+  }
+  if (e.mode != EPI_AFFINE) {
+    s = e.has_table ? e.table[label] : (float)label;
+    ok = ok && (s == s);
+  }
+  score[row] = ok ? s : __builtin_nanf("");
+  valid[row] = ok ? 1 : 0;
+}

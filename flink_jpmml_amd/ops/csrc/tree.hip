@@ -1,0 +1,329 @@
+// Tree-ensemble scoring (PMML TreeModel / MiningModel GBDT, random forest, model chains).
+//
+// Design (MI355X / CDNA4):
+//  * rows-stationary: one 256-thread workgroup (4 wave64s) owns 256 rows, one row per lane, for
+//    the whole ensemble; the prepared feature tile lives in LDS transposed as [F][256] so that a
+//    lane's feature read `feat[f][lane]` is bank-conflict free whatever feature each lane needs;
+//  * trees stream through an LDS chunk buffer shared by the 4 waves (the ensemble is L2/MALL
+//    resident, so every workgroup re-reads it at L2 bandwidth, not HBM);
+//  * PERFECT layout for depth <= 10: every tree is padded to a perfect binary tree of depth D,
+//    nodes are 8 bytes {threshold, meta} in level order, traversal is branch-free
+//    `idx = 2*idx + 1 + (x >= T)` for exactly D steps — no divergence, one ds_read_b64 + one
+//    ds_read_b32 per level, ILP trees interleaved per lane to hide LDS latency;
+//    split operators are canonicalised on the host to "go right iff x >= T" with T rounded so the
+//    fp32 comparison is exact for fp32 inputs (see runtime/plans.py);
+//  * POINTER layout for deeper / wider ensembles: {T, meta, left, right} nodes read from global
+//    memory (L2-resident), divergent walk;
+//  * the per-row epilogue (sum / average / vote / link function / label table) is fused.
+#include "epilogue.h"
+
+namespace {
+
+constexpr int TB = 256;   // rows per workgroup (= threads)
+constexpr int ILP = 4;    // independent trees in flight per lane
+
+struct TreeArgs {
+  const float* X;
+  int n_rows, n_feat, ldx;
+  int pad0;
+  const FieldPrep* prep;        // nullable
+  const uint8_t* row_valid_in;  // nullable
+  const uint32_t* blob;         // perfect: [n_trees][rec_words]; pointer: nodes uint4[]
+  const int* roots;             // pointer layout: per-tree root code (>=0 node, <0 ~leaf)
+  const float* leaves;          // pointer layout: [n_leaves][P]
+  const int* tree_slot;         // general accumulation: slot per tree
+  int n_trees, rec_words, chunk_trees, P;
+  int C, trees_per_split, general, pad1;
+  Epilogue epi;
+  float* score;
+  uint8_t* valid;
+  float* probs;
+  float* partial;               // split mode: [splits][C+1][n_rows]
+};
+
+__device__ __forceinline__ void finish_row(const TreeArgs& a, float acc0, const float* accl, int split,
+                                           bool general, int row, bool row_ok) {
+  if (row >= a.n_rows) return;
+  if (a.partial) {
+    const size_t stride = (size_t)a.n_rows;
+    float* base = a.partial + (size_t)split * (a.C + 1) * stride;
+    if (general) {
+      for (int c = 0; c < a.C; ++c) base[c * stride + row] = accl[c * TB + threadIdx.x];
+    } else {
+      base[row] = acc0;
+    }
+    base[a.C * stride + row] = row_ok ? 0.f : 1.f;
+    return;
+  }
+  if (general) {
+    apply_epilogue(a.epi, [&](int c) { return accl[c * TB + threadIdx.x]; }, row_ok, row, a.n_rows, a.score,
+                   a.valid, a.probs);
+  } else {
+    apply_epilogue(a.epi, [&](int) { return acc0; }, row_ok, row, a.n_rows, a.score, a.valid, a.probs);
+  }
+}
+
+template <int DEPTH, bool GENERAL, bool HAS_DR>
+__global__ __launch_bounds__(TB, 2) void tree_perfect_kernel(TreeArgs a) {
+  extern __shared__ __align__(16) uint32_t smem[];
+  constexpr int NI = (1 << DEPTH) - 1;
+  float* feat = reinterpret_cast<float*>(smem);
+  uint32_t* tbuf = smem + a.n_feat * TB;
+  int* bad = reinterpret_cast<int*>(tbuf + a.chunk_trees * a.rec_words);
+  float* accl = reinterpret_cast<float*>(bad + TB);
+
+  const int tid = threadIdx.x;
+  const int row0 = blockIdx.x * TB;
+  const int split = blockIdx.y;
+  stage_rows_T<TB>(a.X, a.n_rows, a.n_feat, a.ldx, a.prep, feat, bad, row0);
+  const int row = row0 + tid;
+  bool row_ok = bad[tid] == 0;
+  if (a.row_valid_in && row < a.n_rows) row_ok = row_ok && a.row_valid_in[row];
+
+  const int tb = split * a.trees_per_split;
+  const int te = min(a.n_trees, tb + a.trees_per_split);
+  if (GENERAL) {
+    for (int c = 0; c < a.C; ++c) accl[c * TB + tid] = 0.f;
+  }
+  float acc = 0.f;
+  const char* feat_lane = reinterpret_cast<const char*>(feat + tid);
+  const int rw = a.rec_words;
+
+  for (int t0 = tb; t0 < te; t0 += a.chunk_trees) {
+    const int nt = min(a.chunk_trees, te - t0);
+    __syncthreads();  // previous chunk fully consumed
+    {
+      const uint4* src = reinterpret_cast<const uint4*>(a.blob + (size_t)t0 * rw);
+      uint4* dst = reinterpret_cast<uint4*>(tbuf);
+      const int n16 = (nt * rw) >> 2;
+      for (int i = tid; i < n16; i += TB) dst[i] = src[i];
+    }
+    __syncthreads();
+
+    int k = 0;
+    for (; k + ILP <= nt; k += ILP) {
+      uint32_t idx[ILP];
+#pragma unroll
+      for (int j = 0; j < ILP; ++j) idx[j] = 0;
+#pragma unroll
+      for (int d = 0; d < DEPTH; ++d) {
+#pragma unroll
+        for (int j = 0; j < ILP; ++j) {
+          const uint2 nd = *reinterpret_cast<const uint2*>(tbuf + (k + j) * rw + 2 * idx[j]);
+          const float x = *reinterpret_cast<const float*>(feat_lane + (nd.y & 0xFFFFu));
+          bool right = x >= __uint_as_float(nd.x);
+          if (HAS_DR) right = right || ((x != x) && (nd.y >> 31));
+          idx[j] = 2 * idx[j] + 1 + (right ? 1u : 0u);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < ILP; ++j) {
+        const float* lv = reinterpret_cast<const float*>(tbuf + (k + j) * rw + 2 * NI);
+        if (GENERAL) {
+          const int slot = a.tree_slot[t0 + k + j];
+          for (int p = 0; p < a.P; ++p) accl[(slot + p) * TB + tid] += lv[(idx[j] - NI) * a.P + p];
+        } else {
+          acc += lv[idx[j] - NI];
+        }
+      }
+    }
+    for (; k < nt; ++k) {
+      uint32_t idx = 0;
+#pragma unroll
+      for (int d = 0; d < DEPTH; ++d) {
+        const uint2 nd = *reinterpret_cast<const uint2*>(tbuf + k * rw + 2 * idx);
+        const float x = *reinterpret_cast<const float*>(feat_lane + (nd.y & 0xFFFFu));
+        bool right = x >= __uint_as_float(nd.x);
+        if (HAS_DR) right = right || ((x != x) && (nd.y >> 31));
+        idx = 2 * idx + 1 + (right ? 1u : 0u);
+      }
+      const float* lv = reinterpret_cast<const float*>(tbuf + k * rw + 2 * NI);
+      if (GENERAL) {
+        const int slot = a.tree_slot[t0 + k];
+        for (int p = 0; p < a.P; ++p) accl[(slot + p) * TB + tid] += lv[(idx - NI) * a.P + p];
+      } else {
+        acc += lv[idx - NI];
+      }
+    }
+  }
+  finish_row(a, acc, accl, split, GENERAL, row, row_ok);
+}
+
+// Pointer layout: nodes uint4 {T bits, meta, left, right}; child < 0 => leaf ~child.
+template <bool GENERAL, bool FEAT_LDS>
+__global__ __launch_bounds__(TB, 2) void tree_pointer_kernel(TreeArgs a) {
+  extern __shared__ __align__(16) uint32_t smem[];
+  float* feat = reinterpret_cast<float*>(smem);
+  int* bad = reinterpret_cast<int*>(smem + (FEAT_LDS ? a.n_feat * TB : 0));
+  float* accl = reinterpret_cast<float*>(bad + TB);
+  const int tid = threadIdx.x;
+  const int row0 = blockIdx.x * TB;
+  const int split = blockIdx.y;
+  const int row = row0 + tid;
+  if (FEAT_LDS) {
+    stage_rows_T<TB>(a.X, a.n_rows, a.n_feat, a.ldx, a.prep, feat, bad, row0);
+  } else {
+    bad[tid] = 0;
+    __syncthreads();
+  }
+  bool row_ok = bad[tid] == 0;
+  // global-feature mode: apply preparation lazily per read
+  const float* xrow = a.X + (size_t)min(row, a.n_rows - 1) * a.ldx;
+  if (!FEAT_LDS && a.prep && row < a.n_rows) {
+    for (int f = 0; f < a.n_feat; ++f) {
+      bool b = false;
+      (void)prep_value(xrow[f], a.prep[f], &b);
+      if (b) row_ok = false;
+    }
+  }
+  if (a.row_valid_in && row < a.n_rows) row_ok = row_ok && a.row_valid_in[row];
+  const uint4* nodes = reinterpret_cast<const uint4*>(a.blob);
+  const int tb = split * a.trees_per_split;
+  const int te = min(a.n_trees, tb + a.trees_per_split);
+  if (GENERAL) {
+    for (int c = 0; c < a.C; ++c) accl[c * TB + tid] = 0.f;
+  }
+  float acc = 0.f;
+  const char* feat_lane = reinterpret_cast<const char*>(feat + tid);
+  for (int t = tb; t < te; ++t) {
+    int code = a.roots[t];
+    while (code >= 0) {
+      const uint4 nd = nodes[code];
+      float x;
+      if (FEAT_LDS) {
+        x = *reinterpret_cast<const float*>(feat_lane + (nd.y & 0xFFFFu));
+      } else {
+        const int f = nd.y & 0xFFFFu;
+        x = xrow[f];
+        if (a.prep) { bool b = false; x = prep_value(x, a.prep[f], &b); }
+      }
+      bool right = (x >= __uint_as_float(nd.x)) || ((x != x) && (nd.y >> 31));
+      code = right ? (int)nd.w : (int)nd.z;
+    }
+    const int leaf = ~code;
+    if (GENERAL) {
+      const int slot = a.tree_slot[t];
+      for (int p = 0; p < a.P; ++p) accl[(slot + p) * TB + tid] += a.leaves[(size_t)leaf * a.P + p];
+    } else {
+      acc += a.leaves[leaf];
+    }
+  }
+  finish_row(a, acc, accl, split, GENERAL, row, row_ok);
+}
+
+// Split-mode reduction: partial[splits][C+1][n_rows] -> epilogue.
+__global__ __launch_bounds__(TB) void tree_reduce_kernel(TreeArgs a, int splits) {
+  const int row = blockIdx.x * TB + threadIdx.x;
+  if (row >= a.n_rows) return;
+  const size_t stride = (size_t)a.n_rows;
+  float acc[16];
+  const int C = a.C;
+  for (int c = 0; c < 16; ++c) acc[c] = 0.f;
+  bool ok = true;
+  for (int s = 0; s < splits; ++s) {
+    const float* base = a.partial + (size_t)s * (C + 1) * stride;
+    for (int c = 0; c < C && c < 16; ++c) acc[c] += base[c * stride + row];
+    ok = ok && base[C * stride + row] == 0.f;
+  }
+  apply_epilogue(a.epi, [&](int c) { return acc[c]; }, ok, row, a.n_rows, a.score, a.valid, a.probs);
+}
+
+template <typename K>
+int prepare_launch(K kernel, size_t lds) {
+  if (lds > 65536) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return (int)e;
+  }
+  return 0;
+}
+
+template <int D>
+int launch_perfect(hipStream_t st, const TreeArgs& a, dim3 grid, size_t lds, bool has_dr) {
+  int err = 0;
+  if (a.general) {
+    if (has_dr) {
+      err = prepare_launch(tree_perfect_kernel<D, true, true>, lds);
+      if (!err) hipLaunchKernelGGL((tree_perfect_kernel<D, true, true>), grid, dim3(TB), lds, st, a);
+    } else {
+      err = prepare_launch(tree_perfect_kernel<D, true, false>, lds);
+      if (!err) hipLaunchKernelGGL((tree_perfect_kernel<D, true, false>), grid, dim3(TB), lds, st, a);
+    }
+  } else {
+    if (has_dr) {
+      err = prepare_launch(tree_perfect_kernel<D, false, true>, lds);
+      if (!err) hipLaunchKernelGGL((tree_perfect_kernel<D, false, true>), grid, dim3(TB), lds, st, a);
+    } else {
+      err = prepare_launch(tree_perfect_kernel<D, false, false>, lds);
+      if (!err) hipLaunchKernelGGL((tree_perfect_kernel<D, false, false>), grid, dim3(TB), lds, st, a);
+    }
+  }
+  return err;
+}
+
+}  // namespace
+
+PMML_API int pmml_tree_args_size() { return (int)sizeof(TreeArgs); }
+PMML_API int pmml_tree_rows_per_block() { return TB; }
+
+// layout: 0 = perfect (depth in [1,10]), 1 = pointer. splits >= 1 (tree-parallel split of the
+// ensemble across grid.y; > 1 requires a.partial with room for splits*(C+1)*n_rows floats).
+PMML_API int pmml_tree_launch(hipStream_t stream, const TreeArgs* args, int layout, int depth, int has_dr,
+                              int splits) {
+  TreeArgs a = *args;
+  if (a.n_rows <= 0) return 0;
+  if (splits < 1) splits = 1;
+  if (splits > 1 && a.partial == nullptr) return -2;
+  if (splits == 1) a.partial = nullptr;
+  if (a.C > 16) return -3;
+  a.trees_per_split = (a.n_trees + splits - 1) / splits;
+  dim3 grid((a.n_rows + TB - 1) / TB, splits);
+  int err = 0;
+  const size_t acc_lds = a.general ? (size_t)a.C * TB * 4 : 0;
+  if (layout == 0) {
+    if (a.n_feat > 64) return -4;
+    const size_t lds = (size_t)a.n_feat * TB * 4 + (size_t)a.chunk_trees * a.rec_words * 4 + TB * 4 + acc_lds;
+    if (lds > 160 * 1024) return -5;
+    switch (depth) {
+      case 1: err = launch_perfect<1>(stream, a, grid, lds, has_dr); break;
+      case 2: err = launch_perfect<2>(stream, a, grid, lds, has_dr); break;
+      case 3: err = launch_perfect<3>(stream, a, grid, lds, has_dr); break;
+      case 4: err = launch_perfect<4>(stream, a, grid, lds, has_dr); break;
+      case 5: err = launch_perfect<5>(stream, a, grid, lds, has_dr); break;
+      case 6: err = launch_perfect<6>(stream, a, grid, lds, has_dr); break;
+      case 7: err = launch_perfect<7>(stream, a, grid, lds, has_dr); break;
+      case 8: err = launch_perfect<8>(stream, a, grid, lds, has_dr); break;
+      case 9: err = launch_perfect<9>(stream, a, grid, lds, has_dr); break;
+      case 10: err = launch_perfect<10>(stream, a, grid, lds, has_dr); break;
+      default: return -6;
+    }
+  } else {
+    const bool feat_lds = a.n_feat <= 64;
+    const size_t lds = (feat_lds ? (size_t)a.n_feat * TB * 4 : 0) + TB * 4 + acc_lds;
+    if (a.general) {
+      if (feat_lds) {
+        err = prepare_launch(tree_pointer_kernel<true, true>, lds);
+        if (!err) hipLaunchKernelGGL((tree_pointer_kernel<true, true>), grid, dim3(TB), lds, stream, a);
+      } else {
+        err = prepare_launch(tree_pointer_kernel<true, false>, lds);
+        if (!err) hipLaunchKernelGGL((tree_pointer_kernel<true, false>), grid, dim3(TB), lds, stream, a);
+      }
+    } else {
+      if (feat_lds) {
+        err = prepare_launch(tree_pointer_kernel<false, true>, lds);
+        if (!err) hipLaunchKernelGGL((tree_pointer_kernel<false, true>), grid, dim3(TB), lds, stream, a);
+      } else {
+        err = prepare_launch(tree_pointer_kernel<false, false>, lds);
+        if (!err) hipLaunchKernelGGL((tree_pointer_kernel<false, false>), grid, dim3(TB), lds, stream, a);
+      }
+    }
+  }
+  if (err) return err;
+  if (hipGetLastError() != hipSuccess) return -7;
+  if (splits > 1) {
+    dim3 g2((a.n_rows + TB - 1) / TB);
+    hipLaunchKernelGGL(tree_reduce_kernel, g2, dim3(TB), 0, stream, a, splits);
+    if (hipGetLastError() != hipSuccess) return -8;
+  }
+  return 0;
+}

@@ -1,0 +1,19 @@
+"""Multi-GPU data parallelism over RCCL/xGMI (and gloo for CPU tests)."""
+
+from .dist import (
+    DistContext,
+    all_gather_scores,
+    all_gather_varlen,
+    broadcast_control,
+    broadcast_object,
+    broadcast_plan,
+    broadcast_tensors,
+    init_from_env,
+    shard_range,
+    shutdown,
+)
+
+__all__ = [
+    "DistContext", "all_gather_scores", "all_gather_varlen", "broadcast_control", "broadcast_object",
+    "broadcast_plan", "broadcast_tensors", "init_from_env", "shard_range", "shutdown",
+]

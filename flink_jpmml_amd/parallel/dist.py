@@ -1,0 +1,213 @@
+"""Data-parallel runtime over RCCL (``torch.distributed`` backend ``nccl`` = RCCL on ROCm).
+
+One process per GPU. The reference's only parallelism is Flink operator data parallelism
+(one model replica per subtask, control stream broadcast: `S/package.scala:65,81,118`); its MI355X
+form (SURVEY §2.6 F1–F5):
+
+* **F2 model replication** — rank 0 parses + lowers the PMML once and :func:`broadcast_plan`
+  ships the compiled device tensors to every rank over xGMI (``dist.broadcast``), instead of
+  every subtask re-reading and re-parsing the document;
+* **F1 control plane** — :func:`broadcast_control` replicates Add/Del messages (packed into a
+  small byte tensor) from rank 0;
+* **F3 record sharding** — each rank ingests its own contiguous shard (:func:`shard_range`);
+* **F5 sink** — :func:`all_gather_scores` collects every rank's scored shard
+  (``all_gather_into_tensor``), optionally async on RCCL's stream so it overlaps the next batch.
+
+The same code runs on ``gloo`` for CPU tests (world size 2–8 on one host).
+"""
+
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistContext:
+    rank: int = 0
+    world_size: int = 1
+    local_rank: int = 0
+    backend: Optional[str] = None
+    device: torch.device = torch.device("cpu")
+
+    @property
+    def is_distributed(self) -> bool:
+        return self.world_size > 1 and dist.is_available() and dist.is_initialized()
+
+    @property
+    def is_root(self) -> bool:
+        return self.rank == 0
+
+    def barrier(self) -> None:
+        if self.is_distributed:
+            if self.backend == "nccl":
+                dist.barrier(device_ids=[self.device.index])
+            else:
+                dist.barrier()
+
+
+def init_from_env(backend: Optional[str] = None, timeout_s: float = 600.0) -> DistContext:
+    """Initialise from torchrun-style env vars (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_ADDR/PORT).
+
+    ``backend=None`` picks ``nccl`` (RCCL) when a GPU is visible, else ``gloo``."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    use_gpu = torch.cuda.is_available()
+    if backend is None:
+        backend = "nccl" if use_gpu else "gloo"
+    device = torch.device("cuda", local % max(1, torch.cuda.device_count())) if use_gpu and backend == "nccl" \
+        else (torch.device("cuda", local % max(1, torch.cuda.device_count())) if use_gpu else torch.device("cpu"))
+    if use_gpu:
+        torch.cuda.set_device(device)
+    ctx = DistContext(rank, world, local, backend, device)
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
+        if backend == "nccl":
+            kw["device_id"] = device
+        dist.init_process_group(**kw)
+    return ctx
+
+
+def shutdown(ctx: DistContext) -> None:
+    if ctx.is_distributed:
+        dist.destroy_process_group()
+
+
+def shard_range(n: int, rank: int, world: int) -> Tuple[int, int]:
+    """Contiguous, balanced ``[start, end)`` shard of ``n`` rows for ``rank``."""
+    base, rem = divmod(n, world)
+    start = rank * base + min(rank, rem)
+    return start, start + base + (1 if rank < rem else 0)
+
+
+# --------------------------------------------------------------------------- replication
+
+
+def broadcast_object(obj, ctx: DistContext, src: int = 0):
+    if not ctx.is_distributed:
+        return obj
+    box = [obj if ctx.rank == src else None]
+    dist.broadcast_object_list(box, src=src, device=ctx.device if ctx.backend == "nccl" else None)
+    return box[0]
+
+
+def broadcast_tensors(tensors: Optional[dict], spec: Optional[dict], ctx: DistContext, src: int = 0) -> dict:
+    """Broadcast a dict of tensors whose shapes/dtypes are given by ``spec`` (known on all ranks).
+    Tensors travel in one flat byte buffer over the RCCL group (one collective, not one per tensor)."""
+    if not ctx.is_distributed:
+        return dict(tensors or {})
+    dev = ctx.device if ctx.backend == "nccl" else torch.device("cpu")
+    names = sorted(spec)
+    sizes = []
+    for k in names:
+        shape, dt = spec[k]
+        n = 1
+        for s in shape:
+            n *= s
+        sizes.append(n * torch.empty((), dtype=getattr(torch, dt)).element_size())
+    total = sum(sizes)
+    buf = torch.empty(total, dtype=torch.uint8, device=dev)
+    if ctx.rank == src:
+        off = 0
+        for k, nb in zip(names, sizes):
+            t = tensors[k].contiguous()
+            buf[off: off + nb].copy_(t.view(-1).view(torch.uint8).to(dev))
+            off += nb
+    dist.broadcast(buf, src=src)
+    out = {}
+    off = 0
+    for k, nb in zip(names, sizes):
+        shape, dt = spec[k]
+        out[k] = buf[off: off + nb].view(getattr(torch, dt)).view(shape).clone()
+        off += nb
+    return out
+
+
+def broadcast_plan(plan, ctx: DistContext, src: int = 0, device=None):
+    """Replicate a device plan from ``src`` to every rank. Returns the local
+    plan (the original object on ``src``)."""
+    from ..runtime.plans import DevicePlan
+
+    if not ctx.is_distributed:
+        return plan
+    if ctx.rank == src:
+        meta, tensors = plan.export_state()
+    else:
+        meta, tensors = None, None
+    meta = broadcast_object(meta, ctx, src)
+    got = broadcast_tensors(tensors, meta["__tensors__"], ctx, src)
+    if ctx.rank == src:
+        return plan
+    return DevicePlan.from_state(meta, got, device or ctx.device)
+
+
+def broadcast_control(messages: Optional[Sequence], ctx: DistContext, src: int = 0) -> List:
+    """Replicate control messages (Add/Del) from ``src`` as one packed byte tensor (F1)."""
+    from ..domain.control import ServingMessage
+
+    if not ctx.is_distributed:
+        return list(messages or [])
+    dev = ctx.device if ctx.backend == "nccl" else torch.device("cpu")
+    if ctx.rank == src:
+        blobs = [m.pack() for m in messages]
+        payload = b"".join(len(b).to_bytes(4, "little") + b for b in blobs)
+        n = torch.tensor([len(payload)], dtype=torch.int64, device=dev)
+    else:
+        n = torch.zeros(1, dtype=torch.int64, device=dev)
+    dist.broadcast(n, src=src)
+    buf = torch.empty(int(n.item()), dtype=torch.uint8, device=dev)
+    if ctx.rank == src and int(n.item()):
+        buf.copy_(torch.frombuffer(bytearray(payload), dtype=torch.uint8).to(dev))
+    if int(n.item()):
+        dist.broadcast(buf, src=src)
+    raw = bytes(buf.cpu().numpy().tobytes())
+    out, off = [], 0
+    while off < len(raw):
+        ln = int.from_bytes(raw[off: off + 4], "little")
+        out.append(ServingMessage.unpack(raw[off + 4: off + 4 + ln]))
+        off += 4 + ln
+    return out
+
+
+# --------------------------------------------------------------------------- sink
+
+
+def all_gather_scores(score: torch.Tensor, valid: torch.Tensor, ctx: DistContext, async_op: bool = False,
+                      out: Optional[Tuple[torch.Tensor, torch.Tensor]] = None):
+    """All-gather equally sized per-rank score/valid shards (F5). Returns ``(scores, valid, work)``
+    with ``work`` a list of handles when ``async_op`` (wait before reading)."""
+    if not ctx.is_distributed:
+        return score, valid, []
+    n = score.shape[0]
+    if out is None:
+        gs = torch.empty(n * ctx.world_size, dtype=score.dtype, device=score.device)
+        gv = torch.empty(n * ctx.world_size, dtype=valid.dtype, device=valid.device)
+    else:
+        gs, gv = out
+    w1 = dist.all_gather_into_tensor(gs, score.contiguous(), async_op=async_op)
+    w2 = dist.all_gather_into_tensor(gv, valid.contiguous(), async_op=async_op)
+    return gs, gv, ([w1, w2] if async_op else [])
+
+
+def all_gather_varlen(t: torch.Tensor, ctx: DistContext) -> torch.Tensor:
+    """All-gather shards of different lengths (pads to the max, then trims)."""
+    if not ctx.is_distributed:
+        return t
+    n = torch.tensor([t.shape[0]], dtype=torch.int64, device=t.device)
+    sizes = [torch.zeros_like(n) for _ in range(ctx.world_size)]
+    dist.all_gather(sizes, n)
+    sizes_i = [int(s.item()) for s in sizes]
+    m = max(sizes_i)
+    pad = torch.zeros((m,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+    pad[: t.shape[0]] = t
+    out = torch.empty((m * ctx.world_size,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+    dist.all_gather_into_tensor(out, pad)
+    parts = [out[i * m: i * m + s] for i, s in enumerate(sizes_i)]
+    return torch.cat(parts)

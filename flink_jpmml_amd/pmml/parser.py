@@ -1,0 +1,622 @@
+"""Namespace-agnostic PMML 3.x/4.x XML parser producing :mod:`flink_jpmml_amd.pmml.ir`.
+
+The reference parses with JAXB behind an ``ImportFilter`` that rewrites every PMML 3.x/4.x
+namespace to the latest one (`S/api/PmmlModel.scala:53-61`). We get the same effect by ignoring
+namespaces altogether: every tag is matched on its local name, so ``PMML-3_2`` … ``PMML-4_4``
+documents (and documents with no namespace) parse identically.
+
+Parsing uses the C-accelerated ``xml.etree.ElementTree``; for very large ensembles
+(hundreds of MB, `README.md:241-242`) :func:`parse_file` streams the file from disk.
+"""
+
+from __future__ import annotations
+
+import re
+import shlex
+import xml.etree.ElementTree as ET
+from typing import Callable, Dict, Iterable, List, Optional
+
+from ..api.exceptions import PmmlParseError, UnsupportedFeatureException
+from . import ir
+
+# --------------------------------------------------------------------------- helpers
+
+
+def _local(tag: str) -> str:
+    if not isinstance(tag, str):  # comments / processing instructions
+        return ""
+    return tag.rsplit("}", 1)[-1]
+
+
+def _children(el: ET.Element, name: Optional[str] = None) -> List[ET.Element]:
+    out = []
+    for c in el:
+        ln = _local(c.tag)
+        if not ln or ln == "Extension":
+            continue
+        if name is None or ln == name:
+            out.append(c)
+    return out
+
+
+def _child(el: ET.Element, name: str) -> Optional[ET.Element]:
+    for c in el:
+        if _local(c.tag) == name:
+            return c
+    return None
+
+
+def _f(el: ET.Element, attr: str, default: Optional[float] = None) -> Optional[float]:
+    v = el.get(attr)
+    if v is None:
+        return default
+    try:
+        return float(v)
+    except ValueError as e:
+        raise PmmlParseError(f"attribute {attr}={v!r} of <{_local(el.tag)}> is not a number") from e
+
+
+def _parse_array(el: ET.Element) -> List[str]:
+    """``<Array type="real|int|string">`` (and the legacy ``REAL-ARRAY``/``NUM-ARRAY``/``INT-ARRAY``)."""
+    text = (el.text or "").strip()
+    if not text:
+        return []
+    atype = el.get("type", "real")
+    if atype == "string" or '"' in text:
+        lex = shlex.shlex(text, posix=True)
+        lex.whitespace_split = True
+        lex.escapedquotes = '"\\'
+        lex.quotes = '"'
+        return list(lex)
+    return text.split()
+
+
+def _parse_sparse(el: ET.Element) -> List[float]:
+    n = int(el.get("n", "0"))
+    idx_el = _child(el, "Indices")
+    ent_el = _child(el, "REAL-Entries") or _child(el, "INT-Entries") or _child(el, "Entries")
+    out = [0.0] * n
+    if idx_el is not None and ent_el is not None:
+        idx = [int(x) for x in (idx_el.text or "").split()]
+        ent = [float(x) for x in (ent_el.text or "").split()]
+        if len(idx) != len(ent):
+            raise PmmlParseError("sparse array: Indices/Entries length mismatch")
+        if n == 0 and idx:
+            out = [0.0] * max(idx)
+        for i, v in zip(idx, ent):
+            out[i - 1] = v  # PMML sparse indices are 1-based
+    return out
+
+
+def _numeric_array(el: ET.Element) -> List[float]:
+    ln = _local(el.tag)
+    if ln.endswith("SparseArray"):
+        return _parse_sparse(el)
+    return [float(x) for x in _parse_array(el)]
+
+
+def _find_array(el: ET.Element) -> Optional[ET.Element]:
+    for c in el:
+        ln = _local(c.tag)
+        if ln in ("Array", "REAL-ARRAY", "NUM-ARRAY", "INT-ARRAY") or ln.endswith("SparseArray"):
+            return c
+    return None
+
+
+# --------------------------------------------------------------------------- dictionary
+
+
+def _parse_interval(el: ET.Element) -> ir.Interval:
+    return ir.Interval(el.get("closure", "closedClosed"), _f(el, "leftMargin"), _f(el, "rightMargin"))
+
+
+def _parse_data_field(el: ET.Element) -> ir.DataField:
+    df = ir.DataField(
+        name=el.get("name"),
+        optype=el.get("optype", "continuous"),
+        data_type=el.get("dataType", "double"),
+        display_name=el.get("displayName"),
+    )
+    for v in _children(el, "Value"):
+        prop = v.get("property", "valid")
+        val = v.get("value")
+        if prop == "valid":
+            df.values.append(val)
+        elif prop == "invalid":
+            df.invalid_values.append(val)
+        elif prop == "missing":
+            df.missing_values.append(val)
+    df.intervals = [_parse_interval(i) for i in _children(el, "Interval")]
+    return df
+
+
+def _parse_mining_schema(el: Optional[ET.Element]) -> ir.MiningSchema:
+    ms = ir.MiningSchema()
+    if el is None:
+        return ms
+    for mf in _children(el, "MiningField"):
+        ivt = mf.get("invalidValueTreatment", "returnInvalid")
+        ms.fields.append(
+            ir.MiningField(
+                name=mf.get("name"),
+                usage_type=mf.get("usageType", "active"),
+                optype=mf.get("optype"),
+                invalid_value_treatment=ivt,
+                invalid_value_replacement=mf.get("invalidValueReplacement"),
+                missing_value_replacement=mf.get("missingValueReplacement"),
+                missing_value_treatment=mf.get("missingValueTreatment"),
+                outliers=mf.get("outliers", "asIs"),
+                low_value=_f(mf, "lowValue"),
+                high_value=_f(mf, "highValue"),
+                importance=_f(mf, "importance"),
+            )
+        )
+    return ms
+
+
+# --------------------------------------------------------------------------- expressions
+
+_EXPRESSIONS = ("Constant", "FieldRef", "NormContinuous", "NormDiscrete", "Discretize", "MapValues", "Apply",
+                "Aggregate", "TextIndex", "Lag")
+
+
+def _find_expression(el: ET.Element) -> Optional[ET.Element]:
+    for c in el:
+        if _local(c.tag) in _EXPRESSIONS:
+            return c
+    return None
+
+
+def _parse_expression(el: ET.Element) -> ir.Expression:
+    ln = _local(el.tag)
+    if ln == "Constant":
+        return ir.Constant(
+            value=(el.text or "").strip() if el.text is not None else None,
+            data_type=el.get("dataType"),
+            missing=el.get("missing", "false") == "true",
+        )
+    if ln == "FieldRef":
+        return ir.FieldRef(el.get("field"), el.get("mapMissingTo"))
+    if ln == "NormContinuous":
+        norms = [ir.LinearNorm(float(n.get("orig")), float(n.get("norm"))) for n in _children(el, "LinearNorm")]
+        return ir.NormContinuous(el.get("field"), norms, el.get("outliers", "asIs"), _f(el, "mapMissingTo"))
+    if ln == "NormDiscrete":
+        return ir.NormDiscrete(el.get("field"), el.get("value"), _f(el, "mapMissingTo"))
+    if ln == "Discretize":
+        bins = []
+        for b in _children(el, "DiscretizeBin"):
+            iv = _child(b, "Interval")
+            bins.append(ir.DiscretizeBin(b.get("binValue"), _parse_interval(iv)))
+        return ir.Discretize(el.get("field"), bins, el.get("mapMissingTo"), el.get("defaultValue"), el.get("dataType"))
+    if ln == "MapValues":
+        cols = [(fc.get("field"), fc.get("column")) for fc in _children(el, "FieldColumnPair")]
+        rows: List[Dict[str, str]] = []
+        table = _child(el, "InlineTable")
+        if table is not None:
+            for row in _children(table, "row"):
+                rows.append({_local(c.tag): (c.text or "").strip() for c in row if _local(c.tag)})
+        return ir.MapValues(el.get("outputColumn"), cols, rows, el.get("mapMissingTo"), el.get("defaultValue"),
+                            el.get("dataType"))
+    if ln == "Apply":
+        args = [_parse_expression(c) for c in el if _local(c.tag) in _EXPRESSIONS]
+        return ir.Apply(el.get("function"), args, el.get("mapMissingTo"), el.get("defaultValue"),
+                        el.get("invalidValueTreatment", "returnInvalid"))
+    raise UnsupportedFeatureException(f"expression <{ln}> is not supported")
+
+
+def _parse_derived_field(el: ET.Element) -> ir.DerivedField:
+    ex = _find_expression(el)
+    if ex is None:
+        raise PmmlParseError(f"DerivedField {el.get('name')!r} has no expression")
+    return ir.DerivedField(
+        name=el.get("name"),
+        optype=el.get("optype"),
+        data_type=el.get("dataType"),
+        expression=_parse_expression(ex),
+        values=[v.get("value") for v in _children(el, "Value")],
+    )
+
+
+def _parse_transformations(el: Optional[ET.Element]) -> List[ir.DerivedField]:
+    if el is None:
+        return []
+    return [_parse_derived_field(d) for d in _children(el, "DerivedField")]
+
+
+# --------------------------------------------------------------------------- predicates
+
+
+def _parse_predicate(el: ET.Element) -> ir.Predicate:
+    ln = _local(el.tag)
+    if ln == "True":
+        return ir.TruePredicate()
+    if ln == "False":
+        return ir.FalsePredicate()
+    if ln == "SimplePredicate":
+        return ir.SimplePredicate(el.get("field"), el.get("operator"), el.get("value"))
+    if ln == "SimpleSetPredicate":
+        arr = _find_array(el)
+        values = _parse_array(arr) if arr is not None else []
+        return ir.SimpleSetPredicate(el.get("field"), el.get("booleanOperator"), values)
+    if ln == "CompoundPredicate":
+        preds = [_parse_predicate(c) for c in el if _local(c.tag) in _PREDICATES]
+        return ir.CompoundPredicate(el.get("booleanOperator"), preds)
+    raise UnsupportedFeatureException(f"predicate <{ln}> is not supported")
+
+
+_PREDICATES = ("True", "False", "SimplePredicate", "SimpleSetPredicate", "CompoundPredicate")
+
+
+def _find_predicate(el: ET.Element) -> ir.Predicate:
+    for c in el:
+        if _local(c.tag) in _PREDICATES:
+            return _parse_predicate(c)
+    raise PmmlParseError(f"<{_local(el.tag)}> has no predicate")
+
+
+# --------------------------------------------------------------------------- output / targets
+
+
+def _parse_output(el: Optional[ET.Element]) -> List[ir.OutputField]:
+    if el is None:
+        return []
+    out = []
+    for of in _children(el, "OutputField"):
+        ex = _find_expression(of)
+        out.append(
+            ir.OutputField(
+                name=of.get("name"),
+                optype=of.get("optype"),
+                data_type=of.get("dataType"),
+                target_field=of.get("targetField"),
+                feature=of.get("feature", "predictedValue"),
+                value=of.get("value"),
+                segment_id=of.get("segmentId"),
+                rank=int(of.get("rank", "1")),
+                is_final_result=of.get("isFinalResult", "true") == "true",
+                expression=_parse_expression(ex) if ex is not None else None,
+            )
+        )
+    return out
+
+
+def _parse_targets(el: Optional[ET.Element]) -> List[ir.Target]:
+    if el is None:
+        return []
+    out = []
+    for t in _children(el, "Target"):
+        tv = [
+            ir.TargetValue(v.get("value"), v.get("displayValue"), _f(v, "priorProbability"), _f(v, "defaultValue"))
+            for v in _children(t, "TargetValue")
+        ]
+        out.append(
+            ir.Target(
+                field=t.get("field"),
+                optype=t.get("optype"),
+                cast_integer=t.get("castInteger"),
+                min=_f(t, "min"),
+                max=_f(t, "max"),
+                rescale_factor=_f(t, "rescaleFactor", 1.0),
+                rescale_constant=_f(t, "rescaleConstant", 0.0),
+                values=tv,
+            )
+        )
+    return out
+
+
+def _common(el: ET.Element) -> dict:
+    return dict(
+        element=_local(el.tag),
+        model_name=el.get("modelName"),
+        function_name=el.get("functionName", ""),
+        mining_schema=_parse_mining_schema(_child(el, "MiningSchema")),
+        output=_parse_output(_child(el, "Output")),
+        targets=_parse_targets(_child(el, "Targets")),
+        local_transformations=_parse_transformations(_child(el, "LocalTransformations")),
+        is_scorable=el.get("isScorable", "true") == "true",
+        algorithm_name=el.get("algorithmName"),
+    )
+
+
+# --------------------------------------------------------------------------- model parsers
+
+
+def _parse_clustering(el: ET.Element) -> ir.ClusteringModel:
+    m = ir.ClusteringModel(**_common(el))
+    m.model_class = el.get("modelClass", "centerBased")
+    cm = _child(el, "ComparisonMeasure")
+    if cm is None:
+        raise PmmlParseError("ClusteringModel without ComparisonMeasure")
+    m.measure_kind = cm.get("kind", "distance")
+    m.compare_function = cm.get("compareFunction", "absDiff")
+    metric_el = None
+    for c in cm:
+        if _local(c.tag) and _local(c.tag) != "Extension":
+            metric_el = c
+            break
+    if metric_el is None:
+        raise PmmlParseError("ComparisonMeasure without a metric")
+    m.metric = _local(metric_el.tag)
+    if m.metric == "minkowski":
+        m.minkowski_p = _f(metric_el, "p-parameter", 2.0)
+    for cf in _children(el, "ClusteringField"):
+        m.fields.append(
+            ir.ClusteringField(
+                field=cf.get("field"),
+                weight=_f(cf, "fieldWeight", 1.0),
+                compare_function=cf.get("compareFunction"),
+                similarity_scale=_f(cf, "similarityScale"),
+                is_center_field=cf.get("isCenterField", "true") == "true",
+            )
+        )
+    mvw = _child(el, "MissingValueWeights")
+    if mvw is not None:
+        arr = _find_array(mvw)
+        m.missing_value_weights = _numeric_array(arr) if arr is not None else None
+    for c in _children(el, "Cluster"):
+        arr = _find_array(c)
+        center = _numeric_array(arr) if arr is not None else []
+        size = c.get("size")
+        m.clusters.append(ir.Cluster(c.get("name"), c.get("id"), center, int(size) if size else None))
+    if m.model_class != "centerBased":
+        raise UnsupportedFeatureException("only centerBased ClusteringModel is supported")
+    return m
+
+
+def _parse_node(el: ET.Element) -> ir.Node:
+    node = ir.Node(
+        id=el.get("id"),
+        score=el.get("score"),
+        predicate=_find_predicate(el),
+        record_count=_f(el, "recordCount"),
+        default_child=el.get("defaultChild"),
+    )
+    for c in el:
+        ln = _local(c.tag)
+        if ln == "Node":
+            node.children.append(_parse_node(c))
+        elif ln == "ScoreDistribution":
+            node.distributions.append(
+                ir.ScoreDistribution(c.get("value"), float(c.get("recordCount", "0")), _f(c, "probability"),
+                                     _f(c, "confidence"))
+            )
+        elif ln in ("Regression", "DecisionTree"):
+            raise UnsupportedFeatureException("embedded models inside tree nodes are not supported")
+    return node
+
+
+def _parse_tree(el: ET.Element) -> ir.TreeModel:
+    m = ir.TreeModel(**_common(el))
+    root = _child(el, "Node")
+    if root is None:
+        raise PmmlParseError("TreeModel without root Node")
+    m.root = _parse_node(root)
+    m.missing_value_strategy = el.get("missingValueStrategy", "none")
+    m.missing_value_penalty = _f(el, "missingValuePenalty", 1.0)
+    m.no_true_child_strategy = el.get("noTrueChildStrategy", "returnNullPrediction")
+    m.split_characteristic = el.get("splitCharacteristic", "multiSplit")
+    return m
+
+
+def _parse_mining(el: ET.Element) -> ir.MiningModel:
+    m = ir.MiningModel(**_common(el))
+    seg = _child(el, "Segmentation")
+    if seg is None:
+        raise PmmlParseError("MiningModel without Segmentation")
+    m.multiple_model_method = seg.get("multipleModelMethod")
+    m.missing_prediction_treatment = seg.get("missingPredictionTreatment", "continue")
+    m.missing_threshold = _f(seg, "missingThreshold", 1.0)
+    for s in _children(seg, "Segment"):
+        sub = None
+        for c in s:
+            if _local(c.tag) in MODEL_PARSERS:
+                sub = parse_model_element(c)
+                break
+        if sub is None:
+            raise UnsupportedFeatureException(f"segment {s.get('id')!r} holds no supported model")
+        m.segments.append(ir.Segment(s.get("id"), _f(s, "weight", 1.0), _find_predicate(s), sub))
+    return m
+
+
+def _parse_regression(el: ET.Element) -> ir.RegressionModel:
+    m = ir.RegressionModel(**_common(el))
+    m.normalization_method = el.get("normalizationMethod", "none")
+    for t in _children(el, "RegressionTable"):
+        tab = ir.RegressionTable(intercept=_f(t, "intercept", 0.0), target_category=t.get("targetCategory"))
+        for c in t:
+            ln = _local(c.tag)
+            if ln == "NumericPredictor":
+                tab.numeric.append(ir.NumericPredictor(c.get("name"), float(c.get("coefficient")),
+                                                       _f(c, "exponent", 1.0)))
+            elif ln == "CategoricalPredictor":
+                tab.categorical.append(ir.CategoricalPredictor(c.get("name"), c.get("value"),
+                                                               float(c.get("coefficient"))))
+            elif ln == "PredictorTerm":
+                tab.terms.append(ir.PredictorTerm([fr.get("field") for fr in _children(c, "FieldRef")],
+                                                  float(c.get("coefficient"))))
+        m.tables.append(tab)
+    return m
+
+
+def _parse_general_regression(el: ET.Element) -> ir.GeneralRegressionModel:
+    m = ir.GeneralRegressionModel(**_common(el))
+    m.model_type = el.get("modelType", "regression")
+    m.link_function = el.get("linkFunction")
+    m.link_power = _f(el, "linkParameter")
+    m.distribution = el.get("distribution")
+    m.offset_value = _f(el, "offsetValue", 0.0)
+    m.target_reference_category = el.get("targetReferenceCategory")
+    pl = _child(el, "ParameterList")
+    if pl is not None:
+        m.parameters = [p.get("name") for p in _children(pl, "Parameter")]
+    fl = _child(el, "FactorList")
+    if fl is not None:
+        m.factors = [p.get("name") for p in _children(fl, "Predictor")]
+    cl = _child(el, "CovariateList")
+    if cl is not None:
+        m.covariates = [p.get("name") for p in _children(cl, "Predictor")]
+    pp = _child(el, "PPMatrix")
+    if pp is not None:
+        m.pp_cells = [(c.get("predictorName"), c.get("parameterName"), c.get("value")) for c in _children(pp, "PPCell")]
+    pm = _child(el, "ParamMatrix")
+    if pm is not None:
+        m.p_cells = [(c.get("parameterName"), c.get("targetCategory"), float(c.get("beta")))
+                     for c in _children(pm, "PCell")]
+    return m
+
+
+def _parse_neural(el: ET.Element) -> ir.NeuralNetwork:
+    m = ir.NeuralNetwork(**_common(el))
+    m.activation = el.get("activationFunction", "logistic")
+    m.normalization = el.get("normalizationMethod", "none")
+    m.threshold = _f(el, "threshold", 0.0)
+    m.width = _f(el, "width")
+    m.altitude = _f(el, "altitude", 1.0)
+    ni = _child(el, "NeuralInputs")
+    if ni is not None:
+        for inp in _children(ni, "NeuralInput"):
+            m.inputs.append(ir.NeuralInput(inp.get("id"), _parse_derived_field(_child(inp, "DerivedField"))))
+    for layer in _children(el, "NeuralLayer"):
+        neurons = []
+        for n in _children(layer, "Neuron"):
+            cons = [(c.get("from"), float(c.get("weight"))) for c in _children(n, "Con")]
+            neurons.append(ir.Neuron(n.get("id"), _f(n, "bias", 0.0), _f(n, "width"), _f(n, "altitude"), cons))
+        m.layers.append(
+            ir.NeuralLayer(neurons, layer.get("activationFunction"), _f(layer, "threshold"), _f(layer, "width"),
+                           _f(layer, "altitude"), layer.get("normalizationMethod"))
+        )
+    no = _child(el, "NeuralOutputs")
+    if no is not None:
+        for out in _children(no, "NeuralOutput"):
+            m.outputs.append(ir.NeuralOutput(out.get("outputNeuron"), _parse_derived_field(_child(out, "DerivedField"))))
+    return m
+
+
+def _parse_svm(el: ET.Element) -> ir.SupportVectorMachineModel:
+    m = ir.SupportVectorMachineModel(**_common(el))
+    m.representation = el.get("svmRepresentation", "SupportVectors")
+    m.classification_method = el.get("classificationMethod", "OneAgainstAll")
+    m.threshold = _f(el, "threshold", 0.0)
+    m.max_wins = el.get("maxWins", "false") == "true"
+    kern = None
+    for kname in ("LinearKernelType", "PolynomialKernelType", "RadialBasisKernelType", "SigmoidKernelType"):
+        k = _child(el, kname)
+        if k is not None:
+            kind = {"LinearKernelType": "linear", "PolynomialKernelType": "polynomial",
+                    "RadialBasisKernelType": "radialBasis", "SigmoidKernelType": "sigmoid"}[kname]
+            kern = ir.SvmKernel(kind, _f(k, "gamma", 1.0), _f(k, "coef0", 1.0), _f(k, "degree", 1.0))
+            break
+    if kern is None:
+        raise PmmlParseError("SupportVectorMachineModel without kernel type")
+    m.kernel = kern
+    vd = _child(el, "VectorDictionary")
+    if vd is not None:
+        vf = _child(vd, "VectorFields")
+        if vf is not None:
+            m.vector_fields = [c.get("field") for c in vf if _local(c.tag) == "FieldRef"]
+        for vi in _children(vd, "VectorInstance"):
+            arr = _find_array(vi)
+            m.vectors[vi.get("id")] = _numeric_array(arr) if arr is not None else []
+    for svm in _children(el, "SupportVectorMachine"):
+        svs = _child(svm, "SupportVectors")
+        ids = [s.get("vectorId") for s in _children(svs, "SupportVector")] if svs is not None else []
+        co = _child(svm, "Coefficients")
+        coefs = [float(c.get("value", "0")) for c in _children(co, "Coefficient")] if co is not None else []
+        intercept = _f(co, "absoluteValue", 0.0) if co is not None else 0.0
+        m.machines.append(
+            ir.SupportVectorMachine(svm.get("targetCategory"), svm.get("alternateTargetCategory"),
+                                    _f(svm, "threshold"), ids, coefs, intercept)
+        )
+    return m
+
+
+MODEL_PARSERS: Dict[str, Callable[[ET.Element], ir.Model]] = {
+    "ClusteringModel": _parse_clustering,
+    "TreeModel": _parse_tree,
+    "MiningModel": _parse_mining,
+    "RegressionModel": _parse_regression,
+    "GeneralRegressionModel": _parse_general_regression,
+    "NeuralNetwork": _parse_neural,
+    "SupportVectorMachineModel": _parse_svm,
+}
+
+_KNOWN_UNSUPPORTED = ("AssociationModel", "BaselineModel", "BayesianNetworkModel", "GaussianProcessModel",
+                      "NaiveBayesModel", "NearestNeighborModel", "RuleSetModel", "Scorecard", "SequenceModel",
+                      "TextModel", "TimeSeriesModel", "AnomalyDetectionModel")
+
+
+def parse_model_element(el: ET.Element) -> ir.Model:
+    ln = _local(el.tag)
+    p = MODEL_PARSERS.get(ln)
+    if p is None:
+        raise UnsupportedFeatureException(f"model type <{ln}> is not supported")
+    return p(el)
+
+
+# --------------------------------------------------------------------------- document
+
+_VERSION_RE = re.compile(r"PMML-(\d)_(\d)")
+
+
+def parse_element(root: ET.Element) -> ir.PMMLDocument:
+    if _local(root.tag) != "PMML":
+        raise PmmlParseError(f"root element is <{_local(root.tag)}>, expected <PMML>")
+    version = root.get("version")
+    if version is None:
+        m = _VERSION_RE.search(root.tag)
+        version = f"{m.group(1)}.{m.group(2)}" if m else "4.4"
+    header: dict = {}
+    h = _child(root, "Header")
+    if h is not None:
+        header = dict(h.attrib)
+        app = _child(h, "Application")
+        if app is not None:
+            header["application"] = dict(app.attrib)
+    dd = _child(root, "DataDictionary")
+    data_fields: Dict[str, ir.DataField] = {}
+    if dd is not None:
+        for f in _children(dd, "DataField"):
+            df = _parse_data_field(f)
+            data_fields[df.name] = df
+    trans = _parse_transformations(_child(root, "TransformationDictionary"))
+    models: List[ir.Model] = []
+    for c in root:
+        ln = _local(c.tag)
+        if ln in MODEL_PARSERS:
+            models.append(parse_model_element(c))
+        elif ln in _KNOWN_UNSUPPORTED:
+            raise UnsupportedFeatureException(f"model type <{ln}> is not supported")
+    if not models:
+        raise PmmlParseError("PMML document contains no model element")
+    return ir.PMMLDocument(version=version, data_fields=data_fields, transformations=trans, models=models,
+                           header=header)
+
+
+def parse_string(text: str) -> ir.PMMLDocument:
+    """Parse a PMML document held in memory (the reference reads the whole file into a String
+    first: `S/api/reader/FsReader.scala:41-49`)."""
+    if isinstance(text, bytes):
+        text = text.decode("utf-8")
+    try:
+        root = ET.fromstring(text)
+    except ET.ParseError as e:
+        raise PmmlParseError(f"malformed PMML XML: {e}") from e
+    return parse_element(root)
+
+
+def parse_file(path: str) -> ir.PMMLDocument:
+    try:
+        tree = ET.parse(path)
+    except ET.ParseError as e:
+        raise PmmlParseError(f"malformed PMML XML in {path}: {e}") from e
+    return parse_element(tree.getroot())
+
+
+def iter_models(doc: ir.PMMLDocument) -> Iterable[ir.Model]:
+    """Depth-first walk over every model element (including nested segment models)."""
+    stack = list(reversed(doc.models))
+    while stack:
+        m = stack.pop()
+        yield m
+        if isinstance(m, ir.MiningModel):
+            stack.extend(reversed([s.model for s in m.segments]))

@@ -1,0 +1,138 @@
+"""Pipelined micro-batch scoring engine (host records → GPU → host predictions).
+
+The reference scores one record at a time on the JVM (`S/package.scala:76-79`). Here a stream of
+records is scored in micro-batches through a three-stage pipeline on three HIP streams:
+
+    H2D stream:   pinned host slice ──copy──▶ device input slot[i % depth]
+    compute:      wait(H2D[i]) ▶ fused prepare + model kernel ▶ device score/valid (step buffer)
+    D2H stream:   wait(compute[i]) ▶ score/valid slice ──copy──▶ pinned host output
+
+A ring of ``depth`` device input slots lets batch i+1's copy overlap batch i's kernel and batch
+i-1's copy-back. Nothing in :meth:`StreamingScorer.submit` blocks the host; :meth:`wait` is the
+only synchronisation point. PCIe Gen5 (≈50+ GB/s per GPU) is the usual bound for wide fp32
+records; the kernels themselves run far below it (see ``profiles/``).
+"""
+
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass
+from typing import List, Optional
+
+import numpy as np
+
+
+@dataclass
+class StepHandle:
+    n: int
+    done: object  # torch.cuda.Event recorded on the D2H stream
+
+
+class StreamingScorer:
+    def __init__(self, plan, micro_batch: int = 131072, depth: int = 3, max_rows: Optional[int] = None):
+        import torch
+
+        self.plan = plan
+        self.device = plan.device
+        self.F = plan.n_features
+        self.B = int(micro_batch)
+        self.depth = int(depth)
+        self.h2d = torch.cuda.Stream(self.device)
+        self.comp = torch.cuda.Stream(self.device)
+        self.d2h = torch.cuda.Stream(self.device)
+        self.x_slots = [torch.empty((self.B, self.F), dtype=torch.float32, device=self.device)
+                        for _ in range(self.depth)]
+        self.ev_h2d = [torch.cuda.Event() for _ in range(self.depth)]
+        self.ev_comp = [torch.cuda.Event() for _ in range(self.depth)]
+        self.ev_free = [torch.cuda.Event() for _ in range(self.depth)]
+        self._used = [False] * self.depth
+        self._last_out = None  # event: previous submit's consumers of score_dev are done
+        self.max_rows = max_rows or self.B
+        self.score_dev = torch.empty(self.max_rows, dtype=torch.float32, device=self.device)
+        self.valid_dev = torch.empty(self.max_rows, dtype=torch.uint8, device=self.device)
+        self.batch_times_ms: List[float] = []
+
+    def ensure_capacity(self, n: int) -> None:
+        import torch
+
+        if n > self.max_rows:
+            self.max_rows = n
+            self.score_dev = torch.empty(n, dtype=torch.float32, device=self.device)
+            self.valid_dev = torch.empty(n, dtype=torch.uint8, device=self.device)
+
+    def submit(self, X_host, score_host=None, valid_host=None, offset: int = 0) -> StepHandle:
+        """Enqueue scoring of a pinned host matrix ``X_host`` ([n, F] float32 tensor). Scores land in
+        ``self.score_dev[offset: offset+n]`` and, if given, in the pinned host outputs."""
+        import torch
+
+        n = int(X_host.shape[0])
+        self.ensure_capacity(offset + n)
+        if self._last_out is not None:
+            # WAR on the step output buffer: the previous step's copy-back must be done
+            self.comp.wait_event(self._last_out)
+        slot = 0
+        for i, s in enumerate(range(0, n, self.B)):
+            e = min(n, s + self.B)
+            m = e - s
+            slot = i % self.depth
+            with torch.cuda.stream(self.h2d):
+                if self._used[slot]:
+                    self.h2d.wait_event(self.ev_comp[slot])  # kernel finished reading this slot
+                xs = self.x_slots[slot][:m]
+                xs.copy_(X_host[s:e], non_blocking=True)
+                self.ev_h2d[slot].record(self.h2d)
+            with torch.cuda.stream(self.comp):
+                self.comp.wait_event(self.ev_h2d[slot])
+                self.plan.launch(xs, self.score_dev[offset + s: offset + e], self.valid_dev[offset + s: offset + e],
+                                 stream=self.comp)
+                self.ev_comp[slot].record(self.comp)
+            self._used[slot] = True
+            if score_host is not None:
+                with torch.cuda.stream(self.d2h):
+                    self.d2h.wait_event(self.ev_comp[slot])
+                    score_host[s:e].copy_(self.score_dev[offset + s: offset + e], non_blocking=True)
+                    if valid_host is not None:
+                        valid_host[s:e].copy_(self.valid_dev[offset + s: offset + e], non_blocking=True)
+        done = torch.cuda.Event()
+        if score_host is not None:
+            done.record(self.d2h)
+        else:
+            done.record(self.comp)
+        self._last_out = done
+        return StepHandle(n, done)
+
+    def mark_consumed(self, stream) -> None:
+        """Declare that ``stream`` reads the step outputs (e.g. an all-gather): the next submit
+        waits for it before overwriting them."""
+        import torch
+
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        self._last_out = ev
+
+    def join(self, stream=None) -> None:
+        """Make ``stream`` (default: current) wait for all work submitted so far (no host sync)."""
+        import torch
+
+        s = stream or torch.cuda.current_stream(self.device)
+        for st in (self.h2d, self.comp, self.d2h):
+            ev = torch.cuda.Event()
+            ev.record(st)
+            s.wait_event(ev)
+
+    @staticmethod
+    def wait(handle: StepHandle) -> None:
+        handle.done.synchronize()
+
+    def score_numpy(self, X: np.ndarray) -> tuple:
+        """Blocking convenience: score a host numpy matrix, return numpy ``(score, valid)``."""
+        import torch
+
+        Xp = torch.from_numpy(np.ascontiguousarray(X, dtype=np.float32)).pin_memory()
+        sh = torch.empty(X.shape[0], dtype=torch.float32).pin_memory()
+        vh = torch.empty(X.shape[0], dtype=torch.uint8).pin_memory()
+        t0 = time.perf_counter()
+        h = self.submit(Xp, sh, vh)
+        self.wait(h)
+        self.batch_times_ms.append((time.perf_counter() - t0) * 1e3)
+        return sh.numpy().copy(), vh.numpy().astype(bool)

@@ -1,0 +1,765 @@
+"""Device plans: lowering of a :class:`CompiledPmml` into HIP-kernel operands on one GPU.
+
+A plan owns device-resident model tensors (tree blobs, centres, weights, field-preparation
+table) and exposes
+
+* :meth:`DevicePlan.launch` — enqueue scoring of a device ``[rows, F]`` fp32 matrix on a HIP
+  stream, writing ``score`` (fp32) and ``valid`` (u8) — no host synchronisation, graph-capturable;
+* :meth:`DevicePlan.score` — convenience host/device entry point.
+
+Numerics: inputs are fp32 on the device. Every fp64 constant that is compared against an input
+(split thresholds, validity intervals) is rounded *directionally* to fp32 so the fp32 comparison
+gives exactly the fp64 answer for any fp32 input (``_ceil32``/``_floor32``/``_next_up``).
+Accumulations (tree sums, dot products) run in fp32; the parity tolerance against the float64
+oracle is documented per test.
+"""
+
+from __future__ import annotations
+
+import logging
+import math
+from dataclasses import dataclass
+from typing import Any, List, Optional, Tuple
+
+import numpy as np
+
+from ..api.exceptions import UnsupportedFeatureException
+from ..models.clustering import ClusteringEvaluator
+from ..models.mining import MiningEvaluator
+from ..models.regression import RegressionEvaluator
+from ..models.tree import OP_GE, OP_GT, OP_LE, OP_LT, BinaryTree, NotBinary, TreeEvaluator, lower_binary_tree
+from ..pmml import ir
+
+logger = logging.getLogger(__name__)
+
+TB = 256  # rows per workgroup of every row-tile kernel (mirrors csrc)
+
+# FieldPrep flag bits (mirror of csrc/common.h)
+FP_HAS_MISSING_REPL = 1 << 0
+FP_HAS_INTERVAL = 1 << 1
+FP_LO_OPEN = 1 << 2
+FP_HI_OPEN = 1 << 3
+FP_INVALID_RETURN = 1 << 4
+FP_INVALID_AS_MISSING = 1 << 5
+FP_INVALID_AS_VALUE = 1 << 6
+FP_OUTLIER_AS_MISSING = 1 << 7
+FP_OUTLIER_AS_EXTREME = 1 << 8
+FP_INTEGER = 1 << 9
+FP_CODE_RANGE = 1 << 10
+FP_ROW_INVALID = 1 << 11
+
+EPI_AFFINE, EPI_LOGISTIC2, EPI_ARGMAX, EPI_SOFTMAX = 0, 1, 2, 3
+LINKS = {"none": 0, None: 0, "logit": 1, "exp": 2, "probit": 3, "cloglog": 4, "loglog": 5, "cauchit": 6}
+
+
+class NotLowerable(UnsupportedFeatureException):
+    """The model (or one of its fields) uses a feature the device path does not implement."""
+
+
+# --------------------------------------------------------------------------- fp32 rounding
+
+
+def _f32(x: float) -> np.float32:
+    return np.float32(x)
+
+
+def _ceil32(t: float) -> float:
+    f = np.float32(t)
+    if np.isfinite(t) and float(f) < t:
+        f = np.nextafter(f, np.float32(np.inf))
+    return float(f)
+
+
+def _floor32(t: float) -> float:
+    f = np.float32(t)
+    if np.isfinite(t) and float(f) > t:
+        f = np.nextafter(f, np.float32(-np.inf))
+    return float(f)
+
+
+def _next_up32(f: float) -> float:
+    return float(np.nextafter(np.float32(f), np.float32(np.inf)))
+
+
+def canonical_threshold(op: int, t: float) -> Tuple[float, bool]:
+    """Return ``(T, swap)`` such that for every fp32 x: the original "go to first child" test
+    equals ``not (x >= T)`` when ``swap`` is False, or ``x >= T`` when ``swap`` is True."""
+    if op == OP_LT:  # left iff x < t  <=> right iff x >= t
+        return _ceil32(t), False
+    if op == OP_LE:  # left iff x <= t <=> right iff x > t <=> x >= nextup(floor32(t))
+        return _next_up32(_floor32(t)), False
+    if op == OP_GT:  # first iff x > t  -> first child goes RIGHT
+        return _next_up32(_floor32(t)), True
+    if op == OP_GE:  # first iff x >= t
+        return _ceil32(t), True
+    raise ValueError(op)
+
+
+# --------------------------------------------------------------------------- field preparation
+
+
+def build_field_prep(compiled, fields: List[str]) -> Tuple[np.ndarray, bool]:
+    """FieldPrep table (``[F, 8]`` as raw 32-bit words) for the active fields; second value tells
+    whether any field needs preparation at all."""
+    schema = compiled.schema
+    table = np.zeros((len(fields), 8), dtype=np.float32)
+    flags = np.zeros(len(fields), dtype=np.uint32)
+    any_prep = False
+    for j, name in enumerate(fields):
+        df = schema.data_fields.get(name)
+        mf = compiled.mining_fields.get(name)
+        fl = 0
+        lo, hi = -np.inf, np.inf
+        out_lo, out_hi = -np.inf, np.inf
+        mrepl = math.nan
+        irepl = math.nan
+        optype = (mf.optype if mf is not None and mf.optype else None) or (df.optype if df else "continuous")
+        constrained = False
+        if df is not None:
+            if optype != "continuous" and df.intervals:
+                fl |= FP_ROW_INVALID
+            if df.missing_values or df.invalid_values:
+                raise NotLowerable(f"field {name!r}: explicit missing/invalid value lists are host-only")
+            if optype == "continuous" and df.intervals:
+                if len(df.intervals) != 1:
+                    raise NotLowerable(f"field {name!r}: multiple validity intervals are host-only")
+                iv = df.intervals[0]
+                fl |= FP_HAS_INTERVAL
+                constrained = True
+                lo_open = not iv.closure.startswith("closed")
+                hi_open = not iv.closure.endswith("Closed")
+                if iv.left is not None:
+                    lo = _floor32(iv.left) if lo_open else _ceil32(iv.left)
+                if iv.right is not None:
+                    hi = _ceil32(iv.right) if hi_open else _floor32(iv.right)
+                fl |= (FP_LO_OPEN if lo_open else 0) | (FP_HI_OPEN if hi_open else 0)
+            elif df.values and df.is_string:
+                fl |= FP_CODE_RANGE
+                hi = float(len(df.values))
+                constrained = True
+            elif df.values:
+                raise NotLowerable(f"field {name!r}: numeric valid-value lists are host-only")
+            if df.data_type == "integer":
+                fl |= FP_INTEGER
+                constrained = True
+        if mf is not None:
+            if constrained:
+                t = mf.invalid_value_treatment
+                if t == "returnInvalid":
+                    fl |= FP_INVALID_RETURN
+                elif t == "asMissing":
+                    fl |= FP_INVALID_AS_MISSING
+                elif t == "asValue" and mf.invalid_value_replacement is not None:
+                    fl |= FP_INVALID_AS_VALUE
+                    irepl = schema.lookup(name, mf.invalid_value_replacement)
+            if optype == "continuous" and mf.outliers in ("asMissingValues", "asExtremeValues"):
+                fl |= FP_OUTLIER_AS_MISSING if mf.outliers == "asMissingValues" else FP_OUTLIER_AS_EXTREME
+                if mf.low_value is not None:
+                    out_lo = mf.low_value
+                if mf.high_value is not None:
+                    out_hi = mf.high_value
+            if mf.missing_value_replacement is not None:
+                fl |= FP_HAS_MISSING_REPL
+                mrepl = schema.lookup(name, mf.missing_value_replacement)
+        elif constrained:
+            fl |= FP_INVALID_RETURN
+        flags[j] = fl
+        table[j, 1:7] = [lo, hi, mrepl, irepl, out_lo, out_hi]
+        any_prep = any_prep or fl != 0
+    raw = table.view(np.uint32).copy()
+    raw[:, 0] = flags
+    return raw, any_prep
+
+
+# --------------------------------------------------------------------------- plan base
+
+
+class DevicePlan:
+    kind = "base"
+
+    def __init__(self, compiled, device):
+        import torch
+
+        from ..ops import _lib
+
+        self.compiled = compiled
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise ValueError(f"device plans need a cuda (HIP) device, got {self.device}")
+        self.lib = _lib.load()
+        self.n_features = compiled.n_features
+        prep, any_prep = build_field_prep(compiled, compiled.active_fields)
+        self.prep = torch.from_numpy(prep.view(np.int32)).to(self.device) if any_prep else None
+
+    # -- helpers
+    def _t(self, arr, dtype=None):
+        import torch
+
+        t = torch.as_tensor(np.ascontiguousarray(arr))
+        if dtype is not None:
+            t = t.to(dtype)
+        return t.to(self.device)
+
+    _STATE: Tuple[str, ...] = ("n_features", "prep")
+
+    def launch(self, X, score, valid, stream=None, probs=None) -> None:  # pragma: no cover - abstract
+        raise NotImplementedError
+
+    # -- replication (rank 0 lowers, other ranks receive the tensors over RCCL)
+    def export_state(self) -> Tuple[dict, dict]:
+        import torch
+
+        meta, tensors = {"__class__": type(self).__name__}, {}
+        for k in self._STATE:
+            v = getattr(self, k)
+            if isinstance(v, torch.Tensor):
+                tensors[k] = v
+            else:
+                meta[k] = v
+        meta["__tensors__"] = {k: (tuple(t.shape), str(t.dtype).replace("torch.", "")) for k, t in tensors.items()}
+        meta["__none__"] = [k for k in self._STATE if getattr(self, k) is None]
+        return meta, tensors
+
+    @staticmethod
+    def from_state(meta: dict, tensors: dict, device) -> "DevicePlan":
+        import torch
+
+        from ..ops import _lib
+
+        cls = {c.__name__: c for c in (TreePlan, ClusterPlan, LinearPlan)}.get(meta["__class__"])
+        if cls is None:
+            from . import nn_plans
+
+            cls = getattr(nn_plans, meta["__class__"])
+        obj = cls.__new__(cls)
+        obj.compiled = None
+        obj.device = torch.device(device)
+        obj.lib = _lib.load()
+        for k, v in meta.items():
+            if not k.startswith("__"):
+                setattr(obj, k, v)
+        for k in meta.get("__none__", []):
+            setattr(obj, k, None)
+        for k, t in tensors.items():
+            setattr(obj, k, t.to(obj.device))
+        obj._post_state()
+        return obj
+
+    def _post_state(self) -> None:
+        pass
+
+    def alloc_outputs(self, n: int):
+        import torch
+
+        return (torch.empty(n, dtype=torch.float32, device=self.device),
+                torch.empty(n, dtype=torch.uint8, device=self.device))
+
+    def score(self, X: Any, replace_nan: Optional[float] = None, stream=None):
+        """Score a host (numpy) or device (torch) matrix; returns device tensors ``(score, valid)``."""
+        import torch
+
+        if isinstance(X, np.ndarray):
+            Xt = torch.from_numpy(np.ascontiguousarray(X, dtype=np.float32)).to(self.device, non_blocking=False)
+        else:
+            Xt = X.to(self.device, dtype=torch.float32)
+        if Xt.dim() != 2 or Xt.shape[1] != self.n_features:
+            raise ValueError(f"expected [rows, {self.n_features}] input, got {tuple(Xt.shape)}")
+        Xt = Xt.contiguous()
+        if replace_nan is not None:
+            Xt = torch.nan_to_num(Xt, nan=float(replace_nan))
+        score, valid = self.alloc_outputs(Xt.shape[0])
+        self.launch(Xt, score, valid, stream=stream)
+        return score, valid.bool()
+
+
+def _epilogue(mode: int, C: int = 1, a: float = 1.0, b: float = 0.0, thr: float = 0.5, table=None,
+              write_probs: bool = False, link: int = 0):
+    from ..ops._lib import Epilogue
+
+    e = Epilogue()
+    e.mode, e.n_classes, e.a, e.b, e.thr = mode, C, a, b, thr
+    e.has_table = 1 if table is not None else 0
+    e.table = table.data_ptr() if table is not None else None
+    e.write_probs = 1 if write_probs else 0
+    e.link = link
+    return e
+
+
+def _label_table(labels: List[str]) -> np.ndarray:
+    out = np.empty(len(labels), dtype=np.float32)
+    for i, s in enumerate(labels):
+        try:
+            out[i] = float(s)
+        except (TypeError, ValueError):
+            out[i] = np.nan
+    return out
+
+
+# --------------------------------------------------------------------------- clustering
+
+
+class ClusterPlan(DevicePlan):
+    kind = "cluster"
+    _STATE = DevicePlan._STATE + ("centers", "weights", "scales", "qweights", "cfun", "table", "metric_code",
+                                  "similarity", "p")
+    _METRICS = {"squaredEuclidean": 0, "euclidean": 1, "cityBlock": 2, "chebychev": 3, "minkowski": 4}
+    _CF = {"absDiff": 0, "gaussSim": 1, "delta": 2, "equal": 3}
+
+    def __init__(self, compiled, device):
+        super().__init__(compiled, device)
+        ev: ClusteringEvaluator = compiled.evaluator
+        if ev.metric not in self._METRICS:
+            raise NotLowerable(f"clustering metric {ev.metric!r} is host-only")
+        if ev.fields != compiled.active_fields:
+            raise NotLowerable("clustering fields differ from the active fields (derived inputs are host-only)")
+        if not compiled.target_fields:
+            raise NotLowerable("clustering model without a target field")
+        self.metric_code = self._METRICS[ev.metric]
+        self.similarity = 0 if ev.kind_distance else 1
+        self.p = float(ev.p)
+        self.centers = self._t(ev.centers.astype(np.float32))
+        self.weights = self._t(ev.weights.astype(np.float32))
+        self.scales = self._t(ev.scales.astype(np.float32))
+        self.qweights = self._t(ev.missing_weights.astype(np.float32))
+        self.cfun = self._t(np.array([self._CF[c] for c in ev.compare], dtype=np.int32))
+        self.table = self._t(_label_table(ev.entity_ids))
+
+    def launch(self, X, score, valid, stream=None, probs=None, label=None, affinity=None) -> None:
+        from ..ops._lib import ClusterArgs, check, ptr, stream_handle
+
+        a = ClusterArgs()
+        a.X = ptr(X)
+        a.n_rows, a.n_feat, a.ldx, a.K = X.shape[0], X.shape[1], X.stride(0), self.centers.shape[0]
+        a.prep = ptr(self.prep)
+        a.centers, a.weights, a.scales = ptr(self.centers), ptr(self.weights), ptr(self.scales)
+        a.qweights, a.cfun, a.table = ptr(self.qweights), ptr(self.cfun), ptr(self.table)
+        a.metric, a.similarity, a.p = self.metric_code, self.similarity, self.p
+        a.score, a.valid, a.label, a.affinity = ptr(score), ptr(valid), ptr(label), ptr(affinity)
+        import ctypes
+
+        check(self.lib.pmml_cluster_launch(stream_handle(stream), ctypes.byref(a)), "cluster kernel")
+
+
+# --------------------------------------------------------------------------- linear
+
+
+class LinearPlan(DevicePlan):
+    kind = "linear"
+    _STATE = DevicePlan._STATE + ("W", "b", "K", "simplemax", "table", "epi_args")
+
+    def __init__(self, compiled, device):
+        super().__init__(compiled, device)
+        ev: RegressionEvaluator = compiled.evaluator
+        if not ev.is_dense_linear():
+            raise NotLowerable("regression tables with categorical predictors / terms are host-only")
+        if ev.numeric_fields != compiled.active_fields[: len(ev.numeric_fields)] or \
+                set(ev.numeric_fields) != set(compiled.active_fields):
+            # reorder W rows to the active-field order
+            pass
+        W, b = ev.dense_weights()
+        Wf = np.zeros((compiled.n_features, W.shape[1]))
+        for i, name in enumerate(ev.numeric_fields):
+            if name not in compiled.active_fields:
+                raise NotLowerable(f"predictor {name!r} is not an active field")
+            Wf[compiled.active_fields.index(name)] = W[i]
+        self.used = np.zeros(compiled.n_features, dtype=bool)
+        for name in ev.numeric_fields:
+            self.used[compiled.active_fields.index(name)] = True
+        if not self.used.all():
+            raise NotLowerable("unused active fields would wrongly invalidate rows with missing values")
+        self.W = self._t(Wf.astype(np.float32))
+        self.b = self._t(b.astype(np.float32))
+        self.K = W.shape[1]
+        norm = ev.rm.normalization_method
+        self.simplemax = 0
+        if ev.kind == "classification":
+            self.table = self._t(_label_table(ev.categories))
+            if norm == "softmax":
+                self.epi_args = dict(mode=EPI_SOFTMAX, C=self.K)
+            elif norm == "simplemax":
+                self.simplemax = 1
+                self.epi_args = dict(mode=EPI_ARGMAX, C=self.K)
+            elif self.K == 2:
+                if norm not in LINKS:
+                    raise NotLowerable(f"normalizationMethod {norm!r}")
+                # p0 = link(y0); the second table is ignored (PMML binary rule)
+                self.epi_args = dict(mode=EPI_LOGISTIC2, C=2, link=LINKS[norm])
+            else:
+                raise NotLowerable("multi-table element-wise link is host-only")
+        else:
+            self.table = None
+            if norm not in LINKS:
+                raise NotLowerable(f"normalizationMethod {norm!r}")
+            tgt = ev.target
+            if tgt is not None and (tgt.min is not None or tgt.max is not None or tgt.cast_integer):
+                raise NotLowerable("Target min/max/castInteger is host-only")
+            self.epi_args = dict(mode=EPI_AFFINE, link=LINKS[norm])
+            self.post = (tgt.rescale_factor, tgt.rescale_constant) if tgt is not None else (1.0, 0.0)
+            if self.post != (1.0, 0.0) and norm not in ("none", None):
+                raise NotLowerable("Target rescale after a link function is host-only")
+            if norm in ("none", None):
+                self.epi_args.update(a=self.post[0], b=self.post[1])
+                self.W = self.W  # rescale folded into the affine epilogue
+
+    def launch(self, X, score, valid, stream=None, probs=None) -> None:
+        import ctypes
+
+        from ..ops._lib import LinearArgs, check, ptr, stream_handle
+
+        a = LinearArgs()
+        a.X = ptr(X)
+        a.n_rows, a.n_feat, a.ldx, a.K = X.shape[0], X.shape[1], X.stride(0), self.K
+        a.prep, a.W, a.bias, a.simplemax = ptr(self.prep), ptr(self.W), ptr(self.b), self.simplemax
+        a.epi = _epilogue(table=self.table, write_probs=probs is not None, **self.epi_args)
+        a.score, a.valid, a.probs = ptr(score), ptr(valid), ptr(probs)
+        check(self.lib.pmml_linear_launch(stream_handle(stream), ctypes.byref(a)), "linear kernel")
+
+
+# --------------------------------------------------------------------------- tree ensembles
+
+
+@dataclass
+class EnsembleSpec:
+    trees: List[BinaryTree]
+    weights: List[float]
+    P: int  # leaf payload width
+    C: int  # accumulator slots
+    epi: dict
+    labels: Optional[List[str]]
+    slots: Optional[List[int]] = None
+
+
+def _segments_all_true(mm: ir.MiningModel) -> bool:
+    return all(isinstance(s.predicate, ir.TruePredicate) for s in mm.segments)
+
+
+def _target_affine(ev) -> Tuple[float, float]:
+    t = ev.target
+    if t is None:
+        return 1.0, 0.0
+    if t.min is not None or t.max is not None or t.cast_integer:
+        raise NotLowerable("Target min/max/castInteger is host-only")
+    if t.values and t.values[0].default_value is not None:
+        raise NotLowerable("Target defaultValue is host-only")
+    return t.rescale_factor, t.rescale_constant
+
+
+def _regression_ensemble(ev, field_index) -> Tuple[List[BinaryTree], List[float], float, float]:
+    """Flatten a regression tree / MiningModel(sum|average|weightedAverage) of regression trees
+    into (trees, per-tree weights, a, b) with value = a * Σ w_t leaf_t + b."""
+    if isinstance(ev, TreeEvaluator):
+        if ev.kind != "regression":
+            raise NotLowerable("expected a regression tree")
+        a, b = _target_affine(ev)
+        return [lower_binary_tree(ev, field_index)], [1.0], a, b
+    if isinstance(ev, MiningEvaluator):
+        mm = ev.mm
+        if ev.kind != "regression":
+            raise NotLowerable("expected a regression ensemble")
+        if not _segments_all_true(mm):
+            raise NotLowerable("segment predicates other than True are host-only")
+        method = mm.multiple_model_method
+        if method not in ("sum", "average", "weightedAverage"):
+            raise NotLowerable(f"multipleModelMethod {method!r} is host-only for regression ensembles")
+        trees: List[BinaryTree] = []
+        weights: List[float] = []
+        for seg, sub in zip(mm.segments, ev.sub):
+            st, sw, sa, sb = _regression_ensemble(sub, field_index)
+            if sb != 0.0:
+                raise NotLowerable("nested Target rescaleConstant inside an ensemble is host-only")
+            w = seg.weight if method == "weightedAverage" else 1.0
+            trees.extend(st)
+            weights.extend([x * w * sa for x in sw])
+        if method == "average":
+            scale = 1.0 / max(1, len(mm.segments))
+        elif method == "weightedAverage":
+            scale = 1.0 / sum(s.weight for s in mm.segments)
+        else:
+            scale = 1.0
+        a, b = _target_affine(ev)
+        return trees, weights, a * scale, b
+    raise NotLowerable(f"{type(ev).__name__} is not a regression tree ensemble")
+
+
+def ensemble_spec(compiled) -> EnsembleSpec:
+    ev = compiled.evaluator
+    field_index = {f: i for i, f in enumerate(compiled.active_fields)}
+    try:
+        if ev.kind == "regression":
+            trees, w, a, b = _regression_ensemble(ev, field_index)
+            return EnsembleSpec(trees, w, 1, 1, dict(mode=EPI_AFFINE, a=a, b=b), None)
+        if isinstance(ev, MiningEvaluator) and ev.mm.multiple_model_method == "modelChain":
+            return _chain_spec(compiled, ev, field_index)
+        if isinstance(ev, MiningEvaluator) and ev.kind == "classification":
+            return _classification_spec(ev, field_index)
+        if isinstance(ev, TreeEvaluator) and ev.kind == "classification":
+            t = lower_binary_tree(ev, field_index)
+            C = len(ev.categories)
+            return EnsembleSpec([t], [1.0], C, C, dict(mode=EPI_ARGMAX, C=C, a=1.0), list(ev.categories))
+    except NotBinary as e:
+        raise NotLowerable(f"tree is not in binary-split form: {e}") from e
+    raise NotLowerable(f"{type(ev).__name__} ({ev.kind}) is not a lowerable tree ensemble")
+
+
+def _classification_spec(ev: MiningEvaluator, field_index) -> EnsembleSpec:
+    mm = ev.mm
+    if not _segments_all_true(mm):
+        raise NotLowerable("segment predicates other than True are host-only")
+    method = mm.multiple_model_method
+    cats = list(ev.categories)
+    C = len(cats)
+    trees, weights = [], []
+    for seg, sub in zip(mm.segments, ev.sub):
+        if not isinstance(sub, TreeEvaluator) or sub.kind != "classification":
+            raise NotLowerable("classification ensembles must hold classification trees")
+        t = lower_binary_tree(sub, field_index)
+        remap = np.array([cats.index(c) for c in sub.categories])
+        if method in ("majorityVote", "weightedMajorityVote"):
+            probs = np.zeros((len(t.leaf_value), C))
+            ok = ~np.isnan(t.leaf_value)
+            probs[np.nonzero(ok)[0], remap[t.leaf_value[ok].astype(int)]] = 1.0
+        elif method in ("average", "weightedAverage"):
+            probs = np.zeros((len(t.leaf_value), C))
+            probs[:, remap] = np.nan_to_num(t.leaf_probs)
+        else:
+            raise NotLowerable(f"multipleModelMethod {method!r} is host-only for classification")
+        t.leaf_probs = probs
+        trees.append(t)
+        weights.append(seg.weight if method.startswith("weighted") else 1.0)
+    return EnsembleSpec(trees, weights, C, C, dict(mode=EPI_ARGMAX, C=C, a=1.0 / sum(weights)), cats)
+
+
+def _chain_spec(compiled, ev: MiningEvaluator, field_index) -> EnsembleSpec:
+    """modelChain [regression tree ensemble -> binary RegressionModel on its output] (the
+    XGBoost/LightGBM binary-classification export) fused into one kernel + link epilogue."""
+    mm = ev.mm
+    if len(mm.segments) != 2 or not _segments_all_true(mm):
+        raise NotLowerable("only two-segment modelChains (ensemble -> calibrator) are lowered")
+    first, second = ev.sub
+    if not isinstance(second, RegressionEvaluator) or second.kind != "classification":
+        raise NotLowerable("chain calibrator must be a classification RegressionModel")
+    outs = [o for o in first.model.output if o.feature in ("predictedValue", "transformedValue")
+            and o.expression is None]
+    if len(outs) < 1:
+        raise NotLowerable("first chain segment exposes no predictedValue output")
+    out_name = outs[0].name
+    rm = second.rm
+    if len(rm.tables) != 2 or rm.tables[1].numeric or rm.tables[1].categorical or rm.tables[1].terms:
+        raise NotLowerable("calibrator must have two tables, the second constant")
+    t0 = rm.tables[0]
+    if t0.categorical or t0.terms or len(t0.numeric) != 1 or t0.numeric[0].name != out_name \
+            or t0.numeric[0].exponent != 1.0:
+        raise NotLowerable("calibrator must be linear in the ensemble output")
+    if rm.tables[1].intercept != 0.0 and rm.normalization_method not in ("softmax",):
+        pass
+    norm = rm.normalization_method
+    if norm not in LINKS or norm == "none":
+        raise NotLowerable(f"calibrator normalizationMethod {norm!r} is host-only")
+    trees, w, a, b = _regression_ensemble(first, field_index)
+    coef, icpt = t0.numeric[0].coefficient, t0.intercept
+    cats = list(second.categories)
+    # the chain's target is the calibrator's; category table in calibrator order
+    return EnsembleSpec(trees, w, 1, 1, dict(mode=EPI_LOGISTIC2, C=2, a=coef * a, b=coef * b + icpt,
+                                             link=LINKS[norm]), cats)
+
+
+def _perfect_pack(trees: List[BinaryTree], weights: List[float], P: int, D: int) -> Tuple[np.ndarray, int, bool]:
+    """Pack trees into the PERFECT layout: per tree [ (2^D-1) x {T bits, meta} ][ 2^D x P leaves ]."""
+    NI, NL = (1 << D) - 1, 1 << D
+    rec = 2 * NI + NL * P
+    rec = (rec + 3) & ~3
+    blob = np.zeros((len(trees), rec), dtype=np.uint32)
+    has_dr = False
+    for ti, (t, w) in enumerate(zip(trees, weights)):
+        nodes_T = np.zeros(NI, dtype=np.float32)
+        nodes_meta = np.zeros(NI, dtype=np.uint32)
+        leaves = np.zeros((NL, P), dtype=np.float32)
+        stack = [(0, 0, 0)]  # (node k, perfect index p, depth)
+        while stack:
+            k, p, d = stack.pop()
+            if t.feature[k] < 0:
+                val = (t.leaf_probs[k] if t.leaf_probs is not None and P > 1 else np.array([t.leaf_value[k]])) * w
+                # pad: every leaf below perfect index p gets the value
+                lo = p
+                for _ in range(D - d):
+                    lo = 2 * lo + 1
+                span = 1 << (D - d)
+                leaves[lo - NI: lo - NI + span, :] = np.asarray(val, dtype=np.float64)[None, :P]
+                continue
+            T, swap = canonical_threshold(int(t.op[k]), float(t.threshold[k]))
+            first, second = int(t.left[k]), int(t.right[k])
+            dflt_first = bool(t.default_left[k])
+            if swap:
+                left_child, right_child = second, first
+                dr = dflt_first  # default went to the (now right) first child
+            else:
+                left_child, right_child = first, second
+                dr = not dflt_first
+            f = int(t.feature[k])
+            if f > 63:
+                raise NotLowerable("perfect layout supports at most 64 features")
+            nodes_T[p] = T
+            nodes_meta[p] = (f * TB * 4) | (np.uint32(1) << 31 if dr else 0)
+            has_dr = has_dr or dr
+            stack.append((left_child, 2 * p + 1, d + 1))
+            stack.append((right_child, 2 * p + 2, d + 1))
+        blob[ti, 0: 2 * NI: 2] = nodes_T.view(np.uint32)
+        blob[ti, 1: 2 * NI: 2] = nodes_meta
+        blob[ti, 2 * NI: 2 * NI + NL * P] = leaves.reshape(-1).view(np.uint32)
+    return blob, rec, has_dr
+
+
+def _pointer_pack(trees: List[BinaryTree], weights: List[float], P: int):
+    nodes: List[Tuple[int, int, int, int]] = []
+    leaves: List[np.ndarray] = []
+    roots: List[int] = []
+    has_dr = False
+    for t, w in zip(trees, weights):
+        base_map = {}
+        order = []
+        stack = [0]
+        while stack:
+            k = stack.pop()
+            order.append(k)
+            if t.feature[k] >= 0:
+                stack.append(int(t.right[k]))
+                stack.append(int(t.left[k]))
+        for k in order:
+            if t.feature[k] < 0:
+                val = t.leaf_probs[k] if t.leaf_probs is not None and P > 1 else np.array([t.leaf_value[k]])
+                base_map[k] = ~len(leaves)
+                leaves.append(np.asarray(val, dtype=np.float64)[:P] * w)
+            else:
+                base_map[k] = len(nodes)
+                nodes.append((0, 0, 0, 0))
+        for k in order:
+            if t.feature[k] < 0:
+                continue
+            T, swap = canonical_threshold(int(t.op[k]), float(t.threshold[k]))
+            first, second = int(t.left[k]), int(t.right[k])
+            dflt_first = bool(t.default_left[k])
+            if swap:
+                lc, rc, dr = second, first, dflt_first
+            else:
+                lc, rc, dr = first, second, not dflt_first
+            f = int(t.feature[k])
+            meta = (f * TB * 4 if f < 64 else f) | ((1 << 31) if dr else 0)
+            has_dr = has_dr or dr
+            nodes[base_map[k]] = (int(np.float32(T).view(np.uint32)), meta, base_map[lc], base_map[rc])
+        roots.append(base_map[0])
+    nd = np.array(nodes, dtype=np.int64).astype(np.uint32) if nodes else np.zeros((1, 4), np.uint32)
+    lv = np.stack(leaves).astype(np.float32) if leaves else np.zeros((1, P), np.float32)
+    return nd, lv, np.array(roots, dtype=np.int32), has_dr
+
+
+class TreePlan(DevicePlan):
+    """GBDT / random forest / single tree / calibrated chain on the HIP traversal kernel."""
+
+    kind = "tree"
+    _STATE = DevicePlan._STATE + ("depth", "n_trees", "layout", "P", "C", "general", "rec_words", "chunk_trees",
+                                  "blob", "leaves", "roots", "has_dr", "table", "slots", "splits", "epi_args")
+
+    def __init__(self, compiled, device, layout: str = "auto", lds_budget: int = 80 * 1024, splits: int = 0):
+        super().__init__(compiled, device)
+        spec = ensemble_spec(compiled)
+        self.spec = spec
+        self.epi_args = dict(spec.epi)
+        F = compiled.n_features
+        depth = max(1, max(t.depth for t in spec.trees))
+        self.depth = depth
+        self.n_trees = len(spec.trees)
+        if layout == "auto":
+            layout = "perfect" if depth <= 10 and F <= 64 else "pointer"
+        self.layout = layout
+        self.P, self.C = spec.P, spec.C
+        self.general = 1 if spec.P > 1 else 0
+        if self.layout == "perfect":
+            blob, rec, has_dr = _perfect_pack(spec.trees, spec.weights, spec.P, depth)
+            self.rec_words = rec
+            fixed = F * TB * 4 + TB * 4 + (self.C * TB * 4 if self.general else 0)
+            budget = max(lds_budget - fixed, rec * 4)
+            self.chunk_trees = int(max(1, min(self.n_trees, budget // (rec * 4))))
+            self.blob = self._t(blob.reshape(-1).view(np.int32))
+            self.roots = self.leaves = None
+        else:
+            nodes, leaves, roots, has_dr = _pointer_pack(spec.trees, spec.weights, spec.P)
+            self.rec_words = 0
+            self.chunk_trees = 0
+            self.blob = self._t(nodes.reshape(-1).view(np.int32))
+            self.leaves = self._t(leaves.reshape(-1))
+            self.roots = self._t(roots)
+        self.has_dr = has_dr
+        self.table = self._t(_label_table(spec.labels)) if spec.labels is not None else None
+        self.slots = self._t(np.zeros(self.n_trees, dtype=np.int32)) if self.general else None
+        self.splits = splits
+        self._partial = None
+
+    def _post_state(self) -> None:
+        self._partial = None
+
+    def _auto_splits(self, n_rows: int) -> int:
+        if self.splits:
+            return self.splits
+        blocks = (n_rows + TB - 1) // TB
+        target = 512  # ~2 workgroups per CU on 256 CUs
+        if blocks >= target or self.n_trees < 64:
+            return 1
+        return int(max(1, min(self.n_trees // 16, target // max(1, blocks), 64)))
+
+    def launch(self, X, score, valid, stream=None, probs=None, row_valid=None, splits: Optional[int] = None) -> None:
+        import ctypes
+
+        import torch
+
+        from ..ops._lib import TreeArgs, check, ptr, stream_handle
+
+        n = X.shape[0]
+        s = splits if splits is not None else self._auto_splits(n)
+        a = TreeArgs()
+        a.X = ptr(X)
+        a.n_rows, a.n_feat, a.ldx = n, X.shape[1], X.stride(0)
+        a.prep, a.row_valid_in = ptr(self.prep), ptr(row_valid)
+        a.blob, a.roots, a.leaves, a.tree_slot = ptr(self.blob), ptr(self.roots), ptr(self.leaves), ptr(self.slots)
+        a.n_trees, a.rec_words, a.chunk_trees, a.P = self.n_trees, self.rec_words, self.chunk_trees, self.P
+        a.C, a.general = self.C, self.general
+        a.epi = _epilogue(table=self.table, write_probs=probs is not None, **self.epi_args)
+        a.score, a.valid, a.probs = ptr(score), ptr(valid), ptr(probs)
+        if s > 1:
+            need = s * (self.C + 1) * n
+            if self._partial is None or self._partial.numel() < need:
+                self._partial = torch.empty(need, dtype=torch.float32, device=self.device)
+            a.partial = ptr(self._partial)
+        rc = self.lib.pmml_tree_launch(stream_handle(stream), ctypes.byref(a), 0 if self.layout == "perfect" else 1,
+                                       self.depth, 1 if self.has_dr else 0, s)
+        check(rc, f"tree kernel ({self.layout}, depth {self.depth})")
+
+
+# --------------------------------------------------------------------------- dispatch
+
+
+def compile_plan(compiled, device, **opts) -> DevicePlan:
+    """Pick and build the device plan for a compiled model; raises :class:`NotLowerable` when the
+    model needs the host oracle."""
+    ev = compiled.evaluator
+    if not compiled.target_fields:
+        raise NotLowerable("model has no target field (every record scores EmptyScore)")
+    if compiled.model.local_transformations or compiled.doc.transformations:
+        raise NotLowerable("derived fields are evaluated on the host in this revision")
+    if isinstance(ev, ClusteringEvaluator):
+        return ClusterPlan(compiled, device)
+    if isinstance(ev, (TreeEvaluator, MiningEvaluator)):
+        return TreePlan(compiled, device, **opts)
+    if isinstance(ev, RegressionEvaluator):
+        return LinearPlan(compiled, device)
+    from ..models.neural import NeuralEvaluator
+    from ..models.svm import SvmEvaluator
+
+    if isinstance(ev, NeuralEvaluator):
+        from .nn_plans import MlpPlan
+
+        return MlpPlan(compiled, device, **opts)
+    if isinstance(ev, SvmEvaluator):
+        from .nn_plans import SvmPlan
+
+        return SvmPlan(compiled, device)
+    raise NotLowerable(f"no device plan for {type(ev).__name__}")

@@ -1,0 +1,42 @@
+#!/usr/bin/env bash
+# One GPU session on the gpurun box: tests -> bench -> rocprof. Each GPU step has its own time
+# limit; a fault/abort/timeout (rc >= 124 or signal) stops the session, ordinary test failures
+# (rc 1) do not.
+set -u
+ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+OUT="$ROOT/gpurun_out"
+mkdir -p "$OUT"
+cd "$ROOT"
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+STEPS="${STEPS:-tests bench prof}"
+
+fatal() { local rc=$1; [ "$rc" -ge 124 ] || [ "$rc" -gt 128 ]; }
+
+run() {  # name timeout cmd...
+  local name=$1 to=$2; shift 2
+  echo "=== $name: $*" | tee -a "$OUT/session.log"
+  timeout -k 10 "$to" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" | tee -a "$OUT/session.log"
+  tail -n 5 "$OUT/$name.log" | tee -a "$OUT/session.log"
+  if fatal $rc; then echo "fatal rc=$rc in $name: stopping" | tee -a "$OUT/session.log"; exit $rc; fi
+  return 0
+}
+
+run build 300 python -c "import __graft_entry__ as g; g.build()"
+for s in $STEPS; do
+  case $s in
+    tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 600 python bench.py --steps "${BENCH_STEPS:-20}" --warmup 3 ;;
+    prof)
+      mkdir -p "$OUT/prof"
+      ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" \
+          -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --latency-iters 5 \
+          > "$OUT/prof.log" 2>&1 ); rc=$?
+      echo "=== prof rc=$rc" | tee -a "$OUT/session.log"
+      if fatal $rc; then exit $rc; fi ;;
+    *) echo "unknown step $s" ;;
+  esac
+done
+echo "=== session done" | tee -a "$OUT/session.log"

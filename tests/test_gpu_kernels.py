@@ -1,0 +1,153 @@
+"""HIP kernel numerics vs the float64 host oracle (the semantic reference for every model type).
+
+Tolerances: tree ensembles sum leaf values in fp32 (|err| ≲ 1e-5 for 1000 trees of ~0.1-scale
+leaves); split decisions are exact for fp32 inputs (directionally rounded thresholds), so the
+*selected leaves* — and therefore classification labels — must match exactly.
+"""
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _gpu_np(plan, X, **kw):
+    s, v = plan.score(X, **kw)
+    return s.cpu().numpy(), v.cpu().numpy()
+
+
+def test_native_library_loaded(gpu):
+    from flink_jpmml_amd.ops import _lib
+
+    lib = _lib.load()
+    assert lib._name.endswith("_pmml_kernels.so")
+
+
+def test_kmeans_goldens_on_gpu(gpu, fixtures_dir):
+    from flink_jpmml_amd.runtime.compiled import CompiledPmml
+    from flink_jpmml_amd.runtime.plans import ClusterPlan
+
+    c = CompiledPmml.load(fixtures_dir["kmeans"])
+    plan = c.plan(gpu)
+    assert isinstance(plan, ClusterPlan)
+    X = np.array([[1, 1, 1, 1], [1, 2, 3, 4], [1, np.nan, 2, np.nan], [np.nan] * 4, [6.9, 3.1, 5.8, 2.1]], float)
+    s, v = _gpu_np(plan, X)
+    assert s[:3].tolist() == [3.0, 4.0, 3.0]
+    assert v.tolist() == [True, True, True, False, True]
+    ref, vref = c.score_matrix_oracle(X)
+    assert (vref == v).all() and np.allclose(ref[v], s[v])
+    s0, v0 = _gpu_np(plan, X[2:3], replace_nan=0.0)
+    assert v0[0] and s0[0] == 3.0
+
+
+def test_kmeans_random_parity(gpu, fixtures_dir):
+    from flink_jpmml_amd.runtime.compiled import CompiledPmml
+
+    c = CompiledPmml.load(fixtures_dir["kmeans"])
+    rng = np.random.default_rng(0)
+    X = rng.uniform(0, 8, (100_000, 4))
+    X[rng.random(X.shape) < 0.1] = np.nan
+    s, v = _gpu_np(c.plan(gpu), X)
+    ref, vref = c.score_matrix_oracle(X)
+    assert (v == vref).all()
+    assert (s[v] == ref[v]).mean() > 0.9999  # fp32 vs fp64 distance near-ties only
+
+
+@pytest.mark.parametrize("depth,trees,feat,missing", [(6, 200, 32, 0.05), (3, 17, 5, 0.0), (8, 50, 64, 0.1),
+                                                      (10, 8, 16, 0.02)])
+def test_gbdt_regression_parity(gpu, depth, trees, feat, missing):
+    from flink_jpmml_amd.bench.synth import gbdt_pmml, stream_matrix
+    from flink_jpmml_amd.runtime.compiled import CompiledPmml
+
+    c = CompiledPmml.from_string(gbdt_pmml(n_trees=trees, depth=depth, n_features=feat, seed=depth))
+    plan = c.plan(gpu)
+    assert plan.layout == "perfect"
+    X = stream_matrix(20_000, feat, seed=1, missing_rate=missing)
+    s, v = _gpu_np(plan, X)
+    ref, vref = c.score_matrix_oracle(X)
+    assert (v == vref).all()
+    assert np.max(np.abs(s - ref)) < 2e-5 * max(1.0, trees / 100)
+
+
+def test_gbdt_split_and_pointer_layouts(gpu):
+    from flink_jpmml_amd.bench.synth import gbdt_pmml, stream_matrix
+    from flink_jpmml_amd.runtime.compiled import CompiledPmml
+
+    c = CompiledPmml.from_string(gbdt_pmml(n_trees=300, depth=7, n_features=24, seed=11))
+    X = stream_matrix(3000, 24, seed=4, missing_rate=0.05)
+    ref, vref = c.score_matrix_oracle(X)
+    perfect = c.plan(gpu)
+    for splits in (1, 4, 19):
+        s, v = perfect.score(X) if splits == 1 else (None, None)
+        if splits > 1:
+            import torch
+
+            Xt = torch.from_numpy(X.astype(np.float32)).to(gpu)
+            so = torch.empty(len(X), device=gpu)
+            vo = torch.empty(len(X), dtype=torch.uint8, device=gpu)
+            perfect.launch(Xt, so, vo, splits=splits)
+            s, v = so, vo.bool()
+        s, v = s.cpu().numpy(), v.cpu().numpy()
+        assert (v == vref).all()
+        assert np.max(np.abs(s - ref)) < 1e-4
+    pointer = c.plan(gpu, layout="pointer")
+    assert pointer.layout == "pointer"
+    s, v = _gpu_np(pointer, X)
+    assert (v == vref).all() and np.max(np.abs(s - ref)) < 1e-4
+
+
+def test_gbdt_binary_chain(gpu):
+    from flink_jpmml_amd.bench.synth import gbdt_pmml, stream_matrix
+    from flink_jpmml_amd.runtime.compiled import CompiledPmml
+
+    c = CompiledPmml.from_string(gbdt_pmml(n_trees=120, depth=5, n_features=20, seed=5, objective="binary"))
+    plan = c.plan(gpu)
+    X = stream_matrix(50_000, 20, seed=3, missing_rate=0.03)
+    s, v = _gpu_np(plan, X)
+    ref, vref = c.score_matrix_oracle(X)
+    assert (v == vref).all()
+    # labels: only rows whose probability sits within fp32 noise of 0.5 may differ
+    assert (s == ref).mean() > 0.9999
+
+
+def test_random_forest_vote(gpu):
+    from flink_jpmml_amd.bench.synth import random_forest_pmml, stream_matrix
+    from flink_jpmml_amd.runtime.compiled import CompiledPmml
+
+    c = CompiledPmml.from_string(random_forest_pmml(n_trees=101, depth=7, n_features=16, n_classes=3, seed=2))
+    X = stream_matrix(20_000, 16, seed=8, missing_rate=0.02)
+    s, v = _gpu_np(c.plan(gpu), X)
+    ref, vref = c.score_matrix_oracle(X)
+    assert (v == vref).all()
+    assert (s == ref).all()  # integer vote counts are exact in fp32
+
+
+def test_iris_logistic_regression(gpu):
+    from flink_jpmml_amd.assets import IRIS_FIELDS  # noqa: F401
+    from flink_jpmml_amd.bench.synth import iris_logistic_pmml
+    from flink_jpmml_amd.runtime.compiled import CompiledPmml
+    from flink_jpmml_amd.runtime.plans import LinearPlan
+
+    c = CompiledPmml.from_string(iris_logistic_pmml())
+    plan = c.plan(gpu)
+    assert isinstance(plan, LinearPlan)
+    rng = np.random.default_rng(0)
+    X = rng.uniform([4, 2, 1, 0], [8, 4.5, 7, 2.5], (10_000, 4))
+    s, v = _gpu_np(plan, X)
+    ref, vref = c.score_matrix_oracle(X)
+    assert (v == vref).all()
+    # categories are non-numeric strings -> no numeric score, every row EmptyScore
+    assert not v.any()
+
+
+def test_interval_return_invalid_on_gpu(gpu, fixtures_dir):
+    """kmeans40 with returnInvalid semantics vs asIs: rows outside the DataField interval."""
+    from flink_jpmml_amd.assets import kmeans_pmml
+    from flink_jpmml_amd.runtime.compiled import CompiledPmml
+
+    c = CompiledPmml.from_string(kmeans_pmml("4.3", invalid_treatment="returnInvalid"))
+    X = np.array([[1, 1, 1, 1], [5, 3, 2, 1], [7.9, 4.4, 6.9, 2.5], [4.3, 2.0, 1.0, 0.1]], float)
+    s, v = _gpu_np(c.plan(gpu), X)
+    ref, vref = c.score_matrix_oracle(X)
+    assert v.tolist() == vref.tolist() == [False, True, True, True]
+    assert np.allclose(s[v], ref[v])
