@@ -20,7 +20,6 @@
 namespace {
 
 constexpr int TB = 256;   // rows per workgroup (= threads)
-constexpr int ILP = 4;    // independent trees in flight per lane
 
 struct TreeArgs {
   const float* X;
@@ -63,88 +62,185 @@ __device__ __forceinline__ void finish_row(const TreeArgs& a, float acc0, const 
   }
 }
 
-template <int DEPTH, bool GENERAL, bool HAS_DR>
+// Next-chunk prefetch through registers: the global loads are issued before the traversal of the
+// current chunk and written to the other LDS buffer after it, so L2 latency hides under compute.
+// (An LDS-DMA variant was slower: hipcc drains in-flight LDS-DMA before the first ds_read it cannot
+// prove disjoint from the DMA target, which serialised the copy with the traversal.)
+constexpr int PREFETCH_Q = 8;  // uint4 per lane -> up to 32 KiB per chunk
+
+// Loads are unconditional (index clamped into the valid range) so the values stay in VGPRs; only
+// the LDS store is predicated. Written as macros over named registers: an array passed between
+// helpers was demoted to scratch by hipcc.
+#define PF_DECL uint4 pf0, pf1, pf2, pf3, pf4, pf5, pf6, pf7;
+#define PF_LOAD1(R, I, S4, LAST) R = (S4)[min((int)threadIdx.x + (I) * TB, (LAST))];
+#define PF_LOAD(SRC, N16)                                                              \
+  {                                                                                    \
+    const uint4* s4_ = reinterpret_cast<const uint4*>(SRC);                            \
+    const int last_ = (N16) > 0 ? (N16) - 1 : 0;                                      \
+    PF_LOAD1(pf0, 0, s4_, last_) PF_LOAD1(pf1, 1, s4_, last_) PF_LOAD1(pf2, 2, s4_, last_) \
+    PF_LOAD1(pf3, 3, s4_, last_) PF_LOAD1(pf4, 4, s4_, last_) PF_LOAD1(pf5, 5, s4_, last_) \
+    PF_LOAD1(pf6, 6, s4_, last_) PF_LOAD1(pf7, 7, s4_, last_)                          \
+  }
+#define PF_STORE1(R, I, D4, N)                      \
+  {                                                  \
+    const int idx_ = (int)threadIdx.x + (I) * TB;   \
+    if (idx_ < (N)) (D4)[idx_] = R;                  \
+  }
+#define PF_STORE(DST, N16)                                                              \
+  {                                                                                     \
+    uint4* d4_ = reinterpret_cast<uint4*>(DST);                                         \
+    PF_STORE1(pf0, 0, d4_, N16) PF_STORE1(pf1, 1, d4_, N16) PF_STORE1(pf2, 2, d4_, N16) \
+    PF_STORE1(pf3, 3, d4_, N16) PF_STORE1(pf4, 4, d4_, N16) PF_STORE1(pf5, 5, d4_, N16) \
+    PF_STORE1(pf6, 6, d4_, N16) PF_STORE1(pf7, 7, d4_, N16)                             \
+  }
+
+// Traverse `nt` perfect trees of one LDS chunk for this lane's row.
+// Heap index j (root = 1): node j at byte (j-1)*8, children 2j / 2j+1, leaf j - 2^D.
+// Fast path (MISSING=false): one ds_read_b64 node, one ds_read_b32 feature, one v_cmp, index update.
+template <int DEPTH, bool GENERAL, bool MISSING, int ILP>
+__device__ __forceinline__ void traverse_chunk(const TreeArgs& a, const uint32_t* buf, int nt, int t0,
+                                               const char* feat_lane, float& acc, float* accl) {
+  constexpr int NI = (1 << DEPTH) - 1;
+  constexpr int NL = 1 << DEPTH;
+  const int rw = a.rec_words;
+  const int dr_off = 2 * NI + NL * a.P;  // words
+  const int tid = threadIdx.x;
+  int k = 0;
+  for (; k + ILP <= nt; k += ILP) {
+    uint32_t j[ILP];
+    const char* base[ILP];
+#pragma unroll
+    for (int i = 0; i < ILP; ++i) {
+      j[i] = 1u;
+      base[i] = reinterpret_cast<const char*>(buf + (k + i) * rw);
+    }
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) {
+#pragma unroll
+      for (int i = 0; i < ILP; ++i) {
+        const uint2 nd = *reinterpret_cast<const uint2*>(base[i] - 8 + (j[i] << 3));
+        const float x = *reinterpret_cast<const float*>(feat_lane + nd.y);
+        uint32_t right = (x >= __uint_as_float(nd.x)) ? 1u : 0u;
+        if (MISSING) {  // branch-free: NaN takes the node's default direction bit
+          const uint32_t n = j[i] - 1u;
+          const uint32_t w = reinterpret_cast<const uint32_t*>(base[i])[dr_off + (n >> 5)];
+          right |= ((x != x) ? 1u : 0u) & (w >> (n & 31u));
+        }
+        j[i] = j[i] + j[i] + right;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < ILP; ++i) {
+      const float* lv = reinterpret_cast<const float*>(base[i] + NI * 8) - NL * a.P;
+      if (GENERAL) {
+        const int slot = a.tree_slot[t0 + k + i];
+        for (int p = 0; p < a.P; ++p) accl[(slot + p) * TB + tid] += lv[j[i] * a.P + p];
+      } else {
+        acc += lv[j[i]];
+      }
+    }
+  }
+  for (; k < nt; ++k) {
+    uint32_t j = 1u;
+    const char* base = reinterpret_cast<const char*>(buf + k * rw);
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) {
+      const uint2 nd = *reinterpret_cast<const uint2*>(base - 8 + (j << 3));
+      const float x = *reinterpret_cast<const float*>(feat_lane + nd.y);
+      uint32_t right = (x >= __uint_as_float(nd.x)) ? 1u : 0u;
+      if (MISSING) {
+        const uint32_t n = j - 1u;
+        const uint32_t w = reinterpret_cast<const uint32_t*>(base)[dr_off + (n >> 5)];
+        right |= ((x != x) ? 1u : 0u) & (w >> (n & 31u));
+      }
+      j = j + j + right;
+    }
+    const float* lv = reinterpret_cast<const float*>(base + NI * 8) - NL * a.P;
+    if (GENERAL) {
+      const int slot = a.tree_slot[t0 + k];
+      for (int p = 0; p < a.P; ++p) accl[(slot + p) * TB + tid] += lv[j * a.P + p];
+    } else {
+      acc += lv[j];
+    }
+  }
+}
+
+template <int DEPTH, bool GENERAL, int ILP>
 __global__ __launch_bounds__(TB, 2) void tree_perfect_kernel(TreeArgs a) {
   extern __shared__ __align__(16) uint32_t smem[];
-  constexpr int NI = (1 << DEPTH) - 1;
+  const int rw = a.rec_words;
+  const int chunk_words = a.chunk_trees * rw;
   float* feat = reinterpret_cast<float*>(smem);
-  uint32_t* tbuf = smem + a.n_feat * TB;
-  int* bad = reinterpret_cast<int*>(tbuf + a.chunk_trees * a.rec_words);
-  float* accl = reinterpret_cast<float*>(bad + TB);
+  uint32_t* tbuf0 = smem + a.n_feat * TB;
+  uint32_t* tbuf1 = tbuf0 + chunk_words;
+  int* bad = reinterpret_cast<int*>(tbuf1 + chunk_words);
+  int* any_missing = bad + TB;
+  float* accl = reinterpret_cast<float*>(bad + TB + 4);
 
   const int tid = threadIdx.x;
   const int row0 = blockIdx.x * TB;
   const int split = blockIdx.y;
-  stage_rows_T<TB>(a.X, a.n_rows, a.n_feat, a.ldx, a.prep, feat, bad, row0);
+  const int tb = split * a.trees_per_split;
+  const int te = min(a.n_trees, tb + a.trees_per_split);
+
+  // chunk 0: issue its loads before the row staging so the two overlap
+  PF_DECL
+  int n16 = (tb < te) ? (min(a.chunk_trees, te - tb) * rw) >> 2 : 0;
+  PF_LOAD(a.blob + (size_t)tb * rw, n16)
+
+  // stage rows [F][TB] with field preparation; rows past the end are zero (never "missing")
+  if (tid == 0) *any_missing = 0;
+  bad[tid] = 0;
+  __syncthreads();
+  {
+    const int F = a.n_feat;
+    const int total = TB * F;
+    bool miss = false;
+    for (int e = tid; e < total; e += TB) {
+      const int r = e / F;
+      const int f = e - r * F;
+      const int row = row0 + r;
+      float x = 0.f;
+      bool b = false;
+      if (row < a.n_rows) {
+        x = a.X[(size_t)row * a.ldx + f];
+        if (a.prep) x = prep_value(x, a.prep[f], &b);
+        miss = miss || (x != x);
+      }
+      feat[f * TB + r] = x;
+      if (b) bad[r] = 1;
+    }
+    if (__any(miss) && (tid & 63) == 0) *any_missing = 1;
+  }
+  PF_STORE(tbuf0, n16)
+  __syncthreads();
+
   const int row = row0 + tid;
   bool row_ok = bad[tid] == 0;
   if (a.row_valid_in && row < a.n_rows) row_ok = row_ok && a.row_valid_in[row];
-
-  const int tb = split * a.trees_per_split;
-  const int te = min(a.n_trees, tb + a.trees_per_split);
+  const bool missing = *any_missing != 0;
   if (GENERAL) {
     for (int c = 0; c < a.C; ++c) accl[c * TB + tid] = 0.f;
   }
   float acc = 0.f;
   const char* feat_lane = reinterpret_cast<const char*>(feat + tid);
-  const int rw = a.rec_words;
 
-  for (int t0 = tb; t0 < te; t0 += a.chunk_trees) {
+  int c = 0;
+  for (int t0 = tb; t0 < te; t0 += a.chunk_trees, ++c) {
     const int nt = min(a.chunk_trees, te - t0);
-    __syncthreads();  // previous chunk fully consumed
-    {
-      const uint4* src = reinterpret_cast<const uint4*>(a.blob + (size_t)t0 * rw);
-      uint4* dst = reinterpret_cast<uint4*>(tbuf);
-      const int n16 = (nt * rw) >> 2;
-      for (int i = tid; i < n16; i += TB) dst[i] = src[i];
+    const uint32_t* cur = (c & 1) ? tbuf1 : tbuf0;
+    uint32_t* nxt = (c & 1) ? tbuf0 : tbuf1;
+    const int t1 = t0 + a.chunk_trees;
+    n16 = (t1 < te) ? (min(a.chunk_trees, te - t1) * rw) >> 2 : 0;
+    PF_LOAD(a.blob + (size_t)t1 * rw, n16)
+    if (missing) {
+      traverse_chunk<DEPTH, GENERAL, true, ILP>(a, cur, nt, t0, feat_lane, acc, accl);
+    } else {
+      traverse_chunk<DEPTH, GENERAL, false, ILP>(a, cur, nt, t0, feat_lane, acc, accl);
     }
+    // `nxt` was last read in the previous iteration, before that iteration's barrier
+    PF_STORE(nxt, n16)
     __syncthreads();
-
-    int k = 0;
-    for (; k + ILP <= nt; k += ILP) {
-      uint32_t idx[ILP];
-#pragma unroll
-      for (int j = 0; j < ILP; ++j) idx[j] = 0;
-#pragma unroll
-      for (int d = 0; d < DEPTH; ++d) {
-#pragma unroll
-        for (int j = 0; j < ILP; ++j) {
-          const uint2 nd = *reinterpret_cast<const uint2*>(tbuf + (k + j) * rw + 2 * idx[j]);
-          const float x = *reinterpret_cast<const float*>(feat_lane + (nd.y & 0xFFFFu));
-          bool right = x >= __uint_as_float(nd.x);
-          if (HAS_DR) right = right || ((x != x) && (nd.y >> 31));
-          idx[j] = 2 * idx[j] + 1 + (right ? 1u : 0u);
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < ILP; ++j) {
-        const float* lv = reinterpret_cast<const float*>(tbuf + (k + j) * rw + 2 * NI);
-        if (GENERAL) {
-          const int slot = a.tree_slot[t0 + k + j];
-          for (int p = 0; p < a.P; ++p) accl[(slot + p) * TB + tid] += lv[(idx[j] - NI) * a.P + p];
-        } else {
-          acc += lv[idx[j] - NI];
-        }
-      }
-    }
-    for (; k < nt; ++k) {
-      uint32_t idx = 0;
-#pragma unroll
-      for (int d = 0; d < DEPTH; ++d) {
-        const uint2 nd = *reinterpret_cast<const uint2*>(tbuf + k * rw + 2 * idx);
-        const float x = *reinterpret_cast<const float*>(feat_lane + (nd.y & 0xFFFFu));
-        bool right = x >= __uint_as_float(nd.x);
-        if (HAS_DR) right = right || ((x != x) && (nd.y >> 31));
-        idx = 2 * idx + 1 + (right ? 1u : 0u);
-      }
-      const float* lv = reinterpret_cast<const float*>(tbuf + k * rw + 2 * NI);
-      if (GENERAL) {
-        const int slot = a.tree_slot[t0 + k];
-        for (int p = 0; p < a.P; ++p) accl[(slot + p) * TB + tid] += lv[(idx - NI) * a.P + p];
-      } else {
-        acc += lv[idx - NI];
-      }
-    }
   }
   finish_row(a, acc, accl, split, GENERAL, row, row_ok);
 }
@@ -239,24 +335,14 @@ int prepare_launch(K kernel, size_t lds) {
 }
 
 template <int D>
-int launch_perfect(hipStream_t st, const TreeArgs& a, dim3 grid, size_t lds, bool has_dr) {
+int launch_perfect(hipStream_t st, const TreeArgs& a, dim3 grid, size_t lds) {
   int err = 0;
   if (a.general) {
-    if (has_dr) {
-      err = prepare_launch(tree_perfect_kernel<D, true, true>, lds);
-      if (!err) hipLaunchKernelGGL((tree_perfect_kernel<D, true, true>), grid, dim3(TB), lds, st, a);
-    } else {
-      err = prepare_launch(tree_perfect_kernel<D, true, false>, lds);
-      if (!err) hipLaunchKernelGGL((tree_perfect_kernel<D, true, false>), grid, dim3(TB), lds, st, a);
-    }
+    err = prepare_launch(tree_perfect_kernel<D, true, 4>, lds);
+    if (!err) hipLaunchKernelGGL((tree_perfect_kernel<D, true, 4>), grid, dim3(TB), lds, st, a);
   } else {
-    if (has_dr) {
-      err = prepare_launch(tree_perfect_kernel<D, false, true>, lds);
-      if (!err) hipLaunchKernelGGL((tree_perfect_kernel<D, false, true>), grid, dim3(TB), lds, st, a);
-    } else {
-      err = prepare_launch(tree_perfect_kernel<D, false, false>, lds);
-      if (!err) hipLaunchKernelGGL((tree_perfect_kernel<D, false, false>), grid, dim3(TB), lds, st, a);
-    }
+    err = prepare_launch(tree_perfect_kernel<D, false, 8>, lds);
+    if (!err) hipLaunchKernelGGL((tree_perfect_kernel<D, false, 8>), grid, dim3(TB), lds, st, a);
   }
   return err;
 }
@@ -282,19 +368,20 @@ PMML_API int pmml_tree_launch(hipStream_t stream, const TreeArgs* args, int layo
   const size_t acc_lds = a.general ? (size_t)a.C * TB * 4 : 0;
   if (layout == 0) {
     if (a.n_feat > 64) return -4;
-    const size_t lds = (size_t)a.n_feat * TB * 4 + (size_t)a.chunk_trees * a.rec_words * 4 + TB * 4 + acc_lds;
+    if ((size_t)a.chunk_trees * a.rec_words > (size_t)TB * 4 * PREFETCH_Q) return -9;
+    const size_t lds = (size_t)a.n_feat * TB * 4 + 2 * (size_t)a.chunk_trees * a.rec_words * 4 + (TB + 4) * 4 + acc_lds;
     if (lds > 160 * 1024) return -5;
     switch (depth) {
-      case 1: err = launch_perfect<1>(stream, a, grid, lds, has_dr); break;
-      case 2: err = launch_perfect<2>(stream, a, grid, lds, has_dr); break;
-      case 3: err = launch_perfect<3>(stream, a, grid, lds, has_dr); break;
-      case 4: err = launch_perfect<4>(stream, a, grid, lds, has_dr); break;
-      case 5: err = launch_perfect<5>(stream, a, grid, lds, has_dr); break;
-      case 6: err = launch_perfect<6>(stream, a, grid, lds, has_dr); break;
-      case 7: err = launch_perfect<7>(stream, a, grid, lds, has_dr); break;
-      case 8: err = launch_perfect<8>(stream, a, grid, lds, has_dr); break;
-      case 9: err = launch_perfect<9>(stream, a, grid, lds, has_dr); break;
-      case 10: err = launch_perfect<10>(stream, a, grid, lds, has_dr); break;
+      case 1: err = launch_perfect<1>(stream, a, grid, lds); break;
+      case 2: err = launch_perfect<2>(stream, a, grid, lds); break;
+      case 3: err = launch_perfect<3>(stream, a, grid, lds); break;
+      case 4: err = launch_perfect<4>(stream, a, grid, lds); break;
+      case 5: err = launch_perfect<5>(stream, a, grid, lds); break;
+      case 6: err = launch_perfect<6>(stream, a, grid, lds); break;
+      case 7: err = launch_perfect<7>(stream, a, grid, lds); break;
+      case 8: err = launch_perfect<8>(stream, a, grid, lds); break;
+      case 9: err = launch_perfect<9>(stream, a, grid, lds); break;
+      case 10: err = launch_perfect<10>(stream, a, grid, lds); break;
       default: return -6;
     }
   } else {

@@ -128,10 +128,20 @@ def build_field_prep(compiled, fields: List[str]) -> Tuple[np.ndarray, bool]:
                 constrained = True
                 lo_open = not iv.closure.startswith("closed")
                 hi_open = not iv.closure.endswith("Closed")
-                if iv.left is not None:
-                    lo = _floor32(iv.left) if lo_open else _ceil32(iv.left)
-                if iv.right is not None:
-                    hi = _ceil32(iv.right) if hi_open else _floor32(iv.right)
+                if df.data_type == "float":
+                    # fp32 inputs: directional rounding makes the fp32 test exact
+                    if iv.left is not None:
+                        lo = _floor32(iv.left) if lo_open else _ceil32(iv.left)
+                    if iv.right is not None:
+                        hi = _ceil32(iv.right) if hi_open else _floor32(iv.right)
+                else:
+                    # fp64 inputs arrive rounded-to-nearest: rounding the bounds the same way keeps
+                    # every valid value valid (monotonic rounding); only values within half an
+                    # fp32 ulp outside a bound can be misclassified
+                    if iv.left is not None:
+                        lo = float(np.float32(iv.left))
+                    if iv.right is not None:
+                        hi = float(np.float32(iv.right))
                 fl |= (FP_LO_OPEN if lo_open else 0) | (FP_HI_OPEN if hi_open else 0)
             elif df.values and df.is_string:
                 fl |= FP_CODE_RANGE
@@ -564,9 +574,16 @@ def _chain_spec(compiled, ev: MiningEvaluator, field_index) -> EnsembleSpec:
 
 
 def _perfect_pack(trees: List[BinaryTree], weights: List[float], P: int, D: int) -> Tuple[np.ndarray, int, bool]:
-    """Pack trees into the PERFECT layout: per tree [ (2^D-1) x {T bits, meta} ][ 2^D x P leaves ]."""
+    """Pack trees into the PERFECT layout (heap order, root = node 1):
+
+    ``[ (2^D-1) x {T bits, feature byte offset} ][ 2^D x P leaves ][ ceil((2^D-1)/32) default-right words ]``
+
+    padded to 16 bytes. Split tests are canonicalised to "go right iff x >= T"
+    (:func:`canonical_threshold`); a missing value goes right iff the node's default-right bit is
+    set. Leaves above depth D are replicated over their whole padded subtree."""
     NI, NL = (1 << D) - 1, 1 << D
-    rec = 2 * NI + NL * P
+    ndr = (NI + 31) // 32
+    rec = 2 * NI + NL * P + ndr
     rec = (rec + 3) & ~3
     blob = np.zeros((len(trees), rec), dtype=np.uint32)
     has_dr = False
@@ -574,12 +591,12 @@ def _perfect_pack(trees: List[BinaryTree], weights: List[float], P: int, D: int)
         nodes_T = np.zeros(NI, dtype=np.float32)
         nodes_meta = np.zeros(NI, dtype=np.uint32)
         leaves = np.zeros((NL, P), dtype=np.float32)
-        stack = [(0, 0, 0)]  # (node k, perfect index p, depth)
+        dr_bits = np.zeros(ndr * 32, dtype=np.uint32)
+        stack = [(0, 0, 0)]  # (node k, level-order index p, depth)
         while stack:
             k, p, d = stack.pop()
             if t.feature[k] < 0:
                 val = (t.leaf_probs[k] if t.leaf_probs is not None and P > 1 else np.array([t.leaf_value[k]])) * w
-                # pad: every leaf below perfect index p gets the value
                 lo = p
                 for _ in range(D - d):
                     lo = 2 * lo + 1
@@ -599,13 +616,17 @@ def _perfect_pack(trees: List[BinaryTree], weights: List[float], P: int, D: int)
             if f > 63:
                 raise NotLowerable("perfect layout supports at most 64 features")
             nodes_T[p] = T
-            nodes_meta[p] = (f * TB * 4) | (np.uint32(1) << 31 if dr else 0)
-            has_dr = has_dr or dr
+            nodes_meta[p] = f * TB * 4
+            if dr:
+                dr_bits[p] = 1
+                has_dr = True
             stack.append((left_child, 2 * p + 1, d + 1))
             stack.append((right_child, 2 * p + 2, d + 1))
         blob[ti, 0: 2 * NI: 2] = nodes_T.view(np.uint32)
         blob[ti, 1: 2 * NI: 2] = nodes_meta
         blob[ti, 2 * NI: 2 * NI + NL * P] = leaves.reshape(-1).view(np.uint32)
+        words = (dr_bits.reshape(ndr, 32) << np.arange(32, dtype=np.uint32)[None, :]).sum(axis=1, dtype=np.uint64)
+        blob[ti, 2 * NI + NL * P: 2 * NI + NL * P + ndr] = words.astype(np.uint32)
     return blob, rec, has_dr
 
 
@@ -669,16 +690,21 @@ class TreePlan(DevicePlan):
         self.depth = depth
         self.n_trees = len(spec.trees)
         if layout == "auto":
-            layout = "perfect" if depth <= 10 and F <= 64 else "pointer"
+            NI, NL = (1 << depth) - 1, 1 << depth
+            rec_bytes = 4 * (2 * NI + NL * spec.P + (NI + 31) // 32)
+            layout = "perfect" if depth <= 10 and F <= 64 and rec_bytes <= 32 * 1024 else "pointer"
         self.layout = layout
         self.P, self.C = spec.P, spec.C
         self.general = 1 if spec.P > 1 else 0
         if self.layout == "perfect":
             blob, rec, has_dr = _perfect_pack(spec.trees, spec.weights, spec.P, depth)
             self.rec_words = rec
-            fixed = F * TB * 4 + TB * 4 + (self.C * TB * 4 if self.general else 0)
-            budget = max(lds_budget - fixed, rec * 4)
-            self.chunk_trees = int(max(1, min(self.n_trees, budget // (rec * 4))))
+            fixed = F * TB * 4 + (TB + 4) * 4 + (self.C * TB * 4 if self.general else 0)
+            budget = max(lds_budget - fixed, 2 * rec * 4)  # two chunk buffers (double buffering)
+            per_chunk = min(budget // 2, 32 * 1024)  # register prefetch holds <= 32 KiB per chunk
+            if rec * 4 > per_chunk:
+                raise NotLowerable(f"depth-{depth} tree record ({rec * 4} B) exceeds the 32 KiB chunk")
+            self.chunk_trees = int(max(1, min(self.n_trees, per_chunk // (rec * 4))))
             self.blob = self._t(blob.reshape(-1).view(np.int32))
             self.roots = self.leaves = None
         else:

@@ -36,6 +36,17 @@ for s in $STEPS; do
           > "$OUT/prof.log" 2>&1 ); rc=$?
       echo "=== prof rc=$rc" | tee -a "$OUT/session.log"
       if fatal $rc; then exit $rc; fi ;;
+    kbench)
+      run kbench 600 bash -c 'for m in 0 0.02; do for b in 81920 49152 110592; do python scripts/kbench.py --missing $m --lds-budget $b || exit 1; done; done; python scripts/kbench.py --model rf --trees 500 --depth 8; python scripts/kbench.py --model gbdt-binary; python scripts/kbench.py --model kmeans; python scripts/kbench.py --layout pointer --iters 3' ;;
+    pmc)
+      mkdir -p "$OUT/pmc"
+      rocprofv3 -L > "$OUT/pmc/counters.txt" 2>&1 || true
+      ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats \
+          --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY \
+          -d "$OUT/pmc" -o pmc --output-format csv -- python3 "$ROOT/scripts/kbench.py" --iters 3 \
+          > "$OUT/pmc.log" 2>&1 ); rc=$?
+      echo "=== pmc rc=$rc" | tee -a "$OUT/session.log"
+      if fatal $rc; then exit $rc; fi ;;
     *) echo "unknown step $s" ;;
   esac
 done

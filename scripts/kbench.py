@@ -1,0 +1,75 @@
+#!/usr/bin/env python3
+"""Kernel-only micro-benchmark (device-resident records) for profiling the scoring kernels.
+
+python scripts/kbench.py --model gbdt --rows 1048576 --iters 20
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--model", default="gbdt", choices=["gbdt", "gbdt-binary", "rf", "kmeans", "mlp", "svm", "lr"])
+    p.add_argument("--rows", type=int, default=1 << 20)
+    p.add_argument("--iters", type=int, default=20)
+    p.add_argument("--trees", type=int, default=1000)
+    p.add_argument("--depth", type=int, default=6)
+    p.add_argument("--features", type=int, default=32)
+    p.add_argument("--missing", type=float, default=0.0)
+    p.add_argument("--layout", default="auto")
+    p.add_argument("--lds-budget", type=int, default=80 * 1024)
+    args = p.parse_args()
+    import numpy as np
+    import torch
+
+    from flink_jpmml_amd.bench import synth
+    from flink_jpmml_amd.runtime.compiled import CompiledPmml
+
+    if args.model == "gbdt":
+        txt = synth.gbdt_pmml(n_trees=args.trees, depth=args.depth, n_features=args.features)
+    elif args.model == "gbdt-binary":
+        txt = synth.gbdt_pmml(n_trees=args.trees, depth=args.depth, n_features=args.features, objective="binary")
+    elif args.model == "rf":
+        txt = synth.random_forest_pmml(n_trees=args.trees, depth=args.depth, n_features=args.features)
+    elif args.model == "mlp":
+        txt = synth.mlp_pmml(n_features=args.features)
+    elif args.model == "svm":
+        txt = synth.svm_pmml(n_features=args.features)
+    elif args.model == "lr":
+        txt = synth.iris_logistic_pmml()
+    else:
+        from flink_jpmml_amd.assets import kmeans_pmml
+
+        txt = kmeans_pmml()
+    c = CompiledPmml.from_string(txt)
+    opts = {}
+    if args.model.startswith(("gbdt", "rf")):
+        opts = dict(layout=args.layout, lds_budget=args.lds_budget)
+    plan = c.plan("cuda:0", **opts)
+    F = c.n_features
+    X = torch.from_numpy(synth.stream_matrix(args.rows, F, seed=1, missing_rate=args.missing)).cuda()
+    s = torch.empty(args.rows, device="cuda")
+    v = torch.empty(args.rows, dtype=torch.uint8, device="cuda")
+    for _ in range(3):
+        plan.launch(X, s, v)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(args.iters):
+        plan.launch(X, s, v)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / args.iters
+    print(json.dumps({"model": args.model, "rows": args.rows, "features": F, "ms": ms,
+                      "rows_per_s": args.rows / ms * 1e3, "plan": type(plan).__name__,
+                      "layout": getattr(plan, "layout", None), "chunk_trees": getattr(plan, "chunk_trees", None),
+                      "missing": args.missing, "lds_budget": args.lds_budget}))
+
+
+if __name__ == "__main__":
+    main()

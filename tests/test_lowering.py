@@ -1,0 +1,109 @@
+"""CPU checks of the device lowering: a numpy emulation of the PERFECT-layout traversal kernel
+(heap index, canonical ``x >= T`` splits, default-right bit words, fused epilogue) must agree with
+the float64 oracle — this pins the packing format without a GPU."""
+
+import numpy as np
+import pytest
+
+from flink_jpmml_amd.bench.synth import gbdt_pmml, random_forest_pmml, stream_matrix
+from flink_jpmml_amd.models.tree import OP_GE, OP_GT, OP_LE, OP_LT
+from flink_jpmml_amd.runtime.compiled import CompiledPmml
+from flink_jpmml_amd.runtime.plans import TB, _perfect_pack, _pointer_pack, canonical_threshold, ensemble_spec
+
+
+def emulate_perfect(c, X):
+    spec = ensemble_spec(c)
+    D = max(t.depth for t in spec.trees)
+    P = spec.P
+    blob, rec, _ = _perfect_pack(spec.trees, spec.weights, P, D)
+    assert rec % 4 == 0
+    NI, NL = (1 << D) - 1, 1 << D
+    Xf = X.astype(np.float32)
+    n = len(X)
+    acc = np.zeros((n, P), np.float32)
+    for ti in range(blob.shape[0]):
+        T = blob[ti, 0:2 * NI:2].view(np.float32)
+        meta = blob[ti, 1:2 * NI:2]
+        leaves = blob[ti, 2 * NI:2 * NI + NL * P].view(np.float32).reshape(NL, P)
+        drw = blob[ti, 2 * NI + NL * P: 2 * NI + NL * P + (NI + 31) // 32]
+        j = np.ones(n, np.int64)
+        for _ in range(D):
+            f = meta[j - 1] // (TB * 4)
+            x = Xf[np.arange(n), f]
+            dr = (drw[(j - 1) >> 5] >> ((j - 1) & 31)) & 1
+            right = (x >= T[j - 1]) | (np.isnan(x) & (dr == 1))
+            j = 2 * j + right
+        acc += leaves[j - NL]
+    return spec, acc
+
+
+def emulate_pointer(c, X):
+    spec = ensemble_spec(c)
+    nodes, leaves, roots, _ = _pointer_pack(spec.trees, spec.weights, spec.P)
+    Xf = X.astype(np.float32)
+    acc = np.zeros((len(X), spec.P), np.float32)
+    for r in range(len(X)):
+        for root in roots:
+            code = int(root)
+            while code >= 0:
+                T, meta, lc, rc = nodes[code]
+                f = int(meta) & 0xFFFF
+                f = f // (TB * 4)
+                x = Xf[r, f]
+                right = (x >= np.uint32(T).view(np.float32)) or (np.isnan(x) and (int(meta) >> 31) & 1)
+                code = int(np.int32(np.uint32(rc if right else lc)))
+            acc[r] += leaves[~code]
+    return spec, acc
+
+
+def _scores(spec, acc):
+    e = spec.epi
+    if e["mode"] == 0:
+        return e["a"] * acc[:, 0] + e["b"]
+    tab = np.array([float(x) for x in spec.labels])
+    if e["mode"] == 1:
+        p0 = 1.0 / (1.0 + np.exp(-(e["a"] * acc[:, 0] + e["b"])))
+        return tab[np.where(p0 >= 0.5, 0, 1)]
+    return tab[np.argmax(acc, axis=1)]
+
+
+@pytest.mark.parametrize("kind", ["regression", "binary", "rf"])
+def test_perfect_layout_emulation_matches_oracle(kind):
+    if kind == "rf":
+        txt = random_forest_pmml(n_trees=15, depth=6, n_features=10, n_classes=3, seed=3)
+    else:
+        txt = gbdt_pmml(n_trees=40, depth=5, n_features=12, seed=1, objective=kind)
+    c = CompiledPmml.from_string(txt)
+    X = stream_matrix(3000, c.n_features, seed=2, missing_rate=0.05)
+    ref, vref = c.score_matrix_oracle(X)
+    spec, acc = emulate_perfect(c, X)
+    out = _scores(spec, acc)
+    assert vref.all()
+    if kind == "regression":
+        assert np.max(np.abs(out - ref)) < 1e-5
+    else:
+        assert (out == ref).all()
+
+
+def test_pointer_layout_emulation_matches_oracle():
+    c = CompiledPmml.from_string(gbdt_pmml(n_trees=6, depth=7, n_features=9, seed=4))
+    X = stream_matrix(200, 9, seed=5, missing_rate=0.1)
+    ref, _ = c.score_matrix_oracle(X)
+    spec, acc = emulate_pointer(c, X)
+    assert np.max(np.abs(_scores(spec, acc) - ref)) < 1e-5
+
+
+@pytest.mark.parametrize("op", [OP_LT, OP_LE, OP_GT, OP_GE])
+def test_canonical_threshold_exact_for_fp32_inputs(op):
+    """For every fp32 x near t the canonical `x >= T` test reproduces the fp64 comparison."""
+    rng = np.random.default_rng(op)
+    for t in list(rng.standard_normal(200)) + [0.1, 0.5, 1e-30, -2.5, 3.0, 16777217.0]:
+        T, swap = canonical_threshold(op, float(t))
+        f = np.float32(t)
+        cands = [f, np.nextafter(f, np.float32(np.inf)), np.nextafter(f, np.float32(-np.inf)),
+                 np.nextafter(np.nextafter(f, np.float32(np.inf)), np.float32(np.inf))]
+        for x in cands:
+            xd = float(x)
+            first = {OP_LT: xd < t, OP_LE: xd <= t, OP_GT: xd > t, OP_GE: xd >= t}[op]
+            right = bool(np.float32(x) >= np.float32(T))
+            assert first == (right if swap else not right), (op, t, x, T)
