@@ -110,7 +110,7 @@ class TreeArgs(ctypes.Structure):
                 ("prep", c_void_p), ("row_valid_in", c_void_p), ("blob", c_void_p), ("roots", c_void_p),
                 ("leaves", c_void_p), ("tree_slot", c_void_p), ("n_trees", c_int), ("rec_words", c_int),
                 ("chunk_trees", c_int), ("P", c_int), ("C", c_int), ("trees_per_split", c_int),
-                ("general", c_int), ("pad1", c_int), ("epi", Epilogue), ("score", c_void_p),
+                ("general", c_int), ("variant", c_int), ("epi", Epilogue), ("score", c_void_p),
                 ("valid", c_void_p), ("probs", c_void_p), ("partial", c_void_p)]
 
 

@@ -32,7 +32,7 @@ struct TreeArgs {
   const float* leaves;          // pointer layout: [n_leaves][P]
   const int* tree_slot;         // general accumulation: slot per tree
   int n_trees, rec_words, chunk_trees, P;
-  int C, trees_per_split, general, pad1;
+  int C, trees_per_split, general, variant;  // variant 1: wide (v3) perfect kernel
   Epilogue epi;
   float* score;
   uint8_t* valid;
@@ -245,6 +245,188 @@ __global__ __launch_bounds__(TB, 2) void tree_perfect_kernel(TreeArgs a) {
   finish_row(a, acc, accl, split, GENERAL, row, row_ok);
 }
 
+// ------------------------------------------------------------------------------------------
+// v3: wide workgroup, tree-group parallel. 256 rows x G tree groups = 256*G threads (G=4: 16
+// waves, one workgroup per CU). Half-wave hw = 2*wave + (lane >= 32) owns row set hw % 8 (32
+// rows) and tree group hw / 8, so each 32-lane LDS access group reads 32 distinct rows (feature
+// reads conflict free) and both halves of a wave walk the same trees. Group g takes trees
+// k ≡ g (mod G) of every chunk; the G partial sums of a row are added in fixed order g = 0..G-1
+// (deterministic). Twice the resident waves of the v2 layout at the same LDS footprint: the
+// traversal is latency bound (SQ_WAIT_ANY ~49% of wave cycles in v2), so occupancy is the lever.
+#define PF4_DECL uint4 pq0, pq1, pq2, pq3;
+#define PF4_LOAD(SRC, N16, T)                                                          \
+  {                                                                                    \
+    const uint4* s4_ = reinterpret_cast<const uint4*>(SRC);                            \
+    const int last_ = (N16) > 0 ? (N16) - 1 : 0;                                      \
+    pq0 = s4_[min((int)threadIdx.x + 0 * (T), last_)];                                 \
+    pq1 = s4_[min((int)threadIdx.x + 1 * (T), last_)];                                 \
+    pq2 = s4_[min((int)threadIdx.x + 2 * (T), last_)];                                 \
+    pq3 = s4_[min((int)threadIdx.x + 3 * (T), last_)];                                 \
+  }
+#define PF4_STORE(DST, N16, T)                                                         \
+  {                                                                                    \
+    uint4* d4_ = reinterpret_cast<uint4*>(DST);                                        \
+    const int i0_ = (int)threadIdx.x;                                                  \
+    if (i0_ < (N16)) d4_[i0_] = pq0;                                                   \
+    if (i0_ + (T) < (N16)) d4_[i0_ + (T)] = pq1;                                       \
+    if (i0_ + 2 * (T) < (N16)) d4_[i0_ + 2 * (T)] = pq2;                               \
+    if (i0_ + 3 * (T) < (N16)) d4_[i0_ + 3 * (T)] = pq3;                               \
+  }
+
+template <int DEPTH, bool MISSING, int ILP, int G>
+__device__ __forceinline__ float traverse_chunk_g(const TreeArgs& a, const uint32_t* buf, int nt, int g,
+                                                  const char* feat_lane, float acc) {
+  constexpr int NI = (1 << DEPTH) - 1;
+  constexpr int NL = 1 << DEPTH;
+  const int rw = a.rec_words;
+  const int dr_off = 2 * NI + NL;
+  // my trees: k = g + G*m, m = 0..mt-1
+  const int mt = (nt - g + G - 1) / G;
+  int m = 0;
+  for (; m + ILP <= mt; m += ILP) {
+    uint32_t j[ILP];
+    const char* base[ILP];
+#pragma unroll
+    for (int i = 0; i < ILP; ++i) {
+      j[i] = 1u;
+      base[i] = reinterpret_cast<const char*>(buf + (g + G * (m + i)) * rw);
+    }
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) {
+#pragma unroll
+      for (int i = 0; i < ILP; ++i) {
+        const uint2 nd = *reinterpret_cast<const uint2*>(base[i] - 8 + (j[i] << 3));
+        const float x = *reinterpret_cast<const float*>(feat_lane + nd.y);
+        uint32_t right = (x >= __uint_as_float(nd.x)) ? 1u : 0u;
+        if (MISSING) {
+          const uint32_t n = j[i] - 1u;
+          const uint32_t w = reinterpret_cast<const uint32_t*>(base[i])[dr_off + (n >> 5)];
+          right |= ((x != x) ? 1u : 0u) & (w >> (n & 31u));
+        }
+        j[i] = j[i] + j[i] + right;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < ILP; ++i) {
+      const float* lv = reinterpret_cast<const float*>(base[i] + NI * 8) - NL;
+      acc += lv[j[i]];
+    }
+  }
+  for (; m < mt; ++m) {
+    uint32_t j = 1u;
+    const char* base = reinterpret_cast<const char*>(buf + (g + G * m) * rw);
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) {
+      const uint2 nd = *reinterpret_cast<const uint2*>(base - 8 + (j << 3));
+      const float x = *reinterpret_cast<const float*>(feat_lane + nd.y);
+      uint32_t right = (x >= __uint_as_float(nd.x)) ? 1u : 0u;
+      if (MISSING) {
+        const uint32_t n = j - 1u;
+        const uint32_t w = reinterpret_cast<const uint32_t*>(base)[dr_off + (n >> 5)];
+        right |= ((x != x) ? 1u : 0u) & (w >> (n & 31u));
+      }
+      j = j + j + right;
+    }
+    const float* lv = reinterpret_cast<const float*>(base + NI * 8) - NL;
+    acc += lv[j];
+  }
+  return acc;
+}
+
+template <int DEPTH, int ILP, int G>
+__global__ __launch_bounds__(TB * G, 1) void tree_perfect_wide_kernel(TreeArgs a) {
+  constexpr int T = TB * G;
+  extern __shared__ __align__(16) uint32_t smem[];
+  const int rw = a.rec_words;
+  const int chunk_words = a.chunk_trees * rw;
+  float* feat = reinterpret_cast<float*>(smem);
+  uint32_t* tbuf0 = smem + a.n_feat * TB;
+  uint32_t* tbuf1 = tbuf0 + chunk_words;
+  int* bad = reinterpret_cast<int*>(tbuf1 + chunk_words);
+  int* any_missing = bad + TB;
+  float* part = reinterpret_cast<float*>(bad + TB + 4);  // [G][TB]
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int hw = (tid >> 6) * 2 + (lane >> 5);
+  const int r_local = 32 * (hw & 7) + (lane & 31);
+  const int g = hw >> 3;
+  const int row0 = blockIdx.x * TB;
+  const int split = blockIdx.y;
+  const int tb = split * a.trees_per_split;
+  const int te = min(a.n_trees, tb + a.trees_per_split);
+
+  PF4_DECL
+  int n16 = (tb < te) ? (min(a.chunk_trees, te - tb) * rw) >> 2 : 0;
+  PF4_LOAD(a.blob + (size_t)tb * rw, n16, T)
+
+  if (tid == 0) *any_missing = 0;
+  if (tid < TB) bad[tid] = 0;
+  __syncthreads();
+  {
+    const int F = a.n_feat;
+    const int total = TB * F;
+    bool miss = false;
+    for (int e = tid; e < total; e += T) {
+      const int r = e / F;
+      const int f = e - r * F;
+      const int row = row0 + r;
+      float x = 0.f;
+      bool b = false;
+      if (row < a.n_rows) {
+        x = a.X[(size_t)row * a.ldx + f];
+        if (a.prep) x = prep_value(x, a.prep[f], &b);
+        miss = miss || (x != x);
+      }
+      feat[f * TB + r] = x;
+      if (b) bad[r] = 1;
+    }
+    if (__any(miss) && lane == 0) *any_missing = 1;
+  }
+  PF4_STORE(tbuf0, n16, T)
+  __syncthreads();
+
+  const bool missing = *any_missing != 0;
+  float acc = 0.f;
+  const char* feat_lane = reinterpret_cast<const char*>(feat + r_local);
+  int c = 0;
+  for (int t0 = tb; t0 < te; t0 += a.chunk_trees, ++c) {
+    const int nt = min(a.chunk_trees, te - t0);
+    const uint32_t* cur = (c & 1) ? tbuf1 : tbuf0;
+    uint32_t* nxt = (c & 1) ? tbuf0 : tbuf1;
+    const int t1 = t0 + a.chunk_trees;
+    n16 = (t1 < te) ? (min(a.chunk_trees, te - t1) * rw) >> 2 : 0;
+    PF4_LOAD(a.blob + (size_t)t1 * rw, n16, T)
+    if (missing) {
+      acc = traverse_chunk_g<DEPTH, true, ILP, G>(a, cur, nt, g, feat_lane, acc);
+    } else {
+      acc = traverse_chunk_g<DEPTH, false, ILP, G>(a, cur, nt, g, feat_lane, acc);
+    }
+    PF4_STORE(nxt, n16, T)
+    __syncthreads();
+  }
+  part[g * TB + r_local] = acc;
+  __syncthreads();
+  if (g == 0) {
+    float sum = part[r_local];
+#pragma unroll
+    for (int q = 1; q < G; ++q) sum += part[q * TB + r_local];
+    const int row = row0 + r_local;
+    bool row_ok = bad[r_local] == 0;
+    if (a.row_valid_in && row < a.n_rows) row_ok = row_ok && a.row_valid_in[row];
+    if (row < a.n_rows) {
+      if (a.partial) {
+        const size_t stride = (size_t)a.n_rows;
+        float* pbase = a.partial + (size_t)split * 2 * stride;
+        pbase[row] = sum;
+        pbase[stride + row] = row_ok ? 0.f : 1.f;
+      } else {
+        apply_epilogue(a.epi, [&](int) { return sum; }, row_ok, row, a.n_rows, a.score, a.valid, a.probs);
+      }
+    }
+  }
+}
+
 // Pointer layout: nodes uint4 {T bits, meta, left, right}; child < 0 => leaf ~child.
 template <bool GENERAL, bool FEAT_LDS>
 __global__ __launch_bounds__(TB, 2) void tree_pointer_kernel(TreeArgs a) {
@@ -334,9 +516,19 @@ int prepare_launch(K kernel, size_t lds) {
   return 0;
 }
 
+constexpr int WIDE_G = 4;
+
 template <int D>
 int launch_perfect(hipStream_t st, const TreeArgs& a, dim3 grid, size_t lds) {
   int err = 0;
+  if (!a.general && a.variant == 1) {
+    const size_t lds_w = lds + (size_t)WIDE_G * TB * 4;
+    if (lds_w > 160 * 1024) return -5;
+    if ((size_t)a.chunk_trees * a.rec_words > (size_t)TB * WIDE_G * 4 * 4) return -9;
+    err = prepare_launch(tree_perfect_wide_kernel<D, 8, WIDE_G>, lds_w);
+    if (!err) hipLaunchKernelGGL((tree_perfect_wide_kernel<D, 8, WIDE_G>), grid, dim3(TB * WIDE_G), lds_w, st, a);
+    return err;
+  }
   if (a.general) {
     err = prepare_launch(tree_perfect_kernel<D, true, 4>, lds);
     if (!err) hipLaunchKernelGGL((tree_perfect_kernel<D, true, 4>), grid, dim3(TB), lds, st, a);
@@ -368,7 +560,7 @@ PMML_API int pmml_tree_launch(hipStream_t stream, const TreeArgs* args, int layo
   const size_t acc_lds = a.general ? (size_t)a.C * TB * 4 : 0;
   if (layout == 0) {
     if (a.n_feat > 64) return -4;
-    if ((size_t)a.chunk_trees * a.rec_words > (size_t)TB * 4 * PREFETCH_Q) return -9;
+    if (a.variant != 1 && (size_t)a.chunk_trees * a.rec_words > (size_t)TB * 4 * PREFETCH_Q) return -9;
     const size_t lds = (size_t)a.n_feat * TB * 4 + 2 * (size_t)a.chunk_trees * a.rec_words * 4 + (TB + 4) * 4 + acc_lds;
     if (lds > 160 * 1024) return -5;
     switch (depth) {

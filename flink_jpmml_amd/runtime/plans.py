@@ -678,9 +678,13 @@ class TreePlan(DevicePlan):
 
     kind = "tree"
     _STATE = DevicePlan._STATE + ("depth", "n_trees", "layout", "P", "C", "general", "rec_words", "chunk_trees",
-                                  "blob", "leaves", "roots", "has_dr", "table", "slots", "splits", "epi_args")
+                                  "blob", "leaves", "roots", "has_dr", "table", "slots", "splits", "epi_args",
+                                  "variant")
 
-    def __init__(self, compiled, device, layout: str = "auto", lds_budget: int = 80 * 1024, splits: int = 0):
+    WIDE_G = 4  # tree groups of the wide kernel (mirrors csrc)
+
+    def __init__(self, compiled, device, layout: str = "auto", lds_budget: int = 80 * 1024, splits: int = 0,
+                 variant: str = "auto"):
         super().__init__(compiled, device)
         spec = ensemble_spec(compiled)
         self.spec = spec
@@ -699,9 +703,18 @@ class TreePlan(DevicePlan):
         if self.layout == "perfect":
             blob, rec, has_dr = _perfect_pack(spec.trees, spec.weights, spec.P, depth)
             self.rec_words = rec
-            fixed = F * TB * 4 + (TB + 4) * 4 + (self.C * TB * 4 if self.general else 0)
-            budget = max(lds_budget - fixed, 2 * rec * 4)  # two chunk buffers (double buffering)
-            per_chunk = min(budget // 2, 32 * 1024)  # register prefetch holds <= 32 KiB per chunk
+            if variant == "auto":
+                variant = "narrow" if self.general else "wide"
+            self.variant = 1 if variant == "wide" else 0
+            if self.variant == 1:
+                # one 1024-thread workgroup per CU: features + two chunk buffers + [G][256] partials
+                fixed = F * TB * 4 + (TB + 4) * 4 + self.WIDE_G * TB * 4
+                budget = 156 * 1024 - fixed
+                per_chunk = min(budget // 2, 64 * 1024)
+            else:
+                fixed = F * TB * 4 + (TB + 4) * 4 + (self.C * TB * 4 if self.general else 0)
+                budget = max(lds_budget - fixed, 2 * rec * 4)  # two chunk buffers (double buffering)
+                per_chunk = min(budget // 2, 32 * 1024)  # register prefetch holds <= 32 KiB per chunk
             if rec * 4 > per_chunk:
                 raise NotLowerable(f"depth-{depth} tree record ({rec * 4} B) exceeds the 32 KiB chunk")
             self.chunk_trees = int(max(1, min(self.n_trees, per_chunk // (rec * 4))))
@@ -711,6 +724,7 @@ class TreePlan(DevicePlan):
             nodes, leaves, roots, has_dr = _pointer_pack(spec.trees, spec.weights, spec.P)
             self.rec_words = 0
             self.chunk_trees = 0
+            self.variant = 0
             self.blob = self._t(nodes.reshape(-1).view(np.int32))
             self.leaves = self._t(leaves.reshape(-1))
             self.roots = self._t(roots)
@@ -747,7 +761,7 @@ class TreePlan(DevicePlan):
         a.prep, a.row_valid_in = ptr(self.prep), ptr(row_valid)
         a.blob, a.roots, a.leaves, a.tree_slot = ptr(self.blob), ptr(self.roots), ptr(self.leaves), ptr(self.slots)
         a.n_trees, a.rec_words, a.chunk_trees, a.P = self.n_trees, self.rec_words, self.chunk_trees, self.P
-        a.C, a.general = self.C, self.general
+        a.C, a.general, a.variant = self.C, self.general, self.variant
         a.epi = _epilogue(table=self.table, write_probs=probs is not None, **self.epi_args)
         a.score, a.valid, a.probs = ptr(score), ptr(valid), ptr(probs)
         if s > 1:

@@ -37,7 +37,7 @@ for s in $STEPS; do
       echo "=== prof rc=$rc" | tee -a "$OUT/session.log"
       if fatal $rc; then exit $rc; fi ;;
     kbench)
-      run kbench 600 bash -c 'for m in 0 0.02; do for b in 81920 49152 110592; do python scripts/kbench.py --missing $m --lds-budget $b || exit 1; done; done; python scripts/kbench.py --model rf --trees 500 --depth 8; python scripts/kbench.py --model gbdt-binary; python scripts/kbench.py --model kmeans; python scripts/kbench.py --layout pointer --iters 3' ;;
+      run kbench 600 bash -c "${KBENCH_CMD:-python scripts/kbench.py}" ;;
     pmc)
       mkdir -p "$OUT/pmc"
       rocprofv3 -L > "$OUT/pmc/counters.txt" 2>&1 || true

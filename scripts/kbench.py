@@ -14,7 +14,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--model", default="gbdt", choices=["gbdt", "gbdt-binary", "rf", "kmeans", "mlp", "svm", "lr"])
+    p.add_argument("--model", default="gbdt", choices=["gbdt", "gbdt-binary", "rf", "kmeans", "mlp", "svm", "lr", "pcie"])
     p.add_argument("--rows", type=int, default=1 << 20)
     p.add_argument("--iters", type=int, default=20)
     p.add_argument("--trees", type=int, default=1000)
@@ -23,6 +23,7 @@ def main():
     p.add_argument("--missing", type=float, default=0.0)
     p.add_argument("--layout", default="auto")
     p.add_argument("--lds-budget", type=int, default=80 * 1024)
+    p.add_argument("--variant", default="auto")
     args = p.parse_args()
     import numpy as np
     import torch
@@ -30,6 +31,21 @@ def main():
     from flink_jpmml_amd.bench import synth
     from flink_jpmml_amd.runtime.compiled import CompiledPmml
 
+    if args.model == "pcie":
+        F = args.features
+        Xh = torch.from_numpy(synth.stream_matrix(args.rows, F, seed=1)).pin_memory()
+        Xd = torch.empty_like(Xh, device="cuda")
+        res = {}
+        for name, fn in (("h2d", lambda: Xd.copy_(Xh, non_blocking=True)), ("d2h", lambda: Xh.copy_(Xd, non_blocking=True))):
+            fn(); torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(args.iters):
+                fn()
+            torch.cuda.synchronize()
+            dt = (time.perf_counter() - t0) / args.iters
+            res[name + "_GBps"] = Xh.numel() * 4 / dt / 1e9
+        print(json.dumps({"model": "pcie", "bytes": Xh.numel() * 4, **res}))
+        return
     if args.model == "gbdt":
         txt = synth.gbdt_pmml(n_trees=args.trees, depth=args.depth, n_features=args.features)
     elif args.model == "gbdt-binary":
@@ -49,7 +65,7 @@ def main():
     c = CompiledPmml.from_string(txt)
     opts = {}
     if args.model.startswith(("gbdt", "rf")):
-        opts = dict(layout=args.layout, lds_budget=args.lds_budget)
+        opts = dict(layout=args.layout, lds_budget=args.lds_budget, variant=args.variant)
     plan = c.plan("cuda:0", **opts)
     F = c.n_features
     X = torch.from_numpy(synth.stream_matrix(args.rows, F, seed=1, missing_rate=args.missing)).cuda()
@@ -68,7 +84,8 @@ def main():
     print(json.dumps({"model": args.model, "rows": args.rows, "features": F, "ms": ms,
                       "rows_per_s": args.rows / ms * 1e3, "plan": type(plan).__name__,
                       "layout": getattr(plan, "layout", None), "chunk_trees": getattr(plan, "chunk_trees", None),
-                      "missing": args.missing, "lds_budget": args.lds_budget}))
+                      "missing": args.missing, "lds_budget": args.lds_budget,
+                      "variant": getattr(plan, "variant", None)}))
 
 
 if __name__ == "__main__":
