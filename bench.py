@@ -43,6 +43,7 @@ def parse_args(argv=None):
     p.add_argument("--features", type=int, default=32)
     p.add_argument("--rows", type=int, default=1 << 20, help="rows per GPU per step")
     p.add_argument("--micro-batch", type=int, default=1 << 17)
+    p.add_argument("--depth", type=int, default=4, help="input ring slots (H2D/compute overlap)")
     p.add_argument("--objective", choices=["regression", "binary"], default="regression")
     p.add_argument("--latency-batch", type=int, default=4096)
     p.add_argument("--latency-iters", type=int, default=50)
@@ -101,21 +102,24 @@ def main(argv=None) -> int:
     X = torch.from_numpy(stream_matrix(args.rows, args.features, seed=1000 + ctx.rank)).pin_memory()
     score_h = torch.empty(args.rows, dtype=torch.float32).pin_memory()
     valid_h = torch.empty(args.rows, dtype=torch.uint8).pin_memory()
-    scorer = StreamingScorer(plan, micro_batch=args.micro_batch, depth=3, max_rows=args.rows)
+    scorer = StreamingScorer(plan, micro_batch=args.micro_batch, depth=args.depth, max_rows=args.rows)
     gather_out = None
     if N > 1 and not args.no_allgather:
         gather_out = (torch.empty(args.rows * N, dtype=torch.float32, device=device),
                       torch.empty(args.rows * N, dtype=torch.uint8, device=device))
 
+    comm = torch.cuda.Stream(device) if gather_out is not None else None
+
     def step():
         h = scorer.submit(X, score_h, valid_h)
-        works = []
         if gather_out is not None:
-            with torch.cuda.stream(scorer.comp):
-                _, _, works = all_gather_scores(scorer.score_dev[: args.rows], scorer.valid_dev[: args.rows], ctx,
-                                                async_op=True, out=gather_out)
+            # all-gather this step's scored shard on a side stream (overlaps the next step)
+            comm.wait_stream(scorer.comp)
+            with torch.cuda.stream(comm):
+                _, _, works = all_gather_scores(h.score_dev, h.valid_dev, ctx, async_op=True, out=gather_out)
                 for w in works:
-                    w.wait()  # comp stream waits for the gather: next step cannot overwrite the shard early
+                    w.wait()
+            scorer.mark_consumed(h, comm)
         return h
 
     for _ in range(args.warmup):
@@ -125,10 +129,15 @@ def main(argv=None) -> int:
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     h = None
+    host_submit = 0.0
     for _ in range(args.steps):
+        ts = time.perf_counter()
         h = step()
+        host_submit += time.perf_counter() - ts
     scorer.wait(h)
     scorer.join()
+    if comm is not None:
+        torch.cuda.current_stream().wait_stream(comm)
     torch.cuda.synchronize()
     ctx.barrier()
     torch.cuda.synchronize()
@@ -191,6 +200,7 @@ def main(argv=None) -> int:
                 "seq_len": None,
                 "parallelism": f"dp{N}",
                 "micro_batch": args.micro_batch,
+                "pipeline_depth": args.depth,
                 "rows_per_gpu_per_step": args.rows,
                 "allgather_sink": bool(gather_out is not None),
             },
@@ -200,6 +210,7 @@ def main(argv=None) -> int:
             "kernel_only_records_per_s_per_gpu": args.rows / (kernel_ms / 1e3),
             "kernel_ms_per_1M_rows": kernel_ms * (1 << 20) / args.rows,
             "model_load_broadcast_s": load_s,
+            "host_submit_ms_per_step": host_submit / args.steps * 1e3,
             "plan": {"layout": getattr(plan, "layout", None), "depth": getattr(plan, "depth", None),
                      "chunk_trees": getattr(plan, "chunk_trees", None)},
             "check": check,

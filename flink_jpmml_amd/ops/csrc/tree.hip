@@ -186,7 +186,7 @@ __global__ __launch_bounds__(TB, 2) void tree_perfect_kernel(TreeArgs a) {
   // chunk 0: issue its loads before the row staging so the two overlap
   PF_DECL
   int n16 = (tb < te) ? (min(a.chunk_trees, te - tb) * rw) >> 2 : 0;
-  PF_LOAD(a.blob + (size_t)tb * rw, n16)
+  PF_LOAD(n16 > 0 ? a.blob + (size_t)tb * rw : a.blob, n16)
 
   // stage rows [F][TB] with field preparation; rows past the end are zero (never "missing")
   if (tid == 0) *any_missing = 0;
@@ -232,7 +232,7 @@ __global__ __launch_bounds__(TB, 2) void tree_perfect_kernel(TreeArgs a) {
     uint32_t* nxt = (c & 1) ? tbuf0 : tbuf1;
     const int t1 = t0 + a.chunk_trees;
     n16 = (t1 < te) ? (min(a.chunk_trees, te - t1) * rw) >> 2 : 0;
-    PF_LOAD(a.blob + (size_t)t1 * rw, n16)
+    PF_LOAD(n16 > 0 ? a.blob + (size_t)t1 * rw : a.blob, n16)  // never form an OOB address
     if (missing) {
       traverse_chunk<DEPTH, GENERAL, true, ILP>(a, cur, nt, t0, feat_lane, acc, accl);
     } else {
@@ -358,7 +358,7 @@ __global__ __launch_bounds__(TB * G, 1) void tree_perfect_wide_kernel(TreeArgs a
 
   PF4_DECL
   int n16 = (tb < te) ? (min(a.chunk_trees, te - tb) * rw) >> 2 : 0;
-  PF4_LOAD(a.blob + (size_t)tb * rw, n16, T)
+  PF4_LOAD(n16 > 0 ? a.blob + (size_t)tb * rw : a.blob, n16, T)
 
   if (tid == 0) *any_missing = 0;
   if (tid < TB) bad[tid] = 0;
@@ -396,7 +396,7 @@ __global__ __launch_bounds__(TB * G, 1) void tree_perfect_wide_kernel(TreeArgs a
     uint32_t* nxt = (c & 1) ? tbuf0 : tbuf1;
     const int t1 = t0 + a.chunk_trees;
     n16 = (t1 < te) ? (min(a.chunk_trees, te - t1) * rw) >> 2 : 0;
-    PF4_LOAD(a.blob + (size_t)t1 * rw, n16, T)
+    PF4_LOAD(n16 > 0 ? a.blob + (size_t)t1 * rw : a.blob, n16, T)
     if (missing) {
       acc = traverse_chunk_g<DEPTH, true, ILP, G>(a, cur, nt, g, feat_lane, acc);
     } else {

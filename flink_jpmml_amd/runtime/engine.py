@@ -25,11 +25,15 @@ import numpy as np
 @dataclass
 class StepHandle:
     n: int
-    done: object  # torch.cuda.Event recorded on the D2H stream
+    done: object  # torch.cuda.Event recorded on the D2H (or compute) stream
+    score_dev: object = None
+    valid_dev: object = None
+    out_index: int = 0
 
 
 class StreamingScorer:
-    def __init__(self, plan, micro_batch: int = 131072, depth: int = 3, max_rows: Optional[int] = None):
+    def __init__(self, plan, micro_batch: int = 131072, depth: int = 3, max_rows: Optional[int] = None,
+                 out_buffers: int = 2):
         import torch
 
         self.plan = plan
@@ -44,71 +48,96 @@ class StreamingScorer:
                         for _ in range(self.depth)]
         self.ev_h2d = [torch.cuda.Event() for _ in range(self.depth)]
         self.ev_comp = [torch.cuda.Event() for _ in range(self.depth)]
-        self.ev_free = [torch.cuda.Event() for _ in range(self.depth)]
         self._used = [False] * self.depth
-        self._last_out = None  # event: previous submit's consumers of score_dev are done
+        self._slot = 0
         self.max_rows = max_rows or self.B
-        self.score_dev = torch.empty(self.max_rows, dtype=torch.float32, device=self.device)
-        self.valid_dev = torch.empty(self.max_rows, dtype=torch.uint8, device=self.device)
+        # step output buffers, used round-robin: step k+1 never waits for step k's consumers
+        self.n_out = int(out_buffers)
+        self._outs = [self._alloc_out(self.max_rows) for _ in range(self.n_out)]
+        self._out_free: List[Optional[object]] = [None] * self.n_out  # event: consumers of buffer done
+        self._out_i = 0
         self.batch_times_ms: List[float] = []
 
-    def ensure_capacity(self, n: int) -> None:
+    def _alloc_out(self, n: int):
         import torch
 
+        return (torch.empty(n, dtype=torch.float32, device=self.device),
+                torch.empty(n, dtype=torch.uint8, device=self.device))
+
+    @property
+    def score_dev(self):
+        return self._outs[(self._out_i - 1) % self.n_out][0]
+
+    @property
+    def valid_dev(self):
+        return self._outs[(self._out_i - 1) % self.n_out][1]
+
+    def ensure_capacity(self, n: int) -> None:
         if n > self.max_rows:
             self.max_rows = n
-            self.score_dev = torch.empty(n, dtype=torch.float32, device=self.device)
-            self.valid_dev = torch.empty(n, dtype=torch.uint8, device=self.device)
+            self._outs = [self._alloc_out(n) for _ in range(self.n_out)]
+            self._out_free = [None] * self.n_out
 
     def submit(self, X_host, score_host=None, valid_host=None, offset: int = 0) -> StepHandle:
         """Enqueue scoring of a pinned host matrix ``X_host`` ([n, F] float32 tensor). Scores land in
-        ``self.score_dev[offset: offset+n]`` and, if given, in the pinned host outputs."""
+        this step's device output buffer (``handle.score_dev``) and, if given, in the pinned host
+        outputs. Returns immediately."""
         import torch
 
         n = int(X_host.shape[0])
         self.ensure_capacity(offset + n)
-        if self._last_out is not None:
-            # WAR on the step output buffer: the previous step's copy-back must be done
-            self.comp.wait_event(self._last_out)
-        slot = 0
-        for i, s in enumerate(range(0, n, self.B)):
+        oi = self._out_i
+        self._out_i = (oi + 1) % self.n_out
+        score_dev, valid_dev = self._outs[oi]
+        if self._out_free[oi] is not None:
+            self.comp.wait_event(self._out_free[oi])  # WAR: the step that last used this buffer
+        for s in range(0, n, self.B):
             e = min(n, s + self.B)
             m = e - s
-            slot = i % self.depth
+            slot = self._slot
+            self._slot = (slot + 1) % self.depth
             with torch.cuda.stream(self.h2d):
                 if self._used[slot]:
                     self.h2d.wait_event(self.ev_comp[slot])  # kernel finished reading this slot
                 xs = self.x_slots[slot][:m]
                 xs.copy_(X_host[s:e], non_blocking=True)
                 self.ev_h2d[slot].record(self.h2d)
-            with torch.cuda.stream(self.comp):
-                self.comp.wait_event(self.ev_h2d[slot])
-                self.plan.launch(xs, self.score_dev[offset + s: offset + e], self.valid_dev[offset + s: offset + e],
-                                 stream=self.comp)
-                self.ev_comp[slot].record(self.comp)
+            self.comp.wait_event(self.ev_h2d[slot])
+            self.plan.launch(xs, score_dev[offset + s: offset + e], valid_dev[offset + s: offset + e],
+                             stream=self.comp)
+            self.ev_comp[slot].record(self.comp)
             self._used[slot] = True
             if score_host is not None:
                 with torch.cuda.stream(self.d2h):
                     self.d2h.wait_event(self.ev_comp[slot])
-                    score_host[s:e].copy_(self.score_dev[offset + s: offset + e], non_blocking=True)
+                    score_host[s:e].copy_(score_dev[offset + s: offset + e], non_blocking=True)
                     if valid_host is not None:
-                        valid_host[s:e].copy_(self.valid_dev[offset + s: offset + e], non_blocking=True)
+                        valid_host[s:e].copy_(valid_dev[offset + s: offset + e], non_blocking=True)
         done = torch.cuda.Event()
         if score_host is not None:
             done.record(self.d2h)
         else:
             done.record(self.comp)
-        self._last_out = done
-        return StepHandle(n, done)
+        self._out_free[oi] = done
+        h = StepHandle(n, done)
+        h.score_dev = score_dev[offset: offset + n]
+        h.valid_dev = valid_dev[offset: offset + n]
+        h.out_index = oi
+        return h
 
-    def mark_consumed(self, stream) -> None:
-        """Declare that ``stream`` reads the step outputs (e.g. an all-gather): the next submit
-        waits for it before overwriting them."""
+    def mark_consumed(self, handle: StepHandle, stream) -> None:
+        """Declare that ``stream`` also reads this step's device outputs (e.g. an all-gather): the
+        step that next reuses the buffer waits for it."""
         import torch
 
         ev = torch.cuda.Event()
         ev.record(stream)
-        self._last_out = ev
+        prev = self._out_free[handle.out_index]
+        if prev is not None:
+            stream.wait_event(prev)
+            ev = torch.cuda.Event()
+            ev.record(stream)
+        self._out_free[handle.out_index] = ev
 
     def join(self, stream=None) -> None:
         """Make ``stream`` (default: current) wait for all work submitted so far (no host sync)."""

@@ -736,6 +736,28 @@ class TreePlan(DevicePlan):
 
     def _post_state(self) -> None:
         self._partial = None
+        self._args = {}
+
+    def _args_template(self, with_probs: bool):
+        """Per-plan cached argument struct (only row pointers change per launch: keeps the host
+        cost of a launch in the few-µs range)."""
+        import ctypes
+
+        from ..ops._lib import TreeArgs, ptr
+
+        cache = self.__dict__.setdefault("_args", {})
+        a = cache.get(with_probs)
+        if a is None:
+            a = TreeArgs()
+            a.prep = ptr(self.prep)
+            a.blob, a.roots, a.leaves, a.tree_slot = ptr(self.blob), ptr(self.roots), ptr(self.leaves), ptr(self.slots)
+            a.n_trees, a.rec_words, a.chunk_trees, a.P = self.n_trees, self.rec_words, self.chunk_trees, self.P
+            a.C, a.general, a.variant = self.C, self.general, self.variant
+            a.epi = _epilogue(table=self.table, write_probs=with_probs, **self.epi_args)
+            cache[with_probs] = a
+        b = TreeArgs()
+        ctypes.pointer(b)[0] = a
+        return b
 
     def _auto_splits(self, n_rows: int) -> int:
         if self.splits:
@@ -755,15 +777,12 @@ class TreePlan(DevicePlan):
 
         n = X.shape[0]
         s = splits if splits is not None else self._auto_splits(n)
-        a = TreeArgs()
-        a.X = ptr(X)
+        a = self._args_template(probs is not None)
+        a.X = X.data_ptr()
         a.n_rows, a.n_feat, a.ldx = n, X.shape[1], X.stride(0)
-        a.prep, a.row_valid_in = ptr(self.prep), ptr(row_valid)
-        a.blob, a.roots, a.leaves, a.tree_slot = ptr(self.blob), ptr(self.roots), ptr(self.leaves), ptr(self.slots)
-        a.n_trees, a.rec_words, a.chunk_trees, a.P = self.n_trees, self.rec_words, self.chunk_trees, self.P
-        a.C, a.general, a.variant = self.C, self.general, self.variant
-        a.epi = _epilogue(table=self.table, write_probs=probs is not None, **self.epi_args)
-        a.score, a.valid, a.probs = ptr(score), ptr(valid), ptr(probs)
+        a.row_valid_in = ptr(row_valid)
+        a.score, a.valid, a.probs = score.data_ptr(), valid.data_ptr(), ptr(probs)
+        a.partial = None
         if s > 1:
             need = s * (self.C + 1) * n
             if self._partial is None or self._partial.numel() < need:

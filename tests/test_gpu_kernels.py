@@ -151,3 +151,39 @@ def test_interval_return_invalid_on_gpu(gpu, fixtures_dir):
     ref, vref = c.score_matrix_oracle(X)
     assert v.tolist() == vref.tolist() == [False, True, True, True]
     assert np.allclose(s[v], ref[v])
+
+
+def test_streaming_scorer_pipeline_matches_plan(gpu):
+    import torch
+
+    from flink_jpmml_amd.bench.synth import gbdt_pmml, stream_matrix
+    from flink_jpmml_amd.runtime.compiled import CompiledPmml
+    from flink_jpmml_amd.runtime.engine import StreamingScorer
+
+    c = CompiledPmml.from_string(gbdt_pmml(n_trees=100, depth=6, n_features=16, seed=9))
+    plan = c.plan(gpu)
+    X = stream_matrix(50_001, 16, seed=3, missing_rate=0.01)
+    ref_s, ref_v = plan.score(X)
+    scorer = StreamingScorer(plan, micro_batch=4096, depth=3, max_rows=50_001)
+    Xp = torch.from_numpy(X).pin_memory()
+    sh = torch.empty(len(X)).pin_memory()
+    vh = torch.empty(len(X), dtype=torch.uint8).pin_memory()
+    for _ in range(3):  # several steps reuse the ring + output buffers
+        h = scorer.submit(Xp, sh, vh)
+    scorer.wait(h)
+    assert torch.equal(sh, ref_s.cpu()) and torch.equal(vh.bool(), ref_v.cpu())
+    assert torch.equal(h.score_dev.cpu(), ref_s.cpu())
+
+
+def test_stream_dsl_on_gpu(gpu, fixtures_dir):
+    from flink_jpmml_amd import DenseVector, ModelReader, SparseVector
+    from flink_jpmml_amd.domain import EmptyScore, Prediction, Score
+    from flink_jpmml_amd.stream import StreamExecutionEnvironment
+
+    vecs = [DenseVector(1, 1, 1, 1), SparseVector(4, [0, 1, 2, 3], [1, 2, 3, 4]), SparseVector(4, [0, 2], [1, 2]),
+            DenseVector(1, 2, 3)] * 50
+    env = StreamExecutionEnvironment()
+    out = env.from_collection(vecs).quick_evaluate(ModelReader(fixtures_dir["kmeans"]), batch_size=64,
+                                                   device=gpu).collect()
+    exp = [Prediction(Score(3.0)), Prediction(Score(4.0)), Prediction(Score(3.0)), Prediction(EmptyScore)] * 50
+    assert [p for p, _ in out] == exp
