@@ -786,7 +786,10 @@ class TreePlan(DevicePlan):
         if s > 1:
             need = s * (self.C + 1) * n
             if self._partial is None or self._partial.numel() < need:
-                self._partial = torch.empty(need, dtype=torch.float32, device=self.device)
+                if self._partial is not None:
+                    # an in-flight kernel on another stream may still use it: never hand it back
+                    self.__dict__.setdefault("_retired", []).append(self._partial)
+                self._partial = torch.empty(max(need, 1 << 20), dtype=torch.float32, device=self.device)
             a.partial = ptr(self._partial)
         rc = self.lib.pmml_tree_launch(stream_handle(stream), ctypes.byref(a), 0 if self.layout == "perfect" else 1,
                                        self.depth, 1 if self.has_dr else 0, s)

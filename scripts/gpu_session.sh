@@ -47,6 +47,13 @@ for s in $STEPS; do
           > "$OUT/pmc.log" 2>&1 ); rc=$?
       echo "=== pmc rc=$rc" | tee -a "$OUT/session.log"
       if fatal $rc; then exit $rc; fi ;;
+    trace)
+      mkdir -p "$OUT/trace"
+      ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats \
+          -d "$OUT/trace" -o trace --output-format csv -- python3 "$ROOT/bench.py" --steps 4 --warmup 1 \
+          --latency-iters 3 --check-rows 0 > "$OUT/trace.log" 2>&1 ); rc=$?
+      echo "=== trace rc=$rc" | tee -a "$OUT/session.log"
+      if fatal $rc; then exit $rc; fi ;;
     *) echo "unknown step $s" ;;
   esac
 done
