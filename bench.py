@@ -43,7 +43,7 @@ def parse_args(argv=None):
     p.add_argument("--features", type=int, default=32)
     p.add_argument("--rows", type=int, default=1 << 20, help="rows per GPU per step")
     p.add_argument("--micro-batch", type=int, default=1 << 17)
-    p.add_argument("--depth", type=int, default=4, help="input ring slots (H2D/compute overlap)")
+    p.add_argument("--pipeline-depth", type=int, default=4, help="input ring slots (H2D/compute overlap)")
     p.add_argument("--objective", choices=["regression", "binary"], default="regression")
     p.add_argument("--latency-batch", type=int, default=4096)
     p.add_argument("--latency-iters", type=int, default=50)
@@ -102,7 +102,7 @@ def main(argv=None) -> int:
     X = torch.from_numpy(stream_matrix(args.rows, args.features, seed=1000 + ctx.rank)).pin_memory()
     score_h = torch.empty(args.rows, dtype=torch.float32).pin_memory()
     valid_h = torch.empty(args.rows, dtype=torch.uint8).pin_memory()
-    scorer = StreamingScorer(plan, micro_batch=args.micro_batch, depth=args.depth, max_rows=args.rows)
+    scorer = StreamingScorer(plan, micro_batch=args.micro_batch, depth=args.pipeline_depth, max_rows=args.rows)
     gather_out = None
     if N > 1 and not args.no_allgather:
         gather_out = (torch.empty(args.rows * N, dtype=torch.float32, device=device),
@@ -200,7 +200,7 @@ def main(argv=None) -> int:
                 "seq_len": None,
                 "parallelism": f"dp{N}",
                 "micro_batch": args.micro_batch,
-                "pipeline_depth": args.depth,
+                "pipeline_depth": args.pipeline_depth,
                 "rows_per_gpu_per_step": args.rows,
                 "allgather_sink": bool(gather_out is not None),
             },

@@ -171,8 +171,10 @@ def test_streaming_scorer_pipeline_matches_plan(gpu):
     for _ in range(3):  # several steps reuse the ring + output buffers
         h = scorer.submit(Xp, sh, vh)
     scorer.wait(h)
-    assert torch.equal(sh, ref_s.cpu()) and torch.equal(vh.bool(), ref_v.cpu())
-    assert torch.equal(h.score_dev.cpu(), ref_s.cpu())
+    # micro-batches of 4096 rows use the tree-split kernel (different fp32 summation order)
+    assert torch.equal(vh.bool(), ref_v.cpu())
+    assert torch.allclose(sh, ref_s.cpu(), atol=1e-5, rtol=0)
+    assert torch.equal(h.score_dev.cpu(), sh)
 
 
 def test_stream_dsl_on_gpu(gpu, fixtures_dir):
