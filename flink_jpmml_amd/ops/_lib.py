@@ -102,7 +102,8 @@ class FieldPrep(ctypes.Structure):
 
 class Epilogue(ctypes.Structure):
     _fields_ = [("mode", c_int), ("n_classes", c_int), ("a", c_float), ("b", c_float), ("thr", c_float),
-                ("has_table", c_int), ("table", c_void_p), ("write_probs", c_int), ("link", c_int)]
+                ("has_table", c_int), ("table", c_void_p), ("write_probs", c_int), ("link", c_int),
+                ("score2", c_void_p), ("valid2", c_void_p)]
 
 
 class TreeArgs(ctypes.Structure):
@@ -192,6 +193,10 @@ def load(auto_build: bool = True) -> ctypes.CDLL:
             if f is not None:
                 f.restype = c_int
         lib.pmml_tree_launch.argtypes = [c_void_p, ctypes.POINTER(TreeArgs), c_int, c_int, c_int, c_int]
+        lib.pmml_host_device_ptr.argtypes = [c_void_p, ctypes.POINTER(c_void_p)]
+        lib.pmml_host_device_ptr.restype = c_int
+        lib.pmml_memcpy_async.argtypes = [c_void_p, c_void_p, ctypes.c_size_t, c_int, c_void_p]
+        lib.pmml_memcpy_async.restype = c_int
         lib.pmml_cluster_launch.argtypes = [c_void_p, ctypes.POINTER(ClusterArgs)]
         lib.pmml_linear_launch.argtypes = [c_void_p, ctypes.POINTER(LinearArgs)]
         if hasattr(lib, "pmml_mlp_launch"):
@@ -219,3 +224,15 @@ def stream_handle(stream=None) -> int:
 
     s = stream if stream is not None else torch.cuda.current_stream()
     return s.cuda_stream
+
+
+def host_device_ptr(t) -> Optional[int]:
+    """Device-visible address of a pinned host tensor (zero-copy), or None if not mapped."""
+    if t is None or not t.is_pinned():
+        return None
+    lib = load()
+    dev = c_void_p()
+    rc = lib.pmml_host_device_ptr(c_void_p(t.data_ptr()), ctypes.byref(dev))
+    if rc != 0 or not dev.value:
+        return None
+    return int(dev.value)

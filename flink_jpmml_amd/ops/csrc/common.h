@@ -83,6 +83,8 @@ struct Epilogue {
   const float* table;   // [C]
   int write_probs;      // also write probs[row, C]
   int link;             // LINK_* applied after the affine map (EPI_AFFINE, EPI_LOGISTIC2)
+  float* score2;        // optional mirror outputs (e.g. device copy beside a zero-copy host sink)
+  uint8_t* valid2;
 };
 
 enum : int { LINK_NONE = 0, LINK_LOGIT = 1, LINK_EXP = 2, LINK_PROBIT = 3, LINK_CLOGLOG = 4, LINK_LOGLOG = 5,

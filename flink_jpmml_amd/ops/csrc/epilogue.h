@@ -45,6 +45,11 @@ __device__ __forceinline__ void apply_epilogue(const Epilogue& e, Acc acc, bool 
     s = e.has_table ? e.table[label] : (float)label;
     ok = ok && (s == s);
   }
-  score[row] = ok ? s : __builtin_nanf("");
+  const float so = ok ? s : __builtin_nanf("");
+  score[row] = so;
   valid[row] = ok ? 1 : 0;
+  if (e.score2) {
+    e.score2[row] = so;
+    e.valid2[row] = ok ? 1 : 0;
+  }
 }

@@ -33,7 +33,7 @@ class StepHandle:
 
 class StreamingScorer:
     def __init__(self, plan, micro_batch: int = 131072, depth: int = 3, max_rows: Optional[int] = None,
-                 out_buffers: int = 2):
+                 out_buffers: int = 2, direct_host_output: bool = True, keep_device_output: bool = True):
         import torch
 
         self.plan = plan
@@ -57,6 +57,19 @@ class StreamingScorer:
         self._out_free: List[Optional[object]] = [None] * self.n_out  # event: consumers of buffer done
         self._out_i = 0
         self.batch_times_ms: List[float] = []
+        # zero-copy sink: the kernel epilogue writes scores straight into pinned host memory over
+        # PCIe (no D2H copy commands: small D2H copies were measured to stall the H2D stream)
+        self.direct = bool(direct_host_output) and getattr(plan, "supports_direct", False)
+        self.keep_device = keep_device_output
+        self._dev_ptr_cache = {}
+
+    def _host_dev_ptr(self, t):
+        from ..ops._lib import host_device_ptr
+
+        key = (t.data_ptr(), t.numel())
+        if key not in self._dev_ptr_cache:
+            self._dev_ptr_cache[key] = host_device_ptr(t)
+        return self._dev_ptr_cache[key]
 
     def _alloc_out(self, n: int):
         import torch
@@ -91,6 +104,11 @@ class StreamingScorer:
         score_dev, valid_dev = self._outs[oi]
         if self._out_free[oi] is not None:
             self.comp.wait_event(self._out_free[oi])  # WAR: the step that last used this buffer
+        hs = hv = None
+        if self.direct and score_host is not None and valid_host is not None:
+            hs, hv = self._host_dev_ptr(score_host), self._host_dev_ptr(valid_host)
+            if hs is None or hv is None:
+                hs = hv = None
         for s in range(0, n, self.B):
             e = min(n, s + self.B)
             m = e - s
@@ -103,18 +121,24 @@ class StreamingScorer:
                 xs.copy_(X_host[s:e], non_blocking=True)
                 self.ev_h2d[slot].record(self.h2d)
             self.comp.wait_event(self.ev_h2d[slot])
-            self.plan.launch(xs, score_dev[offset + s: offset + e], valid_dev[offset + s: offset + e],
-                             stream=self.comp)
+            if hs is not None:
+                kw = {}
+                if self.keep_device:
+                    kw = dict(score2=score_dev[offset + s: offset + e], valid2=valid_dev[offset + s: offset + e])
+                self.plan.launch(xs, hs + 4 * s, hv + s, stream=self.comp, **kw)
+            else:
+                self.plan.launch(xs, score_dev[offset + s: offset + e], valid_dev[offset + s: offset + e],
+                                 stream=self.comp)
             self.ev_comp[slot].record(self.comp)
             self._used[slot] = True
-            if score_host is not None:
+            if score_host is not None and hs is None:
                 with torch.cuda.stream(self.d2h):
                     self.d2h.wait_event(self.ev_comp[slot])
                     score_host[s:e].copy_(score_dev[offset + s: offset + e], non_blocking=True)
                     if valid_host is not None:
                         valid_host[s:e].copy_(valid_dev[offset + s: offset + e], non_blocking=True)
         done = torch.cuda.Event()
-        if score_host is not None:
+        if score_host is not None and hs is None:
             done.record(self.d2h)
         else:
             done.record(self.comp)

@@ -186,6 +186,7 @@ def build_field_prep(compiled, fields: List[str]) -> Tuple[np.ndarray, bool]:
 
 class DevicePlan:
     kind = "base"
+    supports_direct = False  # kernel can write zero-copy host outputs + device mirror
 
     def __init__(self, compiled, device):
         import torch
@@ -293,6 +294,15 @@ def _epilogue(mode: int, C: int = 1, a: float = 1.0, b: float = 0.0, thr: float 
     e.write_probs = 1 if write_probs else 0
     e.link = link
     return e
+
+
+def _addr(t) -> Optional[int]:
+    """Tensor or raw integer address -> address (None stays NULL)."""
+    if t is None:
+        return None
+    if isinstance(t, int):
+        return t
+    return t.data_ptr()
 
 
 def _label_table(labels: List[str]) -> np.ndarray:
@@ -411,7 +421,9 @@ class LinearPlan(DevicePlan):
                 self.epi_args.update(a=self.post[0], b=self.post[1])
                 self.W = self.W  # rescale folded into the affine epilogue
 
-    def launch(self, X, score, valid, stream=None, probs=None) -> None:
+    supports_direct = True
+
+    def launch(self, X, score, valid, stream=None, probs=None, score2=None, valid2=None) -> None:
         import ctypes
 
         from ..ops._lib import LinearArgs, check, ptr, stream_handle
@@ -421,7 +433,8 @@ class LinearPlan(DevicePlan):
         a.n_rows, a.n_feat, a.ldx, a.K = X.shape[0], X.shape[1], X.stride(0), self.K
         a.prep, a.W, a.bias, a.simplemax = ptr(self.prep), ptr(self.W), ptr(self.b), self.simplemax
         a.epi = _epilogue(table=self.table, write_probs=probs is not None, **self.epi_args)
-        a.score, a.valid, a.probs = ptr(score), ptr(valid), ptr(probs)
+        a.epi.score2, a.epi.valid2 = _addr(score2), _addr(valid2)
+        a.score, a.valid, a.probs = _addr(score), _addr(valid), ptr(probs)
         check(self.lib.pmml_linear_launch(stream_handle(stream), ctypes.byref(a)), "linear kernel")
 
 
@@ -768,7 +781,10 @@ class TreePlan(DevicePlan):
             return 1
         return int(max(1, min(self.n_trees // 16, target // max(1, blocks), 64)))
 
-    def launch(self, X, score, valid, stream=None, probs=None, row_valid=None, splits: Optional[int] = None) -> None:
+    supports_direct = True  # epilogue can write straight into zero-copy host memory (+ mirror)
+
+    def launch(self, X, score, valid, stream=None, probs=None, row_valid=None, splits: Optional[int] = None,
+               score2=None, valid2=None) -> None:
         import ctypes
 
         import torch
@@ -781,7 +797,8 @@ class TreePlan(DevicePlan):
         a.X = X.data_ptr()
         a.n_rows, a.n_feat, a.ldx = n, X.shape[1], X.stride(0)
         a.row_valid_in = ptr(row_valid)
-        a.score, a.valid, a.probs = score.data_ptr(), valid.data_ptr(), ptr(probs)
+        a.score, a.valid, a.probs = _addr(score), _addr(valid), ptr(probs)
+        a.epi.score2, a.epi.valid2 = _addr(score2), _addr(valid2)
         a.partial = None
         if s > 1:
             need = s * (self.C + 1) * n

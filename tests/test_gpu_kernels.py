@@ -164,17 +164,19 @@ def test_streaming_scorer_pipeline_matches_plan(gpu):
     plan = c.plan(gpu)
     X = stream_matrix(50_001, 16, seed=3, missing_rate=0.01)
     ref_s, ref_v = plan.score(X)
-    scorer = StreamingScorer(plan, micro_batch=4096, depth=3, max_rows=50_001)
-    Xp = torch.from_numpy(X).pin_memory()
-    sh = torch.empty(len(X)).pin_memory()
-    vh = torch.empty(len(X), dtype=torch.uint8).pin_memory()
-    for _ in range(3):  # several steps reuse the ring + output buffers
-        h = scorer.submit(Xp, sh, vh)
-    scorer.wait(h)
-    # micro-batches of 4096 rows use the tree-split kernel (different fp32 summation order)
-    assert torch.equal(vh.bool(), ref_v.cpu())
-    assert torch.allclose(sh, ref_s.cpu(), atol=1e-5, rtol=0)
-    assert torch.equal(h.score_dev.cpu(), sh)
+    for direct in (True, False):
+        scorer = StreamingScorer(plan, micro_batch=4096, depth=3, max_rows=50_001, direct_host_output=direct)
+        assert scorer.direct == direct
+        Xp = torch.from_numpy(X).pin_memory()
+        sh = torch.full((len(X),), -7.0).pin_memory()
+        vh = torch.zeros(len(X), dtype=torch.uint8).pin_memory()
+        for _ in range(3):  # several steps reuse the ring + output buffers
+            h = scorer.submit(Xp, sh, vh)
+        scorer.wait(h)
+        # micro-batches of 4096 rows use the tree-split kernel (different fp32 summation order)
+        assert torch.equal(vh.bool(), ref_v.cpu())
+        assert torch.allclose(sh, ref_s.cpu(), atol=1e-5, rtol=0)
+        assert torch.equal(h.score_dev.cpu(), sh)  # device mirror == zero-copy host sink
 
 
 def test_stream_dsl_on_gpu(gpu, fixtures_dir):
