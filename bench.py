@@ -42,7 +42,7 @@ def parse_args(argv=None):
     p.add_argument("--depth", type=int, default=6)
     p.add_argument("--features", type=int, default=32)
     p.add_argument("--rows", type=int, default=1 << 20, help="rows per GPU per step")
-    p.add_argument("--micro-batch", type=int, default=1 << 17)
+    p.add_argument("--micro-batch", type=int, default=1 << 18)
     p.add_argument("--pipeline-depth", type=int, default=4, help="input ring slots (H2D/compute overlap)")
     p.add_argument("--objective", choices=["regression", "binary"], default="regression")
     p.add_argument("--latency-batch", type=int, default=4096)
@@ -98,7 +98,10 @@ def main(argv=None) -> int:
         check = {"oracle_rows": int(args.check_rows), "valid_match": bool((v_ref == v_gpu).all()),
                  "max_abs_err_vs_fp64": err}
 
-    # ---- this rank's synthetic record shard in pinned host memory
+    # ---- this rank's synthetic record shard in pinned host memory, on the GPU's NUMA node
+    from flink_jpmml_amd.utils.numa import bind_to_gpu_numa
+
+    numa_node = bind_to_gpu_numa(device.index or 0)
     X = torch.from_numpy(stream_matrix(args.rows, args.features, seed=1000 + ctx.rank)).pin_memory()
     score_h = torch.empty(args.rows, dtype=torch.float32).pin_memory()
     valid_h = torch.empty(args.rows, dtype=torch.uint8).pin_memory()
@@ -203,6 +206,8 @@ def main(argv=None) -> int:
                 "pipeline_depth": args.pipeline_depth,
                 "rows_per_gpu_per_step": args.rows,
                 "allgather_sink": bool(gather_out is not None),
+                "zero_copy_host_sink": bool(scorer.direct),
+                "numa_node": numa_node,
             },
             "p50_latency_ms": p50,
             "p99_latency_ms": p99,
