@@ -274,8 +274,8 @@ def svm_pmml(n_features: int = 16, n_sv: int = 256, seed: int = 0, kernel: str =
     rng = np.random.default_rng(seed)
     out = io.StringIO()
     _header(out, f"synthetic SVM {kernel} {n_sv} support vectors")
-    cats = ["neg", "pos"] if classification else None
-    _data_dictionary(out, n_features, "y", "string" if classification else "double", cats)
+    cats = ["0", "1"] if classification else None
+    _data_dictionary(out, n_features, "y", "integer" if classification else "double", cats)
     fn = "classification" if classification else "regression"
     out.write(f' <SupportVectorMachineModel functionName="{fn}" svmRepresentation="SupportVectors">\n')
     _mining_schema(out, n_features, "y", "  ")
@@ -290,7 +290,7 @@ def svm_pmml(n_features: int = 16, n_sv: int = 256, seed: int = 0, kernel: str =
         out.write(f'   <VectorInstance id="sv{i}"><Array n="{n_features}" type="real">'
                   + " ".join(f"{v:.6g}" for v in S[i]) + '</Array></VectorInstance>\n')
     out.write('  </VectorDictionary>\n')
-    tc = ' targetCategory="neg" alternateTargetCategory="pos"' if classification else ""
+    tc = ' targetCategory="0" alternateTargetCategory="1"' if classification else ""
     out.write(f'  <SupportVectorMachine{tc}>\n   <SupportVectors numberOfSupportVectors="{n_sv}">')
     out.write("".join(f'<SupportVector vectorId="sv{i}"/>' for i in range(n_sv)))
     out.write('</SupportVectors>\n')

@@ -131,18 +131,20 @@ class LinearArgs(ctypes.Structure):
 
 class MlpArgs(ctypes.Structure):
     _fields_ = [("X", c_void_p), ("n_rows", c_int), ("n_feat", c_int), ("ldx", c_int), ("n_layers", c_int),
-                ("prep", c_void_p), ("in_scale", c_void_p), ("in_shift", c_void_p), ("weights", c_void_p),
-                ("biases", c_void_p), ("dims", c_void_p), ("acts", c_void_p), ("out_scale", c_float),
-                ("out_shift", c_float), ("final_norm", c_int), ("pad", c_int), ("epi", Epilogue),
-                ("score", c_void_p), ("valid", c_void_p), ("probs", c_void_p)]
+                ("in_scale", c_void_p), ("in_shift", c_void_p), ("in_missing", c_void_p), ("in_index", c_void_p),
+                ("n_in", c_int), ("k0", c_int), ("weights", c_void_p), ("biases", c_void_p), ("layers", c_void_p),
+                ("out_scale", c_float), ("out_shift", c_float), ("final_norm", c_int), ("n_out", c_int),
+                ("epi", Epilogue), ("score", c_void_p), ("valid", c_void_p), ("probs", c_void_p)]
 
 
 class SvmArgs(ctypes.Structure):
     _fields_ = [("X", c_void_p), ("n_rows", c_int), ("n_feat", c_int), ("ldx", c_int), ("n_sv", c_int),
-                ("prep", c_void_p), ("sv", c_void_p), ("sv_norm", c_void_p), ("coef", c_void_p),
-                ("intercept", c_void_p), ("n_machines", c_int), ("kernel", c_int), ("gamma", c_float),
-                ("coef0", c_float), ("degree", c_float), ("pad", c_int), ("decision", c_void_p),
-                ("valid", c_void_p)]
+                ("prep", c_void_p), ("in_index", c_void_p), ("sv", c_void_p), ("sv_norm", c_void_p),
+                ("coef", c_void_p), ("intercept", c_void_p), ("thr", c_void_p), ("tgt", c_void_p), ("alt", c_void_p),
+                ("n_in", c_int), ("n_machines", c_int), ("kernel", c_int), ("classification", c_int),
+                ("gamma", c_float), ("coef0", c_float), ("degree", c_float), ("max_wins", c_int),
+                ("n_classes", c_int), ("pad", c_int), ("epi", Epilogue), ("score", c_void_p), ("valid", c_void_p),
+                ("decision", c_void_p)]
 
 
 _ABI = {
@@ -202,7 +204,7 @@ def load(auto_build: bool = True) -> ctypes.CDLL:
         if hasattr(lib, "pmml_mlp_launch"):
             lib.pmml_mlp_launch.argtypes = [c_void_p, ctypes.POINTER(MlpArgs), c_int]
         if hasattr(lib, "pmml_svm_launch"):
-            lib.pmml_svm_launch.argtypes = [c_void_p, ctypes.POINTER(SvmArgs)]
+            lib.pmml_svm_launch.argtypes = [c_void_p, ctypes.POINTER(SvmArgs), c_int]
         _lib = lib
         return lib
 

@@ -191,3 +191,65 @@ def test_stream_dsl_on_gpu(gpu, fixtures_dir):
                                                    device=gpu).collect()
     exp = [Prediction(Score(3.0)), Prediction(Score(4.0)), Prediction(Score(3.0)), Prediction(EmptyScore)] * 50
     assert [p for p, _ in out] == exp
+
+
+@pytest.mark.parametrize("precision,tol", [("fp32", 1e-4), ("bf16", 5e-2)])
+def test_mlp_regression_mfma(gpu, precision, tol):
+    """3-layer NeuralNetwork on the fused MFMA kernel: fp32 MFMA (exact FMA chain) matches the
+    fp64 oracle to ~1e-5 relative; bf16 MFMA (bf16 operands, fp32 accumulate) to a few 1e-3."""
+    from flink_jpmml_amd.bench.synth import mlp_pmml, stream_matrix
+    from flink_jpmml_amd.runtime.compiled import CompiledPmml
+    from flink_jpmml_amd.runtime.nn_plans import MlpPlan
+
+    c = CompiledPmml.from_string(mlp_pmml(n_features=40, hidden=(96, 70), n_out=1, seed=4))
+    plan = c.plan(gpu, precision=precision)
+    assert isinstance(plan, MlpPlan)
+    X = stream_matrix(10_000, 40, seed=2)
+    X[5, 3] = np.nan  # a missing input invalidates the row (PMML NN rule)
+    s, v = _gpu_np(plan, X)
+    ref, vref = c.score_matrix_oracle(X)
+    assert (v == vref).all() and not v[5]
+    scale = np.max(np.abs(ref[vref]))
+    assert np.max(np.abs(s[v] - ref[v])) < tol * max(1.0, scale)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_mlp_classification_softmax(gpu, precision):
+    from flink_jpmml_amd.bench.synth import mlp_pmml, stream_matrix
+    from flink_jpmml_amd.runtime.compiled import CompiledPmml
+
+    c = CompiledPmml.from_string(mlp_pmml(n_features=16, hidden=(64,), n_out=5, seed=1, activation="tanh",
+                                          classification=True))
+    X = stream_matrix(20_000, 16, seed=6)
+    s, v = _gpu_np(c.plan(gpu, precision=precision), X)
+    ref, vref = c.score_matrix_oracle(X)
+    assert (v == vref).all()
+    agree = (s == ref).mean()
+    assert agree > (0.9999 if precision == "fp32" else 0.98)
+
+
+@pytest.mark.parametrize("kernel", ["radialBasis", "linear", "polynomial", "sigmoid"])
+def test_svm_kernels(gpu, kernel):
+    from flink_jpmml_amd.bench.synth import stream_matrix, svm_pmml
+    from flink_jpmml_amd.runtime.compiled import CompiledPmml
+    from flink_jpmml_amd.runtime.nn_plans import SvmPlan
+
+    c = CompiledPmml.from_string(svm_pmml(n_features=12, n_sv=100, seed=3, kernel=kernel))
+    plan = c.plan(gpu)
+    assert isinstance(plan, SvmPlan)
+    X = stream_matrix(20_000, 12, seed=4)
+    s, v = _gpu_np(plan, X)
+    ref, vref = c.score_matrix_oracle(X)
+    assert (v == vref).all()
+    assert not v.any() or (s[v] == ref[v]).mean() > 0.999
+
+
+def test_svm_regression(gpu):
+    from flink_jpmml_amd.bench.synth import stream_matrix, svm_pmml
+    from flink_jpmml_amd.runtime.compiled import CompiledPmml
+
+    c = CompiledPmml.from_string(svm_pmml(n_features=10, n_sv=64, seed=5, classification=False))
+    X = stream_matrix(5000, 10, seed=1)
+    s, v = _gpu_np(c.plan(gpu), X)
+    ref, vref = c.score_matrix_oracle(X)
+    assert (v == vref).all() and np.max(np.abs(s - ref)) < 1e-4

@@ -107,3 +107,71 @@ def test_canonical_threshold_exact_for_fp32_inputs(op):
             first = {OP_LT: xd < t, OP_LE: xd <= t, OP_GT: xd > t, OP_GE: xd >= t}[op]
             right = bool(np.float32(x) >= np.float32(T))
             assert first == (right if swap else not right), (op, t, x, T)
+
+
+# ---------------------------------------------------------------------------- MLP fragment packing
+def _acc_row(r, h):
+    return (r & 3) + 8 * (r >> 2) + 4 * h
+
+
+def emulate_mlp_wave(layers, X32, precision):
+    """Emulate csrc/mlp.hip for one wave (32 rows) at the MFMA fragment level: A fragments from
+    pack_mlp_weights, B fragments from staged inputs (layer 0) or from the previous layer's
+    accumulator registers (layers >= 1), C/D register layout of the 32x32 tile."""
+    from flink_jpmml_amd.models.neural import activate
+    from flink_jpmml_amd.runtime.nn_plans import pack_mlp_weights
+
+    w, bias, meta = pack_mlp_weights([(W, b) for W, b, _ in layers], precision)
+    bf16 = precision == "bf16"
+    kstep = 16 if bf16 else 2
+    lane = np.arange(64)
+    hh, col = lane >> 5, lane & 31
+    regs_prev = None  # [tiles][64 lanes][16 regs]
+    for L, ((kp, mp, mreal, wo, bo), (_, _, act)) in enumerate(zip(meta, layers)):
+        mtiles, ksteps = mp // 32, kp // kstep
+        nfr = 8 if bf16 else 1
+        frags = w[wo: wo + mtiles * ksteps * 64 * nfr].reshape(mtiles, ksteps, 64, nfr)
+        D = np.zeros((mtiles, 32, 32))
+        for t in range(mtiles):
+            D[t] = bias[bo + 32 * t: bo + 32 * t + 32][:, None]
+        for s in range(ksteps):
+            Bl = np.zeros((kstep, 32))
+            for l in range(64):
+                for j in range(nfr):
+                    k = (8 * hh[l] + j) if bf16 else hh[l]
+                    if L == 0:
+                        feat = (16 * s + 8 * hh[l] + j) if bf16 else (2 * s + hh[l])
+                        Bl[k, col[l]] = X32[col[l], feat] if feat < X32.shape[1] else 0.0
+                    elif bf16:
+                        tp, sp = s // 2, s % 2
+                        Bl[k, col[l]] = regs_prev[tp][l][8 * sp + j]
+                    else:
+                        tp, r = s // 16, s % 16
+                        Bl[k, col[l]] = regs_prev[tp][l][r]
+            for t in range(mtiles):
+                Al = np.zeros((32, kstep))
+                for l in range(64):
+                    for j in range(nfr):
+                        k = (8 * hh[l] + j) if bf16 else hh[l]
+                        Al[col[l], k] = frags[t, s, l, j]
+                D[t] += Al @ Bl
+        D = activate(act, D)
+        regs_prev = [[[D[t][_acc_row(r, hh[l]), col[l]] for r in range(16)] for l in range(64)]
+                     for t in range(mtiles)]
+    return D[0]  # [units (tile 0), 32 rows]
+
+
+@pytest.mark.parametrize("precision", ["bf16", "fp32"])
+def test_mlp_fragment_packing_matches_dense_forward(precision):
+    rng = np.random.default_rng(0)
+    dims = [(20, 40), (40, 33), (33, 3)]  # odd sizes exercise K and M padding
+    layers = [(rng.standard_normal(d), rng.standard_normal(d[1]), a)
+              for d, a in zip(dims, ["rectifier", "tanh", "identity"])]
+    X = rng.standard_normal((32, 20))
+    from flink_jpmml_amd.models.neural import activate
+
+    H = X
+    for W, b, act in layers:
+        H = activate(act, H @ W + b)
+    out = emulate_mlp_wave(layers, X, precision)
+    assert np.allclose(out[:3].T, H, atol=1e-9)
