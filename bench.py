@@ -50,6 +50,7 @@ def parse_args(argv=None):
     p.add_argument("--no-allgather", action="store_true")
     p.add_argument("--check-rows", type=int, default=8192, help="rows checked against the fp64 oracle (untimed)")
     p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--no-numa", action="store_true", help="do not bind to the GPU's NUMA node")
     return p.parse_args(argv)
 
 
@@ -101,7 +102,7 @@ def main(argv=None) -> int:
     # ---- this rank's synthetic record shard in pinned host memory, on the GPU's NUMA node
     from flink_jpmml_amd.utils.numa import bind_to_gpu_numa
 
-    numa_node = bind_to_gpu_numa(device.index or 0)
+    numa_node = None if args.no_numa else bind_to_gpu_numa(device.index or 0)
     X = torch.from_numpy(stream_matrix(args.rows, args.features, seed=1000 + ctx.rank)).pin_memory()
     score_h = torch.empty(args.rows, dtype=torch.float32).pin_memory()
     valid_h = torch.empty(args.rows, dtype=torch.uint8).pin_memory()

@@ -1,0 +1,44 @@
+"""Example jobs run end to end on CPU (reference `E/*.scala`)."""
+
+from flink_jpmml_amd.domain import Prediction
+from flink_jpmml_amd.examples import jobs
+from flink_jpmml_amd.examples.sources import ControlSource, IrisSource, ids_and_paths
+
+
+def test_quick_and_evaluate(fixtures_dir, tmp_path):
+    out = jobs.main(["quick", "--model", fixtures_dir["kmeans"], "--output", str(tmp_path / "q.txt"), "--records", "20"])
+    assert out == 0
+    lines = (tmp_path / "q.txt").read_text().splitlines()
+    assert len(lines) == 20 and all(line.startswith("(Prediction(Score(") for line in lines)
+    jobs.main(["evaluate", "--model", fixtures_dir["kmeans"], "--output", str(tmp_path / "e.txt"), "--records", "10",
+               "--batch-size", "4"])
+    assert len((tmp_path / "e.txt").read_text().splitlines()) == 10
+
+
+def test_dynamic_finite(fixtures_dir, tmp_path):
+    args = jobs.build_parser().parse_args(["dynamic", "--models", f"{fixtures_dir['kmeans']},{fixtures_dir['kmeans41']}",
+                                           "--output", str(tmp_path / "d.txt"), "--gen-policy", "finite",
+                                           "--records", "30", "--intervalCheckpoint", "7",
+                                           "--checkpoint-dir", str(tmp_path / "ck")])
+    out = jobs.dynamic_evaluate_kmeans(args)
+    assert len(out) == 30
+    assert all(isinstance(p, Prediction) for _, p in out)
+    assert (tmp_path / "ck").exists() and any((tmp_path / "ck").iterdir())
+
+
+def test_checkpoint_example_with_control_file(fixtures_dir, tmp_path):
+    cf = tmp_path / "paths.txt"
+    cf.write_text(fixtures_dir["kmeans"] + "\n")
+    jobs.main(["checkpoint", "--control-file", str(cf), "--output", str(tmp_path / "c.txt"), "--records", "12"])
+    assert len((tmp_path / "c.txt").read_text().splitlines()) == 12
+
+
+def test_sources_policies():
+    idp = ids_and_paths(["a.xml", "b.xml"])
+    assert len(list(ControlSource(idp, "finite").iterate())) == 2
+    assert len(list(ControlSource(idp, "loop", n=5).iterate())) == 5
+    assert len(list(ControlSource(idp, "random", n=4).iterate())) == 4
+    evs = list(IrisSource(list(idp), n=6).iterate())
+    assert len(evs) == 6 and all(e.model_id.endswith("_1") for e in evs)
+    assert all(0.2 <= v <= 6.0 for e in evs for v in e.to_vector().data)
+    assert list(IrisSource(None, n=2).iterate())[0].model_id is None  # no crash without ids (reference bug)
