@@ -42,8 +42,8 @@ def parse_args(argv=None):
     p.add_argument("--depth", type=int, default=6)
     p.add_argument("--features", type=int, default=32)
     p.add_argument("--rows", type=int, default=1 << 20, help="rows per GPU per step")
-    p.add_argument("--micro-batch", type=int, default=1 << 18)
-    p.add_argument("--pipeline-depth", type=int, default=4, help="input ring slots (H2D/compute overlap)")
+    p.add_argument("--micro-batch", type=int, default=1 << 19)
+    p.add_argument("--pipeline-depth", type=int, default=3, help="input ring slots (H2D/compute overlap)")
     p.add_argument("--objective", choices=["regression", "binary"], default="regression")
     p.add_argument("--latency-batch", type=int, default=4096)
     p.add_argument("--latency-iters", type=int, default=50)
