@@ -1,0 +1,144 @@
+"""Multi-process data-parallel paths on the gloo backend (CPU, world size 2 and 4).
+
+The RCCL path is the same code with backend ``nccl``; it runs on GPU boxes (the 8-GPU scaling run
+is the driver's). These tests cover the collectives' semantics: control-plane replication,
+tensor/plan payload broadcast, varlen all-gather, sharding and the distributed serving protocol.
+"""
+
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _run(world, fn, *args):
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_entry, args=(r, world, port, fn, args, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = {}
+    for _ in range(world):
+        r, res = q.get(timeout=120)
+        results[r] = res
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r, res in results.items():
+        if isinstance(res, BaseException):
+            raise res
+    return results
+
+
+def _entry(rank, world, port, fn, args, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    try:
+        from flink_jpmml_amd.parallel import init_from_env, shutdown
+
+        ctx = init_from_env(backend="gloo")
+        res = fn(ctx, *args)
+        shutdown(ctx)
+        q.put((rank, res))
+    except BaseException as e:  # noqa: BLE001
+        q.put((rank, e))
+
+
+# ---------------------------------------------------------------------------------- workers
+def w_control(ctx):
+    from flink_jpmml_amd.domain import AddMessage, DelMessage
+    from flink_jpmml_amd.parallel import broadcast_control
+
+    msgs = [AddMessage("f5c4e8b3-4a1e-4b3c-9b5e-123456789abc", 1, "/m.xml", 5),
+            DelMessage("f5c4e8b3-4a1e-4b3c-9b5e-123456789abc", 1, 6)] if ctx.rank == 0 else None
+    got = broadcast_control(msgs, ctx)
+    empty = broadcast_control([] if ctx.rank == 0 else None, ctx)
+    return [repr(m) for m in got], len(empty)
+
+
+def w_tensors(ctx):
+    import torch
+
+    from flink_jpmml_amd.parallel import broadcast_tensors
+
+    spec = {"a": ((3, 4), "float32"), "b": ((5,), "int32"), "c": ((2, 2), "uint8")}
+    src = None
+    if ctx.rank == 0:
+        src = {"a": torch.arange(12, dtype=torch.float32).view(3, 4), "b": torch.arange(5, dtype=torch.int32) * 7,
+               "c": torch.tensor([[1, 2], [3, 255]], dtype=torch.uint8)}
+    out = broadcast_tensors(src, spec, ctx)
+    return {k: v.tolist() for k, v in out.items()}
+
+
+def w_gather(ctx):
+    import torch
+
+    from flink_jpmml_amd.parallel import all_gather_scores, all_gather_varlen, shard_range
+
+    lo, hi = shard_range(10, ctx.rank, ctx.world_size)
+    s, v, _ = all_gather_scores(torch.full((3,), float(ctx.rank)), torch.ones(3, dtype=torch.uint8), ctx)
+    var = all_gather_varlen(torch.arange(lo, hi, dtype=torch.float32), ctx)
+    return s.tolist(), var.tolist(), (lo, hi)
+
+
+def w_serving(ctx, kmeans_path, notarget_path):
+    from flink_jpmml_amd.domain import AddMessage, DelMessage
+    from flink_jpmml_amd.parallel import shard_range
+    from flink_jpmml_amd.parallel.serving import DistributedServing
+
+    n1 = "a1b2c3d4-0000-4000-8000-000000000001"
+    n2 = "a1b2c3d4-0000-4000-8000-000000000002"
+    srv = DistributedServing(ctx)
+    srv.apply_control([AddMessage(n1, 1, kmeans_path), AddMessage(n2, 1, notarget_path),
+                       AddMessage(n1, 1, notarget_path)] if ctx.rank == 0 else None)
+    X = np.tile(np.array([[1.0, 1.0, 1.0, 1.0], [1.0, 2.0, 3.0, 4.0]]), (5, 1))
+    lo, hi = shard_range(len(X), ctx.rank, ctx.world_size)
+    s1, v1 = srv.gather(*srv.score(f"{n1}_1", X[lo:hi]))
+    s2, v2 = srv.gather(*srv.score(f"{n2}_1", X[lo:hi]))
+    srv.apply_control([DelMessage(n1, 1)] if ctx.rank == 0 else None)
+    s3, v3 = srv.gather(*srv.score(f"{n1}_1", X[lo:hi]))
+    return s1.tolist(), v1.tolist(), v2.tolist(), v3.tolist(), sorted(str(k) for k in srv.metadata)
+
+
+# ---------------------------------------------------------------------------------- tests
+@pytest.mark.parametrize("world", [2, 4])
+def test_control_plane_broadcast(world):
+    res = _run(world, w_control)
+    assert all(r == res[0] for r in res.values())
+    assert "AddMessage" in res[0][0][0] and "DelMessage" in res[0][0][1] and res[0][1] == 0
+
+
+def test_tensor_broadcast_single_buffer():
+    res = _run(2, w_tensors)
+    assert res[1] == res[0]
+    assert res[1]["b"] == [0, 7, 14, 21, 28] and res[1]["c"] == [[1, 2], [3, 255]]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gather_and_sharding(world):
+    res = _run(world, w_gather)
+    for r, (s, var, (lo, hi)) in res.items():
+        assert s == [float(i) for i in range(world) for _ in range(3)]
+        assert var == [float(i) for i in range(10)]
+    shards = sorted(v[2] for v in res.values())
+    assert shards[0][0] == 0 and shards[-1][1] == 10
+
+
+def test_distributed_serving(fixtures_dir):
+    res = _run(2, w_serving, fixtures_dir["kmeans"], fixtures_dir["kmeans_nooutput_notarget"])
+    for s1, v1, v2, v3, meta in res.values():
+        assert s1 == [3.0, 4.0] * 5 and all(v1)  # duplicate Add ignored on every rank
+        assert not any(v2)  # model without a target -> EmptyScore everywhere
+        assert not any(v3)  # deleted -> EmptyScore
+        assert len(meta) == 1

@@ -253,3 +253,20 @@ def test_svm_regression(gpu):
     s, v = _gpu_np(c.plan(gpu), X)
     ref, vref = c.score_matrix_oracle(X)
     assert (v == vref).all() and np.max(np.abs(s - ref)) < 1e-4
+
+
+def test_plan_state_roundtrip(gpu):
+    """What broadcast_plan ships over RCCL: export_state -> from_state scores identically."""
+    from flink_jpmml_amd.bench.synth import gbdt_pmml, mlp_pmml, stream_matrix
+    from flink_jpmml_amd.runtime.compiled import CompiledPmml
+    from flink_jpmml_amd.runtime.plans import DevicePlan
+
+    for txt, F in ((gbdt_pmml(n_trees=50, depth=5, n_features=12, seed=2), 12), (mlp_pmml(n_features=12), 12)):
+        c = CompiledPmml.from_string(txt)
+        p = c.plan(gpu)
+        meta, tensors = p.export_state()
+        q = DevicePlan.from_state(meta, {k: v.clone() for k, v in tensors.items()}, gpu)
+        X = stream_matrix(3000, F, seed=5)
+        s1, v1 = p.score(X)
+        s2, v2 = q.score(X)
+        assert (s1 == s2).all() and (v1 == v2).all()
