@@ -42,8 +42,8 @@ for s in $STEPS; do
       mkdir -p "$OUT/pmc"
       rocprofv3 -L > "$OUT/pmc/counters.txt" 2>&1 || true
       ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats \
-          --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY \
-          -d "$OUT/pmc" -o pmc --output-format csv -- python3 "$ROOT/scripts/kbench.py" --iters 3 \
+          --pmc ${PMC_COUNTERS:-SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAVE_CYCLES SQ_WAIT_ANY} \
+          -d "$OUT/pmc" -o pmc --output-format csv -- python3 "$ROOT/scripts/kbench.py" --iters 3 ${KB_ARGS:-} \
           > "$OUT/pmc.log" 2>&1 ); rc=$?
       echo "=== pmc rc=$rc" | tee -a "$OUT/session.log"
       if fatal $rc; then exit $rc; fi ;;
