@@ -333,6 +333,92 @@ __device__ __forceinline__ float traverse_chunk_g(const TreeArgs& a, const uint3
   return acc;
 }
 
+// Fast path of the wide kernel (tile without missing values), written against explicit LDS byte
+// addresses so the per-level work is exactly: node ds_read_b64, feature address add, feature
+// ds_read_b32, v_cmp, v_cndmask, v_lshl_add — 4 VALU per level (the plain heap-index form
+// compiled to ~7.5 as hipcc re-expanded `j = 2j + r` into shifted bit sums).
+//  * u = LDS address of the current node of tree i minus i*TS (TS = compile-time tree stride of a
+//    tree group, folded into the ds_read immediate offset); children: u' = 2u + (8 - b0) + 8r.
+//  * last level: the two leaves under a node are adjacent, so the leaf PAIR (one conflict-free
+//    ds_read_b64 at u + C, C folded into the offset) is fetched together with the feature and the
+//    final compare only selects between them — one dependent LDS round trip less per tree, and no
+//    2-way bank conflicts of scattered ds_read_b32 leaf reads.
+// `__asm__("" : "+v"(...))` pins values in VGPRs so the compiler cannot re-derive them.
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) const u32x2_t lds_u2_t;
+typedef __attribute__((address_space(3))) const float lds_f_t;
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const char*)p;
+}
+__device__ __forceinline__ uint2 lds_ld2(uint32_t a) {
+  const u32x2_t v = *(lds_u2_t*)(uintptr_t)a;
+  return make_uint2(v.x, v.y);
+}
+__device__ __forceinline__ float lds_ldf(uint32_t a) { return *(lds_f_t*)(uintptr_t)a; }
+
+__host__ __device__ constexpr int perfect_rec_words(int depth, int P) {
+  return ((2 * ((1 << depth) - 1) + (1 << depth) * P + ((1 << depth) - 1 + 31) / 32) + 3) & ~3;
+}
+
+template <int DEPTH, int ILP, int G>
+__device__ __forceinline__ float traverse_fast_g(const uint32_t* buf, int nt, int g, uint32_t feat_lane,
+                                                 float acc) {
+  constexpr int NI = (1 << DEPTH) - 1;
+  constexpr int NL = 1 << DEPTH;
+  constexpr uint32_t RB = 4u * perfect_rec_words(DEPTH, 1);  // record bytes
+  constexpr uint32_t TS = G * RB;                            // tree stride within a group
+  constexpr uint32_t C = 8u + 8u * NI - 4u * NL;             // last-level node -> its leaf pair
+  const uint32_t lds0 = lds_addr(buf);
+  const int mt = (nt - g + G - 1) / G;
+  int m = 0;
+  for (; m + ILP <= mt; m += ILP) {
+    const uint32_t b0 = lds0 + (uint32_t)(g + G * m) * RB;
+    uint32_t k0 = 8u - b0, k1 = 16u - b0;
+    __asm__("" : "+v"(k0), "+v"(k1));
+    uint32_t u[ILP];
+#pragma unroll
+    for (int i = 0; i < ILP; ++i) {
+      u[i] = b0;
+      __asm__ volatile("" : "+v"(u[i]));  // separate root reads: ds_read2_b64 pairing costs 8 LDS
+                                          // cycles vs 2 x 2 for two ds_read_b64
+    }
+#pragma unroll
+    for (int d = 0; d + 1 < DEPTH; ++d) {
+#pragma unroll
+      for (int i = 0; i < ILP; ++i) {
+        const uint2 nd = lds_ld2(u[i] + i * TS);
+        const float x = lds_ldf(feat_lane + nd.y);
+        u[i] = 2u * u[i] + ((x >= __uint_as_float(nd.x)) ? k1 : k0);
+        __asm__("" : "+v"(u[i]));
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < ILP; ++i) {
+      uint32_t ul = u[i] + C;
+      __asm__ volatile("" : "+v"(ul));  // keep the pair read out of a ds_read2_b64 with the node
+      const uint2 nd = lds_ld2(u[i] + i * TS);
+      const uint2 lv = lds_ld2(ul + i * TS);
+      const float x = lds_ldf(feat_lane + nd.y);
+      acc += (x >= __uint_as_float(nd.x)) ? __uint_as_float(lv.y) : __uint_as_float(lv.x);
+    }
+  }
+  for (; m < mt; ++m) {
+    const uint32_t b0 = lds0 + (uint32_t)(g + G * m) * RB;
+    uint32_t u = b0;
+#pragma unroll
+    for (int d = 0; d + 1 < DEPTH; ++d) {
+      const uint2 nd = lds_ld2(u);
+      const float x = lds_ldf(feat_lane + nd.y);
+      u = 2u * u + 8u - b0 + ((x >= __uint_as_float(nd.x)) ? 8u : 0u);
+    }
+    const uint2 nd = lds_ld2(u);
+    const uint2 lv = lds_ld2(u + C);
+    const float x = lds_ldf(feat_lane + nd.y);
+    acc += (x >= __uint_as_float(nd.x)) ? __uint_as_float(lv.y) : __uint_as_float(lv.x);
+  }
+  return acc;
+}
+
 template <int DEPTH, int ILP, int G>
 __global__ __launch_bounds__(TB * G, 1) void tree_perfect_wide_kernel(TreeArgs a) {
   constexpr int T = TB * G;
@@ -400,7 +486,7 @@ __global__ __launch_bounds__(TB * G, 1) void tree_perfect_wide_kernel(TreeArgs a
     if (missing) {
       acc = traverse_chunk_g<DEPTH, true, ILP, G>(a, cur, nt, g, feat_lane, acc);
     } else {
-      acc = traverse_chunk_g<DEPTH, false, ILP, G>(a, cur, nt, g, feat_lane, acc);
+      acc = traverse_fast_g<DEPTH, ILP, G>(cur, nt, g, lds_addr(feat + r_local), acc);
     }
     PF4_STORE(nxt, n16, T)
     __syncthreads();
@@ -525,6 +611,7 @@ int launch_perfect(hipStream_t st, const TreeArgs& a, dim3 grid, size_t lds) {
     const size_t lds_w = lds + (size_t)WIDE_G * TB * 4;
     if (lds_w > 160 * 1024) return -5;
     if ((size_t)a.chunk_trees * a.rec_words > (size_t)TB * WIDE_G * 4 * 4) return -9;
+    if (a.rec_words != perfect_rec_words(D, 1) || a.P != 1) return -10;
     err = prepare_launch(tree_perfect_wide_kernel<D, 8, WIDE_G>, lds_w);
     if (!err) hipLaunchKernelGGL((tree_perfect_wide_kernel<D, 8, WIDE_G>), grid, dim3(TB * WIDE_G), lds_w, st, a);
     return err;

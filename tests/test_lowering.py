@@ -85,6 +85,38 @@ def test_perfect_layout_emulation_matches_oracle(kind):
         assert (out == ref).all()
 
 
+def emulate_perfect_fast(c, X):
+    """Byte-address form used by the wide kernel's fast path (tree.hip::traverse_fast_g): node
+    address u' = 2u + (8 - b0) + 8r, leaf pair at u + 8 + 8*NI - 4*NL on the last level."""
+    spec = ensemble_spec(c)
+    D = max(t.depth for t in spec.trees)
+    blob, rec, _ = _perfect_pack(spec.trees, spec.weights, 1, D)
+    mem = blob.reshape(-1)
+    NI, NL = (1 << D) - 1, 1 << D
+    C = 8 + 8 * NI - 4 * NL
+    Xf = X.astype(np.float32)
+    rows = np.arange(len(X))
+    acc = np.zeros(len(X), np.float32)
+    for t in range(blob.shape[0]):
+        b0 = t * rec * 4
+        u = np.full(len(X), b0, np.int64)
+        for _ in range(D - 1):
+            x = Xf[rows, mem[u // 4 + 1] // (TB * 4)]
+            u = 2 * u + (8 - b0) + 8 * (x >= mem[u // 4].view(np.float32))
+        x = Xf[rows, mem[u // 4 + 1] // (TB * 4)]
+        right = x >= mem[u // 4].view(np.float32)
+        acc += np.where(right, mem[(u + C) // 4 + 1].view(np.float32), mem[(u + C) // 4].view(np.float32))
+    return acc
+
+
+@pytest.mark.parametrize("depth", [1, 3, 6])
+def test_wide_fast_path_addressing(depth):
+    c = CompiledPmml.from_string(gbdt_pmml(n_trees=12, depth=depth, n_features=7, seed=depth))
+    X = stream_matrix(257, 7, seed=1)
+    _, ref = emulate_perfect(c, X)
+    np.testing.assert_array_equal(emulate_perfect_fast(c, X), ref[:, 0])
+
+
 def test_pointer_layout_emulation_matches_oracle():
     c = CompiledPmml.from_string(gbdt_pmml(n_trees=6, depth=7, n_features=9, seed=4))
     X = stream_matrix(200, 9, seed=5, missing_rate=0.1)
