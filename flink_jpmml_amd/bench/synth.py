@@ -36,12 +36,13 @@ def _fnum(x: float) -> str:
 
 class _TreeGen:
     def __init__(self, rng: np.random.Generator, n_features: int, depth: int, p_split: float,
-                 thresholds: np.ndarray):
+                 thresholds: np.ndarray, field_fmt: str = "f{}"):
         self.rng = rng
         self.F = n_features
         self.depth = depth
         self.p_split = p_split
         self.thr = thresholds
+        self.fmt = field_fmt
         self.next_id = 0
 
     def nid(self) -> int:
@@ -60,11 +61,12 @@ class _TreeGen:
         go_left = bool(self.rng.random() < 0.5)
         # write children into a buffer first to learn the right child's id
         buf = io.StringIO()
-        self.write(buf, depth + 1, f'<SimplePredicate field="f{f}" operator="lessThan" value="{t}"/>', leaf_fn,
+        name = self.fmt.format(f)
+        self.write(buf, depth + 1, f'<SimplePredicate field="{name}" operator="lessThan" value="{t}"/>', leaf_fn,
                    indent + " ")
         right_id = self.next_id + 1
-        self.write(buf, depth + 1, f'<SimplePredicate field="f{f}" operator="greaterOrEqual" value="{t}"/>', leaf_fn,
-                   indent + " ")
+        self.write(buf, depth + 1, f'<SimplePredicate field="{name}" operator="greaterOrEqual" value="{t}"/>',
+                   leaf_fn, indent + " ")
         dflt = left_id if go_left else right_id
         out.write(f'{indent}<Node id="{my}" defaultChild="{dflt}">{pred}\n')
         out.write(buf.getvalue())
@@ -97,17 +99,29 @@ def _mining_schema(out: io.StringIO, F: int, target: Optional[str], indent: str 
 
 def gbdt_pmml(n_trees: int = 1000, depth: int = 6, n_features: int = 32, seed: int = 0,
               objective: str = "regression", p_split: float = 0.9, learning_rate: float = 0.1,
-              base_score: float = 0.5) -> str:
-    """XGBoost-style GBDT PMML (regression or binary:logistic chain)."""
+              base_score: float = 0.5, float_casts: bool = False) -> str:
+    """XGBoost-style GBDT PMML (regression or binary:logistic chain). ``float_casts`` adds the
+    ``float(fj)`` ``LocalTransformations`` casts that pipeline exporters (sklearn2pmml) emit, with
+    every split on the cast field."""
     rng = np.random.default_rng(seed)
     thresholds = np.sort(rng.standard_normal((n_features, 64)).astype(np.float32), axis=1)
     out = io.StringIO()
     _header(out, f"synthetic GBDT {n_trees} trees depth {depth} ({objective})")
     binary = objective == "binary"
     _data_dictionary(out, n_features, "y", "integer" if binary else "double", ["0", "1"] if binary else None)
+    fmt = "float(f{})" if float_casts else "f{}"
 
     def leaf() -> str:
         return _fnum(learning_rate * rng.standard_normal())
+
+    def casts(indent: str) -> None:
+        if not float_casts:
+            return
+        out.write(f'{indent}<LocalTransformations>\n')
+        for j in range(n_features):
+            out.write(f'{indent} <DerivedField name="float(f{j})" optype="continuous" dataType="float">'
+                      f'<FieldRef field="f{j}"/></DerivedField>\n')
+        out.write(f'{indent}</LocalTransformations>\n')
 
     def trees_model(indent: str, target_in_schema: bool, rescale: float) -> None:
         out.write(f'{indent}<MiningModel functionName="regression">\n')
@@ -116,9 +130,10 @@ def gbdt_pmml(n_trees: int = 1000, depth: int = 6, n_features: int = 32, seed: i
             out.write(f'{indent} <Output><OutputField name="xgbValue" optype="continuous" dataType="float" '
                       f'isFinalResult="false"/></Output>\n')
         out.write(f'{indent} <Targets><Target rescaleConstant="{_fnum(rescale)}"/></Targets>\n')
+        casts(indent + " ")
         out.write(f'{indent} <Segmentation multipleModelMethod="sum">\n')
         for t in range(n_trees):
-            g = _TreeGen(rng, n_features, depth, p_split, thresholds)
+            g = _TreeGen(rng, n_features, depth, p_split, thresholds, fmt)
             out.write(f'{indent}  <Segment id="{t + 1}"><True/>\n')
             out.write(f'{indent}   <TreeModel functionName="regression" missingValueStrategy="defaultChild" '
                       f'noTrueChildStrategy="returnLastPrediction" splitCharacteristic="binarySplit">\n')
@@ -131,9 +146,10 @@ def gbdt_pmml(n_trees: int = 1000, depth: int = 6, n_features: int = 32, seed: i
         out.write(' <MiningModel functionName="regression" algorithmName="XGBoost (GBTree)">\n')
         _mining_schema(out, n_features, "y", "  ")
         out.write(f'  <Targets><Target field="y" rescaleConstant="{_fnum(base_score)}"/></Targets>\n')
+        casts("  ")
         out.write('  <Segmentation multipleModelMethod="sum">\n')
         for t in range(n_trees):
-            g = _TreeGen(rng, n_features, depth, p_split, thresholds)
+            g = _TreeGen(rng, n_features, depth, p_split, thresholds, fmt)
             out.write(f'   <Segment id="{t + 1}"><True/>\n')
             out.write('    <TreeModel functionName="regression" missingValueStrategy="defaultChild" '
                       'noTrueChildStrategy="returnLastPrediction" splitCharacteristic="binarySplit">\n')

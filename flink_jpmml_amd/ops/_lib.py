@@ -147,7 +147,14 @@ class SvmArgs(ctypes.Structure):
                 ("decision", c_void_p)]
 
 
+class DeriveArgs(ctypes.Structure):
+    _fields_ = [("X", c_void_p), ("n_rows", c_int), ("n_in", c_int), ("ldx", c_int), ("n_tile", c_int),
+                ("prep", c_void_p), ("prog", c_void_p), ("pool", c_void_p), ("out_cols", c_void_p),
+                ("n_insn", c_int), ("n_sel", c_int), ("out", c_void_p), ("row_ok", c_void_p)]
+
+
 _ABI = {
+    "pmml_derive_args_size": DeriveArgs,
     "pmml_tree_args_size": TreeArgs,
     "pmml_cluster_args_size": ClusterArgs,
     "pmml_linear_args_size": LinearArgs,
@@ -205,6 +212,10 @@ def load(auto_build: bool = True) -> ctypes.CDLL:
             lib.pmml_mlp_launch.argtypes = [c_void_p, ctypes.POINTER(MlpArgs), c_int]
         if hasattr(lib, "pmml_svm_launch"):
             lib.pmml_svm_launch.argtypes = [c_void_p, ctypes.POINTER(SvmArgs), c_int]
+        lib.pmml_derive_launch.argtypes = [c_void_p, ctypes.POINTER(DeriveArgs)]
+        lib.pmml_derive_launch.restype = c_int
+        lib.pmml_mask_invalid.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int]
+        lib.pmml_mask_invalid.restype = c_int
         _lib = lib
         return lib
 

@@ -199,8 +199,11 @@ class DevicePlan:
             raise ValueError(f"device plans need a cuda (HIP) device, got {self.device}")
         self.lib = _lib.load()
         self.n_features = compiled.n_features
-        prep, any_prep = build_field_prep(compiled, compiled.active_fields)
-        self.prep = torch.from_numpy(prep.view(np.int32)).to(self.device) if any_prep else None
+        if getattr(compiled, "prepared_inputs", False):
+            self.prep = None  # a derive pass already applied the MiningField preparation
+        else:
+            prep, any_prep = build_field_prep(compiled, compiled.active_fields)
+            self.prep = torch.from_numpy(prep.view(np.int32)).to(self.device) if any_prep else None
 
     # -- helpers
     def _t(self, arr, dtype=None):
@@ -238,6 +241,8 @@ class DevicePlan:
         from ..ops import _lib
 
         cls = {c.__name__: c for c in (TreePlan, ClusterPlan, LinearPlan)}.get(meta["__class__"])
+        if cls is None and meta["__class__"] == "DerivedPlan":
+            from .derive import DerivedPlan as cls
         if cls is None:
             from . import nn_plans
 
@@ -506,7 +511,7 @@ def _regression_ensemble(ev, field_index) -> Tuple[List[BinaryTree], List[float]
 
 def ensemble_spec(compiled) -> EnsembleSpec:
     ev = compiled.evaluator
-    field_index = {f: i for i, f in enumerate(compiled.active_fields)}
+    field_index = getattr(compiled, "field_index", None) or {f: i for i, f in enumerate(compiled.active_fields)}
     try:
         if ev.kind == "regression":
             trees, w, a, b = _regression_ensemble(ev, field_index)
@@ -822,8 +827,15 @@ def compile_plan(compiled, device, **opts) -> DevicePlan:
     ev = compiled.evaluator
     if not compiled.target_fields:
         raise NotLowerable("model has no target field (every record scores EmptyScore)")
-    if compiled.model.local_transformations or compiled.doc.transformations:
-        raise NotLowerable("derived fields are evaluated on the host in this revision")
+    if not getattr(compiled, "fields_resolved", False):
+        # derived fields: pure casts alias their input column (tree kernels), anything else runs
+        # as a derive-kernel pass in front of the model kernel (runtime/derive.py)
+        from .derive import DerivedPlan, FieldView, plan_field_layout
+
+        layout = plan_field_layout(compiled, allow_alias=isinstance(ev, (TreeEvaluator, MiningEvaluator)))
+        if layout.program is not None:
+            return DerivedPlan(compiled, device, layout, **opts)
+        compiled = FieldView(compiled, layout, prepared=False)
     if isinstance(ev, ClusteringEvaluator):
         return ClusterPlan(compiled, device)
     if isinstance(ev, (TreeEvaluator, MiningEvaluator)):

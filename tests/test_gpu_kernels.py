@@ -270,3 +270,67 @@ def test_plan_state_roundtrip(gpu):
         s1, v1 = p.score(X)
         s2, v2 = q.score(X)
         assert (s1 == s2).all() and (v1 == v2).all()
+
+
+# ------------------------------------------------------------------ derived fields (derive.hip)
+
+
+def test_derived_regression_program_on_gpu(gpu):
+    """Every DerivedField kind through the derive kernel, then the linear kernel (mask fixup)."""
+    from test_derive import inputs, regression_doc
+
+    from flink_jpmml_amd.runtime.compiled import CompiledPmml
+    from flink_jpmml_amd.runtime.derive import DerivedPlan, emulate
+
+    c = CompiledPmml.from_string(regression_doc())
+    plan = c.plan(gpu)
+    assert isinstance(plan, DerivedPlan)
+    X = inputs(20_000, seed=7)
+    s, v = _gpu_np(plan, X)
+    ref, vref = c.score_matrix_oracle(X)
+    assert (v == vref).all()
+    np.testing.assert_allclose(s[v], ref[v], rtol=2e-5, atol=2e-5)
+    # the device program equals its numpy twin column for column
+    import torch
+
+    P, _ = c.prepare(X)
+    Xt = torch.from_numpy(X.astype(np.float32)).to(gpu)
+    Xa, ok = plan._buffers(None, len(X))
+    sc, va = plan.alloc_outputs(len(X))
+    plan.launch(Xt, sc, va)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(Xa.cpu().numpy(), emulate(plan.program, P), rtol=1e-6, atol=1e-7, equal_nan=True)
+
+
+def test_derived_tree_program_on_gpu(gpu):
+    from test_derive import inputs, tree_doc
+
+    from flink_jpmml_amd.runtime.compiled import CompiledPmml
+    from flink_jpmml_amd.runtime.derive import DerivedPlan
+    from flink_jpmml_amd.runtime.plans import DevicePlan, TreePlan
+
+    c = CompiledPmml.from_string(tree_doc())
+    plan = c.plan(gpu)
+    assert isinstance(plan, DerivedPlan) and isinstance(plan.inner, TreePlan)
+    X = inputs(30_000, seed=2)
+    s, v = _gpu_np(plan, X)
+    ref, vref = c.score_matrix_oracle(X)
+    assert (v == vref).all() and (s[v] == ref[v]).all()
+    meta, tensors = plan.export_state()  # RCCL replication of a derived plan
+    q = DevicePlan.from_state(meta, {k: t.clone() for k, t in tensors.items()}, gpu)
+    s2, v2 = _gpu_np(q, X)
+    assert (s2 == s).all() and (v2 == v).all()
+
+
+def test_float_cast_gbdt_aliases_on_gpu(gpu):
+    from flink_jpmml_amd.bench.synth import gbdt_pmml, stream_matrix
+    from flink_jpmml_amd.runtime.compiled import CompiledPmml
+    from flink_jpmml_amd.runtime.plans import TreePlan
+
+    c = CompiledPmml.from_string(gbdt_pmml(n_trees=100, depth=6, n_features=16, seed=9, float_casts=True))
+    plan = c.plan(gpu)
+    assert isinstance(plan, TreePlan)  # casts alias their input columns: no derive pass
+    X = stream_matrix(20_000, 16, seed=3, missing_rate=0.03)
+    s, v = _gpu_np(plan, X)
+    ref, vref = c.score_matrix_oracle(X)
+    assert (v == vref).all() and np.max(np.abs(s - ref)) < 2e-5
