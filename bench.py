@@ -44,7 +44,10 @@ def parse_args(argv=None):
     p.add_argument("--rows", type=int, default=1 << 20, help="rows per GPU per step")
     p.add_argument("--micro-batch", type=int, default=1 << 19)
     p.add_argument("--pipeline-depth", type=int, default=3, help="input ring slots (H2D/compute overlap)")
-    p.add_argument("--objective", choices=["regression", "binary"], default="regression")
+    p.add_argument("--objective", choices=["regression", "binary"], default="regression",
+                   help="binary = modelChain GBDT -> logistic calibrator (BASELINE config 5)")
+    p.add_argument("--precision", choices=["fp32", "fp8"], default="fp32",
+                   help="leaf-value precision (fp8 = OCP e4m3 leaves, fp32 thresholds; config 5)")
     p.add_argument("--latency-batch", type=int, default=4096)
     p.add_argument("--latency-iters", type=int, default=50)
     p.add_argument("--no-allgather", action="store_true")
@@ -81,7 +84,7 @@ def main(argv=None) -> int:
         text = gbdt_pmml(n_trees=args.trees, depth=args.depth, n_features=args.features, seed=args.seed,
                          objective=args.objective)
         compiled = CompiledPmml.from_string(text)
-        plan = compiled.plan(device)
+        plan = compiled.plan(device, precision=args.precision)
     plan = broadcast_plan(plan, ctx)
     torch.cuda.synchronize()
     load_s = time.perf_counter() - t_load
@@ -97,7 +100,7 @@ def main(argv=None) -> int:
         both = v_ref & v_gpu
         err = float(np.max(np.abs(s_gpu[both] - s_ref[both]))) if both.any() else float("nan")
         check = {"oracle_rows": int(args.check_rows), "valid_match": bool((v_ref == v_gpu).all()),
-                 "max_abs_err_vs_fp64": err}
+                 "max_abs_err_vs_fp64": err, "exact_match_rate": float((s_gpu[both] == s_ref[both]).mean())}
 
     # ---- this rank's synthetic record shard in pinned host memory, on the GPU's NUMA node
     from flink_jpmml_amd.utils.numa import bind_to_gpu_numa
@@ -195,11 +198,11 @@ def main(argv=None) -> int:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp32",
+            "dtype": "fp32" if args.precision == "fp32" else "fp32 (fp8 e4m3 leaf values)",
             "data": "synthetic (random-init XGBoost-style GBDT PMML, N(0,1) float records)",
             "config": {
                 "model": f"GBDT {args.trees} trees, depth {args.depth}, {args.features} float features "
-                         f"(XGBoost-style PMML, {args.objective})",
+                         f"(XGBoost-style PMML, {args.objective}, {args.precision} leaves)",
                 "global_batch": args.rows * N,
                 "seq_len": None,
                 "parallelism": f"dp{N}",

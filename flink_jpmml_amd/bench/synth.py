@@ -99,7 +99,7 @@ def _mining_schema(out: io.StringIO, F: int, target: Optional[str], indent: str 
 
 def gbdt_pmml(n_trees: int = 1000, depth: int = 6, n_features: int = 32, seed: int = 0,
               objective: str = "regression", p_split: float = 0.9, learning_rate: float = 0.1,
-              base_score: float = 0.5, float_casts: bool = False) -> str:
+              base_score: float = 0.5, float_casts: bool = False, missing_strategy: str = "defaultChild") -> str:
     """XGBoost-style GBDT PMML (regression or binary:logistic chain). ``float_casts`` adds the
     ``float(fj)`` ``LocalTransformations`` casts that pipeline exporters (sklearn2pmml) emit, with
     every split on the cast field."""
@@ -135,7 +135,7 @@ def gbdt_pmml(n_trees: int = 1000, depth: int = 6, n_features: int = 32, seed: i
         for t in range(n_trees):
             g = _TreeGen(rng, n_features, depth, p_split, thresholds, fmt)
             out.write(f'{indent}  <Segment id="{t + 1}"><True/>\n')
-            out.write(f'{indent}   <TreeModel functionName="regression" missingValueStrategy="defaultChild" '
+            out.write(f'{indent}   <TreeModel functionName="regression" missingValueStrategy="{missing_strategy}" '
                       f'noTrueChildStrategy="returnLastPrediction" splitCharacteristic="binarySplit">\n')
             _mining_schema(out, n_features, None, indent + "    ")
             g.write(out, 0, "<True/>", leaf, indent + "    ", force_split=True)
@@ -151,7 +151,7 @@ def gbdt_pmml(n_trees: int = 1000, depth: int = 6, n_features: int = 32, seed: i
         for t in range(n_trees):
             g = _TreeGen(rng, n_features, depth, p_split, thresholds, fmt)
             out.write(f'   <Segment id="{t + 1}"><True/>\n')
-            out.write('    <TreeModel functionName="regression" missingValueStrategy="defaultChild" '
+            out.write(f'    <TreeModel functionName="regression" missingValueStrategy="{missing_strategy}" '
                       'noTrueChildStrategy="returnLastPrediction" splitCharacteristic="binarySplit">\n')
             _mining_schema(out, n_features, None, "     ")
             g.write(out, 0, "<True/>", leaf, "     ", force_split=True)
@@ -175,9 +175,9 @@ def gbdt_pmml(n_trees: int = 1000, depth: int = 6, n_features: int = 32, seed: i
 
 
 def random_forest_pmml(n_trees: int = 500, depth: int = 8, n_features: int = 32, n_classes: int = 3,
-                       seed: int = 0, p_split: float = 0.85) -> str:
-    """scikit-learn-style majority-vote random forest (classification trees, ``none`` missing
-    strategy with a ``True`` second child)."""
+                       seed: int = 0, p_split: float = 0.85, missing_strategy: str = "defaultChild") -> str:
+    """scikit-learn-style majority-vote random forest (classification trees). ``missing_strategy``
+    ``"nullPrediction"`` is what sklearn2pmml exports: a missing split value voids the tree."""
     rng = np.random.default_rng(seed)
     thresholds = np.sort(rng.standard_normal((n_features, 64)).astype(np.float32), axis=1)
     cats = [str(c) for c in range(n_classes)]
@@ -190,7 +190,7 @@ def random_forest_pmml(n_trees: int = 500, depth: int = 8, n_features: int = 32,
     for t in range(n_trees):
         g = _TreeGen(rng, n_features, depth, p_split, thresholds)
         out.write(f'   <Segment id="{t + 1}"><True/>\n')
-        out.write('    <TreeModel functionName="classification" missingValueStrategy="defaultChild" '
+        out.write(f'    <TreeModel functionName="classification" missingValueStrategy="{missing_strategy}" '
                   'splitCharacteristic="binarySplit">\n')
         _mining_schema(out, n_features, "y", "     ")
         g.write(out, 0, "<True/>", lambda: cats[int(rng.integers(n_classes))], "     ", force_split=True)

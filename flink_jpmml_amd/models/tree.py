@@ -182,10 +182,65 @@ class BinaryTree:
     leaf_value: np.ndarray  # float64 (regression) / class index (classification)
     leaf_probs: Optional[np.ndarray]  # [nodes, C] or None
     depth: int
+    null_missing: bool = False  # a missing value at any visited split -> null prediction
 
 
 class NotBinary(Exception):
     pass
+
+
+def membership_key(field: str, values) -> str:
+    """Name of the synthetic 0/1 column "``field`` is one of ``values``" (derive program)."""
+    return "__in__(" + field + "|" + "|".join(sorted(str(v) for v in values)) + ")"
+
+
+def member_form(pa: ir.Predicate, pb: ir.Predicate):
+    """``(field, values, first_child_is_member)`` when the two child predicates are a categorical
+    binary split — ``isIn S`` / ``isNotIn S`` (LightGBM, sklearn2pmml) or ``== v`` / ``!= v``
+    (R, KNIME) with the complement or ``True`` as second child — else None."""
+    if isinstance(pa, ir.SimpleSetPredicate) and pa.boolean_operator in ("isIn", "isNotIn"):
+        ok = isinstance(pb, ir.TruePredicate) or (
+            isinstance(pb, ir.SimpleSetPredicate) and pb.field == pa.field
+            and sorted(pb.values) == sorted(pa.values) and pb.boolean_operator != pa.boolean_operator)
+        return (pa.field, tuple(pa.values), pa.boolean_operator == "isIn") if ok else None
+    if isinstance(pa, ir.SimplePredicate) and pa.operator in ("equal", "notEqual") and pa.value is not None:
+        neg = "notEqual" if pa.operator == "equal" else "equal"
+        ok = isinstance(pb, ir.TruePredicate) or (
+            isinstance(pb, ir.SimplePredicate) and pb.field == pa.field and pb.value == pa.value
+            and pb.operator == neg)
+        return (pa.field, (pa.value,), pa.operator == "equal") if ok else None
+    return None
+
+
+def membership_fields(model: ir.Model) -> Dict[str, ir.DerivedField]:
+    """Synthetic DerivedFields (MapValues lookups: member 1, non-member 0, missing -> missing) for
+    every categorical binary split of the model's trees (nested segments included)."""
+    out: Dict[str, ir.DerivedField] = {}
+
+    def walk(m: ir.Model) -> None:
+        if isinstance(m, ir.MiningModel):
+            for seg in m.segments:
+                walk(seg.model)
+            return
+        if not isinstance(m, ir.TreeModel):
+            return
+        stack = [m.root]
+        while stack:
+            nd = stack.pop()
+            stack.extend(nd.children)
+            if len(nd.children) != 2:
+                continue
+            f = member_form(nd.children[0].predicate, nd.children[1].predicate)
+            if f is None:
+                continue
+            name = membership_key(f[0], f[1])
+            if name not in out:
+                rows = [{"k": v, "o": "1"} for v in f[1]]
+                expr = ir.MapValues(output_column="o", field_columns=[(f[0], "k")], rows=rows, default_value="0")
+                out[name] = ir.DerivedField(name, "continuous", "double", expr)
+
+    walk(model)
+    return out
 
 
 def lower_binary_tree(ev: TreeEvaluator, field_index: Dict[str, int]) -> BinaryTree:
@@ -194,14 +249,19 @@ def lower_binary_tree(ev: TreeEvaluator, field_index: Dict[str, int]) -> BinaryT
     Accepted node shapes (all exporters we know of use one of them):
 
     * two children ``[x OP t, True]`` or ``[x OP t, x NEG(OP) t]``;
-    * missing values: ``defaultChild`` strategy (per-node default), ``none`` strategy with a
-      ``True`` second child (missing → right), or ``lastPrediction``/``nullPrediction`` are *not*
-      lowered (they need per-node early exit) and raise :class:`NotBinary`.
+    * missing values: ``defaultChild`` strategy (per-node default); ``none`` strategy with a
+      ``True`` second child (missing → right); ``nullPrediction`` — and ``none`` with complement
+      children under ``returnNullPrediction`` — make the whole tree's prediction null on a
+      missing split value (``null_missing``: the kernels poison the row). ``lastPrediction`` (and
+      ``returnLastPrediction`` on a missing value) needs internal-node scores and raises
+      :class:`NotBinary`.
     """
     tm = ev.tree
     strat = tm.missing_value_strategy
-    if strat not in ("none", "defaultChild"):
+    if strat not in ("none", "defaultChild", "nullPrediction"):
         raise NotBinary(f"missingValueStrategy {strat}")
+    null_missing = strat == "nullPrediction"
+    forms = set()  # 'none' strategy: second child True (missing -> right) or complement (-> null)
     if not isinstance(tm.root.predicate, ir.TruePredicate):
         raise NotBinary("root predicate is not True")
     feats: List[int] = []
@@ -245,17 +305,26 @@ def lower_binary_tree(ev: TreeEvaluator, field_index: Dict[str, int]) -> BinaryT
             raise NotBinary("node does not have exactly two children")
         a, b = node.children
         pa, pb = a.predicate, b.predicate
-        if not isinstance(pa, ir.SimplePredicate) or pa.operator not in _OPS:
-            raise NotBinary("first child predicate is not a numeric comparison")
-        if pa.field not in field_index or ev.schema.is_string(pa.field):
-            raise NotBinary("split on a non-input or string field")
-        if isinstance(pb, ir.TruePredicate):
-            pass
-        elif isinstance(pb, ir.SimplePredicate) and pb.field == pa.field and pb.operator == _NEG[pa.operator] \
-                and pb.value == pa.value:
-            pass
+        member = member_form(pa, pb)
+        if member is not None:
+            # categorical split (set / equality): numeric split on its 0/1 membership column
+            split_field = membership_key(member[0], member[1])
+            if split_field not in field_index:
+                raise NotBinary("categorical split without a membership column")
+            split_t, split_op = 0.5, (OP_GE if member[2] else OP_LT)
         else:
-            raise NotBinary("second child is not the complement of the first")
+            if not isinstance(pa, ir.SimplePredicate) or pa.operator not in _OPS:
+                raise NotBinary("first child predicate is not a numeric comparison")
+            if pa.field not in field_index or ev.schema.is_string(pa.field):
+                raise NotBinary("split on a non-input or string field")
+            if isinstance(pb, ir.TruePredicate):
+                pass
+            elif isinstance(pb, ir.SimplePredicate) and pb.field == pa.field and pb.operator == _NEG[pa.operator] \
+                    and pb.value == pa.value:
+                pass
+            else:
+                raise NotBinary("second child is not the complement of the first")
+            split_field, split_t, split_op = pa.field, float(pa.value), _OPS[pa.operator]
         # missing-value direction
         if strat == "defaultChild":
             if node.default_child is None:
@@ -263,16 +332,24 @@ def lower_binary_tree(ev: TreeEvaluator, field_index: Dict[str, int]) -> BinaryT
             go_left = node.default_child == a.id
             if not go_left and node.default_child != b.id:
                 raise NotBinary("defaultChild does not name a child")
+        elif strat == "nullPrediction":
+            go_left = False  # never used: the prediction is null
         else:
             # 'none': UNKNOWN counts as FALSE -> a missing value fails the first predicate; the
-            # second child is taken only if it is True (a complement predicate is also UNKNOWN
-            # -> no true child -> noTrueChildStrategy, which we cannot lower)
-            if not isinstance(pb, ir.TruePredicate):
-                raise NotBinary("missing value with complement predicate needs noTrueChild handling")
+            # second child is taken if it is True; a complement predicate is also UNKNOWN -> no
+            # true child -> noTrueChildStrategy (null prediction lowers, last prediction does not)
+            if isinstance(pb, ir.TruePredicate):
+                forms.add("true")
+            elif tm.no_true_child_strategy == "returnNullPrediction":
+                forms.add("complement")
+            else:
+                raise NotBinary("missing value under returnLastPrediction needs internal-node scores")
+            if len(forms) > 1:
+                raise NotBinary("'none' strategy mixing True and complement second children")
             go_left = False
-        feats[k] = field_index[pa.field]
-        thr[k] = float(pa.value)
-        ops[k] = _OPS[pa.operator]
+        feats[k] = field_index[split_field]
+        thr[k] = split_t
+        ops[k] = split_op
         dleft[k] = go_left
         la, lb = new_node(), new_node()
         lefts[k], rights[k] = la, lb
@@ -288,4 +365,5 @@ def lower_binary_tree(ev: TreeEvaluator, field_index: Dict[str, int]) -> BinaryT
         leaf_value=np.array(leafv, dtype=np.float64),
         leaf_probs=np.stack(leafp) if classification else None,
         depth=max_depth,
+        null_missing=null_missing or forms == {"complement"},
     )

@@ -12,7 +12,7 @@ __device__ __forceinline__ void apply_epilogue(const Epilogue& e, Acc acc, bool 
   int label = 0;
   if (e.mode == EPI_AFFINE) {
     s = apply_link(e.link, fmaf(e.a, acc(0), e.b));
-    ok = ok && (s == s);
+    ok = ok && __builtin_isfinite(s);  // the oracle's regression rule: a non-finite value is no prediction
     if (e.write_probs && probs) probs[row] = s;
   } else if (e.mode == EPI_LOGISTIC2) {
     float p0 = apply_link(e.link, fmaf(e.a, acc(0), e.b));

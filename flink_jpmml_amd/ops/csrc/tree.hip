@@ -15,6 +15,20 @@
 //  * POINTER layout for deeper / wider ensembles: {T, meta, left, right} nodes read from global
 //    memory (L2-resident), divergent walk;
 //  * the per-row epilogue (sum / average / vote / link function / label table) is fused.
+//
+// Missing values: a per-node default-direction bit routes NaN (XGBoost / LightGBM `defaultChild`).
+// PMML `missingValueStrategy="nullPrediction"` (scikit-learn exports) and `none` with complement
+// predicates + `returnNullPrediction` make the tree's prediction null when a visited split sees a
+// missing value: flag bit NI of the perfect record's default-right words (node index NI does not
+// exist), bit 30 of the pointer node's meta. A null tree poisons the row's sum with NaN
+// (-> EmptyScore, the MiningModel `returnMissing`/`continue` rule), or marks the row invalid for
+// multi-slot accumulators.
+//
+// fp8 leaves (variant 2, BASELINE config 5): the two leaves below every last-level node are
+// stored as OCP e4m3 bytes in the upper half of that node's meta word (the lower half is the
+// feature byte offset, < 64 KiB); one global scale is folded into the epilogue. Thresholds and
+// decisions stay fp32 — only the leaf values are quantised. The record shrinks by the whole leaf
+// array (768 -> 512 B at depth 6) and the last level needs no separate leaf read.
 #include "epilogue.h"
 
 namespace {
@@ -32,7 +46,7 @@ struct TreeArgs {
   const float* leaves;          // pointer layout: [n_leaves][P]
   const int* tree_slot;         // general accumulation: slot per tree
   int n_trees, rec_words, chunk_trees, P;
-  int C, trees_per_split, general, variant;  // variant 1: wide (v3) perfect kernel
+  int C, trees_per_split, general, variant;  // variant 1: wide perfect kernel, 2: wide + fp8 leaves
   Epilogue epi;
   float* score;
   uint8_t* valid;
@@ -60,6 +74,14 @@ __device__ __forceinline__ void finish_row(const TreeArgs& a, float acc0, const 
   } else {
     apply_epilogue(a.epi, [&](int) { return acc0; }, row_ok, row, a.n_rows, a.score, a.valid, a.probs);
   }
+}
+
+// Tree-level "null prediction on a missing value" flag of a perfect record (bit NI of the
+// default-right words, which start at word dr_off).
+template <int DEPTH>
+__device__ __forceinline__ bool null_flag(const char* rec, int dr_off) {
+  constexpr int NI = (1 << DEPTH) - 1;
+  return ((reinterpret_cast<const uint32_t*>(rec)[dr_off + (NI >> 5)] >> (NI & 31)) & 1u) != 0u;
 }
 
 // Next-chunk prefetch through registers: the global loads are issued before the traversal of the
@@ -99,7 +121,7 @@ constexpr int PREFETCH_Q = 8;  // uint4 per lane -> up to 32 KiB per chunk
 // Fast path (MISSING=false): one ds_read_b64 node, one ds_read_b32 feature, one v_cmp, index update.
 template <int DEPTH, bool GENERAL, bool MISSING, int ILP>
 __device__ __forceinline__ void traverse_chunk(const TreeArgs& a, const uint32_t* buf, int nt, int t0,
-                                               const char* feat_lane, float& acc, float* accl) {
+                                               const char* feat_lane, float& acc, float* accl, bool& poisoned) {
   constexpr int NI = (1 << DEPTH) - 1;
   constexpr int NL = 1 << DEPTH;
   const int rw = a.rec_words;
@@ -108,10 +130,12 @@ __device__ __forceinline__ void traverse_chunk(const TreeArgs& a, const uint32_t
   int k = 0;
   for (; k + ILP <= nt; k += ILP) {
     uint32_t j[ILP];
+    uint32_t pz[ILP];
     const char* base[ILP];
 #pragma unroll
     for (int i = 0; i < ILP; ++i) {
       j[i] = 1u;
+      pz[i] = 0u;
       base[i] = reinterpret_cast<const char*>(buf + (k + i) * rw);
     }
 #pragma unroll
@@ -124,7 +148,9 @@ __device__ __forceinline__ void traverse_chunk(const TreeArgs& a, const uint32_t
         if (MISSING) {  // branch-free: NaN takes the node's default direction bit
           const uint32_t n = j[i] - 1u;
           const uint32_t w = reinterpret_cast<const uint32_t*>(base[i])[dr_off + (n >> 5)];
-          right |= ((x != x) ? 1u : 0u) & (w >> (n & 31u));
+          const uint32_t isn = (x != x) ? 1u : 0u;
+          right |= isn & (w >> (n & 31u));
+          pz[i] |= isn;
         }
         j[i] = j[i] + j[i] + right;
       }
@@ -132,16 +158,18 @@ __device__ __forceinline__ void traverse_chunk(const TreeArgs& a, const uint32_t
 #pragma unroll
     for (int i = 0; i < ILP; ++i) {
       const float* lv = reinterpret_cast<const float*>(base[i] + NI * 8) - NL * a.P;
+      const bool pzn = MISSING && pz[i] && null_flag<DEPTH>(base[i], dr_off);
       if (GENERAL) {
+        poisoned = poisoned || pzn;
         const int slot = a.tree_slot[t0 + k + i];
         for (int p = 0; p < a.P; ++p) accl[(slot + p) * TB + tid] += lv[j[i] * a.P + p];
       } else {
-        acc += lv[j[i]];
+        acc += pzn ? __builtin_nanf("") : lv[j[i]];
       }
     }
   }
   for (; k < nt; ++k) {
-    uint32_t j = 1u;
+    uint32_t j = 1u, pz = 0u;
     const char* base = reinterpret_cast<const char*>(buf + k * rw);
 #pragma unroll
     for (int d = 0; d < DEPTH; ++d) {
@@ -151,16 +179,20 @@ __device__ __forceinline__ void traverse_chunk(const TreeArgs& a, const uint32_t
       if (MISSING) {
         const uint32_t n = j - 1u;
         const uint32_t w = reinterpret_cast<const uint32_t*>(base)[dr_off + (n >> 5)];
-        right |= ((x != x) ? 1u : 0u) & (w >> (n & 31u));
+        const uint32_t isn = (x != x) ? 1u : 0u;
+        right |= isn & (w >> (n & 31u));
+        pz |= isn;
       }
       j = j + j + right;
     }
     const float* lv = reinterpret_cast<const float*>(base + NI * 8) - NL * a.P;
+    const bool pzn = MISSING && pz && null_flag<DEPTH>(base, dr_off);
     if (GENERAL) {
+      poisoned = poisoned || pzn;
       const int slot = a.tree_slot[t0 + k];
       for (int p = 0; p < a.P; ++p) accl[(slot + p) * TB + tid] += lv[j * a.P + p];
     } else {
-      acc += lv[j];
+      acc += pzn ? __builtin_nanf("") : lv[j];
     }
   }
 }
@@ -223,6 +255,7 @@ __global__ __launch_bounds__(TB, 2) void tree_perfect_kernel(TreeArgs a) {
     for (int c = 0; c < a.C; ++c) accl[c * TB + tid] = 0.f;
   }
   float acc = 0.f;
+  bool poisoned = false;
   const char* feat_lane = reinterpret_cast<const char*>(feat + tid);
 
   int c = 0;
@@ -234,15 +267,15 @@ __global__ __launch_bounds__(TB, 2) void tree_perfect_kernel(TreeArgs a) {
     n16 = (t1 < te) ? (min(a.chunk_trees, te - t1) * rw) >> 2 : 0;
     PF_LOAD(n16 > 0 ? a.blob + (size_t)t1 * rw : a.blob, n16)  // never form an OOB address
     if (missing) {
-      traverse_chunk<DEPTH, GENERAL, true, ILP>(a, cur, nt, t0, feat_lane, acc, accl);
+      traverse_chunk<DEPTH, GENERAL, true, ILP>(a, cur, nt, t0, feat_lane, acc, accl, poisoned);
     } else {
-      traverse_chunk<DEPTH, GENERAL, false, ILP>(a, cur, nt, t0, feat_lane, acc, accl);
+      traverse_chunk<DEPTH, GENERAL, false, ILP>(a, cur, nt, t0, feat_lane, acc, accl, poisoned);
     }
     // `nxt` was last read in the previous iteration, before that iteration's barrier
     PF_STORE(nxt, n16)
     __syncthreads();
   }
-  finish_row(a, acc, accl, split, GENERAL, row, row_ok);
+  finish_row(a, acc, accl, split, GENERAL, row, row_ok && !poisoned);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -273,22 +306,39 @@ __global__ __launch_bounds__(TB, 2) void tree_perfect_kernel(TreeArgs a) {
     if (i0_ + 3 * (T) < (N16)) d4_[i0_ + 3 * (T)] = pq3;                               \
   }
 
-template <int DEPTH, bool MISSING, int ILP, int G>
+__host__ __device__ constexpr int perfect_rec_words(int depth, int P) {
+  return ((2 * ((1 << depth) - 1) + (1 << depth) * P + ((1 << depth) - 1 + 31) / 32) + 3) & ~3;
+}
+// fp8-leaf record: nodes + default-right words only (leaf pairs live in the last-level metas)
+__host__ __device__ constexpr int perfect_rec_words8(int depth) {
+  return ((2 * ((1 << depth) - 1) + ((1 << depth) - 1 + 31) / 32) + 3) & ~3;
+}
+
+// OCP e4m3 leaf pair in bits [31:16] of a last-level node's meta -> (left, right) as fp32
+__device__ __forceinline__ float leaf8_select(uint32_t meta, bool right) {
+  const auto pr = __builtin_amdgcn_cvt_pk_f32_fp8((int)meta, true);
+  return right ? pr[1] : pr[0];
+}
+
+template <int DEPTH, bool MISSING, int ILP, int G, bool LEAF8>
 __device__ __forceinline__ float traverse_chunk_g(const TreeArgs& a, const uint32_t* buf, int nt, int g,
                                                   const char* feat_lane, float acc) {
   constexpr int NI = (1 << DEPTH) - 1;
   constexpr int NL = 1 << DEPTH;
   const int rw = a.rec_words;
-  const int dr_off = 2 * NI + NL;
+  const int dr_off = LEAF8 ? 2 * NI : 2 * NI + NL;
   // my trees: k = g + G*m, m = 0..mt-1
   const int mt = (nt - g + G - 1) / G;
   int m = 0;
   for (; m + ILP <= mt; m += ILP) {
-    uint32_t j[ILP];
+    uint32_t j[ILP], pz[ILP];
+    float lf[ILP];
     const char* base[ILP];
 #pragma unroll
     for (int i = 0; i < ILP; ++i) {
       j[i] = 1u;
+      pz[i] = 0u;
+      lf[i] = 0.f;
       base[i] = reinterpret_cast<const char*>(buf + (g + G * (m + i)) * rw);
     }
 #pragma unroll
@@ -296,39 +346,56 @@ __device__ __forceinline__ float traverse_chunk_g(const TreeArgs& a, const uint3
 #pragma unroll
       for (int i = 0; i < ILP; ++i) {
         const uint2 nd = *reinterpret_cast<const uint2*>(base[i] - 8 + (j[i] << 3));
-        const float x = *reinterpret_cast<const float*>(feat_lane + nd.y);
+        const uint32_t fo = (LEAF8 && d == DEPTH - 1) ? (nd.y & 0xFFFFu) : nd.y;
+        const float x = *reinterpret_cast<const float*>(feat_lane + fo);
         uint32_t right = (x >= __uint_as_float(nd.x)) ? 1u : 0u;
         if (MISSING) {
           const uint32_t n = j[i] - 1u;
           const uint32_t w = reinterpret_cast<const uint32_t*>(base[i])[dr_off + (n >> 5)];
-          right |= ((x != x) ? 1u : 0u) & (w >> (n & 31u));
+          const uint32_t isn = (x != x) ? 1u : 0u;
+          right |= isn & (w >> (n & 31u));
+          pz[i] |= isn;
         }
-        j[i] = j[i] + j[i] + right;
+        if (LEAF8 && d == DEPTH - 1) {
+          lf[i] = leaf8_select(nd.y, right != 0u);
+        } else {
+          j[i] = j[i] + j[i] + right;
+        }
       }
     }
 #pragma unroll
     for (int i = 0; i < ILP; ++i) {
-      const float* lv = reinterpret_cast<const float*>(base[i] + NI * 8) - NL;
-      acc += lv[j[i]];
+      float v = LEAF8 ? lf[i] : (reinterpret_cast<const float*>(base[i] + NI * 8) - NL)[j[i]];
+      if (MISSING && pz[i] && null_flag<DEPTH>(base[i], dr_off)) v = __builtin_nanf("");
+      acc += v;
     }
   }
   for (; m < mt; ++m) {
-    uint32_t j = 1u;
+    uint32_t j = 1u, pz = 0u;
+    float lf = 0.f;
     const char* base = reinterpret_cast<const char*>(buf + (g + G * m) * rw);
 #pragma unroll
     for (int d = 0; d < DEPTH; ++d) {
       const uint2 nd = *reinterpret_cast<const uint2*>(base - 8 + (j << 3));
-      const float x = *reinterpret_cast<const float*>(feat_lane + nd.y);
+      const uint32_t fo = (LEAF8 && d == DEPTH - 1) ? (nd.y & 0xFFFFu) : nd.y;
+      const float x = *reinterpret_cast<const float*>(feat_lane + fo);
       uint32_t right = (x >= __uint_as_float(nd.x)) ? 1u : 0u;
       if (MISSING) {
         const uint32_t n = j - 1u;
         const uint32_t w = reinterpret_cast<const uint32_t*>(base)[dr_off + (n >> 5)];
-        right |= ((x != x) ? 1u : 0u) & (w >> (n & 31u));
+        const uint32_t isn = (x != x) ? 1u : 0u;
+        right |= isn & (w >> (n & 31u));
+        pz |= isn;
       }
-      j = j + j + right;
+      if (LEAF8 && d == DEPTH - 1) {
+        lf = leaf8_select(nd.y, right != 0u);
+      } else {
+        j = j + j + right;
+      }
     }
-    const float* lv = reinterpret_cast<const float*>(base + NI * 8) - NL;
-    acc += lv[j];
+    float v = LEAF8 ? lf : (reinterpret_cast<const float*>(base + NI * 8) - NL)[j];
+    if (MISSING && pz && null_flag<DEPTH>(base, dr_off)) v = __builtin_nanf("");
+    acc += v;
   }
   return acc;
 }
@@ -339,10 +406,11 @@ __device__ __forceinline__ float traverse_chunk_g(const TreeArgs& a, const uint3
 // compiled to ~7.5 as hipcc re-expanded `j = 2j + r` into shifted bit sums).
 //  * u = LDS address of the current node of tree i minus i*TS (TS = compile-time tree stride of a
 //    tree group, folded into the ds_read immediate offset); children: u' = 2u + (8 - b0) + 8r.
-//  * last level: the two leaves under a node are adjacent, so the leaf PAIR (one conflict-free
-//    ds_read_b64 at u + C, C folded into the offset) is fetched together with the feature and the
-//    final compare only selects between them — one dependent LDS round trip less per tree, and no
-//    2-way bank conflicts of scattered ds_read_b32 leaf reads.
+//  * last level, fp32 leaves: the two leaves under a node are adjacent, so the leaf PAIR (one
+//    conflict-free ds_read_b64 at u + C, C folded into the offset) is fetched together with the
+//    feature and the final compare only selects between them — one dependent LDS round trip less
+//    per tree, and no 2-way bank conflicts of scattered ds_read_b32 leaf reads;
+//  * last level, fp8 leaves: the pair is already in the node's meta word (no leaf read at all).
 // `__asm__("" : "+v"(...))` pins values in VGPRs so the compiler cannot re-derive them.
 typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) const u32x2_t lds_u2_t;
@@ -356,16 +424,12 @@ __device__ __forceinline__ uint2 lds_ld2(uint32_t a) {
 }
 __device__ __forceinline__ float lds_ldf(uint32_t a) { return *(lds_f_t*)(uintptr_t)a; }
 
-__host__ __device__ constexpr int perfect_rec_words(int depth, int P) {
-  return ((2 * ((1 << depth) - 1) + (1 << depth) * P + ((1 << depth) - 1 + 31) / 32) + 3) & ~3;
-}
-
-template <int DEPTH, int ILP, int G>
+template <int DEPTH, int ILP, int G, bool LEAF8>
 __device__ __forceinline__ float traverse_fast_g(const uint32_t* buf, int nt, int g, uint32_t feat_lane,
                                                  float acc) {
   constexpr int NI = (1 << DEPTH) - 1;
   constexpr int NL = 1 << DEPTH;
-  constexpr uint32_t RB = 4u * perfect_rec_words(DEPTH, 1);  // record bytes
+  constexpr uint32_t RB = 4u * (LEAF8 ? perfect_rec_words8(DEPTH) : perfect_rec_words(DEPTH, 1));  // record bytes
   constexpr uint32_t TS = G * RB;                            // tree stride within a group
   constexpr uint32_t C = 8u + 8u * NI - 4u * NL;             // last-level node -> its leaf pair
   const uint32_t lds0 = lds_addr(buf);
@@ -394,12 +458,18 @@ __device__ __forceinline__ float traverse_fast_g(const uint32_t* buf, int nt, in
     }
 #pragma unroll
     for (int i = 0; i < ILP; ++i) {
-      uint32_t ul = u[i] + C;
-      __asm__ volatile("" : "+v"(ul));  // keep the pair read out of a ds_read2_b64 with the node
-      const uint2 nd = lds_ld2(u[i] + i * TS);
-      const uint2 lv = lds_ld2(ul + i * TS);
-      const float x = lds_ldf(feat_lane + nd.y);
-      acc += (x >= __uint_as_float(nd.x)) ? __uint_as_float(lv.y) : __uint_as_float(lv.x);
+      if (LEAF8) {
+        const uint2 nd = lds_ld2(u[i] + i * TS);
+        const float x = lds_ldf(feat_lane + (nd.y & 0xFFFFu));
+        acc += leaf8_select(nd.y, x >= __uint_as_float(nd.x));
+      } else {
+        uint32_t ul = u[i] + C;
+        __asm__ volatile("" : "+v"(ul));  // keep the pair read out of a ds_read2_b64 with the node
+        const uint2 nd = lds_ld2(u[i] + i * TS);
+        const uint2 lv = lds_ld2(ul + i * TS);
+        const float x = lds_ldf(feat_lane + nd.y);
+        acc += (x >= __uint_as_float(nd.x)) ? __uint_as_float(lv.y) : __uint_as_float(lv.x);
+      }
     }
   }
   for (; m < mt; ++m) {
@@ -412,14 +482,19 @@ __device__ __forceinline__ float traverse_fast_g(const uint32_t* buf, int nt, in
       u = 2u * u + 8u - b0 + ((x >= __uint_as_float(nd.x)) ? 8u : 0u);
     }
     const uint2 nd = lds_ld2(u);
-    const uint2 lv = lds_ld2(u + C);
-    const float x = lds_ldf(feat_lane + nd.y);
-    acc += (x >= __uint_as_float(nd.x)) ? __uint_as_float(lv.y) : __uint_as_float(lv.x);
+    if (LEAF8) {
+      const float x = lds_ldf(feat_lane + (nd.y & 0xFFFFu));
+      acc += leaf8_select(nd.y, x >= __uint_as_float(nd.x));
+    } else {
+      const uint2 lv = lds_ld2(u + C);
+      const float x = lds_ldf(feat_lane + nd.y);
+      acc += (x >= __uint_as_float(nd.x)) ? __uint_as_float(lv.y) : __uint_as_float(lv.x);
+    }
   }
   return acc;
 }
 
-template <int DEPTH, int ILP, int G>
+template <int DEPTH, int ILP, int G, bool LEAF8>
 __global__ __launch_bounds__(TB * G, 1) void tree_perfect_wide_kernel(TreeArgs a) {
   constexpr int T = TB * G;
   extern __shared__ __align__(16) uint32_t smem[];
@@ -484,9 +559,9 @@ __global__ __launch_bounds__(TB * G, 1) void tree_perfect_wide_kernel(TreeArgs a
     n16 = (t1 < te) ? (min(a.chunk_trees, te - t1) * rw) >> 2 : 0;
     PF4_LOAD(n16 > 0 ? a.blob + (size_t)t1 * rw : a.blob, n16, T)
     if (missing) {
-      acc = traverse_chunk_g<DEPTH, true, ILP, G>(a, cur, nt, g, feat_lane, acc);
+      acc = traverse_chunk_g<DEPTH, true, ILP, G, LEAF8>(a, cur, nt, g, feat_lane, acc);
     } else {
-      acc = traverse_fast_g<DEPTH, ILP, G>(cur, nt, g, lds_addr(feat + r_local), acc);
+      acc = traverse_fast_g<DEPTH, ILP, G, LEAF8>(cur, nt, g, lds_addr(feat + r_local), acc);
     }
     PF4_STORE(nxt, n16, T)
     __syncthreads();
@@ -514,6 +589,8 @@ __global__ __launch_bounds__(TB * G, 1) void tree_perfect_wide_kernel(TreeArgs a
 }
 
 // Pointer layout: nodes uint4 {T bits, meta, left, right}; child < 0 => leaf ~child.
+// meta: feature byte offset (or index when features stay in global memory) | bit 30 null-on-
+// missing | bit 31 default right.
 template <bool GENERAL, bool FEAT_LDS>
 __global__ __launch_bounds__(TB, 2) void tree_pointer_kernel(TreeArgs a) {
   extern __shared__ __align__(16) uint32_t smem[];
@@ -548,9 +625,11 @@ __global__ __launch_bounds__(TB, 2) void tree_pointer_kernel(TreeArgs a) {
     for (int c = 0; c < a.C; ++c) accl[c * TB + tid] = 0.f;
   }
   float acc = 0.f;
+  bool poisoned = false;
   const char* feat_lane = reinterpret_cast<const char*>(feat + tid);
   for (int t = tb; t < te; ++t) {
     int code = a.roots[t];
+    bool pz = false;
     while (code >= 0) {
       const uint4 nd = nodes[code];
       float x;
@@ -561,8 +640,18 @@ __global__ __launch_bounds__(TB, 2) void tree_pointer_kernel(TreeArgs a) {
         x = xrow[f];
         if (a.prep) { bool b = false; x = prep_value(x, a.prep[f], &b); }
       }
-      bool right = (x >= __uint_as_float(nd.x)) || ((x != x) && (nd.y >> 31));
+      const bool isn = (x != x);
+      if (isn && ((nd.y >> 30) & 1u)) {
+        pz = true;
+        break;
+      }
+      bool right = (x >= __uint_as_float(nd.x)) || (isn && (nd.y >> 31));
       code = right ? (int)nd.w : (int)nd.z;
+    }
+    if (pz) {
+      if (GENERAL) poisoned = true;
+      else acc += __builtin_nanf("");
+      continue;
     }
     const int leaf = ~code;
     if (GENERAL) {
@@ -572,7 +661,7 @@ __global__ __launch_bounds__(TB, 2) void tree_pointer_kernel(TreeArgs a) {
       acc += a.leaves[leaf];
     }
   }
-  finish_row(a, acc, accl, split, GENERAL, row, row_ok);
+  finish_row(a, acc, accl, split, GENERAL, row, row_ok && !poisoned);
 }
 
 // Split-mode reduction: partial[splits][C+1][n_rows] -> epilogue.
@@ -607,15 +696,24 @@ constexpr int WIDE_G = 4;
 template <int D>
 int launch_perfect(hipStream_t st, const TreeArgs& a, dim3 grid, size_t lds) {
   int err = 0;
-  if (!a.general && a.variant == 1) {
+  if (!a.general && (a.variant == 1 || a.variant == 2)) {
+    const bool leaf8 = a.variant == 2;
     const size_t lds_w = lds + (size_t)WIDE_G * TB * 4;
     if (lds_w > 160 * 1024) return -5;
     if ((size_t)a.chunk_trees * a.rec_words > (size_t)TB * WIDE_G * 4 * 4) return -9;
-    if (a.rec_words != perfect_rec_words(D, 1) || a.P != 1) return -10;
-    err = prepare_launch(tree_perfect_wide_kernel<D, 8, WIDE_G>, lds_w);
-    if (!err) hipLaunchKernelGGL((tree_perfect_wide_kernel<D, 8, WIDE_G>), grid, dim3(TB * WIDE_G), lds_w, st, a);
+    if (a.P != 1 || a.rec_words != (leaf8 ? perfect_rec_words8(D) : perfect_rec_words(D, 1))) return -10;
+    if (leaf8) {
+      err = prepare_launch(tree_perfect_wide_kernel<D, 8, WIDE_G, true>, lds_w);
+      if (!err)
+        hipLaunchKernelGGL((tree_perfect_wide_kernel<D, 8, WIDE_G, true>), grid, dim3(TB * WIDE_G), lds_w, st, a);
+    } else {
+      err = prepare_launch(tree_perfect_wide_kernel<D, 8, WIDE_G, false>, lds_w);
+      if (!err)
+        hipLaunchKernelGGL((tree_perfect_wide_kernel<D, 8, WIDE_G, false>), grid, dim3(TB * WIDE_G), lds_w, st, a);
+    }
     return err;
   }
+  if (a.variant == 2) return -10;  // fp8 leaves only on the wide (single-accumulator) kernel
   if (a.general) {
     err = prepare_launch(tree_perfect_kernel<D, true, 4>, lds);
     if (!err) hipLaunchKernelGGL((tree_perfect_kernel<D, true, 4>), grid, dim3(TB), lds, st, a);
@@ -647,7 +745,7 @@ PMML_API int pmml_tree_launch(hipStream_t stream, const TreeArgs* args, int layo
   const size_t acc_lds = a.general ? (size_t)a.C * TB * 4 : 0;
   if (layout == 0) {
     if (a.n_feat > 64) return -4;
-    if (a.variant != 1 && (size_t)a.chunk_trees * a.rec_words > (size_t)TB * 4 * PREFETCH_Q) return -9;
+    if (a.variant == 0 && (size_t)a.chunk_trees * a.rec_words > (size_t)TB * 4 * PREFETCH_Q) return -9;
     const size_t lds = (size_t)a.n_feat * TB * 4 + 2 * (size_t)a.chunk_trees * a.rec_words * 4 + (TB + 4) * 4 + acc_lds;
     if (lds > 160 * 1024) return -5;
     switch (depth) {
@@ -664,6 +762,7 @@ PMML_API int pmml_tree_launch(hipStream_t stream, const TreeArgs* args, int layo
       default: return -6;
     }
   } else {
+    if (a.variant == 2) return -10;
     const bool feat_lds = a.n_feat <= 64;
     const size_t lds = (feat_lds ? (size_t)a.n_feat * TB * 4 : 0) + TB * 4 + acc_lds;
     if (a.general) {

@@ -322,12 +322,16 @@ class FieldLayout:
 
 
 def plan_field_layout(compiled, allow_alias: bool = True) -> FieldLayout:
+    from ..models.tree import membership_fields
+
     active = list(compiled.active_fields)
     index = {f: i for i, f in enumerate(active)}
     defs = collect_derived(compiled)
+    members = membership_fields(compiled.model)  # 0/1 columns of categorical tree splits
+    defs.update(members)
     if not defs:
         return FieldLayout(active, index, None)
-    refs = referenced_fields(compiled.model)
+    refs = referenced_fields(compiled.model) + list(members)
     needed = [r for r in refs if r in defs and r not in index]
     if not needed:
         return FieldLayout(active, index, None)

@@ -498,6 +498,7 @@ def _regression_ensemble(ev, field_index) -> Tuple[List[BinaryTree], List[float]
             w = seg.weight if method == "weightedAverage" else 1.0
             trees.extend(st)
             weights.extend([x * w * sa for x in sw])
+        _check_null_trees(mm, trees)
         if method == "average":
             scale = 1.0 / max(1, len(mm.segments))
         elif method == "weightedAverage":
@@ -507,6 +508,13 @@ def _regression_ensemble(ev, field_index) -> Tuple[List[BinaryTree], List[float]
         a, b = _target_affine(ev)
         return trees, weights, a * scale, b
     raise NotLowerable(f"{type(ev).__name__} is not a regression tree ensemble")
+
+
+def _check_null_trees(mm: ir.MiningModel, trees: List[BinaryTree]) -> None:
+    """A null tree poisons the row (the ``returnMissing``/``continue`` rule); ``skipSegment``
+    would need it dropped from the aggregate instead."""
+    if mm.missing_prediction_treatment == "skipSegment" and any(t.null_missing for t in trees):
+        raise NotLowerable("skipSegment over null-on-missing trees is host-only")
 
 
 def ensemble_spec(compiled) -> EnsembleSpec:
@@ -554,6 +562,7 @@ def _classification_spec(ev: MiningEvaluator, field_index) -> EnsembleSpec:
         t.leaf_probs = probs
         trees.append(t)
         weights.append(seg.weight if method.startswith("weighted") else 1.0)
+    _check_null_trees(mm, trees)
     return EnsembleSpec(trees, weights, C, C, dict(mode=EPI_ARGMAX, C=C, a=1.0 / sum(weights)), cats)
 
 
@@ -640,12 +649,55 @@ def _perfect_pack(trees: List[BinaryTree], weights: List[float], P: int, D: int)
                 has_dr = True
             stack.append((left_child, 2 * p + 1, d + 1))
             stack.append((right_child, 2 * p + 2, d + 1))
+        if t.null_missing:
+            dr_bits[NI] = 1  # tree-level null-on-missing flag (node index NI does not exist)
         blob[ti, 0: 2 * NI: 2] = nodes_T.view(np.uint32)
         blob[ti, 1: 2 * NI: 2] = nodes_meta
         blob[ti, 2 * NI: 2 * NI + NL * P] = leaves.reshape(-1).view(np.uint32)
         words = (dr_bits.reshape(ndr, 32) << np.arange(32, dtype=np.uint32)[None, :]).sum(axis=1, dtype=np.uint64)
         blob[ti, 2 * NI + NL * P: 2 * NI + NL * P + ndr] = words.astype(np.uint32)
     return blob, rec, has_dr
+
+
+FP8_MAX = 448.0  # largest finite OCP e4m3fn value
+
+
+def quantize_fp8(values: np.ndarray, scale: float) -> np.ndarray:
+    """fp32 -> OCP e4m3fn bytes of ``values / scale`` (round to nearest even, saturating)."""
+    import torch
+
+    v = np.clip(np.asarray(values, np.float64) / scale, -FP8_MAX, FP8_MAX).astype(np.float32)
+    return torch.from_numpy(v).to(torch.float8_e4m3fn).view(torch.uint8).numpy()
+
+
+def dequantize_fp8(q: np.ndarray) -> np.ndarray:
+    import torch
+
+    return torch.from_numpy(np.ascontiguousarray(q, dtype=np.uint8)).view(torch.float8_e4m3fn).float().numpy()
+
+
+def _leaf8_pack(blob: np.ndarray, D: int) -> Tuple[np.ndarray, int, float]:
+    """Re-pack a P=1 PERFECT blob with fp8 leaves: the two e4m3 leaves under every last-level node
+    go into bits [31:16] of that node's meta (left in [23:16], right in [31:24]); one global
+    scale (max |leaf| -> 448) is returned for the epilogue. Record: nodes + default-right words."""
+    NI, NL = (1 << D) - 1, 1 << D
+    ndr = (NI + 31) // 32
+    leaves = blob[:, 2 * NI: 2 * NI + NL].view(np.float32)
+    amax = float(np.max(np.abs(leaves))) if leaves.size else 0.0
+    scale = amax / FP8_MAX if amax > 0 else 1.0
+    q = quantize_fp8(leaves, scale).astype(np.uint32)  # [trees, NL]
+    rec = (2 * NI + ndr + 3) & ~3
+    out = np.zeros((blob.shape[0], rec), dtype=np.uint32)
+    out[:, : 2 * NI] = blob[:, : 2 * NI]
+    out[:, 2 * NI: 2 * NI + ndr] = blob[:, 2 * NI + NL: 2 * NI + NL + ndr]
+    first_last = NL // 2 - 1  # level-order index of the first last-level node
+    for p in range(first_last, NI):
+        left, right = 2 * p + 1 - NI, 2 * p + 2 - NI
+        meta = out[:, 2 * p + 1]
+        if np.any(meta >> 16):
+            raise NotLowerable("feature byte offset does not fit the fp8 leaf-pair meta")
+        out[:, 2 * p + 1] = meta | (q[:, left] << 16) | (q[:, right] << 24)
+    return out, rec, scale
 
 
 def _pointer_pack(trees: List[BinaryTree], weights: List[float], P: int):
@@ -682,7 +734,7 @@ def _pointer_pack(trees: List[BinaryTree], weights: List[float], P: int):
             else:
                 lc, rc, dr = first, second, not dflt_first
             f = int(t.feature[k])
-            meta = (f * TB * 4 if f < 64 else f) | ((1 << 31) if dr else 0)
+            meta = (f * TB * 4 if f < 64 else f) | ((1 << 31) if dr else 0) | ((1 << 30) if t.null_missing else 0)
             has_dr = has_dr or dr
             nodes[base_map[k]] = (int(np.float32(T).view(np.uint32)), meta, base_map[lc], base_map[rc])
         roots.append(base_map[0])
@@ -702,8 +754,10 @@ class TreePlan(DevicePlan):
     WIDE_G = 4  # tree groups of the wide kernel (mirrors csrc)
 
     def __init__(self, compiled, device, layout: str = "auto", lds_budget: int = 80 * 1024, splits: int = 0,
-                 variant: str = "auto"):
+                 variant: str = "auto", precision: str = "fp32"):
         super().__init__(compiled, device)
+        if precision not in ("fp32", "fp8"):
+            raise ValueError("tree leaf precision must be fp32 or fp8")
         spec = ensemble_spec(compiled)
         self.spec = spec
         self.epi_args = dict(spec.epi)
@@ -720,11 +774,18 @@ class TreePlan(DevicePlan):
         self.general = 1 if spec.P > 1 else 0
         if self.layout == "perfect":
             blob, rec, has_dr = _perfect_pack(spec.trees, spec.weights, spec.P, depth)
-            self.rec_words = rec
             if variant == "auto":
                 variant = "narrow" if self.general else "wide"
             self.variant = 1 if variant == "wide" else 0
-            if self.variant == 1:
+            if precision == "fp8":
+                # e4m3 leaves in the last-level metas, global scale folded into the epilogue
+                if self.general or self.variant != 1:
+                    raise NotLowerable("fp8 leaves need the single-accumulator wide kernel (P = 1)")
+                blob, rec, scale = _leaf8_pack(blob, depth)
+                self.epi_args["a"] = self.epi_args.get("a", 1.0) * scale
+                self.variant = 2
+            self.rec_words = rec
+            if self.variant in (1, 2):
                 # one 1024-thread workgroup per CU: features + two chunk buffers + [G][256] partials
                 fixed = F * TB * 4 + (TB + 4) * 4 + self.WIDE_G * TB * 4
                 budget = 156 * 1024 - fixed
@@ -739,6 +800,8 @@ class TreePlan(DevicePlan):
             self.blob = self._t(blob.reshape(-1).view(np.int32))
             self.roots = self.leaves = None
         else:
+            if precision == "fp8":
+                raise NotLowerable("fp8 leaves need the PERFECT layout")
             nodes, leaves, roots, has_dr = _pointer_pack(spec.trees, spec.weights, spec.P)
             self.rec_words = 0
             self.chunk_trees = 0

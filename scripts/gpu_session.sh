@@ -23,10 +23,12 @@ run() {  # name timeout cmd...
   return 0
 }
 
-run build 300 python -c "import __graft_entry__ as g; g.build()"
+if python -c "from flink_jpmml_amd.ops import _lib; import sys; sys.exit(0 if _lib.is_stale() else 1)"; then
+  run build 600 python -c "import __graft_entry__ as g; g.build()"
+fi
 for s in $STEPS; do
   case $s in
-    tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider ;;
+    tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -v -x -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py --steps "${BENCH_STEPS:-20}" --warmup 3 ;;
     prof)

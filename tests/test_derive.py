@@ -159,3 +159,61 @@ def test_unsupported_expressions_stay_on_host(bad):
     c = CompiledPmml.from_string(doc)
     with pytest.raises(NotLowerable):
         plan_field_layout(c)
+
+
+def categorical_tree_doc(strategy: str = "defaultChild") -> str:
+    """LightGBM / R style categorical splits: isIn / isNotIn sets and == / != on a string field."""
+    return (f'<PMML version="4.4" xmlns="{NS}"><DataDictionary>'
+            '<DataField name="x" optype="continuous" dataType="double"/>'
+            '<DataField name="cat" optype="categorical" dataType="string">'
+            + "".join(f'<Value value="{v}"/>' for v in "abcdef") +
+            '</DataField><DataField name="y" optype="continuous" dataType="double"/></DataDictionary>'
+            f'<TreeModel functionName="regression" missingValueStrategy="{strategy}" splitCharacteristic="binarySplit">'
+            '<MiningSchema><MiningField name="y" usageType="target"/><MiningField name="x"/><MiningField name="cat"/>'
+            '</MiningSchema>'
+            '<Node id="0" defaultChild="2"><True/>'
+            ' <Node id="1" defaultChild="3"><SimpleSetPredicate field="cat" booleanOperator="isIn">'
+            '<Array type="string" n="3">a c "e"</Array></SimpleSetPredicate>'
+            '  <Node id="3" score="1.0"><SimplePredicate field="x" operator="lessThan" value="0.25"/></Node>'
+            '  <Node id="4" defaultChild="5"><SimplePredicate field="x" operator="greaterOrEqual" value="0.25"/>'
+            '   <Node id="5" score="2.0"><SimplePredicate field="cat" operator="equal" value="a"/></Node>'
+            '   <Node id="6" score="3.0"><SimplePredicate field="cat" operator="notEqual" value="a"/></Node>'
+            '  </Node>'
+            ' </Node>'
+            ' <Node id="2" defaultChild="7"><SimpleSetPredicate field="cat" booleanOperator="isNotIn">'
+            '<Array type="string" n="3">a c "e"</Array></SimpleSetPredicate>'
+            '  <Node id="7" score="4.0"><SimpleSetPredicate field="cat" booleanOperator="isNotIn">'
+            '<Array type="string" n="1">f</Array></SimpleSetPredicate></Node>'
+            '  <Node id="8" score="5.0"><SimpleSetPredicate field="cat" booleanOperator="isIn">'
+            '<Array type="string" n="1">f</Array></SimpleSetPredicate></Node>'
+            ' </Node>'
+            '</Node></TreeModel></PMML>')
+
+
+def cat_inputs(n=3000, seed=0):
+    rng = np.random.default_rng(seed)
+    X = np.stack([rng.normal(0, 1, n), rng.integers(0, 6, n).astype(float)], axis=1)
+    X[rng.random((n, 2)) < 0.08] = np.nan
+    return X
+
+
+@pytest.mark.parametrize("strategy", ["defaultChild", "nullPrediction"])
+def test_categorical_splits_lower_to_membership_columns(strategy):
+    from flink_jpmml_amd.runtime.derive import FieldView
+
+    from test_lowering import _scores, emulate_perfect
+
+    c = CompiledPmml.from_string(categorical_tree_doc(strategy))
+    layout = plan_field_layout(c)
+    prog = layout.program
+    members = [n for n in layout.columns if n.startswith("__in__(")]
+    assert sorted(members) == ["__in__(cat|a)", "__in__(cat|a|c|e)", "__in__(cat|f)"]
+    X = cat_inputs()
+    P, ok = c.prepare(X)
+    Xd = emulate(prog, P)
+    view = FieldView(c, layout, prepared=True)
+    spec, acc = emulate_perfect(view, Xd)
+    ref, vref = c.score_matrix_oracle(X)
+    out = _scores(spec, acc)
+    assert (np.isfinite(out) == vref).all()
+    assert (out[vref] == ref[vref]).all()

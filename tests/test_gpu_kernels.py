@@ -334,3 +334,59 @@ def test_float_cast_gbdt_aliases_on_gpu(gpu):
     s, v = _gpu_np(plan, X)
     ref, vref = c.score_matrix_oracle(X)
     assert (v == vref).all() and np.max(np.abs(s - ref)) < 2e-5
+
+
+# ------------------------------------------------------------------ null-on-missing trees, fp8 leaves
+
+
+@pytest.mark.parametrize("kind,layout", [("regression", "perfect"), ("regression", "pointer"), ("rf", "perfect"),
+                                         ("rf", "pointer")])
+def test_null_prediction_trees_on_gpu(gpu, kind, layout):
+    from flink_jpmml_amd.bench.synth import gbdt_pmml, random_forest_pmml, stream_matrix
+    from flink_jpmml_amd.runtime.compiled import CompiledPmml
+
+    if kind == "rf":
+        txt = random_forest_pmml(n_trees=40, depth=6, n_features=10, n_classes=3, seed=4,
+                                 missing_strategy="nullPrediction")
+    else:
+        txt = gbdt_pmml(n_trees=80, depth=5, n_features=10, seed=3, missing_strategy="nullPrediction")
+    c = CompiledPmml.from_string(txt)
+    X = stream_matrix(20_000, 10, seed=6, missing_rate=0.01)
+    ref, vref = c.score_matrix_oracle(X)
+    assert 0 < vref.sum() < len(X)
+    s, v = _gpu_np(c.plan(gpu, layout=layout), X)
+    assert (v == vref).all()
+    if kind == "rf":
+        assert (s[v] == ref[v]).all()
+    else:
+        assert np.max(np.abs(s[v] - ref[v])) < 2e-5
+
+
+def test_fp8_leaf_chain_on_gpu(gpu):
+    """BASELINE config 5: GBDT chain + logistic calibrator with e4m3 leaves. Decisions are exact;
+    the tolerance is the leaf quantisation (3 mantissa bits, one global scale)."""
+    from test_lowering import emulate_leaf8
+
+    from flink_jpmml_amd.bench.synth import gbdt_pmml, stream_matrix
+    from flink_jpmml_amd.runtime.compiled import CompiledPmml
+
+    c = CompiledPmml.from_string(gbdt_pmml(n_trees=300, depth=6, n_features=24, seed=8, objective="binary"))
+    p8 = c.plan(gpu, precision="fp8")
+    assert p8.variant == 2 and p8.rec_words < c.plan(gpu).rec_words
+    X = stream_matrix(30_000, 24, seed=1)
+    probs = torch_probs = None
+    import torch
+
+    Xt = torch.from_numpy(X).to(gpu)
+    s8, v8 = p8.alloc_outputs(len(X))
+    probs = torch.empty((len(X), 2), device=gpu)
+    p8.launch(Xt, s8, v8, probs=probs)
+    torch.cuda.synchronize()
+    spec, acc8, _ = emulate_leaf8(c, X)
+    e = spec.epi
+    p_emul = 1.0 / (1.0 + np.exp(-(e["a"] * acc8.astype(np.float64) + e["b"])))
+    torch_probs = probs[:, 0].cpu().numpy()
+    assert np.max(np.abs(torch_probs - p_emul)) < 1e-4  # kernel == fp8 emulation (fp32 sum order)
+    ref, vref = c.score_matrix_oracle(X)
+    assert v8.bool().all().item() and vref.all()
+    assert (s8.cpu().numpy() == ref).mean() > 0.97  # labels vs the fp64 oracle on fp32 leaves

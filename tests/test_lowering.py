@@ -27,13 +27,16 @@ def emulate_perfect(c, X):
         leaves = blob[ti, 2 * NI:2 * NI + NL * P].view(np.float32).reshape(NL, P)
         drw = blob[ti, 2 * NI + NL * P: 2 * NI + NL * P + (NI + 31) // 32]
         j = np.ones(n, np.int64)
+        pz = np.zeros(n, dtype=bool)
         for _ in range(D):
             f = meta[j - 1] // (TB * 4)
             x = Xf[np.arange(n), f]
             dr = (drw[(j - 1) >> 5] >> ((j - 1) & 31)) & 1
             right = (x >= T[j - 1]) | (np.isnan(x) & (dr == 1))
+            pz |= np.isnan(x)
             j = 2 * j + right
-        acc += leaves[j - NL]
+        null_tree = (drw[NI >> 5] >> (NI & 31)) & 1  # tree-level null-on-missing flag
+        acc += np.where((pz & (null_tree == 1))[:, None], np.float32(np.nan), leaves[j - NL])
     return spec, acc
 
 
@@ -57,14 +60,16 @@ def emulate_pointer(c, X):
 
 
 def _scores(spec, acc):
+    """Epilogue emulation; rows whose accumulator is NaN (a null tree) score NaN (EmptyScore)."""
     e = spec.epi
+    bad = np.isnan(acc).any(axis=1)
     if e["mode"] == 0:
-        return e["a"] * acc[:, 0] + e["b"]
+        return np.where(bad, np.nan, e["a"] * acc[:, 0] + e["b"])
     tab = np.array([float(x) for x in spec.labels])
     if e["mode"] == 1:
         p0 = 1.0 / (1.0 + np.exp(-(e["a"] * acc[:, 0] + e["b"])))
-        return tab[np.where(p0 >= 0.5, 0, 1)]
-    return tab[np.argmax(acc, axis=1)]
+        return np.where(bad, np.nan, tab[np.where(p0 >= 0.5, 0, 1)])
+    return np.where(bad, np.nan, tab[np.argmax(np.nan_to_num(acc), axis=1)])
 
 
 @pytest.mark.parametrize("kind", ["regression", "binary", "rf"])
@@ -207,3 +212,74 @@ def test_mlp_fragment_packing_matches_dense_forward(precision):
         H = activate(act, H @ W + b)
     out = emulate_mlp_wave(layers, X, precision)
     assert np.allclose(out[:3].T, H, atol=1e-9)
+
+
+@pytest.mark.parametrize("kind", ["regression", "rf"])
+def test_null_prediction_trees_poison_rows(kind):
+    """sklearn-style ``nullPrediction`` trees: a missing value at a visited split voids the tree,
+    and with it the ensemble's prediction (MiningModel ``continue`` rule) -> EmptyScore."""
+    if kind == "rf":
+        txt = random_forest_pmml(n_trees=12, depth=5, n_features=8, n_classes=3, seed=4,
+                                 missing_strategy="nullPrediction")
+    else:
+        txt = gbdt_pmml(n_trees=25, depth=4, n_features=8, seed=3, missing_strategy="nullPrediction")
+    c = CompiledPmml.from_string(txt)
+    assert all(t.null_missing for t in ensemble_spec(c).trees)
+    X = stream_matrix(3000, 8, seed=6, missing_rate=0.03)
+    ref, vref = c.score_matrix_oracle(X)
+    assert 0 < vref.sum() < len(X)  # both outcomes occur
+    spec, acc = emulate_perfect(c, X)
+    out = _scores(spec, acc)
+    assert (np.isfinite(out) == vref).all()
+    if kind == "rf":
+        assert (out[vref] == ref[vref]).all()
+    else:
+        assert np.max(np.abs(out[vref] - ref[vref])) < 1e-5
+    # pointer layout: per-node null bit (meta bit 30)
+    nodes, _, _, _ = _pointer_pack(spec.trees, spec.weights, spec.P)
+    internal = nodes[:, 2].astype(np.int64) != nodes[:, 3].astype(np.int64)
+    assert ((nodes[internal, 1] >> 30) & 1).all()
+
+
+def emulate_leaf8(c, X):
+    """fp8-leaf wide-kernel format: the e4m3 leaf pair sits in bits [31:16] of each last-level
+    node's meta; the feature offset is the low half."""
+    from flink_jpmml_amd.runtime.plans import _leaf8_pack, dequantize_fp8
+
+    spec = ensemble_spec(c)
+    D = max(t.depth for t in spec.trees)
+    blob, _, _ = _perfect_pack(spec.trees, spec.weights, 1, D)
+    blob8, rec8, scale = _leaf8_pack(blob, D)
+    NI = (1 << D) - 1
+    assert rec8 == ((2 * NI + (NI + 31) // 32 + 3) & ~3) and rec8 % 4 == 0
+    Xf = X.astype(np.float32)
+    rows = np.arange(len(X))
+    acc = np.zeros(len(X), np.float32)
+    for t in range(blob8.shape[0]):
+        T = blob8[t, 0:2 * NI:2].view(np.float32)
+        meta = blob8[t, 1:2 * NI:2]
+        j = np.ones(len(X), np.int64)
+        for d in range(D):
+            m = meta[j - 1]
+            x = Xf[rows, (m & 0xFFFF) // (TB * 4)]
+            right = x >= T[j - 1]
+            if d == D - 1:
+                byte = np.where(right, m >> 24, (m >> 16) & 0xFF).astype(np.uint8)
+                acc += dequantize_fp8(byte)
+            else:
+                j = 2 * j + right
+    return spec, acc * np.float32(scale), blob
+
+
+@pytest.mark.parametrize("depth", [1, 4, 6])
+def test_fp8_leaf_packing(depth):
+    c = CompiledPmml.from_string(gbdt_pmml(n_trees=60, depth=depth, n_features=9, seed=depth, objective="binary"))
+    X = stream_matrix(2000, 9, seed=2)
+    spec, acc8, _ = emulate_leaf8(c, X)
+    _, acc32 = emulate_perfect(c, X)
+    # decisions are fp32-exact; only leaf values are quantised (e4m3: 3 mantissa bits, |rel err| <= 1/16)
+    leaf_max = max(float(np.max(np.abs(t.leaf_value[t.feature < 0]))) for t in spec.trees)
+    assert np.max(np.abs(acc8 - acc32[:, 0])) <= 60 * leaf_max / 16 + 1e-6
+    ref, _ = c.score_matrix_oracle(X)
+    agree = (_scores(spec, acc8[:, None]) == ref).mean()
+    assert agree > 0.97
