@@ -1,0 +1,157 @@
+"""Native host runtime pieces (C++17, built with g++ into ``_ingest.so``, loaded with ctypes).
+
+:class:`RecordParser` turns delimited text records into the engine's ``[rows, active fields]``
+fp32 matrix on all cores (``csrc/ingest.cpp``), writing straight into a caller-provided (pinned)
+buffer — the host-ingest stage in front of the H2D copy. Categorical tokens are encoded with the
+model's PMML vocabularies (the same codes the float64 oracle uses), missing tokens become NaN.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+import threading
+from typing import Iterable, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SRC = os.path.join(HERE, "csrc", "ingest.cpp")
+LIB_PATH = os.path.join(HERE, "_ingest.so")
+
+_lib: Optional[ctypes.CDLL] = None
+_lock = threading.Lock()
+
+
+class NativeBuildError(RuntimeError):
+    pass
+
+
+def build(force: bool = False) -> str:
+    if not force and os.path.exists(LIB_PATH) and os.path.getmtime(LIB_PATH) >= os.path.getmtime(SRC):
+        return LIB_PATH
+    tmp = LIB_PATH + ".tmp"
+    cmd = ["g++", "-O3", "-std=c++17", "-fPIC", "-shared", "-pthread", "-Wall", "-fvisibility=hidden", SRC, "-o", tmp]
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+    if r.returncode != 0:
+        raise NativeBuildError(r.stdout.decode(errors="replace"))
+    os.replace(tmp, LIB_PATH)
+    return LIB_PATH
+
+
+def load() -> ctypes.CDLL:
+    global _lib
+    with _lock:
+        if _lib is None:
+            build()
+            lib = ctypes.CDLL(LIB_PATH)
+            lib.ingest_vocab_new.restype = ctypes.c_void_p
+            lib.ingest_vocab_new.argtypes = [ctypes.c_int]
+            lib.ingest_vocab_free.argtypes = [ctypes.c_void_p]
+            lib.ingest_vocab_add.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int,
+                                             ctypes.c_float]
+            lib.ingest_parse.restype = ctypes.c_longlong
+            lib.ingest_parse.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char, ctypes.c_int,
+                                         ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int,
+                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+                                         ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_size_t)]
+            _lib = lib
+        return _lib
+
+
+DEFAULT_MISSING = ("", "NA", "NaN", "nan", "?", "null", "NULL")
+
+
+class RecordParser:
+    """Parse delimited records whose columns are ``columns`` (e.g. the CSV header) into the
+    model's active-field matrix. Columns the model does not use are skipped."""
+
+    def __init__(self, compiled, columns: Sequence[str], delimiter: str = ",",
+                 missing: Iterable[str] = DEFAULT_MISSING, threads: int = 0):
+        self.lib = load()
+        self.fields: List[str] = list(compiled.active_fields)
+        pos = {f: j for j, f in enumerate(self.fields)}
+        self.columns = list(columns)
+        absent = [f for f in self.fields if f not in self.columns]
+        if absent:
+            raise ValueError(f"input columns lack active fields {absent}")
+        self.target = np.array([pos.get(c, -1) for c in self.columns], dtype=np.int32)
+        schema = compiled.schema
+        self.kind = np.array([1 if schema.is_string(f) else 0 for f in self.fields], dtype=np.int32)
+        self.vocab = self.lib.ingest_vocab_new(len(self.fields))
+        for j, f in enumerate(self.fields):
+            if self.kind[j]:
+                for code, v in enumerate(schema.values.get(f, [])):
+                    b = v.encode()
+                    self.lib.ingest_vocab_add(self.vocab, j, b, len(b), float(code))
+        self.delim = delimiter.encode()[:1]
+        toks = list(missing)
+        self.missing = b"".join(t.encode() + b"\0" for t in toks)
+        self.n_missing = len(toks)
+        self.threads = threads or max(1, min(16, os.cpu_count() or 1))
+        self.bad_tokens = 0
+
+    def __del__(self):
+        v = getattr(self, "vocab", None)
+        if v:
+            self.lib.ingest_vocab_free(v)
+            self.vocab = None
+
+    def parse(self, data: bytes, out: Optional[np.ndarray] = None, max_rows: Optional[int] = None
+              ) -> Tuple[np.ndarray, int]:
+        """Parse the complete lines of ``data``. Returns ``(rows view of out, bytes consumed)``;
+        ``out`` (float32 ``[cap, fields]``, e.g. a pinned tensor's numpy view) is allocated if
+        omitted."""
+        F = len(self.fields)
+        if out is None:
+            cap = max_rows if max_rows is not None else data.count(b"\n") + 1
+            out = np.empty((cap, F), dtype=np.float32)
+        if out.dtype != np.float32 or not out.flags.c_contiguous or out.shape[1] != F:
+            raise ValueError(f"out must be a C-contiguous float32 [rows, {F}] array")
+        cap = out.shape[0] if max_rows is None else min(max_rows, out.shape[0])
+        consumed, bad = ctypes.c_size_t(0), ctypes.c_size_t(0)
+        n = self.lib.ingest_parse(data, len(data), self.delim, len(self.columns), self.target.ctypes.data, F,
+                                  self.kind.ctypes.data, self.missing, self.n_missing, self.vocab,
+                                  out.ctypes.data, cap, self.threads, ctypes.byref(consumed), ctypes.byref(bad))
+        if n < 0:
+            raise ValueError(f"ingest_parse failed with code {n}")
+        self.bad_tokens += bad.value
+        return out[:n], consumed.value
+
+    def parse_file(self, path: str, chunk_bytes: int = 64 << 20):
+        """Yield ``[rows, fields]`` batches of a delimited file (header line skipped if it
+        matches ``columns``)."""
+        with open(path, "rb") as fh:
+            rest = b""
+            first = True
+            while True:
+                blk = fh.read(chunk_bytes)
+                data = rest + blk
+                if first:
+                    first = False
+                    nl = data.find(b"\n")
+                    head = data[:nl].decode(errors="replace").strip().split(self.delim.decode())
+                    if [h.strip().strip('"') for h in head] == self.columns:
+                        data = data[nl + 1:]
+                if not blk:
+                    if data and not data.endswith(b"\n"):
+                        data += b"\n"
+                    if data:
+                        m, _ = self.parse(data)
+                        if len(m):
+                            yield m
+                    return
+                m, used = self.parse(data)
+                rest = data[used:]
+                if len(m):
+                    yield m
+
+
+def parse_records(compiled, text: bytes, columns: Sequence[str], **kw) -> np.ndarray:
+    """One-shot convenience: delimited ``text`` -> ``[rows, active fields]`` float32."""
+    m, _ = RecordParser(compiled, columns, **kw).parse(text if text.endswith(b"\n") else text + b"\n")
+    return m
+
+
+__all__ = ["RecordParser", "parse_records", "build", "load"]

@@ -3,7 +3,7 @@
 The kernels are plain HIP C++ compiled by ``hipcc --offload-arch=gfx950`` into one shared object
 with ``extern "C"`` launchers that take a raw ``hipStream_t`` and a POD argument struct. Python
 calls them through :mod:`ctypes` with ``torch`` tensor device pointers — no PyTorch C++ headers in
-the build (a full rebuild takes seconds), one HIP runtime in the process (the ``.so`` binds to the
+the build (incremental rebuilds take seconds), one HIP runtime in the process (the ``.so`` binds to the
 ``libamdhip64.so.7`` that ``torch`` already loaded, matched by SONAME).
 
 On a machine with a GPU a missing / unloadable library is an error (:class:`KernelLibraryError`),
@@ -19,6 +19,7 @@ import os
 import shutil
 import subprocess
 import threading
+import time
 from typing import List, Optional
 
 logger = logging.getLogger(__name__)
@@ -55,26 +56,31 @@ def hipcc() -> str:
     raise KernelLibraryError("hipcc not found (set HIPCC or install ROCm)")
 
 
-def build(force: bool = False, verbose: bool = False, jobs: int = 4) -> str:
-    """Compile every ``csrc/*.hip`` for gfx950 and link ``_pmml_kernels.so`` (in-tree)."""
+def build(force: bool = False, verbose: bool = False, jobs: int = 0, incremental: bool = False) -> str:
+    """Compile every ``csrc/*.hip`` for gfx950 and link ``_pmml_kernels.so`` (in-tree).
+    ``incremental``: only recompile sources newer than their object (or than any header)."""
     if not force and not is_stale():
         return LIB_PATH
+    jobs = jobs or max(1, min(8, os.cpu_count() or 1))
     cc = hipcc()
     objdir = os.path.join(HERE, "_build")
     os.makedirs(objdir, exist_ok=True)
     flags = ["-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
              "-ffp-contract=fast", "-munsafe-fp-atomics"]
+    hdr_t = max([os.path.getmtime(h) for h in _headers()] or [0.0])
     procs = []
     objs = []
     for src in sources():
         obj = os.path.join(objdir, os.path.basename(src).replace(".hip", ".o"))
         objs.append(obj)
+        if incremental and os.path.exists(obj) and os.path.getmtime(obj) > max(os.path.getmtime(src), hdr_t):
+            continue
         cmd = [cc, *flags, "-c", src, "-o", obj]
         if verbose:
             logger.info("%s", " ".join(cmd))
         procs.append((src, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
-        if len([p for p in procs if p[1].poll() is None]) >= jobs:
-            procs[0][1].wait()
+        while len([p for p in procs if p[1].poll() is None]) >= jobs:
+            time.sleep(0.05)
     for src, p in procs:
         out, _ = p.communicate()
         if p.returncode != 0:

@@ -390,3 +390,20 @@ def test_fp8_leaf_chain_on_gpu(gpu):
     ref, vref = c.score_matrix_oracle(X)
     assert v8.bool().all().item() and vref.all()
     assert (s8.cpu().numpy() == ref).mean() > 0.97  # labels vs the fp64 oracle on fp32 leaves
+
+
+@pytest.mark.parametrize("strategy", ["defaultChild", "nullPrediction"])
+def test_categorical_splits_on_gpu(gpu, strategy):
+    """isIn / isNotIn / == / != splits: derive-kernel membership columns + the tree kernel."""
+    from test_derive import cat_inputs, categorical_tree_doc
+
+    from flink_jpmml_amd.runtime.compiled import CompiledPmml
+    from flink_jpmml_amd.runtime.derive import DerivedPlan
+
+    c = CompiledPmml.from_string(categorical_tree_doc(strategy))
+    plan = c.plan(gpu)
+    assert isinstance(plan, DerivedPlan)
+    X = cat_inputs(20_000, seed=3)
+    s, v = _gpu_np(plan, X)
+    ref, vref = c.score_matrix_oracle(X)
+    assert (v == vref).all() and (s[v] == ref[v]).all()

@@ -1,0 +1,81 @@
+"""Native C++ record ingest (``flink_jpmml_amd/native``): delimited text -> the engine's fp32
+matrix, checked against numpy / Python parsing and the float64 oracle."""
+
+import numpy as np
+import pytest
+
+from flink_jpmml_amd.native import RecordParser, parse_records
+from flink_jpmml_amd.runtime.compiled import CompiledPmml
+
+
+@pytest.fixture(scope="module")
+def kmeans(fixtures_dir):
+    return CompiledPmml.load(fixtures_dir["kmeans"])
+
+
+def test_numeric_csv_matches_numpy(kmeans):
+    rng = np.random.default_rng(0)
+    X = rng.normal(0, 3, (5000, 4)).astype(np.float32)
+    text = "\n".join(",".join(repr(float(v)) for v in row) for row in X).encode() + b"\n"
+    m = parse_records(kmeans, text, kmeans.active_fields)
+    assert m.shape == X.shape and m.dtype == np.float32
+    np.testing.assert_array_equal(m, X)
+
+
+def test_missing_tokens_reordered_and_skipped_columns(kmeans):
+    cols = ["id"] + list(reversed(kmeans.active_fields)) + ["extra"]
+    text = b"7,4.0,3,,1e0,zz\n8, NA ,?,2.5,-1.25,q\r\n9,1,1,1,1,\n"
+    m = parse_records(kmeans, text, cols)
+    # active order is the reverse of the file order
+    assert m.shape == (3, 4)
+    np.testing.assert_array_equal(m[0], [1.0, np.nan, 3.0, 4.0])
+    np.testing.assert_array_equal(m[1], [-1.25, 2.5, np.nan, np.nan])
+    s, v = kmeans.score_matrix_oracle(m)
+    assert v[2] and s[2] == 3.0  # the reference golden (1,1,1,1) -> cluster 3
+
+
+def test_categorical_codes_and_unknown_tokens():
+    from test_derive import categorical_tree_doc
+
+    c = CompiledPmml.from_string(categorical_tree_doc())
+    text = b"x,cat\n0.5,a\n-1,f\n2,zz\n,c\n"
+    p = RecordParser(c, ["x", "cat"])
+    m, used = p.parse(text.split(b"\n", 1)[1])
+    vocab = c.schema.values["cat"]
+    assert m[0, 1] == vocab.index("a") and m[1, 1] == vocab.index("f")
+    assert m[2, 1] == -1.0  # unknown category -> invalid code
+    assert np.isnan(m[3, 0]) and m[3, 1] == vocab.index("c")
+    s, v = c.score_matrix_oracle(m)
+    assert v.tolist()[:3] == [True, True, False]  # "zz" is not a valid value -> returnInvalid
+
+
+def test_threads_and_partial_lines(kmeans):
+    rng = np.random.default_rng(1)
+    X = rng.normal(0, 1, (200_000, 4)).astype(np.float32)
+    text = "\n".join(",".join(f"{v:.6g}" for v in row) for row in X).encode() + b"\n"
+    p1 = RecordParser(kmeans, kmeans.active_fields, threads=1)
+    p8 = RecordParser(kmeans, kmeans.active_fields, threads=8)
+    a, used_a = p1.parse(text)
+    b, used_b = p8.parse(text)
+    assert used_a == used_b == len(text) and np.array_equal(a, b)
+    np.testing.assert_allclose(a, X, rtol=1e-5)
+    # a trailing partial line is left for the next chunk
+    cut = len(text) - 7
+    m, used = p8.parse(text[:cut])
+    assert len(m) == len(X) - 1 and text[used - 1:used] == b"\n"
+    # max_rows caps the batch and reports the bytes it covered
+    m, used = p8.parse(text, max_rows=1000)
+    assert len(m) == 1000 and text[:used].count(b"\n") == 1000
+
+
+def test_parse_file_chunks(tmp_path, kmeans):
+    rng = np.random.default_rng(2)
+    X = rng.normal(0, 1, (30_000, 4)).astype(np.float32)
+    path = tmp_path / "rec.csv"
+    with open(path, "w") as fh:
+        fh.write(",".join(kmeans.active_fields) + "\n")
+        for row in X:
+            fh.write(",".join(repr(float(v)) for v in row) + "\n")
+    p = RecordParser(kmeans, kmeans.active_fields)
+    got = np.concatenate(list(p.parse_file(str(path), chunk_bytes=50_000)))
+    np.testing.assert_array_equal(got, X)
