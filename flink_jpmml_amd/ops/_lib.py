@@ -121,6 +121,11 @@ class TreeArgs(ctypes.Structure):
                 ("valid", c_void_p), ("probs", c_void_p), ("partial", c_void_p)]
 
 
+class GenTreeArgs(ctypes.Structure):
+    _fields_ = [("t", TreeArgs), ("nodes", c_void_p), ("children", c_void_p), ("preds", c_void_p),
+                ("pool", c_void_p), ("trees", c_void_p), ("max_steps", c_int), ("pad", c_int)]
+
+
 class ClusterArgs(ctypes.Structure):
     _fields_ = [("X", c_void_p), ("n_rows", c_int), ("n_feat", c_int), ("ldx", c_int), ("K", c_int),
                 ("prep", c_void_p), ("centers", c_void_p), ("weights", c_void_p), ("scales", c_void_p),
@@ -162,6 +167,7 @@ class DeriveArgs(ctypes.Structure):
 _ABI = {
     "pmml_derive_args_size": DeriveArgs,
     "pmml_tree_args_size": TreeArgs,
+    "pmml_tree_general_args_size": GenTreeArgs,
     "pmml_cluster_args_size": ClusterArgs,
     "pmml_linear_args_size": LinearArgs,
     "pmml_mlp_args_size": MlpArgs,
@@ -218,6 +224,8 @@ def load(auto_build: bool = True) -> ctypes.CDLL:
             lib.pmml_mlp_launch.argtypes = [c_void_p, ctypes.POINTER(MlpArgs), c_int]
         if hasattr(lib, "pmml_svm_launch"):
             lib.pmml_svm_launch.argtypes = [c_void_p, ctypes.POINTER(SvmArgs), c_int]
+        lib.pmml_tree_general_launch.argtypes = [c_void_p, ctypes.POINTER(GenTreeArgs)]
+        lib.pmml_tree_general_launch.restype = c_int
         lib.pmml_derive_launch.argtypes = [c_void_p, ctypes.POINTER(DeriveArgs)]
         lib.pmml_derive_launch.restype = c_int
         lib.pmml_mask_invalid.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int]

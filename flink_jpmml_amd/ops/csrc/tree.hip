@@ -681,6 +681,182 @@ __global__ __launch_bounds__(TB) void tree_reduce_kernel(TreeArgs a, int splits)
   apply_epilogue(a.epi, [&](int c) { return acc[c]; }, ok, row, a.n_rows, a.score, a.valid, a.probs);
 }
 
+
+// ------------------------------------------------------------------------------------------
+// GENERAL layout: any PMML TreeModel shape — multiway splits, SimpleSetPredicate, Compound
+// and / or / xor / surrogate predicates, every missingValueStrategy except the two aggregating ones,
+// both noTrueChildStrategy values, internal-node scores. Each lane walks its row through a node
+// table, evaluating the children's predicates as postfix programs over PMML's three-valued logic
+// (TRUE 1 / FALSE 0 / UNKNOWN 2, packed 2 bits per entry in a 64-bit register stack). Divergent,
+// node tables read from L2 — the fallback for shapes the branch-free layouts cannot express.
+enum : int {
+  P_END = 0, P_TRUE, P_FALSE, P_GE, P_EQ, P_ISMISS, P_NOTMISS, P_SET, P_AND, P_OR, P_XOR, P_SURR,
+};
+enum : int { S_NONE = 0, S_LAST = 1, S_NULL = 2, S_DEFAULT = 3 };
+constexpr uint32_t V_F = 0u, V_T = 1u, V_U = 2u;
+
+struct GenTreeArgs {
+  TreeArgs t;                  // rows, prep, epilogue, payload (t.leaves [nodes][P]), slots, outputs
+  const int4* nodes;           // {child_off, n_child | has_score << 16, pred_off, default_child}
+  const int* children;         // child node indices
+  const int4* preds;           // {op | neg << 8, field or n, pool offset / count, T bits}
+  const float* pool;           // SimpleSetPredicate values
+  const int2* trees;           // {root node, strategy | returnLastPrediction << 2}
+  int max_steps, pad;
+};
+
+template <bool FEAT_LDS>
+__device__ __forceinline__ float gen_feature(const GenTreeArgs& a, const char* feat_lane, const float* xrow, int f) {
+  if (FEAT_LDS) return *reinterpret_cast<const float*>(feat_lane + f * TB * 4);
+  float x = xrow[f];
+  if (a.t.prep) {
+    bool b = false;
+    x = prep_value(x, a.t.prep[f], &b);
+  }
+  return x;
+}
+
+template <bool FEAT_LDS>
+__device__ uint32_t gen_eval(const GenTreeArgs& a, int pc, const char* feat_lane, const float* xrow) {
+  uint64_t st = 0;
+  for (;; ++pc) {
+    const int4 in = a.preds[pc];
+    const int op = in.x & 0xFF;
+    const uint32_t neg = (uint32_t)(in.x >> 8) & 1u;
+    uint32_t v;
+    if (op == P_END) return (uint32_t)(st & 3u);
+    if (op >= P_AND) {
+      const int n = in.y;
+      bool any_t = false, any_f = false, any_u = false;
+      uint32_t par = 0u, sur = V_U;
+      for (int i = 0; i < n; ++i) {
+        const uint32_t e = (uint32_t)(st & 3u);
+        st >>= 2;
+        any_t |= e == V_T;
+        any_f |= e == V_F;
+        any_u |= e == V_U;
+        par ^= (e == V_T) ? 1u : 0u;
+        if (e != V_U) sur = e;  // popped top-down: ends at the first (bottom-most) known value
+      }
+      if (op == P_AND) v = any_f ? V_F : (any_u ? V_U : V_T);
+      else if (op == P_OR) v = any_t ? V_T : (any_u ? V_U : V_F);
+      else if (op == P_XOR) v = any_u ? V_U : par;
+      else v = sur;
+    } else if (op == P_TRUE) {
+      v = V_T;
+    } else if (op == P_FALSE) {
+      v = V_F;
+    } else {
+      const float x = gen_feature<FEAT_LDS>(a, feat_lane, xrow, in.y);
+      const bool miss = x != x;
+      if (op == P_ISMISS) {
+        v = miss ? V_T : V_F;
+      } else if (op == P_NOTMISS) {
+        v = miss ? V_F : V_T;
+      } else if (miss) {
+        v = V_U;
+      } else {
+        bool r;
+        if (op == P_GE) {
+          r = x >= __int_as_float(in.w);
+        } else if (op == P_EQ) {
+          r = x == __int_as_float(in.w);
+        } else {  // P_SET
+          r = false;
+          for (int i = 0; i < in.w; ++i) r = r || (a.pool[in.z + i] == x);
+        }
+        v = (r ? 1u : 0u) ^ neg;
+      }
+    }
+    st = (st << 2) | v;
+  }
+}
+
+// Returns the scoring node of tree t for this lane's row, or -1 (null prediction).
+template <bool FEAT_LDS>
+__device__ int gen_walk(const GenTreeArgs& a, int t, const char* feat_lane, const float* xrow) {
+  const int2 tr = a.trees[t];
+  const int strat = tr.y & 3;
+  const bool ret_last = ((tr.y >> 2) & 1) != 0;
+  int node = tr.x;
+  if (gen_eval<FEAT_LDS>(a, a.nodes[node].z, feat_lane, xrow) != V_T) return -1;
+  for (int step = 0; step < a.max_steps; ++step) {
+    const int4 nd = a.nodes[node];
+    const int nc = nd.y & 0xFFFF;
+    if (nc == 0) return node;
+    int next = -1;
+    for (int c = 0; c < nc; ++c) {
+      const int ch = a.children[nd.x + c];
+      const uint32_t v = gen_eval<FEAT_LDS>(a, a.nodes[ch].z, feat_lane, xrow);
+      if (v == V_U && strat != S_NONE) {
+        if (strat == S_LAST) return node;
+        if (strat == S_NULL) return -1;
+        next = nd.w;  // defaultChild (-1 when absent: no prediction)
+        if (next < 0) return -1;
+        break;
+      }
+      if (v == V_T) {
+        next = ch;
+        break;
+      }
+    }
+    if (next < 0) return ret_last ? node : -1;
+    node = next;
+  }
+  return -1;
+}
+
+template <bool GENERAL, bool FEAT_LDS>
+__global__ __launch_bounds__(TB, 2) void tree_general_kernel(GenTreeArgs ga) {
+  const TreeArgs& a = ga.t;
+  extern __shared__ __align__(16) uint32_t smem[];
+  float* feat = reinterpret_cast<float*>(smem);
+  int* bad = reinterpret_cast<int*>(smem + (FEAT_LDS ? a.n_feat * TB : 0));
+  float* accl = reinterpret_cast<float*>(bad + TB);
+  const int tid = threadIdx.x;
+  const int row0 = blockIdx.x * TB;
+  const int row = row0 + tid;
+  if (FEAT_LDS) {
+    stage_rows_T<TB>(a.X, a.n_rows, a.n_feat, a.ldx, a.prep, feat, bad, row0);
+  } else {
+    bad[tid] = 0;
+    __syncthreads();
+  }
+  bool row_ok = bad[tid] == 0;
+  const float* xrow = a.X + (size_t)min(row, a.n_rows - 1) * a.ldx;
+  if (!FEAT_LDS && a.prep && row < a.n_rows) {
+    for (int f = 0; f < a.n_feat; ++f) {
+      bool b = false;
+      (void)prep_value(xrow[f], a.prep[f], &b);
+      if (b) row_ok = false;
+    }
+  }
+  if (a.row_valid_in && row < a.n_rows) row_ok = row_ok && a.row_valid_in[row];
+  if (GENERAL) {
+    for (int c = 0; c < a.C; ++c) accl[c * TB + tid] = 0.f;
+  }
+  float acc = 0.f;
+  bool poisoned = false;
+  const char* feat_lane = reinterpret_cast<const char*>(feat + tid);
+  if (row < a.n_rows) {
+    for (int t = 0; t < a.n_trees; ++t) {
+      const int node = gen_walk<FEAT_LDS>(ga, t, feat_lane, xrow);
+      if (node < 0 || ((ga.nodes[node].y >> 16) & 1) == 0) {  // null prediction
+        if (GENERAL) poisoned = true;
+        else acc += __builtin_nanf("");
+        continue;
+      }
+      if (GENERAL) {
+        const int slot = a.tree_slot[t];
+        for (int p = 0; p < a.P; ++p) accl[(slot + p) * TB + tid] += a.leaves[(size_t)node * a.P + p];
+      } else {
+        acc += a.leaves[node];
+      }
+    }
+  }
+  finish_row(a, acc, accl, 0, GENERAL, row, row_ok && !poisoned);
+}
+
 template <typename K>
 int prepare_launch(K kernel, size_t lds) {
   if (lds > 65536) {
@@ -791,4 +967,40 @@ PMML_API int pmml_tree_launch(hipStream_t stream, const TreeArgs* args, int layo
     if (hipGetLastError() != hipSuccess) return -8;
   }
   return 0;
+}
+
+PMML_API int pmml_tree_general_args_size() { return (int)sizeof(GenTreeArgs); }
+
+// GENERAL layout launch (one split; grid over rows only).
+PMML_API int pmml_tree_general_launch(hipStream_t stream, const GenTreeArgs* args) {
+  GenTreeArgs ga = *args;
+  TreeArgs& a = ga.t;
+  if (a.n_rows <= 0) return 0;
+  if (a.C > 16) return -3;
+  a.partial = nullptr;
+  a.trees_per_split = a.n_trees;
+  dim3 grid((a.n_rows + TB - 1) / TB);
+  const bool feat_lds = a.n_feat <= 64;
+  const size_t acc_lds = a.general ? (size_t)a.C * TB * 4 : 0;
+  const size_t lds = (feat_lds ? (size_t)a.n_feat * TB * 4 : 0) + TB * 4 + acc_lds;
+  int err = 0;
+  if (a.general) {
+    if (feat_lds) {
+      err = prepare_launch(tree_general_kernel<true, true>, lds);
+      if (!err) hipLaunchKernelGGL((tree_general_kernel<true, true>), grid, dim3(TB), lds, stream, ga);
+    } else {
+      err = prepare_launch(tree_general_kernel<true, false>, lds);
+      if (!err) hipLaunchKernelGGL((tree_general_kernel<true, false>), grid, dim3(TB), lds, stream, ga);
+    }
+  } else {
+    if (feat_lds) {
+      err = prepare_launch(tree_general_kernel<false, true>, lds);
+      if (!err) hipLaunchKernelGGL((tree_general_kernel<false, true>), grid, dim3(TB), lds, stream, ga);
+    } else {
+      err = prepare_launch(tree_general_kernel<false, false>, lds);
+      if (!err) hipLaunchKernelGGL((tree_general_kernel<false, false>), grid, dim3(TB), lds, stream, ga);
+    }
+  }
+  if (err) return err;
+  return hipGetLastError() == hipSuccess ? 0 : -7;
 }

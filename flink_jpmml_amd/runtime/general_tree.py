@@ -1,0 +1,282 @@
+"""GENERAL tree layout: node tables + predicate programs for ``tree.hip::tree_general_kernel``.
+
+The branch-free PERFECT and POINTER layouts need binary ``x OP t`` splits. Every other PMML
+TreeModel shape — multiway splits, ``SimpleSetPredicate``, ``CompoundPredicate`` (and / or / xor /
+surrogate, the R ``rpart`` export), ``lastPrediction`` / ``nullPrediction`` / ``defaultChild`` /
+``none`` missing strategies, ``returnLastPrediction``, scores on internal nodes — lowers here.
+JPMML evaluates these by walking the object graph per record (`S/api/PmmlModel.scala:159-160`);
+the kernel walks the same graph per lane, the semantics following the float64 oracle
+:meth:`flink_jpmml_amd.models.tree.TreeEvaluator.leaf_index` exactly.
+
+Predicates compile to postfix programs over three-valued logic. Comparisons against a constant
+``t`` are made exact for fp32 inputs the same way as the binary layouts (directional rounding to a
+``x >= T`` test, see :func:`flink_jpmml_amd.runtime.plans.canonical_threshold`); an equality with a
+constant that no fp32 value can equal is compiled to "never equal".
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, List, Optional
+
+import numpy as np
+
+from ..models.tree import TreeEvaluator
+from ..pmml import ir
+from .plans import NotLowerable, _ceil32, _floor32, _next_up32
+
+P_END, P_TRUE, P_FALSE, P_GE, P_EQ, P_ISMISS, P_NOTMISS, P_SET, P_AND, P_OR, P_XOR, P_SURR = range(12)
+_COMPOUND = {"and": P_AND, "or": P_OR, "xor": P_XOR, "surrogate": P_SURR}
+STRATEGY = {"none": 0, "lastPrediction": 1, "nullPrediction": 2, "defaultChild": 3}
+MAX_STACK = 32  # 2-bit entries in the kernel's 64-bit stack
+
+
+@dataclass
+class GeneralTree:
+    """Duck-types :class:`~flink_jpmml_amd.models.tree.BinaryTree` for the ensemble specs: per-node
+    (``ev.nodes`` order) ``leaf_value`` (value or class index, NaN = no score) and ``leaf_probs``."""
+
+    ev: TreeEvaluator
+    field_index: Dict[str, int]
+    leaf_value: np.ndarray
+    leaf_probs: Optional[np.ndarray]
+    has_score: np.ndarray
+    depth: int
+    null_missing: bool = True  # may yield no prediction (checked against skipSegment)
+
+
+def lower_general_tree(ev: TreeEvaluator, field_index: Dict[str, int]) -> GeneralTree:
+    tm = ev.tree
+    if tm.missing_value_strategy not in STRATEGY:
+        raise NotLowerable(f"missingValueStrategy {tm.missing_value_strategy!r} is host-only")
+    classification = ev.kind == "classification"
+    value = ev.node_label.copy() if classification else ev.node_value.copy()
+    probs = ev.node_probs.copy() if classification else None
+    depth = 0
+    stack = [(tm.root, 0)]
+    while stack:
+        nd, d = stack.pop()
+        depth = max(depth, d)
+        stack.extend((c, d + 1) for c in nd.children)
+    return GeneralTree(ev, field_index, value, probs, ~np.isnan(value), depth)
+
+
+class _PredCompiler:
+    def __init__(self, schema, field_index: Dict[str, int]):
+        self.schema = schema
+        self.field_index = field_index
+        self.code: List[tuple] = []
+        self.pool: List[float] = []
+        self.depth = 0
+        self.max_depth = 0
+
+    def _push(self, ins: tuple, pops: int = 0) -> None:
+        self.code.append(ins)
+        self.depth += 1 - pops
+        self.max_depth = max(self.max_depth, self.depth)
+
+    def _field(self, name: str) -> int:
+        f = self.field_index.get(name)
+        if f is None:
+            raise NotLowerable(f"predicate on field {name!r} that is not a kernel input")
+        return f
+
+    def compile(self, p: ir.Predicate) -> int:
+        off = len(self.code)
+        self.depth = 0
+        self._emit(p)
+        self.code.append((P_END, 0, 0, 0))
+        if self.max_depth > MAX_STACK:
+            raise NotLowerable(f"predicate nests {self.max_depth} deep > {MAX_STACK}")
+        return off
+
+    def _emit(self, p: ir.Predicate) -> None:
+        if isinstance(p, ir.TruePredicate):
+            self._push((P_TRUE, 0, 0, 0))
+        elif isinstance(p, ir.FalsePredicate):
+            self._push((P_FALSE, 0, 0, 0))
+        elif isinstance(p, ir.SimplePredicate):
+            f = self._field(p.field)
+            op = p.operator
+            if op == "isMissing":
+                self._push((P_ISMISS, f, 0, 0))
+                return
+            if op == "isNotMissing":
+                self._push((P_NOTMISS, f, 0, 0))
+                return
+            v = float(self.schema.lookup(p.field, p.value))
+            if op in ("lessThan", "greaterOrEqual"):  # x < v <=> not (x >= ceil32(v))
+                T, neg = _ceil32(v), op == "lessThan"
+                self._push((P_GE | (int(neg) << 8), f, 0, _bits(T)))
+            elif op in ("lessOrEqual", "greaterThan"):  # x > v <=> x >= nextup(floor32(v))
+                T, neg = _next_up32(_floor32(v)), op == "lessOrEqual"
+                self._push((P_GE | (int(neg) << 8), f, 0, _bits(T)))
+            elif op in ("equal", "notEqual"):
+                T = float(np.float32(v)) if float(np.float32(v)) == v else float("nan")  # nan: never equal
+                self._push((P_EQ | (int(op == "notEqual") << 8), f, 0, _bits(T)))
+            else:
+                raise NotLowerable(f"SimplePredicate operator {op!r}")
+        elif isinstance(p, ir.SimpleSetPredicate):
+            f = self._field(p.field)
+            vals = [float(self.schema.lookup(p.field, v)) for v in p.values]
+            vals = [v for v in vals if float(np.float32(v)) == v]  # fp32 inputs can only equal these
+            off = len(self.pool)
+            self.pool.extend(vals)
+            self._push((P_SET | (int(p.boolean_operator == "isNotIn") << 8), f, off, len(vals)))
+        elif isinstance(p, ir.CompoundPredicate):
+            op = _COMPOUND.get(p.boolean_operator)
+            if op is None or not p.predicates:
+                raise NotLowerable(f"CompoundPredicate {p.boolean_operator!r}")
+            for q in p.predicates:
+                self._emit(q)
+            self._push((op, len(p.predicates), 0, 0), pops=len(p.predicates))
+        else:
+            raise NotLowerable(f"predicate {type(p).__name__} is host-only")
+
+
+def _bits(x: float) -> int:
+    return int(np.array([x], dtype=np.float32).view(np.int32)[0])
+
+
+def pack_general(trees: List[GeneralTree], weights: List[float], P: int, schema) -> dict:
+    """Concatenate the trees' node tables into the kernel's arrays (``nodes`` int4, ``children``,
+    ``preds`` int4, ``pool`` f32, ``trees`` int2, ``payload`` [nodes][P] f32) + ``max_steps``."""
+    nodes: List[tuple] = []
+    children: List[int] = []
+    payload: List[np.ndarray] = []
+    tree_tab: List[tuple] = []
+    pc: Optional[_PredCompiler] = None
+    max_depth = 0
+    for t, w in zip(trees, weights):
+        ev = t.ev
+        if pc is None:
+            pc = _PredCompiler(schema, t.field_index)
+        pc.field_index = t.field_index
+        base = len(nodes)
+        index = {id(nd): base + i for i, nd in enumerate(ev.nodes)}
+        for i, nd in enumerate(ev.nodes):
+            if len(nd.children) >= 1 << 16:
+                raise NotLowerable("node with more than 65535 children")
+            off = len(children)
+            children.extend(index[id(c)] for c in nd.children)
+            dflt = -1
+            if nd.default_child is not None:
+                for c in nd.children:
+                    if c.id == nd.default_child:
+                        dflt = index[id(c)]
+                        break
+            pred_off = pc.compile(nd.predicate)
+            has = bool(t.has_score[i])
+            nodes.append((off, len(nd.children) | (int(has) << 16), pred_off, dflt))
+            if P > 1 and t.leaf_probs is not None:
+                row = np.nan_to_num(np.asarray(t.leaf_probs[i], dtype=np.float64)[:P]) * w
+            else:
+                row = np.array([t.leaf_value[i] if has else 0.0]) * w
+            payload.append(row)
+        flags = STRATEGY[ev.tree.missing_value_strategy] | (
+            (1 << 2) if ev.tree.no_true_child_strategy == "returnLastPrediction" else 0)
+        tree_tab.append((base, flags))
+        max_depth = max(max_depth, t.depth)
+    return {
+        "nodes": np.array(nodes, dtype=np.int64).astype(np.int32).reshape(-1, 4),
+        "children": np.array(children or [0], dtype=np.int32),
+        "preds": np.array(pc.code if pc else [(P_END, 0, 0, 0)], dtype=np.int64).astype(np.int32).reshape(-1, 4),
+        "pool": np.array(pc.pool if pc and pc.pool else [0.0], dtype=np.float32),
+        "trees": np.array(tree_tab, dtype=np.int32).reshape(-1, 2),
+        "payload": np.stack(payload).astype(np.float32).reshape(len(nodes), -1),
+        "max_steps": int(max_depth + 2),
+    }
+
+
+def emulate_general(packed: dict, X: np.ndarray, P: int, n_trees: int) -> np.ndarray:
+    """numpy twin of the kernel walk (per row, per tree) -> ``[rows, P]`` accumulators, NaN for
+    rows with a null tree (CPU tests)."""
+    nodes, children, preds, pool = packed["nodes"], packed["children"], packed["preds"], packed["pool"]
+    Xf = np.asarray(X, dtype=np.float32)
+    out = np.zeros((len(Xf), P), dtype=np.float32)
+    T = preds[:, 3].copy().view(np.float32)
+
+    def ev(pc: int, x) -> int:
+        st: List[int] = []
+        while True:
+            op, f, a, cnt = (int(v) for v in preds[pc])
+            neg, op = (op >> 8) & 1, op & 0xFF
+            if op == P_END:
+                return st[-1]
+            if op >= P_AND:
+                vals = st[len(st) - f:]
+                del st[len(st) - f:]
+                if op == P_AND:
+                    v = 0 if 0 in vals else (2 if 2 in vals else 1)
+                elif op == P_OR:
+                    v = 1 if 1 in vals else (2 if 2 in vals else 0)
+                elif op == P_XOR:
+                    v = 2 if 2 in vals else sum(1 for e in vals if e == 1) % 2
+                else:
+                    v = next((e for e in vals if e != 2), 2)
+            elif op == P_TRUE:
+                v = 1
+            elif op == P_FALSE:
+                v = 0
+            else:
+                xv = x[f]
+                miss = bool(np.isnan(xv))
+                if op == P_ISMISS:
+                    v = int(miss)
+                elif op == P_NOTMISS:
+                    v = int(not miss)
+                elif miss:
+                    v = 2
+                else:
+                    if op == P_GE:
+                        r = bool(xv >= T[pc])
+                    elif op == P_EQ:
+                        r = bool(xv == T[pc])
+                    else:
+                        r = bool(np.any(pool[a: a + cnt] == xv))
+                    v = int(r) ^ neg
+            st.append(v)
+            pc += 1
+
+    for r in range(len(Xf)):
+        x = Xf[r]
+        for t in range(n_trees):
+            root, flags = (int(v) for v in packed["trees"][t])
+            strat, ret_last = flags & 3, (flags >> 2) & 1
+            node = root
+            res = -1
+            if ev(int(nodes[node, 2]), x) == 1:
+                for _ in range(packed["max_steps"]):
+                    off, nc, _, dflt = (int(v) for v in nodes[node])
+                    nc &= 0xFFFF
+                    if nc == 0:
+                        res = node
+                        break
+                    nxt, stop = -1, False
+                    for c in range(nc):
+                        ch = int(children[off + c])
+                        v = ev(int(nodes[ch, 2]), x)
+                        if v == 2 and strat != 0:
+                            if strat == 1:
+                                res, stop = node, True
+                            elif strat == 2:
+                                res, stop = -1, True
+                            else:
+                                nxt = dflt
+                                if nxt < 0:
+                                    res, stop = -1, True
+                            break
+                        if v == 1:
+                            nxt = ch
+                            break
+                    if stop:
+                        break
+                    if nxt < 0:
+                        res = node if ret_last else -1
+                        break
+                    node = nxt
+            if res < 0 or not ((int(nodes[res, 1]) >> 16) & 1):
+                out[r] = np.nan
+            else:
+                out[r] += packed["payload"][res]
+    return out

@@ -472,14 +472,14 @@ def _target_affine(ev) -> Tuple[float, float]:
     return t.rescale_factor, t.rescale_constant
 
 
-def _regression_ensemble(ev, field_index) -> Tuple[List[BinaryTree], List[float], float, float]:
+def _regression_ensemble(ev, field_index, lower=lower_binary_tree) -> Tuple[List[BinaryTree], List[float], float, float]:
     """Flatten a regression tree / MiningModel(sum|average|weightedAverage) of regression trees
     into (trees, per-tree weights, a, b) with value = a * Σ w_t leaf_t + b."""
     if isinstance(ev, TreeEvaluator):
         if ev.kind != "regression":
             raise NotLowerable("expected a regression tree")
         a, b = _target_affine(ev)
-        return [lower_binary_tree(ev, field_index)], [1.0], a, b
+        return [lower(ev, field_index)], [1.0], a, b
     if isinstance(ev, MiningEvaluator):
         mm = ev.mm
         if ev.kind != "regression":
@@ -492,7 +492,7 @@ def _regression_ensemble(ev, field_index) -> Tuple[List[BinaryTree], List[float]
         trees: List[BinaryTree] = []
         weights: List[float] = []
         for seg, sub in zip(mm.segments, ev.sub):
-            st, sw, sa, sb = _regression_ensemble(sub, field_index)
+            st, sw, sa, sb = _regression_ensemble(sub, field_index, lower)
             if sb != 0.0:
                 raise NotLowerable("nested Target rescaleConstant inside an ensemble is host-only")
             w = seg.weight if method == "weightedAverage" else 1.0
@@ -517,27 +517,31 @@ def _check_null_trees(mm: ir.MiningModel, trees: List[BinaryTree]) -> None:
         raise NotLowerable("skipSegment over null-on-missing trees is host-only")
 
 
-def ensemble_spec(compiled) -> EnsembleSpec:
+class NotBinaryForm(NotLowerable):
+    """A tree is not in binary-split form: only the GENERAL (predicate-VM) layout can score it."""
+
+
+def ensemble_spec(compiled, lower=lower_binary_tree) -> EnsembleSpec:
     ev = compiled.evaluator
     field_index = getattr(compiled, "field_index", None) or {f: i for i, f in enumerate(compiled.active_fields)}
     try:
         if ev.kind == "regression":
-            trees, w, a, b = _regression_ensemble(ev, field_index)
+            trees, w, a, b = _regression_ensemble(ev, field_index, lower)
             return EnsembleSpec(trees, w, 1, 1, dict(mode=EPI_AFFINE, a=a, b=b), None)
         if isinstance(ev, MiningEvaluator) and ev.mm.multiple_model_method == "modelChain":
-            return _chain_spec(compiled, ev, field_index)
+            return _chain_spec(compiled, ev, field_index, lower)
         if isinstance(ev, MiningEvaluator) and ev.kind == "classification":
-            return _classification_spec(ev, field_index)
+            return _classification_spec(ev, field_index, lower)
         if isinstance(ev, TreeEvaluator) and ev.kind == "classification":
-            t = lower_binary_tree(ev, field_index)
+            t = lower(ev, field_index)
             C = len(ev.categories)
             return EnsembleSpec([t], [1.0], C, C, dict(mode=EPI_ARGMAX, C=C, a=1.0), list(ev.categories))
     except NotBinary as e:
-        raise NotLowerable(f"tree is not in binary-split form: {e}") from e
+        raise NotBinaryForm(f"tree is not in binary-split form: {e}") from e
     raise NotLowerable(f"{type(ev).__name__} ({ev.kind}) is not a lowerable tree ensemble")
 
 
-def _classification_spec(ev: MiningEvaluator, field_index) -> EnsembleSpec:
+def _classification_spec(ev: MiningEvaluator, field_index, lower=lower_binary_tree) -> EnsembleSpec:
     mm = ev.mm
     if not _segments_all_true(mm):
         raise NotLowerable("segment predicates other than True are host-only")
@@ -548,7 +552,7 @@ def _classification_spec(ev: MiningEvaluator, field_index) -> EnsembleSpec:
     for seg, sub in zip(mm.segments, ev.sub):
         if not isinstance(sub, TreeEvaluator) or sub.kind != "classification":
             raise NotLowerable("classification ensembles must hold classification trees")
-        t = lower_binary_tree(sub, field_index)
+        t = lower(sub, field_index)
         remap = np.array([cats.index(c) for c in sub.categories])
         if method in ("majorityVote", "weightedMajorityVote"):
             probs = np.zeros((len(t.leaf_value), C))
@@ -566,7 +570,7 @@ def _classification_spec(ev: MiningEvaluator, field_index) -> EnsembleSpec:
     return EnsembleSpec(trees, weights, C, C, dict(mode=EPI_ARGMAX, C=C, a=1.0 / sum(weights)), cats)
 
 
-def _chain_spec(compiled, ev: MiningEvaluator, field_index) -> EnsembleSpec:
+def _chain_spec(compiled, ev: MiningEvaluator, field_index, lower=lower_binary_tree) -> EnsembleSpec:
     """modelChain [regression tree ensemble -> binary RegressionModel on its output] (the
     XGBoost/LightGBM binary-classification export) fused into one kernel + link epilogue."""
     mm = ev.mm
@@ -592,7 +596,7 @@ def _chain_spec(compiled, ev: MiningEvaluator, field_index) -> EnsembleSpec:
     norm = rm.normalization_method
     if norm not in LINKS or norm == "none":
         raise NotLowerable(f"calibrator normalizationMethod {norm!r} is host-only")
-    trees, w, a, b = _regression_ensemble(first, field_index)
+    trees, w, a, b = _regression_ensemble(first, field_index, lower)
     coef, icpt = t0.numeric[0].coefficient, t0.intercept
     cats = list(second.categories)
     # the chain's target is the calibrator's; category table in calibrator order
@@ -749,7 +753,7 @@ class TreePlan(DevicePlan):
     kind = "tree"
     _STATE = DevicePlan._STATE + ("depth", "n_trees", "layout", "P", "C", "general", "rec_words", "chunk_trees",
                                   "blob", "leaves", "roots", "has_dr", "table", "slots", "splits", "epi_args",
-                                  "variant")
+                                  "variant", "children", "preds", "pool", "trees_tab", "max_steps")
 
     WIDE_G = 4  # tree groups of the wide kernel (mirrors csrc)
 
@@ -758,13 +762,46 @@ class TreePlan(DevicePlan):
         super().__init__(compiled, device)
         if precision not in ("fp32", "fp8"):
             raise ValueError("tree leaf precision must be fp32 or fp8")
-        spec = ensemble_spec(compiled)
+        if layout == "general":
+            spec = self._general_spec(compiled)
+        else:
+            try:
+                spec = ensemble_spec(compiled)
+            except NotBinaryForm:
+                if layout != "auto":
+                    raise
+                spec, layout = self._general_spec(compiled), "general"
         self.spec = spec
         self.epi_args = dict(spec.epi)
         F = compiled.n_features
         depth = max(1, max(t.depth for t in spec.trees))
         self.depth = depth
         self.n_trees = len(spec.trees)
+        if layout == "general":
+            if precision == "fp8":
+                raise NotLowerable("fp8 leaves need the PERFECT layout")
+            from .general_tree import pack_general
+
+            g = pack_general(spec.trees, spec.weights, spec.P, compiled.schema)
+            self.layout, self.variant, self.rec_words, self.chunk_trees = "general", 0, 0, 0
+            self.P, self.C = spec.P, spec.C
+            self.general = 1 if spec.P > 1 else 0
+            self.blob = self._t(g["nodes"].reshape(-1))
+            self.children = self._t(g["children"])
+            self.preds = self._t(g["preds"].reshape(-1))
+            self.pool = self._t(g["pool"])
+            self.trees_tab = self._t(g["trees"].reshape(-1))
+            self.leaves = self._t(g["payload"].reshape(-1))
+            self.roots = None
+            self.max_steps = g["max_steps"]
+            self.has_dr = False
+            self.table = self._t(_label_table(spec.labels)) if spec.labels is not None else None
+            self.slots = self._t(np.zeros(self.n_trees, dtype=np.int32)) if self.general else None
+            self.splits = 1
+            self._partial = None
+            return
+        self.children = self.preds = self.pool = self.trees_tab = None
+        self.max_steps = 0
         if layout == "auto":
             NI, NL = (1 << depth) - 1, 1 << depth
             rec_bytes = 4 * (2 * NI + NL * spec.P + (NI + 31) // 32)
@@ -815,6 +852,15 @@ class TreePlan(DevicePlan):
         self.splits = splits
         self._partial = None
 
+    @staticmethod
+    def _general_spec(compiled) -> "EnsembleSpec":
+        from .general_tree import lower_general_tree
+
+        try:
+            return ensemble_spec(compiled, lower=lower_general_tree)
+        except NotBinary as e:  # pragma: no cover - the general lowering never raises NotBinary
+            raise NotLowerable(str(e)) from e
+
     def _post_state(self) -> None:
         self._partial = None
         self._args = {}
@@ -860,6 +906,9 @@ class TreePlan(DevicePlan):
         from ..ops._lib import TreeArgs, check, ptr, stream_handle
 
         n = X.shape[0]
+        if self.layout == "general":
+            self._launch_general(X, score, valid, stream, probs, row_valid, score2, valid2)
+            return
         s = splits if splits is not None else self._auto_splits(n)
         a = self._args_template(probs is not None)
         a.X = X.data_ptr()
@@ -879,6 +928,24 @@ class TreePlan(DevicePlan):
         rc = self.lib.pmml_tree_launch(stream_handle(stream), ctypes.byref(a), 0 if self.layout == "perfect" else 1,
                                        self.depth, 1 if self.has_dr else 0, s)
         check(rc, f"tree kernel ({self.layout}, depth {self.depth})")
+
+
+    def _launch_general(self, X, score, valid, stream, probs, row_valid, score2, valid2) -> None:
+        import ctypes
+
+        from ..ops._lib import GenTreeArgs, check, ptr, stream_handle
+
+        g = GenTreeArgs()
+        g.t = self._args_template(probs is not None)
+        g.t.X = X.data_ptr()
+        g.t.n_rows, g.t.n_feat, g.t.ldx = X.shape[0], X.shape[1], X.stride(0)
+        g.t.row_valid_in = ptr(row_valid)
+        g.t.score, g.t.valid, g.t.probs = _addr(score), _addr(valid), ptr(probs)
+        g.t.epi.score2, g.t.epi.valid2 = _addr(score2), _addr(valid2)
+        g.t.partial = None
+        g.nodes, g.children, g.preds = ptr(self.blob), ptr(self.children), ptr(self.preds)
+        g.pool, g.trees, g.max_steps = ptr(self.pool), ptr(self.trees_tab), int(self.max_steps)
+        check(self.lib.pmml_tree_general_launch(stream_handle(stream), ctypes.byref(g)), "general tree kernel")
 
 
 # --------------------------------------------------------------------------- dispatch

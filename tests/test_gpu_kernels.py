@@ -407,3 +407,44 @@ def test_categorical_splits_on_gpu(gpu, strategy):
     s, v = _gpu_np(plan, X)
     ref, vref = c.score_matrix_oracle(X)
     assert (v == vref).all() and (s[v] == ref[v]).all()
+
+
+@pytest.mark.parametrize("strategy,no_true", [("none", "returnNullPrediction"), ("lastPrediction", "returnLastPrediction"),
+                                              ("nullPrediction", "returnNullPrediction"),
+                                              ("defaultChild", "returnLastPrediction")])
+def test_general_tree_layout_on_gpu(gpu, strategy, no_true):
+    """Multiway / compound / set predicates through the predicate-VM kernel vs the fp64 oracle."""
+    from test_general_tree import general_inputs, general_tree_doc
+
+    from flink_jpmml_amd.runtime.compiled import CompiledPmml
+
+    for seed in range(2):
+        c = CompiledPmml.from_string(general_tree_doc(seed, strategy, no_true))
+        plan = c.plan(gpu)
+        assert plan.layout == "general"
+        X = general_inputs(20_000, seed)
+        s, v = _gpu_np(plan, X)
+        ref, vref = c.score_matrix_oracle(X)
+        assert (v == vref).all()
+        np.testing.assert_allclose(s[v], ref[v], rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("classification", [False, True])
+def test_general_tree_ensemble_on_gpu(gpu, classification):
+    from test_general_tree import general_inputs, general_tree_doc
+
+    from flink_jpmml_amd.runtime.compiled import CompiledPmml
+    from flink_jpmml_amd.runtime.plans import DevicePlan
+
+    c = CompiledPmml.from_string(general_tree_doc(5, "defaultChild", "returnLastPrediction", n_trees=25,
+                                                  classification=classification))
+    plan = c.plan(gpu)
+    X = general_inputs(20_000, 9)
+    s, v = _gpu_np(plan, X)
+    ref, vref = c.score_matrix_oracle(X)
+    assert (v == vref).all()
+    np.testing.assert_allclose(s[v], ref[v], rtol=1e-5, atol=1e-5)
+    meta, tensors = plan.export_state()
+    q = DevicePlan.from_state(meta, {k: t.clone() for k, t in tensors.items()}, gpu)
+    s2, v2 = _gpu_np(q, X)
+    assert (s2 == s).all() and (v2 == v).all()
