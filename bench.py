@@ -44,6 +44,7 @@ def parse_args(argv=None):
     p.add_argument("--rows", type=int, default=1 << 20, help="rows per GPU per step")
     p.add_argument("--micro-batch", type=int, default=1 << 19)
     p.add_argument("--pipeline-depth", type=int, default=3, help="input ring slots (H2D/compute overlap)")
+    p.add_argument("--h2d-streams", type=int, default=4, help="concurrent copy streams per micro-batch")
     p.add_argument("--objective", choices=["regression", "binary"], default="regression",
                    help="binary = modelChain GBDT -> logistic calibrator (BASELINE config 5)")
     p.add_argument("--precision", choices=["fp32", "fp8"], default="fp32",
@@ -109,7 +110,8 @@ def main(argv=None) -> int:
     X = torch.from_numpy(stream_matrix(args.rows, args.features, seed=1000 + ctx.rank)).pin_memory()
     score_h = torch.empty(args.rows, dtype=torch.float32).pin_memory()
     valid_h = torch.empty(args.rows, dtype=torch.uint8).pin_memory()
-    scorer = StreamingScorer(plan, micro_batch=args.micro_batch, depth=args.pipeline_depth, max_rows=args.rows)
+    scorer = StreamingScorer(plan, micro_batch=args.micro_batch, depth=args.pipeline_depth, max_rows=args.rows,
+                             h2d_streams=args.h2d_streams)
     gather_out = None
     if N > 1 and not args.no_allgather:
         gather_out = (torch.empty(args.rows * N, dtype=torch.float32, device=device),
@@ -208,6 +210,7 @@ def main(argv=None) -> int:
                 "parallelism": f"dp{N}",
                 "micro_batch": args.micro_batch,
                 "pipeline_depth": args.pipeline_depth,
+                "h2d_streams": args.h2d_streams,
                 "rows_per_gpu_per_step": args.rows,
                 "allgather_sink": bool(gather_out is not None),
                 "zero_copy_host_sink": bool(scorer.direct),
