@@ -317,6 +317,35 @@ def svm_pmml(n_features: int = 16, n_sv: int = 256, seed: int = 0, kernel: str =
     return out.getvalue()
 
 
+def kmeans_pmml(n_clusters: int = 64, n_features: int = 32, seed: int = 0, metric: str = "squaredEuclidean",
+                weighted: bool = False, compare: str = "absDiff") -> str:
+    """Centre-based ``ClusteringModel`` with ``n_clusters`` standard-normal centres (ids 1..K as the
+    predicted value); ``weighted`` adds random ``ClusteringField`` field weights."""
+    rng = np.random.default_rng(seed)
+    out = io.StringIO()
+    _header(out, f"synthetic k-means {n_clusters} clusters x {n_features} features")
+    out.write(f' <DataDictionary numberOfFields="{n_features + 1}">\n')
+    for j in range(n_features):
+        out.write(f'  <DataField name="f{j}" optype="continuous" dataType="float"/>\n')
+    out.write('  <DataField name="cluster" optype="categorical" dataType="string"/>\n </DataDictionary>\n')
+    out.write(f' <ClusteringModel modelName="kmeans" functionName="clustering" modelClass="centerBased" '
+              f'numberOfClusters="{n_clusters}">\n')
+    out.write('  <MiningSchema>\n   <MiningField name="cluster" usageType="predicted"/>\n')
+    for j in range(n_features):
+        out.write(f'   <MiningField name="f{j}"/>\n')
+    out.write('  </MiningSchema>\n')
+    out.write(f'  <ComparisonMeasure kind="distance"><{metric}/></ComparisonMeasure>\n')
+    for j in range(n_features):
+        w = f' fieldWeight="{_fnum(rng.uniform(0.25, 2.0))}"' if weighted else ""
+        out.write(f'  <ClusteringField field="f{j}" compareFunction="{compare}"{w}/>\n')
+    C = rng.standard_normal((n_clusters, n_features))
+    for k in range(n_clusters):
+        out.write(f'  <Cluster id="{k + 1}" name="c{k + 1}"><Array n="{n_features}" type="real">'
+                  + " ".join(_fnum(v) for v in C[k]) + '</Array></Cluster>\n')
+    out.write(' </ClusteringModel>\n</PMML>\n')
+    return out.getvalue()
+
+
 def stream_matrix(n_rows: int, n_features: int, seed: int = 0, missing_rate: float = 0.0) -> np.ndarray:
     """Synthetic fp32 record batch ``[rows, features]`` (standard normal; NaN = missing)."""
     rng = np.random.default_rng(seed)

@@ -219,6 +219,9 @@ def load(auto_build: bool = True) -> ctypes.CDLL:
         lib.pmml_memcpy_async.argtypes = [c_void_p, c_void_p, ctypes.c_size_t, c_int, c_void_p]
         lib.pmml_memcpy_async.restype = c_int
         lib.pmml_cluster_launch.argtypes = [c_void_p, ctypes.POINTER(ClusterArgs)]
+        lib.pmml_cluster_mfma_launch.restype = ctypes.c_int
+        lib.pmml_cluster_mfma_launch.argtypes = [c_void_p, ctypes.POINTER(ClusterArgs), c_void_p, c_void_p,
+                                                 ctypes.c_int, ctypes.c_int]
         lib.pmml_linear_launch.argtypes = [c_void_p, ctypes.POINTER(LinearArgs)]
         if hasattr(lib, "pmml_mlp_launch"):
             lib.pmml_mlp_launch.argtypes = [c_void_p, ctypes.POINTER(MlpArgs), c_int]

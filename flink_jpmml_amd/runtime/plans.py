@@ -326,11 +326,16 @@ def _label_table(labels: List[str]) -> np.ndarray:
 class ClusterPlan(DevicePlan):
     kind = "cluster"
     _STATE = DevicePlan._STATE + ("centers", "weights", "scales", "qweights", "cfun", "table", "metric_code",
-                                  "similarity", "p")
+                                  "similarity", "p", "variant", "wc", "cc")
     _METRICS = {"squaredEuclidean": 0, "euclidean": 1, "cityBlock": 2, "chebychev": 3, "minkowski": 4}
     _CF = {"absDiff": 0, "gaussSim": 1, "delta": 2, "equal": 3}
+    MFMA_MIN_K = 16  # below this the VALU kernel's per-cluster loop is as fast as a 32-wide MFMA tile
 
-    def __init__(self, compiled, device):
+    def __init__(self, compiled, device, cluster_variant: str = "auto", **_):
+        """``cluster_variant``: ``"valu"`` (exact per-cluster Σ w(x-c)², every metric), ``"mfma"``
+        (matrix-core ‖x‖² − 2x·c + ‖c‖², squared / plain Euclidean with absDiff only; rows with
+        missing values fall back to the exact form inside the kernel) or ``"auto"`` (MFMA when it
+        applies and K ≥ ``MFMA_MIN_K``)."""
         super().__init__(compiled, device)
         ev: ClusteringEvaluator = compiled.evaluator
         if ev.metric not in self._METRICS:
@@ -348,6 +353,33 @@ class ClusterPlan(DevicePlan):
         self.qweights = self._t(ev.missing_weights.astype(np.float32))
         self.cfun = self._t(np.array([self._CF[c] for c in ev.compare], dtype=np.int32))
         self.table = self._t(_label_table(ev.entity_ids))
+        mfma_ok = (self.similarity == 0 and self.metric_code in (0, 1)
+                   and all(c == "absDiff" for c in ev.compare) and compiled.n_features <= 128)
+        if cluster_variant not in ("auto", "valu", "mfma"):
+            raise ValueError(f"cluster_variant {cluster_variant!r}")
+        if cluster_variant == "mfma" and not mfma_ok:
+            raise NotLowerable("MFMA clustering needs squared/plain euclidean distance with absDiff")
+        use = cluster_variant == "mfma" or (cluster_variant == "auto" and mfma_ok
+                                            and len(ev.centers) >= self.MFMA_MIN_K)
+        self.variant = "mfma" if use else "valu"
+        self.wc = self.cc = None
+        if use:
+            wc, cc = self.mfma_operands(ev.centers, ev.weights)
+            self.wc, self.cc = self._t(wc), self._t(cc)
+
+    @staticmethod
+    def mfma_operands(centers: np.ndarray, weights: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+        """``wc [Kp][Fp] = w ∘ c`` zero padded to the 32×2 MFMA tile, ``cc [Kp] = Σ_f w_f c_f²``
+        (fp64 sum, +inf on padded clusters so they never win the argmin)."""
+        K, F = centers.shape
+        Kp, Fp = -(-K // 32) * 32, -(-F // 2) * 2
+        wc = np.zeros((Kp, Fp), dtype=np.float32)
+        c32 = centers.astype(np.float32).astype(np.float64)
+        w32 = weights.astype(np.float32).astype(np.float64)
+        wc[:K, :F] = (c32 * w32).astype(np.float32)
+        cc = np.full(Kp, np.inf, dtype=np.float32)
+        cc[:K] = (c32 * c32 * w32).sum(axis=1).astype(np.float32)
+        return wc, cc
 
     def launch(self, X, score, valid, stream=None, probs=None, label=None, affinity=None) -> None:
         from ..ops._lib import ClusterArgs, check, ptr, stream_handle
@@ -362,7 +394,12 @@ class ClusterPlan(DevicePlan):
         a.score, a.valid, a.label, a.affinity = ptr(score), ptr(valid), ptr(label), ptr(affinity)
         import ctypes
 
-        check(self.lib.pmml_cluster_launch(stream_handle(stream), ctypes.byref(a)), "cluster kernel")
+        if self.variant == "mfma":
+            Kp, Fp = self.wc.shape
+            check(self.lib.pmml_cluster_mfma_launch(stream_handle(stream), ctypes.byref(a), ptr(self.wc),
+                                                    ptr(self.cc), Kp, Fp), "cluster mfma kernel")
+        else:
+            check(self.lib.pmml_cluster_launch(stream_handle(stream), ctypes.byref(a)), "cluster kernel")
 
 
 # --------------------------------------------------------------------------- linear
@@ -967,7 +1004,7 @@ def compile_plan(compiled, device, **opts) -> DevicePlan:
             return DerivedPlan(compiled, device, layout, **opts)
         compiled = FieldView(compiled, layout, prepared=False)
     if isinstance(ev, ClusteringEvaluator):
-        return ClusterPlan(compiled, device)
+        return ClusterPlan(compiled, device, **opts)
     if isinstance(ev, (TreeEvaluator, MiningEvaluator)):
         return TreePlan(compiled, device, **opts)
     if isinstance(ev, RegressionEvaluator):

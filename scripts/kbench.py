@@ -14,7 +14,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--model", default="gbdt", choices=["gbdt", "gbdt-binary", "rf", "kmeans", "mlp", "svm", "lr", "pcie"])
+    p.add_argument("--model", default="gbdt", choices=["gbdt", "gbdt-binary", "rf", "kmeans", "kmeans-big", "mlp", "svm", "lr", "pcie"])
     p.add_argument("--rows", type=int, default=1 << 20)
     p.add_argument("--iters", type=int, default=20)
     p.add_argument("--trees", type=int, default=1000)
@@ -24,6 +24,7 @@ def main():
     p.add_argument("--layout", default="auto")
     p.add_argument("--lds-budget", type=int, default=80 * 1024)
     p.add_argument("--variant", default="auto")
+    p.add_argument("--clusters", type=int, default=256)
     args = p.parse_args()
     import numpy as np
     import torch
@@ -56,6 +57,8 @@ def main():
         txt = synth.mlp_pmml(n_features=args.features)
     elif args.model == "svm":
         txt = synth.svm_pmml(n_features=args.features)
+    elif args.model == "kmeans-big":
+        txt = synth.kmeans_pmml(n_clusters=args.clusters, n_features=args.features, weighted=True)
     elif args.model == "lr":
         txt = synth.iris_logistic_pmml()
     else:
@@ -66,6 +69,8 @@ def main():
     opts = {}
     if args.model.startswith(("gbdt", "rf")):
         opts = dict(layout=args.layout, lds_budget=args.lds_budget, variant=args.variant)
+    elif args.model == "kmeans-big":
+        opts = dict(cluster_variant=args.variant)
     plan = c.plan("cuda:0", **opts)
     F = c.n_features
     X = torch.from_numpy(synth.stream_matrix(args.rows, F, seed=1, missing_rate=args.missing)).cuda()
