@@ -346,6 +346,115 @@ def kmeans_pmml(n_clusters: int = 64, n_features: int = 32, seed: int = 0, metri
     return out.getvalue()
 
 
+_LEVELS = ("red", "green", "blue")
+
+
+def _mixed_dictionary(out: io.StringIO, F: int, target: str, categories: Optional[List[str]]) -> None:
+    out.write(f' <DataDictionary numberOfFields="{F + 2}">\n')
+    for j in range(F):
+        out.write(f'  <DataField name="f{j}" optype="continuous" dataType="double"/>\n')
+    out.write('  <DataField name="color" optype="categorical" dataType="string">'
+              + "".join(f'<Value value="{v}"/>' for v in _LEVELS) + '</DataField>\n')
+    if categories is None:
+        out.write(f'  <DataField name="{target}" optype="continuous" dataType="double"/>\n')
+    else:
+        out.write(f'  <DataField name="{target}" optype="categorical" dataType="string">'
+                  + "".join(f'<Value value="{c}"/>' for c in categories) + '</DataField>\n')
+    out.write(' </DataDictionary>\n')
+
+
+def _mixed_schema(out: io.StringIO, F: int, target: str) -> None:
+    out.write(f'  <MiningSchema>\n   <MiningField name="{target}" usageType="target"/>\n')
+    for j in range(F):
+        out.write(f'   <MiningField name="f{j}"/>\n')
+    out.write('   <MiningField name="color"/>\n  </MiningSchema>\n')
+
+
+def regression_design_pmml(n_features: int = 4, classes: int = 0, normalization: str = "none",
+                           seed: int = 0) -> str:
+    """``RegressionModel`` with exponents, a categorical predictor (string field ``color``) and
+    interaction terms — the non-dense tables the design-matrix lowering handles. ``classes > 0``:
+    one table per class."""
+    rng = np.random.default_rng(seed)
+    out = io.StringIO()
+    _header(out, "synthetic regression with categorical predictors and terms")
+    cats = [str(k) for k in range(classes)] if classes else None
+    _mixed_dictionary(out, n_features, "y", cats)
+    fn = "classification" if classes else "regression"
+    out.write(f' <RegressionModel functionName="{fn}" normalizationMethod="{normalization}">\n')
+    _mixed_schema(out, n_features, "y")
+    for k in range(max(classes, 1)):
+        tc = f' targetCategory="{k}"' if classes else ""
+        out.write(f'  <RegressionTable intercept="{rng.normal():.6g}"{tc}>\n')
+        for j in range(n_features):
+            e = ' exponent="2"' if j % 3 == 1 else ""
+            out.write(f'   <NumericPredictor name="f{j}"{e} coefficient="{rng.normal() * 0.5:.6g}"/>\n')
+        for v in _LEVELS[:2]:
+            out.write(f'   <CategoricalPredictor name="color" value="{v}" coefficient="{rng.normal():.6g}"/>\n')
+        out.write(f'   <PredictorTerm coefficient="{rng.normal() * 0.3:.6g}"><FieldRef field="f0"/>'
+                  f'<FieldRef field="f{n_features - 1}"/></PredictorTerm>\n')
+        out.write('  </RegressionTable>\n')
+    out.write(' </RegressionModel>\n</PMML>\n')
+    return out.getvalue()
+
+
+def glm_pmml(model_type: str = "generalizedLinear", link: str = "log", n_features: int = 3, seed: int = 0,
+             classes: int = 3) -> str:
+    """``GeneralRegressionModel`` (PPMatrix / ParamMatrix) with covariates ``f*`` (one squared),
+    factor ``color`` and a covariate x factor interaction. ``multinomialLogistic`` gets
+    ``classes`` categories, the last one the reference."""
+    rng = np.random.default_rng(seed)
+    out = io.StringIO()
+    _header(out, f"synthetic GLM {model_type} {link}")
+    multi = model_type == "multinomialLogistic"
+    cats = [str(c) for c in range(classes)] if multi else None
+    _mixed_dictionary(out, n_features, "y", cats)
+    fn = "classification" if multi else "regression"
+    attrs = f' targetReferenceCategory="{classes - 1}"' if multi else f' linkFunction="{link}"'
+    if link == "power" and not multi:
+        attrs += ' linkParameter="0"'
+    out.write(f' <GeneralRegressionModel functionName="{fn}" modelType="{model_type}"{attrs} '
+              f'offsetValue="0.25">\n')
+    _mixed_schema(out, n_features, "y")
+    params = ["p0"] + [f"p{j + 1}" for j in range(n_features)] + ["pc1", "pc2", "px"]
+    out.write('  <ParameterList>' + "".join(f'<Parameter name="{p}"/>' for p in params) + '</ParameterList>\n')
+    out.write('  <FactorList><Predictor name="color"/></FactorList>\n')
+    out.write('  <CovariateList>' + "".join(f'<Predictor name="f{j}"/>' for j in range(n_features))
+              + '</CovariateList>\n')
+    out.write('  <PPMatrix>\n')
+    for j in range(n_features):
+        e = "2" if j == 1 else "1"
+        out.write(f'   <PPCell value="{e}" predictorName="f{j}" parameterName="p{j + 1}"/>\n')
+    out.write('   <PPCell value="red" predictorName="color" parameterName="pc1"/>\n')
+    out.write('   <PPCell value="green" predictorName="color" parameterName="pc2"/>\n')
+    out.write('   <PPCell value="blue" predictorName="color" parameterName="px"/>\n')
+    out.write('   <PPCell value="1" predictorName="f0" parameterName="px"/>\n')
+    out.write('  </PPMatrix>\n  <ParamMatrix>\n')
+    for c in (cats[:-1] if multi else [None]):
+        tc = f' targetCategory="{c}"' if c is not None else ""
+        for p in params:
+            out.write(f'   <PCell parameterName="{p}"{tc} beta="{rng.normal() * 0.3:.6g}"/>\n')
+    out.write('  </ParamMatrix>\n </GeneralRegressionModel>\n</PMML>\n')
+    return out.getvalue()
+
+
+def mixed_records(n_rows: int, n_features: int, seed: int = 0, missing_rate: float = 0.0) -> Tuple[list, np.ndarray]:
+    """Records for the ``_mixed_dictionary`` models: ``(list of dicts, [rows, F+1] float matrix with
+    the color vocabulary code in the last column)``."""
+    rng = np.random.default_rng(seed)
+    X = rng.standard_normal((n_rows, n_features + 1))
+    X[:, -1] = rng.integers(0, len(_LEVELS), n_rows)
+    if missing_rate > 0:
+        X[rng.random(X.shape) < missing_rate] = np.nan
+    recs = []
+    for r in X:
+        d = {f"f{j}": float(r[j]) for j in range(n_features) if not np.isnan(r[j])}
+        if not np.isnan(r[-1]):
+            d["color"] = _LEVELS[int(r[-1])]
+        recs.append(d)
+    return recs, X
+
+
 def stream_matrix(n_rows: int, n_features: int, seed: int = 0, missing_rate: float = 0.0) -> np.ndarray:
     """Synthetic fp32 record batch ``[rows, features]`` (standard normal; NaN = missing)."""
     rng = np.random.default_rng(seed)

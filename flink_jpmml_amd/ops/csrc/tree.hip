@@ -46,13 +46,17 @@ struct TreeArgs {
   const float* leaves;          // pointer layout: [n_leaves][P]
   const int* tree_slot;         // general accumulation: slot per tree
   int n_trees, rec_words, chunk_trees, P;
-  int C, trees_per_split, general, variant;  // variant 1: wide perfect kernel, 2: wide + fp8 leaves
+  int C, trees_per_split, general, variant;  // variant & 3: 1 wide perfect kernel, 2 wide + fp8 leaves;
+                                             // | VAR_NAN_FAST | VAR_NAN_PLANES (wide kernel only)
   Epilogue epi;
   float* score;
   uint8_t* valid;
   float* probs;
   float* partial;               // split mode: [splits][C+1][n_rows]
 };
+constexpr int VAR_NAN_FAST = 4;    // wide kernel: take the fast path even on tiles with missing values
+constexpr int VAR_NAN_PLANES = 8;  // ... with a second feature plane (NaN -> +inf) for default-right nodes
+
 
 __device__ __forceinline__ void finish_row(const TreeArgs& a, float acc0, const float* accl, int split,
                                            bool general, int row, bool row_ok) {
@@ -501,7 +505,8 @@ __global__ __launch_bounds__(TB * G, 1) void tree_perfect_wide_kernel(TreeArgs a
   const int rw = a.rec_words;
   const int chunk_words = a.chunk_trees * rw;
   float* feat = reinterpret_cast<float*>(smem);
-  uint32_t* tbuf0 = smem + a.n_feat * TB;
+  const bool planes2 = (a.variant & VAR_NAN_PLANES) != 0;
+  uint32_t* tbuf0 = smem + (planes2 ? 2 : 1) * a.n_feat * TB;
   uint32_t* tbuf1 = tbuf0 + chunk_words;
   int* bad = reinterpret_cast<int*>(tbuf1 + chunk_words);
   int* any_missing = bad + TB;
@@ -540,6 +545,7 @@ __global__ __launch_bounds__(TB * G, 1) void tree_perfect_wide_kernel(TreeArgs a
         miss = miss || (x != x);
       }
       feat[f * TB + r] = x;
+      if (planes2) feat[(F + f) * TB + r] = (x != x) ? __builtin_inff() : x;  // NaN-goes-right plane
       if (b) bad[r] = 1;
     }
     if (__any(miss) && lane == 0) *any_missing = 1;
@@ -547,7 +553,9 @@ __global__ __launch_bounds__(TB * G, 1) void tree_perfect_wide_kernel(TreeArgs a
   PF4_STORE(tbuf0, n16, T)
   __syncthreads();
 
-  const bool missing = *any_missing != 0;
+  // VAR_NAN_FAST: missing values need no per-node work — either no node sends NaN right (a NaN
+  // compare is false: left), or the node's feature offset points into the NaN -> +inf plane
+  const bool missing = *any_missing != 0 && (a.variant & VAR_NAN_FAST) == 0;
   float acc = 0.f;
   const char* feat_lane = reinterpret_cast<const char*>(feat + r_local);
   int c = 0;
@@ -872,9 +880,10 @@ constexpr int WIDE_G = 4;
 template <int D>
 int launch_perfect(hipStream_t st, const TreeArgs& a, dim3 grid, size_t lds) {
   int err = 0;
-  if (!a.general && (a.variant == 1 || a.variant == 2)) {
-    const bool leaf8 = a.variant == 2;
-    const size_t lds_w = lds + (size_t)WIDE_G * TB * 4;
+  const int base = a.variant & 3;
+  if (!a.general && (base == 1 || base == 2)) {
+    const bool leaf8 = base == 2;
+    const size_t lds_w = lds + (size_t)WIDE_G * TB * 4 + ((a.variant & VAR_NAN_PLANES) ? (size_t)a.n_feat * TB * 4 : 0);
     if (lds_w > 160 * 1024) return -5;
     if ((size_t)a.chunk_trees * a.rec_words > (size_t)TB * WIDE_G * 4 * 4) return -9;
     if (a.P != 1 || a.rec_words != (leaf8 ? perfect_rec_words8(D) : perfect_rec_words(D, 1))) return -10;
@@ -889,7 +898,7 @@ int launch_perfect(hipStream_t st, const TreeArgs& a, dim3 grid, size_t lds) {
     }
     return err;
   }
-  if (a.variant == 2) return -10;  // fp8 leaves only on the wide (single-accumulator) kernel
+  if (base == 2 || (a.variant & ~3)) return -10;  // fp8 leaves / NaN planes: wide kernel only
   if (a.general) {
     err = prepare_launch(tree_perfect_kernel<D, true, 4>, lds);
     if (!err) hipLaunchKernelGGL((tree_perfect_kernel<D, true, 4>), grid, dim3(TB), lds, st, a);
@@ -921,7 +930,7 @@ PMML_API int pmml_tree_launch(hipStream_t stream, const TreeArgs* args, int layo
   const size_t acc_lds = a.general ? (size_t)a.C * TB * 4 : 0;
   if (layout == 0) {
     if (a.n_feat > 64) return -4;
-    if (a.variant == 0 && (size_t)a.chunk_trees * a.rec_words > (size_t)TB * 4 * PREFETCH_Q) return -9;
+    if ((a.variant & 3) == 0 && (size_t)a.chunk_trees * a.rec_words > (size_t)TB * 4 * PREFETCH_Q) return -9;
     const size_t lds = (size_t)a.n_feat * TB * 4 + 2 * (size_t)a.chunk_trees * a.rec_words * 4 + (TB + 4) * 4 + acc_lds;
     if (lds > 160 * 1024) return -5;
     switch (depth) {
@@ -938,7 +947,7 @@ PMML_API int pmml_tree_launch(hipStream_t stream, const TreeArgs* args, int layo
       default: return -6;
     }
   } else {
-    if (a.variant == 2) return -10;
+    if (a.variant != 0) return -10;
     const bool feat_lds = a.n_feat <= 64;
     const size_t lds = (feat_lds ? (size_t)a.n_feat * TB * 4 : 0) + TB * 4 + acc_lds;
     if (a.general) {

@@ -319,6 +319,7 @@ class FieldLayout:
     columns: List[str]                 # the model kernel's input columns, in order
     field_index: Dict[str, int]        # every name the model may reference -> kernel column
     program: Optional[DerivedProgram]  # None: the kernel reads the raw input matrix
+    evaluator: Optional[object] = None  # replaces the model's evaluator behind the view (design.py)
 
 
 def plan_field_layout(compiled, allow_alias: bool = True) -> FieldLayout:
@@ -342,6 +343,17 @@ def plan_field_layout(compiled, allow_alias: bool = True) -> FieldLayout:
             fi = dict(index)
             fi.update({n: index[src] for n, src in alias.items()})
             return FieldLayout(active, fi, None)
+    return build_program_layout(compiled, defs, refs)
+
+
+def build_program_layout(compiled, defs: Dict[str, ir.DerivedField], refs: List[str]) -> FieldLayout:
+    """Derive program computing every name of ``refs`` that is a derived field (inputs pass
+    through); the kernel's columns are ``refs`` that resolve, in order."""
+    active = list(compiled.active_fields)
+    index = {f: i for i, f in enumerate(active)}
+    schema = compiled.schema
+    refs = list(dict.fromkeys(refs))
+    needed = [r for r in refs if r in defs and r not in index]
     # evaluation order: depth-first post-order over the derived dependencies
     order: List[str] = []
     state: Dict[str, int] = {}
@@ -514,6 +526,8 @@ class FieldView:
         self.field_index = dict(layout.field_index)
         self.prepared_inputs = prepared
         self.mining_fields = {} if prepared else dict(compiled.mining_fields)
+        if layout.evaluator is not None:
+            self.evaluator = layout.evaluator
 
     @property
     def n_features(self) -> int:

@@ -700,6 +700,24 @@ def _perfect_pack(trees: List[BinaryTree], weights: List[float], P: int, D: int)
     return blob, rec, has_dr
 
 
+VAR_NAN_FAST, VAR_NAN_PLANES = 4, 8  # mirrors csrc/tree.hip
+
+
+def _nan_planes(blob: np.ndarray, D: int, F: int) -> np.ndarray:
+    """Point every default-right node of a P=1 PERFECT blob at the second feature plane (the
+    wide kernel stages it with NaN -> +inf): ``x >= T`` then sends a missing value right at those
+    nodes and left (NaN compares false) everywhere else — the default direction costs nothing
+    per node, so tiles with missing values keep the fast traversal."""
+    NI, NL = (1 << D) - 1, 1 << D
+    ndr = (NI + 31) // 32
+    out = blob.copy()
+    words = out[:, 2 * NI + NL: 2 * NI + NL + ndr]
+    for p in range(NI):
+        dr = ((words[:, p >> 5] >> np.uint32(p & 31)) & np.uint32(1)).astype(bool)
+        out[dr, 2 * p + 1] += np.uint32(F * TB * 4)
+    return out
+
+
 FP8_MAX = 448.0  # largest finite OCP e4m3fn value
 
 
@@ -795,8 +813,13 @@ class TreePlan(DevicePlan):
     WIDE_G = 4  # tree groups of the wide kernel (mirrors csrc)
 
     def __init__(self, compiled, device, layout: str = "auto", lds_budget: int = 80 * 1024, splits: int = 0,
-                 variant: str = "auto", precision: str = "fp32"):
+                 variant: str = "auto", precision: str = "fp32", nan_mode: str = "auto"):
+        """``nan_mode`` (wide PERFECT kernel): ``"auto"`` keeps tiles with missing values on the fast
+        traversal whenever the ensemble has no null-on-missing trees (default-right nodes read a
+        NaN -> +inf second feature plane, :func:`_nan_planes`); ``"off"``: per-node missing test."""
         super().__init__(compiled, device)
+        if nan_mode not in ("auto", "off"):
+            raise ValueError("nan_mode must be 'auto' or 'off'")
         if precision not in ("fp32", "fp8"):
             raise ValueError("tree leaf precision must be fp32 or fp8")
         if layout == "general":
@@ -851,6 +874,13 @@ class TreePlan(DevicePlan):
             if variant == "auto":
                 variant = "narrow" if self.general else "wide"
             self.variant = 1 if variant == "wide" else 0
+            nan_flags = 0
+            if self.variant == 1 and nan_mode == "auto" and not any(t.null_missing for t in spec.trees):
+                if not has_dr:
+                    nan_flags = VAR_NAN_FAST
+                elif precision != "fp8" or (2 * F - 1) * TB * 4 < (1 << 16):  # fp8 metas: 16-bit offsets
+                    blob = _nan_planes(blob, depth, F)
+                    nan_flags = VAR_NAN_FAST | VAR_NAN_PLANES
             if precision == "fp8":
                 # e4m3 leaves in the last-level metas, global scale folded into the epilogue
                 if self.general or self.variant != 1:
@@ -858,10 +888,12 @@ class TreePlan(DevicePlan):
                 blob, rec, scale = _leaf8_pack(blob, depth)
                 self.epi_args["a"] = self.epi_args.get("a", 1.0) * scale
                 self.variant = 2
+            self.variant |= nan_flags
             self.rec_words = rec
-            if self.variant in (1, 2):
-                # one 1024-thread workgroup per CU: features + two chunk buffers + [G][256] partials
-                fixed = F * TB * 4 + (TB + 4) * 4 + self.WIDE_G * TB * 4
+            if self.variant & 3 in (1, 2):
+                # one 1024-thread workgroup per CU: feature plane(s) + two chunk buffers + [G][256] partials
+                planes = 2 if self.variant & VAR_NAN_PLANES else 1
+                fixed = planes * F * TB * 4 + (TB + 4) * 4 + self.WIDE_G * TB * 4
                 budget = 156 * 1024 - fixed
                 per_chunk = min(budget // 2, 64 * 1024)
             else:
@@ -995,6 +1027,13 @@ def compile_plan(compiled, device, **opts) -> DevicePlan:
     if not compiled.target_fields:
         raise NotLowerable("model has no target field (every record scores EmptyScore)")
     if not getattr(compiled, "fields_resolved", False):
+        from .design import design_layout, needs_design
+
+        if needs_design(ev):  # categorical predictors / terms / GLM -> design columns + dense GEMV
+            from .derive import DerivedPlan
+
+            layout, _ = design_layout(compiled)
+            return DerivedPlan(compiled, device, layout, **opts)
         # derived fields: pure casts alias their input column (tree kernels), anything else runs
         # as a derive-kernel pass in front of the model kernel (runtime/derive.py)
         from .derive import DerivedPlan, FieldView, plan_field_layout
@@ -1009,6 +1048,10 @@ def compile_plan(compiled, device, **opts) -> DevicePlan:
         return TreePlan(compiled, device, **opts)
     if isinstance(ev, RegressionEvaluator):
         return LinearPlan(compiled, device)
+    from ..models.regression import GeneralRegressionEvaluator
+
+    if isinstance(ev, GeneralRegressionEvaluator):
+        raise NotLowerable("GeneralRegressionModel lowers through design columns (runtime/design.py)")
     from ..models.neural import NeuralEvaluator
     from ..models.svm import SvmEvaluator
 

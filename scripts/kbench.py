@@ -25,6 +25,7 @@ def main():
     p.add_argument("--lds-budget", type=int, default=80 * 1024)
     p.add_argument("--variant", default="auto")
     p.add_argument("--clusters", type=int, default=256)
+    p.add_argument("--nan-mode", default="auto")
     args = p.parse_args()
     import numpy as np
     import torch
@@ -68,7 +69,7 @@ def main():
     c = CompiledPmml.from_string(txt)
     opts = {}
     if args.model.startswith(("gbdt", "rf")):
-        opts = dict(layout=args.layout, lds_budget=args.lds_budget, variant=args.variant)
+        opts = dict(layout=args.layout, lds_budget=args.lds_budget, variant=args.variant, nan_mode=args.nan_mode)
     elif args.model == "kmeans-big":
         opts = dict(cluster_variant=args.variant)
     plan = c.plan("cuda:0", **opts)

@@ -1,0 +1,94 @@
+"""Design-matrix lowering of RegressionModel (categorical predictors, terms, exponents) and
+GeneralRegressionModel (covariates, factors, interactions; identity / log / logit / power links,
+multinomial logistic) — ``runtime/design.py``.
+
+CPU: the design derive program (numpy twin :func:`derive.emulate`) + the dense tables reproduce the
+float64 oracle; GPU: the DerivedPlan (derive kernel → linear kernel) against the oracle.
+"""
+
+import numpy as np
+import pytest
+
+from flink_jpmml_amd.bench.synth import glm_pmml, mixed_records, regression_design_pmml
+from flink_jpmml_amd.runtime.compiled import CompiledPmml
+
+CASES = {
+    "reg": lambda: regression_design_pmml(),
+    "reg-logit": lambda: regression_design_pmml(normalization="logit"),
+    "reg-softmax": lambda: regression_design_pmml(classes=3, normalization="softmax"),
+    "reg-binary": lambda: regression_design_pmml(classes=2, normalization="logit"),
+    "glm-log": lambda: glm_pmml(link="log"),
+    "glm-logit": lambda: glm_pmml(link="logit"),
+    "glm-identity": lambda: glm_pmml(link="identity"),
+    "glm-power0": lambda: glm_pmml(link="power"),
+    "glm-general-linear": lambda: glm_pmml(model_type="generalLinear"),
+    "glm-multinomial": lambda: glm_pmml(model_type="multinomialLogistic"),
+}
+
+
+def _data(c, n=3000, missing=0.05, seed=0):
+    _, X = mixed_records(n, len(c.active_fields) - 1, seed=seed, missing_rate=missing)
+    return X
+
+
+@pytest.mark.parametrize("name", list(CASES))
+def test_design_program_matches_oracle(name):
+    from flink_jpmml_amd.runtime.derive import emulate
+    from flink_jpmml_amd.runtime.design import design_layout, needs_design
+
+    c = CompiledPmml.from_string(CASES[name]())
+    assert needs_design(c.evaluator)
+    layout, dense = design_layout(c)
+    assert dense.is_dense_linear() and layout.program is not None
+    assert list(layout.columns) == list(dense.numeric_fields)
+    X = _data(c)
+    P, ok = c.prepare(X)
+    D = emulate(layout.program, P).astype(np.float64)
+    W, b = dense.dense_weights()
+    res = dense.finish(D @ W + b, ok & ~np.isnan(D).any(axis=1))
+    ref, vref = c.score_matrix_oracle(X)
+    assert (res.valid == vref).all()
+    if res.kind == "classification":  # categories are "0".."K-1": the index is the label
+        assert (res.value[vref] == ref[vref]).mean() > 0.999
+    else:
+        assert np.allclose(res.value[vref], ref[vref], rtol=1e-5, atol=1e-5)
+
+
+def test_glm_oracle_semantics():
+    """Hand check of the GLM oracle on one record: eta = offset + Σ beta·design, log link."""
+    c = CompiledPmml.from_string(glm_pmml(link="log"))
+    gm = c.evaluator.gm
+    beta = {p: b for p, _, b in gm.p_cells}
+    x = np.array([[0.5, -1.0, 2.0, 2.0]])  # color code 2 = blue
+    eta = gm.offset_value + beta["p0"] + beta["p1"] * 0.5 + beta["p2"] * 1.0 + beta["p3"] * 2.0 + beta["px"] * 0.5
+    s, v = c.score_matrix_oracle(x)
+    assert v[0] and np.isclose(s[0], np.exp(eta))
+
+
+def test_design_not_lowerable_power_link():
+    from flink_jpmml_amd.runtime.design import design_layout
+    from flink_jpmml_amd.runtime.plans import NotLowerable
+
+    txt = glm_pmml(link="power").replace('linkParameter="0"', 'linkParameter="0.5"')
+    with pytest.raises(NotLowerable):
+        design_layout(CompiledPmml.from_string(txt))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", list(CASES))
+def test_design_plan_on_gpu(gpu, name):
+    from flink_jpmml_amd.runtime.derive import DerivedPlan
+    from flink_jpmml_amd.runtime.plans import LinearPlan
+
+    c = CompiledPmml.from_string(CASES[name]())
+    plan = c.plan(gpu)
+    assert isinstance(plan, DerivedPlan) and isinstance(plan.inner, LinearPlan)
+    X = _data(c, n=20000, seed=1)
+    s, v = plan.score(X)
+    s, v = s.cpu().numpy(), v.cpu().numpy()
+    ref, vref = c.score_matrix_oracle(X)
+    assert (v == vref).all()
+    if plan.inner.table is not None:
+        assert (s[v] == ref[v]).mean() > 0.999
+    else:
+        assert np.allclose(s[v], ref[v], rtol=1e-4, atol=1e-4)

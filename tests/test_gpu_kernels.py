@@ -372,7 +372,7 @@ def test_fp8_leaf_chain_on_gpu(gpu):
 
     c = CompiledPmml.from_string(gbdt_pmml(n_trees=300, depth=6, n_features=24, seed=8, objective="binary"))
     p8 = c.plan(gpu, precision="fp8")
-    assert p8.variant == 2 and p8.rec_words < c.plan(gpu).rec_words
+    assert p8.variant & 3 == 2 and p8.rec_words < c.plan(gpu).rec_words
     X = stream_matrix(30_000, 24, seed=1)
     probs = torch_probs = None
     import torch
@@ -390,6 +390,29 @@ def test_fp8_leaf_chain_on_gpu(gpu):
     ref, vref = c.score_matrix_oracle(X)
     assert v8.bool().all().item() and vref.all()
     assert (s8.cpu().numpy() == ref).mean() > 0.97  # labels vs the fp64 oracle on fp32 leaves
+
+
+@pytest.mark.parametrize("precision,feat", [("fp32", 32), ("fp32", 48), ("fp8", 24), ("fp8", 40)])
+def test_nan_planes_match_per_node_missing_path(gpu, precision, feat):
+    """Tiles with missing values: the NaN-plane fast traversal == the per-node missing test
+    (bit-identical scores: same trees, same summation order)."""
+    from flink_jpmml_amd.bench.synth import gbdt_pmml, stream_matrix
+    from flink_jpmml_amd.runtime.compiled import CompiledPmml
+    from flink_jpmml_amd.runtime.plans import VAR_NAN_FAST, VAR_NAN_PLANES
+
+    c = CompiledPmml.from_string(gbdt_pmml(n_trees=120, depth=6, n_features=feat, seed=feat))
+    fast = c.plan(gpu, precision=precision)
+    slow = c.plan(gpu, precision=precision, nan_mode="off")
+    assert fast.variant & VAR_NAN_FAST and not slow.variant & VAR_NAN_FAST
+    if precision == "fp8" and feat > 32:
+        assert not fast.variant & VAR_NAN_PLANES  # 16-bit offsets of the fp8 metas
+    X = stream_matrix(40_000, feat, seed=2, missing_rate=0.03)
+    s1, v1 = _gpu_np(fast, X)
+    s0, v0 = _gpu_np(slow, X)
+    assert (v1 == v0).all() and np.array_equal(s1[v1], s0[v0])
+    if precision == "fp32":
+        ref, vref = c.score_matrix_oracle(X)
+        assert (v1 == vref).all() and np.max(np.abs(s1 - ref)) < 2e-5 * 1.2
 
 
 @pytest.mark.parametrize("strategy", ["defaultChild", "nullPrediction"])

@@ -8,7 +8,7 @@ import pytest
 from flink_jpmml_amd.bench.synth import gbdt_pmml, random_forest_pmml, stream_matrix
 from flink_jpmml_amd.models.tree import OP_GE, OP_GT, OP_LE, OP_LT
 from flink_jpmml_amd.runtime.compiled import CompiledPmml
-from flink_jpmml_amd.runtime.plans import TB, _perfect_pack, _pointer_pack, canonical_threshold, ensemble_spec
+from flink_jpmml_amd.runtime.plans import TB, _nan_planes, _perfect_pack, _pointer_pack, canonical_threshold, ensemble_spec
 
 
 def emulate_perfect(c, X):
@@ -90,12 +90,16 @@ def test_perfect_layout_emulation_matches_oracle(kind):
         assert (out == ref).all()
 
 
-def emulate_perfect_fast(c, X):
+def emulate_perfect_fast(c, X, nan_planes=False):
     """Byte-address form used by the wide kernel's fast path (tree.hip::traverse_fast_g): node
-    address u' = 2u + (8 - b0) + 8r, leaf pair at u + 8 + 8*NI - 4*NL on the last level."""
+    address u' = 2u + (8 - b0) + 8r, leaf pair at u + 8 + 8*NI - 4*NL on the last level.
+    ``nan_planes``: default-right nodes read the second (NaN -> +inf) feature plane."""
     spec = ensemble_spec(c)
     D = max(t.depth for t in spec.trees)
     blob, rec, _ = _perfect_pack(spec.trees, spec.weights, 1, D)
+    if nan_planes:
+        blob = _nan_planes(blob, D, X.shape[1])
+        X = np.concatenate([X, np.where(np.isnan(X), np.inf, X)], axis=1)
     mem = blob.reshape(-1)
     NI, NL = (1 << D) - 1, 1 << D
     C = 8 + 8 * NI - 4 * NL
@@ -120,6 +124,16 @@ def test_wide_fast_path_addressing(depth):
     X = stream_matrix(257, 7, seed=1)
     _, ref = emulate_perfect(c, X)
     np.testing.assert_array_equal(emulate_perfect_fast(c, X), ref[:, 0])
+
+
+@pytest.mark.parametrize("depth", [2, 6])
+def test_nan_planes_fast_path_matches_missing_path(depth):
+    """Missing values on the fast path: the default direction is encoded in the feature plane."""
+    c = CompiledPmml.from_string(gbdt_pmml(n_trees=20, depth=depth, n_features=9, seed=depth + 10))
+    X = stream_matrix(500, 9, seed=3, missing_rate=0.2)
+    _, ref = emulate_perfect(c, X)
+    np.testing.assert_array_equal(emulate_perfect_fast(c, X, nan_planes=True), ref[:, 0])
+    assert not np.array_equal(emulate_perfect_fast(c, X), ref[:, 0])  # without the planes: wrong
 
 
 def test_pointer_layout_emulation_matches_oracle():
