@@ -438,6 +438,147 @@ def glm_pmml(model_type: str = "generalizedLinear", link: str = "log", n_feature
     return out.getvalue()
 
 
+def scorecard_pmml(n_features: int = 4, seed: int = 0, reason_codes: bool = True, missing_attribute: bool = True) -> str:
+    """``Scorecard`` over ``f*`` (3 interval bins each, the middle one a compound ``and``) and the
+    categorical ``color`` (set + equality attributes); with ``missing_attribute`` the first
+    characteristic also matches missing values (``isMissing``)."""
+    rng = np.random.default_rng(seed)
+    out = io.StringIO()
+    _header(out, "synthetic scorecard")
+    _mixed_dictionary(out, n_features, "score", None)
+    rc = ' useReasonCodes="true" reasonCodeAlgorithm="pointsBelow" baselineScore="10"' if reason_codes \
+        else ' useReasonCodes="false"'
+    out.write(f' <Scorecard functionName="regression" initialScore="{rng.uniform(-5, 5):.4f}"{rc}>\n')
+    _mixed_schema(out, n_features, "score")
+    if reason_codes:
+        out.write('  <Output>\n   <OutputField name="RC1" feature="reasonCode" rank="1" dataType="string"/>\n'
+                  '   <OutputField name="RC2" feature="reasonCode" rank="2" dataType="string"/>\n  </Output>\n')
+    out.write('  <Characteristics>\n')
+    for j in range(n_features):
+        a, b = sorted(rng.normal(size=2))
+        out.write(f'   <Characteristic name="ch{j}" reasonCode="R{j}">\n')
+        if missing_attribute and j == 0:
+            out.write(f'    <Attribute partialScore="{rng.uniform(0, 20):.3f}"><SimplePredicate field="f{j}" '
+                      'operator="isMissing"/></Attribute>\n')
+        out.write(f'    <Attribute partialScore="{rng.uniform(0, 20):.3f}"><SimplePredicate field="f{j}" '
+                  f'operator="lessThan" value="{a:.4f}"/></Attribute>\n')
+        out.write(f'    <Attribute partialScore="{rng.uniform(0, 20):.3f}" reasonCode="R{j}m"><CompoundPredicate '
+                  f'booleanOperator="and"><SimplePredicate field="f{j}" operator="greaterOrEqual" value="{a:.4f}"/>'
+                  f'<SimplePredicate field="f{j}" operator="lessThan" value="{b:.4f}"/></CompoundPredicate>'
+                  '</Attribute>\n')
+        out.write(f'    <Attribute partialScore="{rng.uniform(0, 20):.3f}"><SimplePredicate field="f{j}" '
+                  f'operator="greaterOrEqual" value="{b:.4f}"/></Attribute>\n')
+        out.write('   </Characteristic>\n')
+    out.write('   <Characteristic name="color" reasonCode="RC" baselineScore="5">\n')
+    out.write(f'    <Attribute partialScore="{rng.uniform(0, 20):.3f}"><SimpleSetPredicate field="color" '
+              'booleanOperator="isIn"><Array n="2" type="string">red green</Array></SimpleSetPredicate></Attribute>\n')
+    out.write(f'    <Attribute partialScore="{rng.uniform(0, 20):.3f}"><SimplePredicate field="color" '
+              'operator="equal" value="blue"/></Attribute>\n')
+    out.write(f'    <Attribute partialScore="{rng.uniform(0, 20):.3f}"><True/></Attribute>\n')
+    out.write('   </Characteristic>\n  </Characteristics>\n </Scorecard>\n</PMML>\n')
+    return out.getvalue()
+
+
+def ruleset_pmml(n_features: int = 4, n_rules: int = 12, criterion: str = "firstHit", seed: int = 0,
+                 default: bool = True, classes: int = 3) -> str:
+    """``RuleSetModel`` with simple rules on ``f*`` / ``color`` and one ``CompoundRule``."""
+    rng = np.random.default_rng(seed)
+    out = io.StringIO()
+    _header(out, f"synthetic rule set {criterion}")
+    cats = [str(k) for k in range(classes)]
+    _mixed_dictionary(out, n_features, "y", cats)
+    out.write(' <RuleSetModel functionName="classification">\n')
+    _mixed_schema(out, n_features, "y")
+    dflt = ' defaultScore="0" defaultConfidence="0.5"' if default else ""
+    out.write(f'  <RuleSet{dflt}>\n   <RuleSelectionMethod criterion="{criterion}"/>\n')
+
+    def pred() -> str:
+        j = int(rng.integers(n_features))
+        op = ["lessThan", "greaterOrEqual", "greaterThan"][int(rng.integers(3))]
+        p = f'<SimplePredicate field="f{j}" operator="{op}" value="{rng.normal():.4f}"/>'
+        if rng.random() < 0.3:
+            p = (f'<CompoundPredicate booleanOperator="and">{p}<SimplePredicate field="color" operator="notEqual" '
+                 f'value="{_LEVELS[int(rng.integers(3))]}"/></CompoundPredicate>')
+        return p
+
+    def rule(i: int) -> str:
+        return (f'   <SimpleRule id="r{i}" score="{cats[int(rng.integers(classes))]}" weight="{rng.uniform(0.1, 2):.3f}" '
+                f'confidence="{rng.uniform(0.5, 1):.3f}">{pred()}</SimpleRule>\n')
+
+    for i in range(n_rules // 2):
+        out.write(rule(i))
+    out.write(f'   <CompoundRule>{pred()}\n')
+    for i in range(n_rules // 2, n_rules - 2):
+        out.write(rule(i))
+    out.write('   </CompoundRule>\n')
+    for i in range(n_rules - 2, n_rules):
+        out.write(rule(i))
+    out.write('  </RuleSet>\n </RuleSetModel>\n</PMML>\n')
+    return out.getvalue()
+
+
+def naive_bayes_pmml(n_features: int = 4, classes: int = 3, seed: int = 0, threshold: float = 0.001) -> str:
+    """``NaiveBayesModel``: Gaussian ``f*`` inputs and the categorical ``color`` (one level never
+    seen with class 0: exercises the threshold)."""
+    rng = np.random.default_rng(seed)
+    out = io.StringIO()
+    _header(out, "synthetic naive Bayes")
+    cats = [str(k) for k in range(classes)]
+    _mixed_dictionary(out, n_features, "y", cats)
+    out.write(f' <NaiveBayesModel functionName="classification" threshold="{threshold}">\n')
+    _mixed_schema(out, n_features, "y")
+    counts = rng.integers(50, 200, classes)
+    out.write('  <BayesInputs>\n')
+    for j in range(n_features):
+        out.write(f'   <BayesInput fieldName="f{j}"><TargetValueStats>')
+        for k in range(classes):
+            out.write(f'<TargetValueStat value="{cats[k]}"><GaussianDistribution mean="{rng.normal() * 0.7:.4f}" '
+                      f'variance="{rng.uniform(0.5, 2.0):.4f}"/></TargetValueStat>')
+        out.write('</TargetValueStats></BayesInput>\n')
+    out.write('   <BayesInput fieldName="color">\n')
+    for li, lvl in enumerate(_LEVELS):
+        out.write(f'    <PairCounts value="{lvl}"><TargetValueCounts>')
+        for k in range(classes):
+            cnt = 0 if (li == 2 and k == 0) else int(rng.integers(5, counts[k] // 3))
+            out.write(f'<TargetValueCount value="{cats[k]}" count="{cnt}"/>')
+        out.write('</TargetValueCounts></PairCounts>\n')
+    out.write('   </BayesInput>\n  </BayesInputs>\n')
+    out.write('  <BayesOutput fieldName="y"><TargetValueCounts>'
+              + "".join(f'<TargetValueCount value="{cats[k]}" count="{counts[k]}"/>' for k in range(classes))
+              + '</TargetValueCounts></BayesOutput>\n')
+    out.write(' </NaiveBayesModel>\n</PMML>\n')
+    return out.getvalue()
+
+
+def knn_pmml(n_instances: int = 200, n_features: int = 4, k: int = 3, classification: bool = True, seed: int = 0,
+             method: Optional[str] = None, metric: str = "euclidean", classes: int = 3) -> str:
+    """``NearestNeighborModel`` over ``n_instances`` inline training rows of ``f*`` (targets
+    ``0..classes-1`` or real values)."""
+    rng = np.random.default_rng(seed)
+    out = io.StringIO()
+    _header(out, f"synthetic {k}-NN")
+    cats = [str(c) for c in range(classes)] if classification else None
+    _data_dictionary(out, n_features, "y", "string" if classification else "double", cats)
+    fn = "classification" if classification else "regression"
+    meth = (f' categoricalScoringMethod="{method or "majorityVote"}"' if classification
+            else f' continuousScoringMethod="{method or "average"}"')
+    out.write(f' <NearestNeighborModel functionName="{fn}" numberOfNeighbors="{k}"{meth} threshold="0.001">\n')
+    _mining_schema(out, n_features, "y", "  ")
+    out.write(f'  <TrainingInstances recordCount="{n_instances}" fieldCount="{n_features + 1}">\n   <InstanceFields>')
+    out.write("".join(f'<InstanceField field="f{j}" column="c{j}"/>' for j in range(n_features)))
+    out.write('<InstanceField field="y" column="target"/></InstanceFields>\n   <InlineTable>\n')
+    X = rng.standard_normal((n_instances, n_features))
+    for i in range(n_instances):
+        t = str(int(rng.integers(classes))) if classification else f"{rng.normal() * 3:.4f}"
+        out.write("    <row>" + "".join(f"<c{j}>{X[i, j]:.5f}</c{j}>" for j in range(n_features))
+                  + f"<target>{t}</target></row>\n")
+    out.write('   </InlineTable>\n  </TrainingInstances>\n')
+    out.write(f'  <ComparisonMeasure kind="distance"><{metric}/></ComparisonMeasure>\n  <KNNInputs>')
+    out.write("".join(f'<KNNInput field="f{j}"/>' for j in range(n_features)))
+    out.write('</KNNInputs>\n </NearestNeighborModel>\n</PMML>\n')
+    return out.getvalue()
+
+
 def mixed_records(n_rows: int, n_features: int, seed: int = 0, missing_rate: float = 0.0) -> Tuple[list, np.ndarray]:
     """Records for the ``_mixed_dictionary`` models: ``(list of dicts, [rows, F+1] float matrix with
     the color vocabulary code in the last column)``."""

@@ -13,10 +13,13 @@ from .base import ModelEvaluator
 
 def _registry() -> Dict[type, Callable[..., ModelEvaluator]]:
     from .clustering import ClusteringEvaluator
+    from .knn import NearestNeighborEvaluator
     from .mining import MiningEvaluator
+    from .naive_bayes import NaiveBayesEvaluator
     from .neural import NeuralEvaluator
     from .regression import GeneralRegressionEvaluator, RegressionEvaluator
     from .svm import SvmEvaluator
+    from .scorecard import ScorecardEvaluator, make_ruleset_evaluator
     from .tree import TreeEvaluator
 
     return {
@@ -27,6 +30,10 @@ def _registry() -> Dict[type, Callable[..., ModelEvaluator]]:
         ir.GeneralRegressionModel: GeneralRegressionEvaluator,
         ir.NeuralNetwork: NeuralEvaluator,
         ir.SupportVectorMachineModel: SvmEvaluator,
+        ir.Scorecard: ScorecardEvaluator,
+        ir.RuleSetModel: make_ruleset_evaluator,
+        ir.NaiveBayesModel: NaiveBayesEvaluator,
+        ir.NearestNeighborModel: NearestNeighborEvaluator,
     }
 
 

@@ -428,73 +428,70 @@ __device__ __forceinline__ uint2 lds_ld2(uint32_t a) {
 }
 __device__ __forceinline__ float lds_ldf(uint32_t a) { return *(lds_f_t*)(uintptr_t)a; }
 
-template <int DEPTH, int ILP, int G, bool LEAF8>
-__device__ __forceinline__ float traverse_fast_g(const uint32_t* buf, int nt, int g, uint32_t feat_lane,
-                                                 float acc) {
+// N trees of group g starting at its m-th tree, N independent walks interleaved (ILP).
+template <int DEPTH, int N, int G, bool LEAF8>
+__device__ __forceinline__ float fast_batch(uint32_t lds0, int g, int m, uint32_t feat_lane, float acc) {
   constexpr int NI = (1 << DEPTH) - 1;
   constexpr int NL = 1 << DEPTH;
   constexpr uint32_t RB = 4u * (LEAF8 ? perfect_rec_words8(DEPTH) : perfect_rec_words(DEPTH, 1));  // record bytes
   constexpr uint32_t TS = G * RB;                            // tree stride within a group
   constexpr uint32_t C = 8u + 8u * NI - 4u * NL;             // last-level node -> its leaf pair
-  const uint32_t lds0 = lds_addr(buf);
-  const int mt = (nt - g + G - 1) / G;
-  int m = 0;
-  for (; m + ILP <= mt; m += ILP) {
-    const uint32_t b0 = lds0 + (uint32_t)(g + G * m) * RB;
-    uint32_t k0 = 8u - b0, k1 = 16u - b0;
-    __asm__("" : "+v"(k0), "+v"(k1));
-    uint32_t u[ILP];
+  const uint32_t b0 = lds0 + (uint32_t)(g + G * m) * RB;
+  uint32_t k0 = 8u - b0, k1 = 16u - b0;
+  __asm__("" : "+v"(k0), "+v"(k1));
+  uint32_t u[N];
 #pragma unroll
-    for (int i = 0; i < ILP; ++i) {
-      u[i] = b0;
-      __asm__ volatile("" : "+v"(u[i]));  // separate root reads: ds_read2_b64 pairing costs 8 LDS
-                                          // cycles vs 2 x 2 for two ds_read_b64
-    }
+  for (int i = 0; i < N; ++i) {
+    u[i] = b0;
+    __asm__ volatile("" : "+v"(u[i]));  // separate root reads: ds_read2_b64 pairing costs 8 LDS
+                                        // cycles vs 2 x 2 for two ds_read_b64
+  }
 #pragma unroll
-    for (int d = 0; d + 1 < DEPTH; ++d) {
+  for (int d = 0; d + 1 < DEPTH; ++d) {
 #pragma unroll
-      for (int i = 0; i < ILP; ++i) {
-        const uint2 nd = lds_ld2(u[i] + i * TS);
-        const float x = lds_ldf(feat_lane + nd.y);
-        u[i] = 2u * u[i] + ((x >= __uint_as_float(nd.x)) ? k1 : k0);
-        __asm__("" : "+v"(u[i]));
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < ILP; ++i) {
-      if (LEAF8) {
-        const uint2 nd = lds_ld2(u[i] + i * TS);
-        const float x = lds_ldf(feat_lane + (nd.y & 0xFFFFu));
-        acc += leaf8_select(nd.y, x >= __uint_as_float(nd.x));
-      } else {
-        uint32_t ul = u[i] + C;
-        __asm__ volatile("" : "+v"(ul));  // keep the pair read out of a ds_read2_b64 with the node
-        const uint2 nd = lds_ld2(u[i] + i * TS);
-        const uint2 lv = lds_ld2(ul + i * TS);
-        const float x = lds_ldf(feat_lane + nd.y);
-        acc += (x >= __uint_as_float(nd.x)) ? __uint_as_float(lv.y) : __uint_as_float(lv.x);
-      }
+    for (int i = 0; i < N; ++i) {
+      const uint2 nd = lds_ld2(u[i] + i * TS);
+      const float x = lds_ldf(feat_lane + nd.y);
+      u[i] = 2u * u[i] + ((x >= __uint_as_float(nd.x)) ? k1 : k0);
+      __asm__("" : "+v"(u[i]));
     }
   }
-  for (; m < mt; ++m) {
-    const uint32_t b0 = lds0 + (uint32_t)(g + G * m) * RB;
-    uint32_t u = b0;
 #pragma unroll
-    for (int d = 0; d + 1 < DEPTH; ++d) {
-      const uint2 nd = lds_ld2(u);
-      const float x = lds_ldf(feat_lane + nd.y);
-      u = 2u * u + 8u - b0 + ((x >= __uint_as_float(nd.x)) ? 8u : 0u);
-    }
-    const uint2 nd = lds_ld2(u);
+  for (int i = 0; i < N; ++i) {
     if (LEAF8) {
+      const uint2 nd = lds_ld2(u[i] + i * TS);
       const float x = lds_ldf(feat_lane + (nd.y & 0xFFFFu));
       acc += leaf8_select(nd.y, x >= __uint_as_float(nd.x));
     } else {
-      const uint2 lv = lds_ld2(u + C);
+      uint32_t ul = u[i] + C;
+      __asm__ volatile("" : "+v"(ul));  // keep the pair read out of a ds_read2_b64 with the node
+      const uint2 nd = lds_ld2(u[i] + i * TS);
+      const uint2 lv = lds_ld2(ul + i * TS);
       const float x = lds_ldf(feat_lane + nd.y);
       acc += (x >= __uint_as_float(nd.x)) ? __uint_as_float(lv.y) : __uint_as_float(lv.x);
     }
   }
+  return acc;
+}
+
+// The group's trees in ILP-wide batches; the remainder in 4/2/1-wide batches (a plain serial
+// tail is latency bound: one dependent LDS round trip per level and tree).
+template <int DEPTH, int ILP, int G, bool LEAF8>
+__device__ __forceinline__ float traverse_fast_g(const uint32_t* buf, int nt, int g, uint32_t feat_lane,
+                                                 float acc) {
+  const uint32_t lds0 = lds_addr(buf);
+  const int mt = (nt - g + G - 1) / G;
+  int m = 0;
+  for (; m + ILP <= mt; m += ILP) acc = fast_batch<DEPTH, ILP, G, LEAF8>(lds0, g, m, feat_lane, acc);
+  if (ILP > 4 && m + 4 <= mt) {
+    acc = fast_batch<DEPTH, 4, G, LEAF8>(lds0, g, m, feat_lane, acc);
+    m += 4;
+  }
+  if (m + 2 <= mt) {
+    acc = fast_batch<DEPTH, 2, G, LEAF8>(lds0, g, m, feat_lane, acc);
+    m += 2;
+  }
+  if (m < mt) acc = fast_batch<DEPTH, 1, G, LEAF8>(lds0, g, m, feat_lane, acc);
   return acc;
 }
 

@@ -497,3 +497,98 @@ class PMMLDocument:
             if m.is_scorable:
                 return m
         raise IndexError("PMML document contains no scorable model")
+
+
+# scorecard / rule set -------------------------------------------------------
+
+
+@dataclass
+class ScorecardAttribute:
+    predicate: Predicate
+    partial_score: Optional[float]
+    reason_code: Optional[str] = None
+
+
+@dataclass
+class Characteristic:
+    name: Optional[str]
+    attributes: List[ScorecardAttribute] = field(default_factory=list)
+    reason_code: Optional[str] = None
+    baseline_score: Optional[float] = None
+
+
+@dataclass
+class Scorecard(Model):
+    initial_score: float = 0.0
+    use_reason_codes: bool = True
+    reason_code_algorithm: str = "pointsBelow"
+    baseline_score: Optional[float] = None
+    baseline_method: str = "other"
+    characteristics: List[Characteristic] = field(default_factory=list)
+
+
+@dataclass
+class SimpleRule:
+    id: Optional[str]
+    score: str
+    predicate: Predicate
+    confidence: float = 1.0
+    weight: float = 1.0
+    distributions: List[ScoreDistribution] = field(default_factory=list)
+
+
+@dataclass
+class CompoundRule:
+    predicate: Predicate
+    rules: List[object] = field(default_factory=list)  # SimpleRule | CompoundRule
+
+
+@dataclass
+class RuleSetModel(Model):
+    criterion: str = "firstHit"  # first RuleSelectionMethod: firstHit | weightedSum | weightedMax
+    default_score: Optional[str] = None
+    default_confidence: Optional[float] = None
+    rules: List[object] = field(default_factory=list)
+
+
+# naive Bayes ------------------------------------------------------------------
+
+
+@dataclass
+class BayesInput:
+    field: str
+    pair_counts: Dict[str, Dict[str, float]] = field(default_factory=dict)   # value -> {target: count}
+    gaussian: Dict[str, Tuple[float, float]] = field(default_factory=dict)   # target -> (mean, variance)
+
+
+@dataclass
+class NaiveBayesModel(Model):
+    threshold: float = 0.0
+    inputs: List[BayesInput] = field(default_factory=list)
+    output_field: Optional[str] = None
+    target_counts: Dict[str, float] = field(default_factory=dict)  # BayesOutput, document order
+
+
+# k-nearest neighbours ---------------------------------------------------------
+
+
+@dataclass
+class KNNInput:
+    field: str
+    weight: float = 1.0
+    compare_function: Optional[str] = None
+
+
+@dataclass
+class NearestNeighborModel(Model):
+    k: int = 1
+    continuous_method: str = "average"
+    categorical_method: str = "majorityVote"
+    threshold: float = 0.001
+    measure_kind: str = "distance"
+    metric: str = "euclidean"
+    minkowski_p: float = 2.0
+    compare_function: str = "absDiff"
+    inputs: List[KNNInput] = field(default_factory=list)
+    instance_fields: Dict[str, str] = field(default_factory=dict)  # field -> InlineTable column
+    rows: List[Dict[str, str]] = field(default_factory=list)       # InlineTable rows

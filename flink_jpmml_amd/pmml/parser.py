@@ -530,6 +530,120 @@ def _parse_svm(el: ET.Element) -> ir.SupportVectorMachineModel:
     return m
 
 
+def _parse_scorecard(el: ET.Element) -> ir.Scorecard:
+    m = ir.Scorecard(**_common(el))
+    m.initial_score = _f(el, "initialScore", 0.0)
+    m.use_reason_codes = el.get("useReasonCodes", "true") == "true"
+    m.reason_code_algorithm = el.get("reasonCodeAlgorithm", "pointsBelow")
+    m.baseline_score = _f(el, "baselineScore")
+    m.baseline_method = el.get("baselineMethod", "other")
+    chars = _child(el, "Characteristics")
+    if chars is None:
+        raise PmmlParseError("Scorecard without Characteristics")
+    for c in _children(chars, "Characteristic"):
+        ch = ir.Characteristic(c.get("name"), reason_code=c.get("reasonCode"), baseline_score=_f(c, "baselineScore"))
+        for a in _children(c, "Attribute"):
+            if _child(a, "ComplexPartialScore") is not None:
+                raise UnsupportedFeatureException("Scorecard ComplexPartialScore is not supported")
+            ch.attributes.append(ir.ScorecardAttribute(_find_predicate(a), _f(a, "partialScore"), a.get("reasonCode")))
+        m.characteristics.append(ch)
+    return m
+
+
+def _parse_rules(el: ET.Element) -> List[object]:
+    out: List[object] = []
+    for c in el:
+        ln = _local(c.tag)
+        if ln == "SimpleRule":
+            dists = [ir.ScoreDistribution(d.get("value"), float(d.get("recordCount", "0")), _f(d, "probability"),
+                                          _f(d, "confidence")) for d in _children(c, "ScoreDistribution")]
+            out.append(ir.SimpleRule(c.get("id"), c.get("score"), _find_predicate(c), _f(c, "confidence", 1.0),
+                                     _f(c, "weight", 1.0), dists))
+        elif ln == "CompoundRule":
+            out.append(ir.CompoundRule(_find_predicate(c), _parse_rules(c)))
+    return out
+
+
+def _parse_ruleset(el: ET.Element) -> ir.RuleSetModel:
+    m = ir.RuleSetModel(**_common(el))
+    rs = _child(el, "RuleSet")
+    if rs is None:
+        raise PmmlParseError("RuleSetModel without RuleSet")
+    sel = _children(rs, "RuleSelectionMethod")
+    m.criterion = sel[0].get("criterion", "firstHit") if sel else "firstHit"
+    m.default_score = rs.get("defaultScore")
+    m.default_confidence = _f(rs, "defaultConfidence")
+    m.rules = _parse_rules(rs)
+    return m
+
+
+def _target_value_counts(el: Optional[ET.Element]) -> Dict[str, float]:
+    out: Dict[str, float] = {}
+    if el is not None:
+        for t in _children(el, "TargetValueCount"):
+            out[t.get("value")] = float(t.get("count", "0"))
+    return out
+
+
+def _parse_naive_bayes(el: ET.Element) -> ir.NaiveBayesModel:
+    m = ir.NaiveBayesModel(**_common(el))
+    m.threshold = _f(el, "threshold", 0.0)
+    bis = _child(el, "BayesInputs")
+    for bi in _children(bis, "BayesInput") if bis is not None else []:
+        if _child(bi, "DerivedField") is not None:
+            raise UnsupportedFeatureException("BayesInput with a DerivedField (discretisation) is not supported")
+        inp = ir.BayesInput(bi.get("fieldName"))
+        for pc in _children(bi, "PairCounts"):
+            inp.pair_counts[pc.get("value")] = _target_value_counts(_child(pc, "TargetValueCounts"))
+        tvs = _child(bi, "TargetValueStats")
+        for st in _children(tvs, "TargetValueStat") if tvs is not None else []:
+            g = _child(st, "GaussianDistribution")
+            if g is None:
+                raise UnsupportedFeatureException("only GaussianDistribution TargetValueStats are supported")
+            inp.gaussian[st.get("value")] = (float(g.get("mean")), float(g.get("variance")))
+        m.inputs.append(inp)
+    bo = _child(el, "BayesOutput")
+    if bo is None:
+        raise PmmlParseError("NaiveBayesModel without BayesOutput")
+    m.output_field = bo.get("fieldName")
+    m.target_counts = _target_value_counts(_child(bo, "TargetValueCounts"))
+    return m
+
+
+def _parse_knn(el: ET.Element) -> ir.NearestNeighborModel:
+    m = ir.NearestNeighborModel(**_common(el))
+    m.k = int(el.get("numberOfNeighbors", "1"))
+    m.continuous_method = el.get("continuousScoringMethod", "average")
+    m.categorical_method = el.get("categoricalScoringMethod", "majorityVote")
+    m.threshold = _f(el, "threshold", 0.001)
+    cm = _child(el, "ComparisonMeasure")
+    if cm is None:
+        raise PmmlParseError("NearestNeighborModel without ComparisonMeasure")
+    m.measure_kind = cm.get("kind", "distance")
+    m.compare_function = cm.get("compareFunction", "absDiff")
+    metric = next((c for c in cm if _local(c.tag) != "Extension"), None)
+    if metric is None:
+        raise PmmlParseError("ComparisonMeasure without a metric")
+    m.metric = _local(metric.tag)
+    if m.metric == "minkowski":
+        m.minkowski_p = _f(metric, "p-parameter", 2.0)
+    ki = _child(el, "KNNInputs")
+    for k in _children(ki, "KNNInput") if ki is not None else []:
+        m.inputs.append(ir.KNNInput(k.get("field"), _f(k, "fieldWeight", 1.0), k.get("compareFunction")))
+    ti = _child(el, "TrainingInstances")
+    if ti is None:
+        raise PmmlParseError("NearestNeighborModel without TrainingInstances")
+    inf = _child(ti, "InstanceFields")
+    for f in _children(inf, "InstanceField") if inf is not None else []:
+        m.instance_fields[f.get("field")] = f.get("column") or f.get("field")
+    tab = _child(ti, "InlineTable")
+    if tab is None:
+        raise UnsupportedFeatureException("TrainingInstances without an InlineTable")
+    for r in _children(tab, "row"):
+        m.rows.append({_local(c.tag): (c.text or "").strip() for c in r})
+    return m
+
+
 MODEL_PARSERS: Dict[str, Callable[[ET.Element], ir.Model]] = {
     "ClusteringModel": _parse_clustering,
     "TreeModel": _parse_tree,
@@ -538,10 +652,14 @@ MODEL_PARSERS: Dict[str, Callable[[ET.Element], ir.Model]] = {
     "GeneralRegressionModel": _parse_general_regression,
     "NeuralNetwork": _parse_neural,
     "SupportVectorMachineModel": _parse_svm,
+    "Scorecard": _parse_scorecard,
+    "RuleSetModel": _parse_ruleset,
+    "NaiveBayesModel": _parse_naive_bayes,
+    "NearestNeighborModel": _parse_knn,
 }
 
 _KNOWN_UNSUPPORTED = ("AssociationModel", "BaselineModel", "BayesianNetworkModel", "GaussianProcessModel",
-                      "NaiveBayesModel", "NearestNeighborModel", "RuleSetModel", "Scorecard", "SequenceModel",
+                      "SequenceModel",
                       "TextModel", "TimeSeriesModel", "AnomalyDetectionModel")
 
 

@@ -65,6 +65,11 @@ def _opt(v) -> float:
 # --------------------------------------------------------------------------- analysis
 
 
+def _model_of(compiled) -> ir.Model:
+    """The model IR the evaluator runs (Scorecard / RuleSet evaluate a rewritten tree IR)."""
+    return getattr(compiled.evaluator, "model", None) or compiled.model
+
+
 def collect_derived(compiled) -> Dict[str, ir.DerivedField]:
     """Every DerivedField visible to the model: TransformationDictionary + the LocalTransformations
     of the model and of all nested segment models (names must be unambiguous)."""
@@ -86,7 +91,7 @@ def collect_derived(compiled) -> Dict[str, ir.DerivedField]:
             for s in m.segments:
                 walk(s.model)
 
-    walk(compiled.model)
+    walk(_model_of(compiled))
     return out
 
 
@@ -328,11 +333,11 @@ def plan_field_layout(compiled, allow_alias: bool = True) -> FieldLayout:
     active = list(compiled.active_fields)
     index = {f: i for i, f in enumerate(active)}
     defs = collect_derived(compiled)
-    members = membership_fields(compiled.model)  # 0/1 columns of categorical tree splits
+    members = membership_fields(_model_of(compiled))  # 0/1 columns of categorical tree splits
     defs.update(members)
     if not defs:
         return FieldLayout(active, index, None)
-    refs = referenced_fields(compiled.model) + list(members)
+    refs = referenced_fields(_model_of(compiled)) + list(members)
     needed = [r for r in refs if r in defs and r not in index]
     if not needed:
         return FieldLayout(active, index, None)

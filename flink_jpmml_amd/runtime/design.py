@@ -141,8 +141,47 @@ def _glm_tables(ev: GeneralRegressionEvaluator, d: _Design) -> Tuple[List[ir.Reg
     return tabs, "softmax"
 
 
+def _naive_bayes_tables(ev, d: _Design) -> Tuple[List[ir.RegressionTable], str]:
+    """log n_j + Σ_i log P(x_i | T_j), each factor linear in design columns; softmax."""
+    import math
+
+    import numpy as np
+
+    if (ev.counts <= 0).any():
+        raise NotLowerable("NaiveBayes class with a zero count")
+    K = len(ev.categories)
+    coef: List[Dict[str, float]] = [dict() for _ in range(K)]
+
+    def add(name: str, w) -> None:
+        for j in range(K):
+            coef[j][name] = coef[j].get(name, 0.0) + float(w[j])
+
+    for inp in ev.nb.inputs:
+        f = inp.field
+        if inp.gaussian:
+            g = ev.gaussian_params(inp)
+            if np.isnan(g).any() or (g[:, 1] <= 0).any():
+                raise NotLowerable(f"NaiveBayes input {f!r}: Gaussian stats missing for a class")
+            mu, var = g[:, 0], g[:, 1]
+            add(d.column(("present", f), ir.Apply("isNotMissing", [ir.FieldRef(f)])),
+                -0.5 * np.log(2 * math.pi * var) - mu * mu / (2 * var))
+            add(d.column(("x0", f), ir.FieldRef(f, map_missing_to="0")), mu / var)
+            add(d.column(("x2", f), ir.Apply("pow", [ir.FieldRef(f), ir.Constant("2")], map_missing_to="0")),
+                -1.0 / (2 * var))
+        else:
+            for v, lp in ev.level_log_probs(inp):
+                if not np.isfinite(lp).all():
+                    raise NotLowerable("NaiveBayes zero probability without a threshold")
+                add(d.name_of(*d.level(f, v)), lp)
+    tabs = [ir.RegressionTable(float(np.log(ev.counts[j])), c, [ir.NumericPredictor(n, w) for n, w in coef[j].items()])
+            for j, c in enumerate(ev.categories)]
+    return tabs, "softmax"
+
+
 def needs_design(ev) -> bool:
-    if isinstance(ev, GeneralRegressionEvaluator):
+    from ..models.naive_bayes import NaiveBayesEvaluator
+
+    if isinstance(ev, (GeneralRegressionEvaluator, NaiveBayesEvaluator)):
         return True
     return isinstance(ev, RegressionEvaluator) and not ev.is_dense_linear()
 
@@ -152,9 +191,16 @@ def design_layout(compiled):
     them). The layout always carries a derive program unless every column is a plain field."""
     from .derive import FieldLayout, build_program_layout, collect_derived
 
+    from ..models.naive_bayes import NaiveBayesEvaluator
+
     ev = compiled.evaluator
     d = _Design()
-    if isinstance(ev, GeneralRegressionEvaluator):
+    if isinstance(ev, NaiveBayesEvaluator):
+        tables, norm = _naive_bayes_tables(ev, d)
+        base = {f.name: getattr(ev.nb, f.name) for f in dataclasses.fields(ir.Model)}
+        base["element"] = "RegressionModel"
+        model = ir.RegressionModel(**base, normalization_method=norm, tables=tables)
+    elif isinstance(ev, GeneralRegressionEvaluator):
         tables, norm = _glm_tables(ev, d)
         gm = ev.gm
         base = {f.name: getattr(gm, f.name) for f in dataclasses.fields(ir.Model)}

@@ -338,6 +338,8 @@ class ClusterPlan(DevicePlan):
         applies and K ≥ ``MFMA_MIN_K``)."""
         super().__init__(compiled, device)
         ev: ClusteringEvaluator = compiled.evaluator
+        if getattr(ev, "k", 1) > 1:
+            raise NotLowerable("k-NN with k > 1 is host-only (k = 1 runs as a clustering argmin)")
         if ev.metric not in self._METRICS:
             raise NotLowerable(f"clustering metric {ev.metric!r} is host-only")
         if ev.fields != compiled.active_fields:
@@ -813,7 +815,7 @@ class TreePlan(DevicePlan):
     WIDE_G = 4  # tree groups of the wide kernel (mirrors csrc)
 
     def __init__(self, compiled, device, layout: str = "auto", lds_budget: int = 80 * 1024, splits: int = 0,
-                 variant: str = "auto", precision: str = "fp32", nan_mode: str = "auto"):
+                 variant: str = "auto", precision: str = "fp32", nan_mode: str = "auto", max_chunk_trees: int = 0):
         """``nan_mode`` (wide PERFECT kernel): ``"auto"`` keeps tiles with missing values on the fast
         traversal whenever the ensemble has no null-on-missing trees (default-right nodes read a
         NaN -> +inf second feature plane, :func:`_nan_planes`); ``"off"``: per-node missing test."""
@@ -903,6 +905,8 @@ class TreePlan(DevicePlan):
             if rec * 4 > per_chunk:
                 raise NotLowerable(f"depth-{depth} tree record ({rec * 4} B) exceeds the 32 KiB chunk")
             self.chunk_trees = int(max(1, min(self.n_trees, per_chunk // (rec * 4))))
+            if max_chunk_trees > 0:
+                self.chunk_trees = min(self.chunk_trees, max_chunk_trees)
             self.blob = self._t(blob.reshape(-1).view(np.int32))
             self.roots = self.leaves = None
         else:

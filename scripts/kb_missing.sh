@@ -1,4 +1,8 @@
 set -e
 K="timeout -k 10 120 python scripts/kbench.py"
-for m in 0 0.02 0.1; do $K --model gbdt --missing $m; done
+for c in 0 64 48 32; do
+  $K --model gbdt --missing 0 --nan-mode off --max-chunk-trees $c
+  $K --model gbdt --missing 0 --max-chunk-trees $c
+  $K --model gbdt --missing 0.02 --max-chunk-trees $c
+done
 $K --model gbdt --missing 0.02 --nan-mode off

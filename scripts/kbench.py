@@ -26,6 +26,7 @@ def main():
     p.add_argument("--variant", default="auto")
     p.add_argument("--clusters", type=int, default=256)
     p.add_argument("--nan-mode", default="auto")
+    p.add_argument("--max-chunk-trees", type=int, default=0)
     args = p.parse_args()
     import numpy as np
     import torch
@@ -69,7 +70,8 @@ def main():
     c = CompiledPmml.from_string(txt)
     opts = {}
     if args.model.startswith(("gbdt", "rf")):
-        opts = dict(layout=args.layout, lds_budget=args.lds_budget, variant=args.variant, nan_mode=args.nan_mode)
+        opts = dict(layout=args.layout, lds_budget=args.lds_budget, variant=args.variant, nan_mode=args.nan_mode,
+                    max_chunk_trees=args.max_chunk_trees)
     elif args.model == "kmeans-big":
         opts = dict(cluster_variant=args.variant)
     plan = c.plan("cuda:0", **opts)

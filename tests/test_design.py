@@ -9,7 +9,7 @@ float64 oracle; GPU: the DerivedPlan (derive kernel → linear kernel) against t
 import numpy as np
 import pytest
 
-from flink_jpmml_amd.bench.synth import glm_pmml, mixed_records, regression_design_pmml
+from flink_jpmml_amd.bench.synth import glm_pmml, mixed_records, naive_bayes_pmml, regression_design_pmml
 from flink_jpmml_amd.runtime.compiled import CompiledPmml
 
 CASES = {
@@ -23,6 +23,8 @@ CASES = {
     "glm-power0": lambda: glm_pmml(link="power"),
     "glm-general-linear": lambda: glm_pmml(model_type="generalLinear"),
     "glm-multinomial": lambda: glm_pmml(model_type="multinomialLogistic"),
+    "naive-bayes": lambda: naive_bayes_pmml(),
+    "naive-bayes-2": lambda: naive_bayes_pmml(classes=2, seed=3),
 }
 
 
@@ -63,6 +65,28 @@ def test_glm_oracle_semantics():
     eta = gm.offset_value + beta["p0"] + beta["p1"] * 0.5 + beta["p2"] * 1.0 + beta["p3"] * 2.0 + beta["px"] * 0.5
     s, v = c.score_matrix_oracle(x)
     assert v[0] and np.isclose(s[0], np.exp(eta))
+
+
+def test_naive_bayes_oracle_by_hand():
+    """One record, spec formula: n_j · Π N(x_i; μ_ij, σ²_ij) · P(color | j), normalised."""
+    import math
+
+    c = CompiledPmml.from_string(naive_bayes_pmml(seed=1))
+    nb = c.model
+    x = {"f0": 0.3, "f1": -1.2, "f2": 0.0, "f3": 2.0}
+    post = []
+    for k in ("0", "1", "2"):
+        p = nb.target_counts[k]
+        for inp in nb.inputs[:4]:
+            mu, var = inp.gaussian[k]
+            p *= math.exp(-(x[inp.field] - mu) ** 2 / (2 * var)) / math.sqrt(2 * math.pi * var)
+        cnt = nb.inputs[4].pair_counts["blue"][k]
+        p *= (cnt / nb.target_counts[k]) if cnt > 0 else nb.threshold
+        post.append(p)
+    post = np.array(post) / sum(post)
+    res = c.result(np.array([[0.3, -1.2, 0.0, 2.0, 2.0]]))  # color code 2 = blue
+    assert np.allclose(res.probs[0], post, rtol=1e-9)
+    assert res.value[0] == np.argmax(post)
 
 
 def test_design_not_lowerable_power_link():
