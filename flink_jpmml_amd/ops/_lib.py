@@ -118,7 +118,8 @@ class TreeArgs(ctypes.Structure):
                 ("leaves", c_void_p), ("tree_slot", c_void_p), ("n_trees", c_int), ("rec_words", c_int),
                 ("chunk_trees", c_int), ("P", c_int), ("C", c_int), ("trees_per_split", c_int),
                 ("general", c_int), ("variant", c_int), ("epi", Epilogue), ("score", c_void_p),
-                ("valid", c_void_p), ("probs", c_void_p), ("partial", c_void_p)]
+                ("valid", c_void_p), ("probs", c_void_p), ("partial", c_void_p), ("blob_nan", c_void_p),
+                ("chunk_trees_nan", c_int), ("pad1", c_int)]
 
 
 class GenTreeArgs(ctypes.Structure):

@@ -53,9 +53,11 @@ struct TreeArgs {
   uint8_t* valid;
   float* probs;
   float* partial;               // split mode: [splits][C+1][n_rows]
+  const uint32_t* blob_nan;     // wide kernel, nullable: the records re-pointed at the NaN plane
+  int chunk_trees_nan, pad1;    // (tiles with missing values; own chunk size, LDS holds 2 planes)
 };
 constexpr int VAR_NAN_FAST = 4;    // wide kernel: take the fast path even on tiles with missing values
-constexpr int VAR_NAN_PLANES = 8;  // ... with a second feature plane (NaN -> +inf) for default-right nodes
+constexpr int VAR_NAN_PLANES = 8;  // ... via blob_nan + a second feature plane (NaN -> +inf)
 
 
 __device__ __forceinline__ void finish_row(const TreeArgs& a, float acc0, const float* accl, int split,
@@ -500,14 +502,13 @@ __global__ __launch_bounds__(TB * G, 1) void tree_perfect_wide_kernel(TreeArgs a
   constexpr int T = TB * G;
   extern __shared__ __align__(16) uint32_t smem[];
   const int rw = a.rec_words;
-  const int chunk_words = a.chunk_trees * rw;
-  float* feat = reinterpret_cast<float*>(smem);
-  const bool planes2 = (a.variant & VAR_NAN_PLANES) != 0;
-  uint32_t* tbuf0 = smem + (planes2 ? 2 : 1) * a.n_feat * TB;
-  uint32_t* tbuf1 = tbuf0 + chunk_words;
-  int* bad = reinterpret_cast<int*>(tbuf1 + chunk_words);
+  // LDS: [bad TB][flag 4][part G x TB][feature plane(s)][two chunk buffers]. A tile with missing
+  // values and a NaN blob gets two planes (the second NaN -> +inf) and that blob's chunk size;
+  // any other tile one plane and the main blob — the layout is chosen per workgroup.
+  int* bad = reinterpret_cast<int*>(smem);
   int* any_missing = bad + TB;
   float* part = reinterpret_cast<float*>(bad + TB + 4);  // [G][TB]
+  float* feat = part + G * TB;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -521,7 +522,7 @@ __global__ __launch_bounds__(TB * G, 1) void tree_perfect_wide_kernel(TreeArgs a
 
   PF4_DECL
   int n16 = (tb < te) ? (min(a.chunk_trees, te - tb) * rw) >> 2 : 0;
-  PF4_LOAD(n16 > 0 ? a.blob + (size_t)tb * rw : a.blob, n16, T)
+  PF4_LOAD(n16 > 0 ? a.blob + (size_t)tb * rw : a.blob, n16, T)  // speculative: main blob
 
   if (tid == 0) *any_missing = 0;
   if (tid < TB) bad[tid] = 0;
@@ -542,27 +543,42 @@ __global__ __launch_bounds__(TB * G, 1) void tree_perfect_wide_kernel(TreeArgs a
         miss = miss || (x != x);
       }
       feat[f * TB + r] = x;
-      if (planes2) feat[(F + f) * TB + r] = (x != x) ? __builtin_inff() : x;  // NaN-goes-right plane
       if (b) bad[r] = 1;
     }
     if (__any(miss) && lane == 0) *any_missing = 1;
+  }
+  __syncthreads();
+  const bool has_missing = *any_missing != 0;
+  const bool use_nan = has_missing && a.blob_nan != nullptr;
+  const uint32_t* blob = use_nan ? a.blob_nan : a.blob;
+  const int chunk = use_nan ? a.chunk_trees_nan : a.chunk_trees;
+  uint32_t* tbuf0 = reinterpret_cast<uint32_t*>(feat + (use_nan ? 2 : 1) * a.n_feat * TB);
+  uint32_t* tbuf1 = tbuf0 + chunk * rw;
+  if (use_nan) {
+    const int total = TB * a.n_feat;
+    for (int e = tid; e < total; e += T) {  // NaN-goes-right plane
+      const float x = feat[e];
+      feat[total + e] = (x != x) ? __builtin_inff() : x;
+    }
+    n16 = (tb < te) ? (min(chunk, te - tb) * rw) >> 2 : 0;
+    PF4_LOAD(n16 > 0 ? blob + (size_t)tb * rw : blob, n16, T)
   }
   PF4_STORE(tbuf0, n16, T)
   __syncthreads();
 
   // VAR_NAN_FAST: missing values need no per-node work — either no node sends NaN right (a NaN
   // compare is false: left), or the node's feature offset points into the NaN -> +inf plane
-  const bool missing = *any_missing != 0 && (a.variant & VAR_NAN_FAST) == 0;
+  const bool missing = has_missing && (a.variant & VAR_NAN_FAST) == 0;
   float acc = 0.f;
   const char* feat_lane = reinterpret_cast<const char*>(feat + r_local);
   int c = 0;
-  for (int t0 = tb; t0 < te; t0 += a.chunk_trees, ++c) {
-    const int nt = min(a.chunk_trees, te - t0);
+  for (int t0 = tb; t0 < te; t0 += chunk, ++c) {
+    const int nt = min(chunk, te - t0);
     const uint32_t* cur = (c & 1) ? tbuf1 : tbuf0;
     uint32_t* nxt = (c & 1) ? tbuf0 : tbuf1;
-    const int t1 = t0 + a.chunk_trees;
-    n16 = (t1 < te) ? (min(a.chunk_trees, te - t1) * rw) >> 2 : 0;
-    PF4_LOAD(n16 > 0 ? a.blob + (size_t)t1 * rw : a.blob, n16, T)
+    const int t1 = t0 + chunk;
+    n16 = (t1 < te) ? (min(chunk, te - t1) * rw) >> 2 : 0;
+    PF4_LOAD(n16 > 0 ? blob + (size_t)t1 * rw : blob, n16, T)
     if (missing) {
       acc = traverse_chunk_g<DEPTH, true, ILP, G, LEAF8>(a, cur, nt, g, feat_lane, acc);
     } else {
@@ -880,9 +896,16 @@ int launch_perfect(hipStream_t st, const TreeArgs& a, dim3 grid, size_t lds) {
   const int base = a.variant & 3;
   if (!a.general && (base == 1 || base == 2)) {
     const bool leaf8 = base == 2;
-    const size_t lds_w = lds + (size_t)WIDE_G * TB * 4 + ((a.variant & VAR_NAN_PLANES) ? (size_t)a.n_feat * TB * 4 : 0);
-    if (lds_w > 160 * 1024) return -5;
+    (void)lds;
+    const size_t head = (size_t)(TB + 4) * 4 + (size_t)WIDE_G * TB * 4;
+    const size_t plane = (size_t)a.n_feat * TB * 4;
+    size_t lds_w = head + plane + 2 * (size_t)a.chunk_trees * a.rec_words * 4;
     if ((size_t)a.chunk_trees * a.rec_words > (size_t)TB * WIDE_G * 4 * 4) return -9;
+    if (a.blob_nan) {
+      if (a.chunk_trees_nan < 1 || (size_t)a.chunk_trees_nan * a.rec_words > (size_t)TB * WIDE_G * 4 * 4) return -9;
+      lds_w = max(lds_w, head + 2 * plane + 2 * (size_t)a.chunk_trees_nan * a.rec_words * 4);
+    }
+    if (lds_w > 160 * 1024) return -5;
     if (a.P != 1 || a.rec_words != (leaf8 ? perfect_rec_words8(D) : perfect_rec_words(D, 1))) return -10;
     if (leaf8) {
       err = prepare_launch(tree_perfect_wide_kernel<D, 8, WIDE_G, true>, lds_w);

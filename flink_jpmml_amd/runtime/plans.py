@@ -737,15 +737,16 @@ def dequantize_fp8(q: np.ndarray) -> np.ndarray:
     return torch.from_numpy(np.ascontiguousarray(q, dtype=np.uint8)).view(torch.float8_e4m3fn).float().numpy()
 
 
-def _leaf8_pack(blob: np.ndarray, D: int) -> Tuple[np.ndarray, int, float]:
+def _leaf8_pack(blob: np.ndarray, D: int, scale: Optional[float] = None) -> Tuple[np.ndarray, int, float]:
     """Re-pack a P=1 PERFECT blob with fp8 leaves: the two e4m3 leaves under every last-level node
     go into bits [31:16] of that node's meta (left in [23:16], right in [31:24]); one global
     scale (max |leaf| -> 448) is returned for the epilogue. Record: nodes + default-right words."""
     NI, NL = (1 << D) - 1, 1 << D
     ndr = (NI + 31) // 32
     leaves = blob[:, 2 * NI: 2 * NI + NL].view(np.float32)
-    amax = float(np.max(np.abs(leaves))) if leaves.size else 0.0
-    scale = amax / FP8_MAX if amax > 0 else 1.0
+    if scale is None:
+        amax = float(np.max(np.abs(leaves))) if leaves.size else 0.0
+        scale = amax / FP8_MAX if amax > 0 else 1.0
     q = quantize_fp8(leaves, scale).astype(np.uint32)  # [trees, NL]
     rec = (2 * NI + ndr + 3) & ~3
     out = np.zeros((blob.shape[0], rec), dtype=np.uint32)
@@ -810,7 +811,8 @@ class TreePlan(DevicePlan):
     kind = "tree"
     _STATE = DevicePlan._STATE + ("depth", "n_trees", "layout", "P", "C", "general", "rec_words", "chunk_trees",
                                   "blob", "leaves", "roots", "has_dr", "table", "slots", "splits", "epi_args",
-                                  "variant", "children", "preds", "pool", "trees_tab", "max_steps")
+                                  "variant", "children", "preds", "pool", "trees_tab", "max_steps", "blob_nan",
+                                  "chunk_trees_nan")
 
     WIDE_G = 4  # tree groups of the wide kernel (mirrors csrc)
 
@@ -846,6 +848,7 @@ class TreePlan(DevicePlan):
 
             g = pack_general(spec.trees, spec.weights, spec.P, compiled.schema)
             self.layout, self.variant, self.rec_words, self.chunk_trees = "general", 0, 0, 0
+            self.blob_nan, self.chunk_trees_nan = None, 0
             self.P, self.C = spec.P, spec.C
             self.general = 1 if spec.P > 1 else 0
             self.blob = self._t(g["nodes"].reshape(-1))
@@ -877,42 +880,52 @@ class TreePlan(DevicePlan):
                 variant = "narrow" if self.general else "wide"
             self.variant = 1 if variant == "wide" else 0
             nan_flags = 0
+            blob_nan = None
             if self.variant == 1 and nan_mode == "auto" and not any(t.null_missing for t in spec.trees):
                 if not has_dr:
                     nan_flags = VAR_NAN_FAST
                 elif precision != "fp8" or (2 * F - 1) * TB * 4 < (1 << 16):  # fp8 metas: 16-bit offsets
-                    blob = _nan_planes(blob, depth, F)
+                    blob_nan = _nan_planes(blob, depth, F)
                     nan_flags = VAR_NAN_FAST | VAR_NAN_PLANES
             if precision == "fp8":
                 # e4m3 leaves in the last-level metas, global scale folded into the epilogue
                 if self.general or self.variant != 1:
                     raise NotLowerable("fp8 leaves need the single-accumulator wide kernel (P = 1)")
                 blob, rec, scale = _leaf8_pack(blob, depth)
+                if blob_nan is not None:
+                    blob_nan, _, _ = _leaf8_pack(blob_nan, depth, scale)
                 self.epi_args["a"] = self.epi_args.get("a", 1.0) * scale
                 self.variant = 2
             self.variant |= nan_flags
             self.rec_words = rec
-            if self.variant & 3 in (1, 2):
-                # one 1024-thread workgroup per CU: feature plane(s) + two chunk buffers + [G][256] partials
-                planes = 2 if self.variant & VAR_NAN_PLANES else 1
-                fixed = planes * F * TB * 4 + (TB + 4) * 4 + self.WIDE_G * TB * 4
-                budget = 156 * 1024 - fixed
-                per_chunk = min(budget // 2, 64 * 1024)
+            wide = self.variant & 3 in (1, 2)
+            if wide:
+                # one 1024-thread workgroup per CU: [G][256] partials + feature plane(s) + two chunk
+                # buffers; tiles with missing values use the NaN blob with two planes (own chunk size)
+                fixed = F * TB * 4 + (TB + 4) * 4 + self.WIDE_G * TB * 4
+                per_chunk = min((156 * 1024 - fixed) // 2, 64 * 1024)
             else:
                 fixed = F * TB * 4 + (TB + 4) * 4 + (self.C * TB * 4 if self.general else 0)
                 budget = max(lds_budget - fixed, 2 * rec * 4)  # two chunk buffers (double buffering)
                 per_chunk = min(budget // 2, 32 * 1024)  # register prefetch holds <= 32 KiB per chunk
             if rec * 4 > per_chunk:
                 raise NotLowerable(f"depth-{depth} tree record ({rec * 4} B) exceeds the 32 KiB chunk")
-            self.chunk_trees = int(max(1, min(self.n_trees, per_chunk // (rec * 4))))
-            if max_chunk_trees > 0:
-                self.chunk_trees = min(self.chunk_trees, max_chunk_trees)
+            self.chunk_trees = self._chunk(per_chunk // (rec * 4), wide, max_chunk_trees)
+            self.blob_nan, self.chunk_trees_nan = None, 0
+            if blob_nan is not None:
+                per_nan = min((156 * 1024 - fixed - F * TB * 4) // 2, 64 * 1024)
+                if rec * 4 <= per_nan:
+                    self.chunk_trees_nan = self._chunk(per_nan // (rec * 4), wide, max_chunk_trees)
+                    self.blob_nan = self._t(blob_nan.reshape(-1).view(np.int32))
+                else:
+                    self.variant &= ~(VAR_NAN_FAST | VAR_NAN_PLANES)
             self.blob = self._t(blob.reshape(-1).view(np.int32))
             self.roots = self.leaves = None
         else:
             if precision == "fp8":
                 raise NotLowerable("fp8 leaves need the PERFECT layout")
             nodes, leaves, roots, has_dr = _pointer_pack(spec.trees, spec.weights, spec.P)
+            self.blob_nan, self.chunk_trees_nan = None, 0
             self.rec_words = 0
             self.chunk_trees = 0
             self.variant = 0
@@ -924,6 +937,16 @@ class TreePlan(DevicePlan):
         self.slots = self._t(np.zeros(self.n_trees, dtype=np.int32)) if self.general else None
         self.splits = splits
         self._partial = None
+
+    def _chunk(self, fit: int, wide: bool, cap: int) -> int:
+        """Trees per LDS chunk. Wide kernel: whole ILP batches per tree group (G groups x 8-wide
+        walks) — every group gets the same count (no barrier imbalance) and no latency-bound short
+        tail batches (measured: 64 > 79 > 57 trees at depth 6)."""
+        c = int(max(1, min(self.n_trees, fit)))
+        if wide and c < self.n_trees:
+            q = 8 * self.WIDE_G if c >= 16 * self.WIDE_G else 2 * self.WIDE_G
+            c = max(q, c // q * q) if c >= q else c
+        return min(c, cap) if cap > 0 else c
 
     @staticmethod
     def _general_spec(compiled) -> "EnsembleSpec":
@@ -953,6 +976,7 @@ class TreePlan(DevicePlan):
             a.blob, a.roots, a.leaves, a.tree_slot = ptr(self.blob), ptr(self.roots), ptr(self.leaves), ptr(self.slots)
             a.n_trees, a.rec_words, a.chunk_trees, a.P = self.n_trees, self.rec_words, self.chunk_trees, self.P
             a.C, a.general, a.variant = self.C, self.general, self.variant
+            a.blob_nan, a.chunk_trees_nan = ptr(getattr(self, "blob_nan", None)), getattr(self, "chunk_trees_nan", 0)
             a.epi = _epilogue(table=self.table, write_probs=with_probs, **self.epi_args)
             cache[with_probs] = a
         b = TreeArgs()
