@@ -49,9 +49,14 @@ class FsReader:
         if kind == "local":
             local = urlparse(path).path if path.startswith("file://") else path
             with open(local, "rb") as fh:  # loan pattern: the handle is always closed
-                return fh.read()
-        with fs.open(path, "rb") as fh:
-            return fh.read()
+                data = fh.read()
+        else:
+            with fs.open(path, "rb") as fh:
+                data = fh.read()
+        from ..utils.faults import injector
+
+        fi = injector()
+        return fi.on_read(path, data) if fi.active else data
 
     def build_distributed_path(self) -> str:
         """Whole document as text (the reference's — oddly named — ``buildDistributedPath``)."""

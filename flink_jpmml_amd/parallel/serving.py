@@ -28,6 +28,7 @@ from ..api.managers import metadata_manager
 from ..api.reader import ModelReader
 from ..domain.control import AddMessage, DelMessage, ServingMessage
 from ..domain.model_id import ModelId, ModelInfo
+from ..utils.faults import guarded_collective, injector
 from .dist import DistContext, all_gather_varlen, broadcast_control, broadcast_object, broadcast_plan
 
 logger = logging.getLogger(__name__)
@@ -49,12 +50,13 @@ class DistributedServing:
         self.models: "OrderedDict[ModelId, _Entry]" = OrderedDict()
         self.cache_capacity = cache_capacity
         self.plan_opts = plan_opts or {}
+        self.batches = 0  # micro-batches scored on this rank (fault-injection clock)
 
     # ------------------------------------------------------------------ control plane
     def apply_control(self, messages: Optional[Sequence[ServingMessage]] = None) -> List[ServingMessage]:
         """Collective: rank 0 passes its control messages, other ranks pass None. Returns the
         replicated messages (in order) after applying them on every rank."""
-        msgs = broadcast_control(messages, self.ctx)
+        msgs = guarded_collective(broadcast_control, messages, self.ctx, what="control broadcast")
         for m in msgs:
             if isinstance(m, DelMessage):
                 self.models.pop(m.model_id, None)
@@ -103,6 +105,8 @@ class DistributedServing:
     # ------------------------------------------------------------------ data plane
     def score(self, model_id: str, X: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
         """Score this rank's shard for ``model_id``; unknown models give all-invalid rows."""
+        injector().on_batch(self.ctx.rank, self.batches)
+        self.batches += 1
         mid = ModelId.from_identifier(model_id)
         e = self.models.get(mid)
         if e is None:
@@ -124,6 +128,8 @@ class DistributedServing:
         import torch
 
         dev = self.ctx.device if self.ctx.backend == "nccl" else torch.device("cpu")
-        s = all_gather_varlen(torch.as_tensor(np.asarray(scores, np.float32), device=dev), self.ctx)
-        v = all_gather_varlen(torch.as_tensor(np.asarray(valid, np.uint8), device=dev), self.ctx)
+        s = guarded_collective(all_gather_varlen, torch.as_tensor(np.asarray(scores, np.float32), device=dev),
+                               self.ctx, what="score all-gather")
+        v = guarded_collective(all_gather_varlen, torch.as_tensor(np.asarray(valid, np.uint8), device=dev),
+                               self.ctx, what="valid all-gather")
         return s.cpu().numpy(), v.cpu().numpy().astype(bool)

@@ -643,6 +643,21 @@ def _chain_spec(compiled, ev: MiningEvaluator, field_index, lower=lower_binary_t
                                              link=LINKS[norm]), cats)
 
 
+def shard_spec(spec: EnsembleSpec, rank: int, world: int) -> EnsembleSpec:
+    """Rank ``rank``'s contiguous slice of a single-accumulator ensemble with a raw epilogue
+    (``mode=AFFINE, a=1, b=0``, no link): the kernel writes ``Σ w_i·leaf_i`` over its trees, or
+    NaN/invalid for rows a null-on-missing tree poisons."""
+    if spec.P != 1 or spec.epi["mode"] not in (EPI_AFFINE, EPI_LOGISTIC2):
+        raise NotLowerable("tree sharding supports single-score ensembles (regression / binary chains)")
+    if not 0 <= rank < world or len(spec.trees) < world:
+        raise ValueError(f"cannot shard {len(spec.trees)} trees over {world} ranks (rank {rank})")
+    base, rem = divmod(len(spec.trees), world)
+    lo = rank * base + min(rank, rem)
+    hi = lo + base + (1 if rank < rem else 0)
+    return EnsembleSpec(spec.trees[lo:hi], spec.weights[lo:hi], 1, 1, dict(mode=EPI_AFFINE, a=1.0, b=0.0),
+                        None, spec.slots[lo:hi] if spec.slots is not None else None)
+
+
 def _perfect_pack(trees: List[BinaryTree], weights: List[float], P: int, D: int) -> Tuple[np.ndarray, int, bool]:
     """Pack trees into the PERFECT layout (heap order, root = node 1):
 
@@ -812,15 +827,20 @@ class TreePlan(DevicePlan):
     _STATE = DevicePlan._STATE + ("depth", "n_trees", "layout", "P", "C", "general", "rec_words", "chunk_trees",
                                   "blob", "leaves", "roots", "has_dr", "table", "slots", "splits", "epi_args",
                                   "variant", "children", "preds", "pool", "trees_tab", "max_steps", "blob_nan",
-                                  "chunk_trees_nan")
+                                  "chunk_trees_nan", "full_epi", "labels")
 
     WIDE_G = 4  # tree groups of the wide kernel (mirrors csrc)
 
     def __init__(self, compiled, device, layout: str = "auto", lds_budget: int = 80 * 1024, splits: int = 0,
-                 variant: str = "auto", precision: str = "fp32", nan_mode: str = "auto", max_chunk_trees: int = 0):
+                 variant: str = "auto", precision: str = "fp32", nan_mode: str = "auto", max_chunk_trees: int = 0,
+                 tree_shard: Optional[Tuple[int, int]] = None):
         """``nan_mode`` (wide PERFECT kernel): ``"auto"`` keeps tiles with missing values on the fast
         traversal whenever the ensemble has no null-on-missing trees (default-right nodes read a
-        NaN -> +inf second feature plane, :func:`_nan_planes`); ``"off"``: per-node missing test."""
+        NaN -> +inf second feature plane, :func:`_nan_planes`); ``"off"``: per-node missing test.
+
+        ``tree_shard=(rank, world)``: keep only this rank's contiguous slice of the ensemble and
+        emit the RAW weighted leaf sum (the full epilogue is kept in ``full_epi`` and applied after
+        the cross-rank ``all_reduce``, :mod:`flink_jpmml_amd.parallel.tree_shard`)."""
         super().__init__(compiled, device)
         if nan_mode not in ("auto", "off"):
             raise ValueError("nan_mode must be 'auto' or 'off'")
@@ -835,6 +855,11 @@ class TreePlan(DevicePlan):
                 if layout != "auto":
                     raise
                 spec, layout = self._general_spec(compiled), "general"
+        self.full_epi, self.labels = dict(spec.epi), spec.labels
+        if tree_shard is not None:
+            if layout == "general":
+                raise NotLowerable("tree sharding needs the binary (perfect / pointer) layouts")
+            spec = shard_spec(spec, *tree_shard)
         self.spec = spec
         self.epi_args = dict(spec.epi)
         F = compiled.n_features

@@ -142,3 +142,95 @@ def test_distributed_serving(fixtures_dir):
         assert not any(v2)  # model without a target -> EmptyScore everywhere
         assert not any(v3)  # deleted -> EmptyScore
         assert len(meta) == 1
+
+
+# ------------------------------------------------------------------------------ tree sharding
+def w_tree_shard(ctx, objective, missing):
+    from flink_jpmml_amd.bench.synth import gbdt_pmml, stream_matrix
+    from flink_jpmml_amd.parallel import TreeShardedScorer
+    from flink_jpmml_amd.runtime.compiled import CompiledPmml
+
+    c = CompiledPmml.from_string(gbdt_pmml(n_trees=37, depth=5, n_features=10, seed=4, objective=objective,
+                                           missing_strategy=missing))
+    X = stream_matrix(2000, c.n_features, seed=5, missing_rate=0.03)
+    ts = TreeShardedScorer(c, ctx)
+    s, v = ts.score(X)
+    return ts.n_trees_local, s.numpy(), v.numpy()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("objective,missing", [("regression", "defaultChild"), ("binary", "defaultChild"),
+                                               ("regression", "nullPrediction")])
+def test_tree_sharded_ensemble_matches_oracle(world, objective, missing):
+    """TP over trees: each rank scores its slice, all_reduce(SUM/MIN) + epilogue == full model."""
+    from flink_jpmml_amd.bench.synth import gbdt_pmml, stream_matrix
+    from flink_jpmml_amd.runtime.compiled import CompiledPmml
+
+    res = _run(world, w_tree_shard, objective, missing)
+    assert sum(r[0] for r in res.values()) == 37
+    c = CompiledPmml.from_string(gbdt_pmml(n_trees=37, depth=5, n_features=10, seed=4, objective=objective,
+                                           missing_strategy=missing))
+    X = stream_matrix(2000, c.n_features, seed=5, missing_rate=0.03)
+    ref, vref = c.score_matrix_oracle(X)
+    for r in range(world):
+        _, s, v = res[r]
+        assert (v == vref).all()
+        if missing == "nullPrediction":
+            assert not vref.all() and vref.any()
+        if objective == "regression":
+            np.testing.assert_allclose(s[vref], ref[vref], atol=2e-5)
+        else:
+            assert (s[vref] == ref[vref]).all()
+        np.testing.assert_array_equal(s, res[0][1])
+
+
+def test_tree_shard_rejects_multiclass():
+    from flink_jpmml_amd.bench.synth import random_forest_pmml
+    from flink_jpmml_amd.parallel import tree_shard_supported
+    from flink_jpmml_amd.runtime.compiled import CompiledPmml
+
+    c = CompiledPmml.from_string(random_forest_pmml(n_trees=4, depth=3, n_features=5, n_classes=3, seed=1))
+    assert "single-score" in tree_shard_supported(c)
+
+
+# ------------------------------------------------------------------ fault injection (SURVEY §5.3)
+def _kill_entry(rank, world, port, kmeans_path, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), FJA_FAULTS="kill_rank=1@2")
+    from flink_jpmml_amd.domain import AddMessage
+    from flink_jpmml_amd.parallel import init_from_env
+    from flink_jpmml_amd.parallel.serving import DistributedServing
+    from flink_jpmml_amd.utils.faults import RankFailure
+
+    ctx = init_from_env(backend="gloo", timeout_s=20)
+    srv = DistributedServing(ctx)
+    name = "a1b2c3d4-0000-4000-8000-0000000000aa"
+    srv.apply_control([AddMessage(name, 1, kmeans_path)] if rank == 0 else None)
+    X = np.ones((3, 4))
+    done = 0
+    try:
+        for _ in range(5):
+            srv.gather(*srv.score(f"{name}_1", X))
+            done += 1
+        q.put((rank, ("finished", done)))
+    except RankFailure as e:
+        q.put((rank, ("rank-failure", done, str(e)[:200])))
+    os._exit(0)
+
+
+def test_killed_rank_surfaces_as_rank_failure(fixtures_dir):
+    """kill_rank=1@2: rank 1 exits before its third micro-batch; rank 0's next all-gather raises
+    RankFailure (not a hang) after exactly two completed batches."""
+    from flink_jpmml_amd.utils.faults import EXIT_KILLED_RANK
+
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_kill_entry, args=(r, 2, port, fixtures_dir["kmeans"], q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    r, res = q.get(timeout=90)
+    for p in procs:
+        p.join(timeout=60)
+    assert r == 0 and res[0] == "rank-failure" and res[1] == 2
+    assert procs[1].exitcode == EXIT_KILLED_RANK

@@ -1,0 +1,66 @@
+"""Fault-injection hooks and the watchdog: fail-load, torn PMML, heartbeat timeout."""
+
+import time
+
+import pytest
+
+from flink_jpmml_amd.api.exceptions import ModelLoadingException
+from flink_jpmml_amd.utils.faults import FaultInjector, RankFailure, Watchdog, guarded_collective, set_injector
+
+
+@pytest.fixture
+def faults():
+    yield set_injector
+    set_injector(None)
+
+
+def test_parse_env_spec():
+    fi = FaultInjector.parse("fail_load=bad.xml; corrupt_pmml=torn ;kill_rank=1@3")
+    assert fi.fail_load == ["bad.xml"] and fi.corrupt_pmml == ["torn"] and fi.kill_rank == {1: 3}
+    assert not FaultInjector.parse("").active
+    with pytest.raises(ValueError):
+        FaultInjector.parse("explode=1")
+
+
+def test_fail_load_is_fatal_in_static_operator(fixtures_dir, faults):
+    from flink_jpmml_amd.api.reader import ModelReader
+    from flink_jpmml_amd.stream.operators import EvaluationFunction
+
+    faults(FaultInjector(fail_load=["kmeans"]))
+    with pytest.raises(OSError, match="injected"):
+        ModelReader(fixtures_dir["kmeans"]).read_bytes()
+    fn = EvaluationFunction(ModelReader(fixtures_dir["kmeans"]), lambda e, m: None)
+    with pytest.raises(ModelLoadingException):
+        fn.open(None)
+
+
+def test_torn_pmml_never_scores(fixtures_dir, faults):
+    from flink_jpmml_amd.api.pmml_model import PmmlModel
+    from flink_jpmml_amd.api.reader import ModelReader
+
+    ok = PmmlModel.from_reader(ModelReader(fixtures_dir["kmeans"]))
+    assert ok is not None
+    faults(FaultInjector(corrupt_pmml=["kmeans"]))
+    with pytest.raises(Exception):
+        PmmlModel.from_reader(ModelReader(fixtures_dir["kmeans"]))
+
+
+def test_watchdog_fires_without_heartbeat():
+    fired = []
+    with Watchdog(0.2, on_timeout=lambda: fired.append(time.monotonic())) as wd:
+        for _ in range(6):  # kicked: no fire
+            time.sleep(0.05)
+            wd.kick()
+        assert not fired
+        time.sleep(0.5)
+    assert wd.fired and len(fired) == 1
+
+
+def test_guarded_collective_wraps_peer_errors():
+    def boom():
+        raise RuntimeError("Connection closed by peer")
+
+    with pytest.raises(RankFailure) as ei:
+        guarded_collective(boom, what="all-gather")
+    assert isinstance(ei.value.__cause__, RuntimeError)
+    assert guarded_collective(lambda x: x + 1, 1) == 2
