@@ -79,3 +79,24 @@ def test_parse_file_chunks(tmp_path, kmeans):
     p = RecordParser(kmeans, kmeans.active_fields)
     got = np.concatenate(list(p.parse_file(str(path), chunk_bytes=50_000)))
     np.testing.assert_array_equal(got, X)
+
+
+@pytest.mark.parametrize("sanitizer", ["address,undefined", "thread"])
+def test_ingest_under_host_sanitizers(tmp_path, sanitizer):
+    """the C++ host ingest built with ASan+UBSan / TSan and driven by a standalone
+    edge-case harness (exact-size buffers, CRLF, ragged rows, caps inside another thread's range)."""
+    import os
+    import shutil
+    import subprocess
+
+    if shutil.which("g++") is None:
+        pytest.skip("no g++")
+    src = os.path.join(os.path.dirname(__file__), "..", "flink_jpmml_amd", "native", "csrc", "ingest_selftest.cpp")
+    exe = str(tmp_path / "selftest")
+    subprocess.run(["g++", "-std=c++17", "-g", "-O1", f"-fsanitize={sanitizer}", "-fno-omit-frame-pointer",
+                    "-pthread", src, "-o", exe], check=True, capture_output=True, timeout=300)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:halt_on_error=1", UBSAN_OPTIONS="halt_on_error=1",
+               TSAN_OPTIONS="halt_on_error=1")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "ingest selftest: ok" in r.stdout
