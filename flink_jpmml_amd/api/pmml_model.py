@@ -18,6 +18,7 @@ the case where ``predict`` would return ``EmptyScore``.
 
 from __future__ import annotations
 
+import logging
 import math
 from typing import Any, Dict, List, Optional, Sequence
 
@@ -29,12 +30,16 @@ from .evaluator import EMPTY_EVALUATOR, Evaluator
 from .exceptions import InputValidationException, JPMMLExtractionException
 from .pipeline import FieldValue, Pipeline
 from .reader import ModelReader
-from .vectors import Vector, as_vector, pack_vectors
+from .batch import PredictionBatch, RecordBatch, as_record_batch
+from .vectors import Vector, as_vector, pack_vectors_masked
+
+logger = logging.getLogger(__name__)
 
 
 class PmmlModel(Pipeline):
     def __init__(self, evaluator: Evaluator):
         self.evaluator = evaluator
+        self._scorer = None
 
     # ------------------------------------------------------------------ factories
     @staticmethod
@@ -81,8 +86,37 @@ class PmmlModel(Pipeline):
     def is_empty(self) -> bool:
         return self.evaluator is EMPTY_EVALUATOR
 
+    # ------------------------------------------------------------------ device binding
+    def bind(self, device: Any = None, config: Any = None, pipeline: Any = None, plan: Any = None) -> "PmmlModel":
+        """Attach the scorer that record batches go through: the HIP plan on ``device`` (shared
+        ``pipeline`` of streams + input ring), or the host oracle. Operators call this once per
+        subtask and model; :func:`flink_jpmml_amd.runtime.engine.make_scorer` applies the
+        config's fallback policy."""
+        if not self.is_empty:
+            from ..runtime.engine import make_scorer
+
+            self._scorer = make_scorer(self.evaluator.model, device, config, pipeline, plan)
+        return self
+
+    @property
+    def scorer(self):
+        if self._scorer is None and not self.is_empty:
+            self.bind(None)
+        return self._scorer
+
+    @property
+    def on_device(self) -> bool:
+        return self._scorer is not None and getattr(self._scorer, "kind", "") == "device"
+
     # ------------------------------------------------------------------ per-record pipeline
-    def predict(self, input_vector: Any, replace_nan: Optional[float] = None) -> Prediction:
+    def predict(self, input_vector: Any, replace_nan: Optional[float] = None):
+        """Score one vector → :class:`Prediction` (the reference's contract), or a whole
+        :class:`RecordBatch` / ``[rows, fields]`` matrix → :class:`PredictionBatch` (asynchronous
+        on the device; row ``i`` equals ``predict(batch.vector(i))``)."""
+        batch = as_record_batch(input_vector)
+        if batch is not None:
+            return self.predict_records(batch, replace_nan)
+
         def run() -> float:
             validated = self.validate_input(input_vector)
             prepared = self.prepare_input(validated, replace_nan)
@@ -172,6 +206,20 @@ class PmmlModel(Pipeline):
     extractTarget = extract_target  # noqa: N815
 
     # ------------------------------------------------------------------ batch API
+    def predict_records(self, batch: RecordBatch, replace_nan: Optional[float] = None) -> PredictionBatch:
+        """Columnar ``predict``: validation (row width), preparation, evaluation and extraction for
+        a whole batch on the bound scorer. Never raises for bad records: rows the per-record path
+        would score as ``EmptyScore`` are invalid in the result."""
+        n = len(batch)
+        if self.is_empty:  # EmptyEvaluatorException for every record -> EmptyScore
+            return PredictionBatch.empty(n)
+        width = len(self.evaluator.model.active_fields)
+        if batch.n_features != width:  # InputValidationException for every record
+            logger.warning("Error while validate input: batch width %d is not conform to model size %d",
+                           batch.n_features, width)
+            return PredictionBatch.empty(n)
+        return self.scorer.submit_batch(batch, replace_nan)
+
     def predict_batch(self, X: Any, replace_nan: Optional[float] = None, device: Any = None, **opts):
         """Score a ``[rows, active_fields]`` matrix (numpy or torch; NaN = missing) or a sequence
         of vectors. Returns ``(scores, valid)``; numpy on host, torch tensors on device."""
@@ -185,10 +233,9 @@ class PmmlModel(Pipeline):
         """Batch version of :meth:`predict` over vector objects → list of :class:`Prediction`."""
         compiled = self.evaluator.model
         width = len(compiled.active_fields)
-        vs = [as_vector(v) for v in vectors]
-        ok_size = np.array([v.size == width for v in vs], dtype=bool)
-        X = pack_vectors([v if o else np.full(width, np.nan) for v, o in zip(vs, ok_size)], width)
-        scores, valid = compiled.score_matrix(X, replace_nan=replace_nan, device=device, **opts)
+        X, absent, ok_size = pack_vectors_masked(vectors, width)
+        # replace_nan fills only the entries sparse vectors do not store (per-record parity)
+        scores, valid = compiled.score_matrix(X, replace_nan=replace_nan, device=device, absent=absent, **opts)
         if not isinstance(scores, np.ndarray):
             scores = scores.detach().cpu().numpy()
             valid = valid.detach().cpu().numpy()

@@ -113,6 +113,30 @@ def pack_vectors(vectors: Iterable[VectorLike], width: int) -> np.ndarray:
     return out
 
 
+def pack_vectors_masked(vectors: Iterable[VectorLike], width: int):
+    """Like :func:`pack_vectors` but for vectors of any size: returns ``(X, absent, ok)`` where
+    ``absent[i, j]`` marks entries a sparse vector does not store (the only positions the
+    reference's ``replaceNaN`` fills, `S/api/PmmlModel.scala:143-152`; a NaN *stored* in a vector
+    is kept as a PMML missing value) and ``ok[i]`` is False for vectors whose size is not
+    ``width`` (their row is all-NaN; the per-record path fails their validation)."""
+    vs: List[Vector] = [as_vector(v) for v in vectors]
+    n = len(vs)
+    out = np.full((n, width), np.nan)
+    absent = np.zeros((n, width), dtype=bool)
+    ok = np.ones(n, dtype=bool)
+    for i, v in enumerate(vs):
+        if v.size != width:
+            ok[i] = False
+            continue
+        if isinstance(v, SparseVector):
+            absent[i, :] = True
+            absent[i, v.indices] = False
+            out[i, v.indices] = v.data
+        else:
+            out[i, :] = v.data
+    return out, absent, ok
+
+
 def to_csr(vectors: Sequence[VectorLike], width: int):
     """CSR view ``(indptr int32, indices int32, values float32)`` of a vector batch — the input of the
     device-side ``pack_csr`` kernel (dense vectors contribute all their entries)."""

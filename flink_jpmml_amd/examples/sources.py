@@ -18,6 +18,7 @@ from typing import Dict, Iterator, List, Optional, Sequence, Tuple
 
 from ..api.vectors import DenseVector
 from ..domain.control import AddMessage
+from ..stream.clock import current_clock
 from ..stream.functions import SourceContext, SourceFunction
 
 
@@ -66,7 +67,7 @@ class IrisSource(SourceFunction):
             yield Iris(mid, *vals, now_ms())
             i += 1
             if self.rate:
-                time.sleep(1.0 / self.rate)
+                current_clock().sleep(1.0 / self.rate)  # the job clock fires due timers meanwhile
 
     def run(self, ctx: SourceContext) -> None:
         for ev in self._gen():
@@ -110,7 +111,7 @@ class ControlSource(SourceFunction):
             if not self._running or (self.n is not None and count >= self.n):
                 break
             if self.max_interval_ms:
-                time.sleep(rng.uniform(0, self.max_interval_ms) / 1000.0)
+                current_clock().sleep(rng.uniform(0, self.max_interval_ms) / 1000.0)
             yield AddMessage(mid, self.version, path, now_ms())
             count += 1
 

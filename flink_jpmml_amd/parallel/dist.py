@@ -20,7 +20,7 @@ from __future__ import annotations
 
 import datetime
 import os
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 from typing import List, Optional, Sequence, Tuple
 
 import torch
@@ -34,10 +34,27 @@ class DistContext:
     local_rank: int = 0
     backend: Optional[str] = None
     device: torch.device = torch.device("cpu")
+    force: bool = False
+    """Run the collective code path even at world size 1 (a 1-rank RCCL group: lets a single-GPU
+    box execute every broadcast / all-gather / all-reduce on real RCCL)."""
+    groups: dict = field(default_factory=dict)
 
     @property
     def is_distributed(self) -> bool:
-        return self.world_size > 1 and dist.is_available() and dist.is_initialized()
+        return (self.world_size > 1 or self.force) and dist.is_available() and dist.is_initialized()
+
+    def group(self, name: str):
+        """Named process group: ``"ctrl"`` (gloo, CPU objects: control replication, checkpoint
+        manifests, sink gathers) or ``"model"`` (the data backend: model tensor replication from
+        the loader thread). Separate groups keep the collectives of different threads from
+        interleaving on one communicator. Created eagerly by :func:`init_from_env` (every rank
+        must create groups in the same order)."""
+        if not self.is_distributed:
+            return None
+        g = self.groups.get(name)
+        if g is None:
+            raise KeyError(f"process group {name!r} was not created (init_from_env creates ctrl/model)")
+        return g
 
     @property
     def is_root(self) -> bool:
@@ -51,28 +68,46 @@ class DistContext:
                 dist.barrier()
 
 
-def init_from_env(backend: Optional[str] = None, timeout_s: float = 600.0) -> DistContext:
+def init_from_env(backend: Optional[str] = None, timeout_s: Optional[float] = None, force: bool = False) -> DistContext:
     """Initialise from torchrun-style env vars (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_ADDR/PORT).
 
-    ``backend=None`` picks ``nccl`` (RCCL) when a GPU is visible, else ``gloo``."""
+    ``backend=None`` picks ``nccl`` (RCCL) when a GPU is visible, else ``gloo``. ``force=True``
+    creates the process group even at world size 1 (RCCL on a single-GPU box)."""
+    if timeout_s is None:
+        timeout_s = float(os.environ.get("FJA_DIST_TIMEOUT_S", "600"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
     use_gpu = torch.cuda.is_available()
     if backend is None:
         backend = "nccl" if use_gpu else "gloo"
-    device = torch.device("cuda", local % max(1, torch.cuda.device_count())) if use_gpu and backend == "nccl" \
-        else (torch.device("cuda", local % max(1, torch.cuda.device_count())) if use_gpu else torch.device("cpu"))
+    device = torch.device("cuda", local % max(1, torch.cuda.device_count())) if use_gpu else torch.device("cpu")
     if use_gpu:
         torch.cuda.set_device(device)
-    ctx = DistContext(rank, world, local, backend, device)
-    if world > 1 and not dist.is_initialized():
+    ctx = DistContext(rank, world, local, backend, device, force=force)
+    if (world > 1 or force) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if world == 1:
+            os.environ.setdefault("MASTER_PORT", str(_free_port()))
         kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
         if backend == "nccl":
             kw["device_id"] = device
         dist.init_process_group(**kw)
+    if ctx.is_distributed:
+        to = datetime.timedelta(seconds=timeout_s)
+        ctx.groups["ctrl"] = dist.new_group(backend="gloo", timeout=to)
+        ctx.groups["model"] = dist.new_group(backend=backend, timeout=to)
     return ctx
+
+
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
 
 
 def shutdown(ctx: DistContext) -> None:
@@ -90,20 +125,58 @@ def shard_range(n: int, rank: int, world: int) -> Tuple[int, int]:
 # --------------------------------------------------------------------------- replication
 
 
-def broadcast_object(obj, ctx: DistContext, src: int = 0):
+def _obj_device(ctx: DistContext, group):
+    """Device for object collectives: CPU on gloo groups, the GPU on the RCCL default group."""
+    if group is not None and group is ctx.groups.get("ctrl"):
+        return None
+    if group is None and ctx.backend == "nccl":
+        return ctx.device
+    if group is not None and group is ctx.groups.get("model") and ctx.backend == "nccl":
+        return ctx.device
+    return None
+
+
+def broadcast_object(obj, ctx: DistContext, src: int = 0, group=None):
     if not ctx.is_distributed:
         return obj
     box = [obj if ctx.rank == src else None]
-    dist.broadcast_object_list(box, src=src, device=ctx.device if ctx.backend == "nccl" else None)
+    dist.broadcast_object_list(box, src=src, group=group, device=_obj_device(ctx, group))
     return box[0]
 
 
-def broadcast_tensors(tensors: Optional[dict], spec: Optional[dict], ctx: DistContext, src: int = 0) -> dict:
+def gather_object(obj, ctx: DistContext, dst: int = 0, group=None):
+    """Gather one picklable object per rank to ``dst`` (others get None). Rank order."""
+    if not ctx.is_distributed:
+        return [obj]
+    out = [None] * ctx.world_size if ctx.rank == dst else None
+    dist.gather_object(obj, out, dst=dst, group=group)
+    return out
+
+
+def all_gather_object(obj, ctx: DistContext, group=None) -> list:
+    if not ctx.is_distributed:
+        return [obj]
+    out = [None] * ctx.world_size
+    dist.all_gather_object(out, obj, group=group)
+    return out
+
+
+def all_reduce_max(x: int, ctx: DistContext, group=None) -> int:
+    if not ctx.is_distributed:
+        return x
+    dev = _obj_device(ctx, group) or torch.device("cpu")
+    t = torch.tensor([int(x)], dtype=torch.int64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return int(t.item())
+
+
+def broadcast_tensors(tensors: Optional[dict], spec: Optional[dict], ctx: DistContext, src: int = 0,
+                      group=None) -> dict:
     """Broadcast a dict of tensors whose shapes/dtypes are given by ``spec`` (known on all ranks).
     Tensors travel in one flat byte buffer over the RCCL group (one collective, not one per tensor)."""
     if not ctx.is_distributed:
         return dict(tensors or {})
-    dev = ctx.device if ctx.backend == "nccl" else torch.device("cpu")
+    dev = ctx.device if ctx.backend == "nccl" and group is not ctx.groups.get("ctrl") else torch.device("cpu")
     names = sorted(spec)
     sizes = []
     for k in names:
@@ -120,7 +193,7 @@ def broadcast_tensors(tensors: Optional[dict], spec: Optional[dict], ctx: DistCo
             t = tensors[k].contiguous()
             buf[off: off + nb].copy_(t.view(-1).view(torch.uint8).to(dev))
             off += nb
-    dist.broadcast(buf, src=src)
+    dist.broadcast(buf, src=src, group=group)
     out = {}
     off = 0
     for k, nb in zip(names, sizes):
@@ -130,9 +203,10 @@ def broadcast_tensors(tensors: Optional[dict], spec: Optional[dict], ctx: DistCo
     return out
 
 
-def broadcast_plan(plan, ctx: DistContext, src: int = 0, device=None):
+def broadcast_plan(plan, ctx: DistContext, src: int = 0, device=None, group=None, obj_group=None):
     """Replicate a device plan from ``src`` to every rank. Returns the local
-    plan (the original object on ``src``)."""
+    plan (the original object on ``src``). ``group`` carries the tensor payload (RCCL),
+    ``obj_group`` the small metadata object."""
     from ..runtime.plans import DevicePlan
 
     if not ctx.is_distributed:
@@ -141,8 +215,14 @@ def broadcast_plan(plan, ctx: DistContext, src: int = 0, device=None):
         meta, tensors = plan.export_state()
     else:
         meta, tensors = None, None
-    meta = broadcast_object(meta, ctx, src)
-    got = broadcast_tensors(tensors, meta["__tensors__"], ctx, src)
+    meta = broadcast_object(meta, ctx, src, group=obj_group if obj_group is not None else group)
+    got = broadcast_tensors(tensors, meta["__tensors__"], ctx, src, group=group)
+    try:
+        from ..utils.metrics import METRICS
+
+        METRICS.inc("dist.bytes_broadcast", sum(t.numel() * t.element_size() for t in got.values()))
+    except Exception:  # noqa: BLE001 - metrics never fail a broadcast
+        pass
     if ctx.rank == src:
         return plan
     return DevicePlan.from_state(meta, got, device or ctx.device)

@@ -79,16 +79,19 @@ class CompiledPmml:
         outs = self.evaluator.compute_outputs(cols, res) if self.model.output else {}
         return res, outs
 
-    def prepare(self, X: np.ndarray, replace_nan: Optional[float] = None) -> tuple:
+    def prepare(self, X: np.ndarray, replace_nan: Optional[float] = None, absent: Optional[np.ndarray] = None) -> tuple:
+        """MiningField preparation of a raw matrix. ``replace_nan`` fills the ``absent`` entries
+        (entries a sparse vector does not store); without a mask every NaN counts as absent."""
         X = np.asarray(X, dtype=np.float64)
         if X.ndim != 2 or X.shape[1] != self.n_features:
             raise ValueError(f"expected a [rows, {self.n_features}] matrix, got {X.shape}")
         if replace_nan is not None:
-            X = np.where(np.isnan(X), replace_nan, X)
+            X = np.where(np.isnan(X) if absent is None else absent, replace_nan, X)
         return self.schema.prepare_matrix(self.active_fields, X, self.mining_fields)
 
-    def score_matrix_oracle(self, X: np.ndarray, replace_nan: Optional[float] = None) -> tuple:
-        P, ok = self.prepare(X, replace_nan)
+    def score_matrix_oracle(self, X: np.ndarray, replace_nan: Optional[float] = None,
+                            absent: Optional[np.ndarray] = None) -> tuple:
+        P, ok = self.prepare(X, replace_nan, absent)
         if not self.target_fields:
             # no named target: JPMML exposes only the synthetic null-named target, which the
             # reference drops (`S/api/pipeline/Pipeline.scala:79-85`) -> extraction fails
@@ -111,11 +114,12 @@ class CompiledPmml:
                 self._plans[key] = p
             return p
 
-    def score_matrix(self, X, replace_nan: Optional[float] = None, device: Any = None, **opts):
+    def score_matrix(self, X, replace_nan: Optional[float] = None, device: Any = None,
+                     absent: Optional[np.ndarray] = None, **opts):
         """Batch scoring; ``device=None`` → host oracle, else the HIP plan on that device."""
         if device is None:
-            return self.score_matrix_oracle(X, replace_nan)
-        return self.plan(device, **opts).score(X, replace_nan=replace_nan)
+            return self.score_matrix_oracle(X, replace_nan, absent)
+        return self.plan(device, **opts).score(X, replace_nan=replace_nan, absent=absent)
 
     def result(self, X: np.ndarray) -> ModelResult:
         P, _ = self.prepare(X)

@@ -1,25 +1,48 @@
 """Pipelined micro-batch scoring engine (host records → GPU → host predictions).
 
 The reference scores one record at a time on the JVM (`S/package.scala:76-79`). Here a stream of
-records is scored in micro-batches through a three-stage pipeline on three HIP streams:
+records is scored in micro-batches through a three-stage pipeline on HIP streams:
 
     H2D stream:   pinned host slice ──copy──▶ device input slot[i % depth]
-    compute:      wait(H2D[i]) ▶ fused prepare + model kernel ▶ device score/valid (step buffer)
-    D2H stream:   wait(compute[i]) ▶ score/valid slice ──copy──▶ pinned host output
+    compute:      wait(H2D[i]) ▶ fused prepare + model kernel ▶ scores written by the epilogue
+                  straight into pinned host memory (zero-copy) [+ optional device mirror]
+    D2H stream:   only for plans without a zero-copy epilogue: device scores ──copy──▶ host
 
-A ring of ``depth`` device input slots lets batch i+1's copy overlap batch i's kernel and batch
-i-1's copy-back. Nothing in :meth:`StreamingScorer.submit` blocks the host; :meth:`wait` is the
-only synchronisation point. PCIe Gen5 (≈50+ GB/s per GPU) is the usual bound for wide fp32
-records; the kernels themselves run far below it (see ``profiles/``).
+A ring of ``depth`` device input slots lets batch i+1's copy overlap batch i's kernel. Nothing in
+:meth:`StreamingScorer.submit_batch` blocks the host: it returns a
+:class:`~flink_jpmml_amd.api.batch.PredictionBatch` future whose buffers the kernel fills; the
+only synchronisation points are reading that future and the in-flight cap (backpressure). PCIe
+Gen5 (≈50+ GB/s per GPU) is the usual bound for wide fp32 records; the kernels run far below it
+(see ``profiles/``).
+
+One :class:`DevicePipeline` (streams + input ring) is shared by every model an operator serves on
+a device, so a dynamic-serving operator with 64 cached models holds one ring, not 64.
+
+Scorers (all expose ``submit_batch(batch, replace_nan) -> PredictionBatch``):
+
+* :class:`StreamingScorer` — device plan on the pipeline (the GPU path);
+* :class:`HostScorer` — vectorised float64 oracle (``device=None`` or an explicit host fallback);
+* :class:`NullScorer` — a model without a target field: every row is ``EmptyScore``.
+
+:func:`make_scorer` picks one under the :class:`~flink_jpmml_amd.config.ScoringConfig` fallback
+policy (never silently: host fallbacks are logged and counted).
 """
 
 from __future__ import annotations
 
+import collections
+import logging
 import time
 from dataclasses import dataclass
 from typing import List, Optional
 
 import numpy as np
+
+from ..api.batch import PredictionBatch, RecordBatch
+from ..utils.metrics import METRICS
+from ..utils.profiling import prange
+
+logger = logging.getLogger(__name__)
 
 
 @dataclass
@@ -31,50 +54,97 @@ class StepHandle:
     out_index: int = 0
 
 
-class StreamingScorer:
-    def __init__(self, plan, micro_batch: int = 131072, depth: int = 3, max_rows: Optional[int] = None,
-                 out_buffers: int = 2, direct_host_output: bool = True, keep_device_output: bool = True,
-                 h2d_streams: int = 1):
+class DevicePipeline:
+    """HIP streams + the device input ring, shareable by several plans on one device. The ring
+    holds ``depth`` flat fp32 slots of ``micro_batch × max_features`` (grown on demand)."""
+
+    def __init__(self, device, micro_batch: int = 1 << 19, depth: int = 3, h2d_streams: int = 1):
         import torch
 
-        self.plan = plan
-        self.device = plan.device
-        self.F = plan.n_features
+        self.device = torch.device(device)
         self.B = int(micro_batch)
         self.depth = int(depth)
-        # each micro-batch copy is split over `h2d_streams` streams: concurrent SDMA engines
-        # (probe: 52.9 GB/s on one stream, 55.5 GB/s on four — profiles/r1_s3_probe_h2d*.json)
+        # each micro-batch copy may be split over `h2d_streams` streams (concurrent SDMA engines;
+        # measured: one stream is best for whole micro-batches — profiles/r1_s4_bench_h2d*.log)
         self.h2ds = [torch.cuda.Stream(self.device) for _ in range(max(1, int(h2d_streams)))]
         self.h2d = self.h2ds[0]
         self.comp = torch.cuda.Stream(self.device)
         self.d2h = torch.cuda.Stream(self.device)
-        self.x_slots = [torch.empty((self.B, self.F), dtype=torch.float32, device=self.device)
-                        for _ in range(self.depth)]
+        self.slot_elems = 0
+        self.slots: List = []
         self.ev_h2d = [[torch.cuda.Event() for _ in self.h2ds] for _ in range(self.depth)]
         self.ev_comp = [torch.cuda.Event() for _ in range(self.depth)]
-        self._used = [False] * self.depth
-        self._slot = 0
+        self.used = [False] * self.depth
+        self.next = 0
+        self._dev_ptr_cache = {}
+
+    def ensure_slots(self, elems: int) -> None:
+        if elems <= self.slot_elems:
+            return
+        import torch
+
+        for t in self.slots:  # queued kernels / copies may still use the old ring
+            t.record_stream(self.comp)
+            for st in self.h2ds:
+                t.record_stream(st)
+        self.slots = [torch.empty(elems, dtype=torch.float32, device=self.device) for _ in range(self.depth)]
+        self.slot_elems = elems
+
+    def host_dev_ptr(self, t):
+        from ..ops._lib import host_device_ptr
+
+        key = (t.data_ptr(), t.numel())
+        p = self._dev_ptr_cache.get(key)
+        if p is None:
+            p = host_device_ptr(t)
+            if len(self._dev_ptr_cache) > 4096:
+                self._dev_ptr_cache.clear()
+            self._dev_ptr_cache[key] = p
+        return p
+
+
+def _pin(X):
+    """Host matrix → contiguous float32 pinned tensor (one host copy)."""
+    import torch
+
+    if isinstance(X, torch.Tensor):
+        src = X.to(torch.float32).contiguous()
+    else:
+        src = torch.from_numpy(np.ascontiguousarray(X, dtype=np.float32))
+    out = torch.empty(src.shape, dtype=torch.float32, pin_memory=True)
+    out.copy_(src)
+    return out
+
+
+class StreamingScorer:
+    kind = "device"
+
+    def __init__(self, plan, micro_batch: int = 131072, depth: int = 3, max_rows: Optional[int] = None,
+                 out_buffers: int = 2, direct_host_output: bool = True, keep_device_output: bool = True,
+                 h2d_streams: int = 1, pipeline: Optional[DevicePipeline] = None, max_inflight: int = 4):
+        self.plan = plan
+        self.device = plan.device
+        self.F = plan.n_features
+        self.pipe = pipeline if pipeline is not None else DevicePipeline(self.device, micro_batch, depth, h2d_streams)
+        self.B = self.pipe.B
+        self.depth = self.pipe.depth
+        self.h2ds, self.h2d, self.comp, self.d2h = self.pipe.h2ds, self.pipe.h2d, self.pipe.comp, self.pipe.d2h
         self.max_rows = max_rows or self.B
-        # step output buffers, used round-robin: step k+1 never waits for step k's consumers
+        # step output buffers of the step API (bench engine mode), used round-robin
         self.n_out = int(out_buffers)
-        self._outs = [self._alloc_out(self.max_rows) for _ in range(self.n_out)]
-        self._out_free: List[Optional[object]] = [None] * self.n_out  # event: consumers of buffer done
+        self._outs = None
+        self._out_free: List[Optional[object]] = [None] * self.n_out
         self._out_i = 0
         self.batch_times_ms: List[float] = []
         # zero-copy sink: the kernel epilogue writes scores straight into pinned host memory over
         # PCIe (no D2H copy commands: small D2H copies were measured to stall the H2D stream)
         self.direct = bool(direct_host_output) and getattr(plan, "supports_direct", False)
         self.keep_device = keep_device_output
-        self._dev_ptr_cache = {}
+        self.max_inflight = int(max_inflight)
+        self._inflight: "collections.deque" = collections.deque()
+        self.rows_submitted = 0
 
-    def _host_dev_ptr(self, t):
-        from ..ops._lib import host_device_ptr
-
-        key = (t.data_ptr(), t.numel())
-        if key not in self._dev_ptr_cache:
-            self._dev_ptr_cache[key] = host_device_ptr(t)
-        return self._dev_ptr_cache[key]
-
+    # ------------------------------------------------------------------ step API (bench engine mode)
     def _alloc_out(self, n: int):
         import torch
 
@@ -83,17 +153,59 @@ class StreamingScorer:
 
     @property
     def score_dev(self):
+        self.ensure_capacity(0)
         return self._outs[(self._out_i - 1) % self.n_out][0]
 
     @property
     def valid_dev(self):
+        self.ensure_capacity(0)
         return self._outs[(self._out_i - 1) % self.n_out][1]
 
     def ensure_capacity(self, n: int) -> None:
-        if n > self.max_rows:
-            self.max_rows = n
-            self._outs = [self._alloc_out(n) for _ in range(self.n_out)]
+        if n > self.max_rows or self._outs is None:
+            if self._outs is not None:
+                # kernels already queued on the compute stream may still write the old buffers:
+                # the caching allocator recycles them only once that stream's queued work is done
+                for pair in self._outs:
+                    for t in pair:
+                        t.record_stream(self.comp)
+            self.max_rows = max(n, self.max_rows)
+            self._outs = [self._alloc_out(self.max_rows) for _ in range(self.n_out)]
             self._out_free = [None] * self.n_out
+
+    def _slot(self, m: int):
+        p = self.pipe
+        p.ensure_slots(p.B * max(self.F, 1))
+        slot = p.next
+        p.next = (slot + 1) % p.depth
+        return slot, p.slots[slot][: m * self.F].view(m, self.F)
+
+    def _enqueue(self, X_src, s: int, e: int, out_score, out_valid, kw) -> None:
+        """H2D rows ``[s, e)`` of ``X_src`` into the next ring slot (or use them in place when they
+        are on the device already) and launch the plan on the compute stream."""
+        import torch
+
+        p = self.pipe
+        m = e - s
+        if X_src.is_cuda:
+            xs, slot = X_src[s:e], None
+        else:
+            slot, xs = self._slot(m)
+            part = -(-m // len(p.h2ds))
+            for j, st in enumerate(p.h2ds):
+                with torch.cuda.stream(st):
+                    if p.used[slot]:
+                        st.wait_event(p.ev_comp[slot])  # kernel finished reading this slot
+                    a, b = j * part, min(m, (j + 1) * part)
+                    if a < b:
+                        xs[a:b].copy_(X_src[s + a:s + b], non_blocking=True)
+                    p.ev_h2d[slot][j].record(st)
+            for ev in p.ev_h2d[slot]:
+                p.comp.wait_event(ev)
+        self.plan.launch(xs, out_score, out_valid, stream=p.comp, **kw)
+        if slot is not None:
+            p.ev_comp[slot].record(p.comp)
+            p.used[slot] = True
 
     def submit(self, X_host, score_host=None, valid_host=None, offset: int = 0) -> StepHandle:
         """Enqueue scoring of a pinned host matrix ``X_host`` ([n, F] float32 tensor). Scores land in
@@ -110,42 +222,26 @@ class StreamingScorer:
             self.comp.wait_event(self._out_free[oi])  # WAR: the step that last used this buffer
         hs = hv = None
         if self.direct and score_host is not None and valid_host is not None:
-            hs, hv = self._host_dev_ptr(score_host), self._host_dev_ptr(valid_host)
+            hs, hv = self.pipe.host_dev_ptr(score_host), self.pipe.host_dev_ptr(valid_host)
             if hs is None or hv is None:
                 hs = hv = None
         for s in range(0, n, self.B):
             e = min(n, s + self.B)
-            m = e - s
-            slot = self._slot
-            self._slot = (slot + 1) % self.depth
-            xs = self.x_slots[slot][:m]
-            part = -(-m // len(self.h2ds))
-            for j, st in enumerate(self.h2ds):
-                with torch.cuda.stream(st):
-                    if self._used[slot]:
-                        st.wait_event(self.ev_comp[slot])  # kernel finished reading this slot
-                    a, b = j * part, min(m, (j + 1) * part)
-                    if a < b:
-                        xs[a:b].copy_(X_host[s + a:s + b], non_blocking=True)
-                    self.ev_h2d[slot][j].record(st)
-            for ev in self.ev_h2d[slot]:
-                self.comp.wait_event(ev)
             if hs is not None:
                 kw = {}
                 if self.keep_device:
                     kw = dict(score2=score_dev[offset + s: offset + e], valid2=valid_dev[offset + s: offset + e])
-                self.plan.launch(xs, hs + 4 * s, hv + s, stream=self.comp, **kw)
+                self._enqueue(X_host, s, e, hs + 4 * s, hv + s, kw)
             else:
-                self.plan.launch(xs, score_dev[offset + s: offset + e], valid_dev[offset + s: offset + e],
-                                 stream=self.comp)
-            self.ev_comp[slot].record(self.comp)
-            self._used[slot] = True
-            if score_host is not None and hs is None:
-                with torch.cuda.stream(self.d2h):
-                    self.d2h.wait_event(self.ev_comp[slot])
-                    score_host[s:e].copy_(score_dev[offset + s: offset + e], non_blocking=True)
-                    if valid_host is not None:
-                        valid_host[s:e].copy_(valid_dev[offset + s: offset + e], non_blocking=True)
+                self._enqueue(X_host, s, e, score_dev[offset + s: offset + e], valid_dev[offset + s: offset + e], {})
+                if score_host is not None:
+                    ev = torch.cuda.Event()
+                    ev.record(self.comp)
+                    with torch.cuda.stream(self.d2h):
+                        self.d2h.wait_event(ev)
+                        score_host[s:e].copy_(score_dev[offset + s: offset + e], non_blocking=True)
+                        if valid_host is not None:
+                            valid_host[s:e].copy_(valid_dev[offset + s: offset + e], non_blocking=True)
         done = torch.cuda.Event()
         if score_host is not None and hs is None:
             done.record(self.d2h)
@@ -186,15 +282,186 @@ class StreamingScorer:
     def wait(handle: StepHandle) -> None:
         handle.done.synchronize()
 
-    def score_numpy(self, X: np.ndarray) -> tuple:
-        """Blocking convenience: score a host numpy matrix, return numpy ``(score, valid)``."""
+    # ------------------------------------------------------------------ future API (DSL)
+    def _throttle(self) -> None:
+        while len(self._inflight) >= self.max_inflight:
+            self._inflight.popleft().synchronize()
+        while self._inflight and self._inflight[0].query():
+            self._inflight.popleft()
+
+    def submit_batch(self, batch: RecordBatch, replace_nan: Optional[float] = None,
+                     keep_device: bool = False) -> PredictionBatch:
+        """Enqueue a whole RecordBatch; returns its :class:`PredictionBatch` future immediately.
+
+        ``X`` may be pinned host memory (copied in ``micro_batch`` slices on the H2D stream),
+        pageable host memory (staged through one pinned copy) or device memory (scored in place).
+        ``keep_device`` additionally keeps ``[n]`` device mirrors of the outputs
+        (``PredictionBatch.device_out``, for an all-gather sink)."""
         import torch
 
-        Xp = torch.from_numpy(np.ascontiguousarray(X, dtype=np.float32)).pin_memory()
-        sh = torch.empty(X.shape[0], dtype=torch.float32).pin_memory()
-        vh = torch.empty(X.shape[0], dtype=torch.uint8).pin_memory()
+        n = len(batch)
+        if n == 0:
+            return PredictionBatch.empty(0)
+        if batch.n_features != self.F:
+            raise ValueError(f"batch has {batch.n_features} features, model expects {self.F}")
+        X = batch.X
+        if replace_nan is not None:  # sparse-absent entries only (host side: rare path)
+            Xn = np.array(batch.numpy(), dtype=np.float32, copy=True)
+            Xn[batch.absent if batch.absent is not None else np.isnan(Xn)] = replace_nan
+            X = Xn
+        with prange("score.stage"):
+            if not isinstance(X, torch.Tensor):
+                X = _pin(X)
+            elif X.is_cuda:
+                if X.dtype != torch.float32 or not X.is_contiguous():
+                    X = X.to(torch.float32).contiguous()
+            elif not X.is_pinned() or X.dtype != torch.float32 or not X.is_contiguous():
+                X = _pin(X)
+        self._throttle()
+        score_h = torch.empty(n, dtype=torch.float32, pin_memory=True)
+        valid_h = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+        dev_out = None
+        hs = hv = None
+        if self.direct:
+            hs, hv = self.pipe.host_dev_ptr(score_h), self.pipe.host_dev_ptr(valid_h)
+            if hs is None or hv is None:
+                hs = hv = None
+        if keep_device or hs is None:
+            with torch.cuda.stream(self.comp):
+                dev_out = (torch.empty(n, dtype=torch.float32, device=self.device),
+                           torch.empty(n, dtype=torch.uint8, device=self.device))
+        with prange("score.enqueue"):
+            for s in range(0, n, self.B):
+                e = min(n, s + self.B)
+                if hs is not None:
+                    kw = dict(score2=dev_out[0][s:e], valid2=dev_out[1][s:e]) if dev_out is not None else {}
+                    self._enqueue(X, s, e, hs + 4 * s, hv + s, kw)
+                else:
+                    self._enqueue(X, s, e, dev_out[0][s:e], dev_out[1][s:e], {})
+            done = torch.cuda.Event()
+            if hs is None:
+                ev = torch.cuda.Event()
+                ev.record(self.comp)
+                with torch.cuda.stream(self.d2h):
+                    self.d2h.wait_event(ev)
+                    score_h.copy_(dev_out[0], non_blocking=True)
+                    valid_h.copy_(dev_out[1], non_blocking=True)
+                    for t in dev_out:
+                        t.record_stream(self.d2h)
+                done.record(self.d2h)
+            else:
+                done.record(self.comp)
+        self._inflight.append(done)
+        self.rows_submitted += n
+        METRICS.inc("scoring.rows_device", n)
+        METRICS.inc("scoring.batches_device")
+        return PredictionBatch(n, score_h, valid_h, done, owner=(X, dev_out), on_done=_observe_latency,
+                               device_out=dev_out, row_ok=batch.size_ok())
+
+    def score_numpy(self, X: np.ndarray) -> tuple:
+        """Blocking convenience: score a host numpy matrix, return numpy ``(score, valid)``."""
         t0 = time.perf_counter()
-        h = self.submit(Xp, sh, vh)
-        self.wait(h)
+        pb = self.submit_batch(RecordBatch(np.asarray(X, dtype=np.float32)))
+        s, v = pb.scores.copy(), pb.valid.copy()
         self.batch_times_ms.append((time.perf_counter() - t0) * 1e3)
-        return sh.numpy().copy(), vh.numpy().astype(bool)
+        return s, v
+
+    def drain(self) -> None:
+        while self._inflight:
+            self._inflight.popleft().synchronize()
+
+
+def _observe_latency(pb: PredictionBatch) -> None:
+    METRICS.observe("scoring.batch_latency_ms", (pb.completed - pb.submitted) * 1e3)
+
+
+class HostScorer:
+    """Vectorised float64 oracle with the scorer interface (host path / explicit fallback)."""
+
+    kind = "host"
+    direct = False
+
+    def __init__(self, compiled, reason: Optional[str] = None):
+        self.compiled = compiled
+        self.reason = reason
+        self.F = compiled.n_features
+
+    def submit_batch(self, batch: RecordBatch, replace_nan: Optional[float] = None,
+                     keep_device: bool = False) -> PredictionBatch:
+        n = len(batch)
+        if n == 0:
+            return PredictionBatch.empty(0)
+        if batch.n_features != self.F:
+            raise ValueError(f"batch has {batch.n_features} features, model expects {self.F}")
+        t0 = time.perf_counter()
+        with prange("score.host"):
+            s, v = self.compiled.score_matrix_oracle(batch.numpy(), replace_nan, batch.absent)
+        METRICS.inc("scoring.rows_host", n)
+        if self.reason is not None:
+            METRICS.inc("scoring.host_fallback_rows", n)
+        METRICS.observe("scoring.batch_latency_ms", (time.perf_counter() - t0) * 1e3)
+        return PredictionBatch(n, s.astype(np.float32), v, row_ok=batch.size_ok())
+
+    def drain(self) -> None:
+        pass
+
+
+class NullScorer:
+    """A model without a named target field: the reference extracts nothing and every record is
+    ``EmptyScore`` (`S/api/PmmlModel.scala:167-174`)."""
+
+    kind = "null"
+    direct = False
+
+    def __init__(self, n_features: int):
+        self.F = n_features
+
+    def submit_batch(self, batch: RecordBatch, replace_nan: Optional[float] = None,
+                     keep_device: bool = False) -> PredictionBatch:
+        METRICS.inc("scoring.empty_score.no_target", len(batch))
+        return PredictionBatch.empty(len(batch))
+
+    def drain(self) -> None:
+        pass
+
+
+def make_scorer(compiled, device, config=None, pipeline: Optional[DevicePipeline] = None, plan=None,
+                lower_error: Optional[str] = None):
+    """The scorer for ``compiled`` on ``device`` under ``config``'s fallback policy.
+
+    * no target field → :class:`NullScorer`;
+    * ``device is None`` → :class:`HostScorer`;
+    * otherwise the device plan; a model the device path cannot lower goes to the host oracle with
+      a WARNING + ``scoring.host_fallback_models`` (``fallback="warn"``), only counted
+      (``"host"``), or fails the load (``"error"``). Device *runtime* errors always propagate."""
+    from ..config import ScoringConfig
+    from .plans import NotLowerable
+
+    cfg = config or ScoringConfig()
+    if not compiled.target_fields:
+        return NullScorer(compiled.n_features)
+    if device is None:
+        return HostScorer(compiled)
+    if plan is None:
+        try:
+            if lower_error is not None:  # the leader rank already failed to lower this model
+                raise NotLowerable(lower_error)
+            with prange("model.lower"):
+                plan = compiled.plan(device, **cfg.lowering_opts())
+        except NotLowerable as e:
+            if cfg.fallback == "error":
+                from ..api.exceptions import ModelLoadingException
+
+                raise ModelLoadingException(f"model {compiled.model_name!r} is not lowerable to {device}: {e}",
+                                            e) from e
+            METRICS.inc("scoring.host_fallback_models")
+            if cfg.fallback == "warn":
+                logger.warning("model %r cannot run on %s (%s): scoring it on the host oracle "
+                               "(set fallback='error' to refuse)", compiled.model_name, device, e)
+            return HostScorer(compiled, reason=str(e))
+    if pipeline is None:
+        pipeline = DevicePipeline(plan.device, cfg.micro_batch, cfg.pipeline_depth)
+    return StreamingScorer(plan, pipeline=pipeline, max_inflight=cfg.max_inflight)
+
+
+__all__ = ["DevicePipeline", "HostScorer", "NullScorer", "StepHandle", "StreamingScorer", "make_scorer"]

@@ -270,8 +270,9 @@ class DevicePlan:
         return (torch.empty(n, dtype=torch.float32, device=self.device),
                 torch.empty(n, dtype=torch.uint8, device=self.device))
 
-    def score(self, X: Any, replace_nan: Optional[float] = None, stream=None):
-        """Score a host (numpy) or device (torch) matrix; returns device tensors ``(score, valid)``."""
+    def score(self, X: Any, replace_nan: Optional[float] = None, stream=None, absent: Any = None):
+        """Score a host (numpy) or device (torch) matrix; returns device tensors ``(score, valid)``.
+        ``replace_nan`` fills the ``absent`` entries (every NaN when no mask is given)."""
         import torch
 
         if isinstance(X, np.ndarray):
@@ -282,7 +283,11 @@ class DevicePlan:
             raise ValueError(f"expected [rows, {self.n_features}] input, got {tuple(Xt.shape)}")
         Xt = Xt.contiguous()
         if replace_nan is not None:
-            Xt = torch.nan_to_num(Xt, nan=float(replace_nan))
+            if absent is None:
+                Xt = torch.nan_to_num(Xt, nan=float(replace_nan))
+            else:
+                mask = torch.as_tensor(np.asarray(absent, dtype=bool)).to(self.device)
+                Xt = torch.where(mask, torch.full_like(Xt, float(replace_nan)), Xt)
         score, valid = self.alloc_outputs(Xt.shape[0])
         self.launch(Xt, score, valid, stream=stream)
         return score, valid.bool()
@@ -1095,10 +1100,15 @@ def compile_plan(compiled, device, **opts) -> DevicePlan:
         if layout.program is not None:
             return DerivedPlan(compiled, device, layout, **opts)
         compiled = FieldView(compiled, layout, prepared=False)
+    # ``precision`` is a policy (fp32 | bf16 | fp8, see config.ScoringConfig): trees take fp8 leaves
+    # only, neural networks take bf16 (also under fp8), every other family stays fp32
+    policy = opts.pop("precision", "fp32")
+    if policy not in ("fp32", "bf16", "fp8"):
+        raise ValueError(f"precision must be fp32, bf16 or fp8, got {policy!r}")
     if isinstance(ev, ClusteringEvaluator):
         return ClusterPlan(compiled, device, **opts)
     if isinstance(ev, (TreeEvaluator, MiningEvaluator)):
-        return TreePlan(compiled, device, **opts)
+        return TreePlan(compiled, device, precision="fp8" if policy == "fp8" else "fp32", **opts)
     if isinstance(ev, RegressionEvaluator):
         return LinearPlan(compiled, device)
     from ..models.regression import GeneralRegressionEvaluator
@@ -1111,7 +1121,7 @@ def compile_plan(compiled, device, **opts) -> DevicePlan:
     if isinstance(ev, NeuralEvaluator):
         from .nn_plans import MlpPlan
 
-        return MlpPlan(compiled, device, **opts)
+        return MlpPlan(compiled, device, precision="fp32" if policy == "fp32" else "bf16", **opts)
     if isinstance(ev, SvmEvaluator):
         from .nn_plans import SvmPlan
 

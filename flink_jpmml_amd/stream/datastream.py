@@ -2,36 +2,52 @@
 
 DSL (reference `S/package.scala:58-143`)::
 
-    env = StreamExecutionEnvironment()
+    env = StreamExecutionEnvironment.get_execution_environment()   # under torchrun: one rank per GPU
     out = env.from_collection(events).evaluate(ModelReader(path), lambda e, m: m.predict(e.vec))
     out = vectors.quick_evaluate(ModelReader(path))                       # -> (Prediction, vector)
     out = events.with_support_stream(control).evaluate(lambda e, m: ...)  # dynamic serving
     results = out.collect()                                               # runs the job
 
-Every scoring entry point accepts ``batch_size=`` / ``device=`` to switch from per-record host
-evaluation to micro-batched HIP-kernel scoring (see :mod:`.operators`).
+Columnar fast path (the MI355X way to feed a GPU)::
+
+    batches = env.from_batches(X_pinned, batch_rows=1 << 22)      # RecordBatch elements
+    scored = batches.quick_evaluate(ModelReader(path), config=ScoringConfig(device="cuda"))
+    # -> (PredictionBatch, RecordBatch) per batch; PredictionBatch[i] == model.predict(row i)
+
+Every scoring entry point accepts ``config=`` (:class:`~flink_jpmml_amd.config.ScoringConfig`:
+batch size, latency bound, device, precision, fallback policy, …) and the legacy shortcuts
+``batch_size=`` / ``device=``. Under ``torchrun`` :meth:`StreamExecutionEnvironment.get_execution_environment`
+joins the process group and every operator runs as one subtask per rank (SURVEY §2.7 DP).
 """
 
 from __future__ import annotations
 
+import json
+import os
 from typing import Any, Callable, Iterable, List, Optional, Sequence, Tuple
 
 from ..api.reader import ModelReader
+from ..config import ScoringConfig
+from .clock import Clock
 from .functions import CoProcessFunction, SinkFunction, SourceFunction
 from .operators import EvaluationCoFunction, EvaluationFunction, QuickEvaluationFunction
 from .runtime import Executor, JobExecutionResult, Node, SimulatedFailure
+from .sources import BatchSource, CollectionSource, ReplicatedSource, TextBatchSource
 from .state import CheckpointStorage
 
-_counter = [0]
+_DIST: dict = {}  # the process's DistContext (process groups are created once per process)
 
 
-def _uid(prefix: str) -> str:
-    _counter[0] += 1
-    return f"{prefix}-{_counter[0]}"
+def _uid(env: "StreamExecutionEnvironment", prefix: str) -> str:
+    """Per-environment sequential ids: the same job code builds the same ids in every run and on
+    every rank, so checkpoint manifests (operator state, source offsets) map back on restore."""
+    env._uid_counter += 1
+    return f"{prefix}-{env._uid_counter}"
 
 
 class CollectSink(SinkFunction):
-    """Collects into a shared list (the reference's test sink, `T/utils/FlinkTestKits.scala:58-62`)."""
+    """Collects into a shared list (the reference's test sink, `T/utils/FlinkTestKits.scala:58-62`).
+    Under data parallelism :meth:`DataStream.collect` gathers every rank's list (rank order)."""
 
     def __init__(self, target: Optional[list] = None):
         self.values = target if target is not None else []
@@ -43,6 +59,85 @@ class CollectSink(SinkFunction):
         return self.__dict__  # keeps the shared list when cloned for parallel subtasks
 
 
+class FileSink(SinkFunction):
+    """Exactly-once text sink: one JSON line per element, two-phase committed per checkpoint.
+
+    Elements go to an in-progress buffer; ``pre_commit(cid)`` writes them to
+    ``<dir>/part-<rank>-<cid>.pending``; ``commit(cid)`` renames it to ``.jsonl`` once the
+    checkpoint manifest is durable (end of input commits the rest as ``part-<rank>-final``).
+    ``recover()`` (called on restore) deletes pending parts of the crashed run, so the committed
+    parts of both runs together equal one uninterrupted run — no duplicates, no gaps."""
+
+    def __init__(self, directory: str, encode: Optional[Callable[[Any], Any]] = None):
+        self.directory = directory
+        self.encode = encode or _json_default
+        self._buf: List[str] = []
+        self._pending: List[Tuple[int, str]] = []
+        self.rank = 0
+
+    def open(self, context=None) -> None:  # noqa: A003
+        os.makedirs(self.directory, exist_ok=True)
+        if context is not None:
+            self.rank = context.index_of_this_subtask
+
+    def invoke(self, value: Any) -> None:
+        self._buf.append(json.dumps(self.encode(value), default=_json_default))
+
+    def _name(self, cid: int) -> str:
+        tag = "final" if cid < 0 else f"{cid:06d}"
+        return os.path.join(self.directory, f"part-{self.rank:03d}-{tag}")
+
+    def pre_commit(self, cid: int) -> None:
+        path = self._name(cid) + ".pending"
+        with open(path, "w") as fh:
+            fh.write("".join(x + "\n" for x in self._buf))
+            fh.flush()
+            os.fsync(fh.fileno())
+        self._buf = []
+        self._pending.append((cid, path))
+
+    def commit(self, cid: int) -> None:
+        keep = []
+        for c, path in self._pending:
+            if c == cid or cid < 0:
+                os.replace(path, path[: -len(".pending")] + ".jsonl")
+            else:
+                keep.append((c, path))
+        self._pending = keep
+
+    def recover(self) -> None:
+        for f in os.listdir(self.directory):
+            if f.startswith(f"part-{self.rank:03d}-") and f.endswith(".pending"):
+                os.remove(os.path.join(self.directory, f))
+
+    @staticmethod
+    def read(directory: str) -> List[Any]:
+        """Committed output in (rank, checkpoint) order."""
+        out = []
+        for f in sorted(os.listdir(directory)):
+            if f.endswith(".jsonl"):
+                with open(os.path.join(directory, f)) as fh:
+                    out.extend(json.loads(line) for line in fh if line.strip())
+        return out
+
+
+def _json_default(x: Any) -> Any:
+    from ..api.batch import PredictionBatch
+    from ..domain.prediction import Prediction
+
+    if isinstance(x, Prediction):
+        return None if x.value.is_empty else x.value.get()
+    if isinstance(x, PredictionBatch):
+        return [None if not v else float(s) for s, v in zip(x.scores, x.valid)]
+    if isinstance(x, (tuple, list)):
+        return [_json_default(y) for y in x]
+    if hasattr(x, "tolist"):
+        return x.tolist()
+    if hasattr(x, "__dict__"):
+        return {k: _json_default(v) for k, v in vars(x).items()}
+    return x if isinstance(x, (int, float, str, bool, type(None), dict)) else repr(x)
+
+
 class _FnSink(SinkFunction):
     def __init__(self, fn: Callable[[Any], None]):
         self.fn = fn
@@ -52,32 +147,68 @@ class _FnSink(SinkFunction):
 
 
 class StreamExecutionEnvironment:
-    def __init__(self, parallelism: int = 1):
+    def __init__(self, parallelism: int = 1, config: Optional[ScoringConfig] = None, dist_ctx=None,
+                 clock: Optional[Clock] = None):
         self.parallelism = parallelism
+        self.config = config
+        self.dist_ctx = dist_ctx
+        self.clock = clock
         self.checkpoint_every: Optional[int] = None
         self.checkpoint_storage = CheckpointStorage()
         self.fail_after: Optional[int] = None
         self.copy_operators = False
         self._sinks: List[Node] = []
+        self._uid_counter = 0
+        if dist_ctx is not None and dist_ctx.is_distributed:
+            self.parallelism = dist_ctx.world_size
 
     @staticmethod
-    def get_execution_environment() -> "StreamExecutionEnvironment":
-        return StreamExecutionEnvironment()
+    def get_execution_environment(config: Optional[ScoringConfig] = None, backend: Optional[str] = None,
+                                  force_distributed: bool = False) -> "StreamExecutionEnvironment":
+        """Under ``torchrun`` (``WORLD_SIZE > 1``): join the process group (RCCL on GPUs, gloo on
+        CPUs) and return an environment whose operators run one subtask per rank. Otherwise a
+        local environment. ``force_distributed`` forms a 1-rank group (RCCL on one GPU)."""
+        ctx = None
+        if int(os.environ.get("WORLD_SIZE", "1")) > 1 or force_distributed:
+            ctx = _DIST.get("ctx")
+            if ctx is None:
+                from ..parallel.dist import init_from_env
+
+                ctx = _DIST["ctx"] = init_from_env(backend=backend, force=force_distributed)
+        return StreamExecutionEnvironment(config=config, dist_ctx=ctx)
 
     getExecutionEnvironment = get_execution_environment  # noqa: N815
 
+    @property
+    def is_distributed(self) -> bool:
+        return self.dist_ctx is not None and self.dist_ctx.is_distributed
+
     def set_parallelism(self, p: int) -> "StreamExecutionEnvironment":
+        if self.is_distributed and int(p) != self.dist_ctx.world_size:
+            raise ValueError(f"under torchrun the parallelism is the world size ({self.dist_ctx.world_size})")
         self.parallelism = int(p)
         return self
 
     setParallelism = set_parallelism  # noqa: N815
 
+    def set_config(self, config: ScoringConfig) -> "StreamExecutionEnvironment":
+        """Job-wide scoring defaults (operators without an explicit ``config=`` use them)."""
+        self.config = config
+        return self
+
+    def set_clock(self, clock: Clock) -> "StreamExecutionEnvironment":
+        """Processing-time clock (tests inject a :class:`~flink_jpmml_amd.stream.clock.ManualClock`)."""
+        self.clock = clock
+        return self
+
     def enable_checkpointing(self, every_n_records: int, directory: Optional[str] = None) -> "StreamExecutionEnvironment":
-        """Count-based checkpoint barriers (deterministic; the reference uses a time interval,
-        `E/DynamicEvaluateKmeans.scala:48`)."""
+        """Count-based checkpoint barriers on the primary source's offset (deterministic, aligned
+        across ranks; the reference uses a time interval, `E/DynamicEvaluateKmeans.scala:48`)."""
         self.checkpoint_every = int(every_n_records)
         if directory is not None:
             self.checkpoint_storage = CheckpointStorage(directory)
+        elif self.config is not None and self.config.checkpoint_dir:
+            self.checkpoint_storage = CheckpointStorage(self.config.checkpoint_dir)
         return self
 
     def inject_failure(self, after_records: Optional[int]) -> "StreamExecutionEnvironment":
@@ -86,10 +217,16 @@ class StreamExecutionEnvironment:
         return self
 
     # ------------------------------------------------------------------ sources
-    def from_collection(self, items: Iterable[Any], timestamp: Optional[Callable[[Any], Any]] = None,
-                        name: str = "collection") -> "DataStream":
-        node = Node("source", name, 1, source=list(items), timestamp_fn=timestamp, uid=_uid("src"))
+    def _source(self, src: Any, name: str, timestamp=None, mode: str = "shard") -> "DataStream":
+        node = Node("source", name, 1, source=src, timestamp_fn=timestamp, uid=_uid(self, "src"), dist_mode=mode)
         return DataStream(self, node)
+
+    def from_collection(self, items: Iterable[Any], timestamp: Optional[Callable[[Any], Any]] = None,
+                        name: str = "collection", uid: Optional[str] = None) -> "DataStream":
+        s = self._source(CollectionSource(items), name, timestamp)
+        if uid:
+            s.node.uid = uid
+        return s
 
     fromCollection = from_collection  # noqa: N815
 
@@ -97,17 +234,46 @@ class StreamExecutionEnvironment:
         return self.from_collection(items)
 
     def add_source(self, source: SourceFunction, timestamp: Optional[Callable[[Any], Any]] = None,
-                   name: str = "source") -> "DataStream":
-        node = Node("source", name, 1, source=source, timestamp_fn=timestamp, uid=_uid("src"))
-        return DataStream(self, node)
+                   name: str = "source", mode: Optional[str] = None, uid: Optional[str] = None) -> "DataStream":
+        """``mode`` under torchrun: ``shard`` (default for replayable sources), ``parallel`` (every
+        rank runs its own instance; default for sources with ``open_subtask``), ``replicate``
+        (every rank reads it all) or ``leader`` (rank 0 reads, elements are broadcast)."""
+        if mode is None:
+            mode = "parallel" if hasattr(source, "open_subtask") else "shard"
+        if mode == "leader":
+            source, mode = ReplicatedSource(source, self.dist_ctx), "replicate"
+        s = self._source(source, name, timestamp, mode)
+        if uid:
+            s.node.uid = uid
+        return s
 
     addSource = add_source  # noqa: N815
 
-    def from_either(self, sequence: Sequence[Tuple[str, Any]]) -> Tuple["DataStream", "DataStream"]:
+    def from_batches(self, data: Any, batch_rows: Optional[int] = None, repeat: int = 1,
+                     model_id: Optional[str] = None, mode: str = "shard", name: str = "batches",
+                     uid: Optional[str] = None) -> "DataStream":
+        """Columnar source of RecordBatch elements from a ``[rows, F]`` matrix (cut into
+        ``batch_rows``) or an iterable of matrices / RecordBatches."""
+        s = self._source(BatchSource(data, batch_rows, repeat, model_id), name, None, mode)
+        if uid:
+            s.node.uid = uid
+        return s
+
+    fromBatches = from_batches  # noqa: N815
+
+    def read_text_batches(self, path: str, model: Any, batch_rows: int = 1 << 16, **kw) -> "DataStream":
+        """Delimited text file → RecordBatches via the native C++ ingest (pinned output)."""
+        return self._source(TextBatchSource(path, model, batch_rows, **kw), "text-batches", None, "shard")
+
+    def from_either(self, sequence: Sequence[Tuple[str, Any]], uid: Optional[str] = None
+                    ) -> Tuple["DataStream", "DataStream"]:
         """One ordered source split into a left and a right stream: ``[("L", ev), ("R", ctrl)]``.
         The runtime delivers the elements in exactly this order (deterministic two-input tests,
-        the analogue of `T/utils/FlinkTestKits.scala:44-55`)."""
-        tagged = self.from_collection(list(sequence), name="either")
+        the analogue of `T/utils/FlinkTestKits.scala:44-55`). Under torchrun ``L`` elements are
+        sharded across ranks and ``R`` elements replicated to every rank."""
+        tagged = self._source(CollectionSource(list(sequence)), "either", None, "either")
+        if uid:
+            tagged.node.uid = uid
         left = tagged.filter(lambda t: t[0] == "L").map(lambda t: t[1])
         right = tagged.filter(lambda t: t[0] == "R").map(lambda t: t[1])
         return left, right
@@ -129,7 +295,7 @@ class DataStream:
              parallelism: Optional[int] = None) -> "DataStream":
         p = parallelism or self.env.parallelism
         part = partition if p == self.node.parallelism else ("rebalance" if partition == "forward" else partition)
-        node = Node("one", name, p, factory=fn, inputs=[(self.node, part)], uid=_uid(name), op_kind=kind)
+        node = Node("one", name, p, factory=fn, inputs=[(self.node, part)], uid=_uid(self.env, name), op_kind=kind)
         return DataStream(self.env, node)
 
     def map(self, fn: Any, name: str = "map") -> "DataStream":  # noqa: A003
@@ -143,14 +309,35 @@ class DataStream:
 
     flatMap = flat_map  # noqa: N815
 
+    def unbatch(self) -> "DataStream":
+        """``(PredictionBatch, RecordBatch)`` elements → per-record ``(Prediction, vector)``
+        (materialises Prediction objects: for sinks that need the reference's element type)."""
+        from ..api.batch import PredictionBatch
+
+        def explode(x):
+            if isinstance(x, tuple) and len(x) == 2 and isinstance(x[0], PredictionBatch):
+                preds, batch = x
+                return list(zip(preds, batch))
+            if isinstance(x, PredictionBatch):
+                return list(x)
+            return [x]
+
+        return self._one("flat_map", explode, "unbatch")
+
     def set_parallelism(self, p: int) -> "DataStream":
         self.node.parallelism = int(p)
+        return self
+
+    def uid(self, uid: str) -> "DataStream":
+        """Stable operator id (names its state in checkpoint manifests)."""
+        self.node.uid = uid
         return self
 
     def rebalance(self) -> "DataStream":
         return _Partitioned(self, "rebalance")
 
     def broadcast(self) -> "DataStream":
+        _mark_replicated(self.node)
         return _Partitioned(self, "broadcast")
 
     def connect(self, other: "DataStream") -> "ConnectedStreams":
@@ -160,7 +347,7 @@ class DataStream:
         if callable(sink) and not isinstance(sink, SinkFunction):
             sink = _FnSink(sink)
         node = Node("sink", "sink", 1, factory=sink, inputs=[(self.node, "rebalance" if self.node.parallelism != 1
-                                                                  else "forward")], uid=_uid("sink"),
+                                                                  else "forward")], uid=_uid(self.env, "sink"),
                     op_kind="sink")
         self.env._sinks.append(node)
         return node
@@ -168,10 +355,17 @@ class DataStream:
     addSink = add_sink  # noqa: N815
 
     def collect(self, job_name: str = "collect", restore: Optional[str] = None) -> List[Any]:
-        """Attach a collecting sink, run the job, return the outputs."""
+        """Attach a collecting sink, run the job, return the outputs. Under data parallelism every
+        rank returns every rank's outputs, concatenated in rank order (all-gather, F5)."""
         sink = CollectSink()
         self.add_sink(sink)
         self.env.execute(job_name, restore=restore)
+        if self.env.is_distributed:
+            from ..parallel.dist import all_gather_object
+
+            ctx = self.env.dist_ctx
+            parts = all_gather_object(sink.values, ctx, group=ctx.group("ctrl"))
+            return [x for part in parts for x in part]
         return sink.values
 
     executeAndCollect = collect  # noqa: N815
@@ -184,19 +378,37 @@ class DataStream:
     withSupportStream = with_support_stream  # noqa: N815
 
     def evaluate(self, model_reader: ModelReader, f: Callable[[Any, Any], Any], batch_size: Optional[int] = None,
-                 device: Any = None, plan_opts: Optional[dict] = None) -> "DataStream":
+                 device: Any = None, plan_opts: Optional[dict] = None,
+                 config: Optional[ScoringConfig] = None) -> "DataStream":
         """``stream.flatMap(EvaluationFunction(reader){ out.collect(f(value, evaluator)) })``
         (`S/package.scala:76-82`)."""
-        op = EvaluationFunction(model_reader, f, batch_size, device, plan_opts)
+        op = EvaluationFunction(model_reader, f, batch_size, device, plan_opts, config)
         return self._one("flat_map", op, "evaluate")
 
     def quick_evaluate(self, model_reader: ModelReader, batch_size: Optional[int] = None, device: Any = None,
-                       plan_opts: Optional[dict] = None) -> "DataStream":
-        """Vector stream → ``(Prediction, vector)`` (`S/package.scala:138-142`)."""
-        op = QuickEvaluationFunction(model_reader, batch_size, device, plan_opts)
+                       plan_opts: Optional[dict] = None, config: Optional[ScoringConfig] = None) -> "DataStream":
+        """Vector stream → ``(Prediction, vector)`` (`S/package.scala:138-142`); RecordBatch stream
+        → ``(PredictionBatch, RecordBatch)``."""
+        op = QuickEvaluationFunction(model_reader, batch_size, device, plan_opts, config)
         return self._one("flat_map", op, "quick_evaluate")
 
     quickEvaluate = quick_evaluate  # noqa: N815
+
+
+def _mark_replicated(node: Node) -> None:
+    """A broadcast edge: the source feeding it is read by every rank (control streams)."""
+    seen = set()
+    stack = [node]
+    while stack:
+        n = stack.pop()
+        if id(n) in seen:
+            continue
+        seen.add(id(n))
+        if n.kind == "source":
+            if n.dist_mode == "shard":
+                n.dist_mode = "replicate"
+            continue
+        stack.extend(up for up, _ in n.inputs)
 
 
 class _Partitioned(DataStream):
@@ -216,18 +428,20 @@ class ConnectedStreams:
         p1 = getattr(self.first, "partition", "forward" if self.first.node.parallelism == p else "rebalance")
         p2 = getattr(self.second, "partition", "forward" if self.second.node.parallelism == p else "rebalance")
         node = Node("two", name, p, factory=fn, inputs=[(self.first.node, p1), (self.second.node, p2)],
-                    uid=_uid(name), op_kind="co_process")
+                    uid=_uid(self.env, name), op_kind="co_process")
         return DataStream(self.env, node)
 
     def evaluate(self, f: Callable[[Any, Any], Any], batch_size: Optional[int] = None, device: Any = None,
-                 cache_capacity: int = 64, plan_opts: Optional[dict] = None, uid: Optional[str] = None) -> DataStream:
+                 cache_capacity: Optional[int] = None, plan_opts: Optional[dict] = None, uid: Optional[str] = None,
+                 config: Optional[ScoringConfig] = None) -> DataStream:
         """Dynamic multi-model serving (`S/package.scala:107-119`). ``uid`` names the operator's
         state in checkpoints (stable across restarts)."""
-        op = EvaluationCoFunction(f, batch_size, device, cache_capacity, plan_opts)
+        op = EvaluationCoFunction(f, batch_size, device, cache_capacity, plan_opts, config)
         out = self.process(op, "evaluate_co")
         if uid:
             out.node.uid = uid
         return out
 
 
-__all__ = ["CollectSink", "ConnectedStreams", "DataStream", "SimulatedFailure", "StreamExecutionEnvironment"]
+__all__ = ["CollectSink", "ConnectedStreams", "DataStream", "FileSink", "SimulatedFailure",
+           "StreamExecutionEnvironment"]

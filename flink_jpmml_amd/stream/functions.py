@@ -29,12 +29,28 @@ class ListCollector(Collector):
 
 
 class RuntimeContext:
-    def __init__(self, task_name: str, subtask_index: int, parallelism: int):
+    """What an operator instance knows about where it runs: its subtask index / parallelism, the
+    job's processing-time clock and timer service, the job-level scoring config and — under data
+    parallelism across GPUs — the distributed context (``dist``, one subtask per rank)."""
+
+    def __init__(self, task_name: str, subtask_index: int, parallelism: int, clock=None, dist=None,
+                 config=None):
         self.task_name = task_name
         self.index_of_this_subtask = subtask_index
         self.number_of_parallel_subtasks = parallelism
+        self.clock = clock
+        self.dist = dist
+        self.config = config
 
     getIndexOfThisSubtask = property(lambda self: self.index_of_this_subtask)  # noqa: N815
+
+    def now(self) -> float:
+        return self.clock.now() if self.clock is not None else __import__("time").monotonic()
+
+    def register_timer(self, deadline: float, callback) -> None:
+        """Processing-time timer: ``callback(now)`` runs on the job thread at/after ``deadline``."""
+        if self.clock is not None:
+            self.clock.timers.register(deadline, callback)
 
 
 class RichFunction:
@@ -161,15 +177,25 @@ class SourceFunction:
         pass
 
     def iterate(self) -> Iterable[Any]:
-        """Pull-style iteration (default: run into a buffer)."""
+        """Pull-style iteration. Sources that only implement ``run(ctx)`` are run on a thread of
+        their own by the runtime (:class:`flink_jpmml_amd.stream.sources.ThreadedSource`); this
+        default exists for direct callers and drains a finite ``run``."""
         buf: List[Any] = []
         self.run(SourceContext(buf.append))
         return iter(buf)
 
 
 class SinkFunction:
+    """Sink contract. Transactional sinks (exactly-once across restarts) also implement
+    ``pre_commit(checkpoint_id)`` — make everything received so far durable but invisible —
+    ``commit(checkpoint_id)`` — publish it once the checkpoint manifest is written — and
+    ``recover()`` — drop what a crashed run pre-committed but never committed."""
+
     def invoke(self, value: Any) -> None:
         raise NotImplementedError
+
+    def open(self, context: Optional[RuntimeContext] = None) -> None:  # noqa: A003
+        pass
 
     def close(self) -> None:
         pass

@@ -1,51 +1,149 @@
-"""The two scoring operators of the reference, re-built around micro-batched GPU scoring.
+"""The two scoring operators of the reference, re-built around asynchronous GPU scoring.
 
 * :class:`EvaluationFunction` — static single model (`S/api/functions/EvaluationFunction.scala:39-48`):
-  the model is loaded once per subtask in ``open()``; a load failure raises
-  :class:`ModelLoadingException` and fails the job.
+  the model is loaded once per subtask in ``open()`` (under ``torchrun``: parsed once on rank 0 and
+  replicated to every rank); a load failure raises :class:`ModelLoadingException` and fails the job.
 * :class:`EvaluationCoFunction` — dynamic multi-model serving
   (`S/api/functions/EvaluationCoFunction.scala:55-133`): a control stream of Add/Del messages
-  maintains the checkpointed metadata table ``ModelId → ModelInfo``; models are loaded lazily on
-  the first event that needs them and cached (exact-key LRU instead of the reference's
-  ``WeakHashMap[Int, _]`` keyed by hash); events for unknown models get the empty model
-  (→ ``EmptyScore``); a malformed model id fails the job.
+  maintains the checkpointed metadata table ``ModelId → ModelInfo``; an added model is loaded on a
+  background loader thread (parse + lower never stall the event path; under ``torchrun`` the load is
+  one collective: parse on rank 0, RCCL-broadcast of the compiled tensors); models are cached
+  (exact-key LRU instead of the reference's ``WeakHashMap[Int, _]`` keyed by hash); events for
+  unknown models get the empty model (→ ``EmptyScore``); a malformed model id fails the job; a model
+  that failed to load fails the job when an event needs it (the reference's lazy-load semantics).
 
-Both support two execution modes:
+Element kinds, both accepted by every operator:
 
-* ``batch_size=None`` — per-record, exactly the reference's call pattern: ``f(event, model)``
-  with ``model.predict(vec)`` evaluated on the host (float64 oracle);
-* ``batch_size=N`` — **micro-batching**: events are buffered; at flush time ``f`` runs once
-  against a *recording* model that captures every ``predict`` input, the captured vectors are
-  scored in one batch on the device (HIP kernels), and ``f`` runs again against a *replay* model
-  returning those predictions. ``f`` must therefore be deterministic (no side effects besides its
-  return value). Control messages, checkpoint barriers and end of input flush the buffer first,
-  so the reference's ordering semantics ("event before Add → EmptyScore") hold exactly.
+* **RecordBatch** (columnar fast path): ``f(batch, model)`` runs once per batch and
+  ``model.predict(batch)`` returns a :class:`PredictionBatch` future — the kernel epilogue writes
+  scores into pinned host memory while the operator already accepts the next batch. Results are
+  emitted in order, as soon as they are ready, at most ``max_inflight`` batches behind;
+* **single records** (the reference's call pattern): ``batch_size=None`` scores each record on the
+  host float64 oracle exactly like the reference. ``batch_size=N`` micro-batches them:
+  ``f`` runs against a *recording* model capturing every ``predict`` input, the captured vectors are
+  scored as one RecordBatch on the device, and ``f`` runs again against a *replay* model. The replay
+  verifies every call against the capture; an event whose UDF branched differently, or whose
+  capture pass raised (e.g. ``.value.get()`` on the placeholder), is re-run per record — batching
+  never changes a result. Control messages, checkpoint barriers, end of input and the
+  ``max_batch_latency_ms`` timer flush the buffer, so "event before Add → EmptyScore" holds exactly.
 """
 
 from __future__ import annotations
 
+import collections
 import logging
 from collections import OrderedDict
-from typing import Any, Callable, Dict, List, Optional, Tuple
+from concurrent.futures import Future
+from typing import Any, Callable, Deque, Dict, List, Optional, Tuple
 
 import numpy as np
 
+from ..api.batch import PredictionBatch, RecordBatch
 from ..api.exceptions import ModelLoadingException
 from ..api.managers import metadata_manager, models_manager
 from ..api.pmml_model import PmmlModel
 from ..api.reader import ModelReader
 from ..api.vectors import as_vector
+from ..config import ScoringConfig, merge_config
+from ..domain.checkpoint import STATE_NAME
 from ..domain.control import AddMessage, DelMessage, ServingMessage
 from ..domain.events import event_model_id
 from ..domain.model_id import ModelId, ModelInfo
 from ..domain.prediction import EMPTY_PREDICTION, Prediction
-from ..domain.checkpoint import STATE_NAME
+from ..utils.metrics import METRICS
+from ..utils.profiling import prange
 from .functions import CheckpointedFunction, CoProcessFunction, Collector, FlatMapFunction
 
 logger = logging.getLogger(__name__)
 
+DIGEST_STATE = "model-digests"
+
+
+# --------------------------------------------------------------------------- shared plumbing
+
+
+class _ScoringMixin:
+    """Config + device + shared DevicePipeline + ordered in-flight emission of columnar results."""
+
+    config: ScoringConfig
+
+    def _setup(self) -> None:
+        rctx = getattr(self, "runtime_context", None)
+        job_cfg = getattr(rctx, "config", None)
+        if self._cfg_explicit is None and job_cfg is not None:
+            self.config = merge_config(job_cfg, **self._legacy)
+        self.dist = getattr(rctx, "dist", None)
+        local = self.dist.local_rank if self.dist is not None else 0
+        self.device = self.config.resolve_device(local)
+        self._pipeline = None
+        self._pending: Deque[Tuple[Any, List[PredictionBatch], float]] = collections.deque()
+        self._pending_timer = False
+
+    def _pipe(self):
+        if self.device is None:
+            return None
+        if self._pipeline is None:
+            from ..runtime.engine import DevicePipeline
+
+            self._pipeline = DevicePipeline(self.device, self.config.micro_batch, self.config.pipeline_depth)
+        return self._pipeline
+
+    def _now(self) -> float:
+        rctx = getattr(self, "runtime_context", None)
+        return rctx.now() if rctx is not None else __import__("time").monotonic()
+
+    # -- ordered, non-blocking emission of columnar results
+    def _push(self, result: Any, out: Collector) -> None:
+        self._pending.append((result, _futures_of(result), self._now()))
+        self._emit_ready(out)
+        while len(self._pending) > self.config.max_inflight:
+            self._emit_one(out)
+        self._arm_pending_timer(out)
+
+    def _emit_one(self, out: Collector) -> None:
+        res, _, _ = self._pending.popleft()
+        out.collect(res)
+
+    def _emit_ready(self, out: Collector) -> None:
+        while self._pending and all(f.ready for f in self._pending[0][1]):
+            self._emit_one(out)
+
+    def _drain_pending(self, out: Collector) -> None:
+        while self._pending:
+            self._emit_one(out)
+
+    def _arm_pending_timer(self, out: Collector) -> None:
+        lat = self.config.max_batch_latency_ms
+        rctx = getattr(self, "runtime_context", None)
+        if lat is None or not self._pending or self._pending_timer or rctx is None:
+            return
+        self._pending_timer = True
+        t_first = self._pending[0][2]
+
+        def fire(now: float) -> None:
+            self._pending_timer = False
+            # everything older than the bound goes out, waiting for its kernel if needed
+            while self._pending and now >= self._pending[0][2] + lat / 1e3:
+                self._emit_one(out)
+            self._emit_ready(out)
+            self._arm_pending_timer(out)
+
+        rctx.register_timer(max(t_first + lat / 1e3, self._now()), fire)
+
+
+def _futures_of(res: Any) -> List[PredictionBatch]:
+    if isinstance(res, PredictionBatch):
+        return [res]
+    if isinstance(res, (tuple, list)) and len(res) <= 8:
+        return [x for x in res if isinstance(x, PredictionBatch)]
+    return []
+
 
 # --------------------------------------------------------------------------- record / replay models
+
+
+class _CaptureError(Exception):
+    pass
 
 
 class _RecordingModel:
@@ -56,6 +154,8 @@ class _RecordingModel:
         self.calls: List[Tuple[Any, Optional[float]]] = []
 
     def predict(self, input_vector: Any, replace_nan: Optional[float] = None) -> Prediction:
+        if isinstance(input_vector, RecordBatch):
+            raise _CaptureError("columnar predict inside a per-record UDF")
         self.calls.append((input_vector, replace_nan))
         return EMPTY_PREDICTION
 
@@ -63,130 +163,197 @@ class _RecordingModel:
         return getattr(self._real, item)
 
 
+class _ReplayMismatch(Exception):
+    pass
+
+
+def _same_input(a: Any, b: Any) -> bool:
+    if a is b:
+        return True
+    try:
+        return as_vector(a) == as_vector(b)
+    except Exception:  # noqa: BLE001
+        return False
+
+
 class _ReplayModel:
-    def __init__(self, real: PmmlModel, preds: List[Prediction]):
+    """Returns the batch-scored predictions in capture order, verifying each call's input."""
+
+    def __init__(self, real: PmmlModel, calls: List[Tuple[Any, Optional[float]]], preds: List[Prediction]):
         self._real = real
+        self._calls = calls
         self._preds = preds
         self._i = 0
 
     def predict(self, input_vector: Any, replace_nan: Optional[float] = None) -> Prediction:
-        if self._i >= len(self._preds):
-            raise RuntimeError("UDF called predict() more often in replay than in capture: UDF is not deterministic")
-        p = self._preds[self._i]
+        i = self._i
+        if i >= len(self._preds):
+            raise _ReplayMismatch("more predict() calls in replay than in capture")
+        v0, rn0 = self._calls[i]
+        if rn0 != replace_nan or not _same_input(input_vector, v0):
+            raise _ReplayMismatch(f"predict() call {i} differs between capture and replay")
         self._i += 1
-        return p
+        return self._preds[i]
 
     def __getattr__(self, item: str) -> Any:
         return getattr(self._real, item)
 
 
-def _score_calls(model: PmmlModel, calls: List[Tuple[Any, Optional[float]]], device: Any,
-                 plan_opts: dict) -> List[Prediction]:
-    """Batch-score captured predict() calls (grouped by replace_nan) on ``device``."""
+def _score_calls(model: PmmlModel, calls: List[Tuple[Any, Optional[float]]]) -> List[Prediction]:
+    """Score captured predict() calls (grouped by replace_nan) as RecordBatches on the model's
+    bound scorer (device or host oracle). Device errors propagate: no silent fallback."""
     if model.is_empty:
         return [EMPTY_PREDICTION] * len(calls)
+    width = len(model.active_fields)
     out: List[Optional[Prediction]] = [None] * len(calls)
     groups: Dict[Optional[float], List[int]] = {}
     for i, (_, rn) in enumerate(calls):
         groups.setdefault(rn, []).append(i)
     for rn, idxs in groups.items():
-        vecs = [calls[i][0] for i in idxs]
-        try:
-            preds = model.predict_vectors(vecs, replace_nan=rn, device=device, **plan_opts)
-        except Exception as e:  # noqa: BLE001 - device not lowerable etc.: fall back per record
-            if device is not None:
-                logger.warning("batch scoring on %s failed (%s); scoring on the host", device, e)
-            preds = [model.predict(v, rn) for v in vecs]
+        batch = RecordBatch.from_vectors([calls[i][0] for i in idxs], width)
+        preds = model.predict_records(batch, replace_nan=rn)
         for i, p in zip(idxs, preds):
             out[i] = p
     return out  # type: ignore[return-value]
 
 
 class _Batcher:
-    """Buffers (event, model) pairs and runs the capture → batch score → replay protocol."""
+    """Buffers (event, model) pairs and runs the capture → batch score → replay protocol; flushes
+    on size, on the latency timer, and when the owner asks (control / barrier / end)."""
 
-    def __init__(self, f: Callable[[Any, Any], Any], batch_size: int, device: Any, plan_opts: dict):
+    def __init__(self, owner: "_ScoringMixin", f: Callable[[Any, Any], Any], batch_size: int):
+        self.owner = owner
         self.f = f
         self.batch_size = int(batch_size)
-        self.device = device
-        self.plan_opts = plan_opts
         self.buf: List[Tuple[Any, PmmlModel]] = []
+        self.first_ts: Optional[float] = None
+        self._timer_armed = False
 
     def add(self, event: Any, model: PmmlModel, out: Collector) -> None:
+        if not self.buf:
+            self.first_ts = self.owner._now()
         self.buf.append((event, model))
         if len(self.buf) >= self.batch_size:
             self.flush(out)
+        else:
+            self._arm(out)
+
+    def _arm(self, out: Collector) -> None:
+        lat = self.owner.config.max_batch_latency_ms
+        rctx = getattr(self.owner, "runtime_context", None)
+        if lat is None or rctx is None or self._timer_armed or not self.buf:
+            return
+        self._timer_armed = True
+
+        def fire(now: float) -> None:
+            self._timer_armed = False
+            if self.buf and now >= self.first_ts + lat / 1e3:
+                METRICS.inc("batcher.latency_flushes")
+                self.flush(out)
+            self._arm(out)
+
+        rctx.register_timer(self.first_ts + lat / 1e3, fire)
 
     def flush(self, out: Collector) -> None:
         if not self.buf:
             return
         buf, self.buf = self.buf, []
-        # capture pass
-        recs: List[_RecordingModel] = []
-        per_model: "OrderedDict[int, Tuple[PmmlModel, List[Tuple[int, int]]]]" = OrderedDict()
-        all_calls: Dict[int, List[Tuple[Any, Optional[float]]]] = {}
-        for ei, (ev, model) in enumerate(buf):
-            rec = _RecordingModel(model)
-            self.f(ev, rec)
-            recs.append(rec)
-            key = id(model)
-            if key not in per_model:
-                per_model[key] = (model, [])
-                all_calls[key] = []
-            for ci, call in enumerate(rec.calls):
-                per_model[key][1].append((ei, ci))
-                all_calls[key].append(call)
-        # batch scoring, one batch per model
-        preds_of: Dict[Tuple[int, int], Prediction] = {}
-        for key, (model, slots) in per_model.items():
-            preds = _score_calls(model, all_calls[key], self.device, self.plan_opts)
-            for slot, p in zip(slots, preds):
-                preds_of[slot] = p
-        # replay pass, in arrival order
-        for ei, (ev, model) in enumerate(buf):
-            preds = [preds_of[(ei, ci)] for ci in range(len(recs[ei].calls))]
-            out.collect(self.f(ev, _ReplayModel(model, preds)))
+        with prange("batcher.flush"):
+            # capture pass
+            recs: List[Optional[_RecordingModel]] = []
+            per_model: "OrderedDict[int, Tuple[PmmlModel, List[Tuple[int, int]]]]" = OrderedDict()
+            all_calls: Dict[int, List[Tuple[Any, Optional[float]]]] = {}
+            for ei, (ev, model) in enumerate(buf):
+                rec = _RecordingModel(model)
+                try:
+                    self.f(ev, rec)
+                except Exception:  # noqa: BLE001 - e.g. .get() on the placeholder: per-record rerun
+                    recs.append(None)
+                    continue
+                recs.append(rec)
+                key = id(model)
+                if key not in per_model:
+                    per_model[key] = (model, [])
+                    all_calls[key] = []
+                for ci, call in enumerate(rec.calls):
+                    per_model[key][1].append((ei, ci))
+                    all_calls[key].append(call)
+            # batch scoring, one batch per model
+            preds_of: Dict[Tuple[int, int], Prediction] = {}
+            for key, (model, slots) in per_model.items():
+                preds = _score_calls(model, all_calls[key])
+                for slot, p in zip(slots, preds):
+                    preds_of[slot] = p
+            # replay pass, in arrival order; any divergence re-runs that event per record
+            for ei, (ev, model) in enumerate(buf):
+                rec = recs[ei]
+                res = None
+                ok = False
+                if rec is not None:
+                    preds = [preds_of[(ei, ci)] for ci in range(len(rec.calls))]
+                    try:
+                        res = self.f(ev, _ReplayModel(model, rec.calls, preds))
+                        ok = True
+                    except _ReplayMismatch:
+                        METRICS.inc("batcher.replay_mismatch")
+                if not ok:
+                    METRICS.inc("batcher.per_record_reruns")
+                    res = self.f(ev, model)
+                out.collect(res)
 
 
 # --------------------------------------------------------------------------- static operator
 
 
-class EvaluationFunction(FlatMapFunction):
+class EvaluationFunction(FlatMapFunction, _ScoringMixin):
     """``RichFlatMapFunction[IN, OUT]`` holding one model per subtask."""
 
     def __init__(self, reader: ModelReader, f: Optional[Callable[[Any, PmmlModel], Any]] = None,
-                 batch_size: Optional[int] = None, device: Any = None, plan_opts: Optional[dict] = None):
+                 batch_size: Optional[int] = None, device: Any = None, plan_opts: Optional[dict] = None,
+                 config: Optional[ScoringConfig] = None):
         self.reader = reader
         self.f = f
-        self.batch_size = batch_size
-        self.device = device
-        self.plan_opts = plan_opts or {}
+        self._legacy = dict(batch_size=batch_size, device=device, plan_opts=plan_opts)
+        self._cfg_explicit = config
+        self.config = merge_config(config, **self._legacy)
         self._evaluator: Optional[PmmlModel] = None
         self._batcher: Optional[_Batcher] = None
+        self.digest: Optional[str] = None
+
+    @property
+    def batch_size(self) -> Optional[int]:
+        return self.config.batch_size
 
     @property
     def evaluator(self) -> PmmlModel:
         """Lazily loaded model (`S/api/functions/EvaluationFunction.scala:43`)."""
         if self._evaluator is None:
-            self._evaluator = PmmlModel.from_reader(self.reader)
+            from ..runtime.loading import load_local
+
+            lm = load_local(self.reader.source_path, getattr(self, "device", None), self.config, None)
+            self._evaluator, self.digest = lm.model, lm.sha256
         return self._evaluator
 
     def open(self, configuration: Optional[dict] = None) -> None:  # noqa: A003
+        from ..runtime.loading import load_replicated
+
+        self._setup()
         try:
-            model = self.evaluator
+            lm = load_replicated(self.reader.source_path, self.dist, self.device, self.config, self._pipe())
+        except ModelLoadingException:
+            raise
         except Exception as e:  # noqa: BLE001
             raise ModelLoadingException(str(e), e) from e
-        logger.info("Model has been successfully loaded, model name: %s", model.model_name)
-        if self.device is not None:
-            try:
-                model.compiled.plan(self.device, **self.plan_opts)  # compile once, before traffic
-            except Exception as e:  # noqa: BLE001
-                logger.warning("model %s is not lowerable to %s (%s); host scoring", model.model_name, self.device, e)
-        if self.batch_size:
-            self._batcher = _Batcher(self.f, self.batch_size, self.device, self.plan_opts)
+        self._evaluator, self.digest = lm.model, lm.sha256
+        logger.info("Model has been successfully loaded, model name: %s", lm.model.model_name)
+        if self.config.batch_size:
+            self._batcher = _Batcher(self, self.f, self.config.batch_size)
 
     def flat_map(self, value: Any, out: Collector) -> None:
-        if self._batcher is not None:
+        if isinstance(value, RecordBatch):
+            with prange("evaluate.batch"):
+                self._push(self.f(value, self.evaluator), out)
+        elif self._batcher is not None:
             self._batcher.add(value, self.evaluator, out)
         else:
             out.collect(self.f(value, self.evaluator))
@@ -194,13 +361,20 @@ class EvaluationFunction(FlatMapFunction):
     def end_of_input(self, out: Collector) -> None:
         if self._batcher is not None:
             self._batcher.flush(out)
+        self._drain_pending(out)
 
     def on_barrier(self, out: Collector) -> None:
         self.end_of_input(out)
 
+    def checkpoint_models(self) -> Dict[str, dict]:
+        return {f"static:{self.reader.source_path}": {"path": self.reader.source_path, "sha256": self.digest}} \
+            if self.digest else {}
+
     def __getstate__(self):
         d = dict(self.__dict__)
-        d["_evaluator"] = None  # models are reloaded per subtask, never shipped
+        for k in ("_evaluator", "_batcher", "_pipeline", "_pending", "dist", "runtime_context"):
+            d.pop(k, None)  # models are reloaded per subtask, never shipped
+        d["_evaluator"] = None
         d["_batcher"] = None
         return d
 
@@ -223,8 +397,10 @@ class ModelCache:
         if m is not None:
             self._d.move_to_end(key)
             self.hits += 1
+            METRICS.inc("model_cache.hits")
         else:
             self.misses += 1
+            METRICS.inc("model_cache.misses")
         return m
 
     def put(self, key: ModelId, model: PmmlModel) -> None:
@@ -232,6 +408,7 @@ class ModelCache:
         self._d.move_to_end(key)
         while len(self._d) > self.capacity:
             self._d.popitem(last=False)
+            METRICS.inc("model_cache.evictions")
 
     def evict(self, keys) -> None:
         for k in keys:
@@ -247,22 +424,87 @@ class ModelCache:
         return len(self._d)
 
 
-class EvaluationCoFunction(CoProcessFunction, CheckpointedFunction):
+class EvaluationCoFunction(CoProcessFunction, CheckpointedFunction, _ScoringMixin):
     def __init__(self, f: Optional[Callable[[Any, PmmlModel], Any]] = None, batch_size: Optional[int] = None,
-                 device: Any = None, cache_capacity: int = 64, plan_opts: Optional[dict] = None):
+                 device: Any = None, cache_capacity: Optional[int] = None, plan_opts: Optional[dict] = None,
+                 config: Optional[ScoringConfig] = None):
         self.f = f
-        self.batch_size = batch_size
-        self.device = device
-        self.cache_capacity = cache_capacity
-        self.plan_opts = plan_opts or {}
+        self._legacy = dict(batch_size=batch_size, device=device, cache_capacity=cache_capacity,
+                            plan_opts=plan_opts)
+        self._cfg_explicit = config
+        self.config = merge_config(config, **self._legacy)
         self.serving_metadata: Dict[ModelId, ModelInfo] = {}
-        self.serving_models = ModelCache(cache_capacity)
+        self.serving_models = ModelCache(self.config.cache_capacity)
+        self.digests: Dict[ModelId, str] = {}
         self._snapshot_metadata = None
+        self._snapshot_digests = None
         self._batcher: Optional[_Batcher] = None
+        self._loading: Dict[ModelId, Future] = {}
+        self._loader = None
+        self.dist = None
+        self.device = None
+        self._pipeline = None
+        self._pending = collections.deque()
+        self._restored_digests: Dict[ModelId, str] = {}
+
+    @property
+    def batch_size(self) -> Optional[int]:
+        return self.config.batch_size
+
+    @property
+    def cache_capacity(self) -> int:
+        return self.config.cache_capacity
 
     def open(self, configuration: Optional[dict] = None) -> None:  # noqa: A003
-        if self.batch_size:
-            self._batcher = _Batcher(self.f, self.batch_size, self.device, self.plan_opts)
+        self._setup()
+        self.serving_models.capacity = self.config.cache_capacity
+        if self.config.batch_size:
+            self._batcher = _Batcher(self, self.f, self.config.batch_size)
+        # models of a restored checkpoint are re-loaded (and re-replicated) right away
+        if self.config.async_load or self._distributed:
+            for mid, info in self.serving_metadata.items():
+                self._schedule_load(mid, info.path)
+
+    @property
+    def _distributed(self) -> bool:
+        return self.dist is not None and self.dist.is_distributed
+
+    # -- loading
+    def _load_fn(self, path: str):
+        from ..runtime.loading import load_replicated
+
+        return load_replicated(path, self.dist, self.device, self.config, self._pipe())
+
+    def _schedule_load(self, mid: ModelId, path: str) -> None:
+        from ..runtime.loading import ModelLoader
+
+        if self._loader is None:
+            self._loader = ModelLoader(self._load_fn, name=f"model-loader-{id(self):x}")
+        self._loading[mid] = self._loader.submit(path)
+
+    def _accept_loaded(self, mid: ModelId, lm) -> PmmlModel:
+        pinned = self._restored_digests.get(mid)
+        if pinned is not None and pinned != lm.sha256:
+            raise ModelLoadingException(f"model {mid} at {lm.path} changed since the checkpoint "
+                                        f"(sha256 {lm.sha256[:12]}… != {pinned[:12]}…)")
+        self.digests[mid] = lm.sha256
+        self.serving_models.put(mid, lm.model)
+        logger.info("Model has been successfully loaded, model name: %s", lm.model.model_name)
+        return lm.model
+
+    def load_model(self, path: str) -> PmmlModel:
+        """Synchronous local load (`S/api/functions/EvaluationCoFunction.scala:98-104`)."""
+        from ..runtime.loading import load_local
+
+        try:
+            lm = load_local(path, self.device, self.config, self._pipe() if self.device is not None else None)
+        except ModelLoadingException:
+            raise
+        except Exception as e:  # noqa: BLE001
+            raise ModelLoadingException(str(e), e) from e
+        logger.info("Model has been successfully loaded, model name: %s", lm.model.model_name)
+        self._last_digest = lm.sha256
+        return lm.model
 
     # -- event path (reference: `S/package.scala:111-114`)
     def model_for(self, model_id: str) -> PmmlModel:
@@ -270,9 +512,25 @@ class EvaluationCoFunction(CoProcessFunction, CheckpointedFunction):
         m = self.serving_models.get(mid)
         if m is not None:
             return m
+        fut = self._loading.pop(mid, None)
+        if fut is not None and mid in self.serving_metadata:
+            try:
+                with prange("model.wait_load"):
+                    lm = fut.result()
+            except ModelLoadingException:
+                raise
+            except Exception as e:  # noqa: BLE001
+                raise ModelLoadingException(str(e), e) from e
+            return self._accept_loaded(mid, lm)
         return self.from_metadata(model_id)
 
     def process_element1(self, event: Any, ctx, out: Collector) -> None:
+        if isinstance(event, RecordBatch):
+            for sub in event.split_by_model():
+                model = self.model_for(sub.model_id)
+                with prange("evaluate.batch"):
+                    self._push(self.f(sub, model), out)
+            return
         model = self.model_for(event_model_id(event))
         if self._batcher is not None:
             self._batcher.add(event, model, out)
@@ -283,38 +541,38 @@ class EvaluationCoFunction(CoProcessFunction, CheckpointedFunction):
     def process_element2(self, control: ServingMessage, ctx, out: Collector) -> None:
         if self._batcher is not None:
             self._batcher.flush(out)  # control messages are batch barriers
+        self._drain_pending(out)
         self.manage_models(control)
+        known = control.model_id in self.serving_metadata
         self.manage_metadata(control)
+        METRICS.inc(f"control.{type(control).__name__}")
+        if isinstance(control, AddMessage) and not known and (self.config.async_load or self._distributed):
+            self._schedule_load(control.model_id, control.path)
 
     def manage_models(self, control: ServingMessage) -> None:
         if isinstance(control, DelMessage):
             self.serving_models.evict(models_manager(control, self.serving_models.keys()))
+            self._loading.pop(control.model_id, None)  # a running load finishes and is dropped
+            self.digests.pop(control.model_id, None)
 
     def manage_metadata(self, control: ServingMessage) -> None:
         self.serving_metadata = metadata_manager(control, self.serving_metadata)
-
-    # -- model loading (`:98-117`)
-    def load_model(self, path: str) -> PmmlModel:
-        try:
-            model = PmmlModel.from_reader(ModelReader(path))
-        except Exception as e:  # noqa: BLE001
-            raise ModelLoadingException(str(e), e) from e
-        logger.info("Model has been successfully loaded, model name: %s", model.model_name)
-        if self.device is not None:
-            try:
-                model.compiled.plan(self.device, **self.plan_opts)
-            except Exception as e:  # noqa: BLE001
-                logger.warning("model at %s is not lowerable to %s (%s); host scoring", path, self.device, e)
-        return model
 
     def from_metadata(self, model_id: str) -> PmmlModel:
         mid = ModelId.from_identifier(model_id)
         info = self.serving_metadata.get(mid)
         if info is None:
+            METRICS.inc("scoring.unknown_model_events")
             return PmmlModel.empty()
-        model = self.load_model(info.path)
-        self.serving_models.put(mid, model)
-        return model
+        from ..runtime.loading import load_local
+
+        try:  # lazy (non-collective) load: evicted models, or async_load=False
+            lm = load_local(info.path, self.device, self.config, self._pipe() if self.device is not None else None)
+        except ModelLoadingException:
+            raise
+        except Exception as e:  # noqa: BLE001
+            raise ModelLoadingException(str(e), e) from e
+        return self._accept_loaded(mid, lm)
 
     loadModel = load_model  # noqa: N815
     fromMetadata = from_metadata  # noqa: N815
@@ -323,74 +581,146 @@ class EvaluationCoFunction(CoProcessFunction, CheckpointedFunction):
     def snapshot_state(self, context) -> None:
         self._snapshot_metadata.clear()
         self._snapshot_metadata.add(dict(self.serving_metadata))
+        self._snapshot_digests.clear()
+        self._snapshot_digests.add({str(k): v for k, v in self.digests.items() if k in self.serving_metadata})
 
     def initialize_state(self, context) -> None:
         self.serving_metadata = {}
-        self._snapshot_metadata = context.get_operator_state_store().get_union_list_state(STATE_NAME)
+        store = context.get_operator_state_store()
+        self._snapshot_metadata = store.get_union_list_state(STATE_NAME)
+        self._snapshot_digests = store.get_union_list_state(DIGEST_STATE)
         if context.is_restored():
             try:
                 for snap in self._snapshot_metadata.get():
                     self.serving_metadata.update(snap)
+                for snap in self._snapshot_digests.get():
+                    self._restored_digests.update({ModelId.from_identifier(k): v for k, v in snap.items()})
             except Exception:  # noqa: BLE001
                 logger.info("Not available state in ListState!")
+
+    def checkpoint_models(self) -> Dict[str, dict]:
+        return {str(mid): {"path": info.path, "sha256": self.digests.get(mid) or self._restored_digests.get(mid)}
+                for mid, info in self.serving_metadata.items()}
 
     # -- flush hooks
     def end_of_input(self, out: Collector) -> None:
         if self._batcher is not None:
             self._batcher.flush(out)
+        self._drain_pending(out)
 
     def on_barrier(self, out: Collector) -> None:
         self.end_of_input(out)
 
+    def close(self) -> None:
+        if self._loader is not None:
+            self._loader.close(wait=True)
+
     def __getstate__(self):
         d = dict(self.__dict__)
-        d["serving_models"] = ModelCache(self.cache_capacity)
-        d["_batcher"] = None
-        d["_snapshot_metadata"] = None
+        d["serving_models"] = ModelCache(self.config.cache_capacity)
+        for k in ("_batcher", "_snapshot_metadata", "_snapshot_digests", "_loader", "_pipeline", "dist",
+                  "runtime_context"):
+            d[k] = None
+        d["_loading"] = {}
+        d["_pending"] = collections.deque()
         return d
 
 
 # --------------------------------------------------------------------------- quick evaluate
 
 
-def quick_udf(vec: Any, model: PmmlModel) -> Tuple[Prediction, Any]:
-    """``quickEvaluate``'s UDF (`S/package.scala:138-142`)."""
+def quick_udf(vec: Any, model: PmmlModel) -> Tuple[Any, Any]:
+    """``quickEvaluate``'s UDF (`S/package.scala:138-142`): ``(Prediction, vector)`` per record,
+    ``(PredictionBatch, RecordBatch)`` per columnar batch."""
     return model.predict(vec, None), vec
 
 
-class QuickEvaluationFunction(FlatMapFunction):
-    """Vector stream → ``(Prediction, vector)`` with native micro-batching (no capture/replay
-    needed: the input *is* the vector)."""
+class QuickEvaluationFunction(FlatMapFunction, _ScoringMixin):
+    """Vector stream → ``(Prediction, vector)``; RecordBatch stream → ``(PredictionBatch,
+    RecordBatch)``. Per-record vectors are micro-batched natively when ``batch_size`` is set (no
+    capture/replay needed: the input *is* the vector)."""
 
     def __init__(self, reader: ModelReader, batch_size: Optional[int] = None, device: Any = None,
-                 plan_opts: Optional[dict] = None):
-        self.inner = EvaluationFunction(reader, quick_udf, None, device, plan_opts)
-        self.batch_size = batch_size
-        self.device = device
-        self.plan_opts = plan_opts or {}
+                 plan_opts: Optional[dict] = None, config: Optional[ScoringConfig] = None):
+        self.inner = EvaluationFunction(reader, quick_udf, None, device, plan_opts, config)
+        self._legacy = dict(batch_size=batch_size, device=device, plan_opts=plan_opts)
+        self._cfg_explicit = config
+        self.config = merge_config(config, **self._legacy)
         self._buf: List[Any] = []
+        self._first_ts: Optional[float] = None
+        self._timer = False
+
+    @property
+    def batch_size(self) -> Optional[int]:
+        return self.config.batch_size
+
+    def set_runtime_context(self, ctx) -> None:
+        super().set_runtime_context(ctx)
+        self.inner.set_runtime_context(ctx)
 
     def open(self, configuration: Optional[dict] = None) -> None:  # noqa: A003
+        self._setup()
+        self.inner._cfg_explicit = self._cfg_explicit
+        self.inner._legacy = dict(self._legacy, batch_size=None)
         self.inner.open(configuration)
+        self.inner.config = self.inner.config.replace(batch_size=None)
 
     def flat_map(self, value: Any, out: Collector) -> None:
-        if not self.batch_size:
+        if isinstance(value, RecordBatch):
+            with prange("quick_evaluate.batch"):
+                self._push((self.inner.evaluator.predict_records(value), value), out)
+            return
+        if not self.config.batch_size:
             out.collect(quick_udf(value, self.inner.evaluator))
             return
+        if not self._buf:
+            self._first_ts = self._now()
         self._buf.append(value)
-        if len(self._buf) >= self.batch_size:
+        if len(self._buf) >= self.config.batch_size:
             self._flush(out)
+        else:
+            self._arm(out)
+
+    def _arm(self, out: Collector) -> None:
+        lat = self.config.max_batch_latency_ms
+        rctx = getattr(self, "runtime_context", None)
+        if lat is None or rctx is None or self._timer or not self._buf:
+            return
+        self._timer = True
+
+        def fire(now: float) -> None:
+            self._timer = False
+            if self._buf and now >= self._first_ts + lat / 1e3:
+                METRICS.inc("batcher.latency_flushes")
+                self._flush(out)
+            self._arm(out)
+
+        rctx.register_timer(self._first_ts + lat / 1e3, fire)
 
     def _flush(self, out: Collector) -> None:
         if not self._buf:
             return
         buf, self._buf = self._buf, []
-        preds = _score_calls(self.inner.evaluator, [(as_vector(v), None) for v in buf], self.device, self.plan_opts)
+        model = self.inner.evaluator
+        with prange("quick_evaluate.flush"):
+            batch = RecordBatch.from_vectors(buf, len(model.active_fields))
+            preds = model.predict_records(batch)
         for v, p in zip(buf, preds):
             out.collect((p, v))
 
     def end_of_input(self, out: Collector) -> None:
         self._flush(out)
+        self._drain_pending(out)
 
     def on_barrier(self, out: Collector) -> None:
-        self._flush(out)
+        self.end_of_input(out)
+
+    def checkpoint_models(self) -> Dict[str, dict]:
+        return self.inner.checkpoint_models()
+
+    def __getstate__(self):
+        d = dict(self.__dict__)
+        for k in ("_pipeline", "_pending", "dist", "runtime_context"):
+            d.pop(k, None)
+        d["_buf"] = []
+        return d

@@ -1,20 +1,29 @@
-"""A small deterministic dataflow runtime with Flink's operator semantics.
+"""A deterministic dataflow runtime with Flink's operator semantics — in one process, or one
+process per GPU under ``torchrun`` (SPMD data parallelism over RCCL / gloo).
 
 The reference runs on Apache Flink (TaskManagers, network stack, checkpoints). This runtime keeps
-exactly the semantics the reference's operators depend on, in one process:
+exactly the semantics the reference's operators depend on:
 
 * a job graph of sources, one-input operators (map / flat_map / filter / process), two-input
   operators (``connect`` + ``broadcast``) and sinks;
-* per-operator **parallelism**: every subtask holds its own (deep-copied) operator instance —
-  one model replica per subtask, like Flink (`S/api/functions/EvaluationFunction.scala:43`);
-  records are routed ``forward`` / ``rebalance`` (round-robin) / ``broadcast``;
-* **deterministic interleaving** of multiple sources: elements are merged by timestamp when the
-  sources provide one, else by source order — the analogue of the reference's
-  ``TemporizedSourceFunction`` (`T/sources/TemporizedSourceFunction.scala:35-56`) without sleeps;
-* **checkpoints**: count-based barriers; ``CheckpointedFunction``s snapshot into operator state
-  (union / split list state) persisted as JSON by :class:`CheckpointStorage`; ``execute(restore=…)``
-  re-initialises operators from a manifest (`S/api/functions/EvaluationCoFunction.scala:76-96`);
-* failures inside operators abort the job with :class:`JobExecutionException` (as Flink's
+* per-operator **parallelism**: every subtask holds its own operator instance — one model
+  replica per subtask, like Flink (`S/api/functions/EvaluationFunction.scala:43`). In one process
+  the subtasks are copies routed ``forward`` / ``rebalance`` / ``broadcast``; **under torchrun
+  every rank is one subtask of every operator** (parallelism = world size, one GPU each): event
+  sources are sharded by rank, broadcast (control) streams are replicated to every rank, model
+  loads parse once on rank 0 and replicate the compiled tensors (SURVEY §2.6 F1–F5);
+* **deterministic interleaving** of multiple sources (by timestamp when the sources provide one,
+  else round-robin) — the analogue of `T/sources/TemporizedSourceFunction.scala:35-56`;
+* **processing-time timers** on the job :class:`~flink_jpmml_amd.stream.clock.Clock` (latency
+  bound micro-batches flush while a slow source sleeps);
+* **checkpoints** with **source offsets**: count-based barriers on the primary source's global
+  offset, aligned across ranks; ``CheckpointedFunction``s snapshot into operator state (union /
+  split list state); rank 0 writes one JSON manifest (operator state of every subtask, source
+  offsets, sha256 of every served model); transactional sinks pre-commit at the barrier and
+  commit after the manifest is durable. ``execute(restore=…)`` re-broadcasts the manifest,
+  re-initialises operators (`S/api/functions/EvaluationCoFunction.scala:76-96`) and resumes every
+  source at its offset: outputs of a restarted job equal an uninterrupted run's (exactly-once);
+* failures inside operators abort the job with :class:`JobExecutionException` (Flink's
   ``JobExecutionException`` in the reference's tests, `T/RichDataStreamSpec.scala:82-89`).
 """
 
@@ -26,11 +35,13 @@ import itertools
 import logging
 import time
 from dataclasses import dataclass, field
-from typing import Any, Callable, Dict, Iterable, Iterator, List, Optional, Tuple
+from typing import Any, Callable, Dict, Iterator, List, Optional, Tuple
 
+from ..utils.metrics import METRICS
+from ..utils.profiling import prange
+from .clock import Clock, SystemClock, set_current_clock
 from .functions import (
     CheckpointedFunction,
-    CoProcessFunction,
     Collector,
     FunctionInitializationContext,
     FunctionSnapshotContext,
@@ -38,8 +49,8 @@ from .functions import (
     RichFunction,
     RuntimeContext,
     SinkFunction,
-    SourceFunction,
 )
+from .sources import SourceReader
 from .state import CheckpointStorage, OperatorStateStore
 
 logger = logging.getLogger(__name__)
@@ -67,6 +78,7 @@ class Node:
     timestamp_fn: Optional[Callable[[Any], Any]] = None
     uid: str = ""
     op_kind: str = ""  # map | flat_map | filter | process | co_process | sink
+    dist_mode: str = "shard"  # sources under torchrun: shard | replicate | either | parallel
 
     def __hash__(self) -> int:
         return id(self)
@@ -85,7 +97,7 @@ def _encode_state(x: Any) -> Any:
     """JSON encoding of state items: dicts keyed by ModelId become lists of entries."""
     from ..domain.model_id import ModelId, ModelInfo
 
-    if isinstance(x, dict) and all(isinstance(k, ModelId) for k in x):
+    if isinstance(x, dict) and x and all(isinstance(k, ModelId) for k in x):
         return {"__metadata__": [{"name": k.name, "version": k.version, "path": v.path if isinstance(v, ModelInfo)
                                   else str(v)} for k, v in x.items()]}
     return x
@@ -113,6 +125,10 @@ class Executor:
         self.env = env
         self.sinks = sinks
         self.restore = restore
+        self.dist = env.dist_ctx if env.dist_ctx is not None and env.dist_ctx.is_distributed else None
+        self.rank = self.dist.rank if self.dist else 0
+        self.world = self.dist.world_size if self.dist else 1
+        self.clock: Clock = env.clock or SystemClock()
         self.nodes: List[Node] = self._topo(sinks)
         self.down: Dict[int, List[Tuple[Node, str, int]]] = {id(n): [] for n in self.nodes}
         for n in self.nodes:
@@ -121,6 +137,10 @@ class Executor:
         self.subtasks: Dict[int, List[_Subtask]] = {}
         self.records_in = 0
         self.checkpoint_paths: List[str] = []
+        self.readers: Dict[int, SourceReader] = {}
+        self.primary: Optional[Node] = None
+        self.next_cid = 1
+        self.watchdog = None
 
     @staticmethod
     def _topo(sinks: List[Node]) -> List[Node]:
@@ -139,25 +159,42 @@ class Executor:
             visit(s)
         return order
 
+    def _parallelism(self, n: Node) -> int:
+        return self.world if self.dist else n.parallelism
+
     # ------------------------------------------------------------------ setup
-    def _instantiate(self) -> None:
-        restored_state: Dict[str, Dict[str, list]] = {}
-        if self.restore:
+    def _restored_doc(self) -> dict:
+        if not self.restore:
+            return {}
+        doc = None
+        if self.rank == 0:
             doc = CheckpointStorage.read(self.restore)
-            restored_state = doc.get("operators", {})
+        if self.dist:  # rank 0 reads the manifest and re-broadcasts it (F4)
+            from ..parallel.dist import broadcast_object
+
+            doc = broadcast_object(doc, self.dist, group=self.dist.group("ctrl"))
+        return doc or {}
+
+    def _instantiate(self, doc: dict) -> None:
+        restored_state: Dict[str, Dict[str, dict]] = doc.get("operators", {})
         for n in self.nodes:
+            p = self._parallelism(n)
+            if self.dist:
+                indices = [self.rank]  # SPMD: this process is subtask `rank` of every operator
+            else:
+                indices = list(range(n.parallelism))
             subs = []
-            for i in range(n.parallelism):
+            for i in indices:
                 op = None
                 if n.kind in ("one", "two", "sink"):
-                    op = n.factory if n.parallelism == 1 and not self.env.copy_operators else _clone(n.factory)
-                st = _Subtask(n, i, op)
-                subs.append(st)
+                    op = n.factory if len(indices) == 1 and not self.env.copy_operators else _clone(n.factory)
+                subs.append(_Subtask(n, i, op))
             self.subtasks[id(n)] = subs
             for st in subs:
                 op = st.op
+                rctx = RuntimeContext(n.name, st.index, p, clock=self.clock, dist=self.dist, config=self.env.config)
                 if isinstance(op, RichFunction):
-                    op.set_runtime_context(RuntimeContext(n.name, st.index, n.parallelism))
+                    op.set_runtime_context(rctx)
                 if isinstance(op, CheckpointedFunction):
                     restored = None
                     snap = restored_state.get(n.uid)
@@ -166,15 +203,16 @@ class Executor:
                         for name, entries in snap.items():
                             mode = entries.get("mode", "union")
                             parts = entries.get("subtasks", [])
-                            if mode == "union":
-                                items = [_decode_state(x) for part in parts for x in part]
-                            else:  # split: round-robin redistribution
-                                flat = [_decode_state(x) for part in parts for x in part]
-                                items = flat[st.index::n.parallelism]
-                            restored[name] = items
+                            flat = [_decode_state(x) for part in parts for x in part]
+                            # union: every subtask gets all entries; split: round-robin redistribution
+                            restored[name] = flat if mode == "union" else flat[st.index::p]
                     store = OperatorStateStore(restored)
                     op._state_store = store
                     op.initialize_state(FunctionInitializationContext(store, restored is not None))
+                if isinstance(op, SinkFunction):
+                    op.open(rctx)
+                    if self.restore and hasattr(op, "recover"):
+                        op.recover()
         for n in self.nodes:
             for st in self.subtasks[id(n)]:
                 st.out = Collector(self._emitter(n, st))
@@ -188,10 +226,10 @@ class Executor:
         def emit(value: Any) -> None:
             for dn, part, port in downs:
                 subs = self.subtasks[id(dn)]
-                if part == "broadcast":
+                if part == "broadcast" or len(subs) == 1:
                     targets = subs
-                elif part == "forward" and len(subs) == node.parallelism:
-                    targets = [subs[st.index]]
+                elif part == "forward" and len(subs) == len(self.subtasks[id(node)]):
+                    targets = [subs[st.index % len(subs)]]
                 else:  # rebalance
                     targets = [subs[st.rr % len(subs)]]
                     st.rr += 1
@@ -227,30 +265,34 @@ class Executor:
             raise RuntimeError(f"unknown operator kind {k}")
 
     # ------------------------------------------------------------------ sources
-    def _source_iter(self, n: Node) -> Iterator[Any]:
-        src = n.source
-        if isinstance(src, SourceFunction):
-            return iter(src.iterate())
-        return iter(src)
+    def _open_readers(self, doc: dict) -> List[Node]:
+        offsets = {uid: int(v.get("offset", 0)) for uid, v in doc.get("sources", {}).items()}
+        sources = [n for n in self.nodes if n.kind == "source"]
+        for n in sources:
+            self.readers[id(n)] = SourceReader(n, self.rank, self.world, self.clock, offsets.get(n.uid, 0))
+        primaries = [n for n in sources if n.dist_mode != "replicate"] or sources
+        self.primary = primaries[0] if primaries else None
+        if self.env.checkpoint_every and self.primary is not None:
+            done = self.readers[id(self.primary)].offset // self.env.checkpoint_every
+            self.next_cid = done + 1
+        return sources
 
-    def _merged(self) -> Iterator[Tuple[Node, Any]]:
+    def _merged(self, sources: List[Node]) -> Iterator[Tuple[Node, int, Any]]:
         """Deterministic merge of every source: by timestamp when all sources define one, else
         round-robin by source (ties broken by source order)."""
-        sources = [n for n in self.nodes if n.kind == "source"]
-        iters = [(n, self._source_iter(n)) for n in sources]
+        iters = [(n, iter(self.readers[id(n)])) for n in sources]
         timed = all(n.timestamp_fn is not None for n in sources) and len(sources) > 1
         if timed:
             heap = []
             for si, (n, it) in enumerate(iters):
-                for v in it:
-                    heapq.heappush(heap, (n.timestamp_fn(v), si, next(_uid), n, v))
+                for g, v in it:
+                    heapq.heappush(heap, (n.timestamp_fn(v), si, next(_uid), n, g, v))
                     break
             while heap:
-                _, si, _, n, v = heapq.heappop(heap)
-                yield n, v
-                it = iters[si][1]
-                for nv in it:
-                    heapq.heappush(heap, (n.timestamp_fn(nv), si, next(_uid), n, nv))
+                _, si, _, n, g, v = heapq.heappop(heap)
+                yield n, g, v
+                for ng, nv in iters[si][1]:
+                    heapq.heappush(heap, (n.timestamp_fn(nv), si, next(_uid), n, ng, nv))
                     break
             return
         live = list(iters)
@@ -258,59 +300,151 @@ class Executor:
             nxt = []
             for n, it in live:
                 try:
-                    v = next(it)
+                    g, v = next(it)
                 except StopIteration:
                     continue
-                yield n, v
+                yield n, g, v
                 nxt.append((n, it))
             live = nxt
 
     # ------------------------------------------------------------------ checkpoints
-    def _checkpoint(self, cid: int) -> None:
-        for n in self.nodes:
-            for st in self.subtasks[id(n)]:
-                if hasattr(st.op, "on_barrier"):
-                    st.op.on_barrier(st.out)
-        operators: Dict[str, Dict[str, dict]] = {}
-        for n in self.nodes:
-            subs = self.subtasks[id(n)]
-            if not subs or not isinstance(subs[0].op, CheckpointedFunction):
-                continue
-            per_state: Dict[str, dict] = {}
-            for st in subs:
-                st.op.snapshot_state(FunctionSnapshotContext(cid, int(time.time() * 1000)))
-                snap = st.op._state_store.snapshot(_encode_state)
-                for name, s in snap.items():
-                    e = per_state.setdefault(name, {"mode": s["mode"], "subtasks": []})
-                    e["subtasks"].append(s["items"])
-            operators[n.uid] = per_state
-        path = self.env.checkpoint_storage.write(cid, {"operators": operators, "records_in": self.records_in})
-        self.checkpoint_paths.append(path)
+    def _maybe_checkpoint(self, upto: int) -> None:
+        """Take every checkpoint whose barrier offset is <= ``upto`` (primary-source offset)."""
+        every = self.env.checkpoint_every
+        if not every:
+            return
+        while self.next_cid * every <= upto:
+            self._checkpoint(self.next_cid, self.next_cid * every)
+            self.next_cid += 1
+
+    def _checkpoint(self, cid: int, barrier: int) -> None:
+        with prange("checkpoint"):
+            t0 = time.perf_counter()
+            for n in self.nodes:  # flush buffered micro-batches / in-flight scores in topological order
+                for st in self.subtasks[id(n)]:
+                    if hasattr(st.op, "on_barrier"):
+                        st.op.on_barrier(st.out)
+            operators: Dict[str, Dict[str, dict]] = {}
+            models: Dict[str, dict] = {}
+            for n in self.nodes:
+                subs = self.subtasks[id(n)]
+                for st in subs:
+                    if hasattr(st.op, "checkpoint_models"):
+                        models.update(st.op.checkpoint_models())
+                if not subs or not isinstance(subs[0].op, CheckpointedFunction):
+                    continue
+                per_state: Dict[str, dict] = {}
+                for st in subs:
+                    st.op.snapshot_state(FunctionSnapshotContext(cid, int(time.time() * 1000)))
+                    snap = st.op._state_store.snapshot(_encode_state)
+                    for name, s in snap.items():
+                        e = per_state.setdefault(name, {"mode": s["mode"], "subtasks": []})
+                        e["subtasks"].append(s["items"])
+                operators[n.uid] = per_state
+            sources = {}
+            for n in self.nodes:
+                if n.kind == "source":
+                    off = barrier if n is self.primary else self.readers[id(n)].offset
+                    sources[n.uid] = {"offset": off}
+            sinks = [st.op for n in self.nodes if n.kind == "sink" for st in self.subtasks[id(n)]]
+            for sk in sinks:
+                if hasattr(sk, "pre_commit"):
+                    sk.pre_commit(cid)
+            if self.dist:
+                from ..parallel.dist import gather_object
+                from ..utils.faults import guarded_collective
+
+                g = self.dist.group("ctrl")
+                parts = guarded_collective(gather_object, (operators, models), self.dist, group=g,
+                                           what=f"checkpoint {cid} state gather")
+                path = None
+                if self.rank == 0:
+                    merged_ops: Dict[str, Dict[str, dict]] = {}
+                    for ops, mods in parts:  # rank order = subtask order
+                        models.update(mods)
+                        for uid, states in ops.items():
+                            for name, s in states.items():
+                                e = merged_ops.setdefault(uid, {}).setdefault(name, {"mode": s["mode"],
+                                                                                     "subtasks": []})
+                                e["subtasks"].extend(s["subtasks"])
+                    path = self._write_manifest(cid, merged_ops, sources, models)
+                from ..parallel.dist import broadcast_object
+
+                path = guarded_collective(broadcast_object, path, self.dist, group=g,
+                                          what=f"checkpoint {cid} commit")
+            else:
+                path = self._write_manifest(cid, operators, sources, models)
+            for sk in sinks:
+                if hasattr(sk, "commit"):
+                    sk.commit(cid)
+            self.checkpoint_paths.append(path)
+            METRICS.inc("checkpoint.completed")
+            METRICS.observe("checkpoint.duration_ms", (time.perf_counter() - t0) * 1e3)
+
+    def _write_manifest(self, cid: int, operators, sources, models) -> str:
+        payload = {"operators": operators, "sources": sources, "models": models, "records_in": self.records_in,
+                   "world_size": self.world}
+        return self.env.checkpoint_storage.write(cid, payload)
 
     # ------------------------------------------------------------------ run
+    def _finish_input(self) -> None:
+        """End of input: align the last checkpoints across ranks, flush every operator, commit
+        sinks."""
+        if self.env.checkpoint_every and self.primary is not None:
+            # every rank iterates the whole logical stream (skipping other ranks' elements), so the
+            # final global offset is known locally: no collective that could interleave with a
+            # peer's last in-stream checkpoint
+            self._maybe_checkpoint(self.readers[id(self.primary)].offset)
+        for n in self.nodes:  # flush buffered micro-batches, in topological order
+            for st in self.subtasks[id(n)]:
+                if hasattr(st.op, "end_of_input"):
+                    st.op.end_of_input(st.out)
+        for n in self.nodes:
+            if n.kind == "sink":
+                for st in self.subtasks[id(n)]:
+                    if hasattr(st.op, "pre_commit"):
+                        st.op.pre_commit(-1)
+                    if hasattr(st.op, "commit"):
+                        st.op.commit(-1)
+
     def run(self, job_name: str) -> JobExecutionResult:
         t0 = time.perf_counter()
+        self.clock.bind_thread()
+        set_current_clock(self.clock)
+        cfg = self.env.config
         try:
-            self._instantiate()
-            cid = 0
-            every = self.env.checkpoint_every
-            for n, v in self._merged():
+            doc = self._restored_doc()
+            self._instantiate(doc)
+            sources = self._open_readers(doc)
+            if self.dist and cfg is not None and cfg.watchdog_s:
+                from ..utils.faults import Watchdog
+
+                self.watchdog = Watchdog(cfg.watchdog_s, name=f"rank{self.rank}").start()
+            fail_after = self.env.fail_after
+            for n, g, v in self._merged(sources):
+                if n is self.primary:
+                    self._maybe_checkpoint(g)
                 self.records_in += 1
-                if self.env.fail_after is not None and self.records_in > self.env.fail_after:
-                    raise SimulatedFailure(f"injected failure after {self.env.fail_after} records")
+                if fail_after is not None and self.records_in > fail_after:
+                    raise SimulatedFailure(f"injected failure after {fail_after} records")
+                if self.dist is not None:
+                    from ..utils.faults import injector
+
+                    injector().on_batch(self.rank, self.records_in - 1)
                 for st in self.subtasks[id(n)]:
                     st.out.collect(v)
-                    break  # sources have parallelism 1 in this runtime
-                if every and self.records_in % every == 0:
-                    cid += 1
-                    self._checkpoint(cid)
-            for n in self.nodes:  # end of input: flush buffered micro-batches, in topological order
-                for st in self.subtasks[id(n)]:
-                    if hasattr(st.op, "end_of_input"):
-                        st.op.end_of_input(st.out)
+                    break
+                if self.watchdog is not None:
+                    self.watchdog.kick()
+                self.clock.fire_due()
+            self._finish_input()
         except Exception as e:  # noqa: BLE001 - any operator failure fails the job
             raise JobExecutionException(f"Job '{job_name}' failed: {type(e).__name__}: {e}") from e
         finally:
+            if self.watchdog is not None:
+                self.watchdog.stop()
+            self.clock.timers.clear()
+            set_current_clock(None)
             for n in self.nodes:
                 for st in self.subtasks.get(id(n), []):
                     if isinstance(st.op, (RichFunction, SinkFunction)):
@@ -318,6 +452,7 @@ class Executor:
                             st.op.close()
                         except Exception:  # noqa: BLE001
                             logger.exception("close() failed")
+        METRICS.inc("job.records_in", self.records_in)
         return JobExecutionResult(job_name, (time.perf_counter() - t0) * 1e3, self.records_in, self.checkpoint_paths)
 
 

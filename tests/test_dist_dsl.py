@@ -1,0 +1,204 @@
+"""The Flink-shaped DSL under data parallelism: one process per rank (gloo on CPU here; the same
+code runs RCCL on GPUs under torchrun). Every rank builds the same job; operators run as one
+subtask per rank; event streams are sharded, control streams replicated, models parsed once on
+rank 0 and replicated, outputs all-gathered; checkpoints are aligned across ranks and a killed
+rank is recovered from the manifest with exactly-once output (SURVEY §2.6 F1–F5, §5.3, §5.4)."""
+
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+N1 = "a1b2c3d4-0000-4000-8000-000000000001"
+N2 = "a1b2c3d4-0000-4000-8000-000000000002"
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _spawn(world, fn, args, extra_env=None, timeout=180):
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_entry, args=(r, world, port, fn, args, q, extra_env or {})) for r in range(world)]
+    for p in procs:
+        p.start()
+    import queue as _queue
+    import time as _time
+
+    results = {}
+    deadline = _time.monotonic() + timeout
+    try:
+        while len(results) < world and _time.monotonic() < deadline:
+            try:
+                r, res = q.get(timeout=1.0)
+                results[r] = res
+            except _queue.Empty:
+                if not any(p.is_alive() for p in procs):  # a killed rank never reports
+                    break
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    return results, [p.exitcode for p in procs]
+
+
+def _entry(rank, world, port, fn, args, q, extra_env):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), FJA_DIST_TIMEOUT_S="30", **extra_env)
+    try:
+        res = fn(*args)
+        q.put((rank, res))
+    except BaseException as e:  # noqa: BLE001
+        q.put((rank, ("error", type(e).__name__, str(e)[:300], type(e.__cause__).__name__ if e.__cause__ else None)))
+    finally:
+        import torch.distributed as dist
+
+        if dist.is_initialized():
+            try:
+                dist.destroy_process_group()
+            except Exception:  # noqa: BLE001
+                pass
+
+
+# ------------------------------------------------------------------ jobs (run on every rank)
+
+
+def _dynamic_seq(kmeans, notarget):
+    from flink_jpmml_amd import AddMessage, DelMessage
+    from tests.test_stream import DynamicInput
+
+    seq, k = [], 0
+
+    def ev(name, vals=(1.0, 1.0, 1.0, 1.0)):
+        nonlocal k
+        k += 1
+        return ("L", DynamicInput(f"{name}_1", vals, occurred_on=k))
+
+    seq += [ev(N1)]
+    seq += [("R", AddMessage(N1, 1, kmeans, 0)), ("R", AddMessage(N2, 1, notarget, 0))]
+    seq += [ev(N1, (1.0 + i / 7, 2.0, 3.0, 4.0 - i / 9)) for i in range(9)] + [ev(N2) for _ in range(3)]
+    seq += [("R", DelMessage(N1, 1, 0))] + [ev(N1) for _ in range(3)]
+    seq += [("R", AddMessage(N1, 2, kmeans, 0))] + [ev(N1.replace("1", "1"), (6.0, 3.0, 5.0, 2.0)) for _ in range(2)]
+    return seq
+
+
+def job_dynamic(kmeans, notarget, batch):
+    from flink_jpmml_amd.stream import StreamExecutionEnvironment
+
+    env = StreamExecutionEnvironment.get_execution_environment()
+    assert env.is_distributed and env.parallelism == int(os.environ["WORLD_SIZE"])
+    events, control = env.from_either(_dynamic_seq(kmeans, notarget))
+    out = events.with_support_stream(control).evaluate(
+        lambda e, m: (e.occurred_on, m.predict(e.to_vector()).value.get_or_else(-1.0)), batch_size=batch).collect()
+    return sorted(out)
+
+
+def job_columnar(kmeans, n, batch_rows):
+    import numpy as np
+
+    from flink_jpmml_amd import ModelReader
+    from flink_jpmml_amd.stream import StreamExecutionEnvironment
+    from flink_jpmml_amd.utils.metrics import METRICS
+
+    env = StreamExecutionEnvironment.get_execution_environment()
+    X = np.random.default_rng(7).uniform(0.2, 7.0, size=(n, 4))
+    out = env.from_batches(X, batch_rows=batch_rows).quick_evaluate(ModelReader(kmeans)).collect()
+    offs = [b.offset for _, b in out]
+    scores = np.concatenate([p.values(-1.0) for p, _ in out])
+    order = np.argsort(np.concatenate([b.offset + np.arange(len(b)) for _, b in out]))
+    return offs, scores[order].tolist(), METRICS.counters.get("model.loads_replicated", 0)
+
+
+def job_exactly_once(kmeans, out_dir, ck_dir, restore):
+    from flink_jpmml_amd.stream import FileSink, StreamExecutionEnvironment
+    from tests.test_stream import DynamicInput
+
+    from flink_jpmml_amd import AddMessage
+
+    seq = [("R", AddMessage(N1, 1, kmeans, 0))] + \
+          [("L", DynamicInput(f"{N1}_1", (1.0 + i / 10, 2.0, 3.0, 1.0), occurred_on=i)) for i in range(40)]
+    env = StreamExecutionEnvironment.get_execution_environment()
+    env.enable_checkpointing(every_n_records=8, directory=ck_dir)
+    events, control = env.from_either(seq)
+    events.with_support_stream(control).evaluate(
+        lambda e, m: [e.occurred_on, m.predict(e.to_vector()).value.get_or_else(-1.0)], uid="scorer"
+    ).add_sink(FileSink(out_dir))
+    env.execute("dist-exactly-once", restore=restore)
+    return "done"
+
+
+# ------------------------------------------------------------------ tests
+
+
+def _single_process_dynamic(kmeans, notarget):
+    from flink_jpmml_amd.stream import StreamExecutionEnvironment
+
+    env = StreamExecutionEnvironment()
+    events, control = env.from_either(_dynamic_seq(kmeans, notarget))
+    return sorted(events.with_support_stream(control).evaluate(
+        lambda e, m: (e.occurred_on, m.predict(e.to_vector()).value.get_or_else(-1.0))).collect())
+
+
+@pytest.mark.parametrize("world,batch", [(2, None), (4, None), (2, 3), (4, 2)])
+def test_dynamic_job_dp(fixtures_dir, world, batch):
+    """The 15-scenario dynamic-serving contract, sharded over `world` ranks: identical outputs."""
+    ref = _single_process_dynamic(fixtures_dir["kmeans"], fixtures_dir["kmeans_nooutput_notarget"])
+    res, codes = _spawn(world, job_dynamic, (fixtures_dir["kmeans"], fixtures_dir["kmeans_nooutput_notarget"], batch))
+    assert codes == [0] * world, res
+    for r in range(world):
+        assert res[r] == ref, res[r]
+    assert sum(1 for _, s in ref if s == -1.0) >= 7 and sum(1 for _, s in ref if s != -1.0) >= 9
+
+
+def test_columnar_job_dp_shards_and_gathers(fixtures_dir):
+    from flink_jpmml_amd.api.pmml_model import PmmlModel
+
+    n, world = 1000, 2
+    res, codes = _spawn(world, job_columnar, (fixtures_dir["kmeans"], n, 100))
+    assert codes == [0] * world, res
+    X = np.random.default_rng(7).uniform(0.2, 7.0, size=(n, 4))
+    ref = PmmlModel.from_path(fixtures_dir["kmeans"]).predict(X).values(-1.0).tolist()
+    for r in range(world):
+        offs, scores, replicated = res[r]
+        assert scores == ref
+        assert offs == [0, 200, 400, 600, 800, 100, 300, 500, 700, 900]  # rank 0's shard, then rank 1's
+        assert replicated == 1  # parsed once on rank 0, replicated (one collective load per rank)
+
+
+def test_killed_rank_recovers_exactly_once(fixtures_dir, tmp_path):
+    """kill_rank=1@9: rank 1 dies mid-stream; rank 0's next checkpoint collective raises
+    RankFailure; restarting both ranks from the last aligned manifest yields exactly the
+    uninterrupted run's committed output (no duplicates, no gaps)."""
+    from flink_jpmml_amd.stream import FileSink
+    from flink_jpmml_amd.stream.state import CheckpointStorage
+    from flink_jpmml_amd.utils.faults import EXIT_KILLED_RANK
+
+    k = fixtures_dir["kmeans"]
+    ref_dir, ref_ck = str(tmp_path / "ref"), str(tmp_path / "ref-ck")
+    res, codes = _spawn(2, job_exactly_once, (k, ref_dir, ref_ck, None))
+    assert codes == [0, 0] and res[0] == "done", res
+    expected = sorted(map(tuple, FileSink.read(ref_dir)))
+    assert len(expected) == 40
+
+    out_dir, ck = str(tmp_path / "out"), str(tmp_path / "ck")
+    res, codes = _spawn(2, job_exactly_once, (k, out_dir, ck, None), extra_env={"FJA_FAULTS": "kill_rank=1@9"})
+    assert codes[1] == EXIT_KILLED_RANK
+    assert res[0][0] == "error" and res[0][1] == "JobExecutionException" and res[0][3] == "RankFailure", res
+    latest = CheckpointStorage(ck).latest()
+    assert latest is not None
+    doc = CheckpointStorage.read(latest)
+    assert doc["world_size"] == 2 and len(doc["operators"]["scorer"]["metadata-snapshot"]["subtasks"]) == 2
+    partial = FileSink.read(out_dir)
+    assert 0 < len(partial) < 40
+    res, codes = _spawn(2, job_exactly_once, (k, out_dir, ck, latest))
+    assert codes == [0, 0], res
+    assert sorted(map(tuple, FileSink.read(out_dir))) == expected

@@ -258,9 +258,10 @@ def test_checkpoint_restore_metadata_only(fixtures_dir, tmp_path):
     assert isinstance(ei.value.__cause__, SimulatedFailure)
     latest = env.checkpoint_storage.latest()
     assert latest is not None
-    # restart from the checkpoint with only events: the metadata (not the models) was restored
+    # restart from the checkpoint with a NEW source (different uid: no offset to resume) holding
+    # only events: the metadata (not the models) was restored
     env2 = StreamExecutionEnvironment(3)
-    ev2, ctrl2 = env2.from_either([ev(N1, 1), ev(N2, 1), ev(N2, 7)])
+    ev2, ctrl2 = env2.from_either([ev(N1, 1), ev(N2, 1), ev(N2, 7)], uid="fresh-source")
     out = ev2.with_support_stream(ctrl2).evaluate(udf, uid="scorer").collect(restore=latest)
     assert out == [S3, S3, E]
     doc = env.checkpoint_storage.read(latest)
@@ -280,3 +281,42 @@ def test_batched_udf_replays_in_order(fixtures_dir):
         ModelReader(fixtures_dir["kmeans"]), lambda e, m: (e.values, m.predict(e.to_vector()).value.get_or_else(-1.0))
     ).collect()
     assert out == ref and out[0] == (ONES, 3.0) and out[2] == ((1.0, 2.0), -1.0)
+
+
+def test_restore_resumes_source_offsets_exactly_once(fixtures_dir, tmp_path):
+    """Same job restarted from its last checkpoint: the source resumes at the manifest's offset and
+    a transactional FileSink commits per checkpoint, so both runs' committed outputs together
+    equal one uninterrupted run (no duplicates, no gaps)."""
+    from flink_jpmml_amd.stream import FileSink
+
+    seq = [add(N1, 1, fixtures_dir["kmeans"])] + [ev(N1, 1, (1.0 + i / 10, 1.0, 1.0, 1.0)) for i in range(9)] + \
+          [add(N2, 1, fixtures_dir["kmeans"])] + [ev(N2, 1, (5.0, 3.0, 5.0 + i / 10, 2.0)) for i in range(7)]
+
+    def job(out_dir, ckpt_dir, fail_after=None, restore=None):
+        env = StreamExecutionEnvironment()
+        env.enable_checkpointing(every_n_records=4, directory=str(ckpt_dir))
+        env.inject_failure(fail_after)
+        events, control = env.from_either(seq)
+        events.with_support_stream(control).evaluate(
+            lambda e, m: [e.model_id, m.predict(e.to_vector()).value.get_or_else(-1.0)], uid="scorer"
+        ).add_sink(FileSink(str(out_dir)))
+        env.execute("exactly-once", restore=restore)
+        return env
+
+    ref_dir = tmp_path / "ref"
+    job(ref_dir, tmp_path / "ck-ref")
+    expected = FileSink.read(str(ref_dir))
+    assert len(expected) == 16
+
+    out_dir, ck = tmp_path / "out", tmp_path / "ck"
+    with pytest.raises(JobExecutionException):
+        job(out_dir, ck, fail_after=11)
+    from flink_jpmml_amd.stream.state import CheckpointStorage
+
+    latest = CheckpointStorage(str(ck)).latest()
+    doc = CheckpointStorage.read(latest)
+    assert doc["checkpoint_id"] == 2 and list(doc["sources"].values())[0]["offset"] == 8
+    assert all(len(m["sha256"]) == 64 for m in doc["models"].values())
+    assert len(FileSink.read(str(out_dir))) < len(expected)  # the crashed run committed a prefix
+    job(out_dir, ck, restore=latest)
+    assert FileSink.read(str(out_dir)) == expected
