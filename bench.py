@@ -3,21 +3,28 @@
 
 Metric / config from ``BASELINE.json``: "records/sec (whole node) on 1k-tree GBDT PMML at
 1/2/4/8 MI355X; p50 latency" — 1000-tree XGBoost-style GBDT PMML (depth 6, 32 float features),
-synthetic 1M-row stream per GPU per step (weak scaling), random-initialised trees.
+synthetic record stream, random-initialised trees (weak scaling: each GPU scores its own shard).
 
-One step (per rank) = score this rank's 1,048,576-row shard end to end:
-pinned host records → H2D (copy stream) → fused prepare + tree-ensemble HIP kernel → scores D2H
-(pinned host sink), pipelined in micro-batches over three HIP streams; with N > 1 ranks the scored
-shards are also all-gathered over RCCL (the stream sink). Nothing is skipped or
-cached inside the timed region: every step re-copies and re-scores every row.
+**The timed path is the public DSL** (``--api dsl``, default)::
 
-Usage::
+    env = StreamExecutionEnvironment(config=ScoringConfig(device="cuda", ...), dist_ctx=ctx)
+    env.add_source(<pinned RecordBatch per step>, mode="parallel")
+       .quick_evaluate(ModelReader(model.pmml))            # EvaluationFunction, one per rank
+       .add_sink(<waits for every PredictionBatch; all-gathers the scores over RCCL when N > 1>)
+
+One step (per rank) = one RecordBatch of ``--rows`` records in pinned host memory scored end to
+end: H2D in micro-batches on a copy stream → fused prepare + tree-ensemble HIP kernel whose
+epilogue writes scores straight into pinned host memory → the sink waits for the batch (and with
+N > 1 all-gathers the scored shard over RCCL). Nothing is skipped or cached: every
+step re-copies and re-scores every row. ``--api engine`` times the bare StreamingScorer instead.
+
+Under ``torchrun`` the model is parsed once on rank 0 and its compiled tensors are
+RCCL-broadcast to every rank (F2). Rank 0 prints ONE JSON line.
 
     python bench.py                                # 1 GPU, defaults
-    python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \\
         --master-port 29500 bench.py --gpus 8 --steps 20 --warmup 3
-
-Rank 0 prints ONE JSON line.
+    python bench.py --model rf|chain|mlp           # BASELINE configs 3 / 5 / 4
 """
 
 from __future__ import annotations
@@ -26,11 +33,21 @@ import argparse
 import json
 import os
 import sys
+import tempfile
 import time
 
 import numpy as np
 
 METRIC = "records/sec (whole node) on 1k-tree GBDT PMML at 1/2/4/8 MI355X; p50 latency"
+
+MODELS = {
+    # name: (BASELINE config, description)
+    "gbdt": ("1000-tree GBDT PMML (XGBoost-exported), 1M-row synthetic stream, 1xMI355X", "GBDT regression"),
+    "chain": ("MiningModel ensemble (GBDT chain + logistic calibrator), fp8 weights on CDNA4",
+              "GBDT modelChain -> logistic calibrator"),
+    "rf": ("500-tree RandomForest PMML, DP=8 stream shard over xGMI on 8xMI355X", "random forest majority vote"),
+    "mlp": ("3-layer NeuralNetwork PMML, bf16 MFMA GEMM path, 8xMI355X", "NeuralNetwork 64-256-256-1"),
+}
 
 
 def parse_args(argv=None):
@@ -38,24 +55,107 @@ def parse_args(argv=None):
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--trees", type=int, default=1000)
-    p.add_argument("--depth", type=int, default=6)
-    p.add_argument("--features", type=int, default=32)
-    p.add_argument("--rows", type=int, default=1 << 20, help="rows per GPU per step")
+    p.add_argument("--api", choices=["dsl", "engine"], default="dsl")
+    p.add_argument("--model", choices=sorted(MODELS), default="gbdt")
+    p.add_argument("--trees", type=int, default=None, help="default 1000 (gbdt/chain), 500 (rf)")
+    p.add_argument("--depth", type=int, default=None, help="default 6 (gbdt/chain), 8 (rf)")
+    p.add_argument("--features", type=int, default=None, help="default 32 (trees), 64 (mlp)")
+    p.add_argument("--rows", type=int, default=1 << 23,
+                   help="rows per GPU per step (8M: a 20-step timed region is ~0.4 s on one GPU)")
     p.add_argument("--micro-batch", type=int, default=1 << 19)
     p.add_argument("--pipeline-depth", type=int, default=3, help="input ring slots (H2D/compute overlap)")
-    p.add_argument("--h2d-streams", type=int, default=1, help="concurrent copy streams per micro-batch (1 measured best: splitting adds ~2 ms of host submit per step)")
-    p.add_argument("--objective", choices=["regression", "binary"], default="regression",
-                   help="binary = modelChain GBDT -> logistic calibrator (BASELINE config 5)")
-    p.add_argument("--precision", choices=["fp32", "fp8"], default="fp32",
-                   help="leaf-value precision (fp8 = OCP e4m3 leaves, fp32 thresholds; config 5)")
+    p.add_argument("--max-inflight", type=int, default=3, help="scored steps in flight before the sink waits")
+    p.add_argument("--precision", choices=["fp32", "bf16", "fp8"], default=None,
+                   help="default fp32 (trees), bf16 (mlp, BASELINE config 4); fp8 = e4m3 leaves (config 5)")
     p.add_argument("--latency-batch", type=int, default=4096)
     p.add_argument("--latency-iters", type=int, default=50)
     p.add_argument("--no-allgather", action="store_true")
     p.add_argument("--check-rows", type=int, default=8192, help="rows checked against the fp64 oracle (untimed)")
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--no-numa", action="store_true", help="do not bind to the GPU's NUMA node")
-    return p.parse_args(argv)
+    p.add_argument("--force-dist", action="store_true", help="form a 1-rank RCCL group at N=1 (exercise RCCL)")
+    a = p.parse_args(argv)
+    a.trees = a.trees or (500 if a.model == "rf" else 1000)
+    a.depth = a.depth or (8 if a.model == "rf" else 6)
+    a.features = a.features or (64 if a.model == "mlp" else 32)
+    a.precision = a.precision or ("bf16" if a.model == "mlp" else "fp32")
+    return a
+
+
+def model_text(args) -> str:
+    from flink_jpmml_amd.bench import synth
+
+    if args.model == "gbdt":
+        return synth.gbdt_pmml(n_trees=args.trees, depth=args.depth, n_features=args.features, seed=args.seed)
+    if args.model == "chain":
+        return synth.gbdt_pmml(n_trees=args.trees, depth=args.depth, n_features=args.features, seed=args.seed,
+                               objective="binary")
+    if args.model == "rf":
+        return synth.random_forest_pmml(n_trees=args.trees, depth=args.depth, n_features=args.features,
+                                        n_classes=3, seed=args.seed)
+    return synth.mlp_pmml(n_features=args.features, hidden=(256, 256), n_out=1, seed=args.seed)
+
+
+class _StepSource:
+    """``--warmup + --steps`` RecordBatches (one per step) of this rank's pinned shard; calls
+    ``on_step(i)`` right before step i is handed to the pipeline (timer start hook)."""
+
+    def __init__(self, X, n_steps, on_step):
+        self.X = X
+        self.n = n_steps
+        self.on_step = on_step
+
+    def open_subtask(self, rank, world):  # parallel source: every rank scores its own shard
+        pass
+
+    def iterate(self):
+        from flink_jpmml_amd.api.batch import RecordBatch
+
+        for i in range(self.n):
+            self.on_step(i)
+            yield RecordBatch(self.X, offset=i * len(self.X))
+
+
+class _BenchSink:
+    """Waits for every scored step (the host observes completion) and, with N > 1 ranks,
+    all-gathers the scored shard over RCCL on a side stream."""
+
+    def __init__(self, ctx, gather: bool, rows: int):
+        self.ctx = ctx
+        self.gather = gather
+        self.rows_seen = 0
+        self.last = None
+        self._works = []
+        self._bufs = None
+        self._comm = None
+        if gather:
+            import torch
+
+            n = rows * ctx.world_size
+            self._bufs = (torch.empty(n, dtype=torch.float32, device=ctx.device),
+                          torch.empty(n, dtype=torch.uint8, device=ctx.device))
+            self._comm = torch.cuda.Stream(ctx.device)
+
+    def invoke(self, value) -> None:
+        pb, batch = value
+        pb.wait()
+        self.rows_seen += len(pb)
+        self.last = pb
+        if self.gather:
+            import torch
+
+            from flink_jpmml_amd.parallel import all_gather_scores
+
+            for w in self._works:  # one gather in flight: bounded device memory
+                w.wait()
+            with torch.cuda.stream(self._comm):
+                s, v = pb.device_out
+                _, _, self._works = all_gather_scores(s, v, self.ctx, async_op=True, out=self._bufs)
+
+    def finish(self) -> None:
+        for w in self._works:
+            w.wait()
+        self._works = []
 
 
 def main(argv=None) -> int:
@@ -63,41 +163,49 @@ def main(argv=None) -> int:
     import torch
     import torch.distributed as dist
 
-    from flink_jpmml_amd.bench.synth import gbdt_pmml, stream_matrix
-    from flink_jpmml_amd.parallel import all_gather_scores, broadcast_plan, init_from_env
+    from flink_jpmml_amd import ModelReader
+    from flink_jpmml_amd.bench.synth import stream_matrix
+    from flink_jpmml_amd.config import ScoringConfig
+    from flink_jpmml_amd.parallel import broadcast_object, init_from_env
     from flink_jpmml_amd.runtime.compiled import CompiledPmml
     from flink_jpmml_amd.runtime.engine import StreamingScorer
+    from flink_jpmml_amd.runtime.loading import load_replicated
+    from flink_jpmml_amd.utils.metrics import METRICS
 
     if not torch.cuda.is_available():
         print(json.dumps({"metric": METRIC, "error": "no GPU visible"}))
         return 1
-    ctx = init_from_env()
+    ctx = init_from_env(force=args.force_dist)
     device = ctx.device
     N = ctx.world_size
     if args.gpus != N and ctx.rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={N}; using {N}", file=sys.stderr)
+    cfg = ScoringConfig(device=device, micro_batch=args.micro_batch, pipeline_depth=args.pipeline_depth,
+                        max_inflight=args.max_inflight, precision=args.precision, fallback="error")
 
-    # ---- model: rank 0 generates + parses + lowers once; RCCL-broadcast of the device tensors
-    t_load = time.perf_counter()
-    compiled = None
-    plan = None
+    # ---- the model: rank 0 writes the synthetic PMML; every rank loads it through the collective
+    #      parse-once / RCCL-broadcast path the DSL operators use
+    path = None
     if ctx.rank == 0:
-        text = gbdt_pmml(n_trees=args.trees, depth=args.depth, n_features=args.features, seed=args.seed,
-                         objective=args.objective)
-        compiled = CompiledPmml.from_string(text)
-        plan = compiled.plan(device, precision=args.precision)
-    plan = broadcast_plan(plan, ctx)
+        fd, path = tempfile.mkstemp(suffix=".pmml", prefix="bench-")
+        with os.fdopen(fd, "w") as fh:
+            fh.write(model_text(args))
+    path = broadcast_object(path, ctx)
+    t_load = time.perf_counter()
+    lm = load_replicated(path, ctx, device, cfg)
     torch.cuda.synchronize()
     load_s = time.perf_counter() - t_load
+    model = lm.model
+    plan = model.scorer.plan
 
     # ---- untimed correctness spot-check against the float64 oracle (rank 0)
     check = {}
     if ctx.rank == 0 and args.check_rows > 0:
+        compiled = CompiledPmml.from_string(open(path).read())
         Xc = stream_matrix(args.check_rows, args.features, seed=99, missing_rate=0.02)
         s_ref, v_ref = compiled.score_matrix_oracle(Xc)
-        s_gpu, v_gpu = plan.score(Xc)
-        s_gpu = s_gpu.cpu().numpy()
-        v_gpu = v_gpu.cpu().numpy()
+        pb = model.predict(Xc)
+        s_gpu, v_gpu = pb.scores, pb.valid
         both = v_ref & v_gpu
         err = float(np.max(np.abs(s_gpu[both] - s_ref[both]))) if both.any() else float("nan")
         check = {"oracle_rows": int(args.check_rows), "valid_match": bool((v_ref == v_gpu).all()),
@@ -108,49 +216,52 @@ def main(argv=None) -> int:
 
     numa_node = None if args.no_numa else bind_to_gpu_numa(device.index or 0)
     X = torch.from_numpy(stream_matrix(args.rows, args.features, seed=1000 + ctx.rank)).pin_memory()
-    score_h = torch.empty(args.rows, dtype=torch.float32).pin_memory()
-    valid_h = torch.empty(args.rows, dtype=torch.uint8).pin_memory()
-    scorer = StreamingScorer(plan, micro_batch=args.micro_batch, depth=args.pipeline_depth, max_rows=args.rows,
-                             h2d_streams=args.h2d_streams)
-    gather_out = None
-    if N > 1 and not args.no_allgather:
-        gather_out = (torch.empty(args.rows * N, dtype=torch.float32, device=device),
-                      torch.empty(args.rows * N, dtype=torch.uint8, device=device))
+    gather = N > 1 and not args.no_allgather
+    timing = {}
 
-    comm = torch.cuda.Stream(device) if gather_out is not None else None
+    def barrier_sync():
+        torch.cuda.synchronize()
+        ctx.barrier()
+        torch.cuda.synchronize()
 
-    def step():
-        h = scorer.submit(X, score_h, valid_h)
-        if gather_out is not None:
-            # all-gather this step's scored shard on a side stream (overlaps the next step)
-            comm.wait_stream(scorer.comp)
-            with torch.cuda.stream(comm):
-                _, _, works = all_gather_scores(h.score_dev, h.valid_dev, ctx, async_op=True, out=gather_out)
-                for w in works:
-                    w.wait()
-            scorer.mark_consumed(h, comm)
-        return h
+    if args.api == "dsl":
+        from flink_jpmml_amd.stream import StreamExecutionEnvironment
 
-    for _ in range(args.warmup):
-        scorer.wait(step())
-    torch.cuda.synchronize()
-    ctx.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    h = None
-    host_submit = 0.0
-    for _ in range(args.steps):
-        ts = time.perf_counter()
-        h = step()
-        host_submit += time.perf_counter() - ts
-    scorer.wait(h)
-    scorer.join()
-    if comm is not None:
-        torch.cuda.current_stream().wait_stream(comm)
-    torch.cuda.synchronize()
-    ctx.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+        def on_step(i):
+            if i == args.warmup:
+                barrier_sync()
+                timing["t0"] = time.perf_counter()
+
+        env = StreamExecutionEnvironment(config=cfg, dist_ctx=ctx if ctx.is_distributed else None)
+        sink = _BenchSink(ctx, gather, args.rows)
+        op_cfg = cfg
+        stream = env.add_source(_StepSource(X, args.warmup + args.steps, on_step), mode="parallel")
+        if gather:
+            # keep [n] device mirrors of every PredictionBatch for the RCCL all-gather sink
+            stream = stream.evaluate(ModelReader(path), lambda b, m: (m.scorer.submit_batch(b, keep_device=True), b),
+                                     config=op_cfg)
+        else:
+            stream = stream.quick_evaluate(ModelReader(path), config=op_cfg)
+        stream.add_sink(sink)
+        env.execute("bench")
+        sink.finish()
+        barrier_sync()
+        elapsed = time.perf_counter() - timing["t0"]
+        assert sink.rows_seen == (args.warmup + args.steps) * args.rows
+    else:
+        scorer = StreamingScorer(plan, micro_batch=args.micro_batch, depth=args.pipeline_depth, max_rows=args.rows)
+        score_h = torch.empty(args.rows, dtype=torch.float32).pin_memory()
+        valid_h = torch.empty(args.rows, dtype=torch.uint8).pin_memory()
+        for _ in range(args.warmup):
+            scorer.wait(scorer.submit(X, score_h, valid_h))
+        barrier_sync()
+        t0 = time.perf_counter()
+        h = None
+        for _ in range(args.steps):
+            h = scorer.submit(X, score_h, valid_h)
+        scorer.wait(h)
+        barrier_sync()
+        elapsed = time.perf_counter() - t0
     if ctx.is_distributed:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -159,14 +270,15 @@ def main(argv=None) -> int:
     records_per_s = N * args.rows * args.steps / elapsed
 
     # ---- device-resident kernel throughput (records already in HBM) — reported separately
-    Xd = X[: args.rows].to(device)
-    sd = torch.empty(args.rows, dtype=torch.float32, device=device)
-    vd = torch.empty(args.rows, dtype=torch.uint8, device=device)
+    n_k = min(args.rows, 1 << 22)
+    Xd = X[:n_k].to(device)
+    sd = torch.empty(n_k, dtype=torch.float32, device=device)
+    vd = torch.empty(n_k, dtype=torch.uint8, device=device)
     for _ in range(2):
         plan.launch(Xd, sd, vd)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    kiters = 5
+    kiters = 10
     e0.record()
     for _ in range(kiters):
         plan.launch(Xd, sd, vd)
@@ -174,23 +286,23 @@ def main(argv=None) -> int:
     torch.cuda.synchronize()
     kernel_ms = e0.elapsed_time(e1) / kiters
 
-    # ---- p50 latency: one micro-batch end to end (host records -> host scores), unpipelined
-    lat_scorer = StreamingScorer(plan, micro_batch=args.latency_batch, depth=1, max_rows=args.latency_batch)
-    Xl = torch.from_numpy(stream_matrix(args.latency_batch, args.features, seed=7)).pin_memory()
-    sl = torch.empty(args.latency_batch, dtype=torch.float32).pin_memory()
-    vl = torch.empty(args.latency_batch, dtype=torch.uint8).pin_memory()
+    # ---- p50 latency: one small RecordBatch through model.predict (host records -> host scores)
+    from flink_jpmml_amd.api.batch import RecordBatch
+
+    Xl = RecordBatch(torch.from_numpy(stream_matrix(args.latency_batch, args.features, seed=7)).pin_memory())
     lats = []
     for i in range(args.latency_iters + 5):
         t1 = time.perf_counter()
-        lat_scorer.wait(lat_scorer.submit(Xl, sl, vl))
+        model.predict(Xl).wait()
         if i >= 5:
             lats.append((time.perf_counter() - t1) * 1e3)
     p50 = float(np.percentile(lats, 50))
     p99 = float(np.percentile(lats, 99))
 
     if ctx.rank == 0:
+        default = args.model == "gbdt"
         out = {
-            "metric": METRIC,
+            "metric": METRIC if default else f"records/sec (whole node) on {MODELS[args.model][1]} PMML; p50 latency",
             "value": records_per_s,
             "unit": "records/s",
             "n_gpus": N,
@@ -200,34 +312,43 @@ def main(argv=None) -> int:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp32" if args.precision == "fp32" else "fp32 (fp8 e4m3 leaf values)",
-            "data": "synthetic (random-init XGBoost-style GBDT PMML, N(0,1) float records)",
+            "dtype": {"fp32": "fp32", "bf16": "bf16", "fp8": "fp32 (fp8 e4m3 leaf values)"}[args.precision],
+            "data": "synthetic (random-init PMML model, N(0,1) float records)",
             "config": {
-                "model": f"GBDT {args.trees} trees, depth {args.depth}, {args.features} float features "
-                         f"(XGBoost-style PMML, {args.objective}, {args.precision} leaves)",
+                "model": (f"GBDT {args.trees} trees, depth {args.depth}, {args.features} float features "
+                          f"(XGBoost-style PMML, regression, {args.precision} leaves)") if default else
+                         f"{MODELS[args.model][1]}: trees={args.trees} depth={args.depth} "
+                         f"features={args.features} precision={args.precision}",
+                "baseline_config": MODELS[args.model][0],
                 "global_batch": args.rows * N,
                 "seq_len": None,
                 "parallelism": f"dp{N}",
+                "api": args.api,
                 "micro_batch": args.micro_batch,
                 "pipeline_depth": args.pipeline_depth,
-                "h2d_streams": args.h2d_streams,
                 "rows_per_gpu_per_step": args.rows,
-                "allgather_sink": bool(gather_out is not None),
-                "zero_copy_host_sink": bool(scorer.direct),
+                "allgather_sink": gather,
+                "zero_copy_host_sink": bool(getattr(model.scorer, "direct", False)),
                 "numa_node": numa_node,
             },
             "p50_latency_ms": p50,
             "p99_latency_ms": p99,
             "latency_batch_rows": args.latency_batch,
-            "kernel_only_records_per_s_per_gpu": args.rows / (kernel_ms / 1e3),
-            "kernel_ms_per_1M_rows": kernel_ms * (1 << 20) / args.rows,
+            "kernel_only_records_per_s_per_gpu": n_k / (kernel_ms / 1e3),
+            "kernel_ms_per_1M_rows": kernel_ms * (1 << 20) / n_k,
+            "h2d_gbps_effective": args.rows * args.features * 4 * args.steps / elapsed / 1e9,
             "model_load_broadcast_s": load_s,
-            "host_submit_ms_per_step": host_submit / args.steps * 1e3,
+            "timed_region_s": elapsed,
             "plan": {"layout": getattr(plan, "layout", None), "depth": getattr(plan, "depth", None),
-                     "chunk_trees": getattr(plan, "chunk_trees", None)},
+                     "chunk_trees": getattr(plan, "chunk_trees", None), "kind": getattr(plan, "kind", None)},
             "check": check,
+            "metrics": {k: v for k, v in METRICS.summary()["counters"].items() if not k.startswith("model_cache")},
         }
         print(json.dumps(out), flush=True)
+        try:
+            os.unlink(path)
+        except OSError:
+            pass
     if ctx.is_distributed:
         dist.destroy_process_group()
     return 0

@@ -49,6 +49,21 @@ def is_stale() -> bool:
     return any(os.path.getmtime(p) > t for p in sources() + _headers())
 
 
+def _deps(path: str, seen=None) -> List[str]:
+    """``path`` plus every local header it includes (transitively, ``#include "x.h"``)."""
+    import re
+
+    seen = seen if seen is not None else set()
+    if path in seen or not os.path.exists(path):
+        return []
+    seen.add(path)
+    out = [path]
+    with open(path) as fh:
+        for m in re.finditer(r'^\s*#include\s+"([^"]+)"', fh.read(), re.M):
+            out += _deps(os.path.join(os.path.dirname(path), m.group(1)), seen)
+    return out
+
+
 def hipcc() -> str:
     for cand in (os.environ.get("HIPCC"), shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
         if cand and os.path.exists(cand):
@@ -67,13 +82,14 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 0, incremental
     os.makedirs(objdir, exist_ok=True)
     flags = ["-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
              "-ffp-contract=fast", "-munsafe-fp-atomics"]
-    hdr_t = max([os.path.getmtime(h) for h in _headers()] or [0.0])
     procs = []
     objs = []
-    for src in sources():
+    # slowest translation units first (they bound the wall time of the parallel build)
+    for src in sorted(sources(), key=lambda p: -os.path.getsize(p)):
         obj = os.path.join(objdir, os.path.basename(src).replace(".hip", ".o"))
         objs.append(obj)
-        if incremental and os.path.exists(obj) and os.path.getmtime(obj) > max(os.path.getmtime(src), hdr_t):
+        dep_t = max(os.path.getmtime(d) for d in _deps(src))
+        if incremental and os.path.exists(obj) and os.path.getmtime(obj) > dep_t:
             continue
         cmd = [cc, *flags, "-c", src, "-o", obj]
         if verbose:

@@ -1,614 +1,9 @@
-// Tree-ensemble scoring (PMML TreeModel / MiningModel GBDT, random forest, model chains).
-//
-// Design (MI355X / CDNA4):
-//  * rows-stationary: one 256-thread workgroup (4 wave64s) owns 256 rows, one row per lane, for
-//    the whole ensemble; the prepared feature tile lives in LDS transposed as [F][256] so that a
-//    lane's feature read `feat[f][lane]` is bank-conflict free whatever feature each lane needs;
-//  * trees stream through an LDS chunk buffer shared by the 4 waves (the ensemble is L2/MALL
-//    resident, so every workgroup re-reads it at L2 bandwidth, not HBM);
-//  * PERFECT layout for depth <= 10: every tree is padded to a perfect binary tree of depth D,
-//    nodes are 8 bytes {threshold, meta} in level order, traversal is branch-free
-//    `idx = 2*idx + 1 + (x >= T)` for exactly D steps — no divergence, one ds_read_b64 + one
-//    ds_read_b32 per level, ILP trees interleaved per lane to hide LDS latency;
-//    split operators are canonicalised on the host to "go right iff x >= T" with T rounded so the
-//    fp32 comparison is exact for fp32 inputs (see runtime/plans.py);
-//  * POINTER layout for deeper / wider ensembles: {T, meta, left, right} nodes read from global
-//    memory (L2-resident), divergent walk;
-//  * the per-row epilogue (sum / average / vote / link function / label table) is fused.
-//
-// Missing values: a per-node default-direction bit routes NaN (XGBoost / LightGBM `defaultChild`).
-// PMML `missingValueStrategy="nullPrediction"` (scikit-learn exports) and `none` with complement
-// predicates + `returnNullPrediction` make the tree's prediction null when a visited split sees a
-// missing value: flag bit NI of the perfect record's default-right words (node index NI does not
-// exist), bit 30 of the pointer node's meta. A null tree poisons the row's sum with NaN
-// (-> EmptyScore, the MiningModel `returnMissing`/`continue` rule), or marks the row invalid for
-// multi-slot accumulators.
-//
-// fp8 leaves (variant 2, BASELINE config 5): the two leaves below every last-level node are
-// stored as OCP e4m3 bytes in the upper half of that node's meta word (the lower half is the
-// feature byte offset, < 64 KiB); one global scale is folded into the epilogue. Thresholds and
-// decisions stay fp32 — only the leaf values are quantised. The record shrinks by the whole leaf
-// array (768 -> 512 B at depth 6) and the last level needs no separate leaf read.
-#include "epilogue.h"
+// Tree-ensemble scoring: POINTER / GENERAL layouts, split reduction and the C entry points.
+// The PERFECT-layout kernels live in tree_common.h (one translation unit per depth: tree_d<D>.hip).
+#include "tree_common.h"
 
+namespace pmml_tree {
 namespace {
-
-constexpr int TB = 256;   // rows per workgroup (= threads)
-
-struct TreeArgs {
-  const float* X;
-  int n_rows, n_feat, ldx;
-  int pad0;
-  const FieldPrep* prep;        // nullable
-  const uint8_t* row_valid_in;  // nullable
-  const uint32_t* blob;         // perfect: [n_trees][rec_words]; pointer: nodes uint4[]
-  const int* roots;             // pointer layout: per-tree root code (>=0 node, <0 ~leaf)
-  const float* leaves;          // pointer layout: [n_leaves][P]
-  const int* tree_slot;         // general accumulation: slot per tree
-  int n_trees, rec_words, chunk_trees, P;
-  int C, trees_per_split, general, variant;  // variant & 3: 1 wide perfect kernel, 2 wide + fp8 leaves;
-                                             // | VAR_NAN_FAST | VAR_NAN_PLANES (wide kernel only)
-  Epilogue epi;
-  float* score;
-  uint8_t* valid;
-  float* probs;
-  float* partial;               // split mode: [splits][C+1][n_rows]
-  const uint32_t* blob_nan;     // wide kernel, nullable: the records re-pointed at the NaN plane
-  int chunk_trees_nan, pad1;    // (tiles with missing values; own chunk size, LDS holds 2 planes)
-};
-constexpr int VAR_NAN_FAST = 4;    // wide kernel: take the fast path even on tiles with missing values
-constexpr int VAR_NAN_PLANES = 8;  // ... via blob_nan + a second feature plane (NaN -> +inf)
-
-
-__device__ __forceinline__ void finish_row(const TreeArgs& a, float acc0, const float* accl, int split,
-                                           bool general, int row, bool row_ok) {
-  if (row >= a.n_rows) return;
-  if (a.partial) {
-    const size_t stride = (size_t)a.n_rows;
-    float* base = a.partial + (size_t)split * (a.C + 1) * stride;
-    if (general) {
-      for (int c = 0; c < a.C; ++c) base[c * stride + row] = accl[c * TB + threadIdx.x];
-    } else {
-      base[row] = acc0;
-    }
-    base[a.C * stride + row] = row_ok ? 0.f : 1.f;
-    return;
-  }
-  if (general) {
-    apply_epilogue(a.epi, [&](int c) { return accl[c * TB + threadIdx.x]; }, row_ok, row, a.n_rows, a.score,
-                   a.valid, a.probs);
-  } else {
-    apply_epilogue(a.epi, [&](int) { return acc0; }, row_ok, row, a.n_rows, a.score, a.valid, a.probs);
-  }
-}
-
-// Tree-level "null prediction on a missing value" flag of a perfect record (bit NI of the
-// default-right words, which start at word dr_off).
-template <int DEPTH>
-__device__ __forceinline__ bool null_flag(const char* rec, int dr_off) {
-  constexpr int NI = (1 << DEPTH) - 1;
-  return ((reinterpret_cast<const uint32_t*>(rec)[dr_off + (NI >> 5)] >> (NI & 31)) & 1u) != 0u;
-}
-
-// Next-chunk prefetch through registers: the global loads are issued before the traversal of the
-// current chunk and written to the other LDS buffer after it, so L2 latency hides under compute.
-// (An LDS-DMA variant was slower: hipcc drains in-flight LDS-DMA before the first ds_read it cannot
-// prove disjoint from the DMA target, which serialised the copy with the traversal.)
-constexpr int PREFETCH_Q = 8;  // uint4 per lane -> up to 32 KiB per chunk
-
-// Loads are unconditional (index clamped into the valid range) so the values stay in VGPRs; only
-// the LDS store is predicated. Written as macros over named registers: an array passed between
-// helpers was demoted to scratch by hipcc.
-#define PF_DECL uint4 pf0, pf1, pf2, pf3, pf4, pf5, pf6, pf7;
-#define PF_LOAD1(R, I, S4, LAST) R = (S4)[min((int)threadIdx.x + (I) * TB, (LAST))];
-#define PF_LOAD(SRC, N16)                                                              \
-  {                                                                                    \
-    const uint4* s4_ = reinterpret_cast<const uint4*>(SRC);                            \
-    const int last_ = (N16) > 0 ? (N16) - 1 : 0;                                      \
-    PF_LOAD1(pf0, 0, s4_, last_) PF_LOAD1(pf1, 1, s4_, last_) PF_LOAD1(pf2, 2, s4_, last_) \
-    PF_LOAD1(pf3, 3, s4_, last_) PF_LOAD1(pf4, 4, s4_, last_) PF_LOAD1(pf5, 5, s4_, last_) \
-    PF_LOAD1(pf6, 6, s4_, last_) PF_LOAD1(pf7, 7, s4_, last_)                          \
-  }
-#define PF_STORE1(R, I, D4, N)                      \
-  {                                                  \
-    const int idx_ = (int)threadIdx.x + (I) * TB;   \
-    if (idx_ < (N)) (D4)[idx_] = R;                  \
-  }
-#define PF_STORE(DST, N16)                                                              \
-  {                                                                                     \
-    uint4* d4_ = reinterpret_cast<uint4*>(DST);                                         \
-    PF_STORE1(pf0, 0, d4_, N16) PF_STORE1(pf1, 1, d4_, N16) PF_STORE1(pf2, 2, d4_, N16) \
-    PF_STORE1(pf3, 3, d4_, N16) PF_STORE1(pf4, 4, d4_, N16) PF_STORE1(pf5, 5, d4_, N16) \
-    PF_STORE1(pf6, 6, d4_, N16) PF_STORE1(pf7, 7, d4_, N16)                             \
-  }
-
-// Traverse `nt` perfect trees of one LDS chunk for this lane's row.
-// Heap index j (root = 1): node j at byte (j-1)*8, children 2j / 2j+1, leaf j - 2^D.
-// Fast path (MISSING=false): one ds_read_b64 node, one ds_read_b32 feature, one v_cmp, index update.
-template <int DEPTH, bool GENERAL, bool MISSING, int ILP>
-__device__ __forceinline__ void traverse_chunk(const TreeArgs& a, const uint32_t* buf, int nt, int t0,
-                                               const char* feat_lane, float& acc, float* accl, bool& poisoned) {
-  constexpr int NI = (1 << DEPTH) - 1;
-  constexpr int NL = 1 << DEPTH;
-  const int rw = a.rec_words;
-  const int dr_off = 2 * NI + NL * a.P;  // words
-  const int tid = threadIdx.x;
-  int k = 0;
-  for (; k + ILP <= nt; k += ILP) {
-    uint32_t j[ILP];
-    uint32_t pz[ILP];
-    const char* base[ILP];
-#pragma unroll
-    for (int i = 0; i < ILP; ++i) {
-      j[i] = 1u;
-      pz[i] = 0u;
-      base[i] = reinterpret_cast<const char*>(buf + (k + i) * rw);
-    }
-#pragma unroll
-    for (int d = 0; d < DEPTH; ++d) {
-#pragma unroll
-      for (int i = 0; i < ILP; ++i) {
-        const uint2 nd = *reinterpret_cast<const uint2*>(base[i] - 8 + (j[i] << 3));
-        const float x = *reinterpret_cast<const float*>(feat_lane + nd.y);
-        uint32_t right = (x >= __uint_as_float(nd.x)) ? 1u : 0u;
-        if (MISSING) {  // branch-free: NaN takes the node's default direction bit
-          const uint32_t n = j[i] - 1u;
-          const uint32_t w = reinterpret_cast<const uint32_t*>(base[i])[dr_off + (n >> 5)];
-          const uint32_t isn = (x != x) ? 1u : 0u;
-          right |= isn & (w >> (n & 31u));
-          pz[i] |= isn;
-        }
-        j[i] = j[i] + j[i] + right;
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < ILP; ++i) {
-      const float* lv = reinterpret_cast<const float*>(base[i] + NI * 8) - NL * a.P;
-      const bool pzn = MISSING && pz[i] && null_flag<DEPTH>(base[i], dr_off);
-      if (GENERAL) {
-        poisoned = poisoned || pzn;
-        const int slot = a.tree_slot[t0 + k + i];
-        for (int p = 0; p < a.P; ++p) accl[(slot + p) * TB + tid] += lv[j[i] * a.P + p];
-      } else {
-        acc += pzn ? __builtin_nanf("") : lv[j[i]];
-      }
-    }
-  }
-  for (; k < nt; ++k) {
-    uint32_t j = 1u, pz = 0u;
-    const char* base = reinterpret_cast<const char*>(buf + k * rw);
-#pragma unroll
-    for (int d = 0; d < DEPTH; ++d) {
-      const uint2 nd = *reinterpret_cast<const uint2*>(base - 8 + (j << 3));
-      const float x = *reinterpret_cast<const float*>(feat_lane + nd.y);
-      uint32_t right = (x >= __uint_as_float(nd.x)) ? 1u : 0u;
-      if (MISSING) {
-        const uint32_t n = j - 1u;
-        const uint32_t w = reinterpret_cast<const uint32_t*>(base)[dr_off + (n >> 5)];
-        const uint32_t isn = (x != x) ? 1u : 0u;
-        right |= isn & (w >> (n & 31u));
-        pz |= isn;
-      }
-      j = j + j + right;
-    }
-    const float* lv = reinterpret_cast<const float*>(base + NI * 8) - NL * a.P;
-    const bool pzn = MISSING && pz && null_flag<DEPTH>(base, dr_off);
-    if (GENERAL) {
-      poisoned = poisoned || pzn;
-      const int slot = a.tree_slot[t0 + k];
-      for (int p = 0; p < a.P; ++p) accl[(slot + p) * TB + tid] += lv[j * a.P + p];
-    } else {
-      acc += pzn ? __builtin_nanf("") : lv[j];
-    }
-  }
-}
-
-template <int DEPTH, bool GENERAL, int ILP>
-__global__ __launch_bounds__(TB, 2) void tree_perfect_kernel(TreeArgs a) {
-  extern __shared__ __align__(16) uint32_t smem[];
-  const int rw = a.rec_words;
-  const int chunk_words = a.chunk_trees * rw;
-  float* feat = reinterpret_cast<float*>(smem);
-  uint32_t* tbuf0 = smem + a.n_feat * TB;
-  uint32_t* tbuf1 = tbuf0 + chunk_words;
-  int* bad = reinterpret_cast<int*>(tbuf1 + chunk_words);
-  int* any_missing = bad + TB;
-  float* accl = reinterpret_cast<float*>(bad + TB + 4);
-
-  const int tid = threadIdx.x;
-  const int row0 = blockIdx.x * TB;
-  const int split = blockIdx.y;
-  const int tb = split * a.trees_per_split;
-  const int te = min(a.n_trees, tb + a.trees_per_split);
-
-  // chunk 0: issue its loads before the row staging so the two overlap
-  PF_DECL
-  int n16 = (tb < te) ? (min(a.chunk_trees, te - tb) * rw) >> 2 : 0;
-  PF_LOAD(n16 > 0 ? a.blob + (size_t)tb * rw : a.blob, n16)
-
-  // stage rows [F][TB] with field preparation; rows past the end are zero (never "missing")
-  if (tid == 0) *any_missing = 0;
-  bad[tid] = 0;
-  __syncthreads();
-  {
-    const int F = a.n_feat;
-    const int total = TB * F;
-    bool miss = false;
-    for (int e = tid; e < total; e += TB) {
-      const int r = e / F;
-      const int f = e - r * F;
-      const int row = row0 + r;
-      float x = 0.f;
-      bool b = false;
-      if (row < a.n_rows) {
-        x = a.X[(size_t)row * a.ldx + f];
-        if (a.prep) x = prep_value(x, a.prep[f], &b);
-        miss = miss || (x != x);
-      }
-      feat[f * TB + r] = x;
-      if (b) bad[r] = 1;
-    }
-    if (__any(miss) && (tid & 63) == 0) *any_missing = 1;
-  }
-  PF_STORE(tbuf0, n16)
-  __syncthreads();
-
-  const int row = row0 + tid;
-  bool row_ok = bad[tid] == 0;
-  if (a.row_valid_in && row < a.n_rows) row_ok = row_ok && a.row_valid_in[row];
-  const bool missing = *any_missing != 0;
-  if (GENERAL) {
-    for (int c = 0; c < a.C; ++c) accl[c * TB + tid] = 0.f;
-  }
-  float acc = 0.f;
-  bool poisoned = false;
-  const char* feat_lane = reinterpret_cast<const char*>(feat + tid);
-
-  int c = 0;
-  for (int t0 = tb; t0 < te; t0 += a.chunk_trees, ++c) {
-    const int nt = min(a.chunk_trees, te - t0);
-    const uint32_t* cur = (c & 1) ? tbuf1 : tbuf0;
-    uint32_t* nxt = (c & 1) ? tbuf0 : tbuf1;
-    const int t1 = t0 + a.chunk_trees;
-    n16 = (t1 < te) ? (min(a.chunk_trees, te - t1) * rw) >> 2 : 0;
-    PF_LOAD(n16 > 0 ? a.blob + (size_t)t1 * rw : a.blob, n16)  // never form an OOB address
-    if (missing) {
-      traverse_chunk<DEPTH, GENERAL, true, ILP>(a, cur, nt, t0, feat_lane, acc, accl, poisoned);
-    } else {
-      traverse_chunk<DEPTH, GENERAL, false, ILP>(a, cur, nt, t0, feat_lane, acc, accl, poisoned);
-    }
-    // `nxt` was last read in the previous iteration, before that iteration's barrier
-    PF_STORE(nxt, n16)
-    __syncthreads();
-  }
-  finish_row(a, acc, accl, split, GENERAL, row, row_ok && !poisoned);
-}
-
-// ------------------------------------------------------------------------------------------
-// v3: wide workgroup, tree-group parallel. 256 rows x G tree groups = 256*G threads (G=4: 16
-// waves, one workgroup per CU). Half-wave hw = 2*wave + (lane >= 32) owns row set hw % 8 (32
-// rows) and tree group hw / 8, so each 32-lane LDS access group reads 32 distinct rows (feature
-// reads conflict free) and both halves of a wave walk the same trees. Group g takes trees
-// k ≡ g (mod G) of every chunk; the G partial sums of a row are added in fixed order g = 0..G-1
-// (deterministic). Twice the resident waves of the v2 layout at the same LDS footprint: the
-// traversal is latency bound (SQ_WAIT_ANY ~49% of wave cycles in v2), so occupancy is the lever.
-#define PF4_DECL uint4 pq0, pq1, pq2, pq3;
-#define PF4_LOAD(SRC, N16, T)                                                          \
-  {                                                                                    \
-    const uint4* s4_ = reinterpret_cast<const uint4*>(SRC);                            \
-    const int last_ = (N16) > 0 ? (N16) - 1 : 0;                                      \
-    pq0 = s4_[min((int)threadIdx.x + 0 * (T), last_)];                                 \
-    pq1 = s4_[min((int)threadIdx.x + 1 * (T), last_)];                                 \
-    pq2 = s4_[min((int)threadIdx.x + 2 * (T), last_)];                                 \
-    pq3 = s4_[min((int)threadIdx.x + 3 * (T), last_)];                                 \
-  }
-#define PF4_STORE(DST, N16, T)                                                         \
-  {                                                                                    \
-    uint4* d4_ = reinterpret_cast<uint4*>(DST);                                        \
-    const int i0_ = (int)threadIdx.x;                                                  \
-    if (i0_ < (N16)) d4_[i0_] = pq0;                                                   \
-    if (i0_ + (T) < (N16)) d4_[i0_ + (T)] = pq1;                                       \
-    if (i0_ + 2 * (T) < (N16)) d4_[i0_ + 2 * (T)] = pq2;                               \
-    if (i0_ + 3 * (T) < (N16)) d4_[i0_ + 3 * (T)] = pq3;                               \
-  }
-
-__host__ __device__ constexpr int perfect_rec_words(int depth, int P) {
-  return ((2 * ((1 << depth) - 1) + (1 << depth) * P + ((1 << depth) - 1 + 31) / 32) + 3) & ~3;
-}
-// fp8-leaf record: nodes + default-right words only (leaf pairs live in the last-level metas)
-__host__ __device__ constexpr int perfect_rec_words8(int depth) {
-  return ((2 * ((1 << depth) - 1) + ((1 << depth) - 1 + 31) / 32) + 3) & ~3;
-}
-
-// OCP e4m3 leaf pair in bits [31:16] of a last-level node's meta -> (left, right) as fp32
-__device__ __forceinline__ float leaf8_select(uint32_t meta, bool right) {
-  const auto pr = __builtin_amdgcn_cvt_pk_f32_fp8((int)meta, true);
-  return right ? pr[1] : pr[0];
-}
-
-template <int DEPTH, bool MISSING, int ILP, int G, bool LEAF8>
-__device__ __forceinline__ float traverse_chunk_g(const TreeArgs& a, const uint32_t* buf, int nt, int g,
-                                                  const char* feat_lane, float acc) {
-  constexpr int NI = (1 << DEPTH) - 1;
-  constexpr int NL = 1 << DEPTH;
-  const int rw = a.rec_words;
-  const int dr_off = LEAF8 ? 2 * NI : 2 * NI + NL;
-  // my trees: k = g + G*m, m = 0..mt-1
-  const int mt = (nt - g + G - 1) / G;
-  int m = 0;
-  for (; m + ILP <= mt; m += ILP) {
-    uint32_t j[ILP], pz[ILP];
-    float lf[ILP];
-    const char* base[ILP];
-#pragma unroll
-    for (int i = 0; i < ILP; ++i) {
-      j[i] = 1u;
-      pz[i] = 0u;
-      lf[i] = 0.f;
-      base[i] = reinterpret_cast<const char*>(buf + (g + G * (m + i)) * rw);
-    }
-#pragma unroll
-    for (int d = 0; d < DEPTH; ++d) {
-#pragma unroll
-      for (int i = 0; i < ILP; ++i) {
-        const uint2 nd = *reinterpret_cast<const uint2*>(base[i] - 8 + (j[i] << 3));
-        const uint32_t fo = (LEAF8 && d == DEPTH - 1) ? (nd.y & 0xFFFFu) : nd.y;
-        const float x = *reinterpret_cast<const float*>(feat_lane + fo);
-        uint32_t right = (x >= __uint_as_float(nd.x)) ? 1u : 0u;
-        if (MISSING) {
-          const uint32_t n = j[i] - 1u;
-          const uint32_t w = reinterpret_cast<const uint32_t*>(base[i])[dr_off + (n >> 5)];
-          const uint32_t isn = (x != x) ? 1u : 0u;
-          right |= isn & (w >> (n & 31u));
-          pz[i] |= isn;
-        }
-        if (LEAF8 && d == DEPTH - 1) {
-          lf[i] = leaf8_select(nd.y, right != 0u);
-        } else {
-          j[i] = j[i] + j[i] + right;
-        }
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < ILP; ++i) {
-      float v = LEAF8 ? lf[i] : (reinterpret_cast<const float*>(base[i] + NI * 8) - NL)[j[i]];
-      if (MISSING && pz[i] && null_flag<DEPTH>(base[i], dr_off)) v = __builtin_nanf("");
-      acc += v;
-    }
-  }
-  for (; m < mt; ++m) {
-    uint32_t j = 1u, pz = 0u;
-    float lf = 0.f;
-    const char* base = reinterpret_cast<const char*>(buf + (g + G * m) * rw);
-#pragma unroll
-    for (int d = 0; d < DEPTH; ++d) {
-      const uint2 nd = *reinterpret_cast<const uint2*>(base - 8 + (j << 3));
-      const uint32_t fo = (LEAF8 && d == DEPTH - 1) ? (nd.y & 0xFFFFu) : nd.y;
-      const float x = *reinterpret_cast<const float*>(feat_lane + fo);
-      uint32_t right = (x >= __uint_as_float(nd.x)) ? 1u : 0u;
-      if (MISSING) {
-        const uint32_t n = j - 1u;
-        const uint32_t w = reinterpret_cast<const uint32_t*>(base)[dr_off + (n >> 5)];
-        const uint32_t isn = (x != x) ? 1u : 0u;
-        right |= isn & (w >> (n & 31u));
-        pz |= isn;
-      }
-      if (LEAF8 && d == DEPTH - 1) {
-        lf = leaf8_select(nd.y, right != 0u);
-      } else {
-        j = j + j + right;
-      }
-    }
-    float v = LEAF8 ? lf : (reinterpret_cast<const float*>(base + NI * 8) - NL)[j];
-    if (MISSING && pz && null_flag<DEPTH>(base, dr_off)) v = __builtin_nanf("");
-    acc += v;
-  }
-  return acc;
-}
-
-// Fast path of the wide kernel (tile without missing values), written against explicit LDS byte
-// addresses so the per-level work is exactly: node ds_read_b64, feature address add, feature
-// ds_read_b32, v_cmp, v_cndmask, v_lshl_add — 4 VALU per level (the plain heap-index form
-// compiled to ~7.5 as hipcc re-expanded `j = 2j + r` into shifted bit sums).
-//  * u = LDS address of the current node of tree i minus i*TS (TS = compile-time tree stride of a
-//    tree group, folded into the ds_read immediate offset); children: u' = 2u + (8 - b0) + 8r.
-//  * last level, fp32 leaves: the two leaves under a node are adjacent, so the leaf PAIR (one
-//    conflict-free ds_read_b64 at u + C, C folded into the offset) is fetched together with the
-//    feature and the final compare only selects between them — one dependent LDS round trip less
-//    per tree, and no 2-way bank conflicts of scattered ds_read_b32 leaf reads;
-//  * last level, fp8 leaves: the pair is already in the node's meta word (no leaf read at all).
-// `__asm__("" : "+v"(...))` pins values in VGPRs so the compiler cannot re-derive them.
-typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
-typedef __attribute__((address_space(3))) const u32x2_t lds_u2_t;
-typedef __attribute__((address_space(3))) const float lds_f_t;
-__device__ __forceinline__ uint32_t lds_addr(const void* p) {
-  return (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const char*)p;
-}
-__device__ __forceinline__ uint2 lds_ld2(uint32_t a) {
-  const u32x2_t v = *(lds_u2_t*)(uintptr_t)a;
-  return make_uint2(v.x, v.y);
-}
-__device__ __forceinline__ float lds_ldf(uint32_t a) { return *(lds_f_t*)(uintptr_t)a; }
-
-// N trees of group g starting at its m-th tree, N independent walks interleaved (ILP).
-template <int DEPTH, int N, int G, bool LEAF8>
-__device__ __forceinline__ float fast_batch(uint32_t lds0, int g, int m, uint32_t feat_lane, float acc) {
-  constexpr int NI = (1 << DEPTH) - 1;
-  constexpr int NL = 1 << DEPTH;
-  constexpr uint32_t RB = 4u * (LEAF8 ? perfect_rec_words8(DEPTH) : perfect_rec_words(DEPTH, 1));  // record bytes
-  constexpr uint32_t TS = G * RB;                            // tree stride within a group
-  constexpr uint32_t C = 8u + 8u * NI - 4u * NL;             // last-level node -> its leaf pair
-  const uint32_t b0 = lds0 + (uint32_t)(g + G * m) * RB;
-  uint32_t k0 = 8u - b0, k1 = 16u - b0;
-  __asm__("" : "+v"(k0), "+v"(k1));
-  uint32_t u[N];
-#pragma unroll
-  for (int i = 0; i < N; ++i) {
-    u[i] = b0;
-    __asm__ volatile("" : "+v"(u[i]));  // separate root reads: ds_read2_b64 pairing costs 8 LDS
-                                        // cycles vs 2 x 2 for two ds_read_b64
-  }
-#pragma unroll
-  for (int d = 0; d + 1 < DEPTH; ++d) {
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-      const uint2 nd = lds_ld2(u[i] + i * TS);
-      const float x = lds_ldf(feat_lane + nd.y);
-      u[i] = 2u * u[i] + ((x >= __uint_as_float(nd.x)) ? k1 : k0);
-      __asm__("" : "+v"(u[i]));
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < N; ++i) {
-    if (LEAF8) {
-      const uint2 nd = lds_ld2(u[i] + i * TS);
-      const float x = lds_ldf(feat_lane + (nd.y & 0xFFFFu));
-      acc += leaf8_select(nd.y, x >= __uint_as_float(nd.x));
-    } else {
-      uint32_t ul = u[i] + C;
-      __asm__ volatile("" : "+v"(ul));  // keep the pair read out of a ds_read2_b64 with the node
-      const uint2 nd = lds_ld2(u[i] + i * TS);
-      const uint2 lv = lds_ld2(ul + i * TS);
-      const float x = lds_ldf(feat_lane + nd.y);
-      acc += (x >= __uint_as_float(nd.x)) ? __uint_as_float(lv.y) : __uint_as_float(lv.x);
-    }
-  }
-  return acc;
-}
-
-// The group's trees in ILP-wide batches; the remainder in 4/2/1-wide batches (a plain serial
-// tail is latency bound: one dependent LDS round trip per level and tree).
-template <int DEPTH, int ILP, int G, bool LEAF8>
-__device__ __forceinline__ float traverse_fast_g(const uint32_t* buf, int nt, int g, uint32_t feat_lane,
-                                                 float acc) {
-  const uint32_t lds0 = lds_addr(buf);
-  const int mt = (nt - g + G - 1) / G;
-  int m = 0;
-  for (; m + ILP <= mt; m += ILP) acc = fast_batch<DEPTH, ILP, G, LEAF8>(lds0, g, m, feat_lane, acc);
-  if (ILP > 4 && m + 4 <= mt) {
-    acc = fast_batch<DEPTH, 4, G, LEAF8>(lds0, g, m, feat_lane, acc);
-    m += 4;
-  }
-  if (m + 2 <= mt) {
-    acc = fast_batch<DEPTH, 2, G, LEAF8>(lds0, g, m, feat_lane, acc);
-    m += 2;
-  }
-  if (m < mt) acc = fast_batch<DEPTH, 1, G, LEAF8>(lds0, g, m, feat_lane, acc);
-  return acc;
-}
-
-template <int DEPTH, int ILP, int G, bool LEAF8>
-__global__ __launch_bounds__(TB * G, 1) void tree_perfect_wide_kernel(TreeArgs a) {
-  constexpr int T = TB * G;
-  extern __shared__ __align__(16) uint32_t smem[];
-  const int rw = a.rec_words;
-  // LDS: [bad TB][flag 4][part G x TB][feature plane(s)][two chunk buffers]. A tile with missing
-  // values and a NaN blob gets two planes (the second NaN -> +inf) and that blob's chunk size;
-  // any other tile one plane and the main blob — the layout is chosen per workgroup.
-  int* bad = reinterpret_cast<int*>(smem);
-  int* any_missing = bad + TB;
-  float* part = reinterpret_cast<float*>(bad + TB + 4);  // [G][TB]
-  float* feat = part + G * TB;
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int hw = (tid >> 6) * 2 + (lane >> 5);
-  const int r_local = 32 * (hw & 7) + (lane & 31);
-  const int g = hw >> 3;
-  const int row0 = blockIdx.x * TB;
-  const int split = blockIdx.y;
-  const int tb = split * a.trees_per_split;
-  const int te = min(a.n_trees, tb + a.trees_per_split);
-
-  PF4_DECL
-  int n16 = (tb < te) ? (min(a.chunk_trees, te - tb) * rw) >> 2 : 0;
-  PF4_LOAD(n16 > 0 ? a.blob + (size_t)tb * rw : a.blob, n16, T)  // speculative: main blob
-
-  if (tid == 0) *any_missing = 0;
-  if (tid < TB) bad[tid] = 0;
-  __syncthreads();
-  {
-    const int F = a.n_feat;
-    const int total = TB * F;
-    bool miss = false;
-    for (int e = tid; e < total; e += T) {
-      const int r = e / F;
-      const int f = e - r * F;
-      const int row = row0 + r;
-      float x = 0.f;
-      bool b = false;
-      if (row < a.n_rows) {
-        x = a.X[(size_t)row * a.ldx + f];
-        if (a.prep) x = prep_value(x, a.prep[f], &b);
-        miss = miss || (x != x);
-      }
-      feat[f * TB + r] = x;
-      if (b) bad[r] = 1;
-    }
-    if (__any(miss) && lane == 0) *any_missing = 1;
-  }
-  __syncthreads();
-  const bool has_missing = *any_missing != 0;
-  const bool use_nan = has_missing && a.blob_nan != nullptr;
-  const uint32_t* blob = use_nan ? a.blob_nan : a.blob;
-  const int chunk = use_nan ? a.chunk_trees_nan : a.chunk_trees;
-  uint32_t* tbuf0 = reinterpret_cast<uint32_t*>(feat + (use_nan ? 2 : 1) * a.n_feat * TB);
-  uint32_t* tbuf1 = tbuf0 + chunk * rw;
-  if (use_nan) {
-    const int total = TB * a.n_feat;
-    for (int e = tid; e < total; e += T) {  // NaN-goes-right plane
-      const float x = feat[e];
-      feat[total + e] = (x != x) ? __builtin_inff() : x;
-    }
-    n16 = (tb < te) ? (min(chunk, te - tb) * rw) >> 2 : 0;
-    PF4_LOAD(n16 > 0 ? blob + (size_t)tb * rw : blob, n16, T)
-  }
-  PF4_STORE(tbuf0, n16, T)
-  __syncthreads();
-
-  // VAR_NAN_FAST: missing values need no per-node work — either no node sends NaN right (a NaN
-  // compare is false: left), or the node's feature offset points into the NaN -> +inf plane
-  const bool missing = has_missing && (a.variant & VAR_NAN_FAST) == 0;
-  float acc = 0.f;
-  const char* feat_lane = reinterpret_cast<const char*>(feat + r_local);
-  int c = 0;
-  for (int t0 = tb; t0 < te; t0 += chunk, ++c) {
-    const int nt = min(chunk, te - t0);
-    const uint32_t* cur = (c & 1) ? tbuf1 : tbuf0;
-    uint32_t* nxt = (c & 1) ? tbuf0 : tbuf1;
-    const int t1 = t0 + chunk;
-    n16 = (t1 < te) ? (min(chunk, te - t1) * rw) >> 2 : 0;
-    PF4_LOAD(n16 > 0 ? blob + (size_t)t1 * rw : blob, n16, T)
-    if (missing) {
-      acc = traverse_chunk_g<DEPTH, true, ILP, G, LEAF8>(a, cur, nt, g, feat_lane, acc);
-    } else {
-      acc = traverse_fast_g<DEPTH, ILP, G, LEAF8>(cur, nt, g, lds_addr(feat + r_local), acc);
-    }
-    PF4_STORE(nxt, n16, T)
-    __syncthreads();
-  }
-  part[g * TB + r_local] = acc;
-  __syncthreads();
-  if (g == 0) {
-    float sum = part[r_local];
-#pragma unroll
-    for (int q = 1; q < G; ++q) sum += part[q * TB + r_local];
-    const int row = row0 + r_local;
-    bool row_ok = bad[r_local] == 0;
-    if (a.row_valid_in && row < a.n_rows) row_ok = row_ok && a.row_valid_in[row];
-    if (row < a.n_rows) {
-      if (a.partial) {
-        const size_t stride = (size_t)a.n_rows;
-        float* pbase = a.partial + (size_t)split * 2 * stride;
-        pbase[row] = sum;
-        pbase[stride + row] = row_ok ? 0.f : 1.f;
-      } else {
-        apply_epilogue(a.epi, [&](int) { return sum; }, row_ok, row, a.n_rows, a.score, a.valid, a.probs);
-      }
-    }
-  }
-}
-
 // Pointer layout: nodes uint4 {T bits, meta, left, right}; child < 0 => leaf ~child.
 // meta: feature byte offset (or index when features stay in global memory) | bit 30 null-on-
 // missing | bit 31 default right.
@@ -878,58 +273,10 @@ __global__ __launch_bounds__(TB, 2) void tree_general_kernel(GenTreeArgs ga) {
   finish_row(a, acc, accl, 0, GENERAL, row, row_ok && !poisoned);
 }
 
-template <typename K>
-int prepare_launch(K kernel, size_t lds) {
-  if (lds > 65536) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return (int)e;
-  }
-  return 0;
-}
-
-constexpr int WIDE_G = 4;
-
-template <int D>
-int launch_perfect(hipStream_t st, const TreeArgs& a, dim3 grid, size_t lds) {
-  int err = 0;
-  const int base = a.variant & 3;
-  if (!a.general && (base == 1 || base == 2)) {
-    const bool leaf8 = base == 2;
-    (void)lds;
-    const size_t head = (size_t)(TB + 4) * 4 + (size_t)WIDE_G * TB * 4;
-    const size_t plane = (size_t)a.n_feat * TB * 4;
-    size_t lds_w = head + plane + 2 * (size_t)a.chunk_trees * a.rec_words * 4;
-    if ((size_t)a.chunk_trees * a.rec_words > (size_t)TB * WIDE_G * 4 * 4) return -9;
-    if (a.blob_nan) {
-      if (a.chunk_trees_nan < 1 || (size_t)a.chunk_trees_nan * a.rec_words > (size_t)TB * WIDE_G * 4 * 4) return -9;
-      lds_w = max(lds_w, head + 2 * plane + 2 * (size_t)a.chunk_trees_nan * a.rec_words * 4);
-    }
-    if (lds_w > 160 * 1024) return -5;
-    if (a.P != 1 || a.rec_words != (leaf8 ? perfect_rec_words8(D) : perfect_rec_words(D, 1))) return -10;
-    if (leaf8) {
-      err = prepare_launch(tree_perfect_wide_kernel<D, 8, WIDE_G, true>, lds_w);
-      if (!err)
-        hipLaunchKernelGGL((tree_perfect_wide_kernel<D, 8, WIDE_G, true>), grid, dim3(TB * WIDE_G), lds_w, st, a);
-    } else {
-      err = prepare_launch(tree_perfect_wide_kernel<D, 8, WIDE_G, false>, lds_w);
-      if (!err)
-        hipLaunchKernelGGL((tree_perfect_wide_kernel<D, 8, WIDE_G, false>), grid, dim3(TB * WIDE_G), lds_w, st, a);
-    }
-    return err;
-  }
-  if (base == 2 || (a.variant & ~3)) return -10;  // fp8 leaves / NaN planes: wide kernel only
-  if (a.general) {
-    err = prepare_launch(tree_perfect_kernel<D, true, 4>, lds);
-    if (!err) hipLaunchKernelGGL((tree_perfect_kernel<D, true, 4>), grid, dim3(TB), lds, st, a);
-  } else {
-    err = prepare_launch(tree_perfect_kernel<D, false, 8>, lds);
-    if (!err) hipLaunchKernelGGL((tree_perfect_kernel<D, false, 8>), grid, dim3(TB), lds, st, a);
-  }
-  return err;
-}
-
 }  // namespace
+}  // namespace pmml_tree
+
+using namespace pmml_tree;
 
 PMML_API int pmml_tree_args_size() { return (int)sizeof(TreeArgs); }
 PMML_API int pmml_tree_rows_per_block() { return TB; }
@@ -954,16 +301,16 @@ PMML_API int pmml_tree_launch(hipStream_t stream, const TreeArgs* args, int layo
     const size_t lds = (size_t)a.n_feat * TB * 4 + 2 * (size_t)a.chunk_trees * a.rec_words * 4 + (TB + 4) * 4 + acc_lds;
     if (lds > 160 * 1024) return -5;
     switch (depth) {
-      case 1: err = launch_perfect<1>(stream, a, grid, lds); break;
-      case 2: err = launch_perfect<2>(stream, a, grid, lds); break;
-      case 3: err = launch_perfect<3>(stream, a, grid, lds); break;
-      case 4: err = launch_perfect<4>(stream, a, grid, lds); break;
-      case 5: err = launch_perfect<5>(stream, a, grid, lds); break;
-      case 6: err = launch_perfect<6>(stream, a, grid, lds); break;
-      case 7: err = launch_perfect<7>(stream, a, grid, lds); break;
-      case 8: err = launch_perfect<8>(stream, a, grid, lds); break;
-      case 9: err = launch_perfect<9>(stream, a, grid, lds); break;
-      case 10: err = launch_perfect<10>(stream, a, grid, lds); break;
+      case 1: err = launch_perfect_d1(stream, a, grid, lds); break;
+      case 2: err = launch_perfect_d2(stream, a, grid, lds); break;
+      case 3: err = launch_perfect_d3(stream, a, grid, lds); break;
+      case 4: err = launch_perfect_d4(stream, a, grid, lds); break;
+      case 5: err = launch_perfect_d5(stream, a, grid, lds); break;
+      case 6: err = launch_perfect_d6(stream, a, grid, lds); break;
+      case 7: err = launch_perfect_d7(stream, a, grid, lds); break;
+      case 8: err = launch_perfect_d8(stream, a, grid, lds); break;
+      case 9: err = launch_perfect_d9(stream, a, grid, lds); break;
+      case 10: err = launch_perfect_d10(stream, a, grid, lds); break;
       default: return -6;
     }
   } else {

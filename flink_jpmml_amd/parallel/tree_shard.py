@@ -29,7 +29,7 @@ import torch
 import torch.distributed as dist
 
 from ..models.tree import OP_GE, OP_GT, OP_LE, OP_LT
-from ..runtime.plans import EPI_AFFINE, EPI_LOGISTIC2, ensemble_spec, shard_spec
+from ..runtime.plans import EPI_AFFINE, EPI_LOGISTIC2, NotLowerable, _label_table, ensemble_spec, shard_spec
 from .dist import DistContext
 
 
@@ -64,7 +64,8 @@ def finish_epilogue(raw: torch.Tensor, valid: torch.Tensor, epi: dict, labels=No
         label = (y < epi.get("thr", 0.5)).long()  # p0 >= thr -> class 0
         ok = ok & ~torch.isnan(y)
         if labels is not None:
-            tab = torch.tensor([float(x) for x in labels], dtype=raw.dtype, device=raw.device)
+            # the kernel's table: non-numeric labels are NaN -> the row is invalid (EmptyScore)
+            tab = torch.as_tensor(_label_table(list(labels)), dtype=raw.dtype, device=raw.device)
             s = tab[label]
         else:
             s = label.to(raw.dtype)
@@ -129,6 +130,11 @@ class TreeShardedScorer:
             self.epi, self.labels = dict(tp.full_epi), tp.labels
             self.n_trees_local = tp.n_trees
         else:
+            if compiled.schema.derived:
+                # the host traversal reads raw active-field columns; derived inputs need the derive
+                # program only the device plan runs
+                raise NotLowerable("host (gloo) tree-shard ranks need a model without derived fields")
+            self.compiled = compiled
             full = ensemble_spec(compiled)
             self.epi, self.labels = dict(full.epi), full.labels
             self.spec = shard_spec(full, self.rank, self.world)
@@ -141,7 +147,11 @@ class TreeShardedScorer:
             raw, valid = self.plan.alloc_outputs(Xt.shape[0])
             self.plan.launch(Xt, raw, valid)
             return raw, valid
-        acc, ok = host_partial(self.spec, np.asarray(X))
+        # MiningField preparation (missing / invalid replacement, outliers) exactly as the device
+        # kernels' fused prologue applies it, then the float64 traversal
+        P, row_ok = self.compiled.prepare(np.asarray(X, dtype=np.float64))
+        acc, ok = host_partial(self.spec, P)
+        ok = ok & row_ok
         return torch.from_numpy(acc.astype(np.float32)), torch.from_numpy(ok.astype(np.uint8))
 
     def score(self, X) -> Tuple[torch.Tensor, torch.Tensor]:

@@ -260,6 +260,10 @@ def iter_source(src: Any, clock: Optional[Clock] = None, offset: int = 0) -> Ite
             it = ThreadedSource(src).iterate(clock)
         else:
             it = iter(src.iterate())
+    elif callable(getattr(src, "iterate", None)):  # duck-typed pull source
+        it = iter(src.iterate())
+    elif callable(getattr(src, "run", None)) and not hasattr(src, "__iter__"):  # duck-typed push source
+        it = ThreadedSource(src).iterate(clock)
     else:
         it = iter(src)
     if offset:

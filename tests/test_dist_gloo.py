@@ -234,3 +234,61 @@ def test_killed_rank_surfaces_as_rank_failure(fixtures_dir):
         p.join(timeout=60)
     assert r == 0 and res[0] == "rank-failure" and res[1] == 2
     assert procs[1].exitcode == EXIT_KILLED_RANK
+
+
+# ------------------------------------------------------------------ ADVICE r1 (tree-shard host path)
+def _string_label_chain(n_trees, depth, F, seed):
+    from flink_jpmml_amd.bench.synth import gbdt_pmml
+
+    t = gbdt_pmml(n_trees=n_trees, depth=depth, n_features=F, seed=seed, objective="binary")
+    t = t.replace('<DataField name="y" optype="categorical" dataType="integer">\n   <Value value="0"/>\n'
+                  '   <Value value="1"/>', '<DataField name="y" optype="categorical" dataType="string">\n'
+                  '   <Value value="no"/>\n   <Value value="yes"/>')
+    t = t.replace('targetCategory="1"', 'targetCategory="yes"').replace('targetCategory="0"', 'targetCategory="no"')
+    # a missingValueReplacement on f0 of the top-level schema: host ranks must prepare like the kernel
+    return t.replace('<MiningField name="y" usageType="target"/>\n   <MiningField name="f0"/>',
+                     '<MiningField name="y" usageType="target"/>\n   <MiningField name="f0" '
+                     'missingValueReplacement="0.25"/>', 1)
+
+
+def w_tree_shard_text(ctx, text):
+    from flink_jpmml_amd.bench.synth import stream_matrix
+    from flink_jpmml_amd.parallel import TreeShardedScorer
+    from flink_jpmml_amd.runtime.compiled import CompiledPmml
+
+    c = CompiledPmml.from_string(text)
+    X = stream_matrix(1500, c.n_features, seed=8, missing_rate=0.05)
+    s, v = TreeShardedScorer(c, ctx).score(X)
+    return s.numpy(), v.numpy()
+
+
+def test_tree_shard_string_labels_and_missing_replacement():
+    """String calibrator categories give EmptyScore (NaN label table, like the kernel) instead of
+    a ValueError; host ranks apply MiningField missingValueReplacement before traversing."""
+    from flink_jpmml_amd.bench.synth import stream_matrix
+    from flink_jpmml_amd.parallel import finish_epilogue
+    from flink_jpmml_amd.runtime.compiled import CompiledPmml
+
+    text = _string_label_chain(23, 4, 6, 3)
+    c = CompiledPmml.from_string(text)
+    assert c.mining_fields["f0"].missing_value_replacement is not None
+    res = _run(2, w_tree_shard_text, text)
+    X = stream_matrix(1500, c.n_features, seed=8, missing_rate=0.05)
+    _, vref = c.score_matrix_oracle(X)
+    for r in range(2):
+        s, v = res[r]
+        assert not v.any() and not vref.any()  # string labels are not numeric targets -> EmptyScore
+    import torch
+
+    s, ok = finish_epilogue(torch.zeros(3), torch.ones(3, dtype=torch.uint8), {"mode": 1, "a": 1.0, "b": 0.0,
+                                                                               "link": 1}, ["no", "yes"])
+    assert not ok.any()
+    # numeric labels + the replacement: shard sums match the oracle exactly where f0 is missing
+    num = text.replace('"yes"', '"1"').replace('"no"', '"0"').replace('dataType="string"', 'dataType="integer"')
+    cn = CompiledPmml.from_string(num)
+    res = _run(2, w_tree_shard_text, num)
+    ref, vref = cn.score_matrix_oracle(X)
+    assert vref.all() and np.isnan(X[:, 0]).any()
+    for r in range(2):
+        s, v = res[r]
+        assert v.all() and (s == ref).all()

@@ -1,0 +1,163 @@
+"""The DSL's columnar fast path on the MI355X: RecordBatch → async PredictionBatch through the HIP
+kernels, compared with the float64 oracle and with the per-record contract; plus RCCL executed on
+hardware through a 1-rank process group (every collective of the data-parallel path)."""
+
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+N1 = "a1b2c3d4-0000-4000-8000-000000000001"
+
+
+def _gbdt_file(tmp_path, **kw):
+    from flink_jpmml_amd.bench.synth import gbdt_pmml
+
+    p = tmp_path / "gbdt.pmml"
+    p.write_text(gbdt_pmml(**kw))
+    return str(p)
+
+
+def test_quick_evaluate_columnar_on_gpu(gpu, tmp_path):
+    import torch
+
+    from flink_jpmml_amd import ModelReader
+    from flink_jpmml_amd.api.batch import PredictionBatch
+    from flink_jpmml_amd.bench.synth import stream_matrix
+    from flink_jpmml_amd.config import ScoringConfig
+    from flink_jpmml_amd.runtime.compiled import CompiledPmml
+    from flink_jpmml_amd.stream import StreamExecutionEnvironment
+
+    path = _gbdt_file(tmp_path, n_trees=200, depth=6, n_features=16, seed=2)
+    X = stream_matrix(300_000, 16, seed=4, missing_rate=0.02)
+    Xp = torch.from_numpy(X).pin_memory()
+    cfg = ScoringConfig(device=gpu, micro_batch=1 << 16, max_inflight=2, fallback="error")
+    env = StreamExecutionEnvironment(config=cfg)
+    out = env.from_batches(Xp, batch_rows=70_000).quick_evaluate(ModelReader(path)).collect()
+    assert len(out) == 5 and all(isinstance(p, PredictionBatch) for p, _ in out)
+    s = np.concatenate([p.scores for p, _ in out])
+    v = np.concatenate([p.valid for p, _ in out])
+    ref, vref = CompiledPmml.from_string(open(path).read()).score_matrix_oracle(X)
+    assert (v == vref).all()
+    np.testing.assert_allclose(s[v], ref[v], atol=2e-5, rtol=0)
+
+
+def test_model_predict_batch_is_async_and_matches_per_record(gpu, fixtures_dir):
+    from flink_jpmml_amd import DenseVector
+    from flink_jpmml_amd.api.batch import RecordBatch
+    from flink_jpmml_amd.api.pmml_model import PmmlModel
+    from flink_jpmml_amd.config import ScoringConfig
+
+    model = PmmlModel.from_path(fixtures_dir["kmeans"]).bind(gpu, ScoringConfig(device=gpu, fallback="error"))
+    assert model.on_device
+    X = np.random.default_rng(3).uniform(0.2, 7.0, size=(5000, 4))
+    X[::7, 1] = np.nan
+    pb = model.predict(RecordBatch(X))
+    per_record = [model.predict(DenseVector(r)) for r in X[:300]]
+    assert pb.to_list()[:300] == per_record
+
+
+def test_dynamic_columnar_on_gpu(gpu, fixtures_dir):
+    from flink_jpmml_amd import AddMessage
+    from flink_jpmml_amd.api.batch import RecordBatch
+    from flink_jpmml_amd.api.pmml_model import PmmlModel
+    from flink_jpmml_amd.config import ScoringConfig
+    from flink_jpmml_amd.stream import StreamExecutionEnvironment
+
+    X = np.random.default_rng(5).uniform(0.2, 7.0, size=(20_000, 4)).astype(np.float32)
+    seq = [("R", AddMessage(N1, 1, fixtures_dir["kmeans"], 0))] + \
+          [("L", RecordBatch(X[i:i + 5000], model_id=f"{N1}_1")) for i in range(0, 20_000, 5000)]
+    env = StreamExecutionEnvironment(config=ScoringConfig(device=gpu, fallback="error"))
+    ev, ctrl = env.from_either(seq)
+    out = ev.with_support_stream(ctrl).evaluate(lambda b, m: (m.on_device, m.predict(b))).collect()
+    assert all(on for on, _ in out)
+    ref = PmmlModel.from_path(fixtures_dir["kmeans"]).predict(X.astype(np.float64)).values(-1)
+    got = np.concatenate([p.values(-1) for _, p in out])
+    np.testing.assert_array_equal(got, ref)
+
+
+def test_latency_trigger_on_gpu(gpu, fixtures_dir):
+    """A slow per-record source with batch_size=65536: every prediction is emitted within the
+    latency bound (virtual clock), scored on the GPU."""
+    from flink_jpmml_amd import DenseVector, ModelReader
+    from flink_jpmml_amd.config import ScoringConfig
+    from flink_jpmml_amd.stream import ManualClock, StreamExecutionEnvironment
+    from flink_jpmml_amd.stream.clock import current_clock
+
+    arrivals, emitted = [], []
+
+    class Slow:
+        def __iter__(self):
+            c = current_clock()
+            for i in range(5):
+                c.sleep(1.0)
+                arrivals.append(c.now())
+                yield DenseVector(1.0, 1.0, 1.0, 1.0)
+
+    clock = ManualClock()
+    env = StreamExecutionEnvironment(clock=clock)
+    env.add_source(Slow()).quick_evaluate(
+        ModelReader(fixtures_dir["kmeans"]),
+        config=ScoringConfig(device=gpu, batch_size=65536, max_batch_latency_ms=50.0)).add_sink(
+        lambda x: emitted.append((clock.now(), x[0])))
+    env.execute()
+    assert [round(t - a, 6) for (t, _), a in zip(emitted[:-1], arrivals[:-1])] == [0.05] * 4
+    assert all(p.value.get() == 3.0 for _, p in emitted)
+
+
+RCCL_SCRIPT = r"""
+import os, sys, json
+sys.path.insert(0, os.environ["FJA_ROOT"])
+import numpy as np, torch
+from flink_jpmml_amd import AddMessage, ModelReader
+from flink_jpmml_amd.api.batch import RecordBatch
+from flink_jpmml_amd.config import ScoringConfig
+from flink_jpmml_amd.stream import StreamExecutionEnvironment
+from flink_jpmml_amd.parallel import all_gather_scores, all_gather_varlen, broadcast_control
+from flink_jpmml_amd.utils.metrics import METRICS
+kmeans, gbdt = sys.argv[1], sys.argv[2]
+N1 = "a1b2c3d4-0000-4000-8000-000000000001"
+env = StreamExecutionEnvironment.get_execution_environment(
+    config=ScoringConfig(device="cuda", fallback="error"), force_distributed=True)
+ctx = env.dist_ctx
+assert ctx.is_distributed and ctx.backend == "nccl" and ctx.world_size == 1
+X = np.random.default_rng(1).uniform(0.2, 7.0, size=(4096, 4)).astype(np.float32)
+seq = [("R", AddMessage(N1, 1, kmeans, 0))] + [("L", RecordBatch(X, model_id=f"{N1}_1"))] * 3
+ev, ctrl = env.from_either(seq)
+out = ev.with_support_stream(ctrl).evaluate(lambda b, m: m.predict(b).values(-1.0)).collect()  # all_gather_object
+env2 = StreamExecutionEnvironment.get_execution_environment(force_distributed=True,
+    config=ScoringConfig(device="cuda", fallback="error"))
+res = env2.from_batches(torch.from_numpy(np.random.default_rng(2).standard_normal((50000, 16)).astype(np.float32)).pin_memory(),
+    batch_rows=10000).quick_evaluate(ModelReader(gbdt)).collect()
+s = torch.tensor(np.concatenate([p.scores for p, _ in res]), device="cuda")
+v = torch.tensor(np.concatenate([p.valid for p, _ in res]).astype(np.uint8), device="cuda")
+gs, gv, _ = all_gather_scores(s, v, ctx)
+var = all_gather_varlen(s[:123], ctx)
+msgs = broadcast_control([AddMessage(N1, 2, "/x.xml", 1)], ctx)
+torch.cuda.synchronize()
+print(json.dumps({"n_out": len(out), "first": float(out[0][0]), "replicated": METRICS.counters.get("model.loads_replicated", 0),
+                  "bytes_bcast": METRICS.counters.get("dist.bytes_broadcast", 0), "gather_ok": bool(torch.equal(gs, s)),
+                  "var_ok": int(var.numel()), "ctrl": repr(msgs[0])}))
+"""
+
+
+def test_rccl_one_rank_group_executes_every_collective(gpu, fixtures_dir, tmp_path):
+    """A 1-rank RCCL group forces the data-parallel code path on a single-GPU box: parse-once
+    model replication (broadcast_object + broadcast of the compiled tensors), control broadcast,
+    all_gather_into_tensor / varlen gather, all_gather_object of the collected outputs."""
+    import json
+
+    gbdt = _gbdt_file(tmp_path, n_trees=64, depth=5, n_features=16, seed=1)
+    env = dict(os.environ, FJA_ROOT=ROOT, MASTER_ADDR="127.0.0.1", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, "-c", RCCL_SCRIPT, fixtures_dir["kmeans"], gbdt], env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["n_out"] == 3 and res["replicated"] >= 2 and res["bytes_bcast"] > 0
+    assert res["gather_ok"] and res["var_ok"] == 123 and "AddMessage" in res["ctrl"]
