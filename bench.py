@@ -62,7 +62,8 @@ def parse_args(argv=None):
     p.add_argument("--features", type=int, default=None, help="default 32 (trees), 64 (mlp)")
     p.add_argument("--rows", type=int, default=1 << 23,
                    help="rows per GPU per step (8M: a 20-step timed region is ~0.4 s on one GPU)")
-    p.add_argument("--micro-batch", type=int, default=1 << 19)
+    p.add_argument("--micro-batch", type=int, default=1 << 20,
+                   help="rows per H2D slice + kernel launch (1M measured best: profiles/r2_h2d_probe.md)")
     p.add_argument("--pipeline-depth", type=int, default=3, help="input ring slots (H2D/compute overlap)")
     p.add_argument("--max-inflight", type=int, default=3, help="scored steps in flight before the sink waits")
     p.add_argument("--precision", choices=["fp32", "bf16", "fp8"], default=None,
