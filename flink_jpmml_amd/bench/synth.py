@@ -99,8 +99,11 @@ def _mining_schema(out: io.StringIO, F: int, target: Optional[str], indent: str 
 
 def gbdt_pmml(n_trees: int = 1000, depth: int = 6, n_features: int = 32, seed: int = 0,
               objective: str = "regression", p_split: float = 0.9, learning_rate: float = 0.1,
-              base_score: float = 0.5, float_casts: bool = False, missing_strategy: str = "defaultChild") -> str:
-    """XGBoost-style GBDT PMML (regression or binary:logistic chain). ``float_casts`` adds the
+              base_score: float = 0.5, float_casts: bool = False, missing_strategy: str = "defaultChild",
+              n_classes: int = 3) -> str:
+    """XGBoost-style GBDT PMML: regression, ``binary`` (binary:logistic chain) or ``multiclass``
+    (multi:softprob — ``n_classes`` chained ensembles of ``n_trees`` each + a softmax
+    RegressionModel over their ``xgbValue(k)`` outputs). ``float_casts`` adds the
     ``float(fj)`` ``LocalTransformations`` casts that pipeline exporters (sklearn2pmml) emit, with
     every split on the cast field."""
     rng = np.random.default_rng(seed)
@@ -108,7 +111,9 @@ def gbdt_pmml(n_trees: int = 1000, depth: int = 6, n_features: int = 32, seed: i
     out = io.StringIO()
     _header(out, f"synthetic GBDT {n_trees} trees depth {depth} ({objective})")
     binary = objective == "binary"
-    _data_dictionary(out, n_features, "y", "integer" if binary else "double", ["0", "1"] if binary else None)
+    multi = objective == "multiclass"
+    cats = [str(k) for k in range(n_classes)] if multi else ["0", "1"]
+    _data_dictionary(out, n_features, "y", "integer" if binary or multi else "double", cats if binary or multi else None)
     fmt = "float(f{})" if float_casts else "f{}"
 
     def leaf() -> str:
@@ -123,11 +128,11 @@ def gbdt_pmml(n_trees: int = 1000, depth: int = 6, n_features: int = 32, seed: i
                       f'<FieldRef field="f{j}"/></DerivedField>\n')
         out.write(f'{indent}</LocalTransformations>\n')
 
-    def trees_model(indent: str, target_in_schema: bool, rescale: float) -> None:
+    def trees_model(indent: str, target_in_schema: bool, rescale: float, out_name: str = "xgbValue") -> None:
         out.write(f'{indent}<MiningModel functionName="regression">\n')
         _mining_schema(out, n_features, None if not target_in_schema else "y", indent + " ")
-        if binary:
-            out.write(f'{indent} <Output><OutputField name="xgbValue" optype="continuous" dataType="float" '
+        if binary or multi:
+            out.write(f'{indent} <Output><OutputField name="{out_name}" optype="continuous" dataType="float" '
                       f'isFinalResult="false"/></Output>\n')
         out.write(f'{indent} <Targets><Target rescaleConstant="{_fnum(rescale)}"/></Targets>\n')
         casts(indent + " ")
@@ -142,7 +147,7 @@ def gbdt_pmml(n_trees: int = 1000, depth: int = 6, n_features: int = 32, seed: i
             out.write(f'{indent}   </TreeModel>\n{indent}  </Segment>\n')
         out.write(f'{indent} </Segmentation>\n{indent}</MiningModel>\n')
 
-    if not binary:
+    if not binary and not multi:
         out.write(' <MiningModel functionName="regression" algorithmName="XGBoost (GBTree)">\n')
         _mining_schema(out, n_features, "y", "  ")
         out.write(f'  <Targets><Target field="y" rescaleConstant="{_fnum(base_score)}"/></Targets>\n')
@@ -161,6 +166,20 @@ def gbdt_pmml(n_trees: int = 1000, depth: int = 6, n_features: int = 32, seed: i
     out.write(' <MiningModel functionName="classification" algorithmName="XGBoost (GBTree)">\n')
     _mining_schema(out, n_features, "y", "  ")
     out.write('  <Segmentation multipleModelMethod="modelChain">\n')
+    if multi:
+        for k in range(n_classes):
+            out.write(f'   <Segment id="{k + 1}"><True/>\n')
+            trees_model("    ", False, 0.0, f"xgbValue({k})")
+            out.write('   </Segment>\n')
+        out.write(f'   <Segment id="{n_classes + 1}"><True/>\n')
+        out.write('    <RegressionModel functionName="classification" normalizationMethod="softmax">\n')
+        out.write('     <MiningSchema><MiningField name="y" usageType="target"/>'
+                  + "".join(f'<MiningField name="xgbValue({k})"/>' for k in range(n_classes)) + '</MiningSchema>\n')
+        for k in range(n_classes):
+            out.write(f'     <RegressionTable intercept="{_fnum(0.1 * k)}" targetCategory="{k}">'
+                      f'<NumericPredictor name="xgbValue({k})" coefficient="1.0"/></RegressionTable>\n')
+        out.write('    </RegressionModel>\n   </Segment>\n  </Segmentation>\n </MiningModel>\n</PMML>\n')
+        return out.getvalue()
     out.write('   <Segment id="1"><True/>\n')
     trees_model("    ", False, float(np.log(base_score / (1 - base_score))))
     out.write('   </Segment>\n   <Segment id="2"><True/>\n')

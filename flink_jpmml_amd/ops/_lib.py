@@ -135,7 +135,8 @@ class TreeArgs(ctypes.Structure):
                 ("chunk_trees", c_int), ("P", c_int), ("C", c_int), ("trees_per_split", c_int),
                 ("general", c_int), ("variant", c_int), ("epi", Epilogue), ("score", c_void_p),
                 ("valid", c_void_p), ("probs", c_void_p), ("partial", c_void_p), ("blob_nan", c_void_p),
-                ("chunk_trees_nan", c_int), ("pad1", c_int)]
+                ("chunk_trees_nan", c_int), ("pad1", c_int), ("tree_w", c_void_p), ("acc_init", c_void_p),
+                ("feat_map", c_void_p), ("rows_wide", c_int), ("mode", c_int), ("n_stage", c_int), ("pad2", c_int)]
 
 
 class GenTreeArgs(ctypes.Structure):
@@ -162,7 +163,8 @@ class MlpArgs(ctypes.Structure):
                 ("in_scale", c_void_p), ("in_shift", c_void_p), ("in_missing", c_void_p), ("in_index", c_void_p),
                 ("n_in", c_int), ("k0", c_int), ("weights", c_void_p), ("biases", c_void_p), ("layers", c_void_p),
                 ("out_scale", c_float), ("out_shift", c_float), ("final_norm", c_int), ("n_out", c_int),
-                ("epi", Epilogue), ("score", c_void_p), ("valid", c_void_p), ("probs", c_void_p)]
+                ("epi", Epilogue), ("score", c_void_p), ("valid", c_void_p), ("probs", c_void_p),
+                ("panels", c_void_p), ("n_panels", c_int), ("contiguous", c_int)]
 
 
 class SvmArgs(ctypes.Structure):

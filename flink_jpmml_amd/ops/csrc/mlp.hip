@@ -1,18 +1,29 @@
-// NeuralNetwork (MLP) scoring on the matrix cores: all layers fused in one kernel.
+// NeuralNetwork (MLP) scoring on the matrix cores: all layers fused in one persistent kernel.
 //
-// Data rows sit on the MFMA N dimension (lanes) and neurons on M (registers): each layer computes
-// Zᵀ[units, 32 rows] = Wᵀ[units, K] · Hᵀ[K, 32 rows]. With that orientation the 32x32 accumulator
-// of one layer (rows of Zᵀ in registers, data rows on lanes) is directly the B operand of the next
-// layer's MFMA — no LDS round trip, no lane shuffles between layers (cdna_hip_programming.md §3,
-// "An accumulator tile as the next MFMA's operand"). The A operands (weights) are pre-permuted on
-// the host into exactly the k order the accumulator registers provide and streamed from L2.
+// Orientation (unchanged from the first version): data rows on the MFMA N dimension (lanes),
+// neurons on M (registers): each layer computes Zᵀ[units, 32 rows] = Wᵀ[units, K] · Hᵀ[K, 32 rows].
+// The 32x32 accumulator of one output tile (units on registers, rows on lanes) is directly the B
+// operand of the next layer's MFMA (cdna_hip_programming.md §3, "An accumulator tile as the next
+// MFMA's operand"), so activations never leave the register file between layers.
 //
-// Two precisions:
+// What changed (round 2): the weights (A operands) are no longer fetched from L2 by every wave
+// for every MFMA. They stream through an LDS ring of PANELS — one panel = all k-step fragments of
+// one 32-unit output tile of one layer, pre-permuted on the host into exactly the k order the
+// registers provide. One 512-thread workgroup (8 waves x 32 rows = 256 rows) shares every panel,
+// so each weight byte read from L2 serves 256 rows (was 32), and the A-fragment read is a
+// conflict-free ds_read_b128 per MFMA with LDS latency instead of L2 latency. The panel for
+// step p+2 is loaded into registers while step p computes and stored after it (one barrier per
+// panel). Each output tile is ONE accumulation chain (16 MFMAs back to back on one accumulator,
+// which the 32x32x16 pipe sustains at full rate), so only 16 accumulator registers are live and
+// the activations of the current and the next layer fit in 2 x 64 VGPRs (bf16) — two waves per
+// SIMD. The grid is persistent (one workgroup per CU walks row tiles), so the panel pipeline
+// runs across tile boundaries without draining.
+//
+// Two precisions (one template):
 //   BF16 = true : v_mfma_f32_32x32x16_bf16 (bf16 in, fp32 accumulate) — the throughput path;
-//   BF16 = false: v_mfma_f32_32x32x2_f32  (exact fp32 FMA chain)     — the parity path.
-// One wave owns 32 data rows; a 256-thread workgroup owns 128. Input normalisation
-// (NormContinuous as scale/shift), missing handling, activations, output layer normalisation
-// (softmax) and the target decode are fused.
+//   BF16 = false: v_mfma_f32_32x32x2_f32  (exact fp32 FMA chain)     — the parity path (default).
+// Input normalisation (NormContinuous as scale/shift), missing handling, activations, output-layer
+// normalisation (softmax / simplemax) and the target decode are fused.
 #include "epilogue.h"
 
 namespace {
@@ -20,9 +31,10 @@ namespace {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int WAVES = 4;
-constexpr int MT = 8;          // max 32-unit tiles per layer -> 256 units
-constexpr int MAXL = 4;        // max layers
+constexpr int MT = 8;          // max 32-unit output tiles per layer -> 256 units per layer
+constexpr int MAXL = 8;        // max layers (biases staged in LDS)
+constexpr int KMAX = 256;      // max inputs per layer
+constexpr int NSLOT = 4;       // LDS panel ring slots
 
 enum : int { A_IDENTITY = 0, A_LOGISTIC = 1, A_TANH = 2, A_RELU = 3, A_EXP = 4, A_RECIP = 5, A_SQUARE = 6,
              A_GAUSS = 7, A_SINE = 8, A_COSINE = 9, A_ELLIOTT = 10, A_ARCTAN = 11, A_THRESHOLD = 12 };
@@ -55,6 +67,8 @@ struct MlpArgs {
   float* score;
   uint8_t* valid;
   float* probs;
+  const int2* panels;       // [n_panels] {offset, size} in 16-byte units, consumption order
+  int n_panels, contiguous; // contiguous: in_index[k] == k (vector input loads)
 };
 
 __device__ __forceinline__ float activate(int a, float z, float thr) {
@@ -78,165 +92,270 @@ __device__ __forceinline__ float activate(int a, float z, float thr) {
 // row (unit) index inside a 32x32 accumulator tile held by register r of lane half h
 __device__ __forceinline__ int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
+template <bool BF16> struct Cfg;
+template <> struct Cfg<true> {
+  static constexpr int WAVES = 8, KS = KMAX / 16, Q = 2;   // Q: uint4 per thread per 16 KiB panel
+  static constexpr int PANEL = 16 * 1024;
+  typedef bf16x8 B;
+};
+template <> struct Cfg<false> {
+  static constexpr int WAVES = 4, KS = KMAX / 2, Q = 8;    // 32 KiB panels (128 k-steps x 256 B)
+  static constexpr int PANEL = 32 * 1024;
+  typedef float B;
+};
+
+// Input normalisation tables in LDS are padded to KMAX with neutral entries (index 0, scale 0,
+// shift 0, replacement 0): padded k read column 0 and contribute exactly 0. `contiguous` (identity
+// index) is only set by the host when n_in == k0, so no record load leaves the row.
+
 template <bool BF16>
-__global__ __launch_bounds__(64 * WAVES, BF16 ? 2 : 1) void mlp_kernel(MlpArgs a) {
-  extern __shared__ __align__(16) float xs[];  // [WAVES][32][stride]
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+__device__ __forceinline__ void load_panel(const MlpArgs& a, int p, int tid, uint4 (&q)[Cfg<BF16>::Q]) {
+  constexpr int T = 64 * Cfg<BF16>::WAVES;
+  const uint4* W4 = reinterpret_cast<const uint4*>(a.weights);
+  const int2 d = a.panels[p % a.n_panels];
+  const int last = d.y > 0 ? d.y - 1 : 0;
+#pragma unroll
+  for (int i = 0; i < Cfg<BF16>::Q; ++i) q[i] = W4[d.x + min(tid + i * T, last)];
+}
+
+template <bool BF16>
+__device__ __forceinline__ void store_panel(const MlpArgs& a, int p, int tid, uint4* ring,
+                                            const uint4 (&q)[Cfg<BF16>::Q]) {
+  constexpr int T = 64 * Cfg<BF16>::WAVES;
+  const int2 d = a.panels[p % a.n_panels];
+  uint4* dst = ring + (p % NSLOT) * (Cfg<BF16>::PANEL / 16);
+#pragma unroll
+  for (int i = 0; i < Cfg<BF16>::Q; ++i)
+    if (tid + i * T < d.y) dst[tid + i * T] = q[i];
+}
+
+// One 32-unit output tile TI of one layer: a single accumulation chain over the layer's k-steps
+// (A from the LDS panel, B from registers), activation, and the result written into the next
+// layer's B-operand registers (TI is a compile-time index, so nb stays in VGPRs).
+template <bool BF16, int TI>
+__device__ __forceinline__ void tile_step(const MlpArgs& a, const LayerMeta& m, int ksteps, bool last, int h,
+                                          int lane, int tid, uint4* ring, const float* s_b,
+                                          const typename Cfg<BF16>::B (&pb)[Cfg<BF16>::KS],
+                                          typename Cfg<BF16>::B (&nb)[Cfg<BF16>::KS], f32x16& out, int& p,
+                                          uint4 (&q)[Cfg<BF16>::Q]) {
+  using C = Cfg<BF16>;
+  // prefetch panel p+2 into registers while this one is multiplied
+  load_panel<BF16>(a, p + 2, tid, q);
+  const uint4* slot = ring + (p % NSLOT) * (C::PANEL / 16);
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = s_b[m.b_off + 32 * TI + acc_row(r, h)];
+#pragma unroll
+  for (int s = 0; s < C::KS; ++s) {
+    if (s < ksteps) {
+      if constexpr (BF16) {
+        const uint4 w = slot[s * 64 + lane];
+        bf16x8 A;
+        __builtin_memcpy(&A, &w, 16);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, pb[s], acc, 0, 0, 0);
+      } else {
+        const float A = reinterpret_cast<const float*>(slot)[s * 64 + lane];
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(A, pb[s], acc, 0, 0, 0);
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = activate(m.act, acc[r], m.thr);
+  if (last) {
+    if (TI == 0) out = acc;
+  } else {
+    if constexpr (BF16) {
+      bf16x8 lo, hi;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        lo[j] = (__bf16)acc[j];
+        hi[j] = (__bf16)acc[8 + j];
+      }
+      nb[2 * TI] = lo;
+      nb[2 * TI + 1] = hi;
+    } else {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) nb[16 * TI + r] = acc[r];
+    }
+  }
+  // slot (p+2) % NSLOT was last read at step p-2, before the previous barrier
+  store_panel<BF16>(a, p + 2, tid, ring, q);
+  __syncthreads();
+  ++p;
+}
+
+template <bool BF16>
+__global__ __launch_bounds__(64 * Cfg<BF16>::WAVES, 1) void mlp_kernel(MlpArgs a) {
+  using C = Cfg<BF16>;
+  typedef typename C::B BT;
+  constexpr int T = 64 * C::WAVES;
+  constexpr int KS = C::KS;
+  extern __shared__ __align__(16) uint4 smem4[];
+  uint4* ring = smem4;                                             // [NSLOT][PANEL/16]
+  float* s_sc = reinterpret_cast<float*>(ring + NSLOT * (C::PANEL / 16));
+  float* s_sh = s_sc + KMAX;
+  float* s_ms = s_sh + KMAX;
+  int* s_ix = reinterpret_cast<int*>(s_ms + KMAX);
+  float* s_b = reinterpret_cast<float*>(s_ix + KMAX);              // [MAXL * MT * 32]
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
   const int h = lane >> 5;
   const int col = lane & 31;
-  const int stride = BF16 ? a.k0 + 4 : a.k0 + 1;
-  float* xw = xs + wave * 32 * stride;
-  const int row0 = (blockIdx.x * WAVES + wave) * 32;
-  if (row0 >= a.n_rows) return;
 
-  // ---- stage + normalise this wave's 32 input rows: xw[r][k], k < k0 (zero padded)
-  for (int e = lane; e < 32 * a.k0; e += 64) {
-    const int r = e / a.k0;
-    const int k = e - r * a.k0;
-    const int row = row0 + r;
-    float v = 0.f;
-    if (k < a.n_in && row < a.n_rows) {
-      const float x = a.X[(size_t)row * a.ldx + a.in_index[k]];
-      v = (x != x) ? a.in_missing[k] : fmaf(x, a.in_scale[k], a.in_shift[k]);
-    }
-    xw[r * stride + k] = v;
+  // ---- once per workgroup: preparation tables + biases into LDS
+  for (int k = tid; k < KMAX; k += T) {
+    const bool u = k < a.n_in;
+    s_sc[k] = u ? a.in_scale[k] : 0.f;
+    s_sh[k] = u ? a.in_shift[k] : 0.f;
+    s_ms[k] = u ? a.in_missing[k] : 0.f;
+    s_ix[k] = u ? a.in_index[k] : 0;
   }
-  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's LDS writes are done
-  __builtin_amdgcn_wave_barrier();
-  bool bad = false;
-  for (int k = 0; k < a.n_in; ++k) bad = bad || (xw[col * stride + k] != xw[col * stride + k]);
+  int nbias = 0;
+  for (int L = 0; L < a.n_layers; ++L) nbias = max(nbias, a.layers[L].b_off + a.layers[L].mp);
+  for (int i = tid; i < nbias; i += T) s_b[i] = a.biases[i];
 
-  // Named registers instead of arrays: hipcc demoted f32x16 acc[8] / bf16x8 pb[8][2] arrays to
-  // scratch (mixed whole-vector and element accesses); one variable per tile stays in VGPR/AGPRs.
-#define TILES(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
-#define DECL(i) f32x16 acc##i = {}; bf16x8 pb##i##a = {}, pb##i##b = {}; f32x16 pf##i = {};
-  TILES(DECL)
-#undef DECL
-  int ptiles = 0;
+  // ---- panel ring prologue: panels 0 and 1
+  uint4 q[C::Q];
+  load_panel<BF16>(a, 0, tid, q);
+  store_panel<BF16>(a, 0, tid, ring, q);
+  load_panel<BF16>(a, 1, tid, q);
+  store_panel<BF16>(a, 1, tid, ring, q);
+  __syncthreads();
 
+  const int n_tiles = (a.n_rows + 32 * C::WAVES - 1) / (32 * C::WAVES);
+  int p = 0;  // panel counter (runs across row tiles)
+  for (int tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+    const int row = (tile * C::WAVES + wave) * 32 + col;
+    const bool in_range = row < a.n_rows;
+    const float* xrow = a.X + (size_t)(in_range ? row : 0) * a.ldx;
+    bool bad = false;
+
+    // ---- layer-0 B operands straight from the record (normalised), into pb. The lane's table
+    // offset goes through an opaque register each tile, so the per-k LDS addresses stay
+    // base + immediate (hoisting them out of the tile loop would cost hundreds of VGPRs).
+    BT pb[KS], nb[KS];
+    {
+      uint32_t kb = BF16 ? 8u * h : (uint32_t)h;  // first k of this lane half
+      __asm__ volatile("" : "+v"(kb));
+      const float* tsc = s_sc + kb;
+      const float* tsh = s_sh + kb;
+      const float* tms = s_ms + kb;
+      const int* tix = s_ix + kb;
+      const float* xr = xrow + (a.contiguous ? kb : 0u);
 #pragma unroll
-  for (int L = 0; L < MAXL; ++L) {
-    if (L >= a.n_layers) break;
-    const LayerMeta m = a.layers[L];
-    const int mtiles = m.mp >> 5;
-    const bool last = (L == a.n_layers - 1);
-#define INIT(i)                                                                        \
-    if (i < mtiles) {                                                                  \
-      _Pragma("unroll") for (int r = 0; r < 16; ++r) acc##i[r] = a.biases[m.b_off + 32 * i + acc_row(r, h)]; \
-    }
-    TILES(INIT)
-#undef INIT
-    if (BF16) {
-      const bf16x8* W = reinterpret_cast<const bf16x8*>(a.weights) + m.w_off / 8;
-      const int ksteps = m.kp >> 4;
-#define MF(t, B, S) \
-      if (t < mtiles) acc##t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(W[(t * ksteps + (S)) * 64 + lane], B, acc##t, 0, 0, 0);
-#define MF_ALL(B, S) MF(0, B, S) MF(1, B, S) MF(2, B, S) MF(3, B, S) MF(4, B, S) MF(5, B, S) MF(6, B, S) MF(7, B, S)
-      if (L == 0) {
-        for (int s = 0; s < ksteps; ++s) {
-          const float* src = xw + col * stride + 16 * s + 8 * h;
-          bf16x8 b;
+      for (int s = 0; s < KS; ++s) {
+        if constexpr (BF16) {
+          if (16 * s < a.k0) {
+            bf16x8 v;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) b[j] = (__bf16)src[j];
-          MF_ALL(b, s)
+            for (int j = 0; j < 8; ++j) {
+              const int o = 16 * s + j;
+              const float x = a.contiguous ? xr[o] : xrow[tix[o]];
+              const float y = (x != x) ? tms[o] : fmaf(x, tsc[o], tsh[o]);
+              bad = bad || (y != y);
+              v[j] = (__bf16)y;
+            }
+            pb[s] = v;
+          }
+          if ((s & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+        } else {
+          if (2 * s < a.k0) {
+            const int o = 2 * s;
+            const float x = a.contiguous ? xr[o] : xrow[tix[o]];
+            const float y = (x != x) ? tms[o] : fmaf(x, tsc[o], tsh[o]);
+            bad = bad || (y != y);
+            pb[s] = y;
+          }
+          if ((s & 15) == 15) __builtin_amdgcn_sched_barrier(0);
         }
-      } else {
-#define LTP(tp) \
-        if (tp < ptiles) { MF_ALL(pb##tp##a, 2 * tp) MF_ALL(pb##tp##b, 2 * tp + 1) }
-        TILES(LTP)
-#undef LTP
       }
-#undef MF_ALL
-#undef MF
-    } else {
-      const float* W = reinterpret_cast<const float*>(a.weights) + m.w_off;
-      const int ksteps = m.kp >> 1;
-#define MF(t, B, S) \
-      if (t < mtiles) acc##t = __builtin_amdgcn_mfma_f32_32x32x2f32(W[(t * ksteps + (S)) * 64 + lane], B, acc##t, 0, 0, 0);
-#define MF_ALL(B, S) MF(0, B, S) MF(1, B, S) MF(2, B, S) MF(3, B, S) MF(4, B, S) MF(5, B, S) MF(6, B, S) MF(7, B, S)
-      if (L == 0) {
-        for (int s = 0; s < ksteps; ++s) {
-          const float b = xw[col * stride + 2 * s + h];
-          MF_ALL(b, s)
-        }
-      } else {
-#define LTP(tp) \
-        if (tp < ptiles) { _Pragma("unroll") for (int r = 0; r < 16; ++r) { MF_ALL(pf##tp[r], 16 * tp + r) } }
-        TILES(LTP)
-#undef LTP
-      }
-#undef MF_ALL
-#undef MF
     }
-    // activation (padded units: zero weights + zero bias; their activations only ever meet zero
-    // weight columns of the next layer)
-#define ACT(i)                                                                         \
-    if (i < mtiles) {                                                                  \
-      _Pragma("unroll") for (int r = 0; r < 16; ++r) {                                 \
-        const float v = activate(m.act, acc##i[r], m.thr);                             \
-        if (last) acc##i[r] = v;                                                       \
-        else if (BF16) { if (r < 8) pb##i##a[r] = (__bf16)v; else pb##i##b[r - 8] = (__bf16)v; } \
-        else pf##i[r] = v;                                                             \
-      }                                                                                \
-    }
-    TILES(ACT)
-#undef ACT
-    ptiles = mtiles;
-  }
-  const f32x16 out0 = acc0;
-#undef TILES
+    bad = bad && in_range;
+    bad = bad || (__shfl_xor((int)bad, 32) != 0);
 
-  // ---- output layer: units 0..n_out-1 live in tile 0; lanes l and l^32 hold the two halves
-  const int row = row0 + col;
-  const bool in_range = row < a.n_rows;
-  if (a.final_norm == 0 && a.n_out == 1) {
+    f32x16 out = {};
+    for (int L = 0; L < a.n_layers; ++L) {
+      const LayerMeta m = a.layers[L];
+      const int mtiles = m.mp >> 5;
+      const int ksteps = BF16 ? (m.kp >> 4) : (m.kp >> 1);
+      const bool last = L == a.n_layers - 1;
+#define PMML_TILE(TI) \
+      if (TI < mtiles) tile_step<BF16, TI>(a, m, ksteps, last, h, lane, tid, ring, s_b, pb, nb, out, p, q);
+      PMML_TILE(0) PMML_TILE(1) PMML_TILE(2) PMML_TILE(3) PMML_TILE(4) PMML_TILE(5) PMML_TILE(6) PMML_TILE(7)
+#undef PMML_TILE
+      if (!last) {
+#pragma unroll
+        for (int s = 0; s < KS; ++s) pb[s] = nb[s];
+      }
+    }
+
+    // ---- output layer: units 0..n_out-1 live in tile 0; lanes l and l^32 hold the two halves
+    if (a.final_norm == 0 && a.n_out == 1) {
+      if (h == 0 && in_range) {
+        apply_epilogue(a.epi, [&](int) { return out[0]; }, !bad, row, a.n_rows, a.score, a.valid, a.probs);
+      }
+      continue;
+    }
+    float mx = -__builtin_inff();
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      if (acc_row(r, h) < a.n_out) mx = fmaxf(mx, out[r]);
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    float pr[16];
+    float sum = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const bool u = acc_row(r, h) < a.n_out;
+      float v = out[r];
+      if (a.final_norm == 1) v = __expf(v - mx);
+      pr[r] = u ? v : 0.f;
+      sum += pr[r];
+    }
+    sum += __shfl_xor(sum, 32);
+    float best = -__builtin_inff();
+    int best_u = 1 << 30;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int u = acc_row(r, h);
+      if (u < a.n_out) {
+        if (a.final_norm != 0) pr[r] /= sum;
+        if (pr[r] > best || (pr[r] == best && u < best_u)) { best = pr[r]; best_u = u; }
+        if (a.probs && in_range) a.probs[(size_t)row * a.n_out + u] = pr[r];
+      }
+    }
+    const float ob = __shfl_xor(best, 32);
+    const int ou = __shfl_xor(best_u, 32);
+    if (ob > best || (ob == best && ou < best_u)) { best = ob; best_u = ou; }
     if (h == 0 && in_range) {
-      apply_epilogue(a.epi, [&](int) { return out0[0]; }, !bad, row, a.n_rows, a.score, a.valid, a.probs);
-    }
-    return;
-  }
-  float mx = -__builtin_inff();
-#pragma unroll
-  for (int r = 0; r < 16; ++r)
-    if (acc_row(r, h) < a.n_out) mx = fmaxf(mx, out0[r]);
-  mx = fmaxf(mx, __shfl_xor(mx, 32));
-  float p[16];
-  float sum = 0.f;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const bool u = acc_row(r, h) < a.n_out;
-    float v = out0[r];
-    if (a.final_norm == 1) v = __expf(v - mx);
-    p[r] = u ? v : 0.f;
-    sum += p[r];
-  }
-  sum += __shfl_xor(sum, 32);
-  float best = -__builtin_inff();
-  int best_u = 1 << 30;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int u = acc_row(r, h);
-    if (u < a.n_out) {
-      if (a.final_norm != 0) p[r] /= sum;
-      if (p[r] > best || (p[r] == best && u < best_u)) { best = p[r]; best_u = u; }
-      if (a.probs && in_range) a.probs[(size_t)row * a.n_out + u] = p[r];
+      bool ok = !bad && best == best && best_u < a.n_out;
+      float sc = ok ? (a.epi.has_table ? a.epi.table[best_u] : (float)best_u) : __builtin_nanf("");
+      ok = ok && (sc == sc);
+      a.score[row] = ok ? sc : __builtin_nanf("");
+      a.valid[row] = ok ? 1 : 0;
+      if (a.epi.score2) {
+        a.epi.score2[row] = ok ? sc : __builtin_nanf("");
+        a.epi.valid2[row] = ok ? 1 : 0;
+      }
     }
   }
-  const float ob = __shfl_xor(best, 32);
-  const int ou = __shfl_xor(best_u, 32);
-  if (ob > best || (ob == best && ou < best_u)) { best = ob; best_u = ou; }
-  if (h == 0 && in_range) {
-    bool ok = !bad && best == best && best_u < a.n_out;
-    float sc = ok ? (a.epi.has_table ? a.epi.table[best_u] : (float)best_u) : __builtin_nanf("");
-    ok = ok && (sc == sc);
-    a.score[row] = ok ? sc : __builtin_nanf("");
-    a.valid[row] = ok ? 1 : 0;
-    if (a.epi.score2) {
-      a.epi.score2[row] = ok ? sc : __builtin_nanf("");
-      a.epi.valid2[row] = ok ? 1 : 0;
-    }
+}
+
+template <bool BF16>
+size_t lds_bytes() {
+  return (size_t)NSLOT * Cfg<BF16>::PANEL + 4 * KMAX * 4 + (size_t)MAXL * MT * 32 * 4;
+}
+
+int n_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
   }
+  return n;
 }
 
 }  // namespace
@@ -247,11 +366,21 @@ PMML_API int pmml_mlp_layer_meta_size() { return (int)sizeof(LayerMeta); }
 PMML_API int pmml_mlp_launch(hipStream_t stream, const MlpArgs* args, int bf16) {
   const MlpArgs a = *args;
   if (a.n_rows <= 0) return 0;
-  if (a.n_layers < 1 || a.n_layers > MAXL || a.n_out > 32 || a.k0 > 256) return -4;
-  const int stride = bf16 ? a.k0 + 4 : a.k0 + 1;
-  const size_t lds = (size_t)WAVES * 32 * stride * 4;
-  dim3 grid((a.n_rows + 32 * WAVES - 1) / (32 * WAVES));
-  if (bf16) hipLaunchKernelGGL(mlp_kernel<true>, grid, dim3(64 * WAVES), lds, stream, a);
-  else hipLaunchKernelGGL(mlp_kernel<false>, grid, dim3(64 * WAVES), lds, stream, a);
+  if (a.n_layers < 1 || a.n_layers > MAXL || a.n_out > 32 || a.k0 > KMAX || a.n_in > KMAX || a.n_panels < 1)
+    return -4;
+  const int waves = bf16 ? Cfg<true>::WAVES : Cfg<false>::WAVES;
+  const int n_tiles = (a.n_rows + 32 * waves - 1) / (32 * waves);
+  dim3 grid(min(n_tiles, n_cus()));
+  if (bf16) {
+    const size_t lds = lds_bytes<true>();
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(mlp_kernel<true>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return -5;
+    hipLaunchKernelGGL(mlp_kernel<true>, grid, dim3(64 * waves), lds, stream, a);
+  } else {
+    const size_t lds = lds_bytes<false>();
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(mlp_kernel<false>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return -5;
+    hipLaunchKernelGGL(mlp_kernel<false>, grid, dim3(64 * waves), lds, stream, a);
+  }
   return hipGetLastError() == hipSuccess ? 0 : -7;
 }

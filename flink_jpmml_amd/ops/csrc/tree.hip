@@ -296,9 +296,15 @@ PMML_API int pmml_tree_launch(hipStream_t stream, const TreeArgs* args, int layo
   int err = 0;
   const size_t acc_lds = a.general ? (size_t)a.C * TB * 4 : 0;
   if (layout == 0) {
-    if (a.n_feat > 64) return -4;
-    if ((a.variant & 3) == 0 && (size_t)a.chunk_trees * a.rec_words > (size_t)TB * 4 * PREFETCH_Q) return -9;
-    const size_t lds = (size_t)a.n_feat * TB * 4 + 2 * (size_t)a.chunk_trees * a.rec_words * 4 + (TB + 4) * 4 + acc_lds;
+    const bool wide = (a.variant & 3) != 0;
+    if (wide) {
+      if (a.n_stage < 1 || a.n_stage > 256 || !(a.rows_wide == 256 || a.rows_wide == 128 || a.rows_wide == 64)) return -4;
+      if ((size_t)a.n_stage * (a.rows_wide + 1) > 64 * 256 + 64) return -4;  // planes <= ~64 KiB
+    } else if (a.n_feat > 64) {
+      return -4;
+    }
+    if (!wide && (size_t)a.chunk_trees * a.rec_words > (size_t)TB * 4 * PREFETCH_Q) return -9;
+    const size_t lds = wide ? 0 : (size_t)a.n_feat * TB * 4 + 2 * (size_t)a.chunk_trees * a.rec_words * 4 + (TB + 4) * 4 + acc_lds;
     if (lds > 160 * 1024) return -5;
     switch (depth) {
       case 1: err = launch_perfect_d1(stream, a, grid, lds); break;

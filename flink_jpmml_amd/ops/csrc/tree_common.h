@@ -59,6 +59,11 @@ struct TreeArgs {
   float* partial;               // split mode: [splits][C+1][n_rows]
   const uint32_t* blob_nan;     // wide kernel, nullable: the records re-pointed at the NaN plane
   int chunk_trees_nan, pad1;    // (tiles with missing values; own chunk size, LDS holds 2 planes)
+  const float* tree_w;          // wide MODE_CLASS: per-tree vote weight (nullable = 1)
+  const float* acc_init;        // wide multi-class: per-class initial accumulator (nullable = 0)
+  const int* feat_map;          // wide kernel: staged column j -> X column (nullable = identity)
+  int rows_wide, mode;          // wide kernel: rows per workgroup (256/128/64), accumulation mode
+  int n_stage, pad2;            // wide kernel: staged feature columns
 };
 constexpr int VAR_NAN_FAST = 4;    // wide kernel: take the fast path even on tiles with missing values
 constexpr int VAR_NAN_PLANES = 8;  // ... via blob_nan + a second feature plane (NaN -> +inf)
@@ -297,13 +302,35 @@ __global__ __launch_bounds__(TB, 2) void tree_perfect_kernel(TreeArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------
-// v3: wide workgroup, tree-group parallel. 256 rows x G tree groups = 256*G threads (G=4: 16
-// waves, one workgroup per CU). Half-wave hw = 2*wave + (lane >= 32) owns row set hw % 8 (32
-// rows) and tree group hw / 8, so each 32-lane LDS access group reads 32 distinct rows (feature
-// reads conflict free) and both halves of a wave walk the same trees. Group g takes trees
-// k ≡ g (mod G) of every chunk; the G partial sums of a row are added in fixed order g = 0..G-1
-// (deterministic). Twice the resident waves of the v2 layout at the same LDS footprint: the
-// traversal is latency bound (SQ_WAIT_ANY ~49% of wave cycles in v2), so occupancy is the lever.
+// ------------------------------------------------------------------------------------------
+// Wide kernel (v4): one 1024-thread workgroup (16 waves) per ROWS-row tile, tree-group parallel.
+// Half-wave hw = 2*wave + (lane >= 32) owns row set hw % RS (32 rows, RS = ROWS/32) and tree
+// group g = hw / RS (G = 32/RS groups: 4 / 8 / 16 for ROWS = 256 / 128 / 64). Each 32-lane LDS
+// access group reads 32 distinct rows of one feature plane (conflict free); both halves of a wave
+// walk the same trees (g is wave-uniform). Group g takes trees k ≡ g (mod G) of every chunk; the
+// G partial results of a row are combined in fixed order (deterministic).
+//  * ROWS shrinks as the staged feature count grows (<= 64 / 128 / 256 columns): the feature
+//    planes stay <= 64 KiB and 16 waves stay resident; beyond that the POINTER layout takes over;
+//  * feature planes are [F][ROWS + 1] (one pad float per plane): the staging store of one row's
+//    consecutive features hits consecutive banks (it was a 32-way conflict with a [F][ROWS]
+//    image), the traversal read of one feature by 32 consecutive rows stays conflict free, and
+//    the pad is folded into the per-node feature byte offset (no extra VALU per level);
+//  * `feat_map` stages only the columns the trees use (compaction of wide records);
+//  * accumulation modes: SUM (regression / binary chain), SLOT (multi-class GBDT: each tree adds
+//    its leaf to one class slot — wave-uniform, contiguous runs), CLASS (majority vote: the leaf is
+//    a class index, the tree adds its weight to that class), VOTE8 (unweighted vote with <= 4
+//    classes: the leaf is a packed increment `1 << 8*class`, one integer add per tree).
+enum : int { MODE_SUM = 0, MODE_SLOT = 1, MODE_CLASS = 2, MODE_VOTE8 = 3 };
+constexpr int WIDE_T = 1024;
+constexpr int CMAX = 8;  // class slots of the multi-class wide modes
+
+template <int ROWS>
+struct WideGeom {
+  static constexpr int RS = ROWS / 32;  // row sets
+  static constexpr int G = 32 / RS;     // tree groups
+  static constexpr int PS = ROWS + 1;   // feature plane stride (floats)
+};
+
 #define PF4_DECL uint4 pq0, pq1, pq2, pq3;
 #define PF4_LOAD(SRC, N16, T)                                                          \
   {                                                                                    \
@@ -338,57 +365,82 @@ __device__ __forceinline__ float leaf8_select(uint32_t meta, bool right) {
   return right ? pr[1] : pr[0];
 }
 
-template <int DEPTH, bool MISSING, int ILP, int G, bool LEAF8>
-__device__ __forceinline__ float traverse_chunk_g(const TreeArgs& a, const uint32_t* buf, int nt, int g,
-                                                  const char* feat_lane, float acc) {
+// Per-thread accumulator of one accumulation mode. `t` is the (wave-uniform) global tree index.
+template <int MODE>
+struct WAcc;
+template <>
+struct WAcc<MODE_SUM> {
+  float s = 0.f;
+  __device__ __forceinline__ void add(const TreeArgs&, int, float v) { s += v; }
+  __device__ __forceinline__ void poison() { s = __builtin_nanf(""); }  // NaN sum -> EmptyScore
+  __device__ __forceinline__ bool poisoned() const { return false; }
+  __device__ __forceinline__ void finish() {}
+};
+template <>
+struct WAcc<MODE_VOTE8> {
+  uint32_t packed = 0u;
+  bool pz = false;
+  __device__ __forceinline__ void add(const TreeArgs&, int, float v) { packed += __float_as_uint(v); }
+  __device__ __forceinline__ void poison() { pz = true; }
+  __device__ __forceinline__ bool poisoned() const { return pz; }
+  __device__ __forceinline__ void finish() {}
+};
+template <>
+struct WAcc<MODE_CLASS> {
+  float c[CMAX];
+  bool pz = false;
+  __device__ __forceinline__ WAcc() {
+#pragma unroll
+    for (int k = 0; k < CMAX; ++k) c[k] = 0.f;
+  }
+  __device__ __forceinline__ void add(const TreeArgs& a, int t, float v) {
+    const float w = a.tree_w ? a.tree_w[t] : 1.f;
+#pragma unroll
+    for (int k = 0; k < CMAX; ++k) c[k] += (v == (float)k) ? w : 0.f;
+    pz = pz || (v != v);  // a leaf without a class: the segment's prediction is missing
+  }
+  __device__ __forceinline__ void poison() { pz = true; }
+  __device__ __forceinline__ bool poisoned() const { return pz; }
+  __device__ __forceinline__ void finish() {}
+};
+template <>
+struct WAcc<MODE_SLOT> {
+  float c[CMAX];
+  float run = 0.f;
+  int cur = 0;
+  bool pz = false;
+  __device__ __forceinline__ WAcc() {
+#pragma unroll
+    for (int k = 0; k < CMAX; ++k) c[k] = 0.f;
+  }
+  __device__ __forceinline__ void flush() {
+#pragma unroll
+    for (int k = 0; k < CMAX; ++k) c[k] += (k == cur) ? run : 0.f;
+    run = 0.f;
+  }
+  __device__ __forceinline__ void add(const TreeArgs& a, int t, float v) {
+    const int sl = __builtin_amdgcn_readfirstlane(a.tree_slot[t]);  // runs of equal slots
+    if (sl != cur) {
+      flush();
+      cur = sl;
+    }
+    run += v;
+  }
+  __device__ __forceinline__ void poison() { pz = true; }
+  __device__ __forceinline__ bool poisoned() const { return pz; }
+  __device__ __forceinline__ void finish() { flush(); }
+};
+
+// Missing-aware traversal of group g's trees of one chunk (per-node default-direction bits).
+template <int DEPTH, int ILP, int G, bool LEAF8, int MODE>
+__device__ __forceinline__ void traverse_chunk_g(const TreeArgs& a, const uint32_t* buf, int nt, int g, int t0,
+                                                 const char* feat_lane, WAcc<MODE>& acc) {
   constexpr int NI = (1 << DEPTH) - 1;
   constexpr int NL = 1 << DEPTH;
   const int rw = a.rec_words;
   const int dr_off = LEAF8 ? 2 * NI : 2 * NI + NL;
-  // my trees: k = g + G*m, m = 0..mt-1
   const int mt = (nt - g + G - 1) / G;
-  int m = 0;
-  for (; m + ILP <= mt; m += ILP) {
-    uint32_t j[ILP], pz[ILP];
-    float lf[ILP];
-    const char* base[ILP];
-#pragma unroll
-    for (int i = 0; i < ILP; ++i) {
-      j[i] = 1u;
-      pz[i] = 0u;
-      lf[i] = 0.f;
-      base[i] = reinterpret_cast<const char*>(buf + (g + G * (m + i)) * rw);
-    }
-#pragma unroll
-    for (int d = 0; d < DEPTH; ++d) {
-#pragma unroll
-      for (int i = 0; i < ILP; ++i) {
-        const uint2 nd = *reinterpret_cast<const uint2*>(base[i] - 8 + (j[i] << 3));
-        const uint32_t fo = (LEAF8 && d == DEPTH - 1) ? (nd.y & 0xFFFFu) : nd.y;
-        const float x = *reinterpret_cast<const float*>(feat_lane + fo);
-        uint32_t right = (x >= __uint_as_float(nd.x)) ? 1u : 0u;
-        if (MISSING) {
-          const uint32_t n = j[i] - 1u;
-          const uint32_t w = reinterpret_cast<const uint32_t*>(base[i])[dr_off + (n >> 5)];
-          const uint32_t isn = (x != x) ? 1u : 0u;
-          right |= isn & (w >> (n & 31u));
-          pz[i] |= isn;
-        }
-        if (LEAF8 && d == DEPTH - 1) {
-          lf[i] = leaf8_select(nd.y, right != 0u);
-        } else {
-          j[i] = j[i] + j[i] + right;
-        }
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < ILP; ++i) {
-      float v = LEAF8 ? lf[i] : (reinterpret_cast<const float*>(base[i] + NI * 8) - NL)[j[i]];
-      if (MISSING && pz[i] && null_flag<DEPTH>(base[i], dr_off)) v = __builtin_nanf("");
-      acc += v;
-    }
-  }
-  for (; m < mt; ++m) {
+  for (int m = 0; m < mt; ++m) {
     uint32_t j = 1u, pz = 0u;
     float lf = 0.f;
     const char* base = reinterpret_cast<const char*>(buf + (g + G * m) * rw);
@@ -398,36 +450,31 @@ __device__ __forceinline__ float traverse_chunk_g(const TreeArgs& a, const uint3
       const uint32_t fo = (LEAF8 && d == DEPTH - 1) ? (nd.y & 0xFFFFu) : nd.y;
       const float x = *reinterpret_cast<const float*>(feat_lane + fo);
       uint32_t right = (x >= __uint_as_float(nd.x)) ? 1u : 0u;
-      if (MISSING) {
-        const uint32_t n = j - 1u;
-        const uint32_t w = reinterpret_cast<const uint32_t*>(base)[dr_off + (n >> 5)];
-        const uint32_t isn = (x != x) ? 1u : 0u;
-        right |= isn & (w >> (n & 31u));
-        pz |= isn;
-      }
+      const uint32_t n = j - 1u;
+      const uint32_t w = reinterpret_cast<const uint32_t*>(base)[dr_off + (n >> 5)];
+      const uint32_t isn = (x != x) ? 1u : 0u;
+      right |= isn & (w >> (n & 31u));
+      pz |= isn;
       if (LEAF8 && d == DEPTH - 1) {
         lf = leaf8_select(nd.y, right != 0u);
       } else {
         j = j + j + right;
       }
     }
-    float v = LEAF8 ? lf : (reinterpret_cast<const float*>(base + NI * 8) - NL)[j];
-    if (MISSING && pz && null_flag<DEPTH>(base, dr_off)) v = __builtin_nanf("");
-    acc += v;
+    const float v = LEAF8 ? lf : (reinterpret_cast<const float*>(base + NI * 8) - NL)[j];
+    if (pz && null_flag<DEPTH>(base, dr_off)) acc.poison();
+    else acc.add(a, t0 + g + G * m, v);
   }
-  return acc;
 }
 
-// Fast path of the wide kernel (tile without missing values), written against explicit LDS byte
-// addresses so the per-level work is exactly: node ds_read_b64, feature address add, feature
-// ds_read_b32, v_cmp, v_cndmask, v_lshl_add — 4 VALU per level (the plain heap-index form
-// compiled to ~7.5 as hipcc re-expanded `j = 2j + r` into shifted bit sums).
+// Fast path (tile without missing values, or missing values routed by the NaN plane), written
+// against explicit LDS byte addresses so the per-level work is: node ds_read_b64, feature address
+// add, feature ds_read_b32, v_cmp, v_cndmask, v_lshl_add.
 //  * u = LDS address of the current node of tree i minus i*TS (TS = compile-time tree stride of a
 //    tree group, folded into the ds_read immediate offset); children: u' = 2u + (8 - b0) + 8r.
 //  * last level, fp32 leaves: the two leaves under a node are adjacent, so the leaf PAIR (one
-//    conflict-free ds_read_b64 at u + C, C folded into the offset) is fetched together with the
-//    feature and the final compare only selects between them — one dependent LDS round trip less
-//    per tree, and no 2-way bank conflicts of scattered ds_read_b32 leaf reads;
+//    ds_read_b64 at u + C, C folded into the offset) is fetched together with the feature and the
+//    final compare only selects between them;
 //  * last level, fp8 leaves: the pair is already in the node's meta word (no leaf read at all).
 // `__asm__("" : "+v"(...))` pins values in VGPRs so the compiler cannot re-derive them.
 typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
@@ -444,7 +491,7 @@ __device__ __forceinline__ float lds_ldf(uint32_t a) { return *(lds_f_t*)(uintpt
 
 // N trees of group g starting at its m-th tree, N independent walks interleaved (ILP).
 template <int DEPTH, int N, int G, bool LEAF8>
-__device__ __forceinline__ float fast_batch(uint32_t lds0, int g, int m, uint32_t feat_lane, float acc) {
+__device__ __forceinline__ void fast_batch(uint32_t lds0, int g, int m, uint32_t feat_lane, float (&v)[N]) {
   constexpr int NI = (1 << DEPTH) - 1;
   constexpr int NL = 1 << DEPTH;
   constexpr uint32_t RB = 4u * (LEAF8 ? perfect_rec_words8(DEPTH) : perfect_rec_words(DEPTH, 1));  // record bytes
@@ -475,59 +522,68 @@ __device__ __forceinline__ float fast_batch(uint32_t lds0, int g, int m, uint32_
     if (LEAF8) {
       const uint2 nd = lds_ld2(u[i] + i * TS);
       const float x = lds_ldf(feat_lane + (nd.y & 0xFFFFu));
-      acc += leaf8_select(nd.y, x >= __uint_as_float(nd.x));
+      v[i] = leaf8_select(nd.y, x >= __uint_as_float(nd.x));
     } else {
       uint32_t ul = u[i] + C;
       __asm__ volatile("" : "+v"(ul));  // keep the pair read out of a ds_read2_b64 with the node
       const uint2 nd = lds_ld2(u[i] + i * TS);
       const uint2 lv = lds_ld2(ul + i * TS);
       const float x = lds_ldf(feat_lane + nd.y);
-      acc += (x >= __uint_as_float(nd.x)) ? __uint_as_float(lv.y) : __uint_as_float(lv.x);
+      v[i] = (x >= __uint_as_float(nd.x)) ? __uint_as_float(lv.y) : __uint_as_float(lv.x);
     }
   }
-  return acc;
+}
+
+template <int DEPTH, int N, int G, bool LEAF8, int MODE>
+__device__ __forceinline__ void fast_batch_acc(const TreeArgs& a, uint32_t lds0, int g, int m, int t0,
+                                               uint32_t feat_lane, WAcc<MODE>& acc) {
+  float v[N];
+  fast_batch<DEPTH, N, G, LEAF8>(lds0, g, m, feat_lane, v);
+#pragma unroll
+  for (int i = 0; i < N; ++i) acc.add(a, t0 + g + G * (m + i), v[i]);
 }
 
 // The group's trees in ILP-wide batches; the remainder in 4/2/1-wide batches (a plain serial
 // tail is latency bound: one dependent LDS round trip per level and tree).
-template <int DEPTH, int ILP, int G, bool LEAF8>
-__device__ __forceinline__ float traverse_fast_g(const uint32_t* buf, int nt, int g, uint32_t feat_lane,
-                                                 float acc) {
+template <int DEPTH, int ILP, int G, bool LEAF8, int MODE>
+__device__ __forceinline__ void traverse_fast_g(const TreeArgs& a, const uint32_t* buf, int nt, int g, int t0,
+                                                uint32_t feat_lane, WAcc<MODE>& acc) {
   const uint32_t lds0 = lds_addr(buf);
   const int mt = (nt - g + G - 1) / G;
   int m = 0;
-  for (; m + ILP <= mt; m += ILP) acc = fast_batch<DEPTH, ILP, G, LEAF8>(lds0, g, m, feat_lane, acc);
+  for (; m + ILP <= mt; m += ILP) fast_batch_acc<DEPTH, ILP, G, LEAF8, MODE>(a, lds0, g, m, t0, feat_lane, acc);
   if (ILP > 4 && m + 4 <= mt) {
-    acc = fast_batch<DEPTH, 4, G, LEAF8>(lds0, g, m, feat_lane, acc);
+    fast_batch_acc<DEPTH, 4, G, LEAF8, MODE>(a, lds0, g, m, t0, feat_lane, acc);
     m += 4;
   }
   if (m + 2 <= mt) {
-    acc = fast_batch<DEPTH, 2, G, LEAF8>(lds0, g, m, feat_lane, acc);
+    fast_batch_acc<DEPTH, 2, G, LEAF8, MODE>(a, lds0, g, m, t0, feat_lane, acc);
     m += 2;
   }
-  if (m < mt) acc = fast_batch<DEPTH, 1, G, LEAF8>(lds0, g, m, feat_lane, acc);
-  return acc;
+  if (m < mt) fast_batch_acc<DEPTH, 1, G, LEAF8, MODE>(a, lds0, g, m, t0, feat_lane, acc);
 }
 
-template <int DEPTH, int ILP, int G, bool LEAF8>
-__global__ __launch_bounds__(TB * G, 1) void tree_perfect_wide_kernel(TreeArgs a) {
-  constexpr int T = TB * G;
+template <int DEPTH, int ILP, int ROWS, bool LEAF8, int MODE>
+__global__ __launch_bounds__(WIDE_T, 1) void tree_perfect_wide_kernel(TreeArgs a) {
+  using WG = WideGeom<ROWS>;
+  constexpr int G = WG::G, RS = WG::RS, PS = WG::PS, T = WIDE_T;
   extern __shared__ __align__(16) uint32_t smem[];
   const int rw = a.rec_words;
-  // LDS: [bad TB][flag 4][part G x TB][feature plane(s)][two chunk buffers]. A tile with missing
-  // values and a NaN blob gets two planes (the second NaN -> +inf) and that blob's chunk size;
-  // any other tile one plane and the main blob — the layout is chosen per workgroup.
+  // LDS: [bad ROWS][flag 4][part G x ROWS][feature plane(s) F x PS][two chunk buffers]. A tile
+  // with missing values and a NaN blob gets two planes (the second NaN -> +inf) and that blob's
+  // chunk size; any other tile one plane and the main blob — chosen per workgroup.
   int* bad = reinterpret_cast<int*>(smem);
-  int* any_missing = bad + TB;
-  float* part = reinterpret_cast<float*>(bad + TB + 4);  // [G][TB]
-  float* feat = part + G * TB;
+  int* any_missing = bad + ROWS;
+  float* part = reinterpret_cast<float*>(bad + ROWS + 4);  // [G][ROWS]
+  float* feat = part + G * ROWS;
+  const int F = a.n_stage;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int hw = (tid >> 6) * 2 + (lane >> 5);
-  const int r_local = 32 * (hw & 7) + (lane & 31);
-  const int g = hw >> 3;
-  const int row0 = blockIdx.x * TB;
+  const int r_local = 32 * (hw % RS) + (lane & 31);
+  const int g = __builtin_amdgcn_readfirstlane(hw / RS);  // both halves of a wave: same group
+  const int row0 = blockIdx.x * ROWS;
   const int split = blockIdx.y;
   const int tb = split * a.trees_per_split;
   const int te = min(a.n_trees, tb + a.trees_per_split);
@@ -537,11 +593,10 @@ __global__ __launch_bounds__(TB * G, 1) void tree_perfect_wide_kernel(TreeArgs a
   PF4_LOAD(n16 > 0 ? a.blob + (size_t)tb * rw : a.blob, n16, T)  // speculative: main blob
 
   if (tid == 0) *any_missing = 0;
-  if (tid < TB) bad[tid] = 0;
+  if (tid < ROWS) bad[tid] = 0;
   __syncthreads();
   {
-    const int F = a.n_feat;
-    const int total = TB * F;
+    const int total = ROWS * F;
     bool miss = false;
     for (int e = tid; e < total; e += T) {
       const int r = e / F;
@@ -550,11 +605,12 @@ __global__ __launch_bounds__(TB * G, 1) void tree_perfect_wide_kernel(TreeArgs a
       float x = 0.f;
       bool b = false;
       if (row < a.n_rows) {
-        x = a.X[(size_t)row * a.ldx + f];
-        if (a.prep) x = prep_value(x, a.prep[f], &b);
+        const int col = a.feat_map ? a.feat_map[f] : f;
+        x = a.X[(size_t)row * a.ldx + col];
+        if (a.prep) x = prep_value(x, a.prep[col], &b);
         miss = miss || (x != x);
       }
-      feat[f * TB + r] = x;
+      feat[f * PS + r] = x;
       if (b) bad[r] = 1;
     }
     if (__any(miss) && lane == 0) *any_missing = 1;
@@ -564,11 +620,11 @@ __global__ __launch_bounds__(TB * G, 1) void tree_perfect_wide_kernel(TreeArgs a
   const bool use_nan = has_missing && a.blob_nan != nullptr;
   const uint32_t* blob = use_nan ? a.blob_nan : a.blob;
   const int chunk = use_nan ? a.chunk_trees_nan : a.chunk_trees;
-  uint32_t* tbuf0 = reinterpret_cast<uint32_t*>(feat + (use_nan ? 2 : 1) * a.n_feat * TB);
+  uint32_t* tbuf0 = reinterpret_cast<uint32_t*>(feat + (use_nan ? 2 : 1) * F * PS);
   uint32_t* tbuf1 = tbuf0 + chunk * rw;
   if (use_nan) {
-    const int total = TB * a.n_feat;
-    for (int e = tid; e < total; e += T) {  // NaN-goes-right plane
+    const int total = PS * F;
+    for (int e = tid; e < total; e += T) {  // NaN-goes-right plane (pads copied along)
       const float x = feat[e];
       feat[total + e] = (x != x) ? __builtin_inff() : x;
     }
@@ -581,7 +637,7 @@ __global__ __launch_bounds__(TB * G, 1) void tree_perfect_wide_kernel(TreeArgs a
   // VAR_NAN_FAST: missing values need no per-node work — either no node sends NaN right (a NaN
   // compare is false: left), or the node's feature offset points into the NaN -> +inf plane
   const bool missing = has_missing && (a.variant & VAR_NAN_FAST) == 0;
-  float acc = 0.f;
+  WAcc<MODE> acc;
   const char* feat_lane = reinterpret_cast<const char*>(feat + r_local);
   int c = 0;
   for (int t0 = tb; t0 < te; t0 += chunk, ++c) {
@@ -592,31 +648,80 @@ __global__ __launch_bounds__(TB * G, 1) void tree_perfect_wide_kernel(TreeArgs a
     n16 = (t1 < te) ? (min(chunk, te - t1) * rw) >> 2 : 0;
     PF4_LOAD(n16 > 0 ? blob + (size_t)t1 * rw : blob, n16, T)
     if (missing) {
-      acc = traverse_chunk_g<DEPTH, true, ILP, G, LEAF8>(a, cur, nt, g, feat_lane, acc);
+      traverse_chunk_g<DEPTH, ILP, G, LEAF8, MODE>(a, cur, nt, g, t0, feat_lane, acc);
     } else {
-      acc = traverse_fast_g<DEPTH, ILP, G, LEAF8>(cur, nt, g, lds_addr(feat + r_local), acc);
+      traverse_fast_g<DEPTH, ILP, G, LEAF8, MODE>(a, cur, nt, g, t0, lds_addr(feat + r_local), acc);
     }
     PF4_STORE(nxt, n16, T)
     __syncthreads();
   }
-  part[g * TB + r_local] = acc;
-  __syncthreads();
-  if (g == 0) {
-    float sum = part[r_local];
+  acc.finish();
+  if (acc.poisoned()) bad[r_local] = 1;  // a null tree invalidates a multi-class row
+  const int row = row0 + r_local;
+  if constexpr (MODE == MODE_SUM) {
+    part[g * ROWS + r_local] = acc.s;
+    __syncthreads();
+    if (g == 0) {
+      float sum = part[r_local];
 #pragma unroll
-    for (int q = 1; q < G; ++q) sum += part[q * TB + r_local];
-    const int row = row0 + r_local;
-    bool row_ok = bad[r_local] == 0;
-    if (a.row_valid_in && row < a.n_rows) row_ok = row_ok && a.row_valid_in[row];
-    if (row < a.n_rows) {
-      if (a.partial) {
-        const size_t stride = (size_t)a.n_rows;
-        float* pbase = a.partial + (size_t)split * 2 * stride;
-        pbase[row] = sum;
-        pbase[stride + row] = row_ok ? 0.f : 1.f;
-      } else {
-        apply_epilogue(a.epi, [&](int) { return sum; }, row_ok, row, a.n_rows, a.score, a.valid, a.probs);
+      for (int q = 1; q < G; ++q) sum += part[q * ROWS + r_local];
+      bool row_ok = bad[r_local] == 0;
+      if (a.row_valid_in && row < a.n_rows) row_ok = row_ok && a.row_valid_in[row];
+      if (row < a.n_rows) {
+        if (a.partial) {
+          const size_t stride = (size_t)a.n_rows;
+          float* pbase = a.partial + (size_t)split * 2 * stride;
+          pbase[row] = sum;
+          pbase[stride + row] = row_ok ? 0.f : 1.f;
+        } else {
+          apply_epilogue(a.epi, [&](int) { return sum; }, row_ok, row, a.n_rows, a.score, a.valid, a.probs);
+        }
       }
+    }
+  } else {
+    float tot[CMAX];
+#pragma unroll
+    for (int k = 0; k < CMAX; ++k) tot[k] = 0.f;
+    if constexpr (MODE == MODE_VOTE8) {
+      reinterpret_cast<uint32_t*>(part)[g * ROWS + r_local] = acc.packed;
+      __syncthreads();
+      if (g == 0) {
+#pragma unroll
+        for (int q = 0; q < G; ++q) {
+          const uint32_t pk = reinterpret_cast<const uint32_t*>(part)[q * ROWS + r_local];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) tot[k] += (float)((pk >> (8 * k)) & 0xFFu);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < CMAX; ++k) {
+        if (k < a.C) {  // uniform
+          part[g * ROWS + r_local] = acc.c[k];
+          __syncthreads();
+          if (g == 0) {
+#pragma unroll
+            for (int q = 0; q < G; ++q) tot[k] += part[q * ROWS + r_local];
+          }
+          __syncthreads();
+        }
+      }
+    }
+    if (g == 0 && row < a.n_rows) {
+      if (a.acc_init) {
+#pragma unroll
+        for (int k = 0; k < CMAX; ++k)
+          if (k < a.C) tot[k] += a.acc_init[k];
+      }
+      bool row_ok = bad[r_local] == 0;
+      if (a.row_valid_in) row_ok = row_ok && a.row_valid_in[row];
+      auto sel = [&](int cls) {
+        float r = tot[0];
+#pragma unroll
+        for (int k = 1; k < CMAX; ++k) r = (cls == k) ? tot[k] : r;
+        return r;
+      };
+      apply_epilogue(a.epi, sel, row_ok, row, a.n_rows, a.score, a.valid, a.probs);
     }
   }
 }
@@ -631,35 +736,55 @@ int prepare_launch(K kernel, size_t lds) {
   return 0;
 }
 
-constexpr int WIDE_G = 4;
+template <int D, int ROWS, bool LEAF8, int MODE>
+int launch_wide(hipStream_t st, const TreeArgs& a, size_t lds_w) {
+  using WG = WideGeom<ROWS>;
+  dim3 grid((a.n_rows + ROWS - 1) / ROWS, (a.n_trees + a.trees_per_split - 1) / a.trees_per_split);
+  (void)WG::G;
+  auto k = tree_perfect_wide_kernel<D, 8, ROWS, LEAF8, MODE>;
+  int err = prepare_launch(k, lds_w);
+  if (!err) hipLaunchKernelGGL(k, grid, dim3(WIDE_T), lds_w, st, a);
+  return err;
+}
 
 template <int D>
 int launch_perfect(hipStream_t st, const TreeArgs& a, dim3 grid, size_t lds) {
   int err = 0;
   const int base = a.variant & 3;
-  if (!a.general && (base == 1 || base == 2)) {
+  if (base == 1 || base == 2) {
     const bool leaf8 = base == 2;
-    (void)lds;
-    const size_t head = (size_t)(TB + 4) * 4 + (size_t)WIDE_G * TB * 4;
-    const size_t plane = (size_t)a.n_feat * TB * 4;
+    const int rows = a.rows_wide;
+    const int G = WIDE_T / rows;
+    const size_t head = (size_t)(rows + 4) * 4 + (size_t)G * rows * 4;
+    const size_t plane = (size_t)a.n_stage * (rows + 1) * 4;
     size_t lds_w = head + plane + 2 * (size_t)a.chunk_trees * a.rec_words * 4;
-    if ((size_t)a.chunk_trees * a.rec_words > (size_t)TB * WIDE_G * 4 * 4) return -9;
+    if ((size_t)a.chunk_trees * a.rec_words > (size_t)WIDE_T * 4 * 4) return -9;
     if (a.blob_nan) {
-      if (a.chunk_trees_nan < 1 || (size_t)a.chunk_trees_nan * a.rec_words > (size_t)TB * WIDE_G * 4 * 4) return -9;
+      if (a.chunk_trees_nan < 1 || (size_t)a.chunk_trees_nan * a.rec_words > (size_t)WIDE_T * 4 * 4) return -9;
       lds_w = max(lds_w, head + 2 * plane + 2 * (size_t)a.chunk_trees_nan * a.rec_words * 4);
     }
     if (lds_w > 160 * 1024) return -5;
     if (a.P != 1 || a.rec_words != (leaf8 ? perfect_rec_words8(D) : perfect_rec_words(D, 1))) return -10;
-    if (leaf8) {
-      err = prepare_launch(tree_perfect_wide_kernel<D, 8, WIDE_G, true>, lds_w);
-      if (!err)
-        hipLaunchKernelGGL((tree_perfect_wide_kernel<D, 8, WIDE_G, true>), grid, dim3(TB * WIDE_G), lds_w, st, a);
-    } else {
-      err = prepare_launch(tree_perfect_wide_kernel<D, 8, WIDE_G, false>, lds_w);
-      if (!err)
-        hipLaunchKernelGGL((tree_perfect_wide_kernel<D, 8, WIDE_G, false>), grid, dim3(TB * WIDE_G), lds_w, st, a);
+    if (a.mode != MODE_SUM && (a.partial || a.C > CMAX || (a.mode == MODE_VOTE8 && a.C > 4) || leaf8)) return -11;
+    if (a.mode == MODE_SLOT && !a.tree_slot) return -11;
+    (void)grid;
+    (void)lds;
+#define PMML_WIDE_ROWS(R)                                                                     \
+    if (rows == R) {                                                                          \
+      switch (a.mode) {                                                                       \
+        case MODE_SUM: return leaf8 ? launch_wide<D, R, true, MODE_SUM>(st, a, lds_w)         \
+                                    : launch_wide<D, R, false, MODE_SUM>(st, a, lds_w);       \
+        case MODE_SLOT: return launch_wide<D, R, false, MODE_SLOT>(st, a, lds_w);             \
+        case MODE_CLASS: return launch_wide<D, R, false, MODE_CLASS>(st, a, lds_w);           \
+        case MODE_VOTE8: return launch_wide<D, R, false, MODE_VOTE8>(st, a, lds_w);           \
+        default: return -11;                                                                  \
+      }                                                                                       \
     }
-    return err;
+    PMML_WIDE_ROWS(256)
+    PMML_WIDE_ROWS(128)
+    PMML_WIDE_ROWS(64)
+#undef PMML_WIDE_ROWS
+    return -12;
   }
   if (base == 2 || (a.variant & ~3)) return -10;  // fp8 leaves / NaN planes: wide kernel only
   if (a.general) {

@@ -22,7 +22,8 @@ from .plans import EPI_AFFINE, LINKS, DevicePlan, NotLowerable, _addr, _epilogue
 ACT_CODES = {"identity": 0, "logistic": 1, "tanh": 2, "rectifier": 3, "exponential": 4, "reciprocal": 5,
              "square": 6, "Gauss": 7, "sine": 8, "cosine": 9, "Elliott": 10, "arctan": 11, "threshold": 12}
 MT = 8  # max 32-unit tiles per layer (mirrors csrc/mlp.hip)
-MAXL = 4
+MAXL = 8  # max layers of the fused kernel
+KMAX = 256  # max inputs per layer
 
 
 def _affine_of(ex) -> Tuple[float, float, float]:
@@ -38,6 +39,24 @@ def _affine_of(ex) -> Tuple[float, float, float]:
         miss = float(ex.map_missing_to) if ex.map_missing_to is not None else float("nan")
         return sc, n0 - o0 * sc, miss
     raise NotLowerable(f"NeuralInput expression {type(ex).__name__} is host-only")
+
+
+def mlp_panels(meta, precision: str) -> np.ndarray:
+    """The fused kernel's weight-panel schedule: one ``(offset, size)`` pair (16-byte units) per
+    (layer, 32-unit output tile), in consumption order — every panel holds all k-step fragments
+    of one output tile (``csrc/mlp.hip``)."""
+    bf16 = precision == "bf16"
+    esize, per_step = (2, 8) if bf16 else (4, 1)  # bytes per element, elements per lane per k-step
+    out = []
+    for kp, mp, _, w_off, _ in meta:
+        ksteps = kp // (16 if bf16 else 2)
+        tile_elems = ksteps * 64 * per_step
+        for t in range(mp // 32):
+            off = (w_off + t * tile_elems) * esize
+            size = tile_elems * esize
+            assert off % 16 == 0 and size % 16 == 0
+            out.append((off // 16, size // 16))
+    return np.array(out, dtype=np.int32)
 
 
 def pack_mlp_weights(layers: List[Tuple[np.ndarray, np.ndarray]], precision: str):
@@ -102,9 +121,9 @@ class MlpPlan(DevicePlan):
     supports_direct = True
     _STATE = DevicePlan._STATE + ("weights", "biases", "layer_meta", "in_scale", "in_shift", "in_missing", "in_index",
                                   "n_in", "k0", "n_layers", "bf16", "out_a", "out_b", "final_norm", "n_out", "table",
-                                  "is_classification")
+                                  "is_classification", "panels", "n_panels", "contiguous")
 
-    def __init__(self, compiled, device, precision: str = "bf16"):
+    def __init__(self, compiled, device, precision: str = "fp32"):
         import torch
 
         super().__init__(compiled, device)
@@ -112,8 +131,37 @@ class MlpPlan(DevicePlan):
         if precision not in ("bf16", "fp32"):
             raise ValueError("precision must be bf16 or fp32")
         self.bf16 = 1 if precision == "bf16" else 0
+        layers, index = self._io(compiled, ev)
+        if len(layers) > MAXL:
+            raise NotLowerable(f"{len(layers)} layers > {MAXL} (fused kernel)")
+        for W, b, act, thr, norm in layers:
+            if W.shape[1] > 32 * MT:
+                raise NotLowerable(f"layers wider than {32 * MT} units (fused kernel)")
+        if self.n_in > KMAX:
+            raise NotLowerable(f"more than {KMAX} inputs (fused kernel)")
+        if self.n_out > 32:
+            raise NotLowerable("more than 32 output neurons (fused kernel)")
+        w, bias, meta = pack_mlp_weights([(W, b) for W, b, *_ in layers], precision)
+        pan = mlp_panels(meta, precision)
+        self.panels = self._t(pan.reshape(-1))
+        self.n_panels = int(len(pan))
+        identity = index == list(range(len(index)))
+        self.contiguous = 1 if identity and self.n_in == meta[0][0] else 0
+        self.n_layers = len(layers)
+        lm = np.zeros((self.n_layers, 8), dtype=np.int32)
+        for i, ((kp, mp, mreal, wo, bo), (_, _, act, thr, _)) in enumerate(zip(meta, layers)):
+            lm[i, :6] = [kp, mp, mreal, wo, bo, ACT_CODES[act]]
+            lm[i, 6] = np.float32(thr).view(np.int32)
+        self.k0 = meta[0][0]
+        wt = torch.from_numpy(w.astype(np.float32))
+        self.weights = (wt.to(torch.bfloat16) if self.bf16 else wt).to(self.device)
+        self.biases = self._t(bias.astype(np.float32))
+        self.layer_meta = self._t(lm)
+
+    def _io(self, compiled, ev):
+        """Inputs (NormContinuous affine maps, missing replacements, active-field index), the
+        dense layers, output normalisation and the target decode. Returns ``(layers, index)``."""
         nn = ev.nn
-        # inputs
         scales, shifts, misses, index = [], [], [], []
         for inp in nn.inputs:
             ex = inp.derived.expression
@@ -127,28 +175,11 @@ class MlpPlan(DevicePlan):
             index.append(compiled.active_fields.index(field))
         self.n_in = len(index)
         layers = ev.dense_layers()
-        if len(layers) > MAXL:
-            raise NotLowerable(f"{len(layers)} layers > {MAXL}")
         for i, (W, b, act, thr, norm) in enumerate(layers):
             if act not in ACT_CODES:
                 raise NotLowerable(f"activation {act!r}")
-            if W.shape[1] > 32 * MT:
-                raise NotLowerable("layers wider than 256 units are host-only")
             if norm not in (None, "none") and i != len(layers) - 1:
                 raise NotLowerable("hidden-layer normalisation is host-only")
-        if self.n_in > 256:
-            raise NotLowerable("more than 256 inputs")
-        w, bias, meta = pack_mlp_weights([(W, b) for W, b, *_ in layers], precision)
-        self.n_layers = len(layers)
-        lm = np.zeros((self.n_layers, 8), dtype=np.int32)
-        for i, ((kp, mp, mreal, wo, bo), (_, _, act, thr, _)) in enumerate(zip(meta, layers)):
-            lm[i, :6] = [kp, mp, mreal, wo, bo, ACT_CODES[act]]
-            lm[i, 6] = np.float32(thr).view(np.int32)
-        self.k0 = meta[0][0]
-        wt = torch.from_numpy(w.astype(np.float32))
-        self.weights = (wt.to(torch.bfloat16) if self.bf16 else wt).to(self.device)
-        self.biases = self._t(bias.astype(np.float32))
-        self.layer_meta = self._t(lm)
         self.in_scale = self._t(np.array(scales, np.float32))
         self.in_shift = self._t(np.array(shifts, np.float32))
         self.in_missing = self._t(np.array(misses, np.float32))
@@ -158,8 +189,6 @@ class MlpPlan(DevicePlan):
         if self.final_norm is None:
             raise NotLowerable(f"output normalisation {last_norm!r}")
         self.n_out = layers[-1][0].shape[1]
-        if self.n_out > 32:
-            raise NotLowerable("more than 32 output neurons")
         out_neurons = [n.id for n in nn.layers[-1].neurons]
         self.is_classification = ev.kind == "classification"
         if self.is_classification:
@@ -190,6 +219,7 @@ class MlpPlan(DevicePlan):
                 a, b = a * tgt.rescale_factor, b * tgt.rescale_factor + tgt.rescale_constant
             self.out_a, self.out_b = a, b
             self.table = None
+        return layers, index
 
     def launch(self, X, score, valid, stream=None, probs=None, score2=None, valid2=None) -> None:
         import ctypes
@@ -203,10 +233,91 @@ class MlpPlan(DevicePlan):
         a.in_index, a.n_in, a.k0 = ptr(self.in_index), self.n_in, self.k0
         a.weights, a.biases, a.layers = ptr(self.weights), ptr(self.biases), ptr(self.layer_meta)
         a.out_scale, a.out_shift, a.final_norm, a.n_out = self.out_a, self.out_b, self.final_norm, self.n_out
+        a.panels, a.n_panels, a.contiguous = ptr(self.panels), self.n_panels, self.contiguous
         a.epi = _epilogue(mode=EPI_AFFINE, a=self.out_a, b=self.out_b, table=self.table)
         a.epi.score2, a.epi.valid2 = _addr(score2), _addr(valid2)
         a.score, a.valid, a.probs = _addr(score), _addr(valid), ptr(probs)
         check(self.lib.pmml_mlp_launch(stream_handle(stream), ctypes.byref(a), self.bf16), "mlp kernel")
+
+
+_TORCH_ACT = {
+    0: lambda z, t: z, 1: lambda z, t: z.sigmoid(), 2: lambda z, t: z.tanh(), 3: lambda z, t: z.clamp_min(0.0),
+    4: lambda z, t: z.exp(), 5: lambda z, t: z.reciprocal(), 6: lambda z, t: z * z,
+    7: lambda z, t: (-z * z).exp(), 8: lambda z, t: z.sin(), 9: lambda z, t: z.cos(),
+    10: lambda z, t: z / (1.0 + z.abs()), 11: lambda z, t: z.atan() * 0.63661977236758134,
+    12: lambda z, t: (z > t).to(z.dtype),
+}
+
+
+class GemmMlpPlan(MlpPlan):
+    """NeuralNetworks beyond the fused kernel's register budget (more than 8 layers, 256 units per
+    layer, 256 inputs or 32 outputs): every layer is one library GEMM on the matrix cores
+    (``torch.addmm`` → hipBLASLt, fp32 or bf16 operands with fp32 accumulation) and the activations
+    round-trip through HBM; input normalisation, activations, output normalisation and the target
+    decode run as torch element-wise ops on the same stream. Slower than the fused kernel but no
+    width / depth limit and no host fallback."""
+
+    kind = "mlp_gemm"
+    supports_direct = False
+    _STATE = DevicePlan._STATE + ("in_scale", "in_shift", "in_missing", "in_index", "n_in", "bf16", "out_a", "out_b",
+                                  "final_norm", "n_out", "table", "is_classification", "gemm_w", "gemm_b",
+                                  "acts", "n_layers")
+
+    def __init__(self, compiled, device, precision: str = "fp32"):
+        import torch
+
+        DevicePlan.__init__(self, compiled, device)
+        ev: NeuralEvaluator = compiled.evaluator
+        if precision not in ("bf16", "fp32"):
+            raise ValueError("precision must be bf16 or fp32")
+        self.bf16 = 1 if precision == "bf16" else 0
+        layers, _ = self._io(compiled, ev)
+        dt = torch.bfloat16 if self.bf16 else torch.float32
+        self.n_layers = len(layers)
+        # one flat buffer per kind (replicable as plan state): W_l stored [in, out] back to back
+        self.gemm_w = torch.cat([torch.from_numpy(np.ascontiguousarray(W, np.float32)).reshape(-1)
+                                 for W, *_ in layers]).to(dt).to(self.device)
+        self.gemm_b = self._t(np.concatenate([np.asarray(b, np.float32) for _, b, *_ in layers]))
+        self.acts = [(int(W.shape[0]), int(W.shape[1]), ACT_CODES[act], float(thr)) for W, b, act, thr, _ in layers]
+
+    def launch(self, X, score, valid, stream=None, probs=None, score2=None, valid2=None) -> None:
+        import torch
+
+        ctx = torch.cuda.stream(stream) if stream is not None else torch.cuda.stream(torch.cuda.current_stream())
+        with ctx:
+            x = X.index_select(1, self.in_index.long())
+            miss = torch.isnan(x)
+            v = torch.where(miss, self.in_missing.expand_as(x), x * self.in_scale + self.in_shift)
+            ok = ~torch.isnan(v).any(dim=1)
+            h = torch.nan_to_num(v, nan=0.0)
+            wo = bo = 0
+            for k, m, act, thr in self.acts:
+                W = self.gemm_w[wo: wo + k * m].view(k, m)
+                b = self.gemm_b[bo: bo + m]
+                wo += k * m
+                bo += m
+                z = torch.addmm(b.to(W.dtype), h.to(W.dtype), W).float()
+                h = _TORCH_ACT[act](z, thr)
+            if self.is_classification:
+                if self.final_norm == 1:
+                    p = torch.softmax(h, dim=1)
+                elif self.final_norm == 2:
+                    p = h / h.sum(dim=1, keepdim=True)
+                else:
+                    p = h
+                lab = torch.argmax(torch.nan_to_num(p, nan=-float("inf")), dim=1)
+                s = self.table[lab]
+                ok = ok & ~torch.isnan(p).any(dim=1) & ~torch.isnan(s)
+                if probs is not None:
+                    probs.copy_(p)
+            else:
+                s = self.out_a * h[:, 0] + self.out_b
+                ok = ok & torch.isfinite(s)
+            s = torch.where(ok, s, torch.full_like(s, float("nan")))
+            for so, vo in ((score, valid), (score2, valid2)):
+                if so is not None and not isinstance(so, int):
+                    so.copy_(s)
+                    vo.copy_(ok.to(torch.uint8))
 
 
 class SvmPlan(DevicePlan):

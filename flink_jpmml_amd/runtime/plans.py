@@ -16,6 +16,7 @@ oracle is documented per test.
 
 from __future__ import annotations
 
+import dataclasses
 import logging
 import math
 from dataclasses import dataclass
@@ -184,6 +185,24 @@ def build_field_prep(compiled, fields: List[str]) -> Tuple[np.ndarray, bool]:
 # --------------------------------------------------------------------------- plan base
 
 
+_DRY_RUN = 0
+
+
+class lowering_dry_run:
+    """Context manager: build plans on ``device="cpu"`` without the HIP library, so CPU tests can
+    inspect a plan's lowering decisions and emulate its kernel on the packed tensors."""
+
+    def __enter__(self):
+        global _DRY_RUN
+        _DRY_RUN += 1
+        return self
+
+    def __exit__(self, *exc):
+        global _DRY_RUN
+        _DRY_RUN -= 1
+        return False
+
+
 class DevicePlan:
     kind = "base"
     supports_direct = False  # kernel can write zero-copy host outputs + device mirror
@@ -195,9 +214,12 @@ class DevicePlan:
 
         self.compiled = compiled
         self.device = torch.device(device)
-        if self.device.type != "cuda":
+        if self.device.type == "cpu" and _DRY_RUN:
+            self.lib = None  # lowering only: tensors stay on the host, launch() is unavailable
+        elif self.device.type != "cuda":
             raise ValueError(f"device plans need a cuda (HIP) device, got {self.device}")
-        self.lib = _lib.load()
+        else:
+            self.lib = _lib.load()
         self.n_features = compiled.n_features
         if getattr(compiled, "prepared_inputs", False):
             self.prep = None  # a derive pass already applied the MiningField preparation
@@ -499,6 +521,39 @@ class EnsembleSpec:
     epi: dict
     labels: Optional[List[str]]
     slots: Optional[List[int]] = None
+    mode: str = "sum"  # sum | slot (multi-class chains) | class (majority vote: leaf = class index)
+    tree_w: Optional[List[float]] = None  # mode "class": per-tree vote weight
+    acc_init: Optional[List[float]] = None  # multi-class: per-class initial accumulator
+
+
+def to_general(spec: "EnsembleSpec") -> "EnsembleSpec":
+    """The same ensemble in the P=C payload form the narrow / pointer kernels accumulate in LDS:
+    votes become weighted one-hot leaves, per-class biases become constant stump trees."""
+    if spec.mode == "sum":
+        return spec
+    if spec.mode == "class":
+        trees = []
+        for t, w in zip(spec.trees, spec.tree_w or [1.0] * len(spec.trees)):
+            probs = np.zeros((len(t.leaf_value), spec.C))
+            ok = ~np.isnan(t.leaf_value)
+            probs[np.nonzero(ok)[0], t.leaf_value[ok].astype(int)] = w
+            trees.append(dataclasses.replace(t, leaf_probs=probs))
+        return EnsembleSpec(trees, [1.0] * len(trees), spec.C, spec.C, spec.epi, spec.labels)
+    # slot: one payload value per tree into its class slot; biases as constant stumps
+    trees, weights, slots = list(spec.trees), list(spec.weights), list(spec.slots)
+    for k, b in enumerate(spec.acc_init or []):
+        if b != 0.0:
+            trees.append(_stump(b))
+            weights.append(1.0)
+            slots.append(k)
+    return EnsembleSpec(trees, weights, 1, spec.C, spec.epi, spec.labels, slots)
+
+
+def _stump(value: float) -> BinaryTree:
+    """A single-leaf tree scoring ``value`` for every row."""
+    return BinaryTree(feature=np.array([-1]), threshold=np.zeros(1), op=np.zeros(1, dtype=np.int64),
+                      left=np.array([-1]), right=np.array([-1]), default_left=np.zeros(1, dtype=bool),
+                      leaf_value=np.array([float(value)]), leaf_probs=None, depth=0, null_missing=False)
 
 
 def _segments_all_true(mm: ir.MiningModel) -> bool:
@@ -593,66 +648,98 @@ def _classification_spec(ev: MiningEvaluator, field_index, lower=lower_binary_tr
     cats = list(ev.categories)
     C = len(cats)
     trees, weights = [], []
+    vote = method in ("majorityVote", "weightedMajorityVote")
     for seg, sub in zip(mm.segments, ev.sub):
         if not isinstance(sub, TreeEvaluator) or sub.kind != "classification":
             raise NotLowerable("classification ensembles must hold classification trees")
         t = lower(sub, field_index)
         remap = np.array([cats.index(c) for c in sub.categories])
-        if method in ("majorityVote", "weightedMajorityVote"):
-            probs = np.zeros((len(t.leaf_value), C))
+        if vote:
+            # the leaf is the (ensemble-order) class index; the tree's weight is its vote
             ok = ~np.isnan(t.leaf_value)
-            probs[np.nonzero(ok)[0], remap[t.leaf_value[ok].astype(int)]] = 1.0
+            lv = np.full(len(t.leaf_value), np.nan)
+            lv[ok] = remap[t.leaf_value[ok].astype(int)]
+            t.leaf_value = lv
         elif method in ("average", "weightedAverage"):
             probs = np.zeros((len(t.leaf_value), C))
             probs[:, remap] = np.nan_to_num(t.leaf_probs)
+            t.leaf_probs = probs
         else:
             raise NotLowerable(f"multipleModelMethod {method!r} is host-only for classification")
-        t.leaf_probs = probs
         trees.append(t)
         weights.append(seg.weight if method.startswith("weighted") else 1.0)
     _check_null_trees(mm, trees)
-    return EnsembleSpec(trees, weights, C, C, dict(mode=EPI_ARGMAX, C=C, a=1.0 / sum(weights)), cats)
+    epi = dict(mode=EPI_ARGMAX, C=C, a=1.0 / sum(weights))
+    if vote:
+        return EnsembleSpec(trees, [1.0] * len(trees), 1, C, epi, cats, mode="class", tree_w=weights)
+    return EnsembleSpec(trees, weights, C, C, epi, cats)
 
 
 def _chain_spec(compiled, ev: MiningEvaluator, field_index, lower=lower_binary_tree) -> EnsembleSpec:
-    """modelChain [regression tree ensemble -> binary RegressionModel on its output] (the
-    XGBoost/LightGBM binary-classification export) fused into one kernel + link epilogue."""
+    """modelChain [regression tree ensemble(s) -> classification RegressionModel on their outputs]
+    fused into one kernel + epilogue: the XGBoost / LightGBM binary export (one ensemble + logistic
+    calibrator) and the K-class export (K ensembles, one per class, + softmax RegressionModel)."""
     mm = ev.mm
-    if len(mm.segments) != 2 or not _segments_all_true(mm):
-        raise NotLowerable("only two-segment modelChains (ensemble -> calibrator) are lowered")
-    first, second = ev.sub
+    if len(mm.segments) < 2 or not _segments_all_true(mm):
+        raise NotLowerable("modelChain needs >= 2 segments with True predicates")
+    *firsts, second = ev.sub
     if not isinstance(second, RegressionEvaluator) or second.kind != "classification":
         raise NotLowerable("chain calibrator must be a classification RegressionModel")
-    outs = [o for o in first.model.output if o.feature in ("predictedValue", "transformedValue")
-            and o.expression is None]
-    if len(outs) < 1:
-        raise NotLowerable("first chain segment exposes no predictedValue output")
-    out_name = outs[0].name
+    outs = {}  # output field -> ensemble index
+    for i, first in enumerate(firsts):
+        o = [o for o in first.model.output if o.feature in ("predictedValue", "transformedValue")
+             and o.expression is None]
+        if len(o) < 1:
+            raise NotLowerable("chain segment exposes no predictedValue output")
+        outs[o[0].name] = i
     rm = second.rm
-    if len(rm.tables) != 2 or rm.tables[1].numeric or rm.tables[1].categorical or rm.tables[1].terms:
-        raise NotLowerable("calibrator must have two tables, the second constant")
-    t0 = rm.tables[0]
-    if t0.categorical or t0.terms or len(t0.numeric) != 1 or t0.numeric[0].name != out_name \
-            or t0.numeric[0].exponent != 1.0:
-        raise NotLowerable("calibrator must be linear in the ensemble output")
-    if rm.tables[1].intercept != 0.0 and rm.normalization_method not in ("softmax",):
-        pass
     norm = rm.normalization_method
-    if norm not in LINKS or norm == "none":
-        raise NotLowerable(f"calibrator normalizationMethod {norm!r} is host-only")
-    trees, w, a, b = _regression_ensemble(first, field_index, lower)
-    coef, icpt = t0.numeric[0].coefficient, t0.intercept
     cats = list(second.categories)
-    # the chain's target is the calibrator's; category table in calibrator order
-    return EnsembleSpec(trees, w, 1, 1, dict(mode=EPI_LOGISTIC2, C=2, a=coef * a, b=coef * b + icpt,
-                                             link=LINKS[norm]), cats)
+    if len(firsts) == 1:
+        out_name = next(iter(outs))
+        if len(rm.tables) != 2 or rm.tables[1].numeric or rm.tables[1].categorical or rm.tables[1].terms:
+            raise NotLowerable("calibrator must have two tables, the second constant")
+        t0 = rm.tables[0]
+        if t0.categorical or t0.terms or len(t0.numeric) != 1 or t0.numeric[0].name != out_name \
+                or t0.numeric[0].exponent != 1.0:
+            raise NotLowerable("calibrator must be linear in the ensemble output")
+        if norm not in LINKS or norm == "none":
+            raise NotLowerable(f"calibrator normalizationMethod {norm!r} is host-only")
+        trees, w, a, b = _regression_ensemble(firsts[0], field_index, lower)
+        coef, icpt = t0.numeric[0].coefficient, t0.intercept
+        # the chain's target is the calibrator's; category table in calibrator order
+        return EnsembleSpec(trees, w, 1, 1, dict(mode=EPI_LOGISTIC2, C=2, a=coef * a, b=coef * b + icpt,
+                                                 link=LINKS[norm]), cats)
+    # K-class: table k = intercept_k + coef_k * output(ensemble e_k); softmax over the K tables
+    if norm != "softmax":
+        raise NotLowerable(f"K-class chain normalizationMethod {norm!r} is host-only (softmax only)")
+    K = len(rm.tables)
+    if K < 2 or K > 16:
+        raise NotLowerable(f"K-class chains with {K} classes are host-only (2..16)")
+    trees, weights, slots, init = [], [], [], []
+    for k, tab in enumerate(rm.tables):
+        if tab.categorical or tab.terms or len(tab.numeric) > 1:
+            raise NotLowerable("K-class calibrator tables must be linear in one ensemble output")
+        if not tab.numeric:
+            init.append(tab.intercept)
+            continue
+        p = tab.numeric[0]
+        if p.exponent != 1.0 or p.name not in outs:
+            raise NotLowerable("K-class calibrator tables must reference a chain output linearly")
+        et, ew, ea, eb = _regression_ensemble(firsts[outs[p.name]], field_index, lower)
+        trees.extend(et)
+        weights.extend(x * ea * p.coefficient for x in ew)
+        slots.extend([k] * len(et))
+        init.append(tab.intercept + p.coefficient * eb)
+    return EnsembleSpec(trees, weights, 1, K, dict(mode=EPI_SOFTMAX, C=K, a=1.0), cats, slots=slots, mode="slot",
+                        acc_init=init)
 
 
 def shard_spec(spec: EnsembleSpec, rank: int, world: int) -> EnsembleSpec:
     """Rank ``rank``'s contiguous slice of a single-accumulator ensemble with a raw epilogue
     (``mode=AFFINE, a=1, b=0``, no link): the kernel writes ``Σ w_i·leaf_i`` over its trees, or
     NaN/invalid for rows a null-on-missing tree poisons."""
-    if spec.P != 1 or spec.epi["mode"] not in (EPI_AFFINE, EPI_LOGISTIC2):
+    if spec.P != 1 or spec.mode != "sum" or spec.epi["mode"] not in (EPI_AFFINE, EPI_LOGISTIC2):
         raise NotLowerable("tree sharding supports single-score ensembles (regression / binary chains)")
     if not 0 <= rank < world or len(spec.trees) < world:
         raise ValueError(f"cannot shard {len(spec.trees)} trees over {world} ranks (rank {rank})")
@@ -663,14 +750,20 @@ def shard_spec(spec: EnsembleSpec, rank: int, world: int) -> EnsembleSpec:
                         None, spec.slots[lo:hi] if spec.slots is not None else None)
 
 
-def _perfect_pack(trees: List[BinaryTree], weights: List[float], P: int, D: int) -> Tuple[np.ndarray, int, bool]:
+def _perfect_pack(trees: List[BinaryTree], weights: List[float], P: int, D: int, stride: int = TB,
+                  fmap: Optional[dict] = None, leaf_bits: Optional[str] = None) -> Tuple[np.ndarray, int, bool]:
     """Pack trees into the PERFECT layout (heap order, root = node 1):
 
     ``[ (2^D-1) x {T bits, feature byte offset} ][ 2^D x P leaves ][ ceil((2^D-1)/32) default-right words ]``
 
     padded to 16 bytes. Split tests are canonicalised to "go right iff x >= T"
     (:func:`canonical_threshold`); a missing value goes right iff the node's default-right bit is
-    set. Leaves above depth D are replicated over their whole padded subtree."""
+    set. Leaves above depth D are replicated over their whole padded subtree.
+
+    The feature byte offset is ``column * stride * 4`` with ``column = fmap[feature]`` (the
+    kernel's staged-column order) and ``stride`` its feature-plane stride in floats (``TB`` for
+    the narrow kernel, ``rows + 1`` for the wide one). ``leaf_bits="vote8"`` stores the packed
+    vote increment ``1 << 8*class`` as the leaf's bit pattern (class-index leaves)."""
     NI, NL = (1 << D) - 1, 1 << D
     ndr = (NI + 31) // 32
     rec = 2 * NI + NL * P + ndr
@@ -686,12 +779,18 @@ def _perfect_pack(trees: List[BinaryTree], weights: List[float], P: int, D: int)
         while stack:
             k, p, d = stack.pop()
             if t.feature[k] < 0:
-                val = (t.leaf_probs[k] if t.leaf_probs is not None and P > 1 else np.array([t.leaf_value[k]])) * w
+                if leaf_bits == "vote8":
+                    val = np.array([np.uint32(1 << (8 * int(t.leaf_value[k]))).view(np.float32)])
+                else:
+                    val = (t.leaf_probs[k] if t.leaf_probs is not None and P > 1 else np.array([t.leaf_value[k]])) * w
                 lo = p
                 for _ in range(D - d):
                     lo = 2 * lo + 1
                 span = 1 << (D - d)
-                leaves[lo - NI: lo - NI + span, :] = np.asarray(val, dtype=np.float64)[None, :P]
+                if leaf_bits == "vote8":
+                    leaves[lo - NI: lo - NI + span, :] = val[None, :P]
+                else:
+                    leaves[lo - NI: lo - NI + span, :] = np.asarray(val, dtype=np.float64)[None, :P]
                 continue
             T, swap = canonical_threshold(int(t.op[k]), float(t.threshold[k]))
             first, second = int(t.left[k]), int(t.right[k])
@@ -702,11 +801,11 @@ def _perfect_pack(trees: List[BinaryTree], weights: List[float], P: int, D: int)
             else:
                 left_child, right_child = first, second
                 dr = not dflt_first
-            f = int(t.feature[k])
-            if f > 63:
-                raise NotLowerable("perfect layout supports at most 64 features")
+            f = int(t.feature[k]) if fmap is None else fmap[int(t.feature[k])]
+            if stride == TB and f > 63:
+                raise NotLowerable("the narrow perfect layout supports at most 64 features")
             nodes_T[p] = T
-            nodes_meta[p] = f * TB * 4
+            nodes_meta[p] = f * stride * 4
             if dr:
                 dr_bits[p] = 1
                 has_dr = True
@@ -725,7 +824,7 @@ def _perfect_pack(trees: List[BinaryTree], weights: List[float], P: int, D: int)
 VAR_NAN_FAST, VAR_NAN_PLANES = 4, 8  # mirrors csrc/tree.hip
 
 
-def _nan_planes(blob: np.ndarray, D: int, F: int) -> np.ndarray:
+def _nan_planes(blob: np.ndarray, D: int, F: int, stride: int = TB) -> np.ndarray:
     """Point every default-right node of a P=1 PERFECT blob at the second feature plane (the
     wide kernel stages it with NaN -> +inf): ``x >= T`` then sends a missing value right at those
     nodes and left (NaN compares false) everywhere else — the default direction costs nothing
@@ -736,7 +835,7 @@ def _nan_planes(blob: np.ndarray, D: int, F: int) -> np.ndarray:
     words = out[:, 2 * NI + NL: 2 * NI + NL + ndr]
     for p in range(NI):
         dr = ((words[:, p >> 5] >> np.uint32(p & 31)) & np.uint32(1)).astype(bool)
-        out[dr, 2 * p + 1] += np.uint32(F * TB * 4)
+        out[dr, 2 * p + 1] += np.uint32(F * stride * 4)
     return out
 
 
@@ -832,7 +931,8 @@ class TreePlan(DevicePlan):
     _STATE = DevicePlan._STATE + ("depth", "n_trees", "layout", "P", "C", "general", "rec_words", "chunk_trees",
                                   "blob", "leaves", "roots", "has_dr", "table", "slots", "splits", "epi_args",
                                   "variant", "children", "preds", "pool", "trees_tab", "max_steps", "blob_nan",
-                                  "chunk_trees_nan", "full_epi", "labels")
+                                  "chunk_trees_nan", "full_epi", "labels", "mode", "tree_w", "acc_init", "feat_map",
+                                  "rows_wide", "n_stage")
 
     WIDE_G = 4  # tree groups of the wide kernel (mirrors csrc)
 
@@ -861,6 +961,8 @@ class TreePlan(DevicePlan):
                     raise
                 spec, layout = self._general_spec(compiled), "general"
         self.full_epi, self.labels = dict(spec.epi), spec.labels
+        if spec.C > 16:
+            raise NotLowerable(f"{spec.C} class slots: the tree kernels accumulate at most 16")
         if tree_shard is not None:
             if layout == "general":
                 raise NotLowerable("tree sharding needs the binary (perfect / pointer) layouts")
@@ -875,6 +977,11 @@ class TreePlan(DevicePlan):
             if precision == "fp8":
                 raise NotLowerable("fp8 leaves need the PERFECT layout")
             from .general_tree import pack_general
+
+            if spec.mode == "slot" and any(b != 0.0 for b in (spec.acc_init or [])):
+                raise NotLowerable("K-class chains with intercepts over non-binary trees are host-only")
+            spec = to_general(spec)
+            self.spec = spec
 
             g = pack_general(spec.trees, spec.weights, spec.P, compiled.schema)
             self.layout, self.variant, self.rec_words, self.chunk_trees = "general", 0, 0, 0
@@ -897,30 +1004,68 @@ class TreePlan(DevicePlan):
             return
         self.children = self.preds = self.pool = self.trees_tab = None
         self.max_steps = 0
+        NI, NL = (1 << depth) - 1, 1 << depth
+        # wide kernel geometry: stage only the columns the trees read (+ columns whose preparation
+        # can reject a row); row tiles of 256 / 128 / 64 rows keep the feature planes <= 64 KiB
+        stage = self._stage_columns(compiled, spec.trees)
+        rows = next((r for r, lim in ((256, 64), (128, 128), (64, 256)) if len(stage) <= lim), None)
+        wide_ok = (spec.P == 1 and depth <= 10 and rows is not None and variant != "narrow"
+                   and (spec.mode == "sum" or spec.C <= 8))
         if layout == "auto":
-            NI, NL = (1 << depth) - 1, 1 << depth
             rec_bytes = 4 * (2 * NI + NL * spec.P + (NI + 31) // 32)
-            layout = "perfect" if depth <= 10 and F <= 64 and rec_bytes <= 32 * 1024 else "pointer"
+            layout = "perfect" if depth <= 10 and (wide_ok or F <= 64) and rec_bytes <= 32 * 1024 else "pointer"
+        if spec.mode != "sum" and not (layout == "perfect" and wide_ok):
+            spec = to_general(spec)  # votes / class slots accumulate in LDS on the narrow kernels
+        self.spec = spec
         self.layout = layout
         self.P, self.C = spec.P, spec.C
-        self.general = 1 if spec.P > 1 else 0
+        self.general = 1 if (spec.P > 1 or (spec.mode == "sum" and spec.slots is not None)) else 0
+        self.mode = {"sum": 0, "slot": 1, "class": 2}[spec.mode]
+        self.tree_w = self.acc_init = self.feat_map = None
+        self.rows_wide, self.n_stage = TB, F
         if self.layout == "perfect":
-            blob, rec, has_dr = _perfect_pack(spec.trees, spec.weights, spec.P, depth)
             if variant == "auto":
-                variant = "narrow" if self.general else "wide"
+                variant = "narrow" if self.general or not wide_ok else "wide"
             self.variant = 1 if variant == "wide" else 0
+            if self.variant == 1:
+                if not wide_ok:
+                    raise NotLowerable("the wide tree kernel needs P = 1 and <= 256 staged columns")
+                self.rows_wide, self.n_stage = rows, len(stage)
+                stride = rows + 1  # one pad float per feature plane (conflict-free staging)
+                fmap = {f: j for j, f in enumerate(stage)}
+                if stage != list(range(F)):
+                    self.feat_map = self._t(np.array(stage, dtype=np.int32))
+            else:
+                if F > 64:
+                    raise NotLowerable("the narrow perfect kernel stages at most 64 features")
+                stride, fmap = TB, None
+            leaf_bits = None
+            if spec.mode == "class":
+                self.mode = self._vote_mode(spec, rows)
+                if self.mode == 3:  # VOTE8: packed u8 counters, the leaf is the increment 1 << 8*class
+                    leaf_bits = "vote8"
+                elif spec.tree_w is not None and any(w != 1.0 for w in spec.tree_w):
+                    self.tree_w = self._t(np.asarray(spec.tree_w, np.float32))
+            if spec.mode == "slot":
+                if spec.acc_init is not None and any(b != 0.0 for b in spec.acc_init):
+                    self.acc_init = self._t(np.asarray(spec.acc_init, np.float32))
+            blob, rec, has_dr = _perfect_pack(spec.trees, spec.weights, spec.P, depth, stride=stride, fmap=fmap,
+                                              leaf_bits=leaf_bits)
             nan_flags = 0
             blob_nan = None
+            Fs = self.n_stage
             if self.variant == 1 and nan_mode == "auto" and not any(t.null_missing for t in spec.trees):
                 if not has_dr:
                     nan_flags = VAR_NAN_FAST
-                elif precision != "fp8" or (2 * F - 1) * TB * 4 < (1 << 16):  # fp8 metas: 16-bit offsets
-                    blob_nan = _nan_planes(blob, depth, F)
+                elif precision != "fp8" or (2 * Fs - 1) * stride * 4 < (1 << 16):  # fp8 metas: 16-bit offsets
+                    blob_nan = _nan_planes(blob, depth, Fs, stride)
                     nan_flags = VAR_NAN_FAST | VAR_NAN_PLANES
             if precision == "fp8":
                 # e4m3 leaves in the last-level metas, global scale folded into the epilogue
-                if self.general or self.variant != 1:
+                if self.general or self.variant != 1 or spec.mode != "sum":
                     raise NotLowerable("fp8 leaves need the single-accumulator wide kernel (P = 1)")
+                if (Fs - 1) * stride * 4 >= (1 << 16):
+                    raise NotLowerable("fp8 leaf pairs need feature offsets below 64 KiB")
                 blob, rec, scale = _leaf8_pack(blob, depth)
                 if blob_nan is not None:
                     blob_nan, _, _ = _leaf8_pack(blob_nan, depth, scale)
@@ -930,20 +1075,23 @@ class TreePlan(DevicePlan):
             self.rec_words = rec
             wide = self.variant & 3 in (1, 2)
             if wide:
-                # one 1024-thread workgroup per CU: [G][256] partials + feature plane(s) + two chunk
-                # buffers; tiles with missing values use the NaN blob with two planes (own chunk size)
-                fixed = F * TB * 4 + (TB + 4) * 4 + self.WIDE_G * TB * 4
+                # one 1024-thread workgroup per row tile: [G][rows] partials + feature plane(s) + two
+                # chunk buffers; tiles with missing values use the NaN blob with two planes
+                G = 1024 // self.rows_wide
+                plane = Fs * stride * 4
+                fixed = plane + (self.rows_wide + 4) * 4 + G * self.rows_wide * 4
                 per_chunk = min((156 * 1024 - fixed) // 2, 64 * 1024)
             else:
-                fixed = F * TB * 4 + (TB + 4) * 4 + (self.C * TB * 4 if self.general else 0)
+                plane = F * TB * 4
+                fixed = plane + (TB + 4) * 4 + (self.C * TB * 4 if self.general else 0)
                 budget = max(lds_budget - fixed, 2 * rec * 4)  # two chunk buffers (double buffering)
                 per_chunk = min(budget // 2, 32 * 1024)  # register prefetch holds <= 32 KiB per chunk
             if rec * 4 > per_chunk:
-                raise NotLowerable(f"depth-{depth} tree record ({rec * 4} B) exceeds the 32 KiB chunk")
+                raise NotLowerable(f"depth-{depth} tree record ({rec * 4} B) exceeds the chunk buffer")
             self.chunk_trees = self._chunk(per_chunk // (rec * 4), wide, max_chunk_trees)
             self.blob_nan, self.chunk_trees_nan = None, 0
             if blob_nan is not None:
-                per_nan = min((156 * 1024 - fixed - F * TB * 4) // 2, 64 * 1024)
+                per_nan = min((156 * 1024 - fixed - plane) // 2, 64 * 1024)
                 if rec * 4 <= per_nan:
                     self.chunk_trees_nan = self._chunk(per_nan // (rec * 4), wide, max_chunk_trees)
                     self.blob_nan = self._t(blob_nan.reshape(-1).view(np.int32))
@@ -962,19 +1110,50 @@ class TreePlan(DevicePlan):
             self.blob = self._t(nodes.reshape(-1).view(np.int32))
             self.leaves = self._t(leaves.reshape(-1))
             self.roots = self._t(roots)
+        if not (self.variant & 3):
+            self.mode = 0  # narrow / pointer kernels: plain sums or LDS slot accumulators
         self.has_dr = has_dr
         self.table = self._t(_label_table(spec.labels)) if spec.labels is not None else None
-        self.slots = self._t(np.zeros(self.n_trees, dtype=np.int32)) if self.general else None
-        self.splits = splits
+        if self.general or self.mode == 1:
+            sl = spec.slots if spec.slots is not None else [0] * self.n_trees
+            self.slots = self._t(np.asarray(sl, dtype=np.int32))
+        else:
+            self.slots = None
+        self.splits = 1 if self.mode else splits
         self._partial = None
+
+    @staticmethod
+    def _stage_columns(compiled, trees) -> List[int]:
+        """Active-field columns the wide kernel stages: every feature a split reads, plus every
+        field whose preparation can reject the row (its validity must still be checked)."""
+        used = set()
+        for t in trees:
+            used.update(int(f) for f in t.feature if f >= 0)
+        prep, _ = build_field_prep(compiled, compiled.active_fields) if compiled.active_fields else (None, False)
+        if prep is not None:
+            for j in range(len(compiled.active_fields)):
+                if prep[j, 0] & (FP_INVALID_RETURN | FP_ROW_INVALID | FP_INTEGER | FP_CODE_RANGE | FP_HAS_INTERVAL):
+                    used.add(j)
+        return sorted(used) if used else [0]
+
+    def _vote_mode(self, spec, rows) -> int:
+        """MODE_VOTE8 (packed u8 counters, one add per tree) when the vote is unweighted, <= 4
+        classes, no leaf lacks a class and no thread's counter can pass 255; else MODE_CLASS."""
+        G = 1024 // (rows or 256)
+        unweighted = spec.tree_w is None or all(w == 1.0 for w in spec.tree_w)
+        no_nan = all(not np.isnan(t.leaf_value[t.feature < 0]).any() for t in spec.trees)
+        if unweighted and spec.C <= 4 and no_nan and -(-len(spec.trees) // G) <= 255:
+            return 3
+        return 2
 
     def _chunk(self, fit: int, wide: bool, cap: int) -> int:
         """Trees per LDS chunk. Wide kernel: whole ILP batches per tree group (G groups x 8-wide
         walks) — every group gets the same count (no barrier imbalance) and no latency-bound short
         tail batches (measured: 64 > 79 > 57 trees at depth 6)."""
         c = int(max(1, min(self.n_trees, fit)))
+        G = 1024 // getattr(self, "rows_wide", 256)
         if wide and c < self.n_trees:
-            q = 8 * self.WIDE_G if c >= 16 * self.WIDE_G else 2 * self.WIDE_G
+            q = 8 * G if c >= 16 * G else 2 * G
             c = max(q, c // q * q) if c >= q else c
         return min(c, cap) if cap > 0 else c
 
@@ -983,7 +1162,10 @@ class TreePlan(DevicePlan):
         from .general_tree import lower_general_tree
 
         try:
-            return ensemble_spec(compiled, lower=lower_general_tree)
+            spec = ensemble_spec(compiled, lower=lower_general_tree)
+            if spec.mode == "slot" and any(b != 0.0 for b in (spec.acc_init or [])):
+                raise NotLowerable("K-class chains with intercepts over non-binary trees are host-only")
+            return to_general(spec)  # the predicate VM accumulates P = C payloads in LDS
         except NotBinary as e:  # pragma: no cover - the general lowering never raises NotBinary
             raise NotLowerable(str(e)) from e
 
@@ -1007,6 +1189,10 @@ class TreePlan(DevicePlan):
             a.n_trees, a.rec_words, a.chunk_trees, a.P = self.n_trees, self.rec_words, self.chunk_trees, self.P
             a.C, a.general, a.variant = self.C, self.general, self.variant
             a.blob_nan, a.chunk_trees_nan = ptr(getattr(self, "blob_nan", None)), getattr(self, "chunk_trees_nan", 0)
+            a.tree_w, a.acc_init = ptr(getattr(self, "tree_w", None)), ptr(getattr(self, "acc_init", None))
+            a.feat_map = ptr(getattr(self, "feat_map", None))
+            a.rows_wide, a.mode = getattr(self, "rows_wide", TB), getattr(self, "mode", 0)
+            a.n_stage = getattr(self, "n_stage", self.n_features)
             a.epi = _epilogue(table=self.table, write_probs=with_probs, **self.epi_args)
             cache[with_probs] = a
         b = TreeArgs()
@@ -1119,9 +1305,15 @@ def compile_plan(compiled, device, **opts) -> DevicePlan:
     from ..models.svm import SvmEvaluator
 
     if isinstance(ev, NeuralEvaluator):
-        from .nn_plans import MlpPlan
+        from .nn_plans import GemmMlpPlan, MlpPlan
 
-        return MlpPlan(compiled, device, precision="fp32" if policy == "fp32" else "bf16", **opts)
+        prec = "fp32" if policy == "fp32" else "bf16"
+        try:
+            return MlpPlan(compiled, device, precision=prec, **opts)
+        except NotLowerable as e:
+            if "fused kernel" not in str(e):
+                raise
+            return GemmMlpPlan(compiled, device, precision=prec)
     if isinstance(ev, SvmEvaluator):
         from .nn_plans import SvmPlan
 

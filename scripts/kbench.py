@@ -27,6 +27,8 @@ def main():
     p.add_argument("--clusters", type=int, default=256)
     p.add_argument("--nan-mode", default="auto")
     p.add_argument("--max-chunk-trees", type=int, default=0)
+    p.add_argument("--precision", default="fp32", choices=["fp32", "bf16", "fp8"])
+    p.add_argument("--hidden", default="256,256", help="mlp hidden widths")
     args = p.parse_args()
     import numpy as np
     import torch
@@ -56,7 +58,7 @@ def main():
     elif args.model == "rf":
         txt = synth.random_forest_pmml(n_trees=args.trees, depth=args.depth, n_features=args.features)
     elif args.model == "mlp":
-        txt = synth.mlp_pmml(n_features=args.features)
+        txt = synth.mlp_pmml(n_features=args.features, hidden=tuple(int(x) for x in args.hidden.split(",")))
     elif args.model == "svm":
         txt = synth.svm_pmml(n_features=args.features)
     elif args.model == "kmeans-big":
@@ -74,6 +76,8 @@ def main():
                     max_chunk_trees=args.max_chunk_trees)
     elif args.model == "kmeans-big":
         opts = dict(cluster_variant=args.variant)
+    if args.precision != "fp32":
+        opts["precision"] = args.precision
     plan = c.plan("cuda:0", **opts)
     F = c.n_features
     X = torch.from_numpy(synth.stream_matrix(args.rows, F, seed=1, missing_rate=args.missing)).cuda()
@@ -89,7 +93,12 @@ def main():
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / args.iters
+    flops = None
+    if args.model == "mlp":
+        dims = [F] + [int(x) for x in args.hidden.split(",")] + [1]
+        flops = 2.0 * args.rows * sum(a * b for a, b in zip(dims[:-1], dims[1:]))
     print(json.dumps({"model": args.model, "rows": args.rows, "features": F, "ms": ms,
+                      "tflops": (flops / ms / 1e9) if flops else None, "precision": args.precision,
                       "rows_per_s": args.rows / ms * 1e3, "plan": type(plan).__name__,
                       "layout": getattr(plan, "layout", None), "chunk_trees": getattr(plan, "chunk_trees", None),
                       "missing": args.missing, "lds_budget": args.lds_budget,

@@ -8,11 +8,11 @@ import pytest
 from flink_jpmml_amd.bench.synth import gbdt_pmml, random_forest_pmml, stream_matrix
 from flink_jpmml_amd.models.tree import OP_GE, OP_GT, OP_LE, OP_LT
 from flink_jpmml_amd.runtime.compiled import CompiledPmml
-from flink_jpmml_amd.runtime.plans import TB, _nan_planes, _perfect_pack, _pointer_pack, canonical_threshold, ensemble_spec
+from flink_jpmml_amd.runtime.plans import TB, _nan_planes, _perfect_pack, _pointer_pack, canonical_threshold, ensemble_spec, to_general
 
 
 def emulate_perfect(c, X):
-    spec = ensemble_spec(c)
+    spec = to_general(ensemble_spec(c))  # the narrow kernel's P = C payload form
     D = max(t.depth for t in spec.trees)
     P = spec.P
     blob, rec, _ = _perfect_pack(spec.trees, spec.weights, P, D)
@@ -41,7 +41,7 @@ def emulate_perfect(c, X):
 
 
 def emulate_pointer(c, X):
-    spec = ensemble_spec(c)
+    spec = to_general(ensemble_spec(c))
     nodes, leaves, roots, _ = _pointer_pack(spec.trees, spec.weights, spec.P)
     Xf = X.astype(np.float32)
     acc = np.zeros((len(X), spec.P), np.float32)
