@@ -622,3 +622,26 @@ def stream_matrix(n_rows: int, n_features: int, seed: int = 0, missing_rate: flo
     if missing_rate > 0:
         X[rng.random((n_rows, n_features)) < missing_rate] = np.nan
     return X
+
+
+def set_target(txt: str, field: str = "y", min: Optional[float] = None, max: Optional[float] = None,
+               factor: float = 1.0, constant: float = 0.0, cast: Optional[str] = None,
+               default: Optional[float] = None) -> str:
+    """Replace (or insert) the top-level model's ``<Targets>`` with one ``Target`` carrying the
+    given min / max / rescale / castInteger / TargetValue defaultValue."""
+    import re
+
+    attrs = f'field="{field}" rescaleFactor="{_fnum(factor)}" rescaleConstant="{_fnum(constant)}"'
+    if min is not None:
+        attrs += f' min="{_fnum(min)}"'
+    if max is not None:
+        attrs += f' max="{_fnum(max)}"'
+    if cast is not None:
+        attrs += f' castInteger="{cast}"'
+    body = f'<TargetValue defaultValue="{_fnum(default)}"/>' if default is not None else ""
+    new = f'<Targets><Target {attrs}>{body}</Target></Targets>'
+    m = re.search(r"<Targets>.*?</Targets>", txt, flags=re.S)
+    if m is not None and m.start() < txt.find("<Segment"):
+        return txt[:m.start()] + new + txt[m.end():]
+    i = txt.find("</MiningSchema>") + len("</MiningSchema>")
+    return txt[:i] + "\n  " + new + txt[i:]

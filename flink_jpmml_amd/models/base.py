@@ -105,12 +105,13 @@ class ModelEvaluator:
         if t is None:
             return
         v = res.value
-        if t.rescale_factor != 1.0 or t.rescale_constant != 0.0:
-            v = v * t.rescale_factor + t.rescale_constant
+        # JPMML TargetUtil order: clip to [min, max] first, then rescale, then castInteger
         if t.min is not None:
             v = np.maximum(v, t.min)
         if t.max is not None:
             v = np.minimum(v, t.max)
+        if t.rescale_factor != 1.0 or t.rescale_constant != 0.0:
+            v = v * t.rescale_factor + t.rescale_constant
         if t.cast_integer == "round":
             v = np.floor(v + 0.5)
         elif t.cast_integer == "ceiling":

@@ -125,7 +125,8 @@ class FieldPrep(ctypes.Structure):
 class Epilogue(ctypes.Structure):
     _fields_ = [("mode", c_int), ("n_classes", c_int), ("a", c_float), ("b", c_float), ("thr", c_float),
                 ("has_table", c_int), ("table", c_void_p), ("write_probs", c_int), ("link", c_int),
-                ("score2", c_void_p), ("valid2", c_void_p)]
+                ("score2", c_void_p), ("valid2", c_void_p), ("tgt", c_int), ("lo", c_float), ("hi", c_float),
+                ("ta", c_float), ("tb", c_float), ("dflt", c_float)]
 
 
 class TreeArgs(ctypes.Structure):
@@ -209,10 +210,12 @@ def load(auto_build: bool = True) -> ctypes.CDLL:
             try:
                 build()
             except KernelLibraryError:
-                if not os.path.exists(LIB_PATH):
+                # never run kernels older than their sources: a stale library silently computes
+                # with an old ABI / old numerics. FJA_ALLOW_STALE_LIB=1 opts in explicitly.
+                if not os.path.exists(LIB_PATH) or os.environ.get("FJA_ALLOW_STALE_LIB") != "1":
                     raise
-                logger.warning("kernel sources newer than %s but rebuild failed; using the existing library",
-                               LIB_PATH)
+                logger.warning("kernel sources newer than %s but rebuild failed; FJA_ALLOW_STALE_LIB=1: "
+                               "using the existing library", LIB_PATH)
         if not os.path.exists(LIB_PATH):
             raise KernelLibraryError(f"{LIB_PATH} missing: run `python -c 'import __graft_entry__ as g; g.build()'`")
         try:

@@ -85,7 +85,16 @@ struct Epilogue {
   int link;             // LINK_* applied after the affine map (EPI_AFFINE, EPI_LOGISTIC2)
   float* score2;        // optional mirror outputs (e.g. device copy beside a zero-copy host sink)
   uint8_t* valid2;
+  int tgt;              // TGT_* flags: PMML Target post-processing of an EPI_AFFINE value
+  float lo, hi;         // Target min / max (clip, applied first)
+  float ta, tb;         // Target rescaleFactor / rescaleConstant (after the clip)
+  float dflt;           // TargetValue defaultValue (rows without a prediction)
 };
+
+// Target post-processing (JPMML TargetUtil order): clip to [min, max], rescale, castInteger;
+// a row without a prediction takes the default value when one is declared.
+enum : int { TGT_ON = 1, TGT_LO = 2, TGT_HI = 4, TGT_DEFAULT = 8, TGT_CAST_SHIFT = 4 };
+enum : int { CAST_NONE = 0, CAST_ROUND = 1, CAST_CEIL = 2, CAST_FLOOR = 3 };
 
 enum : int { LINK_NONE = 0, LINK_LOGIT = 1, LINK_EXP = 2, LINK_PROBIT = 3, LINK_CLOGLOG = 4, LINK_LOGLOG = 5,
              LINK_CAUCHIT = 6 };

@@ -2,6 +2,18 @@
 #pragma once
 #include "common.h"
 
+__device__ __forceinline__ float apply_target(const Epilogue& e, float v) {
+  if ((e.tgt & TGT_LO) && v < e.lo) v = e.lo;  // compare form: a NaN stays NaN (no prediction)
+  if ((e.tgt & TGT_HI) && v > e.hi) v = e.hi;
+  v = fmaf(v, e.ta, e.tb);
+  switch ((e.tgt >> TGT_CAST_SHIFT) & 3) {
+    case CAST_ROUND: return floorf(v + 0.5f);
+    case CAST_CEIL: return ceilf(v);
+    case CAST_FLOOR: return floorf(v);
+    default: return v;
+  }
+}
+
 // acc: C accumulator values of this row (registers or LDS, read through the accessor).
 template <typename Acc>
 __device__ __forceinline__ void apply_epilogue(const Epilogue& e, Acc acc, bool row_ok, int row, int n_rows,
@@ -12,7 +24,12 @@ __device__ __forceinline__ void apply_epilogue(const Epilogue& e, Acc acc, bool 
   int label = 0;
   if (e.mode == EPI_AFFINE) {
     s = apply_link(e.link, fmaf(e.a, acc(0), e.b));
+    if (e.tgt) s = apply_target(e, s);
     ok = ok && __builtin_isfinite(s);  // the oracle's regression rule: a non-finite value is no prediction
+    if (!ok && (e.tgt & TGT_DEFAULT)) {
+      s = e.dflt;
+      ok = true;
+    }
     if (e.write_probs && probs) probs[row] = s;
   } else if (e.mode == EPI_LOGISTIC2) {
     float p0 = apply_link(e.link, fmaf(e.a, acc(0), e.b));

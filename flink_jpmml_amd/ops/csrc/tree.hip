@@ -299,7 +299,7 @@ PMML_API int pmml_tree_launch(hipStream_t stream, const TreeArgs* args, int layo
     const bool wide = (a.variant & 3) != 0;
     if (wide) {
       if (a.n_stage < 1 || a.n_stage > 256 || !(a.rows_wide == 256 || a.rows_wide == 128 || a.rows_wide == 64)) return -4;
-      if ((size_t)a.n_stage * (a.rows_wide + 1) > 64 * 256 + 64) return -4;  // planes <= ~64 KiB
+      if (a.n_stage > (64 * 256) / a.rows_wide) return -4;  // planes <= 64 KiB (+ one pad float each)
     } else if (a.n_feat > 64) {
       return -4;
     }

@@ -4,6 +4,7 @@ from .dist import (
     DistContext,
     all_gather_scores,
     all_gather_varlen,
+    all_to_all_varlen,
     broadcast_control,
     broadcast_object,
     broadcast_plan,
@@ -15,7 +16,7 @@ from .dist import (
 from .tree_shard import TreeShardedScorer, finish_epilogue, host_partial, tree_shard_supported
 
 __all__ = [
-    "DistContext", "all_gather_scores", "all_gather_varlen", "broadcast_control", "broadcast_object",
+    "DistContext", "all_gather_scores", "all_gather_varlen", "all_to_all_varlen", "broadcast_control", "broadcast_object",
     "broadcast_plan", "broadcast_tensors", "init_from_env", "shard_range", "shutdown",
     "TreeShardedScorer", "finish_epilogue", "host_partial", "tree_shard_supported",
 ]

@@ -291,3 +291,25 @@ def all_gather_varlen(t: torch.Tensor, ctx: DistContext) -> torch.Tensor:
     dist.all_gather_into_tensor(out, pad)
     parts = [out[i * m: i * m + s] for i, s in enumerate(sizes_i)]
     return torch.cat(parts)
+
+
+def all_to_all_varlen(t: torch.Tensor, send_counts: Sequence[int], ctx: DistContext,
+                      group=None) -> Tuple[torch.Tensor, List[int]]:
+    """Personalised exchange of variable-size row blocks: rows ``[sum(send_counts[:j]),
+    sum(send_counts[:j+1]))`` of ``t`` go to rank ``j``; returns the received rows (ordered by
+    source rank) and the per-source counts. Two collectives: the count matrix, then the payload
+    (``all_to_all_single`` — RCCL on GPU tensors, gloo on host tensors). Used by model-sharded
+    serving to route events to the rank that owns their model."""
+    if not ctx.is_distributed:
+        return t, [t.shape[0]]
+    sc = torch.tensor(list(send_counts), dtype=torch.int64, device=t.device)
+    rc = torch.empty_like(sc)
+    dist.all_to_all_single(rc, sc, group=group)
+    recv_counts = [int(x) for x in rc.tolist()]
+    out = torch.empty((sum(recv_counts),) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+    dist.all_to_all_single(out, t.contiguous(), output_split_sizes=recv_counts,
+                           input_split_sizes=[int(x) for x in send_counts], group=group)
+    from ..utils.metrics import METRICS
+
+    METRICS.inc("dist.bytes_all_to_all", t.numel() * t.element_size())
+    return out, recv_counts

@@ -29,7 +29,8 @@ import torch
 import torch.distributed as dist
 
 from ..models.tree import OP_GE, OP_GT, OP_LE, OP_LT
-from ..runtime.plans import EPI_AFFINE, EPI_LOGISTIC2, NotLowerable, _label_table, ensemble_spec, shard_spec
+from ..runtime.plans import (EPI_AFFINE, EPI_LOGISTIC2, NotLowerable, _label_table, apply_target_torch, ensemble_spec,
+                             shard_spec)
 from .dist import DistContext
 
 
@@ -60,6 +61,7 @@ def finish_epilogue(raw: torch.Tensor, valid: torch.Tensor, epi: dict, labels=No
     if epi["mode"] == EPI_AFFINE:
         s = y
         ok = ok & torch.isfinite(s)
+        s, ok = apply_target_torch(s, ok, epi.get("tgt"))
     elif epi["mode"] == EPI_LOGISTIC2:
         label = (y < epi.get("thr", 0.5)).long()  # p0 >= thr -> class 0
         ok = ok & ~torch.isnan(y)

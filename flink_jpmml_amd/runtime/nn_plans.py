@@ -17,7 +17,8 @@ import numpy as np
 from ..api.exceptions import UnsupportedFeatureException
 from ..models.neural import NeuralEvaluator
 from ..pmml import ir
-from .plans import EPI_AFFINE, LINKS, DevicePlan, NotLowerable, _addr, _epilogue, _label_table
+from .plans import (EPI_AFFINE, LINKS, DevicePlan, NotLowerable, _addr, _epilogue, _label_table, apply_target_torch,
+                    target_post)
 
 ACT_CODES = {"identity": 0, "logistic": 1, "tanh": 2, "rectifier": 3, "exponential": 4, "reciprocal": 5,
              "square": 6, "Gauss": 7, "sine": 8, "cosine": 9, "Elliott": 10, "arctan": 11, "threshold": 12}
@@ -121,7 +122,7 @@ class MlpPlan(DevicePlan):
     supports_direct = True
     _STATE = DevicePlan._STATE + ("weights", "biases", "layer_meta", "in_scale", "in_shift", "in_missing", "in_index",
                                   "n_in", "k0", "n_layers", "bf16", "out_a", "out_b", "final_norm", "n_out", "table",
-                                  "is_classification", "panels", "n_panels", "contiguous")
+                                  "is_classification", "panels", "n_panels", "contiguous", "target_stage")
 
     def __init__(self, compiled, device, precision: str = "fp32"):
         import torch
@@ -200,6 +201,7 @@ class MlpPlan(DevicePlan):
                 labels[out_neurons.index(o.neuron)] = ex.value
             self.table = self._t(_label_table([x if x is not None else "nan" for x in labels]))
             self.out_a, self.out_b = 1.0, 0.0
+            self.target_stage = None
         else:
             if self.n_out != 1 or len(nn.outputs) != 1 or nn.outputs[0].neuron != out_neurons[0]:
                 raise NotLowerable("regression NN must have one output neuron")
@@ -213,9 +215,8 @@ class MlpPlan(DevicePlan):
             else:
                 raise NotLowerable("regression NeuralOutput must be FieldRef or 2-point NormContinuous")
             tgt = ev.target
-            if tgt is not None:
-                if tgt.min is not None or tgt.max is not None or tgt.cast_integer:
-                    raise NotLowerable("Target min/max/castInteger is host-only")
+            self.target_stage = target_post(tgt)
+            if tgt is not None and self.target_stage is None:  # pure rescale: folded into the affine map
                 a, b = a * tgt.rescale_factor, b * tgt.rescale_factor + tgt.rescale_constant
             self.out_a, self.out_b = a, b
             self.table = None
@@ -234,7 +235,7 @@ class MlpPlan(DevicePlan):
         a.weights, a.biases, a.layers = ptr(self.weights), ptr(self.biases), ptr(self.layer_meta)
         a.out_scale, a.out_shift, a.final_norm, a.n_out = self.out_a, self.out_b, self.final_norm, self.n_out
         a.panels, a.n_panels, a.contiguous = ptr(self.panels), self.n_panels, self.contiguous
-        a.epi = _epilogue(mode=EPI_AFFINE, a=self.out_a, b=self.out_b, table=self.table)
+        a.epi = _epilogue(mode=EPI_AFFINE, a=self.out_a, b=self.out_b, table=self.table, tgt=self.target_stage)
         a.epi.score2, a.epi.valid2 = _addr(score2), _addr(valid2)
         a.score, a.valid, a.probs = _addr(score), _addr(valid), ptr(probs)
         check(self.lib.pmml_mlp_launch(stream_handle(stream), ctypes.byref(a), self.bf16), "mlp kernel")
@@ -261,7 +262,7 @@ class GemmMlpPlan(MlpPlan):
     supports_direct = False
     _STATE = DevicePlan._STATE + ("in_scale", "in_shift", "in_missing", "in_index", "n_in", "bf16", "out_a", "out_b",
                                   "final_norm", "n_out", "table", "is_classification", "gemm_w", "gemm_b",
-                                  "acts", "n_layers")
+                                  "acts", "n_layers", "target_stage")
 
     def __init__(self, compiled, device, precision: str = "fp32"):
         import torch
@@ -313,6 +314,7 @@ class GemmMlpPlan(MlpPlan):
             else:
                 s = self.out_a * h[:, 0] + self.out_b
                 ok = ok & torch.isfinite(s)
+                s, ok = apply_target_torch(s, ok, self.target_stage)
             s = torch.where(ok, s, torch.full_like(s, float("nan")))
             for so, vo in ((score, valid), (score2, valid2)):
                 if so is not None and not isinstance(so, int):

@@ -316,7 +316,7 @@ class DevicePlan:
 
 
 def _epilogue(mode: int, C: int = 1, a: float = 1.0, b: float = 0.0, thr: float = 0.5, table=None,
-              write_probs: bool = False, link: int = 0):
+              write_probs: bool = False, link: int = 0, tgt: Optional[dict] = None):
     from ..ops._lib import Epilogue
 
     e = Epilogue()
@@ -325,7 +325,58 @@ def _epilogue(mode: int, C: int = 1, a: float = 1.0, b: float = 0.0, thr: float 
     e.table = table.data_ptr() if table is not None else None
     e.write_probs = 1 if write_probs else 0
     e.link = link
+    if tgt:
+        e.tgt, e.lo, e.hi, e.ta, e.tb, e.dflt = tgt["flags"], tgt["lo"], tgt["hi"], tgt["ta"], tgt["tb"], tgt["dflt"]
     return e
+
+
+TGT_ON, TGT_LO, TGT_HI, TGT_DEFAULT, TGT_CAST_SHIFT = 1, 2, 4, 8, 4  # mirrors csrc/common.h
+_CASTS = {None: 0, "round": 1, "ceiling": 2, "floor": 3}
+
+
+def target_post(t, force: bool = False) -> Optional[dict]:
+    """The epilogue's PMML Target stage for a regression value (JPMML ``TargetUtil`` order: clip
+    to [min, max], then ``* rescaleFactor + rescaleConstant``, then ``castInteger``; a row without
+    a prediction takes ``TargetValue defaultValue``). None when the target is a pure rescale that
+    the caller folds into the affine map (``force``: always build the stage, e.g. after a link)."""
+    if t is None:
+        return None
+    dflt = t.values[0].default_value if t.values and t.values[0].default_value is not None else None
+    if not force and t.min is None and t.max is None and not t.cast_integer and dflt is None:
+        return None
+    if t.cast_integer not in _CASTS:
+        raise NotLowerable(f"Target castInteger {t.cast_integer!r}")
+    flags = TGT_ON | (TGT_LO if t.min is not None else 0) | (TGT_HI if t.max is not None else 0) \
+        | (TGT_DEFAULT if dflt is not None else 0) | (_CASTS[t.cast_integer] << TGT_CAST_SHIFT)
+    return dict(flags=flags, lo=float(t.min) if t.min is not None else 0.0,
+                hi=float(t.max) if t.max is not None else 0.0, ta=float(t.rescale_factor),
+                tb=float(t.rescale_constant), dflt=float(dflt) if dflt is not None else 0.0)
+
+
+def apply_target_torch(s, ok, tgt: Optional[dict]):
+    """Torch twin of ``apply_target`` in csrc/epilogue.h (host epilogues: split / sharded / GEMM paths)."""
+    import torch
+
+    if not tgt:
+        return s, ok
+    f = tgt["flags"]
+    if f & TGT_LO:
+        s = torch.where(s < tgt["lo"], torch.full_like(s, tgt["lo"]), s)
+    if f & TGT_HI:
+        s = torch.where(s > tgt["hi"], torch.full_like(s, tgt["hi"]), s)
+    s = s * tgt["ta"] + tgt["tb"]
+    cast = (f >> TGT_CAST_SHIFT) & 3
+    if cast == 1:
+        s = torch.floor(s + 0.5)
+    elif cast == 2:
+        s = torch.ceil(s)
+    elif cast == 3:
+        s = torch.floor(s)
+    ok = ok & torch.isfinite(s)
+    if f & TGT_DEFAULT:
+        s = torch.where(ok, s, torch.full_like(s, tgt["dflt"]))
+        ok = torch.ones_like(ok)
+    return s, ok
 
 
 def _addr(t) -> Optional[int]:
@@ -482,15 +533,12 @@ class LinearPlan(DevicePlan):
             if norm not in LINKS:
                 raise NotLowerable(f"normalizationMethod {norm!r}")
             tgt = ev.target
-            if tgt is not None and (tgt.min is not None or tgt.max is not None or tgt.cast_integer):
-                raise NotLowerable("Target min/max/castInteger is host-only")
             self.epi_args = dict(mode=EPI_AFFINE, link=LINKS[norm])
-            self.post = (tgt.rescale_factor, tgt.rescale_constant) if tgt is not None else (1.0, 0.0)
-            if self.post != (1.0, 0.0) and norm not in ("none", None):
-                raise NotLowerable("Target rescale after a link function is host-only")
-            if norm in ("none", None):
-                self.epi_args.update(a=self.post[0], b=self.post[1])
-                self.W = self.W  # rescale folded into the affine epilogue
+            post = target_post(tgt, force=norm not in ("none", None))  # rescale after a link: Target stage
+            if post is not None:
+                self.epi_args["tgt"] = post
+            elif tgt is not None:
+                self.epi_args.update(a=tgt.rescale_factor, b=tgt.rescale_constant)  # folded
 
     supports_direct = True
 
@@ -560,24 +608,28 @@ def _segments_all_true(mm: ir.MiningModel) -> bool:
     return all(isinstance(s.predicate, ir.TruePredicate) for s in mm.segments)
 
 
-def _target_affine(ev) -> Tuple[float, float]:
+def _target_affine(ev, allow_post: bool = False) -> Tuple[float, float]:
+    """The target's rescale as an affine map folded into the ensemble epilogue; with a clip / cast /
+    default stage (:func:`target_post`) the rescale moves into that stage (``allow_post``: only at
+    the top level, where the epilogue applies it) and the affine map is the identity."""
     t = ev.target
     if t is None:
         return 1.0, 0.0
-    if t.min is not None or t.max is not None or t.cast_integer:
-        raise NotLowerable("Target min/max/castInteger is host-only")
-    if t.values and t.values[0].default_value is not None:
-        raise NotLowerable("Target defaultValue is host-only")
+    if target_post(t) is not None:
+        if not allow_post:
+            raise NotLowerable("nested Target min/max/castInteger/defaultValue is host-only")
+        return 1.0, 0.0
     return t.rescale_factor, t.rescale_constant
 
 
-def _regression_ensemble(ev, field_index, lower=lower_binary_tree) -> Tuple[List[BinaryTree], List[float], float, float]:
+def _regression_ensemble(ev, field_index, lower=lower_binary_tree,
+                         allow_post: bool = False) -> Tuple[List[BinaryTree], List[float], float, float]:
     """Flatten a regression tree / MiningModel(sum|average|weightedAverage) of regression trees
     into (trees, per-tree weights, a, b) with value = a * Σ w_t leaf_t + b."""
     if isinstance(ev, TreeEvaluator):
         if ev.kind != "regression":
             raise NotLowerable("expected a regression tree")
-        a, b = _target_affine(ev)
+        a, b = _target_affine(ev, allow_post)
         return [lower(ev, field_index)], [1.0], a, b
     if isinstance(ev, MiningEvaluator):
         mm = ev.mm
@@ -604,7 +656,7 @@ def _regression_ensemble(ev, field_index, lower=lower_binary_tree) -> Tuple[List
             scale = 1.0 / sum(s.weight for s in mm.segments)
         else:
             scale = 1.0
-        a, b = _target_affine(ev)
+        a, b = _target_affine(ev, allow_post)
         return trees, weights, a * scale, b
     raise NotLowerable(f"{type(ev).__name__} is not a regression tree ensemble")
 
@@ -625,8 +677,12 @@ def ensemble_spec(compiled, lower=lower_binary_tree) -> EnsembleSpec:
     field_index = getattr(compiled, "field_index", None) or {f: i for i, f in enumerate(compiled.active_fields)}
     try:
         if ev.kind == "regression":
-            trees, w, a, b = _regression_ensemble(ev, field_index, lower)
-            return EnsembleSpec(trees, w, 1, 1, dict(mode=EPI_AFFINE, a=a, b=b), None)
+            trees, w, a, b = _regression_ensemble(ev, field_index, lower, allow_post=True)
+            epi = dict(mode=EPI_AFFINE, a=a, b=b)
+            post = target_post(ev.target)
+            if post is not None:
+                epi["tgt"] = post
+            return EnsembleSpec(trees, w, 1, 1, epi, None)
         if isinstance(ev, MiningEvaluator) and ev.mm.multiple_model_method == "modelChain":
             return _chain_spec(compiled, ev, field_index, lower)
         if isinstance(ev, MiningEvaluator) and ev.kind == "classification":
@@ -1308,10 +1364,15 @@ def compile_plan(compiled, device, **opts) -> DevicePlan:
         from .nn_plans import GemmMlpPlan, MlpPlan
 
         prec = "fp32" if policy == "fp32" else "bf16"
+        impl = opts.pop("mlp_impl", "auto")  # auto | fused | gemm
+        if impl not in ("auto", "fused", "gemm"):
+            raise ValueError("mlp_impl must be auto, fused or gemm")
+        if impl == "gemm":
+            return GemmMlpPlan(compiled, device, precision=prec)
         try:
             return MlpPlan(compiled, device, precision=prec, **opts)
         except NotLowerable as e:
-            if "fused kernel" not in str(e):
+            if "fused kernel" not in str(e) or impl == "fused":
                 raise
             return GemmMlpPlan(compiled, device, precision=prec)
     if isinstance(ev, SvmEvaluator):

@@ -292,3 +292,79 @@ def test_tree_shard_string_labels_and_missing_replacement():
     for r in range(2):
         s, v = res[r]
         assert v.all() and (s == ref).all()
+
+
+# ------------------------------------------------------------ model-sharded serving
+def w_sharded(ctx, paths, X, ids_per_rank):
+    from flink_jpmml_amd.domain import AddMessage, DelMessage
+    from flink_jpmml_amd.parallel.serving import DistributedServing
+    from flink_jpmml_amd.utils.metrics import METRICS
+
+    srv = DistributedServing(ctx, placement="sharded")
+    names = [f"a1b2c3d4-0000-4000-8000-{i:012d}" for i in range(len(paths))]
+    srv.apply_control([AddMessage(n, 1, p) for n, p in zip(names, paths)] if ctx.rank == 0 else None)
+    held = sorted(str(k) for k in srv.models)
+    owners = {f"{n}_1": srv.owner(f"{n}_1") for n in names}
+    ids = [f"{names[i]}_1" if i >= 0 else "ffffffff-0000-4000-8000-000000000000_1" for i in ids_per_rank[ctx.rank]]
+    s, v = srv.score_routed(ids, X[ctx.rank])
+    srv.apply_control([DelMessage(names[0], 1)] if ctx.rank == 0 else None)
+    s2, v2 = srv.score_routed(ids, X[ctx.rank])
+    routed = METRICS.summary().get("counters", {}).get("serving.routed_rows", 0)
+    return held, owners, s.tolist(), v.tolist(), v2.tolist(), routed
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_model_sharded_serving_routes_to_owner(world, tmp_path):
+    """Every model is held by exactly one rank; mixed-model batches arriving on any rank are
+    routed to the owners (all_to_all), scored and returned in arrival order == the oracle."""
+    from flink_jpmml_amd.bench.synth import gbdt_pmml, random_forest_pmml, stream_matrix
+    from flink_jpmml_amd.runtime.compiled import CompiledPmml
+
+    txts = [gbdt_pmml(n_trees=5, depth=3, n_features=6, seed=s) for s in range(4)] + \
+        [random_forest_pmml(n_trees=5, depth=3, n_features=6, n_classes=3, seed=9)]
+    paths = []
+    for i, t in enumerate(txts):
+        p = tmp_path / f"m{i}.pmml"
+        p.write_text(t)
+        paths.append(str(p))
+    rng = np.random.default_rng(0)
+    X = [stream_matrix(40 + 7 * r, 6, seed=r) for r in range(world)]
+    ids = [rng.integers(-1, len(paths), len(x)).tolist() for x in X]
+    res = _run(world, w_sharded, paths, X, ids)
+    held_all = sorted(m for r in res.values() for m in r[0])
+    assert len(held_all) == len(paths) and len(set(held_all)) == len(paths)  # one owner per model
+    owners = res[0][1]
+    for r, (held, own, s, v, v2, routed) in res.items():
+        assert own == owners and all(owners[m] == r for m in held)
+        s, v, v2 = np.array(s), np.array(v), np.array(v2)
+        for i, code in enumerate(ids[r]):
+            if code < 0:
+                assert not v[i]
+                continue
+            ref, vref = CompiledPmml.from_string(txts[code]).score_matrix_oracle(X[r][i:i + 1])
+            assert v[i] == vref[0]
+            assert s[i] == pytest.approx(ref[0], abs=1e-6)  # float32 score buffers
+            assert v2[i] == (vref[0] and code != 0)  # model 0 deleted everywhere
+        assert routed > 0
+
+
+def w_evict(ctx, paths):
+    from flink_jpmml_amd.domain import AddMessage
+    from flink_jpmml_amd.parallel.serving import DistributedServing
+    from flink_jpmml_amd.utils.metrics import METRICS
+
+    METRICS.reset()
+    srv = DistributedServing(ctx, cache_capacity=1)
+    names = [f"a1b2c3d4-0000-4000-8000-{i:012d}" for i in range(2)]
+    srv.apply_control([AddMessage(n, 1, p) for n, p in zip(names, paths)] if ctx.rank == 0 else None)
+    X = np.tile(np.array([[1.0, 1.0, 1.0, 1.0], [1.0, 2.0, 3.0, 4.0]]), (3, 1))
+    out = [srv.score(f"{names[i]}_1", X)[0].tolist() for i in (0, 1, 0)]
+    c = METRICS.summary()["counters"]
+    return out, c.get("serving.cache_misses", 0), c.get("serving.cache_evictions", 0)
+
+
+def test_serving_cache_eviction_reloads(fixtures_dir):
+    res = _run(2, w_evict, [fixtures_dir["kmeans"], fixtures_dir["kmeans"]])
+    for out, misses, evictions in res.values():
+        assert out[0] == out[2] == [3.0, 4.0] * 3
+        assert misses >= 2 and evictions >= 2

@@ -1,0 +1,66 @@
+"""PMML ``Target`` post-processing on the device epilogue (csrc/epilogue.h ``apply_target``):
+clip to [min, max], rescale, castInteger, TargetValue defaultValue — tree ensembles, a GLM with a
+link function followed by a rescale, the fused MLP and the GEMM MLP — vs the float64 oracle."""
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _cmp(gpu, txt, F, missing=0.0, n=20_000, tol=1e-4, **kw):
+    from flink_jpmml_amd.bench.synth import stream_matrix
+    from flink_jpmml_amd.runtime.compiled import CompiledPmml
+
+    c = CompiledPmml.from_string(txt)
+    plan = c.plan(gpu, **kw)
+    X = stream_matrix(n, F, seed=3, missing_rate=missing)
+    s, v = plan.score(X)
+    s, v = s.cpu().numpy(), v.cpu().numpy()
+    ref, vref = c.score_matrix_oracle(X)
+    assert (v == vref).all()
+    close = np.abs(s[v] - ref[v]) <= tol
+    return plan, close.mean(), s, ref
+
+
+@pytest.mark.parametrize("cast", [None, "round", "ceiling", "floor"])
+def test_tree_target_clip_rescale_cast(gpu, cast):
+    from flink_jpmml_amd.bench.synth import gbdt_pmml, set_target
+
+    txt = set_target(gbdt_pmml(n_trees=50, depth=5, n_features=8, seed=2), min=-0.2, max=0.25, factor=10.0,
+                     constant=3.0, cast=cast)
+    plan, agree, s, _ = _cmp(gpu, txt, 8, missing=0.02)
+    assert "tgt" in plan.epi_args
+    # castInteger: only values within fp32 noise of a rounding boundary may differ
+    assert agree > (0.999 if cast else 0.99999)
+    assert s.min() >= -2.0 - 1e-5 and s.max() <= 5.5 + 1e-5
+
+
+def test_tree_target_default_value(gpu):
+    from flink_jpmml_amd.bench.synth import gbdt_pmml, set_target
+
+    txt = set_target(gbdt_pmml(n_trees=20, depth=4, n_features=6, seed=1, missing_strategy="nullPrediction"),
+                     default=-5.0)
+    plan, agree, s, ref = _cmp(gpu, txt, 6, missing=0.1)
+    assert agree == 1.0 and (s == -5.0).any() and (s != -5.0).any()
+
+
+def test_glm_link_then_rescale(gpu):
+    from flink_jpmml_amd.bench.synth import glm_pmml, set_target
+
+    txt = set_target(glm_pmml(model_type="generalizedLinear", link="log", n_features=3, seed=1), max=3.0,
+                     factor=0.5, constant=1.0)
+    plan, agree, _, _ = _cmp(gpu, txt, 3, missing=0.0, tol=1e-4)
+    assert agree > 0.9999
+
+
+@pytest.mark.parametrize("kind", ["fused", "gemm"])
+def test_mlp_target(gpu, kind):
+    from flink_jpmml_amd.bench.synth import mlp_pmml, set_target
+
+    txt = set_target(mlp_pmml(n_features=8, hidden=(32, 16), n_out=1, seed=4), min=-0.5, max=0.5, factor=10.0,
+                     cast="floor")
+    opts = {} if kind == "fused" else {"mlp_impl": "gemm"}
+    plan, agree, _, _ = _cmp(gpu, txt, 8, **opts)
+    assert plan.kind == ("mlp" if kind == "fused" else "mlp_gemm")
+    assert agree > 0.999
