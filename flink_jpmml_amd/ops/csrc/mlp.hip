@@ -108,57 +108,126 @@ template <> struct Cfg<false> {
 // shift 0, replacement 0): padded k read column 0 and contribute exactly 0. `contiguous` (identity
 // index) is only set by the host when n_in == k0, so no record load leaves the row.
 
-template <bool BF16>
-__device__ __forceinline__ void load_panel(const MlpArgs& a, int p, int tid, uint4 (&q)[Cfg<BF16>::Q]) {
-  constexpr int T = 64 * Cfg<BF16>::WAVES;
-  const uint4* W4 = reinterpret_cast<const uint4*>(a.weights);
-  const int2 d = a.panels[p % a.n_panels];
-  const int last = d.y > 0 ? d.y - 1 : 0;
-#pragma unroll
-  for (int i = 0; i < Cfg<BF16>::Q; ++i) q[i] = W4[d.x + min(tid + i * T, last)];
+// Panel p -> LDS ring slot p % NSLOT with direct global->LDS loads (global_load_lds_dwordx4, no
+// VGPR staging): thread t copies 16-byte elements t, t+T, ... The LDS destination of one
+// wave-instruction is its wave-uniform base + 16*lane, i.e. elements [64w + jT, 64w + jT + 63]
+// land contiguously, exactly the panel image. Elements past the panel's size re-read its last
+// element into the slot's unused tail (the slot holds a full PANEL).
+//
+// Issued as inline asm rather than __builtin_amdgcn_global_load_lds: the compiler treats the
+// builtin as an LDS write that may alias every later ds_read and drains it (vmcnt(0)) before the
+// chain's first A-fragment read, which serialises the copy with the MFMAs it should overlap.
+// Here the kernel owns the ordering: panel_barrier() retires a panel before any wave reads it,
+// and a slot is rewritten only two steps after its last read (NSLOT = 4). The compiler's own
+// vmcnt waits stay correct: loads retire in order, so an unseen younger load only makes them
+// wait longer.
+__device__ __forceinline__ void glds16(const void* g, uint32_t lds_byte_addr) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(g), "s"(lds_byte_addr) : "memory");
 }
 
 template <bool BF16>
-__device__ __forceinline__ void store_panel(const MlpArgs& a, int p, int tid, uint4* ring,
-                                            const uint4 (&q)[Cfg<BF16>::Q]) {
+__device__ __forceinline__ void issue_panel(const MlpArgs& a, const int2* s_pan, int p, int tid, uint4* ring) {
   constexpr int T = 64 * Cfg<BF16>::WAVES;
-  const int2 d = a.panels[p % a.n_panels];
-  uint4* dst = ring + (p % NSLOT) * (Cfg<BF16>::PANEL / 16);
+  const uint4* W4 = reinterpret_cast<const uint4*>(a.weights);
+  const int2 d = s_pan[p % a.n_panels];
+  const int last = d.y > 0 ? d.y - 1 : 0;
+  // LDS byte address of this wave's destination: the dynamic LDS (ring = its start) begins right
+  // after the kernel's static LDS
+  const uint32_t off = 16u * (uint32_t)((p % NSLOT) * (Cfg<BF16>::PANEL / 16) + (tid & ~63));
+  const uint32_t base = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_groupstaticsize() + off);
+  (void)ring;
 #pragma unroll
-  for (int i = 0; i < Cfg<BF16>::Q; ++i)
-    if (tid + i * T < d.y) dst[tid + i * T] = q[i];
+  for (int i = 0; i < Cfg<BF16>::Q; ++i) glds16(W4 + d.x + min(tid + i * T, last), base + 16u * i * T);
+}
+
+// Retire this thread's loads of the panel issued one step earlier (the one just issued may stay
+// in flight: Q glds per panel), then a raw barrier: every thread's share has landed. A raw
+// s_barrier, not __syncthreads(), whose fence would also drain the panel still in flight.
+template <bool BF16>
+__device__ __forceinline__ void panel_barrier() {
+  if constexpr (Cfg<BF16>::Q == 2) {
+    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+}
+
+// The accumulation chain of one output tile over STEPS k-steps, fully unrolled with no per-step
+// predicate: the A fragments come from the LDS panel (the compiler can issue the ds_reads ahead
+// of the MFMAs), B from registers (compile-time indices keep them in VGPRs).
+template <bool BF16, int STEPS>
+__device__ __forceinline__ void mfma_chain(const uint4* slot, int lane, const typename Cfg<BF16>::B (&pb)[Cfg<BF16>::KS],
+                                           f32x16& acc) {
+  // A fragments run W steps ahead of the MFMA that consumes them (a rolling register window), so
+  // the LDS latency of step s+W overlaps the MFMAs of steps s..s+W-1 instead of stalling each one
+  constexpr int W = STEPS < (BF16 ? 4 : 8) ? STEPS : (BF16 ? 4 : 8);
+  if constexpr (BF16) {
+    uint4 win[W];
+#pragma unroll
+    for (int i = 0; i < W; ++i) win[i] = slot[i * 64 + lane];
+    __builtin_amdgcn_sched_barrier(0);  // keep the window: the scheduler would sink each read to its use
+#pragma unroll
+    for (int s = 0; s < STEPS; ++s) {
+      const uint4 w = win[s % W];
+      if (s + W < STEPS) win[s % W] = slot[(s + W) * 64 + lane];
+      bf16x8 A;
+      __builtin_memcpy(&A, &w, 16);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, pb[s], acc, 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  } else {
+    const float* fs = reinterpret_cast<const float*>(slot);
+    float win[W];
+#pragma unroll
+    for (int i = 0; i < W; ++i) win[i] = fs[i * 64 + lane];
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int s = 0; s < STEPS; ++s) {
+      const float A = win[s % W];
+      if (s + W < STEPS) win[s % W] = fs[(s + W) * 64 + lane];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(A, pb[s], acc, 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+}
+
+// k-step groups: bf16 one k-step (K = 16) per group, fp32 eight (K = 16); the host pads every
+// layer's K to a multiple of 16, so a layer has 1..16 groups and each count is its own chain.
+template <bool BF16>
+__device__ __forceinline__ void mfma_chain_n(int groups, const uint4* slot, int lane,
+                                             const typename Cfg<BF16>::B (&pb)[Cfg<BF16>::KS], f32x16& acc) {
+  constexpr int G = BF16 ? 1 : 8;
+  switch (groups) {
+#define PMML_CHAIN(N) \
+    case N: mfma_chain<BF16, N * G>(slot, lane, pb, acc); break;
+    PMML_CHAIN(1) PMML_CHAIN(2) PMML_CHAIN(3) PMML_CHAIN(4) PMML_CHAIN(5) PMML_CHAIN(6) PMML_CHAIN(7)
+    PMML_CHAIN(8) PMML_CHAIN(9) PMML_CHAIN(10) PMML_CHAIN(11) PMML_CHAIN(12) PMML_CHAIN(13) PMML_CHAIN(14)
+    PMML_CHAIN(15) PMML_CHAIN(16)
+#undef PMML_CHAIN
+    default: break;
+  }
 }
 
 // One 32-unit output tile TI of one layer: a single accumulation chain over the layer's k-steps
 // (A from the LDS panel, B from registers), activation, and the result written into the next
 // layer's B-operand registers (TI is a compile-time index, so nb stays in VGPRs).
 template <bool BF16, int TI>
-__device__ __forceinline__ void tile_step(const MlpArgs& a, const LayerMeta& m, int ksteps, bool last, int h,
-                                          int lane, int tid, uint4* ring, const float* s_b,
+__device__ __forceinline__ void tile_step(const MlpArgs& a, const LayerMeta& m, int groups, bool last, int h,
+                                          int lane, int tid, uint4* ring, const float* s_b, const int2* s_pan,
                                           const typename Cfg<BF16>::B (&pb)[Cfg<BF16>::KS],
-                                          typename Cfg<BF16>::B (&nb)[Cfg<BF16>::KS], f32x16& out, int& p,
-                                          uint4 (&q)[Cfg<BF16>::Q]) {
+                                          typename Cfg<BF16>::B (&nb)[Cfg<BF16>::KS], f32x16& out, int& p) {
   using C = Cfg<BF16>;
-  // prefetch panel p+2 into registers while this one is multiplied
-  load_panel<BF16>(a, p + 2, tid, q);
+  // panel p+2 streams into slot (p+2) % NSLOT while this one is multiplied; that slot was last
+  // read at step p-2, before the previous barrier
+  issue_panel<BF16>(a, s_pan, p + 2, tid, ring);
   const uint4* slot = ring + (p % NSLOT) * (C::PANEL / 16);
   f32x16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = s_b[m.b_off + 32 * TI + acc_row(r, h)];
-#pragma unroll
-  for (int s = 0; s < C::KS; ++s) {
-    if (s < ksteps) {
-      if constexpr (BF16) {
-        const uint4 w = slot[s * 64 + lane];
-        bf16x8 A;
-        __builtin_memcpy(&A, &w, 16);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, pb[s], acc, 0, 0, 0);
-      } else {
-        const float A = reinterpret_cast<const float*>(slot)[s * 64 + lane];
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(A, pb[s], acc, 0, 0, 0);
-      }
-    }
-  }
+  mfma_chain_n<BF16>(groups, slot, lane, pb, acc);
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = activate(m.act, acc[r], m.thr);
   if (last) {
@@ -178,9 +247,7 @@ __device__ __forceinline__ void tile_step(const MlpArgs& a, const LayerMeta& m, 
       for (int r = 0; r < 16; ++r) nb[16 * TI + r] = acc[r];
     }
   }
-  // slot (p+2) % NSLOT was last read at step p-2, before the previous barrier
-  store_panel<BF16>(a, p + 2, tid, ring, q);
-  __syncthreads();
+  panel_barrier<BF16>();  // panel p+1 resident for the next step
   ++p;
 }
 
@@ -197,6 +264,7 @@ __global__ __launch_bounds__(64 * Cfg<BF16>::WAVES, 1) void mlp_kernel(MlpArgs a
   float* s_ms = s_sh + KMAX;
   int* s_ix = reinterpret_cast<int*>(s_ms + KMAX);
   float* s_b = reinterpret_cast<float*>(s_ix + KMAX);              // [MAXL * MT * 32]
+  int2* s_pan = reinterpret_cast<int2*>(s_b + MAXL * MT * 32);      // [MAXL * MT] panel schedule
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -215,14 +283,13 @@ __global__ __launch_bounds__(64 * Cfg<BF16>::WAVES, 1) void mlp_kernel(MlpArgs a
   int nbias = 0;
   for (int L = 0; L < a.n_layers; ++L) nbias = max(nbias, a.layers[L].b_off + a.layers[L].mp);
   for (int i = tid; i < nbias; i += T) s_b[i] = a.biases[i];
-
-  // ---- panel ring prologue: panels 0 and 1
-  uint4 q[C::Q];
-  load_panel<BF16>(a, 0, tid, q);
-  store_panel<BF16>(a, 0, tid, ring, q);
-  load_panel<BF16>(a, 1, tid, q);
-  store_panel<BF16>(a, 1, tid, ring, q);
+  for (int i = tid; i < a.n_panels; i += T) s_pan[i] = a.panels[i];
   __syncthreads();
+
+  // ---- panel ring prologue: panels 0 and 1 (panel 1 may stay in flight into step 0)
+  issue_panel<BF16>(a, s_pan, 0, tid, ring);
+  issue_panel<BF16>(a, s_pan, 1, tid, ring);
+  panel_barrier<BF16>();
 
   const int n_tiles = (a.n_rows + 32 * C::WAVES - 1) / (32 * C::WAVES);
   int p = 0;  // panel counter (runs across row tiles)
@@ -254,23 +321,28 @@ __global__ __launch_bounds__(64 * Cfg<BF16>::WAVES, 1) void mlp_kernel(MlpArgs a
               const int o = 16 * s + j;
               const float x = a.contiguous ? xr[o] : xrow[tix[o]];
               const float y = (x != x) ? tms[o] : fmaf(x, tsc[o], tsh[o]);
-              bad = bad || (y != y);
               v[j] = (__bf16)y;
             }
             pb[s] = v;
           }
           if ((s & 3) == 3) __builtin_amdgcn_sched_barrier(0);
         } else {
-          if (2 * s < a.k0) {
+          if (16 * (s >> 3) < a.k0) {  // whole K=16 groups (k0 is a multiple of 16)
             const int o = 2 * s;
             const float x = a.contiguous ? xr[o] : xrow[tix[o]];
             const float y = (x != x) ? tms[o] : fmaf(x, tsc[o], tsh[o]);
-            bad = bad || (y != y);
             pb[s] = y;
           }
           if ((s & 15) == 15) __builtin_amdgcn_sched_barrier(0);
         }
       }
+    }
+    // Row validity, separately from the unrolled staging (a flag threaded through 128 predicated
+    // steps was mis-scheduled in the fp32 variant): a missing input without a replacement value
+    // invalidates the row (PMML NN rule). Lane halves split the inputs; the loads hit L1.
+    for (int k = h; k < a.n_in; k += 2) {
+      const float x = xrow[s_ix[k]];
+      bad = bad || ((x != x) && (s_ms[k] != s_ms[k]));
     }
     bad = bad && in_range;
     bad = bad || (__shfl_xor((int)bad, 32) != 0);
@@ -279,10 +351,10 @@ __global__ __launch_bounds__(64 * Cfg<BF16>::WAVES, 1) void mlp_kernel(MlpArgs a
     for (int L = 0; L < a.n_layers; ++L) {
       const LayerMeta m = a.layers[L];
       const int mtiles = m.mp >> 5;
-      const int ksteps = BF16 ? (m.kp >> 4) : (m.kp >> 1);
+      const int groups = m.kp >> 4;  // k-step groups of K = 16 (the host pads K to a multiple of 16)
       const bool last = L == a.n_layers - 1;
 #define PMML_TILE(TI) \
-      if (TI < mtiles) tile_step<BF16, TI>(a, m, ksteps, last, h, lane, tid, ring, s_b, pb, nb, out, p, q);
+      if (TI < mtiles) tile_step<BF16, TI>(a, m, groups, last, h, lane, tid, ring, s_b, s_pan, pb, nb, out, p);
       PMML_TILE(0) PMML_TILE(1) PMML_TILE(2) PMML_TILE(3) PMML_TILE(4) PMML_TILE(5) PMML_TILE(6) PMML_TILE(7)
 #undef PMML_TILE
       if (!last) {
@@ -344,7 +416,7 @@ __global__ __launch_bounds__(64 * Cfg<BF16>::WAVES, 1) void mlp_kernel(MlpArgs a
 
 template <bool BF16>
 size_t lds_bytes() {
-  return (size_t)NSLOT * Cfg<BF16>::PANEL + 4 * KMAX * 4 + (size_t)MAXL * MT * 32 * 4;
+  return (size_t)NSLOT * Cfg<BF16>::PANEL + 4 * KMAX * 4 + (size_t)MAXL * MT * 32 * 4 + (size_t)MAXL * MT * 8;
 }
 
 int n_cus() {
@@ -366,7 +438,8 @@ PMML_API int pmml_mlp_layer_meta_size() { return (int)sizeof(LayerMeta); }
 PMML_API int pmml_mlp_launch(hipStream_t stream, const MlpArgs* args, int bf16) {
   const MlpArgs a = *args;
   if (a.n_rows <= 0) return 0;
-  if (a.n_layers < 1 || a.n_layers > MAXL || a.n_out > 32 || a.k0 > KMAX || a.n_in > KMAX || a.n_panels < 1)
+  if (a.n_layers < 1 || a.n_layers > MAXL || a.n_out > 32 || a.k0 > KMAX || a.n_in > KMAX || a.n_panels < 1 ||
+      a.n_panels > MAXL * MT)
     return -4;
   const int waves = bf16 ? Cfg<true>::WAVES : Cfg<false>::WAVES;
   const int n_tiles = (a.n_rows + 32 * waves - 1) / (32 * waves);

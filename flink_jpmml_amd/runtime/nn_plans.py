@@ -75,9 +75,8 @@ def pack_mlp_weights(layers: List[Tuple[np.ndarray, np.ndarray]], precision: str
     for L, (W, b) in enumerate(layers):
         K, M = W.shape
         mp = ((M + 31) // 32) * 32
-        kp = ((K + kstep - 1) // kstep) * kstep if L == 0 else prev_mp
-        if L == 0 and bf16:
-            kp = ((K + 15) // 16) * 16
+        # K padded to whole k-step groups of 16 (csrc/mlp.hip runs one unrolled chain per group count)
+        kp = ((K + 15) // 16) * 16 if L == 0 else prev_mp
         At = np.zeros((mp, kp))  # Wᵀ padded: [units, inputs]
         At[:M, :K] = W.T
         ksteps = kp // kstep

@@ -1040,6 +1040,8 @@ class TreePlan(DevicePlan):
             self.spec = spec
 
             g = pack_general(spec.trees, spec.weights, spec.P, compiled.schema)
+            self.mode, self.tree_w, self.acc_init, self.feat_map = 0, None, None, None
+            self.rows_wide, self.n_stage = TB, F
             self.layout, self.variant, self.rec_words, self.chunk_trees = "general", 0, 0, 0
             self.blob_nan, self.chunk_trees_nan = None, 0
             self.P, self.C = spec.P, spec.C

@@ -25,10 +25,14 @@ def test_mlp_64_256_256_1_many_tiles(gpu, precision, tol):
     plan = c.plan(gpu, precision=precision)
     assert isinstance(plan, MlpPlan) and plan.contiguous == 1 and plan.n_panels == 17
     X = stream_matrix(300_000, 64, seed=11)
-    X[[7, 123_456, 299_999], [1, 63, 0]] = np.nan
+    nan_rows = [7, 123_456, 299_999]
+    X[nan_rows, [1, 63, 0]] = np.nan
     s, v = _np(plan, X)
-    ref, vref = c.score_matrix_oracle(X)
-    assert (v == vref).all() and not v[[7, 123_456, 299_999]].any()
+    # the per-connection oracle is slow: check every 97th row (all tiles, both lane halves) + the NaN rows
+    idx = np.union1d(np.arange(0, len(X), 97), nan_rows)
+    s, v = s[idx], v[idx]
+    ref, vref = c.score_matrix_oracle(X[idx])
+    assert (v == vref).all() and not v[np.searchsorted(idx, nan_rows)].any()
     scale = max(1.0, float(np.max(np.abs(ref[vref]))))
     assert np.max(np.abs(s[v] - ref[v])) < tol * scale
 

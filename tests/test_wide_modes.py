@@ -170,3 +170,34 @@ def test_feature_compaction_map():
     c, plan = _plan(gbdt_pmml(n_trees=3, depth=2, n_features=300, seed=7))
     assert plan.feat_map is not None and plan.n_stage <= 12 and plan.rows_wide == 256
     _check(c, plan, stream_matrix(600, 300, seed=8, missing_rate=0.1), tol=1e-4)
+
+
+@pytest.mark.parametrize("case", ["general-reg", "general-cls", "vote8", "slot", "pointer", "fp8"])
+def test_plan_state_roundtrip_dry(case):
+    """Every TreePlan variant exports / re-imports its state (the RCCL model replication path)."""
+    import sys
+
+    from flink_jpmml_amd.runtime.plans import DevicePlan
+
+    sys.path.insert(0, __file__.rsplit("/", 1)[0])
+    from test_general_tree import general_tree_doc
+
+    txt, kw = {
+        "general-reg": (general_tree_doc(4, "defaultChild", "returnLastPrediction", n_trees=5), {}),
+        "general-cls": (general_tree_doc(4, "defaultChild", "returnLastPrediction", n_trees=5,
+                                         classification=True), {}),
+        "vote8": (random_forest_pmml(n_trees=8, depth=4, n_features=6, n_classes=3), {}),
+        "slot": (gbdt_pmml(n_trees=4, depth=3, n_features=6, objective="multiclass", n_classes=3), {}),
+        "pointer": (gbdt_pmml(n_trees=4, depth=3, n_features=6), {"layout": "pointer"}),
+        "fp8": (gbdt_pmml(n_trees=4, depth=3, n_features=6), {"precision": "fp8"}),
+    }[case]
+    c, plan = _plan(txt, **kw)
+    with lowering_dry_run():
+        meta, tensors = plan.export_state()
+        q = DevicePlan.from_state(meta, {k: t.clone() for k, t in tensors.items()}, torch.device("cpu"))
+    for k in TreePlan._STATE:
+        a, b = getattr(plan, k), getattr(q, k)
+        if isinstance(a, torch.Tensor):
+            assert torch.equal(a, b), k
+        else:
+            assert a == b, k
