@@ -147,18 +147,27 @@ class Prediction:
     def on_failed_prediction(err: BaseException) -> "Prediction":
         """Log by failure class and return the shared empty prediction
         (`S/models/prediction/Prediction.scala:47-62`)."""
+        from ..utils.metrics import METRICS
+
         if isinstance(err, JPMMLExtractionException):
+            cause = "extraction"
             logger.warning("Error while extracting results: %s", err)
         elif isinstance(err, InputPreparationException):
+            cause = "preparation"
             logger.warning("Error while preparing input: %s", err)
         elif isinstance(err, InputValidationException):
+            cause = "validation"
             logger.warning("Error while validate input: %s", err)
         elif isinstance(err, EvaluationException):
+            cause = "evaluation"
             logger.warning("Error while evaluate model: %s", err)
         elif isinstance(err, (TypeError, ValueError)):  # ClassCastException analogue
+            cause = "target_cast"
             logger.error("Error while extract target: %s", err)
         else:
+            cause = "other"
             logger.error("Error: %r", err)
+        METRICS.inc(f"scoring.empty_score.{cause}")  # EmptyScore counts by failure cause (SURVEY §5.5)
         return EMPTY_PREDICTION
 
     extractPrediction = extract_prediction  # noqa: N815 - Scala-style alias

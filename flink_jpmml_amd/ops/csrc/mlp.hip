@@ -211,13 +211,33 @@ __device__ __forceinline__ void mfma_chain_n(int groups, const uint4* slot, int 
   }
 }
 
-// One 32-unit output tile TI of one layer: a single accumulation chain over the layer's k-steps
-// (A from the LDS panel, B from registers), activation, and the result written into the next
-// layer's B-operand registers (TI is a compile-time index, so nb stays in VGPRs).
+// Write the activated accumulator of output tile TI into the next layer's B registers. TI is a
+// compile-time index so nb stays in VGPRs; this is the only per-tile code copy (the MFMA chain is
+// shared by all tiles, keeping the hot loop small enough for the instruction cache).
 template <bool BF16, int TI>
-__device__ __forceinline__ void tile_step(const MlpArgs& a, const LayerMeta& m, int groups, bool last, int h,
-                                          int lane, int tid, uint4* ring, const float* s_b, const int2* s_pan,
-                                          const typename Cfg<BF16>::B (&pb)[Cfg<BF16>::KS],
+__device__ __forceinline__ void store_nb(const f32x16& acc, typename Cfg<BF16>::B (&nb)[Cfg<BF16>::KS]) {
+  if constexpr (BF16) {
+    bf16x8 lo, hi;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      lo[j] = (__bf16)acc[j];
+      hi[j] = (__bf16)acc[8 + j];
+    }
+    nb[2 * TI] = lo;
+    nb[2 * TI + 1] = hi;
+  } else {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) nb[16 * TI + r] = acc[r];
+  }
+}
+
+// One 32-unit output tile ti of one layer: a single accumulation chain over the layer's k-steps
+// (A from the LDS panel, B from registers), activation, and the result written into the next
+// layer's B-operand registers.
+template <bool BF16>
+__device__ __forceinline__ void tile_step(const MlpArgs& a, const LayerMeta& m, int ti, int groups, bool last,
+                                          int h, int lane, int tid, const float* s_b, const int2* s_pan,
+                                          uint4* ring, const typename Cfg<BF16>::B (&pb)[Cfg<BF16>::KS],
                                           typename Cfg<BF16>::B (&nb)[Cfg<BF16>::KS], f32x16& out, int& p) {
   using C = Cfg<BF16>;
   // panel p+2 streams into slot (p+2) % NSLOT while this one is multiplied; that slot was last
@@ -226,25 +246,22 @@ __device__ __forceinline__ void tile_step(const MlpArgs& a, const LayerMeta& m, 
   const uint4* slot = ring + (p % NSLOT) * (C::PANEL / 16);
   f32x16 acc;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = s_b[m.b_off + 32 * TI + acc_row(r, h)];
+  for (int r = 0; r < 16; ++r) acc[r] = s_b[m.b_off + 32 * ti + acc_row(r, h)];
   mfma_chain_n<BF16>(groups, slot, lane, pb, acc);
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = activate(m.act, acc[r], m.thr);
   if (last) {
-    if (TI == 0) out = acc;
+    if (ti == 0) out = acc;
   } else {
-    if constexpr (BF16) {
-      bf16x8 lo, hi;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        lo[j] = (__bf16)acc[j];
-        hi[j] = (__bf16)acc[8 + j];
-      }
-      nb[2 * TI] = lo;
-      nb[2 * TI + 1] = hi;
-    } else {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) nb[16 * TI + r] = acc[r];
+    switch (ti) {
+      case 0: store_nb<BF16, 0>(acc, nb); break;
+      case 1: store_nb<BF16, 1>(acc, nb); break;
+      case 2: store_nb<BF16, 2>(acc, nb); break;
+      case 3: store_nb<BF16, 3>(acc, nb); break;
+      case 4: store_nb<BF16, 4>(acc, nb); break;
+      case 5: store_nb<BF16, 5>(acc, nb); break;
+      case 6: store_nb<BF16, 6>(acc, nb); break;
+      default: store_nb<BF16, 7>(acc, nb); break;
     }
   }
   panel_barrier<BF16>();  // panel p+1 resident for the next step
@@ -265,6 +282,7 @@ __global__ __launch_bounds__(64 * Cfg<BF16>::WAVES, 1) void mlp_kernel(MlpArgs a
   int* s_ix = reinterpret_cast<int*>(s_ms + KMAX);
   float* s_b = reinterpret_cast<float*>(s_ix + KMAX);              // [MAXL * MT * 32]
   int2* s_pan = reinterpret_cast<int2*>(s_b + MAXL * MT * 32);      // [MAXL * MT] panel schedule
+  int* s_rowbad = reinterpret_cast<int*>(s_pan + MAXL * MT);          // [WAVES * 32] row invalid flags
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -297,7 +315,6 @@ __global__ __launch_bounds__(64 * Cfg<BF16>::WAVES, 1) void mlp_kernel(MlpArgs a
     const int row = (tile * C::WAVES + wave) * 32 + col;
     const bool in_range = row < a.n_rows;
     const float* xrow = a.X + (size_t)(in_range ? row : 0) * a.ldx;
-    bool bad = false;
 
     // ---- layer-0 B operands straight from the record (normalised), into pb. The lane's table
     // offset goes through an opaque register each tile, so the per-k LDS addresses stay
@@ -337,15 +354,17 @@ __global__ __launch_bounds__(64 * Cfg<BF16>::WAVES, 1) void mlp_kernel(MlpArgs a
         }
       }
     }
-    // Row validity, separately from the unrolled staging (a flag threaded through 128 predicated
-    // steps was mis-scheduled in the fp32 variant): a missing input without a replacement value
-    // invalidates the row (PMML NN rule). Lane halves split the inputs; the loads hit L1.
+    // Row validity: a missing input without a replacement value invalidates the row (PMML NN
+    // rule). Kept in LDS (one int per row of the tile), not in a register flag: a boolean lives in
+    // an SGPR lane mask across the whole layer loop, and that mask came back wrong on the GPU
+    // (twice, in differently scheduled variants). Lane halves split the inputs; the record loads
+    // hit L1. Same-wave LDS operations complete in order: the h == 0 clear lands before any set.
+    volatile int* rbad = s_rowbad + wave * 32 + col;  // both lane halves write it: no forwarding
+    if (h == 0) *rbad = 0;
     for (int k = h; k < a.n_in; k += 2) {
       const float x = xrow[s_ix[k]];
-      bad = bad || ((x != x) && (s_ms[k] != s_ms[k]));
+      if ((x != x) && (s_ms[k] != s_ms[k])) *rbad = 1;
     }
-    bad = bad && in_range;
-    bad = bad || (__shfl_xor((int)bad, 32) != 0);
 
     f32x16 out = {};
     for (int L = 0; L < a.n_layers; ++L) {
@@ -353,10 +372,9 @@ __global__ __launch_bounds__(64 * Cfg<BF16>::WAVES, 1) void mlp_kernel(MlpArgs a
       const int mtiles = m.mp >> 5;
       const int groups = m.kp >> 4;  // k-step groups of K = 16 (the host pads K to a multiple of 16)
       const bool last = L == a.n_layers - 1;
-#define PMML_TILE(TI) \
-      if (TI < mtiles) tile_step<BF16, TI>(a, m, groups, last, h, lane, tid, ring, s_b, s_pan, pb, nb, out, p);
-      PMML_TILE(0) PMML_TILE(1) PMML_TILE(2) PMML_TILE(3) PMML_TILE(4) PMML_TILE(5) PMML_TILE(6) PMML_TILE(7)
-#undef PMML_TILE
+#pragma unroll 1
+      for (int ti = 0; ti < mtiles; ++ti)
+        tile_step<BF16>(a, m, ti, groups, last, h, lane, tid, s_b, s_pan, ring, pb, nb, out, p);
       if (!last) {
 #pragma unroll
         for (int s = 0; s < KS; ++s) pb[s] = nb[s];
@@ -366,6 +384,7 @@ __global__ __launch_bounds__(64 * Cfg<BF16>::WAVES, 1) void mlp_kernel(MlpArgs a
     // ---- output layer: units 0..n_out-1 live in tile 0; lanes l and l^32 hold the two halves
     if (a.final_norm == 0 && a.n_out == 1) {
       if (h == 0 && in_range) {
+        const bool bad = *rbad != 0;
         apply_epilogue(a.epi, [&](int) { return out[0]; }, !bad, row, a.n_rows, a.score, a.valid, a.probs);
       }
       continue;
@@ -401,7 +420,7 @@ __global__ __launch_bounds__(64 * Cfg<BF16>::WAVES, 1) void mlp_kernel(MlpArgs a
     const int ou = __shfl_xor(best_u, 32);
     if (ob > best || (ob == best && ou < best_u)) { best = ob; best_u = ou; }
     if (h == 0 && in_range) {
-      bool ok = !bad && best == best && best_u < a.n_out;
+      bool ok = *rbad == 0 && best == best && best_u < a.n_out;
       float sc = ok ? (a.epi.has_table ? a.epi.table[best_u] : (float)best_u) : __builtin_nanf("");
       ok = ok && (sc == sc);
       a.score[row] = ok ? sc : __builtin_nanf("");
@@ -416,7 +435,8 @@ __global__ __launch_bounds__(64 * Cfg<BF16>::WAVES, 1) void mlp_kernel(MlpArgs a
 
 template <bool BF16>
 size_t lds_bytes() {
-  return (size_t)NSLOT * Cfg<BF16>::PANEL + 4 * KMAX * 4 + (size_t)MAXL * MT * 32 * 4 + (size_t)MAXL * MT * 8;
+  return (size_t)NSLOT * Cfg<BF16>::PANEL + 4 * KMAX * 4 + (size_t)MAXL * MT * 32 * 4 + (size_t)MAXL * MT * 8 +
+         (size_t)Cfg<BF16>::WAVES * 32 * 4;
 }
 
 int n_cus() {

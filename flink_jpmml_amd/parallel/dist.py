@@ -273,6 +273,9 @@ def all_gather_scores(score: torch.Tensor, valid: torch.Tensor, ctx: DistContext
         gs, gv = out
     w1 = dist.all_gather_into_tensor(gs, score.contiguous(), async_op=async_op)
     w2 = dist.all_gather_into_tensor(gv, valid.contiguous(), async_op=async_op)
+    from ..utils.metrics import METRICS
+
+    METRICS.inc("dist.bytes_all_gather", gs.numel() * gs.element_size() + gv.numel() * gv.element_size())
     return gs, gv, ([w1, w2] if async_op else [])
 
 
@@ -289,6 +292,9 @@ def all_gather_varlen(t: torch.Tensor, ctx: DistContext) -> torch.Tensor:
     pad[: t.shape[0]] = t
     out = torch.empty((m * ctx.world_size,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
     dist.all_gather_into_tensor(out, pad)
+    from ..utils.metrics import METRICS
+
+    METRICS.inc("dist.bytes_all_gather", out.numel() * out.element_size())
     parts = [out[i * m: i * m + s] for i, s in enumerate(sizes_i)]
     return torch.cat(parts)
 

@@ -1038,6 +1038,7 @@ class TreePlan(DevicePlan):
                 raise NotLowerable("K-class chains with intercepts over non-binary trees are host-only")
             spec = to_general(spec)
             self.spec = spec
+            self.n_trees = len(spec.trees)
 
             g = pack_general(spec.trees, spec.weights, spec.P, compiled.schema)
             self.mode, self.tree_w, self.acc_init, self.feat_map = 0, None, None, None
@@ -1074,6 +1075,7 @@ class TreePlan(DevicePlan):
             layout = "perfect" if depth <= 10 and (wide_ok or F <= 64) and rec_bytes <= 32 * 1024 else "pointer"
         if spec.mode != "sum" and not (layout == "perfect" and wide_ok):
             spec = to_general(spec)  # votes / class slots accumulate in LDS on the narrow kernels
+            self.n_trees = len(spec.trees)  # + constant stumps carrying the per-class intercepts
         self.spec = spec
         self.layout = layout
         self.P, self.C = spec.P, spec.C

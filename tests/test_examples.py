@@ -42,3 +42,23 @@ def test_sources_policies():
     assert len(evs) == 6 and all(e.model_id.endswith("_1") for e in evs)
     assert all(0.2 <= v <= 6.0 for e in evs for v in e.to_vector().data)
     assert list(IrisSource(None, n=2).iterate())[0].model_id is None  # no crash without ids (reference bug)
+
+
+def test_example_config_flags_and_metrics(fixtures_dir, tmp_path):
+    """Config flags reach the job (size-or-time flush under a rate-limited source) and the run's
+    metrics are written as JSON."""
+    import json
+
+    from flink_jpmml_amd.examples.jobs import main, scoring_config, build_parser
+
+    out, met = tmp_path / "q.txt", tmp_path / "m.jsonl"
+    rc = main(["quick", "--model", fixtures_dir["kmeans"], "--output", str(out), "--records", "12",
+               "--batch-size", "1024", "--max-batch-latency-ms", "5", "--rate", "400", "--fallback", "error",
+               "--metrics-out", str(met)])
+    assert rc == 0 and len(out.read_text().splitlines()) == 12
+    m = json.loads(met.read_text().splitlines()[-1])
+    assert m["counters"].get("batcher.latency_flushes", 0) >= 1  # a 1024 batch never fills: time flushes
+    args = build_parser().parse_args(["quick", "--model", "x", "--output", "-", "--precision", "bf16",
+                                      "--cache-capacity", "3", "--micro-batch", "4096"])
+    cfg = scoring_config(args)
+    assert cfg.precision == "bf16" and cfg.cache_capacity == 3 and cfg.micro_batch == 4096

@@ -8,13 +8,13 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def _cmp(gpu, txt, F, missing=0.0, n=20_000, tol=1e-4, **kw):
+def _cmp(gpu, txt, F=None, missing=0.0, n=20_000, tol=1e-4, **kw):
     from flink_jpmml_amd.bench.synth import stream_matrix
     from flink_jpmml_amd.runtime.compiled import CompiledPmml
 
     c = CompiledPmml.from_string(txt)
     plan = c.plan(gpu, **kw)
-    X = stream_matrix(n, F, seed=3, missing_rate=missing)
+    X = stream_matrix(n, F or c.n_features, seed=3, missing_rate=missing)
     s, v = plan.score(X)
     s, v = s.cpu().numpy(), v.cpu().numpy()
     ref, vref = c.score_matrix_oracle(X)
@@ -33,7 +33,7 @@ def test_tree_target_clip_rescale_cast(gpu, cast):
     assert "tgt" in plan.epi_args
     # castInteger: only values within fp32 noise of a rounding boundary may differ
     assert agree > (0.999 if cast else 0.99999)
-    assert s.min() >= -2.0 - 1e-5 and s.max() <= 5.5 + 1e-5
+    assert s.min() >= 1.0 - 1e-5 and s.max() <= 6.0 + 1e-5  # clip [-0.2, 0.25] * 10 + 3, then the cast
 
 
 def test_tree_target_default_value(gpu):
@@ -50,7 +50,7 @@ def test_glm_link_then_rescale(gpu):
 
     txt = set_target(glm_pmml(model_type="generalizedLinear", link="log", n_features=3, seed=1), max=3.0,
                      factor=0.5, constant=1.0)
-    plan, agree, _, _ = _cmp(gpu, txt, 3, missing=0.0, tol=1e-4)
+    plan, agree, _, _ = _cmp(gpu, txt, None, missing=0.0, tol=1e-4)
     assert agree > 0.9999
 
 

@@ -201,3 +201,30 @@ def test_plan_state_roundtrip_dry(case):
             assert torch.equal(a, b), k
         else:
             assert a == b, k
+
+
+def test_many_class_chain_general_slots_with_intercept_stumps():
+    """K > 8 classes: the narrow kernel's LDS class slots; intercepts travel as constant stump
+    trees (to_general) and must be counted in n_trees."""
+    from flink_jpmml_amd.runtime.plans import TB
+
+    c, p = _plan(gbdt_pmml(n_trees=10, depth=4, n_features=12, objective="multiclass", n_classes=12, seed=2))
+    assert p.variant == 0 and p.general == 1 and p.C == 12 and p.n_trees == 120 + 11
+    X = stream_matrix(2000, 12, seed=3)
+    ref, _ = c.score_matrix_oracle(X)
+    D = p.depth
+    NI, NL = (1 << D) - 1, 1 << D
+    blob = p.blob.numpy().view(np.uint32).reshape(p.n_trees, p.rec_words)
+    slots = p.slots.numpy()
+    acc = np.zeros((len(X), p.C))
+    Xf = X.astype(np.float32)
+    for t in range(p.n_trees):
+        T = blob[t, 0:2 * NI:2].view(np.float32)
+        meta = blob[t, 1:2 * NI:2]
+        leaves = blob[t, 2 * NI:2 * NI + NL].view(np.float32)
+        j = np.ones(len(X), np.int64)
+        for _ in range(D):
+            j = 2 * j + (Xf[np.arange(len(X)), meta[j - 1] // (TB * 4)] >= T[j - 1])
+        acc[:, slots[t]] += leaves[j - NL]
+    tab = np.array([float(v) for v in p.labels])
+    assert (tab[np.argmax(acc, axis=1)] == ref).all()
