@@ -645,3 +645,69 @@ def set_target(txt: str, field: str = "y", min: Optional[float] = None, max: Opt
         return txt[:m.start()] + new + txt[m.end():]
     i = txt.find("</MiningSchema>") + len("</MiningSchema>")
     return txt[:i] + "\n  " + new + txt[i:]
+
+
+def segmented_pmml(method: str = "selectFirst", classification: bool = False, n_segments: int = 4,
+                   depth: int = 3, n_features: int = 6, n_classes: int = 3, seed: int = 0,
+                   predicates: bool = True, missing_treatment: Optional[str] = None,
+                   linear_segment: bool = False) -> str:
+    """MiningModel with per-segment predicates over small trees (and optionally one
+    RegressionModel segment): ``selectFirst`` / ``max`` / ``min`` / ``median`` / ``sum`` /
+    ``average`` / ``weightedAverage`` (regression) or ``majorityVote`` / ``weightedMajorityVote``
+    / ``selectFirst`` (classification) — the segmentations the fused ensemble kernels refuse.
+    Segment predicates mix Simple (incl. isMissing), SimpleSet and Compound(and/or/surrogate)."""
+    rng = np.random.default_rng(seed)
+    thresholds = np.sort(rng.standard_normal((n_features, 64)).astype(np.float32), axis=1)
+    cats = [str(c) for c in range(n_classes)]
+    out = io.StringIO()
+    _header(out, f"synthetic segmented MiningModel ({method})")
+    _data_dictionary(out, n_features, "y", "integer" if classification else "double",
+                     cats if classification else None)
+    fn = "classification" if classification else "regression"
+    mpt = f' missingPredictionTreatment="{missing_treatment}"' if missing_treatment else ""
+    out.write(f' <MiningModel functionName="{fn}">\n')
+    _mining_schema(out, n_features, "y", "  ")
+    out.write(f'  <Segmentation multipleModelMethod="{method}"{mpt}>\n')
+
+    def pred(i: int) -> str:
+        if not predicates:
+            return "<True/>"
+        f, g = int(rng.integers(n_features)), int(rng.integers(n_features))
+        v = _fnum(float(rng.standard_normal() * 0.5))
+        kind = i % 5
+        if kind == 0:
+            return f'<SimplePredicate field="f{f}" operator="greaterThan" value="{v}"/>'
+        if kind == 1:
+            return (f'<CompoundPredicate booleanOperator="and"><SimplePredicate field="f{f}" operator="lessOrEqual" '
+                    f'value="{v}"/><SimplePredicate field="f{g}" operator="notEqual" value="0"/></CompoundPredicate>')
+        if kind == 2:
+            return (f'<CompoundPredicate booleanOperator="surrogate"><SimplePredicate field="f{f}" '
+                    f'operator="lessThan" value="{v}"/><SimplePredicate field="f{g}" operator="isMissing"/>'
+                    '</CompoundPredicate>')
+        if kind == 3:
+            return (f'<CompoundPredicate booleanOperator="or"><SimplePredicate field="f{f}" operator="greaterOrEqual" '
+                    f'value="{v}"/><SimplePredicate field="f{g}" operator="isMissing"/></CompoundPredicate>')
+        return "<True/>"
+
+    for i in range(n_segments):
+        w = _fnum(float(rng.uniform(0.5, 2.0)))
+        out.write(f'   <Segment id="{i + 1}" weight="{w}">{pred(i)}\n')
+        if linear_segment and i == n_segments - 1 and not classification:
+            out.write('    <RegressionModel functionName="regression">\n')
+            _mining_schema(out, n_features, "y", "     ")
+            out.write(f'     <RegressionTable intercept="{_fnum(float(rng.standard_normal()))}">')
+            for j in range(n_features):
+                out.write(f'<NumericPredictor name="f{j}" coefficient="{_fnum(float(rng.standard_normal()))}"/>')
+            out.write('</RegressionTable>\n    </RegressionModel>\n')
+        else:
+            g = _TreeGen(rng, n_features, depth, 0.9, thresholds)
+            out.write(f'    <TreeModel functionName="{fn}" missingValueStrategy="defaultChild" '
+                      'splitCharacteristic="binarySplit">\n')
+            _mining_schema(out, n_features, "y", "     ")
+            leaf = (lambda: cats[int(rng.integers(n_classes))]) if classification \
+                else (lambda: _fnum(float(rng.standard_normal())))
+            g.write(out, 0, "<True/>", leaf, "     ", force_split=True)
+            out.write('    </TreeModel>\n')
+        out.write('   </Segment>\n')
+    out.write('  </Segmentation>\n </MiningModel>\n</PMML>\n')
+    return out.getvalue()

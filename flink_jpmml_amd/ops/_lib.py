@@ -125,8 +125,8 @@ class FieldPrep(ctypes.Structure):
 class Epilogue(ctypes.Structure):
     _fields_ = [("mode", c_int), ("n_classes", c_int), ("a", c_float), ("b", c_float), ("thr", c_float),
                 ("has_table", c_int), ("table", c_void_p), ("write_probs", c_int), ("link", c_int),
-                ("score2", c_void_p), ("valid2", c_void_p), ("tgt", c_int), ("lo", c_float), ("hi", c_float),
-                ("ta", c_float), ("tb", c_float), ("dflt", c_float)]
+                ("score2", c_void_p), ("valid2", c_void_p), ("tgt", c_int), ("dflt", c_float),
+                ("lo", ctypes.c_double), ("hi", ctypes.c_double), ("ta", ctypes.c_double), ("tb", ctypes.c_double)]
 
 
 class TreeArgs(ctypes.Structure):

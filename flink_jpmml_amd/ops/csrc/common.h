@@ -86,9 +86,11 @@ struct Epilogue {
   float* score2;        // optional mirror outputs (e.g. device copy beside a zero-copy host sink)
   uint8_t* valid2;
   int tgt;              // TGT_* flags: PMML Target post-processing of an EPI_AFFINE value
-  float lo, hi;         // Target min / max (clip, applied first)
-  float ta, tb;         // Target rescaleFactor / rescaleConstant (after the clip)
   float dflt;           // TargetValue defaultValue (rows without a prediction)
+  double lo, hi;        // Target min / max (clip, applied first)
+  double ta, tb;        // Target rescaleFactor / rescaleConstant (after the clip)
+                        // fp64 like the oracle: a clipped value rescales to the exact constant
+                        // (fp32 -0.2 * 10 + 3 lands below 1.0 and floors to 0)
 };
 
 // Target post-processing (JPMML TargetUtil order): clip to [min, max], rescale, castInteger;

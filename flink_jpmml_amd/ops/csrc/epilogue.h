@@ -2,16 +2,18 @@
 #pragma once
 #include "common.h"
 
-__device__ __forceinline__ float apply_target(const Epilogue& e, float v) {
+__device__ __forceinline__ float apply_target(const Epilogue& e, float s) {
+  double v = (double)s;
   if ((e.tgt & TGT_LO) && v < e.lo) v = e.lo;  // compare form: a NaN stays NaN (no prediction)
   if ((e.tgt & TGT_HI) && v > e.hi) v = e.hi;
-  v = fmaf(v, e.ta, e.tb);
+  v = v * e.ta + e.tb;
   switch ((e.tgt >> TGT_CAST_SHIFT) & 3) {
-    case CAST_ROUND: return floorf(v + 0.5f);
-    case CAST_CEIL: return ceilf(v);
-    case CAST_FLOOR: return floorf(v);
-    default: return v;
+    case CAST_ROUND: v = floor(v + 0.5); break;
+    case CAST_CEIL: v = ceil(v); break;
+    case CAST_FLOOR: v = floor(v); break;
+    default: break;
   }
+  return (float)v;
 }
 
 // acc: C accumulator values of this row (registers or LDS, read through the accessor).
@@ -24,8 +26,8 @@ __device__ __forceinline__ void apply_epilogue(const Epilogue& e, Acc acc, bool 
   int label = 0;
   if (e.mode == EPI_AFFINE) {
     s = apply_link(e.link, fmaf(e.a, acc(0), e.b));
-    if (e.tgt) s = apply_target(e, s);
     ok = ok && __builtin_isfinite(s);  // the oracle's regression rule: a non-finite value is no prediction
+    if (e.tgt) s = apply_target(e, s);  // on the model value, after its validity (oracle order)
     if (!ok && (e.tgt & TGT_DEFAULT)) {
       s = e.dflt;
       ok = true;

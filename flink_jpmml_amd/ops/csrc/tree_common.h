@@ -311,10 +311,12 @@ __global__ __launch_bounds__(TB, 2) void tree_perfect_kernel(TreeArgs a) {
 // G partial results of a row are combined in fixed order (deterministic).
 //  * ROWS shrinks as the staged feature count grows (<= 64 / 128 / 256 columns): the feature
 //    planes stay <= 64 KiB and 16 waves stay resident; beyond that the POINTER layout takes over;
-//  * feature planes are [F][ROWS + 1] (one pad float per plane): the staging store of one row's
-//    consecutive features hits consecutive banks (it was a 32-way conflict with a [F][ROWS]
-//    image), the traversal read of one feature by 32 consecutive rows stays conflict free, and
-//    the pad is folded into the per-node feature byte offset (no extra VALU per level);
+//  * feature planes are [F][ROWS]: a traversal read by 32 consecutive rows hits bank r mod 32
+//    whatever feature each lane's node tests (measured: a +1 pad per plane made that bank
+//    (f + r) mod 32 and cost 35 % extra LDS cycles, SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE).
+//    The staging store keeps the same property: each 32-lane group writes 32 consecutive rows
+//    of one feature (its global reads are row-strided; staging is once per tile, traversal once
+//    per tree and level);
 //  * `feat_map` stages only the columns the trees use (compaction of wide records);
 //  * accumulation modes: SUM (regression / binary chain), SLOT (multi-class GBDT: each tree adds
 //    its leaf to one class slot — wave-uniform, contiguous runs), CLASS (majority vote: the leaf is
@@ -328,7 +330,7 @@ template <int ROWS>
 struct WideGeom {
   static constexpr int RS = ROWS / 32;  // row sets
   static constexpr int G = 32 / RS;     // tree groups
-  static constexpr int PS = ROWS + 1;   // feature plane stride (floats)
+  static constexpr int PS = ROWS;       // feature plane stride (floats)
 };
 
 #define PF4_DECL uint4 pq0, pq1, pq2, pq3;
@@ -599,8 +601,12 @@ __global__ __launch_bounds__(WIDE_T, 1) void tree_perfect_wide_kernel(TreeArgs a
     const int total = ROWS * F;
     bool miss = false;
     for (int e = tid; e < total; e += T) {
-      const int r = e / F;
-      const int f = e - r * F;
+      // item e: row (e & 31) + 32 * ((e >> 5) / F) of feature (e >> 5) % F — the 32 lanes of a
+      // group store 32 consecutive rows of one plane (distinct banks)
+      const int q = e >> 5;
+      const int rh = q / F;
+      const int f = q - rh * F;
+      const int r = 32 * rh + (e & 31);
       const int row = row0 + r;
       float x = 0.f;
       bool b = false;
@@ -756,7 +762,7 @@ int launch_perfect(hipStream_t st, const TreeArgs& a, dim3 grid, size_t lds) {
     const int rows = a.rows_wide;
     const int G = WIDE_T / rows;
     const size_t head = (size_t)(rows + 4) * 4 + (size_t)G * rows * 4;
-    const size_t plane = (size_t)a.n_stage * (rows + 1) * 4;
+    const size_t plane = (size_t)a.n_stage * rows * 4;
     size_t lds_w = head + plane + 2 * (size_t)a.chunk_trees * a.rec_words * 4;
     if ((size_t)a.chunk_trees * a.rec_words > (size_t)WIDE_T * 4 * 4) return -9;
     if (a.blob_nan) {

@@ -265,6 +265,8 @@ class DevicePlan:
         cls = {c.__name__: c for c in (TreePlan, ClusterPlan, LinearPlan)}.get(meta["__class__"])
         if cls is None and meta["__class__"] == "DerivedPlan":
             from .derive import DerivedPlan as cls
+        if cls is None and meta["__class__"] == "SegmentedPlan":
+            from .segmented import SegmentedPlan as cls
         if cls is None:
             from . import nn_plans
 
@@ -360,6 +362,8 @@ def apply_target_torch(s, ok, tgt: Optional[dict]):
     if not tgt:
         return s, ok
     f = tgt["flags"]
+    out_dtype = s.dtype
+    s = s.double()  # fp64 like csrc/epilogue.h apply_target (and the oracle)
     if f & TGT_LO:
         s = torch.where(s < tgt["lo"], torch.full_like(s, tgt["lo"]), s)
     if f & TGT_HI:
@@ -372,11 +376,10 @@ def apply_target_torch(s, ok, tgt: Optional[dict]):
         s = torch.ceil(s)
     elif cast == 3:
         s = torch.floor(s)
-    ok = ok & torch.isfinite(s)
     if f & TGT_DEFAULT:
         s = torch.where(ok, s, torch.full_like(s, tgt["dflt"]))
         ok = torch.ones_like(ok)
-    return s, ok
+    return s.to(out_dtype), ok
 
 
 def _addr(t) -> Optional[int]:
@@ -818,7 +821,7 @@ def _perfect_pack(trees: List[BinaryTree], weights: List[float], P: int, D: int,
 
     The feature byte offset is ``column * stride * 4`` with ``column = fmap[feature]`` (the
     kernel's staged-column order) and ``stride`` its feature-plane stride in floats (``TB`` for
-    the narrow kernel, ``rows + 1`` for the wide one). ``leaf_bits="vote8"`` stores the packed
+    the narrow kernel, ``rows`` for the wide one). ``leaf_bits="vote8"`` stores the packed
     vote increment ``1 << 8*class`` as the leaf's bit pattern (class-index leaves)."""
     NI, NL = (1 << D) - 1, 1 << D
     ndr = (NI + 31) // 32
@@ -1091,7 +1094,7 @@ class TreePlan(DevicePlan):
                 if not wide_ok:
                     raise NotLowerable("the wide tree kernel needs P = 1 and <= 256 staged columns")
                 self.rows_wide, self.n_stage = rows, len(stage)
-                stride = rows + 1  # one pad float per feature plane (conflict-free staging)
+                stride = rows  # [F][rows] planes: traversal reads hit bank row mod 32 (csrc WideGeom)
                 fmap = {f: j for j, f in enumerate(stage)}
                 if stage != list(range(F)):
                     self.feat_map = self._t(np.array(stage, dtype=np.int32))
@@ -1324,6 +1327,26 @@ class TreePlan(DevicePlan):
 # --------------------------------------------------------------------------- dispatch
 
 
+def _segmented_plan(compiled, device, fused_error: Exception, opts: dict) -> DevicePlan:
+    """A MiningModel the fused ensemble kernels refuse: per-segment plans + device predicates
+    (runtime/segmented.py), behind a prepare-only derive pass when the inputs need MiningField
+    treatment (segment plans and predicates read prepared columns, as the oracle's do)."""
+    from .segmented import SegmentedPlan, segmentable
+
+    why = segmentable(compiled.evaluator, compiled)
+    if why:
+        raise NotLowerable(f"{fused_error}; segmentation: {why}") from fused_error
+    if not getattr(compiled, "prepared_inputs", False):
+        prep, any_prep = build_field_prep(compiled, compiled.active_fields) if compiled.active_fields \
+            else (None, False)
+        if any_prep:
+            from .derive import DerivedPlan, build_program_layout
+
+            layout = build_program_layout(compiled, {}, list(compiled.active_fields))
+            return DerivedPlan(compiled, device, layout, **opts)
+    return SegmentedPlan(compiled, device, **opts)
+
+
 def compile_plan(compiled, device, **opts) -> DevicePlan:
     """Pick and build the device plan for a compiled model; raises :class:`NotLowerable` when the
     model needs the host oracle."""
@@ -1354,7 +1377,12 @@ def compile_plan(compiled, device, **opts) -> DevicePlan:
     if isinstance(ev, ClusteringEvaluator):
         return ClusterPlan(compiled, device, **opts)
     if isinstance(ev, (TreeEvaluator, MiningEvaluator)):
-        return TreePlan(compiled, device, precision="fp8" if policy == "fp8" else "fp32", **opts)
+        try:
+            return TreePlan(compiled, device, precision="fp8" if policy == "fp8" else "fp32", **opts)
+        except NotLowerable as e:
+            if not isinstance(ev, MiningEvaluator):
+                raise
+            return _segmented_plan(compiled, device, e, dict(opts, precision=policy))
     if isinstance(ev, RegressionEvaluator):
         return LinearPlan(compiled, device)
     from ..models.regression import GeneralRegressionEvaluator

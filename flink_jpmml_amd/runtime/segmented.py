@@ -1,0 +1,365 @@
+"""MiningModel segmentations the fused tree kernel cannot express, on the device.
+
+The fused ensemble kernels (:class:`~flink_jpmml_amd.runtime.plans.TreePlan`) cover ``sum`` /
+``average`` / ``weightedAverage`` / majority votes over ``True`` segments of binary trees and the
+model chains of XGBoost / LightGBM. Everything else a JPMML user can hand the reference
+(`S/api/PmmlModel.scala:159-160` evaluates any segmentation JPMML supports) lowers here:
+
+* ``multipleModelMethod`` ``selectFirst``, ``max``, ``min``, ``median`` and every supported
+  method under **non-True segment predicates** (the segment participates only where its
+  predicate is TRUE; three-valued logic, UNKNOWN does not select);
+* segments that are not binary trees: each segment is lowered by :func:`compile_plan` on its own
+  (trees, linear models, neural networks, SVMs, nested ensembles — recursively).
+
+Execution: every segment plan scores the (already prepared) input matrix on the caller's stream,
+the segment predicates are evaluated with fp64 tensor ops on the same matrix (exact parity with
+the oracle's float64 comparisons of the fp32 inputs), and the aggregation — the oracle's
+``MiningEvaluator._select/_regress/_classify`` (`models/mining.py`) — runs as tensor ops. No host
+round trip; the per-segment launches make this a slower path than the fused kernels, which is
+why it is only taken when they refuse the model.
+
+Inputs must be prepared (MiningField treatment applied once, as the oracle does at the top
+level): :func:`compile_plan` puts a prepare-only derive pass in front when the model needs one.
+"""
+
+from __future__ import annotations
+
+import contextlib
+from typing import List, Optional
+
+import numpy as np
+
+from ..models.mining import MiningEvaluator
+from ..pmml import ir
+from .plans import DevicePlan, NotLowerable, _label_table, apply_target_torch, target_post
+
+REGRESSION_METHODS = ("sum", "average", "weightedAverage", "max", "min", "median", "selectFirst")
+CLASSIFICATION_METHODS = ("majorityVote", "weightedMajorityVote", "selectFirst")
+
+
+class SubView:
+    """One segment's model seen through its parent's (prepared) input columns."""
+
+    fields_resolved = True
+    prepared_inputs = True
+
+    def __init__(self, parent, evaluator):
+        self._p = parent
+        self.evaluator = evaluator
+        self.model = evaluator.model
+        self.mining_fields = {}
+        self.target_fields = list(parent.target_fields)
+
+    def __getattr__(self, name):
+        return getattr(self._p, name)
+
+
+def segmentable(ev, compiled) -> Optional[str]:
+    """None when :class:`SegmentedPlan` can lower ``ev``; else the reason."""
+    if not isinstance(ev, MiningEvaluator):
+        return "not a MiningModel"
+    method = ev.method
+    if ev.kind == "regression" and method not in REGRESSION_METHODS:
+        return f"regression multipleModelMethod {method!r}"
+    if ev.kind == "classification" and method not in CLASSIFICATION_METHODS:
+        return f"classification multipleModelMethod {method!r}"
+    if ev.kind not in ("regression", "classification"):
+        return f"{ev.kind} segmentation"
+    if ev.mm.local_transformations:
+        return "MiningModel LocalTransformations"
+    for seg in ev.segments:
+        if seg.model.local_transformations:
+            return "segment LocalTransformations"
+        why = _predicate_fields_ok(seg.predicate, compiled)
+        if why:
+            return why
+    return None
+
+
+def _predicate_fields_ok(p, compiled) -> Optional[str]:
+    if isinstance(p, (ir.TruePredicate, ir.FalsePredicate)):
+        return None
+    if isinstance(p, (ir.SimplePredicate, ir.SimpleSetPredicate)):
+        fi = getattr(compiled, "field_index", None) or {f: i for i, f in enumerate(compiled.active_fields)}
+        return None if p.field in fi else f"segment predicate on non-input field {p.field!r}"
+    if isinstance(p, ir.CompoundPredicate):
+        if p.boolean_operator not in ("and", "or", "xor", "surrogate"):
+            return f"CompoundPredicate {p.boolean_operator!r}"
+        for q in p.predicates:
+            why = _predicate_fields_ok(q, compiled)
+            if why:
+                return why
+        return None
+    return f"segment predicate {type(p).__name__}"
+
+
+def compile_predicate(p, compiled):
+    """A segment predicate as a picklable program with columns and categorical codes resolved:
+    ``("T",)`` / ``("F",)`` / ``("S", col, op, value)`` / ``("M", col, isMissing)`` /
+    ``("I", col, isIn, values)`` / ``("C", op, [children])``."""
+    fi = getattr(compiled, "field_index", None) or {f: i for i, f in enumerate(compiled.active_fields)}
+    schema = compiled.schema
+    if isinstance(p, ir.TruePredicate):
+        return ("T",)
+    if isinstance(p, ir.FalsePredicate):
+        return ("F",)
+    if isinstance(p, ir.SimplePredicate):
+        if p.operator in ("isMissing", "isNotMissing"):
+            return ("M", fi[p.field], p.operator == "isMissing")
+        if p.operator not in _OPS:
+            raise NotLowerable(f"SimplePredicate operator {p.operator!r}")
+        return ("S", fi[p.field], p.operator, float(schema.lookup(p.field, p.value)))
+    if isinstance(p, ir.SimpleSetPredicate):
+        return ("I", fi[p.field], p.boolean_operator == "isIn",
+                [float(schema.lookup(p.field, v)) for v in p.values])
+    return ("C", p.boolean_operator, [compile_predicate(q, compiled) for q in p.predicates])
+
+
+_OPS = ("equal", "notEqual", "lessThan", "lessOrEqual", "greaterThan", "greaterOrEqual")
+
+
+def eval_predicate_device(prog, X):
+    """``(true, unknown)`` boolean columns of a compiled predicate over the device matrix ``X``:
+    fp64 comparisons of the fp32 inputs, the oracle's three-valued logic
+    (`pmml/fields.py::eval_predicate`)."""
+    import torch
+
+    n = X.shape[0]
+    ones = torch.ones(n, dtype=torch.bool, device=X.device)
+    zeros = torch.zeros(n, dtype=torch.bool, device=X.device)
+    tag = prog[0]
+    if tag == "T":
+        return ones, zeros
+    if tag == "F":
+        return zeros, zeros
+    if tag == "M":
+        miss = torch.isnan(X[:, prog[1]])
+        return (miss if prog[2] else ~miss), zeros
+    if tag == "S":
+        x = X[:, prog[1]].double()
+        miss = torch.isnan(x)
+        v = prog[3]
+        t = {"equal": x == v, "notEqual": x != v, "lessThan": x < v, "lessOrEqual": x <= v,
+             "greaterThan": x > v, "greaterOrEqual": x >= v}[prog[2]]
+        return t & ~miss, miss
+    if tag == "I":
+        x = X[:, prog[1]].double()
+        miss = torch.isnan(x)
+        inside = torch.isin(x, torch.tensor(prog[3], dtype=torch.float64, device=X.device))
+        return (inside if prog[2] else ~inside) & ~miss, miss
+    op = prog[1]
+    parts = [eval_predicate_device(q, X) for q in prog[2]]
+    if op == "surrogate":
+        t, u = zeros.clone(), ones.clone()
+        for pt, pu in parts:
+            take = u & ~pu
+            t = torch.where(take, pt, t)
+            u = u & pu
+        return t, u
+    if op == "and":
+        anyfalse, anyunk = zeros.clone(), zeros.clone()
+        for pt, pu in parts:
+            anyfalse |= ~pt & ~pu
+            anyunk |= pu
+        return ~anyfalse & ~anyunk, anyunk & ~anyfalse
+    if op == "or":
+        anytrue, anyunk = zeros.clone(), zeros.clone()
+        for pt, pu in parts:
+            anytrue |= pt
+            anyunk |= pu
+        return anytrue, anyunk & ~anytrue
+    acc, unk = zeros.clone(), zeros.clone()  # xor
+    for pt, pu in parts:
+        acc ^= pt
+        unk |= pu
+    return acc & ~unk, unk
+
+
+def _index_outputs(plan) -> None:
+    """Make a classification segment plan emit class *indices* (its epilogue's label table off)."""
+    if getattr(plan, "table", None) is not None:
+        plan.table = None
+        plan.__dict__.pop("_args", None)
+    inner = getattr(plan, "inner", None)
+    if inner is not None:
+        _index_outputs(inner)
+
+
+class SegmentedPlan(DevicePlan):
+    """Per-segment device plans + device predicates + tensor-op aggregation (module docstring)."""
+
+    kind = "segmented"
+    supports_direct = False
+    _STATE = DevicePlan._STATE + ("method", "kind_", "skip", "weights", "progs", "remap_lists", "table", "tgt",
+                                  "categories", "n_subs")
+
+    def __init__(self, compiled, device, **opts):
+        from .plans import compile_plan
+
+        super().__init__(compiled, device)
+        ev = compiled.evaluator
+        why = segmentable(ev, compiled)
+        if why:
+            raise NotLowerable(why)
+        if self.prep is not None:
+            raise NotLowerable("segmented plans read prepared inputs (compile_plan adds the prepare pass)")
+        self.method = ev.method
+        self.kind_ = ev.kind
+        self.skip = ev.mm.missing_prediction_treatment == "skipSegment"
+        self.weights = [float(s.weight) for s in ev.segments]
+        self.progs = [compile_predicate(s.predicate, compiled) for s in ev.segments]
+        self.subs: List[DevicePlan] = []
+        for seg, sub in zip(ev.segments, ev.sub):
+            try:
+                plan = compile_plan(SubView(compiled, sub), device, **dict(opts))
+            except NotLowerable as e:
+                raise NotLowerable(f"segment {seg.id!r}: {e}") from e
+            if self.kind_ == "classification":
+                if sub.kind != "classification":
+                    raise NotLowerable("classification segmentation over non-classification segments")
+                _index_outputs(plan)
+            self.subs.append(plan)
+        self.n_subs = len(self.subs)
+        self.table, self.tgt, self.categories, self.remap_lists = None, None, None, None
+        if self.kind_ == "classification":
+            cats = list(ev.sub[0].categories) if self.method == "selectFirst" else list(ev.categories)
+            self.remap_lists = [[cats.index(c) if c in cats else -1 for c in sub.categories] + [-1]
+                                for sub in ev.sub]
+            self.categories = cats
+            self.table = self._t(_label_table(cats))
+        elif ev.target is not None:
+            self.tgt = target_post(ev.target, force=True)
+        self._post_build()
+
+    def _post_build(self) -> None:
+        import torch
+
+        self.remaps = [torch.tensor(r, dtype=torch.int64, device=self.device) for r in (self.remap_lists or [])]
+
+    # replication: the container's scalars + every segment plan's state under "sub<i>/"
+    def export_state(self):
+        meta, tensors = super().export_state()
+        meta["sub_metas"] = []
+        for i, plan in enumerate(self.subs):
+            m, t = plan.export_state()
+            meta["sub_metas"].append(m)
+            for k, v in t.items():
+                tensors[f"sub{i}/{k}"] = v
+                meta["__tensors__"][f"sub{i}/{k}"] = (tuple(v.shape), str(v.dtype).replace("torch.", ""))
+        return meta, tensors
+
+    def _post_state(self) -> None:
+        subs = []
+        for i, m in enumerate(self.sub_metas):
+            pre = f"sub{i}/"
+            t = {k[len(pre):]: v for k, v in self.__dict__.items() if k.startswith(pre)}
+            subs.append(DevicePlan.from_state(m, t, self.device))
+        for k in [k for k in self.__dict__ if k.startswith("sub") and "/" in k]:
+            del self.__dict__[k]
+        self.subs = subs
+        self._post_build()
+
+    def launch(self, X, score, valid, stream=None, probs=None, score2=None, valid2=None, **kw) -> None:
+        import torch
+
+        n = X.shape[0]
+        if self.device.type == "cuda":
+            st = stream if stream is not None else torch.cuda.current_stream(self.device)
+            ctx = torch.cuda.stream(st)
+        else:  # lowering dry run (CPU tests with stand-in segment plans)
+            st, ctx = None, contextlib.nullcontext()
+        with ctx:
+            S = torch.empty((self.n_subs, n), dtype=torch.float32, device=self.device)
+            V = torch.empty((self.n_subs, n), dtype=torch.uint8, device=self.device)
+            for i, plan in enumerate(self.subs):
+                plan.launch(X, S[i], V[i], stream=st)
+            T = torch.stack([eval_predicate_device(p, X)[0] for p in self.progs])  # [K, n] TRUE masks
+            ok = V.bool() & ~torch.isnan(S)
+            if self.method == "selectFirst":
+                s, v = self._select(S, ok, T)
+            elif self.kind_ == "classification":
+                s, v = self._vote(S, ok, T)
+            else:
+                s, v = self._regress(S.double(), ok, T)
+            s = torch.where(v, s, torch.full_like(s, float("nan")))
+            for so, vo in ((score, valid), (score2, valid2)):
+                if so is not None and not isinstance(so, int):
+                    so.copy_(s.to(so.dtype))
+                    vo.copy_(v.to(torch.uint8))
+
+    def _select(self, S, ok, T):
+        import torch
+
+        K, n = S.shape
+        idx = torch.arange(K, device=S.device)[:, None].expand(K, n)
+        first = torch.where(T, idx, torch.full_like(idx, K)).min(dim=0).values  # K: no segment
+        hit = first < K
+        f = first.clamp(max=K - 1)[None, :]
+        s = S.gather(0, f)[0]
+        v = ok.gather(0, f)[0] & hit
+        if self.kind_ == "classification":
+            seg_idx = torch.stack([r[torch.where(torch.isnan(S[i]), -1, S[i]).long().clamp(min=-1)]
+                                   for i, r in enumerate(self.remaps)])
+            lab = seg_idx.gather(0, f)[0]
+            v = v & (lab >= 0)
+            s = self.table[lab.clamp(min=0)].double()
+            v = v & ~torch.isnan(s)
+            return s, v
+        s = s.double()
+        s, v = apply_target_torch(s, v & torch.isfinite(s), self.tgt)
+        return s, v
+
+    def _regress(self, S, ok, T):
+        import torch
+
+        use = T & ok
+        miss = T & ~ok
+        m = self.method
+        Vz = torch.where(use, S, torch.zeros_like(S))
+        cnt = use.sum(dim=0)
+        if m == "sum":
+            out = Vz.sum(dim=0)
+        elif m == "average":
+            out = Vz.sum(dim=0) / cnt
+        elif m == "weightedAverage":
+            w = torch.tensor(self.weights, dtype=torch.float64, device=S.device)[:, None]
+            out = (Vz * w).sum(dim=0) / torch.where(use, w.expand_as(S), torch.zeros_like(S)).sum(dim=0)
+        elif m in ("max", "min"):
+            fill = float("-inf") if m == "max" else float("inf")
+            Vf = torch.where(use, S, torch.full_like(S, fill))
+            out = Vf.max(dim=0).values if m == "max" else Vf.min(dim=0).values
+        else:  # median: mean of the two middle values of the participating segments (numpy rule)
+            srt = torch.where(use, S, torch.full_like(S, float("inf"))).sort(dim=0).values
+            c = cnt.clamp(min=1)
+            lo = srt.gather(0, ((c - 1) // 2)[None, :])[0]
+            hi = srt.gather(0, (c // 2)[None, :])[0]
+            out = (lo + hi) / 2
+        v = cnt > 0
+        if not self.skip:
+            v = v & ~miss.any(dim=0)
+        v = v & torch.isfinite(out)
+        out, v = apply_target_torch(out, v, self.tgt)
+        return out, v
+
+    def _vote(self, S, ok, T):
+        import torch
+
+        K, n = S.shape
+        C = len(self.categories)
+        use = T & ok
+        anymiss = (T & ~ok).any(dim=0)
+        acc = torch.zeros((n, C), dtype=torch.float64, device=S.device)
+        for i in range(K):
+            lab = self.remaps[i][torch.where(use[i], S[i], torch.zeros_like(S[i])).long()]
+            w = self.weights[i] if self.method == "weightedMajorityVote" else 1.0
+            u = use[i] & (lab >= 0)
+            acc.scatter_add_(1, lab.clamp(min=0)[:, None], torch.where(u, w, 0.0).double()[:, None])
+        v = use.any(dim=0)
+        if not self.skip:
+            v = v & ~anymiss
+        lab = acc.argmax(dim=1)  # ties -> lowest index, as np.argmax
+        s = self.table[lab].double()
+        return s, v & ~torch.isnan(s)
+
+
+__all__ = ["SegmentedPlan", "SubView", "segmentable"]

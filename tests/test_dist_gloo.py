@@ -215,6 +215,8 @@ def _kill_entry(rank, world, port, kmeans_path, q):
         q.put((rank, ("finished", done)))
     except RankFailure as e:
         q.put((rank, ("rank-failure", done, str(e)[:200])))
+    q.close()
+    q.join_thread()  # flush the queue's feeder thread: os._exit would drop the pending message
     os._exit(0)
 
 

@@ -1,6 +1,6 @@
 """CPU emulation of the wide PERFECT tree kernel (csrc/tree_common.h ``tree_perfect_wide_kernel``)
 over the tensors a real :class:`TreePlan` lowers to (``lowering_dry_run``: no GPU, no HIP library):
-feature planes of stride ``rows + 1``, staged-column compaction (``feat_map``), the NaN -> +inf
+feature planes of stride ``rows``, staged-column compaction (``feat_map``), the NaN -> +inf
 second plane, and the four accumulation modes (SUM, SLOT for K-class GBDT chains, CLASS for
 weighted votes, VOTE8 for packed u8 vote counters). Each must reproduce the float64 oracle.
 
@@ -29,7 +29,7 @@ def emulate_wide(plan, X, use_nan_blob):
     default-right bits (traverse_chunk_g)."""
     D, n_t, rec = plan.depth, plan.n_trees, plan.rec_words
     NI, NL = (1 << D) - 1, 1 << D
-    PS = plan.rows_wide + 1
+    PS = plan.rows_wide
     G = 1024 // plan.rows_wide
     stage = plan.feat_map.numpy() if plan.feat_map is not None else np.arange(plan.n_features)
     Xs = X[:, stage].astype(np.float32)
