@@ -65,6 +65,7 @@ def parse_args(argv=None):
     p.add_argument("--micro-batch", type=int, default=1 << 20,
                    help="rows per H2D slice + kernel launch (1M measured best: profiles/r2_h2d_probe.md)")
     p.add_argument("--pipeline-depth", type=int, default=3, help="input ring slots (H2D/compute overlap)")
+    p.add_argument("--h2d-streams", type=int, default=1, help="copy streams per micro-batch (SDMA engines)")
     p.add_argument("--max-inflight", type=int, default=3, help="scored steps in flight before the sink waits")
     p.add_argument("--precision", choices=["fp32", "bf16", "fp8"], default=None,
                    help="default fp32 (trees), bf16 (mlp, BASELINE config 4); fp8 = e4m3 leaves (config 5)")
@@ -182,7 +183,8 @@ def main(argv=None) -> int:
     if args.gpus != N and ctx.rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={N}; using {N}", file=sys.stderr)
     cfg = ScoringConfig(device=device, micro_batch=args.micro_batch, pipeline_depth=args.pipeline_depth,
-                        max_inflight=args.max_inflight, precision=args.precision, fallback="error")
+                        max_inflight=args.max_inflight, precision=args.precision, fallback="error",
+                        h2d_streams=args.h2d_streams)
 
     # ---- the model: rank 0 writes the synthetic PMML; every rank loads it through the collective
     #      parse-once / RCCL-broadcast path the DSL operators use
@@ -250,7 +252,8 @@ def main(argv=None) -> int:
         elapsed = time.perf_counter() - timing["t0"]
         assert sink.rows_seen == (args.warmup + args.steps) * args.rows
     else:
-        scorer = StreamingScorer(plan, micro_batch=args.micro_batch, depth=args.pipeline_depth, max_rows=args.rows)
+        scorer = StreamingScorer(plan, micro_batch=args.micro_batch, depth=args.pipeline_depth, max_rows=args.rows,
+                                 h2d_streams=args.h2d_streams)
         score_h = torch.empty(args.rows, dtype=torch.float32).pin_memory()
         valid_h = torch.empty(args.rows, dtype=torch.uint8).pin_memory()
         for _ in range(args.warmup):

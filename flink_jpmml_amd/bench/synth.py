@@ -305,8 +305,12 @@ def mlp_pmml(n_features: int = 64, hidden: Tuple[int, ...] = (256, 256), n_out: 
 
 
 def svm_pmml(n_features: int = 16, n_sv: int = 256, seed: int = 0, kernel: str = "radialBasis",
-             classification: bool = True, gamma: float = 0.05) -> str:
+             classification: bool = True, gamma: float = 0.05, n_classes: int = 2) -> str:
+    """libsvm / sklearn-style SVM PMML; ``n_classes > 2`` exports one-against-one machines (one per
+    class pair, each over its own subset of the shared support vectors)."""
     rng = np.random.default_rng(seed)
+    if classification and n_classes > 2:
+        return _svm_ovo_pmml(rng, n_features, n_sv, kernel, gamma, n_classes)
     out = io.StringIO()
     _header(out, f"synthetic SVM {kernel} {n_sv} support vectors")
     cats = ["0", "1"] if classification else None
@@ -710,4 +714,40 @@ def segmented_pmml(method: str = "selectFirst", classification: bool = False, n_
             out.write('    </TreeModel>\n')
         out.write('   </Segment>\n')
     out.write('  </Segmentation>\n </MiningModel>\n</PMML>\n')
+    return out.getvalue()
+
+
+def _svm_ovo_pmml(rng, n_features: int, n_sv: int, kernel: str, gamma: float, n_classes: int) -> str:
+    out = io.StringIO()
+    _header(out, f"synthetic one-against-one SVM {kernel} {n_classes} classes")
+    cats = [str(c) for c in range(n_classes)]
+    _data_dictionary(out, n_features, "y", "integer", cats)
+    out.write(' <SupportVectorMachineModel functionName="classification" svmRepresentation="SupportVectors" '
+              'classificationMethod="OneAgainstOne">\n')
+    _mining_schema(out, n_features, "y", "  ")
+    ktag = {"radialBasis": f'<RadialBasisKernelType gamma="{gamma}"/>', "linear": '<LinearKernelType/>',
+            "polynomial": f'<PolynomialKernelType gamma="{gamma}" coef0="1" degree="3"/>',
+            "sigmoid": f'<SigmoidKernelType gamma="{gamma}" coef0="0.5"/>'}[kernel]
+    out.write(f'  {ktag}\n  <VectorDictionary numberOfVectors="{n_sv}">\n   <VectorFields numberOfFields="{n_features}">')
+    out.write("".join(f'<FieldRef field="f{j}"/>' for j in range(n_features)))
+    out.write('</VectorFields>\n')
+    S = rng.standard_normal((n_sv, n_features))
+    for i in range(n_sv):
+        out.write(f'   <VectorInstance id="sv{i}"><Array n="{n_features}" type="real">'
+                  + " ".join(f"{v:.6g}" for v in S[i]) + '</Array></VectorInstance>\n')
+    out.write('  </VectorDictionary>\n')
+    owner = rng.integers(n_classes, size=n_sv)  # each support vector belongs to one class
+    for a in range(n_classes):
+        for b in range(a + 1, n_classes):
+            ids = [i for i in range(n_sv) if owner[i] in (a, b)]
+            out.write(f'  <SupportVectorMachine targetCategory="{cats[a]}" alternateTargetCategory="{cats[b]}">\n'
+                      f'   <SupportVectors numberOfSupportVectors="{len(ids)}">')
+            out.write("".join(f'<SupportVector vectorId="sv{i}"/>' for i in ids))
+            out.write('</SupportVectors>\n')
+            coef = rng.standard_normal(len(ids)) * 0.5
+            out.write(f'   <Coefficients numberOfCoefficients="{len(ids)}" '
+                      f'absoluteValue="{rng.standard_normal() * 0.1:.6g}">')
+            out.write("".join(f'<Coefficient value="{c:.6g}"/>' for c in coef))
+            out.write('</Coefficients>\n  </SupportVectorMachine>\n')
+    out.write(' </SupportVectorMachineModel>\n</PMML>\n')
     return out.getvalue()

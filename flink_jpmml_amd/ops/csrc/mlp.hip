@@ -282,7 +282,7 @@ __global__ __launch_bounds__(64 * Cfg<BF16>::WAVES, 1) void mlp_kernel(MlpArgs a
   int* s_ix = reinterpret_cast<int*>(s_ms + KMAX);
   float* s_b = reinterpret_cast<float*>(s_ix + KMAX);              // [MAXL * MT * 32]
   int2* s_pan = reinterpret_cast<int2*>(s_b + MAXL * MT * 32);      // [MAXL * MT] panel schedule
-  int* s_rowbad = reinterpret_cast<int*>(s_pan + MAXL * MT);          // [WAVES * 32] row invalid flags
+  int* s_rowbad = reinterpret_cast<int*>(s_pan + MAXL * MT);          // [WAVES * 32][2] NaN-operand counts
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -320,6 +320,7 @@ __global__ __launch_bounds__(64 * Cfg<BF16>::WAVES, 1) void mlp_kernel(MlpArgs a
     // offset goes through an opaque register each tile, so the per-k LDS addresses stay
     // base + immediate (hoisting them out of the tile loop would cost hundreds of VGPRs).
     BT pb[KS], nb[KS];
+    int nbad = 0;
     {
       uint32_t kb = BF16 ? 8u * h : (uint32_t)h;  // first k of this lane half
       __asm__ volatile("" : "+v"(kb));
@@ -338,6 +339,7 @@ __global__ __launch_bounds__(64 * Cfg<BF16>::WAVES, 1) void mlp_kernel(MlpArgs a
               const int o = 16 * s + j;
               const float x = a.contiguous ? xr[o] : xrow[tix[o]];
               const float y = (x != x) ? tms[o] : fmaf(x, tsc[o], tsh[o]);
+              nbad += (y != y) ? 1 : 0;
               v[j] = (__bf16)y;
             }
             pb[s] = v;
@@ -348,6 +350,7 @@ __global__ __launch_bounds__(64 * Cfg<BF16>::WAVES, 1) void mlp_kernel(MlpArgs a
             const int o = 2 * s;
             const float x = a.contiguous ? xr[o] : xrow[tix[o]];
             const float y = (x != x) ? tms[o] : fmaf(x, tsc[o], tsh[o]);
+            nbad += (y != y) ? 1 : 0;
             pb[s] = y;
           }
           if ((s & 15) == 15) __builtin_amdgcn_sched_barrier(0);
@@ -355,16 +358,11 @@ __global__ __launch_bounds__(64 * Cfg<BF16>::WAVES, 1) void mlp_kernel(MlpArgs a
       }
     }
     // Row validity: a missing input without a replacement value invalidates the row (PMML NN
-    // rule). Kept in LDS (one int per row of the tile), not in a register flag: a boolean lives in
-    // an SGPR lane mask across the whole layer loop, and that mask came back wrong on the GPU
-    // (twice, in differently scheduled variants). Lane halves split the inputs; the record loads
-    // hit L1. Same-wave LDS operations complete in order: the h == 0 clear lands before any set.
-    volatile int* rbad = s_rowbad + wave * 32 + col;  // both lane halves write it: no forwarding
-    if (h == 0) *rbad = 0;
-    for (int k = h; k < a.n_in; k += 2) {
-      const float x = xrow[s_ix[k]];
-      if ((x != x) && (s_ms[k] != s_ms[k])) *rbad = 1;
-    }
+    // rule). Each lane half counts its NaN operands (an integer in a VGPR, not a boolean: a flag
+    // kept as an SGPR lane mask across the whole layer loop came back wrong on the GPU) and parks
+    // the count in LDS for the epilogue.
+    int* rbad = s_rowbad + 2 * (wave * 32 + col);  // read back after the layer loop (barriers between)
+    rbad[h] = nbad;
 
     f32x16 out = {};
     for (int L = 0; L < a.n_layers; ++L) {
@@ -384,7 +382,7 @@ __global__ __launch_bounds__(64 * Cfg<BF16>::WAVES, 1) void mlp_kernel(MlpArgs a
     // ---- output layer: units 0..n_out-1 live in tile 0; lanes l and l^32 hold the two halves
     if (a.final_norm == 0 && a.n_out == 1) {
       if (h == 0 && in_range) {
-        const bool bad = *rbad != 0;
+        const bool bad = (rbad[0] | rbad[1]) != 0;
         apply_epilogue(a.epi, [&](int) { return out[0]; }, !bad, row, a.n_rows, a.score, a.valid, a.probs);
       }
       continue;
@@ -420,7 +418,7 @@ __global__ __launch_bounds__(64 * Cfg<BF16>::WAVES, 1) void mlp_kernel(MlpArgs a
     const int ou = __shfl_xor(best_u, 32);
     if (ob > best || (ob == best && ou < best_u)) { best = ob; best_u = ou; }
     if (h == 0 && in_range) {
-      bool ok = *rbad == 0 && best == best && best_u < a.n_out;
+      bool ok = (rbad[0] | rbad[1]) == 0 && best == best && best_u < a.n_out;
       float sc = ok ? (a.epi.has_table ? a.epi.table[best_u] : (float)best_u) : __builtin_nanf("");
       ok = ok && (sc == sc);
       a.score[row] = ok ? sc : __builtin_nanf("");
@@ -436,7 +434,7 @@ __global__ __launch_bounds__(64 * Cfg<BF16>::WAVES, 1) void mlp_kernel(MlpArgs a
 template <bool BF16>
 size_t lds_bytes() {
   return (size_t)NSLOT * Cfg<BF16>::PANEL + 4 * KMAX * 4 + (size_t)MAXL * MT * 32 * 4 + (size_t)MAXL * MT * 8 +
-         (size_t)Cfg<BF16>::WAVES * 32 * 4;
+         (size_t)Cfg<BF16>::WAVES * 32 * 2 * 4;
 }
 
 int n_cus() {

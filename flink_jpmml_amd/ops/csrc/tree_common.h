@@ -67,6 +67,7 @@ struct TreeArgs {
 };
 constexpr int VAR_NAN_FAST = 4;    // wide kernel: take the fast path even on tiles with missing values
 constexpr int VAR_NAN_PLANES = 8;  // ... via blob_nan + a second feature plane (NaN -> +inf)
+constexpr int VAR_ILP16 = 16;      // wide kernel, SUM mode: 16-wide tree-walk batches
 
 // per-depth launchers (tree_d<D>.hip)
 #define PMML_TREE_DECL(D) int launch_perfect_d##D(hipStream_t st, const TreeArgs& a, dim3 grid, size_t lds);
@@ -554,6 +555,10 @@ __device__ __forceinline__ void traverse_fast_g(const TreeArgs& a, const uint32_
   const int mt = (nt - g + G - 1) / G;
   int m = 0;
   for (; m + ILP <= mt; m += ILP) fast_batch_acc<DEPTH, ILP, G, LEAF8, MODE>(a, lds0, g, m, t0, feat_lane, acc);
+  if (ILP > 8 && m + 8 <= mt) {
+    fast_batch_acc<DEPTH, 8, G, LEAF8, MODE>(a, lds0, g, m, t0, feat_lane, acc);
+    m += 8;
+  }
   if (ILP > 4 && m + 4 <= mt) {
     fast_batch_acc<DEPTH, 4, G, LEAF8, MODE>(a, lds0, g, m, t0, feat_lane, acc);
     m += 4;
@@ -747,7 +752,9 @@ int launch_wide(hipStream_t st, const TreeArgs& a, size_t lds_w) {
   using WG = WideGeom<ROWS>;
   dim3 grid((a.n_rows + ROWS - 1) / ROWS, (a.n_trees + a.trees_per_split - 1) / a.trees_per_split);
   (void)WG::G;
-  auto k = tree_perfect_wide_kernel<D, 8, ROWS, LEAF8, MODE>;
+  // VAR_ILP16: 16 independent tree walks per batch (more LDS round trips in flight per wave)
+  auto k = (MODE == MODE_SUM && (a.variant & VAR_ILP16)) ? tree_perfect_wide_kernel<D, 16, ROWS, LEAF8, MODE>
+                                                          : tree_perfect_wide_kernel<D, 8, ROWS, LEAF8, MODE>;
   int err = prepare_launch(k, lds_w);
   if (!err) hipLaunchKernelGGL(k, grid, dim3(WIDE_T), lds_w, st, a);
   return err;

@@ -135,7 +135,8 @@ class DistributedServing:
         from ..runtime.engine import DevicePipeline, make_scorer
 
         if self.device is not None and self._pipeline is None:
-            self._pipeline = DevicePipeline(self.device, self.config.micro_batch, self.config.pipeline_depth)
+            self._pipeline = DevicePipeline(self.device, self.config.micro_batch, self.config.pipeline_depth,
+                                            self.config.h2d_streams)
         return make_scorer(compiled, self.device, self.config, pipeline=self._pipeline, plan=plan,
                            lower_error=lower_error)
 

@@ -460,7 +460,7 @@ def make_scorer(compiled, device, config=None, pipeline: Optional[DevicePipeline
                                "(set fallback='error' to refuse)", compiled.model_name, device, e)
             return HostScorer(compiled, reason=str(e))
     if pipeline is None:
-        pipeline = DevicePipeline(plan.device, cfg.micro_batch, cfg.pipeline_depth)
+        pipeline = DevicePipeline(plan.device, cfg.micro_batch, cfg.pipeline_depth, cfg.h2d_streams)
     return StreamingScorer(plan, pipeline=pipeline, max_inflight=cfg.max_inflight)
 
 

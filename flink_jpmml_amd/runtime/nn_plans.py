@@ -10,6 +10,7 @@ accumulator registers are consumed as the B operand (see ``csrc/mlp.hip``).
 
 from __future__ import annotations
 
+import contextlib
 from typing import List, Optional, Tuple
 
 import numpy as np
@@ -416,3 +417,114 @@ class SvmPlan(DevicePlan):
         a.epi.score2, a.epi.valid2 = _addr(score2), _addr(valid2)
         a.score, a.valid, a.decision = _addr(score), _addr(valid), ptr(decision)
         check(self.lib.pmml_svm_launch(stream_handle(stream), ctypes.byref(a), self.fmax), "svm kernel")
+
+
+class SvmGemmPlan(DevicePlan):
+    """SupportVectorMachineModel as two library GEMMs on the matrix cores (hipBLASLt, fp32):
+    ``G = X·Sᵀ`` → kernel function (element-wise) → ``D = K·A + b`` (``A`` = dual coefficients of
+    every machine over the shared support-vector set), then one-against-one / one-against-all
+    votes as a tiny ``[machines, classes]`` product. Coalesced, MFMA-backed and without the fused
+    kernel's limits (any number of machines, fields, support vectors); used when those limits bite.
+    Reads prepared inputs (compile_plan puts a prepare-only derive pass in front when needed).
+    Parity: the oracle's `models/svm.py::SvmEvaluator.decision_values/finish`."""
+
+    kind = "svm_gemm"
+    supports_direct = False
+    ROW_CHUNK = 1 << 18  # bounds the [rows, n_sv] kernel matrix
+    _STATE = DevicePlan._STATE + ("in_index", "S", "s_norm", "A", "b", "W_lin", "thr", "vote_t", "vote_a",
+                                  "kernel_kind", "gamma", "coef0", "degree", "max_wins", "classification",
+                                  "table", "coefficients")
+
+    def __init__(self, compiled, device):
+        import torch
+
+        from ..models.svm import SvmEvaluator
+
+        super().__init__(compiled, device)
+        if self.prep is not None:
+            raise NotLowerable("SvmGemmPlan reads prepared inputs (compile_plan adds the prepare pass)")
+        ev: SvmEvaluator = compiled.evaluator
+        sm = ev.sm
+        fi = getattr(compiled, "field_index", None) or {f: i for i, f in enumerate(compiled.active_fields)}
+        for f in ev.fields:
+            if f not in fi:
+                raise NotLowerable(f"SVM vector field {f!r} is not an input column")
+        self.in_index = self._t(np.array([fi[f] for f in ev.fields], np.int64))
+        self.coefficients = 1 if sm.representation == "Coefficients" else 0
+        M = len(sm.machines)
+        self.kernel_kind = "linear" if self.coefficients else sm.kernel.kind
+        if self.kernel_kind not in ("linear", "polynomial", "radialBasis", "sigmoid"):
+            raise NotLowerable(f"SVM kernel {self.kernel_kind!r}")
+        k = sm.kernel
+        self.gamma, self.coef0, self.degree = float(k.gamma), float(k.coef0), float(k.degree)
+        self.W_lin = self._t(ev.linear_coef.astype(np.float32)) if self.coefficients else None
+        self.S = self._t(ev.S.astype(np.float32)) if not self.coefficients else None
+        self.s_norm = self._t((ev.S ** 2).sum(1).astype(np.float32)) if not self.coefficients else None
+        self.A = self._t(ev.A.astype(np.float32)) if not self.coefficients else None
+        self.b = self._t(ev.b.astype(np.float32))
+        self.max_wins = 1 if sm.max_wins else 0
+        self.classification = 1 if ev.kind == "classification" else 0
+        self.table = self.thr = self.vote_t = self.vote_a = None
+        if self.classification:
+            cats = ev.categories
+            C = len(cats)
+            thr = np.zeros(M, np.float32)
+            vt = np.zeros((M, C), np.float32)
+            va = np.zeros((M, C), np.float32)
+            for m, mach in enumerate(sm.machines):
+                thr[m] = mach.threshold if mach.threshold is not None else sm.threshold
+                vt[m, cats.index(mach.target_category)] = 1.0
+                if mach.alternate_target_category is not None:
+                    va[m, cats.index(mach.alternate_target_category)] = 1.0
+            self.thr, self.vote_t, self.vote_a = self._t(thr), self._t(vt), self._t(va)
+            self.table = self._t(_label_table(cats))
+        elif M != 1:
+            raise NotLowerable("regression SVM must have one machine")
+        del torch
+
+    def _decision(self, x):
+        import torch
+
+        if self.coefficients:
+            return torch.addmm(self.b, x, self.W_lin)
+        G = x @ self.S.T
+        kk = self.kernel_kind
+        if kk == "radialBasis":
+            d2 = (x * x).sum(1, keepdim=True) - 2.0 * G + self.s_norm[None, :]
+            K = torch.exp(-self.gamma * d2.clamp_min(0.0))
+        elif kk == "linear":
+            K = G
+        elif kk == "polynomial":
+            K = torch.pow(self.gamma * G + self.coef0, self.degree)
+        else:
+            K = torch.tanh(self.gamma * G + self.coef0)
+        return torch.addmm(self.b, K, self.A)
+
+    def launch(self, X, score, valid, stream=None, probs=None, score2=None, valid2=None, **kw) -> None:
+        import torch
+
+        if self.device.type == "cuda":
+            ctx = torch.cuda.stream(stream if stream is not None else torch.cuda.current_stream(self.device))
+        else:  # lowering dry run: the same tensor program on the host (CPU tests)
+            ctx = contextlib.nullcontext()
+        with ctx:
+            n = X.shape[0]
+            for lo in range(0, n, self.ROW_CHUNK):
+                hi = min(n, lo + self.ROW_CHUNK)
+                x = X[lo:hi].index_select(1, self.in_index)
+                ok = ~torch.isnan(x).any(dim=1)
+                D = self._decision(torch.nan_to_num(x, nan=0.0))
+                if self.classification:
+                    first = D < self.thr[None, :]
+                    if self.max_wins:
+                        first = ~first
+                    votes = first.float() @ self.vote_t + (~first).float() @ self.vote_a
+                    s = self.table[votes.argmax(dim=1)]  # ties -> first category, as np.argmax
+                    ok = ok & ~torch.isnan(s)
+                else:
+                    s = D[:, 0]
+                s = torch.where(ok, s, torch.full_like(s, float("nan")))
+                for so, vo in ((score, valid), (score2, valid2)):
+                    if so is not None and not isinstance(so, int):
+                        so[lo:hi].copy_(s)
+                        vo[lo:hi].copy_(ok.to(torch.uint8))

@@ -85,7 +85,8 @@ class _ScoringMixin:
         if self._pipeline is None:
             from ..runtime.engine import DevicePipeline
 
-            self._pipeline = DevicePipeline(self.device, self.config.micro_batch, self.config.pipeline_depth)
+            self._pipeline = DevicePipeline(self.device, self.config.micro_batch, self.config.pipeline_depth,
+                                            self.config.h2d_streams)
         return self._pipeline
 
     def _now(self) -> float:

@@ -24,6 +24,7 @@ def main():
     p.add_argument("--layout", default="auto")
     p.add_argument("--lds-budget", type=int, default=80 * 1024)
     p.add_argument("--variant", default="auto")
+    p.add_argument("--ilp", type=int, default=8, help="wide tree kernel: independent walks per batch (8|16)")
     p.add_argument("--clusters", type=int, default=256)
     p.add_argument("--nan-mode", default="auto")
     p.add_argument("--max-chunk-trees", type=int, default=0)
@@ -73,7 +74,7 @@ def main():
     opts = {}
     if args.model.startswith(("gbdt", "rf")):
         opts = dict(layout=args.layout, lds_budget=args.lds_budget, variant=args.variant, nan_mode=args.nan_mode,
-                    max_chunk_trees=args.max_chunk_trees)
+                    max_chunk_trees=args.max_chunk_trees, ilp=args.ilp)
     elif args.model == "kmeans-big":
         opts = dict(cluster_variant=args.variant)
     if args.precision != "fp32":

@@ -1,0 +1,52 @@
+"""Iris multinomial logistic regression probabilities and class index on the linear kernel, and
+one-against-one SVMs on the fused kernel (<= 8 machines) and the GEMM path (more machines),
+against the float64 oracle."""
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def test_iris_logistic_probs_and_argmax(gpu):
+    import torch
+
+    from flink_jpmml_amd.bench.synth import iris_logistic_pmml
+    from flink_jpmml_amd.runtime.compiled import CompiledPmml
+    from flink_jpmml_amd.runtime.plans import LinearPlan
+
+    c = CompiledPmml.from_string(iris_logistic_pmml())
+    plan = c.plan(gpu)
+    assert isinstance(plan, LinearPlan)
+    plan.table = None  # emit the class index instead of the (string) label's numeric value
+    plan.__dict__.pop("_args", None)
+    rng = np.random.default_rng(0)
+    X = rng.uniform([4, 2, 1, 0], [8, 4.5, 7, 2.5], (20_000, 4))
+    Xt = torch.from_numpy(X.astype(np.float32)).to(gpu)
+    s = torch.empty(len(X), device=gpu)
+    v = torch.empty(len(X), dtype=torch.uint8, device=gpu)
+    probs = torch.empty((len(X), 3), device=gpu)
+    plan.launch(Xt, s, v, probs=probs)
+    torch.cuda.synchronize()
+    res, _ = c.evaluate_prepared(c.prepare(X.astype(np.float32))[0])
+    assert v.cpu().numpy().astype(bool).all()
+    np.testing.assert_allclose(probs.cpu().numpy(), res.probs, atol=2e-5)
+    lab = s.cpu().numpy()
+    agree = (lab == np.argmax(res.probs, axis=1)).mean()
+    assert agree > 0.9999  # fp32 vs fp64 near-ties only
+
+
+@pytest.mark.parametrize("n_classes,kind", [(3, "SvmPlan"), (5, "SvmGemmPlan")])
+def test_one_against_one_svm_on_gpu(gpu, n_classes, kind):
+    from flink_jpmml_amd.bench.synth import stream_matrix, svm_pmml
+    from flink_jpmml_amd.runtime.compiled import CompiledPmml
+
+    c = CompiledPmml.from_string(svm_pmml(n_features=12, n_sv=160, seed=6, n_classes=n_classes, gamma=0.2))
+    plan = c.plan(gpu)
+    assert type(plan).__name__ == kind
+    X = stream_matrix(30_000, 12, seed=3, missing_rate=0.01)
+    s, v = plan.score(X)
+    s, v = s.cpu().numpy(), v.cpu().numpy()
+    ref, vref = c.score_matrix_oracle(X)
+    assert (v == vref).all()
+    assert (s[v] == ref[v]).mean() > 0.999

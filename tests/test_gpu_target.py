@@ -8,13 +8,14 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def _cmp(gpu, txt, F=None, missing=0.0, n=20_000, tol=1e-4, **kw):
+def _cmp(gpu, txt, F=None, missing=0.0, n=20_000, tol=1e-4, X=None, **kw):
     from flink_jpmml_amd.bench.synth import stream_matrix
     from flink_jpmml_amd.runtime.compiled import CompiledPmml
 
     c = CompiledPmml.from_string(txt)
     plan = c.plan(gpu, **kw)
-    X = stream_matrix(n, F or c.n_features, seed=3, missing_rate=missing)
+    if X is None:
+        X = stream_matrix(n, F or c.n_features, seed=3, missing_rate=missing)
     s, v = plan.score(X)
     s, v = s.cpu().numpy(), v.cpu().numpy()
     ref, vref = c.score_matrix_oracle(X)
@@ -33,7 +34,9 @@ def test_tree_target_clip_rescale_cast(gpu, cast):
     assert "tgt" in plan.epi_args
     # castInteger: only values within fp32 noise of a rounding boundary may differ
     assert agree > (0.999 if cast else 0.99999)
-    assert s.min() >= 1.0 - 1e-5 and s.max() <= 6.0 + 1e-5  # clip [-0.2, 0.25] * 10 + 3, then the cast
+    v = ~np.isnan(s)
+    # clip [-0.2, 0.25] * 10 + 3 (fp64: -0.2 * 10 + 3 = 0.9999999999999996, which floors to 0)
+    assert s[v].min() >= (0.0 if cast == "floor" else 1.0) - 1e-5 and s[v].max() <= 6.0 + 1e-5
 
 
 def test_tree_target_default_value(gpu):
@@ -48,10 +51,13 @@ def test_tree_target_default_value(gpu):
 def test_glm_link_then_rescale(gpu):
     from flink_jpmml_amd.bench.synth import glm_pmml, set_target
 
+    from flink_jpmml_amd.bench.synth import mixed_records
+
     txt = set_target(glm_pmml(model_type="generalizedLinear", link="log", n_features=3, seed=1), max=3.0,
                      factor=0.5, constant=1.0)
-    plan, agree, _, _ = _cmp(gpu, txt, None, missing=0.0, tol=1e-4)
-    assert agree > 0.9999
+    _, X = mixed_records(20_000, 3, seed=2)  # valid vocabulary codes in the categorical column
+    plan, agree, s, _ = _cmp(gpu, txt, X=X, tol=1e-4)
+    assert agree > 0.9999 and np.nanmax(s) <= 2.5 + 1e-6
 
 
 @pytest.mark.parametrize("kind", ["fused", "gemm"])
