@@ -12,13 +12,18 @@
 //  * categorical (string) fields: per-column dictionaries map the token to the PMML vocabulary code
 //    (`pmml/fields.py::FieldSchema`), unknown tokens to -1 (an invalid code: the kernels' FieldPrep
 //    code-range check applies invalidValueTreatment);
-//  * a column map selects / reorders input columns into the model's active-field order.
+//  * a column map selects / reorders input columns into the model's active-field order;
+//  * the parse passes run on a persistent worker pool (threads are created once, on first use,
+//    and parked on a condition variable between calls — no thread creation per batch).
 #include <algorithm>
 #include <atomic>
 #include <charconv>
 #include <cmath>
+#include <condition_variable>
 #include <cstdint>
 #include <cstring>
+#include <functional>
+#include <mutex>
 #include <string>
 #include <string_view>
 #include <thread>
@@ -105,6 +110,97 @@ size_t parse_range(const Spec& sp, const char* b, const char* e, float* out, int
   return r;
 }
 
+// Persistent fork-join pool: run(T, fn) executes fn(0..T-1) across the workers and the caller and
+// returns when all are done. One job at a time (callers serialise on job_mu_).
+class Pool {
+ public:
+  static Pool& instance() {
+    static Pool p;
+    return p;
+  }
+
+  void run(int T, const std::function<void(int)>& fn) {
+    if (T <= 1) {
+      if (T == 1) fn(0);
+      return;
+    }
+    std::lock_guard<std::mutex> job_lock(job_mu_);
+    grow(T - 1);
+    uint64_t g;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      fn_ = &fn;
+      n_tasks_ = T;
+      next_ = 0;
+      remaining_ = T;
+      g = ++gen_;
+    }
+    cv_.notify_all();
+    work(g);  // the caller takes tasks too
+    std::unique_lock<std::mutex> lk(mu_);
+    done_cv_.wait(lk, [&] { return remaining_ == 0; });
+    fn_ = nullptr;
+  }
+
+  ~Pool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+      ++gen_;
+    }
+    cv_.notify_all();
+    for (auto& t : workers_) t.join();
+  }
+
+ private:
+  void grow(int n) {
+    while ((int)workers_.size() < std::min(n, 63)) workers_.emplace_back([this] { loop(); });
+  }
+
+  // Claim tasks of job generation g under the lock: a worker that wakes late can never run a
+  // finished job's function (the job cannot complete while one of its tasks is claimed).
+  void work(uint64_t g) {
+    for (;;) {
+      const std::function<void(int)>* fn;
+      int t;
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (gen_ != g || fn_ == nullptr || next_ >= n_tasks_) return;
+        t = next_++;
+        fn = fn_;
+      }
+      (*fn)(t);
+      std::lock_guard<std::mutex> lk(mu_);
+      if (--remaining_ == 0) done_cv_.notify_all();
+    }
+  }
+
+  void loop() {
+    uint64_t seen;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      seen = gen_;
+    }
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return gen_ != seen; });
+        seen = gen_;
+        if (stop_) return;
+      }
+      work(seen);
+    }
+  }
+
+  std::mutex job_mu_, mu_;
+  std::condition_variable cv_, done_cv_;
+  std::vector<std::thread> workers_;
+  const std::function<void(int)>* fn_ = nullptr;
+  int n_tasks_ = 0, remaining_ = 0, next_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
 size_t count_lines(const char* b, const char* e) {
   size_t n = 0;
   while (b < e) {
@@ -173,22 +269,16 @@ INGEST_API long long ingest_parse(const char* buf, size_t len, char delim, int n
     if (cut[(size_t)t] < cut[(size_t)t - 1]) cut[(size_t)t] = cut[(size_t)t - 1];
   }
   std::vector<size_t> lines((size_t)T, 0), start((size_t)T + 1, 0), bads((size_t)T, 0);
-  std::vector<std::thread> th;
-  for (int t = 0; t < T; ++t)
-    th.emplace_back([&, t] { lines[(size_t)t] = count_lines(cut[(size_t)t], cut[(size_t)t + 1]); });
-  for (auto& x : th) x.join();
-  th.clear();
+  Pool& pool = Pool::instance();
+  pool.run(T, [&](int t) { lines[(size_t)t] = count_lines(cut[(size_t)t], cut[(size_t)t + 1]); });
   for (int t = 0; t < T; ++t) start[(size_t)t + 1] = start[(size_t)t] + lines[(size_t)t];
   const size_t rows = std::min(start[(size_t)T], max_rows);
-  for (int t = 0; t < T; ++t) {
-    if (start[(size_t)t] >= rows) break;
-    th.emplace_back([&, t] {
-      const size_t cap = std::min(lines[(size_t)t], rows - start[(size_t)t]);
-      parse_range(sp, cut[(size_t)t], cut[(size_t)t + 1], out + start[(size_t)t] * (size_t)n_out, n_out, cap,
-                  &bads[(size_t)t]);
-    });
-  }
-  for (auto& x : th) x.join();
+  pool.run(T, [&](int t) {
+    if (start[(size_t)t] >= rows) return;
+    const size_t cap = std::min(lines[(size_t)t], rows - start[(size_t)t]);
+    parse_range(sp, cut[(size_t)t], cut[(size_t)t + 1], out + start[(size_t)t] * (size_t)n_out, n_out, cap,
+                &bads[(size_t)t]);
+  });
   if (rows < start[(size_t)T]) {
     // stopped at max_rows: report the bytes actually covered (lines before the cap)
     size_t seen = 0;
