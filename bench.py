@@ -65,7 +65,8 @@ def parse_args(argv=None):
     p.add_argument("--micro-batch", type=int, default=1 << 20,
                    help="rows per H2D slice + kernel launch (1M measured best: profiles/r2_h2d_probe.md)")
     p.add_argument("--pipeline-depth", type=int, default=3, help="input ring slots (H2D/compute overlap)")
-    p.add_argument("--h2d-streams", type=int, default=1, help="copy streams per micro-batch (SDMA engines)")
+    p.add_argument("--h2d-streams", type=int, default=0,
+                   help="copy streams per micro-batch (copy engines); 0 = calibrate 1 vs 2 on this box")
     p.add_argument("--max-inflight", type=int, default=3, help="scored steps in flight before the sink waits")
     p.add_argument("--precision", choices=["fp32", "bf16", "fp8"], default=None,
                    help="default fp32 (trees), bf16 (mlp, BASELINE config 4); fp8 = e4m3 leaves (config 5)")
@@ -158,6 +159,14 @@ class _BenchSink:
         for w in self._works:
             w.wait()
         self._works = []
+
+
+def _h2d_streams(model, args):
+    """Copy streams the pipeline used (auto mode: what the calibration chose on this box)."""
+    from flink_jpmml_amd.utils.metrics import METRICS
+
+    chosen = METRICS.summary()["counters"].get("pipeline.h2d_streams_chosen")
+    return int(chosen) if chosen else args.h2d_streams
 
 
 def main(argv=None) -> int:
@@ -330,6 +339,7 @@ def main(argv=None) -> int:
                 "api": args.api,
                 "micro_batch": args.micro_batch,
                 "pipeline_depth": args.pipeline_depth,
+                "h2d_streams": _h2d_streams(model, args),
                 "rows_per_gpu_per_step": args.rows,
                 "allgather_sink": gather,
                 "zero_copy_host_sink": bool(getattr(model.scorer, "direct", False)),

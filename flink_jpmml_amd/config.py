@@ -54,9 +54,9 @@ class ScoringConfig:
     """Rows per device kernel launch when a RecordBatch is split (H2D / kernel overlap)."""
     pipeline_depth: int = 3
     """Device input slots of the H2D → kernel ring (copy of batch i+1 overlaps kernel i)."""
-    h2d_streams: int = 1
-    """Copy streams each micro-batch's host→device transfer is split over (concurrent SDMA
-    engines; 1 saturates the link on the boxes measured so far)."""
+    h2d_streams: int = 0
+    """Copy streams each micro-batch's host→device transfer is split over (concurrent copy
+    engines); 0 = calibrate 1 vs 2 on the first copy and keep the faster (boxes differ)."""
     max_inflight: int = 4
     """Scored batches an operator keeps in flight before it waits for the oldest (backpressure)."""
 

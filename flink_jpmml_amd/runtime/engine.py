@@ -58,15 +58,19 @@ class DevicePipeline:
     """HIP streams + the device input ring, shareable by several plans on one device. The ring
     holds ``depth`` flat fp32 slots of ``micro_batch × max_features`` (grown on demand)."""
 
-    def __init__(self, device, micro_batch: int = 1 << 19, depth: int = 3, h2d_streams: int = 1):
+    def __init__(self, device, micro_batch: int = 1 << 19, depth: int = 3, h2d_streams: int = 0):
         import torch
 
         self.device = torch.device(device)
         self.B = int(micro_batch)
         self.depth = int(depth)
-        # each micro-batch copy may be split over `h2d_streams` streams (concurrent SDMA engines;
-        # measured: one stream is best for whole micro-batches — profiles/r1_s4_bench_h2d*.log)
-        self.h2ds = [torch.cuda.Stream(self.device) for _ in range(max(1, int(h2d_streams)))]
+        # each micro-batch copy may be split over `h2d_streams` streams (concurrent copy engines).
+        # 0 = auto: the first copy calibrates 1 vs 2 streams on this box and keeps the faster —
+        # measured: one box moves a whole 128 MiB micro-batch at 56 GB/s on one stream, another at
+        # 34 GB/s on one and 56 GB/s split over two (profiles/r2_h2d_probe.md)
+        self.auto_h2d = int(h2d_streams) <= 0
+        self.h2ds = [torch.cuda.Stream(self.device) for _ in range(2 if self.auto_h2d else int(h2d_streams))]
+        self.n_h2d = None if self.auto_h2d else len(self.h2ds)
         self.h2d = self.h2ds[0]
         self.comp = torch.cuda.Stream(self.device)
         self.d2h = torch.cuda.Stream(self.device)
@@ -89,6 +93,43 @@ class DevicePipeline:
                 t.record_stream(st)
         self.slots = [torch.empty(elems, dtype=torch.float32, device=self.device) for _ in range(self.depth)]
         self.slot_elems = elems
+
+    def active_h2d(self) -> List:
+        """The copy streams in use (calibrated on first use in auto mode)."""
+        if self.n_h2d is None:
+            self.n_h2d = self._calibrate_h2d()
+        return self.h2ds[: self.n_h2d]
+
+    def _calibrate_h2d(self, mib: int = 128, reps: int = 3) -> int:
+        import time
+
+        import torch
+
+        n = mib * (1 << 18)  # fp32 elements
+        src = torch.empty(n, dtype=torch.float32, pin_memory=True)
+        src.fill_(1.0)
+        dst = torch.empty(n, dtype=torch.float32, device=self.device)
+        best = {}
+        for k in (1, 2):
+            part = -(-n // k)
+            ts = []
+            for _ in range(reps + 1):
+                torch.cuda.synchronize(self.device)
+                t0 = time.perf_counter()
+                for j in range(k):
+                    with torch.cuda.stream(self.h2ds[j]):
+                        dst[j * part:(j + 1) * part].copy_(src[j * part:(j + 1) * part], non_blocking=True)
+                torch.cuda.synchronize(self.device)
+                ts.append(time.perf_counter() - t0)
+            best[k] = min(ts[1:])
+        del src, dst
+        choice = 2 if best[2] < 0.97 * best[1] else 1
+        from ..utils.metrics import METRICS
+
+        METRICS.observe("pipeline.h2d_calibration_gbps_1", mib * 1.048576e-3 / best[1])
+        METRICS.observe("pipeline.h2d_calibration_gbps_2", mib * 1.048576e-3 / best[2])
+        METRICS.inc("pipeline.h2d_streams_chosen", choice)
+        return choice
 
     def host_dev_ptr(self, t):
         from ..ops._lib import host_device_ptr
@@ -121,7 +162,7 @@ class StreamingScorer:
 
     def __init__(self, plan, micro_batch: int = 131072, depth: int = 3, max_rows: Optional[int] = None,
                  out_buffers: int = 2, direct_host_output: bool = True, keep_device_output: bool = True,
-                 h2d_streams: int = 1, pipeline: Optional[DevicePipeline] = None, max_inflight: int = 4):
+                 h2d_streams: int = 0, pipeline: Optional[DevicePipeline] = None, max_inflight: int = 4):
         self.plan = plan
         self.device = plan.device
         self.F = plan.n_features
@@ -191,8 +232,9 @@ class StreamingScorer:
             xs, slot = X_src[s:e], None
         else:
             slot, xs = self._slot(m)
-            part = -(-m // len(p.h2ds))
-            for j, st in enumerate(p.h2ds):
+            h2ds = p.active_h2d()
+            part = -(-m // len(h2ds))
+            for j, st in enumerate(h2ds):
                 with torch.cuda.stream(st):
                     if p.used[slot]:
                         st.wait_event(p.ev_comp[slot])  # kernel finished reading this slot
@@ -200,7 +242,7 @@ class StreamingScorer:
                     if a < b:
                         xs[a:b].copy_(X_src[s + a:s + b], non_blocking=True)
                     p.ev_h2d[slot][j].record(st)
-            for ev in p.ev_h2d[slot]:
+            for ev in p.ev_h2d[slot][: len(h2ds)]:
                 p.comp.wait_event(ev)
         self.plan.launch(xs, out_score, out_valid, stream=p.comp, **kw)
         if slot is not None:
