@@ -69,6 +69,8 @@ struct MlpArgs {
   float* probs;
   const int2* panels;       // [n_panels] {offset, size} in 16-byte units, consumption order
   int n_panels, contiguous; // contiguous: in_index[k] == k (vector input loads)
+  unsigned long long* prof; // optional phase timers of workgroup 0 / wave 0 (s_memtime ticks):
+                            // [stage, chain, barrier, epilogue, tiles, steps]
 };
 
 __device__ __forceinline__ float activate(int a, float z, float thr) {
@@ -238,10 +240,12 @@ template <bool BF16>
 __device__ __forceinline__ void tile_step(const MlpArgs& a, const LayerMeta& m, int ti, int groups, bool last,
                                           int h, int lane, int tid, const float* s_b, const int2* s_pan,
                                           uint4* ring, const typename Cfg<BF16>::B (&pb)[Cfg<BF16>::KS],
-                                          typename Cfg<BF16>::B (&nb)[Cfg<BF16>::KS], f32x16& out, int& p) {
+                                          typename Cfg<BF16>::B (&nb)[Cfg<BF16>::KS], f32x16& out, int& p,
+                                          bool prof_on, unsigned long long* prof_acc) {
   using C = Cfg<BF16>;
   // panel p+2 streams into slot (p+2) % NSLOT while this one is multiplied; that slot was last
   // read at step p-2, before the previous barrier
+  const unsigned long long t0 = prof_on ? __builtin_amdgcn_s_memtime() : 0ull;
   issue_panel<BF16>(a, s_pan, p + 2, tid, ring);
   const uint4* slot = ring + (p % NSLOT) * (C::PANEL / 16);
   f32x16 acc;
@@ -264,7 +268,13 @@ __device__ __forceinline__ void tile_step(const MlpArgs& a, const LayerMeta& m, 
       default: store_nb<BF16, 7>(acc, nb); break;
     }
   }
+  const unsigned long long t1 = prof_on ? __builtin_amdgcn_s_memtime() : 0ull;
   panel_barrier<BF16>();  // panel p+1 resident for the next step
+  if (prof_on && lane == 0) {
+    prof_acc[1] += t1 - t0;
+    prof_acc[2] += __builtin_amdgcn_s_memtime() - t1;
+    prof_acc[5] += 1;
+  }
   ++p;
 }
 
@@ -311,7 +321,13 @@ __global__ __launch_bounds__(64 * Cfg<BF16>::WAVES, 1) void mlp_kernel(MlpArgs a
 
   const int n_tiles = (a.n_rows + 32 * C::WAVES - 1) / (32 * C::WAVES);
   int p = 0;  // panel counter (runs across row tiles)
+  const bool prof_on = a.prof != nullptr && blockIdx.x == 0 && wave == 0;
+  unsigned long long* prof_acc = reinterpret_cast<unsigned long long*>(s_rowbad + C::WAVES * 64);  // [6] in LDS
+  if (prof_on && lane == 0) {
+    for (int i = 0; i < 6; ++i) prof_acc[i] = 0ull;
+  }
   for (int tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+    const unsigned long long ts0 = prof_on ? __builtin_amdgcn_s_memtime() : 0ull;
     const int row = (tile * C::WAVES + wave) * 32 + col;
     const bool in_range = row < a.n_rows;
     const float* xrow = a.X + (size_t)(in_range ? row : 0) * a.ldx;
@@ -363,6 +379,10 @@ __global__ __launch_bounds__(64 * Cfg<BF16>::WAVES, 1) void mlp_kernel(MlpArgs a
     // the count in LDS for the epilogue.
     int* rbad = s_rowbad + 2 * (wave * 32 + col);  // read back after the layer loop (barriers between)
     rbad[h] = nbad;
+    if (prof_on && lane == 0) {
+      prof_acc[0] += __builtin_amdgcn_s_memtime() - ts0;
+      prof_acc[4] += 1;
+    }
 
     f32x16 out = {};
     for (int L = 0; L < a.n_layers; ++L) {
@@ -372,7 +392,7 @@ __global__ __launch_bounds__(64 * Cfg<BF16>::WAVES, 1) void mlp_kernel(MlpArgs a
       const bool last = L == a.n_layers - 1;
 #pragma unroll 1
       for (int ti = 0; ti < mtiles; ++ti)
-        tile_step<BF16>(a, m, ti, groups, last, h, lane, tid, s_b, s_pan, ring, pb, nb, out, p);
+        tile_step<BF16>(a, m, ti, groups, last, h, lane, tid, s_b, s_pan, ring, pb, nb, out, p, prof_on, prof_acc);
       if (!last) {
 #pragma unroll
         for (int s = 0; s < KS; ++s) pb[s] = nb[s];
@@ -380,11 +400,14 @@ __global__ __launch_bounds__(64 * Cfg<BF16>::WAVES, 1) void mlp_kernel(MlpArgs a
     }
 
     // ---- output layer: units 0..n_out-1 live in tile 0; lanes l and l^32 hold the two halves
+    const unsigned long long te0 = prof_on ? __builtin_amdgcn_s_memtime() : 0ull;
+    if (prof_on && lane == 0) prof_acc[3] -= te0;  // closed at the loop end (both epilogue paths)
     if (a.final_norm == 0 && a.n_out == 1) {
       if (h == 0 && in_range) {
         const bool bad = (rbad[0] | rbad[1]) != 0;
         apply_epilogue(a.epi, [&](int) { return out[0]; }, !bad, row, a.n_rows, a.score, a.valid, a.probs);
       }
+      if (prof_on && lane == 0) prof_acc[3] += __builtin_amdgcn_s_memtime();
       continue;
     }
     float mx = -__builtin_inff();
@@ -428,13 +451,18 @@ __global__ __launch_bounds__(64 * Cfg<BF16>::WAVES, 1) void mlp_kernel(MlpArgs a
         a.epi.valid2[row] = ok ? 1 : 0;
       }
     }
+    if (prof_on && lane == 0) prof_acc[3] += __builtin_amdgcn_s_memtime();
+  }
+  if (prof_on && lane == 0) {
+#pragma unroll
+    for (int i = 0; i < 6; ++i) a.prof[i] = prof_acc[i];
   }
 }
 
 template <bool BF16>
 size_t lds_bytes() {
   return (size_t)NSLOT * Cfg<BF16>::PANEL + 4 * KMAX * 4 + (size_t)MAXL * MT * 32 * 4 + (size_t)MAXL * MT * 8 +
-         (size_t)Cfg<BF16>::WAVES * 32 * 2 * 4;
+         (size_t)Cfg<BF16>::WAVES * 32 * 2 * 4 + 6 * 8;
 }
 
 int n_cus() {

@@ -67,7 +67,6 @@ struct TreeArgs {
 };
 constexpr int VAR_NAN_FAST = 4;    // wide kernel: take the fast path even on tiles with missing values
 constexpr int VAR_NAN_PLANES = 8;  // ... via blob_nan + a second feature plane (NaN -> +inf)
-constexpr int VAR_ILP16 = 16;      // wide kernel, SUM mode: 16-wide tree-walk batches
 
 // per-depth launchers (tree_d<D>.hip)
 #define PMML_TREE_DECL(D) int launch_perfect_d##D(hipStream_t st, const TreeArgs& a, dim3 grid, size_t lds);
@@ -752,9 +751,9 @@ int launch_wide(hipStream_t st, const TreeArgs& a, size_t lds_w) {
   using WG = WideGeom<ROWS>;
   dim3 grid((a.n_rows + ROWS - 1) / ROWS, (a.n_trees + a.trees_per_split - 1) / a.trees_per_split);
   (void)WG::G;
-  // VAR_ILP16: 16 independent tree walks per batch (more LDS round trips in flight per wave)
-  auto k = (MODE == MODE_SUM && (a.variant & VAR_ILP16)) ? tree_perfect_wide_kernel<D, 16, ROWS, LEAF8, MODE>
-                                                          : tree_perfect_wide_kernel<D, 8, ROWS, LEAF8, MODE>;
+  // 8 independent tree walks per batch (measured: 16 was 1.42x slower at depth 6, 1000 trees —
+  // profiles/r2_tree_kernel.md)
+  auto k = tree_perfect_wide_kernel<D, 8, ROWS, LEAF8, MODE>;
   int err = prepare_launch(k, lds_w);
   if (!err) hipLaunchKernelGGL(k, grid, dim3(WIDE_T), lds_w, st, a);
   return err;

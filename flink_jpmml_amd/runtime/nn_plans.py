@@ -235,6 +235,7 @@ class MlpPlan(DevicePlan):
         a.weights, a.biases, a.layers = ptr(self.weights), ptr(self.biases), ptr(self.layer_meta)
         a.out_scale, a.out_shift, a.final_norm, a.n_out = self.out_a, self.out_b, self.final_norm, self.n_out
         a.panels, a.n_panels, a.contiguous = ptr(self.panels), self.n_panels, self.contiguous
+        a.prof = ptr(getattr(self, "prof", None))  # optional phase timers (scripts/kbench.py --mlp-prof)
         a.epi = _epilogue(mode=EPI_AFFINE, a=self.out_a, b=self.out_b, table=self.table, tgt=self.target_stage)
         a.epi.score2, a.epi.valid2 = _addr(score2), _addr(valid2)
         a.score, a.valid, a.probs = _addr(score), _addr(valid), ptr(probs)

@@ -882,7 +882,7 @@ def _perfect_pack(trees: List[BinaryTree], weights: List[float], P: int, D: int,
     return blob, rec, has_dr
 
 
-VAR_NAN_FAST, VAR_NAN_PLANES, VAR_ILP16 = 4, 8, 16  # mirrors csrc/tree_common.h
+VAR_NAN_FAST, VAR_NAN_PLANES = 4, 8  # mirrors csrc/tree_common.h
 
 
 def _nan_planes(blob: np.ndarray, D: int, F: int, stride: int = TB) -> np.ndarray:
@@ -999,7 +999,7 @@ class TreePlan(DevicePlan):
 
     def __init__(self, compiled, device, layout: str = "auto", lds_budget: int = 80 * 1024, splits: int = 0,
                  variant: str = "auto", precision: str = "fp32", nan_mode: str = "auto", max_chunk_trees: int = 0,
-                 tree_shard: Optional[Tuple[int, int]] = None, ilp: int = 8):
+                 tree_shard: Optional[Tuple[int, int]] = None):
         """``nan_mode`` (wide PERFECT kernel): ``"auto"`` keeps tiles with missing values on the fast
         traversal whenever the ensemble has no null-on-missing trees (default-right nodes read a
         NaN -> +inf second feature plane, :func:`_nan_planes`); ``"off"``: per-node missing test.
@@ -1010,9 +1010,6 @@ class TreePlan(DevicePlan):
         super().__init__(compiled, device)
         if nan_mode not in ("auto", "off"):
             raise ValueError("nan_mode must be 'auto' or 'off'")
-        if ilp not in (8, 16):
-            raise ValueError("ilp (independent tree walks per batch, wide kernel) must be 8 or 16")
-        self.ilp = ilp
         if precision not in ("fp32", "fp8"):
             raise ValueError("tree leaf precision must be fp32 or fp8")
         if layout == "general":
@@ -1140,8 +1137,6 @@ class TreePlan(DevicePlan):
                 self.epi_args["a"] = self.epi_args.get("a", 1.0) * scale
                 self.variant = 2
             self.variant |= nan_flags
-            if self.ilp == 16 and self.variant & 3 and self.mode == 0:
-                self.variant |= VAR_ILP16
             self.rec_words = rec
             wide = self.variant & 3 in (1, 2)
             if wide:
@@ -1222,9 +1217,8 @@ class TreePlan(DevicePlan):
         tail batches (measured: 64 > 79 > 57 trees at depth 6)."""
         c = int(max(1, min(self.n_trees, fit)))
         G = 1024 // getattr(self, "rows_wide", 256)
-        ilp = 16 if getattr(self, "ilp", 8) == 16 and getattr(self, "mode", 0) == 0 else 8
         if wide and c < self.n_trees:
-            q = ilp * G if c >= 2 * ilp * G else 2 * G
+            q = 8 * G if c >= 16 * G else 2 * G
             c = max(q, c // q * q) if c >= q else c
         return min(c, cap) if cap > 0 else c
 

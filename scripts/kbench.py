@@ -24,7 +24,7 @@ def main():
     p.add_argument("--layout", default="auto")
     p.add_argument("--lds-budget", type=int, default=80 * 1024)
     p.add_argument("--variant", default="auto")
-    p.add_argument("--ilp", type=int, default=8, help="wide tree kernel: independent walks per batch (8|16)")
+    p.add_argument("--mlp-prof", action="store_true", help="MLP: per-phase s_memtime ticks of workgroup 0")
     p.add_argument("--clusters", type=int, default=256)
     p.add_argument("--nan-mode", default="auto")
     p.add_argument("--max-chunk-trees", type=int, default=0)
@@ -74,7 +74,7 @@ def main():
     opts = {}
     if args.model.startswith(("gbdt", "rf")):
         opts = dict(layout=args.layout, lds_budget=args.lds_budget, variant=args.variant, nan_mode=args.nan_mode,
-                    max_chunk_trees=args.max_chunk_trees, ilp=args.ilp)
+                    max_chunk_trees=args.max_chunk_trees)
     elif args.model == "kmeans-big":
         opts = dict(cluster_variant=args.variant)
     if args.precision != "fp32":
@@ -94,6 +94,16 @@ def main():
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / args.iters
+    prof = None
+    if args.model == "mlp" and args.mlp_prof:
+        plan.prof = torch.zeros(6, dtype=torch.int64, device="cuda")
+        plan.launch(X, s, v)
+        torch.cuda.synchronize()
+        st, ch, ba, ep, tiles, steps = plan.prof.cpu().tolist()
+        prof = {"ticks_stage_per_tile": st / max(tiles, 1), "ticks_chain_per_step": ch / max(steps, 1),
+                "ticks_barrier_per_step": ba / max(steps, 1), "ticks_epilogue_per_tile": ep / max(tiles, 1),
+                "tiles": tiles, "steps": steps, "total_ticks": st + ch + ba + ep}
+        plan.prof = None
     flops = None
     if args.model == "mlp":
         dims = [F] + [int(x) for x in args.hidden.split(",")] + [1]
@@ -103,7 +113,7 @@ def main():
                       "rows_per_s": args.rows / ms * 1e3, "plan": type(plan).__name__,
                       "layout": getattr(plan, "layout", None), "chunk_trees": getattr(plan, "chunk_trees", None),
                       "missing": args.missing, "lds_budget": args.lds_budget,
-                      "variant": getattr(plan, "variant", None)}))
+                      "variant": getattr(plan, "variant", None), "mlp_prof": prof}))
 
 
 if __name__ == "__main__":
