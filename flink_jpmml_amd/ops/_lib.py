@@ -165,7 +165,8 @@ class MlpArgs(ctypes.Structure):
                 ("n_in", c_int), ("k0", c_int), ("weights", c_void_p), ("biases", c_void_p), ("layers", c_void_p),
                 ("out_scale", c_float), ("out_shift", c_float), ("final_norm", c_int), ("n_out", c_int),
                 ("epi", Epilogue), ("score", c_void_p), ("valid", c_void_p), ("probs", c_void_p),
-                ("panels", c_void_p), ("n_panels", c_int), ("contiguous", c_int), ("prof", c_void_p)]
+                ("panels", c_void_p), ("n_panels", c_int), ("contiguous", c_int), ("prof", c_void_p),
+                ("reg_kernel", c_int), ("pad_", c_int)]
 
 
 class SvmArgs(ctypes.Structure):

@@ -71,6 +71,8 @@ struct MlpArgs {
   int n_panels, contiguous; // contiguous: in_index[k] == k (vector input loads)
   unsigned long long* prof; // optional phase timers of workgroup 0 / wave 0 (s_memtime ticks):
                             // [stage, chain, barrier, epilogue, tiles, steps]
+  int reg_kernel;           // bf16: 1 = register-weight kernel (host checked the shape), 0 = panel kernel
+  int pad_;
 };
 
 __device__ __forceinline__ float activate(int a, float z, float thr) {
@@ -476,6 +478,407 @@ int n_cus() {
   return n;
 }
 
+
+// ================================================================================================
+// Register-weight kernel (bf16; 1 or 2 hidden layers of <= 256 units over <= 256 inputs, then an
+// output layer of <= 32 units) — the shape of almost every exported PMML NeuralNetwork.
+//
+// The panel kernel above keeps each wave's ROWS stationary (activations in registers) and streams
+// every weight through LDS, one barrier per 32-unit output tile. Here the WEIGHTS are stationary:
+// wave w of the 8 owns output tile t = w % T of every hidden layer and holds that tile's A
+// fragments (all k-steps) in VGPRs for the whole persistent kernel — loaded once per workgroup,
+// never re-read. Activations move through LDS instead: a 128-row block is staged once (fp32 ->
+// normalised bf16, already in B-operand layout), each hidden layer reads its B fragments from one
+// LDS buffer (one conflict-free ds_read_b128 per MFMA, issued 4 ahead) and writes its activated
+// tile into the other (two ds_write_b128 per 32 rows: with the host's k permutation an accumulator
+// register IS the next layer's B element, so no lane exchange). One barrier per LAYER per block
+// (64 MFMAs per wave between barriers for a 256-unit layer) instead of one per tile; the next
+// block's records are prefetched into registers while the current block computes. The small
+// output layer takes its A fragments from LDS (staged once) and its fp32 result goes through LDS to
+// one epilogue thread per row (final normalisation, argmax / label table, target decode).
+//
+// LDS: 2 activation buffers [4 column blocks][16 k-steps][64 lanes] x 16 B (2 x 64 KiB), output-
+// layer fragments (<= 16 KiB), normalisation tables, biases, per-row flags: ~152 KiB -> one
+// 512-thread workgroup per CU, two waves per SIMD.
+constexpr int RR = 128;        // rows per block
+constexpr int RCB = RR / 32;   // 32-row column blocks (MFMA N)
+constexpr int RKS = 16;        // k-steps per column block in a buffer (K <= 256)
+constexpr int RWV = 8;         // waves
+constexpr int RT = RWV * 64;   // threads
+constexpr int RBUF = RCB * RKS * 64;  // uint4 per activation buffer
+
+template <int N>
+__device__ __forceinline__ void rchain_rb_n(const bf16x8* A, const uint4* b, f32x16& acc) {
+  // A from registers (compile-time indices after inlining), B from LDS with a 4-deep read window
+  constexpr int W = N < 4 ? N : 4;
+  uint4 win[W];
+#pragma unroll
+  for (int i = 0; i < W; ++i) win[i] = b[i * 64];
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int s = 0; s < N; ++s) {
+    const uint4 w = win[s % W];
+    if (s + W < N) win[s % W] = b[(s + W) * 64];
+    bf16x8 B;
+    __builtin_memcpy(&B, &w, 16);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[s], B, acc, 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+template <int KA, int N = 1>
+__device__ __forceinline__ void rchain_rb(int ks, const bf16x8 (&A)[KA], const uint4* b, f32x16& acc) {
+  if (ks == N) {
+    rchain_rb_n<N>(A, b, acc);
+  } else if constexpr (N < KA) {
+    rchain_rb<KA, N + 1>(ks, A, b, acc);
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void rchain_ll_n(const uint4* a, const uint4* b, f32x16& acc) {
+  constexpr int W = N < 4 ? N : 4;
+  uint4 wa[W], wb[W];
+#pragma unroll
+  for (int i = 0; i < W; ++i) {
+    wa[i] = a[i * 64];
+    wb[i] = b[i * 64];
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int s = 0; s < N; ++s) {
+    const uint4 x = wa[s % W], y = wb[s % W];
+    if (s + W < N) {
+      wa[s % W] = a[(s + W) * 64];
+      wb[s % W] = b[(s + W) * 64];
+    }
+    bf16x8 A, B;
+    __builtin_memcpy(&A, &x, 16);
+    __builtin_memcpy(&B, &y, 16);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, B, acc, 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+template <int N = 1>
+__device__ __forceinline__ void rchain_ll(int ks, const uint4* a, const uint4* b, f32x16& acc) {
+  if (ks == N) {
+    rchain_ll_n<N>(a, b, acc);
+  } else if constexpr (N < RKS) {
+    rchain_ll<N + 1>(ks, a, b, acc);
+  }
+}
+
+__device__ __forceinline__ void activate16(int act, float thr, f32x16& acc) {
+  switch (act) {  // uniform
+    case A_IDENTITY: break;
+    case A_RELU:
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = fmaxf(acc[r], 0.0f);
+      break;
+    case A_LOGISTIC:
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 1.0f / (1.0f + __expf(-acc[r]));
+      break;
+    default:
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = activate(act, acc[r], thr);
+      break;
+  }
+}
+
+__device__ __forceinline__ void bias16(const float* s_b, int t, int h, f32x16& acc) {
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = s_b[32 * t + acc_row(r, h)];
+}
+
+// One hidden layer for wave w: its tile t = w % T over the column blocks it shares with the other
+// waves of that tile; B from `bin`, activated bf16 result into `bout` (B layout of the next layer).
+template <int KA>
+__device__ __forceinline__ void rhidden(const LayerMeta& m, const bf16x8 (&A)[KA], int w, int lane, int h,
+                                        const uint4* bin, uint4* bout, const float* s_b) {
+  const int T = m.mp >> 5;
+  const int ks = m.kp >> 4;
+  const int t = w % T;
+  const int q = w / T;
+  const int nq = (RWV - 1 - t) / T + 1;
+  const bool partial = 32 * t + 32 > m.mreal;  // padded units must stay 0 (e.g. reciprocal(0))
+  for (int cb = q; cb < RCB; cb += nq) {
+    f32x16 acc;
+    bias16(s_b, t, h, acc);
+    rchain_rb<KA>(ks, A, bin + cb * RKS * 64 + lane, acc);
+    activate16(m.act, m.thr, acc);
+    if (partial) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (32 * t + acc_row(r, h) >= m.mreal) acc[r] = 0.0f;
+    }
+    bf16x8 lo, hi;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      lo[j] = (__bf16)acc[j];
+      hi[j] = (__bf16)acc[8 + j];
+    }
+    uint4 ulo, uhi;
+    __builtin_memcpy(&ulo, &lo, 16);
+    __builtin_memcpy(&uhi, &hi, 16);
+    bout[(cb * RKS + 2 * t) * 64 + lane] = ulo;
+    bout[(cb * RKS + 2 * t + 1) * 64 + lane] = uhi;
+  }
+}
+
+// Staging item i of a block: 8 consecutive inputs (k-group kg) of one row; 8 consecutive items are
+// 8 consecutive rows of one k-group (coalesced row segments, conflict-free 16-B LDS stores).
+struct RItem {
+  int row, kg;
+};
+__device__ __forceinline__ RItem ritem(int i, int KG) {
+  const int c_lo = i & 7;
+  const int rest = i >> 3;
+  return RItem{8 * (rest / KG) + c_lo, rest % KG};
+}
+
+__device__ __forceinline__ void rload(const MlpArgs& a, const int* s_ix, int row, int kg, bool vec, float (&v)[8]) {
+  if (row >= a.n_rows) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = 0.f;
+    return;
+  }
+  const float* xr = a.X + (size_t)row * a.ldx;
+  if (vec) {
+    const float4 p = *reinterpret_cast<const float4*>(xr + 8 * kg);
+    const float4 q = *reinterpret_cast<const float4*>(xr + 8 * kg + 4);
+    v[0] = p.x; v[1] = p.y; v[2] = p.z; v[3] = p.w;
+    v[4] = q.x; v[5] = q.y; v[6] = q.z; v[7] = q.w;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = 8 * kg + j;
+      v[j] = k < a.n_in ? xr[s_ix[k]] : 0.f;
+    }
+  }
+}
+
+__device__ __forceinline__ void rstore(const MlpArgs& a, const float* s_sc, const float* s_sh, const float* s_ms,
+                                       int row, int row0, int kg, const float (&v)[8], uint4* buf, int* s_bad) {
+  bf16x8 o;
+  bool bad = false;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = 8 * kg + j;
+    const float x = v[j];
+    float y = (x != x) ? s_ms[k] : fmaf(x, s_sc[k], s_sh[k]);
+    if (k >= a.n_in || row0 + row >= a.n_rows) y = 0.f;
+    bad = bad || (y != y);
+    o[j] = (__bf16)y;
+  }
+  if (bad && row0 + row < a.n_rows) s_bad[row] = 1;
+  uint4 u;
+  __builtin_memcpy(&u, &o, 16);
+  const int s = kg >> 1, hh = kg & 1, cb = row >> 5, col = row & 31;
+  buf[(cb * RKS + s) * 64 + hh * 32 + col] = u;
+}
+
+// NH hidden layers (A in registers: KA0 k-steps for layer 0, 16 for layer 1) + output layer.
+// PF: staging items prefetched per thread (k0 <= 64: 2 items = 16 VGPRs); 0 = load at staging.
+template <int NH, int KA0, int PF>
+__global__ __launch_bounds__(RT, 1) void mlp_reg_kernel(MlpArgs a) {
+  extern __shared__ __align__(16) uint4 rsm[];
+  uint4* buf0 = rsm;
+  uint4* buf1 = rsm + RBUF;
+  uint4* s_oa = rsm + 2 * RBUF;                                    // output-layer A [RKS][64]
+  float* s_sc = reinterpret_cast<float*>(s_oa + RKS * 64);
+  float* s_sh = s_sc + KMAX;
+  float* s_ms = s_sh + KMAX;
+  int* s_ix = reinterpret_cast<int*>(s_ms + KMAX);
+  float* s_b = reinterpret_cast<float*>(s_ix + KMAX);              // [3][256]
+  int* s_bad = reinterpret_cast<int*>(s_b + 3 * 256);              // [RR]
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = lane >> 5;
+  const int col = lane & 31;
+  const LayerMeta m0 = a.layers[0];
+  const LayerMeta m1 = a.layers[NH >= 2 ? 1 : 0];
+  const LayerMeta mo = a.layers[NH];
+  const int KG = a.k0 >> 3;  // k-groups of 8 inputs (k0 is a multiple of 16)
+  const bool vec = a.contiguous && (a.ldx & 3) == 0 && ((uintptr_t)a.X & 15) == 0;
+
+  // ---- once per workgroup: tables, biases, output-layer fragments, this wave's A fragments
+  for (int k = tid; k < KMAX; k += RT) {
+    const bool u = k < a.n_in;
+    s_sc[k] = u ? a.in_scale[k] : 0.f;
+    s_sh[k] = u ? a.in_shift[k] : 0.f;
+    s_ms[k] = u ? a.in_missing[k] : 0.f;
+    s_ix[k] = u ? a.in_index[k] : 0;
+  }
+  for (int i = tid; i < (NH + 1) * 256; i += RT) {
+    const int L = i >> 8, u = i & 255;
+    const LayerMeta& m = L == 0 ? m0 : (L == NH ? mo : m1);
+    s_b[i] = u < m.mp ? a.biases[m.b_off + u] : 0.f;
+  }
+  for (int i = tid; i < RR; i += RT) s_bad[i] = 0;
+  const uint4* W4 = reinterpret_cast<const uint4*>(a.weights);
+  const int kso = mo.kp >> 4;
+  for (int i = tid; i < kso * 64; i += RT) s_oa[i] = W4[mo.w_off / 8 + i];
+  bf16x8 A0[KA0];
+  bf16x8 A1[NH >= 2 ? RKS : 1];
+  {
+    const int ks = m0.kp >> 4, t = w % (m0.mp >> 5);
+#pragma unroll
+    for (int s = 0; s < KA0; ++s) {
+      if (s < ks) {
+        const uint4 u = W4[m0.w_off / 8 + (t * ks + s) * 64 + lane];
+        __builtin_memcpy(&A0[s], &u, 16);
+      }
+    }
+    if constexpr (NH >= 2) {
+      const int ks1 = m1.kp >> 4, t1 = w % (m1.mp >> 5);
+#pragma unroll
+      for (int s = 0; s < RKS; ++s) {
+        if (s < ks1) {
+          const uint4 u = W4[m1.w_off / 8 + (t1 * ks1 + s) * 64 + lane];
+          __builtin_memcpy(&A1[s], &u, 16);
+        }
+      }
+    }
+  }
+  float* s_out = reinterpret_cast<float*>(NH == 2 ? buf1 : buf0);  // [RR][33] fp32 output layer
+
+  const int n_blk = (a.n_rows + RR - 1) / RR;
+  const int n_items = RR * KG;
+  // PF > 0 (the host checked vector-loadable rows): this thread's staging items are the same in
+  // every block (i = tid + it * RT), so only their row pointers advance between blocks
+  float4 pf[PF > 0 ? PF : 1][2];
+  int blk = blockIdx.x;
+  if constexpr (PF > 0) {
+#pragma unroll
+    for (int it = 0; it < PF; ++it) {
+      const int i = tid + it * RT;
+      const RItem ri = ritem(i, KG);
+      const int row = min(blk * RR + ri.row, a.n_rows - 1);
+      const float4* src = reinterpret_cast<const float4*>(a.X + (size_t)row * a.ldx + 8 * ri.kg);
+      if (i < n_items) {
+        pf[it][0] = src[0];
+        pf[it][1] = src[1];
+      }
+    }
+  }
+  __syncthreads();
+
+  for (; blk < n_blk; blk += gridDim.x) {
+    const int row0 = blk * RR;
+    // ---- stage this block into buf0 (normalised bf16, B layout of layer 0)
+    if constexpr (PF > 0) {
+#pragma unroll
+      for (int it = 0; it < PF; ++it) {
+        const int i = tid + it * RT;
+        if (i < n_items) {
+          const RItem ri = ritem(i, KG);
+          const float v[8] = {pf[it][0].x, pf[it][0].y, pf[it][0].z, pf[it][0].w,
+                              pf[it][1].x, pf[it][1].y, pf[it][1].z, pf[it][1].w};
+          rstore(a, s_sc, s_sh, s_ms, ri.row, row0, ri.kg, v, buf0, s_bad);
+        }
+      }
+      const int nb = blk + gridDim.x;  // prefetch the next block while this one computes
+      if (nb < n_blk) {
+#pragma unroll
+        for (int it = 0; it < PF; ++it) {
+          const int i = tid + it * RT;
+          const RItem ri = ritem(i, KG);
+          const int row = min(nb * RR + ri.row, a.n_rows - 1);
+          const float4* src = reinterpret_cast<const float4*>(a.X + (size_t)row * a.ldx + 8 * ri.kg);
+          if (i < n_items) {
+            pf[it][0] = src[0];
+            pf[it][1] = src[1];
+          }
+        }
+      }
+    } else {
+      for (int i = tid; i < n_items; i += RT) {
+        const RItem ri = ritem(i, KG);
+        float v[8];
+        rload(a, s_ix, row0 + ri.row, ri.kg, vec, v);
+        rstore(a, s_sc, s_sh, s_ms, ri.row, row0, ri.kg, v, buf0, s_bad);
+      }
+    }
+    __syncthreads();
+    // ---- hidden layers
+    rhidden<KA0>(m0, A0, w, lane, h, buf0, buf1, s_b);
+    __syncthreads();
+    if constexpr (NH >= 2) {
+      rhidden<RKS>(m1, A1, w, lane, h, buf1, buf0, s_b + 256);
+      __syncthreads();
+    }
+    // ---- output layer: one tile, waves 0..3 take one column block each
+    const uint4* bo = NH == 2 ? buf0 : buf1;
+    if (w < RCB) {
+      const int cb = w;
+      f32x16 acc;
+      bias16(s_b + NH * 256, 0, h, acc);
+      rchain_ll(kso, s_oa + lane, bo + cb * RKS * 64 + lane, acc);
+      activate16(mo.act, mo.thr, acc);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int u = acc_row(r, h);
+        if (u < a.n_out) s_out[(32 * cb + col) * 33 + u] = acc[r];
+      }
+    }
+    __syncthreads();
+    // ---- epilogue: one thread per row
+    if (tid < RR) {
+      const int row = row0 + tid;
+      const bool bad = s_bad[tid] != 0;
+      s_bad[tid] = 0;
+      const float* o = s_out + tid * 33;
+      if (row < a.n_rows) {
+        if (a.final_norm == 0 && a.n_out == 1) {
+          apply_epilogue(a.epi, [&](int) { return o[0]; }, !bad, row, a.n_rows, a.score, a.valid, a.probs);
+        } else {
+          float mx = -__builtin_inff();
+          for (int u = 0; u < a.n_out; ++u) mx = fmaxf(mx, o[u]);
+          float sum = 0.f;
+          for (int u = 0; u < a.n_out; ++u) sum += (a.final_norm == 1) ? __expf(o[u] - mx) : o[u];
+          float best = -__builtin_inff();
+          int best_u = 1 << 30;
+          for (int u = 0; u < a.n_out; ++u) {
+            float p = (a.final_norm == 1) ? __expf(o[u] - mx) : o[u];
+            if (a.final_norm != 0) p /= sum;
+            if (p > best || (p == best && u < best_u)) { best = p; best_u = u; }
+            if (a.probs) a.probs[(size_t)row * a.n_out + u] = p;
+          }
+          bool ok = !bad && best == best && best_u < a.n_out;
+          float sc = ok ? (a.epi.has_table ? a.epi.table[best_u] : (float)best_u) : __builtin_nanf("");
+          ok = ok && (sc == sc);
+          a.score[row] = ok ? sc : __builtin_nanf("");
+          a.valid[row] = ok ? 1 : 0;
+          if (a.epi.score2) {
+            a.epi.score2[row] = ok ? sc : __builtin_nanf("");
+            a.epi.valid2[row] = ok ? 1 : 0;
+          }
+        }
+      }
+    }
+    if constexpr (NH == 1) __syncthreads();  // s_out (buf0) is the next block's staging buffer
+  }
+}
+
+constexpr size_t reg_lds_bytes() {
+  return (size_t)(2 * RBUF + RKS * 64) * 16 + 4 * KMAX * 4 + 3 * 256 * 4 + RR * 4;
+}
+
+template <int NH, int KA0, int PF>
+int launch_reg(hipStream_t stream, const MlpArgs& a) {
+  const int n_blk = (a.n_rows + RR - 1) / RR;
+  dim3 grid(min(n_blk, n_cus()));
+  const size_t lds = reg_lds_bytes();
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(mlp_reg_kernel<NH, KA0, PF>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return -5;
+  hipLaunchKernelGGL((mlp_reg_kernel<NH, KA0, PF>), grid, dim3(RT), lds, stream, a);
+  return hipGetLastError() == hipSuccess ? 0 : -7;
+}
+
 }  // namespace
 
 PMML_API int pmml_mlp_args_size() { return (int)sizeof(MlpArgs); }
@@ -487,6 +890,15 @@ PMML_API int pmml_mlp_launch(hipStream_t stream, const MlpArgs* args, int bf16) 
   if (a.n_layers < 1 || a.n_layers > MAXL || a.n_out > 32 || a.k0 > KMAX || a.n_in > KMAX || a.n_panels < 1 ||
       a.n_panels > MAXL * MT)
     return -4;
+  if (bf16 && a.reg_kernel) {
+    // register-weight kernel: the host (runtime/nn_plans.py::reg_kernel_ok) checked every layer's
+    // shape (hidden K, M <= 256, output layer <= 32 units)
+    if (a.n_layers < 2 || a.n_layers > 3) return -4;
+    const bool vec = a.contiguous && (a.ldx & 3) == 0 && ((uintptr_t)a.X & 15) == 0;
+    const bool narrow = a.k0 <= 64 && vec;  // prefetching variant: vector row loads
+    if (a.n_layers == 2) return narrow ? launch_reg<1, 4, 2>(stream, a) : launch_reg<1, 16, 0>(stream, a);
+    return narrow ? launch_reg<2, 4, 2>(stream, a) : launch_reg<2, 16, 0>(stream, a);
+  }
   const int waves = bf16 ? Cfg<true>::WAVES : Cfg<false>::WAVES;
   const int n_tiles = (a.n_rows + 32 * waves - 1) / (32 * waves);
   dim3 grid(min(n_tiles, n_cus()));

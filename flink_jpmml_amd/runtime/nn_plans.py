@@ -117,12 +117,23 @@ def pack_mlp_weights(layers: List[Tuple[np.ndarray, np.ndarray]], precision: str
     return np.concatenate(frags), np.concatenate(biases), meta
 
 
+def reg_kernel_ok(meta) -> bool:
+    """Shapes the bf16 register-weight kernel runs (``csrc/mlp.hip::mlp_reg_kernel``): one or two
+    hidden layers of at most 256 units over at most 256 inputs (their A fragments live in VGPRs)
+    and an output layer of one 32-unit tile. ``meta`` rows: ``(kp, mp, mreal, w_off, b_off)``."""
+    if len(meta) not in (2, 3):
+        return False
+    if any(kp > KMAX or mp > 32 * MT for kp, mp, *_ in meta):
+        return False
+    return meta[-1][1] == 32
+
+
 class MlpPlan(DevicePlan):
     kind = "mlp"
     supports_direct = True
     _STATE = DevicePlan._STATE + ("weights", "biases", "layer_meta", "in_scale", "in_shift", "in_missing", "in_index",
                                   "n_in", "k0", "n_layers", "bf16", "out_a", "out_b", "final_norm", "n_out", "table",
-                                  "is_classification", "panels", "n_panels", "contiguous", "target_stage")
+                                  "is_classification", "panels", "n_panels", "contiguous", "target_stage", "reg_kernel")
 
     def __init__(self, compiled, device, precision: str = "fp32"):
         import torch
@@ -158,6 +169,17 @@ class MlpPlan(DevicePlan):
         self.weights = (wt.to(torch.bfloat16) if self.bf16 else wt).to(self.device)
         self.biases = self._t(bias.astype(np.float32))
         self.layer_meta = self._t(lm)
+        self.reg_kernel = 1 if self.bf16 and reg_kernel_ok(meta) else 0
+
+    def set_kernel(self, name: str) -> None:
+        """Force the bf16 kernel: ``"reg"`` (register-weight, when the shape allows) or ``"panel"``."""
+        if name not in ("reg", "panel"):
+            raise ValueError(name)
+        self.reg_kernel = 1 if name == "reg" and self.bf16 and reg_kernel_ok(self._meta()) else 0
+
+    def _meta(self):
+        lm = self.layer_meta.cpu().numpy()
+        return [tuple(int(x) for x in row[:5]) for row in lm]
 
     def _io(self, compiled, ev):
         """Inputs (NormContinuous affine maps, missing replacements, active-field index), the
@@ -236,6 +258,7 @@ class MlpPlan(DevicePlan):
         a.out_scale, a.out_shift, a.final_norm, a.n_out = self.out_a, self.out_b, self.final_norm, self.n_out
         a.panels, a.n_panels, a.contiguous = ptr(self.panels), self.n_panels, self.contiguous
         a.prof = ptr(getattr(self, "prof", None))  # optional phase timers (scripts/kbench.py --mlp-prof)
+        a.reg_kernel = self.reg_kernel
         a.epi = _epilogue(mode=EPI_AFFINE, a=self.out_a, b=self.out_b, table=self.table, tgt=self.target_stage)
         a.epi.score2, a.epi.valid2 = _addr(score2), _addr(valid2)
         a.score, a.valid, a.probs = _addr(score), _addr(valid), ptr(probs)

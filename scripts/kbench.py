@@ -30,6 +30,7 @@ def main():
     p.add_argument("--max-chunk-trees", type=int, default=0)
     p.add_argument("--precision", default="fp32", choices=["fp32", "bf16", "fp8"])
     p.add_argument("--hidden", default="256,256", help="mlp hidden widths")
+    p.add_argument("--mlp-kernel", default="auto", choices=["auto", "reg", "panel"], help="bf16 MLP kernel")
     args = p.parse_args()
     import numpy as np
     import torch
@@ -80,6 +81,8 @@ def main():
     if args.precision != "fp32":
         opts["precision"] = args.precision
     plan = c.plan("cuda:0", **opts)
+    if args.model == "mlp" and args.mlp_kernel != "auto":
+        plan.set_kernel(args.mlp_kernel)
     F = c.n_features
     X = torch.from_numpy(synth.stream_matrix(args.rows, F, seed=1, missing_rate=args.missing)).cuda()
     s = torch.empty(args.rows, device="cuda")
@@ -113,7 +116,8 @@ def main():
                       "rows_per_s": args.rows / ms * 1e3, "plan": type(plan).__name__,
                       "layout": getattr(plan, "layout", None), "chunk_trees": getattr(plan, "chunk_trees", None),
                       "missing": args.missing, "lds_budget": args.lds_budget,
-                      "variant": getattr(plan, "variant", None), "mlp_prof": prof}))
+                      "variant": getattr(plan, "variant", None), "mlp_prof": prof,
+                      "mlp_kernel": ("reg" if getattr(plan, "reg_kernel", 0) else "panel") if args.model == "mlp" else None}))
 
 
 if __name__ == "__main__":

@@ -79,3 +79,36 @@ def test_mlp_beyond_fused_kernel_runs_on_device(gpu, hidden):
     assert (v == vref).all() and not v[3]
     scale = max(1.0, float(np.max(np.abs(ref[vref]))))
     assert np.max(np.abs(s[v] - ref[v])) < 1e-3 * scale
+
+
+@pytest.mark.parametrize("kernel", ["reg", "panel"])
+@pytest.mark.parametrize("shape", [
+    dict(n_features=64, hidden=(256, 256), n_out=1, activation="rectifier"),     # BASELINE config 4
+    dict(n_features=32, hidden=(100,), n_out=1, activation="logistic"),          # 1 hidden layer, partial tile
+    dict(n_features=21, hidden=(50, 33), n_out=7, activation="tanh", classification=True),  # gathered, softmax
+    dict(n_features=130, hidden=(256, 64), n_out=1, activation="rectifier"),     # k0 > 64: no prefetch
+])
+def test_mlp_bf16_kernels_vs_oracle(gpu, kernel, shape):
+    """Both bf16 kernels (register-weight and panel-ring) on several shapes over a row count that is
+    not a multiple of either kernel's block, with missing inputs, against the float64 oracle."""
+    from flink_jpmml_amd.bench.synth import mlp_pmml, stream_matrix
+    from flink_jpmml_amd.runtime.compiled import CompiledPmml
+
+    c = CompiledPmml.from_string(mlp_pmml(seed=4, **shape))
+    plan = c.plan(gpu, precision="bf16")
+    plan.set_kernel(kernel)
+    assert plan.reg_kernel == (1 if kernel == "reg" else 0)
+    n = 70_001
+    X = stream_matrix(n, shape["n_features"], seed=9)
+    nan_rows = [0, 127, 128, 40_000, n - 1]
+    X[nan_rows, 3] = np.nan
+    s, v = _np(plan, X)
+    idx = np.union1d(np.arange(0, n, 13), nan_rows)
+    ref, vref = c.score_matrix_oracle(X[idx])
+    s, v = s[idx], v[idx]
+    assert (v == vref).all() and not v[np.searchsorted(idx, nan_rows)].any()
+    if shape.get("classification"):
+        assert (s[v] == ref[v]).mean() > 0.97
+    else:
+        scale = max(1.0, float(np.max(np.abs(ref[vref]))))
+        assert np.max(np.abs(s[v] - ref[v])) < 3e-2 * scale
