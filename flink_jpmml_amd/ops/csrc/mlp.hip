@@ -489,27 +489,38 @@ int n_cus() {
 // fragments (all k-steps) in VGPRs for the whole persistent kernel — loaded once per workgroup,
 // never re-read. Activations move through LDS instead: a 128-row block is staged once (fp32 ->
 // normalised bf16, already in B-operand layout), each hidden layer reads its B fragments from one
-// LDS buffer (one conflict-free ds_read_b128 per MFMA, issued 4 ahead) and writes its activated
-// tile into the other (two ds_write_b128 per 32 rows: with the host's k permutation an accumulator
-// register IS the next layer's B element, so no lane exchange). One barrier per LAYER per block
-// (64 MFMAs per wave between barriers for a 256-unit layer) instead of one per tile; the next
-// block's records are prefetched into registers while the current block computes. The small
-// output layer takes its A fragments from LDS (staged once) and its fp32 result goes through LDS to
-// one epilogue thread per row (final normalisation, argmax / label table, target decode).
+// LDS buffer (conflict-free ds_read_b128, issued ahead) and writes its activated tile into the
+// other (two ds_write_b128 per 32 rows: with the host's k permutation an accumulator register IS
+// the next layer's B element, so no lane exchange). Two 32-row column blocks run as interleaved
+// accumulation chains on the same A registers, so each wave keeps two independent MFMA chains and
+// their LDS reads in flight.
 //
-// LDS: 2 activation buffers [4 column blocks][16 k-steps][64 lanes] x 16 B (2 x 64 KiB), output-
-// layer fragments (<= 16 KiB), normalisation tables, biases, per-row flags: ~152 KiB -> one
-// 512-thread workgroup per CU, two waves per SIMD.
+// FOLD (output layer of <= 4 units, the regression / binary case): the output layer is folded into
+// the last hidden layer — each wave dots its fp32 activated tile with the output weights (VALU,
+// 16 units per lane + one lane-half exchange) and parks the partial sum per (tile, row) in LDS;
+// the epilogue adds the tiles' partials in a fixed order (deterministic), the output bias and
+// activation. The software pipeline is then two phases / two barriers per 128-row block:
+//   NH = 2:  [hidden 0: buf0 -> buf1 | epilogue of the previous block]  barrier
+//            [hidden 1: buf1 -> partials | stage next block -> buf0]     barrier
+//   NH = 1:  [hidden 0: buf0 -> partials]  barrier  [epilogue | stage next -> buf0]  barrier
+// Without FOLD (more outputs) the output layer is a 1-tile MFMA layer with A fragments staged in
+// LDS once, and its fp32 result reaches the epilogue through LDS (four barriers per block).
+//
+// LDS (<= 156 KiB): 2 activation buffers [4 column blocks][16 k-steps][64 lanes] x 16 B
+// (2 x 64 KiB); FOLD: partials [8][128][4] fp32 + output weights [4][256] fp32; else output-layer
+// fragments (<= 16 KiB); normalisation tables, biases, per-row flags -> one 512-thread workgroup
+// per CU, two waves per SIMD.
 constexpr int RR = 128;        // rows per block
 constexpr int RCB = RR / 32;   // 32-row column blocks (MFMA N)
 constexpr int RKS = 16;        // k-steps per column block in a buffer (K <= 256)
 constexpr int RWV = 8;         // waves
 constexpr int RT = RWV * 64;   // threads
 constexpr int RBUF = RCB * RKS * 64;  // uint4 per activation buffer
+constexpr int RFO = 4;         // max outputs of the folded output layer
 
+// ---- accumulation chains: A from registers (compile-time indices after inlining), B from LDS
 template <int N>
-__device__ __forceinline__ void rchain_rb_n(const bf16x8* A, const uint4* b, f32x16& acc) {
-  // A from registers (compile-time indices after inlining), B from LDS with a 4-deep read window
+__device__ __forceinline__ void rchain1_n(const bf16x8* A, const uint4* b, f32x16& acc) {
   constexpr int W = N < 4 ? N : 4;
   uint4 win[W];
 #pragma unroll
@@ -517,24 +528,63 @@ __device__ __forceinline__ void rchain_rb_n(const bf16x8* A, const uint4* b, f32
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int s = 0; s < N; ++s) {
-    const uint4 w = win[s % W];
+    const uint4 x = win[s % W];
     if (s + W < N) win[s % W] = b[(s + W) * 64];
     bf16x8 B;
-    __builtin_memcpy(&B, &w, 16);
+    __builtin_memcpy(&B, &x, 16);
     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[s], B, acc, 0, 0, 0);
     __builtin_amdgcn_sched_barrier(0);
   }
 }
 
-template <int KA, int N = 1>
-__device__ __forceinline__ void rchain_rb(int ks, const bf16x8 (&A)[KA], const uint4* b, f32x16& acc) {
-  if (ks == N) {
-    rchain_rb_n<N>(A, b, acc);
-  } else if constexpr (N < KA) {
-    rchain_rb<KA, N + 1>(ks, A, b, acc);
+// two column blocks on the same A fragments: two independent chains, interleaved MFMA by MFMA
+template <int N>
+__device__ __forceinline__ void rchain2_n(const bf16x8* A, const uint4* b0, const uint4* b1, f32x16& c0,
+                                          f32x16& c1) {
+  constexpr int W = N < 2 ? N : 2;
+  uint4 w0[W], w1[W];
+#pragma unroll
+  for (int i = 0; i < W; ++i) {
+    w0[i] = b0[i * 64];
+    w1[i] = b1[i * 64];
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int s = 0; s < N; ++s) {
+    const uint4 x0 = w0[s % W], x1 = w1[s % W];
+    if (s + W < N) {
+      w0[s % W] = b0[(s + W) * 64];
+      w1[s % W] = b1[(s + W) * 64];
+    }
+    bf16x8 B0, B1;
+    __builtin_memcpy(&B0, &x0, 16);
+    __builtin_memcpy(&B1, &x1, 16);
+    c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[s], B0, c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[s], B1, c1, 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
   }
 }
 
+template <int KA, int N = 1>
+__device__ __forceinline__ void rchain1(int ks, const bf16x8 (&A)[KA], const uint4* b, f32x16& acc) {
+  if (ks == N) {
+    rchain1_n<N>(A, b, acc);
+  } else if constexpr (N < KA) {
+    rchain1<KA, N + 1>(ks, A, b, acc);
+  }
+}
+
+template <int KA, int N = 1>
+__device__ __forceinline__ void rchain2(int ks, const bf16x8 (&A)[KA], const uint4* b0, const uint4* b1,
+                                        f32x16& c0, f32x16& c1) {
+  if (ks == N) {
+    rchain2_n<N>(A, b0, b1, c0, c1);
+  } else if constexpr (N < KA) {
+    rchain2<KA, N + 1>(ks, A, b0, b1, c0, c1);
+  }
+}
+
+// output layer without FOLD: both operands from LDS
 template <int N>
 __device__ __forceinline__ void rchain_ll_n(const uint4* a, const uint4* b, f32x16& acc) {
   constexpr int W = N < 4 ? N : 4;
@@ -592,27 +642,38 @@ __device__ __forceinline__ void bias16(const float* s_b, int t, int h, f32x16& a
   for (int r = 0; r < 16; ++r) acc[r] = s_b[32 * t + acc_row(r, h)];
 }
 
-// One hidden layer for wave w: its tile t = w % T over the column blocks it shares with the other
-// waves of that tile; B from `bin`, activated bf16 result into `bout` (B layout of the next layer).
-template <int KA>
-__device__ __forceinline__ void rhidden(const LayerMeta& m, const bf16x8 (&A)[KA], int w, int lane, int h,
-                                        const uint4* bin, uint4* bout, const float* s_b) {
+struct RLayer {  // one hidden layer as wave w sees it
+  int ks, t, q, nq, mreal, act;
+  float thr;
+};
+__device__ __forceinline__ RLayer rlayer(const LayerMeta& m, int w) {
   const int T = m.mp >> 5;
-  const int ks = m.kp >> 4;
   const int t = w % T;
-  const int q = w / T;
-  const int nq = (RWV - 1 - t) / T + 1;
-  const bool partial = 32 * t + 32 > m.mreal;  // padded units must stay 0 (e.g. reciprocal(0))
-  for (int cb = q; cb < RCB; cb += nq) {
-    f32x16 acc;
-    bias16(s_b, t, h, acc);
-    rchain_rb<KA>(ks, A, bin + cb * RKS * 64 + lane, acc);
-    activate16(m.act, m.thr, acc);
-    if (partial) {
+  return RLayer{m.kp >> 4, t, w / T, (RWV - 1 - t) / T + 1, m.mreal, m.act, m.thr};
+}
+
+// activation, zeroed padded units (a padded unit's 0 must stay 0 through e.g. reciprocal), then
+// either the bf16 B fragments of the next layer or (FOLD) the partial output dot products
+template <bool LAST_FOLD>
+__device__ __forceinline__ void rfinish(const RLayer& L, f32x16& acc, int cb, int lane, int h, uint4* bout,
+                                        float* s_part, const float* s_wo, int n_out) {
+  activate16(L.act, L.thr, acc);
+  if (32 * L.t + 32 > L.mreal) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r)
-        if (32 * t + acc_row(r, h) >= m.mreal) acc[r] = 0.0f;
+    for (int r = 0; r < 16; ++r)
+      if (32 * L.t + acc_row(r, h) >= L.mreal) acc[r] = 0.0f;
+  }
+  if constexpr (LAST_FOLD) {
+    const int col = lane & 31;
+    for (int o = 0; o < n_out; ++o) {  // uniform, <= 4
+      const float* wo = s_wo + o * 256 + 32 * L.t;
+      float p = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) p = fmaf(acc[r], wo[acc_row(r, h)], p);
+      p += __shfl_xor(p, 32);
+      if (h == 0) s_part[(L.t * RR + 32 * cb + col) * RFO + o] = p;
     }
+  } else {
     bf16x8 lo, hi;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -622,8 +683,31 @@ __device__ __forceinline__ void rhidden(const LayerMeta& m, const bf16x8 (&A)[KA
     uint4 ulo, uhi;
     __builtin_memcpy(&ulo, &lo, 16);
     __builtin_memcpy(&uhi, &hi, 16);
-    bout[(cb * RKS + 2 * t) * 64 + lane] = ulo;
-    bout[(cb * RKS + 2 * t + 1) * 64 + lane] = uhi;
+    bout[(cb * RKS + 2 * L.t) * 64 + lane] = ulo;
+    bout[(cb * RKS + 2 * L.t + 1) * 64 + lane] = uhi;
+  }
+}
+
+// One hidden layer for wave w: its tile over the column blocks it owns, two at a time.
+template <int KA, bool LAST_FOLD>
+__device__ __forceinline__ void rhidden(const RLayer& L, const bf16x8 (&A)[KA], int lane, int h, const uint4* bin,
+                                        uint4* bout, const float* s_b, float* s_part, const float* s_wo,
+                                        int n_out) {
+  int cb = L.q;
+  for (; cb + L.nq < RCB; cb += 2 * L.nq) {
+    const int cb1 = cb + L.nq;
+    f32x16 c0;
+    bias16(s_b, L.t, h, c0);
+    f32x16 c1 = c0;
+    rchain2<KA>(L.ks, A, bin + cb * RKS * 64 + lane, bin + cb1 * RKS * 64 + lane, c0, c1);
+    rfinish<LAST_FOLD>(L, c0, cb, lane, h, bout, s_part, s_wo, n_out);
+    rfinish<LAST_FOLD>(L, c1, cb1, lane, h, bout, s_part, s_wo, n_out);
+  }
+  if (cb < RCB) {
+    f32x16 c0;
+    bias16(s_b, L.t, h, c0);
+    rchain1<KA>(L.ks, A, bin + cb * RKS * 64 + lane, c0);
+    rfinish<LAST_FOLD>(L, c0, cb, lane, h, bout, s_part, s_wo, n_out);
   }
 }
 
@@ -679,20 +763,54 @@ __device__ __forceinline__ void rstore(const MlpArgs& a, const float* s_sc, cons
   buf[(cb * RKS + s) * 64 + hh * 32 + col] = u;
 }
 
+// Output values of one row (accessor out(u), u < n_out) -> final normalisation, label / target
+// decode, score / valid / probability stores.
+template <typename Out>
+__device__ __forceinline__ void repilogue(const MlpArgs& a, Out out, bool bad, int row) {
+  if (a.final_norm == 0 && a.n_out == 1) {
+    apply_epilogue(a.epi, [&](int) { return out(0); }, !bad, row, a.n_rows, a.score, a.valid, a.probs);
+    return;
+  }
+  float mx = -__builtin_inff();
+  for (int u = 0; u < a.n_out; ++u) mx = fmaxf(mx, out(u));
+  float sum = 0.f;
+  for (int u = 0; u < a.n_out; ++u) sum += (a.final_norm == 1) ? __expf(out(u) - mx) : out(u);
+  float best = -__builtin_inff();
+  int best_u = 1 << 30;
+  for (int u = 0; u < a.n_out; ++u) {
+    float p = (a.final_norm == 1) ? __expf(out(u) - mx) : out(u);
+    if (a.final_norm != 0) p /= sum;
+    if (p > best || (p == best && u < best_u)) { best = p; best_u = u; }
+    if (a.probs) a.probs[(size_t)row * a.n_out + u] = p;
+  }
+  bool ok = !bad && best == best && best_u < a.n_out;
+  float sc = ok ? (a.epi.has_table ? a.epi.table[best_u] : (float)best_u) : __builtin_nanf("");
+  ok = ok && (sc == sc);
+  a.score[row] = ok ? sc : __builtin_nanf("");
+  a.valid[row] = ok ? 1 : 0;
+  if (a.epi.score2) {
+    a.epi.score2[row] = ok ? sc : __builtin_nanf("");
+    a.epi.valid2[row] = ok ? 1 : 0;
+  }
+}
+
 // NH hidden layers (A in registers: KA0 k-steps for layer 0, 16 for layer 1) + output layer.
-// PF: staging items prefetched per thread (k0 <= 64: 2 items = 16 VGPRs); 0 = load at staging.
-template <int NH, int KA0, int PF>
+// PF: staging items prefetched per thread (vector-loadable rows, k0 <= 64: 2 items = 16 VGPRs);
+// 0 = load at staging. FOLD: output layer (<= 4 units) folded into the last hidden layer.
+template <int NH, int KA0, int PF, bool FOLD>
 __global__ __launch_bounds__(RT, 1) void mlp_reg_kernel(MlpArgs a) {
   extern __shared__ __align__(16) uint4 rsm[];
   uint4* buf0 = rsm;
   uint4* buf1 = rsm + RBUF;
-  uint4* s_oa = rsm + 2 * RBUF;                                    // output-layer A [RKS][64]
-  float* s_sc = reinterpret_cast<float*>(s_oa + RKS * 64);
+  uint4* s_oa = rsm + 2 * RBUF;                                    // !FOLD: output-layer A [RKS][64]
+  float* s_part = reinterpret_cast<float*>(rsm + 2 * RBUF);        // FOLD: [8 tiles][RR][RFO]
+  float* s_wo = s_part + RWV * RR * RFO;                           // FOLD: [RFO][256] output weights
+  float* s_sc = FOLD ? s_wo + RFO * 256 : reinterpret_cast<float*>(s_oa + RKS * 64);
   float* s_sh = s_sc + KMAX;
   float* s_ms = s_sh + KMAX;
   int* s_ix = reinterpret_cast<int*>(s_ms + KMAX);
   float* s_b = reinterpret_cast<float*>(s_ix + KMAX);              // [3][256]
-  int* s_bad = reinterpret_cast<int*>(s_b + 3 * 256);              // [RR]
+  int* s_bad = reinterpret_cast<int*>(s_b + 3 * 256);              // [2][RR] per block parity
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -704,8 +822,9 @@ __global__ __launch_bounds__(RT, 1) void mlp_reg_kernel(MlpArgs a) {
   const LayerMeta mo = a.layers[NH];
   const int KG = a.k0 >> 3;  // k-groups of 8 inputs (k0 is a multiple of 16)
   const bool vec = a.contiguous && (a.ldx & 3) == 0 && ((uintptr_t)a.X & 15) == 0;
+  const int n_out = a.n_out;
 
-  // ---- once per workgroup: tables, biases, output-layer fragments, this wave's A fragments
+  // ---- once per workgroup: tables, biases, output layer, this wave's A fragments
   for (int k = tid; k < KMAX; k += RT) {
     const bool u = k < a.n_in;
     s_sc[k] = u ? a.in_scale[k] : 0.f;
@@ -718,58 +837,80 @@ __global__ __launch_bounds__(RT, 1) void mlp_reg_kernel(MlpArgs a) {
     const LayerMeta& m = L == 0 ? m0 : (L == NH ? mo : m1);
     s_b[i] = u < m.mp ? a.biases[m.b_off + u] : 0.f;
   }
-  for (int i = tid; i < RR; i += RT) s_bad[i] = 0;
+  for (int i = tid; i < 2 * RR; i += RT) s_bad[i] = 0;
   const uint4* W4 = reinterpret_cast<const uint4*>(a.weights);
   const int kso = mo.kp >> 4;
-  for (int i = tid; i < kso * 64; i += RT) s_oa[i] = W4[mo.w_off / 8 + i];
+  if constexpr (FOLD) {
+    // the output layer's weights W[o][k] back from its A fragments (one 32-unit tile):
+    // fragment (s, lane = (h', r)) element j = W[unit r][B-k index 16 s + 8 h' + j]
+    const __bf16* Wb = reinterpret_cast<const __bf16*>(a.weights) + mo.w_off;
+    for (int i = tid; i < RFO * 256; i += RT) {
+      const int o = i >> 8, k = i & 255;
+      float v = 0.f;
+      if (o < n_out && k < mo.kp) {
+        const int s = k >> 4, hh = (k >> 3) & 1, j = k & 7;
+        v = (float)Wb[((size_t)s * 64 + hh * 32 + o) * 8 + j];
+      }
+      // B-k index k of the last hidden layer's output = unit acc_row(r, h) of tile k / 32 with
+      // r = 8 * ((k >> 4) & 1) + (k & 7), h = (k >> 3) & 1 (the host permutation, inverted)
+      const int t = k >> 5, rr = 8 * ((k >> 4) & 1) + (k & 7), hh2 = (k >> 3) & 1;
+      s_wo[o * 256 + 32 * t + acc_row(rr, hh2)] = v;
+    }
+  } else {
+    for (int i = tid; i < kso * 64; i += RT) s_oa[i] = W4[mo.w_off / 8 + i];
+  }
   bf16x8 A0[KA0];
   bf16x8 A1[NH >= 2 ? RKS : 1];
-  {
-    const int ks = m0.kp >> 4, t = w % (m0.mp >> 5);
+  const RLayer L0 = rlayer(m0, w);
+  const RLayer L1 = rlayer(m1, w);
 #pragma unroll
-    for (int s = 0; s < KA0; ++s) {
-      if (s < ks) {
-        const uint4 u = W4[m0.w_off / 8 + (t * ks + s) * 64 + lane];
-        __builtin_memcpy(&A0[s], &u, 16);
-      }
+  for (int s = 0; s < KA0; ++s) {
+    if (s < L0.ks) {
+      const uint4 u = W4[m0.w_off / 8 + (L0.t * L0.ks + s) * 64 + lane];
+      __builtin_memcpy(&A0[s], &u, 16);
     }
-    if constexpr (NH >= 2) {
-      const int ks1 = m1.kp >> 4, t1 = w % (m1.mp >> 5);
+  }
+  if constexpr (NH >= 2) {
 #pragma unroll
-      for (int s = 0; s < RKS; ++s) {
-        if (s < ks1) {
-          const uint4 u = W4[m1.w_off / 8 + (t1 * ks1 + s) * 64 + lane];
-          __builtin_memcpy(&A1[s], &u, 16);
-        }
+    for (int s = 0; s < RKS; ++s) {
+      if (s < L1.ks) {
+        const uint4 u = W4[m1.w_off / 8 + (L1.t * L1.ks + s) * 64 + lane];
+        __builtin_memcpy(&A1[s], &u, 16);
       }
     }
   }
-  float* s_out = reinterpret_cast<float*>(NH == 2 ? buf1 : buf0);  // [RR][33] fp32 output layer
+  const int T_last = ((NH == 2 ? m1.mp : m0.mp) >> 5);
+  float* s_out = reinterpret_cast<float*>(NH == 2 ? buf1 : buf0);  // !FOLD: [RR][33] fp32 output layer
+  // Retire the A-fragment loads here, explicitly: otherwise the compiler's wait for them sits at
+  // their first use INSIDE the block loop as a vmcnt(0), which every block would then also spend
+  // waiting for the record prefetch of the next block (issued just before).
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
 
   const int n_blk = (a.n_rows + RR - 1) / RR;
   const int n_items = RR * KG;
-  // PF > 0 (the host checked vector-loadable rows): this thread's staging items are the same in
-  // every block (i = tid + it * RT), so only their row pointers advance between blocks
+  // PF > 0: this thread's staging items are the same in every block (i = tid + it * RT), so only
+  // their row pointers advance between blocks
   float4 pf[PF > 0 ? PF : 1][2];
-  int blk = blockIdx.x;
-  if constexpr (PF > 0) {
+  auto prefetch = [&](int b) {
+    if constexpr (PF > 0) {
+      if (b < n_blk) {
 #pragma unroll
-    for (int it = 0; it < PF; ++it) {
-      const int i = tid + it * RT;
-      const RItem ri = ritem(i, KG);
-      const int row = min(blk * RR + ri.row, a.n_rows - 1);
-      const float4* src = reinterpret_cast<const float4*>(a.X + (size_t)row * a.ldx + 8 * ri.kg);
-      if (i < n_items) {
-        pf[it][0] = src[0];
-        pf[it][1] = src[1];
+        for (int it = 0; it < PF; ++it) {
+          const int i = tid + it * RT;
+          const RItem ri = ritem(i, KG);
+          const int row = min(b * RR + ri.row, a.n_rows - 1);
+          const float4* src = reinterpret_cast<const float4*>(a.X + (size_t)row * a.ldx + 8 * ri.kg);
+          if (i < n_items) {
+            pf[it][0] = src[0];
+            pf[it][1] = src[1];
+          }
+        }
       }
     }
-  }
-  __syncthreads();
-
-  for (; blk < n_blk; blk += gridDim.x) {
-    const int row0 = blk * RR;
-    // ---- stage this block into buf0 (normalised bf16, B layout of layer 0)
+  };
+  auto stage = [&](int b, int par) {  // block b -> buf0 (normalised bf16, B layout of layer 0)
+    const int row0 = b * RR;
+    int* bad = s_bad + par * RR;
     if constexpr (PF > 0) {
 #pragma unroll
       for (int it = 0; it < PF; ++it) {
@@ -778,105 +919,158 @@ __global__ __launch_bounds__(RT, 1) void mlp_reg_kernel(MlpArgs a) {
           const RItem ri = ritem(i, KG);
           const float v[8] = {pf[it][0].x, pf[it][0].y, pf[it][0].z, pf[it][0].w,
                               pf[it][1].x, pf[it][1].y, pf[it][1].z, pf[it][1].w};
-          rstore(a, s_sc, s_sh, s_ms, ri.row, row0, ri.kg, v, buf0, s_bad);
+          rstore(a, s_sc, s_sh, s_ms, ri.row, row0, ri.kg, v, buf0, bad);
         }
       }
-      const int nb = blk + gridDim.x;  // prefetch the next block while this one computes
-      if (nb < n_blk) {
-#pragma unroll
-        for (int it = 0; it < PF; ++it) {
-          const int i = tid + it * RT;
-          const RItem ri = ritem(i, KG);
-          const int row = min(nb * RR + ri.row, a.n_rows - 1);
-          const float4* src = reinterpret_cast<const float4*>(a.X + (size_t)row * a.ldx + 8 * ri.kg);
-          if (i < n_items) {
-            pf[it][0] = src[0];
-            pf[it][1] = src[1];
-          }
-        }
-      }
+      prefetch(b + gridDim.x);  // the next block's records load while this one computes
     } else {
       for (int i = tid; i < n_items; i += RT) {
         const RItem ri = ritem(i, KG);
         float v[8];
         rload(a, s_ix, row0 + ri.row, ri.kg, vec, v);
-        rstore(a, s_sc, s_sh, s_ms, ri.row, row0, ri.kg, v, buf0, s_bad);
+        rstore(a, s_sc, s_sh, s_ms, ri.row, row0, ri.kg, v, buf0, bad);
       }
     }
-    __syncthreads();
-    // ---- hidden layers
-    rhidden<KA0>(m0, A0, w, lane, h, buf0, buf1, s_b);
-    __syncthreads();
-    if constexpr (NH >= 2) {
-      rhidden<RKS>(m1, A1, w, lane, h, buf1, buf0, s_b + 256);
-      __syncthreads();
-    }
-    // ---- output layer: one tile, waves 0..3 take one column block each
-    const uint4* bo = NH == 2 ? buf0 : buf1;
-    if (w < RCB) {
-      const int cb = w;
-      f32x16 acc;
-      bias16(s_b + NH * 256, 0, h, acc);
-      rchain_ll(kso, s_oa + lane, bo + cb * RKS * 64 + lane, acc);
-      activate16(mo.act, mo.thr, acc);
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int u = acc_row(r, h);
-        if (u < a.n_out) s_out[(32 * cb + col) * 33 + u] = acc[r];
-      }
-    }
-    __syncthreads();
-    // ---- epilogue: one thread per row
+  };
+  auto epilogue_fold = [&](int b, int par) {  // block b's rows from the partials (fixed tile order)
     if (tid < RR) {
-      const int row = row0 + tid;
-      const bool bad = s_bad[tid] != 0;
-      s_bad[tid] = 0;
-      const float* o = s_out + tid * 33;
+      const int row = b * RR + tid;
+      const bool bad = s_bad[par * RR + tid] != 0;
+      s_bad[par * RR + tid] = 0;
       if (row < a.n_rows) {
-        if (a.final_norm == 0 && a.n_out == 1) {
-          apply_epilogue(a.epi, [&](int) { return o[0]; }, !bad, row, a.n_rows, a.score, a.valid, a.probs);
-        } else {
-          float mx = -__builtin_inff();
-          for (int u = 0; u < a.n_out; ++u) mx = fmaxf(mx, o[u]);
-          float sum = 0.f;
-          for (int u = 0; u < a.n_out; ++u) sum += (a.final_norm == 1) ? __expf(o[u] - mx) : o[u];
-          float best = -__builtin_inff();
-          int best_u = 1 << 30;
-          for (int u = 0; u < a.n_out; ++u) {
-            float p = (a.final_norm == 1) ? __expf(o[u] - mx) : o[u];
-            if (a.final_norm != 0) p /= sum;
-            if (p > best || (p == best && u < best_u)) { best = p; best_u = u; }
-            if (a.probs) a.probs[(size_t)row * a.n_out + u] = p;
-          }
-          bool ok = !bad && best == best && best_u < a.n_out;
-          float sc = ok ? (a.epi.has_table ? a.epi.table[best_u] : (float)best_u) : __builtin_nanf("");
-          ok = ok && (sc == sc);
-          a.score[row] = ok ? sc : __builtin_nanf("");
-          a.valid[row] = ok ? 1 : 0;
-          if (a.epi.score2) {
-            a.epi.score2[row] = ok ? sc : __builtin_nanf("");
-            a.epi.valid2[row] = ok ? 1 : 0;
+        float z[RFO];
+#pragma unroll
+        for (int o = 0; o < RFO; ++o) {
+          if (o < n_out) {
+            float acc = s_b[NH * 256 + o];
+            for (int t = 0; t < T_last; ++t) acc += s_part[(t * RR + tid) * RFO + o];
+            z[o] = activate(mo.act, acc, mo.thr);
           }
         }
+        repilogue(a, [&](int u) {
+          float r = z[0];
+#pragma unroll
+          for (int o = 1; o < RFO; ++o) r = (u == o) ? z[o] : r;
+          return r;
+        }, bad, row);
       }
     }
-    if constexpr (NH == 1) __syncthreads();  // s_out (buf0) is the next block's staging buffer
+  };
+
+  const bool prof_on = a.prof != nullptr && blockIdx.x == 0 && w == 0;
+  unsigned long long pacc[6] = {0ull, 0ull, 0ull, 0ull, 0ull, 0ull};
+  unsigned long long tp = prof_on ? __builtin_amdgcn_s_memtime() : 0ull;
+  auto stamp = [&](int i) {  // optional phase timers (kbench --mlp-prof): wave 0 of workgroup 0
+    if (prof_on) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      pacc[i] += t - tp;
+      tp = t;
+    }
+  };
+
+  int blk = blockIdx.x;
+  int par = 0;  // block parity: s_bad half of the current block
+  prefetch(blk);
+  if (blk < n_blk) stage(blk, 0);
+  __syncthreads();
+  stamp(4);
+
+  if constexpr (FOLD) {
+    int prev = -1;
+    for (; blk < n_blk; blk += gridDim.x, par ^= 1) {
+      const int nxt = blk + gridDim.x;
+      if constexpr (NH == 2) {
+        rhidden<KA0, false>(L0, A0, lane, h, buf0, buf1, s_b, s_part, s_wo, n_out);
+        stamp(0);
+        if (prev >= 0) epilogue_fold(prev, par ^ 1);
+        __syncthreads();
+        stamp(1);
+        rhidden<RKS, true>(L1, A1, lane, h, buf1, nullptr, s_b + 256, s_part, s_wo, n_out);
+        stamp(2);
+        if (nxt < n_blk) stage(nxt, par ^ 1);
+        __syncthreads();
+        stamp(3);
+        prev = blk;
+      } else {
+        rhidden<KA0, true>(L0, A0, lane, h, buf0, nullptr, s_b, s_part, s_wo, n_out);
+        __syncthreads();
+        stamp(1);
+        epilogue_fold(blk, par);
+        if (nxt < n_blk) stage(nxt, par ^ 1);
+        __syncthreads();
+        stamp(2);
+      }
+      pacc[5] += 1;
+    }
+    if (NH == 2 && prev >= 0) epilogue_fold(prev, par ^ 1);
+  } else {
+    for (; blk < n_blk; blk += gridDim.x, par ^= 1) {
+      const int row0 = blk * RR;
+      rhidden<KA0, false>(L0, A0, lane, h, buf0, buf1, s_b, nullptr, nullptr, 0);
+      __syncthreads();
+      stamp(1);
+      if constexpr (NH >= 2) {
+        rhidden<RKS, false>(L1, A1, lane, h, buf1, buf0, s_b + 256, nullptr, nullptr, 0);
+        __syncthreads();
+      }
+      stamp(2);
+      // output layer: one tile, waves 0..3 take one column block each
+      const uint4* bo = NH == 2 ? buf0 : buf1;
+      if (w < RCB) {
+        const int cb = w;
+        f32x16 acc;
+        bias16(s_b + NH * 256, 0, h, acc);
+        rchain_ll(kso, s_oa + lane, bo + cb * RKS * 64 + lane, acc);
+        activate16(mo.act, mo.thr, acc);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int u = acc_row(r, h);
+          if (u < n_out) s_out[(32 * cb + col) * 33 + u] = acc[r];
+        }
+      }
+      __syncthreads();
+      stamp(3);
+      if (tid < RR) {
+        const int row = row0 + tid;
+        const bool bad = s_bad[par * RR + tid] != 0;
+        s_bad[par * RR + tid] = 0;
+        const float* o = s_out + tid * 33;
+        if (row < a.n_rows) repilogue(a, [&](int u) { return o[u]; }, bad, row);
+      }
+      __syncthreads();  // s_out / buf0 are read above and restaged below
+      const int nxt = blk + gridDim.x;
+      if (nxt < n_blk) stage(nxt, par ^ 1);
+      __syncthreads();
+      stamp(4);
+      pacc[5] += 1;
+    }
+  }
+  if (prof_on && lane == 0) {
+#pragma unroll
+    for (int i = 0; i < 6; ++i) a.prof[i] = pacc[i];
   }
 }
 
+template <bool FOLD>
 constexpr size_t reg_lds_bytes() {
-  return (size_t)(2 * RBUF + RKS * 64) * 16 + 4 * KMAX * 4 + 3 * 256 * 4 + RR * 4;
+  return (size_t)2 * RBUF * 16 + (FOLD ? (size_t)(RWV * RR * RFO + RFO * 256) * 4 : (size_t)RKS * 64 * 16) +
+         4 * KMAX * 4 + 3 * 256 * 4 + 2 * RR * 4;
 }
 
-template <int NH, int KA0, int PF>
+template <int NH, int KA0, int PF, bool FOLD>
 int launch_reg(hipStream_t stream, const MlpArgs& a) {
   const int n_blk = (a.n_rows + RR - 1) / RR;
   dim3 grid(min(n_blk, n_cus()));
-  const size_t lds = reg_lds_bytes();
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(mlp_reg_kernel<NH, KA0, PF>),
+  const size_t lds = reg_lds_bytes<FOLD>();
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(mlp_reg_kernel<NH, KA0, PF, FOLD>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return -5;
-  hipLaunchKernelGGL((mlp_reg_kernel<NH, KA0, PF>), grid, dim3(RT), lds, stream, a);
+  hipLaunchKernelGGL((mlp_reg_kernel<NH, KA0, PF, FOLD>), grid, dim3(RT), lds, stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -7;
+}
+
+template <int NH, bool FOLD>
+int launch_reg_nh(hipStream_t stream, const MlpArgs& a, bool narrow) {
+  return narrow ? launch_reg<NH, 4, 2, FOLD>(stream, a) : launch_reg<NH, 16, 0, FOLD>(stream, a);
 }
 
 }  // namespace
@@ -892,12 +1086,14 @@ PMML_API int pmml_mlp_launch(hipStream_t stream, const MlpArgs* args, int bf16) 
     return -4;
   if (bf16 && a.reg_kernel) {
     // register-weight kernel: the host (runtime/nn_plans.py::reg_kernel_ok) checked every layer's
-    // shape (hidden K, M <= 256, output layer <= 32 units)
+    // shape (hidden K, M <= 256, output layer one 32-unit tile)
     if (a.n_layers < 2 || a.n_layers > 3) return -4;
     const bool vec = a.contiguous && (a.ldx & 3) == 0 && ((uintptr_t)a.X & 15) == 0;
     const bool narrow = a.k0 <= 64 && vec;  // prefetching variant: vector row loads
-    if (a.n_layers == 2) return narrow ? launch_reg<1, 4, 2>(stream, a) : launch_reg<1, 16, 0>(stream, a);
-    return narrow ? launch_reg<2, 4, 2>(stream, a) : launch_reg<2, 16, 0>(stream, a);
+    const bool fold = a.n_out <= RFO;
+    if (a.n_layers == 2)
+      return fold ? launch_reg_nh<1, true>(stream, a, narrow) : launch_reg_nh<1, false>(stream, a, narrow);
+    return fold ? launch_reg_nh<2, true>(stream, a, narrow) : launch_reg_nh<2, false>(stream, a, narrow);
   }
   const int waves = bf16 ? Cfg<true>::WAVES : Cfg<false>::WAVES;
   const int n_tiles = (a.n_rows + 32 * waves - 1) / (32 * waves);

@@ -103,9 +103,14 @@ def main():
         plan.launch(X, s, v)
         torch.cuda.synchronize()
         st, ch, ba, ep, tiles, steps = plan.prof.cpu().tolist()
-        prof = {"ticks_stage_per_tile": st / max(tiles, 1), "ticks_chain_per_step": ch / max(steps, 1),
-                "ticks_barrier_per_step": ba / max(steps, 1), "ticks_epilogue_per_tile": ep / max(tiles, 1),
-                "tiles": tiles, "steps": steps, "total_ticks": st + ch + ba + ep}
+        if getattr(plan, "reg_kernel", 0):  # register-weight kernel: per-block phases (incl. barrier)
+            blocks = max(steps, 1)
+            prof = {"ticks_per_block": {"p0": st / blocks, "p1": ch / blocks, "p2": ba / blocks,
+                                        "p3": ep / blocks, "p4": tiles / blocks}, "blocks": steps}
+        else:
+            prof = {"ticks_stage_per_tile": st / max(tiles, 1), "ticks_chain_per_step": ch / max(steps, 1),
+                    "ticks_barrier_per_step": ba / max(steps, 1), "ticks_epilogue_per_tile": ep / max(tiles, 1),
+                    "tiles": tiles, "steps": steps, "total_ticks": st + ch + ba + ep}
         plan.prof = None
     flops = None
     if args.model == "mlp":
