@@ -509,29 +509,46 @@ __device__ __forceinline__ void fast_batch(uint32_t lds0, int g, int m, uint32_t
     __asm__ volatile("" : "+v"(u[i]));  // separate root reads: ds_read2_b64 pairing costs 8 LDS
                                         // cycles vs 2 x 2 for two ds_read_b64
   }
+  // Each level in three phases — N node reads, N feature reads, N child updates — with scheduling
+  // barriers between them, so the N walks stay interleaved (the scheduler otherwise may serialise
+  // them tree by tree, one LDS round trip at a time: it did so for the fp8-leaf variant).
 #pragma unroll
   for (int d = 0; d + 1 < DEPTH; ++d) {
+    uint2 nd[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) nd[i] = lds_ld2(u[i] + i * TS);
+    __builtin_amdgcn_sched_barrier(0);
+    float x[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) x[i] = lds_ldf(feat_lane + nd[i].y);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int i = 0; i < N; ++i) {
-      const uint2 nd = lds_ld2(u[i] + i * TS);
-      const float x = lds_ldf(feat_lane + nd.y);
-      u[i] = 2u * u[i] + ((x >= __uint_as_float(nd.x)) ? k1 : k0);
+      u[i] = 2u * u[i] + ((x[i] >= __uint_as_float(nd[i].x)) ? k1 : k0);
       __asm__("" : "+v"(u[i]));
     }
   }
+  uint2 nd[N], lv[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    nd[i] = lds_ld2(u[i] + i * TS);
+    if (!LEAF8) {
+      uint32_t ul = u[i] + C;
+      __asm__ volatile("" : "+v"(ul));  // keep the pair read out of a ds_read2_b64 with the node
+      lv[i] = lds_ld2(ul + i * TS);
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  float x[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) x[i] = lds_ldf(feat_lane + (LEAF8 ? (nd[i].y & 0xFFFFu) : nd[i].y));
+  __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int i = 0; i < N; ++i) {
     if (LEAF8) {
-      const uint2 nd = lds_ld2(u[i] + i * TS);
-      const float x = lds_ldf(feat_lane + (nd.y & 0xFFFFu));
-      v[i] = leaf8_select(nd.y, x >= __uint_as_float(nd.x));
+      v[i] = leaf8_select(nd[i].y, x[i] >= __uint_as_float(nd[i].x));
     } else {
-      uint32_t ul = u[i] + C;
-      __asm__ volatile("" : "+v"(ul));  // keep the pair read out of a ds_read2_b64 with the node
-      const uint2 nd = lds_ld2(u[i] + i * TS);
-      const uint2 lv = lds_ld2(ul + i * TS);
-      const float x = lds_ldf(feat_lane + nd.y);
-      v[i] = (x >= __uint_as_float(nd.x)) ? __uint_as_float(lv.y) : __uint_as_float(lv.x);
+      v[i] = (x[i] >= __uint_as_float(nd[i].x)) ? __uint_as_float(lv[i].y) : __uint_as_float(lv[i].x);
     }
   }
 }
