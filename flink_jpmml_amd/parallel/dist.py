@@ -80,7 +80,8 @@ def init_from_env(backend: Optional[str] = None, timeout_s: Optional[float] = No
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
     use_gpu = torch.cuda.is_available()
     if backend is None:
-        backend = "nccl" if use_gpu else "gloo"
+        # FJA_DIST_BACKEND=gloo rehearses N ranks sharing one GPU (RCCL needs one GPU per rank)
+        backend = os.environ.get("FJA_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
     device = torch.device("cuda", local % max(1, torch.cuda.device_count())) if use_gpu else torch.device("cpu")
     if use_gpu:
         torch.cuda.set_device(device)
@@ -271,6 +272,15 @@ def all_gather_scores(score: torch.Tensor, valid: torch.Tensor, ctx: DistContext
         gv = torch.empty(n * ctx.world_size, dtype=valid.dtype, device=valid.device)
     else:
         gs, gv = out
+    if ctx.backend != "nccl":  # gloo: host-staged list all-gather (rehearsal / CPU ranks)
+        for src, dst in ((score, gs), (valid, gv)):
+            parts = [torch.empty(n, dtype=src.dtype) for _ in range(ctx.world_size)]
+            dist.all_gather(parts, src.detach().cpu().contiguous())
+            dst.copy_(torch.cat(parts).to(dst.device))
+        from ..utils.metrics import METRICS
+
+        METRICS.inc("dist.bytes_all_gather", gs.numel() * gs.element_size() + gv.numel() * gv.element_size())
+        return gs, gv, []
     w1 = dist.all_gather_into_tensor(gs, score.contiguous(), async_op=async_op)
     w2 = dist.all_gather_into_tensor(gv, valid.contiguous(), async_op=async_op)
     from ..utils.metrics import METRICS
