@@ -670,7 +670,9 @@ __device__ __forceinline__ void rfinish(const RLayer& L, f32x16& acc, int cb, in
       float p = 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) p = fmaf(acc[r], wo[acc_row(r, h)], p);
-      p += __shfl_xor(p, 32);
+      // lane-half sum without an LDS round trip: v_permlane32_swap (CDNA4)
+      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(p), __float_as_uint(p), false, false);
+      p = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
       if (h == 0) s_part[(L.t * RR + 32 * cb + col) * RFO + o] = p;
     }
   } else {
