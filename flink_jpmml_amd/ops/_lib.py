@@ -137,7 +137,8 @@ class TreeArgs(ctypes.Structure):
                 ("general", c_int), ("variant", c_int), ("epi", Epilogue), ("score", c_void_p),
                 ("valid", c_void_p), ("probs", c_void_p), ("partial", c_void_p), ("blob_nan", c_void_p),
                 ("chunk_trees_nan", c_int), ("pad1", c_int), ("tree_w", c_void_p), ("acc_init", c_void_p),
-                ("feat_map", c_void_p), ("rows_wide", c_int), ("mode", c_int), ("n_stage", c_int), ("pad2", c_int)]
+                ("feat_map", c_void_p), ("rows_wide", c_int), ("mode", c_int), ("n_stage", c_int), ("pad2", c_int),
+                ("prof", c_void_p)]
 
 
 class GenTreeArgs(ctypes.Structure):
@@ -249,7 +250,7 @@ def load(auto_build: bool = True) -> ctypes.CDLL:
         if hasattr(lib, "pmml_mlp_launch"):
             lib.pmml_mlp_launch.argtypes = [c_void_p, ctypes.POINTER(MlpArgs), c_int]
         if hasattr(lib, "pmml_svm_launch"):
-            lib.pmml_svm_launch.argtypes = [c_void_p, ctypes.POINTER(SvmArgs), c_int]
+            lib.pmml_svm_launch.argtypes = [c_void_p, ctypes.POINTER(SvmArgs), c_int, c_int]
         lib.pmml_tree_general_launch.argtypes = [c_void_p, ctypes.POINTER(GenTreeArgs)]
         lib.pmml_tree_general_launch.restype = c_int
         lib.pmml_derive_launch.argtypes = [c_void_p, ctypes.POINTER(DeriveArgs)]

@@ -64,6 +64,7 @@ struct TreeArgs {
   const int* feat_map;          // wide kernel: staged column j -> X column (nullable = identity)
   int rows_wide, mode;          // wide kernel: rows per workgroup (256/128/64), accumulation mode
   int n_stage, pad2;            // wide kernel: staged feature columns
+  unsigned long long* prof;     // nullable: per-wave phase ticks of one workgroup ([16][4], s_memtime)
 };
 constexpr int VAR_NAN_FAST = 4;    // wide kernel: take the fast path even on tiles with missing values
 constexpr int VAR_NAN_PLANES = 8;  // ... via blob_nan + a second feature plane (NaN -> +inf)
@@ -324,6 +325,8 @@ __global__ __launch_bounds__(TB, 2) void tree_perfect_kernel(TreeArgs a) {
 //    classes: the leaf is a packed increment `1 << 8*class`, one integer add per tree).
 enum : int { MODE_SUM = 0, MODE_SLOT = 1, MODE_CLASS = 2, MODE_VOTE8 = 3 };
 constexpr int WIDE_T = 1024;
+constexpr int DYN_B = 8;       // MODE_SUM: trees per dynamically claimed batch
+constexpr int DYN_SLOTS = 16;  // MODE_SUM: per-chunk batch slots (chunk <= DYN_B * DYN_SLOTS trees)
 constexpr int CMAX = 8;  // class slots of the multi-class wide modes
 
 template <int ROWS>
@@ -433,38 +436,48 @@ struct WAcc<MODE_SLOT> {
   __device__ __forceinline__ void finish() { flush(); }
 };
 
-// Missing-aware traversal of group g's trees of one chunk (per-node default-direction bits).
+// Missing-aware walk of one tree record (per-node default-direction bits): the leaf value, or
+// NaN when the tree's prediction is null (a visited split saw a missing value and the tree is
+// flagged null-on-missing).
+template <int DEPTH, bool LEAF8>
+__device__ __forceinline__ float walk_missing(const TreeArgs& a, const char* base, const char* feat_lane,
+                                              bool& null_pred) {
+  constexpr int NI = (1 << DEPTH) - 1;
+  constexpr int NL = 1 << DEPTH;
+  const int dr_off = LEAF8 ? 2 * NI : 2 * NI + NL;
+  uint32_t j = 1u, pz = 0u;
+  float lf = 0.f;
+#pragma unroll
+  for (int d = 0; d < DEPTH; ++d) {
+    const uint2 nd = *reinterpret_cast<const uint2*>(base - 8 + (j << 3));
+    const uint32_t fo = (LEAF8 && d == DEPTH - 1) ? (nd.y & 0xFFFFu) : nd.y;
+    const float x = *reinterpret_cast<const float*>(feat_lane + fo);
+    uint32_t right = (x >= __uint_as_float(nd.x)) ? 1u : 0u;
+    const uint32_t n = j - 1u;
+    const uint32_t w = reinterpret_cast<const uint32_t*>(base)[dr_off + (n >> 5)];
+    const uint32_t isn = (x != x) ? 1u : 0u;
+    right |= isn & (w >> (n & 31u));
+    pz |= isn;
+    if (LEAF8 && d == DEPTH - 1) {
+      lf = leaf8_select(nd.y, right != 0u);
+    } else {
+      j = j + j + right;
+    }
+  }
+  null_pred = pz && null_flag<DEPTH>(base, dr_off);
+  return LEAF8 ? lf : (reinterpret_cast<const float*>(base + NI * 8) - NL)[j];
+}
+
+// Missing-aware traversal of group g's trees of one chunk.
 template <int DEPTH, int ILP, int G, bool LEAF8, int MODE>
 __device__ __forceinline__ void traverse_chunk_g(const TreeArgs& a, const uint32_t* buf, int nt, int g, int t0,
                                                  const char* feat_lane, WAcc<MODE>& acc) {
-  constexpr int NI = (1 << DEPTH) - 1;
-  constexpr int NL = 1 << DEPTH;
   const int rw = a.rec_words;
-  const int dr_off = LEAF8 ? 2 * NI : 2 * NI + NL;
   const int mt = (nt - g + G - 1) / G;
   for (int m = 0; m < mt; ++m) {
-    uint32_t j = 1u, pz = 0u;
-    float lf = 0.f;
-    const char* base = reinterpret_cast<const char*>(buf + (g + G * m) * rw);
-#pragma unroll
-    for (int d = 0; d < DEPTH; ++d) {
-      const uint2 nd = *reinterpret_cast<const uint2*>(base - 8 + (j << 3));
-      const uint32_t fo = (LEAF8 && d == DEPTH - 1) ? (nd.y & 0xFFFFu) : nd.y;
-      const float x = *reinterpret_cast<const float*>(feat_lane + fo);
-      uint32_t right = (x >= __uint_as_float(nd.x)) ? 1u : 0u;
-      const uint32_t n = j - 1u;
-      const uint32_t w = reinterpret_cast<const uint32_t*>(base)[dr_off + (n >> 5)];
-      const uint32_t isn = (x != x) ? 1u : 0u;
-      right |= isn & (w >> (n & 31u));
-      pz |= isn;
-      if (LEAF8 && d == DEPTH - 1) {
-        lf = leaf8_select(nd.y, right != 0u);
-      } else {
-        j = j + j + right;
-      }
-    }
-    const float v = LEAF8 ? lf : (reinterpret_cast<const float*>(base + NI * 8) - NL)[j];
-    if (pz && null_flag<DEPTH>(base, dr_off)) acc.poison();
+    bool nul;
+    const float v = walk_missing<DEPTH, LEAF8>(a, reinterpret_cast<const char*>(buf + (g + G * m) * rw), feat_lane, nul);
+    if (nul) acc.poison();
     else acc.add(a, t0 + g + G * m, v);
   }
 }
@@ -490,6 +503,14 @@ __device__ __forceinline__ uint2 lds_ld2(uint32_t a) {
   return make_uint2(v.x, v.y);
 }
 __device__ __forceinline__ float lds_ldf(uint32_t a) { return *(lds_f_t*)(uintptr_t)a; }
+// s_waitcnt lgkmcnt(0) between scheduling barriers: the traversal's issue slots are its bound
+// (every instruction of a wave, s_waitcnt and s_nop included, takes one), so a phase of N
+// independent LDS reads is drained by ONE wait rather than one lgkmcnt(k) per consumer.
+__device__ __forceinline__ void lds_wait_all() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __builtin_amdgcn_sched_barrier(0);
+}
 
 // N trees of group g starting at its m-th tree, N independent walks interleaved (ILP).
 template <int DEPTH, int N, int G, bool LEAF8>
@@ -517,14 +538,20 @@ __device__ __forceinline__ void fast_batch(uint32_t lds0, int g, int m, uint32_t
     uint2 nd[N];
 #pragma unroll
     for (int i = 0; i < N; ++i) nd[i] = lds_ld2(u[i] + i * TS);
-    __builtin_amdgcn_sched_barrier(0);
+    lds_wait_all();  // one wait for the N node reads instead of one per consumer
     float x[N];
 #pragma unroll
     for (int i = 0; i < N; ++i) x[i] = lds_ldf(feat_lane + nd[i].y);
+    lds_wait_all();
+    // compares into N separate lane masks (v_cmp_e64 -> SGPR pairs), then the child updates: no
+    // VCC reuse, so no hazard s_nop between a compare and the select that reads it
+    uint64_t r[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) r[i] = __builtin_amdgcn_ballot_w64(x[i] >= __uint_as_float(nd[i].x));
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int i = 0; i < N; ++i) {
-      u[i] = 2u * u[i] + ((x[i] >= __uint_as_float(nd[i].x)) ? k1 : k0);
+      u[i] = 2u * u[i] + (__builtin_amdgcn_inverse_ballot_w64(r[i]) ? k1 : k0);
       __asm__("" : "+v"(u[i]));
     }
   }
@@ -538,11 +565,11 @@ __device__ __forceinline__ void fast_batch(uint32_t lds0, int g, int m, uint32_t
       lv[i] = lds_ld2(ul + i * TS);
     }
   }
-  __builtin_amdgcn_sched_barrier(0);
+  lds_wait_all();
   float x[N];
 #pragma unroll
   for (int i = 0; i < N; ++i) x[i] = lds_ldf(feat_lane + (LEAF8 ? (nd[i].y & 0xFFFFu) : nd[i].y));
-  __builtin_amdgcn_sched_barrier(0);
+  lds_wait_all();
 #pragma unroll
   for (int i = 0; i < N; ++i) {
     if (LEAF8) {
@@ -592,13 +619,19 @@ __global__ __launch_bounds__(WIDE_T, 1) void tree_perfect_wide_kernel(TreeArgs a
   constexpr int G = WG::G, RS = WG::RS, PS = WG::PS, T = WIDE_T;
   extern __shared__ __align__(16) uint32_t smem[];
   const int rw = a.rec_words;
-  // LDS: [bad ROWS][flag 4][part G x ROWS][feature plane(s) F x PS][two chunk buffers]. A tile
-  // with missing values and a NaN blob gets two planes (the second NaN -> +inf) and that blob's
-  // chunk size; any other tile one plane and the main blob — chosen per workgroup.
+  // LDS: [bad ROWS][flag 4][claim counters 2 x 4][part P x ROWS][feature plane(s) F x PS][two chunk
+  // buffers], P = max(G, DYN_SLOTS) for MODE_SUM, else G. A tile with missing values and a NaN
+  // blob gets two planes (the second NaN -> +inf) and that blob's chunk size; any other tile one
+  // plane and the main blob — chosen per workgroup.
+  // dynamic batches (MODE_SUM, 256-row tiles: 4 waves per row-set pair; with 8 or 16 waves per
+  // pair a chunk has too few batches to keep them busy — measured 6 % slower at 128 rows)
+  constexpr bool DYN = MODE == MODE_SUM && ROWS == 256;
+  constexpr int NPART = DYN ? DYN_SLOTS : G;
   int* bad = reinterpret_cast<int*>(smem);
   int* any_missing = bad + ROWS;
-  float* part = reinterpret_cast<float*>(bad + ROWS + 4);  // [G][ROWS]
-  float* feat = part + G * ROWS;
+  int* claim = bad + ROWS + 4;                              // [2][4] per rowset pair, per chunk parity
+  float* part = reinterpret_cast<float*>(claim + 8);        // [NPART][ROWS]
+  float* feat = part + NPART * ROWS;
   const int F = a.n_stage;
 
   const int tid = threadIdx.x;
@@ -611,12 +644,20 @@ __global__ __launch_bounds__(WIDE_T, 1) void tree_perfect_wide_kernel(TreeArgs a
   const int tb = split * a.trees_per_split;
   const int te = min(a.n_trees, tb + a.trees_per_split);
 
+  // optional per-wave phase timers of one workgroup (kbench --tree-prof): staging, traversal,
+  // chunk store + barrier, total
+  const bool prof_on = a.prof != nullptr && blockIdx.x == gridDim.x / 2 && blockIdx.y == 0;
+  const unsigned long long tstart = prof_on ? __builtin_amdgcn_s_memtime() : 0ull;
   PF4_DECL
   int n16 = (tb < te) ? (min(a.chunk_trees, te - tb) * rw) >> 2 : 0;
   PF4_LOAD(n16 > 0 ? a.blob + (size_t)tb * rw : a.blob, n16, T)  // speculative: main blob
 
   if (tid == 0) *any_missing = 0;
   if (tid < ROWS) bad[tid] = 0;
+  if (tid < 8) claim[tid] = 0;
+  if constexpr (DYN) {
+    for (int e = tid; e < NPART * ROWS; e += T) part[e] = 0.f;
+  }
   __syncthreads();
   {
     const int total = ROWS * F;
@@ -666,6 +707,8 @@ __global__ __launch_bounds__(WIDE_T, 1) void tree_perfect_wide_kernel(TreeArgs a
   const bool missing = has_missing && (a.variant & VAR_NAN_FAST) == 0;
   WAcc<MODE> acc;
   const char* feat_lane = reinterpret_cast<const char*>(feat + r_local);
+  unsigned long long tp0 = 0, tp1 = 0, tp2 = 0, tq = 0;
+  if (prof_on) tq = __builtin_amdgcn_s_memtime(), tp0 = tq - tstart;
   int c = 0;
   for (int t0 = tb; t0 < te; t0 += chunk, ++c) {
     const int nt = min(chunk, te - t0);
@@ -674,24 +717,95 @@ __global__ __launch_bounds__(WIDE_T, 1) void tree_perfect_wide_kernel(TreeArgs a
     const int t1 = t0 + chunk;
     n16 = (t1 < te) ? (min(chunk, te - t1) * rw) >> 2 : 0;
     PF4_LOAD(n16 > 0 ? blob + (size_t)t1 * rw : blob, n16, T)
-    if (missing) {
+    if constexpr (DYN) {
+      // Dynamic batches. The waves that share a row-set pair (one per tree group, all on one
+      // SIMD) claim DYN_B-tree batches of the chunk from an LDS counter instead of walking a fixed
+      // share each: the SIMD's issue arbitration favours older waves, so with a static split the
+      // youngest wave's trees were the critical path and the others idled at the chunk barrier
+      // (profiles/r2_tree_variants.md). A batch's sum (its trees added in order, from 0) goes to
+      // its slot, which only its claimer touches in this chunk and which accumulates over chunks
+      // in chunk order: the row sum (slots added in slot order) is deterministic whichever wave
+      // walked a batch, and the same on the per-node missing path and the fast paths. Slots are
+      // indexed by the batch's position in the split (mod DYN_SLOTS, chunks are whole batches),
+      // so the NaN blob's smaller chunks group the trees exactly as the main blob's.
+      int* ctr = claim + (c & 1) * 4 + ((tid >> 6) % (RS / 2 > 0 ? RS / 2 : 1));
+      if (tid < 4) claim[((c + 1) & 1) * 4 + tid] = 0;  // next chunk's counters (free since the last barrier)
+      const uint32_t lds0 = lds_addr(cur);
+      const uint32_t fl = lds_addr(feat + r_local);
+      const int nb = (nt + DYN_B - 1) / DYN_B;
+      for (;;) {
+        int b = 0;
+        if (lane == 0) b = atomicAdd(ctr, 1);
+        b = __builtin_amdgcn_readfirstlane(b);
+        if (b >= nb) break;
+        const int m = b * DYN_B;
+        float sum = 0.f;
+        if (missing) {
+          const int me = min(m + DYN_B, nt);
+          for (int t = m; t < me; ++t) {
+            bool nul;
+            const float v = walk_missing<DEPTH, LEAF8>(a, reinterpret_cast<const char*>(cur + t * rw), feat_lane, nul);
+            sum += nul ? __builtin_nanf("") : v;
+          }
+        } else if (m + DYN_B <= nt) {
+          float v[DYN_B];
+          fast_batch<DEPTH, DYN_B, 1, LEAF8>(lds0, 0, m, fl, v);
+#pragma unroll
+          for (int i = 0; i < DYN_B; ++i) sum += v[i];
+        } else {
+          int mm = m;
+          if (mm + 4 <= nt) {
+            float v[4];
+            fast_batch<DEPTH, 4, 1, LEAF8>(lds0, 0, mm, fl, v);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) sum += v[i];
+            mm += 4;
+          }
+          if (mm + 2 <= nt) {
+            float v[2];
+            fast_batch<DEPTH, 2, 1, LEAF8>(lds0, 0, mm, fl, v);
+            sum += v[0];
+            sum += v[1];
+            mm += 2;
+          }
+          if (mm < nt) {
+            float v[1];
+            fast_batch<DEPTH, 1, 1, LEAF8>(lds0, 0, mm, fl, v);
+            sum += v[0];
+          }
+        }
+        part[(((t0 - tb) / DYN_B + b) % DYN_SLOTS) * ROWS + r_local] += sum;
+      }
+    } else if (missing) {
       traverse_chunk_g<DEPTH, ILP, G, LEAF8, MODE>(a, cur, nt, g, t0, feat_lane, acc);
     } else {
       traverse_fast_g<DEPTH, ILP, G, LEAF8, MODE>(a, cur, nt, g, t0, lds_addr(feat + r_local), acc);
     }
+    unsigned long long tm = 0;
+    if (prof_on) tm = __builtin_amdgcn_s_memtime(), tp1 += tm - tq;
     PF4_STORE(nxt, n16, T)
     __syncthreads();
+    if (prof_on) tq = __builtin_amdgcn_s_memtime(), tp2 += tq - tm;
   }
   acc.finish();
+  if (prof_on && lane == 0) {
+    unsigned long long* pw = a.prof + (tid >> 6) * 4;
+    pw[0] = tp0;
+    pw[1] = tp1;
+    pw[2] = tp2;
+    pw[3] = __builtin_amdgcn_s_memtime() - tstart;
+  }
   if (acc.poisoned()) bad[r_local] = 1;  // a null tree invalidates a multi-class row
   const int row = row0 + r_local;
   if constexpr (MODE == MODE_SUM) {
-    part[g * ROWS + r_local] = acc.s;
-    __syncthreads();
+    if constexpr (!DYN) {
+      part[g * ROWS + r_local] = acc.s;
+      __syncthreads();
+    }  // DYN: the batch slots are complete since the last chunk barrier
     if (g == 0) {
       float sum = part[r_local];
 #pragma unroll
-      for (int q = 1; q < G; ++q) sum += part[q * ROWS + r_local];
+      for (int q = 1; q < NPART; ++q) sum += part[q * ROWS + r_local];
       bool row_ok = bad[r_local] == 0;
       if (a.row_valid_in && row < a.n_rows) row_ok = row_ok && a.row_valid_in[row];
       if (row < a.n_rows) {
@@ -784,7 +898,12 @@ int launch_perfect(hipStream_t st, const TreeArgs& a, dim3 grid, size_t lds) {
     const bool leaf8 = base == 2;
     const int rows = a.rows_wide;
     const int G = WIDE_T / rows;
-    const size_t head = (size_t)(rows + 4) * 4 + (size_t)G * rows * 4;
+    const bool dyn = a.mode == MODE_SUM && rows == 256;  // kernel's DYN / NPART
+    const int npart = dyn ? DYN_SLOTS : G;
+    const size_t head = (size_t)(rows + 4 + 8) * 4 + (size_t)npart * rows * 4;
+    if (dyn &&
+        (a.chunk_trees > DYN_B * DYN_SLOTS || (a.blob_nan && a.chunk_trees_nan > DYN_B * DYN_SLOTS)))
+      return -14;  // more batches per chunk than slots
     const size_t plane = (size_t)a.n_stage * rows * 4;
     size_t lds_w = head + plane + 2 * (size_t)a.chunk_trees * a.rec_words * 4;
     if ((size_t)a.chunk_trees * a.rec_words > (size_t)WIDE_T * 4 * 4) return -9;

@@ -355,7 +355,7 @@ class SvmPlan(DevicePlan):
     _KERNELS = {"linear": 0, "polynomial": 1, "radialBasis": 2, "sigmoid": 3}
     _STATE = DevicePlan._STATE + ("in_index", "sv", "sv_norm", "coef", "intercept", "thr", "tgt", "alt", "n_in",
                                   "n_sv", "n_machines", "kernel_code", "classification", "gamma", "coef0", "degree",
-                                  "max_wins", "n_classes", "table", "fmax")
+                                  "max_wins", "n_classes", "table", "fmax", "n_svp")
 
     def __init__(self, compiled, device):
         from ..models.svm import SvmEvaluator
@@ -384,9 +384,12 @@ class SvmPlan(DevicePlan):
             A = ev.A
             kind = sm.kernel.kind
         nsv = S.shape[0]
-        Sp = np.zeros((max(1, nsv), self.fmax), np.float32)
+        # >= 32 support vectors: the matrix-core kernel, support vectors padded to whole 32-vector
+        # tiles (zero coefficients); fewer: the VALU kernel
+        self.n_svp = -(-nsv // 32) * 32 if nsv >= 32 else 0
+        Sp = np.zeros((max(1, nsv, self.n_svp), self.fmax), np.float32)
         Sp[:nsv, :F] = S
-        Ap = np.zeros((max(1, nsv), self.MMAX), np.float32)
+        Ap = np.zeros((max(1, nsv, self.n_svp), self.MMAX), np.float32)
         Ap[:nsv, :M] = A
         self.n_sv, self.n_in, self.n_machines = nsv, F, M
         self.sv = self._t(Sp)
@@ -440,7 +443,8 @@ class SvmPlan(DevicePlan):
         a.epi = _epilogue(mode=EPI_AFFINE, table=self.table)
         a.epi.score2, a.epi.valid2 = _addr(score2), _addr(valid2)
         a.score, a.valid, a.decision = _addr(score), _addr(valid), ptr(decision)
-        check(self.lib.pmml_svm_launch(stream_handle(stream), ctypes.byref(a), self.fmax), "svm kernel")
+        check(self.lib.pmml_svm_launch(stream_handle(stream), ctypes.byref(a), self.fmax,
+                                       getattr(self, "n_svp", 0)), "svm kernel")
 
 
 class SvmGemmPlan(DevicePlan):

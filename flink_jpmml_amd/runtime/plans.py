@@ -883,6 +883,7 @@ def _perfect_pack(trees: List[BinaryTree], weights: List[float], P: int, D: int,
 
 
 VAR_NAN_FAST, VAR_NAN_PLANES = 4, 8  # mirrors csrc/tree_common.h
+DYN_B, DYN_SLOTS = 8, 16  # csrc: MODE_SUM trees per claimed batch, batch slots per chunk
 
 
 def _nan_planes(blob: np.ndarray, D: int, F: int, stride: int = TB) -> np.ndarray:
@@ -1139,12 +1140,15 @@ class TreePlan(DevicePlan):
             self.variant |= nan_flags
             self.rec_words = rec
             wide = self.variant & 3 in (1, 2)
+            dyn = False
             if wide:
                 # one 1024-thread workgroup per row tile: [G][rows] partials + feature plane(s) + two
                 # chunk buffers; tiles with missing values use the NaN blob with two planes
                 G = 1024 // self.rows_wide
                 plane = Fs * stride * 4
-                fixed = plane + (self.rows_wide + 4) * 4 + G * self.rows_wide * 4
+                dyn = self.mode == 0 and self.rows_wide == 256  # MODE_SUM batch slots (csrc DYN / NPART)
+                npart = DYN_SLOTS if dyn else G
+                fixed = plane + (self.rows_wide + 4 + 8) * 4 + npart * self.rows_wide * 4
                 per_chunk = min((156 * 1024 - fixed) // 2, 64 * 1024)
             else:
                 plane = F * TB * 4
@@ -1153,12 +1157,13 @@ class TreePlan(DevicePlan):
                 per_chunk = min(budget // 2, 32 * 1024)  # register prefetch holds <= 32 KiB per chunk
             if rec * 4 > per_chunk:
                 raise NotLowerable(f"depth-{depth} tree record ({rec * 4} B) exceeds the chunk buffer")
-            self.chunk_trees = self._chunk(per_chunk // (rec * 4), wide, max_chunk_trees)
+            cap = DYN_B * DYN_SLOTS if wide and dyn else 0  # dynamic batches: one slot per batch
+            self.chunk_trees = self._chunk(per_chunk // (rec * 4), wide, max_chunk_trees, cap)
             self.blob_nan, self.chunk_trees_nan = None, 0
             if blob_nan is not None:
                 per_nan = min((156 * 1024 - fixed - plane) // 2, 64 * 1024)
                 if rec * 4 <= per_nan:
-                    self.chunk_trees_nan = self._chunk(per_nan // (rec * 4), wide, max_chunk_trees)
+                    self.chunk_trees_nan = self._chunk(per_nan // (rec * 4), wide, max_chunk_trees, cap)
                     self.blob_nan = self._t(blob_nan.reshape(-1).view(np.int32))
                 else:
                     self.variant &= ~(VAR_NAN_FAST | VAR_NAN_PLANES)
@@ -1211,14 +1216,17 @@ class TreePlan(DevicePlan):
             return 3
         return 2
 
-    def _chunk(self, fit: int, wide: bool, cap: int) -> int:
+    def _chunk(self, fit: int, wide: bool, cap: int, slot_cap: int = 0) -> int:
         """Trees per LDS chunk. Wide kernel: whole ILP batches per tree group (G groups x 8-wide
         walks) — every group gets the same count (no barrier imbalance) and no latency-bound short
-        tail batches (measured: 64 > 79 > 57 trees at depth 6)."""
+        tail batches (measured: 64 > 79 > 57 trees at depth 6). MODE_SUM claims 8-tree batches
+        dynamically: whole batches, at most ``slot_cap`` trees (one LDS slot per batch)."""
         c = int(max(1, min(self.n_trees, fit)))
+        if slot_cap:
+            c = min(c, slot_cap)
         G = 1024 // getattr(self, "rows_wide", 256)
         if wide and c < self.n_trees:
-            q = 8 * G if c >= 16 * G else 2 * G
+            q = DYN_B if slot_cap else (8 * G if c >= 16 * G else 2 * G)
             c = max(q, c // q * q) if c >= q else c
         return min(c, cap) if cap > 0 else c
 
@@ -1258,6 +1266,7 @@ class TreePlan(DevicePlan):
             a.feat_map = ptr(getattr(self, "feat_map", None))
             a.rows_wide, a.mode = getattr(self, "rows_wide", TB), getattr(self, "mode", 0)
             a.n_stage = getattr(self, "n_stage", self.n_features)
+            a.prof = ptr(getattr(self, "prof", None))  # kbench --tree-prof phase timers (nullable)
             a.epi = _epilogue(table=self.table, write_probs=with_probs, **self.epi_args)
             cache[with_probs] = a
         b = TreeArgs()

@@ -27,6 +27,7 @@ def main():
     p.add_argument("--mlp-prof", action="store_true", help="MLP: per-phase s_memtime ticks of workgroup 0")
     p.add_argument("--clusters", type=int, default=256)
     p.add_argument("--nan-mode", default="auto")
+    p.add_argument("--tree-prof", action="store_true", help="tree: per-wave phase ticks of one workgroup")
     p.add_argument("--max-chunk-trees", type=int, default=0)
     p.add_argument("--precision", default="fp32", choices=["fp32", "bf16", "fp8"])
     p.add_argument("--hidden", default="256,256", help="mlp hidden widths")
@@ -112,6 +113,16 @@ def main():
                     "ticks_barrier_per_step": ba / max(steps, 1), "ticks_epilogue_per_tile": ep / max(tiles, 1),
                     "tiles": tiles, "steps": steps, "total_ticks": st + ch + ba + ep}
         plan.prof = None
+    if args.tree_prof and args.model.startswith(("gbdt", "rf")):
+        plan.prof = torch.zeros(64, dtype=torch.int64, device="cuda")
+        plan._args = {}
+        plan.launch(X, s, v)
+        torch.cuda.synchronize()
+        w = plan.prof.cpu().view(16, 4).tolist()
+        prof = {"per_wave_stage_trav_barrier_total": w,
+                "mean": [sum(r[k] for r in w) / 16 for k in range(4)]}
+        plan.prof = None
+        plan._args = {}
     flops = None
     if args.model == "mlp":
         dims = [F] + [int(x) for x in args.hidden.split(",")] + [1]
