@@ -100,12 +100,14 @@ def _mining_schema(out: io.StringIO, F: int, target: Optional[str], indent: str 
 def gbdt_pmml(n_trees: int = 1000, depth: int = 6, n_features: int = 32, seed: int = 0,
               objective: str = "regression", p_split: float = 0.9, learning_rate: float = 0.1,
               base_score: float = 0.5, float_casts: bool = False, missing_strategy: str = "defaultChild",
-              n_classes: int = 3) -> str:
+              n_classes: int = 3, scaled: bool = False) -> str:
     """XGBoost-style GBDT PMML: regression, ``binary`` (binary:logistic chain) or ``multiclass``
     (multi:softprob — ``n_classes`` chained ensembles of ``n_trees`` each + a softmax
     RegressionModel over their ``xgbValue(k)`` outputs). ``float_casts`` adds the
     ``float(fj)`` ``LocalTransformations`` casts that pipeline exporters (sklearn2pmml) emit, with
-    every split on the cast field."""
+    every split on the cast field. ``scaled`` splits on monotone derived fields ``d(fj)`` instead:
+    StandardScaler-style ``(x - mu) / sd``, increasing and clamped ``NormContinuous``, and a
+    decreasing ``(c - x) * k`` (the sklearn2pmml preprocessing shapes)."""
     rng = np.random.default_rng(seed)
     thresholds = np.sort(rng.standard_normal((n_features, 64)).astype(np.float32), axis=1)
     out = io.StringIO()
@@ -114,12 +116,33 @@ def gbdt_pmml(n_trees: int = 1000, depth: int = 6, n_features: int = 32, seed: i
     multi = objective == "multiclass"
     cats = [str(k) for k in range(n_classes)] if multi else ["0", "1"]
     _data_dictionary(out, n_features, "y", "integer" if binary or multi else "double", cats if binary or multi else None)
-    fmt = "float(f{})" if float_casts else "f{}"
+    fmt = "d(f{})" if scaled else ("float(f{})" if float_casts else "f{}")
 
     def leaf() -> str:
         return _fnum(learning_rate * rng.standard_normal())
 
+    def scalers(indent: str) -> None:
+        out.write(f'{indent}<LocalTransformations>\n')
+        for j in range(n_features):
+            kind = j % 4
+            if kind == 0:
+                ex = (f'<Apply function="/"><Apply function="-"><FieldRef field="f{j}"/><Constant>{0.1 * j:.3f}'
+                      f'</Constant></Apply><Constant>1.25</Constant></Apply>')
+            elif kind == 1:
+                ex = (f'<NormContinuous field="f{j}"><LinearNorm orig="-2" norm="-1.5"/><LinearNorm orig="0" '
+                      f'norm="0.25"/><LinearNorm orig="1.5" norm="1"/></NormContinuous>')
+            elif kind == 2:
+                ex = f'<Apply function="*"><Apply function="-"><Constant>0.5</Constant><FieldRef field="f{j}"/></Apply><Constant>0.8</Constant></Apply>'
+            else:
+                ex = (f'<NormContinuous field="f{j}" outliers="asExtremeValues"><LinearNorm orig="-1" norm="-1"/>'
+                      f'<LinearNorm orig="1" norm="1"/></NormContinuous>')
+            out.write(f'{indent} <DerivedField name="d(f{j})" optype="continuous" dataType="double">{ex}</DerivedField>\n')
+        out.write(f'{indent}</LocalTransformations>\n')
+
     def casts(indent: str) -> None:
+        if scaled:
+            scalers(indent)
+            return
         if not float_casts:
             return
         out.write(f'{indent}<LocalTransformations>\n')

@@ -286,6 +286,8 @@ def lower_binary_tree(ev: TreeEvaluator, field_index: Dict[str, int]) -> BinaryT
             leafp.append(np.zeros(len(ev.categories)))
         return len(feats) - 1
 
+    folds = getattr(field_index, "folds", None) or {}  # runtime/derive.py: monotone derived fields
+    folded: Dict[str, List[int]] = {}
     max_depth = 0
     stack = [(tm.root, new_node(), 0)]
     while stack:
@@ -347,6 +349,8 @@ def lower_binary_tree(ev: TreeEvaluator, field_index: Dict[str, int]) -> BinaryT
             if len(forms) > 1:
                 raise NotBinary("'none' strategy mixing True and complement second children")
             go_left = False
+        if split_field in folds:
+            folded.setdefault(split_field, []).append(k)
         feats[k] = field_index[split_field]
         thr[k] = split_t
         ops[k] = split_op
@@ -355,10 +359,22 @@ def lower_binary_tree(ev: TreeEvaluator, field_index: Dict[str, int]) -> BinaryT
         lefts[k], rights[k] = la, lb
         stack.append((a, la, depth + 1))
         stack.append((b, lb, depth + 1))
+    thr_a, ops_a = np.array(thr, dtype=np.float64), np.array(ops, dtype=np.int8)
+    if folded:  # splits on a monotone derived field -> splits on its source input
+        from ..runtime.derive import fold_splits
+
+        for name, ks in folded.items():
+            _, f, memo = folds[name]
+            for k in ks:
+                hit = memo.get((int(ops_a[k]), float(thr_a[k])))
+                if hit is None:  # not pre-resolved (runtime/derive.py::_resolve_folds)
+                    o, t = fold_splits(f, ops_a[k:k + 1], thr_a[k:k + 1])
+                    hit = memo[(int(ops_a[k]), float(thr_a[k]))] = (int(o[0]), float(t[0]))
+                ops_a[k], thr_a[k] = hit
     return BinaryTree(
         feature=np.array(feats, dtype=np.int32),
-        threshold=np.array(thr, dtype=np.float64),
-        op=np.array(ops, dtype=np.int8),
+        threshold=thr_a,
+        op=ops_a,
         default_left=np.array(dleft, dtype=bool),
         left=np.array(lefts, dtype=np.int32),
         right=np.array(rights, dtype=np.int32),

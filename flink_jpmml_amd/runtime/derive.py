@@ -10,6 +10,13 @@ forms (:func:`plan_field_layout`):
 * **aliases** — a derived field that is a pure numeric cast of an input (``float(x)`` /
   ``double(x)`` ``FieldRef``, the XGBoost / LightGBM / sklearn2pmml idiom) is resolved to the
   input's column: the tree kernel reads the raw matrix, no extra pass;
+* **folds** (tree ensembles) — a derived field that is a *monotone* function of one input
+  (``(x - mu) / sd``, ``(c - x) * k``, ``NormContinuous`` with ``asIs`` / ``asExtremeValues``
+  outliers, and chains of these) and that the model reads only as a tree split field: every
+  split ``f(x) OP t`` is rewritten at lowering time into ``x < C`` or ``x >= C`` on the raw
+  input, with ``C`` the fp32 cut found by bisecting the fp32 line against the float64 oracle's
+  own evaluation of ``f`` (:func:`fold_splits`) — exact for every fp32 input, and the derive pass
+  disappears (the transform is fused into the thresholds, zero device work);
 * **program** — anything else becomes a postfix program over a per-row fp64 stack, run by
   ``ops/csrc/derive.hip`` in one memory-bound pass that also applies the MiningField
   preparation; it writes the ``[rows, columns the model reads]`` matrix that the model kernel
@@ -319,15 +326,190 @@ def _alias_source(name: str, defs: Dict[str, ir.DerivedField], inputs: Dict[str,
     return name if name in inputs else None
 
 
+def _monotone_expr(ex: ir.Expression, defs: Dict[str, ir.DerivedField], inputs: Dict[str, int], schema,
+                   seen: set) -> Optional[str]:
+    """Input field ``ex`` is a monotone (either direction), missing-preserving function of, or
+    None. Accepted: casts, ``+`` / ``-`` / ``*`` with a constant, ``/`` by a non-zero constant,
+    NormContinuous with strictly monotone norms and asIs / asExtremeValues outliers."""
+    if isinstance(ex, ir.FieldRef):
+        if ex.map_missing_to is not None or schema.is_string(ex.field):
+            return None
+        return _monotone_source(ex.field, defs, inputs, schema, seen)
+    if isinstance(ex, ir.NormContinuous):
+        norm = np.array([ln.norm for ln in ex.norms], dtype=np.float64)
+        orig = np.array([ln.orig for ln in ex.norms], dtype=np.float64)
+        if (ex.map_missing_to is not None or ex.outliers == "asMissingValues" or len(norm) < 2
+                or not (np.diff(orig) > 0).all() or not ((np.diff(norm) > 0).all() or (np.diff(norm) < 0).all())
+                or schema.is_string(ex.field)):
+            return None
+        return _monotone_source(ex.field, defs, inputs, schema, seen)
+    if isinstance(ex, ir.Apply):
+        if ex.map_missing_to is not None or ex.default_value is not None or len(ex.args) != 2 \
+                or ex.function not in ("+", "-", "*", "/"):
+            return None
+        consts = [isinstance(a, ir.Constant) for a in ex.args]
+        if consts.count(True) != 1:
+            return None
+        c = ex.args[consts.index(True)]
+        try:
+            cv = float(c.value)
+        except (TypeError, ValueError):
+            return None
+        if c.missing or not math.isfinite(cv):
+            return None
+        if ex.function == "*" and cv == 0.0:
+            return None
+        if ex.function == "/" and (consts[0] or cv == 0.0):  # c / x is not monotone over the line
+            return None
+        return _monotone_expr(ex.args[consts.index(False)], defs, inputs, schema, seen)
+    return None
+
+
+def _monotone_source(name: str, defs: Dict[str, ir.DerivedField], inputs: Dict[str, int], schema,
+                     seen: Optional[set] = None) -> Optional[str]:
+    if name in inputs:
+        return name
+    seen = set() if seen is None else seen
+    if name not in defs or name in seen:
+        return None
+    seen.add(name)
+    d = defs[name]
+    if d.data_type not in (None, "float", "double", "integer"):
+        return None
+    return _monotone_expr(d.expression, defs, inputs, schema, seen)
+
+
+def _non_split_refs(model: ir.Model) -> set:
+    """Fields read anywhere but in a TreeModel node predicate (segment predicates, non-tree
+    models): a derived field read there cannot be folded into split thresholds."""
+    out: set = set()
+
+    def walk(m: ir.Model) -> None:
+        if isinstance(m, ir.TreeModel):
+            return
+        if isinstance(m, ir.MiningModel):
+            for sg in m.segments:
+                _pred_fields(sg.predicate, out.add)
+                walk(sg.model)
+            return
+        out.update(referenced_fields(m))
+
+    walk(model)
+    return out
+
+
+class FoldIndex(dict):
+    """``field_index`` whose folded derived names map to their source input's column; ``folds``
+    holds, per folded name, ``(source, f)`` with ``f`` the float64 oracle evaluation of the
+    derived value from source values (:func:`fold_splits` rewrites the thresholds)."""
+
+    def __init__(self, base: Dict[str, int], folds: Dict[str, tuple]):
+        super().__init__(base)
+        self.folds = folds
+
+
+def _fold_fn(compiled, name: str, source: str, defs: Dict[str, ir.DerivedField]):
+    from ..pmml.fields import Columns
+
+    def f(xs: np.ndarray) -> np.ndarray:
+        cols = Columns(compiled.schema, len(xs), {source: np.asarray(xs, dtype=np.float64)}, defs)
+        return cols.get(name)
+
+    return f
+
+
+_F32_MAX_KEY = int(np.array(np.finfo(np.float32).max, np.float32).view(np.int32))
+
+
+def _f32_from_key(k: np.ndarray) -> np.ndarray:
+    k = np.asarray(k, dtype=np.int64)
+    bits = np.where(k < 0, (-k) | 0x80000000, k).astype(np.uint32)
+    return bits.view(np.float32).astype(np.float64)
+
+
+def fold_splits(f, ops: np.ndarray, ts: np.ndarray) -> tuple:
+    """Rewrite splits ``f(x) OP t`` (OP codes of models/tree.py) on a monotone ``f`` into
+    ``x < C`` (OP_LT) or ``x >= C`` (OP_GE) with fp32 ``C``, exact for every finite fp32 x: ``P(x)
+    = f(x) OP t`` is monotone in x, so the cut is found by bisecting the ordered fp32 keys (33
+    steps) with the oracle's ``f`` — vectorised over all splits of one field."""
+    from ..models.tree import OP_GE, OP_GT, OP_LE, OP_LT
+
+    ops = np.asarray(ops)
+    ts = np.asarray(ts, dtype=np.float64)
+
+    def P(x: np.ndarray) -> np.ndarray:
+        y = f(x)
+        return np.select([ops == OP_LT, ops == OP_LE, ops == OP_GT, ops == OP_GE],
+                         [y < ts, y <= ts, y > ts, y >= ts], False)
+
+    n = len(ts)
+    lo = np.full(n, -_F32_MAX_KEY, np.int64)
+    hi = np.full(n, _F32_MAX_KEY, np.int64)
+    p_lo, p_hi = P(_f32_from_key(lo)), P(_f32_from_key(hi))
+    rising = ~p_lo & p_hi   # P(x) <=> x >= C
+    falling = p_lo & ~p_hi  # P(x) <=> x < C
+    active = rising | falling
+    for _ in range(34):
+        if not active.any() or not (hi - lo > 1)[active].any():
+            break
+        mid = lo + (hi - lo) // 2
+        pm = P(_f32_from_key(mid))
+        below = np.where(rising, ~pm, pm)  # mid is still on lo's side of the cut
+        lo = np.where(active & below & (hi - lo > 1), mid, lo)
+        hi = np.where(active & ~below & (hi - lo > 1), mid, hi)
+    cut = _f32_from_key(hi)
+    new_ops = np.where(rising, OP_GE, OP_LT).astype(ops.dtype)
+    # constant predicates: always true -> x < +inf, always false -> x < -inf
+    new_t = np.where(active, cut, np.where(p_lo, np.inf, -np.inf))
+    return new_ops, new_t
+
+
+def _resolve_folds(model: ir.Model, folds: Dict[str, tuple]) -> None:
+    """Fold every distinct ``(operator, value)`` split the model's trees make on each folded field
+    in one vectorised bisection per field; ``folds[name]`` becomes ``(source, f, memo)`` with
+    ``memo[(op, t)] = (op', t')`` for the tree lowering (exporters reuse split values heavily)."""
+    from ..models.tree import _OPS
+
+    want: Dict[str, Dict[tuple, None]] = {n: {} for n in folds}
+
+    def walk(m: ir.Model) -> None:
+        if isinstance(m, ir.TreeModel):
+            stack = [m.root]
+            while stack:
+                nd = stack.pop()
+                stack.extend(nd.children)
+                p = nd.predicate
+                if isinstance(p, ir.SimplePredicate) and p.field in want and p.operator in _OPS:
+                    try:
+                        want[p.field][(_OPS[p.operator], float(p.value))] = None
+                    except (TypeError, ValueError):
+                        pass
+        elif isinstance(m, ir.MiningModel):
+            for sg in m.segments:
+                walk(sg.model)
+
+    walk(model)
+    for name, (src, f) in list(folds.items()):
+        keys = list(want[name])
+        memo = {}
+        if keys:
+            ops = np.array([k[0] for k in keys], np.int8)
+            ts = np.array([k[1] for k in keys], np.float64)
+            new_ops, new_ts = fold_splits(f, ops, ts)
+            memo = {k: (int(o), float(t)) for k, o, t in zip(keys, new_ops, new_ts)}
+        folds[name] = (src, f, memo)
+
+
 @dataclass
 class FieldLayout:
     columns: List[str]                 # the model kernel's input columns, in order
     field_index: Dict[str, int]        # every name the model may reference -> kernel column
     program: Optional[DerivedProgram]  # None: the kernel reads the raw input matrix
     evaluator: Optional[object] = None  # replaces the model's evaluator behind the view (design.py)
+    folds: Optional[Dict[str, tuple]] = None  # folded derived names (tree split thresholds)
 
 
-def plan_field_layout(compiled, allow_alias: bool = True) -> FieldLayout:
+def plan_field_layout(compiled, allow_alias: bool = True, allow_fold: bool = False) -> FieldLayout:
     from ..models.tree import membership_fields
 
     active = list(compiled.active_fields)
@@ -344,10 +526,24 @@ def plan_field_layout(compiled, allow_alias: bool = True) -> FieldLayout:
     schema = compiled.schema
     if allow_alias:
         alias = {n: _alias_source(n, defs, index, schema) for n in needed}
-        if all(v is not None for v in alias.values()):
+        folds: Dict[str, tuple] = {}
+        if allow_fold and not all(v is not None for v in alias.values()):
+            model = _model_of(compiled)
+            blocked = _non_split_refs(model)
+            for m in members.values():  # membership columns are computed from their field
+                _expr_fields(m.expression, blocked.add)
+            for n in needed:
+                if alias[n] is None and n not in blocked and n not in members:
+                    src = _monotone_source(n, defs, index, schema)
+                    if src is not None:
+                        folds[n] = (src, _fold_fn(compiled, n, src, defs))
+        if folds:
+            _resolve_folds(_model_of(compiled), folds)
+        if all(v is not None or n in folds for n, v in alias.items()):
             fi = dict(index)
-            fi.update({n: index[src] for n, src in alias.items()})
-            return FieldLayout(active, fi, None)
+            fi.update({n: index[src] for n, src in alias.items() if src is not None})
+            fi.update({n: index[fd[0]] for n, fd in folds.items()})
+            return FieldLayout(active, fi, None, folds=folds or None)
     return build_program_layout(compiled, defs, refs)
 
 
@@ -528,7 +724,8 @@ class FieldView:
     def __init__(self, compiled, layout: FieldLayout, prepared: bool):
         self._c = compiled
         self.active_fields = list(layout.columns)
-        self.field_index = dict(layout.field_index)
+        self.field_index = FoldIndex(layout.field_index, layout.folds) if layout.folds else dict(layout.field_index)
+        self.folds = layout.folds
         self.prepared_inputs = prepared
         self.mining_fields = {} if prepared else dict(compiled.mining_fields)
         if layout.evaluator is not None:

@@ -46,6 +46,8 @@ class GeneralTree:
 
 
 def lower_general_tree(ev: TreeEvaluator, field_index: Dict[str, int]) -> GeneralTree:
+    if getattr(field_index, "folds", None):
+        raise NotLowerable("folded derived fields need the binary tree lowering")
     tm = ev.tree
     if tm.missing_value_strategy not in STRATEGY:
         raise NotLowerable(f"missingValueStrategy {tm.missing_value_strategy!r} is host-only")

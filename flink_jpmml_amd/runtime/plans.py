@@ -1383,7 +1383,15 @@ def compile_plan(compiled, device, **opts) -> DevicePlan:
         # as a derive-kernel pass in front of the model kernel (runtime/derive.py)
         from .derive import DerivedPlan, FieldView, plan_field_layout
 
-        layout = plan_field_layout(compiled, allow_alias=isinstance(ev, (TreeEvaluator, MiningEvaluator)))
+        is_tree = isinstance(ev, (TreeEvaluator, MiningEvaluator))
+        layout = plan_field_layout(compiled, allow_alias=is_tree, allow_fold=is_tree)
+        if layout.folds:  # monotone derived fields folded into the split thresholds (derive.py)
+            try:
+                prec = "fp8" if opts.get("precision") == "fp8" else "fp32"
+                return TreePlan(FieldView(compiled, layout, prepared=False), device, precision=prec,
+                                **{k: v for k, v in opts.items() if k != "precision"})
+            except NotLowerable:
+                layout = plan_field_layout(compiled, allow_alias=True, allow_fold=False)
         if layout.program is not None:
             return DerivedPlan(compiled, device, layout, **opts)
         compiled = FieldView(compiled, layout, prepared=False)

@@ -86,3 +86,15 @@ def test_feature_compaction_on_gpu(gpu):
     plan, s, v, ref, vref = _run(gpu, gbdt_pmml(n_trees=4, depth=3, n_features=400, seed=9), 10_000, 400, 0.05)
     assert plan.feat_map is not None and plan.rows_wide == 256
     assert (v == vref).all() and np.max(np.abs(s - ref)) < 1e-5
+
+
+def test_folded_derived_fields_on_gpu(gpu):
+    """Monotone derived fields (StandardScaler / NormContinuous / decreasing affine) folded into the
+    split thresholds: the tree kernel reads the raw inputs (no derive pass) and matches the oracle."""
+    from flink_jpmml_amd.bench.synth import gbdt_pmml
+
+    plan, s, v, ref, vref = _run(gpu, gbdt_pmml(n_trees=200, depth=6, n_features=32, scaled=True, seed=7),
+                                 60_000, 32, 0.03, seed=8)
+    assert type(plan).__name__ == "TreePlan" and plan.variant & 3 == 1
+    assert (v.astype(bool) == vref).all()
+    assert np.max(np.abs(s[vref] - ref[vref])) < 1e-4

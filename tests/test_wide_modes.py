@@ -228,3 +228,39 @@ def test_many_class_chain_general_slots_with_intercept_stumps():
         acc[:, slots[t]] += leaves[j - NL]
     tab = np.array([float(v) for v in p.labels])
     assert (tab[np.argmax(acc, axis=1)] == ref).all()
+
+
+@pytest.mark.parametrize("missing", [0.0, 0.04])
+def test_monotone_derived_fields_fold_into_thresholds(missing):
+    """StandardScaler / NormContinuous / decreasing affine derived fields read only as split
+    fields: folded into fp32 thresholds on the raw inputs (no derive pass), exact vs the oracle."""
+    from flink_jpmml_amd.runtime.derive import plan_field_layout
+    from flink_jpmml_amd.runtime.plans import compile_plan
+
+    txt = gbdt_pmml(n_trees=40, depth=6, n_features=12, scaled=True, seed=11)
+    c = CompiledPmml.from_string(txt)
+    layout = plan_field_layout(c, allow_fold=True)
+    assert layout.program is None and len(layout.folds) == 12
+    with lowering_dry_run():
+        plan = compile_plan(c, torch.device("cpu"))
+    assert type(plan).__name__ == "TreePlan" and plan.variant & 3 == 1
+    _check(c, plan, stream_matrix(6000, 12, seed=5, missing_rate=missing), tol=1e-4)
+
+
+def test_fold_splits_exact_on_the_fp32_line():
+    from flink_jpmml_amd.models.tree import OP_GE, OP_GT, OP_LE, OP_LT
+    from flink_jpmml_amd.runtime.derive import fold_splits
+
+    rng = np.random.default_rng(0)
+    xs = np.concatenate([rng.standard_normal(200_000), np.linspace(-3, 3, 200_001)]).astype(np.float32)
+    xs = xs.astype(np.float64)
+    for f in (lambda x: (x - 0.3) / 1.25, lambda x: (0.5 - x) * 0.8, lambda x: np.clip(x, -1, 1)):
+        ts = np.array([-2.0, -0.7, 0.0, 0.123456789, 0.9, 5.0])
+        for op in (OP_LT, OP_LE, OP_GT, OP_GE):
+            ops = np.full(len(ts), op, np.int8)
+            o2, t2 = fold_splits(f, ops, ts)
+            for i, t in enumerate(ts):
+                y = f(xs)
+                P = {OP_LT: y < t, OP_LE: y <= t, OP_GT: y > t, OP_GE: y >= t}[op]
+                Q = xs < t2[i] if o2[i] == OP_LT else xs >= t2[i]
+                assert (P == Q).all(), (op, t)
