@@ -660,8 +660,38 @@ __global__ __launch_bounds__(WIDE_T, 1) void tree_perfect_wide_kernel(TreeArgs a
   }
   __syncthreads();
   {
-    const int total = ROWS * F;
     bool miss = false;
+    // identity column map, 16-byte aligned rows: each lane loads 4 consecutive columns of its row
+    // (one 16-byte load instead of four 4-byte ones — the per-lane row stride makes every lane of
+    // a load touch its own cache line) and stores them to 4 planes (still 32 consecutive rows per
+    // store: conflict-free)
+    const bool vec4 = a.feat_map == nullptr && (a.ldx & 3) == 0 && (reinterpret_cast<uintptr_t>(a.X) & 15) == 0;
+    const int F4 = (F + 3) >> 2;
+    for (int e = tid; vec4 && e < ROWS * F4; e += T) {
+      const int q = e >> 5;
+      const int rh = q / F4;
+      const int fq = q - rh * F4;
+      const int r = 32 * rh + (e & 31);
+      const int row = row0 + r;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (row < a.n_rows) v = *reinterpret_cast<const float4*>(a.X + (size_t)row * a.ldx + 4 * fq);
+      const float vv[4] = {v.x, v.y, v.z, v.w};
+      bool b = false;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int f = 4 * fq + k;
+        if (f < F) {
+          float x = vv[k];
+          if (row < a.n_rows) {
+            if (a.prep) x = prep_value(x, a.prep[f], &b);
+            miss = miss || (x != x);
+          }
+          feat[f * PS + r] = x;
+        }
+      }
+      if (b) bad[r] = 1;
+    }
+    const int total = vec4 ? 0 : ROWS * F;
     for (int e = tid; e < total; e += T) {
       // item e: row (e & 31) + 32 * ((e >> 5) / F) of feature (e >> 5) % F — the 32 lanes of a
       // group store 32 consecutive rows of one plane (distinct banks)
