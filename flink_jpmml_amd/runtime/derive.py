@@ -379,10 +379,29 @@ def _monotone_source(name: str, defs: Dict[str, ir.DerivedField], inputs: Dict[s
     return _monotone_expr(d.expression, defs, inputs, schema, seen)
 
 
+def _treated_fields(model: ir.Model) -> set:
+    """Fields a (nested) MiningField prepares — missing / outlier / invalid treatment applied to
+    the field's value itself: a derived field treated so can be neither aliased nor folded."""
+    out: set = set()
+
+    def walk(m: ir.Model) -> None:
+        for mf in m.mining_schema.fields:
+            if (mf.missing_value_replacement is not None or mf.outliers not in (None, "asIs")
+                    or mf.invalid_value_treatment not in (None, "returnInvalid")):
+                out.add(mf.name)
+        if isinstance(m, ir.MiningModel):
+            for sg in m.segments:
+                walk(sg.model)
+
+    walk(model)
+    return out
+
+
 def _non_split_refs(model: ir.Model) -> set:
     """Fields read anywhere but in a TreeModel node predicate (segment predicates, non-tree
-    models): a derived field read there cannot be folded into split thresholds."""
-    out: set = set()
+    models), or treated by a MiningField: such a derived field cannot be folded into split
+    thresholds."""
+    out: set = _treated_fields(model)
 
     def walk(m: ir.Model) -> None:
         if isinstance(m, ir.TreeModel):
@@ -525,7 +544,8 @@ def plan_field_layout(compiled, allow_alias: bool = True, allow_fold: bool = Fal
         return FieldLayout(active, index, None)
     schema = compiled.schema
     if allow_alias:
-        alias = {n: _alias_source(n, defs, index, schema) for n in needed}
+        treated = _treated_fields(_model_of(compiled))
+        alias = {n: None if n in treated else _alias_source(n, defs, index, schema) for n in needed}
         folds: Dict[str, tuple] = {}
         if allow_fold and not all(v is not None for v in alias.values()):
             model = _model_of(compiled)

@@ -264,3 +264,16 @@ def test_fold_splits_exact_on_the_fp32_line():
                 P = {OP_LT: y < t, OP_LE: y <= t, OP_GT: y > t, OP_GE: y >= t}[op]
                 Q = xs < t2[i] if o2[i] == OP_LT else xs >= t2[i]
                 assert (P == Q).all(), (op, t)
+
+
+def test_fold_skips_derived_fields_with_mining_treatment():
+    """A segment MiningField that treats the derived value itself (here: missing replacement) is
+    applied to d, not x — such a field must not be folded (derive pass instead)."""
+    from flink_jpmml_amd.runtime.derive import plan_field_layout
+
+    txt = gbdt_pmml(n_trees=3, depth=3, n_features=4, scaled=True, seed=2)
+    i = txt.index('<MiningField name="f0"/>', txt.index('<Segment'))  # the first segment's schema
+    txt = txt[:i] + '<MiningField name="d(f1)" missingValueReplacement="0.5"/>' + txt[i:]
+    c = CompiledPmml.from_string(txt)
+    layout = plan_field_layout(c, allow_fold=True)
+    assert layout.folds is None and layout.program is not None
