@@ -365,7 +365,11 @@ __host__ __device__ constexpr int perfect_rec_words8(int depth) {
 }
 
 // OCP e4m3 leaf pair in bits [31:16] of a last-level node's meta -> (left, right) as fp32
-__device__ __forceinline__ float leaf8_select(uint32_t meta, bool right) {
+// VOTE8 forests with class codes (VC): bits [23:16] / [31:24] of a last-level meta are the left /
+// right leaf's class index; the walk returns the packed-vote increment 1 << 8*class (as float bits)
+template <bool VC>
+__device__ __forceinline__ float leaf_pair_select(uint32_t meta, bool right) {
+  if constexpr (VC) return __uint_as_float(1u << (8u * ((meta >> (right ? 24 : 16)) & 3u)));
   const auto pr = __builtin_amdgcn_cvt_pk_f32_fp8((int)meta, true);
   return right ? pr[1] : pr[0];
 }
@@ -439,7 +443,7 @@ struct WAcc<MODE_SLOT> {
 // Missing-aware walk of one tree record (per-node default-direction bits): the leaf value, or
 // NaN when the tree's prediction is null (a visited split saw a missing value and the tree is
 // flagged null-on-missing).
-template <int DEPTH, bool LEAF8>
+template <int DEPTH, bool LEAF8, bool VC = false>
 __device__ __forceinline__ float walk_missing(const TreeArgs& a, const char* base, const char* feat_lane,
                                               bool& null_pred) {
   constexpr int NI = (1 << DEPTH) - 1;
@@ -459,7 +463,7 @@ __device__ __forceinline__ float walk_missing(const TreeArgs& a, const char* bas
     right |= isn & (w >> (n & 31u));
     pz |= isn;
     if (LEAF8 && d == DEPTH - 1) {
-      lf = leaf8_select(nd.y, right != 0u);
+      lf = leaf_pair_select<VC>(nd.y, right != 0u);
     } else {
       j = j + j + right;
     }
@@ -476,7 +480,8 @@ __device__ __forceinline__ void traverse_chunk_g(const TreeArgs& a, const uint32
   const int mt = (nt - g + G - 1) / G;
   for (int m = 0; m < mt; ++m) {
     bool nul;
-    const float v = walk_missing<DEPTH, LEAF8>(a, reinterpret_cast<const char*>(buf + (g + G * m) * rw), feat_lane, nul);
+    const float v = walk_missing<DEPTH, LEAF8, LEAF8 && MODE == MODE_VOTE8>(
+        a, reinterpret_cast<const char*>(buf + (g + G * m) * rw), feat_lane, nul);
     if (nul) acc.poison();
     else acc.add(a, t0 + g + G * m, v);
   }
@@ -513,7 +518,7 @@ __device__ __forceinline__ void lds_wait_all() {
 }
 
 // N trees of group g starting at its m-th tree, N independent walks interleaved (ILP).
-template <int DEPTH, int N, int G, bool LEAF8>
+template <int DEPTH, int N, int G, bool LEAF8, bool VC = false>
 __device__ __forceinline__ void fast_batch(uint32_t lds0, int g, int m, uint32_t feat_lane, float (&v)[N]) {
   constexpr int NI = (1 << DEPTH) - 1;
   constexpr int NL = 1 << DEPTH;
@@ -573,7 +578,7 @@ __device__ __forceinline__ void fast_batch(uint32_t lds0, int g, int m, uint32_t
 #pragma unroll
   for (int i = 0; i < N; ++i) {
     if (LEAF8) {
-      v[i] = leaf8_select(nd[i].y, x[i] >= __uint_as_float(nd[i].x));
+      v[i] = leaf_pair_select<VC>(nd[i].y, x[i] >= __uint_as_float(nd[i].x));
     } else {
       v[i] = (x[i] >= __uint_as_float(nd[i].x)) ? __uint_as_float(lv[i].y) : __uint_as_float(lv[i].x);
     }
@@ -584,7 +589,7 @@ template <int DEPTH, int N, int G, bool LEAF8, int MODE>
 __device__ __forceinline__ void fast_batch_acc(const TreeArgs& a, uint32_t lds0, int g, int m, int t0,
                                                uint32_t feat_lane, WAcc<MODE>& acc) {
   float v[N];
-  fast_batch<DEPTH, N, G, LEAF8>(lds0, g, m, feat_lane, v);
+  fast_batch<DEPTH, N, G, LEAF8, LEAF8 && MODE == MODE_VOTE8>(lds0, g, m, feat_lane, v);
 #pragma unroll
   for (int i = 0; i < N; ++i) acc.add(a, t0 + g + G * (m + i), v[i]);
 }
@@ -943,7 +948,9 @@ int launch_perfect(hipStream_t st, const TreeArgs& a, dim3 grid, size_t lds) {
     }
     if (lds_w > 160 * 1024) return -5;
     if (a.P != 1 || a.rec_words != (leaf8 ? perfect_rec_words8(D) : perfect_rec_words(D, 1))) return -10;
-    if (a.mode != MODE_SUM && (a.partial || a.C > CMAX || (a.mode == MODE_VOTE8 && a.C > 4) || leaf8)) return -11;
+    if (a.mode != MODE_SUM && (a.partial || a.C > CMAX || (a.mode == MODE_VOTE8 && a.C > 4) ||
+                               (leaf8 && a.mode != MODE_VOTE8)))
+      return -11;  // leaf pairs in the metas: fp8 sums or VOTE8 class codes
     if (a.mode == MODE_SLOT && !a.tree_slot) return -11;
     (void)grid;
     (void)lds;
@@ -954,7 +961,8 @@ int launch_perfect(hipStream_t st, const TreeArgs& a, dim3 grid, size_t lds) {
                                     : launch_wide<D, R, false, MODE_SUM>(st, a, lds_w);       \
         case MODE_SLOT: return launch_wide<D, R, false, MODE_SLOT>(st, a, lds_w);             \
         case MODE_CLASS: return launch_wide<D, R, false, MODE_CLASS>(st, a, lds_w);           \
-        case MODE_VOTE8: return launch_wide<D, R, false, MODE_VOTE8>(st, a, lds_w);           \
+        case MODE_VOTE8: return leaf8 ? launch_wide<D, R, true, MODE_VOTE8>(st, a, lds_w)     \
+                                      : launch_wide<D, R, false, MODE_VOTE8>(st, a, lds_w);   \
         default: return -11;                                                                  \
       }                                                                                       \
     }

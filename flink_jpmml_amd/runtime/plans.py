@@ -943,6 +943,32 @@ def _leaf8_pack(blob: np.ndarray, D: int, scale: Optional[float] = None) -> Tupl
     return out, rec, scale
 
 
+def _vote_codes_pack(blob: np.ndarray, D: int) -> Tuple[np.ndarray, int]:
+    """Re-pack a VOTE8 PERFECT blob (leaves = packed-vote increments ``1 << 8*class``) with the
+    class index of the two leaves under every last-level node in bits [23:16] / [31:24] of that
+    node's meta, like :func:`_leaf8_pack`: no leaf array (a depth-8 record shrinks 3104 -> 2080
+    bytes: larger LDS chunks) and no leaf-pair read at the last level."""
+    NI, NL = (1 << D) - 1, 1 << D
+    ndr = (NI + 31) // 32
+    inc = blob[:, 2 * NI: 2 * NI + NL]
+    cls = np.zeros_like(inc)
+    for k in range(1, 4):
+        cls[inc == np.uint32(1 << (8 * k))] = k
+    if not np.isin(inc, [np.uint32(1 << (8 * k)) for k in range(4)]).all():
+        raise NotLowerable("vote leaves are not single-class increments")
+    rec = (2 * NI + ndr + 3) & ~3
+    out = np.zeros((blob.shape[0], rec), dtype=np.uint32)
+    out[:, : 2 * NI] = blob[:, : 2 * NI]
+    out[:, 2 * NI: 2 * NI + ndr] = blob[:, 2 * NI + NL: 2 * NI + NL + ndr]
+    for p in range(NL // 2 - 1, NI):
+        left, right = 2 * p + 1 - NI, 2 * p + 2 - NI
+        meta = out[:, 2 * p + 1]
+        if np.any(meta >> 16):
+            raise NotLowerable("feature byte offset does not fit the class-code meta")
+        out[:, 2 * p + 1] = meta | (cls[:, left] << 16) | (cls[:, right] << 24)
+    return out, rec
+
+
 def _pointer_pack(trees: List[BinaryTree], weights: List[float], P: int):
     nodes: List[Tuple[int, int, int, int]] = []
     leaves: List[np.ndarray] = []
@@ -1126,6 +1152,13 @@ class TreePlan(DevicePlan):
                 elif precision != "fp8" or (2 * Fs - 1) * stride * 4 < (1 << 16):  # fp8 metas: 16-bit offsets
                     blob_nan = _nan_planes(blob, depth, Fs, stride)
                     nan_flags = VAR_NAN_FAST | VAR_NAN_PLANES
+            if self.variant == 1 and self.mode == 3 and precision != "fp8" and depth >= 2 \
+                    and (Fs * 2 if blob_nan is not None else Fs) * stride * 4 <= (1 << 16):
+                # VOTE8 forest: class codes in the last-level metas (no leaf array, no leaf read)
+                blob, rec = _vote_codes_pack(blob, depth)
+                if blob_nan is not None:
+                    blob_nan, _ = _vote_codes_pack(blob_nan, depth)
+                self.variant = 2
             if precision == "fp8":
                 # e4m3 leaves in the last-level metas, global scale folded into the epilogue
                 if self.general or self.variant != 1 or spec.mode != "sum":

@@ -49,12 +49,13 @@ def emulate_wide(plan, X, use_nan_blob):
     for t in range(n_t):
         T = blob[t, 0:2 * NI:2].view(np.float32)
         meta = blob[t, 1:2 * NI:2]
-        leaves = blob[t, 2 * NI:2 * NI + NL]
-        drw = blob[t, 2 * NI + NL:2 * NI + NL + (NI + 31) // 32]
+        codes = plan.variant & 3 == 2  # VOTE8 class codes in the last-level metas (no leaf array)
+        leaves = None if codes else blob[t, 2 * NI:2 * NI + NL]
+        drw = blob[t, 2 * NI + (0 if codes else NL):2 * NI + (0 if codes else NL) + (NI + 31) // 32]
         j = np.ones(n, np.int64)
         miss = np.zeros(n, bool)
-        for _ in range(D):
-            off = meta[j - 1].astype(np.int64)
+        for lev in range(D):
+            off = meta[j - 1].astype(np.int64) & (0xFFFF if codes and lev == D - 1 else 0xFFFFFFFF)
             assert (off % (PS * 4) == 0).all()
             x = planes[rows, off // (PS * 4)]
             right = x >= T[j - 1]
@@ -64,7 +65,11 @@ def emulate_wide(plan, X, use_nan_blob):
                 miss |= isn
             j = 2 * j + right
         null_tree = (drw[NI >> 5] >> (NI & 31)) & 1
-        lv = leaves[j - NL]
+        if codes:
+            pm = meta[(j >> 1) - 1]
+            lv = np.uint32(1) << (np.uint32(8) * ((pm >> np.where(j & 1, 24, 16).astype(np.uint32)) & 3))
+        else:
+            lv = leaves[j - NL]
         poison = miss & (null_tree == 1)
         if plan.mode == 0:
             acc[:, 0] += np.where(poison, np.nan, lv.view(np.float32))
@@ -131,7 +136,7 @@ def test_multiclass_chain_nine_classes_stays_general():
 
 def test_unweighted_forest_uses_vote8():
     c, plan = _plan(random_forest_pmml(n_trees=40, depth=6, n_features=12, n_classes=3, seed=1))
-    assert plan.mode == 3 and plan.variant & 3 == 1
+    assert plan.mode == 3 and plan.variant & 3 == 2  # class codes in the last-level metas
     _check(c, plan, stream_matrix(3000, 12, seed=2, missing_rate=0.04))
 
 
