@@ -43,38 +43,62 @@ __global__ __launch_bounds__(TB, 2) void tree_pointer_kernel(TreeArgs a) {
   float acc = 0.f;
   bool poisoned = false;
   const char* feat_lane = reinterpret_cast<const char*>(feat + tid);
-  for (int t = tb; t < te; ++t) {
-    int code = a.roots[t];
-    bool pz = false;
-    while (code >= 0) {
-      const uint4 nd = nodes[code];
-      float x;
-      if (FEAT_LDS) {
-        x = *reinterpret_cast<const float*>(feat_lane + (nd.y & 0xFFFFu));
+  // PILP trees walked in lock-step per lane: every level issues the PILP node loads (L2 gathers)
+  // together, so one L2 round trip serves PILP walks instead of one — the walk is latency-bound
+  // (dependent loads, divergent depths). Finished walks keep re-loading node 0 (clamped index,
+  // no branch around the loads) and are masked out; leaves are accumulated in tree order, so the
+  // sums are bit-identical to a serial walk.
+  constexpr int PILP = 8;
+  for (int t0 = tb; t0 < te; t0 += PILP) {
+    const int nt = min(PILP, te - t0);
+    int code[PILP];
+    bool pz[PILP];
+#pragma unroll
+    for (int i = 0; i < PILP; ++i) {
+      code[i] = i < nt ? a.roots[t0 + i] : -1;
+      pz[i] = false;
+    }
+    bool live = true;
+    while (live) {
+      uint4 nd[PILP];
+#pragma unroll
+      for (int i = 0; i < PILP; ++i) nd[i] = nodes[max(code[i], 0)];
+      live = false;
+#pragma unroll
+      for (int i = 0; i < PILP; ++i) {  // branch-free: finished walks compute on node 0 and keep their leaf
+        const bool act = code[i] >= 0;
+        float x;
+        if (FEAT_LDS) {
+          x = *reinterpret_cast<const float*>(feat_lane + (nd[i].y & 0xFFFFu));
+        } else {
+          const int f = nd[i].y & 0xFFFFu;
+          x = xrow[f];
+          if (a.prep) { bool b = false; x = prep_value(x, a.prep[f], &b); }
+        }
+        const bool isn = (x != x);
+        const bool nulled = act && isn && ((nd[i].y >> 30) & 1u);  // null prediction: walk ends, poisoned
+        const bool right = (x >= __uint_as_float(nd[i].x)) || (isn && (nd[i].y >> 31));
+        const int nc = right ? (int)nd[i].w : (int)nd[i].z;
+        pz[i] = pz[i] || nulled;
+        code[i] = act ? (nulled ? -1 : nc) : code[i];
+        live = live || code[i] >= 0;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < PILP; ++i) {
+      if (i >= nt) break;
+      if (pz[i]) {
+        if (GENERAL) poisoned = true;
+        else acc += __builtin_nanf("");
+        continue;
+      }
+      const int leaf = ~code[i];
+      if (GENERAL) {
+        const int slot = a.tree_slot[t0 + i];
+        for (int p = 0; p < a.P; ++p) accl[(slot + p) * TB + tid] += a.leaves[(size_t)leaf * a.P + p];
       } else {
-        const int f = nd.y & 0xFFFFu;
-        x = xrow[f];
-        if (a.prep) { bool b = false; x = prep_value(x, a.prep[f], &b); }
+        acc += a.leaves[leaf];
       }
-      const bool isn = (x != x);
-      if (isn && ((nd.y >> 30) & 1u)) {
-        pz = true;
-        break;
-      }
-      bool right = (x >= __uint_as_float(nd.x)) || (isn && (nd.y >> 31));
-      code = right ? (int)nd.w : (int)nd.z;
-    }
-    if (pz) {
-      if (GENERAL) poisoned = true;
-      else acc += __builtin_nanf("");
-      continue;
-    }
-    const int leaf = ~code;
-    if (GENERAL) {
-      const int slot = a.tree_slot[t];
-      for (int p = 0; p < a.P; ++p) accl[(slot + p) * TB + tid] += a.leaves[(size_t)leaf * a.P + p];
-    } else {
-      acc += a.leaves[leaf];
     }
   }
   finish_row(a, acc, accl, split, GENERAL, row, row_ok && !poisoned);
