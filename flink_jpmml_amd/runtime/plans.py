@@ -829,6 +829,16 @@ def _perfect_pack(trees: List[BinaryTree], weights: List[float], P: int, D: int,
     ndr = (NI + 31) // 32
     rec = 2 * NI + NL * P + ndr
     rec = (rec + 3) & ~3
+    if trees and (P == 1 or all(t.leaf_probs is not None for t in trees)):
+        return _perfect_pack_vec(trees, weights, P, D, stride, fmap, leaf_bits, rec)
+    return _perfect_pack_loop(trees, weights, P, D, stride, fmap, leaf_bits, rec)
+
+
+def _perfect_pack_loop(trees, weights, P: int, D: int, stride: int, fmap, leaf_bits, rec: int):
+    """Per-node reference implementation of :func:`_perfect_pack` (the vectorised packer is
+    tested bit-identical against it)."""
+    NI, NL = (1 << D) - 1, 1 << D
+    ndr = (NI + 31) // 32
     blob = np.zeros((len(trees), rec), dtype=np.uint32)
     has_dr = False
     for ti, (t, w) in enumerate(zip(trees, weights)):
@@ -879,6 +889,87 @@ def _perfect_pack(trees: List[BinaryTree], weights: List[float], P: int, D: int,
         blob[ti, 2 * NI: 2 * NI + NL * P] = leaves.reshape(-1).view(np.uint32)
         words = (dr_bits.reshape(ndr, 32) << np.arange(32, dtype=np.uint32)[None, :]).sum(axis=1, dtype=np.uint64)
         blob[ti, 2 * NI + NL * P: 2 * NI + NL * P + ndr] = words.astype(np.uint32)
+    return blob, rec, has_dr
+
+
+def _canonical_vec(op: np.ndarray, t: np.ndarray):
+    """:func:`canonical_threshold` over arrays: ``(T, swap)``."""
+    t32 = t.astype(np.float32)
+    back = t32.astype(np.float64)
+    ceil32 = np.where(back < t, np.nextafter(t32, np.float32(np.inf)), t32)     # smallest fp32 >= t
+    floor32 = np.where(back > t, np.nextafter(t32, np.float32(-np.inf)), t32)   # largest fp32 <= t
+    up_floor = np.nextafter(floor32, np.float32(np.inf))
+    T = np.where((op == OP_LT) | (op == OP_GE), ceil32, up_floor)
+    swap = (op == OP_GT) | (op == OP_GE)
+    return T.astype(np.float32), swap
+
+
+def _perfect_pack_vec(trees, weights, P: int, D: int, stride: int, fmap, leaf_bits, rec: int):
+    """Vectorised :func:`_perfect_pack` (bit-identical): all trees advance one heap level at a
+    time over concatenated node arrays — no per-node Python loop (model load time)."""
+    NI, NL = (1 << D) - 1, 1 << D
+    ndr = (NI + 31) // 32
+    n = len(trees)
+    sizes = np.array([len(t.feature) for t in trees], np.int64)
+    off = np.concatenate([[0], np.cumsum(sizes)[:-1]])
+    feat = np.concatenate([t.feature for t in trees]).astype(np.int64)
+    thr = np.concatenate([t.threshold for t in trees]).astype(np.float64)
+    ops = np.concatenate([t.op for t in trees])
+    dleft = np.concatenate([t.default_left for t in trees])
+    tree_of = np.repeat(np.arange(n), sizes)
+    left = np.concatenate([t.left for t in trees]).astype(np.int64) + off[tree_of]
+    right = np.concatenate([t.right for t in trees]).astype(np.int64) + off[tree_of]
+    w_node = np.asarray(weights, np.float64)[tree_of]
+    T, swap = _canonical_vec(ops, thr)
+    lc = np.where(swap, right, left)
+    rc = np.where(swap, left, right)
+    dr = np.where(swap, dleft, ~dleft)
+    if fmap is None:
+        col = feat
+    else:
+        lut = np.full(max(fmap) + 1 if fmap else 1, -1, np.int64)
+        for k, v in fmap.items():
+            lut[k] = v
+        col = np.where(feat >= 0, lut[np.clip(feat, 0, len(lut) - 1)], -1)
+    if stride == TB and (col[feat >= 0] > 63).any():
+        raise NotLowerable("the narrow perfect layout supports at most 64 features")
+    nodes_T = np.zeros((n, NI), np.float32)
+    nodes_meta = np.zeros((n, NI), np.uint32)
+    dr_bits = np.zeros((n, ndr * 32), np.uint32)
+    cur = off.copy()[:, None]  # [n, 1] node at each heap position of the current level
+    for d in range(D):
+        split = feat[cur] >= 0
+        p0 = (1 << d) - 1
+        sl = slice(p0, p0 + (1 << d))
+        nodes_T[:, sl] = np.where(split, T[cur], 0.0)
+        nodes_meta[:, sl] = np.where(split, (col[cur] * stride * 4).astype(np.uint32), 0)
+        dr_bits[:, sl] = np.where(split, dr[cur], False)
+        # a leaf above depth D covers its whole padded subtree: both "children" are itself
+        nxt = np.empty((n, 2 << d), np.int64)
+        nxt[:, 0::2] = np.where(split, lc[cur], cur)
+        nxt[:, 1::2] = np.where(split, rc[cur], cur)
+        cur = nxt
+    if (feat[cur] >= 0).any():
+        raise NotLowerable("tree deeper than the PERFECT depth")
+    if leaf_bits == "vote8":
+        lv = np.concatenate([t.leaf_value for t in trees])
+        leaves = (np.uint32(1) << (np.uint32(8) * lv[cur].astype(np.uint32))).view(np.float32)[..., None]
+    elif P > 1:
+        probs = np.concatenate([t.leaf_probs for t in trees])
+        leaves = (probs[cur][..., :P] * w_node[cur][..., None]).astype(np.float32)
+    else:
+        lv = np.concatenate([t.leaf_value for t in trees])
+        leaves = (lv[cur] * w_node[cur]).astype(np.float32)[..., None]
+    has_dr = bool(dr_bits.any())
+    for ti, t in enumerate(trees):
+        if t.null_missing:
+            dr_bits[ti, NI] = 1
+    blob = np.zeros((n, rec), dtype=np.uint32)
+    blob[:, 0:2 * NI:2] = nodes_T.view(np.uint32)
+    blob[:, 1:2 * NI:2] = nodes_meta
+    blob[:, 2 * NI:2 * NI + NL * P] = np.ascontiguousarray(leaves).reshape(n, NL * P).view(np.uint32)
+    words = (dr_bits.reshape(n, ndr, 32).astype(np.uint64) << np.arange(32, dtype=np.uint64)).sum(axis=2)
+    blob[:, 2 * NI + NL * P: 2 * NI + NL * P + ndr] = words.astype(np.uint32)
     return blob, rec, has_dr
 
 

@@ -297,3 +297,32 @@ def test_fp8_leaf_packing(depth):
     ref, _ = c.score_matrix_oracle(X)
     agree = (_scores(spec, acc8[:, None]) == ref).mean()
     assert agree > 0.97
+
+
+def test_vectorised_perfect_pack_is_bit_identical():
+    """The level-at-a-time packer (model load time) == the per-node reference, for regression /
+    K-class / vote8 / null-prediction / sparse trees, both strides, with a column map, and P > 1."""
+    import numpy as np
+
+    from flink_jpmml_amd.bench.synth import gbdt_pmml, random_forest_pmml
+    from flink_jpmml_amd.runtime.compiled import CompiledPmml
+    from flink_jpmml_amd.runtime.plans import TB, _perfect_pack_loop, _perfect_pack_vec, ensemble_spec, to_general
+
+    cases = [(gbdt_pmml(n_trees=30, depth=6, n_features=32, seed=1), None, False),
+             (gbdt_pmml(n_trees=10, depth=5, n_features=10, objective="multiclass", n_classes=4, seed=2), None, False),
+             (random_forest_pmml(n_trees=20, depth=7, n_features=12, n_classes=3, seed=3), "vote8", False),
+             (random_forest_pmml(n_trees=20, depth=5, n_features=12, n_classes=3, seed=4,
+                                 missing_strategy="nullPrediction"), None, False),
+             (random_forest_pmml(n_trees=20, depth=5, n_features=12, n_classes=3, seed=6), None, True),
+             (gbdt_pmml(n_trees=30, depth=6, n_features=20, seed=5, p_split=0.6), None, False)]
+    for txt, leaf_bits, general in cases:
+        spec = ensemble_spec(CompiledPmml.from_string(txt))
+        if general:
+            spec = to_general(spec)
+        D = max(t.depth for t in spec.trees)
+        NI, NL = (1 << D) - 1, 1 << D
+        rec = ((2 * NI + NL * spec.P + (NI + 31) // 32) + 3) & ~3
+        for stride, fmap in ((TB, None), (256, {f: (f * 7) % 40 for f in range(40)})):
+            a = _perfect_pack_loop(spec.trees, spec.weights, spec.P, D, stride, fmap, leaf_bits, rec)
+            b = _perfect_pack_vec(spec.trees, spec.weights, spec.P, D, stride, fmap, leaf_bits, rec)
+            assert np.array_equal(a[0], b[0]) and a[1:] == b[1:], (leaf_bits, general, stride)
