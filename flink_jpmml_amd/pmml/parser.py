@@ -22,10 +22,17 @@ from . import ir
 # --------------------------------------------------------------------------- helpers
 
 
+_LOCAL: Dict[str, str] = {}  # namespaced tag -> local name (a document repeats a few dozen tags)
+
+
 def _local(tag: str) -> str:
-    if not isinstance(tag, str):  # comments / processing instructions
-        return ""
-    return tag.rsplit("}", 1)[-1]
+    try:
+        return _LOCAL[tag]
+    except (KeyError, TypeError):
+        if not isinstance(tag, str):  # comments / processing instructions
+            return ""
+        name = _LOCAL[tag] = tag.rsplit("}", 1)[-1]
+        return name
 
 
 def _children(el: ET.Element, name: Optional[str] = None) -> List[ET.Element]:
