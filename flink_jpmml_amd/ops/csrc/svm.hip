@@ -1,11 +1,13 @@
 // SupportVectorMachineModel scoring: kernel evaluation against every support vector + dual
 // coefficients + machine votes, fused in one pass.
 //
-// One lane per row; the row's (prepared) features live in registers (FMAX template bucket, zero
-// padded) so the per-support-vector dot product needs no memory traffic besides the support
-// vector itself, which every lane reads at the same address (scalar loads, broadcast). Machines
-// (<= MMAX) accumulate in registers. fp32 throughout (parity path; the SV x row product is tiny
-// compared to the tree and MLP workloads, see profiles/).
+// Two kernels, fp32 throughout (parity path):
+//  * svm_mfma_kernel (>= 32 support vectors, the common case): the x . sv products on the matrix
+//    cores (exact-fp32 MFMA, support vectors on M, rows on N), kernel function and dual
+//    coefficients applied on the accumulator registers — see its comment below;
+//  * svm_kernel (few support vectors): one lane per row, the row's (prepared) features in
+//    registers (FMAX template bucket, zero padded), every support vector read by all lanes at the
+//    same address (broadcast); machines (<= MMAX) accumulate in registers.
 #include "epilogue.h"
 
 namespace {

@@ -14,7 +14,11 @@
 //    fp32 comparison is exact for fp32 inputs (see runtime/plans.py);
 //  * POINTER layout for deeper / wider ensembles: {T, meta, left, right} nodes read from global
 //    memory (L2-resident), divergent walk;
-//  * the per-row epilogue (sum / average / vote / link function / label table) is fused.
+//  * the per-row epilogue (sum / average / vote / link function / label table) is fused;
+//  * WIDE kernel (the default for P = 1 ensembles, tree_perfect_wide_kernel): 1024 threads per CU
+//    own 256 / 128 / 64 rows x G tree groups; sum ensembles on 256-row tiles claim 8-tree batches
+//    dynamically (deterministic slot sums); fp8 leaf pairs / VOTE8 class codes live in the
+//    last-level node words. Its walk is LDS-port bound (profiles/r2_tree_variants.md).
 //
 // Missing values: a per-node default-direction bit routes NaN (XGBoost / LightGBM `defaultChild`).
 // PMML `missingValueStrategy="nullPrediction"` (scikit-learn exports) and `none` with complement
