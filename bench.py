@@ -12,11 +12,14 @@ synthetic record stream, random-initialised trees (weak scaling: each GPU scores
        .quick_evaluate(ModelReader(model.pmml))            # EvaluationFunction, one per rank
        .add_sink(<waits for every PredictionBatch; all-gathers the scores over RCCL when N > 1>)
 
-One step (per rank) = one RecordBatch of ``--rows`` records in pinned host memory scored end to
-end: H2D in micro-batches on a copy stream → fused prepare + tree-ensemble HIP kernel whose
-epilogue writes scores straight into pinned host memory → the sink waits for the batch (and with
-N > 1 all-gathers the scored shard over RCCL). Nothing is skipped or cached: every
-step re-copies and re-scores every row. ``--api engine`` times the bare StreamingScorer instead.
+One step (per rank) = ``--passes`` RecordBatches of ``--rows`` records each (passes over this
+rank's pinned shard) scored end to end: H2D in micro-batches on a copy stream → fused prepare +
+tree-ensemble HIP kernel whose epilogue writes scores straight into pinned host memory → the
+library :class:`~flink_jpmml_amd.parallel.sinks.GatherSink` (lockstep) waits for every batch and,
+with N > 1, all-gathers the scored shard's device mirrors over RCCL on a comm stream (SURVEY §2.6
+F5). Nothing is skipped or cached: every pass re-copies and re-scores every row (a step is
+``passes × rows`` records, so the timed region is seconds long). ``--api engine`` times the bare
+StreamingScorer instead.
 
 Under ``torchrun`` the model is parsed once on rank 0 and its compiled tensors are
 RCCL-broadcast to every rank (F2). Rank 0 prints ONE JSON line.
@@ -61,7 +64,9 @@ def parse_args(argv=None):
     p.add_argument("--depth", type=int, default=None, help="default 6 (gbdt/chain), 8 (rf)")
     p.add_argument("--features", type=int, default=None, help="default 32 (trees), 64 (mlp)")
     p.add_argument("--rows", type=int, default=1 << 23,
-                   help="rows per GPU per step (8M: a 20-step timed region is ~0.4 s on one GPU)")
+                   help="rows per pass (this rank's pinned shard: 8M rows x 32 fp32 = 1 GiB)")
+    p.add_argument("--passes", type=int, default=16,
+                   help="passes over the pinned shard per step (16: a 20-step timed region is ~6 s on one GPU)")
     p.add_argument("--micro-batch", type=int, default=1 << 20,
                    help="rows per H2D slice + kernel launch (1M measured best: profiles/r2_h2d_probe.md)")
     p.add_argument("--pipeline-depth", type=int, default=3, help="input ring slots (H2D/compute overlap)")
@@ -103,9 +108,10 @@ class _StepSource:
     """``--warmup + --steps`` RecordBatches (one per step) of this rank's pinned shard; calls
     ``on_step(i)`` right before step i is handed to the pipeline (timer start hook)."""
 
-    def __init__(self, X, n_steps, on_step):
+    def __init__(self, X, n_steps, passes, on_step):
         self.X = X
         self.n = n_steps
+        self.passes = passes
         self.on_step = on_step
 
     def open_subtask(self, rank, world):  # parallel source: every rank scores its own shard
@@ -114,59 +120,31 @@ class _StepSource:
     def iterate(self):
         from flink_jpmml_amd.api.batch import RecordBatch
 
+        rows = len(self.X)
         for i in range(self.n):
             self.on_step(i)
-            yield RecordBatch(self.X, offset=i * len(self.X))
+            for p in range(self.passes):
+                yield RecordBatch(self.X, offset=(i * self.passes + p) * rows)
 
 
-class _BenchSink:
-    """Waits for every scored step (the host observes completion) and, with N > 1 ranks,
-    all-gathers the scored shard over RCCL on a side stream."""
+class _WaitSink:
+    """``--no-allgather`` at N > 1: every rank only waits for its own scored batches."""
 
-    def __init__(self, ctx, gather: bool, rows: int):
-        self.ctx = ctx
-        self.gather = gather
+    def __init__(self):
         self.rows_seen = 0
-        self.last = None
-        self._works = []
-        self._bufs = None
-        self._comm = None
-        if gather:
-            import torch
-
-            n = rows * ctx.world_size
-            self._bufs = (torch.empty(n, dtype=torch.float32, device=ctx.device),
-                          torch.empty(n, dtype=torch.uint8, device=ctx.device))
-            self._comm = torch.cuda.Stream(ctx.device)
 
     def invoke(self, value) -> None:
-        pb, batch = value
-        pb.wait()
-        self.rows_seen += len(pb)
-        self.last = pb
-        if self.gather:
-            import torch
-
-            from flink_jpmml_amd.parallel import all_gather_scores
-
-            for w in self._works:  # one gather in flight: bounded device memory
-                w.wait()
-            with torch.cuda.stream(self._comm):
-                s, v = pb.device_out
-                _, _, self._works = all_gather_scores(s, v, self.ctx, async_op=True, out=self._bufs)
+        value[0].wait()
+        self.rows_seen += len(value[0])
 
     def finish(self) -> None:
-        for w in self._works:
-            w.wait()
-        self._works = []
+        pass
 
 
-def _h2d_streams(model, args):
-    """Copy streams the pipeline used (auto mode: what the calibration chose on this box)."""
-    from flink_jpmml_amd.utils.metrics import METRICS
-
-    chosen = METRICS.summary()["counters"].get("pipeline.h2d_streams_chosen")
-    return int(chosen) if chosen else args.h2d_streams
+def _h2d_streams(pipe, args):
+    """Copy streams of the pipeline the timed operator used (auto mode: its calibration's choice)."""
+    n = getattr(pipe, "h2d_streams_in_use", None) if pipe is not None else None
+    return int(n) if n else (args.h2d_streams or None)
 
 
 def main(argv=None) -> int:
@@ -236,7 +214,11 @@ def main(argv=None) -> int:
         ctx.barrier()
         torch.cuda.synchronize()
 
+    pipe = None
+    job = {}
+    rows_per_step = args.rows * args.passes
     if args.api == "dsl":
+        from flink_jpmml_amd.parallel.sinks import GatherSink
         from flink_jpmml_amd.stream import StreamExecutionEnvironment
 
         def on_step(i):
@@ -245,32 +227,35 @@ def main(argv=None) -> int:
                 timing["t0"] = time.perf_counter()
 
         env = StreamExecutionEnvironment(config=cfg, dist_ctx=ctx if ctx.is_distributed else None)
-        sink = _BenchSink(ctx, gather, args.rows)
-        op_cfg = cfg
-        stream = env.add_source(_StepSource(X, args.warmup + args.steps, on_step), mode="parallel")
-        if gather:
-            # keep [n] device mirrors of every PredictionBatch for the RCCL all-gather sink
-            stream = stream.evaluate(ModelReader(path), lambda b, m: (m.scorer.submit_batch(b, keep_device=True), b),
-                                     config=op_cfg)
-        else:
-            stream = stream.quick_evaluate(ModelReader(path), config=op_cfg)
-        stream.add_sink(sink)
-        env.execute("bench")
+        # the library F5 sink: waits for every scored batch; with N > 1 all-gathers the device
+        # mirrors over RCCL on its comm stream, overlapping the next batch
+        sink = GatherSink(to="all", lockstep=True, keep=False) if gather or N == 1 else _WaitSink()
+        op_cfg = cfg.replace(device_mirror=gather)
+        stream = env.add_source(_StepSource(X, args.warmup + args.steps, args.passes, on_step), mode="parallel")
+        scored = stream.quick_evaluate(ModelReader(path), config=op_cfg)
+        scored.add_sink(sink)
+        res = env.execute("bench")
         sink.finish()
         barrier_sync()
         elapsed = time.perf_counter() - timing["t0"]
-        assert sink.rows_seen == (args.warmup + args.steps) * args.rows
+        job.update(records_in=res.records_in, elements_in=res.elements_in)
+        seen = sink.rows_seen
+        assert seen == (args.warmup + args.steps) * rows_per_step, (seen, rows_per_step)
+        assert res.records_in == seen
+        op = scored.node.factory  # the operator instance this (single-subtask) rank ran
+        pipe = getattr(getattr(op, "inner", op), "_pipeline", None)
     else:
         scorer = StreamingScorer(plan, micro_batch=args.micro_batch, depth=args.pipeline_depth, max_rows=args.rows,
                                  h2d_streams=args.h2d_streams)
+        pipe = scorer.pipe
         score_h = torch.empty(args.rows, dtype=torch.float32).pin_memory()
         valid_h = torch.empty(args.rows, dtype=torch.uint8).pin_memory()
-        for _ in range(args.warmup):
+        for _ in range(args.warmup * args.passes):
             scorer.wait(scorer.submit(X, score_h, valid_h))
         barrier_sync()
         t0 = time.perf_counter()
         h = None
-        for _ in range(args.steps):
+        for _ in range(args.steps * args.passes):
             h = scorer.submit(X, score_h, valid_h)
         scorer.wait(h)
         barrier_sync()
@@ -280,7 +265,7 @@ def main(argv=None) -> int:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms_per_step = elapsed / args.steps * 1e3
-    records_per_s = N * args.rows * args.steps / elapsed
+    records_per_s = N * rows_per_step * args.steps / elapsed
 
     # ---- device-resident kernel throughput (records already in HBM) — reported separately
     n_k = min(args.rows, 1 << 22)
@@ -333,14 +318,16 @@ def main(argv=None) -> int:
                          f"{MODELS[args.model][1]}: trees={args.trees} depth={args.depth} "
                          f"features={args.features} precision={args.precision}",
                 "baseline_config": MODELS[args.model][0],
-                "global_batch": args.rows * N,
+                "global_batch": rows_per_step * N,
                 "seq_len": None,
                 "parallelism": f"dp{N}",
                 "api": args.api,
                 "micro_batch": args.micro_batch,
                 "pipeline_depth": args.pipeline_depth,
-                "h2d_streams": _h2d_streams(model, args),
-                "rows_per_gpu_per_step": args.rows,
+                "h2d_streams": _h2d_streams(pipe, args),
+                "rows_per_gpu_per_step": rows_per_step,
+                "passes_per_step": args.passes,
+                "rows_per_pass": args.rows,
                 "allgather_sink": gather,
                 "zero_copy_host_sink": bool(getattr(model.scorer, "direct", False)),
                 "numa_node": numa_node,
@@ -350,7 +337,8 @@ def main(argv=None) -> int:
             "latency_batch_rows": args.latency_batch,
             "kernel_only_records_per_s_per_gpu": n_k / (kernel_ms / 1e3),
             "kernel_ms_per_1M_rows": kernel_ms * (1 << 20) / n_k,
-            "h2d_gbps_effective": args.rows * args.features * 4 * args.steps / elapsed / 1e9,
+            "h2d_gbps_effective": rows_per_step * args.features * 4 * args.steps / elapsed / 1e9,
+            "job": job,
             "model_load_broadcast_s": load_s,
             "timed_region_s": elapsed,
             "plan": {"layout": getattr(plan, "layout", None), "depth": getattr(plan, "depth", None),

@@ -80,10 +80,11 @@ class RecordBatch:
     @staticmethod
     def pinned(n: int, n_features: int) -> "RecordBatch":
         """An uninitialised batch in pinned host memory (fill ``X`` in place, e.g. from the native
-        ingest)."""
+        ingest). Pageable memory on hosts without a GPU (nothing to DMA to)."""
         import torch
 
-        return RecordBatch(torch.empty((n, n_features), dtype=torch.float32, pin_memory=True))
+        return RecordBatch(torch.empty((n, n_features), dtype=torch.float32,
+                                       pin_memory=torch.cuda.is_available()))
 
     def to_pinned(self) -> "RecordBatch":
         """This batch with ``X`` copied into pinned host memory (no-op if already pinned)."""

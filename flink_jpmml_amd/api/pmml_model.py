@@ -206,7 +206,8 @@ class PmmlModel(Pipeline):
     extractTarget = extract_target  # noqa: N815
 
     # ------------------------------------------------------------------ batch API
-    def predict_records(self, batch: RecordBatch, replace_nan: Optional[float] = None) -> PredictionBatch:
+    def predict_records(self, batch: RecordBatch, replace_nan: Optional[float] = None,
+                        keep_device: bool = False) -> PredictionBatch:
         """Columnar ``predict``: validation (row width), preparation, evaluation and extraction for
         a whole batch on the bound scorer. Never raises for bad records: rows the per-record path
         would score as ``EmptyScore`` are invalid in the result."""
@@ -218,7 +219,7 @@ class PmmlModel(Pipeline):
             logger.warning("Error while validate input: batch width %d is not conform to model size %d",
                            batch.n_features, width)
             return PredictionBatch.empty(n)
-        return self.scorer.submit_batch(batch, replace_nan)
+        return self.scorer.submit_batch(batch, replace_nan, keep_device=keep_device)
 
     def predict_batch(self, X: Any, replace_nan: Optional[float] = None, device: Any = None, **opts):
         """Score a ``[rows, active_fields]`` matrix (numpy or torch; NaN = missing) or a sequence

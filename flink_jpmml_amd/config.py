@@ -59,6 +59,10 @@ class ScoringConfig:
     engines); 0 = calibrate 1 vs 2 on the first copy and keep the faster (boxes differ)."""
     max_inflight: int = 4
     """Scored batches an operator keeps in flight before it waits for the oldest (backpressure)."""
+    device_mirror: bool = False
+    """Keep ``[rows]`` device copies of every columnar result (``PredictionBatch.device_out``) next
+    to the pinned host scores, so a :class:`~flink_jpmml_amd.parallel.sinks.GatherSink` all-gathers
+    them over RCCL without a host round trip (SURVEY §2.6 F5)."""
 
     # -- dynamic serving
     cache_capacity: int = 64

@@ -2,13 +2,15 @@
 
     python -m flink_jpmml_amd.examples quick     --model kmeans.xml --output out.txt [--device cuda]
     python -m flink_jpmml_amd.examples evaluate  --model kmeans.xml --output out.txt
-    python -m flink_jpmml_amd.examples dynamic   --models a.xml,b.xml --output out.txt --gen-policy finite \
-                                                 --intervalCheckpoint 1000 --maxIntervalControlStream 0
-    python -m flink_jpmml_amd.examples checkpoint --output out.txt --control-file paths.txt
+    python -m flink_jpmml_amd.examples dynamic   --models a.xml,b.xml --output out.txt --gen-policy random \
+                                                 --intervalCheckpoint 1000 --maxIntervalControlStream 5000
+    python -m flink_jpmml_amd.examples checkpoint --output out.txt --socket localhost:9999   # nc -lk 9999
 
-Flags keep the reference's names (`E/util/DynamicParams.scala:28-68`,
-`E/util/EnsureParameters.scala:24-29`); ``--device``/``--batch-size`` switch to micro-batched GPU
-scoring. ``--intervalCheckpoint`` counts records (the runtime's barriers are count based).
+Flags keep the reference's names and defaults (`E/util/DynamicParams.scala:28-68`,
+`E/util/EnsureParameters.scala:24-29`): ``--intervalCheckpoint`` is a time interval in ms,
+``--maxIntervalControlStream`` 5000 ms, events at 1 record/s (``--rate``); every job streams its
+output with ``writeAsText`` semantics. ``--device``/``--batch-size`` switch to micro-batched GPU
+scoring.
 
 Scoring configuration (:class:`~flink_jpmml_amd.config.ScoringConfig`) from flags:
 ``--max-batch-latency-ms`` (size-or-time flush), ``--precision fp32|bf16|fp8``, ``--fallback
@@ -20,9 +22,7 @@ Iris source to N records/s (the reference's sources emit 1 record/s, `E/sources/
 from __future__ import annotations
 
 import argparse
-import socket
 import sys
-import uuid
 from typing import List, Optional
 
 from ..api.reader import ModelReader
@@ -33,14 +33,14 @@ from ..utils.metrics import METRICS
 from .sources import ControlSource, IrisSource, ids_and_paths, now_ms
 
 
-def _write(out: List, path: Optional[str]) -> None:
-    if path in (None, "-"):
-        for x in out:
-            print(x)
-        return
-    with open(path, "w") as fh:
-        for x in out:
-            fh.write(f"{x}\n")
+def _sink(stream, args, keep: bool = True) -> List:
+    """``writeAsText(output)`` — lines are written as results arrive (the file grows while the
+    job runs) — plus an in-memory copy the CLI returns (bounded runs only)."""
+    out: List = []
+    stream.write_as_text(args.output)
+    if keep:
+        stream.add_sink(out.append)
+    return out
 
 
 def scoring_config(args) -> ScoringConfig:
@@ -55,83 +55,90 @@ def _env(args) -> StreamExecutionEnvironment:
     return StreamExecutionEnvironment(args.parallelism, config=scoring_config(args))
 
 
+def _rate(args) -> Optional[float]:
+    return args.rate if args.rate and args.rate > 0 else None
+
+
 def quick_evaluate_kmeans(args) -> List:
-    """X1 (`E/QuickEvaluateKmeans.scala:29-54`): Iris vectors → quick_evaluate → sink."""
+    """X1 (`E/QuickEvaluateKmeans.scala:29-54`): Iris vectors → quick_evaluate → writeAsText."""
     env = _env(args)
-    vectors = env.add_source(IrisSource(None, n=args.records, rate=args.rate, seed=args.seed)).map(
+    vectors = env.add_source(IrisSource(None, n=args.records, rate=_rate(args), seed=args.seed)).map(
         lambda e: e.to_vector())
-    out = vectors.quick_evaluate(ModelReader(args.model), batch_size=args.batch_size, device=args.device).collect()
-    _write(out, args.output)
+    out = _sink(vectors.quick_evaluate(ModelReader(args.model), batch_size=args.batch_size, device=args.device), args)
+    env.execute("Quick Evaluate Kmeans")
     return out
 
 
 def evaluate_kmeans(args) -> List:
     """X2 (`E/EvaluateKmeans.scala:29-57`): full UDF with ``predict(vec, Some(0.0))``."""
     env = _env(args)
-    events = env.add_source(IrisSource(None, n=args.records, rate=args.rate, seed=args.seed))
+    events = env.add_source(IrisSource(None, n=args.records, rate=_rate(args), seed=args.seed))
 
     def udf(event, model):
         prediction = model.predict(event.to_vector(), 0.0)
         return event, prediction.value.get_or_else(-1.0)
 
-    out = events.evaluate(ModelReader(args.model), udf, batch_size=args.batch_size, device=args.device).collect()
-    _write(out, args.output)
+    out = _sink(events.evaluate(ModelReader(args.model), udf, batch_size=args.batch_size, device=args.device), args)
+    env.execute("Evaluate Kmeans")
     return out
+
+
+def _enable_checkpointing(env: StreamExecutionEnvironment, args) -> None:
+    """``env.enableCheckpointing(ckpInterval, EXACTLY_ONCE)``: ``--intervalCheckpoint`` is in ms,
+    like the reference's (`E/util/DynamicParams.scala:38`)."""
+    if args.intervalCheckpoint and args.intervalCheckpoint > 0:
+        env.enable_checkpointing(interval_ms=args.intervalCheckpoint, directory=args.checkpoint_dir)
+
+
+def _predict_udf(event, model):
+    """The reference's UDF (`E/DynamicEvaluateKmeans.scala:54-60`, `E/CheckpointEvaluate.scala:89-95`):
+    ``(event, model.predict(vectorized, Some(0.0)).value)``."""
+    return event, model.predict(event.to_vector(), 0.0).value
 
 
 def dynamic_evaluate_kmeans(args) -> List:
-    """X3 (`E/DynamicEvaluateKmeans.scala:38-67`): events tagged with model ids + a control stream."""
+    """X3 (`E/DynamicEvaluateKmeans.scala:38-67`): events tagged with model ids + a control stream
+    with random gaps up to ``--maxIntervalControlStream`` ms; events keep flowing meanwhile."""
     paths = [p for p in args.models.split(",") if p]
     idp = ids_and_paths(paths)
     env = _env(args)
-    if args.intervalCheckpoint:
-        env.enable_checkpointing(args.intervalCheckpoint, args.checkpoint_dir)
+    _enable_checkpointing(env, args)
     control = env.add_source(ControlSource(idp, args.gen_policy, n=args.control_messages,
-                                           max_interval_ms=args.maxIntervalControlStream, seed=args.seed),
-                             timestamp=lambda m: m.occurred_on)
-    events = env.add_source(IrisSource(list(idp), n=args.records, rate=args.rate, seed=args.seed),
-                            timestamp=lambda e: e.occurred_on)
-
-    def udf(event, model):
-        return event.model_id, model.predict(event.to_vector(), None)
-
-    out = events.with_support_stream(control).evaluate(udf, batch_size=args.batch_size, device=args.device,
-                                                       uid="dynamic-kmeans").collect(restore=args.restore)
-    _write(out, args.output)
+                                           max_interval_ms=args.maxIntervalControlStream, seed=args.seed))
+    events = env.add_source(IrisSource(list(idp), n=args.records, rate=_rate(args), seed=args.seed))
+    preds = events.with_support_stream(control).evaluate(_predict_udf, batch_size=args.batch_size,
+                                                         device=args.device, uid="dynamic-kmeans")
+    out = _sink(preds, args, keep=args.records is not None)
+    env.execute("Dynamic Clustering Example", restore=args.restore)
     return out
 
 
-def _control_lines(args):
-    if args.control_file:
-        with open(args.control_file) as fh:
-            for line in fh:
-                line = line.strip()
-                if line:
-                    yield line
-    elif args.socket:
-        host, port = args.socket.split(":")
-        with socket.create_connection((host, int(port))) as s, s.makefile() as fh:
-            for line in fh:
-                line = line.strip()
-                if line:
-                    yield line
-
-
 def checkpoint_evaluate(args) -> List:
-    """X4 (`E/CheckpointEvaluate.scala:36-102`): fixed ids, each control line is a model path mapped
-    to ``AddMessage(randomId, 1, path, now)``; metadata checkpoints every N records."""
-    ids = [str(uuid.UUID(int=1)), str(uuid.UUID(int=2))]
+    """X4 (`E/CheckpointEvaluate.scala:36-102`): two fixed ids; 1 Hz Iris events; the control
+    stream is a **live socket** (``--socket host:port``, one model path per line, mapped to
+    ``AddMessage(randomId, 1, path, now)``) or a file; time-based EXACTLY_ONCE checkpoints; the
+    output file is written as results arrive."""
+    import random
+
+    ids = ["4897c9f4-5226-43c7-8f2d-f9fd388cf2bc", "5f919c52-2ef8-4ff2-94b2-2e64bb85005e"]
+    rng = random.Random(args.seed)
     env = _env(args)
-    env.enable_checkpointing(args.intervalCheckpoint or 10, args.checkpoint_dir)
-    lines = list(_control_lines(args))
-    ctrl = [AddMessage(ids[i % len(ids)], 1, p, now_ms()) for i, p in enumerate(lines)]
-    control = env.from_collection(ctrl, timestamp=lambda m: m.occurred_on)
-    events = env.add_source(IrisSource(ids, n=args.records, rate=args.rate, seed=args.seed),
-                            timestamp=lambda e: e.occurred_on)
-    out = events.with_support_stream(control).evaluate(
-        lambda e, m: (e.model_id, m.predict(e.to_vector()).value.get_or_else(-1.0)),
-        uid="checkpoint-evaluate").collect(restore=args.restore)
-    _write(out, args.output)
+    _enable_checkpointing(env, args)
+    if args.socket:
+        host, port = args.socket.rsplit(":", 1)
+        lines = env.socket_text_stream(host, int(port), uid="control-socket")
+    elif args.control_file:
+        with open(args.control_file) as fh:
+            lines = env.from_collection([ln.strip() for ln in fh if ln.strip()], uid="control-file")
+    else:
+        raise SystemExit("checkpoint: give --socket host:port or --control-file")
+    control = lines.filter(lambda ln: bool(ln.strip())).map(
+        lambda path: AddMessage(ids[rng.randrange(len(ids))], 1, path.strip(), now_ms()))
+    events = env.add_source(IrisSource(ids, n=args.records, rate=_rate(args), seed=args.seed))
+    preds = events.with_support_stream(control).evaluate(_predict_udf, batch_size=args.batch_size,
+                                                         device=args.device, uid="checkpoint-evaluate")
+    out = _sink(preds, args, keep=args.records is not None)
+    env.execute("Checkpoint Evaluate Example", restore=args.restore)
     return out
 
 
@@ -146,7 +153,8 @@ def build_parser() -> argparse.ArgumentParser:
         sp.add_argument("--batch-size", type=int, default=None)
         sp.add_argument("--device", default=None)
         sp.add_argument("--seed", type=int, default=0)
-        sp.add_argument("--rate", type=float, default=None, help="source records per second (None: unthrottled)")
+        sp.add_argument("--rate", type=float, default=1.0,
+                        help="Iris records per second (reference: 1, IrisSource.scala:52); 0 = unthrottled")
         sp.add_argument("--max-batch-latency-ms", type=float, default=None)
         sp.add_argument("--precision", default=None, choices=("fp32", "bf16", "fp8"))
         sp.add_argument("--fallback", default=None, choices=("host", "warn", "error"))
@@ -163,8 +171,9 @@ def build_parser() -> argparse.ArgumentParser:
     sp = sub.add_parser("dynamic")
     sp.add_argument("--models", required=True, help="comma-separated model paths")
     sp.add_argument("--gen-policy", default="random", choices=ControlSource.POLICIES)
-    sp.add_argument("--intervalCheckpoint", type=int, default=1000)
-    sp.add_argument("--maxIntervalControlStream", type=int, default=0)
+    sp.add_argument("--intervalCheckpoint", type=int, default=1000, help="checkpoint interval in ms (0 = off)")
+    sp.add_argument("--maxIntervalControlStream", type=int, default=5000,
+                    help="max random gap between control messages, ms (reference default 5000)")
     sp.add_argument("--control-messages", type=int, default=None)
     sp.add_argument("--checkpoint-dir", default=None)
     sp.add_argument("--restore", default=None)
@@ -173,7 +182,7 @@ def build_parser() -> argparse.ArgumentParser:
     sp = sub.add_parser("checkpoint")
     sp.add_argument("--control-file", default=None)
     sp.add_argument("--socket", default=None, help="host:port, one model path per line")
-    sp.add_argument("--intervalCheckpoint", type=int, default=10)
+    sp.add_argument("--intervalCheckpoint", type=int, default=1000, help="checkpoint interval in ms (0 = off)")
     sp.add_argument("--checkpoint-dir", default=None)
     sp.add_argument("--restore", default=None)
     common(sp)

@@ -58,6 +58,11 @@ class IrisSource(SourceFunction):
         self.version = version
         self._running = True
 
+    @property
+    def live(self) -> bool:
+        """Paced sources block between records: the runtime reads them on a thread of their own."""
+        return bool(self.rate)
+
     def _gen(self) -> Iterator[Iris]:
         rng = random.Random(self.seed)
         i = 0
@@ -97,6 +102,10 @@ class ControlSource(SourceFunction):
         self.seed = seed
         self.version = version
         self._running = True
+
+    @property
+    def live(self) -> bool:
+        return bool(self.max_interval_ms)
 
     def _gen(self) -> Iterator[AddMessage]:
         rng = random.Random(self.seed)

@@ -13,10 +13,11 @@ from .dist import (
     shard_range,
     shutdown,
 )
+from .sinks import GatherSink, gather_varlen
 from .tree_shard import TreeShardedScorer, finish_epilogue, host_partial, tree_shard_supported
 
 __all__ = [
     "DistContext", "all_gather_scores", "all_gather_varlen", "all_to_all_varlen", "broadcast_control", "broadcast_object",
     "broadcast_plan", "broadcast_tensors", "init_from_env", "shard_range", "shutdown",
-    "TreeShardedScorer", "finish_epilogue", "host_partial", "tree_shard_supported",
+    "GatherSink", "gather_varlen", "TreeShardedScorer", "finish_epilogue", "host_partial", "tree_shard_supported",
 ]

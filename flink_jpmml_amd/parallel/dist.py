@@ -44,11 +44,16 @@ class DistContext:
         return (self.world_size > 1 or self.force) and dist.is_available() and dist.is_initialized()
 
     def group(self, name: str):
-        """Named process group: ``"ctrl"`` (gloo, CPU objects: control replication, checkpoint
-        manifests, sink gathers) or ``"model"`` (the data backend: model tensor replication from
-        the loader thread). Separate groups keep the collectives of different threads from
-        interleaving on one communicator. Created eagerly by :func:`init_from_env` (every rank
-        must create groups in the same order)."""
+        """Named process group, one per thread that issues collectives, so the collectives of
+        different threads never interleave on one communicator:
+
+        * ``"ctrl"`` (gloo) — the job thread: checkpoint state gathers, manifest broadcast, sink
+          gathers of host objects;
+        * ``"model"`` (the data backend) — the model-loader thread: parse-once replication;
+        * ``"replicate"`` (gloo) — the leader-read source pump thread (control streams, sockets);
+        * ``"ckpt"`` (gloo) — the checkpoint-coordinator thread (time-based triggers).
+
+        Created eagerly by :func:`init_from_env` (every rank creates them in the same order)."""
         if not self.is_distributed:
             return None
         g = self.groups.get(name)
@@ -98,6 +103,8 @@ def init_from_env(backend: Optional[str] = None, timeout_s: Optional[float] = No
         to = datetime.timedelta(seconds=timeout_s)
         ctx.groups["ctrl"] = dist.new_group(backend="gloo", timeout=to)
         ctx.groups["model"] = dist.new_group(backend=backend, timeout=to)
+        ctx.groups["replicate"] = dist.new_group(backend="gloo", timeout=to)
+        ctx.groups["ckpt"] = dist.new_group(backend="gloo", timeout=to)
     return ctx
 
 

@@ -94,6 +94,12 @@ class DevicePipeline:
         self.slots = [torch.empty(elems, dtype=torch.float32, device=self.device) for _ in range(self.depth)]
         self.slot_elems = elems
 
+    @property
+    def h2d_streams_in_use(self) -> Optional[int]:
+        """Copy streams this pipeline splits each micro-batch over (``None`` before the auto
+        calibration ran)."""
+        return self.n_h2d
+
     def active_h2d(self) -> List:
         """The copy streams in use (calibrated on first use in auto mode)."""
         if self.n_h2d is None:
@@ -357,6 +363,10 @@ class StreamingScorer:
             elif X.is_cuda:
                 if X.dtype != torch.float32 or not X.is_contiguous():
                     X = X.to(torch.float32).contiguous()
+                # device-resident input: the kernels on the compute stream must see the producer's
+                # writes (its current stream), and the allocator must not recycle X while they read
+                self.comp.wait_stream(torch.cuda.current_stream(self.device))
+                X.record_stream(self.comp)
             elif not X.is_pinned() or X.dtype != torch.float32 or not X.is_contiguous():
                 X = _pin(X)
         self._throttle()

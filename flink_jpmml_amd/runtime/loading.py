@@ -124,13 +124,14 @@ def _sync_device(device) -> None:
 def load_replicated(path: str, ctx, device: Any = None, config: Any = None, pipeline: Any = None) -> LoadedModel:
     """Collective over ``ctx``'s ``model`` group (every rank calls it, in the same order): rank 0
     reads, parses and lowers; ranks receive the document and the compiled device tensors."""
+    if ctx is None or not ctx.is_distributed:
+        return load_local(path, device, config, pipeline)
     from ..config import ScoringConfig
     from ..parallel.dist import broadcast_object, broadcast_tensors
     from .compiled import CompiledPmml
-    from .plans import DevicePlan, NotLowerable
+    from .plans import DevicePlan
 
-    if ctx is None or not ctx.is_distributed:
-        return load_local(path, device, config, pipeline)
+
     cfg = config or ScoringConfig()
     g = ctx.group("model")
     t0 = time.perf_counter()
@@ -149,8 +150,11 @@ def load_replicated(path: str, ctx, device: Any = None, config: Any = None, pipe
                     with prange("model.lower"):
                         plan = compiled.plan(device, **cfg.lowering_opts())
                     head["plan_meta"] = plan.export_state()[0]
-                except NotLowerable as e:
-                    head["lower_error"] = str(e)
+                except Exception as e:  # noqa: BLE001 - reported to every rank before the broadcast
+                    # (a lowering error escaping here would leave the peers blocked in the
+                    # broadcast until the timeout): all ranks then fall back or fail alike
+                    plan = None
+                    head["lower_error"] = f"{type(e).__name__}: {e}"
         head = broadcast_object(head, ctx, group=g)
         if "err" in head:
             raise ModelLoadingException(f"model at {path}: {head['err']}")

@@ -32,7 +32,7 @@ from .clock import Clock
 from .functions import CoProcessFunction, SinkFunction, SourceFunction
 from .operators import EvaluationCoFunction, EvaluationFunction, QuickEvaluationFunction
 from .runtime import Executor, JobExecutionResult, Node, SimulatedFailure
-from .sources import BatchSource, CollectionSource, ReplicatedSource, TextBatchSource
+from .sources import BatchSource, CollectionSource, ReplicatedSource, SocketTextSource, TextBatchSource
 from .state import CheckpointStorage
 
 _DIST: dict = {}  # the process's DistContext (process groups are created once per process)
@@ -65,8 +65,12 @@ class FileSink(SinkFunction):
     Elements go to an in-progress buffer; ``pre_commit(cid)`` writes them to
     ``<dir>/part-<rank>-<cid>.pending``; ``commit(cid)`` renames it to ``.jsonl`` once the
     checkpoint manifest is durable (end of input commits the rest as ``part-<rank>-final``).
-    ``recover()`` (called on restore) deletes pending parts of the crashed run, so the committed
-    parts of both runs together equal one uninterrupted run — no duplicates, no gaps."""
+    ``recover(cid)`` (called on restore from checkpoint ``cid``) finishes the crashed run's
+    transactions like Flink's two-phase-commit sink: parts pre-committed for checkpoints
+    ``<= cid`` are covered by the restored manifest and are committed (the process may have died
+    between writing the manifest and renaming them); newer pending parts are discarded (the
+    restored job re-produces them). The committed parts of both runs together equal one
+    uninterrupted run — no duplicates, no gaps."""
 
     def __init__(self, directory: str, encode: Optional[Callable[[Any], Any]] = None):
         self.directory = directory
@@ -105,10 +109,17 @@ class FileSink(SinkFunction):
                 keep.append((c, path))
         self._pending = keep
 
-    def recover(self) -> None:
-        for f in os.listdir(self.directory):
-            if f.startswith(f"part-{self.rank:03d}-") and f.endswith(".pending"):
-                os.remove(os.path.join(self.directory, f))
+    def recover(self, restored_cid: Optional[int] = None) -> None:
+        prefix = f"part-{self.rank:03d}-"
+        for f in sorted(os.listdir(self.directory)):
+            if not (f.startswith(prefix) and f.endswith(".pending")):
+                continue
+            path = os.path.join(self.directory, f)
+            tag = f[len(prefix): -len(".pending")]
+            if tag.isdigit() and restored_cid is not None and int(tag) <= int(restored_cid):
+                os.replace(path, path[: -len(".pending")] + ".jsonl")
+            else:
+                os.remove(path)
 
     @staticmethod
     def read(directory: str) -> List[Any]:
@@ -119,6 +130,53 @@ class FileSink(SinkFunction):
                 with open(os.path.join(directory, f)) as fh:
                     out.extend(json.loads(line) for line in fh if line.strip())
         return out
+
+
+class TextSink(SinkFunction):
+    """``writeAsText(path)`` (`E/EvaluateKmeans.scala:53`, `E/CheckpointEvaluate.scala:97-98`):
+    one line per element, written and flushed **as results arrive** (the file grows while the job
+    runs; at-least-once across restarts, like Flink's ``writeAsText``). Under data parallelism
+    rank ``r`` writes ``<path>.<r>`` unless ``path`` is ``"-"`` (stdout)."""
+
+    def __init__(self, path: str, fmt: Optional[Callable[[Any], str]] = None, flush_every: int = 1):
+        self.path = path
+        self.fmt = fmt or str
+        self.flush_every = max(1, int(flush_every))
+        self._fh = None
+        self._n = 0
+
+    def open(self, context=None) -> None:  # noqa: A003
+        import sys
+
+        if self.path in (None, "-"):
+            self._fh = sys.stdout
+            return
+        path = self.path
+        if context is not None and context.number_of_parallel_subtasks > 1:
+            path = f"{path}.{context.index_of_this_subtask}"
+        d = os.path.dirname(os.path.abspath(path))
+        os.makedirs(d, exist_ok=True)
+        self._fh = open(path, "w")
+
+    def invoke(self, value: Any) -> None:
+        self._fh.write(self.fmt(value) + "\n")
+        self._n += 1
+        if self._n % self.flush_every == 0:
+            self._fh.flush()
+
+    def close(self) -> None:
+        import sys
+
+        if self._fh is not None:
+            self._fh.flush()
+            if self._fh is not sys.stdout:
+                self._fh.close()
+            self._fh = None
+
+    def __getstate__(self):
+        d = dict(self.__dict__)
+        d["_fh"] = None
+        return d
 
 
 def _json_default(x: Any) -> Any:
@@ -154,6 +212,8 @@ class StreamExecutionEnvironment:
         self.dist_ctx = dist_ctx
         self.clock = clock
         self.checkpoint_every: Optional[int] = None
+        self.checkpoint_interval_ms: Optional[float] = None
+        self.input_mode = "auto"
         self.checkpoint_storage = CheckpointStorage()
         self.fail_after: Optional[int] = None
         self.copy_operators = False
@@ -201,14 +261,35 @@ class StreamExecutionEnvironment:
         self.clock = clock
         return self
 
-    def enable_checkpointing(self, every_n_records: int, directory: Optional[str] = None) -> "StreamExecutionEnvironment":
-        """Count-based checkpoint barriers on the primary source's offset (deterministic, aligned
-        across ranks; the reference uses a time interval, `E/DynamicEvaluateKmeans.scala:48`)."""
-        self.checkpoint_every = int(every_n_records)
+    def enable_checkpointing(self, interval_ms: Optional[float] = None, directory: Optional[str] = None,
+                             every_n_records: Optional[int] = None) -> "StreamExecutionEnvironment":
+        """``enableCheckpointing(interval)`` (`E/DynamicEvaluateKmeans.scala:48`): a checkpoint
+        every ``interval_ms`` of processing time — across ranks rank 0 decides and every rank
+        snapshots at its own exact cut. ``every_n_records`` instead places count-based barriers on
+        the primary source's global offset (deterministic: aligned across ranks without
+        communication; for replayable inputs and tests)."""
+        if (interval_ms is None) == (every_n_records is None):
+            raise ValueError("give exactly one of interval_ms / every_n_records")
+        if every_n_records is not None:
+            self.checkpoint_every, self.checkpoint_interval_ms = int(every_n_records), None
+        else:
+            if float(interval_ms) <= 0:
+                raise ValueError("interval_ms must be > 0")
+            self.checkpoint_every, self.checkpoint_interval_ms = None, float(interval_ms)
         if directory is not None:
             self.checkpoint_storage = CheckpointStorage(directory)
         elif self.config is not None and self.config.checkpoint_dir:
             self.checkpoint_storage = CheckpointStorage(self.config.checkpoint_dir)
+        return self
+
+    enableCheckpointing = enable_checkpointing  # noqa: N815
+
+    def set_input_mode(self, mode: str) -> "StreamExecutionEnvironment":
+        """``auto`` (default: live reader threads when any source can block, else the
+        deterministic merge), ``live`` or ``deterministic`` (see :mod:`~flink_jpmml_amd.stream.inputs`)."""
+        if mode not in ("auto", "live", "deterministic"):
+            raise ValueError(f"input mode must be auto / live / deterministic, not {mode!r}")
+        self.input_mode = mode
         return self
 
     def inject_failure(self, after_records: Optional[int]) -> "StreamExecutionEnvironment":
@@ -240,8 +321,8 @@ class StreamExecutionEnvironment:
         (every rank reads it all) or ``leader`` (rank 0 reads, elements are broadcast)."""
         if mode is None:
             mode = "parallel" if hasattr(source, "open_subtask") else "shard"
-        if mode == "leader":
-            source, mode = ReplicatedSource(source, self.dist_ctx), "replicate"
+        if mode == "leader":  # rank 0 reads; elements are sharded, or replicated behind broadcast()
+            source, mode = ReplicatedSource(source, self.dist_ctx), "shard"
         s = self._source(source, name, timestamp, mode)
         if uid:
             s.node.uid = uid
@@ -262,8 +343,21 @@ class StreamExecutionEnvironment:
     fromBatches = from_batches  # noqa: N815
 
     def read_text_batches(self, path: str, model: Any, batch_rows: int = 1 << 16, **kw) -> "DataStream":
-        """Delimited text file → RecordBatches via the native C++ ingest (pinned output)."""
-        return self._source(TextBatchSource(path, model, batch_rows, **kw), "text-batches", None, "shard")
+        """Delimited text file → RecordBatches via the native C++ ingest (pinned output). Under
+        torchrun every rank parses only its own byte range (rank-local split, F3)."""
+        return self._source(TextBatchSource(path, model, batch_rows, **kw), "text-batches", None, "parallel")
+
+    def socket_text_stream(self, host: str, port: int, delimiter: str = "\n", max_retry: int = 0,
+                           uid: Optional[str] = None) -> "DataStream":
+        """``socketTextStream(host, port)`` (`E/CheckpointEvaluate.scala:80-82`): lines read live
+        as they arrive. Under torchrun rank 0 reads and the lines are replicated (behind
+        ``broadcast()`` / ``with_support_stream``) or sharded across ranks."""
+        s = self.add_source(SocketTextSource(host, port, delimiter, max_retry), name="socket", mode="leader")
+        if uid:
+            s.node.uid = uid
+        return s
+
+    socketTextStream = socket_text_stream  # noqa: N815
 
     def from_either(self, sequence: Sequence[Tuple[str, Any]], uid: Optional[str] = None
                     ) -> Tuple["DataStream", "DataStream"]:
@@ -353,6 +447,12 @@ class DataStream:
         return node
 
     addSink = add_sink  # noqa: N815
+
+    def write_as_text(self, path: str, fmt: Optional[Callable[[Any], str]] = None) -> Node:
+        """Streaming text sink (``writeAsText``): the file grows as results arrive."""
+        return self.add_sink(TextSink(path, fmt))
+
+    writeAsText = write_as_text  # noqa: N815
 
     def collect(self, job_name: str = "collect", restore: Optional[str] = None) -> List[Any]:
         """Attach a collecting sink, run the job, return the outputs. Under data parallelism every
@@ -444,4 +544,4 @@ class ConnectedStreams:
 
 
 __all__ = ["CollectSink", "ConnectedStreams", "DataStream", "FileSink", "SimulatedFailure",
-           "StreamExecutionEnvironment"]
+           "StreamExecutionEnvironment", "TextSink"]

@@ -669,7 +669,8 @@ class QuickEvaluationFunction(FlatMapFunction, _ScoringMixin):
     def flat_map(self, value: Any, out: Collector) -> None:
         if isinstance(value, RecordBatch):
             with prange("quick_evaluate.batch"):
-                self._push((self.inner.evaluator.predict_records(value), value), out)
+                self._push((self.inner.evaluator.predict_records(value, keep_device=self.config.device_mirror),
+                            value), out)
             return
         if not self.config.batch_size:
             out.collect(quick_udf(value, self.inner.evaluator))

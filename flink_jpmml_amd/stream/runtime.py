@@ -12,12 +12,20 @@ exactly the semantics the reference's operators depend on:
   every rank is one subtask of every operator** (parallelism = world size, one GPU each): event
   sources are sharded by rank, broadcast (control) streams are replicated to every rank, model
   loads parse once on rank 0 and replicate the compiled tensors (SURVEY §2.6 F1–F5);
-* **deterministic interleaving** of multiple sources (by timestamp when the sources provide one,
-  else round-robin) — the analogue of `T/sources/TemporizedSourceFunction.scala:35-56`;
+* **live, available-first input** (:mod:`~flink_jpmml_amd.stream.inputs`): sources that can block
+  (sockets, paced generators, push sources, leader-read streams) run on reader threads and the job
+  thread processes whichever input has data — an idle control stream never holds events back.
+  Bounded, non-blocking sources and timestamped test harnesses keep a **deterministic merge** (by
+  timestamp when every source provides one, else round-robin — the analogue of
+  `T/sources/TemporizedSourceFunction.scala:35-56`);
 * **processing-time timers** on the job :class:`~flink_jpmml_amd.stream.clock.Clock` (latency
   bound micro-batches flush while a slow source sleeps);
-* **checkpoints** with **source offsets**: count-based barriers on the primary source's global
-  offset, aligned across ranks; ``CheckpointedFunction``s snapshot into operator state (union /
+* **checkpoints** with **source offsets**, either **time-based** (``interval_ms``, the reference's
+  ``enableCheckpointing(ms)``, `E/DynamicEvaluateKmeans.scala:48`; across ranks rank 0 decides and
+  the :class:`~flink_jpmml_amd.stream.coordinator.CheckpointCoordinator` injects the barrier into
+  every rank's input) or **count-based** (barriers on the primary source's global offset, aligned
+  across ranks without communication). Offsets are what each rank *processed* before the barrier
+  (an exact cut, per rank). ``CheckpointedFunction``s snapshot into operator state (union /
   split list state); rank 0 writes one JSON manifest (operator state of every subtask, source
   offsets, sha256 of every served model); transactional sinks pre-commit at the barrier and
   commit after the manifest is durable. ``execute(restore=…)`` re-broadcasts the manifest,
@@ -30,13 +38,12 @@ exactly the semantics the reference's operators depend on:
 from __future__ import annotations
 
 import copy
-import heapq
-import itertools
 import logging
 import time
 from dataclasses import dataclass, field
 from typing import Any, Callable, Dict, Iterator, List, Optional, Tuple
 
+from ..api.batch import RecordBatch
 from ..utils.metrics import METRICS
 from ..utils.profiling import prange
 from .clock import Clock, SystemClock, set_current_clock
@@ -64,9 +71,6 @@ class SimulatedFailure(RuntimeError):
     """Raised by the fault-injection hook (:meth:`StreamExecutionEnvironment.inject_failure`)."""
 
 
-_uid = itertools.count()
-
-
 @dataclass
 class Node:
     kind: str  # source | one | two | sink
@@ -91,6 +95,8 @@ class JobExecutionResult:
     records_in: int
     checkpoints: List[str]
     accumulators: Dict[str, Any] = field(default_factory=dict)
+    elements_in: int = 0
+    input_mode: Optional[str] = None
 
 
 def _encode_state(x: Any) -> Any:
@@ -135,12 +141,16 @@ class Executor:
             for port, (up, part) in enumerate(n.inputs):
                 self.down[id(up)].append((n, part, port))
         self.subtasks: Dict[int, List[_Subtask]] = {}
-        self.records_in = 0
+        self.records_in = 0  # rows (a RecordBatch counts its rows)
+        self.elements_in = 0  # stream elements
         self.checkpoint_paths: List[str] = []
         self.readers: Dict[int, SourceReader] = {}
+        self.processed: Dict[int, int] = {}  # per source: next global offset after what was processed
         self.primary: Optional[Node] = None
         self.next_cid = 1
         self.watchdog = None
+        self.coordinator = None
+        self._next_due: Optional[float] = None
 
     @staticmethod
     def _topo(sinks: List[Node]) -> List[Node]:
@@ -212,7 +222,7 @@ class Executor:
                 if isinstance(op, SinkFunction):
                     op.open(rctx)
                     if self.restore and hasattr(op, "recover"):
-                        op.recover()
+                        op.recover(doc.get("checkpoint_id"))
         for n in self.nodes:
             for st in self.subtasks[id(n)]:
                 st.out = Collector(self._emitter(n, st))
@@ -266,58 +276,80 @@ class Executor:
 
     # ------------------------------------------------------------------ sources
     def _open_readers(self, doc: dict) -> List[Node]:
-        offsets = {uid: int(v.get("offset", 0)) for uid, v in doc.get("sources", {}).items()}
         sources = [n for n in self.nodes if n.kind == "source"]
+        saved = doc.get("sources", {})
         for n in sources:
-            self.readers[id(n)] = SourceReader(n, self.rank, self.world, self.clock, offsets.get(n.uid, 0))
+            entry = saved.get(n.uid, {})
+            off = int(entry.get("offset", 0))
+            ranks = entry.get("ranks")
+            leader = None
+            if ranks is not None and len(ranks) == self.world:
+                off = int(ranks[self.rank])  # per-rank cut of a time-based checkpoint
+                leader = int(min(ranks))
+            elif ranks is not None and n.dist_mode in ("parallel",):
+                raise RuntimeError(f"source {n.uid}: checkpoint was taken at world size {len(ranks)}, "
+                                   f"restoring at {self.world} needs the same rank-local splits")
+            self.readers[id(n)] = SourceReader(n, self.rank, self.world, self.clock, off, leader_offset=leader)
+            self.processed[id(n)] = off
         primaries = [n for n in sources if n.dist_mode != "replicate"] or sources
         self.primary = primaries[0] if primaries else None
         if self.env.checkpoint_every and self.primary is not None:
             done = self.readers[id(self.primary)].offset // self.env.checkpoint_every
             self.next_cid = done + 1
+        elif doc.get("checkpoint_id") is not None:
+            self.next_cid = int(doc["checkpoint_id"]) + 1
         return sources
 
-    def _merged(self, sources: List[Node]) -> Iterator[Tuple[Node, int, Any]]:
-        """Deterministic merge of every source: by timestamp when all sources define one, else
-        round-robin by source (ties broken by source order)."""
-        iters = [(n, iter(self.readers[id(n)])) for n in sources]
-        timed = all(n.timestamp_fn is not None for n in sources) and len(sources) > 1
-        if timed:
-            heap = []
-            for si, (n, it) in enumerate(iters):
-                for g, v in it:
-                    heapq.heappush(heap, (n.timestamp_fn(v), si, next(_uid), n, g, v))
-                    break
-            while heap:
-                _, si, _, n, g, v = heapq.heappop(heap)
-                yield n, g, v
-                for ng, nv in iters[si][1]:
-                    heapq.heappush(heap, (n.timestamp_fn(nv), si, next(_uid), n, ng, nv))
-                    break
+    def _input_mode(self, sources: List[Node]) -> str:
+        from .clock import ManualClock
+        from .inputs import is_live_source
+
+        mode = getattr(self.env, "input_mode", "auto")
+        if mode != "auto":
+            return mode
+        if isinstance(self.clock, ManualClock):
+            return "deterministic"  # virtual time lives on the job thread
+        if self.env.checkpoint_interval_ms and self.dist:
+            return "live"  # barriers arrive from the coordinator thread
+        return "live" if any(is_live_source(n.source) for n in sources) else "deterministic"
+
+    def _check_checkpoint_config(self, sources: List[Node], mode: str) -> None:
+        every = self.env.checkpoint_every
+        if not every or not self.dist:
             return
-        live = list(iters)
-        while live:
-            nxt = []
-            for n, it in live:
-                try:
-                    g, v = next(it)
-                except StopIteration:
-                    continue
-                yield n, g, v
-                nxt.append((n, it))
-            live = nxt
+        prim = self.primary
+        if prim is not None and prim.dist_mode == "parallel":
+            raise ValueError("count-based checkpoints need a globally numbered primary source (shard / either "
+                             "mode); rank-local sources have per-rank lengths: use enable_checkpointing(interval_ms=…)")
+        if mode == "live":
+            raise ValueError("count-based checkpoints across ranks need deterministic input; live sources "
+                             "checkpoint on time: use enable_checkpointing(interval_ms=…)")
 
     # ------------------------------------------------------------------ checkpoints
     def _maybe_checkpoint(self, upto: int) -> None:
-        """Take every checkpoint whose barrier offset is <= ``upto`` (primary-source offset)."""
+        """Take every count-based checkpoint whose barrier offset is <= ``upto`` (primary-source
+        global offset)."""
         every = self.env.checkpoint_every
         if not every:
             return
         while self.next_cid * every <= upto:
-            self._checkpoint(self.next_cid, self.next_cid * every)
+            self._checkpoint(self.next_cid, barrier=self.next_cid * every)
             self.next_cid += 1
 
-    def _checkpoint(self, cid: int, barrier: int) -> None:
+    def _time_checkpoint_due(self) -> None:
+        """Single-process time-based checkpoints: taken between elements on the job thread."""
+        iv = self.env.checkpoint_interval_ms
+        if not iv or self.coordinator is not None:
+            return
+        now = self.clock.now()
+        if self._next_due is None:
+            self._next_due = now + iv / 1e3
+        elif now >= self._next_due:
+            self._checkpoint(self.next_cid)
+            self.next_cid += 1
+            self._next_due = self.clock.now() + iv / 1e3
+
+    def _checkpoint(self, cid: int, barrier: Optional[int] = None) -> None:
         with prange("checkpoint"):
             t0 = time.perf_counter()
             for n in self.nodes:  # flush buffered micro-batches / in-flight scores in topological order
@@ -341,38 +373,40 @@ class Executor:
                         e = per_state.setdefault(name, {"mode": s["mode"], "subtasks": []})
                         e["subtasks"].append(s["items"])
                 operators[n.uid] = per_state
-            sources = {}
+            # source positions = what this rank has *processed* (never what a reader buffered)
+            local_src: Dict[str, int] = {}
             for n in self.nodes:
                 if n.kind == "source":
-                    off = barrier if n is self.primary else self.readers[id(n)].offset
-                    sources[n.uid] = {"offset": off}
+                    local_src[n.uid] = barrier if (barrier is not None and n is self.primary) else \
+                        self.processed[id(n)]
             sinks = [st.op for n in self.nodes if n.kind == "sink" for st in self.subtasks[id(n)]]
             for sk in sinks:
                 if hasattr(sk, "pre_commit"):
                     sk.pre_commit(cid)
             if self.dist:
-                from ..parallel.dist import gather_object
+                from ..parallel.dist import broadcast_object, gather_object
                 from ..utils.faults import guarded_collective
 
                 g = self.dist.group("ctrl")
-                parts = guarded_collective(gather_object, (operators, models), self.dist, group=g,
+                parts = guarded_collective(gather_object, (operators, models, local_src), self.dist, group=g,
                                            what=f"checkpoint {cid} state gather")
                 path = None
                 if self.rank == 0:
                     merged_ops: Dict[str, Dict[str, dict]] = {}
-                    for ops, mods in parts:  # rank order = subtask order
+                    for ops, mods, _ in parts:  # rank order = subtask order
                         models.update(mods)
                         for uid, states in ops.items():
                             for name, s in states.items():
                                 e = merged_ops.setdefault(uid, {}).setdefault(name, {"mode": s["mode"],
                                                                                      "subtasks": []})
                                 e["subtasks"].extend(s["subtasks"])
+                    sources = {uid: {"offset": off, "ranks": [p[2][uid] for p in parts]}
+                               for uid, off in local_src.items()}
                     path = self._write_manifest(cid, merged_ops, sources, models)
-                from ..parallel.dist import broadcast_object
-
                 path = guarded_collective(broadcast_object, path, self.dist, group=g,
                                           what=f"checkpoint {cid} commit")
             else:
+                sources = {uid: {"offset": off} for uid, off in local_src.items()}
                 path = self._write_manifest(cid, operators, sources, models)
             for sk in sinks:
                 if hasattr(sk, "commit"):
@@ -383,18 +417,33 @@ class Executor:
 
     def _write_manifest(self, cid: int, operators, sources, models) -> str:
         payload = {"operators": operators, "sources": sources, "models": models, "records_in": self.records_in,
-                   "world_size": self.world}
+                   "world_size": self.world,
+                   "trigger": "count" if self.env.checkpoint_every else "time"}
         return self.env.checkpoint_storage.write(cid, payload)
 
     # ------------------------------------------------------------------ run
-    def _finish_input(self) -> None:
+    def _finish_input(self, inputs) -> None:
         """End of input: align the last checkpoints across ranks, flush every operator, commit
         sinks."""
         if self.env.checkpoint_every and self.primary is not None:
-            # every rank iterates the whole logical stream (skipping other ranks' elements), so the
-            # final global offset is known locally: no collective that could interleave with a
+            # the final global offset is known locally (strided sources report their global
+            # length, filtered ones read everything): no collective that could interleave with a
             # peer's last in-stream checkpoint
             self._maybe_checkpoint(self.readers[id(self.primary)].offset)
+        if self.coordinator is not None:
+            # a finished rank keeps taking the checkpoints its peers trigger until all are done
+            self.coordinator.finish_input()
+            for m in inputs.markers():
+                if self.watchdog is not None:
+                    self.watchdog.kick()
+                if m.kind == "barrier":
+                    self._checkpoint(m.cid)
+                    self.next_cid = m.cid + 1
+                elif m.kind == "error":
+                    raise m.exc
+                elif m.kind == "stop":
+                    break
+                self.clock.fire_due()
         for n in self.nodes:  # flush buffered micro-batches, in topological order
             for st in self.subtasks[id(n)]:
                 if hasattr(st.op, "end_of_input"):
@@ -407,40 +456,84 @@ class Executor:
                     if hasattr(st.op, "commit"):
                         st.op.commit(-1)
 
+    def _make_inputs(self, sources: List[Node], mode: str):
+        from .inputs import DeterministicInputs, LiveInputs
+
+        if mode == "live":
+            poll = 0.05
+            cfg = self.env.config
+            if cfg is not None and cfg.watchdog_s:
+                poll = min(poll, cfg.watchdog_s / 4)
+            if self.env.checkpoint_interval_ms:
+                poll = min(poll, self.env.checkpoint_interval_ms / 4e3)
+            return LiveInputs(sources, self.readers, self.clock, poll_s=poll)
+        return DeterministicInputs(sources, self.readers)
+
     def run(self, job_name: str) -> JobExecutionResult:
         t0 = time.perf_counter()
         self.clock.bind_thread()
         set_current_clock(self.clock)
         cfg = self.env.config
+        inputs = None
         try:
             doc = self._restored_doc()
             self._instantiate(doc)
             sources = self._open_readers(doc)
+            mode = self._input_mode(sources)
+            self.input_mode = mode
+            self._check_checkpoint_config(sources, mode)
+            inputs = self._make_inputs(sources, mode)
+            if self.env.checkpoint_interval_ms and self.dist:
+                from .coordinator import CheckpointCoordinator
+
+                self.coordinator = CheckpointCoordinator(self.dist, self.env.checkpoint_interval_ms / 1e3,
+                                                         inputs.inject, first_cid=self.next_cid).start()
             if self.dist and cfg is not None and cfg.watchdog_s:
                 from ..utils.faults import Watchdog
 
                 self.watchdog = Watchdog(cfg.watchdog_s, name=f"rank{self.rank}").start()
             fail_after = self.env.fail_after
-            for n, g, v in self._merged(sources):
-                if n is self.primary:
-                    self._maybe_checkpoint(g)
-                self.records_in += 1
-                if fail_after is not None and self.records_in > fail_after:
-                    raise SimulatedFailure(f"injected failure after {fail_after} records")
-                if self.dist is not None:
-                    from ..utils.faults import injector
+            count_ckpt = bool(self.env.checkpoint_every)
+            time_ckpt = bool(self.env.checkpoint_interval_ms)
+            primary = self.primary
+            dist_hooks = self.dist is not None
+            for item in inputs:
+                if type(item) is tuple:
+                    n, g, v = item
+                    if count_ckpt and n is primary:
+                        self._maybe_checkpoint(g)
+                    self.processed[id(n)] = g + 1
+                    self.elements_in += 1
+                    self.records_in += len(v) if isinstance(v, RecordBatch) else 1
+                    if fail_after is not None and self.elements_in > fail_after:
+                        raise SimulatedFailure(f"injected failure after {fail_after} records")
+                    if dist_hooks:
+                        from ..utils.faults import injector
 
-                    injector().on_batch(self.rank, self.records_in - 1)
-                for st in self.subtasks[id(n)]:
-                    st.out.collect(v)
+                        injector().on_batch(self.rank, self.elements_in - 1)
+                    for st in self.subtasks[id(n)]:
+                        st.out.collect(v)
+                        break
+                elif item.kind == "barrier":
+                    self._checkpoint(item.cid)
+                    self.next_cid = item.cid + 1
+                elif item.kind == "error":
+                    raise item.exc
+                elif item.kind == "stop":  # pragma: no cover - only after end of input
                     break
                 if self.watchdog is not None:
                     self.watchdog.kick()
                 self.clock.fire_due()
-            self._finish_input()
+                if time_ckpt:
+                    self._time_checkpoint_due()
+            self._finish_input(inputs)
         except Exception as e:  # noqa: BLE001 - any operator failure fails the job
             raise JobExecutionException(f"Job '{job_name}' failed: {type(e).__name__}: {e}") from e
         finally:
+            if self.coordinator is not None:
+                self.coordinator.stop()
+            if inputs is not None:
+                inputs.close()
             if self.watchdog is not None:
                 self.watchdog.stop()
             self.clock.timers.clear()
@@ -453,7 +546,9 @@ class Executor:
                         except Exception:  # noqa: BLE001
                             logger.exception("close() failed")
         METRICS.inc("job.records_in", self.records_in)
-        return JobExecutionResult(job_name, (time.perf_counter() - t0) * 1e3, self.records_in, self.checkpoint_paths)
+        METRICS.inc("job.elements_in", self.elements_in)
+        return JobExecutionResult(job_name, (time.perf_counter() - t0) * 1e3, self.records_in, self.checkpoint_paths,
+                                  elements_in=self.elements_in, input_mode=getattr(self, "input_mode", None))
 
 
 def _clone(op: Any) -> Any:

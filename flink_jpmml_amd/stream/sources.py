@@ -22,8 +22,11 @@ from __future__ import annotations
 
 import itertools
 import logging
+import os
 import queue
+import socket
 import threading
+import time
 from typing import Any, Callable, Iterable, Iterator, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -48,6 +51,15 @@ class CollectionSource(SourceFunction):
 
     def seek(self, offset: int) -> Iterator[Any]:
         return iter(self.items[offset:])
+
+    def iterate_shard(self, rank: int, world: int, start: int = 0) -> Iterator[Tuple[int, Any]]:
+        """This rank's elements (global offset ``g % world == rank``, ``g >= start``) only."""
+        first = start + ((rank - start) % world)
+        for g in range(first, len(self.items), world):
+            yield g, self.items[g]
+
+    def global_length(self) -> int:
+        return len(self.items)
 
     def __len__(self) -> int:
         return len(self.items)
@@ -85,8 +97,34 @@ class BatchSource(SourceFunction):
                 yield RecordBatch(X[s:s + step], model_id=self.model_id, offset=row)
                 row += min(step, n - s)
 
+    def _is_matrix(self) -> bool:
+        return hasattr(self.data, "shape") and len(getattr(self.data, "shape", ())) == 2
+
+    def global_length(self) -> int:
+        n = int(self.data.shape[0])
+        step = int(self.batch_rows or n) or 1
+        return self.repeat * ((n + step - 1) // step)
+
+    def iterate_shard(self, rank: int, world: int, start: int = 0) -> Iterator[Tuple[int, RecordBatch]]:
+        """Rank-local slices of a matrix source: batch ``g`` belongs to rank ``g % world``; only
+        this rank's batches are cut (views, no copies). Iterables fall back to filtering."""
+        if not self._is_matrix():
+            for g, b in enumerate(self.iterate()):
+                if g >= start and g % world == rank:
+                    yield g, b
+            return
+        X = self.data
+        n = int(X.shape[0])
+        step = int(self.batch_rows or n) or 1
+        per = (n + step - 1) // step
+        first = start + ((rank - start) % world)
+        for g in range(first, self.global_length(), world):
+            rep, k = divmod(g, per)
+            s = k * step
+            yield g, RecordBatch(X[s:s + step], model_id=self.model_id, offset=rep * n + s)
+
     def iterate(self) -> Iterator[RecordBatch]:
-        if hasattr(self.data, "shape") and len(getattr(self.data, "shape", ())) == 2:
+        if self._is_matrix():
             return self._matrix_batches()
 
         def gen():
@@ -126,26 +164,51 @@ class TextBatchSource(SourceFunction):
             return m.compiled
         return CompiledPmml.load(getattr(m, "source_path", m))
 
+    _rank = 0
+    _world = 1
+    bytes_parsed = 0
+
+    def open_subtask(self, rank: int, world: int) -> None:
+        """Rank-local split: this rank parses only the lines that *start* in its
+        ``1/world`` byte range of the data section — every input byte is parsed by exactly one
+        rank, and no rank reads the others' lines."""
+        self._rank, self._world = int(rank), int(world)
+
+    def _line_start_at_or_after(self, fh, p: int, data_start: int) -> int:
+        if p <= data_start:
+            return data_start
+        fh.seek(p - 1)
+        return p - 1 + len(fh.readline())
+
     def iterate(self) -> Iterator[RecordBatch]:
         from .. import native
+        from ..utils.metrics import METRICS
 
         compiled = self._compiled()
         F = compiled.n_features
+        self.bytes_parsed = 0
         with open(self.path, "rb") as fh:
-            head = fh.readline()
+            size = os.fstat(fh.fileno()).st_size
             cols = self.columns
+            data_start = 0
             if cols is None:
+                head = fh.readline()
+                data_start = len(head)
                 cols = [h.strip().strip('"') for h in head.decode(errors="replace").strip().split(self.delimiter)]
-            else:
-                fh.seek(0)
             parser = native.RecordParser(compiled, cols, delimiter=self.delimiter, threads=self.threads)
+            span = size - data_start
+            lo = self._line_start_at_or_after(fh, data_start + span * self._rank // self._world, data_start)
+            hi = self._line_start_at_or_after(fh, data_start + span * (self._rank + 1) // self._world, data_start)
+            fh.seek(lo)
+            left = hi - lo
             rest = b""
             row = 0
-            eof = False
+            eof = left <= 0
             while not eof or rest:
                 if not eof and len(rest) < self.chunk_bytes:
-                    blk = fh.read(self.chunk_bytes)
-                    eof = not blk
+                    blk = fh.read(min(self.chunk_bytes, left))
+                    left -= len(blk)
+                    eof = not blk or left <= 0
                     rest += blk
                     if eof and rest and not rest.endswith(b"\n"):
                         rest += b"\n"
@@ -157,6 +220,8 @@ class TextBatchSource(SourceFunction):
                 m, used = parser.parse(rest, out=rb.X.numpy(), max_rows=self.batch_rows)
                 if used == 0:
                     break
+                self.bytes_parsed += min(used, len(rest))
+                METRICS.inc("ingest.bytes_parsed", min(used, len(rest)))
                 rest = rest[used:]
                 rb = RecordBatch(rb.X[: len(m)], model_id=self.model_id, offset=row)
                 row += len(m)
@@ -168,6 +233,8 @@ class ThreadedSource(SourceFunction):
     """Runs a push-style ``SourceFunction.run(ctx)`` (which may block / sleep forever) on its own
     thread; the job thread pulls its elements through a bounded queue, firing timers while it
     waits (so latency-bound micro-batches flush between slow records)."""
+
+    live = True
 
     def __init__(self, inner: SourceFunction, capacity: int = 1024):
         self.inner = inner
@@ -202,28 +269,37 @@ class ThreadedSource(SourceFunction):
 
 class ReplicatedSource(SourceFunction):
     """A source only rank 0 can read (a socket, a queue): rank 0 iterates it and every element is
-    broadcast to all ranks on the control process group; all ranks then see the
-    same sequence. Replication runs on a background thread per rank."""
+    broadcast to all ranks; all ranks then see the same sequence. Replication runs
+    on a background pump thread per rank, on the dedicated ``replicate`` process group — no other
+    thread issues collectives on it, so they cannot interleave with the job thread's checkpoint
+    collectives on ``ctrl``. ``start`` is where the leader resumes after a restore."""
+
+    live = True
 
     def __init__(self, inner: Any, ctx=None):
         self.inner = inner
         self.ctx = ctx
 
-    def iterate(self, clock: Optional[Clock] = None) -> Iterator[Any]:
+    def cancel(self) -> None:
+        cancel = getattr(self.inner, "cancel", None)
+        if callable(cancel):
+            cancel()
+
+    def iterate(self, clock: Optional[Clock] = None, start: int = 0) -> Iterator[Any]:
         from ..parallel.dist import broadcast_object
 
         ctx = self.ctx
         if ctx is None or not ctx.is_distributed:
-            yield from iter_source(self.inner, clock)
+            yield from iter_source(self.inner, clock, start)
             return
         clock = clock or current_clock()
         q: "queue.Queue" = queue.Queue(1024)
         err: List[BaseException] = []
-        group = ctx.group("ctrl")
+        group = ctx.group("replicate")
 
         def pump():
             try:
-                it = iter_source(self.inner, None) if ctx.is_root else None
+                it = iter_source(self.inner, None, start) if ctx.is_root else None
                 while True:
                     x = None
                     if ctx.is_root:
@@ -249,9 +325,95 @@ class ReplicatedSource(SourceFunction):
             yield x
 
 
+class SocketTextSource(SourceFunction):
+    """``socketTextStream(host, port)`` (the reference's control stream,
+    `E/CheckpointEvaluate.scala:80-82`): one element per delimited line, read **live** as the
+    lines arrive (never to EOF first). ``max_retry`` reconnects (with ``retry_delay_s``) when
+    the connection cannot be opened or drops, like Flink's ``SocketTextStreamFunction``; the
+    stream ends when the peer closes and no retry is left. Under ``torchrun`` the environment
+    reads it on rank 0 and replicates the lines (leader mode)."""
+
+    live = True
+
+    def __init__(self, host: str, port: int, delimiter: str = "\n", max_retry: int = 0,
+                 retry_delay_s: float = 0.5, connect_timeout_s: float = 10.0):
+        self.host = host
+        self.port = int(port)
+        self.delimiter = delimiter
+        self.max_retry = int(max_retry)
+        self.retry_delay_s = float(retry_delay_s)
+        self.connect_timeout_s = float(connect_timeout_s)
+        self._running = True
+        self._sock: Optional[socket.socket] = None
+
+    def cancel(self) -> None:
+        self._running = False
+        s = self._sock
+        if s is not None:
+            try:
+                s.shutdown(socket.SHUT_RDWR)
+            except OSError:
+                pass
+
+    def _connect(self) -> Optional[socket.socket]:
+        deadline = time.monotonic() + self.connect_timeout_s
+        while self._running:
+            try:
+                return socket.create_connection((self.host, self.port), timeout=self.connect_timeout_s)
+            except OSError:
+                if time.monotonic() >= deadline:
+                    raise
+                time.sleep(0.05)
+        return None
+
+    def iterate(self) -> Iterator[str]:
+        attempts = 0
+        delim = self.delimiter.encode()
+        while self._running:
+            try:
+                s = self._connect()
+            except OSError:
+                if attempts >= self.max_retry:
+                    raise
+                attempts += 1
+                time.sleep(self.retry_delay_s)
+                continue
+            if s is None:
+                return
+            self._sock = s
+            s.settimeout(None)
+            buf = b""
+            try:
+                while self._running:
+                    try:
+                        blk = s.recv(1 << 16)
+                    except OSError:
+                        blk = b""
+                    if not blk:
+                        break
+                    buf += blk
+                    while True:
+                        i = buf.find(delim)
+                        if i < 0:
+                            break
+                        line, buf = buf[:i], buf[i + len(delim):]
+                        yield line.decode(errors="replace").rstrip("\r")
+            finally:
+                self._sock = None
+                s.close()
+            if buf.strip():
+                yield buf.decode(errors="replace").rstrip("\r")
+            if attempts >= self.max_retry:
+                return
+            attempts += 1
+            time.sleep(self.retry_delay_s)
+
+
 def iter_source(src: Any, clock: Optional[Clock] = None, offset: int = 0) -> Iterator[Any]:
     """Iterator over a source's elements starting at ``offset`` (seek when supported)."""
-    if isinstance(src, (ThreadedSource, ReplicatedSource)):
+    if isinstance(src, ReplicatedSource):
+        return src.iterate(clock, offset)
+    if isinstance(src, ThreadedSource):
         it = src.iterate(clock)
     elif hasattr(src, "seek") and offset:
         return iter(src.seek(offset))
@@ -272,15 +434,25 @@ def iter_source(src: Any, clock: Optional[Clock] = None, offset: int = 0) -> Ite
 
 
 class SourceReader:
-    """Reads one source node for subtask ``rank`` of ``world``, tracking the global offset."""
+    """Reads one source node for subtask ``rank`` of ``world``, tracking the global offset.
 
-    def __init__(self, node, rank: int = 0, world: int = 1, clock: Optional[Clock] = None, offset: int = 0):
+    ``shard`` mode is rank-local: sources implementing ``iterate_shard(rank, world, start)`` (the
+    collections and columnar matrices here) hand this rank only its own elements — the other
+    ranks' elements are never materialised. Other sources are read in full and filtered
+    (``source.foreign_elements`` counts what that costs). ``leader_offset`` is where a leader-read
+    replicated source resumes (the minimum over ranks); this rank then skips to its own ``offset``.
+    """
+
+    def __init__(self, node, rank: int = 0, world: int = 1, clock: Optional[Clock] = None, offset: int = 0,
+                 leader_offset: Optional[int] = None):
         self.node = node
         self.rank = rank
         self.world = world
         self.mode = node.dist_mode if world > 1 else "all"
         self.offset = int(offset)  # global elements consumed (next element's global index)
         self.l_count = 0  # "either" mode: L elements seen (round-robin key)
+        self._strided = False
+        self._skip_until = 0
         src = node.source
         if self.mode == "parallel" and hasattr(src, "open_subtask"):
             src.open_subtask(rank, world)
@@ -291,22 +463,47 @@ class SourceReader:
                 tag, _ = next(self._it)
                 if tag == "L":
                     self.l_count += 1
+        elif self.mode == "shard" and callable(getattr(src, "iterate_shard", None)):
+            self._strided = True
+            self._it = src.iterate_shard(rank, world, offset)
+        elif isinstance(src, ReplicatedSource) and leader_offset is not None and leader_offset < offset:
+            self._it = iter_source(src, clock, leader_offset)
+            self._skip_until = offset
+            self.offset = int(leader_offset)
         else:
             self._it = iter_source(src, clock, offset)
 
     def __iter__(self) -> Iterator[Tuple[int, Any]]:
-        for x in self._it:
-            g = self.offset
-            self.offset += 1
-            if self.mode == "shard" and g % self.world != self.rank:
-                continue
-            if self.mode == "either" and x[0] == "L":
-                keep = self.l_count % self.world == self.rank
-                self.l_count += 1
-                if not keep:
+        if self._strided:  # (global offset, element) pairs of this rank only
+            for g, x in self._it:
+                self.offset = g + 1
+                yield g, x
+            total = getattr(self.node.source, "global_length", None)
+            if callable(total):
+                self.offset = max(self.offset, int(total()))
+            return
+        foreign = 0
+        try:
+            for x in self._it:
+                g = self.offset
+                self.offset += 1
+                if g < self._skip_until:
                     continue
-            yield g, x
+                if self.mode == "shard" and g % self.world != self.rank:
+                    foreign += 1
+                    continue
+                if self.mode == "either" and x[0] == "L":
+                    keep = self.l_count % self.world == self.rank
+                    self.l_count += 1
+                    if not keep:
+                        continue
+                yield g, x
+        finally:
+            if foreign:
+                from ..utils.metrics import METRICS
+
+                METRICS.inc("source.foreign_elements", foreign)
 
 
-__all__ = ["BatchSource", "CollectionSource", "GeneratorSource", "ReplicatedSource", "SourceReader",
-           "TextBatchSource", "ThreadedSource", "iter_source"]
+__all__ = ["BatchSource", "CollectionSource", "GeneratorSource", "ReplicatedSource", "SocketTextSource",
+           "SourceReader", "TextBatchSource", "ThreadedSource", "iter_source"]

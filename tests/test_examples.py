@@ -1,36 +1,47 @@
 """Example jobs run end to end on CPU (reference `E/*.scala`)."""
 
-from flink_jpmml_amd.domain import Prediction
+from flink_jpmml_amd.domain import Target
 from flink_jpmml_amd.examples import jobs
 from flink_jpmml_amd.examples.sources import ControlSource, IrisSource, ids_and_paths
 
 
 def test_quick_and_evaluate(fixtures_dir, tmp_path):
-    out = jobs.main(["quick", "--model", fixtures_dir["kmeans"], "--output", str(tmp_path / "q.txt"), "--records", "20"])
+    out = jobs.main(["quick", "--model", fixtures_dir["kmeans"], "--output", str(tmp_path / "q.txt"), "--records", "20",
+                     "--rate", "0"])
     assert out == 0
     lines = (tmp_path / "q.txt").read_text().splitlines()
     assert len(lines) == 20 and all(line.startswith("(Prediction(Score(") for line in lines)
     jobs.main(["evaluate", "--model", fixtures_dir["kmeans"], "--output", str(tmp_path / "e.txt"), "--records", "10",
-               "--batch-size", "4"])
+               "--batch-size", "4", "--rate", "0"])
     assert len((tmp_path / "e.txt").read_text().splitlines()) == 10
 
 
 def test_dynamic_finite(fixtures_dir, tmp_path):
     args = jobs.build_parser().parse_args(["dynamic", "--models", f"{fixtures_dir['kmeans']},{fixtures_dir['kmeans41']}",
                                            "--output", str(tmp_path / "d.txt"), "--gen-policy", "finite",
-                                           "--records", "30", "--intervalCheckpoint", "7",
+                                           "--records", "30", "--intervalCheckpoint", "20", "--rate", "200",
+                                           "--maxIntervalControlStream", "50",
                                            "--checkpoint-dir", str(tmp_path / "ck")])
     out = jobs.dynamic_evaluate_kmeans(args)
     assert len(out) == 30
-    assert all(isinstance(p, Prediction) for _, p in out)
+    assert all(isinstance(t, Target) for _, t in out)
+    assert len((tmp_path / "d.txt").read_text().splitlines()) == 30
     assert (tmp_path / "ck").exists() and any((tmp_path / "ck").iterdir())
 
 
 def test_checkpoint_example_with_control_file(fixtures_dir, tmp_path):
     cf = tmp_path / "paths.txt"
     cf.write_text(fixtures_dir["kmeans"] + "\n")
-    jobs.main(["checkpoint", "--control-file", str(cf), "--output", str(tmp_path / "c.txt"), "--records", "12"])
+    jobs.main(["checkpoint", "--control-file", str(cf), "--output", str(tmp_path / "c.txt"), "--records", "12",
+               "--rate", "0"])
     assert len((tmp_path / "c.txt").read_text().splitlines()) == 12
+
+
+def test_reference_defaults():
+    """Defaults are the reference's (`E/util/DynamicParams.scala:38-40`, `E/sources/IrisSource.scala:52`)."""
+    args = jobs.build_parser().parse_args(["dynamic", "--models", "a.xml", "--output", "-"])
+    assert args.maxIntervalControlStream == 5000 and args.intervalCheckpoint == 1000 and args.rate == 1.0
+    assert IrisSource(None, rate=1.0).live and ControlSource({}, "finite", max_interval_ms=5000).live
 
 
 def test_sources_policies():

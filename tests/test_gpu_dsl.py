@@ -161,3 +161,76 @@ def test_rccl_one_rank_group_executes_every_collective(gpu, fixtures_dir, tmp_pa
     res = json.loads(r.stdout.strip().splitlines()[-1])
     assert res["n_out"] == 3 and res["replicated"] >= 2 and res["bytes_bcast"] > 0
     assert res["gather_ok"] and res["var_ok"] == 123 and "AddMessage" in res["ctrl"]
+
+
+def test_device_resident_batch_scored_right_after_producer(gpu, tmp_path):
+    """a RecordBatch built on the default stream and scored immediately — the compute
+    stream must wait for the producer (and keep X alive); compare with the oracle."""
+    import torch
+
+    from flink_jpmml_amd.api.batch import RecordBatch
+    from flink_jpmml_amd.api.pmml_model import PmmlModel
+    from flink_jpmml_amd.bench.synth import stream_matrix
+    from flink_jpmml_amd.config import ScoringConfig
+    from flink_jpmml_amd.runtime.compiled import CompiledPmml
+
+    path = _gbdt_file(tmp_path, n_trees=300, depth=6, n_features=16, seed=8)
+    model = PmmlModel.from_path(path).bind(gpu, ScoringConfig(device=gpu, fallback="error"))
+    X = stream_matrix(200_000, 16, seed=6, missing_rate=0.01)
+    Xd0 = torch.from_numpy(X).to(gpu)
+    outs = []
+    for k in range(4):  # the producer writes X on the default stream, a long kernel right before
+        Xd = torch.empty_like(Xd0)
+        big = torch.randn(4096, 4096, device=gpu)
+        _ = big @ big  # keep the default stream busy so a missing wait would read garbage
+        Xd.copy_(Xd0 * 1.0)
+        outs.append(model.predict(RecordBatch(Xd)))
+        del Xd  # dropped right away: the allocator must not hand it out under the kernel
+    ref, vref = CompiledPmml.from_string(open(path).read()).score_matrix_oracle(X)
+    for pb in outs:
+        assert (pb.valid == vref).all()
+        np.testing.assert_allclose(pb.scores[vref], ref[vref], atol=2e-5, rtol=0)
+
+
+GATHER_SCRIPT = r"""
+import os, sys, json
+sys.path.insert(0, os.environ["FJA_ROOT"])
+import numpy as np, torch
+from flink_jpmml_amd import ModelReader
+from flink_jpmml_amd.config import ScoringConfig
+from flink_jpmml_amd.parallel.sinks import GatherSink
+from flink_jpmml_amd.stream import StreamExecutionEnvironment
+gbdt = sys.argv[1]
+out = {}
+for lockstep in (False, True):
+    env = StreamExecutionEnvironment.get_execution_environment(force_distributed=True,
+        config=ScoringConfig(device="cuda", fallback="error", device_mirror=True))
+    X = np.random.default_rng(3).standard_normal((60000, 16)).astype(np.float32)
+    sink = GatherSink(to="all", lockstep=lockstep)
+    env.from_batches(torch.from_numpy(X).pin_memory(), batch_rows=15000).quick_evaluate(ModelReader(gbdt)).add_sink(sink)
+    env.execute("gather")
+    order = np.argsort(sink.offsets, kind="stable")
+    out[str(lockstep)] = {"rows": int(len(sink.offsets)), "scores": sink.scores[order].tolist()[:50],
+                          "valid": int(sink.valid.sum())}
+from flink_jpmml_amd.runtime.compiled import CompiledPmml
+ref, v = CompiledPmml.from_string(open(gbdt).read()).score_matrix_oracle(X)
+out["ref"] = ref[:50].tolist(); out["ref_valid"] = int(v.sum())
+print(json.dumps(out))
+"""
+
+
+def test_gather_sink_rccl_device_path(gpu, tmp_path):
+    """The library F5 sink on a 1-rank RCCL group: device mirrors gathered with
+    all_gather_into_tensor on the sink's comm stream (buffered and lockstep cadences)."""
+    import json
+
+    gbdt = _gbdt_file(tmp_path, n_trees=64, depth=5, n_features=16, seed=1)
+    env = dict(os.environ, FJA_ROOT=ROOT, MASTER_ADDR="127.0.0.1", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, "-c", GATHER_SCRIPT, gbdt], env=env, capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    for key in ("False", "True"):
+        assert res[key]["rows"] == 60000 and res[key]["valid"] == res["ref_valid"]
+        np.testing.assert_allclose(res[key]["scores"], res["ref"], atol=2e-5, rtol=0)
