@@ -72,9 +72,10 @@ class RecordBatch:
         X, absent, ok = pack_vectors_masked(vectors, width)
         # float64 on the host (the oracle then matches per-record predict bit for bit); the device
         # path stages it as float32 like every other input
-        b = RecordBatch(X, model_id=model_id, absent=absent if absent.any() else None,
-                        payload=payload)
-        b._size_ok = ok if not ok.all() else None
+        if absent is not None and not absent.any() and not np.isnan(X).any():
+            absent = None  # no NaN at all: "every NaN is absent" and "nothing absent" coincide
+        b = RecordBatch(X, model_id=model_id, absent=absent, payload=payload)
+        b._size_ok = ok if ok is not None and not ok.all() else None
         return b
 
     @staticmethod
@@ -266,7 +267,25 @@ class PredictionBatch:
             yield Prediction(Score(float(s[i]))) if v[i] else EMPTY_PREDICTION
 
     def to_list(self) -> List[Prediction]:
-        return list(self)
+        return self.predictions()
+
+    def predictions(self) -> List[Prediction]:
+        """Every row as a :class:`Prediction` (one vectorised pass; the per-record streams'
+        output path)."""
+        valid = self.valid
+        from ..native import fastpath
+
+        fp = fastpath()
+        if fp is not None:
+            s = np.ascontiguousarray(self.scores, dtype=np.float32)
+            out = fp.make_predictions(s, np.ascontiguousarray(valid), Prediction, Score, EMPTY_PREDICTION)
+            if out is not None:
+                return out
+        out = list(map(Prediction, map(Score, self.scores.tolist())))
+        if not valid.all():
+            for i in np.flatnonzero(~valid).tolist():
+                out[i] = EMPTY_PREDICTION
+        return out
 
     def empty_count(self) -> int:
         return int(self._n - np.count_nonzero(self.valid))

@@ -240,7 +240,7 @@ class PmmlModel(Pipeline):
         if not isinstance(scores, np.ndarray):
             scores = scores.detach().cpu().numpy()
             valid = valid.detach().cpu().numpy()
-        valid = np.asarray(valid, dtype=bool) & ok_size
+        valid = np.asarray(valid, dtype=bool) if ok_size is None else np.asarray(valid, dtype=bool) & ok_size
         return [Prediction(Score(float(s))) if v else Prediction(EmptyScore) for s, v in zip(scores, valid)]
 
     def __repr__(self) -> str:

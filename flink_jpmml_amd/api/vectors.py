@@ -118,8 +118,21 @@ def pack_vectors_masked(vectors: Iterable[VectorLike], width: int):
     ``absent[i, j]`` marks entries a sparse vector does not store (the only positions the
     reference's ``replaceNaN`` fills, `S/api/PmmlModel.scala:143-152`; a NaN *stored* in a vector
     is kept as a PMML missing value) and ``ok[i]`` is False for vectors whose size is not
-    ``width`` (their row is all-NaN; the per-record path fails their validation)."""
-    vs: List[Vector] = [as_vector(v) for v in vectors]
+    ``width`` (their row is all-NaN; the per-record path fails their validation).
+
+    Fast path: a batch of equal-width DenseVectors is one ``np.stack`` and returns ``ok=None``
+    (every row conforms) and ``absent=None`` when no entry is NaN (nothing to tell apart); stored
+    NaNs get an all-False mask so ``replace_nan`` leaves them missing, as per record."""
+    vs = vectors if isinstance(vectors, list) else list(vectors)
+    fp = _fastpath()
+    if fp is not None and vs:
+        X = np.empty((len(vs), width))
+        if fp.pack_dense(vs, DenseVector, int(width), X) >= 0:
+            return X, (np.zeros(X.shape, dtype=bool) if np.isnan(X).any() else None), None
+    if vs and all(type(v) is DenseVector and len(v.data) == width for v in vs):
+        X = np.concatenate([v.data for v in vs]).reshape(len(vs), width)
+        return X, (np.zeros(X.shape, dtype=bool) if np.isnan(X).any() else None), None
+    vs = [as_vector(v) for v in vs]
     n = len(vs)
     out = np.full((n, width), np.nan)
     absent = np.zeros((n, width), dtype=bool)
@@ -135,6 +148,12 @@ def pack_vectors_masked(vectors: Iterable[VectorLike], width: int):
         else:
             out[i, :] = v.data
     return out, absent, ok
+
+
+def _fastpath():
+    from ..native import fastpath
+
+    return fastpath()
 
 
 def to_csr(vectors: Sequence[VectorLike], width: int):

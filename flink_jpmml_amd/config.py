@@ -30,6 +30,10 @@ class ScoringConfig:
     batch_size: Optional[int] = None
     """Flush a per-record micro-batch once it holds this many records (``None`` = score each record
     as it arrives, exactly the reference's call pattern)."""
+    udf_mode: str = "deferred"
+    """How a micro-batched per-record UDF is run: ``deferred`` — exactly once per event, its
+    ``predict`` calls resolved when the batch is scored; ``replay`` — capture, batch score, replay
+    (the UDF runs twice: pure UDFs that read the score inside ``f`` batch fully)."""
     max_batch_latency_ms: Optional[float] = None
     """Flush a non-empty micro-batch once its oldest record has waited this long (size-or-time
     trigger). ``None`` = size, control message, checkpoint barrier or end of input only."""
@@ -83,6 +87,8 @@ class ScoringConfig:
     def __post_init__(self) -> None:
         if self.precision not in PRECISIONS:
             raise ValueError(f"precision must be one of {PRECISIONS}, got {self.precision!r}")
+        if self.udf_mode not in ("deferred", "replay"):
+            raise ValueError(f"udf_mode must be 'deferred' or 'replay', got {self.udf_mode!r}")
         if self.fallback not in FALLBACKS:
             raise ValueError(f"fallback must be one of {FALLBACKS}, got {self.fallback!r}")
         if self.batch_size is not None and int(self.batch_size) < 1:

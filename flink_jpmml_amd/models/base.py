@@ -155,12 +155,25 @@ class ModelEvaluator:
                 col[i] = self.schema.lookup(name, lab)
         return col
 
+    def _encode_result_labels(self, name: str, res: ModelResult) -> np.ndarray:
+        """Vectorised ``_encode_label(name, res.label_strings())``: the field encoding of each of
+        the K categories / entities is looked up once, then gathered by the winning index."""
+        labels = res.categories if res.kind == "classification" else \
+            res.entity_ids if res.kind == "clustering" else None
+        if labels is None:
+            return np.full(res.n, NAN)
+        codes = np.array([self.schema.lookup(name, lab) if lab is not None else NAN for lab in labels] + [NAN])
+        v = np.asarray(res.value, dtype=np.float64)
+        ok = np.asarray(res.valid, dtype=bool) & ~np.isnan(v)
+        idx = np.where(ok, np.nan_to_num(v, nan=0.0), len(labels)).astype(np.int64)
+        return codes[idx]
+
     def _output_column(self, of: ir.OutputField, cols: Columns, res: ModelResult, n: int) -> np.ndarray:
         feat = of.feature
         if feat in ("predictedValue", "predictedDisplayValue"):
             if res.kind == "regression":
                 return np.where(res.valid, res.value, NAN)
-            return self._encode_label(of.name, res.label_strings())
+            return self._encode_result_labels(of.name, res)
         if feat == "probability":
             if res.probs is None or res.categories is None:
                 raise UnsupportedFeatureException(f"output {of.name!r}: model has no probabilities")
@@ -176,7 +189,7 @@ class ModelEvaluator:
             if res.kind == "clustering":
                 if feat == "clusterId":
                     return np.where(res.valid, res.value + 1.0, NAN)
-                return self._encode_label(of.name, res.label_strings())
+                return self._encode_result_labels(of.name, res)
             ents = res.extra.get("entity_labels")
             if ents is not None:
                 return self._encode_label(of.name, ents)

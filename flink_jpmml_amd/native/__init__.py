@@ -1,9 +1,12 @@
-"""Native host runtime pieces (C++17, built with g++ into ``_ingest.so``, loaded with ctypes).
+"""Native host runtime pieces (C++17, built with g++).
 
-:class:`RecordParser` turns delimited text records into the engine's ``[rows, active fields]``
-fp32 matrix on all cores (``csrc/ingest.cpp``), writing straight into a caller-provided (pinned)
-buffer — the host-ingest stage in front of the H2D copy. Categorical tokens are encoded with the
-model's PMML vocabularies (the same codes the float64 oracle uses), missing tokens become NaN.
+* ``_ingest.so`` (ctypes) — :class:`RecordParser` turns delimited text records into the engine's
+  ``[rows, active fields]`` fp32 matrix on all cores (``csrc/ingest.cpp``), writing straight into a
+  caller-provided (pinned) buffer — the host-ingest stage in front of the H2D copy. Categorical
+  tokens are encoded with the model's PMML vocabularies (the same codes the float64 oracle uses),
+  missing tokens become NaN.
+* ``_fastpath`` (CPython extension, ``csrc/fastpath.cpp``) — the per-record stream path's object
+  traffic: DenseVector lists → matrix, scored arrays → ``Prediction`` objects (:func:`fastpath`).
 """
 
 from __future__ import annotations
@@ -38,6 +41,53 @@ def build(force: bool = False) -> str:
         raise NativeBuildError(r.stdout.decode(errors="replace"))
     os.replace(tmp, LIB_PATH)
     return LIB_PATH
+
+
+FAST_SRC = os.path.join(HERE, "csrc", "fastpath.cpp")
+_fast = None
+
+
+def _fast_path() -> str:
+    import sysconfig
+
+    return os.path.join(HERE, "_fastpath" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so"))
+
+
+def build_fastpath(force: bool = False) -> str:
+    """Compile the CPython fast-path extension in-tree (g++, Python + NumPy headers)."""
+    import sysconfig
+
+    out = _fast_path()
+    if not force and os.path.exists(out) and os.path.getmtime(out) >= os.path.getmtime(FAST_SRC):
+        return out
+    tmp = out + ".tmp"
+    cmd = ["g++", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall", "-fvisibility=hidden",
+           "-I" + sysconfig.get_paths()["include"], "-I" + np.get_include(), FAST_SRC, "-o", tmp]
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+    if r.returncode != 0:
+        raise NativeBuildError(r.stdout.decode(errors="replace"))
+    os.replace(tmp, out)
+    return out
+
+
+def fastpath():
+    """The ``_fastpath`` extension module (built on first use; ``None`` if it cannot be built, the
+    callers then use their pure-Python paths)."""
+    global _fast
+    if _fast is None:
+        with _lock:
+            if _fast is None:
+                try:
+                    import importlib.util
+
+                    path = build_fastpath()
+                    spec = importlib.util.spec_from_file_location("flink_jpmml_amd.native._fastpath", path)
+                    mod = importlib.util.module_from_spec(spec)
+                    spec.loader.exec_module(mod)
+                    _fast = mod
+                except Exception:  # noqa: BLE001 - pure-Python fallback keeps results identical
+                    _fast = False
+    return _fast or None
 
 
 def load() -> ctypes.CDLL:

@@ -1,0 +1,142 @@
+// Per-record fast path of the stream runtime (CPython C API + NumPy C API, built with g++).
+//
+// The reference scores one record at a time: every event is a FlinkML vector and every result a
+// `Prediction(Score(x))` object (`S/package.scala:76-82,138-142`, `S/models/prediction/Prediction.scala:72`).
+// The MI355X engine keeps that API but scores micro-batches on the GPU, so the per-record cost that
+// remains is purely host-side object traffic:
+//
+//   * pack_dense      — a list of DenseVector objects -> one [n, width] float64 matrix. Reads each
+//                       vector's `data` slot through the slot's member offset (no attribute lookup)
+//                       and memcpy's its contiguous float64 payload.
+//   * make_predictions — scores/valid arrays -> list of Prediction(Score(x)) / the shared
+//                       EmptyScore prediction. Objects are allocated with tp_alloc and their slots
+//                       filled directly (the Python __init__s only assign those same slots).
+//
+// Both return None / -1 when an input does not have the exact expected shape; the Python caller
+// then takes its general (slower, element-wise) path — results are identical either way.
+
+#define PY_SSIZE_T_CLEAN
+#include <Python.h>
+#include <structmember.h>
+#define NPY_NO_DEPRECATED_API NPY_1_7_API_VERSION
+#include <numpy/arrayobject.h>
+
+#include <cstring>
+
+namespace {
+
+// Byte offset of the __slots__ member `name` of heap type `tp` (-1 if it is not a slot).
+Py_ssize_t slot_offset(PyTypeObject *tp, const char *name) {
+    PyObject *descr = PyObject_GetAttrString(reinterpret_cast<PyObject *>(tp), name);
+    if (!descr) {
+        PyErr_Clear();
+        return -1;
+    }
+    Py_ssize_t off = -1;
+    if (Py_IS_TYPE(descr, &PyMemberDescr_Type)) {
+        PyMemberDef *m = reinterpret_cast<PyMemberDescrObject *>(descr)->d_member;
+        if (m->type == T_OBJECT_EX || m->type == T_OBJECT) off = m->offset;
+    }
+    Py_DECREF(descr);
+    return off;
+}
+
+// pack_dense(vectors: list, dense_type: type, width: int, out: ndarray[float64, n*width]) -> int
+// Returns n on success, -1 if some element is not an exact `dense_type` whose `data` slot holds a
+// C-contiguous float64 1-D array of `width` values (nothing is guaranteed about `out` then).
+PyObject *pack_dense(PyObject *, PyObject *args) {
+    PyObject *seq, *type_obj, *out_obj;
+    Py_ssize_t width;
+    if (!PyArg_ParseTuple(args, "O!OnO", &PyList_Type, &seq, &type_obj, &width, &out_obj)) return nullptr;
+    if (!PyType_Check(type_obj) || !PyArray_Check(out_obj)) {
+        PyErr_SetString(PyExc_TypeError, "pack_dense(list, type, int, ndarray)");
+        return nullptr;
+    }
+    PyTypeObject *tp = reinterpret_cast<PyTypeObject *>(type_obj);
+    PyArrayObject *out = reinterpret_cast<PyArrayObject *>(out_obj);
+    const Py_ssize_t n = PyList_GET_SIZE(seq);
+    if (PyArray_TYPE(out) != NPY_DOUBLE || !PyArray_IS_C_CONTIGUOUS(out) || PyArray_SIZE(out) < n * width) {
+        PyErr_SetString(PyExc_ValueError, "pack_dense: out must be a C-contiguous float64 array of n*width");
+        return nullptr;
+    }
+    const Py_ssize_t off = slot_offset(tp, "data");
+    if (off < 0) return PyLong_FromLong(-1);
+    double *dst = static_cast<double *>(PyArray_DATA(out));
+    const size_t row_bytes = static_cast<size_t>(width) * sizeof(double);
+    for (Py_ssize_t i = 0; i < n; ++i) {
+        PyObject *v = PyList_GET_ITEM(seq, i);
+        if (Py_TYPE(v) != tp) return PyLong_FromLong(-1);
+        PyObject *data = *reinterpret_cast<PyObject **>(reinterpret_cast<char *>(v) + off);
+        if (!data || !PyArray_Check(data)) return PyLong_FromLong(-1);
+        PyArrayObject *a = reinterpret_cast<PyArrayObject *>(data);
+        if (PyArray_TYPE(a) != NPY_DOUBLE || PyArray_NDIM(a) != 1 || PyArray_DIM(a, 0) != width ||
+            !PyArray_IS_C_CONTIGUOUS(a))
+            return PyLong_FromLong(-1);
+        std::memcpy(dst + i * width, PyArray_DATA(a), row_bytes);
+    }
+    return PyLong_FromSsize_t(n);
+}
+
+// make_predictions(scores: float32[n], valid: bool/uint8[n], prediction_type, score_type, empty) -> list
+PyObject *make_predictions(PyObject *, PyObject *args) {
+    PyObject *s_obj, *v_obj, *ptype_obj, *stype_obj, *empty;
+    if (!PyArg_ParseTuple(args, "OOOOO", &s_obj, &v_obj, &ptype_obj, &stype_obj, &empty)) return nullptr;
+    if (!PyArray_Check(s_obj) || !PyArray_Check(v_obj) || !PyType_Check(ptype_obj) || !PyType_Check(stype_obj)) {
+        PyErr_SetString(PyExc_TypeError, "make_predictions(ndarray, ndarray, type, type, object)");
+        return nullptr;
+    }
+    PyArrayObject *sa = reinterpret_cast<PyArrayObject *>(s_obj);
+    PyArrayObject *va = reinterpret_cast<PyArrayObject *>(v_obj);
+    if (PyArray_TYPE(sa) != NPY_FLOAT || !PyArray_IS_C_CONTIGUOUS(sa) || PyArray_ITEMSIZE(va) != 1 ||
+        !PyArray_IS_C_CONTIGUOUS(va) || PyArray_SIZE(va) != PyArray_SIZE(sa)) {
+        Py_RETURN_NONE;
+    }
+    PyTypeObject *ptype = reinterpret_cast<PyTypeObject *>(ptype_obj);
+    PyTypeObject *stype = reinterpret_cast<PyTypeObject *>(stype_obj);
+    const Py_ssize_t p_val = slot_offset(ptype, "value"), p_out = slot_offset(ptype, "outputs");
+    const Py_ssize_t s_val = slot_offset(stype, "value");
+    if (p_val < 0 || p_out < 0 || s_val < 0) Py_RETURN_NONE;
+    const Py_ssize_t n = PyArray_SIZE(sa);
+    const float *s = static_cast<const float *>(PyArray_DATA(sa));
+    const unsigned char *ok = static_cast<const unsigned char *>(PyArray_DATA(va));
+    PyObject *list = PyList_New(n);
+    if (!list) return nullptr;
+    for (Py_ssize_t i = 0; i < n; ++i) {
+        if (!ok[i]) {
+            Py_INCREF(empty);
+            PyList_SET_ITEM(list, i, empty);
+            continue;
+        }
+        PyObject *f = PyFloat_FromDouble(static_cast<double>(s[i]));
+        PyObject *score = f ? stype->tp_alloc(stype, 0) : nullptr;
+        PyObject *pred = score ? ptype->tp_alloc(ptype, 0) : nullptr;
+        if (!pred) {
+            Py_XDECREF(f);
+            Py_XDECREF(score);
+            Py_DECREF(list);
+            return nullptr;
+        }
+        *reinterpret_cast<PyObject **>(reinterpret_cast<char *>(score) + s_val) = f;  // steals f
+        *reinterpret_cast<PyObject **>(reinterpret_cast<char *>(pred) + p_val) = score;  // steals score
+        Py_INCREF(Py_None);
+        *reinterpret_cast<PyObject **>(reinterpret_cast<char *>(pred) + p_out) = Py_None;
+        PyList_SET_ITEM(list, i, pred);
+    }
+    return list;
+}
+
+PyMethodDef methods[] = {
+    {"pack_dense", pack_dense, METH_VARARGS, "Pack a list of DenseVector objects into a float64 matrix."},
+    {"make_predictions", make_predictions, METH_VARARGS, "Prediction objects for a scored batch."},
+    {nullptr, nullptr, 0, nullptr},
+};
+
+PyModuleDef module = {PyModuleDef_HEAD_INIT, "_fastpath", "Per-record fast path of the stream runtime.", -1,
+                      methods, nullptr, nullptr, nullptr, nullptr};
+
+}  // namespace
+
+PyMODINIT_FUNC PyInit__fastpath(void) {
+    import_array();
+    return PyModule_Create(&module);
+}

@@ -55,6 +55,9 @@ class CollectSink(SinkFunction):
     def invoke(self, value: Any) -> None:
         self.values.append(value)
 
+    def invoke_many(self, values: list) -> None:
+        self.values.extend(values)
+
     def __getstate__(self):
         return self.__dict__  # keeps the shared list when cloned for parallel subtasks
 
@@ -203,6 +206,11 @@ class _FnSink(SinkFunction):
     def invoke(self, value: Any) -> None:
         self.fn(value)
 
+    def invoke_many(self, values: list) -> None:
+        fn = self.fn
+        for v in values:
+            fn(v)
+
 
 class StreamExecutionEnvironment:
     def __init__(self, parallelism: int = 1, config: Optional[ScoringConfig] = None, dist_ctx=None,
@@ -214,6 +222,7 @@ class StreamExecutionEnvironment:
         self.checkpoint_every: Optional[int] = None
         self.checkpoint_interval_ms: Optional[float] = None
         self.input_mode = "auto"
+        self.gc_tuning = True
         self.checkpoint_storage = CheckpointStorage()
         self.fail_after: Optional[int] = None
         self.copy_operators = False
@@ -405,18 +414,37 @@ class DataStream:
 
     def unbatch(self) -> "DataStream":
         """``(PredictionBatch, RecordBatch)`` elements → per-record ``(Prediction, vector)``
-        (materialises Prediction objects: for sinks that need the reference's element type)."""
+        (materialises Prediction objects: for sinks that need the reference's element type). A
+        batch built by :meth:`to_batches` pairs each Prediction with its original event."""
         from ..api.batch import PredictionBatch
 
         def explode(x):
             if isinstance(x, tuple) and len(x) == 2 and isinstance(x[0], PredictionBatch):
                 preds, batch = x
-                return list(zip(preds, batch))
+                rows = batch.payload if getattr(batch, "payload", None) is not None else batch
+                return list(zip(preds.predictions(), rows))
             if isinstance(x, PredictionBatch):
-                return list(x)
+                return x.predictions()
             return [x]
 
         return self._one("flat_map", explode, "unbatch")
+
+    def to_batches(self, extract: Optional[Callable[[Any], Any]] = None, batch_rows: int = 65536,
+                   model_id: Optional[Callable[[Any], str]] = None, keep_events: bool = True,
+                   max_latency_ms: Optional[float] = None) -> "DataStream":
+        """Per-record events → columnar :class:`~flink_jpmml_amd.api.batch.RecordBatch` elements
+        (the vectorised adapter in front of the GPU path): ``extract(event)`` gives the event's
+        feature row in the model's active-field order (a DenseVector, sequence or array; default:
+        the event itself), ``model_id(event)`` its serving id (dynamic mode, ``BaseEvent.modelId``).
+        A batch is emitted every ``batch_rows`` events, at checkpoint barriers, at end of input and
+        — with ``max_latency_ms`` — when its oldest event has waited that long. The original events
+        ride along as the batch ``payload`` (``unbatch()`` pairs each prediction with its event)."""
+        from .operators import ToBatchesFunction
+
+        op = ToBatchesFunction(extract, batch_rows, model_id, keep_events, max_latency_ms)
+        return self._one("flat_map", op, "to_batches")
+
+    toBatches = to_batches  # noqa: N815
 
     def set_parallelism(self, p: int) -> "DataStream":
         self.node.parallelism = int(p)

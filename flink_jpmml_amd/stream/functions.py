@@ -11,21 +11,31 @@ from typing import Any, Callable, Iterable, List, Optional
 
 
 class Collector:
-    """Output collector handed to ``flat_map`` / ``process_element*``."""
+    """Output collector handed to ``flat_map`` / ``process_element*``. ``collect_many`` hands a
+    whole chunk of outputs downstream in one call (the runtime's chunked path: operators that
+    implement ``flat_map_many`` / ``process_elements1`` / ``invoke_many`` receive chunks)."""
 
-    __slots__ = ("_emit",)
+    __slots__ = ("_emit", "_emit_many")
 
-    def __init__(self, emit: Callable[[Any], None]):
+    def __init__(self, emit: Callable[[Any], None], emit_many: Optional[Callable[[list], None]] = None):
         self._emit = emit
+        self._emit_many = emit_many
 
     def collect(self, value: Any) -> None:
         self._emit(value)
+
+    def collect_many(self, values: list) -> None:
+        if self._emit_many is not None:
+            self._emit_many(values)
+        else:
+            for v in values:
+                self._emit(v)
 
 
 class ListCollector(Collector):
     def __init__(self):
         self.items: List[Any] = []
-        super().__init__(self.items.append)
+        super().__init__(self.items.append, self.items.extend)
 
 
 class RuntimeContext:

@@ -55,6 +55,23 @@ class Marker:
 IDLE = Marker("idle")
 
 
+class Chunk:
+    """Several consecutive ``(global_offset, element)`` pairs of one source, delivered downstream
+    with one ``collect_many`` (amortises the per-element dispatch of per-record streams)."""
+
+    __slots__ = ("node", "pairs")
+
+    def __init__(self, node: Any, pairs: list):
+        self.node = node
+        self.pairs = pairs
+
+
+def is_chunkable_source(src: Any) -> bool:
+    """Sources whose reads never block or sleep (in-memory collections, columnar matrices, files):
+    the deterministic merge may pull several elements ahead and deliver them as one chunk."""
+    return bool(getattr(src, "chunkable", False)) and not is_live_source(src)
+
+
 class _Eos:
     __slots__ = ("si",)
 
@@ -93,13 +110,27 @@ def is_live_source(src: Any) -> bool:
 class DeterministicInputs:
     """Reproducible merge of pull sources (see module docstring)."""
 
-    def __init__(self, sources: List[Any], readers: dict):
+    def __init__(self, sources: List[Any], readers: dict, chunk: int = 1024):
         self.sources = sources
         self.readers = readers
+        self.chunk = int(chunk)
 
     def __iter__(self) -> Iterator[Any]:
         sources = self.sources
         iters = [(n, iter(self.readers[id(n)])) for n in sources]
+        if len(sources) == 1 and self.chunk > 1 and is_chunkable_source(sources[0].source):
+            n, it = iters[0]
+            size = self.chunk
+            direct = self.readers[id(n)].chunks(size)
+            if direct is not None:
+                for pairs in direct:
+                    yield Chunk(n, pairs)
+                return
+            while True:
+                pairs = list(itertools.islice(it, size))
+                if not pairs:
+                    return
+                yield Chunk(n, pairs) if len(pairs) > 1 else (n, pairs[0][0], pairs[0][1])
         timed = len(sources) > 1 and all(n.timestamp_fn is not None for n in sources)
         if timed:
             heap = []
@@ -214,9 +245,11 @@ class LiveInputs:
             if type(item) is tuple:
                 si, chunk = item
                 self._sems[si].release()
-                n = nodes[si]
-                for g, v in chunk:
-                    yield n, g, v
+                if len(chunk) > 1:
+                    yield Chunk(nodes[si], chunk)
+                else:
+                    g, v = chunk[0]
+                    yield nodes[si], g, v
             elif isinstance(item, _Eos):
                 self._active -= 1
             elif isinstance(item, _Err):
@@ -247,4 +280,5 @@ class LiveInputs:
                     pass
 
 
-__all__ = ["DeterministicInputs", "IDLE", "LiveInputs", "Marker", "is_live_source"]
+__all__ = ["Chunk", "DeterministicInputs", "IDLE", "LiveInputs", "Marker", "is_chunkable_source",
+           "is_live_source"]

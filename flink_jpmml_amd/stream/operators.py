@@ -43,13 +43,13 @@ from ..api.exceptions import ModelLoadingException
 from ..api.managers import metadata_manager, models_manager
 from ..api.pmml_model import PmmlModel
 from ..api.reader import ModelReader
-from ..api.vectors import as_vector
+from ..api.vectors import DenseVector, SparseVector, as_vector
 from ..config import ScoringConfig, merge_config
 from ..domain.checkpoint import STATE_NAME
 from ..domain.control import AddMessage, DelMessage, ServingMessage
 from ..domain.events import event_model_id
 from ..domain.model_id import ModelId, ModelInfo
-from ..domain.prediction import EMPTY_PREDICTION, Prediction
+from ..domain.prediction import EMPTY_PREDICTION, Prediction, Target
 from ..utils.metrics import METRICS
 from ..utils.profiling import prange
 from .functions import CheckpointedFunction, CoProcessFunction, Collector, FlatMapFunction
@@ -218,37 +218,195 @@ def _score_calls(model: PmmlModel, calls: List[Tuple[Any, Optional[float]]]) -> 
     return out  # type: ignore[return-value]
 
 
-class _Batcher:
-    """Buffers (event, model) pairs and runs the capture → batch score → replay protocol; flushes
-    on size, on the latency timer, and when the owner asks (control / barrier / end)."""
+class _DeferredTarget(Target):
+    """``prediction.value`` of a not-yet-scored :class:`DeferredPrediction`: resolves (scoring the
+    pending micro-batch) only when its score is actually read."""
 
-    def __init__(self, owner: "_ScoringMixin", f: Callable[[Any, Any], Any], batch_size: int):
+    __slots__ = ("_dp",)
+
+    def __init__(self, dp: "DeferredPrediction"):
+        self._dp = dp
+
+    def _t(self) -> Target:
+        return self._dp._get().value
+
+    def get(self) -> float:
+        return self._t().get()
+
+    def get_or_else(self, default: float) -> float:
+        return self._t().get_or_else(default)
+
+    @property
+    def is_empty(self) -> bool:
+        return self._t().is_empty
+
+    @property
+    def value(self) -> float:
+        return self._t().value
+
+    def __eq__(self, other: object) -> bool:
+        return self._t() == (other._t() if isinstance(other, _DeferredTarget) else other)
+
+    def __hash__(self) -> int:
+        return hash(self._t())
+
+    def __repr__(self) -> str:
+        return repr(self._t())
+
+    def __reduce__(self):
+        return self._t().__reduce__()
+
+
+class DeferredPrediction(Prediction):
+    """The :class:`Prediction` a per-record UDF gets from ``model.predict`` inside a micro-batch.
+
+    The UDF runs **exactly once per event**, when the event arrives; its ``predict`` calls are
+    collected and scored together (one RecordBatch per model) when the micro-batch flushes — on
+    size, latency timer, control message, barrier or end of input. A UDF that reads the score
+    inside ``f`` (``.value.get_or_else(..)``) resolves the pending calls right there (a smaller
+    batch, never a second call of ``f``); ``prediction.value`` itself stays lazy."""
+
+    __slots__ = ("_batcher", "_resolved")
+
+    def __init__(self, batcher: "_Batcher"):  # noqa: super().__init__ is not called: value is lazy
+        self._batcher = batcher
+        self._resolved: Optional[Prediction] = None
+
+    def _get(self) -> Prediction:
+        r = self._resolved
+        if r is None:
+            self._batcher.resolve()
+            r = self._resolved
+        return r
+
+    @property
+    def value(self) -> Target:  # type: ignore[override]
+        r = self._resolved
+        return r.value if r is not None else _DeferredTarget(self)
+
+    @property
+    def outputs(self):  # type: ignore[override]
+        return self._get().outputs
+
+    @property
+    def resolved(self) -> bool:
+        return self._resolved is not None
+
+    def __eq__(self, other: object) -> bool:
+        if not isinstance(other, Prediction):
+            return NotImplemented
+        o = other._get() if isinstance(other, DeferredPrediction) else other
+        return self._get() == o
+
+    def __hash__(self) -> int:
+        return hash(self._get())
+
+    def __repr__(self) -> str:
+        return repr(self._get())
+
+    def __reduce__(self):
+        return self._get().__reduce__()
+
+
+class _DeferredModel:
+    """Stands in for :class:`PmmlModel` inside a micro-batched UDF: ``predict`` on a vector
+    registers the call and returns a :class:`DeferredPrediction`."""
+
+    __slots__ = ("_real", "_batcher")
+
+    def __init__(self, real: PmmlModel, batcher: "_Batcher"):
+        self._real = real
+        self._batcher = batcher
+
+    def predict(self, input_vector: Any, replace_nan: Optional[float] = None):
+        if isinstance(input_vector, RecordBatch) or getattr(input_vector, "ndim", 1) == 2:
+            return self._real.predict(input_vector, replace_nan)
+        return self._batcher.defer(self._real, input_vector, replace_nan)
+
+    def __getattr__(self, item: str) -> Any:
+        return getattr(self._real, item)
+
+
+class _Batcher:
+    """Micro-batches a per-record UDF (``batch_size`` set). Two modes (``ScoringConfig.udf_mode``):
+
+    * ``deferred`` (default) — ``f(event, model)`` runs **exactly once**, as the event arrives;
+      ``model.predict`` returns a :class:`DeferredPrediction`; results are emitted in arrival order
+      when the batch flushes (size / latency timer / control / barrier / end), after one batched
+      scoring pass per model. The reference calls ``f`` once per record
+      (`S/package.scala:77-79,111-114`) — so does this mode, side effects included.
+    * ``replay`` — for pure UDFs that read the score inside ``f``: ``f`` runs against a recording
+      model, the captured calls are scored as one batch, and ``f`` runs again against a replay
+      model that verifies every call (divergent events are re-run per record). ``f`` runs twice.
+    """
+
+    def __init__(self, owner: "_ScoringMixin", f: Callable[[Any, Any], Any], batch_size: int, mode: str = "deferred"):
         self.owner = owner
         self.f = f
         self.batch_size = int(batch_size)
-        self.buf: List[Tuple[Any, PmmlModel]] = []
+        self.mode = mode
+        self.buf: List[Tuple[Any, PmmlModel]] = []  # replay mode: (event, model)
+        self.results: List[Any] = []  # deferred mode: UDF results, arrival order
+        self.calls: List[Tuple[PmmlModel, Any, Optional[float], DeferredPrediction]] = []  # unscored
         self.first_ts: Optional[float] = None
         self._timer_armed = False
 
+    def __len__(self) -> int:
+        return len(self.results) if self.mode == "deferred" else len(self.buf)
+
+    # -- deferred mode
+    def defer(self, model: PmmlModel, vec: Any, replace_nan: Optional[float]) -> DeferredPrediction:
+        dp = DeferredPrediction(self)
+        self.calls.append((model, vec, replace_nan, dp))
+        return dp
+
+    def resolve(self) -> None:
+        """Score every pending predict() call: one RecordBatch per (model, replace_nan)."""
+        calls, self.calls = self.calls, []
+        if not calls:
+            return
+        groups: "OrderedDict[Tuple[int, Optional[float]], list]" = OrderedDict()
+        for c in calls:
+            groups.setdefault((id(c[0]), c[2]), []).append(c)
+        with prange("batcher.resolve"):
+            for (_, rn), cs in groups.items():
+                preds = _score_calls(cs[0][0], [(c[1], rn) for c in cs])
+                for c, p in zip(cs, preds):
+                    c[3]._resolved = p
+        METRICS.inc("batcher.resolves")
+
     def add(self, event: Any, model: PmmlModel, out: Collector) -> None:
-        if not self.buf:
+        if not len(self):
             self.first_ts = self.owner._now()
-        self.buf.append((event, model))
-        if len(self.buf) >= self.batch_size:
+        if self.mode == "deferred":
+            self.results.append(self.f(event, _DeferredModel(model, self)))
+        else:
+            self.buf.append((event, model))
+        if len(self) >= self.batch_size:
             self.flush(out)
         else:
             self._arm(out)
 
+    def add_many(self, events: List[Any], model_of: Callable[[Any], PmmlModel], out: Collector) -> None:
+        """A chunk of events (deferred mode): one UDF call each, flushes at every full batch."""
+        for ev in events:
+            if not self.results:
+                self.first_ts = self.owner._now()
+            self.results.append(self.f(ev, _DeferredModel(model_of(ev), self)))
+            if len(self.results) >= self.batch_size:
+                self.flush(out)
+        self._arm(out)
+
     def _arm(self, out: Collector) -> None:
         lat = self.owner.config.max_batch_latency_ms
         rctx = getattr(self.owner, "runtime_context", None)
-        if lat is None or rctx is None or self._timer_armed or not self.buf:
+        if lat is None or rctx is None or self._timer_armed or not len(self):
             return
         self._timer_armed = True
 
         def fire(now: float) -> None:
             self._timer_armed = False
-            if self.buf and now >= self.first_ts + lat / 1e3:
+            if len(self) and now >= self.first_ts + lat / 1e3:
                 METRICS.inc("batcher.latency_flushes")
                 self.flush(out)
             self._arm(out)
@@ -256,6 +414,18 @@ class _Batcher:
         rctx.register_timer(self.first_ts + lat / 1e3, fire)
 
     def flush(self, out: Collector) -> None:
+        if self.mode == "deferred":
+            if not self.results:
+                return
+            results, self.results = self.results, []
+            with prange("batcher.flush"):
+                self.resolve()
+            out.collect_many(results)
+            return
+        self._flush_replay(out)
+
+    # -- replay mode
+    def _flush_replay(self, out: Collector) -> None:
         if not self.buf:
             return
         buf, self.buf = self.buf, []
@@ -348,7 +518,7 @@ class EvaluationFunction(FlatMapFunction, _ScoringMixin):
         self._evaluator, self.digest = lm.model, lm.sha256
         logger.info("Model has been successfully loaded, model name: %s", lm.model.model_name)
         if self.config.batch_size:
-            self._batcher = _Batcher(self, self.f, self.config.batch_size)
+            self._batcher = _Batcher(self, self.f, self.config.batch_size, self.config.udf_mode)
 
     def flat_map(self, value: Any, out: Collector) -> None:
         if isinstance(value, RecordBatch):
@@ -358,6 +528,23 @@ class EvaluationFunction(FlatMapFunction, _ScoringMixin):
             self._batcher.add(value, self.evaluator, out)
         else:
             out.collect(self.f(value, self.evaluator))
+
+    def flat_map_many(self, values: List[Any], out: Collector) -> None:
+        """Chunked delivery of per-record events (same results as element-wise)."""
+        if any(type(v) is RecordBatch for v in values):
+            for v in values:
+                self.flat_map(v, out)
+            return
+        model = self.evaluator
+        b = self._batcher
+        if b is None:
+            f = self.f
+            out.collect_many([f(v, model) for v in values])
+        elif b.mode == "deferred":
+            b.add_many(values, lambda ev: model, out)
+        else:
+            for v in values:
+                b.add(v, model, out)
 
     def end_of_input(self, out: Collector) -> None:
         if self._batcher is not None:
@@ -447,6 +634,7 @@ class EvaluationCoFunction(CoProcessFunction, CheckpointedFunction, _ScoringMixi
         self._pipeline = None
         self._pending = collections.deque()
         self._restored_digests: Dict[ModelId, str] = {}
+        self._by_str: Dict[str, PmmlModel] = {}
 
     @property
     def batch_size(self) -> Optional[int]:
@@ -460,7 +648,7 @@ class EvaluationCoFunction(CoProcessFunction, CheckpointedFunction, _ScoringMixi
         self._setup()
         self.serving_models.capacity = self.config.cache_capacity
         if self.config.batch_size:
-            self._batcher = _Batcher(self, self.f, self.config.batch_size)
+            self._batcher = _Batcher(self, self.f, self.config.batch_size, self.config.udf_mode)
         # models of a restored checkpoint are re-loaded (and re-replicated) right away
         if self.config.async_load or self._distributed:
             for mid, info in self.serving_metadata.items():
@@ -525,6 +713,30 @@ class EvaluationCoFunction(CoProcessFunction, CheckpointedFunction, _ScoringMixi
             return self._accept_loaded(mid, lm)
         return self.from_metadata(model_id)
 
+    def _model_of_event(self, event: Any) -> PmmlModel:
+        """``model_for`` with a per-id-string memo (cleared by every control message): a stream of
+        events for the same few models skips the id parse and the cache lookup."""
+        key = event_model_id(event)
+        m = self._by_str.get(key)
+        if m is None:
+            m = self.model_for(key)
+            if not m.is_empty:
+                self._by_str[key] = m
+        return m
+
+    def process_elements1(self, events: List[Any], ctx, out: Collector) -> None:
+        """Chunked delivery of per-record events (same results as element-wise)."""
+        b = self._batcher
+        if any(type(e) is RecordBatch for e in events) or (b is not None and b.mode != "deferred"):
+            for e in events:
+                self.process_element1(e, ctx, out)
+            return
+        if b is None:
+            f = self.f
+            out.collect_many([f(e, self._model_of_event(e)) for e in events])
+        else:
+            b.add_many(events, self._model_of_event, out)
+
     def process_element1(self, event: Any, ctx, out: Collector) -> None:
         if isinstance(event, RecordBatch):
             for sub in event.split_by_model():
@@ -543,6 +755,7 @@ class EvaluationCoFunction(CoProcessFunction, CheckpointedFunction, _ScoringMixi
         if self._batcher is not None:
             self._batcher.flush(out)  # control messages are batch barriers
         self._drain_pending(out)
+        self._by_str.clear()
         self.manage_models(control)
         known = control.model_id in self.serving_metadata
         self.manage_metadata(control)
@@ -624,6 +837,7 @@ class EvaluationCoFunction(CoProcessFunction, CheckpointedFunction, _ScoringMixi
             d[k] = None
         d["_loading"] = {}
         d["_pending"] = collections.deque()
+        d["_by_str"] = {}
         return d
 
 
@@ -683,6 +897,29 @@ class QuickEvaluationFunction(FlatMapFunction, _ScoringMixin):
         else:
             self._arm(out)
 
+    def flat_map_many(self, values: List[Any], out: Collector) -> None:
+        """Chunked delivery: per-record vectors are appended in bulk and flushed per full batch."""
+        has_rb = RecordBatch in set(map(type, values))
+        if not self.config.batch_size or has_rb:
+            if not self.config.batch_size and not has_rb:
+                model = self.inner.evaluator
+                out.collect_many([quick_udf(v, model) for v in values])
+                return
+            for v in values:
+                self.flat_map(v, out)
+            return
+        bs = self.config.batch_size
+        i, n = 0, len(values)
+        while i < n:
+            if not self._buf:
+                self._first_ts = self._now()
+            take = min(n - i, bs - len(self._buf))
+            self._buf.extend(values[i:i + take] if (i or take < n) else values)
+            i += take
+            if len(self._buf) >= bs:
+                self._flush(out)
+        self._arm(out)
+
     def _arm(self, out: Collector) -> None:
         lat = self.config.max_batch_latency_ms
         rctx = getattr(self, "runtime_context", None)
@@ -706,9 +943,8 @@ class QuickEvaluationFunction(FlatMapFunction, _ScoringMixin):
         model = self.inner.evaluator
         with prange("quick_evaluate.flush"):
             batch = RecordBatch.from_vectors(buf, len(model.active_fields))
-            preds = model.predict_records(batch)
-        for v, p in zip(buf, preds):
-            out.collect((p, v))
+            preds = model.predict_records(batch).predictions()
+        out.collect_many(list(zip(preds, buf)))
 
     def end_of_input(self, out: Collector) -> None:
         self._flush(out)
@@ -725,4 +961,107 @@ class QuickEvaluationFunction(FlatMapFunction, _ScoringMixin):
         for k in ("_pipeline", "_pending", "dist", "runtime_context"):
             d.pop(k, None)
         d["_buf"] = []
+        return d
+
+
+# --------------------------------------------------------------------------- event -> batch adapter
+
+
+def _row_of(x: Any) -> Any:
+    data = getattr(x, "data", None)
+    if data is not None and not isinstance(x, SparseVector):
+        return data
+    if isinstance(x, SparseVector):
+        return x.to_dense_array()
+    return x
+
+
+class ToBatchesFunction(FlatMapFunction):
+    """``DataStream.to_batches``: accumulates per-record events into RecordBatches (see there)."""
+
+    def __init__(self, extract: Optional[Callable[[Any], Any]], batch_rows: int,
+                 model_id: Optional[Callable[[Any], str]], keep_events: bool, max_latency_ms: Optional[float]):
+        self.extract = extract
+        self.batch_rows = int(batch_rows)
+        self.model_id = model_id
+        self.keep_events = bool(keep_events)
+        self.max_latency_ms = max_latency_ms
+        self._rows: List[Any] = []
+        self._events: List[Any] = []
+        self._first: Optional[float] = None
+        self._timer = False
+        self._offset = 0
+
+    def _now(self) -> float:
+        rctx = getattr(self, "runtime_context", None)
+        return rctx.now() if rctx is not None else __import__("time").monotonic()
+
+    def flat_map(self, value: Any, out: Collector) -> None:
+        self.flat_map_many([value], out)
+
+    def flat_map_many(self, values: List[Any], out: Collector) -> None:
+        ex = self.extract
+        i, n = 0, len(values)
+        while i < n:
+            if not self._events:
+                self._first = self._now()
+            take = min(n - i, self.batch_rows - len(self._events))
+            part = values[i:i + take] if (i or take < n) else values
+            self._rows.extend(map(ex, part) if ex is not None else map(_row_of, part))
+            self._events.extend(part)
+            i += take
+            if len(self._events) >= self.batch_rows:
+                self._emit(out)
+        self._arm(out)
+
+    def _emit(self, out: Collector) -> None:
+        if not self._events:
+            return
+        rows, events = self._rows, self._events
+        self._rows, self._events = [], []
+        rows = [_row_of(r) if isinstance(r, (DenseVector, SparseVector)) else r for r in rows] \
+            if rows and isinstance(rows[0], (DenseVector, SparseVector)) else rows
+        X = None
+        if rows and type(rows[0]) is np.ndarray and rows[0].ndim == 1:
+            w = rows[0].shape[0]
+            if all(type(r) is np.ndarray and r.shape == (w,) for r in rows):
+                X = np.concatenate(rows).astype(np.float64, copy=False).reshape(len(rows), w)
+        if X is None:
+            X = np.asarray(rows, dtype=np.float64)
+        if X.ndim != 2:
+            raise ValueError(f"to_batches: extract() must give one feature row per event, got shape {X.shape}")
+        ids = [self.model_id(e) for e in events] if self.model_id is not None else None
+        uniq = set(ids) if ids is not None else None
+        b = RecordBatch(X, model_id=next(iter(uniq)) if uniq is not None and len(uniq) == 1 else None,
+                        model_ids=ids if uniq is not None and len(uniq) > 1 else None,
+                        payload=events if self.keep_events else None, offset=self._offset)
+        self._offset += len(events)
+        METRICS.inc("to_batches.batches")
+        out.collect(b)
+
+    def _arm(self, out: Collector) -> None:
+        lat = self.max_latency_ms
+        rctx = getattr(self, "runtime_context", None)
+        if lat is None or rctx is None or self._timer or not self._events:
+            return
+        self._timer = True
+
+        def fire(now: float) -> None:
+            self._timer = False
+            if self._events and now >= self._first + lat / 1e3:
+                self._emit(out)
+            self._arm(out)
+
+        rctx.register_timer(self._first + lat / 1e3, fire)
+
+    def end_of_input(self, out: Collector) -> None:
+        self._emit(out)
+
+    def on_barrier(self, out: Collector) -> None:
+        self._emit(out)
+
+    def __getstate__(self):
+        d = dict(self.__dict__)
+        d["_rows"], d["_events"] = [], []
+        d.pop("runtime_context", None)
         return d

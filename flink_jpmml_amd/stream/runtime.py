@@ -37,6 +37,7 @@ exactly the semantics the reference's operators depend on:
 
 from __future__ import annotations
 
+import bisect
 import copy
 import logging
 import time
@@ -57,6 +58,7 @@ from .functions import (
     RuntimeContext,
     SinkFunction,
 )
+from .inputs import Chunk
 from .sources import SourceReader
 from .state import CheckpointStorage, OperatorStateStore
 
@@ -225,7 +227,7 @@ class Executor:
                         op.recover(doc.get("checkpoint_id"))
         for n in self.nodes:
             for st in self.subtasks[id(n)]:
-                st.out = Collector(self._emitter(n, st))
+                st.out = Collector(self._emitter(n, st), self._emitter_many(n, st))
                 if isinstance(st.op, RichFunction):
                     st.op.open({})
 
@@ -247,6 +249,77 @@ class Executor:
                     self._deliver(dn, t, port, value)
 
         return emit
+
+    def _emitter_many(self, node: Node, st: _Subtask) -> Callable[[list], None]:
+        downs = self.down[id(node)]
+
+        if len(downs) > 1:  # fan-out: branches may merge again downstream (from_either's split
+            emit = self._emitter(node, st)  # into events + control): keep element order across them
+
+            def emit_each(values: list) -> None:
+                for v in values:
+                    emit(v)
+
+            return emit_each
+
+        def emit_many(values: list) -> None:
+            if not values:
+                return
+            for dn, part, port in downs:
+                subs = self.subtasks[id(dn)]
+                if part == "broadcast" or len(subs) == 1:
+                    for t in subs:
+                        self._deliver_many(dn, t, port, values)
+                elif part == "forward" and len(subs) == len(self.subtasks[id(node)]):
+                    self._deliver_many(dn, subs[st.index % len(subs)], port, values)
+                else:  # rebalance: element-wise round robin
+                    for v in values:
+                        self._deliver(dn, subs[st.rr % len(subs)], port, v)
+                        st.rr += 1
+
+        return emit_many
+
+    def _deliver_many(self, node: Node, st: _Subtask, port: int, values: list) -> None:
+        """Chunked delivery: one call per chunk for map / filter / plain functions and for
+        operators implementing the ``*_many`` hooks (order and results are those of element-wise
+        delivery; operators keeping a collector for later, e.g. timers, always get ``st.out``)."""
+        op = st.op
+        k = node.op_kind
+        if k == "map":
+            f = op.map if hasattr(op, "map") else op
+            st.out.collect_many([f(v) for v in values])
+        elif k == "filter":
+            f = op.filter if hasattr(op, "filter") else op
+            st.out.collect_many([v for v in values if f(v)])
+        elif k in ("flat_map", "process"):
+            many = getattr(op, "flat_map_many", None)
+            if many is not None:
+                many(values, st.out)
+            elif hasattr(op, "flat_map"):
+                for v in values:
+                    op.flat_map(v, st.out)
+            else:
+                res: list = []
+                for v in values:
+                    res.extend(op(v))
+                st.out.collect_many(res)
+        elif k == "co_process":
+            many = getattr(op, "process_elements1", None) if port == 0 else None
+            if many is not None:
+                many(values, ProcessContext(None), st.out)
+            else:
+                for v in values:
+                    self._deliver(node, st, port, v)
+        elif k == "sink":
+            many = getattr(op, "invoke_many", None)
+            if many is not None:
+                many(values)
+            else:
+                inv = op.invoke if hasattr(op, "invoke") else op
+                for v in values:
+                    inv(v)
+        else:  # pragma: no cover
+            raise RuntimeError(f"unknown operator kind {k}")
 
     def _deliver(self, node: Node, st: _Subtask, port: int, value: Any) -> None:
         op = st.op
@@ -456,6 +529,75 @@ class Executor:
                     if hasattr(st.op, "commit"):
                         st.op.commit(-1)
 
+    def _gc_tune(self):
+        """Per-record streams allocate a few objects per record; CPython's cyclic collector would
+        rescan every live object (inputs, buffered outputs) again and again. During the job the
+        objects that existed before it are frozen out of collection and young collections run
+        every 50k allocations (``env.gc_tuning = False`` keeps the interpreter defaults)."""
+        if not getattr(self.env, "gc_tuning", True):
+            return None
+        import gc
+
+        saved = gc.get_threshold()
+        gc.freeze()
+        gc.set_threshold(max(saved[0], 200_000), saved[1], saved[2])
+        return saved
+
+    @staticmethod
+    def _gc_restore(saved) -> None:
+        if saved is None:
+            return
+        import gc
+
+        gc.set_threshold(*saved)
+        gc.unfreeze()
+
+    @staticmethod
+    def _faults_active() -> bool:
+        from ..utils.faults import injector
+
+        return injector().active
+
+    def _run_chunk(self, n: Node, pairs: list, faults: bool, fail_after: Optional[int]) -> None:
+        """Deliver a chunk of ``(global_offset, element)`` pairs of one source: split at
+        count-based barriers, then handed downstream as one ``collect_many``."""
+        st = self.subtasks[id(n)][0]
+        if faults:  # per-element semantics of the fault hooks
+            for g, v in pairs:
+                self._run_one(n, g, v, st, fail_after)
+            return
+        every = self.env.checkpoint_every if n is self.primary else None
+        i, m = 0, len(pairs)
+        while i < m:
+            j = m
+            if every:
+                self._maybe_checkpoint(pairs[i][0])
+                nb = self.next_cid * every
+                j = bisect.bisect_left(pairs, nb, lo=i, key=_first)
+                j = max(j, i + 1)
+            sub = pairs if (i == 0 and j == m) else pairs[i:j]
+            self.processed[id(n)] = sub[-1][0] + 1
+            vals = [v for _, v in sub]
+            self.elements_in += len(vals)
+            self.records_in += len(vals) if RecordBatch not in set(map(type, vals)) else \
+                sum(len(v) if type(v) is RecordBatch else 1 for v in vals)
+            st.out.collect_many(vals)
+            i = j
+
+    def _run_one(self, n: Node, g: int, v: Any, st: _Subtask, fail_after: Optional[int]) -> None:
+        if self.env.checkpoint_every and n is self.primary:
+            self._maybe_checkpoint(g)
+        self.processed[id(n)] = g + 1
+        self.elements_in += 1
+        self.records_in += len(v) if isinstance(v, RecordBatch) else 1
+        if fail_after is not None and self.elements_in > fail_after:
+            raise SimulatedFailure(f"injected failure after {fail_after} records")
+        if self.dist is not None:
+            from ..utils.faults import injector
+
+            injector().on_batch(self.rank, self.elements_in - 1)
+        st.out.collect(v)
+
     def _make_inputs(self, sources: List[Node], mode: str):
         from .inputs import DeterministicInputs, LiveInputs
 
@@ -471,6 +613,7 @@ class Executor:
 
     def run(self, job_name: str) -> JobExecutionResult:
         t0 = time.perf_counter()
+        gc_saved = self._gc_tune()
         self.clock.bind_thread()
         set_current_clock(self.clock)
         cfg = self.env.config
@@ -493,27 +636,15 @@ class Executor:
 
                 self.watchdog = Watchdog(cfg.watchdog_s, name=f"rank{self.rank}").start()
             fail_after = self.env.fail_after
-            count_ckpt = bool(self.env.checkpoint_every)
             time_ckpt = bool(self.env.checkpoint_interval_ms)
-            primary = self.primary
             dist_hooks = self.dist is not None
+            faults = fail_after is not None or (dist_hooks and self._faults_active())
             for item in inputs:
-                if type(item) is tuple:
+                if type(item) is Chunk:
+                    self._run_chunk(item.node, item.pairs, faults, fail_after)
+                elif type(item) is tuple:
                     n, g, v = item
-                    if count_ckpt and n is primary:
-                        self._maybe_checkpoint(g)
-                    self.processed[id(n)] = g + 1
-                    self.elements_in += 1
-                    self.records_in += len(v) if isinstance(v, RecordBatch) else 1
-                    if fail_after is not None and self.elements_in > fail_after:
-                        raise SimulatedFailure(f"injected failure after {fail_after} records")
-                    if dist_hooks:
-                        from ..utils.faults import injector
-
-                        injector().on_batch(self.rank, self.elements_in - 1)
-                    for st in self.subtasks[id(n)]:
-                        st.out.collect(v)
-                        break
+                    self._run_one(n, g, v, self.subtasks[id(n)][0], fail_after)
                 elif item.kind == "barrier":
                     self._checkpoint(item.cid)
                     self.next_cid = item.cid + 1
@@ -538,6 +669,7 @@ class Executor:
                 self.watchdog.stop()
             self.clock.timers.clear()
             set_current_clock(None)
+            self._gc_restore(gc_saved)
             for n in self.nodes:
                 for st in self.subtasks.get(id(n), []):
                     if isinstance(st.op, (RichFunction, SinkFunction)):
@@ -549,6 +681,10 @@ class Executor:
         METRICS.inc("job.elements_in", self.elements_in)
         return JobExecutionResult(job_name, (time.perf_counter() - t0) * 1e3, self.records_in, self.checkpoint_paths,
                                   elements_in=self.elements_in, input_mode=getattr(self, "input_mode", None))
+
+
+def _first(pair):
+    return pair[0]
 
 
 def _clone(op: Any) -> Any:

@@ -43,6 +43,8 @@ _EOS = object()
 class CollectionSource(SourceFunction):
     """A finite, replayable sequence (``from_collection``)."""
 
+    chunkable = True
+
     def __init__(self, items: Iterable[Any]):
         self.items = list(items)
 
@@ -60,6 +62,16 @@ class CollectionSource(SourceFunction):
 
     def global_length(self) -> int:
         return len(self.items)
+
+    def read_chunks(self, rank: int, world: int, start: int, size: int) -> Iterator[list]:
+        """``(global_offset, element)`` pairs of this rank in lists of ``size`` (C-speed slicing:
+        the chunked per-record path)."""
+        items = self.items
+        first = start + ((rank - start) % world)
+        step = size * world
+        for a in range(first, len(items), step):
+            b = min(len(items), a + step)
+            yield list(zip(range(a, b, world), items[a:b:world]))
 
     def __len__(self) -> int:
         return len(self.items)
@@ -79,6 +91,8 @@ class BatchSource(SourceFunction):
     """Columnar source: a ``[rows, F]`` matrix (numpy or torch, pinned preferred) cut into
     RecordBatches of ``batch_rows``, or an iterable of matrices / RecordBatches. ``repeat``
     replays the matrix that many times (synthetic streams). Seekable by batch index."""
+
+    chunkable = True
 
     def __init__(self, data: Any, batch_rows: Optional[int] = None, repeat: int = 1,
                  model_id: Optional[str] = None):
@@ -141,6 +155,8 @@ class TextBatchSource(SourceFunction):
     C++ ingest (:class:`flink_jpmml_amd.native.RecordParser`) straight into the batch buffer.
     Columns are matched to the model's active fields by header name (``columns`` overrides the
     header); categorical tokens get the model's PMML codes, missing tokens become NaN."""
+
+    chunkable = False  # each batch is a large parse: hand it downstream as soon as it exists
 
     def __init__(self, path: str, model: Any, batch_rows: int = 1 << 16, delimiter: str = ",",
                  columns: Optional[Sequence[str]] = None, threads: int = 0, model_id: Optional[str] = None,
@@ -472,6 +488,25 @@ class SourceReader:
             self.offset = int(leader_offset)
         else:
             self._it = iter_source(src, clock, offset)
+
+    def chunks(self, size: int) -> Optional[Iterator[list]]:
+        """Lists of ``(global_offset, element)`` pairs when the source can cut them itself
+        (``read_chunks``), else ``None`` (iterate element-wise)."""
+        src = self.node.source
+        rc = getattr(src, "read_chunks", None)
+        if rc is None or self.mode not in ("all", "shard") or self._skip_until:
+            return None
+        rank, world = (self.rank, self.world) if self.mode == "shard" else (0, 1)
+
+        def gen():
+            for pairs in rc(rank, world, self.offset, size):
+                self.offset = pairs[-1][0] + 1
+                yield pairs
+            total = getattr(src, "global_length", None)
+            if callable(total):
+                self.offset = max(self.offset, int(total()))
+
+        return gen()
 
     def __iter__(self) -> Iterator[Tuple[int, Any]]:
         if self._strided:  # (global offset, element) pairs of this rank only

@@ -173,9 +173,12 @@ def test_udf_branching_on_score_is_batch_invariant(fixtures_dir):
         return ("lo", p)
 
     ref = StreamExecutionEnvironment().from_collection(vals).evaluate(ModelReader(fixtures_dir["kmeans"]), udf).collect()
-    before = METRICS.counters.get("batcher.per_record_reruns", 0)
     out = StreamExecutionEnvironment().from_collection(vals).evaluate(
         ModelReader(fixtures_dir["kmeans"]), udf, batch_size=5).collect()
+    assert out == ref  # deferred mode: the branch resolves the pending calls, f runs once
+    before = METRICS.counters.get("batcher.per_record_reruns", 0)
+    out = StreamExecutionEnvironment().from_collection(vals).evaluate(
+        ModelReader(fixtures_dir["kmeans"]), udf, config=ScoringConfig(batch_size=5, udf_mode="replay")).collect()
     assert out == ref
     assert METRICS.counters.get("batcher.per_record_reruns", 0) > before
 
@@ -238,3 +241,95 @@ def test_host_fallback_policy_counts_and_can_refuse(fixtures_dir, monkeypatch):
         engine.make_scorer(model.compiled, "cuda:0", ScoringConfig(fallback="error"))
     X = _matrix(7, seed=9)
     assert sc.submit_batch(RecordBatch(X)).to_list() == [model.predict(DenseVector(r)) for r in X]
+
+
+def test_dense_nan_is_not_replaced_in_batches(fixtures_dir):
+    """A NaN *stored* in a DenseVector stays a PMML missing value under replace_nan (the key is
+    present in the reference's input map, `S/api/PmmlModel.scala:143-152`): batched == per record."""
+    from flink_jpmml_amd.api.pmml_model import PmmlModel
+
+    m = PmmlModel.from_path(fixtures_dir["kmeans"])
+    vecs = [DenseVector(1.0, float("nan"), 1.0, 1.0), DenseVector(6.9, 3.1, 5.8, 2.1)]
+    per = [m.predict(v, 0.0) for v in vecs]
+    batch = RecordBatch.from_vectors(vecs, 4)
+    assert m.predict_records(batch, replace_nan=0.0).to_list() == per
+    assert m.predict_vectors(vecs, replace_nan=0.0) == per
+
+
+@pytest.mark.parametrize("chunked", [True, False])
+def test_batched_udf_runs_exactly_once_per_event(fixtures_dir, chunked):
+    """with batch_size set the UDF is called once per event (side effects
+    once), its predictions are scored in one batch per flush, results equal per-record."""
+    calls = []
+    vals = [(1.0, 1.0, 1.0, 1.0), (1.0, 2.0, 3.0, 4.0), (1.0, 2.0), (6.9, 3.1, 5.8, 2.1)] * 25
+
+    def udf(e, m):
+        calls.append(e)
+        return e, m.predict(DenseVector(*e))
+
+    ref = StreamExecutionEnvironment().from_collection(vals).evaluate(
+        ModelReader(fixtures_dir["kmeans"]), lambda e, m: (e, m.predict(DenseVector(*e)))).collect()
+    env = StreamExecutionEnvironment()
+    src = env.from_collection(vals) if chunked else env.add_source(_IterSource(vals))
+    before = METRICS.counters.get("batcher.resolves", 0)
+    out = src.evaluate(ModelReader(fixtures_dir["kmeans"]), udf, batch_size=16).collect()
+    assert len(calls) == len(vals)  # exactly once per event
+    assert out == ref
+    assert METRICS.counters.get("batcher.resolves", 0) - before == -(-len(vals) // 16)  # one per batch
+
+
+def test_dynamic_batched_udf_exactly_once_with_lazy_value(fixtures_dir):
+    """The reference's dynamic UDF returns ``prediction.value`` (E/DynamicEvaluateKmeans.scala:54-60):
+    the Target stays lazy, so events still batch; Add/Del boundaries keep their semantics."""
+    seen = []
+    seq = [("L", (N1, (1.0, 1.0, 1.0, 1.0))), ("R", AddMessage(N1, 1, fixtures_dir["kmeans"], 0))] + \
+          [("L", (N1, (1.0 + i / 10, 2.0, 3.0, 1.0))) for i in range(20)] + [("R", DelMessage(N1, 1, 0))] + \
+          [("L", (N1, (1.0, 1.0, 1.0, 1.0)))]
+
+    class Ev:
+        def __init__(self, mid, v):
+            self.model_id, self.v = f"{mid}_1", v
+
+    def udf(e, m):
+        seen.append(e)
+        return m.predict(DenseVector(*e.v), 0.0).value
+
+    def run(bs):
+        env = StreamExecutionEnvironment()
+        ev, ctrl = env.from_either([(t, Ev(*x) if t == "L" else x) for t, x in seq])
+        return ev.with_support_stream(ctrl).evaluate(udf, batch_size=bs).collect()
+
+    ref = run(None)
+    n = len(seen)
+    out = run(8)
+    assert len(seen) == 2 * n  # once per event in each run
+    assert [repr(t) for t in out] == [repr(t) for t in ref]
+    assert repr(out[0]) == "EmptyScore" and repr(out[-1]) == "EmptyScore" and out[1] == Score(3.0)
+
+
+def test_to_batches_adapter_matches_per_record(fixtures_dir):
+    """events.to_batches(extract) → RecordBatches → quick_evaluate → unbatch gives each event's
+    per-record prediction (vectorised event → RecordBatch adapter)."""
+    from tests.test_stream import DynamicInput
+
+    m = PmmlModel.from_path(fixtures_dir["kmeans"])
+    evs = [DynamicInput(f"{N1}_1", (1.0 + (i % 9) / 2, 2.0, 3.0 - (i % 4) / 3, 1.0), occurred_on=i) for i in range(700)]
+    env = StreamExecutionEnvironment()
+    out = env.from_collection(evs).to_batches(lambda e: e.values, batch_rows=128) \
+        .quick_evaluate(ModelReader(fixtures_dir["kmeans"])).unbatch().collect()
+    assert [e for _, e in out] == evs
+    assert [p for p, _ in out] == [m.predict(e.to_vector()) for e in evs]
+
+
+def test_to_batches_dynamic_ids_and_latency(fixtures_dir):
+    seq = [("R", AddMessage(N1, 1, fixtures_dir["kmeans"], 0))] + \
+          [("L", (f"{N1 if i % 2 else N2}_1", (1.0, 1.0, 1.0, 1.0))) for i in range(10)]
+    env = StreamExecutionEnvironment()
+    ev, ctrl = env.from_either(seq)
+    batches = ev.to_batches(lambda e: e[1], batch_rows=4, model_id=lambda e: e[0])
+    out = batches.with_support_stream(ctrl).evaluate(lambda b, m: (b.model_id, m.predict(b).values(-1.0).tolist())) \
+        .collect()
+    got = {}
+    for mid, vals in out:
+        got.setdefault(mid, []).extend(vals)
+    assert got[f"{N1}_1"] == [3.0] * 5 and got[f"{N2}_1"] == [-1.0] * 5
