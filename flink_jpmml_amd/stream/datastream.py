@@ -289,6 +289,8 @@ class StreamExecutionEnvironment:
             self.checkpoint_storage = CheckpointStorage(directory)
         elif self.config is not None and self.config.checkpoint_dir:
             self.checkpoint_storage = CheckpointStorage(self.config.checkpoint_dir)
+        elif os.environ.get("FJA_CHECKPOINT_DIR"):  # set by the restart supervisor
+            self.checkpoint_storage = CheckpointStorage(os.environ["FJA_CHECKPOINT_DIR"])
         return self
 
     enableCheckpointing = enable_checkpointing  # noqa: N815
@@ -383,6 +385,10 @@ class StreamExecutionEnvironment:
 
     # ------------------------------------------------------------------ execution
     def execute(self, job_name: str = "flink_jpmml_amd job", restore: Optional[str] = None) -> JobExecutionResult:
+        """Run the job. ``restore`` resumes from a checkpoint manifest; without one a job started by
+        the restart supervisor (:mod:`flink_jpmml_amd.launch`) resumes from ``FJA_RESTORE``."""
+        if restore is None:
+            restore = os.environ.get("FJA_RESTORE") or None
         sinks, self._sinks = self._sinks, []
         if not sinks:
             raise RuntimeError("no sinks defined: nothing to execute")

@@ -16,6 +16,8 @@ path is exercised deterministically:
 
 Environment form (read once by :func:`injector`): ``FJA_FAULTS="fail_load=bad.xml;
 corrupt_pmml=torn;kill_rank=1@3"`` (``;``-separated, ``kill_rank=<rank>@<batch>``).
+``FJA_FAULT_ATTEMPTS=k`` limits the faults to the first ``k`` attempts of a job run under the
+restart supervisor (``FJA_ATTEMPT``, :mod:`flink_jpmml_amd.launch`): the restarted job runs clean.
 """
 
 from __future__ import annotations
@@ -88,7 +90,11 @@ def injector() -> FaultInjector:
     """Process-wide injector (from ``FJA_FAULTS`` on first use)."""
     global _INJECTOR
     if _INJECTOR is None:
-        _INJECTOR = FaultInjector.parse(os.environ.get("FJA_FAULTS", ""))
+        spec = os.environ.get("FJA_FAULTS", "")
+        limit = os.environ.get("FJA_FAULT_ATTEMPTS")
+        if limit is not None and int(os.environ.get("FJA_ATTEMPT", "0")) >= int(limit):
+            spec = ""
+        _INJECTOR = FaultInjector.parse(spec)
     return _INJECTOR
 
 

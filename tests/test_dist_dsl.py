@@ -349,3 +349,54 @@ def test_text_source_splits_bytes_across_ranks(fixtures_dir, tmp_path):
     per_rank = [res[r][0] for r in range(4)]
     assert all(b > 0 for b in per_rank) and sum(per_rank) == data_bytes
     assert all(res[r][1] == 997 for r in range(4))  # collect() all-gathers every rank's rows
+
+
+# ------------------------------------------------------------------ restart strategy
+
+SUPERVISED_JOB = r"""
+import os, sys
+sys.path.insert(0, os.environ["FJA_ROOT"])
+from tests.test_dist_dsl import job_exactly_once
+kmeans, out_dir = sys.argv[1], sys.argv[2]
+job_exactly_once(kmeans, out_dir, os.environ["FJA_CHECKPOINT_DIR"], None)
+"""
+
+
+def test_supervisor_restarts_killed_job_exactly_once(fixtures_dir, tmp_path):
+    """kill_rank=1@9 on the first attempt: the supervisor sees the dead rank, stops the survivor,
+    relaunches both ranks as fresh processes restoring CheckpointStorage.latest() on their own —
+    the committed output equals the uninterrupted run's (no manual restore=)."""
+    import sys
+
+    from flink_jpmml_amd.launch import Supervisor
+    from flink_jpmml_amd.stream import FileSink
+    from flink_jpmml_amd.utils.faults import EXIT_KILLED_RANK
+
+    k = fixtures_dir["kmeans"]
+    ref_dir, ref_ck = str(tmp_path / "ref"), str(tmp_path / "ref-ck")
+    res, codes = _spawn(2, job_exactly_once, (k, ref_dir, ref_ck, None))
+    assert codes == [0, 0], res
+    expected = sorted(map(tuple, FileSink.read(ref_dir)))
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out_dir, ck = str(tmp_path / "out"), str(tmp_path / "ck")
+    env = dict(os.environ, FJA_ROOT=root, FJA_FAULTS="kill_rank=1@9", FJA_FAULT_ATTEMPTS="1",
+               FJA_DIST_TIMEOUT_S="20")
+    env.pop("FJA_RESTORE", None)
+    sup = Supervisor([sys.executable, "-c", SUPERVISED_JOB, k, out_dir], nproc=2, checkpoint_dir=ck,
+                     max_restarts=2, restart_delay_s=0.2, grace_s=2.0, env=env, attempt_timeout_s=150)
+    assert sup.run() == 0
+    assert len(sup.attempts) == 2
+    assert EXIT_KILLED_RANK in sup.attempts[0].exit_codes
+    assert sup.attempts[1].restore is not None and sup.attempts[1].ok
+    assert sorted(map(tuple, FileSink.read(out_dir))) == expected
+
+
+def test_supervisor_gives_up_after_max_restarts(tmp_path):
+    import sys
+
+    from flink_jpmml_amd.launch import Supervisor
+
+    sup = Supervisor([sys.executable, "-c", "import sys; sys.exit(3)"], nproc=2, checkpoint_dir=str(tmp_path),
+                     max_restarts=1, restart_delay_s=0.0, grace_s=0.5)
+    assert sup.run() == 3 and len(sup.attempts) == 2
