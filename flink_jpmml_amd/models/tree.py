@@ -53,14 +53,12 @@ class TreeEvaluator(ModelEvaluator):
         self.tree = model
         if model.missing_value_strategy in ("weightedConfidence", "aggregateNodes"):
             raise UnsupportedFeatureException(f"missingValueStrategy {model.missing_value_strategy!r}")
-        self.nodes: List[ir.Node] = []
-        self._index: Dict[int, int] = {}
-        stack = [model.root]
-        while stack:
-            nd = stack.pop()
-            self._index[id(nd)] = len(self.nodes)
-            self.nodes.append(nd)
-            stack.extend(reversed(nd.children))
+        self._nodes: Optional[List[ir.Node]] = None
+        self._index_map: Optional[Dict[int, int]] = None
+        if model.flat is not None:
+            self._init_flat(model.flat)
+            return
+        self._build_node_list()
         if self.kind == "classification":
             cats = self.classification_categories()
             seen = set(cats)
@@ -86,6 +84,77 @@ class TreeEvaluator(ModelEvaluator):
         else:
             self.categories = None
             self.node_value = np.array([_num(nd.score) for nd in self.nodes], dtype=np.float64)
+
+    # -- node list (preorder, first child first): built from the IR, or materialised lazily from a
+    #    flat body (pmml/flat.py) only when an object-level consumer needs it
+    def _build_node_list(self) -> None:
+        nodes: List[ir.Node] = []
+        index: Dict[int, int] = {}
+        stack = [self.tree.root]
+        while stack:
+            nd = stack.pop()
+            index[id(nd)] = len(nodes)
+            nodes.append(nd)
+            stack.extend(reversed(nd.children))
+        self._nodes, self._index_map = nodes, index
+
+    @property
+    def nodes(self) -> List[ir.Node]:
+        if self._nodes is None:
+            self._build_node_list()
+        return self._nodes
+
+    @property
+    def _index(self) -> Dict[int, int]:
+        if self._index_map is None:
+            self._build_node_list()
+        return self._index_map
+
+    def _init_flat(self, ft) -> None:
+        """Node tables straight from the flat arrays (same values as the object path)."""
+        a = ft.a
+        n = ft.n
+        if self.kind != "classification":
+            self.categories = None
+            self.node_value = np.array(a["score_d"], dtype=np.float64)
+            return
+        cats = self.classification_categories()
+        strings = ft.strings
+        # categories beyond the declared ones, in first-appearance order over (score, distributions…)
+        keys = np.concatenate([np.arange(n, dtype=np.int64) * 2, a["dist_node"].astype(np.int64) * 2 + 1])
+        vals = np.concatenate([a["score_s"], a["dist_value_s"]]).astype(np.int64)
+        order = np.argsort(keys, kind="stable")
+        seq = vals[order]
+        seq = seq[seq >= 0]
+        uniq, first = np.unique(seq, return_index=True)
+        seen = set(cats)
+        for k in uniq[np.argsort(first)]:
+            v = strings[int(k)]
+            if v not in seen:
+                cats.append(v)
+                seen.add(v)
+        self.categories = cats
+        cat_of = {c: i for i, c in enumerate(cats)}
+        code = np.full(len(strings) + 1, -1, dtype=np.int64)  # string index -> category (-1: none)
+        for k in np.unique(np.concatenate([a["score_s"], a["dist_value_s"]])).tolist():
+            if k >= 0:
+                code[k] = cat_of[strings[k]]
+        C = len(cats)
+        sc = code[a["score_s"]]
+        self.node_label = np.where(sc >= 0, sc, NAN).astype(np.float64)
+        probs = np.zeros((n, C))
+        has_score = sc >= 0
+        probs[np.nonzero(has_score)[0], sc[has_score]] = 1.0
+        dn = a["dist_node"].astype(np.int64)
+        if dn.size:
+            tot = np.bincount(dn, weights=a["dist_count"], minlength=n)
+            p = np.where(np.isnan(a["dist_prob"]),
+                         np.divide(a["dist_count"], tot[dn], out=np.zeros(dn.size), where=tot[dn] != 0),
+                         a["dist_prob"])
+            with_d = np.unique(dn)
+            probs[with_d] = 0.0  # distributions replace the score's one-hot
+            probs[dn, code[a["dist_value_s"]]] = p
+        self.node_probs = probs
 
     def leaf_index(self, cols: Columns) -> np.ndarray:
         """Index (into ``self.nodes``) of the scoring node per row; -1 = null prediction."""
@@ -212,6 +281,19 @@ def member_form(pa: ir.Predicate, pb: ir.Predicate):
     return None
 
 
+def _flat_member_candidates(ft) -> bool:
+    """Whether a flat body has binary splits whose first child is a set or (in)equality
+    predicate (the shapes :func:`member_form` turns into membership columns)."""
+    from ..pmml.flat import P_RAW, P_SIMPLE
+
+    internal = np.nonzero(ft.n_children == 2)[0]
+    if internal.size == 0:
+        return False
+    ca = ft.child(internal, 0)
+    kind, op = ft.a["pred_kind"][ca], ft.a["pred_op"][ca]
+    return bool(np.any(kind == P_RAW) or np.any((kind == P_SIMPLE) & (op <= 1)))
+
+
 def membership_fields(model: ir.Model) -> Dict[str, ir.DerivedField]:
     """Synthetic DerivedFields (MapValues lookups: member 1, non-member 0, missing -> missing) for
     every categorical binary split of the model's trees (nested segments included)."""
@@ -224,6 +306,8 @@ def membership_fields(model: ir.Model) -> Dict[str, ir.DerivedField]:
             return
         if not isinstance(m, ir.TreeModel):
             return
+        if m.flat is not None and not _flat_member_candidates(m.flat):
+            return  # no set / equality splits: nothing to add (no object materialisation)
         stack = [m.root]
         while stack:
             nd = stack.pop()
@@ -243,6 +327,105 @@ def membership_fields(model: ir.Model) -> Dict[str, ir.DerivedField]:
     return out
 
 
+_FLAT_NUMERIC_OPS = {2: "lessThan", 3: "lessOrEqual", 4: "greaterThan", 5: "greaterOrEqual"}
+
+
+def _lower_flat(ev: TreeEvaluator, ft, field_index: Dict[str, int]) -> Optional[BinaryTree]:
+    """:func:`lower_binary_tree` on a flat body, vectorised (no per-node Python). Returns ``None``
+    for shapes it leaves to the object path (categorical member splits, folded fields)."""
+    from ..pmml.flat import P_RAW, P_SIMPLE, P_TRUE
+
+    tm = ev.tree
+    strat = tm.missing_value_strategy
+    a = ft.a
+    kind = a["pred_kind"]
+    if kind[0] != P_TRUE:
+        raise NotBinary("root predicate is not True")
+    n = ft.n
+    nch = ft.n_children
+    internal = np.nonzero(nch > 0)[0]
+    leaves = nch == 0
+    if np.any(nch[internal] != 2):
+        raise NotBinary("node does not have exactly two children")
+    ca, cb = ft.child(internal, 0), ft.child(internal, 1)
+    ka, kb = kind[ca], kind[cb]
+    opa, opb = a["pred_op"][ca], a["pred_op"][cb]
+    if np.any(ka == P_RAW) or np.any(kb == P_RAW) or np.any((ka == P_SIMPLE) & (opa <= 1)):
+        return None  # SimpleSet / equality splits: membership columns (object path)
+    folds = getattr(field_index, "folds", None) or {}
+    if np.any(ka != P_SIMPLE) or np.any((opa < 2) | (opa > 5)):
+        raise NotBinary("first child predicate is not a numeric comparison")
+    fa = a["pred_field"][ca]
+    uniq_f = np.unique(fa)
+    fcol = np.full(len(ft.strings) + 1, -1, dtype=np.int32)
+    for k in uniq_f.tolist():
+        name = ft.strings[k]
+        if name in folds:
+            return None  # monotone derived fields fold per split value (object path)
+        if name not in field_index or ev.schema.is_string(name):
+            raise NotBinary("split on a non-input or string field")
+        fcol[k] = field_index[name]
+    neg = np.array([1, 0, 5, 4, 3, 2, 7, 6], dtype=np.int8)  # _NEG on operator codes
+    comp = (kb == P_SIMPLE) & (a["pred_field"][cb] == fa) & (opb == neg[opa]) & \
+        (a["pred_value_s"][cb] == a["pred_value_s"][ca])
+    second_true = kb == P_TRUE
+    if not np.all(second_true | comp):
+        raise NotBinary("second child is not the complement of the first")
+    t = a["pred_value_d"][ca]
+    if np.any(np.isnan(t)) and np.any(np.isnan(t) & (a["pred_value_s"][ca] >= 0)):
+        raise NotBinary("non-numeric split value")
+    forms = set()
+    if strat == "defaultChild":
+        if np.any(a["default_s"][internal] < 0):
+            raise NotBinary("defaultChild strategy without defaultChild attribute")
+        dp = a["default_pos"][internal]
+        if np.any((dp != 0) & (dp != 1)):
+            raise NotBinary("defaultChild does not name a child")
+        go_left = dp == 0
+    elif strat == "nullPrediction":
+        go_left = np.zeros(internal.size, dtype=bool)
+    else:
+        if second_true.any():
+            forms.add("true")
+        if (~second_true).any():
+            if tm.no_true_child_strategy != "returnNullPrediction":
+                raise NotBinary("missing value under returnLastPrediction needs internal-node scores")
+            forms.add("complement")
+        if len(forms) > 1:
+            raise NotBinary("'none' strategy mixing True and complement second children")
+        go_left = np.zeros(internal.size, dtype=bool)
+    classification = ev.kind == "classification"
+    leaf_idx = np.nonzero(leaves)[0]
+    leafv = np.full(n, NAN)
+    if classification:
+        leafv[leaf_idx] = ev.node_label[leaf_idx]
+    else:
+        leafv[leaf_idx] = ev.node_value[leaf_idx]
+    if np.any(np.isnan(leafv[leaf_idx])):
+        raise NotBinary("leaf without score")
+    feature = np.full(n, -1, dtype=np.int32)
+    thr = np.zeros(n)
+    op = np.zeros(n, dtype=np.int8)
+    dleft = np.zeros(n, dtype=bool)
+    left = np.full(n, -1, dtype=np.int32)
+    right = np.full(n, -1, dtype=np.int32)
+    feature[internal] = fcol[fa]
+    thr[internal] = t
+    code = np.zeros(8, dtype=np.int8)
+    for k, name in _FLAT_NUMERIC_OPS.items():
+        code[k] = _OPS[name]
+    op[internal] = code[opa]
+    dleft[internal] = go_left
+    left[internal], right[internal] = ca, cb
+    probs = None
+    if classification:
+        probs = np.zeros((n, len(ev.categories)))
+        probs[leaf_idx] = ev.node_probs[leaf_idx]
+    return BinaryTree(feature=feature, threshold=thr, op=op, default_left=dleft, left=left, right=right,
+                      leaf_value=leafv, leaf_probs=probs, depth=int(a["depth"][leaves].max()) if n else 0,
+                      null_missing=strat == "nullPrediction" or forms == {"complement"})
+
+
 def lower_binary_tree(ev: TreeEvaluator, field_index: Dict[str, int]) -> BinaryTree:
     """Lower a TreeModel into pointer-form binary arrays, or raise :class:`NotBinary`.
 
@@ -260,6 +443,10 @@ def lower_binary_tree(ev: TreeEvaluator, field_index: Dict[str, int]) -> BinaryT
     strat = tm.missing_value_strategy
     if strat not in ("none", "defaultChild", "nullPrediction"):
         raise NotBinary(f"missingValueStrategy {strat}")
+    if tm.flat is not None:
+        bt = _lower_flat(ev, tm.flat, field_index)
+        if bt is not None:
+            return bt
     null_missing = strat == "nullPrediction"
     forms = set()  # 'none' strategy: second child True (missing -> right) or complement (-> null)
     if not isinstance(tm.root.predicate, ir.TruePredicate):

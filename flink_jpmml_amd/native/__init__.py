@@ -44,6 +44,7 @@ def build(force: bool = False) -> str:
 
 
 FAST_SRC = os.path.join(HERE, "csrc", "fastpath.cpp")
+FAST_SRCS = [FAST_SRC, os.path.join(HERE, "csrc", "pmml_scan.cpp")]
 _fast = None
 
 
@@ -58,11 +59,11 @@ def build_fastpath(force: bool = False) -> str:
     import sysconfig
 
     out = _fast_path()
-    if not force and os.path.exists(out) and os.path.getmtime(out) >= os.path.getmtime(FAST_SRC):
+    if not force and os.path.exists(out) and all(os.path.getmtime(out) >= os.path.getmtime(s) for s in FAST_SRCS):
         return out
     tmp = out + ".tmp"
     cmd = ["g++", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall", "-fvisibility=hidden",
-           "-I" + sysconfig.get_paths()["include"], "-I" + np.get_include(), FAST_SRC, "-o", tmp]
+           "-I" + sysconfig.get_paths()["include"], "-I" + np.get_include(), *FAST_SRCS, "-o", tmp]
     r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
     if r.returncode != 0:
         raise NativeBuildError(r.stdout.decode(errors="replace"))

@@ -11,6 +11,7 @@
 //   * make_predictions — scores/valid arrays -> list of Prediction(Score(x)) / the shared
 //                       EmptyScore prediction. Objects are allocated with tp_alloc and their slots
 //                       filled directly (the Python __init__s only assign those same slots).
+//   * scan_trees      — the streaming TreeModel reader of large PMML documents (pmml_scan.cpp).
 //
 // Both return None / -1 when an input does not have the exact expected shape; the Python caller
 // then takes its general (slower, element-wise) path — results are identical either way.
@@ -19,9 +20,12 @@
 #include <Python.h>
 #include <structmember.h>
 #define NPY_NO_DEPRECATED_API NPY_1_7_API_VERSION
+#define PY_ARRAY_UNIQUE_SYMBOL fja_fastpath_ARRAY_API
 #include <numpy/arrayobject.h>
 
 #include <cstring>
+
+PyObject *fja_scan_trees(PyObject *, PyObject *args);  // pmml_scan.cpp
 
 namespace {
 
@@ -128,6 +132,7 @@ PyObject *make_predictions(PyObject *, PyObject *args) {
 PyMethodDef methods[] = {
     {"pack_dense", pack_dense, METH_VARARGS, "Pack a list of DenseVector objects into a float64 matrix."},
     {"make_predictions", make_predictions, METH_VARARGS, "Prediction objects for a scored batch."},
+    {"scan_trees", fja_scan_trees, METH_VARARGS, "Streaming TreeModel reader: (skeleton, flat trees, strings)."},
     {nullptr, nullptr, 0, nullptr},
 };
 

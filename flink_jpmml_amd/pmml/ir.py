@@ -323,6 +323,25 @@ class TreeModel(Model):
     missing_value_penalty: float = 1.0
     no_true_child_strategy: str = "returnNullPrediction"
     split_characteristic: str = "multiSplit"
+    flat: Any = field(default=None, repr=False, compare=False)
+    """:class:`~flink_jpmml_amd.pmml.flat.FlatTree` when the body came from the streaming scanner
+    (``root`` is then materialised from it on first access)."""
+
+
+def _tree_root_get(self):
+    r = self.__dict__.get("_root")
+    if r is None:
+        flat = self.__dict__.get("flat")
+        if flat is not None:
+            r = self.__dict__["_root"] = flat.materialize()
+    return r
+
+
+def _tree_root_set(self, v):
+    self.__dict__["_root"] = v
+
+
+TreeModel.root = property(_tree_root_get, _tree_root_set)  # type: ignore[assignment]
 
 
 # mining ---------------------------------------------------------------------

@@ -11,6 +11,7 @@ Parsing uses the C-accelerated ``xml.etree.ElementTree``; for very large ensembl
 
 from __future__ import annotations
 
+import contextvars
 import re
 import shlex
 import xml.etree.ElementTree as ET
@@ -397,7 +398,12 @@ def _parse_tree(el: ET.Element) -> ir.TreeModel:
     root = _child(el, "Node")
     if root is None:
         raise PmmlParseError("TreeModel without root Node")
-    m.root = _parse_node(root)
+    flat_k = root.get("fjaFlat")
+    flats = _FLATS.get()
+    if flat_k is not None and flats is not None:
+        m.flat = flats[int(flat_k)]  # body read by the streaming scanner (pmml/flat.py)
+    else:
+        m.root = _parse_node(root)
     m.missing_value_strategy = el.get("missingValueStrategy", "none")
     m.missing_value_penalty = _f(el, "missingValuePenalty", 1.0)
     m.no_true_child_strategy = el.get("noTrueChildStrategy", "returnNullPrediction")
@@ -717,9 +723,30 @@ def parse_element(root: ET.Element) -> ir.PMMLDocument:
                            header=header)
 
 
-def parse_string(text: str) -> ir.PMMLDocument:
+_FLATS: "contextvars.ContextVar[Optional[list]]" = contextvars.ContextVar("fja_flat_trees", default=None)
+
+
+def parse_string(text) -> ir.PMMLDocument:
     """Parse a PMML document held in memory (the reference reads the whole file into a String
-    first: `S/api/reader/FsReader.scala:41-49`)."""
+    first: `S/api/reader/FsReader.scala:41-49`). Large documents (``str`` or ``bytes``) go through
+    the native streaming scanner first: tree bodies become flat arrays, only the small skeleton is
+    parsed here (:mod:`flink_jpmml_amd.pmml.flat`)."""
+    from .flat import SCAN_MIN_BYTES, scan_document
+
+    if len(text) >= SCAN_MIN_BYTES:
+        data = text.encode("utf-8") if isinstance(text, str) else text
+        scanned = scan_document(data)
+        if scanned is not None:
+            skeleton, flats = scanned
+            token = _FLATS.set(flats)
+            try:
+                try:
+                    root = ET.fromstring(skeleton)
+                except ET.ParseError as e:
+                    raise PmmlParseError(f"malformed PMML XML: {e}") from e
+                return parse_element(root)
+            finally:
+                _FLATS.reset(token)
     if isinstance(text, bytes):
         text = text.decode("utf-8")
     try:
@@ -730,6 +757,13 @@ def parse_string(text: str) -> ir.PMMLDocument:
 
 
 def parse_file(path: str) -> ir.PMMLDocument:
+    import os
+
+    from .flat import SCAN_MIN_BYTES
+
+    if os.path.getsize(path) >= SCAN_MIN_BYTES:
+        with open(path, "rb") as fh:
+            return parse_string(fh.read())
     try:
         tree = ET.parse(path)
     except ET.ParseError as e:

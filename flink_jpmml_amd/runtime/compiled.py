@@ -45,7 +45,8 @@ class CompiledPmml:
 
     # ------------------------------------------------------------------ construction
     @staticmethod
-    def from_string(text: str, source: Optional[str] = None) -> "CompiledPmml":
+    def from_string(text, source: Optional[str] = None) -> "CompiledPmml":
+        """From the document text (``str``) or its UTF-8 bytes."""
         return CompiledPmml(parse_string(text), source)
 
     @staticmethod
@@ -53,8 +54,7 @@ class CompiledPmml:
         from ..api.reader import ModelReader
 
         try:
-            text = ModelReader(path).build_distributed_path()
-            return CompiledPmml.from_string(text, source=path)
+            return CompiledPmml.from_string(ModelReader(path).read_bytes(), source=path)
         except (OSError, PmmlParseError, ValueError) as e:
             raise ModelLoadingException(str(e), e) from e
 

@@ -131,7 +131,10 @@ def referenced_fields(model: ir.Model) -> List[str]:
 
     def walk(m: ir.Model) -> None:
         active = [f.name for f in m.mining_schema.active]
-        if isinstance(m, ir.TreeModel):
+        if isinstance(m, ir.TreeModel) and m.flat is not None:
+            for f in m.flat.field_names():
+                add(f)
+        elif isinstance(m, ir.TreeModel):
             stack = [m.root]
             while stack:
                 nd = stack.pop()
@@ -492,7 +495,17 @@ def _resolve_folds(model: ir.Model, folds: Dict[str, tuple]) -> None:
     want: Dict[str, Dict[tuple, None]] = {n: {} for n in folds}
 
     def walk(m: ir.Model) -> None:
-        if isinstance(m, ir.TreeModel):
+        if isinstance(m, ir.TreeModel) and m.flat is not None and not m.flat.raw:
+            from ..pmml.flat import OP_NAMES, P_SIMPLE
+
+            a = m.flat.a
+            simple = np.nonzero(a["pred_kind"] == P_SIMPLE)[0]
+            for k in simple.tolist():
+                name = m.flat.strings[int(a["pred_field"][k])]
+                opn = OP_NAMES[int(a["pred_op"][k])]
+                if name in want and opn in _OPS and not np.isnan(a["pred_value_d"][k]):
+                    want[name][(_OPS[opn], float(a["pred_value_d"][k]))] = None
+        elif isinstance(m, ir.TreeModel):
             stack = [m.root]
             while stack:
                 nd = stack.pop()

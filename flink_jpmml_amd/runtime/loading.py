@@ -88,8 +88,10 @@ def _header(compiled) -> dict:
             "output_fields": list(getattr(compiled, "output_fields", [])), "model_name": compiled.model_name}
 
 
-def _read(path: str) -> str:
-    return ModelReader(path).build_distributed_path()
+def _read(path: str) -> bytes:
+    """The document's bytes (UTF-8): parsed directly by the streaming scanner for large models and
+    hashed as-is — no 2× decode/encode of a several-hundred-MB string."""
+    return ModelReader(path).read_bytes()
 
 
 def load_local(path: str, device: Any = None, config: Any = None, pipeline: Any = None) -> LoadedModel:
@@ -108,7 +110,7 @@ def load_local(path: str, device: Any = None, config: Any = None, pipeline: Any 
     ms = (time.perf_counter() - t0) * 1e3
     METRICS.observe("model.load_ms", ms)
     METRICS.inc("model.loads")
-    return LoadedModel(model, hashlib.sha256(text.encode()).hexdigest(), path, ms)
+    return LoadedModel(model, hashlib.sha256(text).hexdigest(), path, ms)
 
 
 def _sync_device(device) -> None:
@@ -176,7 +178,7 @@ def load_replicated(path: str, ctx, device: Any = None, config: Any = None, pipe
     ms = (time.perf_counter() - t0) * 1e3
     METRICS.observe("model.load_ms", ms)
     METRICS.inc("model.loads_replicated")
-    return LoadedModel(model, hashlib.sha256(head["text"].encode()).hexdigest(), path, ms)
+    return LoadedModel(model, hashlib.sha256(head["text"]).hexdigest(), path, ms)
 
 
 class ModelLoader:
