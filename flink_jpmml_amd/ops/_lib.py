@@ -146,6 +146,10 @@ class GenTreeArgs(ctypes.Structure):
                 ("pool", c_void_p), ("trees", c_void_p), ("max_steps", c_int), ("pad", c_int)]
 
 
+class HybridArgs(ctypes.Structure):
+    _fields_ = [("t", TreeArgs), ("heads", c_void_p), ("head_words", c_int), ("pad", c_int)]
+
+
 class ClusterArgs(ctypes.Structure):
     _fields_ = [("X", c_void_p), ("n_rows", c_int), ("n_feat", c_int), ("ldx", c_int), ("K", c_int),
                 ("prep", c_void_p), ("centers", c_void_p), ("weights", c_void_p), ("scales", c_void_p),
@@ -190,6 +194,7 @@ _ABI = {
     "pmml_derive_args_size": DeriveArgs,
     "pmml_tree_args_size": TreeArgs,
     "pmml_tree_general_args_size": GenTreeArgs,
+    "pmml_tree_hybrid_args_size": HybridArgs,
     "pmml_cluster_args_size": ClusterArgs,
     "pmml_linear_args_size": LinearArgs,
     "pmml_mlp_args_size": MlpArgs,
@@ -253,6 +258,8 @@ def load(auto_build: bool = True) -> ctypes.CDLL:
             lib.pmml_svm_launch.argtypes = [c_void_p, ctypes.POINTER(SvmArgs), c_int, c_int]
         lib.pmml_tree_general_launch.argtypes = [c_void_p, ctypes.POINTER(GenTreeArgs)]
         lib.pmml_tree_general_launch.restype = c_int
+        lib.pmml_tree_hybrid_launch.argtypes = [c_void_p, ctypes.POINTER(HybridArgs), c_int, c_int]
+        lib.pmml_tree_hybrid_launch.restype = c_int
         lib.pmml_derive_launch.argtypes = [c_void_p, ctypes.POINTER(DeriveArgs)]
         lib.pmml_derive_launch.restype = c_int
         lib.pmml_mask_invalid.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int]

@@ -1111,13 +1111,13 @@ class TreePlan(DevicePlan):
                                   "blob", "leaves", "roots", "has_dr", "table", "slots", "splits", "epi_args",
                                   "variant", "children", "preds", "pool", "trees_tab", "max_steps", "blob_nan",
                                   "chunk_trees_nan", "full_epi", "labels", "mode", "tree_w", "acc_init", "feat_map",
-                                  "rows_wide", "n_stage")
+                                  "rows_wide", "n_stage", "heads", "head_depth")
 
     WIDE_G = 4  # tree groups of the wide kernel (mirrors csrc)
 
     def __init__(self, compiled, device, layout: str = "auto", lds_budget: int = 80 * 1024, splits: int = 0,
                  variant: str = "auto", precision: str = "fp32", nan_mode: str = "auto", max_chunk_trees: int = 0,
-                 tree_shard: Optional[Tuple[int, int]] = None):
+                 tree_shard: Optional[Tuple[int, int]] = None, head_depth: int = 0):
         """``nan_mode`` (wide PERFECT kernel): ``"auto"`` keeps tiles with missing values on the fast
         traversal whenever the ensemble has no null-on-missing trees (default-right nodes read a
         NaN -> +inf second feature plane, :func:`_nan_planes`); ``"off"``: per-node missing test.
@@ -1186,6 +1186,7 @@ class TreePlan(DevicePlan):
             return
         self.children = self.preds = self.pool = self.trees_tab = None
         self.max_steps = 0
+        self.heads, self.head_depth = None, 0
         NI, NL = (1 << depth) - 1, 1 << depth
         # wide kernel geometry: stage only the columns the trees read (+ columns whose preparation
         # can reject a row); row tiles of 256 / 128 / 64 rows keep the feature planes <= 64 KiB
@@ -1195,7 +1196,7 @@ class TreePlan(DevicePlan):
                    and (spec.mode == "sum" or spec.C <= 8))
         if layout == "auto":
             rec_bytes = 4 * (2 * NI + NL * spec.P + (NI + 31) // 32)
-            layout = "perfect" if depth <= 10 and (wide_ok or F <= 64) and rec_bytes <= 32 * 1024 else "pointer"
+            layout = "perfect" if depth <= 10 and (wide_ok or F <= 64) and rec_bytes <= 32 * 1024 else "hybrid"
         if spec.mode != "sum" and not (layout == "perfect" and wide_ok):
             spec = to_general(spec)  # votes / class slots accumulate in LDS on the narrow kernels
             self.n_trees = len(spec.trees)  # + constant stumps carrying the per-class intercepts
@@ -1296,14 +1297,34 @@ class TreePlan(DevicePlan):
         else:
             if precision == "fp8":
                 raise NotLowerable("fp8 leaves need the PERFECT layout")
-            nodes, leaves, roots, has_dr = _pointer_pack(spec.trees, spec.weights, spec.P)
+            from .hybrid import head_words, pack_trees
+
+            feat_lds = F <= 64
+            H = 0
+            if self.layout == "hybrid":
+                # PERFECT head of the top H levels in LDS + POINTER tail from L2 (tree_hybrid.hip)
+                H = head_depth or (8 if depth > 8 else max(4, depth // 2 * 2))
+                if H not in (4, 6, 8, 10):
+                    raise ValueError("head_depth must be 4, 6, 8 or 10")
+                fixed = (F * TB * 4 if feat_lds else 0) + TB * 4 + (self.C * TB * 4 if self.general else 0)
+                per_tree = head_words(H) * 4
+                fit = (lds_budget - fixed) // per_tree
+                if fit < 1:
+                    H, fit = 4, (lds_budget - fixed) // (head_words(4) * 4)
+                if fit < 1:
+                    raise NotLowerable("no LDS left for a hybrid head chunk")
+                self.chunk_trees = int(min(fit, self.n_trees, max_chunk_trees or 64))
+            else:
+                self.chunk_trees = 0
+            heads, nodes, leaves, roots, has_dr = pack_trees(spec.trees, spec.weights, spec.P, H, feat_lds)
             self.blob_nan, self.chunk_trees_nan = None, 0
-            self.rec_words = 0
-            self.chunk_trees = 0
+            self.head_depth = H
+            self.rec_words = head_words(H) if H else 0
             self.variant = 0
             self.blob = self._t(nodes.reshape(-1).view(np.int32))
             self.leaves = self._t(leaves.reshape(-1))
             self.roots = self._t(roots)
+            self.heads = self._t(heads.reshape(-1).view(np.int32)) if heads is not None else None
         if not (self.variant & 3):
             self.mode = 0  # narrow / pointer kernels: plain sums or LDS slot accumulators
         self.has_dr = has_dr
@@ -1436,6 +1457,15 @@ class TreePlan(DevicePlan):
                     self.__dict__.setdefault("_retired", []).append(self._partial)
                 self._partial = torch.empty(max(need, 1 << 20), dtype=torch.float32, device=self.device)
             a.partial = ptr(self._partial)
+        if self.layout == "hybrid":
+            from ..ops._lib import HybridArgs
+
+            h = HybridArgs()
+            h.t = a
+            h.heads, h.head_words = ptr(self.heads), int(self.rec_words)
+            rc = self.lib.pmml_tree_hybrid_launch(stream_handle(stream), ctypes.byref(h), int(self.head_depth), s)
+            check(rc, f"tree kernel (hybrid, head {self.head_depth}, depth {self.depth})")
+            return
         rc = self.lib.pmml_tree_launch(stream_handle(stream), ctypes.byref(a), 0 if self.layout == "perfect" else 1,
                                        self.depth, 1 if self.has_dr else 0, s)
         check(rc, f"tree kernel ({self.layout}, depth {self.depth})")

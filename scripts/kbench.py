@@ -29,6 +29,8 @@ def main():
     p.add_argument("--nan-mode", default="auto")
     p.add_argument("--tree-prof", action="store_true", help="tree: per-wave phase ticks of one workgroup")
     p.add_argument("--max-chunk-trees", type=int, default=0)
+    p.add_argument("--head-depth", type=int, default=0, help="hybrid layout: PERFECT head levels (4/6/8/10)")
+    p.add_argument("--p-split", type=float, default=None, help="tree generators: split probability per node")
     p.add_argument("--precision", default="fp32", choices=["fp32", "bf16", "fp8"])
     p.add_argument("--hidden", default="256,256", help="mlp hidden widths")
     p.add_argument("--mlp-kernel", default="auto", choices=["auto", "reg", "panel"], help="bf16 MLP kernel")
@@ -59,7 +61,8 @@ def main():
     elif args.model == "gbdt-binary":
         txt = synth.gbdt_pmml(n_trees=args.trees, depth=args.depth, n_features=args.features, objective="binary")
     elif args.model == "rf":
-        txt = synth.random_forest_pmml(n_trees=args.trees, depth=args.depth, n_features=args.features)
+        kw = {"p_split": args.p_split} if args.p_split is not None else {}
+        txt = synth.random_forest_pmml(n_trees=args.trees, depth=args.depth, n_features=args.features, **kw)
     elif args.model == "mlp":
         txt = synth.mlp_pmml(n_features=args.features, hidden=tuple(int(x) for x in args.hidden.split(",")))
     elif args.model == "svm":
@@ -76,7 +79,7 @@ def main():
     opts = {}
     if args.model.startswith(("gbdt", "rf")):
         opts = dict(layout=args.layout, lds_budget=args.lds_budget, variant=args.variant, nan_mode=args.nan_mode,
-                    max_chunk_trees=args.max_chunk_trees)
+                    max_chunk_trees=args.max_chunk_trees, head_depth=args.head_depth)
     elif args.model == "kmeans-big":
         opts = dict(cluster_variant=args.variant)
     if args.precision != "fp32":
@@ -131,6 +134,8 @@ def main():
                       "tflops": (flops / ms / 1e9) if flops else None, "precision": args.precision,
                       "rows_per_s": args.rows / ms * 1e3, "plan": type(plan).__name__,
                       "layout": getattr(plan, "layout", None), "chunk_trees": getattr(plan, "chunk_trees", None),
+                      "head_depth": getattr(plan, "head_depth", None), "depth": getattr(plan, "depth", None),
+                      "trees": getattr(plan, "n_trees", None),
                       "missing": args.missing, "lds_budget": args.lds_budget,
                       "variant": getattr(plan, "variant", None), "mlp_prof": prof,
                       "mlp_kernel": ("reg" if getattr(plan, "reg_kernel", 0) else "panel") if args.model == "mlp" else None}))

@@ -1,0 +1,64 @@
+"""Deep forests on the MI355X: HYBRID layout (PERFECT head in LDS + POINTER tail) and the
+vectorised POINTER layout against the float64 oracle, incl. an unbounded-depth (depth-20)
+sklearn-style forest."""
+
+import numpy as np
+import pytest
+
+from flink_jpmml_amd.bench.synth import gbdt_pmml, random_forest_pmml, stream_matrix
+from flink_jpmml_amd.runtime.compiled import CompiledPmml
+
+pytestmark = pytest.mark.gpu
+
+
+def _score(c, plan, X):
+    import torch
+
+    Xd = torch.from_numpy(X.astype(np.float32)).cuda()
+    s, v = plan.alloc_outputs(len(X))
+    plan.launch(Xd, s, v)
+    torch.cuda.synchronize()
+    return s.cpu().numpy(), v.cpu().numpy().astype(bool)
+
+
+@pytest.mark.parametrize("layout,head", [("hybrid", 8), ("hybrid", 6), ("hybrid", 10), ("pointer", 0)])
+@pytest.mark.parametrize("missing", ["defaultChild", "nullPrediction"])
+def test_deep_gbdt_on_gpu(gpu, layout, head, missing):
+    txt = gbdt_pmml(n_trees=40, depth=14, n_features=24, seed=7, p_split=0.8, missing_strategy=missing)
+    c = CompiledPmml.from_string(txt)
+    plan = c.plan(gpu, layout=layout, head_depth=head)
+    assert plan.layout == layout
+    X = stream_matrix(100_000, 24, seed=3, missing_rate=0.03)
+    s, v = _score(c, plan, X)
+    ref, vref = c.score_matrix_oracle(X)
+    assert (v == vref).all()
+    np.testing.assert_allclose(s[v], ref[v], rtol=0, atol=5e-5)
+
+
+@pytest.mark.parametrize("depth", [14, 20])
+def test_deep_random_forest_votes_on_gpu(gpu, depth):
+    """sklearn RandomForest with max_depth=None: majority vote over deep unbalanced trees; the
+    depth-20 document goes through the streaming parser (flat arrays) as well."""
+    txt = random_forest_pmml(n_trees=6 if depth == 20 else 30, depth=depth, n_features=16, n_classes=3, seed=5,
+                             p_split=0.8)
+    c = CompiledPmml.from_string(txt.encode())
+    plan = c.plan(gpu)
+    assert plan.layout == "hybrid" and plan.depth == depth
+    X = stream_matrix(50_000, 16, seed=8, missing_rate=0.02)
+    s, v = _score(c, plan, X)
+    ref, vref = c.score_matrix_oracle(X)
+    assert (v == vref).all()
+    np.testing.assert_array_equal(s[v], ref[v])
+
+
+def test_wide_feature_deep_forest_global_features(gpu):
+    """n_features > 64: the hybrid walk reads features from global memory (indices in the metas)."""
+    txt = gbdt_pmml(n_trees=20, depth=12, n_features=90, seed=4)
+    c = CompiledPmml.from_string(txt)
+    X = stream_matrix(30_000, 90, seed=2, missing_rate=0.02)
+    ref, vref = c.score_matrix_oracle(X)
+    for layout in ("hybrid", "pointer"):
+        plan = c.plan(gpu, layout=layout)
+        s, v = _score(c, plan, X)
+        assert (v == vref).all()
+        np.testing.assert_allclose(s[v], ref[v], rtol=0, atol=5e-5)

@@ -1,0 +1,111 @@
+"""HYBRID tree layout (deep forests: PERFECT head in LDS + POINTER tail from L2,
+``ops/csrc/tree_hybrid.hip``) and the vectorised POINTER packer: a numpy emulation of the kernel
+walk over the packed tensors reproduces the float64 oracle (CPU, dry-run plans)."""
+
+import numpy as np
+import pytest
+import torch
+
+from flink_jpmml_amd.bench.synth import gbdt_pmml, random_forest_pmml, stream_matrix
+from flink_jpmml_amd.runtime.compiled import CompiledPmml
+from flink_jpmml_amd.runtime.plans import TB, TreePlan, lowering_dry_run
+
+
+def _plan(txt, **kw):
+    c = CompiledPmml.from_string(txt)
+    with lowering_dry_run():
+        return c, TreePlan(c, torch.device("cpu"), **kw)
+
+
+def _feature(X, meta, feat_lds):
+    f = (meta & 0xFFFF) // (TB * 4) if feat_lds else (meta & 0xFFFF)
+    return X[np.arange(len(X)), f]
+
+
+def emulate(plan, X):
+    """Per-row accumulator (P = 1) of the hybrid / pointer kernel, NaN where the row is poisoned."""
+    Xf = X.astype(np.float32)
+    n = len(X)
+    feat_lds = plan.n_features <= 64
+    tail = plan.blob.numpy().view(np.uint32).reshape(-1, 4)
+    leaves = plan.leaves.numpy().reshape(-1, plan.P)[:, 0]
+    H = plan.head_depth
+    NI = (1 << H) - 1
+    acc = np.zeros(n)
+    heads = plan.heads.numpy().view(np.uint32).reshape(plan.n_trees, -1) if H else None
+    for t in range(plan.n_trees):
+        pz = np.zeros(n, bool)
+        if H:
+            rec = heads[t]
+            j = np.zeros(n, np.int64)
+            for _ in range(H):
+                T = rec[2 * j].view(np.float32)
+                meta = rec[2 * j + 1]
+                x = _feature(Xf, meta, feat_lds)
+                isn = np.isnan(x)
+                pz |= isn & ((meta >> 30) & 1).astype(bool)
+                right = (x >= T) | (isn & (meta >> 31).astype(bool))
+                j = 2 * j + 1 + right
+            code = rec[2 * NI + (j - NI)].view(np.int32).astype(np.int64)
+        else:
+            code = np.full(n, plan.roots.numpy()[t], np.int64)
+        code = np.where(pz, -1, code)
+        while (code >= 0).any():
+            act = code >= 0
+            nd = tail[np.maximum(code, 0)]
+            x = _feature(Xf, nd[:, 1], feat_lds)
+            isn = np.isnan(x)
+            nulled = act & isn & ((nd[:, 1] >> 30) & 1).astype(bool)
+            right = (x >= nd[:, 0].view(np.float32)) | (isn & (nd[:, 1] >> 31).astype(bool))
+            nc = np.where(right, nd[:, 3].view(np.int32), nd[:, 2].view(np.int32)).astype(np.int64)
+            pz |= nulled
+            code = np.where(act, np.where(nulled, -1, nc), code)
+        acc += np.where(pz, np.nan, leaves[np.where(pz, 0, ~code)])
+    return acc
+
+
+@pytest.mark.parametrize("layout,head", [("hybrid", 8), ("hybrid", 4), ("hybrid", 10), ("pointer", 0)])
+@pytest.mark.parametrize("missing", ["defaultChild", "nullPrediction"])
+def test_deep_regression_forest_layouts_match_oracle(layout, head, missing):
+    txt = gbdt_pmml(n_trees=12, depth=13, n_features=20, seed=3, p_split=0.8)
+    if missing == "nullPrediction":
+        txt = txt.replace('missingValueStrategy="defaultChild"', 'missingValueStrategy="nullPrediction"')
+    c, plan = _plan(txt, layout=layout, head_depth=head)
+    assert plan.layout == layout and plan.head_depth == head
+    X = stream_matrix(4000, 20, seed=5, missing_rate=0.03)
+    ref, vref = c.score_matrix_oracle(X)
+    out = emulate(plan, X)
+    a, b = plan.epi_args.get("a", 1.0), plan.epi_args.get("b", 0.0)
+    got = a * out + b
+    assert (np.isfinite(got) == vref).all()
+    np.testing.assert_allclose(got[vref], ref[vref], rtol=0, atol=2e-4)
+
+
+def test_auto_layout_picks_hybrid_for_deep_forests():
+    c, plan = _plan(random_forest_pmml(n_trees=6, depth=14, n_features=16, n_classes=3, seed=2))
+    assert plan.layout == "hybrid" and plan.head_depth == 8 and plan.chunk_trees >= 1
+    assert plan.general == 1  # class votes accumulate in LDS slots
+
+
+def test_shallow_trees_and_stumps_in_the_head():
+    """Trees shallower than the head (and a single-leaf stump) route through padding nodes."""
+    txt = gbdt_pmml(n_trees=9, depth=5, n_features=6, seed=11, p_split=0.6)
+    c, plan = _plan(txt, layout="hybrid", head_depth=8)
+    X = stream_matrix(3000, 6, seed=1, missing_rate=0.05)
+    ref, vref = c.score_matrix_oracle(X)
+    got = plan.epi_args.get("a", 1.0) * emulate(plan, X) + plan.epi_args.get("b", 0.0)
+    assert (np.isfinite(got) == vref).all()
+    np.testing.assert_allclose(got[vref], ref[vref], rtol=0, atol=2e-5)
+
+
+def test_wide_feature_pointer_offsets():
+    """n_features > 64: features stay in global memory; metas hold indices (the old packer wrote
+    LDS byte offsets for features < 64 there)."""
+    txt = gbdt_pmml(n_trees=5, depth=12, n_features=90, seed=4)
+    c, plan = _plan(txt, layout="pointer")
+    meta = plan.blob.numpy().view(np.uint32).reshape(-1, 4)[:, 1] & 0xFFFF
+    assert meta.max() < 90
+    X = stream_matrix(1500, 90, seed=2, missing_rate=0.02)
+    ref, vref = c.score_matrix_oracle(X)
+    got = plan.epi_args.get("a", 1.0) * emulate(plan, X) + plan.epi_args.get("b", 0.0)
+    np.testing.assert_allclose(got[vref], ref[vref], rtol=0, atol=2e-4)
