@@ -6,7 +6,10 @@
 // (pinned) host buffer the H2D stage ships:
 //  * pass 1 splits the buffer into per-thread line ranges (memchr for '\n'), pass 2 parses every
 //    range into its row slice in place — no intermediate objects, no per-record allocation;
-//  * numeric fields: std::from_chars (locale-free, exact round-to-nearest fp32); empty fields and
+//  * numeric fields: a Clinger fast path for plain decimals (<= 19 significant digits, exponent
+//    within +-22: the decimal is exact in double, so one double operation rounds it correctly; the
+//    double -> fp32 rounding is exact unless that double sits on an fp32 midpoint, which falls
+//    back), otherwise std::from_chars (locale-free, exact round-to-nearest fp32); empty fields and
 //    the configured missing tokens become NaN (PMML missing); unparsable numerics become NaN and are
 //    counted;
 //  * categorical (string) fields: per-column dictionaries map the token to the PMML vocabulary code
@@ -60,6 +63,66 @@ inline bool is_missing(const Spec& sp, std::string_view tok) {
   return false;
 }
 
+constexpr double kPow10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
+                                1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+
+// Clinger fast path: [+-]digits[.digits][(e|E)[+-]digits]. Returns false when the token is not of
+// that form or is outside the exact range (the caller then uses std::from_chars).
+inline bool fast_decimal(const char* s, const char* e, float* out) {
+  bool neg = false;
+  if (s < e && (*s == '-' || *s == '+')) neg = *s++ == '-';
+  uint64_t w = 0;
+  int digits = 0, exp10 = 0;
+  bool any = false;
+  while (s < e && static_cast<unsigned>(*s - '0') < 10u) {
+    if (w != 0 || *s != '0') ++digits;
+    w = w * 10u + static_cast<unsigned>(*s - '0');
+    ++s;
+    any = true;
+  }
+  if (s < e && *s == '.') {
+    ++s;
+    while (s < e && static_cast<unsigned>(*s - '0') < 10u) {
+      if (w != 0 || *s != '0') ++digits;
+      w = w * 10u + static_cast<unsigned>(*s - '0');
+      --exp10;
+      ++s;
+      any = true;
+    }
+  }
+  if (!any || digits > 19) return false;
+  if (s < e && (*s == 'e' || *s == 'E')) {
+    ++s;
+    bool eneg = false;
+    if (s < e && (*s == '-' || *s == '+')) eneg = *s++ == '-';
+    int ev = 0, ed = 0;
+    while (s < e && static_cast<unsigned>(*s - '0') < 10u && ed < 6) {
+      ev = ev * 10 + (*s - '0');
+      ++s;
+      ++ed;
+    }
+    if (ed == 0) return false;
+    exp10 += eneg ? -ev : ev;
+  }
+  if (s != e) return false;
+  if (w > (uint64_t{1} << 53) || exp10 < -22 || exp10 > 22) return false;
+  double d = static_cast<double>(w);
+  d = exp10 < 0 ? d / kPow10[-exp10] : d * kPow10[exp10];
+  // double -> float is exact unless d lies on a float rounding midpoint (then the decimal may be
+  // on either side of it: let from_chars decide)
+  uint64_t bits;
+  std::memcpy(&bits, &d, 8);
+  const int be = static_cast<int>((bits >> 52) & 0x7FF);
+  if (be != 0 && be >= 1023 - 126) {  // normal float range: 29 dropped mantissa bits
+    if ((bits & ((uint64_t{1} << 29) - 1)) == (uint64_t{1} << 28)) return false;
+  } else if (d != 0.0) {
+    return false;  // subnormal / underflow region: from_chars
+  }
+  const float f = static_cast<float>(d);
+  *out = neg ? -f : f;
+  return true;
+}
+
 // Parse lines [b, e) into rows out[0..]; returns rows written; bad numeric tokens counted.
 size_t parse_range(const Spec& sp, const char* b, const char* e, float* out, int n_out, size_t max_rows,
                    size_t* bad) {
@@ -82,16 +145,21 @@ size_t parse_range(const Spec& sp, const char* b, const char* e, float* out, int
             if (sp.kind[oc] == 0) {
               float v;
               const char* s = tok.data();
-              if (*s == '+') ++s;
-              auto res = std::from_chars(s, tok.data() + tok.size(), v);
-              if (res.ec == std::errc() && res.ptr == tok.data() + tok.size()) {
+              const char* te2 = tok.data() + tok.size();
+              if (fast_decimal(s, te2, &v)) {
                 row[oc] = v;
-              } else if (tok == "inf" || tok == "Infinity" || tok == "+inf") {
-                row[oc] = INFINITY;
-              } else if (tok == "-inf" || tok == "-Infinity") {
-                row[oc] = -INFINITY;
               } else {
-                ++*bad;
+                if (*s == '+') ++s;
+                auto res = std::from_chars(s, te2, v);
+                if (res.ec == std::errc() && res.ptr == te2) {
+                  row[oc] = v;
+                } else if (tok == "inf" || tok == "Infinity" || tok == "+inf") {
+                  row[oc] = INFINITY;
+                } else if (tok == "-inf" || tok == "-Infinity") {
+                  row[oc] = -INFINITY;
+                } else {
+                  ++*bad;
+                }
               }
             } else {
               const auto& m = sp.vocab->cols[oc];

@@ -11,14 +11,18 @@
 //    in heap order) plus 2^H exit codes (tail node index, or ~leaf). A tree shallower than H below
 //    some node is padded with "always left" nodes (T = NaN: x >= NaN is false, no default-right bit)
 //    so the walk still takes exactly H branch-free steps and lands on that leaf's exit;
-//  * tail: pointer nodes {T, meta, left, right} of everything below depth H, walked like the pointer
-//    kernel (8 trees in lock-step per lane);
+//  * tail: COMPACT depth-first subtrees of everything below depth H — uint2 {x, meta} nodes, the
+//    left child right after its parent, the right child at a relative offset in the meta, leaves
+//    holding their value (P = 1) or payload row: half a pointer node's bytes per gathered level and
+//    no separate leaf gather; 8 trees walked in lock-step per lane;
 //  * chunks of trees' head records are copied cooperatively into LDS; rows stay stationary (one
 //    lane = one row, features transposed [F][256] in LDS — conflict-free reads).
 //
-// Splits are canonicalised on the host to "go right iff x >= T" (exact for fp32 inputs); meta =
+// Splits are canonicalised on the host to "go right iff x >= T" (exact for fp32 inputs). Head meta =
 // feature byte offset in the LDS tile (index when features stay global) | bit 30 null-on-missing |
-// bit 31 missing goes right. Leaves, epilogue, slots and split mode are the pointer kernel's.
+// bit 31 missing goes right; tail meta = feature index (bits 0-7) | right offset (8-28) | bit 29
+// leaf | bits 30/31 as in the head (runtime/hybrid.py packs both). Epilogue, slots and split mode
+// are the pointer kernel's.
 #include "tree_common.h"
 
 namespace pmml_tree {
@@ -74,7 +78,7 @@ __global__ __launch_bounds__(TB, 2) void tree_hybrid_kernel(HybridArgs ha) {
   if (GENERAL) {
     for (int c = 0; c < a.C; ++c) accl[c * TB + tid] = 0.f;
   }
-  const uint4* tail = reinterpret_cast<const uint4*>(a.blob);
+  const uint2* tail = reinterpret_cast<const uint2*>(a.blob);
   const int tb = blockIdx.y * a.trees_per_split;
   const int te = min(a.n_trees, tb + a.trees_per_split);
   const int rw = ha.head_words;
@@ -118,32 +122,44 @@ __global__ __launch_bounds__(TB, 2) void tree_hybrid_kernel(HybridArgs ha) {
           j[i] = 2u * j[i] + 1u + right;
         }
       }
+      // tail: COMPACT depth-first subtrees from L2 — {x, meta} uint2 per node, left child adjacent,
+      // right child at +rel, leaves carry their value (P = 1) or payload row (bit 29)
       int code[PILP];
+      bool done[PILP];
+      uint32_t val[PILP];
 #pragma unroll
       for (int i = 0; i < PILP; ++i) {
         code[i] = reinterpret_cast<const int*>(rec[i] + 2 * NI)[j[i] - NI];
-        if (pz[i]) code[i] = -1;  // null prediction: no tail walk (flagged below)
+        done[i] = pz[i] || i >= m;
+        val[i] = 0u;
       }
-      // tail: pointer walk from L2 for the trees whose exit is an internal node
       bool live = false;
 #pragma unroll
-      for (int i = 0; i < PILP; ++i) live = live || code[i] >= 0;
+      for (int i = 0; i < PILP; ++i) live = live || !done[i];
       while (live) {
-        uint4 nd[PILP];
+        uint2 nd[PILP];
 #pragma unroll
-        for (int i = 0; i < PILP; ++i) nd[i] = tail[max(code[i], 0)];
+        for (int i = 0; i < PILP; ++i) nd[i] = tail[code[i]];
         live = false;
 #pragma unroll
         for (int i = 0; i < PILP; ++i) {
-          const bool act = code[i] >= 0;
-          const float x = hy_feature<FEAT_LDS>(a, feat_lane, xrow, nd[i].y);
+          const bool act = !done[i];
+          const bool leaf = (nd[i].y >> 29) & 1u;
+          float x;
+          if (FEAT_LDS) {
+            x = *reinterpret_cast<const float*>(feat_lane + ((nd[i].y & 0xFFu) << 10));  // f * TB * 4
+          } else {
+            x = hy_feature<false>(a, feat_lane, xrow, nd[i].y & 0xFFu);
+          }
           const bool isn = x != x;
-          const bool nulled = act && isn && ((nd[i].y >> 30) & 1u);
+          const bool nulled = act && !leaf && isn && ((nd[i].y >> 30) & 1u);
           const bool right = (x >= __uint_as_float(nd[i].x)) || (isn && (nd[i].y >> 31));
-          const int nc = right ? (int)nd[i].w : (int)nd[i].z;
+          const int next = right ? code[i] + (int)((nd[i].y >> 8) & 0x1FFFFFu) : code[i] + 1;
           pz[i] = pz[i] || nulled;
-          code[i] = act ? (nulled ? -1 : nc) : code[i];
-          live = live || code[i] >= 0;
+          val[i] = (act && leaf) ? nd[i].x : val[i];
+          code[i] = (act && !leaf && !nulled) ? next : code[i];
+          done[i] = done[i] || leaf || nulled;
+          live = live || !done[i];
         }
       }
 #pragma unroll
@@ -154,12 +170,13 @@ __global__ __launch_bounds__(TB, 2) void tree_hybrid_kernel(HybridArgs ha) {
           else acc += __builtin_nanf("");
           continue;
         }
-        const int leaf = ~code[i];
         if (GENERAL) {
           const int slot = a.tree_slot[c0 + k + i];
-          for (int p = 0; p < a.P; ++p) accl[(slot + p) * TB + tid] += a.leaves[(size_t)leaf * a.P + p];
+          for (int p = 0; p < a.P; ++p) accl[(slot + p) * TB + tid] += a.leaves[(size_t)val[i] * a.P + p];
+        } else if (a.P > 1) {
+          acc += a.leaves[(size_t)val[i] * a.P];
         } else {
-          acc += a.leaves[leaf];
+          acc += __uint_as_float(val[i]);
         }
       }
     }

@@ -122,4 +122,125 @@ def pack_trees(trees, weights: List[float], P: int, H: int, feat_lds: bool
     return heads, nodes, lv, roots, has_dr
 
 
-__all__ = ["head_words", "pack_trees"]
+def _levels_and_heap(lc, rc, internal, H):
+    n = lc.shape[0]
+    lvl = np.full(n, -1, dtype=np.int64)
+    heap = np.full(n, -1, dtype=np.int64)
+    lvl[0], heap[0] = 0, 0
+    frontier = np.array([0], dtype=np.int64)
+    by_level = [frontier]
+    L = 0
+    while frontier.size:
+        fi = frontier[internal[frontier]]
+        if fi.size == 0:
+            break
+        a, b = lc[fi], rc[fi]
+        lvl[a] = lvl[b] = L + 1
+        if L + 1 <= H:
+            heap[a] = 2 * heap[fi] + 1
+            heap[b] = 2 * heap[fi] + 2
+        frontier = np.concatenate([a, b])
+        by_level.append(frontier)
+        L += 1
+    return lvl, heap, by_level
+
+
+COMPACT_REL_BITS = 21  # right-child offset field of a compact tail node
+
+
+def pack_hybrid_compact(trees, weights: List[float], P: int, H: int, n_features: int):
+    """HYBRID layout with a COMPACT tail: ``uint2 {x, meta}`` nodes in depth-first preorder per
+    subtree, the left child right after its parent and the right child at ``+ rel``:
+
+    * internal: ``x`` = threshold bits; meta = feature index (bits 0-7) | right-child offset
+      (bits 8-28) | bit 30 null-on-missing | bit 31 missing goes right;
+    * leaf (bit 29): ``x`` = the weighted leaf value (P = 1) or the leaf's payload row (P > 1).
+
+    Half the bytes of a POINTER node per visited level, and no separate leaf gather for sums.
+    Every head exit points at a tail node (a leaf above depth H is a one-node tail subtree).
+    Returns ``(heads, tail [n, 2] u32, payload [n_leaves, P] f32 or None, has_dr)``; raises
+    ``ValueError`` when a subtree outgrows the offset field or the features the index field."""
+    from .plans import _canonical_vec
+
+    if n_features > 256:
+        raise ValueError("compact tail nodes index at most 256 features")
+    NI, NL = (1 << H) - 1, 1 << H
+    rw = head_words(H)
+    heads = np.zeros((len(trees), rw), dtype=np.uint32)
+    tails: List[np.ndarray] = []
+    payload: List[np.ndarray] = []
+    n_tail = n_leaf = 0
+    has_dr = False
+    for ti, (t, w) in enumerate(zip(trees, weights)):
+        feat = np.asarray(t.feature, dtype=np.int64)
+        n = feat.shape[0]
+        internal = feat >= 0
+        T, swap = _canonical_vec(np.asarray(t.op), np.asarray(t.threshold, dtype=np.float64))
+        left, right = np.asarray(t.left, dtype=np.int64), np.asarray(t.right, dtype=np.int64)
+        dflt_left = np.asarray(t.default_left, dtype=bool)
+        lc = np.where(swap, right, left)
+        rc = np.where(swap, left, right)
+        dr = np.where(swap, dflt_left, ~dflt_left) & internal
+        has_dr = has_dr or bool(dr.any())
+        lvl, heap, by_level = _levels_and_heap(lc, rc, internal, H)
+        # subtree sizes bottom-up, then depth-first positions top-down (left child adjacent)
+        size = np.ones(n, dtype=np.int64)
+        for nodes in reversed(by_level):
+            k = nodes[internal[nodes]]
+            size[k] = 1 + size[lc[k]] + size[rc[k]]
+        is_leaf = ~internal
+        tail_node = lvl >= H
+        roots = np.nonzero((lvl == H) | (is_leaf & (lvl < H)))[0]
+        pos = np.full(n, -1, dtype=np.int64)
+        pos[roots] = np.concatenate([[0], np.cumsum(size[roots])[:-1]]) if roots.size else roots
+        for nodes in by_level:
+            k = nodes[internal[nodes] & (pos[nodes] >= 0)]
+            pos[lc[k]] = pos[k] + 1
+            pos[rc[k]] = pos[k] + 1 + size[lc[k]]
+        members = np.nonzero((pos >= 0) & (tail_node | is_leaf))[0]
+        m = int(size[roots].sum()) if roots.size else 0
+        if members.size != m:
+            raise AssertionError("hybrid tail packing lost nodes")
+        nd = np.zeros((m, 2), dtype=np.uint32)
+        ik = members[internal[members]]
+        rel = pos[rc[ik]] - pos[ik]
+        if rel.size and rel.max() >= (1 << COMPACT_REL_BITS):
+            raise ValueError("subtree too large for the compact tail's right-child offset")
+        nd[pos[ik], 0] = T[ik].view(np.uint32)
+        nd[pos[ik], 1] = (feat[ik].astype(np.uint64) | (rel.astype(np.uint64) << 8)
+                          | (dr[ik].astype(np.uint64) << 31)
+                          | (np.uint64(bool(t.null_missing)) << np.uint64(30))).astype(np.uint32)
+        lk = members[is_leaf[members]]
+        if P > 1:
+            probs = np.asarray(t.leaf_probs, dtype=np.float64)[lk, :P] * w
+            payload.append(probs)
+            nd[pos[lk], 0] = (n_leaf + np.arange(lk.size)).astype(np.uint32)
+            n_leaf += lk.size
+        else:
+            nd[pos[lk], 0] = (np.asarray(t.leaf_value, dtype=np.float64)[lk] * w).astype(np.float32).view(np.uint32)
+        nd[pos[lk], 1] = np.uint32(1 << 29)
+        tails.append(nd)
+        code = n_tail + pos  # global tail index of every tail-subtree node
+        # head
+        rec = heads[ti]
+        hT = np.full(NI, NAN_BITS, dtype=np.uint32)
+        hM = np.zeros(NI, dtype=np.uint32)
+        hk = np.nonzero(internal & (lvl < H))[0]
+        hT[heap[hk]] = T[hk].view(np.uint32)
+        hM[heap[hk]] = (feat[hk] * TB * 4 if n_features <= 64 else feat[hk]).astype(np.uint32) \
+            | (dr[hk].astype(np.uint32) << np.uint32(31)) | (np.uint32(bool(t.null_missing)) << np.uint32(30))
+        exits = np.full(NL, n_tail, dtype=np.int64)  # unreachable exits: any valid tail node
+        at = np.nonzero(lvl == H)[0]
+        exits[heap[at] - NI] = code[at]
+        up = np.nonzero(is_leaf & (lvl < H))[0]
+        exits[(heap[up] + 1) * (np.int64(1) << (H - lvl[up])) - 1 - NI] = code[up]
+        rec[0: 2 * NI: 2] = hT
+        rec[1: 2 * NI: 2] = hM
+        rec[2 * NI: 2 * NI + NL] = exits.astype(np.int32).view(np.uint32)
+        n_tail += m
+    tail = np.concatenate(tails) if tails else np.zeros((1, 2), np.uint32)
+    pay = np.concatenate(payload).astype(np.float32) if payload else None
+    return heads, tail, pay, has_dr
+
+
+__all__ = ["head_words", "pack_hybrid_compact", "pack_trees"]

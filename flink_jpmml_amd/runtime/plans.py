@@ -1297,26 +1297,34 @@ class TreePlan(DevicePlan):
         else:
             if precision == "fp8":
                 raise NotLowerable("fp8 leaves need the PERFECT layout")
-            from .hybrid import head_words, pack_trees
+            from .hybrid import head_words, pack_hybrid_compact, pack_trees
 
             feat_lds = F <= 64
             H = 0
+            heads = None
             if self.layout == "hybrid":
-                # PERFECT head of the top H levels in LDS + POINTER tail from L2 (tree_hybrid.hip)
-                H = head_depth or (8 if depth > 8 else max(4, depth // 2 * 2))
+                # PERFECT head of the top H levels in LDS + COMPACT depth-first tail from L2
+                # (tree_hybrid.hip); H = 4 measured best at depth 14 (profiles/r3c: larger heads
+                # pay more for the per-workgroup head copy and LDS bank conflicts than they save)
+                H = head_depth or 4
                 if H not in (4, 6, 8, 10):
                     raise ValueError("head_depth must be 4, 6, 8 or 10")
                 fixed = (F * TB * 4 if feat_lds else 0) + TB * 4 + (self.C * TB * 4 if self.general else 0)
-                per_tree = head_words(H) * 4
-                fit = (lds_budget - fixed) // per_tree
-                if fit < 1:
-                    H, fit = 4, (lds_budget - fixed) // (head_words(4) * 4)
+                fit = (lds_budget - fixed) // (head_words(H) * 4)
                 if fit < 1:
                     raise NotLowerable("no LDS left for a hybrid head chunk")
-                self.chunk_trees = int(min(fit, self.n_trees, max_chunk_trees or 64))
+                self.chunk_trees = int(min(fit, self.n_trees, max_chunk_trees or 512))
+                try:
+                    heads, nodes, leaves, has_dr = pack_hybrid_compact(spec.trees, spec.weights, spec.P, H, F)
+                    roots = np.zeros(self.n_trees, dtype=np.int32)
+                    if leaves is None:
+                        leaves = np.zeros((1, 1), np.float32)
+                except ValueError:
+                    self.layout, H, heads, self.chunk_trees = "pointer", 0, None, 0
             else:
                 self.chunk_trees = 0
-            heads, nodes, leaves, roots, has_dr = pack_trees(spec.trees, spec.weights, spec.P, H, feat_lds)
+            if heads is None:
+                _, nodes, leaves, roots, has_dr = pack_trees(spec.trees, spec.weights, spec.P, 0, feat_lds)
             self.blob_nan, self.chunk_trees_nan = None, 0
             self.head_depth = H
             self.rec_words = head_words(H) if H else 0

@@ -27,9 +27,9 @@ def emulate(plan, X):
     Xf = X.astype(np.float32)
     n = len(X)
     feat_lds = plan.n_features <= 64
-    tail = plan.blob.numpy().view(np.uint32).reshape(-1, 4)
-    leaves = plan.leaves.numpy().reshape(-1, plan.P)[:, 0]
     H = plan.head_depth
+    tail = plan.blob.numpy().view(np.uint32).reshape(-1, 2 if H else 4)
+    leaves = plan.leaves.numpy().reshape(-1, plan.P)[:, 0]
     NI = (1 << H) - 1
     acc = np.zeros(n)
     heads = plan.heads.numpy().view(np.uint32).reshape(plan.n_trees, -1) if H else None
@@ -49,6 +49,26 @@ def emulate(plan, X):
             code = rec[2 * NI + (j - NI)].view(np.int32).astype(np.int64)
         else:
             code = np.full(n, plan.roots.numpy()[t], np.int64)
+        if H:  # COMPACT depth-first tail: left child adjacent, right at +rel, leaves carry values
+            done = pz.copy()
+            val = np.zeros(n, np.uint32)
+            while (~done).any():
+                nd = tail[code]
+                act = ~done
+                leaf = ((nd[:, 1] >> 29) & 1).astype(bool)
+                f = nd[:, 1] & 0xFF
+                x = Xf[np.arange(n), f]
+                isn = np.isnan(x)
+                nulled = act & ~leaf & isn & ((nd[:, 1] >> 30) & 1).astype(bool)
+                right = (x >= nd[:, 0].view(np.float32)) | (isn & (nd[:, 1] >> 31).astype(bool))
+                nxt = np.where(right, code + ((nd[:, 1] >> 8) & 0x1FFFFF), code + 1)
+                pz |= nulled
+                val = np.where(act & leaf, nd[:, 0], val)
+                code = np.where(act & ~leaf & ~nulled, nxt, code)
+                done |= leaf | nulled
+            lv = leaves[val] if plan.P > 1 else val.view(np.float32)
+            acc += np.where(pz, np.nan, lv)
+            continue
         code = np.where(pz, -1, code)
         while (code >= 0).any():
             act = code >= 0
@@ -83,7 +103,7 @@ def test_deep_regression_forest_layouts_match_oracle(layout, head, missing):
 
 def test_auto_layout_picks_hybrid_for_deep_forests():
     c, plan = _plan(random_forest_pmml(n_trees=6, depth=14, n_features=16, n_classes=3, seed=2))
-    assert plan.layout == "hybrid" and plan.head_depth == 8 and plan.chunk_trees >= 1
+    assert plan.layout == "hybrid" and plan.head_depth == 4 and plan.chunk_trees >= 1
     assert plan.general == 1  # class votes accumulate in LDS slots
 
 

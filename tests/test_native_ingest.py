@@ -137,3 +137,52 @@ def test_numeric_tokens_are_correctly_rounded(kmeans):
     m = parse_records(kmeans, text, kmeans.active_fields).reshape(-1)
     ref = np.array([_f32_correctly_rounded(t) for t in toks], np.float32)
     assert np.array_equal(m.view(np.uint32), ref.view(np.uint32))
+
+
+def _round_to_f32(s: str) -> np.float32:
+    """Correctly rounded decimal -> fp32 (exact rational arithmetic, ties to even)."""
+    from fractions import Fraction
+
+    x = Fraction(s)
+    if x == 0:
+        return np.float32(-0.0) if s.startswith("-") else np.float32(0.0)
+    f = np.float32(float(x))  # within one ulp (double rounding)
+    best, best_err = None, None
+    for c in (np.nextafter(f, np.float32(-np.inf)), f, np.nextafter(f, np.float32(np.inf))):
+        if not np.isfinite(c):
+            continue
+        err = abs(Fraction(float(c)) - x)
+        if best is None or err < best_err or (err == best_err and int(c.view(np.uint32)) % 2 == 0):
+            best, best_err = c, err
+    return best
+
+
+def test_fast_decimal_path_is_correctly_rounded(kmeans):
+    """The Clinger fast path of the native parser (plain decimals, <= 19 digits, |exp| <= 22) and
+    its from_chars fallback round every token exactly like a correctly rounded decimal->fp32
+    conversion — including decimals whose double image sits on an fp32 midpoint."""
+    rng = np.random.default_rng(123)
+    toks = []
+    for _ in range(4000):
+        nd = int(rng.integers(1, 20))
+        digits = "".join(str(int(d)) for d in rng.integers(0, 10, nd))
+        dot = int(rng.integers(0, nd + 1))
+        t = digits[:dot] + "." + digits[dot:] if dot < nd else digits
+        if rng.random() < 0.3:
+            t += f"e{int(rng.integers(-25, 16))}"
+        if rng.random() < 0.5:
+            t = "-" + t
+        toks.append(t.lstrip(".") if t.startswith(".") and rng.random() < 0.5 else t)
+    # exact fp32 midpoints written out (their double images are midpoints too)
+    for v in rng.standard_normal(300).astype(np.float32):
+        up = np.nextafter(v, np.float32(np.inf))
+        mid = (np.float64(v) + np.float64(up)) / 2
+        toks.append(repr(float(mid)))
+    toks += ["0", "-0.0", "1e-40", "3.4028235e38", "123456789012345678", "0.1", "7.0000005"]
+    width = len(kmeans.active_fields)
+    lines = [",".join([t] + ["0"] * (width - 1)) for t in toks]
+    X = parse_records(kmeans, ("\n".join(lines) + "\n").encode(), kmeans.active_fields)
+    got = X[:, 0]
+    want = np.array([_round_to_f32(t) for t in toks], dtype=np.float32)
+    bad = [(t, g, w) for t, g, w in zip(toks, got, want) if g.view(np.uint32) != w.view(np.uint32)]
+    assert not bad, bad[:10]
