@@ -59,6 +59,10 @@ def parse_args(argv=None):
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--api", choices=["dsl", "engine"], default="dsl")
+    p.add_argument("--source", choices=["synthetic", "binary", "text"], default="synthetic",
+                   help="synthetic: pinned in-memory shard (headline); binary: memory-mapped fp32 record file "
+                        "(zero-parse ingest); text: CSV through the native parser -- reported separately")
+    p.add_argument("--ingest-threads", type=int, default=8, help="binary copy / text parse threads per rank")
     p.add_argument("--model", choices=sorted(MODELS), default="gbdt")
     p.add_argument("--trees", type=int, default=None, help="default 1000 (gbdt/chain), 500 (rf)")
     p.add_argument("--depth", type=int, default=None, help="default 6 (gbdt/chain), 8 (rf)")
@@ -125,6 +129,47 @@ class _StepSource:
             self.on_step(i)
             for p in range(self.passes):
                 yield RecordBatch(self.X, offset=(i * self.passes + p) * rows)
+
+
+class _FileStepSource:
+    """``--source binary|text``: every step reads this rank's record file ``passes`` times through
+    the library's file source (binary: mmap + parallel copy into pinned buffers; text: the native
+    multi-threaded parser into pinned buffers); ``on_step(i)`` fires at step boundaries."""
+
+    def __init__(self, make_source, n_steps, passes, on_step):
+        self.make_source = make_source
+        self.n = n_steps
+        self.passes = passes
+        self.on_step = on_step
+
+    def open_subtask(self, rank, world):
+        pass
+
+    def iterate(self):
+        off = 0
+        for i in range(self.n):
+            self.on_step(i)
+            for _ in range(self.passes):
+                for b in self.make_source().iterate():
+                    b.offset = off
+                    off += len(b)
+                    yield b
+
+
+def _write_source_file(args, X, rank):
+    """This rank's record file for ``--source binary|text`` (page-cache resident after writing)."""
+    import tempfile
+
+    d = "/dev/shm" if os.path.isdir("/dev/shm") else tempfile.gettempdir()
+    if args.source == "binary":
+        from flink_jpmml_amd.stream.binary import write_binary
+
+        return write_binary(os.path.join(d, f"fja-bench-{os.getpid()}-{rank}.fjab"), X)
+    path = os.path.join(d, f"fja-bench-{os.getpid()}-{rank}.csv")
+    with open(path, "w") as fh:
+        fh.write(",".join(f"f{j}" for j in range(X.shape[1])) + "\n")
+        np.savetxt(fh, X, fmt="%.7g", delimiter=",")
+    return path
 
 
 class _WaitSink:
@@ -231,7 +276,23 @@ def main(argv=None) -> int:
         # mirrors over RCCL on its comm stream, overlapping the next batch
         sink = GatherSink(to="all", lockstep=True, keep=False) if gather or N == 1 else _WaitSink()
         op_cfg = cfg.replace(device_mirror=gather)
-        stream = env.add_source(_StepSource(X, args.warmup + args.steps, args.passes, on_step), mode="parallel")
+        if args.source == "synthetic":
+            src = _StepSource(X, args.warmup + args.steps, args.passes, on_step)
+        else:
+            from flink_jpmml_amd.stream.binary import BinaryBatchSource
+            from flink_jpmml_amd.stream.sources import TextBatchSource
+
+            src_path = _write_source_file(args, X.numpy(), ctx.rank)
+            job["source_file_bytes"] = os.path.getsize(src_path)
+            if args.source == "binary":
+                make = lambda: BinaryBatchSource(src_path, batch_rows=args.micro_batch,  # noqa: E731
+                                                 threads=args.ingest_threads)
+            else:
+                text_model = CompiledPmml.load(path)  # parsed once: field names + vocabularies
+                make = lambda: TextBatchSource(src_path, text_model, batch_rows=args.micro_batch,  # noqa: E731
+                                               threads=args.ingest_threads)
+            src = _FileStepSource(make, args.warmup + args.steps, args.passes, on_step)
+        stream = env.add_source(src, mode="parallel")
         scored = stream.quick_evaluate(ModelReader(path), config=op_cfg)
         scored.add_sink(sink)
         res = env.execute("bench")
@@ -244,6 +305,8 @@ def main(argv=None) -> int:
         assert res.records_in == seen
         op = scored.node.factory  # the operator instance this (single-subtask) rank ran
         pipe = getattr(getattr(op, "inner", op), "_pipeline", None)
+        if args.source != "synthetic":
+            os.unlink(src_path)
     else:
         scorer = StreamingScorer(plan, micro_batch=args.micro_batch, depth=args.pipeline_depth, max_rows=args.rows,
                                  h2d_streams=args.h2d_streams)
@@ -298,9 +361,12 @@ def main(argv=None) -> int:
     p99 = float(np.percentile(lats, 99))
 
     if ctx.rank == 0:
-        default = args.model == "gbdt"
+        default = args.model == "gbdt" and args.source == "synthetic"
+        metric = METRIC if default else f"records/sec (whole node) on {MODELS[args.model][1]} PMML; p50 latency"
+        if args.source != "synthetic":
+            metric += f" [source: {args.source} record file, end to end incl. ingest]"
         out = {
-            "metric": METRIC if default else f"records/sec (whole node) on {MODELS[args.model][1]} PMML; p50 latency",
+            "metric": metric,
             "value": records_per_s,
             "unit": "records/s",
             "n_gpus": N,
@@ -311,7 +377,8 @@ def main(argv=None) -> int:
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": {"fp32": "fp32", "bf16": "bf16", "fp8": "fp32 (fp8 e4m3 leaf values)"}[args.precision],
-            "data": "synthetic (random-init PMML model, N(0,1) float records)",
+            "data": "synthetic (random-init PMML model, N(0,1) float records)" + (
+                "" if args.source == "synthetic" else f", read from a {args.source} record file per rank"),
             "config": {
                 "model": (f"GBDT {args.trees} trees, depth {args.depth}, {args.features} float features "
                           f"(XGBoost-style PMML, regression, {args.precision} leaves)") if default else
@@ -322,6 +389,7 @@ def main(argv=None) -> int:
                 "seq_len": None,
                 "parallelism": f"dp{N}",
                 "api": args.api,
+                "source": args.source,
                 "micro_batch": args.micro_batch,
                 "pipeline_depth": args.pipeline_depth,
                 "h2d_streams": _h2d_streams(pipe, args),

@@ -20,9 +20,11 @@
 //
 // Splits are canonicalised on the host to "go right iff x >= T" (exact for fp32 inputs). Head meta =
 // feature byte offset in the LDS tile (index when features stay global) | bit 30 null-on-missing |
-// bit 31 missing goes right; tail meta = feature index (bits 0-7) | right offset (8-28) | bit 29
-// leaf | bits 30/31 as in the head (runtime/hybrid.py packs both). Epilogue, slots and split mode
-// are the pointer kernel's.
+// bit 31 missing goes right; head exits = tail subtree root, or ~leaf. Tail meta = feature index
+// (bits 0-7) | right offset (8-27) | bit 28 right child is a leaf | bit 29 left child is a leaf |
+// bits 30/31 as in the head (runtime/hybrid.py packs both). A walk stops at its leaf's parent and
+// the leaves of the 8 lock-step trees are read together afterwards: no serial extra round trip.
+// Epilogue, slots and split mode are the pointer kernel's.
 #include "tree_common.h"
 
 namespace pmml_tree {
@@ -123,15 +125,14 @@ __global__ __launch_bounds__(TB, 2) void tree_hybrid_kernel(HybridArgs ha) {
         }
       }
       // tail: COMPACT depth-first subtrees from L2 — {x, meta} uint2 per node, left child adjacent,
-      // right child at +rel, leaves carry their value (P = 1) or payload row (bit 29)
+      // right child at +rel; a walk stops at the parent of its leaf (child-is-leaf bits 28/29)
       int code[PILP];
       bool done[PILP];
-      uint32_t val[PILP];
 #pragma unroll
       for (int i = 0; i < PILP; ++i) {
-        code[i] = reinterpret_cast<const int*>(rec[i] + 2 * NI)[j[i] - NI];
-        done[i] = pz[i] || i >= m;
-        val[i] = 0u;
+        const int e = reinterpret_cast<const int*>(rec[i] + 2 * NI)[j[i] - NI];
+        done[i] = pz[i] || i >= m || e < 0;
+        code[i] = e < 0 ? ~e : e;
       }
       bool live = false;
 #pragma unroll
@@ -144,7 +145,6 @@ __global__ __launch_bounds__(TB, 2) void tree_hybrid_kernel(HybridArgs ha) {
 #pragma unroll
         for (int i = 0; i < PILP; ++i) {
           const bool act = !done[i];
-          const bool leaf = (nd[i].y >> 29) & 1u;
           float x;
           if (FEAT_LDS) {
             x = *reinterpret_cast<const float*>(feat_lane + ((nd[i].y & 0xFFu) << 10));  // f * TB * 4
@@ -152,17 +152,19 @@ __global__ __launch_bounds__(TB, 2) void tree_hybrid_kernel(HybridArgs ha) {
             x = hy_feature<false>(a, feat_lane, xrow, nd[i].y & 0xFFu);
           }
           const bool isn = x != x;
-          const bool nulled = act && !leaf && isn && ((nd[i].y >> 30) & 1u);
+          const bool nulled = act && isn && ((nd[i].y >> 30) & 1u);
           const bool right = (x >= __uint_as_float(nd[i].x)) || (isn && (nd[i].y >> 31));
-          const int next = right ? code[i] + (int)((nd[i].y >> 8) & 0x1FFFFFu) : code[i] + 1;
+          const int next = right ? code[i] + (int)((nd[i].y >> 8) & 0xFFFFFu) : code[i] + 1;
+          const bool child_leaf = ((nd[i].y >> (right ? 28 : 29)) & 1u) != 0u;
           pz[i] = pz[i] || nulled;
-          val[i] = (act && leaf) ? nd[i].x : val[i];
-          code[i] = (act && !leaf && !nulled) ? next : code[i];
-          done[i] = done[i] || leaf || nulled;
+          code[i] = (act && !nulled) ? next : code[i];
+          done[i] = done[i] || nulled || child_leaf;
           live = live || !done[i];
         }
       }
+      uint32_t val[PILP];
 #pragma unroll
+      for (int i = 0; i < PILP; ++i) val[i] = tail[code[i]].x;  // the leaves, read together
       for (int i = 0; i < PILP; ++i) {
         if (i >= m) break;
         if (pz[i]) {

@@ -145,7 +145,7 @@ def _levels_and_heap(lc, rc, internal, H):
     return lvl, heap, by_level
 
 
-COMPACT_REL_BITS = 21  # right-child offset field of a compact tail node
+COMPACT_REL_BITS = 20  # right-child offset field of a compact tail node
 
 
 def pack_hybrid_compact(trees, weights: List[float], P: int, H: int, n_features: int):
@@ -153,11 +153,14 @@ def pack_hybrid_compact(trees, weights: List[float], P: int, H: int, n_features:
     subtree, the left child right after its parent and the right child at ``+ rel``:
 
     * internal: ``x`` = threshold bits; meta = feature index (bits 0-7) | right-child offset
-      (bits 8-28) | bit 30 null-on-missing | bit 31 missing goes right;
-    * leaf (bit 29): ``x`` = the weighted leaf value (P = 1) or the leaf's payload row (P > 1).
+      (bits 8-27) | bit 28 right child is a leaf | bit 29 left child is a leaf | bit 30
+      null-on-missing | bit 31 missing goes right;
+    * leaf: ``x`` = the weighted leaf value (P = 1) or the leaf's payload row (P > 1).
 
-    Half the bytes of a POINTER node per visited level, and no separate leaf gather for sums.
-    Every head exit points at a tail node (a leaf above depth H is a one-node tail subtree).
+    Half the bytes of a POINTER node per visited level. The walk stops at the parent of a leaf
+    (the child-is-leaf bits): the leaf itself is read once after the lock-step loop, with the
+    other trees' leaves, never as an extra serial L2 round trip. Head exits hold the index of a
+    tail subtree root, or ``~index`` of a leaf (a leaf above depth H).
     Returns ``(heads, tail [n, 2] u32, payload [n_leaves, P] f32 or None, has_dr)``; raises
     ``ValueError`` when a subtree outgrows the offset field or the features the index field."""
     from .plans import _canonical_vec
@@ -208,6 +211,7 @@ def pack_hybrid_compact(trees, weights: List[float], P: int, H: int, n_features:
             raise ValueError("subtree too large for the compact tail's right-child offset")
         nd[pos[ik], 0] = T[ik].view(np.uint32)
         nd[pos[ik], 1] = (feat[ik].astype(np.uint64) | (rel.astype(np.uint64) << 8)
+                          | (is_leaf[rc[ik]].astype(np.uint64) << 28) | (is_leaf[lc[ik]].astype(np.uint64) << 29)
                           | (dr[ik].astype(np.uint64) << 31)
                           | (np.uint64(bool(t.null_missing)) << np.uint64(30))).astype(np.uint32)
         lk = members[is_leaf[members]]
@@ -218,9 +222,8 @@ def pack_hybrid_compact(trees, weights: List[float], P: int, H: int, n_features:
             n_leaf += lk.size
         else:
             nd[pos[lk], 0] = (np.asarray(t.leaf_value, dtype=np.float64)[lk] * w).astype(np.float32).view(np.uint32)
-        nd[pos[lk], 1] = np.uint32(1 << 29)
         tails.append(nd)
-        code = n_tail + pos  # global tail index of every tail-subtree node
+        code = np.where(is_leaf, ~(n_tail + pos), n_tail + pos)  # exits: ~leaf / subtree root
         # head
         rec = heads[ti]
         hT = np.full(NI, NAN_BITS, dtype=np.uint32)

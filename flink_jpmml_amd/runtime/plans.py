@@ -1313,7 +1313,9 @@ class TreePlan(DevicePlan):
                 fit = (lds_budget - fixed) // (head_words(H) * 4)
                 if fit < 1:
                     raise NotLowerable("no LDS left for a hybrid head chunk")
-                self.chunk_trees = int(min(fit, self.n_trees, max_chunk_trees or 512))
+                # small chunks: the head buffer must not cost occupancy (the tail walk hides L2 latency
+                # with waves; profiles/r3e: 234-tree chunks -> 2 workgroups per CU, 1.5x slower)
+                self.chunk_trees = int(min(fit, self.n_trees, max_chunk_trees or 32))
                 try:
                     heads, nodes, leaves, has_dr = pack_hybrid_compact(spec.trees, spec.weights, spec.P, H, F)
                     roots = np.zeros(self.n_trees, dtype=np.int32)

@@ -358,6 +358,22 @@ class StreamExecutionEnvironment:
         torchrun every rank parses only its own byte range (rank-local split, F3)."""
         return self._source(TextBatchSource(path, model, batch_rows, **kw), "text-batches", None, "parallel")
 
+    def read_binary_batches(self, path: str, batch_rows: int = 1 << 20, threads: int = 4, repeat: int = 1,
+                            model_id: Optional[str] = None) -> "DataStream":
+        """Binary fp32 record file (:mod:`~flink_jpmml_amd.stream.binary`) → pinned RecordBatches:
+        memory-mapped, copied into pinned buffers by ``threads`` workers, no parsing. Under torchrun
+        every rank maps only its own row range."""
+        from .binary import BinaryBatchSource
+
+        return self._source(BinaryBatchSource(path, batch_rows, threads, repeat=repeat, model_id=model_id),
+                            "binary-batches", None, "parallel")
+
+    def socket_binary_stream(self, host: str, port: int, model_id: Optional[str] = None) -> "DataStream":
+        """TCP stream of binary record frames (``binary.send_binary``) → pinned RecordBatches."""
+        from .binary import SocketBinarySource
+
+        return self._source(SocketBinarySource(host, port, model_id=model_id), "binary-socket", None, "parallel")
+
     def socket_text_stream(self, host: str, port: int, delimiter: str = "\n", max_retry: int = 0,
                            uid: Optional[str] = None) -> "DataStream":
         """``socketTextStream(host, port)`` (`E/CheckpointEvaluate.scala:80-82`): lines read live

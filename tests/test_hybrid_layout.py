@@ -49,23 +49,23 @@ def emulate(plan, X):
             code = rec[2 * NI + (j - NI)].view(np.int32).astype(np.int64)
         else:
             code = np.full(n, plan.roots.numpy()[t], np.int64)
-        if H:  # COMPACT depth-first tail: left child adjacent, right at +rel, leaves carry values
-            done = pz.copy()
-            val = np.zeros(n, np.uint32)
+        if H:  # COMPACT depth-first tail: left child adjacent, right at +rel, stop at the leaf's parent
+            done = pz | (code < 0)
+            code = np.where(code < 0, ~code, code)
             while (~done).any():
                 nd = tail[code]
                 act = ~done
-                leaf = ((nd[:, 1] >> 29) & 1).astype(bool)
                 f = nd[:, 1] & 0xFF
                 x = Xf[np.arange(n), f]
                 isn = np.isnan(x)
-                nulled = act & ~leaf & isn & ((nd[:, 1] >> 30) & 1).astype(bool)
+                nulled = act & isn & ((nd[:, 1] >> 30) & 1).astype(bool)
                 right = (x >= nd[:, 0].view(np.float32)) | (isn & (nd[:, 1] >> 31).astype(bool))
-                nxt = np.where(right, code + ((nd[:, 1] >> 8) & 0x1FFFFF), code + 1)
+                nxt = np.where(right, code + ((nd[:, 1] >> 8) & 0xFFFFF), code + 1)
+                child_leaf = np.where(right, (nd[:, 1] >> 28) & 1, (nd[:, 1] >> 29) & 1).astype(bool)
                 pz |= nulled
-                val = np.where(act & leaf, nd[:, 0], val)
-                code = np.where(act & ~leaf & ~nulled, nxt, code)
-                done |= leaf | nulled
+                code = np.where(act & ~nulled, nxt, code)
+                done |= nulled | child_leaf
+            val = tail[code, 0]
             lv = leaves[val] if plan.P > 1 else val.view(np.float32)
             acc += np.where(pz, np.nan, lv)
             continue
