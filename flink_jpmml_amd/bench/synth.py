@@ -448,15 +448,20 @@ def glm_pmml(model_type: str = "generalizedLinear", link: str = "log", n_feature
              classes: int = 3) -> str:
     """``GeneralRegressionModel`` (PPMatrix / ParamMatrix) with covariates ``f*`` (one squared),
     factor ``color`` and a covariate x factor interaction. ``multinomialLogistic`` gets
-    ``classes`` categories, the last one the reference."""
+    ``classes`` categories, the last one the reference; ``ordinalMultinomial`` gets ``classes``
+    ordered categories, one increasing cut point (``p0``) per category but the last, the other
+    parameters shared, and ``link`` as its ``cumulativeLink``."""
     rng = np.random.default_rng(seed)
     out = io.StringIO()
     _header(out, f"synthetic GLM {model_type} {link}")
-    multi = model_type == "multinomialLogistic"
+    ordinal = model_type == "ordinalMultinomial"
+    multi = model_type == "multinomialLogistic" or ordinal
     cats = [str(c) for c in range(classes)] if multi else None
     _mixed_dictionary(out, n_features, "y", cats)
     fn = "classification" if multi else "regression"
     attrs = f' targetReferenceCategory="{classes - 1}"' if multi else f' linkFunction="{link}"'
+    if ordinal:
+        attrs = f' cumulativeLink="{link}"'
     if link == "power" and not multi:
         attrs += ' linkParameter="0"'
     out.write(f' <GeneralRegressionModel functionName="{fn}" modelType="{model_type}"{attrs} '
@@ -476,7 +481,13 @@ def glm_pmml(model_type: str = "generalizedLinear", link: str = "log", n_feature
     out.write('   <PPCell value="blue" predictorName="color" parameterName="px"/>\n')
     out.write('   <PPCell value="1" predictorName="f0" parameterName="px"/>\n')
     out.write('  </PPMatrix>\n  <ParamMatrix>\n')
-    for c in (cats[:-1] if multi else [None]):
+    if ordinal:
+        cuts = np.sort(rng.normal(size=classes - 1)) * 1.5
+        for c, cut in zip(cats[:-1], cuts):
+            out.write(f'   <PCell parameterName="p0" targetCategory="{c}" beta="{cut:.6g}"/>\n')
+        for p in params[1:]:
+            out.write(f'   <PCell parameterName="{p}" beta="{rng.normal() * 0.5:.6g}"/>\n')
+    for c in ([] if ordinal else cats[:-1] if multi else [None]):
         tc = f' targetCategory="{c}"' if c is not None else ""
         for p in params:
             out.write(f'   <PCell parameterName="{p}"{tc} beta="{rng.normal() * 0.3:.6g}"/>\n')
@@ -597,9 +608,12 @@ def naive_bayes_pmml(n_features: int = 4, classes: int = 3, seed: int = 0, thres
 
 
 def knn_pmml(n_instances: int = 200, n_features: int = 4, k: int = 3, classification: bool = True, seed: int = 0,
-             method: Optional[str] = None, metric: str = "euclidean", classes: int = 3) -> str:
+             method: Optional[str] = None, metric: str = "euclidean", classes: int = 3,
+             measure: str = "distance", compare: Optional[str] = None, target: Optional[str] = None) -> str:
     """``NearestNeighborModel`` over ``n_instances`` inline training rows of ``f*`` (targets
-    ``0..classes-1`` or real values)."""
+    ``0..classes-1`` or real values). ``metric`` is the ComparisonMeasure element body (e.g.
+    ``'minkowski p-parameter="3"'``), ``measure`` its kind, ``compare`` a compareFunction, ``target``
+    the attributes of a ``<Target field="y" .../>`` (regression rescale / clip / cast)."""
     rng = np.random.default_rng(seed)
     out = io.StringIO()
     _header(out, f"synthetic {k}-NN")
@@ -610,6 +624,8 @@ def knn_pmml(n_instances: int = 200, n_features: int = 4, k: int = 3, classifica
             else f' continuousScoringMethod="{method or "average"}"')
     out.write(f' <NearestNeighborModel functionName="{fn}" numberOfNeighbors="{k}"{meth} threshold="0.001">\n')
     _mining_schema(out, n_features, "y", "  ")
+    if target:
+        out.write(f'  <Targets><Target field="y" {target}/></Targets>\n')
     out.write(f'  <TrainingInstances recordCount="{n_instances}" fieldCount="{n_features + 1}">\n   <InstanceFields>')
     out.write("".join(f'<InstanceField field="f{j}" column="c{j}"/>' for j in range(n_features)))
     out.write('<InstanceField field="y" column="target"/></InstanceFields>\n   <InlineTable>\n')
@@ -619,7 +635,8 @@ def knn_pmml(n_instances: int = 200, n_features: int = 4, k: int = 3, classifica
         out.write("    <row>" + "".join(f"<c{j}>{X[i, j]:.5f}</c{j}>" for j in range(n_features))
                   + f"<target>{t}</target></row>\n")
     out.write('   </InlineTable>\n  </TrainingInstances>\n')
-    out.write(f'  <ComparisonMeasure kind="distance"><{metric}/></ComparisonMeasure>\n  <KNNInputs>')
+    cf = f' compareFunction="{compare}"' if compare else ""
+    out.write(f'  <ComparisonMeasure kind="{measure}"{cf}><{metric}/></ComparisonMeasure>\n  <KNNInputs>')
     out.write("".join(f'<KNNInput field="f{j}"/>' for j in range(n_features)))
     out.write('</KNNInputs>\n </NearestNeighborModel>\n</PMML>\n')
     return out.getvalue()

@@ -10,7 +10,8 @@ the training instances as centres; the ``k`` nearest (ties: lower instance index
 
 JPMML scores it per record (`S/api/PmmlModel.scala:159-160`). Device: ``k == 1`` *is* a
 ClusteringModel whose centres are the instances and whose entity labels are their targets, so it
-runs on ``cluster.hip`` (the MFMA distance expansion for many instances); ``k > 1`` is host-only.
+runs on ``cluster.hip`` (the MFMA distance expansion for many instances); ``k > 1`` (and any model
+with a ``Targets`` rescale) runs on ``knn.hip`` (register top-k + aggregation, ``KnnPlan``).
 Parity unpinned (no JPMML here): follows the PMML 4.4 specification text.
 """
 
@@ -55,6 +56,7 @@ class NearestNeighborEvaluator(ClusteringEvaluator):
         super().__init__(knn_as_clustering(model, schema), schema)
         self.knn = model
         self.model = model  # outputs / targets / transformations of the original element
+        self.target = next((t for t in model.targets if t.field is None or t.field == self.target_field), None)
         self.k = max(1, int(model.k))
         self.kind = "classification" if model.function_name == "classification" else "regression"
         self.targets = list(self.entity_ids)  # instance target strings

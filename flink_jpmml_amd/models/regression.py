@@ -126,6 +126,10 @@ class RegressionEvaluator(ModelEvaluator):
                 P = E / E.sum(axis=1, keepdims=True)
             elif norm == "simplemax":
                 P = Y / Y.sum(axis=1, keepdims=True)
+            elif norm.startswith("cumulative:"):  # ordinal GLM lowered to tables (runtime/design.py)
+                cum = link(norm.split(":", 1)[1], Y)
+                cum[:, -1] = 1.0
+                P = np.diff(cum, axis=1, prepend=0.0)
             elif T == 2 and norm != "none":
                 p0 = link(norm, Y[:, 0])
                 P = np.stack([p0, 1.0 - p0], axis=1)
@@ -141,7 +145,9 @@ class RegressionEvaluator(ModelEvaluator):
 
 class GeneralRegressionEvaluator(ModelEvaluator):
     """GeneralRegressionModel for ``regression``, ``generalLinear``, ``generalizedLinear``
-    (identity/log/logit/probit/cloglog/power links) and ``multinomialLogistic``."""
+    (identity/log/logit/probit/cloglog/power links), ``multinomialLogistic`` and
+    ``ordinalMultinomial`` (cumulative logit/probit/cloglog/loglog/cauchit). Parity unpinned (no
+    JPMML here): follows the PMML 4.4 GeneralRegression text."""
 
     def __init__(self, model: ir.GeneralRegressionModel, schema: FieldSchema):
         super().__init__(model, schema)
@@ -214,6 +220,8 @@ class GeneralRegressionEvaluator(ModelEvaluator):
             return ModelResult("regression", np.where(miss, NAN, y), ~miss & np.isfinite(y))
         cats = self.categories
         n = cols.n
+        if gm.model_type == "ordinalMultinomial":
+            return self._ordinal(cols)
         etas = np.zeros((n, len(cats)))
         miss = np.zeros(n, dtype=bool)
         for k, c in enumerate(cats):
@@ -230,5 +238,28 @@ class GeneralRegressionEvaluator(ModelEvaluator):
             raise UnsupportedFeatureException(f"classification GeneralRegressionModel {gm.model_type!r}")
         lab = np.argmax(P, axis=1).astype(np.float64)
         ok = ~miss
+        return ModelResult("classification", np.where(ok, lab, NAN), ok, categories=cats,
+                           probs=np.where(ok[:, None], P, NAN))
+
+    def _ordinal(self, cols: Columns) -> ModelResult:
+        """``ordinalMultinomial``: cumulative link over the ordered categories. Category j < J-1 has
+        ``η_j = offset + Σ β`` over its own cells (the cut point) and the cells without a
+        targetCategory (the shared slopes); ``P(Y ≤ j) = F(η_j)`` with F the inverse
+        ``cumulativeLink``; ``P(j) = P(Y ≤ j) − P(Y ≤ j−1)``, the last category takes the rest."""
+        gm = self.gm
+        cats = self.categories
+        n, J = cols.n, len(cats)
+        F = gm.cumulative_link or "logit"
+        if F not in ("logit", "probit", "cloglog", "loglog", "cauchit"):
+            raise UnsupportedFeatureException(f"cumulativeLink {F!r}")
+        shared, miss = self._linear(cols, None)
+        cum = np.ones((n, J))
+        for j, c in enumerate(cats[:-1]):
+            e, m = self._linear(cols, c)
+            miss |= m
+            cum[:, j] = link(F, e + shared - gm.offset_value)  # offset counted once
+        P = np.diff(cum, axis=1, prepend=0.0)
+        lab = np.argmax(np.nan_to_num(P, nan=-np.inf), axis=1).astype(np.float64)
+        ok = ~miss & np.isfinite(P).all(axis=1)
         return ModelResult("classification", np.where(ok, lab, NAN), ok, categories=cats,
                            probs=np.where(ok[:, None], P, NAN))

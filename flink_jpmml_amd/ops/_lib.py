@@ -158,6 +158,15 @@ class ClusterArgs(ctypes.Structure):
                 ("label", c_void_p), ("affinity", c_void_p)]
 
 
+class KnnArgs(ctypes.Structure):
+    _fields_ = [("X", c_void_p), ("n_rows", c_int), ("n_feat", c_int), ("ldx", c_int), ("n_inst", c_int),
+                ("prep", c_void_p), ("inst", c_void_p), ("weights", c_void_p), ("scales", c_void_p),
+                ("qweights", c_void_p), ("cfun", c_void_p), ("inst_value", c_void_p), ("inst_class", c_void_p),
+                ("class_table", c_void_p), ("metric", c_int), ("similarity", c_int), ("p", c_float), ("k", c_int),
+                ("agg", c_int), ("threshold", c_float), ("epi", Epilogue), ("score", c_void_p),
+                ("valid", c_void_p)]
+
+
 class LinearArgs(ctypes.Structure):
     _fields_ = [("X", c_void_p), ("n_rows", c_int), ("n_feat", c_int), ("ldx", c_int), ("K", c_int),
                 ("prep", c_void_p), ("W", c_void_p), ("bias", c_void_p), ("simplemax", c_int), ("pad", c_int),
@@ -196,6 +205,7 @@ _ABI = {
     "pmml_tree_general_args_size": GenTreeArgs,
     "pmml_tree_hybrid_args_size": HybridArgs,
     "pmml_cluster_args_size": ClusterArgs,
+    "pmml_knn_args_size": KnnArgs,
     "pmml_linear_args_size": LinearArgs,
     "pmml_mlp_args_size": MlpArgs,
     "pmml_svm_args_size": SvmArgs,
@@ -251,6 +261,9 @@ def load(auto_build: bool = True) -> ctypes.CDLL:
         lib.pmml_cluster_mfma_launch.restype = ctypes.c_int
         lib.pmml_cluster_mfma_launch.argtypes = [c_void_p, ctypes.POINTER(ClusterArgs), c_void_p, c_void_p,
                                                  ctypes.c_int, ctypes.c_int]
+        lib.pmml_knn_launch.restype = ctypes.c_int
+        lib.pmml_knn_launch.argtypes = [c_void_p, ctypes.POINTER(KnnArgs), c_void_p, c_void_p, ctypes.c_int,
+                                        ctypes.c_int]
         lib.pmml_linear_launch.argtypes = [c_void_p, ctypes.POINTER(LinearArgs)]
         if hasattr(lib, "pmml_mlp_launch"):
             lib.pmml_mlp_launch.argtypes = [c_void_p, ctypes.POINTER(MlpArgs), c_int]

@@ -72,6 +72,7 @@ enum : int {
   EPI_LOGISTIC2 = 1,    // p0 = link(a * acc0 + b), p1 = 1 - p0; label = p0 >= thr ? 0 : 1
   EPI_ARGMAX = 2,       // label = argmax_c acc_c (ties -> lowest c); probs = acc * a
   EPI_SOFTMAX = 3,      // probs = softmax(acc); label = argmax
+  EPI_CUMULATIVE = 4,   // ordinal: cum_c = link(acc_c) (c < C-1), cum_{C-1} = 1; p_c = cum_c - cum_{c-1}
 };
 
 struct Epilogue {

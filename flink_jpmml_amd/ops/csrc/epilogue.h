@@ -41,6 +41,18 @@ __device__ __forceinline__ void apply_epilogue(const Epilogue& e, Acc acc, bool 
       probs[(size_t)row * 2 + 1] = 1.0f - p0;
     }
     ok = ok && (p0 == p0);
+  } else if (e.mode == EPI_CUMULATIVE) {
+    const int C = e.n_classes;
+    float best = -__builtin_inff();
+    float prev = 0.f;
+    for (int c = 0; c < C; ++c) {
+      const float cum = c < C - 1 ? apply_link(e.link, acc(c)) : 1.0f;
+      const float pv = cum - prev;
+      prev = cum;
+      if (pv > best) { best = pv; label = c; }
+      ok = ok && (pv == pv);
+      if (e.write_probs && probs) probs[(size_t)row * C + c] = pv;
+    }
   } else {
     const int C = e.n_classes;
     float best = -__builtin_inff();

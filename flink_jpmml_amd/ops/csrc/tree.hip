@@ -104,6 +104,111 @@ __global__ __launch_bounds__(TB, 2) void tree_pointer_kernel(TreeArgs a) {
   finish_row(a, acc, accl, split, GENERAL, row, row_ok && !poisoned);
 }
 
+// Pointer layout, refill schedule. The lock-step kernel above runs each group of PILP walks until
+// the deepest of its 64 x PILP walks ends: at depth 14 with ~6-level average paths most lanes idle
+// through half of every group. Here each of a lane's PILP slots is a work queue over the tree
+// range: the step that reaches a leaf accumulates it and immediately loads the next tree's root,
+// so every slot stays busy until the range is exhausted and the wave's loop count tracks the
+// AVERAGE path length, not the maximum. Root indices are staged in LDS (the refill hop is an LDS
+// read, not an L2 round trip). Leaves are added in completion order — deterministic for a given
+// forest, but not the tree-order fp32 sum of the lock-step kernel.
+constexpr int REFILL_ROOTS_LDS = 2048;
+
+template <bool GENERAL, bool FEAT_LDS>
+__global__ __launch_bounds__(TB, 2) void tree_pointer_refill_kernel(TreeArgs a) {
+  extern __shared__ __align__(16) uint32_t smem[];
+  float* feat = reinterpret_cast<float*>(smem);
+  int* bad = reinterpret_cast<int*>(smem + (FEAT_LDS ? a.n_feat * TB : 0));
+  float* accl = reinterpret_cast<float*>(bad + TB);
+  int* roots_l = reinterpret_cast<int*>(accl + (GENERAL ? a.C * TB : 0));
+  const int tid = threadIdx.x;
+  const int row0 = blockIdx.x * TB;
+  const int split = blockIdx.y;
+  const int row = row0 + tid;
+  const int tb = split * a.trees_per_split;
+  const int te = min(a.n_trees, tb + a.trees_per_split);
+  const bool roots_in_lds = te - tb <= REFILL_ROOTS_LDS;
+  if (roots_in_lds)
+    for (int t = tid; t < te - tb; t += TB) roots_l[t] = a.roots[tb + t];
+  if (FEAT_LDS) {
+    stage_rows_T<TB>(a.X, a.n_rows, a.n_feat, a.ldx, a.prep, feat, bad, row0);  // ends with a barrier
+  } else {
+    bad[tid] = 0;
+    __syncthreads();
+  }
+  bool row_ok = bad[tid] == 0;
+  const float* xrow = a.X + (size_t)min(row, a.n_rows - 1) * a.ldx;
+  if (!FEAT_LDS && a.prep && row < a.n_rows) {
+    for (int f = 0; f < a.n_feat; ++f) {
+      bool b = false;
+      (void)prep_value(xrow[f], a.prep[f], &b);
+      if (b) row_ok = false;
+    }
+  }
+  if (a.row_valid_in && row < a.n_rows) row_ok = row_ok && a.row_valid_in[row];
+  const uint4* nodes = reinterpret_cast<const uint4*>(a.blob);
+  if (GENERAL) {
+    for (int c = 0; c < a.C; ++c) accl[c * TB + tid] = 0.f;
+  }
+  auto root_of = [&](int t) { return roots_in_lds ? roots_l[t - tb] : a.roots[t]; };
+  float acc = 0.f;
+  bool poisoned = false;
+  const char* feat_lane = reinterpret_cast<const char*>(feat + tid);
+  constexpr int PILP = 8;
+  int code[PILP], tix[PILP];
+  int next = tb;
+#pragma unroll
+  for (int i = 0; i < PILP; ++i) {
+    const bool take = next < te;
+    tix[i] = next;
+    code[i] = take ? root_of(next) : -1;
+    next += take ? 1 : 0;
+  }
+  bool live = te > tb;
+  while (live) {
+    uint4 nd[PILP];
+#pragma unroll
+    for (int i = 0; i < PILP; ++i) nd[i] = nodes[max(code[i], 0)];
+    live = false;
+#pragma unroll
+    for (int i = 0; i < PILP; ++i) {
+      const bool act = code[i] >= 0;
+      float x;
+      if (FEAT_LDS) {
+        x = *reinterpret_cast<const float*>(feat_lane + (nd[i].y & 0xFFFFu));
+      } else {
+        const int f = nd[i].y & 0xFFFFu;
+        x = xrow[f];
+        if (a.prep) { bool b = false; x = prep_value(x, a.prep[f], &b); }
+      }
+      const bool isn = (x != x);
+      const bool nulled = act && isn && ((nd[i].y >> 30) & 1u);
+      const bool right = (x >= __uint_as_float(nd[i].x)) || (isn && (nd[i].y >> 31));
+      const int nc = right ? (int)nd[i].w : (int)nd[i].z;
+      const bool done = act && (nulled || nc < 0);
+      if (done) {
+        if (nulled) {
+          if (GENERAL) poisoned = true;
+          else acc += __builtin_nanf("");
+        } else if (GENERAL) {
+          const int slot = a.tree_slot[tix[i]];
+          for (int p = 0; p < a.P; ++p) accl[(slot + p) * TB + tid] += a.leaves[(size_t)(~nc) * a.P + p];
+        } else {
+          acc += a.leaves[~nc];
+        }
+        const bool take = next < te;
+        tix[i] = next;
+        code[i] = take ? root_of(next) : -1;
+        next += take ? 1 : 0;
+      } else if (act) {
+        code[i] = nc;
+      }
+      live = live || code[i] >= 0;
+    }
+  }
+  finish_row(a, acc, accl, split, GENERAL, row, row_ok && !poisoned);
+}
+
 // Split-mode reduction: partial[splits][C+1][n_rows] -> epilogue.
 __global__ __launch_bounds__(TB) void tree_reduce_kernel(TreeArgs a, int splits) {
   const int row = blockIdx.x * TB + threadIdx.x;
@@ -344,10 +449,29 @@ PMML_API int pmml_tree_launch(hipStream_t stream, const TreeArgs* args, int layo
       default: return -6;
     }
   } else {
-    if (a.variant != 0) return -10;
+    if (a.variant != 0 && a.variant != VAR_POINTER_REFILL) return -10;
     const bool feat_lds = a.n_feat <= 64;
-    const size_t lds = (feat_lds ? (size_t)a.n_feat * TB * 4 : 0) + TB * 4 + acc_lds;
-    if (a.general) {
+    size_t lds = (feat_lds ? (size_t)a.n_feat * TB * 4 : 0) + TB * 4 + acc_lds;
+    if (a.variant == VAR_POINTER_REFILL) {
+      lds += (size_t)REFILL_ROOTS_LDS * 4;
+      if (a.general) {
+        if (feat_lds) {
+          err = prepare_launch(tree_pointer_refill_kernel<true, true>, lds);
+          if (!err) hipLaunchKernelGGL((tree_pointer_refill_kernel<true, true>), grid, dim3(TB), lds, stream, a);
+        } else {
+          err = prepare_launch(tree_pointer_refill_kernel<true, false>, lds);
+          if (!err) hipLaunchKernelGGL((tree_pointer_refill_kernel<true, false>), grid, dim3(TB), lds, stream, a);
+        }
+      } else {
+        if (feat_lds) {
+          err = prepare_launch(tree_pointer_refill_kernel<false, true>, lds);
+          if (!err) hipLaunchKernelGGL((tree_pointer_refill_kernel<false, true>), grid, dim3(TB), lds, stream, a);
+        } else {
+          err = prepare_launch(tree_pointer_refill_kernel<false, false>, lds);
+          if (!err) hipLaunchKernelGGL((tree_pointer_refill_kernel<false, false>), grid, dim3(TB), lds, stream, a);
+        }
+      }
+    } else if (a.general) {
       if (feat_lds) {
         err = prepare_launch(tree_pointer_kernel<true, true>, lds);
         if (!err) hipLaunchKernelGGL((tree_pointer_kernel<true, true>), grid, dim3(TB), lds, stream, a);

@@ -72,6 +72,7 @@ struct TreeArgs {
 };
 constexpr int VAR_NAN_FAST = 4;    // wide kernel: take the fast path even on tiles with missing values
 constexpr int VAR_NAN_PLANES = 8;  // ... via blob_nan + a second feature plane (NaN -> +inf)
+constexpr int VAR_POINTER_REFILL = 16;  // pointer layout: refill schedule (tree.hip)
 
 // per-depth launchers (tree_d<D>.hip)
 #define PMML_TREE_DECL(D) int launch_perfect_d##D(hipStream_t st, const TreeArgs& a, dim3 grid, size_t lds);

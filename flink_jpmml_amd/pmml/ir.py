@@ -417,6 +417,7 @@ class GeneralRegressionModel(Model):
     pp_cells: List[Tuple[str, str, str]] = field(default_factory=list)  # (predictor, parameter, value)
     p_cells: List[Tuple[str, Optional[str], float]] = field(default_factory=list)  # (parameter, targetCategory, beta)
     target_reference_category: Optional[str] = None
+    cumulative_link: Optional[str] = None  # ordinalMultinomial: logit | probit | cloglog | loglog | cauchit
 
 
 # neural network --------------------------------------------------------------

@@ -459,6 +459,7 @@ def _parse_general_regression(el: ET.Element) -> ir.GeneralRegressionModel:
     m.distribution = el.get("distribution")
     m.offset_value = _f(el, "offsetValue", 0.0)
     m.target_reference_category = el.get("targetReferenceCategory")
+    m.cumulative_link = el.get("cumulativeLink")
     pl = _child(el, "ParameterList")
     if pl is not None:
         m.parameters = [p.get("name") for p in _children(pl, "Parameter")]

@@ -133,6 +133,20 @@ def _glm_tables(ev: GeneralRegressionEvaluator, d: _Design) -> Tuple[List[ir.Reg
         else:
             raise NotLowerable(f"GLM linkFunction {lf!r} is host-only")
         return [table(None)], norm
+    if gm.model_type == "ordinalMultinomial":
+        # one table per category: cut point + shared slopes (cells without a targetCategory); the
+        # last category's table is a placeholder — the cumulative epilogue gives it 1 - F(η_{J-2})
+        shared = table(None)
+        tabs = []
+        for c in ev.categories[:-1]:
+            own = table(c)
+            coef: Dict[str, float] = {}
+            for p in own.numeric + shared.numeric:
+                coef[p.name] = coef.get(p.name, 0.0) + p.coefficient
+            tabs.append(ir.RegressionTable(own.intercept + shared.intercept - gm.offset_value, c,
+                                           [ir.NumericPredictor(n, w) for n, w in coef.items()]))
+        tabs.append(ir.RegressionTable(0.0, ev.categories[-1], []))
+        return tabs, f"cumulative:{gm.cumulative_link or 'logit'}"
     if gm.model_type != "multinomialLogistic":
         raise NotLowerable(f"classification GeneralRegressionModel {gm.model_type!r} is host-only")
     tabs = []

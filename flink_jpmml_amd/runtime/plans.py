@@ -49,7 +49,7 @@ FP_INTEGER = 1 << 9
 FP_CODE_RANGE = 1 << 10
 FP_ROW_INVALID = 1 << 11
 
-EPI_AFFINE, EPI_LOGISTIC2, EPI_ARGMAX, EPI_SOFTMAX = 0, 1, 2, 3
+EPI_AFFINE, EPI_LOGISTIC2, EPI_ARGMAX, EPI_SOFTMAX, EPI_CUMULATIVE = 0, 1, 2, 3, 4
 LINKS = {"none": 0, None: 0, "logit": 1, "exp": 2, "probit": 3, "cloglog": 4, "loglog": 5, "cauchit": 6}
 
 
@@ -262,7 +262,7 @@ class DevicePlan:
 
         from ..ops import _lib
 
-        cls = {c.__name__: c for c in (TreePlan, ClusterPlan, LinearPlan)}.get(meta["__class__"])
+        cls = {c.__name__: c for c in (TreePlan, ClusterPlan, KnnPlan, LinearPlan)}.get(meta["__class__"])
         if cls is None and meta["__class__"] == "DerivedPlan":
             from .derive import DerivedPlan as cls
         if cls is None and meta["__class__"] == "SegmentedPlan":
@@ -421,8 +421,8 @@ class ClusterPlan(DevicePlan):
         applies and K ≥ ``MFMA_MIN_K``)."""
         super().__init__(compiled, device)
         ev: ClusteringEvaluator = compiled.evaluator
-        if getattr(ev, "k", 1) > 1:
-            raise NotLowerable("k-NN with k > 1 is host-only (k = 1 runs as a clustering argmin)")
+        if getattr(ev, "knn", None) is not None and (min(ev.k, len(ev.targets)) > 1 or ev.target is not None):
+            raise NotLowerable("k-NN with k > 1 or a Target runs on the k-NN kernel (KnnPlan)")
         if ev.metric not in self._METRICS:
             raise NotLowerable(f"clustering metric {ev.metric!r} is host-only")
         if ev.fields != compiled.active_fields:
@@ -487,6 +487,94 @@ class ClusterPlan(DevicePlan):
             check(self.lib.pmml_cluster_launch(stream_handle(stream), ctypes.byref(a)), "cluster kernel")
 
 
+class KnnPlan(DevicePlan):
+    """NearestNeighborModel with ``k > 1`` on ``knn.hip``: instance distances (VALU, or MFMA
+    expansion for squared / plain euclidean absDiff distances over many instances), a register
+    top-k and the PMML aggregation (vote / average / median / weighted forms) in the same kernel.
+    Mirrors :class:`~flink_jpmml_amd.models.knn.NearestNeighborEvaluator`; ``k == 1`` stays a
+    clustering argmin (:class:`ClusterPlan`)."""
+
+    kind = "knn"
+    _STATE = DevicePlan._STATE + ("inst", "weights", "scales", "qweights", "cfun", "inst_value", "inst_class",
+                                  "class_table", "metric_code", "similarity", "p", "k", "agg", "threshold",
+                                  "variant", "wc", "cc", "tgt")
+    _AGG = {"majorityVote": 0, "weightedMajorityVote": 1, "average": 2, "median": 3, "weightedAverage": 4}
+    K_MAX = 32
+    MFMA_MIN_INSTANCES = 64
+
+    def __init__(self, compiled, device, knn_variant: str = "auto", **_):
+        super().__init__(compiled, device)
+        ev = compiled.evaluator
+        m = ev.knn
+        k = min(ev.k, len(ev.targets))
+        if k > self.K_MAX:
+            raise NotLowerable(f"k-NN with k = {k} > {self.K_MAX} is host-only")
+        if ev.metric not in ClusterPlan._METRICS:
+            raise NotLowerable(f"k-NN metric {ev.metric!r} is host-only")
+        if ev.fields != compiled.active_fields:
+            raise NotLowerable("k-NN inputs differ from the active fields (derived inputs are host-only)")
+        if compiled.n_features > 128:
+            raise NotLowerable("k-NN over more than 128 inputs is host-only")
+        method = m.categorical_method if ev.kind == "classification" else m.continuous_method
+        if method not in self._AGG or (ev.kind == "classification") != (self._AGG[method] < 2):
+            raise NotLowerable(f"k-NN scoring method {method!r} is host-only")
+        self.metric_code = ClusterPlan._METRICS[ev.metric]
+        self.similarity = 0 if ev.kind_distance else 1
+        self.p = float(ev.p)
+        self.k = int(k)
+        self.agg = self._AGG[method]
+        self.threshold = float(m.threshold)
+        self.inst = self._t(ev.centers.astype(np.float32))
+        self.weights = self._t(ev.weights.astype(np.float32))
+        self.scales = self._t(ev.scales.astype(np.float32))
+        self.qweights = self._t(ev.missing_weights.astype(np.float32))
+        self.cfun = self._t(np.array([ClusterPlan._CF[c] for c in ev.compare], dtype=np.int32))
+        if ev.kind == "classification":
+            self.inst_class = self._t(np.asarray(ev.inst_class, dtype=np.int32))
+            self.class_table = self._t(_label_table(ev.categories))
+            self.inst_value = None
+            self.tgt = None
+        else:
+            self.inst_value = self._t(ev.inst_value.astype(np.float32))
+            self.inst_class = self.class_table = None
+            self.tgt = target_post(ev.target, force=True) if ev.target is not None else None
+        mfma_ok = (self.similarity == 0 and self.metric_code in (0, 1) and all(c == "absDiff" for c in ev.compare))
+        if knn_variant not in ("auto", "valu", "mfma"):
+            raise ValueError(f"knn_variant {knn_variant!r}")
+        if knn_variant == "mfma" and not mfma_ok:
+            raise NotLowerable("MFMA k-NN needs squared/plain euclidean distance with absDiff")
+        use = knn_variant == "mfma" or (knn_variant == "auto" and mfma_ok
+                                        and len(ev.centers) >= self.MFMA_MIN_INSTANCES)
+        self.variant = "mfma" if use else "valu"
+        self.wc = self.cc = None
+        if use:
+            wc, cc = ClusterPlan.mfma_operands(ev.centers, ev.weights)
+            self.wc, self.cc = self._t(wc), self._t(cc)
+
+    def launch(self, X, score, valid, stream=None, probs=None) -> None:
+        import ctypes
+
+        from ..ops._lib import KnnArgs, check, ptr, stream_handle
+
+        a = KnnArgs()
+        a.X = ptr(X)
+        a.n_rows, a.n_feat, a.ldx, a.n_inst = X.shape[0], X.shape[1], X.stride(0), self.inst.shape[0]
+        a.prep = ptr(self.prep)
+        a.inst, a.weights, a.scales, a.qweights = ptr(self.inst), ptr(self.weights), ptr(self.scales), ptr(self.qweights)
+        a.cfun, a.inst_value, a.inst_class = ptr(self.cfun), ptr(self.inst_value), ptr(self.inst_class)
+        a.class_table = ptr(self.class_table)
+        a.metric, a.similarity, a.p, a.k = self.metric_code, self.similarity, self.p, self.k
+        a.agg, a.threshold = self.agg, self.threshold
+        a.epi = _epilogue(0, tgt=self.tgt)
+        a.score, a.valid = ptr(score), ptr(valid)
+        if self.variant == "mfma":
+            Np, Fp = self.wc.shape
+            check(self.lib.pmml_knn_launch(stream_handle(stream), ctypes.byref(a), ptr(self.wc), ptr(self.cc),
+                                           Np, Fp), "k-NN mfma kernel")
+        else:
+            check(self.lib.pmml_knn_launch(stream_handle(stream), ctypes.byref(a), None, None, 0, 0), "k-NN kernel")
+
+
 # --------------------------------------------------------------------------- linear
 
 
@@ -526,6 +614,11 @@ class LinearPlan(DevicePlan):
             elif norm == "simplemax":
                 self.simplemax = 1
                 self.epi_args = dict(mode=EPI_ARGMAX, C=self.K)
+            elif norm.startswith("cumulative:"):  # ordinal GLM (runtime/design.py)
+                lk = norm.split(":", 1)[1]
+                if lk not in LINKS or lk in ("none", "exp"):
+                    raise NotLowerable(f"cumulativeLink {lk!r}")
+                self.epi_args = dict(mode=EPI_CUMULATIVE, C=self.K, link=LINKS[lk])
             elif self.K == 2:
                 if norm not in LINKS:
                     raise NotLowerable(f"normalizationMethod {norm!r}")
@@ -973,7 +1066,7 @@ def _perfect_pack_vec(trees, weights, P: int, D: int, stride: int, fmap, leaf_bi
     return blob, rec, has_dr
 
 
-VAR_NAN_FAST, VAR_NAN_PLANES = 4, 8  # mirrors csrc/tree_common.h
+VAR_NAN_FAST, VAR_NAN_PLANES, VAR_POINTER_REFILL = 4, 8, 16  # mirrors csrc/tree_common.h
 DYN_B, DYN_SLOTS = 8, 16  # csrc: MODE_SUM trees per claimed batch, batch slots per chunk
 
 
@@ -1117,8 +1210,13 @@ class TreePlan(DevicePlan):
 
     def __init__(self, compiled, device, layout: str = "auto", lds_budget: int = 80 * 1024, splits: int = 0,
                  variant: str = "auto", precision: str = "fp32", nan_mode: str = "auto", max_chunk_trees: int = 0,
-                 tree_shard: Optional[Tuple[int, int]] = None, head_depth: int = 0):
-        """``nan_mode`` (wide PERFECT kernel): ``"auto"`` keeps tiles with missing values on the fast
+                 tree_shard: Optional[Tuple[int, int]] = None, head_depth: int = 0,
+                 pointer_schedule: str = "refill"):
+        """``pointer_schedule`` (pointer layout): ``"refill"`` (each walk slot restarts on the next
+        tree the step its walk ends; leaves summed in completion order) or ``"lockstep"`` (groups
+        of walks run to the deepest one; tree-order sums).
+
+        ``nan_mode`` (wide PERFECT kernel): ``"auto"`` keeps tiles with missing values on the fast
         traversal whenever the ensemble has no null-on-missing trees (default-right nodes read a
         NaN -> +inf second feature plane, :func:`_nan_planes`); ``"off"``: per-node missing test.
 
@@ -1128,6 +1226,9 @@ class TreePlan(DevicePlan):
         super().__init__(compiled, device)
         if nan_mode not in ("auto", "off"):
             raise ValueError("nan_mode must be 'auto' or 'off'")
+        if pointer_schedule not in ("refill", "lockstep"):
+            raise ValueError("pointer_schedule must be 'refill' or 'lockstep'")
+        self.heads, self.head_depth = None, 0  # hybrid layout only
         if precision not in ("fp32", "fp8"):
             raise ValueError("tree leaf precision must be fp32 or fp8")
         if layout == "general":
@@ -1330,7 +1431,9 @@ class TreePlan(DevicePlan):
             self.blob_nan, self.chunk_trees_nan = None, 0
             self.head_depth = H
             self.rec_words = head_words(H) if H else 0
-            self.variant = 0
+            # pointer walks: refill schedule (each PILP slot restarts on the next tree as soon as
+            # its walk ends) unless pinned to the lock-step kernel's tree-order sums
+            self.variant = VAR_POINTER_REFILL if (self.layout == "pointer" and pointer_schedule == "refill") else 0
             self.blob = self._t(nodes.reshape(-1).view(np.int32))
             self.leaves = self._t(leaves.reshape(-1))
             self.roots = self._t(roots)
@@ -1565,6 +1668,8 @@ def compile_plan(compiled, device, **opts) -> DevicePlan:
     if policy not in ("fp32", "bf16", "fp8"):
         raise ValueError(f"precision must be fp32, bf16 or fp8, got {policy!r}")
     if isinstance(ev, ClusteringEvaluator):
+        if getattr(ev, "knn", None) is not None and (min(ev.k, len(ev.targets)) > 1 or ev.target is not None):
+            return KnnPlan(compiled, device, **opts)
         return ClusterPlan(compiled, device, **opts)
     if isinstance(ev, (TreeEvaluator, MiningEvaluator)):
         try:

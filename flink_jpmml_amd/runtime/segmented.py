@@ -5,9 +5,12 @@ The fused ensemble kernels (:class:`~flink_jpmml_amd.runtime.plans.TreePlan`) co
 model chains of XGBoost / LightGBM. Everything else a JPMML user can hand the reference
 (`S/api/PmmlModel.scala:159-160` evaluates any segmentation JPMML supports) lowers here:
 
-* ``multipleModelMethod`` ``selectFirst``, ``max``, ``min``, ``median`` and every supported
-  method under **non-True segment predicates** (the segment participates only where its
-  predicate is TRUE; three-valued logic, UNKNOWN does not select);
+* ``multipleModelMethod`` ``selectFirst``, ``max``, ``min``, ``median``, ``weightedMedian`` and
+  every supported method under **non-True segment predicates** (the segment participates only
+  where its predicate is TRUE; three-valued logic, UNKNOWN does not select);
+* classification ``average`` / ``weightedAverage`` / ``max`` / ``median`` over the segments'
+  probability vectors (each segment plan writes its ``[n, C_i]`` probabilities through its fused
+  epilogue; they are scattered into the ensemble's category order on the device);
 * segments that are not binary trees: each segment is lowered by :func:`compile_plan` on its own
   (trees, linear models, neural networks, SVMs, nested ensembles — recursively).
 
@@ -33,8 +36,9 @@ from ..models.mining import MiningEvaluator
 from ..pmml import ir
 from .plans import DevicePlan, NotLowerable, _label_table, apply_target_torch, target_post
 
-REGRESSION_METHODS = ("sum", "average", "weightedAverage", "max", "min", "median", "selectFirst")
-CLASSIFICATION_METHODS = ("majorityVote", "weightedMajorityVote", "selectFirst")
+REGRESSION_METHODS = ("sum", "average", "weightedAverage", "max", "min", "median", "weightedMedian", "selectFirst")
+PROB_METHODS = ("average", "weightedAverage", "max", "median")  # classification over segment probabilities
+CLASSIFICATION_METHODS = ("majorityVote", "weightedMajorityVote", "selectFirst") + PROB_METHODS
 
 
 class SubView:
@@ -175,6 +179,24 @@ def eval_predicate_device(prog, X):
     return acc & ~unk, unk
 
 
+def probs_width(plan) -> Optional[int]:
+    """Number of probability columns a classification plan writes through ``launch(probs=...)``
+    (the oracle's ``ModelResult.probs`` of that model), or None when it cannot."""
+    from .plans import EPI_ARGMAX, EPI_CUMULATIVE, EPI_LOGISTIC2, EPI_SOFTMAX, LinearPlan, TreePlan
+
+    inner = getattr(plan, "inner", None)
+    if inner is not None:
+        return probs_width(inner)
+    if isinstance(plan, (LinearPlan, TreePlan)):
+        e = getattr(plan, "epi_args", {})
+        if e.get("mode") in (EPI_ARGMAX, EPI_SOFTMAX, EPI_CUMULATIVE, EPI_LOGISTIC2):
+            if isinstance(plan, TreePlan) and getattr(plan, "sharded", False):
+                return None
+            return 2 if e["mode"] == EPI_LOGISTIC2 else int(e.get("C", 0)) or None
+        return None
+    return None
+
+
 def _index_outputs(plan) -> None:
     """Make a classification segment plan emit class *indices* (its epilogue's label table off)."""
     if getattr(plan, "table", None) is not None:
@@ -217,6 +239,8 @@ class SegmentedPlan(DevicePlan):
             if self.kind_ == "classification":
                 if sub.kind != "classification":
                     raise NotLowerable("classification segmentation over non-classification segments")
+                if self.method in PROB_METHODS and probs_width(plan) != len(sub.categories):
+                    raise NotLowerable(f"segment {seg.id!r}: {type(plan).__name__} does not expose probabilities")
                 _index_outputs(plan)
             self.subs.append(plan)
         self.n_subs = len(self.subs)
@@ -271,12 +295,19 @@ class SegmentedPlan(DevicePlan):
         with ctx:
             S = torch.empty((self.n_subs, n), dtype=torch.float32, device=self.device)
             V = torch.empty((self.n_subs, n), dtype=torch.uint8, device=self.device)
+            probs = self.kind_ == "classification" and self.method in PROB_METHODS
+            Pr = []
             for i, plan in enumerate(self.subs):
-                plan.launch(X, S[i], V[i], stream=st)
+                if probs:
+                    Pr.append(torch.full((n, len(self.remap_lists[i]) - 1), float("nan"), dtype=torch.float32,
+                                         device=self.device))
+                plan.launch(X, S[i], V[i], stream=st, **({"probs": Pr[i]} if probs else {}))
             T = torch.stack([eval_predicate_device(p, X)[0] for p in self.progs])  # [K, n] TRUE masks
             ok = V.bool() & ~torch.isnan(S)
             if self.method == "selectFirst":
                 s, v = self._select(S, ok, T)
+            elif probs:
+                s, v = self._prob_combine(Pr, ok, T)
             elif self.kind_ == "classification":
                 s, v = self._vote(S, ok, T)
             else:
@@ -328,18 +359,55 @@ class SegmentedPlan(DevicePlan):
             fill = float("-inf") if m == "max" else float("inf")
             Vf = torch.where(use, S, torch.full_like(S, fill))
             out = Vf.max(dim=0).values if m == "max" else Vf.min(dim=0).values
+        elif m == "weightedMedian":  # first value whose cumulative weight reaches half the total
+            w = torch.tensor(self.weights, dtype=torch.float64, device=S.device)[:, None].expand_as(S)
+            srt, order = torch.where(use, S, torch.full_like(S, float("inf"))).sort(dim=0, stable=True)
+            cw = torch.where(use, w, torch.zeros_like(w)).gather(0, order).cumsum(dim=0)
+            below = (cw < 0.5 * cw[-1:]).sum(dim=0).clamp(max=S.shape[0] - 1)
+            out = srt.gather(0, below[None, :])[0]
         else:  # median: mean of the two middle values of the participating segments (numpy rule)
-            srt = torch.where(use, S, torch.full_like(S, float("inf"))).sort(dim=0).values
-            c = cnt.clamp(min=1)
-            lo = srt.gather(0, ((c - 1) // 2)[None, :])[0]
-            hi = srt.gather(0, (c // 2)[None, :])[0]
-            out = (lo + hi) / 2
+            out = _median0(torch.where(use, S, torch.full_like(S, float("nan"))))
         v = cnt > 0
         if not self.skip:
             v = v & ~miss.any(dim=0)
         v = v & torch.isfinite(out)
         out, v = apply_target_torch(out, v, self.tgt)
         return out, v
+
+    def _prob_combine(self, Pr, ok, T):
+        """Classification ``average`` / ``weightedAverage`` / ``max`` / ``median`` over segment
+        probabilities (oracle: ``MiningEvaluator._classify``)."""
+        import torch
+
+        K, n = ok.shape
+        C = len(self.categories)
+        use = T & ok
+        anymiss = (T & ~ok).any(dim=0)
+        m = self.method
+        fill = float("nan") if m == "median" else 0.0
+        P = torch.full((K, n, C), fill, dtype=torch.float64, device=ok.device)
+        for i in range(K):
+            cols = self.remaps[i][:-1]
+            keep = cols >= 0
+            src = Pr[i].double()
+            if m != "median":
+                src = torch.nan_to_num(src, nan=0.0)
+            P[i][:, cols[keep]] = src[:, keep]
+        if m in ("average", "weightedAverage"):
+            w = torch.tensor([w if m == "weightedAverage" else 1.0 for w in self.weights], dtype=torch.float64,
+                             device=ok.device)[:, None]
+            wu = torch.where(use, w.expand(K, n), torch.zeros((K, n), dtype=torch.float64, device=ok.device))
+            probs = (P * wu[:, :, None]).sum(dim=0) / wu.sum(dim=0)[:, None]
+        elif m == "max":
+            probs = torch.where(use[:, :, None], P, torch.zeros_like(P)).max(dim=0).values.clamp(min=0.0)
+        else:
+            probs = _median0(torch.where(use[:, :, None], P, torch.full_like(P, float("nan"))))
+        v = use.any(dim=0)
+        if not self.skip:
+            v = v & ~anymiss
+        lab = torch.nan_to_num(probs, nan=-1.0).argmax(dim=1)  # ties -> lowest index, as np.argmax
+        s = self.table[lab].double()
+        return s, v & ~torch.isnan(s)
 
     def _vote(self, S, ok, T):
         import torch
@@ -362,4 +430,16 @@ class SegmentedPlan(DevicePlan):
         return s, v & ~torch.isnan(s)
 
 
-__all__ = ["SegmentedPlan", "SubView", "segmentable"]
+def _median0(A):
+    """``numpy.nanmedian`` along dim 0 (mean of the two middle values; NaN where nothing is left)."""
+    import torch
+
+    cnt = (~torch.isnan(A)).sum(dim=0)
+    srt = torch.where(torch.isnan(A), torch.full_like(A, float("inf")), A).sort(dim=0).values
+    c = cnt.clamp(min=1)
+    lo = srt.gather(0, ((c - 1) // 2).unsqueeze(0))[0]
+    hi = srt.gather(0, (c // 2).unsqueeze(0))[0]
+    return torch.where(cnt > 0, (lo + hi) / 2, torch.full_like(lo, float("nan")))
+
+
+__all__ = ["SegmentedPlan", "SubView", "probs_width", "segmentable"]

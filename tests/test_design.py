@@ -23,6 +23,11 @@ CASES = {
     "glm-power0": lambda: glm_pmml(link="power"),
     "glm-general-linear": lambda: glm_pmml(model_type="generalLinear"),
     "glm-multinomial": lambda: glm_pmml(model_type="multinomialLogistic"),
+    "glm-ordinal-logit": lambda: glm_pmml(model_type="ordinalMultinomial", link="logit", classes=4),
+    "glm-ordinal-probit": lambda: glm_pmml(model_type="ordinalMultinomial", link="probit", seed=2),
+    "glm-ordinal-cloglog": lambda: glm_pmml(model_type="ordinalMultinomial", link="cloglog", classes=5, seed=3),
+    "glm-ordinal-loglog": lambda: glm_pmml(model_type="ordinalMultinomial", link="loglog", seed=4),
+    "glm-ordinal-cauchit": lambda: glm_pmml(model_type="ordinalMultinomial", link="cauchit", seed=5),
     "naive-bayes": lambda: naive_bayes_pmml(),
     "naive-bayes-2": lambda: naive_bayes_pmml(classes=2, seed=3),
 }
@@ -54,6 +59,28 @@ def test_design_program_matches_oracle(name):
         assert (res.value[vref] == ref[vref]).mean() > 0.999
     else:
         assert np.allclose(res.value[vref], ref[vref], rtol=1e-5, atol=1e-5)
+
+
+def test_ordinal_glm_oracle_by_hand():
+    """eta_j = offset + cut_j + shared slopes, P(Y<=j) = logistic(eta_j), P(j) = differences."""
+    c = CompiledPmml.from_string(glm_pmml(model_type="ordinalMultinomial", link="logit", classes=4, seed=7))
+    gm = c.evaluator.gm
+    _, X = mixed_records(6, 3, seed=11, missing_rate=0.1)
+    beta = {(p, tc): b for p, tc, b in gm.p_cells}
+    res = c.result(X)
+    for r in range(len(X)):
+        f0, f1, f2, code = X[r]
+        if np.isnan([f0, f1, f2]).any():
+            assert not res.valid[r]
+            continue
+        lvl = ["red", "green", "blue"][int(code)] if not np.isnan(code) else None
+        cols = {"p1": f0, "p2": f1 ** 2, "p3": f2, "pc1": float(lvl == "red"), "pc2": float(lvl == "green"),
+                "px": float(lvl == "blue") * f0}
+        shared = 0.25 + sum(beta[(p, None)] * v for p, v in cols.items())
+        cum = [1 / (1 + np.exp(-(beta[("p0", str(j))] + shared))) for j in range(3)] + [1.0]
+        probs = np.diff(cum, prepend=0.0)
+        np.testing.assert_allclose(res.probs[r], probs, rtol=1e-12)
+        assert res.value[r] == float(np.argmax(probs))
 
 
 def test_glm_oracle_semantics():

@@ -20,7 +20,7 @@ def _run(gpu, txt, n=20_000, missing=0.05):
     return plan, s.cpu().numpy(), v.cpu().numpy(), ref, vref
 
 
-@pytest.mark.parametrize("method", ["selectFirst", "max", "median", "weightedAverage"])
+@pytest.mark.parametrize("method", ["selectFirst", "max", "median", "weightedAverage", "weightedMedian"])
 def test_regression_segmentation_on_gpu(gpu, method):
     from flink_jpmml_amd.bench.synth import segmented_pmml
 
@@ -30,7 +30,7 @@ def test_regression_segmentation_on_gpu(gpu, method):
     np.testing.assert_allclose(s[v], ref[v], rtol=1e-5, atol=1e-5)
 
 
-@pytest.mark.parametrize("method", ["majorityVote", "selectFirst"])
+@pytest.mark.parametrize("method", ["majorityVote", "selectFirst", "average", "weightedAverage", "max", "median"])
 def test_classification_segmentation_on_gpu(gpu, method):
     from flink_jpmml_amd.bench.synth import segmented_pmml
 

@@ -27,6 +27,8 @@ class _OracleSegment:
         r = self.sub.evaluate(cols)
         score.copy_(torch.from_numpy(np.where(r.valid, r.value, np.nan)).float())
         valid.copy_(torch.from_numpy(r.valid.astype(np.uint8)))
+        if kw.get("probs") is not None:
+            kw["probs"].copy_(torch.from_numpy(r.probs).float())
 
 
 def _run(txt, n=4000, missing=0.08, seed=3):
@@ -43,7 +45,8 @@ def _run(txt, n=4000, missing=0.08, seed=3):
     return plan, s.numpy(), v.numpy().astype(bool), ref, vref
 
 
-@pytest.mark.parametrize("method", ["selectFirst", "max", "min", "median", "sum", "average", "weightedAverage"])
+@pytest.mark.parametrize("method", ["selectFirst", "max", "min", "median", "sum", "average", "weightedAverage",
+                                    "weightedMedian"])
 @pytest.mark.parametrize("treatment", [None, "skipSegment"])
 def test_regression_segmentations(method, treatment):
     plan, s, v, ref, vref = _run(segmented_pmml(method, False, n_segments=5, seed=7, missing_treatment=treatment))
@@ -52,9 +55,12 @@ def test_regression_segmentations(method, treatment):
     np.testing.assert_allclose(s[v], ref[v], rtol=1e-6, atol=1e-6)
 
 
-@pytest.mark.parametrize("method", ["majorityVote", "weightedMajorityVote", "selectFirst"])
-def test_classification_segmentations(method):
-    plan, s, v, ref, vref = _run(segmented_pmml(method, True, n_segments=6, n_classes=4, seed=11))
+@pytest.mark.parametrize("method", ["majorityVote", "weightedMajorityVote", "selectFirst", "average",
+                                    "weightedAverage", "max", "median"])
+@pytest.mark.parametrize("treatment", [None, "skipSegment"])
+def test_classification_segmentations(method, treatment):
+    plan, s, v, ref, vref = _run(segmented_pmml(method, True, n_segments=6, n_classes=4, seed=11,
+                                                missing_treatment=treatment))
     assert (v == vref).all() and v.any()
     assert (s[v] == ref[v]).all()
 
@@ -78,7 +84,7 @@ def test_true_segment_sums_stay_fused():
 
 
 def test_unsupported_segmentation_reason():
-    c = CompiledPmml.from_string(segmented_pmml("max", True, seed=1))  # classification max: host only
+    c = CompiledPmml.from_string(segmented_pmml("sum", True, seed=1))  # classification sum: not a PMML rule
     assert "classification multipleModelMethod" in segmentable(c.evaluator, c)
 
 
