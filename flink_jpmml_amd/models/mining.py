@@ -22,6 +22,7 @@ import numpy as np
 from ..api.exceptions import UnsupportedFeatureException
 from ..pmml import ir
 from ..pmml.fields import NAN, Columns, FieldSchema, eval_predicate
+from ..pmml.mathcontext import is_float
 from .base import ModelEvaluator, ModelResult
 
 
@@ -128,7 +129,9 @@ class MiningEvaluator(ModelEvaluator):
         method = self.method
         with np.errstate(invalid="ignore", divide="ignore"):
             Vz = np.where(use, V, 0.0)
-            if method == "sum":
+            if is_float(self.mm) and method in ("sum", "average", "weightedAverage"):
+                out = _float_aggregate(method, Vz, W, use)
+            elif method == "sum":
                 out = np.sum(Vz, axis=1)
             elif method == "average":
                 out = np.sum(Vz, axis=1) / np.sum(use, axis=1)
@@ -205,6 +208,20 @@ class MiningEvaluator(ModelEvaluator):
         lab = np.argmax(np.nan_to_num(probs, nan=-1.0), axis=1).astype(np.float64)
         return ModelResult("classification", np.where(valid, lab, NAN), valid, categories=cats,
                            probs=np.where(valid[:, None], probs, NAN))
+
+
+def _float_aggregate(method: str, Vz: np.ndarray, W: np.ndarray, use: np.ndarray) -> np.ndarray:
+    """``x-mathContext="float"``: the segment values summed in float32, in segment order."""
+    acc = np.zeros(Vz.shape[0], dtype=np.float32)
+    wsum = np.zeros(Vz.shape[0], dtype=np.float32)
+    for j in range(Vz.shape[1]):
+        v = Vz[:, j].astype(np.float32)
+        w = W[:, j].astype(np.float32) if method == "weightedAverage" else np.float32(1.0)
+        acc = acc + (w * v if method == "weightedAverage" else v)
+        wsum = wsum + np.where(use[:, j], w, np.float32(0.0))
+    if method == "sum":
+        return acc.astype(np.float64)
+    return (acc / wsum).astype(np.float64)
 
 
 def _weighted_median(V: np.ndarray, W: np.ndarray, use: np.ndarray) -> np.ndarray:

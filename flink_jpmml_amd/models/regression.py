@@ -23,6 +23,7 @@ import numpy as np
 from ..api.exceptions import UnsupportedFeatureException
 from ..pmml import ir
 from ..pmml.fields import NAN, Columns, FieldSchema
+from ..pmml.mathcontext import is_float
 from .base import ModelEvaluator, ModelResult
 
 _SQRT2 = math.sqrt(2.0)
@@ -86,6 +87,8 @@ class RegressionEvaluator(ModelEvaluator):
         return W, b
 
     def raw_scores(self, cols: Columns) -> tuple:
+        if is_float(self.rm):
+            return self._raw_scores_f32(cols)
         n = cols.n
         Y = np.zeros((n, len(self.rm.tables)))
         miss = np.zeros(n, dtype=bool)
@@ -106,6 +109,33 @@ class RegressionEvaluator(ModelEvaluator):
                     miss |= np.isnan(x)
                     prod = prod * x
                 y = y + term.coefficient * prod
+            Y[:, k] = y
+        return Y, miss
+
+    def _raw_scores_f32(self, cols: Columns) -> tuple:
+        """``x-mathContext="float"``: every product and partial sum in float32, in term order."""
+        n = cols.n
+        f32 = np.float32
+        Y = np.zeros((n, len(self.rm.tables)), dtype=np.float32)
+        miss = np.zeros(n, dtype=bool)
+        for k, t in enumerate(self.rm.tables):
+            y = np.full(n, f32(t.intercept), dtype=np.float32)
+            for p in t.numeric:
+                x = cols.get(p.name).astype(np.float32)
+                miss |= np.isnan(x)
+                xe = x if p.exponent == 1.0 else np.power(x, f32(p.exponent))
+                y = y + f32(p.coefficient) * xe
+            for p in t.categorical:
+                x = cols.get(p.name)
+                lit = self.schema.lookup(p.name, p.value)
+                y = y + np.where(x == lit, f32(p.coefficient), f32(0.0))
+            for term in t.terms:
+                prod = np.ones(n, dtype=np.float32)
+                for f in term.fields:
+                    x = cols.get(f).astype(np.float32)
+                    miss |= np.isnan(x)
+                    prod = prod * x
+                y = y + f32(term.coefficient) * prod
             Y[:, k] = y
         return Y, miss
 

@@ -260,6 +260,7 @@ class Model:
     local_transformations: List[DerivedField] = field(default_factory=list)
     is_scorable: bool = True
     algorithm_name: Optional[str] = None
+    math_context: Optional[str] = None  # x-mathContext: "float" | "double" (pmml/mathcontext.py)
 
 
 # clustering ---------------------------------------------------------------

@@ -323,6 +323,7 @@ def _common(el: ET.Element) -> dict:
         local_transformations=_parse_transformations(_child(el, "LocalTransformations")),
         is_scorable=el.get("isScorable", "true") == "true",
         algorithm_name=el.get("algorithmName"),
+        math_context=el.get("x-mathContext") or el.get("mathContext"),
     )
 
 
@@ -720,8 +721,10 @@ def parse_element(root: ET.Element) -> ir.PMMLDocument:
             raise UnsupportedFeatureException(f"model type <{ln}> is not supported")
     if not models:
         raise PmmlParseError("PMML document contains no model element")
-    return ir.PMMLDocument(version=version, data_fields=data_fields, transformations=trans, models=models,
-                           header=header)
+    from .mathcontext import apply_math_context
+
+    return apply_math_context(ir.PMMLDocument(version=version, data_fields=data_fields, transformations=trans,
+                                              models=models, header=header))
 
 
 _FLATS: "contextvars.ContextVar[Optional[list]]" = contextvars.ContextVar("fja_flat_trees", default=None)
