@@ -167,6 +167,20 @@ class KnnArgs(ctypes.Structure):
                 ("valid", c_void_p)]
 
 
+class GemmArgs(ctypes.Structure):
+    _fields_ = [("A", c_void_p), ("Wt", c_void_p), ("bias", c_void_p), ("C", c_void_p), ("rows", c_int),
+                ("rows_p", c_int), ("K", c_int), ("Mp", c_int), ("lda", c_int), ("ldw", c_int), ("ldc", c_int),
+                ("act", c_int), ("thr", c_float), ("n_out", c_int), ("final_norm", c_int), ("pad", c_int),
+                ("row_ok", c_void_p), ("epi", Epilogue), ("score", c_void_p), ("valid", c_void_p),
+                ("probs", c_void_p)]
+
+
+class NnPrepArgs(ctypes.Structure):
+    _fields_ = [("X", c_void_p), ("n_rows", c_int), ("rows_p", c_int), ("ldx", c_int), ("n_in", c_int),
+                ("in_index", c_void_p), ("in_scale", c_void_p), ("in_shift", c_void_p), ("in_missing", c_void_p),
+                ("H", c_void_p), ("ldh", c_int), ("k0", c_int), ("row_ok", c_void_p)]
+
+
 class LinearArgs(ctypes.Structure):
     _fields_ = [("X", c_void_p), ("n_rows", c_int), ("n_feat", c_int), ("ldx", c_int), ("K", c_int),
                 ("prep", c_void_p), ("W", c_void_p), ("bias", c_void_p), ("simplemax", c_int), ("pad", c_int),
@@ -206,6 +220,8 @@ _ABI = {
     "pmml_tree_hybrid_args_size": HybridArgs,
     "pmml_cluster_args_size": ClusterArgs,
     "pmml_knn_args_size": KnnArgs,
+    "pmml_gemm_args_size": GemmArgs,
+    "pmml_nn_prep_args_size": NnPrepArgs,
     "pmml_linear_args_size": LinearArgs,
     "pmml_mlp_args_size": MlpArgs,
     "pmml_svm_args_size": SvmArgs,
@@ -261,6 +277,10 @@ def load(auto_build: bool = True) -> ctypes.CDLL:
         lib.pmml_cluster_mfma_launch.restype = ctypes.c_int
         lib.pmml_cluster_mfma_launch.argtypes = [c_void_p, ctypes.POINTER(ClusterArgs), c_void_p, c_void_p,
                                                  ctypes.c_int, ctypes.c_int]
+        lib.pmml_gemm_launch.restype = ctypes.c_int
+        lib.pmml_gemm_launch.argtypes = [c_void_p, ctypes.POINTER(GemmArgs), ctypes.c_int]
+        lib.pmml_nn_prep_launch.restype = ctypes.c_int
+        lib.pmml_nn_prep_launch.argtypes = [c_void_p, ctypes.POINTER(NnPrepArgs)]
         lib.pmml_knn_launch.restype = ctypes.c_int
         lib.pmml_knn_launch.argtypes = [c_void_p, ctypes.POINTER(KnnArgs), c_void_p, c_void_p, ctypes.c_int,
                                         ctypes.c_int]

@@ -1,0 +1,310 @@
+// Wide NeuralNetwork layers on the matrix cores: a tiled bf16 MFMA GEMM with the bias, the
+// activation and (for the output layer) the whole PMML output decode fused into its epilogue.
+//
+// The fused MLP kernel (mlp.hip) keeps every activation in registers, which caps a layer at 256
+// units. Beyond that each layer is one launch of this kernel:
+//
+//   H_{l+1}[rows, M] = act(H_l[rows, K] · W_l[K, M] + b_l)      (bf16 in / out, fp32 accumulate)
+//
+// * Block tile 256 rows x BN units (BN = 256 for hidden layers, 32 for the output layer), K staged
+//   in BK = 64 slices through two LDS buffers with direct global->LDS loads
+//   (__builtin_amdgcn_global_load_lds, 16 B per lane): the load of slice k+1 is in flight while
+//   slice k feeds the MFMAs. 512 threads = 8 waves; a hidden-layer wave owns a 128 x 64 sub-tile
+//   (4 x 2 accumulators of v_mfma_f32_32x32x16_bf16).
+// * LDS images are [row][64 k] with the 16-byte chunks XOR-swizzled by (row & 7) — the swizzle is
+//   applied to the per-lane GLOBAL source address (the LDS side of an LDS-DMA is lane-linear), so
+//   the ds_read_b128 fragment reads of 32 consecutive rows hit distinct banks.
+// * Weights are stored unit-major (Wᵀ, [M][K]) so both MFMA operands read 8 consecutive k.
+// * Tile order is XCD-aware: consecutive tiles (the column tiles of one row tile, which share the
+//   A slice) are placed on the same XCD, so the A tile is fetched into one L2 once.
+// * Epilogue (hidden): + bias, activation, bf16, lane pairs merged into 4-byte stores.
+//   Epilogue (output layer): + bias into an LDS row tile, then one thread per row applies the
+//   output activation, softmax / simplemax, label table or regression affine + Target stage and
+//   writes score / valid / probabilities (the zero-copy sink pointers of the pipeline).
+#include "epilogue.h"
+#include "nn_act.h"
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int BM = 256;  // rows per block
+constexpr int BK = 64;   // k per LDS slice (128 B per row)
+constexpr int NT = 512;  // threads (8 waves)
+constexpr int HEAD_LD = 33;
+
+struct GemmArgs {
+  const __bf16* A;        // [rows_p][lda] activations, rows_p = rows rounded up to BM
+  const __bf16* Wt;       // [Mp][ldw] weights, unit-major, Mp a multiple of BN
+  const float* bias;      // [Mp]
+  __bf16* C;              // hidden layer output [rows_p][ldc]
+  int rows, rows_p, K, Mp;  // K: multiple of BK
+  int lda, ldw, ldc, act;
+  float thr;              // threshold activation parameter
+  int n_out, final_norm;  // output layer: real units, 0 none / 1 softmax / 2 simplemax
+  int pad;
+  const uint8_t* row_ok;  // [rows] input-stage validity (output layer)
+  Epilogue epi;           // output layer decode (affine + Target, or label table)
+  float* score;
+  uint8_t* valid;
+  float* probs;
+};
+
+struct PrepArgs {
+  const float* X;
+  int n_rows, rows_p, ldx, n_in;
+  const int* in_index;     // [n_in] active-field column of each network input
+  const float* in_scale;   // [n_in] NormContinuous as an affine map
+  const float* in_shift;
+  const float* in_missing; // [n_in] value for a missing input (NaN: the row has no prediction)
+  __bf16* H;               // [rows_p][ldh]
+  int ldh, k0;             // k0: padded width (zero columns past n_in)
+  uint8_t* row_ok;         // [rows_p]
+};
+
+// Input layer: gather the network inputs, normalise, replace missing, bf16; one thread per row.
+__global__ __launch_bounds__(256) void nn_prep_kernel(PrepArgs a) {
+  const int row = blockIdx.x * 256 + threadIdx.x;
+  if (row >= a.rows_p) return;
+  const bool live = row < a.n_rows;
+  const float* x = a.X + (size_t)(live ? row : 0) * a.ldx;
+  bool ok = live;
+  __bf16* h = a.H + (size_t)row * a.ldh;
+  for (int k0 = 0; k0 < a.k0; k0 += 8) {
+    bf16x8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = k0 + j;
+      float z = 0.f;
+      if (live && k < a.n_in) {
+        const float xv = x[a.in_index[k]];
+        z = xv == xv ? fmaf(xv, a.in_scale[k], a.in_shift[k]) : a.in_missing[k];
+        ok = ok && (z == z);
+        z = z == z ? z : 0.f;
+      }
+      v[j] = (__bf16)z;
+    }
+    *reinterpret_cast<bf16x8*>(h + k0) = v;
+  }
+  a.row_ok[row] = ok ? 1 : 0;
+}
+
+__device__ __forceinline__ void glds16(const void* g, void* lds) {
+  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
+}
+
+// Stage one BK slice of `nrows` rows of a [.][ld] bf16 matrix into a swizzled LDS image.
+// Instruction q of the block covers 1 KiB = 8 rows; lane L lands at byte q*1024 + 16 L.
+template <int NROWS>
+__device__ __forceinline__ void stage_slice(const __bf16* src, int ld, int k0, unsigned char* img, int wave,
+                                            int lane) {
+  constexpr int NINSTR = NROWS / 8;
+  constexpr int PER_WAVE = (NINSTR + 7) / 8;
+#pragma unroll
+  for (int i = 0; i < PER_WAVE; ++i) {
+    const int q = wave * PER_WAVE + i;
+    if (NINSTR % 8 == 0 || q < NINSTR) {
+      const int p = q * 64 + lane;
+      const int r = p >> 3;
+      const int c = (p & 7) ^ (r & 7);
+      glds16(src + (size_t)r * ld + k0 + 8 * c, img + q * 1024);
+    }
+  }
+}
+
+__device__ __forceinline__ bf16x8 frag(const unsigned char* img, int r, int c) {
+  return *reinterpret_cast<const bf16x8*>(img + r * 128 + (((c ^ (r & 7)) & 7) << 4));
+}
+
+__device__ __noinline__ float activate_any(int act, float z, float thr) { return activate(act, z, thr); }
+
+template <int ACT>
+__device__ __forceinline__ float act_of(float z, int act, float thr) {
+  if constexpr (ACT == A_IDENTITY) return z;
+  else if constexpr (ACT == A_RELU) return fmaxf(z, 0.f);
+  else if constexpr (ACT == A_LOGISTIC) return 1.0f / (1.0f + __expf(-z));
+  else if constexpr (ACT == A_TANH) return tanhf(z);
+  else return activate_any(act, z, thr);
+}
+
+// Hidden-layer epilogue: D[row][unit] (unit = lane & 31, row = (reg & 3) + 8 (reg >> 2) + 4 h) +
+// bias, activation, bf16; even lanes store the (unit, unit + 1) pair as one 32-bit word.
+template <int ACT, int TM, int TN>
+__device__ __forceinline__ void store_hidden(const GemmArgs& a, const f32x16 (&acc)[TM][TN], int row0, int col0,
+                                             int wm, int wn, int lane) {
+  const int h = lane >> 5, l32 = lane & 31;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int unit = col0 + (wn * TN + j) * 32 + l32;
+    const float b = a.bias[unit];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int rb = row0 + (wm * TM + i) * 32 + 4 * h;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float v = act_of<ACT>(acc[i][j][r] + b, a.act, a.thr);
+        const float o = __shfl_xor(v, 1);
+        const uint32_t lo = __builtin_bit_cast(uint16_t, (__bf16)v);
+        const uint32_t hi = __builtin_bit_cast(uint16_t, (__bf16)o);
+        if ((lane & 1) == 0) {
+          const int row = rb + (r & 3) + 8 * (r >> 2);
+          *reinterpret_cast<uint32_t*>(a.C + (size_t)row * a.ldc + unit) = lo | (hi << 16);
+        }
+      }
+    }
+  }
+}
+
+template <int BN, bool HEAD>
+__global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmArgs a) {
+  constexpr int WM = BN == 256 ? 2 : 8;  // waves along rows
+  constexpr int WN = 8 / WM;             // waves along units
+  constexpr int TM = BM / WM / 32;       // 32-row accumulator tiles per wave
+  constexpr int TN = BN / WN / 32;       // 32-unit accumulator tiles per wave
+  constexpr int A_BYTES = BM * BK * 2;
+  constexpr int B_BYTES = BN * BK * 2;
+  extern __shared__ __align__(16) unsigned char smem[];
+  unsigned char* As = smem;
+  unsigned char* Bs = smem + 2 * A_BYTES;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, l32 = lane & 31;
+  const int n_ct = a.Mp / BN;
+  const int total = (a.rows_p / BM) * n_ct;
+  int t = blockIdx.x;
+  if ((total & 7) == 0) t = (t & 7) * (total >> 3) + (t >> 3);  // XCD-contiguous tile ranges
+  const int row0 = (t / n_ct) * BM;
+  const int col0 = (t % n_ct) * BN;
+  const int wm = wave / WN, wn = wave % WN;
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x16{};
+
+  const __bf16* Ab = a.A + (size_t)row0 * a.lda;
+  const __bf16* Bb = a.Wt + (size_t)col0 * a.ldw;
+  const int KT = a.K / BK;
+  stage_slice<BM>(Ab, a.lda, 0, As, wave, lane);
+  stage_slice<BN>(Bb, a.ldw, 0, Bs, wave, lane);
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  for (int kt = 0; kt < KT; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < KT) {  // next slice in flight while this one computes
+      stage_slice<BM>(Ab, a.lda, (kt + 1) * BK, As + (cur ^ 1) * A_BYTES, wave, lane);
+      stage_slice<BN>(Bb, a.ldw, (kt + 1) * BK, Bs + (cur ^ 1) * B_BYTES, wave, lane);
+    }
+    const unsigned char* ai = As + cur * A_BYTES;
+    const unsigned char* bi = Bs + cur * B_BYTES;
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = frag(ai, (wm * TM + i) * 32 + l32, 2 * ks + h);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j] = frag(bi, (wn * TN + j) * 32 + l32, 2 * ks + h);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    __builtin_amdgcn_s_waitcnt(0);  // the slice in flight has landed (LDS-DMA retires on vmcnt)
+    __syncthreads();                // ... for every wave before anyone reads / overwrites it
+  }
+
+  if constexpr (!HEAD) {
+    switch (a.act) {  // uniform: one unrolled epilogue per common activation
+      case A_IDENTITY: store_hidden<A_IDENTITY, TM, TN>(a, acc, row0, col0, wm, wn, lane); break;
+      case A_RELU: store_hidden<A_RELU, TM, TN>(a, acc, row0, col0, wm, wn, lane); break;
+      case A_LOGISTIC: store_hidden<A_LOGISTIC, TM, TN>(a, acc, row0, col0, wm, wn, lane); break;
+      case A_TANH: store_hidden<A_TANH, TM, TN>(a, acc, row0, col0, wm, wn, lane); break;
+      default: store_hidden<-1, TM, TN>(a, acc, row0, col0, wm, wn, lane); break;
+    }
+  } else {
+    float* zt = reinterpret_cast<float*>(smem);  // [BM][HEAD_LD] (the staging buffers are drained)
+    const int unit = l32;
+    const float b = unit < a.n_out ? a.bias[unit] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int rl = (wm * TM) * 32 + 4 * h + (r & 3) + 8 * (r >> 2);
+      zt[rl * HEAD_LD + unit] = activate(a.act, acc[0][0][r] + b, a.thr);
+    }
+    __syncthreads();
+    if (tid < BM) {
+      const int row = row0 + tid;
+      if (row < a.rows) {
+        const float* z = zt + tid * HEAD_LD;
+        const bool bad = !a.row_ok[row];
+        if (a.final_norm == 0 && a.n_out == 1) {
+          apply_epilogue(a.epi, [&](int) { return z[0]; }, !bad, row, a.rows, a.score, a.valid, a.probs);
+        } else {
+          float mx = -__builtin_inff();
+          for (int u = 0; u < a.n_out; ++u) mx = fmaxf(mx, z[u]);
+          float sum = 0.f;
+          for (int u = 0; u < a.n_out; ++u) sum += (a.final_norm == 1) ? __expf(z[u] - mx) : z[u];
+          float best = -__builtin_inff();
+          int best_u = 1 << 30;
+          for (int u = 0; u < a.n_out; ++u) {
+            float p = (a.final_norm == 1) ? __expf(z[u] - mx) : z[u];
+            if (a.final_norm != 0) p /= sum;
+            if (p > best || (p == best && u < best_u)) { best = p; best_u = u; }
+            if (a.probs) a.probs[(size_t)row * a.n_out + u] = p;
+          }
+          bool ok = !bad && best == best && best_u < a.n_out;
+          float sc = ok ? (a.epi.has_table ? a.epi.table[best_u] : (float)best_u) : __builtin_nanf("");
+          ok = ok && (sc == sc);
+          a.score[row] = ok ? sc : __builtin_nanf("");
+          a.valid[row] = ok ? 1 : 0;
+          if (a.epi.score2) {
+            a.epi.score2[row] = ok ? sc : __builtin_nanf("");
+            a.epi.valid2[row] = ok ? 1 : 0;
+          }
+        }
+      }
+    }
+  }
+}
+
+template <int BN, bool HEAD>
+int launch(hipStream_t stream, const GemmArgs& a) {
+  const size_t stage = 2 * (size_t)BM * BK * 2 + 2 * (size_t)BN * BK * 2;
+  const size_t head = HEAD ? (size_t)BM * HEAD_LD * 4 : 0;
+  const size_t lds = stage > head ? stage : head;
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_kernel<BN, HEAD>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return -5;
+  dim3 grid((a.rows_p / BM) * (a.Mp / BN));
+  hipLaunchKernelGGL((gemm_kernel<BN, HEAD>), grid, dim3(NT), lds, stream, a);
+  return 0;
+}
+
+}  // namespace
+
+PMML_API int pmml_gemm_args_size() { return (int)sizeof(GemmArgs); }
+PMML_API int pmml_nn_prep_args_size() { return (int)sizeof(PrepArgs); }
+
+PMML_API int pmml_nn_prep_launch(hipStream_t stream, const PrepArgs* args) {
+  const PrepArgs a = *args;
+  if (a.rows_p <= 0) return 0;
+  if ((a.k0 & 7) || a.k0 < a.n_in || (a.ldh & 7) || (reinterpret_cast<uintptr_t>(a.H) & 15)) return -4;
+  hipLaunchKernelGGL(nn_prep_kernel, dim3((a.rows_p + 255) / 256), dim3(256), 0, stream, a);
+  return hipGetLastError() == hipSuccess ? 0 : -7;
+}
+
+// head = 0: hidden layer (BN 256, bf16 output C); head = 1: output layer (BN 32, n_out <= 32, decode).
+PMML_API int pmml_gemm_launch(hipStream_t stream, const GemmArgs* args, int head) {
+  const GemmArgs a = *args;
+  if (a.rows <= 0) return 0;
+  const int BN = head ? 32 : 256;
+  if (a.rows_p % BM || a.rows_p < a.rows || a.K % BK || a.K <= 0 || a.Mp % BN || a.Mp <= 0) return -4;
+  if ((a.lda & 7) || (a.ldw & 7) || a.lda < a.K || a.ldw < a.K) return -4;
+  if ((reinterpret_cast<uintptr_t>(a.A) & 15) || (reinterpret_cast<uintptr_t>(a.Wt) & 15)) return -4;
+  if (head && (a.n_out < 1 || a.n_out > 32 || a.Mp != 32 || !a.row_ok || !a.score || !a.valid)) return -4;
+  if (!head && ((a.ldc & 1) || a.ldc < a.Mp || !a.C)) return -4;
+  const int rc = head ? launch<32, true>(stream, a) : launch<256, false>(stream, a);
+  if (rc) return rc;
+  return hipGetLastError() == hipSuccess ? 0 : -7;
+}

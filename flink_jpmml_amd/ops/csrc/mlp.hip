@@ -25,6 +25,7 @@
 // Input normalisation (NormContinuous as scale/shift), missing handling, activations, output-layer
 // normalisation (softmax / simplemax) and the target decode are fused.
 #include "epilogue.h"
+#include "nn_act.h"
 
 namespace {
 
@@ -36,8 +37,6 @@ constexpr int MAXL = 8;        // max layers (biases staged in LDS)
 constexpr int KMAX = 256;      // max inputs per layer
 constexpr int NSLOT = 4;       // LDS panel ring slots
 
-enum : int { A_IDENTITY = 0, A_LOGISTIC = 1, A_TANH = 2, A_RELU = 3, A_EXP = 4, A_RECIP = 5, A_SQUARE = 6,
-             A_GAUSS = 7, A_SINE = 8, A_COSINE = 9, A_ELLIOTT = 10, A_ARCTAN = 11, A_THRESHOLD = 12 };
 
 struct LayerMeta {
   int kp;      // padded K (inputs), multiple of 16 (bf16) / 2 (f32)
@@ -75,23 +74,6 @@ struct MlpArgs {
   int pad_;
 };
 
-__device__ __forceinline__ float activate(int a, float z, float thr) {
-  switch (a) {
-    case A_LOGISTIC: return 1.0f / (1.0f + __expf(-z));
-    case A_TANH: return tanhf(z);
-    case A_RELU: return fmaxf(z, 0.0f);
-    case A_EXP: return __expf(z);
-    case A_RECIP: return 1.0f / z;
-    case A_SQUARE: return z * z;
-    case A_GAUSS: return __expf(-z * z);
-    case A_SINE: return __sinf(z);
-    case A_COSINE: return __cosf(z);
-    case A_ELLIOTT: return z / (1.0f + fabsf(z));
-    case A_ARCTAN: return 0.63661977236758134f * atanf(z);
-    case A_THRESHOLD: return z > thr ? 1.0f : 0.0f;
-    default: return z;
-  }
-}
 
 // row (unit) index inside a 32x32 accumulator tile held by register r of lane half h
 __device__ __forceinline__ int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }

@@ -346,6 +346,105 @@ class GemmMlpPlan(MlpPlan):
                     vo.copy_(ok.to(torch.uint8))
 
 
+def _ceil(x: int, m: int) -> int:
+    return -(-x // m) * m
+
+
+class WideMlpPlan(MlpPlan):
+    """NeuralNetworks beyond the fused kernel (layers wider than 256 units, more than 8 layers or
+    256 inputs) on ``gemm.hip``: an input-stage kernel (gather, NormContinuous, missing values,
+    bf16), then ONE fused MFMA GEMM launch per layer — bias and activation in the epilogue,
+    bf16 activations ping-pong through HBM — and an output-layer GEMM whose epilogue does the
+    whole decode (output activation, softmax / simplemax, label table or affine + Target) into
+    the score / valid / probability sinks. bf16 operands, fp32 accumulation."""
+
+    kind = "mlp_wide"
+    supports_direct = True
+    _STATE = DevicePlan._STATE + ("in_scale", "in_shift", "in_missing", "in_index", "n_in", "out_a", "out_b",
+                                  "final_norm", "n_out", "table", "is_classification", "target_stage", "wts", "bss",
+                                  "dims", "k0", "bf16")
+    ROWS = 256  # GEMM block rows (mirrors csrc/gemm.hip BM)
+
+    def __init__(self, compiled, device, precision: str = "bf16"):
+        import torch
+
+        DevicePlan.__init__(self, compiled, device)
+        ev: NeuralEvaluator = compiled.evaluator
+        if precision != "bf16":
+            raise NotLowerable("the wide-layer GEMM runs bf16 operands (precision policy bf16 / fp8)")
+        self.bf16 = 1
+        layers, _ = self._io(compiled, ev)
+        if self.n_out > 32:
+            raise NotLowerable("more than 32 output neurons")
+        self.k0 = _ceil(max(self.n_in, 1), 64)
+        wts, bss, dims = [], [], []
+        wo = bo = 0
+        kp = self.k0
+        for li, (W, b, act, thr, _) in enumerate(layers):
+            k, m = W.shape
+            head = li == len(layers) - 1
+            mp = 32 if head else _ceil(m, 256)
+            Wt = np.zeros((mp, kp), dtype=np.float32)
+            Wt[:m, :k] = np.asarray(W, np.float32).T
+            bias = np.zeros(mp, dtype=np.float32)
+            bias[:m] = b
+            wts.append(Wt.reshape(-1))
+            bss.append(bias)
+            dims.append((kp, mp, ACT_CODES[act], float(thr), wo, bo))
+            wo += Wt.size
+            bo += mp
+            kp = mp
+        self.wts = torch.from_numpy(np.concatenate(wts)).to(torch.bfloat16).to(self.device)
+        self.bss = self._t(np.concatenate(bss))
+        self.dims = dims
+
+    def launch(self, X, score, valid, stream=None, probs=None, score2=None, valid2=None) -> None:
+        import ctypes
+
+        import torch
+
+        from ..ops._lib import GemmArgs, NnPrepArgs, check, ptr, stream_handle
+
+        n = X.shape[0]
+        if n == 0:
+            return
+        rows_p = _ceil(n, self.ROWS)
+        st = stream if stream is not None else torch.cuda.current_stream(self.device)
+        h = stream_handle(st)
+        with torch.cuda.stream(st):
+            widest = max(mp for _, mp, *_ in self.dims[:-1]) if len(self.dims) > 1 else 0
+            H0 = torch.empty((rows_p, self.k0), dtype=torch.bfloat16, device=self.device)
+            bufs = [torch.empty((rows_p, widest), dtype=torch.bfloat16, device=self.device) for _ in range(2)] \
+                if widest else []
+            ok = torch.empty(rows_p, dtype=torch.uint8, device=self.device)
+        p = NnPrepArgs()
+        p.X, p.n_rows, p.rows_p, p.ldx, p.n_in = X.data_ptr(), n, rows_p, X.stride(0), self.n_in
+        p.in_index, p.in_scale, p.in_shift = ptr(self.in_index), ptr(self.in_scale), ptr(self.in_shift)
+        p.in_missing, p.H, p.ldh, p.k0, p.row_ok = ptr(self.in_missing), H0.data_ptr(), self.k0, self.k0, ok.data_ptr()
+        check(self.lib.pmml_nn_prep_launch(h, ctypes.byref(p)), "nn input stage")
+        wbase, bbase = self.wts.data_ptr(), self.bss.data_ptr()
+        cur, lda = H0, self.k0
+        for li, (kp, mp, act, thr, wo, bo) in enumerate(self.dims):
+            head = li == len(self.dims) - 1
+            a = GemmArgs()
+            a.A, a.Wt, a.bias = cur.data_ptr(), wbase + 2 * wo, bbase + 4 * bo
+            a.rows, a.rows_p, a.K, a.Mp = n, rows_p, kp, mp
+            a.lda, a.ldw, a.act, a.thr = lda, kp, act, thr
+            if head:
+                a.n_out, a.final_norm, a.row_ok = self.n_out, self.final_norm, ok.data_ptr()
+                a.epi = _epilogue(mode=EPI_AFFINE, a=self.out_a, b=self.out_b, table=self.table, tgt=self.target_stage)
+                a.epi.score2, a.epi.valid2 = _addr(score2), _addr(valid2)
+                a.score, a.valid, a.probs = _addr(score), _addr(valid), ptr(probs)
+                check(self.lib.pmml_gemm_launch(h, ctypes.byref(a), 1), "nn output-layer gemm")
+            else:
+                out = bufs[li & 1]
+                a.C, a.ldc = out.data_ptr(), out.stride(0)
+                check(self.lib.pmml_gemm_launch(h, ctypes.byref(a), 0), "nn layer gemm")
+                cur, lda = out, out.stride(0)
+        for t in [H0, ok] + bufs:  # freed by the caching allocator only after this stream's work
+            t.record_stream(st)
+
+
 class SvmPlan(DevicePlan):
     """SupportVectorMachineModel on the fused kernel-evaluation + vote kernel (fp32)."""
 

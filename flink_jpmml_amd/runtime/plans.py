@@ -1688,19 +1688,23 @@ def compile_plan(compiled, device, **opts) -> DevicePlan:
     from ..models.svm import SvmEvaluator
 
     if isinstance(ev, NeuralEvaluator):
-        from .nn_plans import GemmMlpPlan, MlpPlan
+        from .nn_plans import GemmMlpPlan, MlpPlan, WideMlpPlan
 
         prec = "fp32" if policy == "fp32" else "bf16"
-        impl = opts.pop("mlp_impl", "auto")  # auto | fused | gemm
-        if impl not in ("auto", "fused", "gemm"):
-            raise ValueError("mlp_impl must be auto, fused or gemm")
+        impl = opts.pop("mlp_impl", "auto")  # auto | fused | wide | gemm
+        if impl not in ("auto", "fused", "wide", "gemm"):
+            raise ValueError("mlp_impl must be auto, fused, wide or gemm")
         if impl == "gemm":
             return GemmMlpPlan(compiled, device, precision=prec)
+        if impl == "wide":
+            return WideMlpPlan(compiled, device, precision="bf16")
         try:
             return MlpPlan(compiled, device, precision=prec, **opts)
         except NotLowerable as e:
             if "fused kernel" not in str(e) or impl == "fused":
                 raise
+            if prec == "bf16":  # wide layers: one fused MFMA GEMM launch per layer (ops/csrc/gemm.hip)
+                return WideMlpPlan(compiled, device, precision=prec)
             return GemmMlpPlan(compiled, device, precision=prec)
     if isinstance(ev, SvmEvaluator):
         from .nn_plans import SvmGemmPlan, SvmPlan

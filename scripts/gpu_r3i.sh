@@ -1,6 +1,6 @@
 set -o pipefail
 mkdir -p gpurun_out/r3i
-timeout -k 10 500 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_hybrid.py tests/test_gpu_segmented.py tests/test_design.py tests/test_math_context.py -x -q --timeout 200 --timeout-method thread > gpurun_out/r3i/pytest.log 2>&1 || { tail -40 gpurun_out/r3i/pytest.log; exit 1; }
+timeout -k 10 500 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_hybrid.py tests/test_gpu_segmented.py tests/test_design.py tests/test_math_context.py tests/test_gpu_surface.py -x -q --timeout 200 --timeout-method thread > gpurun_out/r3i/pytest.log 2>&1 || { tail -40 gpurun_out/r3i/pytest.log; exit 1; }
 tail -1 gpurun_out/r3i/pytest.log
 for M in gbdt rf; do
   for S in lockstep refill; do

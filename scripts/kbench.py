@@ -35,6 +35,8 @@ def main():
     p.add_argument("--precision", default="fp32", choices=["fp32", "bf16", "fp8"])
     p.add_argument("--hidden", default="256,256", help="mlp hidden widths")
     p.add_argument("--mlp-kernel", default="auto", choices=["auto", "reg", "panel"], help="bf16 MLP kernel")
+    p.add_argument("--mlp-impl", default="auto", choices=["auto", "fused", "wide", "gemm"],
+                   help="MLP plan: fused kernel, wide-layer MFMA GEMM, or library GEMM")
     args = p.parse_args()
     import numpy as np
     import torch
@@ -86,8 +88,10 @@ def main():
         opts = dict(cluster_variant=args.variant)
     if args.precision != "fp32":
         opts["precision"] = args.precision
+    if args.model == "mlp" and args.mlp_impl != "auto":
+        opts["mlp_impl"] = args.mlp_impl
     plan = c.plan("cuda:0", **opts)
-    if args.model == "mlp" and args.mlp_kernel != "auto":
+    if args.model == "mlp" and args.mlp_kernel != "auto" and hasattr(plan, "set_kernel"):
         plan.set_kernel(args.mlp_kernel)
     F = c.n_features
     X = torch.from_numpy(synth.stream_matrix(args.rows, F, seed=1, missing_rate=args.missing)).cuda()

@@ -1,0 +1,110 @@
+"""Wide NeuralNetworks on the fused MFMA GEMM (``ops/csrc/gemm.hip``, ``WideMlpPlan``).
+
+CPU: the plan's packed operands (unit-major bf16 weights padded to the kernel tiles, fp32 biases,
+the input stage) run through a numpy model of the kernels' arithmetic — bf16 operands, fp32
+accumulation, bf16 activations between layers — and must reproduce the float64 oracle within bf16
+tolerance. GPU: the kernels against the same model (tight) and the oracle (bf16 tolerance)."""
+
+import numpy as np
+import pytest
+import torch
+
+from flink_jpmml_amd.bench.synth import mlp_pmml, stream_matrix
+from flink_jpmml_amd.runtime.compiled import CompiledPmml
+
+SHAPES = [
+    dict(n_features=32, hidden=(1024,), n_out=1, activation="rectifier"),
+    dict(n_features=40, hidden=(300, 1024), n_out=1, activation="logistic"),
+    dict(n_features=21, hidden=(512,), n_out=5, activation="tanh", classification=True),
+    dict(n_features=16, hidden=(64,) * 9, n_out=1, activation="rectifier"),
+]
+_ACT = {0: lambda z: z, 1: lambda z: 1 / (1 + np.exp(-z)), 2: np.tanh, 3: lambda z: np.maximum(z, 0)}
+
+
+def _bf16(x):
+    return torch.from_numpy(np.ascontiguousarray(x, np.float32)).to(torch.bfloat16).float().numpy()
+
+
+def emulate_wide(plan, X):
+    """numpy model of nn_prep_kernel + gemm_kernel (hidden + output layer decode)."""
+    X = np.asarray(X, np.float32)
+    idx = plan.in_index.cpu().numpy()
+    x = X[:, idx]
+    sc, sh, ms = (t.cpu().numpy() for t in (plan.in_scale, plan.in_shift, plan.in_missing))
+    z = np.where(np.isnan(x), ms, x * sc + sh)
+    ok = ~np.isnan(z).any(axis=1)
+    H = np.zeros((len(X), plan.k0), np.float32)
+    H[:, : plan.n_in] = np.nan_to_num(z)
+    H = _bf16(H)
+    W = plan.wts.float().cpu().numpy()
+    B = plan.bss.cpu().numpy()
+    for li, (kp, mp, act, thr, wo, bo) in enumerate(plan.dims):
+        Wt = W[wo: wo + mp * kp].reshape(mp, kp)
+        Z = (H[:, :kp].astype(np.float64) @ Wt.T.astype(np.float64)).astype(np.float32) + B[bo: bo + mp]
+        Z = _ACT[act](Z).astype(np.float32)
+        H = _bf16(Z) if li < len(plan.dims) - 1 else Z
+    out = H[:, : plan.n_out]
+    if plan.is_classification:
+        P = np.exp(out - out.max(1, keepdims=True)) if plan.final_norm == 1 else out
+        if plan.final_norm:
+            P = P / P.sum(1, keepdims=True)
+        lab = P.argmax(1)
+        s = plan.table.cpu().numpy()[lab].astype(np.float64)
+    else:
+        s = plan.out_a * out[:, 0].astype(np.float64) + plan.out_b
+    return np.where(ok, s, np.nan), ok
+
+
+@pytest.mark.parametrize("shape", SHAPES, ids=lambda d: "x".join(map(str, d["hidden"])))
+def test_wide_plan_packing_matches_oracle(shape):
+    from flink_jpmml_amd.runtime.nn_plans import WideMlpPlan
+    from flink_jpmml_amd.runtime.plans import compile_plan, lowering_dry_run
+
+    c = CompiledPmml.from_string(mlp_pmml(seed=5, **shape))
+    with lowering_dry_run():
+        plan = compile_plan(c, torch.device("cpu"), precision="bf16")
+    assert isinstance(plan, WideMlpPlan)
+    assert all(kp % 64 == 0 and mp % (32 if i == len(plan.dims) - 1 else 256) == 0
+               for i, (kp, mp, *_) in enumerate(plan.dims))
+    X = stream_matrix(3000, shape["n_features"], seed=2, missing_rate=0.01)
+    s, v = emulate_wide(plan, X)
+    ref, vref = c.score_matrix_oracle(X)
+    assert (v == vref).all()
+    if shape.get("classification"):
+        assert (s[v] == ref[v]).mean() > 0.98
+    else:
+        scale = max(1.0, float(np.abs(ref[v]).max()))
+        assert np.abs(s[v] - ref[v]).max() < 3e-2 * scale
+
+
+def test_fp32_policy_keeps_library_gemm():
+    """fp32 precision policy: wide layers stay fp32 (library GEMM); bf16 operands are opt-in."""
+    from flink_jpmml_amd.runtime.nn_plans import GemmMlpPlan
+    from flink_jpmml_amd.runtime.plans import compile_plan, lowering_dry_run
+
+    c = CompiledPmml.from_string(mlp_pmml(n_features=32, hidden=(1024,), seed=1))
+    with lowering_dry_run():
+        assert isinstance(compile_plan(c, torch.device("cpu")), GemmMlpPlan)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", SHAPES, ids=lambda d: "x".join(map(str, d["hidden"])))
+def test_wide_gemm_kernels_on_gpu(gpu, shape):
+    from flink_jpmml_amd.runtime.nn_plans import WideMlpPlan
+
+    c = CompiledPmml.from_string(mlp_pmml(seed=5, **shape))
+    plan = c.plan(gpu, precision="bf16")
+    assert isinstance(plan, WideMlpPlan)
+    X = stream_matrix(10_001, shape["n_features"], seed=3, missing_rate=0.01)  # not a multiple of 256
+    s, v = plan.score(X)
+    s, v = s.cpu().numpy(), v.cpu().numpy()
+    es, ev = emulate_wide(plan, X)
+    ref, vref = c.score_matrix_oracle(X)
+    assert (v == ev).all() and (v == vref).all()
+    if shape.get("classification"):
+        assert (s[v] == es[v]).mean() > 0.995
+        assert (s[v] == ref[v]).mean() > 0.98
+    else:
+        scale = max(1.0, float(np.abs(ref[v]).max()))
+        assert np.abs(s[v] - es[v]).max() < 5e-3 * scale  # same bf16 operands: summation order only
+        assert np.abs(s[v] - ref[v]).max() < 3e-2 * scale
