@@ -18,6 +18,7 @@
 // * Tile order is XCD-aware: consecutive tiles (the column tiles of one row tile, which share the
 //   A slice) are placed on the same XCD, so the A tile is fetched into one L2 once.
 // * Epilogue (hidden): + bias, activation, bf16, lane pairs merged into 4-byte stores.
+// * The input stage is its own small kernel: one lane per (row, 8 inputs), validity by ballot.
 //   Epilogue (output layer): + bias into an LDS row tile, then one thread per row applies the
 //   output activation, softmax / simplemax, label table or regression affine + Target stage and
 //   writes score / valid / probabilities (the zero-copy sink pointers of the pipeline).
@@ -63,31 +64,41 @@ struct PrepArgs {
   uint8_t* row_ok;         // [rows_p]
 };
 
-// Input layer: gather the network inputs, normalise, replace missing, bf16; one thread per row.
-__global__ __launch_bounds__(256) void nn_prep_kernel(PrepArgs a) {
-  const int row = blockIdx.x * 256 + threadIdx.x;
-  if (row >= a.rows_p) return;
-  const bool live = row < a.n_rows;
-  const float* x = a.X + (size_t)(live ? row : 0) * a.ldx;
-  bool ok = live;
-  __bf16* h = a.H + (size_t)row * a.ldh;
-  for (int k0 = 0; k0 < a.k0; k0 += 8) {
+// Input layer: gather the network inputs, normalise, replace missing, bf16. One thread per
+// (row, 8-input chunk) — a row's chunks are GP consecutive lanes (GP = chunks rounded up to a
+// power of two <= 64), so its reads and its 16-byte stores are contiguous, and the row's validity
+// is the AND over its lane group (one wave ballot).
+__global__ __launch_bounds__(256) void nn_prep_kernel(PrepArgs a, int gp_log2) {
+  const int GP = 1 << gp_log2;
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  const int row = t >> gp_log2;
+  const int chunk = t & (GP - 1);
+  const int nchunk = a.k0 >> 3;
+  const bool live_row = row < a.n_rows;
+  const bool active = row < a.rows_p && chunk < nchunk;
+  bool bad = false;
+  if (active) {
+    const float* x = a.X + (size_t)(live_row ? row : 0) * a.ldx;
     bf16x8 v;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int k = k0 + j;
+      const int k = chunk * 8 + j;
       float z = 0.f;
-      if (live && k < a.n_in) {
+      if (live_row && k < a.n_in) {
         const float xv = x[a.in_index[k]];
         z = xv == xv ? fmaf(xv, a.in_scale[k], a.in_shift[k]) : a.in_missing[k];
-        ok = ok && (z == z);
+        bad = bad || (z != z);
         z = z == z ? z : 0.f;
       }
       v[j] = (__bf16)z;
     }
-    *reinterpret_cast<bf16x8*>(h + k0) = v;
+    *reinterpret_cast<bf16x8*>(a.H + (size_t)row * a.ldh + chunk * 8) = v;
   }
-  a.row_ok[row] = ok ? 1 : 0;
+  const unsigned long long m = __ballot(bad);
+  const int lane = threadIdx.x & 63;
+  const int g0 = lane & ~(GP - 1);
+  const unsigned long long grp = GP == 64 ? ~0ull : ((1ull << GP) - 1) << g0;
+  if (active && chunk == 0) a.row_ok[row] = (live_row && (m & grp) == 0) ? 1 : 0;
 }
 
 __device__ __forceinline__ void glds16(const void* g, void* lds) {
@@ -129,7 +140,11 @@ __device__ __forceinline__ float act_of(float z, int act, float thr) {
 }
 
 // Hidden-layer epilogue: D[row][unit] (unit = lane & 31, row = (reg & 3) + 8 (reg >> 2) + 4 h) +
-// bias, activation, bf16; even lanes store the (unit, unit + 1) pair as one 32-bit word.
+// bias, activation, bf16; even lanes store the (unit, unit + 1) pair as one 32-bit word, straight
+// from the registers. (Staging the 256 x 256 tile through LDS for full-row 16-byte stores was
+// measured SLOWER — 3.02 vs 2.62 ms for a 1024 x 1024 layer over 1M rows, profiles/r3l: with one
+// workgroup per CU the block-wide barrier exposes the whole store phase, while direct stores
+// drain behind the other waves' MFMAs.)
 template <int ACT, int TM, int TN>
 __device__ __forceinline__ void store_hidden(const GemmArgs& a, const f32x16 (&acc)[TM][TN], int row0, int col0,
                                              int wm, int wn, int lane) {
@@ -289,8 +304,12 @@ PMML_API int pmml_nn_prep_args_size() { return (int)sizeof(PrepArgs); }
 PMML_API int pmml_nn_prep_launch(hipStream_t stream, const PrepArgs* args) {
   const PrepArgs a = *args;
   if (a.rows_p <= 0) return 0;
-  if ((a.k0 & 7) || a.k0 < a.n_in || (a.ldh & 7) || (reinterpret_cast<uintptr_t>(a.H) & 15)) return -4;
-  hipLaunchKernelGGL(nn_prep_kernel, dim3((a.rows_p + 255) / 256), dim3(256), 0, stream, a);
+  if ((a.k0 & 7) || a.k0 < a.n_in || a.k0 > 512 || (a.ldh & 7) || (reinterpret_cast<uintptr_t>(a.H) & 15))
+    return -4;
+  int g = 0;
+  while ((1 << g) < (a.k0 >> 3)) ++g;  // lanes per row: chunks rounded up to a power of two (<= 64)
+  const long long threads = (long long)a.rows_p << g;
+  hipLaunchKernelGGL(nn_prep_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, stream, a, g);
   return hipGetLastError() == hipSuccess ? 0 : -7;
 }
 
@@ -303,7 +322,7 @@ PMML_API int pmml_gemm_launch(hipStream_t stream, const GemmArgs* args, int head
   if ((a.lda & 7) || (a.ldw & 7) || a.lda < a.K || a.ldw < a.K) return -4;
   if ((reinterpret_cast<uintptr_t>(a.A) & 15) || (reinterpret_cast<uintptr_t>(a.Wt) & 15)) return -4;
   if (head && (a.n_out < 1 || a.n_out > 32 || a.Mp != 32 || !a.row_ok || !a.score || !a.valid)) return -4;
-  if (!head && ((a.ldc & 1) || a.ldc < a.Mp || !a.C)) return -4;
+  if (!head && ((a.ldc & 7) || a.ldc < a.Mp || !a.C || (reinterpret_cast<uintptr_t>(a.C) & 15))) return -4;
   const int rc = head ? launch<32, true>(stream, a) : launch<256, false>(stream, a);
   if (rc) return rc;
   return hipGetLastError() == hipSuccess ? 0 : -7;

@@ -30,10 +30,18 @@ def head_words(H: int) -> int:
     return (w + 3) // 4 * 4
 
 
-def pack_trees(trees, weights: List[float], P: int, H: int, feat_lds: bool
+def pack_trees(trees, weights: List[float], P: int, H: int, feat_lds: bool, order: str = "bfs"
                ) -> Tuple[Optional[np.ndarray], np.ndarray, np.ndarray, np.ndarray, bool]:
     """``(heads [n_trees, head_words] u32 or None when H == 0, tail nodes [n, 4] u32,
-    leaves [n_leaves, P] f32, root codes [n_trees] i32, has_default_right)``."""
+    leaves [n_leaves, P] f32, root codes [n_trees] i32, has_default_right)``.
+
+    ``order``: node / leaf order inside a tree. ``"bfs"`` (default) stores the tree level by level
+    with the two children of every node adjacent: the lock-step walk moves all lanes of a wave
+    through the same level of the same tree together, so their loads share cache lines (the
+    top levels of a tree sit in a few lines; a node's two children always share one). ``"dfs"``:
+    the lowered tree's own (preorder) order."""
+    if order not in ("bfs", "dfs"):
+        raise ValueError("order must be 'bfs' or 'dfs'")
     from .plans import _canonical_vec
 
     NI, NL = (1 << H) - 1, 1 << H
@@ -64,6 +72,9 @@ def pack_trees(trees, weights: List[float], P: int, H: int, feat_lds: bool
         lvl = np.full(n, -1, dtype=np.int64)
         heap = np.full(n, -1, dtype=np.int64)
         lvl[0], heap[0] = 0, 0
+        rank = np.arange(n, dtype=np.int64)  # storage order key ("dfs": the lowered order)
+        if order == "bfs":
+            rank[0], seen = 0, 1
         frontier = np.array([0], dtype=np.int64)
         L = 0
         while frontier.size:
@@ -75,22 +86,31 @@ def pack_trees(trees, weights: List[float], P: int, H: int, feat_lds: bool
             if L + 1 <= H:
                 heap[a] = 2 * heap[fi] + 1
                 heap[b] = 2 * heap[fi] + 2
-            frontier = np.concatenate([a, b])
+            frontier = np.stack([a, b], axis=1).reshape(-1)  # siblings adjacent
+            if order == "bfs":
+                rank[frontier] = seen + np.arange(frontier.size)
+                seen += frontier.size
             L += 1
         is_leaf = ~internal
-        leaf_rank = np.cumsum(is_leaf) - 1
         tail_mask = internal & (lvl >= H)
-        tail_rank = np.cumsum(tail_mask) - 1
+        leaf_rank = np.zeros(n, dtype=np.int64)
+        tail_rank = np.zeros(n, dtype=np.int64)
+        lk_sorted = np.nonzero(is_leaf)[0]
+        lk_sorted = lk_sorted[np.argsort(rank[lk_sorted], kind="stable")]
+        leaf_rank[lk_sorted] = np.arange(lk_sorted.size)
+        tk_sorted = np.nonzero(tail_mask)[0]
+        tk_sorted = tk_sorted[np.argsort(rank[tk_sorted], kind="stable")]
+        tail_rank[tk_sorted] = np.arange(tk_sorted.size)
         code = np.where(is_leaf, ~(n_leaf + leaf_rank), n_tail + tail_rank).astype(np.int64)
-        # leaves (node order), weighted payloads
-        lk = np.nonzero(is_leaf)[0]
+        # leaves (storage order), weighted payloads
+        lk = lk_sorted
         if t.leaf_probs is not None and P > 1:
             vals = np.asarray(t.leaf_probs, dtype=np.float64)[lk, :P] * w
         else:
             vals = np.asarray(t.leaf_value, dtype=np.float64)[lk, None] * w
         leaves.append(vals)
-        # tail nodes
-        tk = np.nonzero(tail_mask)[0]
+        # tail nodes (storage order)
+        tk = tk_sorted
         if tk.size:
             nd = np.empty((tk.size, 4), dtype=np.uint32)
             nd[:, 0] = T[tk].view(np.uint32)

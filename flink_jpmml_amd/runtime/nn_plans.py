@@ -377,6 +377,8 @@ class WideMlpPlan(MlpPlan):
         if self.n_out > 32:
             raise NotLowerable("more than 32 output neurons")
         self.k0 = _ceil(max(self.n_in, 1), 64)
+        if self.k0 > 512:
+            raise NotLowerable("more than 512 network inputs (wide-layer input stage)")
         wts, bss, dims = [], [], []
         wo = bo = 0
         kp = self.k0

@@ -1211,10 +1211,13 @@ class TreePlan(DevicePlan):
     def __init__(self, compiled, device, layout: str = "auto", lds_budget: int = 80 * 1024, splits: int = 0,
                  variant: str = "auto", precision: str = "fp32", nan_mode: str = "auto", max_chunk_trees: int = 0,
                  tree_shard: Optional[Tuple[int, int]] = None, head_depth: int = 0,
-                 pointer_schedule: str = "refill"):
-        """``pointer_schedule`` (pointer layout): ``"refill"`` (each walk slot restarts on the next
-        tree the step its walk ends; leaves summed in completion order) or ``"lockstep"`` (groups
-        of walks run to the deepest one; tree-order sums).
+                 pointer_schedule: str = "lockstep", node_order: str = "bfs"):
+        """``pointer_schedule`` (pointer layout): ``"lockstep"`` (default: groups of walks run to the
+        deepest one; tree-order sums) or ``"refill"`` (each walk slot restarts on the next tree the
+        step its walk ends). Measured (profiles/r3j): refill is 2.3-2.6x SLOWER at depth 14 — lanes
+        drift onto different trees and every load instruction touches up to 64 distinct lines,
+        while lock-step lanes share the lines of the same tree level. ``node_order``: pointer-node
+        storage order (``"bfs"``: level by level, siblings adjacent; ``"dfs"``: preorder).
 
         ``nan_mode`` (wide PERFECT kernel): ``"auto"`` keeps tiles with missing values on the fast
         traversal whenever the ensemble has no null-on-missing trees (default-right nodes read a
@@ -1427,7 +1430,8 @@ class TreePlan(DevicePlan):
             else:
                 self.chunk_trees = 0
             if heads is None:
-                _, nodes, leaves, roots, has_dr = pack_trees(spec.trees, spec.weights, spec.P, 0, feat_lds)
+                _, nodes, leaves, roots, has_dr = pack_trees(spec.trees, spec.weights, spec.P, 0, feat_lds,
+                                                             order=node_order)
             self.blob_nan, self.chunk_trees_nan = None, 0
             self.head_depth = H
             self.rec_words = head_words(H) if H else 0

@@ -1,6 +1,6 @@
 set -o pipefail
 mkdir -p gpurun_out/r3j
-timeout -k 10 600 python -u -m pytest tests/test_wide_mlp.py tests/test_gpu_mlp.py tests/test_gpu_kernels.py tests/test_gpu_hybrid.py tests/test_gpu_segmented.py tests/test_design.py tests/test_math_context.py tests/test_gpu_surface.py -x -q --timeout 200 --timeout-method thread > gpurun_out/r3j/pytest.log 2>&1 || { tail -40 gpurun_out/r3j/pytest.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests/test_math_context.py tests/test_wide_mlp.py tests/test_gpu_mlp.py tests/test_gpu_kernels.py tests/test_gpu_hybrid.py tests/test_gpu_segmented.py tests/test_design.py tests/test_gpu_surface.py -x -q --timeout 200 --timeout-method thread > gpurun_out/r3j/pytest.log 2>&1 || { tail -40 gpurun_out/r3j/pytest.log; exit 1; }
 tail -1 gpurun_out/r3j/pytest.log
 for M in gbdt rf; do
   for S in lockstep refill; do

@@ -90,8 +90,8 @@ def test_gbdt_split_and_pointer_layouts(gpu):
         s, v = s.cpu().numpy(), v.cpu().numpy()
         assert (v == vref).all()
         assert np.max(np.abs(s - ref)) < 1e-4
-    for schedule in ("refill", "lockstep"):
-        pointer = c.plan(gpu, layout="pointer", pointer_schedule=schedule)
+    for schedule, order in (("lockstep", "bfs"), ("lockstep", "dfs"), ("refill", "bfs")):
+        pointer = c.plan(gpu, layout="pointer", pointer_schedule=schedule, node_order=order)
         assert pointer.layout == "pointer" and (pointer.variant == 16) == (schedule == "refill")
         s, v = _gpu_np(pointer, X)
         assert (v == vref).all() and np.max(np.abs(s - ref)) < 1e-4
@@ -341,7 +341,7 @@ def test_float_cast_gbdt_aliases_on_gpu(gpu):
 
 
 @pytest.mark.parametrize("kind,layout", [("regression", "perfect"), ("regression", "pointer"), ("rf", "perfect"),
-                                         ("rf", "pointer"), ("regression", "lockstep"), ("rf", "lockstep")])
+                                         ("rf", "pointer"), ("regression", "refill"), ("rf", "refill")])
 def test_null_prediction_trees_on_gpu(gpu, kind, layout):
     from flink_jpmml_amd.bench.synth import gbdt_pmml, random_forest_pmml, stream_matrix
     from flink_jpmml_amd.runtime.compiled import CompiledPmml
@@ -355,7 +355,7 @@ def test_null_prediction_trees_on_gpu(gpu, kind, layout):
     X = stream_matrix(20_000, 10, seed=6, missing_rate=0.01)
     ref, vref = c.score_matrix_oracle(X)
     assert 0 < vref.sum() < len(X)
-    opts = dict(layout="pointer", pointer_schedule="lockstep") if layout == "lockstep" else dict(layout=layout)
+    opts = dict(layout="pointer", pointer_schedule="refill") if layout == "refill" else dict(layout=layout)
     s, v = _gpu_np(c.plan(gpu, **opts), X)
     assert (v == vref).all()
     if kind == "rf":

@@ -95,7 +95,8 @@ def test_float_context_changes_edge_decisions(reader):
 @pytest.mark.parametrize("layout", ["auto", "pointer"])
 def test_float_context_gpu_matches_float_oracle(gpu, layout):
     """The fp32 kernels agree with the float-context oracle: identical decisions on the edge rows;
-    sums differ only by fp32 re-association (documented tolerance 4 ulp of the ensemble sum)."""
+    sums differ only by fp32 re-association (documented tolerance: 1e-5 absolute, a few ulp of the
+    partial sums, vs ~0.1 for one leaf routed differently)."""
     txt = _float_ctx(_decimal_thresholds(gbdt_pmml(n_trees=200, depth=6, n_features=12, seed=3)))
     c = CompiledPmml.from_string(txt)
     X = _edge_inputs(c, n=20000, seed=4)
@@ -103,5 +104,11 @@ def test_float_context_gpu_matches_float_oracle(gpu, layout):
     s, v = c.plan(gpu, layout=layout).score(X)
     s, v = s.cpu().numpy(), v.cpu().numpy()
     assert (v == vref).all()
-    ulp = np.spacing(np.abs(ref[v]).astype(np.float32)).astype(np.float64)
-    assert (np.abs(s[v] - ref[v]) <= 4 * ulp + 1e-7).all()
+    # fp32 re-association of the 200-leaf sum and the fp32 base-score add: a few ulp of the partial
+    # sums (|partial| <= ~4 here, ulp 4.8e-7), i.e. far below one leaf (~0.1) of a different route
+    err = np.abs(s[v] - ref[v])
+    print(f"float-context max |gpu - oracle| = {err.max():.3g}")
+    assert err.max() < 1e-5
+    # ... while a double evaluation of the same document routes the edge rows differently
+    ref64, _ = CompiledPmml.from_string(txt.replace(' x-mathContext="float"', "")).score_matrix_oracle(X)
+    assert (np.abs(ref64[v] - ref[v]) > 1e-3).mean() > 0.05
