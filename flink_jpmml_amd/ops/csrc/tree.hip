@@ -7,7 +7,7 @@ namespace {
 // Pointer layout: nodes uint4 {T bits, meta, left, right}; child < 0 => leaf ~child.
 // meta: feature byte offset (or index when features stay in global memory) | bit 30 null-on-
 // missing | bit 31 default right.
-template <bool GENERAL, bool FEAT_LDS>
+template <bool GENERAL, bool FEAT_LDS, int PILP = 8>
 __global__ __launch_bounds__(TB, 2) void tree_pointer_kernel(TreeArgs a) {
   extern __shared__ __align__(16) uint32_t smem[];
   float* feat = reinterpret_cast<float*>(smem);
@@ -48,7 +48,6 @@ __global__ __launch_bounds__(TB, 2) void tree_pointer_kernel(TreeArgs a) {
   // (dependent loads, divergent depths). Finished walks keep re-loading node 0 (clamped index,
   // no branch around the loads) and are masked out; leaves are accumulated in tree order, so the
   // sums are bit-identical to a serial walk.
-  constexpr int PILP = 8;
   for (int t0 = tb; t0 < te; t0 += PILP) {
     const int nt = min(PILP, te - t0);
     int code[PILP];
@@ -98,6 +97,88 @@ __global__ __launch_bounds__(TB, 2) void tree_pointer_kernel(TreeArgs a) {
         for (int p = 0; p < a.P; ++p) accl[(slot + p) * TB + tid] += a.leaves[(size_t)leaf * a.P + p];
       } else {
         acc += a.leaves[leaf];
+      }
+    }
+  }
+  finish_row(a, acc, accl, split, GENERAL, row, row_ok && !poisoned);
+}
+
+// Compact pointer layout (runtime/hybrid.py::pack_compact_bfs): 8-byte slots {T | leaf value,
+// meta}, trees stored level by level with a node's two children in adjacent slots, so the
+// lock-step walk of a wave (every lane in the same level of the same tree) touches half the cache
+// lines of the 16-byte layout and a node's children always share one. meta: feature (bits 0-5,
+// LDS plane) | left-is-leaf (6) | right-is-leaf (7) | first child - slot (8-29) | null (30) |
+// default right (31). The walk ends on a leaf's parent; the leaf slot's x is read after the
+// loop (P = 1: the weighted value itself; P > 1: its row of `leaves`). Features in LDS only.
+template <bool GENERAL>
+__global__ __launch_bounds__(TB, 2) void tree_compact_kernel(TreeArgs a) {
+  extern __shared__ __align__(16) uint32_t smem[];
+  float* feat = reinterpret_cast<float*>(smem);
+  int* bad = reinterpret_cast<int*>(smem + a.n_feat * TB);
+  float* accl = reinterpret_cast<float*>(bad + TB);
+  const int tid = threadIdx.x;
+  const int row0 = blockIdx.x * TB;
+  const int split = blockIdx.y;
+  const int row = row0 + tid;
+  stage_rows_T<TB>(a.X, a.n_rows, a.n_feat, a.ldx, a.prep, feat, bad, row0);
+  bool row_ok = bad[tid] == 0;
+  if (a.row_valid_in && row < a.n_rows) row_ok = row_ok && a.row_valid_in[row];
+  const uint2* nodes = reinterpret_cast<const uint2*>(a.blob);
+  const int tb = split * a.trees_per_split;
+  const int te = min(a.n_trees, tb + a.trees_per_split);
+  if (GENERAL) {
+    for (int c = 0; c < a.C; ++c) accl[c * TB + tid] = 0.f;
+  }
+  float acc = 0.f;
+  bool poisoned = false;
+  const char* feat_lane = reinterpret_cast<const char*>(feat + tid);
+  constexpr int PILP = 8;
+  for (int t0 = tb; t0 < te; t0 += PILP) {
+    const int nt = min(PILP, te - t0);
+    int pos[PILP];
+    bool act[PILP], pz[PILP];
+#pragma unroll
+    for (int i = 0; i < PILP; ++i) {
+      const int r = i < nt ? a.roots[t0 + i] : ~0;
+      pos[i] = r >= 0 ? r : ~r;
+      act[i] = r >= 0;  // a single-leaf tree starts on its leaf
+      pz[i] = false;
+    }
+    bool live = true;
+    while (live) {
+      uint2 nd[PILP];
+#pragma unroll
+      for (int i = 0; i < PILP; ++i) nd[i] = nodes[act[i] ? pos[i] : 0];
+      live = false;
+#pragma unroll
+      for (int i = 0; i < PILP; ++i) {
+        const uint32_t m = nd[i].y;
+        const float x = *reinterpret_cast<const float*>(feat_lane + ((m & 63u) << 10));
+        const bool isn = (x != x);
+        const bool nulled = act[i] && isn && ((m >> 30) & 1u);
+        const bool right = (x >= __uint_as_float(nd[i].x)) || (isn && (m >> 31));
+        const int child = pos[i] + (int)((m >> 8) & 0x3FFFFFu) + (right ? 1 : 0);
+        const bool leaf = right ? ((m >> 7) & 1u) : ((m >> 6) & 1u);
+        pz[i] = pz[i] || nulled;
+        pos[i] = act[i] && !nulled ? child : pos[i];
+        act[i] = act[i] && !nulled && !leaf;
+        live = live || act[i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < PILP; ++i) {
+      if (i >= nt) break;
+      if (pz[i]) {
+        if (GENERAL) poisoned = true;
+        else acc += __builtin_nanf("");
+        continue;
+      }
+      const uint32_t lv = nodes[pos[i]].x;
+      if (GENERAL) {
+        const int slot = a.tree_slot[t0 + i];
+        for (int p = 0; p < a.P; ++p) accl[(slot + p) * TB + tid] += a.leaves[(size_t)lv * a.P + p];
+      } else {
+        acc += __uint_as_float(lv);
       }
     }
   }
@@ -449,10 +530,19 @@ PMML_API int pmml_tree_launch(hipStream_t stream, const TreeArgs* args, int layo
       default: return -6;
     }
   } else {
-    if (a.variant != 0 && a.variant != VAR_POINTER_REFILL) return -10;
+    if (a.variant != 0 && a.variant != VAR_POINTER_REFILL && a.variant != VAR_POINTER_COMPACT) return -10;
     const bool feat_lds = a.n_feat <= 64;
     size_t lds = (feat_lds ? (size_t)a.n_feat * TB * 4 : 0) + TB * 4 + acc_lds;
-    if (a.variant == VAR_POINTER_REFILL) {
+    if (a.variant == VAR_POINTER_COMPACT) {
+      if (!feat_lds) return -4;
+      if (a.general) {
+        err = prepare_launch(tree_compact_kernel<true>, lds);
+        if (!err) hipLaunchKernelGGL((tree_compact_kernel<true>), grid, dim3(TB), lds, stream, a);
+      } else {
+        err = prepare_launch(tree_compact_kernel<false>, lds);
+        if (!err) hipLaunchKernelGGL((tree_compact_kernel<false>), grid, dim3(TB), lds, stream, a);
+      }
+    } else if (a.variant == VAR_POINTER_REFILL) {
       lds += (size_t)REFILL_ROOTS_LDS * 4;
       if (a.general) {
         if (feat_lds) {
@@ -480,7 +570,13 @@ PMML_API int pmml_tree_launch(hipStream_t stream, const TreeArgs* args, int layo
         if (!err) hipLaunchKernelGGL((tree_pointer_kernel<true, false>), grid, dim3(TB), lds, stream, a);
       }
     } else {
-      if (feat_lds) {
+      if (feat_lds && a.pilp == 16) {
+        err = prepare_launch(tree_pointer_kernel<false, true, 16>, lds);
+        if (!err) hipLaunchKernelGGL((tree_pointer_kernel<false, true, 16>), grid, dim3(TB), lds, stream, a);
+      } else if (feat_lds && a.pilp == 4) {
+        err = prepare_launch(tree_pointer_kernel<false, true, 4>, lds);
+        if (!err) hipLaunchKernelGGL((tree_pointer_kernel<false, true, 4>), grid, dim3(TB), lds, stream, a);
+      } else if (feat_lds) {
         err = prepare_launch(tree_pointer_kernel<false, true>, lds);
         if (!err) hipLaunchKernelGGL((tree_pointer_kernel<false, true>), grid, dim3(TB), lds, stream, a);
       } else {

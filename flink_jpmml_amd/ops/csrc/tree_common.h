@@ -67,12 +67,13 @@ struct TreeArgs {
   const float* acc_init;        // wide multi-class: per-class initial accumulator (nullable = 0)
   const int* feat_map;          // wide kernel: staged column j -> X column (nullable = identity)
   int rows_wide, mode;          // wide kernel: rows per workgroup (256/128/64), accumulation mode
-  int n_stage, pad2;            // wide kernel: staged feature columns
+  int n_stage, pilp;            // wide kernel: staged feature columns; pointer kernel: walks per lane (4/8/16)
   unsigned long long* prof;     // nullable: per-wave phase ticks of one workgroup ([16][4], s_memtime)
 };
 constexpr int VAR_NAN_FAST = 4;    // wide kernel: take the fast path even on tiles with missing values
 constexpr int VAR_NAN_PLANES = 8;  // ... via blob_nan + a second feature plane (NaN -> +inf)
 constexpr int VAR_POINTER_REFILL = 16;  // pointer layout: refill schedule (tree.hip)
+constexpr int VAR_POINTER_COMPACT = 32; // pointer layout: 8-byte BFS slots (tree.hip::tree_compact_kernel)
 
 // per-depth launchers (tree_d<D>.hip)
 #define PMML_TREE_DECL(D) int launch_perfect_d##D(hipStream_t st, const TreeArgs& a, dim3 grid, size_t lds);

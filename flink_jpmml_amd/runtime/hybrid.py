@@ -267,3 +267,88 @@ def pack_hybrid_compact(trees, weights: List[float], P: int, H: int, n_features:
 
 
 __all__ = ["head_words", "pack_hybrid_compact", "pack_trees"]
+
+
+# --------------------------------------------------------------------------- compact BFS pointer layout
+
+C2_FEAT_MASK = 63        # bits 0-5: feature (LDS plane index)
+C2_LLEAF, C2_RLEAF = 1 << 6, 1 << 7
+C2_REL_SHIFT, C2_REL_BITS = 8, 22
+C2_NULL, C2_DR = 1 << 30, 1 << 31
+
+
+def pack_compact_bfs(trees, weights: List[float], P: int):
+    """8-byte pointer nodes, each tree stored level by level with the two children of a node in
+    adjacent slots (``tree.hip::tree_compact_kernel``).
+
+    A slot is ``uint2 {x, meta}``. Internal node: ``x`` = canonical fp32 threshold ("go right iff
+    x >= T"), ``meta`` = feature | left-is-leaf | right-is-leaf | (first child - this slot) << 8 |
+    null-on-missing | default-right. Leaf slot: ``x`` = the weighted leaf value (P == 1) or the
+    row of ``leaves`` (P > 1). The walk stops on the parent of a leaf and reads ``x`` of the
+    leaf slot after the lock-step loop. Root codes: slot index, or ``~slot`` for a single-leaf tree.
+
+    Returns ``(nodes [n, 2] u32, leaves [n_leaves, P] f32 or None, roots [n_trees] i32, has_dr)``;
+    ``ValueError`` when a tree has more than 2^22 slots or a feature index >= 64."""
+    from .plans import _canonical_vec
+
+    slots_all: List[np.ndarray] = []
+    leaves_all: List[np.ndarray] = []
+    roots = np.zeros(len(trees), dtype=np.int32)
+    base = n_leaf = 0
+    has_dr = False
+    for ti, (t, w) in enumerate(zip(trees, weights)):
+        feat = np.asarray(t.feature, dtype=np.int64)
+        n = feat.shape[0]
+        internal = feat >= 0
+        if internal.any() and feat[internal].max() > C2_FEAT_MASK:
+            raise ValueError("compact pointer layout: feature index >= 64")
+        T, swap = _canonical_vec(np.asarray(t.op), np.asarray(t.threshold, dtype=np.float64))
+        left, right = np.asarray(t.left, dtype=np.int64), np.asarray(t.right, dtype=np.int64)
+        lc = np.where(swap, right, left)
+        rc = np.where(swap, left, right)
+        dr = np.where(swap, np.asarray(t.default_left, bool), ~np.asarray(t.default_left, bool)) & internal
+        has_dr = has_dr or bool(dr.any())
+        # slots: root, then per level the (left, right) pairs of the level's internal nodes
+        pos = np.full(n, -1, dtype=np.int64)
+        pos[0] = 0
+        first = np.full(n, -1, dtype=np.int64)
+        nxt = 1
+        frontier = np.array([0], dtype=np.int64)
+        while frontier.size:
+            fi = frontier[internal[frontier]]
+            if fi.size == 0:
+                break
+            first[fi] = nxt + 2 * np.arange(fi.size)
+            pos[lc[fi]] = first[fi]
+            pos[rc[fi]] = first[fi] + 1
+            nxt += 2 * fi.size
+            frontier = np.stack([lc[fi], rc[fi]], axis=1).reshape(-1)
+        if nxt > (1 << C2_REL_BITS):
+            raise ValueError("compact pointer layout: tree larger than 2^22 slots")
+        slots = np.zeros((nxt, 2), dtype=np.uint32)
+        ik = np.nonzero(internal & (pos >= 0))[0]
+        rel = (first[ik] - pos[ik]).astype(np.uint64)
+        meta = (feat[ik].astype(np.uint64)
+                | (np.uint64(C2_LLEAF) * (~internal[lc[ik]]).astype(np.uint64))
+                | (np.uint64(C2_RLEAF) * (~internal[rc[ik]]).astype(np.uint64))
+                | (rel << np.uint64(C2_REL_SHIFT))
+                | (np.uint64(C2_NULL) * np.uint64(bool(t.null_missing)))
+                | (np.uint64(C2_DR) * dr[ik].astype(np.uint64)))
+        slots[pos[ik], 0] = T[ik].view(np.uint32)
+        slots[pos[ik], 1] = meta.astype(np.uint32)
+        lk = np.nonzero(~internal & (pos >= 0))[0]
+        if P == 1:
+            vals = (np.asarray(t.leaf_value, dtype=np.float64)[lk] * w).astype(np.float32)
+            slots[pos[lk], 0] = vals.view(np.uint32)
+        else:
+            lk = lk[np.argsort(pos[lk], kind="stable")]
+            vals = np.asarray(t.leaf_probs, dtype=np.float64)[lk, :P] * w
+            slots[pos[lk], 0] = (n_leaf + np.arange(lk.size)).astype(np.uint32)
+            leaves_all.append(vals)
+            n_leaf += lk.size
+        roots[ti] = base if internal[0] else ~base
+        slots_all.append(slots)
+        base += nxt
+    nodes = np.concatenate(slots_all) if slots_all else np.zeros((1, 2), np.uint32)
+    leaves = np.concatenate(leaves_all).astype(np.float32) if leaves_all else None
+    return nodes, leaves, roots, has_dr

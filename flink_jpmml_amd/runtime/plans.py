@@ -1066,7 +1066,7 @@ def _perfect_pack_vec(trees, weights, P: int, D: int, stride: int, fmap, leaf_bi
     return blob, rec, has_dr
 
 
-VAR_NAN_FAST, VAR_NAN_PLANES, VAR_POINTER_REFILL = 4, 8, 16  # mirrors csrc/tree_common.h
+VAR_NAN_FAST, VAR_NAN_PLANES, VAR_POINTER_REFILL, VAR_POINTER_COMPACT = 4, 8, 16, 32  # csrc/tree_common.h
 DYN_B, DYN_SLOTS = 8, 16  # csrc: MODE_SUM trees per claimed batch, batch slots per chunk
 
 
@@ -1204,20 +1204,26 @@ class TreePlan(DevicePlan):
                                   "blob", "leaves", "roots", "has_dr", "table", "slots", "splits", "epi_args",
                                   "variant", "children", "preds", "pool", "trees_tab", "max_steps", "blob_nan",
                                   "chunk_trees_nan", "full_epi", "labels", "mode", "tree_w", "acc_init", "feat_map",
-                                  "rows_wide", "n_stage", "heads", "head_depth")
+                                  "rows_wide", "n_stage", "heads", "head_depth", "pointer_ilp")
 
     WIDE_G = 4  # tree groups of the wide kernel (mirrors csrc)
 
     def __init__(self, compiled, device, layout: str = "auto", lds_budget: int = 80 * 1024, splits: int = 0,
                  variant: str = "auto", precision: str = "fp32", nan_mode: str = "auto", max_chunk_trees: int = 0,
                  tree_shard: Optional[Tuple[int, int]] = None, head_depth: int = 0,
-                 pointer_schedule: str = "lockstep", node_order: str = "bfs"):
+                 pointer_schedule: str = "lockstep", node_order: str = "bfs", node_format: str = "wide",
+                 pointer_ilp: int = 8):
         """``pointer_schedule`` (pointer layout): ``"lockstep"`` (default: groups of walks run to the
         deepest one; tree-order sums) or ``"refill"`` (each walk slot restarts on the next tree the
         step its walk ends). Measured (profiles/r3j): refill is 2.3-2.6x SLOWER at depth 14 — lanes
         drift onto different trees and every load instruction touches up to 64 distinct lines,
         while lock-step lanes share the lines of the same tree level. ``node_order``: pointer-node
         storage order (``"bfs"``: level by level, siblings adjacent; ``"dfs"``: preorder).
+        ``node_format`` (pointer layout): ``"wide"`` (default) 16-byte nodes, ``"compact"`` 8-byte
+        BFS slots with inline leaves (:func:`~flink_jpmml_amd.runtime.hybrid.pack_compact_bfs`;
+        features staged in LDS, i.e. at most 64) — measured 1.34x SLOWER (profiles/r3n), kept as
+        an option; ``"auto"``: compact whenever it applies. ``pointer_ilp``: walks per lane in
+        lock-step (4, 8 or 16; regression sums with features in LDS).
 
         ``nan_mode`` (wide PERFECT kernel): ``"auto"`` keeps tiles with missing values on the fast
         traversal whenever the ensemble has no null-on-missing trees (default-right nodes read a
@@ -1229,6 +1235,9 @@ class TreePlan(DevicePlan):
         super().__init__(compiled, device)
         if nan_mode not in ("auto", "off"):
             raise ValueError("nan_mode must be 'auto' or 'off'")
+        if pointer_ilp not in (4, 8, 16):
+            raise ValueError("pointer_ilp must be 4, 8 or 16")
+        self.pointer_ilp = int(pointer_ilp)
         if pointer_schedule not in ("refill", "lockstep"):
             raise ValueError("pointer_schedule must be 'refill' or 'lockstep'")
         self.heads, self.head_depth = None, 0  # hybrid layout only
@@ -1401,7 +1410,7 @@ class TreePlan(DevicePlan):
         else:
             if precision == "fp8":
                 raise NotLowerable("fp8 leaves need the PERFECT layout")
-            from .hybrid import head_words, pack_hybrid_compact, pack_trees
+            from .hybrid import head_words, pack_compact_bfs, pack_hybrid_compact, pack_trees
 
             feat_lds = F <= 64
             H = 0
@@ -1429,7 +1438,20 @@ class TreePlan(DevicePlan):
                     self.layout, H, heads, self.chunk_trees = "pointer", 0, None, 0
             else:
                 self.chunk_trees = 0
-            if heads is None:
+            compact = False
+            if heads is None and feat_lds and pointer_schedule == "lockstep" and node_format != "wide" \
+                    and node_order == "bfs":
+                try:
+                    nodes, leaves, roots, has_dr = pack_compact_bfs(spec.trees, spec.weights, spec.P)
+                    compact = True
+                    if leaves is None:
+                        leaves = np.zeros((1, 1), np.float32)
+                except ValueError:
+                    if node_format == "compact":
+                        raise NotLowerable("compact pointer layout does not apply")
+            elif node_format == "compact":
+                raise NotLowerable("compact pointer layout needs features in LDS, lock-step, bfs")
+            if heads is None and not compact:
                 _, nodes, leaves, roots, has_dr = pack_trees(spec.trees, spec.weights, spec.P, 0, feat_lds,
                                                              order=node_order)
             self.blob_nan, self.chunk_trees_nan = None, 0
@@ -1438,6 +1460,8 @@ class TreePlan(DevicePlan):
             # pointer walks: refill schedule (each PILP slot restarts on the next tree as soon as
             # its walk ends) unless pinned to the lock-step kernel's tree-order sums
             self.variant = VAR_POINTER_REFILL if (self.layout == "pointer" and pointer_schedule == "refill") else 0
+            if compact:
+                self.variant = VAR_POINTER_COMPACT
             self.blob = self._t(nodes.reshape(-1).view(np.int32))
             self.leaves = self._t(leaves.reshape(-1))
             self.roots = self._t(roots)
@@ -1528,6 +1552,7 @@ class TreePlan(DevicePlan):
             a.feat_map = ptr(getattr(self, "feat_map", None))
             a.rows_wide, a.mode = getattr(self, "rows_wide", TB), getattr(self, "mode", 0)
             a.n_stage = getattr(self, "n_stage", self.n_features)
+            a.pilp = getattr(self, "pointer_ilp", 8)
             a.prof = ptr(getattr(self, "prof", None))  # kbench --tree-prof phase timers (nullable)
             a.epi = _epilogue(table=self.table, write_probs=with_probs, **self.epi_args)
             cache[with_probs] = a

@@ -32,6 +32,8 @@ def main():
     p.add_argument("--head-depth", type=int, default=0, help="hybrid layout: PERFECT head levels (4/6/8/10)")
     p.add_argument("--pointer-schedule", default="lockstep", choices=["refill", "lockstep"])
     p.add_argument("--node-order", default="bfs", choices=["bfs", "dfs"])
+    p.add_argument("--node-format", default="wide", choices=["auto", "compact", "wide"])
+    p.add_argument("--pointer-ilp", type=int, default=8, choices=[4, 8, 16])
     p.add_argument("--p-split", type=float, default=None, help="tree generators: split probability per node")
     p.add_argument("--precision", default="fp32", choices=["fp32", "bf16", "fp8"])
     p.add_argument("--hidden", default="256,256", help="mlp hidden widths")
@@ -84,7 +86,8 @@ def main():
     if args.model.startswith(("gbdt", "rf")):
         opts = dict(layout=args.layout, lds_budget=args.lds_budget, variant=args.variant, nan_mode=args.nan_mode,
                     max_chunk_trees=args.max_chunk_trees, head_depth=args.head_depth,
-                    pointer_schedule=args.pointer_schedule, node_order=args.node_order)
+                    pointer_schedule=args.pointer_schedule, node_order=args.node_order,
+                    node_format=args.node_format, pointer_ilp=args.pointer_ilp)
     elif args.model == "kmeans-big":
         opts = dict(cluster_variant=args.variant)
     if args.precision != "fp32":
@@ -142,7 +145,7 @@ def main():
                       "rows_per_s": args.rows / ms * 1e3, "plan": type(plan).__name__,
                       "layout": getattr(plan, "layout", None), "chunk_trees": getattr(plan, "chunk_trees", None),
                       "head_depth": getattr(plan, "head_depth", None), "depth": getattr(plan, "depth", None),
-                      "pointer_schedule": args.pointer_schedule, "node_order": args.node_order,
+                      "pointer_schedule": args.pointer_schedule, "node_order": args.node_order, "node_format": args.node_format, "pointer_ilp": args.pointer_ilp,
                       "trees": getattr(plan, "n_trees", None),
                       "missing": args.missing, "lds_budget": args.lds_budget,
                       "variant": getattr(plan, "variant", None), "mlp_prof": prof,

@@ -28,6 +28,8 @@ def emulate(plan, X):
     n = len(X)
     feat_lds = plan.n_features <= 64
     H = plan.head_depth
+    if plan.variant == 32:
+        return emulate_compact(plan, Xf)
     tail = plan.blob.numpy().view(np.uint32).reshape(-1, 2 if H else 4)
     leaves = plan.leaves.numpy().reshape(-1, plan.P)[:, 0]
     NI = (1 << H) - 1
@@ -84,14 +86,46 @@ def emulate(plan, X):
     return acc
 
 
-@pytest.mark.parametrize("layout,head", [("hybrid", 8), ("hybrid", 4), ("hybrid", 10), ("pointer", 0)])
+def emulate_compact(plan, Xf):
+    """The 8-byte BFS pointer kernel (``tree_compact_kernel``): children at first, first + 1;
+    the walk stops on a leaf's parent and reads the leaf slot's x."""
+    n = len(Xf)
+    nodes = plan.blob.numpy().view(np.uint32).reshape(-1, 2)
+    leaves = plan.leaves.numpy().reshape(-1, plan.P)[:, 0]
+    acc = np.zeros(n)
+    for t in range(plan.n_trees):
+        r = int(plan.roots.numpy()[t])
+        pos = np.full(n, r if r >= 0 else ~r, np.int64)
+        act = np.full(n, r >= 0)
+        pz = np.zeros(n, bool)
+        while act.any():
+            nd = nodes[np.where(act, pos, 0)]
+            m = nd[:, 1]
+            x = Xf[np.arange(n), m & 63]
+            isn = np.isnan(x)
+            nulled = act & isn & ((m >> 30) & 1).astype(bool)
+            right = (x >= nd[:, 0].view(np.float32)) | (isn & (m >> 31).astype(bool))
+            child = pos + ((m >> 8) & 0x3FFFFF) + right
+            leaf = np.where(right, (m >> 7) & 1, (m >> 6) & 1).astype(bool)
+            pz |= nulled
+            pos = np.where(act & ~nulled, child, pos)
+            act = act & ~nulled & ~leaf
+        val = nodes[pos, 0]
+        lv = leaves[val] if plan.P > 1 else val.view(np.float32)
+        acc += np.where(pz, np.nan, lv)
+    return acc
+
+
+@pytest.mark.parametrize("layout,head,fmt", [("hybrid", 8, "auto"), ("hybrid", 4, "auto"), ("hybrid", 10, "auto"),
+                                             ("pointer", 0, "compact"), ("pointer", 0, "wide")])
 @pytest.mark.parametrize("missing", ["defaultChild", "nullPrediction"])
-def test_deep_regression_forest_layouts_match_oracle(layout, head, missing):
+def test_deep_regression_forest_layouts_match_oracle(layout, head, fmt, missing):
     txt = gbdt_pmml(n_trees=12, depth=13, n_features=20, seed=3, p_split=0.8)
     if missing == "nullPrediction":
         txt = txt.replace('missingValueStrategy="defaultChild"', 'missingValueStrategy="nullPrediction"')
-    c, plan = _plan(txt, layout=layout, head_depth=head)
+    c, plan = _plan(txt, layout=layout, head_depth=head, node_format=fmt)
     assert plan.layout == layout and plan.head_depth == head
+    assert (plan.variant == 32) == (fmt == "compact")
     X = stream_matrix(4000, 20, seed=5, missing_rate=0.03)
     ref, vref = c.score_matrix_oracle(X)
     out = emulate(plan, X)
