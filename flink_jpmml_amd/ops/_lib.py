@@ -136,7 +136,7 @@ class TreeArgs(ctypes.Structure):
                 ("chunk_trees", c_int), ("P", c_int), ("C", c_int), ("trees_per_split", c_int),
                 ("general", c_int), ("variant", c_int), ("epi", Epilogue), ("score", c_void_p),
                 ("valid", c_void_p), ("probs", c_void_p), ("partial", c_void_p), ("blob_nan", c_void_p),
-                ("chunk_trees_nan", c_int), ("pad1", c_int), ("tree_w", c_void_p), ("acc_init", c_void_p),
+                ("chunk_trees_nan", c_int), ("xcd_split", c_int), ("tree_w", c_void_p), ("acc_init", c_void_p),
                 ("feat_map", c_void_p), ("rows_wide", c_int), ("mode", c_int), ("n_stage", c_int), ("pilp", c_int),
                 ("prof", c_void_p)]
 

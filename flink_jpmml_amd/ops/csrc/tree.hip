@@ -14,8 +14,9 @@ __global__ __launch_bounds__(TB, 2) void tree_pointer_kernel(TreeArgs a) {
   int* bad = reinterpret_cast<int*>(smem + (FEAT_LDS ? a.n_feat * TB : 0));
   float* accl = reinterpret_cast<float*>(bad + TB);
   const int tid = threadIdx.x;
-  const int row0 = blockIdx.x * TB;
-  const int split = blockIdx.y;
+  const int2 blk = tree_block(a);
+  const int row0 = blk.x * TB;
+  const int split = blk.y;
   const int row = row0 + tid;
   if (FEAT_LDS) {
     stage_rows_T<TB>(a.X, a.n_rows, a.n_feat, a.ldx, a.prep, feat, bad, row0);
@@ -117,8 +118,9 @@ __global__ __launch_bounds__(TB, 2) void tree_compact_kernel(TreeArgs a) {
   int* bad = reinterpret_cast<int*>(smem + a.n_feat * TB);
   float* accl = reinterpret_cast<float*>(bad + TB);
   const int tid = threadIdx.x;
-  const int row0 = blockIdx.x * TB;
-  const int split = blockIdx.y;
+  const int2 blk = tree_block(a);
+  const int row0 = blk.x * TB;
+  const int split = blk.y;
   const int row = row0 + tid;
   stage_rows_T<TB>(a.X, a.n_rows, a.n_feat, a.ldx, a.prep, feat, bad, row0);
   bool row_ok = bad[tid] == 0;
@@ -203,8 +205,9 @@ __global__ __launch_bounds__(TB, 2) void tree_pointer_refill_kernel(TreeArgs a) 
   float* accl = reinterpret_cast<float*>(bad + TB);
   int* roots_l = reinterpret_cast<int*>(accl + (GENERAL ? a.C * TB : 0));
   const int tid = threadIdx.x;
-  const int row0 = blockIdx.x * TB;
-  const int split = blockIdx.y;
+  const int2 blk = tree_block(a);
+  const int row0 = blk.x * TB;
+  const int split = blk.y;
   const int row = row0 + tid;
   const int tb = split * a.trees_per_split;
   const int te = min(a.n_trees, tb + a.trees_per_split);
@@ -502,7 +505,11 @@ PMML_API int pmml_tree_launch(hipStream_t stream, const TreeArgs* args, int layo
   if (splits == 1) a.partial = nullptr;
   if (a.C > 16) return -3;
   a.trees_per_split = (a.n_trees + splits - 1) / splits;
-  dim3 grid((a.n_rows + TB - 1) / TB, splits);
+  const int row_blocks = (a.n_rows + TB - 1) / TB;
+  if (layout == 0 || splits == 1) a.xcd_split = 0;  // PERFECT kernels: grid.y splits (forests fit L2)
+  if (a.xcd_split > 0) a.xcd_split = splits;
+  if (a.xcd_split > 0 && (long long)row_blocks * splits > 0x7FFFFFFFLL) return -11;
+  dim3 grid = a.xcd_split > 0 ? dim3(row_blocks * splits) : dim3(row_blocks, splits);
   int err = 0;
   const size_t acc_lds = a.general ? (size_t)a.C * TB * 4 : 0;
   if (layout == 0) {

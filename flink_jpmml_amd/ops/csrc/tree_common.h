@@ -62,7 +62,8 @@ struct TreeArgs {
   float* probs;
   float* partial;               // split mode: [splits][C+1][n_rows]
   const uint32_t* blob_nan;     // wide kernel, nullable: the records re-pointed at the NaN plane
-  int chunk_trees_nan, pad1;    // (tiles with missing values; own chunk size, LDS holds 2 planes)
+  int chunk_trees_nan;          // (tiles with missing values; own chunk size, LDS holds 2 planes)
+  int xcd_split;                // pointer / hybrid layouts: > 0 = XCD-aware tree splits (tree_block)
   const float* tree_w;          // wide MODE_CLASS: per-tree vote weight (nullable = 1)
   const float* acc_init;        // wide multi-class: per-class initial accumulator (nullable = 0)
   const int* feat_map;          // wide kernel: staged column j -> X column (nullable = identity)
@@ -83,6 +84,21 @@ PMML_TREE_DECL(6) PMML_TREE_DECL(7) PMML_TREE_DECL(8) PMML_TREE_DECL(9) PMML_TRE
 
 namespace {
 
+// Workgroup -> (row block, tree split). Default: grid (row blocks, splits). XCD-aware mode
+// (a.xcd_split = S > 0): a 1-D grid of row_blocks * S workgroups where workgroup L scores tree
+// split L % S of row block L / S. The dispatcher deals workgroups to the 8 XCDs round-robin
+// (L % 8), so with S = 8 every XCD only ever walks ONE eighth of the forest: a deep forest too big
+// for one 4 MiB L2 (300 trees x depth 14 = 14 MB of nodes) is split into 8 slices that each stay
+// L2-resident, instead of every XCD gathering the whole forest from the Infinity Cache. The 8
+// workgroups of one row block run side by side, so the row tile they each stage is one HBM read.
+// Placement is a speed hint only; correctness never depends on it.
+__device__ __forceinline__ int2 tree_block(const TreeArgs& a) {
+  if (a.xcd_split > 0) {
+    const int L = blockIdx.x;
+    return make_int2(L / a.xcd_split, L % a.xcd_split);
+  }
+  return make_int2(blockIdx.x, blockIdx.y);
+}
 
 __device__ __forceinline__ void finish_row(const TreeArgs& a, float acc0, const float* accl, int split,
                                            bool general, int row, bool row_ok) {

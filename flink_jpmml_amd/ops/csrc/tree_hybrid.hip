@@ -59,7 +59,8 @@ __global__ __launch_bounds__(TB, 2) void tree_hybrid_kernel(HybridArgs ha) {
   float* accl = reinterpret_cast<float*>(bad + TB);
   uint32_t* hbuf = reinterpret_cast<uint32_t*>(accl + (GENERAL ? a.C * TB : 0));
   const int tid = threadIdx.x;
-  const int row0 = blockIdx.x * TB;
+  const int2 blk = tree_block(a);
+  const int row0 = blk.x * TB;
   const int row = row0 + tid;
   if (FEAT_LDS) {
     stage_rows_T<TB>(a.X, a.n_rows, a.n_feat, a.ldx, a.prep, feat, bad, row0);
@@ -81,7 +82,7 @@ __global__ __launch_bounds__(TB, 2) void tree_hybrid_kernel(HybridArgs ha) {
     for (int c = 0; c < a.C; ++c) accl[c * TB + tid] = 0.f;
   }
   const uint2* tail = reinterpret_cast<const uint2*>(a.blob);
-  const int tb = blockIdx.y * a.trees_per_split;
+  const int tb = blk.y * a.trees_per_split;
   const int te = min(a.n_trees, tb + a.trees_per_split);
   const int rw = ha.head_words;
   const int CT = a.chunk_trees;
@@ -183,7 +184,7 @@ __global__ __launch_bounds__(TB, 2) void tree_hybrid_kernel(HybridArgs ha) {
       }
     }
   }
-  finish_row(a, acc, accl, blockIdx.y, GENERAL, row, row_ok && !poisoned);
+  finish_row(a, acc, accl, blk.y, GENERAL, row, row_ok && !poisoned);
 }
 
 // Split-mode reduction (same partial layout as the pointer kernel).
@@ -245,7 +246,11 @@ PMML_API int pmml_tree_hybrid_launch(hipStream_t stream, const HybridArgs* args,
   const size_t lds = (feat_lds ? (size_t)a.n_feat * TB * 4 : 0) + TB * 4 + (a.general ? (size_t)a.C * TB * 4 : 0) +
                      (size_t)a.chunk_trees * ha.head_words * 4;
   if (lds > 160 * 1024) return -5;
-  dim3 grid((a.n_rows + TB - 1) / TB, splits);
+  const int row_blocks = (a.n_rows + TB - 1) / TB;
+  if (splits == 1) a.xcd_split = 0;
+  if (a.xcd_split > 0) a.xcd_split = splits;
+  if (a.xcd_split > 0 && (long long)row_blocks * splits > 0x7FFFFFFFLL) return -11;
+  dim3 grid = a.xcd_split > 0 ? dim3(row_blocks * splits) : dim3(row_blocks, splits);
   int err;
   switch (head_depth) {
     case 4: err = launch_hybrid_h<4>(stream, ha, grid, lds, a.general != 0, feat_lds); break;

@@ -1196,6 +1196,10 @@ def _pointer_pack(trees: List[BinaryTree], weights: List[float], P: int):
     return nd, lv, np.array(roots, dtype=np.int32), has_dr
 
 
+# XCD-aware tree slicing of pointer / hybrid forests (csrc tree_block): one slice per XCD
+XCD_SLICES = 8
+
+
 class TreePlan(DevicePlan):
     """GBDT / random forest / single tree / calibrated chain on the HIP traversal kernel."""
 
@@ -1204,7 +1208,7 @@ class TreePlan(DevicePlan):
                                   "blob", "leaves", "roots", "has_dr", "table", "slots", "splits", "epi_args",
                                   "variant", "children", "preds", "pool", "trees_tab", "max_steps", "blob_nan",
                                   "chunk_trees_nan", "full_epi", "labels", "mode", "tree_w", "acc_init", "feat_map",
-                                  "rows_wide", "n_stage", "heads", "head_depth", "pointer_ilp")
+                                  "rows_wide", "n_stage", "heads", "head_depth", "pointer_ilp", "xcd_split")
 
     WIDE_G = 4  # tree groups of the wide kernel (mirrors csrc)
 
@@ -1212,8 +1216,15 @@ class TreePlan(DevicePlan):
                  variant: str = "auto", precision: str = "fp32", nan_mode: str = "auto", max_chunk_trees: int = 0,
                  tree_shard: Optional[Tuple[int, int]] = None, head_depth: int = 0,
                  pointer_schedule: str = "lockstep", node_order: str = "bfs", node_format: str = "wide",
-                 pointer_ilp: int = 8):
-        """``pointer_schedule`` (pointer layout): ``"lockstep"`` (default: groups of walks run to the
+                 pointer_ilp: int = 8, xcd_split: str = "off"):
+        """``xcd_split`` (pointer / hybrid layouts): ``"on"`` splits the forest into 8 tree slices
+        scored by workgroups placed on the 8 XCDs (csrc ``tree_block``), so each XCD's 4 MiB L2
+        holds one slice instead of the whole forest; ``"off"`` (default): grid.y splits only.
+        Measured (profiles/r3q): no gain on a 14 MB depth-14 forest — its L2 hit rate is already
+        96 % unsplit; the walk is bound by the vector cache's per-line tag rate (26 distinct lines
+        per gather instruction, ~1.3 line accesses per clock per CU), not by L2 capacity.
+
+        ``pointer_schedule`` (pointer layout): ``"lockstep"`` (default: groups of walks run to the
         deepest one; tree-order sums) or ``"refill"`` (each walk slot restarts on the next tree the
         step its walk ends). Measured (profiles/r3j): refill is 2.3-2.6x SLOWER at depth 14 — lanes
         drift onto different trees and every load instruction touches up to 64 distinct lines,
@@ -1241,6 +1252,9 @@ class TreePlan(DevicePlan):
         if pointer_schedule not in ("refill", "lockstep"):
             raise ValueError("pointer_schedule must be 'refill' or 'lockstep'")
         self.heads, self.head_depth = None, 0  # hybrid layout only
+        if xcd_split not in ("on", "off"):
+            raise ValueError("xcd_split must be 'on' or 'off'")
+        self.xcd_split = 0
         if precision not in ("fp32", "fp8"):
             raise ValueError("tree leaf precision must be fp32 or fp8")
         if layout == "general":
@@ -1309,7 +1323,9 @@ class TreePlan(DevicePlan):
                    and (spec.mode == "sum" or spec.C <= 8))
         if layout == "auto":
             rec_bytes = 4 * (2 * NI + NL * spec.P + (NI + 31) // 32)
-            layout = "perfect" if depth <= 10 and (wide_ok or F <= 64) and rec_bytes <= 32 * 1024 else "hybrid"
+            # deeper trees: the POINTER walk (profiles/r3q: 300 trees x depth 14, pointer 3.39 /
+            # 2.60 ms vs hybrid-head 4.55 / 3.11 ms for the forest / GBDT)
+            layout = "perfect" if depth <= 10 and (wide_ok or F <= 64) and rec_bytes <= 32 * 1024 else "pointer"
         if spec.mode != "sum" and not (layout == "perfect" and wide_ok):
             spec = to_general(spec)  # votes / class slots accumulate in LDS on the narrow kernels
             self.n_trees = len(spec.trees)  # + constant stumps carrying the per-class intercepts
@@ -1466,6 +1482,8 @@ class TreePlan(DevicePlan):
             self.leaves = self._t(leaves.reshape(-1))
             self.roots = self._t(roots)
             self.heads = self._t(heads.reshape(-1).view(np.int32)) if heads is not None else None
+            if xcd_split == "on":
+                self.xcd_split = XCD_SLICES
         if not (self.variant & 3):
             self.mode = 0  # narrow / pointer kernels: plain sums or LDS slot accumulators
         self.has_dr = has_dr
@@ -1564,6 +1582,8 @@ class TreePlan(DevicePlan):
         if self.splits:
             return self.splits
         blocks = (n_rows + TB - 1) // TB
+        if getattr(self, "xcd_split", 0) and self.n_trees >= 2 * XCD_SLICES:
+            return XCD_SLICES
         target = 512  # ~2 workgroups per CU on 256 CUs
         if blocks >= target or self.n_trees < 64:
             return 1
@@ -1591,6 +1611,7 @@ class TreePlan(DevicePlan):
         a.score, a.valid, a.probs = _addr(score), _addr(valid), ptr(probs)
         a.epi.score2, a.epi.valid2 = _addr(score2), _addr(valid2)
         a.partial = None
+        a.xcd_split = 1 if getattr(self, "xcd_split", 0) and s > 1 else 0
         if s > 1:
             need = s * (self.C + 1) * n
             if self._partial is None or self._partial.numel() < need:

@@ -1,0 +1,84 @@
+#!/usr/bin/env python3
+"""Kernel-only sweep of deep-forest tree layouts on ONE parsed model (the 200 MB PMML is
+generated and parsed once): device-resident rows, CUDA-event timing of ``plan.launch``.
+
+python scripts/deep_forest_sweep.py --model rf --trees 300 --depth 14 --p-split 0.85
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+CONFIGS = {
+    "pointer": dict(layout="pointer", xcd_split="off"),
+    "pointer+xcd": dict(layout="pointer", xcd_split="on"),
+    "compact": dict(layout="pointer", node_format="compact", xcd_split="off"),
+    "compact+xcd": dict(layout="pointer", node_format="compact", xcd_split="on"),
+    "refill+xcd": dict(layout="pointer", pointer_schedule="refill", xcd_split="on"),
+    "ilp4+xcd": dict(layout="pointer", pointer_ilp=4, xcd_split="on"),
+    "ilp16+xcd": dict(layout="pointer", pointer_ilp=16, xcd_split="on"),
+    "hybrid4": dict(layout="hybrid", head_depth=4, xcd_split="off"),
+    "hybrid4+xcd": dict(layout="hybrid", head_depth=4, xcd_split="on"),
+    "hybrid6+xcd": dict(layout="hybrid", head_depth=6, xcd_split="on"),
+    "auto": dict(),
+}
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--model", default="rf", choices=["rf", "gbdt"])
+    p.add_argument("--trees", type=int, default=300)
+    p.add_argument("--depth", type=int, default=14)
+    p.add_argument("--features", type=int, default=32)
+    p.add_argument("--p-split", type=float, default=0.85)
+    p.add_argument("--rows", type=int, default=1 << 20)
+    p.add_argument("--iters", type=int, default=10)
+    p.add_argument("--configs", default=",".join(CONFIGS))
+    p.add_argument("--check-rows", type=int, default=4096, help="rows compared with the fp64 oracle per config")
+    args = p.parse_args()
+    import numpy as np
+    import torch
+
+    from flink_jpmml_amd.bench import synth
+    from flink_jpmml_amd.runtime.compiled import CompiledPmml
+
+    t0 = time.perf_counter()
+    gen = synth.random_forest_pmml if args.model == "rf" else synth.gbdt_pmml
+    txt = gen(n_trees=args.trees, depth=args.depth, n_features=args.features, p_split=args.p_split)
+    c = CompiledPmml.from_string(txt.encode())
+    del txt
+    print(json.dumps({"event": "loaded", "s": time.perf_counter() - t0}), flush=True)
+    Xh = synth.stream_matrix(args.rows, c.n_features, seed=1)
+    X = torch.from_numpy(Xh).cuda()
+    ref, vref = c.score_matrix_oracle(Xh[: args.check_rows])
+    for name in args.configs.split(","):
+        plan = c.plan("cuda:0", **CONFIGS[name])
+        s, v = plan.alloc_outputs(args.rows)
+        for _ in range(2):
+            plan.launch(X, s, v)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(args.iters):
+            plan.launch(X, s, v)
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / args.iters
+        sc = s[: args.check_rows].cpu().numpy()
+        vc = v[: args.check_rows].cpu().numpy().astype(bool)
+        ok = bool((vc == vref).all())
+        err = float(np.max(np.abs(sc[vc] - ref[vc]))) if vc.any() else 0.0
+        print(json.dumps({"config": name, "model": args.model, "trees": args.trees, "depth": args.depth,
+                          "p_split": args.p_split, "rows": args.rows, "ms": ms, "rows_per_s": args.rows / ms * 1e3,
+                          "layout": plan.layout, "variant": plan.variant, "xcd_split": plan.xcd_split,
+                          "splits": plan._auto_splits(args.rows), "valid_match": ok, "max_abs_err": err}), flush=True)
+        del plan, s, v
+        c._plans.clear()
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

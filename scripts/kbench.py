@@ -34,7 +34,10 @@ def main():
     p.add_argument("--node-order", default="bfs", choices=["bfs", "dfs"])
     p.add_argument("--node-format", default="wide", choices=["auto", "compact", "wide"])
     p.add_argument("--pointer-ilp", type=int, default=8, choices=[4, 8, 16])
-    p.add_argument("--p-split", type=float, default=None, help="tree generators: split probability per node")
+    p.add_argument("--p-split", type=float, default=None, help="rf generator: split probability per node (gbdt: fixed 0.9)")
+    p.add_argument("--xcd-split", default="off", choices=["on", "off"], help="pointer/hybrid: XCD tree slices")
+    p.add_argument("--cache-dir", default="", help="tree models: reuse the generated PMML text across runs")
+    p.add_argument("--splits", type=int, default=0, help="tree: force this many tree splits (0 = auto)")
     p.add_argument("--precision", default="fp32", choices=["fp32", "bf16", "fp8"])
     p.add_argument("--hidden", default="256,256", help="mlp hidden widths")
     p.add_argument("--mlp-kernel", default="auto", choices=["auto", "reg", "panel"], help="bf16 MLP kernel")
@@ -62,7 +65,14 @@ def main():
             res[name + "_GBps"] = Xh.numel() * 4 / dt / 1e9
         print(json.dumps({"model": "pcie", "bytes": Xh.numel() * 4, **res}))
         return
-    if args.model == "gbdt":
+    cache = None
+    if args.cache_dir and args.model.startswith(("gbdt", "rf")):
+        os.makedirs(args.cache_dir, exist_ok=True)
+        cache = os.path.join(args.cache_dir, f"{args.model}_{args.trees}_{args.depth}_{args.features}_{args.p_split}.pmml")
+    if cache and os.path.exists(cache):
+        with open(cache) as fh:
+            txt = fh.read()
+    elif args.model == "gbdt":
         txt = synth.gbdt_pmml(n_trees=args.trees, depth=args.depth, n_features=args.features)
     elif args.model == "gbdt-binary":
         txt = synth.gbdt_pmml(n_trees=args.trees, depth=args.depth, n_features=args.features, objective="binary")
@@ -81,13 +91,17 @@ def main():
         from flink_jpmml_amd.assets import kmeans_pmml
 
         txt = kmeans_pmml()
+    if cache and not os.path.exists(cache):
+        with open(cache, "w") as fh:
+            fh.write(txt)
     c = CompiledPmml.from_string(txt)
     opts = {}
     if args.model.startswith(("gbdt", "rf")):
         opts = dict(layout=args.layout, lds_budget=args.lds_budget, variant=args.variant, nan_mode=args.nan_mode,
                     max_chunk_trees=args.max_chunk_trees, head_depth=args.head_depth,
                     pointer_schedule=args.pointer_schedule, node_order=args.node_order,
-                    node_format=args.node_format, pointer_ilp=args.pointer_ilp)
+                    node_format=args.node_format, pointer_ilp=args.pointer_ilp, xcd_split=args.xcd_split,
+                    splits=args.splits)
     elif args.model == "kmeans-big":
         opts = dict(cluster_variant=args.variant)
     if args.precision != "fp32":
@@ -146,7 +160,8 @@ def main():
                       "layout": getattr(plan, "layout", None), "chunk_trees": getattr(plan, "chunk_trees", None),
                       "head_depth": getattr(plan, "head_depth", None), "depth": getattr(plan, "depth", None),
                       "pointer_schedule": args.pointer_schedule, "node_order": args.node_order, "node_format": args.node_format, "pointer_ilp": args.pointer_ilp,
-                      "trees": getattr(plan, "n_trees", None),
+                      "trees": getattr(plan, "n_trees", None), "xcd_split": getattr(plan, "xcd_split", None),
+                      "splits": plan._auto_splits(args.rows) if hasattr(plan, "_auto_splits") else None,
                       "missing": args.missing, "lds_budget": args.lds_budget,
                       "variant": getattr(plan, "variant", None), "mlp_prof": prof,
                       "mlp_kernel": ("reg" if getattr(plan, "reg_kernel", 0) else "panel") if args.model == "mlp" else None}))

@@ -43,7 +43,7 @@ def test_deep_random_forest_votes_on_gpu(gpu, depth):
                              p_split=0.8)
     c = CompiledPmml.from_string(txt.encode())
     plan = c.plan(gpu)
-    assert plan.layout == "hybrid" and plan.depth == depth
+    assert plan.layout == "pointer" and plan.depth == depth
     X = stream_matrix(50_000, 16, seed=8, missing_rate=0.02)
     s, v = _score(c, plan, X)
     ref, vref = c.score_matrix_oracle(X)
@@ -62,3 +62,36 @@ def test_wide_feature_deep_forest_global_features(gpu):
         s, v = _score(c, plan, X)
         assert (v == vref).all()
         np.testing.assert_allclose(s[v], ref[v], rtol=0, atol=5e-5)
+
+
+@pytest.mark.parametrize("opts", [dict(layout="pointer"), dict(layout="pointer", node_format="compact"),
+                                  dict(layout="pointer", pointer_schedule="refill"),
+                                  dict(layout="hybrid", head_depth=4)])
+@pytest.mark.parametrize("n_rows", [100_000, 777])
+def test_xcd_split_forest_on_gpu(gpu, opts, n_rows):
+    """XCD-aware tree slices (csrc ``tree_block``: workgroup L scores slice L % 8 of row block
+    L / 8) against the fp64 oracle and against the unsplit launch, incl. a ragged last row block."""
+    txt = gbdt_pmml(n_trees=40, depth=14, n_features=24, seed=11, p_split=0.8)
+    c = CompiledPmml.from_string(txt)
+    X = stream_matrix(n_rows, 24, seed=4, missing_rate=0.03)
+    ref, vref = c.score_matrix_oracle(X)
+    on = c.plan(gpu, xcd_split="on", **opts)
+    off = c.plan(gpu, xcd_split="off", **opts)
+    assert on.xcd_split == 8 and off.xcd_split == 0 and on._auto_splits(n_rows) == 8
+    s1, v1 = _score(c, on, X)
+    s0, v0 = _score(c, off, X)
+    assert (v1 == vref).all() and (v0 == vref).all()
+    np.testing.assert_allclose(s1[v1], ref[v1], rtol=0, atol=5e-5)
+    np.testing.assert_allclose(s1[v1], s0[v0], rtol=0, atol=5e-5)
+
+
+def test_xcd_split_vote_forest_on_gpu(gpu):
+    """Random-forest votes (P = 3 class slots accumulated in LDS) over XCD slices."""
+    txt = random_forest_pmml(n_trees=48, depth=14, n_features=16, n_classes=3, seed=9, p_split=0.8)
+    c = CompiledPmml.from_string(txt)
+    X = stream_matrix(60_000, 16, seed=1, missing_rate=0.02)
+    ref, vref = c.score_matrix_oracle(X)
+    plan = c.plan(gpu, layout="pointer", xcd_split="on")
+    s, v = _score(c, plan, X)
+    assert (v == vref).all()
+    np.testing.assert_array_equal(s[v], ref[v])

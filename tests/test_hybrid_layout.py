@@ -135,10 +135,25 @@ def test_deep_regression_forest_layouts_match_oracle(layout, head, fmt, missing)
     np.testing.assert_allclose(got[vref], ref[vref], rtol=0, atol=2e-4)
 
 
-def test_auto_layout_picks_hybrid_for_deep_forests():
+def test_auto_layout_picks_pointer_for_deep_forests():
+    """Deeper than the PERFECT layout's 10 levels -> the pointer walk (profiles/r3q: faster than
+    the hybrid head on 300 x depth-14 forests); the hybrid layout stays available on request."""
     c, plan = _plan(random_forest_pmml(n_trees=6, depth=14, n_features=16, n_classes=3, seed=2))
-    assert plan.layout == "hybrid" and plan.head_depth == 4 and plan.chunk_trees >= 1
+    assert plan.layout == "pointer" and plan.head_depth == 0 and plan.xcd_split == 0
     assert plan.general == 1  # class votes accumulate in LDS slots
+    _, hyb = _plan(random_forest_pmml(n_trees=6, depth=14, n_features=16, n_classes=3, seed=2), layout="hybrid")
+    assert hyb.layout == "hybrid" and hyb.head_depth == 4 and hyb.chunk_trees >= 1
+
+
+def test_xcd_split_option():
+    """XCD tree slices: opt-in, 8 slices (one per XCD) once the forest has >= 16 trees."""
+    txt = gbdt_pmml(n_trees=20, depth=12, n_features=8, seed=2, p_split=0.7)
+    _, on = _plan(txt, layout="pointer", xcd_split="on")
+    _, off = _plan(txt, layout="pointer")
+    assert on.xcd_split == 8 and on._auto_splits(1 << 20) == 8
+    assert off.xcd_split == 0 and off._auto_splits(1 << 20) == 1
+    with pytest.raises(ValueError):
+        _plan(txt, layout="pointer", xcd_split="maybe")
 
 
 def test_shallow_trees_and_stumps_in_the_head():
