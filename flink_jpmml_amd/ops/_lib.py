@@ -207,6 +207,11 @@ class SvmArgs(ctypes.Structure):
                 ("decision", c_void_p)]
 
 
+class SvmWideArgs(ctypes.Structure):
+    _fields_ = [("s", SvmArgs), ("svA", c_void_p), ("coefA", c_void_p), ("svnP", c_void_p), ("n_tiles", c_int),
+                ("n_mtiles", c_int), ("n_groups", c_int), ("pad", c_int)]
+
+
 class DeriveArgs(ctypes.Structure):
     _fields_ = [("X", c_void_p), ("n_rows", c_int), ("n_in", c_int), ("ldx", c_int), ("n_tile", c_int),
                 ("prep", c_void_p), ("prog", c_void_p), ("pool", c_void_p), ("out_cols", c_void_p),
@@ -225,6 +230,7 @@ _ABI = {
     "pmml_linear_args_size": LinearArgs,
     "pmml_mlp_args_size": MlpArgs,
     "pmml_svm_args_size": SvmArgs,
+    "pmml_svm_wide_args_size": SvmWideArgs,
 }
 
 _lib: Optional[ctypes.CDLL] = None
@@ -289,6 +295,9 @@ def load(auto_build: bool = True) -> ctypes.CDLL:
             lib.pmml_mlp_launch.argtypes = [c_void_p, ctypes.POINTER(MlpArgs), c_int]
         if hasattr(lib, "pmml_svm_launch"):
             lib.pmml_svm_launch.argtypes = [c_void_p, ctypes.POINTER(SvmArgs), c_int, c_int]
+        if hasattr(lib, "pmml_svm_wide_launch"):
+            lib.pmml_svm_wide_launch.restype = c_int
+            lib.pmml_svm_wide_launch.argtypes = [c_void_p, ctypes.POINTER(SvmWideArgs), c_int, c_int]
         lib.pmml_tree_general_launch.argtypes = [c_void_p, ctypes.POINTER(GenTreeArgs)]
         lib.pmml_tree_general_launch.restype = c_int
         lib.pmml_tree_hybrid_launch.argtypes = [c_void_p, ctypes.POINTER(HybridArgs), c_int, c_int]

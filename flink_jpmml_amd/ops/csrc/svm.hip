@@ -239,6 +239,184 @@ int launch_svm_mfma(hipStream_t stream, const SvmArgs& a, int n_svp, dim3 grid, 
     default: return launch_svm_mfma_k<FMAX, K_LINEAR>(stream, a, n_svp, grid, lds);
   }
 }
+
+// ------------------------------------------------------------------------------------------
+// Wide SVM kernel: any number of machines (one-against-one over many classes), up to 64 classes,
+// up to 128 vector fields, any number of support vectors — the chained two-GEMM form of the
+// decision function fused in one pass, both GEMMs on the exact-fp32 matrix cores:
+//   G^T = S . X^T      (32 support vectors x 32 rows per MFMA tile, K = fields)
+//   K   = kfun(G)      (on the accumulator registers, VALU)
+//   D^T = A^T . K^T    (32 machines x 32 rows per tile, K = support vectors)
+// The first product's accumulator IS the second product's B operand: lane l of the G tile holds
+// G[sv p(i, l>>5)][row l&31] for i < 16 (p(i, h) = (i&3) + 8(i>>2) + 4h), and MFMA step j of the
+// second product takes k = l>>5 — so step j feeds register j of every lane as B, and the host
+// permutes the dual coefficients to match (A operand of lane l at step j = coef[p(j, l>>5)][l&31]).
+// No [rows x support vectors] kernel matrix ever leaves the registers (the library-GEMM plan
+// writes and re-reads it through HBM). Operands are pre-swizzled on the host so each lane streams
+// contiguous 16-byte loads: svA [tile][lane][FMAX/2], coefA [tile][mtile][lane][16], svnP
+// [tile][half][16]. Machines run in groups of MT tiles (acc registers); a model with more
+// machines loops over groups, recomputing G per group. Votes go to packed u16 LDS counters.
+struct SvmWideArgs {
+  SvmArgs s;              // rows, preparation, intercept / thr / tgt / alt ([n_groups*MT*32]), outputs
+  const float* svA;       // [n_tiles][64][FMAX/2]
+  const float* coefA;     // [n_tiles][n_mtiles][64][16]
+  const float* svnP;      // [n_tiles][2][16]
+  int n_tiles, n_mtiles, n_groups, pad;
+};
+
+constexpr int WTB = 512;  // wide kernel: 8 waves x 32 rows (one MFMA N tile per wave) = TB rows
+
+template <int FMAX, int MT>
+__global__ __launch_bounds__(WTB) void svm_wide_kernel(SvmWideArgs w) {
+  const SvmArgs& a = w.s;
+  constexpr int Q = FMAX / 2;
+  extern __shared__ __align__(16) uint32_t votes[];  // [TB][CW] packed u16 class counters
+  const int CW = (a.n_classes + 1) >> 1;
+  const int tid = threadIdx.x, lane = tid & 63, half = lane >> 5, l31 = lane & 31;
+  const int rl = (tid >> 6) * 32 + l31;  // this lane's row within the tile (both halves share it)
+  const int row = blockIdx.x * TB + rl;
+  for (int e = tid; e < TB * CW; e += WTB) votes[e] = 0u;
+  // B operand of the first product: vector field 2q + half of the row (prepared, zero padded)
+  float xb[Q];
+  bool bad;
+  float xx;
+  {
+    const float* xr = a.X + (size_t)min(row, a.n_rows - 1) * a.ldx;
+    bool b = false;
+    if (a.prep)  // row rejection by ANY active field's preparation (the halves split the columns)
+      for (int c = half; c < a.n_feat; c += 2) (void)prep_value(xr[c], a.prep[c], &b);
+    float sq = 0.f;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int f = 2 * q + half;
+      float x = 0.f;
+      if (f < a.n_in) {
+        const int c = a.in_index[f];
+        x = xr[c];
+        if (a.prep) x = prep_value(x, a.prep[c], &b);
+        if (x != x) { b = true; x = 0.f; }  // a missing vector field invalidates the row
+      }
+      xb[q] = x;
+      sq = fmaf(x, x, sq);
+    }
+    xx = sq + __shfl_xor(sq, 32);
+    const uint64_t mb = __ballot(b);
+    bad = (((mb >> l31) | (mb >> (l31 + 32))) & 1ull) != 0ull;
+  }
+  __syncthreads();  // vote counters zeroed
+  const int M = a.n_machines;
+  float reg = 0.f;
+  for (int g = 0; g < w.n_groups; ++g) {
+    f32x16_t acc[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x16_t{};
+    for (int t = 0; t < w.n_tiles; ++t) {
+      f32x16_t d = {};
+      const float* sa = w.svA + ((size_t)t * 64 + lane) * Q;
+#pragma unroll
+      for (int q0 = 0; q0 < Q; q0 += 4) {
+        const float4 v = *reinterpret_cast<const float4*>(sa + q0);
+        d = __builtin_amdgcn_mfma_f32_32x32x2f32(v.x, xb[q0], d, 0, 0, 0);
+        d = __builtin_amdgcn_mfma_f32_32x32x2f32(v.y, xb[q0 + 1], d, 0, 0, 0);
+        d = __builtin_amdgcn_mfma_f32_32x32x2f32(v.z, xb[q0 + 2], d, 0, 0, 0);
+        d = __builtin_amdgcn_mfma_f32_32x32x2f32(v.w, xb[q0 + 3], d, 0, 0, 0);
+      }
+      // kernel function in place: register i <-> support vector 32t + p(i, half)
+      const float* sn = w.svnP + ((size_t)t * 2 + half) * 16;
+      switch (a.kernel) {  // wave-uniform
+        case K_POLY:
+#pragma unroll
+          for (int i = 0; i < 16; ++i) d[i] = svm_kernel_t<K_POLY>(a, d[i], xx, 0.f);
+          break;
+        case K_RBF:
+#pragma unroll
+          for (int i = 0; i < 16; ++i) d[i] = svm_kernel_t<K_RBF>(a, d[i], xx, sn[i]);
+          break;
+        case K_SIGMOID:
+#pragma unroll
+          for (int i = 0; i < 16; ++i) d[i] = svm_kernel_t<K_SIGMOID>(a, d[i], xx, 0.f);
+          break;
+        default:
+          break;
+      }
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const float4* ca = reinterpret_cast<const float4*>(
+            w.coefA + (((size_t)t * w.n_mtiles + g * MT + mt) * 64 + lane) * 16);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float4 c = ca[u];
+          acc[mt] = __builtin_amdgcn_mfma_f32_32x32x2f32(c.x, d[4 * u], acc[mt], 0, 0, 0);
+          acc[mt] = __builtin_amdgcn_mfma_f32_32x32x2f32(c.y, d[4 * u + 1], acc[mt], 0, 0, 0);
+          acc[mt] = __builtin_amdgcn_mfma_f32_32x32x2f32(c.z, d[4 * u + 2], acc[mt], 0, 0, 0);
+          acc[mt] = __builtin_amdgcn_mfma_f32_32x32x2f32(c.w, d[4 * u + 3], acc[mt], 0, 0, 0);
+        }
+      }
+    }
+    // this group's decision values: the lane holds machines (g*MT + mt)*32 + p(i, half) of its row
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int m = (g * MT + mt) * 32 + (i & 3) + 8 * (i >> 2) + 4 * half;
+        if (m >= M) continue;
+        const float dv = acc[mt][i] + a.intercept[m];
+        if (a.decision && row < a.n_rows) a.decision[(size_t)row * M + m] = dv;
+        if (!a.classification) {
+          reg = dv;  // M == 1: machine 0 sits in half 0, register 0
+          continue;
+        }
+        bool first = dv < a.thr[m];
+        if (a.max_wins) first = !first;
+        const int c = first ? a.tgt[m] : a.alt[m];
+        if (c >= 0) atomicAdd(&votes[rl * CW + (c >> 1)], 1u << (16 * (c & 1)));
+      }
+    }
+  }
+  __syncthreads();
+  if (half != 0 || row >= a.n_rows) return;
+  float sc;
+  if (a.classification) {
+    int best = 0;
+    uint32_t bv = votes[rl * CW] & 0xFFFFu;
+    for (int c = 1; c < a.n_classes; ++c) {
+      const uint32_t v = (votes[rl * CW + (c >> 1)] >> (16 * (c & 1))) & 0xFFFFu;
+      if (v > bv) { bv = v; best = c; }  // ties: the first category
+    }
+    sc = a.epi.table[best];
+  } else {
+    sc = reg;
+  }
+  const bool ok = !bad && (sc == sc);
+  const float so = ok ? sc : __builtin_nanf("");
+  a.score[row] = so;
+  a.valid[row] = ok ? 1 : 0;
+  if (a.epi.score2) {
+    a.epi.score2[row] = so;
+    a.epi.valid2[row] = ok ? 1 : 0;
+  }
+}
+
+template <int FMAX, int MT>
+int launch_svm_wide_t(hipStream_t stream, const SvmWideArgs& w, dim3 grid, size_t lds) {
+  auto k = svm_wide_kernel<FMAX, MT>;
+  if (lds > 65536 &&
+      hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+          hipSuccess)
+    return -5;
+  hipLaunchKernelGGL(k, grid, dim3(WTB), lds, stream, w);
+  return hipGetLastError() == hipSuccess ? 0 : -7;
+}
+
+template <int FMAX>
+int launch_svm_wide_f(hipStream_t stream, const SvmWideArgs& w, int mt, dim3 grid, size_t lds) {
+  switch (mt) {
+    case 1: return launch_svm_wide_t<FMAX, 1>(stream, w, grid, lds);
+    case 2: return launch_svm_wide_t<FMAX, 2>(stream, w, grid, lds);
+    case 4: return launch_svm_wide_t<FMAX, 4>(stream, w, grid, lds);
+    default: return -6;
+  }
+}
 }  // namespace
 
 PMML_API int pmml_svm_args_size() { return (int)sizeof(SvmArgs); }
@@ -267,4 +445,27 @@ PMML_API int pmml_svm_launch(hipStream_t stream, const SvmArgs* args, int fmax, 
     default: return -6;
   }
   return hipGetLastError() == hipSuccess ? 0 : -7;
+}
+
+PMML_API int pmml_svm_wide_args_size() { return (int)sizeof(SvmWideArgs); }
+
+// fmax in {16, 32, 64, 128} (vector fields padded), mt in {1, 2, 4} (machine tiles per group);
+// intercept / thr / tgt / alt hold n_groups * mt * 32 entries; n_classes <= 64.
+PMML_API int pmml_svm_wide_launch(hipStream_t stream, const SvmWideArgs* args, int fmax, int mt) {
+  const SvmWideArgs w = *args;
+  const SvmArgs& a = w.s;
+  if (a.n_rows <= 0) return 0;
+  if (a.n_in > fmax || a.n_classes > 64 || (a.classification && a.n_classes < 1)) return -4;
+  if (w.n_tiles < 1 || w.n_groups < 1 || w.n_mtiles != w.n_groups * mt || a.n_machines > w.n_mtiles * 32) return -4;
+  if (!a.classification && a.n_machines != 1) return -4;
+  if (a.kernel < 0 || a.kernel > 3) return -4;
+  dim3 grid((a.n_rows + TB - 1) / TB);
+  const size_t lds = (size_t)TB * ((a.n_classes + 1) / 2 > 0 ? (a.n_classes + 1) / 2 : 1) * 4;
+  switch (fmax) {
+    case 16: return launch_svm_wide_f<16>(stream, w, mt, grid, lds);
+    case 32: return launch_svm_wide_f<32>(stream, w, mt, grid, lds);
+    case 64: return launch_svm_wide_f<64>(stream, w, mt, grid, lds);
+    case 128: return launch_svm_wide_f<128>(stream, w, mt, grid, lds);
+    default: return -6;
+  }
 }

@@ -548,6 +548,136 @@ class SvmPlan(DevicePlan):
                                        getattr(self, "n_svp", 0)), "svm kernel")
 
 
+def _pperm(i, h):
+    """Row of a 32x32 MFMA accumulator held in register ``i`` by lane half ``h`` (csrc svm.hip)."""
+    return (i & 3) + 8 * (i >> 2) + 4 * h
+
+
+class SvmWidePlan(DevicePlan):
+    """SupportVectorMachineModel beyond the fused kernel's limits — one-against-one over up to 64
+    classes (any number of machines), up to 128 vector fields, any number of support vectors — on
+    ``svm_wide_kernel`` (``ops/csrc/svm.hip``): the decision function as two chained exact-fp32
+    MFMA products (``G = S·xᵀ`` → kernel function on the accumulators → ``D = Aᵀ·K``) fused in
+    one pass, votes in LDS; the [rows x support vectors] kernel matrix never leaves the registers.
+
+    Host side: the support vectors, squared norms and dual coefficients are pre-swizzled so each
+    lane streams contiguous 16-byte loads in the order the MFMA fragments consume them (the
+    second product's B operand is the first product's accumulator register file, so the dual
+    coefficients are permuted by the accumulator row map :func:`_pperm`). Parity: the oracle's
+    ``models/svm.py::SvmEvaluator.decision_values/finish``."""
+
+    kind = "svm_wide"
+    supports_direct = True
+    FMAXES = (16, 32, 64, 128)
+    CMAX = 64
+    _KERNELS = SvmPlan._KERNELS
+    _STATE = DevicePlan._STATE + ("in_index", "svA", "coefA", "svnP", "intercept", "thr", "tgt", "alt", "n_in",
+                                  "n_sv", "n_machines", "kernel_code", "classification", "gamma", "coef0", "degree",
+                                  "max_wins", "n_classes", "table", "fmax", "mt", "n_tiles", "n_groups")
+
+    def __init__(self, compiled, device):
+        from ..models.svm import SvmEvaluator
+
+        super().__init__(compiled, device)
+        ev: SvmEvaluator = compiled.evaluator
+        sm = ev.sm
+        fields = ev.fields
+        for f in fields:
+            if f not in compiled.active_fields:
+                raise NotLowerable(f"SVM vector field {f!r} is not an active field")
+        F = len(fields)
+        self.fmax = next((b for b in self.FMAXES if F <= b), None)
+        if self.fmax is None:
+            raise NotLowerable(f"SVM with more than {self.FMAXES[-1]} vector fields (wide kernel)")
+        M = len(sm.machines)
+        if sm.representation == "Coefficients":
+            S, A, kind = ev.linear_coef.T, np.eye(M), "linear"
+        else:
+            S, A, kind = ev.S, ev.A, sm.kernel.kind
+        if kind not in self._KERNELS:
+            raise NotLowerable(f"SVM kernel {kind!r}")
+        self.classification = 1 if ev.kind == "classification" else 0
+        if not self.classification and M != 1:
+            raise NotLowerable("regression SVM must have one machine")
+        nsv = S.shape[0]
+        self.n_sv, self.n_in, self.n_machines = nsv, F, M
+        self.mt = 1 if M <= 32 else 2 if M <= 64 else 4
+        self.n_groups = -(-M // (32 * self.mt))
+        n_mtiles = self.n_groups * self.mt
+        self.n_tiles = max(1, -(-nsv // 32))
+        Sp = np.zeros((self.n_tiles * 32, self.fmax), np.float64)
+        Sp[:nsv, :F] = S
+        Ap = np.zeros((self.n_tiles * 32, n_mtiles * 32), np.float64)
+        Ap[:nsv, :M] = A
+        lane = np.arange(64)
+        q = np.arange(self.fmax // 2)
+        # svA[t, lane, q] = S[32t + (lane & 31), 2q + (lane >> 5)]
+        rows = (np.arange(self.n_tiles)[:, None, None] * 32 + (lane & 31)[None, :, None])
+        cols = 2 * q[None, None, :] + (lane >> 5)[None, :, None]
+        self.svA = self._t(Sp[rows, cols].astype(np.float32))
+        # coefA[t, mtile, lane, j] = A[32t + p(j, lane >> 5), 32 mtile + (lane & 31)]
+        j = np.arange(16)
+        sv_idx = (np.arange(self.n_tiles)[:, None, None, None] * 32
+                  + _pperm(j[None, None, None, :], (lane >> 5)[None, None, :, None]))
+        m_idx = np.arange(n_mtiles)[None, :, None, None] * 32 + (lane & 31)[None, None, :, None]
+        self.coefA = self._t(Ap[sv_idx, m_idx].astype(np.float32))
+        # svnP[t, h, i] = |S[32t + p(i, h)]|^2 (RBF)
+        norms = (Sp.astype(np.float32).astype(np.float64) ** 2).sum(1).astype(np.float32)
+        nidx = (np.arange(self.n_tiles)[:, None, None] * 32
+                + _pperm(np.arange(16)[None, None, :], np.arange(2)[None, :, None]))
+        self.svnP = self._t(norms[nidx])
+        pad = n_mtiles * 32
+        ic = np.zeros(pad, np.float32)
+        ic[:M] = ev.b
+        self.intercept = self._t(ic)
+        self.in_index = self._t(np.array([compiled.active_fields.index(f) for f in fields], np.int32))
+        self.kernel_code = self._KERNELS[kind]
+        k = sm.kernel
+        self.gamma, self.coef0, self.degree = float(k.gamma), float(k.coef0), float(k.degree)
+        self.max_wins = 1 if sm.max_wins else 0
+        thr = np.zeros(pad, np.float32)
+        tgt = np.full(pad, -1, np.int32)
+        alt = np.full(pad, -1, np.int32)
+        if self.classification:
+            cats = ev.categories
+            if len(cats) > self.CMAX:
+                raise NotLowerable(f"more than {self.CMAX} SVM classes (wide kernel vote counters)")
+            for m, mach in enumerate(sm.machines):
+                thr[m] = mach.threshold if mach.threshold is not None else sm.threshold
+                tgt[m] = cats.index(mach.target_category)
+                if mach.alternate_target_category is not None:
+                    alt[m] = cats.index(mach.alternate_target_category)
+            self.table = self._t(_label_table(cats))
+            self.n_classes = len(cats)
+        else:
+            self.table = None
+            self.n_classes = 0
+        self.thr, self.tgt, self.alt = self._t(thr), self._t(tgt), self._t(alt)
+
+    def launch(self, X, score, valid, stream=None, probs=None, score2=None, valid2=None, decision=None) -> None:
+        import ctypes
+
+        from ..ops._lib import SvmWideArgs, check, ptr, stream_handle
+
+        w = SvmWideArgs()
+        a = w.s
+        a.X = X.data_ptr()
+        a.n_rows, a.n_feat, a.ldx, a.n_sv = X.shape[0], X.shape[1], X.stride(0), self.n_sv
+        a.prep, a.in_index = ptr(self.prep), ptr(self.in_index)
+        a.intercept, a.thr, a.tgt, a.alt = ptr(self.intercept), ptr(self.thr), ptr(self.tgt), ptr(self.alt)
+        a.n_in, a.n_machines, a.kernel, a.classification = self.n_in, self.n_machines, self.kernel_code, \
+            self.classification
+        a.gamma, a.coef0, a.degree = self.gamma, self.coef0, self.degree
+        a.max_wins, a.n_classes = self.max_wins, self.n_classes
+        a.epi = _epilogue(mode=EPI_AFFINE, table=self.table)
+        a.epi.score2, a.epi.valid2 = _addr(score2), _addr(valid2)
+        a.score, a.valid, a.decision = _addr(score), _addr(valid), ptr(decision)
+        w.svA, w.coefA, w.svnP = ptr(self.svA), ptr(self.coefA), ptr(self.svnP)
+        w.n_tiles, w.n_mtiles, w.n_groups = self.n_tiles, self.n_groups * self.mt, self.n_groups
+        check(self.lib.pmml_svm_wide_launch(stream_handle(stream), ctypes.byref(w), self.fmax, self.mt),
+              "svm wide kernel")
+
+
 class SvmGemmPlan(DevicePlan):
     """SupportVectorMachineModel as two library GEMMs on the matrix cores (hipBLASLt, fp32):
     ``G = X·Sᵀ`` → kernel function (element-wise) → ``D = K·A + b`` (``A`` = dual coefficients of

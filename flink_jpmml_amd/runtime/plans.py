@@ -1757,14 +1757,22 @@ def compile_plan(compiled, device, **opts) -> DevicePlan:
                 return WideMlpPlan(compiled, device, precision=prec)
             return GemmMlpPlan(compiled, device, precision=prec)
     if isinstance(ev, SvmEvaluator):
-        from .nn_plans import SvmGemmPlan, SvmPlan
+        from .nn_plans import SvmGemmPlan, SvmPlan, SvmWidePlan
 
-        impl = opts.pop("svm_impl", "auto")  # auto | fused | gemm
-        if impl != "gemm":
+        impl = opts.pop("svm_impl", "auto")  # auto | fused | wide | gemm
+        if impl not in ("auto", "fused", "wide", "gemm"):
+            raise ValueError("svm_impl must be auto, fused, wide or gemm")
+        if impl in ("auto", "fused"):
             try:
                 return SvmPlan(compiled, device)
             except NotLowerable:
                 if impl == "fused":
+                    raise
+        if impl in ("auto", "wide"):
+            try:  # many machines / classes / fields: the two-GEMM fused MFMA kernel
+                return SvmWidePlan(compiled, device)
+            except NotLowerable:
+                if impl == "wide":
                     raise
         return _with_prepared_inputs(compiled, device, lambda c: SvmGemmPlan(c, device),
                                      dict(opts, svm_impl="gemm"))

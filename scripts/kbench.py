@@ -26,6 +26,9 @@ def main():
     p.add_argument("--variant", default="auto")
     p.add_argument("--mlp-prof", action="store_true", help="MLP: per-phase s_memtime ticks of workgroup 0")
     p.add_argument("--clusters", type=int, default=256)
+    p.add_argument("--n-sv", type=int, default=256, help="svm: support vectors")
+    p.add_argument("--classes", type=int, default=2, help="svm: classes (> 2: one-against-one machines)")
+    p.add_argument("--svm-impl", default="auto", choices=["auto", "fused", "wide", "gemm"])
     p.add_argument("--nan-mode", default="auto")
     p.add_argument("--tree-prof", action="store_true", help="tree: per-wave phase ticks of one workgroup")
     p.add_argument("--max-chunk-trees", type=int, default=0)
@@ -82,7 +85,7 @@ def main():
     elif args.model == "mlp":
         txt = synth.mlp_pmml(n_features=args.features, hidden=tuple(int(x) for x in args.hidden.split(",")))
     elif args.model == "svm":
-        txt = synth.svm_pmml(n_features=args.features)
+        txt = synth.svm_pmml(n_features=args.features, n_sv=args.n_sv, n_classes=args.classes, gamma=0.05)
     elif args.model == "kmeans-big":
         txt = synth.kmeans_pmml(n_clusters=args.clusters, n_features=args.features, weighted=True)
     elif args.model == "lr":
@@ -104,6 +107,8 @@ def main():
                     splits=args.splits)
     elif args.model == "kmeans-big":
         opts = dict(cluster_variant=args.variant)
+    elif args.model == "svm" and args.svm_impl != "auto":
+        opts = dict(svm_impl=args.svm_impl)
     if args.precision != "fp32":
         opts["precision"] = args.precision
     if args.model == "mlp" and args.mlp_impl != "auto":
@@ -154,6 +159,8 @@ def main():
     if args.model == "mlp":
         dims = [F] + [int(x) for x in args.hidden.split(",")] + [1]
         flops = 2.0 * args.rows * sum(a * b for a, b in zip(dims[:-1], dims[1:]))
+    elif args.model == "svm" and type(plan).__name__ == "SvmWidePlan":  # the MFMA work as issued (padded)
+        flops = 2.0 * args.rows * plan.n_tiles * 32 * (plan.fmax + plan.n_groups * plan.mt * 32)
     print(json.dumps({"model": args.model, "rows": args.rows, "features": F, "ms": ms,
                       "tflops": (flops / ms / 1e9) if flops else None, "precision": args.precision,
                       "rows_per_s": args.rows / ms * 1e3, "plan": type(plan).__name__,

@@ -36,7 +36,7 @@ def test_iris_logistic_probs_and_argmax(gpu):
     assert agree > 0.9999  # fp32 vs fp64 near-ties only
 
 
-@pytest.mark.parametrize("n_classes,kind", [(3, "SvmPlan"), (5, "SvmGemmPlan")])
+@pytest.mark.parametrize("n_classes,kind", [(3, "SvmPlan"), (5, "SvmWidePlan"), (20, "SvmWidePlan")])
 def test_one_against_one_svm_on_gpu(gpu, n_classes, kind):
     from flink_jpmml_amd.bench.synth import stream_matrix, svm_pmml
     from flink_jpmml_amd.runtime.compiled import CompiledPmml
@@ -50,3 +50,43 @@ def test_one_against_one_svm_on_gpu(gpu, n_classes, kind):
     ref, vref = c.score_matrix_oracle(X)
     assert (v == vref).all()
     assert (s[v] == ref[v]).mean() > 0.999
+
+
+@pytest.mark.parametrize("kernel", ["radialBasis", "linear", "polynomial", "sigmoid"])
+@pytest.mark.parametrize("n_classes,n_feat,n_rows", [(7, 24, 40_000), (12, 70, 20_000), (24, 16, 777)])
+def test_wide_svm_kernel_on_gpu(gpu, kernel, n_classes, n_feat, n_rows):
+    """svm_wide_kernel (two chained exact-fp32 MFMA products, LDS votes) against the fp64 oracle
+    and the library-GEMM plan: 21 / 66 / 276 machines (1 group of 1 tile, 1 group of 4 tiles,
+    3 groups of 4 tiles), 24 / 70 / 16 fields, a ragged last tile."""
+    from flink_jpmml_amd.bench.synth import stream_matrix, svm_pmml
+    from flink_jpmml_amd.runtime.compiled import CompiledPmml
+
+    c = CompiledPmml.from_string(svm_pmml(n_features=n_feat, n_sv=150, seed=8, kernel=kernel, n_classes=n_classes,
+                                          gamma=0.08))
+    plan = c.plan(gpu)
+    assert type(plan).__name__ == "SvmWidePlan"
+    X = stream_matrix(n_rows, n_feat, seed=5, missing_rate=0.01)
+    s, v = plan.score(X)
+    s, v = s.cpu().numpy(), v.cpu().numpy().astype(bool)
+    ref, vref = c.score_matrix_oracle(X)
+    assert (v == vref).all()
+    assert (s[v] == ref[v]).mean() > 0.998
+    g = c.plan(gpu, svm_impl="gemm")
+    sg, vg = g.score(X)
+    sg = sg.cpu().numpy()
+    assert (s[v] == sg[v]).mean() > 0.998
+
+
+def test_wide_regression_svm_on_gpu(gpu):
+    from flink_jpmml_amd.bench.synth import stream_matrix, svm_pmml
+    from flink_jpmml_amd.runtime.compiled import CompiledPmml
+
+    c = CompiledPmml.from_string(svm_pmml(n_features=100, n_sv=300, seed=1, classification=False, gamma=0.01))
+    plan = c.plan(gpu)
+    assert type(plan).__name__ == "SvmWidePlan" and plan.fmax == 128
+    X = stream_matrix(50_000, 100, seed=3, missing_rate=0.005)
+    s, v = plan.score(X)
+    s, v = s.cpu().numpy(), v.cpu().numpy().astype(bool)
+    ref, vref = c.score_matrix_oracle(X)
+    assert (v == vref).all()
+    np.testing.assert_allclose(s[v], ref[v], rtol=1e-4, atol=1e-4)

@@ -1,6 +1,6 @@
-"""SVMs beyond the fused VALU kernel (more than 8 machines — one-against-one over many classes —
-or more than 64 vector fields) lower to :class:`SvmGemmPlan`: two fp32 GEMMs + element-wise kernel
-+ vote product. Its tensor program runs on the host in a lowering dry run and must match the
+"""The library-GEMM SVM plan (:class:`SvmGemmPlan`: two fp32 GEMMs + element-wise kernel + vote
+product) — the fallback beyond the wide MFMA kernel's limits (> 128 vector fields or > 64
+classes), and ``svm_impl="gemm"`` on request. Its tensor program runs on the host in a lowering dry run and must match the
 float64 oracle (tests/test_gpu_kernels.py runs it on the MI355X)."""
 
 import numpy as np
@@ -25,7 +25,7 @@ def test_one_against_one_many_classes(kernel):
     c = CompiledPmml.from_string(svm_pmml(n_features=10, n_sv=150, seed=4, kernel=kernel, n_classes=5))
     assert len(c.evaluator.sm.machines) == 10  # > 8: beyond the fused kernel
     X = stream_matrix(3000, 10, seed=2, missing_rate=0.01)
-    plan, s, v = _score(c, X)
+    plan, s, v = _score(c, X, svm_impl="gemm")
     assert isinstance(plan, SvmGemmPlan)
     ref, vref = c.score_matrix_oracle(X)
     assert (v == vref).all()
@@ -35,8 +35,8 @@ def test_one_against_one_many_classes(kernel):
 def test_wide_regression_svm_and_forced_gemm():
     c = CompiledPmml.from_string(svm_pmml(n_features=80, n_sv=64, seed=1, classification=False))
     X = stream_matrix(2000, 80, seed=3)
-    plan, s, v = _score(c, X)
-    assert isinstance(plan, SvmGemmPlan)  # 80 vector fields > 64
+    plan, s, v = _score(c, X, svm_impl="gemm")
+    assert isinstance(plan, SvmGemmPlan)
     ref, vref = c.score_matrix_oracle(X)
     assert (v == vref).all()
     np.testing.assert_allclose(s, ref, rtol=1e-4, atol=1e-4)
