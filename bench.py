@@ -251,7 +251,9 @@ def main(argv=None) -> int:
 
     numa_node = None if args.no_numa else bind_to_gpu_numa(device.index or 0)
     X = torch.from_numpy(stream_matrix(args.rows, args.features, seed=1000 + ctx.rank)).pin_memory()
-    gather = N > 1 and not args.no_allgather
+    # every distributed run all-gathers (a 1-rank RCCL group under --force-dist takes the same
+    # device-mirror / RCCL path as N > 1)
+    gather = ctx.is_distributed and not args.no_allgather
     timing = {}
 
     def barrier_sync():
@@ -274,7 +276,7 @@ def main(argv=None) -> int:
         env = StreamExecutionEnvironment(config=cfg, dist_ctx=ctx if ctx.is_distributed else None)
         # the library F5 sink: waits for every scored batch; with N > 1 all-gathers the device
         # mirrors over RCCL on its comm stream, overlapping the next batch
-        sink = GatherSink(to="all", lockstep=True, keep=False) if gather or N == 1 else _WaitSink()
+        sink = GatherSink(to="all", lockstep=True, keep=False) if gather or not ctx.is_distributed else _WaitSink()
         op_cfg = cfg.replace(device_mirror=gather)
         if args.source == "synthetic":
             src = _StepSource(X, args.warmup + args.steps, args.passes, on_step)
