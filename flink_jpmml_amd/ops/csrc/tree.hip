@@ -7,7 +7,9 @@ namespace {
 // Pointer layout: nodes uint4 {T bits, meta, left, right}; child < 0 => leaf ~child.
 // meta: feature byte offset (or index when features stay in global memory) | bit 30 null-on-
 // missing | bit 31 default right.
-template <bool GENERAL, bool FEAT_LDS, int PILP = 8>
+// MASKED: finished walks skip their load (exec-masked) instead of re-loading node 0 — the vector
+// memory pipe then only processes the lanes still walking.
+template <bool GENERAL, bool FEAT_LDS, int PILP = 8, bool MASKED = false>
 __global__ __launch_bounds__(TB, 2) void tree_pointer_kernel(TreeArgs a) {
   extern __shared__ __align__(16) uint32_t smem[];
   float* feat = reinterpret_cast<float*>(smem);
@@ -62,7 +64,14 @@ __global__ __launch_bounds__(TB, 2) void tree_pointer_kernel(TreeArgs a) {
     while (live) {
       uint4 nd[PILP];
 #pragma unroll
-      for (int i = 0; i < PILP; ++i) nd[i] = nodes[max(code[i], 0)];
+      for (int i = 0; i < PILP; ++i) {
+        if (MASKED) {
+          nd[i] = make_uint4(0u, 0u, 0u, 0u);
+          if (code[i] >= 0) nd[i] = nodes[code[i]];
+        } else {
+          nd[i] = nodes[max(code[i], 0)];
+        }
+      }
       live = false;
 #pragma unroll
       for (int i = 0; i < PILP; ++i) {  // branch-free: finished walks compute on node 0 and keep their leaf
@@ -181,6 +190,108 @@ __global__ __launch_bounds__(TB, 2) void tree_compact_kernel(TreeArgs a) {
         for (int p = 0; p < a.P; ++p) accl[(slot + p) * TB + tid] += a.leaves[(size_t)lv * a.P + p];
       } else {
         acc += __uint_as_float(lv);
+      }
+    }
+  }
+  finish_row(a, acc, accl, split, GENERAL, row, row_ok && !poisoned);
+}
+
+// SUPER pointer layout (runtime/hybrid.py::pack_super): two tree levels per 16-byte load. The
+// deep-forest walk is bound by the vector memory pipe's cost per gather INSTRUCTION (profiles/r3u:
+// ~20 TA cycles per 64-lane load, the same for 8- and 16-byte lanes and for exec-masked lanes), so
+// a slot {T_j, T_l | leaf, T_r | leaf, meta} that carries a split and both children's splits halves
+// the loads of a walk. Per step: x_j (LDS) picks the child c, x_c (LDS) picks the grandchild, the
+// next slot is base + 1 + 4 * block + 2 (c == r) + (x_c >= T_c). meta: f_j | f_l << 5 | f_r << 10
+// (LDS planes, <= 32 features) | l-leaf 15 | r-leaf 16 | self-leaf 17 | default-right j / l / r
+// 18-20 | grandchild block 21-31. Root words: tree base slot | nullPrediction flag << 31. Lock-step
+// walks, leaves accumulated in tree order (bit-identical to tree_pointer_kernel).
+constexpr uint32_t SN_LLEAF = 1u << 15, SN_RLEAF = 1u << 16, SN_SELF = 1u << 17;
+constexpr uint32_t SN_DRJ = 1u << 18, SN_DRL = 1u << 19, SN_DRR = 1u << 20;
+
+template <bool GENERAL, int PILP = 8>
+__global__ __launch_bounds__(TB, 2) void tree_super_kernel(TreeArgs a) {
+  extern __shared__ __align__(16) uint32_t smem[];
+  float* feat = reinterpret_cast<float*>(smem);
+  int* bad = reinterpret_cast<int*>(smem + a.n_feat * TB);
+  float* accl = reinterpret_cast<float*>(bad + TB);
+  const int tid = threadIdx.x;
+  const int2 blk = tree_block(a);
+  const int row0 = blk.x * TB;
+  const int split = blk.y;
+  const int row = row0 + tid;
+  stage_rows_T<TB>(a.X, a.n_rows, a.n_feat, a.ldx, a.prep, feat, bad, row0);
+  bool row_ok = bad[tid] == 0;
+  if (a.row_valid_in && row < a.n_rows) row_ok = row_ok && a.row_valid_in[row];
+  const uint4* nodes = reinterpret_cast<const uint4*>(a.blob);
+  const uint32_t* roots = reinterpret_cast<const uint32_t*>(a.roots);
+  const int tb = split * a.trees_per_split;
+  const int te = min(a.n_trees, tb + a.trees_per_split);
+  if (GENERAL) {
+    for (int c = 0; c < a.C; ++c) accl[c * TB + tid] = 0.f;
+  }
+  float acc = 0.f;
+  bool poisoned = false;
+  const char* feat_lane = reinterpret_cast<const char*>(feat + tid);
+  for (int t0 = tb; t0 < te; t0 += PILP) {
+    const int nt = min(PILP, te - t0);
+    int pos[PILP], base[PILP];
+    uint32_t leafv[PILP];
+    bool act[PILP], pz[PILP], nul[PILP];
+#pragma unroll
+    for (int i = 0; i < PILP; ++i) {
+      const uint32_t r = i < nt ? roots[t0 + i] : 0u;
+      base[i] = (int)(r & 0x7FFFFFFFu);
+      pos[i] = base[i];
+      nul[i] = (r >> 31) != 0u;
+      act[i] = i < nt;
+      pz[i] = false;
+      leafv[i] = 0u;
+    }
+    bool live = nt > 0;
+    while (live) {
+      uint4 nd[PILP];
+#pragma unroll
+      for (int i = 0; i < PILP; ++i) nd[i] = nodes[act[i] ? pos[i] : 0];
+      live = false;
+#pragma unroll
+      for (int i = 0; i < PILP; ++i) {
+        const uint32_t m = nd[i].w;
+        const bool self_leaf = (m & SN_SELF) != 0u;
+        // the three feature reads are independent (both children's features read speculatively):
+        // one LDS round trip per step instead of two dependent ones
+        const float xj = *reinterpret_cast<const float*>(feat_lane + ((m & 31u) << 10));
+        const float xl = *reinterpret_cast<const float*>(feat_lane + (((m >> 5) & 31u) << 10));
+        const float xr = *reinterpret_cast<const float*>(feat_lane + (((m >> 10) & 31u) << 10));
+        const bool nj = (xj != xj);
+        const bool r1 = (xj >= __uint_as_float(nd[i].x)) || (nj && (m & SN_DRJ));
+        const uint32_t tc = r1 ? nd[i].z : nd[i].y;
+        const bool cleaf = (m & (r1 ? SN_RLEAF : SN_LLEAF)) != 0u;
+        const bool drc = (m & (r1 ? SN_DRR : SN_DRL)) != 0u;
+        const float xc = r1 ? xr : xl;
+        const bool nc = (xc != xc);
+        const bool r2 = (xc >= __uint_as_float(tc)) || (nc && drc);
+        const bool nulled = act[i] && !self_leaf && nul[i] && (nj || (!cleaf && nc));
+        const bool done = self_leaf || cleaf;
+        leafv[i] = act[i] ? (self_leaf ? nd[i].x : (cleaf ? tc : leafv[i])) : leafv[i];
+        pz[i] = pz[i] || nulled;
+        pos[i] = (act[i] && !done) ? base[i] + 1 + 4 * (int)(m >> 21) + (r1 ? 2 : 0) + (r2 ? 1 : 0) : pos[i];
+        act[i] = act[i] && !done && !nulled;
+        live = live || act[i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < PILP; ++i) {
+      if (i >= nt) break;
+      if (pz[i]) {
+        if (GENERAL) poisoned = true;
+        else acc += __builtin_nanf("");
+        continue;
+      }
+      if (GENERAL) {
+        const int slot = a.tree_slot[t0 + i];
+        for (int p = 0; p < a.P; ++p) accl[(slot + p) * TB + tid] += a.leaves[(size_t)leafv[i] * a.P + p];
+      } else {
+        acc += __uint_as_float(leafv[i]);
       }
     }
   }
@@ -537,10 +648,27 @@ PMML_API int pmml_tree_launch(hipStream_t stream, const TreeArgs* args, int layo
       default: return -6;
     }
   } else {
-    if (a.variant != 0 && a.variant != VAR_POINTER_REFILL && a.variant != VAR_POINTER_COMPACT) return -10;
+    if (a.variant != 0 && a.variant != VAR_POINTER_REFILL && a.variant != VAR_POINTER_COMPACT &&
+        a.variant != VAR_POINTER_MASKED && a.variant != VAR_POINTER_SUPER)
+      return -10;
     const bool feat_lds = a.n_feat <= 64;
     size_t lds = (feat_lds ? (size_t)a.n_feat * TB * 4 : 0) + TB * 4 + acc_lds;
-    if (a.variant == VAR_POINTER_COMPACT) {
+    if (a.variant == VAR_POINTER_SUPER) {
+      if (a.n_feat > 32) return -4;  // 5-bit feature fields
+      if (a.general) {
+        err = prepare_launch(tree_super_kernel<true>, lds);
+        if (!err) hipLaunchKernelGGL((tree_super_kernel<true>), grid, dim3(TB), lds, stream, a);
+      } else if (a.pilp == 16) {
+        err = prepare_launch(tree_super_kernel<false, 16>, lds);
+        if (!err) hipLaunchKernelGGL((tree_super_kernel<false, 16>), grid, dim3(TB), lds, stream, a);
+      } else if (a.pilp == 4) {
+        err = prepare_launch(tree_super_kernel<false, 4>, lds);
+        if (!err) hipLaunchKernelGGL((tree_super_kernel<false, 4>), grid, dim3(TB), lds, stream, a);
+      } else {
+        err = prepare_launch(tree_super_kernel<false>, lds);
+        if (!err) hipLaunchKernelGGL((tree_super_kernel<false>), grid, dim3(TB), lds, stream, a);
+      }
+    } else if (a.variant == VAR_POINTER_COMPACT) {
       if (!feat_lds) return -4;
       if (a.general) {
         err = prepare_launch(tree_compact_kernel<true>, lds);
@@ -569,7 +697,10 @@ PMML_API int pmml_tree_launch(hipStream_t stream, const TreeArgs* args, int layo
         }
       }
     } else if (a.general) {
-      if (feat_lds) {
+      if (feat_lds && (a.variant & VAR_POINTER_MASKED)) {
+        err = prepare_launch(tree_pointer_kernel<true, true, 8, true>, lds);
+        if (!err) hipLaunchKernelGGL((tree_pointer_kernel<true, true, 8, true>), grid, dim3(TB), lds, stream, a);
+      } else if (feat_lds) {
         err = prepare_launch(tree_pointer_kernel<true, true>, lds);
         if (!err) hipLaunchKernelGGL((tree_pointer_kernel<true, true>), grid, dim3(TB), lds, stream, a);
       } else {
@@ -577,7 +708,10 @@ PMML_API int pmml_tree_launch(hipStream_t stream, const TreeArgs* args, int layo
         if (!err) hipLaunchKernelGGL((tree_pointer_kernel<true, false>), grid, dim3(TB), lds, stream, a);
       }
     } else {
-      if (feat_lds && a.pilp == 16) {
+      if (feat_lds && (a.variant & VAR_POINTER_MASKED)) {
+        err = prepare_launch(tree_pointer_kernel<false, true, 8, true>, lds);
+        if (!err) hipLaunchKernelGGL((tree_pointer_kernel<false, true, 8, true>), grid, dim3(TB), lds, stream, a);
+      } else if (feat_lds && a.pilp == 16) {
         err = prepare_launch(tree_pointer_kernel<false, true, 16>, lds);
         if (!err) hipLaunchKernelGGL((tree_pointer_kernel<false, true, 16>), grid, dim3(TB), lds, stream, a);
       } else if (feat_lds && a.pilp == 4) {

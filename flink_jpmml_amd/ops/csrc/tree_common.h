@@ -75,6 +75,8 @@ constexpr int VAR_NAN_FAST = 4;    // wide kernel: take the fast path even on ti
 constexpr int VAR_NAN_PLANES = 8;  // ... via blob_nan + a second feature plane (NaN -> +inf)
 constexpr int VAR_POINTER_REFILL = 16;  // pointer layout: refill schedule (tree.hip)
 constexpr int VAR_POINTER_COMPACT = 32; // pointer layout: 8-byte BFS slots (tree.hip::tree_compact_kernel)
+constexpr int VAR_POINTER_MASKED = 64;  // pointer layout, lock-step sums: exec-masked loads of finished walks
+constexpr int VAR_POINTER_SUPER = 128;  // pointer layout: two levels per 16-byte slot (tree.hip::tree_super_kernel)
 
 // per-depth launchers (tree_d<D>.hip)
 #define PMML_TREE_DECL(D) int launch_perfect_d##D(hipStream_t st, const TreeArgs& a, dim3 grid, size_t lds);

@@ -352,3 +352,122 @@ def pack_compact_bfs(trees, weights: List[float], P: int):
     nodes = np.concatenate(slots_all) if slots_all else np.zeros((1, 2), np.uint32)
     leaves = np.concatenate(leaves_all).astype(np.float32) if leaves_all else None
     return nodes, leaves, roots, has_dr
+
+
+# --------------------------------------------------------------------------- SUPER pointer layout
+# Two tree levels per 16-byte load (``tree.hip::tree_super_kernel``). The deep-forest walk is bound
+# by the vector memory pipe's cost per load INSTRUCTION (profiles/r3u: ~20 TA cycles per 64-lane
+# gather whether the lanes fetch 8 or 16 bytes, whether finished lanes are masked or not), so the
+# lever is fewer loads per walk: a super-node packs a split and both of its children's splits.
+
+SN_FEAT_BITS = 5               # feature index fields (LDS planes): f_j bits 0-4, f_l 5-9, f_r 10-14
+SN_LLEAF, SN_RLEAF, SN_SELF = 1 << 15, 1 << 16, 1 << 17
+SN_DRJ, SN_DRL, SN_DRR = 1 << 18, 1 << 19, 1 << 20
+SN_BLOCK_SHIFT, SN_BLOCK_BITS = 21, 11
+SN_NULL_ROOT = np.uint32(1 << 31)  # root word flag: the tree's nullPrediction missing strategy
+
+
+def pack_super(trees, weights: List[float], P: int):
+    """``uint4`` super-node slots, per tree: slot 0 the root super-node, then blocks of 4 slots
+    (block b = slots 1 + 4b .. 4 + 4b) holding the four grandchildren of one super-node, blocks in
+    breadth-first order.
+
+    Internal super-node at node j with children l, r: ``x`` = T_j, ``y`` = T_l (or l's leaf value
+    when l is a leaf), ``z`` = T_r (or r's leaf value), ``w`` = f_j | f_l << 5 | f_r << 10 |
+    l-is-leaf | r-is-leaf | default-right bits of j, l, r | grandchild block << 21. The walk at j
+    picks c = r if x_j >= T_j, then the grandchild 2 (c == r) + (x_c >= T_c) of the block; a leaf
+    child ends the walk with its value in hand, a leaf grandchild is a slot flagged SN_SELF whose
+    ``x`` is the value. Leaf values: the weighted fp32 value (P == 1) or the row of ``leaves``.
+    Canonical splits ("go right iff x >= T", fp32-exact thresholds) as the other layouts.
+
+    Returns ``(nodes [n, 4] u32, leaves [n_leaves, P] f32 or None, roots [n_trees] u32 (slot |
+    SN_NULL_ROOT), has_dr)``; ``ValueError`` when a feature index is >= 32 or a tree needs more
+    than 2^11 blocks."""
+    from .plans import _canonical_vec
+
+    slots_all: List[np.ndarray] = []
+    leaves_all: List[np.ndarray] = []
+    roots = np.zeros(len(trees), dtype=np.uint32)
+    base = n_leaf = 0
+    has_dr = False
+    fmax = (1 << SN_FEAT_BITS) - 1
+    for ti, (t, w) in enumerate(zip(trees, weights)):
+        feat = np.asarray(t.feature, dtype=np.int64)
+        n = feat.shape[0]
+        internal = feat >= 0
+        if internal.any() and feat[internal].max() > fmax:
+            raise ValueError(f"super layout: feature index > {fmax}")
+        T, swap = _canonical_vec(np.asarray(t.op), np.asarray(t.threshold, dtype=np.float64))
+        left, right = np.asarray(t.left, dtype=np.int64), np.asarray(t.right, dtype=np.int64)
+        lc = np.where(swap, right, left)
+        rc = np.where(swap, left, right)
+        dr = np.where(swap, np.asarray(t.default_left, bool), ~np.asarray(t.default_left, bool)) & internal
+        has_dr = has_dr or bool(dr.any())
+        # leaf payloads: value bits (P == 1) or payload row (P > 1), one per leaf node
+        leafword = np.zeros(n, dtype=np.uint32)
+        lk = np.nonzero(~internal)[0]
+        if P == 1:
+            leafword[lk] = (np.asarray(t.leaf_value, dtype=np.float64)[lk] * w).astype(np.float32).view(np.uint32)
+        else:
+            leafword[lk] = (n_leaf + np.arange(lk.size)).astype(np.uint32)
+            leaves_all.append(np.asarray(t.leaf_probs, dtype=np.float64)[lk, :P] * w)
+            n_leaf += lk.size
+        fi = np.where(internal, feat, 0).astype(np.uint64)
+        Tw = T.view(np.uint32) if T.dtype == np.float32 else T.astype(np.float32).view(np.uint32)
+        word = np.where(internal, Tw, leafword)  # y / z of a parent: T of an internal child, else its value
+        # breadth-first over super-nodes
+        recs: List[np.ndarray] = []
+        slot_of = {}
+        frontier = np.array([0], dtype=np.int64)   # super-node roots (or leaf slots) of this level
+        fslots = np.array([0], dtype=np.int64)
+        n_slots, n_blocks = 1, 0
+        while frontier.size:
+            rec = np.zeros((frontier.size, 4), dtype=np.uint32)
+            isl = ~internal[frontier]
+            rec[isl, 0] = leafword[frontier[isl]]
+            rec[isl, 3] = SN_SELF
+            j = frontier[~isl]
+            l, r = lc[j], rc[j]
+            il, ir = internal[l], internal[r]
+            need = il | ir
+            blk = np.full(j.size, 0, dtype=np.int64)
+            blk[need] = n_blocks + np.arange(int(need.sum()))
+            n_blocks += int(need.sum())
+            if n_blocks > (1 << SN_BLOCK_BITS):
+                raise ValueError("super layout: tree needs more than 2^11 grandchild blocks")
+            w3 = (fi[j] | (fi[l] * il) << np.uint64(5) | (fi[r] * ir) << np.uint64(10)
+                  | np.uint64(SN_LLEAF) * (~il).astype(np.uint64) | np.uint64(SN_RLEAF) * (~ir).astype(np.uint64)
+                  | np.uint64(SN_DRJ) * dr[j].astype(np.uint64) | np.uint64(SN_DRL) * (dr[l] & il).astype(np.uint64)
+                  | np.uint64(SN_DRR) * (dr[r] & ir).astype(np.uint64)
+                  | blk.astype(np.uint64) << np.uint64(SN_BLOCK_SHIFT))
+            rec[~isl, 0] = Tw[j]
+            rec[~isl, 1] = word[l]
+            rec[~isl, 2] = word[r]
+            rec[~isl, 3] = w3.astype(np.uint32)
+            recs.append((fslots, rec))
+            # next level: the 4 grandchild slots of every super-node that has a block
+            jn, bn = j[need], blk[need]
+            ln, rn = lc[jn], rc[jn]
+            kids, kslots = [], []
+            for k, (c, ok) in enumerate(((ln, internal[ln]), (rn, internal[rn]))):
+                for h, g in enumerate((lc, rc)):
+                    sel = ok
+                    kids.append(g[c[sel]])
+                    kslots.append(1 + 4 * bn[sel] + 2 * k + h)
+            frontier = np.concatenate(kids) if kids else np.zeros(0, np.int64)
+            fslots = np.concatenate(kslots) if kslots else np.zeros(0, np.int64)
+            n_slots = max(n_slots, 1 + 4 * n_blocks)
+        slots = np.zeros((n_slots, 4), dtype=np.uint32)
+        for s, rec in recs:
+            slots[s] = rec
+        roots[ti] = np.uint32(base) | (SN_NULL_ROOT if bool(t.null_missing) else np.uint32(0))
+        slots_all.append(slots)
+        base += n_slots
+        if base >= (1 << 31):
+            raise ValueError("super layout: more than 2^31 slots")
+    nodes = np.concatenate(slots_all) if slots_all else np.zeros((1, 4), np.uint32)
+    leaves = np.concatenate(leaves_all).astype(np.float32) if leaves_all else None
+    return nodes, leaves, roots, has_dr
+
+
+__all__ += ["pack_compact_bfs", "pack_super"]

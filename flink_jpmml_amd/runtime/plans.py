@@ -1066,7 +1066,8 @@ def _perfect_pack_vec(trees, weights, P: int, D: int, stride: int, fmap, leaf_bi
     return blob, rec, has_dr
 
 
-VAR_NAN_FAST, VAR_NAN_PLANES, VAR_POINTER_REFILL, VAR_POINTER_COMPACT = 4, 8, 16, 32  # csrc/tree_common.h
+VAR_NAN_FAST, VAR_NAN_PLANES, VAR_POINTER_REFILL, VAR_POINTER_COMPACT, VAR_POINTER_MASKED = 4, 8, 16, 32, 64  # tree_common.h
+VAR_POINTER_SUPER = 128
 DYN_B, DYN_SLOTS = 8, 16  # csrc: MODE_SUM trees per claimed batch, batch slots per chunk
 
 
@@ -1216,8 +1217,11 @@ class TreePlan(DevicePlan):
                  variant: str = "auto", precision: str = "fp32", nan_mode: str = "auto", max_chunk_trees: int = 0,
                  tree_shard: Optional[Tuple[int, int]] = None, head_depth: int = 0,
                  pointer_schedule: str = "lockstep", node_order: str = "bfs", node_format: str = "wide",
-                 pointer_ilp: int = 8, xcd_split: str = "off"):
-        """``xcd_split`` (pointer / hybrid layouts): ``"on"`` splits the forest into 8 tree slices
+                 pointer_ilp: int = 8, xcd_split: str = "off", pointer_load: str = "clamped"):
+        """``pointer_load`` (pointer lock-step kernel, features in LDS): ``"clamped"`` (finished walks
+        re-load node 0, no branch) or ``"masked"`` (their loads are exec-masked off).
+
+        ``xcd_split`` (pointer / hybrid layouts): ``"on"`` splits the forest into 8 tree slices
         scored by workgroups placed on the 8 XCDs (csrc ``tree_block``), so each XCD's 4 MiB L2
         holds one slice instead of the whole forest; ``"off"`` (default): grid.y splits only.
         Measured (profiles/r3q): no gain on a 14 MB depth-14 forest — its L2 hit rate is already
@@ -1230,7 +1234,8 @@ class TreePlan(DevicePlan):
         drift onto different trees and every load instruction touches up to 64 distinct lines,
         while lock-step lanes share the lines of the same tree level. ``node_order``: pointer-node
         storage order (``"bfs"``: level by level, siblings adjacent; ``"dfs"``: preorder).
-        ``node_format`` (pointer layout): ``"wide"`` (default) 16-byte nodes, ``"compact"`` 8-byte
+        ``node_format`` (pointer layout): ``"super"``: two tree levels per 16-byte slot
+        (:func:`~flink_jpmml_amd.runtime.hybrid.pack_super`, <= 32 features), ``"wide"`` (default) 16-byte nodes, ``"compact"`` 8-byte
         BFS slots with inline leaves (:func:`~flink_jpmml_amd.runtime.hybrid.pack_compact_bfs`;
         features staged in LDS, i.e. at most 64) — measured 1.34x SLOWER (profiles/r3n), kept as
         an option; ``"auto"``: compact whenever it applies. ``pointer_ilp``: walks per lane in
@@ -1252,6 +1257,8 @@ class TreePlan(DevicePlan):
         if pointer_schedule not in ("refill", "lockstep"):
             raise ValueError("pointer_schedule must be 'refill' or 'lockstep'")
         self.heads, self.head_depth = None, 0  # hybrid layout only
+        if pointer_load not in ("clamped", "masked"):
+            raise ValueError("pointer_load must be 'clamped' or 'masked'")
         if xcd_split not in ("on", "off"):
             raise ValueError("xcd_split must be 'on' or 'off'")
         self.xcd_split = 0
@@ -1426,7 +1433,7 @@ class TreePlan(DevicePlan):
         else:
             if precision == "fp8":
                 raise NotLowerable("fp8 leaves need the PERFECT layout")
-            from .hybrid import head_words, pack_compact_bfs, pack_hybrid_compact, pack_trees
+            from .hybrid import head_words, pack_compact_bfs, pack_hybrid_compact, pack_super, pack_trees
 
             feat_lds = F <= 64
             H = 0
@@ -1454,8 +1461,19 @@ class TreePlan(DevicePlan):
                     self.layout, H, heads, self.chunk_trees = "pointer", 0, None, 0
             else:
                 self.chunk_trees = 0
-            compact = False
-            if heads is None and feat_lds and pointer_schedule == "lockstep" and node_format != "wide" \
+            compact = superl = False
+            if node_format == "super":
+                if heads is not None or not feat_lds or pointer_schedule != "lockstep" or F > 32:
+                    raise NotLowerable("super pointer layout needs <= 32 features in LDS and the lock-step walk")
+                try:
+                    nodes, leaves, roots, has_dr = pack_super(spec.trees, spec.weights, spec.P)
+                    roots = roots.view(np.int32)
+                    superl = True
+                    if leaves is None:
+                        leaves = np.zeros((1, 1), np.float32)
+                except ValueError as e:
+                    raise NotLowerable(f"super pointer layout: {e}") from e
+            elif heads is None and feat_lds and pointer_schedule == "lockstep" and node_format != "wide" \
                     and node_order == "bfs":
                 try:
                     nodes, leaves, roots, has_dr = pack_compact_bfs(spec.trees, spec.weights, spec.P)
@@ -1467,7 +1485,7 @@ class TreePlan(DevicePlan):
                         raise NotLowerable("compact pointer layout does not apply")
             elif node_format == "compact":
                 raise NotLowerable("compact pointer layout needs features in LDS, lock-step, bfs")
-            if heads is None and not compact:
+            if heads is None and not compact and not superl:
                 _, nodes, leaves, roots, has_dr = pack_trees(spec.trees, spec.weights, spec.P, 0, feat_lds,
                                                              order=node_order)
             self.blob_nan, self.chunk_trees_nan = None, 0
@@ -1476,8 +1494,12 @@ class TreePlan(DevicePlan):
             # pointer walks: refill schedule (each PILP slot restarts on the next tree as soon as
             # its walk ends) unless pinned to the lock-step kernel's tree-order sums
             self.variant = VAR_POINTER_REFILL if (self.layout == "pointer" and pointer_schedule == "refill") else 0
-            if compact:
+            if superl:
+                self.variant = VAR_POINTER_SUPER
+            elif compact:
                 self.variant = VAR_POINTER_COMPACT
+            elif pointer_load == "masked" and self.layout == "pointer" and self.variant == 0 and feat_lds:
+                self.variant = VAR_POINTER_MASKED  # finished walks skip their node load (exec mask)
             self.blob = self._t(nodes.reshape(-1).view(np.int32))
             self.leaves = self._t(leaves.reshape(-1))
             self.roots = self._t(roots)

@@ -15,6 +15,11 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 CONFIGS = {
     "pointer": dict(layout="pointer", xcd_split="off"),
     "pointer+xcd": dict(layout="pointer", xcd_split="on"),
+    "pointer+masked": dict(layout="pointer", pointer_load="masked"),
+    "super": dict(layout="pointer", node_format="super"),
+    "super+xcd": dict(layout="pointer", node_format="super", xcd_split="on"),
+    "super16": dict(layout="pointer", node_format="super", pointer_ilp=16),
+    "super4": dict(layout="pointer", node_format="super", pointer_ilp=4),
     "compact": dict(layout="pointer", node_format="compact", xcd_split="off"),
     "compact+xcd": dict(layout="pointer", node_format="compact", xcd_split="on"),
     "refill+xcd": dict(layout="pointer", pointer_schedule="refill", xcd_split="on"),

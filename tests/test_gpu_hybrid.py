@@ -95,3 +95,33 @@ def test_xcd_split_vote_forest_on_gpu(gpu):
     s, v = _score(c, plan, X)
     assert (v == vref).all()
     np.testing.assert_array_equal(s[v], ref[v])
+
+
+@pytest.mark.parametrize("missing", ["defaultChild", "nullPrediction"])
+@pytest.mark.parametrize("xcd", ["off", "on"])
+def test_super_layout_on_gpu(gpu, missing, xcd):
+    """Two levels per 16-byte slot (tree_super_kernel): against the fp64 oracle, and bit-identical
+    to the one-level pointer walk (both accumulate leaves in tree order)."""
+    txt = gbdt_pmml(n_trees=40, depth=14, n_features=24, seed=7, p_split=0.8, missing_strategy=missing)
+    c = CompiledPmml.from_string(txt)
+    sup = c.plan(gpu, layout="pointer", node_format="super", xcd_split=xcd)
+    ptr = c.plan(gpu, layout="pointer", xcd_split=xcd)
+    assert sup.variant == 128
+    X = stream_matrix(100_000, 24, seed=3, missing_rate=0.03)
+    s, v = _score(c, sup, X)
+    s0, v0 = _score(c, ptr, X)
+    ref, vref = c.score_matrix_oracle(X)
+    assert (v == vref).all()
+    np.testing.assert_allclose(s[v], ref[v], rtol=0, atol=5e-5)
+    assert (v == v0).all() and np.array_equal(s[v], s0[v0])
+
+
+def test_super_layout_votes_on_gpu(gpu):
+    txt = random_forest_pmml(n_trees=30, depth=16, n_features=16, n_classes=3, seed=5, p_split=0.8)
+    c = CompiledPmml.from_string(txt.encode())
+    plan = c.plan(gpu, layout="pointer", node_format="super")
+    X = stream_matrix(50_000, 16, seed=8, missing_rate=0.02)
+    s, v = _score(c, plan, X)
+    ref, vref = c.score_matrix_oracle(X)
+    assert (v == vref).all()
+    np.testing.assert_array_equal(s[v], ref[v])

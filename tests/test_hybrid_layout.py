@@ -178,3 +178,74 @@ def test_wide_feature_pointer_offsets():
     ref, vref = c.score_matrix_oracle(X)
     got = plan.epi_args.get("a", 1.0) * emulate(plan, X) + plan.epi_args.get("b", 0.0)
     np.testing.assert_allclose(got[vref], ref[vref], rtol=0, atol=2e-4)
+
+
+def emulate_super(plan, X):
+    """``tree_super_kernel`` over the packed super-node slots: per step x_j picks the child, x_c the
+    grandchild slot ``base + 1 + 4 * block + 2 (c == r) + (x_c >= T_c)``."""
+    Xf = X.astype(np.float32)
+    n = len(X)
+    nodes = plan.blob.numpy().view(np.uint32).reshape(-1, 4)
+    roots = plan.roots.numpy().view(np.uint32)
+    leaves = plan.leaves.numpy().reshape(-1, plan.P)[:, 0]
+    rows = np.arange(n)
+    acc = np.zeros(n)
+    for t in range(plan.n_trees):
+        base = int(roots[t] & 0x7FFFFFFF)
+        nul = bool(roots[t] >> 31)
+        pos = np.full(n, base)
+        act = np.ones(n, bool)
+        pz = np.zeros(n, bool)
+        leafv = np.zeros(n, np.uint32)
+        while act.any():
+            nd = nodes[np.where(act, pos, 0)]
+            m = nd[:, 3]
+            self_leaf = (m & (1 << 17)) != 0
+            xj = Xf[rows, m & 31]
+            nj = np.isnan(xj)
+            r1 = (xj >= nd[:, 0].view(np.float32)) | (nj & ((m >> 18) & 1).astype(bool))
+            tc = np.where(r1, nd[:, 2], nd[:, 1])
+            fc = np.where(r1, (m >> 10) & 31, (m >> 5) & 31)
+            cleaf = np.where(r1, (m >> 16) & 1, (m >> 15) & 1).astype(bool)
+            drc = np.where(r1, (m >> 20) & 1, (m >> 19) & 1).astype(bool)
+            xc = Xf[rows, fc]
+            nc = np.isnan(xc)
+            r2 = (xc >= tc.view(np.float32)) | (nc & drc)
+            nulled = act & ~self_leaf & nul & (nj | (~cleaf & nc))
+            done = self_leaf | cleaf
+            leafv = np.where(act, np.where(self_leaf, nd[:, 0], np.where(cleaf, tc, leafv)), leafv)
+            pz |= nulled
+            nxt = base + 1 + 4 * (m >> 21).astype(np.int64) + 2 * r1 + r2
+            pos = np.where(act & ~done, nxt, pos)
+            act = act & ~done & ~nulled
+        lv = leaves[leafv] if plan.P > 1 else leafv.view(np.float32)
+        acc += np.where(pz, np.nan, lv)
+    return acc
+
+
+@pytest.mark.parametrize("missing", ["defaultChild", "nullPrediction"])
+@pytest.mark.parametrize("depth,p_split", [(13, 0.8), (5, 0.6), (16, 0.75)])
+def test_super_layout_matches_oracle(missing, depth, p_split):
+    txt = gbdt_pmml(n_trees=10, depth=depth, n_features=20, seed=7, p_split=p_split)
+    if missing == "nullPrediction":
+        txt = txt.replace('missingValueStrategy="defaultChild"', 'missingValueStrategy="nullPrediction"')
+    c, plan = _plan(txt, layout="pointer", node_format="super")
+    assert plan.variant == 128
+    X = stream_matrix(3000, 20, seed=5, missing_rate=0.03)
+    ref, vref = c.score_matrix_oracle(X)
+    got = plan.epi_args.get("a", 1.0) * emulate_super(plan, X) + plan.epi_args.get("b", 0.0)
+    assert (np.isfinite(got) == vref).all()
+    np.testing.assert_allclose(got[vref], ref[vref], rtol=0, atol=2e-4)
+
+
+def test_super_layout_votes_and_limits():
+    txt = random_forest_pmml(n_trees=5, depth=12, n_features=16, n_classes=3, seed=4, p_split=0.8)
+    c, plan = _plan(txt, layout="pointer", node_format="super")
+    assert plan.variant == 128 and plan.P == 3
+    nodes = plan.blob.numpy().view(np.uint32).reshape(-1, 4)
+    roots = plan.roots.numpy().view(np.uint32)
+    assert (roots >> 31 == 0).all() and int(roots.max()) < len(nodes)
+    from flink_jpmml_amd.runtime.plans import NotLowerable
+
+    with pytest.raises(NotLowerable):  # 5-bit feature fields
+        _plan(gbdt_pmml(n_trees=3, depth=6, n_features=40, seed=1), layout="pointer", node_format="super")
