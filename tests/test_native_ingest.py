@@ -186,3 +186,28 @@ def test_fast_decimal_path_is_correctly_rounded(kmeans):
     want = np.array([_round_to_f32(t) for t in toks], dtype=np.float32)
     bad = [(t, g, w) for t, g, w in zip(toks, got, want) if g.view(np.uint32) != w.view(np.uint32)]
     assert not bad, bad[:10]
+
+
+def test_swar_digit_runs_and_buffer_edges(kmeans):
+    """Single-pass numeric fields with SWAR digit runs: integer / fraction runs of 1-20 digits
+    (8- and 16-digit run boundaries, > 19 digits through the scalar path), leading zeros, signs,
+    exponents, CRLF, a numeric missing token, and fields in the last bytes of the buffer."""
+    toks = []
+    for n in list(range(1, 21)):
+        digits = "".join(str((i * 7 + 3) % 10) for i in range(n))
+        toks += [digits, "-" + digits, "0." + digits, digits[: max(1, n // 2)] + "." + digits[n // 2:],
+                 "+" + digits + "e-3", "00000" + digits[:6]]
+    toks += ["0", "-0", "0.0", "1e22", "1e-22", "123456789012345678", "9007199254740993", "3.4028235e38"]
+    rows = [toks[i: i + 4] for i in range(0, len(toks) - 3, 4)]
+    text = "\n".join(",".join(r) for r in rows).encode()
+    for tail in (b"\n", b"\r\n"):
+        m = parse_records(kmeans, text + tail, kmeans.active_fields)
+        want = np.array([[np.float32(float(t)) for t in r] for r in rows], dtype=np.float32)
+        np.testing.assert_array_equal(m, want)
+    # short final line: the SWAR loads must stay inside the buffer (scalar path near the end)
+    m = parse_records(kmeans, b"1,2,3,4\n5,6,7,8", kmeans.active_fields)
+    np.testing.assert_array_equal(m, [[1, 2, 3, 4], [5, 6, 7, 8]])
+    # a numeric missing token keeps its meaning (the single-pass path is off then)
+    p = RecordParser(kmeans, kmeans.active_fields, missing=("-999",))
+    m, _ = p.parse(b"-999,1.5,-999.5,2\n")
+    np.testing.assert_array_equal(m, [[np.nan, 1.5, -999.5, 2.0]])
