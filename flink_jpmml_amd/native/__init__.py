@@ -15,7 +15,7 @@ import ctypes
 import os
 import subprocess
 import threading
-from typing import Iterable, List, Optional, Sequence, Tuple
+from typing import Any, Iterable, List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -103,7 +103,7 @@ def load() -> ctypes.CDLL:
             lib.ingest_vocab_add.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int,
                                              ctypes.c_float]
             lib.ingest_parse.restype = ctypes.c_longlong
-            lib.ingest_parse.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char, ctypes.c_int,
+            lib.ingest_parse.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_char, ctypes.c_int,
                                          ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int,
                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
                                          ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_size_t)]
@@ -149,20 +149,40 @@ class RecordParser:
             self.lib.ingest_vocab_free(v)
             self.vocab = None
 
-    def parse(self, data: bytes, out: Optional[np.ndarray] = None, max_rows: Optional[int] = None
-              ) -> Tuple[np.ndarray, int]:
-        """Parse the complete lines of ``data``. Returns ``(rows view of out, bytes consumed)``;
-        ``out`` (float32 ``[cap, fields]``, e.g. a pinned tensor's numpy view) is allocated if
-        omitted."""
+    def parse(self, data: Any, out: Optional[np.ndarray] = None, max_rows: Optional[int] = None,
+              length: Optional[int] = None) -> Tuple[np.ndarray, int]:
+        """Parse the complete lines of ``data`` (``bytes``, or a ``bytearray`` whose first
+        ``length`` bytes are parsed in place — no copy). Returns ``(rows view of out, bytes
+        consumed)``; ``out`` (float32 ``[cap, fields]``, e.g. a pinned tensor's numpy view) is
+        allocated if omitted."""
         F = len(self.fields)
+        if isinstance(data, bytearray):
+            n_bytes = len(data) if length is None else int(length)
+            if n_bytes > len(data):
+                raise ValueError("length exceeds the buffer")
+            if out is None:
+                data = bytes(data[:n_bytes])  # sizing pass below needs the line count
+            else:
+                view = (ctypes.c_char * max(1, len(data))).from_buffer(data)  # exported while parsing
+                return self._parse_ptr(ctypes.addressof(view), n_bytes, out, max_rows)
+        elif length is not None:
+            data = data[:length]
         if out is None:
             cap = max_rows if max_rows is not None else data.count(b"\n") + 1
             out = np.empty((cap, F), dtype=np.float32)
         if out.dtype != np.float32 or not out.flags.c_contiguous or out.shape[1] != F:
             raise ValueError(f"out must be a C-contiguous float32 [rows, {F}] array")
+        return self._parse_ptr(data, len(data), out, max_rows)
+
+    def _parse_ptr(self, data: Any, n_bytes: int, out: np.ndarray, max_rows: Optional[int]) -> Tuple[np.ndarray, int]:
+        F = len(self.fields)
+        if out.dtype != np.float32 or not out.flags.c_contiguous or out.shape[1] != F:
+            raise ValueError(f"out must be a C-contiguous float32 [rows, {F}] array")
         cap = out.shape[0] if max_rows is None else min(max_rows, out.shape[0])
         consumed, bad = ctypes.c_size_t(0), ctypes.c_size_t(0)
-        n = self.lib.ingest_parse(data, len(data), self.delim, len(self.columns), self.target.ctypes.data, F,
+        if n_bytes == 0 or cap == 0:
+            return out[:0], 0
+        n = self.lib.ingest_parse(data, n_bytes, self.delim, len(self.columns), self.target.ctypes.data, F,
                                   self.kind.ctypes.data, self.missing, self.n_missing, self.vocab,
                                   out.ctypes.data, cap, self.threads, ctypes.byref(consumed), ctypes.byref(bad))
         if n < 0:

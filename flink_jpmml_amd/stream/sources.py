@@ -217,32 +217,57 @@ class TextBatchSource(SourceFunction):
             hi = self._line_start_at_or_after(fh, data_start + span * (self._rank + 1) // self._world, data_start)
             fh.seek(lo)
             left = hi - lo
-            rest = b""
+            # one reusable read window (no per-chunk bytes concatenation): the unparsed tail of a
+            # chunk (a partial line) moves to the front, the next read lands behind it; batches
+            # are filled to ``batch_rows`` rows across chunks, so a pinned batch buffer is never
+            # handed downstream a few percent full
+            buf = bytearray(self.chunk_bytes)
+            view = memoryview(buf)
+            n_valid = 0
             row = 0
             eof = left <= 0
-            while not eof or rest:
-                if not eof and len(rest) < self.chunk_bytes:
-                    blk = fh.read(min(self.chunk_bytes, left))
-                    left -= len(blk)
-                    eof = not blk or left <= 0
-                    rest += blk
-                    if eof and rest and not rest.endswith(b"\n"):
-                        rest += b"\n"
-                    if not eof:
-                        continue
-                if not rest:
+            rb, filled = None, 0
+            while True:
+                if not eof and n_valid < len(buf):
+                    k = fh.readinto(view[n_valid: n_valid + min(len(buf) - n_valid, left)])
+                    left -= k
+                    n_valid += k
+                    eof = k == 0 or left <= 0
+                if eof and n_valid and buf[n_valid - 1] != 0x0A:  # final line without its newline
+                    if n_valid == len(buf):
+                        view.release()
+                        buf.extend(b"\n")
+                        view = memoryview(buf)
+                    else:
+                        buf[n_valid] = 0x0A
+                    n_valid += 1
+                if rb is None:
+                    rb, filled = RecordBatch.pinned(self.batch_rows, F), 0
+                used = 0
+                if n_valid:
+                    m, used = parser.parse(buf, out=rb.X.numpy()[filled:], max_rows=self.batch_rows - filled,
+                                           length=n_valid)
+                    filled += len(m)
+                    self.bytes_parsed += used
+                    METRICS.inc("ingest.bytes_parsed", used)
+                    if used:
+                        tail = bytes(view[used:n_valid])  # the partial line (short)
+                        buf[: len(tail)] = tail
+                        n_valid -= used
+                done = eof and n_valid == 0
+                if filled and (filled == self.batch_rows or done):
+                    yield RecordBatch(rb.X[:filled], model_id=self.model_id, offset=row)
+                    row += filled
+                    rb, filled = None, 0
+                if done:
                     break
-                rb = RecordBatch.pinned(self.batch_rows, F)
-                m, used = parser.parse(rest, out=rb.X.numpy(), max_rows=self.batch_rows)
-                if used == 0:
-                    break
-                self.bytes_parsed += min(used, len(rest))
-                METRICS.inc("ingest.bytes_parsed", min(used, len(rest)))
-                rest = rest[used:]
-                rb = RecordBatch(rb.X[: len(m)], model_id=self.model_id, offset=row)
-                row += len(m)
-                if len(m):
-                    yield rb
+                if not used and (eof or n_valid == len(buf)):
+                    if eof:  # unparsable remainder
+                        break
+                    view.release()
+                    buf.extend(bytes(len(buf)))  # a line longer than the window: grow it
+                    view = memoryview(buf)
+            view.release()
 
 
 class ThreadedSource(SourceFunction):

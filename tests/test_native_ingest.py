@@ -211,3 +211,30 @@ def test_swar_digit_runs_and_buffer_edges(kmeans):
     p = RecordParser(kmeans, kmeans.active_fields, missing=("-999",))
     m, _ = p.parse(b"-999,1.5,-999.5,2\n")
     np.testing.assert_array_equal(m, [[np.nan, 1.5, -999.5, 2.0]])
+
+
+@pytest.mark.parametrize("trailing_newline", [True, False])
+@pytest.mark.parametrize("chunk,batch_rows", [(64, 7), (1000, 1000), (1 << 20, 100000)])
+def test_text_source_window_fills_batches(tmp_path, trailing_newline, chunk, batch_rows):
+    """TextBatchSource's reusable read window: lines longer than the window grow it, partial lines
+    carry over, batches are filled to ``batch_rows`` across chunks, rank splits cover every row."""
+    from flink_jpmml_amd.bench.synth import gbdt_pmml, stream_matrix
+    from flink_jpmml_amd.stream.sources import TextBatchSource
+
+    c = CompiledPmml.from_string(gbdt_pmml(n_trees=2, depth=2, n_features=4))
+    X = stream_matrix(3000, 4, seed=1, missing_rate=0.05)
+    path = tmp_path / "x.csv"
+    body = "\n".join(",".join("" if np.isnan(v) else f"{v:.9g}" for v in r) for r in X)
+    path.write_text("f0,f1,f2,f3\n" + body + ("\n" if trailing_newline else ""))
+    for world in (1, 3):
+        got = []
+        for r in range(world):
+            src = TextBatchSource(str(path), c, batch_rows=batch_rows, chunk_bytes=chunk)
+            src.open_subtask(r, world)
+            bs = list(src.iterate())
+            assert all(len(b) == batch_rows for b in bs[:-1])
+            got += [b.X.numpy() for b in bs]
+        M = np.concatenate(got)
+        assert M.shape == X.shape
+        np.testing.assert_array_equal(np.isnan(M), np.isnan(X))
+        np.testing.assert_allclose(np.nan_to_num(M), np.nan_to_num(X), rtol=1e-7)
