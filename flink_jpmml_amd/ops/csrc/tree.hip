@@ -616,6 +616,8 @@ PMML_API int pmml_tree_launch(hipStream_t stream, const TreeArgs* args, int layo
   if (splits == 1) a.partial = nullptr;
   if (a.C > 16) return -3;
   a.trees_per_split = (a.n_trees + splits - 1) / splits;
+  if (a.n_trees > 0) splits = (a.n_trees + a.trees_per_split - 1) / a.trees_per_split;  // no empty split
+  if (splits == 1) a.partial = nullptr;
   const int row_blocks = (a.n_rows + TB - 1) / TB;
   if (layout == 0 || splits == 1) a.xcd_split = 0;  // PERFECT kernels: grid.y splits (forests fit L2)
   if (a.xcd_split > 0) a.xcd_split = splits;

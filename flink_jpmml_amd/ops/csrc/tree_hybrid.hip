@@ -242,6 +242,8 @@ PMML_API int pmml_tree_hybrid_launch(hipStream_t stream, const HybridArgs* args,
   if (ha.head_words < words || (ha.head_words & 3) != 0) return -4;
   if (a.chunk_trees < 1) return -4;
   a.trees_per_split = (a.n_trees + splits - 1) / splits;
+  if (a.n_trees > 0) splits = (a.n_trees + a.trees_per_split - 1) / a.trees_per_split;  // no empty split
+  if (splits == 1) a.partial = nullptr;
   const bool feat_lds = a.n_feat <= 64;
   const size_t lds = (feat_lds ? (size_t)a.n_feat * TB * 4 : 0) + TB * 4 + (a.general ? (size_t)a.C * TB * 4 : 0) +
                      (size_t)a.chunk_trees * ha.head_words * 4;

@@ -54,6 +54,9 @@ class StepHandle:
     out_index: int = 0
 
 
+SPLIT_COPY_MIN_BYTES = 8 << 20  # micro-batch copies below this size use one copy stream
+
+
 class DevicePipeline:
     """HIP streams + the device input ring, shareable by several plans on one device. The ring
     holds ``depth`` flat fp32 slots of ``micro_batch × max_features`` (grown on demand)."""
@@ -190,6 +193,9 @@ class StreamingScorer:
         self.max_inflight = int(max_inflight)
         self._inflight: "collections.deque" = collections.deque()
         self.rows_submitted = 0
+        from ..ops import _lib
+
+        self._lib = _lib.load()
 
     # ------------------------------------------------------------------ step API (bench engine mode)
     def _alloc_out(self, n: int):
@@ -239,15 +245,27 @@ class StreamingScorer:
         else:
             slot, xs = self._slot(m)
             h2ds = p.active_h2d()
+            if len(h2ds) > 1 and m * self.F * 4 < SPLIT_COPY_MIN_BYTES:
+                h2ds = h2ds[:1]  # a small copy gains nothing from a second copy engine, only API calls
             part = -(-m // len(h2ds))
+            raw = X_src.is_contiguous() and X_src.dtype == torch.float32
+            if raw:  # hipMemcpyAsync straight from the pinned rows: no torch stream contexts per copy
+                rowb = self.F * 4
+                src0, dst0 = X_src.data_ptr() + s * rowb, xs.data_ptr()
             for j, st in enumerate(h2ds):
-                with torch.cuda.stream(st):
-                    if p.used[slot]:
-                        st.wait_event(p.ev_comp[slot])  # kernel finished reading this slot
-                    a, b = j * part, min(m, (j + 1) * part)
-                    if a < b:
-                        xs[a:b].copy_(X_src[s + a:s + b], non_blocking=True)
-                    p.ev_h2d[slot][j].record(st)
+                if p.used[slot]:
+                    st.wait_event(p.ev_comp[slot])  # kernel finished reading this slot
+                a, b = j * part, min(m, (j + 1) * part)
+                if a < b:
+                    if raw:
+                        rc = self._lib.pmml_memcpy_async(dst0 + a * rowb, src0 + a * rowb, (b - a) * rowb, 1,
+                                                             st.cuda_stream)
+                        if rc != 0:
+                            raise RuntimeError(f"hipMemcpyAsync H2D failed ({rc})")
+                    else:
+                        with torch.cuda.stream(st):
+                            xs[a:b].copy_(X_src[s + a:s + b], non_blocking=True)
+                p.ev_h2d[slot][j].record(st)
             for ev in p.ev_h2d[slot][: len(h2ds)]:
                 p.comp.wait_event(ev)
         self.plan.launch(xs, out_score, out_valid, stream=p.comp, **kw)
@@ -332,9 +350,11 @@ class StreamingScorer:
 
     # ------------------------------------------------------------------ future API (DSL)
     def _throttle(self) -> None:
+        # entries: (completion event, source rows): raw hipMemcpyAsync copies do not register with
+        # torch's pinned-memory allocator, so the rows stay referenced until their work is done
         while len(self._inflight) >= self.max_inflight:
-            self._inflight.popleft().synchronize()
-        while self._inflight and self._inflight[0].query():
+            self._inflight.popleft()[0].synchronize()
+        while self._inflight and self._inflight[0][0].query():
             self._inflight.popleft()
 
     def submit_batch(self, batch: RecordBatch, replace_nan: Optional[float] = None,
@@ -403,7 +423,7 @@ class StreamingScorer:
                 done.record(self.d2h)
             else:
                 done.record(self.comp)
-        self._inflight.append(done)
+        self._inflight.append((done, X))
         self.rows_submitted += n
         METRICS.inc("scoring.rows_device", n)
         METRICS.inc("scoring.batches_device")
@@ -420,7 +440,7 @@ class StreamingScorer:
 
     def drain(self) -> None:
         while self._inflight:
-            self._inflight.popleft().synchronize()
+            self._inflight.popleft()[0].synchronize()
 
 
 def _observe_latency(pb: PredictionBatch) -> None:

@@ -19,6 +19,7 @@ from __future__ import annotations
 import dataclasses
 import logging
 import math
+import threading
 from dataclasses import dataclass
 from typing import Any, List, Optional, Tuple
 
@@ -1571,6 +1572,7 @@ class TreePlan(DevicePlan):
     def _post_state(self) -> None:
         self._partial = None
         self._args = {}
+        self._args_buf = {}
 
     def _args_template(self, with_probs: bool):
         """Per-plan cached argument struct (only row pointers change per launch: keeps the host
@@ -1596,7 +1598,15 @@ class TreePlan(DevicePlan):
             a.prof = ptr(getattr(self, "prof", None))  # kbench --tree-prof phase timers (nullable)
             a.epi = _epilogue(table=self.table, write_probs=with_probs, **self.epi_args)
             cache[with_probs] = a
-        b = TreeArgs()
+        # one mutable copy per thread, reused across launches: the C launcher copies the struct
+        # before returning, and every per-launch field is rewritten by launch()
+        bufs = self.__dict__.setdefault("_args_buf", {})
+        key = (threading.get_ident(), with_probs)
+        b = bufs.get(key)
+        if b is None:
+            if len(bufs) > 64:  # threads come and go (loader / job threads): bounded
+                bufs.clear()
+            b = bufs[key] = TreeArgs()
         ctypes.pointer(b)[0] = a
         return b
 
@@ -1606,6 +1616,11 @@ class TreePlan(DevicePlan):
         blocks = (n_rows + TB - 1) // TB
         if getattr(self, "xcd_split", 0) and self.n_trees >= 2 * XCD_SLICES:
             return XCD_SLICES
+        if self.layout == "perfect" and self.variant & 3 and self.n_trees >= 64:
+            # wide kernel (one 1024-thread workgroup per 256-row tile): about one workgroup per CU
+            # and at most 16 tree slices — measured best for 256-64K rows (profiles/r3y/splits.jsonl:
+            # 4096 rows 16.9 us at 16 slices vs 25.4 / 42.6 us at 32 / 62, 64K rows 83 us unsplit)
+            return int(max(1, min(16, 256 // max(1, blocks), self.n_trees // 8)))
         target = 512  # ~2 workgroups per CU on 256 CUs
         if blocks >= target or self.n_trees < 64:
             return 1
