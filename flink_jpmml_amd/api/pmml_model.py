@@ -194,10 +194,15 @@ class PmmlModel(Pipeline):
             validated = self.validate_input(input_vector)
             prepared = self.prepare_input(validated, replace_nan)
             result = self.evaluate_input(prepared)
-            target = self.extract_target(result)
         except Exception as e:  # noqa: BLE001
             return Prediction.on_failed_prediction(e)
-        return Prediction(Score(target), self.outputs_of(result))
+        outputs = self.outputs_of(result)
+        try:
+            target = self.extract_target(result)
+        except Exception as e:  # noqa: BLE001 - no / null target: EmptyScore, outputs still reported
+            empty = Prediction.on_failed_prediction(e)
+            return Prediction(empty.value, outputs)  # (e.g. AssociationModel: rules, no target field)
+        return Prediction(Score(target), outputs)
 
     # Scala-style aliases
     validateInput = validate_input  # noqa: N815

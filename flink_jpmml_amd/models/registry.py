@@ -12,6 +12,7 @@ from .base import ModelEvaluator
 
 
 def _registry() -> Dict[type, Callable[..., ModelEvaluator]]:
+    from .association import AssociationEvaluator
     from .clustering import ClusteringEvaluator
     from .knn import NearestNeighborEvaluator
     from .mining import MiningEvaluator
@@ -34,6 +35,7 @@ def _registry() -> Dict[type, Callable[..., ModelEvaluator]]:
         ir.RuleSetModel: make_ruleset_evaluator,
         ir.NaiveBayesModel: NaiveBayesEvaluator,
         ir.NearestNeighborModel: NearestNeighborEvaluator,
+        ir.AssociationModel: AssociationEvaluator,
     }
 
 

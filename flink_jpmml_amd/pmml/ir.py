@@ -222,6 +222,11 @@ class OutputField:
     rank: int = 1
     is_final_result: bool = True
     expression: Optional[Expression] = None
+    # association rules (feature="ruleValue" / "entityId" on an AssociationModel)
+    rule_feature: str = "consequent"
+    algorithm: str = "exclusiveRecommendation"
+    rank_basis: str = "confidence"
+    rank_order: str = "descending"
 
 
 @dataclass
@@ -613,3 +618,32 @@ class NearestNeighborModel(Model):
     inputs: List[KNNInput] = field(default_factory=list)
     instance_fields: Dict[str, str] = field(default_factory=dict)  # field -> InlineTable column
     rows: List[Dict[str, str]] = field(default_factory=list)       # InlineTable rows
+
+
+# association rules ---------------------------------------------------------------
+
+
+@dataclass
+class AssociationRule:
+    antecedent: str  # itemset id
+    consequent: str  # itemset id
+    support: float
+    confidence: float
+    lift: Optional[float] = None
+    leverage: Optional[float] = None
+    affinity: Optional[float] = None
+    rule_id: Optional[str] = None
+
+
+@dataclass
+class AssociationModel(Model):
+    """``AssociationModel`` (`functionName="associationRules"`): items, itemsets and rules. It has
+    no target field, so the reference's target extraction yields ``EmptyScore`` for every record;
+    the rules are exposed through ``ruleValue`` output fields."""
+
+    items: Dict[str, str] = field(default_factory=dict)          # item id -> value
+    itemsets: Dict[str, List[str]] = field(default_factory=dict)  # itemset id -> item ids
+    rules: List[AssociationRule] = field(default_factory=list)
+    number_of_transactions: int = 0
+    minimum_support: float = 0.0
+    minimum_confidence: float = 0.0

@@ -283,6 +283,10 @@ def _parse_output(el: Optional[ET.Element]) -> List[ir.OutputField]:
                 rank=int(of.get("rank", "1")),
                 is_final_result=of.get("isFinalResult", "true") == "true",
                 expression=_parse_expression(ex) if ex is not None else None,
+                rule_feature=of.get("ruleFeature", "consequent"),
+                algorithm=of.get("algorithm", "exclusiveRecommendation"),
+                rank_basis=of.get("rankBasis", "confidence"),
+                rank_order=of.get("rankOrder", "descending"),
             )
         )
     return out
@@ -659,6 +663,29 @@ def _parse_knn(el: ET.Element) -> ir.NearestNeighborModel:
     return m
 
 
+def _parse_association(el: ET.Element) -> ir.AssociationModel:
+    m = ir.AssociationModel(**_common(el))
+    m.number_of_transactions = int(float(el.get("numberOfTransactions", "0")))
+    m.minimum_support = _f(el, "minimumSupport", 0.0)
+    m.minimum_confidence = _f(el, "minimumConfidence", 0.0)
+    for it in _children(el, "Item"):
+        m.items[it.get("id")] = it.get("value")
+    for s in _children(el, "Itemset"):
+        m.itemsets[s.get("id")] = [r.get("itemRef") for r in _children(s, "ItemRef")]
+    for r in _children(el, "AssociationRule"):
+        for ref in (r.get("antecedent"), r.get("consequent")):
+            if ref not in m.itemsets:
+                raise PmmlParseError(f"AssociationRule references unknown itemset {ref!r}")
+        m.rules.append(ir.AssociationRule(r.get("antecedent"), r.get("consequent"), _f(r, "support", 0.0),
+                                          _f(r, "confidence", 0.0), _f(r, "lift"), _f(r, "leverage"),
+                                          _f(r, "affinity"), r.get("id")))
+    for ids in m.itemsets.values():
+        for i in ids:
+            if i not in m.items:
+                raise PmmlParseError(f"Itemset references unknown item {i!r}")
+    return m
+
+
 MODEL_PARSERS: Dict[str, Callable[[ET.Element], ir.Model]] = {
     "ClusteringModel": _parse_clustering,
     "TreeModel": _parse_tree,
@@ -671,9 +698,10 @@ MODEL_PARSERS: Dict[str, Callable[[ET.Element], ir.Model]] = {
     "RuleSetModel": _parse_ruleset,
     "NaiveBayesModel": _parse_naive_bayes,
     "NearestNeighborModel": _parse_knn,
+    "AssociationModel": _parse_association,
 }
 
-_KNOWN_UNSUPPORTED = ("AssociationModel", "BaselineModel", "BayesianNetworkModel", "GaussianProcessModel",
+_KNOWN_UNSUPPORTED = ("BaselineModel", "BayesianNetworkModel", "GaussianProcessModel",
                       "SequenceModel",
                       "TextModel", "TimeSeriesModel", "AnomalyDetectionModel")
 
