@@ -666,6 +666,9 @@ PMML_API int pmml_tree_launch(hipStream_t stream, const TreeArgs* args, int layo
       } else if (a.pilp == 4) {
         err = prepare_launch(tree_super_kernel<false, 4>, lds);
         if (!err) hipLaunchKernelGGL((tree_super_kernel<false, 4>), grid, dim3(TB), lds, stream, a);
+      } else if (a.pilp == 2) {
+        err = prepare_launch(tree_super_kernel<false, 2>, lds);
+        if (!err) hipLaunchKernelGGL((tree_super_kernel<false, 2>), grid, dim3(TB), lds, stream, a);
       } else {
         err = prepare_launch(tree_super_kernel<false>, lds);
         if (!err) hipLaunchKernelGGL((tree_super_kernel<false>), grid, dim3(TB), lds, stream, a);
@@ -710,7 +713,10 @@ PMML_API int pmml_tree_launch(hipStream_t stream, const TreeArgs* args, int layo
         if (!err) hipLaunchKernelGGL((tree_pointer_kernel<true, false>), grid, dim3(TB), lds, stream, a);
       }
     } else {
-      if (feat_lds && (a.variant & VAR_POINTER_MASKED)) {
+      if (feat_lds && a.pilp == 2) {
+        err = prepare_launch(tree_pointer_kernel<false, true, 2>, lds);
+        if (!err) hipLaunchKernelGGL((tree_pointer_kernel<false, true, 2>), grid, dim3(TB), lds, stream, a);
+      } else if (feat_lds && (a.variant & VAR_POINTER_MASKED)) {
         err = prepare_launch(tree_pointer_kernel<false, true, 8, true>, lds);
         if (!err) hipLaunchKernelGGL((tree_pointer_kernel<false, true, 8, true>), grid, dim3(TB), lds, stream, a);
       } else if (feat_lds && a.pilp == 16) {

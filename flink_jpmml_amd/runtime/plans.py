@@ -1252,8 +1252,8 @@ class TreePlan(DevicePlan):
         super().__init__(compiled, device)
         if nan_mode not in ("auto", "off"):
             raise ValueError("nan_mode must be 'auto' or 'off'")
-        if pointer_ilp not in (4, 8, 16):
-            raise ValueError("pointer_ilp must be 4, 8 or 16")
+        if pointer_ilp not in (2, 4, 8, 16):
+            raise ValueError("pointer_ilp must be 2, 4, 8 or 16")
         self.pointer_ilp = int(pointer_ilp)
         if pointer_schedule not in ("refill", "lockstep"):
             raise ValueError("pointer_schedule must be 'refill' or 'lockstep'")

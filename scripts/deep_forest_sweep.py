@@ -20,6 +20,9 @@ CONFIGS = {
     "super+xcd": dict(layout="pointer", node_format="super", xcd_split="on"),
     "super16": dict(layout="pointer", node_format="super", pointer_ilp=16),
     "super4": dict(layout="pointer", node_format="super", pointer_ilp=4),
+    "super2": dict(layout="pointer", node_format="super", pointer_ilp=2),
+    "pointer2": dict(layout="pointer", pointer_ilp=2),
+    "pointer4": dict(layout="pointer", pointer_ilp=4),
     "compact": dict(layout="pointer", node_format="compact", xcd_split="off"),
     "compact+xcd": dict(layout="pointer", node_format="compact", xcd_split="on"),
     "refill+xcd": dict(layout="pointer", pointer_schedule="refill", xcd_split="on"),

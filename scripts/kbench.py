@@ -36,7 +36,7 @@ def main():
     p.add_argument("--pointer-schedule", default="lockstep", choices=["refill", "lockstep"])
     p.add_argument("--node-order", default="bfs", choices=["bfs", "dfs"])
     p.add_argument("--node-format", default="wide", choices=["auto", "compact", "wide"])
-    p.add_argument("--pointer-ilp", type=int, default=8, choices=[4, 8, 16])
+    p.add_argument("--pointer-ilp", type=int, default=8, choices=[2, 4, 8, 16])
     p.add_argument("--p-split", type=float, default=None, help="rf generator: split probability per node (gbdt: fixed 0.9)")
     p.add_argument("--xcd-split", default="off", choices=["on", "off"], help="pointer/hybrid: XCD tree slices")
     p.add_argument("--cache-dir", default="", help="tree models: reuse the generated PMML text across runs")
