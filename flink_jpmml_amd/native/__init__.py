@@ -174,6 +174,12 @@ class RecordParser:
             raise ValueError(f"out must be a C-contiguous float32 [rows, {F}] array")
         return self._parse_ptr(data, len(data), out, max_rows)
 
+    def parse_address(self, addr: int, n_bytes: int, out: np.ndarray, max_rows: Optional[int] = None
+                      ) -> Tuple[np.ndarray, int]:
+        """:meth:`parse` over ``n_bytes`` of host memory at ``addr`` (e.g. a memory-mapped file:
+        parsed where it lies, no copy). The memory must stay valid for the call."""
+        return self._parse_ptr(ctypes.c_void_p(int(addr)), int(n_bytes), out, max_rows)
+
     def _parse_ptr(self, data: Any, n_bytes: int, out: np.ndarray, max_rows: Optional[int]) -> Tuple[np.ndarray, int]:
         F = len(self.fields)
         if out.dtype != np.float32 or not out.flags.c_contiguous or out.shape[1] != F:

@@ -22,6 +22,7 @@ from __future__ import annotations
 
 import itertools
 import logging
+import mmap
 import os
 import queue
 import socket
@@ -160,7 +161,7 @@ class TextBatchSource(SourceFunction):
 
     def __init__(self, path: str, model: Any, batch_rows: int = 1 << 16, delimiter: str = ",",
                  columns: Optional[Sequence[str]] = None, threads: int = 0, model_id: Optional[str] = None,
-                 chunk_bytes: int = 16 << 20):
+                 chunk_bytes: int = 16 << 20, use_mmap: bool = True):
         self.path = path
         self.model = model  # CompiledPmml, PmmlModel or ModelReader / path
         self.batch_rows = int(batch_rows)
@@ -169,6 +170,7 @@ class TextBatchSource(SourceFunction):
         self.threads = threads
         self.model_id = model_id
         self.chunk_bytes = int(chunk_bytes)
+        self.use_mmap = bool(use_mmap)  # parse regular files where they lie (read-window loop otherwise)
 
     def _compiled(self):
         from ..runtime.compiled import CompiledPmml
@@ -215,6 +217,17 @@ class TextBatchSource(SourceFunction):
             span = size - data_start
             lo = self._line_start_at_or_after(fh, data_start + span * self._rank // self._world, data_start)
             hi = self._line_start_at_or_after(fh, data_start + span * (self._rank + 1) // self._world, data_start)
+            if hi > lo and self.use_mmap:
+                try:
+                    mm = mmap.mmap(fh.fileno(), 0, access=mmap.ACCESS_READ)
+                except (OSError, ValueError):
+                    mm = None
+                if mm is not None:
+                    try:
+                        yield from self._iterate_mapped(mm, lo, hi, parser, F)
+                    finally:
+                        mm.close()
+                    return
             fh.seek(lo)
             left = hi - lo
             # one reusable read window (no per-chunk bytes concatenation): the unparsed tail of a
@@ -268,6 +281,49 @@ class TextBatchSource(SourceFunction):
                     buf.extend(bytes(len(buf)))  # a line longer than the window: grow it
                     view = memoryview(buf)
             view.release()
+
+
+    def _iterate_mapped(self, mm, lo: int, hi: int, parser, F: int) -> Iterator[RecordBatch]:
+        """Parse the rank's byte range [lo, hi) where it lies in the page cache (the file is
+        memory-mapped: no read() copy, the parser threads fault the pages in in parallel)."""
+        from ..utils.metrics import METRICS
+
+        try:
+            mm.madvise(mmap.MADV_SEQUENTIAL)
+        except (AttributeError, OSError, ValueError):
+            pass
+        base = np.frombuffer(mm, dtype=np.uint8)  # read-only view: its address, no copy
+        try:
+            addr0 = base.ctypes.data
+            window = max(64, self.chunk_bytes)
+            pos, row = lo, 0
+            rb, filled = None, 0
+            while pos < hi:
+                if rb is None:
+                    rb, filled = RecordBatch.pinned(self.batch_rows, F), 0
+                n = min(hi - pos, window)
+                out = rb.X.numpy()[filled:]
+                m, used = parser.parse_address(addr0 + pos, n, out, max_rows=self.batch_rows - filled)
+                if used == 0:
+                    if pos + n < hi:
+                        window *= 2  # a line longer than the window
+                        continue
+                    # the file's last line has no newline: parse a terminated copy of it
+                    m, used = parser.parse(bytes(mm[pos:hi]) + b"\n", out=out, max_rows=self.batch_rows - filled)
+                    used = hi - pos if used else 0
+                    if not used:
+                        break
+                filled += len(m)
+                pos += used
+                self.bytes_parsed += used
+                METRICS.inc("ingest.bytes_parsed", used)
+                if filled == self.batch_rows or pos >= hi:
+                    if filled:
+                        yield RecordBatch(rb.X[:filled], model_id=self.model_id, offset=row)
+                        row += filled
+                    rb, filled = None, 0
+        finally:
+            del base
 
 
 class ThreadedSource(SourceFunction):

@@ -213,9 +213,10 @@ def test_swar_digit_runs_and_buffer_edges(kmeans):
     np.testing.assert_array_equal(m, [[np.nan, 1.5, -999.5, 2.0]])
 
 
+@pytest.mark.parametrize("use_mmap", [True, False])
 @pytest.mark.parametrize("trailing_newline", [True, False])
 @pytest.mark.parametrize("chunk,batch_rows", [(64, 7), (1000, 1000), (1 << 20, 100000)])
-def test_text_source_window_fills_batches(tmp_path, trailing_newline, chunk, batch_rows):
+def test_text_source_window_fills_batches(tmp_path, trailing_newline, chunk, batch_rows, use_mmap):
     """TextBatchSource's reusable read window: lines longer than the window grow it, partial lines
     carry over, batches are filled to ``batch_rows`` across chunks, rank splits cover every row."""
     from flink_jpmml_amd.bench.synth import gbdt_pmml, stream_matrix
@@ -229,7 +230,7 @@ def test_text_source_window_fills_batches(tmp_path, trailing_newline, chunk, bat
     for world in (1, 3):
         got = []
         for r in range(world):
-            src = TextBatchSource(str(path), c, batch_rows=batch_rows, chunk_bytes=chunk)
+            src = TextBatchSource(str(path), c, batch_rows=batch_rows, chunk_bytes=chunk, use_mmap=use_mmap)
             src.open_subtask(r, world)
             bs = list(src.iterate())
             assert all(len(b) == batch_rows for b in bs[:-1])
