@@ -20,6 +20,7 @@ and ``outliers`` handling from the ``MiningField``.
 from __future__ import annotations
 
 import math
+import re
 from typing import Any, Callable, Dict, Iterable, List, Optional
 
 import numpy as np
@@ -515,9 +516,128 @@ _UNARY_NUM: Dict[str, Callable] = {
 }
 
 
+# String built-ins of the PMML function library (JPMML-Evaluator's FunctionRegistry): evaluated over
+# decoded row strings, the result re-encoded into the output field's vocabulary.
+_STRING_FUNCS = ("uppercase", "lowercase", "substring", "trimBlanks", "concat", "replace", "formatNumber")
+
+
+def _text(v: Any) -> Optional[str]:
+    if v is None or (isinstance(v, float) and math.isnan(v)):
+        return None
+    if isinstance(v, float):
+        return str(int(v)) if v.is_integer() else repr(v)
+    return str(v)
+
+
+def _to_number(v: str) -> float:
+    try:
+        return float(v)
+    except ValueError:
+        return NAN
+
+
+def eval_strings(ex: ir.Expression, cols: Columns) -> List[Optional[str]]:
+    """Row-wise string values of ``ex`` (``None`` = missing): string fields decode their codes,
+    numbers are written as in a document (3.0 -> ``3``), string built-ins apply row by row."""
+    n = cols.n
+    schema = cols.schema
+    if isinstance(ex, ir.Constant):
+        v = None if ex.missing else ex.value
+        return [v] * n
+    if isinstance(ex, ir.FieldRef):
+        col = cols.get(ex.field)
+        out = [_text(schema.decode(ex.field, float(c))) for c in col]
+        if ex.map_missing_to is not None:
+            out = [ex.map_missing_to if o is None else o for o in out]
+        return out
+    if isinstance(ex, ir.Apply) and ex.function in _STRING_FUNCS:
+        return _apply_strings(ex, cols)
+    col = eval_expression(ex, cols)
+    return [_text(float(c)) for c in col]
+
+
+def _apply_strings(ex: ir.Apply, cols: Columns) -> List[Optional[str]]:
+    fn = ex.function
+    n = cols.n
+    if fn == "formatNumber":
+        x = eval_expression(ex.args[0], cols)
+        pat = eval_strings(ex.args[1], cols)
+        out = []
+        for v, p in zip(x, pat):
+            if math.isnan(v) or p is None:
+                out.append(None)
+                continue
+            try:
+                out.append(p % (int(v) if re.search(r"%[-+ 0#]*\d*[dxXo]", p) else v))
+            except (TypeError, ValueError):
+                out.append(None)
+        return out
+    args = [eval_strings(a, cols) for a in ex.args]
+    out: List[Optional[str]] = []
+    for i in range(n):
+        a = [arg[i] for arg in args]
+        if fn == "concat":  # missing arguments are skipped (JPMML: null-safe concatenation)
+            parts = [x for x in a if x is not None]
+            out.append("".join(parts) if parts else None)
+            continue
+        if a[0] is None:
+            out.append(None)
+            continue
+        if fn == "uppercase":
+            out.append(a[0].upper())
+        elif fn == "lowercase":
+            out.append(a[0].lower())
+        elif fn == "trimBlanks":
+            out.append(a[0].strip())
+        elif fn == "substring":  # substring(s, start (1-based), length)
+            try:
+                st, ln = int(float(a[1])), int(float(a[2]))
+            except (TypeError, ValueError):
+                out.append(None)
+                continue
+            out.append(a[0][max(st - 1, 0): max(st - 1, 0) + max(ln, 0)])
+        elif fn == "replace":  # replace(s, regex, replacement)
+            if a[1] is None or a[2] is None:
+                out.append(None)
+            else:
+                out.append(re.sub(a[1], re.sub(r"\$(\d)", r"\\\1", a[2]), a[0]))
+    return out
+
+
 def _eval_apply(ex: ir.Apply, cols: Columns, out_field: Optional[str]) -> np.ndarray:
     n = cols.n
     fn = ex.function
+    if fn in _STRING_FUNCS:
+        vals = _apply_strings(ex, cols)
+        if ex.map_missing_to is not None:
+            vals = [ex.map_missing_to if v is None else v for v in vals]
+        name = out_field or "__string__"
+        if out_field is not None and not cols.schema.is_string(out_field):
+            return np.array([NAN if v is None else _to_number(v) for v in vals], dtype=np.float64)
+        return np.array([NAN if v is None else float(cols.schema.code(name, v)) for v in vals], dtype=np.float64)
+    if fn == "matches":  # matches(s, regex): boolean
+        s_, pat = eval_strings(ex.args[0], cols), eval_strings(ex.args[1], cols)
+        return np.array([NAN if a is None or b is None else float(re.search(b, a) is not None)
+                         for a, b in zip(s_, pat)], dtype=np.float64)
+    if fn in ("isIn", "isNotIn"):  # isIn(field, value, value, ...): membership in the constant list
+        x = eval_strings(ex.args[0], cols)
+        members = set()
+        for a in ex.args[1:]:
+            if isinstance(a, ir.Constant) and not a.missing and a.value is not None:
+                members.add(a.value)
+                try:
+                    members.add(_text(float(a.value)))
+                except ValueError:
+                    pass
+            else:
+                raise UnsupportedFeatureException(f"{fn}: only constant member lists are supported")
+        hit = np.array([v is not None and v in members for v in x])
+        res = hit if fn == "isIn" else ~hit
+        res = res.astype(np.float64)
+        res[np.array([v is None for v in x], dtype=bool)] = NAN
+        if ex.map_missing_to is not None:
+            res = np.where(np.isnan(res), float(ex.map_missing_to), res)
+        return res
     args = [eval_expression(a, cols) for a in ex.args]
     with np.errstate(all="ignore"):
         if fn in ("isMissing", "isNotMissing"):
