@@ -292,6 +292,23 @@ class _Emitter:
             mm = s.lookup(tgt, ex.map_missing_to) if ex.map_missing_to is not None else NAN
             dv = s.lookup(tgt, ex.default_value) if ex.default_value is not None else NAN
             self.emit(OP_MAPVALUES, a=self.table(rows), b=len(ex.rows), c=k, x=mm, y=dv, pops=k, pushes=1)
+        elif isinstance(ex, ir.Apply) and ex.function in ("isIn", "isNotIn") and ex.args \
+                and isinstance(ex.args[0], ir.FieldRef) and ex.args[0].map_missing_to is None \
+                and len(ex.args) > 1 and all(isinstance(a, ir.Constant) and not a.missing and a.value is not None
+                                             for a in ex.args[1:]):
+            # membership in a constant list = a one-column MapValues table (member -> 1 / 0, anything
+            # else -> the default 0 / 1, a missing input -> mapMissingTo or missing)
+            fname = ex.args[0].field
+            self.load(fname)
+            hit, other = (1.0, 0.0) if ex.function == "isIn" else (0.0, 1.0)
+            rows = []
+            for a in ex.args[1:]:
+                rows += [s.lookup(fname, a.value), hit]
+            try:
+                mm = _opt(ex.map_missing_to)
+            except ValueError as e:
+                raise NotLowerable("non-numeric isIn mapMissingTo") from e
+            self.emit(OP_MAPVALUES, a=self.table(rows), b=len(ex.args) - 1, c=1, x=mm, y=other, pops=1, pushes=1)
         elif isinstance(ex, ir.Apply):
             fn = ex.function
             fid = APPLY_FN.get(fn)

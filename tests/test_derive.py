@@ -34,10 +34,13 @@ DICT = """
   <DerivedField name="miss_b" optype="continuous" dataType="double"><Apply function="isMissing"><FieldRef field="b"/></Apply></DerivedField>
   <DerivedField name="modv" optype="continuous" dataType="double"><Apply function="modulo"><FieldRef field="ab"/><Constant>-0.75</Constant></Apply></DerivedField>
   <DerivedField name="fa" optype="continuous" dataType="float"><FieldRef field="a"/></DerivedField>
+  <DerivedField name="in_c" optype="continuous" dataType="double"><Apply function="isIn"><FieldRef field="c"/><Constant>red</Constant><Constant>blue</Constant></Apply></DerivedField>
+  <DerivedField name="notin_a" optype="continuous" dataType="double"><Apply function="isNotIn" mapMissingTo="5"><FieldRef field="a"/><Constant>0</Constant><Constant>1.5</Constant></Apply></DerivedField>
  </TransformationDictionary>
 """
 
-DERIVED = ["log_a", "ab", "nb", "is_red", "bin_a", "code_c", "mx", "md", "cond", "miss_b", "modv", "fa"]
+DERIVED = ["log_a", "ab", "nb", "is_red", "bin_a", "code_c", "mx", "md", "cond", "miss_b", "modv", "fa", "in_c",
+           "notin_a"]
 
 
 def regression_doc() -> str:
