@@ -63,6 +63,10 @@ class ScoringConfig:
     engines); 0 = calibrate 1 vs 2 on the first copy and keep the faster (boxes differ)."""
     max_inflight: int = 4
     """Scored batches an operator keeps in flight before it waits for the oldest (backpressure)."""
+    graph_max_rows: int = 16384
+    """Micro-batches of at most this many rows run multi-kernel plans (wide NeuralNetworks,
+    segmented ensembles, derive pass + model) as one HIP-graph replay per row bucket
+    (:mod:`flink_jpmml_amd.runtime.graphs`); 0 = always launch kernel by kernel."""
     device_mirror: bool = False
     """Keep ``[rows]`` device copies of every columnar result (``PredictionBatch.device_out``) next
     to the pinned host scores, so a :class:`~flink_jpmml_amd.parallel.sinks.GatherSink` all-gathers
@@ -134,7 +138,8 @@ class ScoringConfig:
         kw = dict(batch_size=get("BATCH_SIZE", int), max_batch_latency_ms=get("MAX_BATCH_LATENCY_MS", float),
                   device=get("DEVICE", str), precision=get("PRECISION", str), fallback=get("FALLBACK", str),
                   micro_batch=get("MICRO_BATCH", int), cache_capacity=get("CACHE_CAPACITY", int),
-                  checkpoint_dir=get("CHECKPOINT_DIR", str), watchdog_s=get("WATCHDOG_S", float))
+                  checkpoint_dir=get("CHECKPOINT_DIR", str), watchdog_s=get("WATCHDOG_S", float),
+                  graph_max_rows=get("GRAPH_MAX_ROWS", int))
         kw = {k: v for k, v in kw.items() if v is not None}
         kw.update({k: v for k, v in overrides.items() if v is not None})
         return ScoringConfig(**kw)

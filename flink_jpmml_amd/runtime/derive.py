@@ -792,6 +792,7 @@ class FieldView:
 class DerivedPlan(DevicePlan):
     """derive kernel (prepare + derived fields) → model plan on the augmented matrix."""
 
+
     kind = "derived"
     _STATE = DevicePlan._STATE + ("insns", "pool", "out_cols", "n_tile", "n_sel", "n_insn", "supports_direct")
 

@@ -171,7 +171,8 @@ class StreamingScorer:
 
     def __init__(self, plan, micro_batch: int = 131072, depth: int = 3, max_rows: Optional[int] = None,
                  out_buffers: int = 2, direct_host_output: bool = True, keep_device_output: bool = True,
-                 h2d_streams: int = 0, pipeline: Optional[DevicePipeline] = None, max_inflight: int = 4):
+                 h2d_streams: int = 0, pipeline: Optional[DevicePipeline] = None, max_inflight: int = 4,
+                 graph_max_rows: int = 0):
         self.plan = plan
         self.device = plan.device
         self.F = plan.n_features
@@ -196,6 +197,12 @@ class StreamingScorer:
         from ..ops import _lib
 
         self._lib = _lib.load()
+        # multi-kernel plans: small micro-batches as one HIP-graph replay (runtime/graphs.py)
+        self._graphs = None
+        if graph_max_rows > 0 and getattr(plan, "graph_small_batches", False):
+            from .graphs import GraphLauncher
+
+            self._graphs = GraphLauncher(plan, max_rows=graph_max_rows)
 
     # ------------------------------------------------------------------ step API (bench engine mode)
     def _alloc_out(self, n: int):
@@ -268,7 +275,11 @@ class StreamingScorer:
                 p.ev_h2d[slot][j].record(st)
             for ev in p.ev_h2d[slot][: len(h2ds)]:
                 p.comp.wait_event(ev)
-        self.plan.launch(xs, out_score, out_valid, stream=p.comp, **kw)
+        g = self._graphs
+        if g is not None and g.applies(m, kw):
+            g.launch(xs, out_score, out_valid, stream=p.comp, **kw)
+        else:
+            self.plan.launch(xs, out_score, out_valid, stream=p.comp, **kw)
         if slot is not None:
             p.ev_comp[slot].record(p.comp)
             p.used[slot] = True
@@ -533,7 +544,7 @@ def make_scorer(compiled, device, config=None, pipeline: Optional[DevicePipeline
             return HostScorer(compiled, reason=str(e))
     if pipeline is None:
         pipeline = DevicePipeline(plan.device, cfg.micro_batch, cfg.pipeline_depth, cfg.h2d_streams)
-    return StreamingScorer(plan, pipeline=pipeline, max_inflight=cfg.max_inflight)
+    return StreamingScorer(plan, pipeline=pipeline, max_inflight=cfg.max_inflight, graph_max_rows=cfg.graph_max_rows)
 
 
 __all__ = ["DevicePipeline", "HostScorer", "NullScorer", "StepHandle", "StreamingScorer", "make_scorer"]

@@ -282,6 +282,8 @@ class GemmMlpPlan(MlpPlan):
     decode run as torch element-wise ops on the same stream. Slower than the fused kernel but no
     width / depth limit and no host fallback."""
 
+    graph_small_batches = True  # several launches per call: HIP-graph replay for small batches (runtime/graphs.py)
+
     kind = "mlp_gemm"
     supports_direct = False
     _STATE = DevicePlan._STATE + ("in_scale", "in_shift", "in_missing", "in_index", "n_in", "bf16", "out_a", "out_b",
@@ -357,6 +359,8 @@ class WideMlpPlan(MlpPlan):
     bf16 activations ping-pong through HBM — and an output-layer GEMM whose epilogue does the
     whole decode (output activation, softmax / simplemax, label table or affine + Target) into
     the score / valid / probability sinks. bf16 operands, fp32 accumulation."""
+
+    graph_small_batches = False  # measured slower replayed (profiles/r3ag): few, large kernels; the graph's copies cost more
 
     kind = "mlp_wide"
     supports_direct = True
@@ -686,6 +690,8 @@ class SvmGemmPlan(DevicePlan):
     kernel's limits (any number of machines, fields, support vectors); used when those limits bite.
     Reads prepared inputs (compile_plan puts a prepare-only derive pass in front when needed).
     Parity: the oracle's `models/svm.py::SvmEvaluator.decision_values/finish`."""
+
+    graph_small_batches = True  # several launches per call: HIP-graph replay for small batches (runtime/graphs.py)
 
     kind = "svm_gemm"
     supports_direct = False

@@ -210,6 +210,8 @@ def _index_outputs(plan) -> None:
 class SegmentedPlan(DevicePlan):
     """Per-segment device plans + device predicates + tensor-op aggregation (module docstring)."""
 
+    graph_small_batches = True  # several launches per call: HIP-graph replay for small batches (runtime/graphs.py)
+
     kind = "segmented"
     supports_direct = False
     _STATE = DevicePlan._STATE + ("method", "kind_", "skip", "weights", "progs", "remap_lists", "table", "tgt",
