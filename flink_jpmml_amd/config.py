@@ -63,6 +63,9 @@ class ScoringConfig:
     engines); 0 = calibrate 1 vs 2 on the first copy and keep the faster (boxes differ)."""
     max_inflight: int = 4
     """Scored batches an operator keeps in flight before it waits for the oldest (backpressure)."""
+    metrics_port: int = 0
+    """> 0: every rank serves its metrics in the Prometheus text format on ``GET /metrics`` at
+    ``metrics_port + rank`` (127.0.0.1) while a job runs (``utils/metrics.py``)."""
     graph_max_rows: int = 16384
     """Micro-batches of at most this many rows run multi-kernel plans (wide NeuralNetworks,
     segmented ensembles, derive pass + model) as one HIP-graph replay per row bucket
@@ -139,7 +142,7 @@ class ScoringConfig:
                   device=get("DEVICE", str), precision=get("PRECISION", str), fallback=get("FALLBACK", str),
                   micro_batch=get("MICRO_BATCH", int), cache_capacity=get("CACHE_CAPACITY", int),
                   checkpoint_dir=get("CHECKPOINT_DIR", str), watchdog_s=get("WATCHDOG_S", float),
-                  graph_max_rows=get("GRAPH_MAX_ROWS", int))
+                  graph_max_rows=get("GRAPH_MAX_ROWS", int), metrics_port=get("METRICS_PORT", int))
         kw = {k: v for k, v in kw.items() if v is not None}
         kw.update({k: v for k, v in overrides.items() if v is not None})
         return ScoringConfig(**kw)

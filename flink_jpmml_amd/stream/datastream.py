@@ -408,7 +408,19 @@ class StreamExecutionEnvironment:
         sinks, self._sinks = self._sinks, []
         if not sinks:
             raise RuntimeError("no sinks defined: nothing to execute")
-        return Executor(self, sinks, restore).run(job_name)
+        srv = None
+        port = int(getattr(self.config, "metrics_port", 0) or 0)
+        if port > 0:  # Prometheus scrape endpoint per rank for the job's lifetime
+            from ..utils.metrics import METRICS
+
+            rank = self.dist_ctx.rank if self.dist_ctx is not None else 0
+            srv = METRICS.serve_prometheus(port + rank, labels={"rank": str(rank), "job": job_name})
+        try:
+            return Executor(self, sinks, restore).run(job_name)
+        finally:
+            if srv is not None:
+                srv.shutdown()
+                srv.server_close()
 
 
 class DataStream:

@@ -142,3 +142,27 @@ def test_control_messages_pack_roundtrip():
         assert back == m and type(back) is type(m)
     a = AddMessage(NAME, 1, "/p", 0)
     assert a.model_id == ModelId(NAME, 1) and a.modelId == a.model_id and a.model_info == ModelInfo("/p")
+
+
+def test_metrics_prometheus_exposition():
+    import urllib.request
+
+    from flink_jpmml_amd.utils.metrics import Metrics
+
+    m = Metrics()
+    m.inc("scoring.rows_device", 4096)
+    m.inc("scoring.empty_score.preparation")
+    for v in (1.0, 2.0, 3.0):
+        m.observe("scoring.batch_latency_ms", v)
+    txt = m.prometheus_text(labels={"rank": "0"})
+    assert '# TYPE fja_scoring_rows_device counter' in txt
+    assert 'fja_scoring_rows_device{rank="0"} 4096' in txt
+    assert 'fja_scoring_batch_latency_ms{rank="0",quantile="0.5"} 2' in txt
+    assert 'fja_scoring_batch_latency_ms_count{rank="0"} 3' in txt
+    srv = m.serve_prometheus(port=0)
+    try:
+        port = srv.server_address[1]
+        body = urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics", timeout=5).read().decode()
+        assert "fja_scoring_rows_device 4096" in body
+    finally:
+        srv.shutdown()
