@@ -170,7 +170,7 @@ class KnnArgs(ctypes.Structure):
 class GemmArgs(ctypes.Structure):
     _fields_ = [("A", c_void_p), ("Wt", c_void_p), ("bias", c_void_p), ("C", c_void_p), ("rows", c_int),
                 ("rows_p", c_int), ("K", c_int), ("Mp", c_int), ("lda", c_int), ("ldw", c_int), ("ldc", c_int),
-                ("act", c_int), ("thr", c_float), ("n_out", c_int), ("final_norm", c_int), ("pad", c_int),
+                ("act", c_int), ("thr", c_float), ("n_out", c_int), ("final_norm", c_int), ("f32", c_int),
                 ("row_ok", c_void_p), ("epi", Epilogue), ("score", c_void_p), ("valid", c_void_p),
                 ("probs", c_void_p)]
 
@@ -178,7 +178,8 @@ class GemmArgs(ctypes.Structure):
 class NnPrepArgs(ctypes.Structure):
     _fields_ = [("X", c_void_p), ("n_rows", c_int), ("rows_p", c_int), ("ldx", c_int), ("n_in", c_int),
                 ("in_index", c_void_p), ("in_scale", c_void_p), ("in_shift", c_void_p), ("in_missing", c_void_p),
-                ("H", c_void_p), ("ldh", c_int), ("k0", c_int), ("row_ok", c_void_p)]
+                ("H", c_void_p), ("ldh", c_int), ("k0", c_int), ("row_ok", c_void_p), ("f32", c_int),
+                ("pad", c_int)]
 
 
 class LinearArgs(ctypes.Structure):

@@ -18,6 +18,11 @@
 // * Tile order is XCD-aware: consecutive tiles (the column tiles of one row tile, which share the
 //   A slice) are placed on the same XCD, so the A tile is fetched into one L2 once.
 // * Epilogue (hidden): + bias, activation, bf16, lane pairs merged into 4-byte stores.
+// * fp32 operands (the default fp32 precision policy): the same tiles, LDS images and schedule on
+//   the exact-fp32 v_mfma_f32_32x32x2f32 — a BK slice is 32 floats (still 128 B per row); a lane
+//   reads one 16-byte chunk (4 k) per operand tile and feeds it to 4 consecutive MFMAs, the k order
+//   permuted identically in A and B (k = 4 * chunk + element, chunk = 2 g + half), so the dot
+//   products are unchanged; activations stay fp32 between layers.
 // * The input stage is its own small kernel: one lane per (row, 8 inputs), validity by ballot.
 //   Epilogue (output layer): + bias into an LDS row tile, then one thread per row applies the
 //   output activation, softmax / simplemax, label table or regression affine + Target stage and
@@ -29,22 +34,24 @@ namespace {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int BM = 256;  // rows per block
-constexpr int BK = 64;   // k per LDS slice (128 B per row)
+constexpr int BK = 64;   // bf16 k per LDS slice (128 B per row); fp32: 32
+constexpr int SLICE_B = 128;  // bytes of one row in one LDS slice
 constexpr int NT = 512;  // threads (8 waves)
 constexpr int HEAD_LD = 33;
 
 struct GemmArgs {
-  const __bf16* A;        // [rows_p][lda] activations, rows_p = rows rounded up to BM
-  const __bf16* Wt;       // [Mp][ldw] weights, unit-major, Mp a multiple of BN
+  const void* A;          // [rows_p][lda] activations (bf16 or fp32), rows_p = rows rounded up to BM
+  const void* Wt;         // [Mp][ldw] weights, unit-major, Mp a multiple of BN
   const float* bias;      // [Mp]
-  __bf16* C;              // hidden layer output [rows_p][ldc]
-  int rows, rows_p, K, Mp;  // K: multiple of BK
+  void* C;                // hidden layer output [rows_p][ldc]
+  int rows, rows_p, K, Mp;  // K: multiple of the slice (64 bf16 / 32 fp32)
   int lda, ldw, ldc, act;
   float thr;              // threshold activation parameter
   int n_out, final_norm;  // output layer: real units, 0 none / 1 softmax / 2 simplemax
-  int pad;
+  int f32;                // operand / activation type: 0 bf16, 1 fp32
   const uint8_t* row_ok;  // [rows] input-stage validity (output layer)
   Epilogue epi;           // output layer decode (affine + Target, or label table)
   float* score;
@@ -59,15 +66,17 @@ struct PrepArgs {
   const float* in_scale;   // [n_in] NormContinuous as an affine map
   const float* in_shift;
   const float* in_missing; // [n_in] value for a missing input (NaN: the row has no prediction)
-  __bf16* H;               // [rows_p][ldh]
+  void* H;                 // [rows_p][ldh] bf16 or fp32
   int ldh, k0;             // k0: padded width (zero columns past n_in)
   uint8_t* row_ok;         // [rows_p]
+  int f32, pad;
 };
 
 // Input layer: gather the network inputs, normalise, replace missing, bf16. One thread per
 // (row, 8-input chunk) — a row's chunks are GP consecutive lanes (GP = chunks rounded up to a
 // power of two <= 64), so its reads and its 16-byte stores are contiguous, and the row's validity
 // is the AND over its lane group (one wave ballot).
+template <bool F32>
 __global__ __launch_bounds__(256) void nn_prep_kernel(PrepArgs a, int gp_log2) {
   const int GP = 1 << gp_log2;
   const int t = blockIdx.x * 256 + threadIdx.x;
@@ -79,7 +88,7 @@ __global__ __launch_bounds__(256) void nn_prep_kernel(PrepArgs a, int gp_log2) {
   bool bad = false;
   if (active) {
     const float* x = a.X + (size_t)(live_row ? row : 0) * a.ldx;
-    bf16x8 v;
+    float v[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int k = chunk * 8 + j;
@@ -90,9 +99,18 @@ __global__ __launch_bounds__(256) void nn_prep_kernel(PrepArgs a, int gp_log2) {
         bad = bad || (z != z);
         z = z == z ? z : 0.f;
       }
-      v[j] = (__bf16)z;
+      v[j] = z;
     }
-    *reinterpret_cast<bf16x8*>(a.H + (size_t)row * a.ldh + chunk * 8) = v;
+    if constexpr (F32) {
+      f32x4* o = reinterpret_cast<f32x4*>(static_cast<float*>(a.H) + (size_t)row * a.ldh + chunk * 8);
+      o[0] = f32x4{v[0], v[1], v[2], v[3]};
+      o[1] = f32x4{v[4], v[5], v[6], v[7]};
+    } else {
+      bf16x8 b;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) b[j] = (__bf16)v[j];
+      *reinterpret_cast<bf16x8*>(static_cast<__bf16*>(a.H) + (size_t)row * a.ldh + chunk * 8) = b;
+    }
   }
   const unsigned long long m = __ballot(bad);
   const int lane = threadIdx.x & 63;
@@ -105,11 +123,12 @@ __device__ __forceinline__ void glds16(const void* g, void* lds) {
   __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
 }
 
-// Stage one BK slice of `nrows` rows of a [.][ld] bf16 matrix into a swizzled LDS image.
+// Stage one 128-byte-per-row slice of `nrows` rows of a matrix with row pitch `ldb` bytes,
+// starting at byte column `kb0`, into a swizzled LDS image.
 // Instruction q of the block covers 1 KiB = 8 rows; lane L lands at byte q*1024 + 16 L.
 template <int NROWS>
-__device__ __forceinline__ void stage_slice(const __bf16* src, int ld, int k0, unsigned char* img, int wave,
-                                            int lane) {
+__device__ __forceinline__ void stage_slice(const unsigned char* src, size_t ldb, size_t kb0, unsigned char* img,
+                                            int wave, int lane) {
   constexpr int NINSTR = NROWS / 8;
   constexpr int PER_WAVE = (NINSTR + 7) / 8;
 #pragma unroll
@@ -119,13 +138,14 @@ __device__ __forceinline__ void stage_slice(const __bf16* src, int ld, int k0, u
       const int p = q * 64 + lane;
       const int r = p >> 3;
       const int c = (p & 7) ^ (r & 7);
-      glds16(src + (size_t)r * ld + k0 + 8 * c, img + q * 1024);
+      glds16(src + (size_t)r * ldb + kb0 + 16 * c, img + q * 1024);
     }
   }
 }
 
-__device__ __forceinline__ bf16x8 frag(const unsigned char* img, int r, int c) {
-  return *reinterpret_cast<const bf16x8*>(img + r * 128 + (((c ^ (r & 7)) & 7) << 4));
+template <typename V = bf16x8>
+__device__ __forceinline__ V frag(const unsigned char* img, int r, int c) {
+  return *reinterpret_cast<const V*>(img + r * SLICE_B + (((c ^ (r & 7)) & 7) << 4));
 }
 
 __device__ __noinline__ float activate_any(int act, float z, float thr) { return activate(act, z, thr); }
@@ -145,7 +165,7 @@ __device__ __forceinline__ float act_of(float z, int act, float thr) {
 // measured SLOWER — 3.02 vs 2.62 ms for a 1024 x 1024 layer over 1M rows, profiles/r3l: with one
 // workgroup per CU the block-wide barrier exposes the whole store phase, while direct stores
 // drain behind the other waves' MFMAs.)
-template <int ACT, int TM, int TN>
+template <int ACT, int TM, int TN, bool F32>
 __device__ __forceinline__ void store_hidden(const GemmArgs& a, const f32x16 (&acc)[TM][TN], int row0, int col0,
                                              int wm, int wn, int lane) {
   const int h = lane >> 5, l32 = lane & 31;
@@ -156,6 +176,17 @@ __device__ __forceinline__ void store_hidden(const GemmArgs& a, const f32x16 (&a
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int rb = row0 + (wm * TM + i) * 32 + 4 * h;
+      if constexpr (F32) {  // 32 consecutive units per half-wave: one 128-byte segment per store.
+        // One running pointer (rows rb + 0..3, +8..11, ...) instead of a 64-bit address per store.
+        float* p = static_cast<float*>(a.C) + (size_t)rb * a.ldc + unit;
+        const size_t ld = (size_t)a.ldc;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          *p = act_of<ACT>(acc[i][j][r] + b, a.act, a.thr);
+          p += (r & 3) == 3 ? 5 * ld : ld;
+        }
+        continue;
+      }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const float v = act_of<ACT>(acc[i][j][r] + b, a.act, a.thr);
@@ -164,21 +195,23 @@ __device__ __forceinline__ void store_hidden(const GemmArgs& a, const f32x16 (&a
         const uint32_t hi = __builtin_bit_cast(uint16_t, (__bf16)o);
         if ((lane & 1) == 0) {
           const int row = rb + (r & 3) + 8 * (r >> 2);
-          *reinterpret_cast<uint32_t*>(a.C + (size_t)row * a.ldc + unit) = lo | (hi << 16);
+          *reinterpret_cast<uint32_t*>(static_cast<__bf16*>(a.C) + (size_t)row * a.ldc + unit) = lo | (hi << 16);
         }
       }
     }
   }
 }
 
-template <int BN, bool HEAD>
+template <int BN, bool HEAD, bool F32>
 __global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmArgs a) {
   constexpr int WM = BN == 256 ? 2 : 8;  // waves along rows
   constexpr int WN = 8 / WM;             // waves along units
   constexpr int TM = BM / WM / 32;       // 32-row accumulator tiles per wave
   constexpr int TN = BN / WN / 32;       // 32-unit accumulator tiles per wave
-  constexpr int A_BYTES = BM * BK * 2;
-  constexpr int B_BYTES = BN * BK * 2;
+  constexpr int ES = F32 ? 4 : 2;          // element bytes
+  constexpr int SK = SLICE_B / ES;          // k per slice
+  constexpr int A_BYTES = BM * SLICE_B;
+  constexpr int B_BYTES = BN * SLICE_B;
   extern __shared__ __align__(16) unsigned char smem[];
   unsigned char* As = smem;
   unsigned char* Bs = smem + 2 * A_BYTES;
@@ -199,32 +232,52 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmArgs a) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x16{};
 
-  const __bf16* Ab = a.A + (size_t)row0 * a.lda;
-  const __bf16* Bb = a.Wt + (size_t)col0 * a.ldw;
-  const int KT = a.K / BK;
-  stage_slice<BM>(Ab, a.lda, 0, As, wave, lane);
-  stage_slice<BN>(Bb, a.ldw, 0, Bs, wave, lane);
+  const size_t lda_b = (size_t)a.lda * ES, ldw_b = (size_t)a.ldw * ES;
+  const unsigned char* Ab = static_cast<const unsigned char*>(a.A) + (size_t)row0 * lda_b;
+  const unsigned char* Bb = static_cast<const unsigned char*>(a.Wt) + (size_t)col0 * ldw_b;
+  const int KT = a.K / SK;
+  stage_slice<BM>(Ab, lda_b, 0, As, wave, lane);
+  stage_slice<BN>(Bb, ldw_b, 0, Bs, wave, lane);
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
   for (int kt = 0; kt < KT; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < KT) {  // next slice in flight while this one computes
-      stage_slice<BM>(Ab, a.lda, (kt + 1) * BK, As + (cur ^ 1) * A_BYTES, wave, lane);
-      stage_slice<BN>(Bb, a.ldw, (kt + 1) * BK, Bs + (cur ^ 1) * B_BYTES, wave, lane);
+      stage_slice<BM>(Ab, lda_b, (size_t)(kt + 1) * SLICE_B, As + (cur ^ 1) * A_BYTES, wave, lane);
+      stage_slice<BN>(Bb, ldw_b, (size_t)(kt + 1) * SLICE_B, Bs + (cur ^ 1) * B_BYTES, wave, lane);
     }
     const unsigned char* ai = As + cur * A_BYTES;
     const unsigned char* bi = Bs + cur * B_BYTES;
+    if constexpr (F32) {
 #pragma unroll
-    for (int ks = 0; ks < BK / 16; ++ks) {
-      bf16x8 af[TM], bfr[TN];
+      for (int g = 0; g < 4; ++g) {  // chunk 2g + h: 4 k per lane, one MFMA each
+        f32x4 af[TM], bfr[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = frag(ai, (wm * TM + i) * 32 + l32, 2 * ks + h);
+        for (int i = 0; i < TM; ++i) af[i] = frag<f32x4>(ai, (wm * TM + i) * 32 + l32, 2 * g + h);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) bfr[j] = frag(bi, (wn * TN + j) * 32 + l32, 2 * ks + h);
+        for (int j = 0; j < TN; ++j) bfr[j] = frag<f32x4>(bi, (wn * TN + j) * 32 + l32, 2 * g + h);
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+        for (int e = 0; e < 4; ++e)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][e], bfr[j][e], acc[i][j], 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < BK / 16; ++ks) {
+        bf16x8 af[TM], bfr[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) af[i] = frag(ai, (wm * TM + i) * 32 + l32, 2 * ks + h);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) bfr[j] = frag(bi, (wn * TN + j) * 32 + l32, 2 * ks + h);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
     }
     __builtin_amdgcn_s_waitcnt(0);  // the slice in flight has landed (LDS-DMA retires on vmcnt)
     __syncthreads();                // ... for every wave before anyone reads / overwrites it
@@ -232,11 +285,11 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmArgs a) {
 
   if constexpr (!HEAD) {
     switch (a.act) {  // uniform: one unrolled epilogue per common activation
-      case A_IDENTITY: store_hidden<A_IDENTITY, TM, TN>(a, acc, row0, col0, wm, wn, lane); break;
-      case A_RELU: store_hidden<A_RELU, TM, TN>(a, acc, row0, col0, wm, wn, lane); break;
-      case A_LOGISTIC: store_hidden<A_LOGISTIC, TM, TN>(a, acc, row0, col0, wm, wn, lane); break;
-      case A_TANH: store_hidden<A_TANH, TM, TN>(a, acc, row0, col0, wm, wn, lane); break;
-      default: store_hidden<-1, TM, TN>(a, acc, row0, col0, wm, wn, lane); break;
+      case A_IDENTITY: store_hidden<A_IDENTITY, TM, TN, F32>(a, acc, row0, col0, wm, wn, lane); break;
+      case A_RELU: store_hidden<A_RELU, TM, TN, F32>(a, acc, row0, col0, wm, wn, lane); break;
+      case A_LOGISTIC: store_hidden<A_LOGISTIC, TM, TN, F32>(a, acc, row0, col0, wm, wn, lane); break;
+      case A_TANH: store_hidden<A_TANH, TM, TN, F32>(a, acc, row0, col0, wm, wn, lane); break;
+      default: store_hidden<-1, TM, TN, F32>(a, acc, row0, col0, wm, wn, lane); break;
     }
   } else {
     float* zt = reinterpret_cast<float*>(smem);  // [BM][HEAD_LD] (the staging buffers are drained)
@@ -283,16 +336,16 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmArgs a) {
   }
 }
 
-template <int BN, bool HEAD>
+template <int BN, bool HEAD, bool F32>
 int launch(hipStream_t stream, const GemmArgs& a) {
-  const size_t stage = 2 * (size_t)BM * BK * 2 + 2 * (size_t)BN * BK * 2;
+  const size_t stage = 2 * (size_t)BM * SLICE_B + 2 * (size_t)BN * SLICE_B;
   const size_t head = HEAD ? (size_t)BM * HEAD_LD * 4 : 0;
   const size_t lds = stage > head ? stage : head;
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_kernel<BN, HEAD>),
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_kernel<BN, HEAD, F32>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return -5;
   dim3 grid((a.rows_p / BM) * (a.Mp / BN));
-  hipLaunchKernelGGL((gemm_kernel<BN, HEAD>), grid, dim3(NT), lds, stream, a);
+  hipLaunchKernelGGL((gemm_kernel<BN, HEAD, F32>), grid, dim3(NT), lds, stream, a);
   return 0;
 }
 
@@ -306,24 +359,31 @@ PMML_API int pmml_nn_prep_launch(hipStream_t stream, const PrepArgs* args) {
   if (a.rows_p <= 0) return 0;
   if ((a.k0 & 7) || a.k0 < a.n_in || a.k0 > 512 || (a.ldh & 7) || (reinterpret_cast<uintptr_t>(a.H) & 15))
     return -4;
+  if (a.f32 != 0 && a.f32 != 1) return -4;
   int g = 0;
   while ((1 << g) < (a.k0 >> 3)) ++g;  // lanes per row: chunks rounded up to a power of two (<= 64)
   const long long threads = (long long)a.rows_p << g;
-  hipLaunchKernelGGL(nn_prep_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, stream, a, g);
+  const dim3 grid((unsigned)((threads + 255) / 256));
+  if (a.f32) hipLaunchKernelGGL(nn_prep_kernel<true>, grid, dim3(256), 0, stream, a, g);
+  else hipLaunchKernelGGL(nn_prep_kernel<false>, grid, dim3(256), 0, stream, a, g);
   return hipGetLastError() == hipSuccess ? 0 : -7;
 }
 
-// head = 0: hidden layer (BN 256, bf16 output C); head = 1: output layer (BN 32, n_out <= 32, decode).
+// head = 0: hidden layer (BN 256, output C in the operand type); head = 1: output layer (BN 32,
+// n_out <= 32, decode). args->f32 selects bf16 (0) or fp32 (1) operands.
 PMML_API int pmml_gemm_launch(hipStream_t stream, const GemmArgs* args, int head) {
   const GemmArgs a = *args;
   if (a.rows <= 0) return 0;
   const int BN = head ? 32 : 256;
-  if (a.rows_p % BM || a.rows_p < a.rows || a.K % BK || a.K <= 0 || a.Mp % BN || a.Mp <= 0) return -4;
+  if (a.f32 != 0 && a.f32 != 1) return -4;
+  const int sk = a.f32 ? SLICE_B / 4 : SLICE_B / 2;
+  if (a.rows_p % BM || a.rows_p < a.rows || a.K % sk || a.K <= 0 || a.Mp % BN || a.Mp <= 0) return -4;
   if ((a.lda & 7) || (a.ldw & 7) || a.lda < a.K || a.ldw < a.K) return -4;
   if ((reinterpret_cast<uintptr_t>(a.A) & 15) || (reinterpret_cast<uintptr_t>(a.Wt) & 15)) return -4;
   if (head && (a.n_out < 1 || a.n_out > 32 || a.Mp != 32 || !a.row_ok || !a.score || !a.valid)) return -4;
   if (!head && ((a.ldc & 7) || a.ldc < a.Mp || !a.C || (reinterpret_cast<uintptr_t>(a.C) & 15))) return -4;
-  const int rc = head ? launch<32, true>(stream, a) : launch<256, false>(stream, a);
+  const int rc = a.f32 ? (head ? launch<32, true, true>(stream, a) : launch<256, false, true>(stream, a))
+                       : (head ? launch<32, true, false>(stream, a) : launch<256, false, false>(stream, a));
   if (rc) return rc;
   return hipGetLastError() == hipSuccess ? 0 : -7;
 }

@@ -358,7 +358,8 @@ class WideMlpPlan(MlpPlan):
     bf16), then ONE fused MFMA GEMM launch per layer — bias and activation in the epilogue,
     bf16 activations ping-pong through HBM — and an output-layer GEMM whose epilogue does the
     whole decode (output activation, softmax / simplemax, label table or affine + Target) into
-    the score / valid / probability sinks. bf16 operands, fp32 accumulation."""
+    the score / valid / probability sinks. bf16 operands (precision bf16 / fp8) or exact fp32
+    operands on ``v_mfma_f32_32x32x2f32`` (the default fp32 policy); fp32 accumulation."""
 
     graph_small_batches = False  # measured slower replayed (profiles/r3ag): few, large kernels; the graph's copies cost more
 
@@ -374,9 +375,9 @@ class WideMlpPlan(MlpPlan):
 
         DevicePlan.__init__(self, compiled, device)
         ev: NeuralEvaluator = compiled.evaluator
-        if precision != "bf16":
-            raise NotLowerable("the wide-layer GEMM runs bf16 operands (precision policy bf16 / fp8)")
-        self.bf16 = 1
+        if precision not in ("bf16", "fp32"):
+            raise ValueError("precision must be bf16 or fp32")
+        self.bf16 = 1 if precision == "bf16" else 0
         layers, _ = self._io(compiled, ev)
         if self.n_out > 32:
             raise NotLowerable("more than 32 output neurons")
@@ -400,9 +401,14 @@ class WideMlpPlan(MlpPlan):
             wo += Wt.size
             bo += mp
             kp = mp
-        self.wts = torch.from_numpy(np.concatenate(wts)).to(torch.bfloat16).to(self.device)
+        self.wts = torch.from_numpy(np.concatenate(wts)).to(self._dtype()).to(self.device)
         self.bss = self._t(np.concatenate(bss))
         self.dims = dims
+
+    def _dtype(self):
+        import torch
+
+        return torch.bfloat16 if self.bf16 else torch.float32
 
     def launch(self, X, score, valid, stream=None, probs=None, score2=None, valid2=None) -> None:
         import ctypes
@@ -419,21 +425,23 @@ class WideMlpPlan(MlpPlan):
         h = stream_handle(st)
         with torch.cuda.stream(st):
             widest = max(mp for _, mp, *_ in self.dims[:-1]) if len(self.dims) > 1 else 0
-            H0 = torch.empty((rows_p, self.k0), dtype=torch.bfloat16, device=self.device)
-            bufs = [torch.empty((rows_p, widest), dtype=torch.bfloat16, device=self.device) for _ in range(2)] \
+            dt = self._dtype()
+            H0 = torch.empty((rows_p, self.k0), dtype=dt, device=self.device)
+            bufs = [torch.empty((rows_p, widest), dtype=dt, device=self.device) for _ in range(2)] \
                 if widest else []
             ok = torch.empty(rows_p, dtype=torch.uint8, device=self.device)
         p = NnPrepArgs()
         p.X, p.n_rows, p.rows_p, p.ldx, p.n_in = X.data_ptr(), n, rows_p, X.stride(0), self.n_in
         p.in_index, p.in_scale, p.in_shift = ptr(self.in_index), ptr(self.in_scale), ptr(self.in_shift)
         p.in_missing, p.H, p.ldh, p.k0, p.row_ok = ptr(self.in_missing), H0.data_ptr(), self.k0, self.k0, ok.data_ptr()
+        p.f32 = 1 - self.bf16
         check(self.lib.pmml_nn_prep_launch(h, ctypes.byref(p)), "nn input stage")
-        wbase, bbase = self.wts.data_ptr(), self.bss.data_ptr()
+        wbase, bbase, es = self.wts.data_ptr(), self.bss.data_ptr(), 2 if self.bf16 else 4
         cur, lda = H0, self.k0
         for li, (kp, mp, act, thr, wo, bo) in enumerate(self.dims):
             head = li == len(self.dims) - 1
             a = GemmArgs()
-            a.A, a.Wt, a.bias = cur.data_ptr(), wbase + 2 * wo, bbase + 4 * bo
+            a.A, a.Wt, a.bias, a.f32 = cur.data_ptr(), wbase + es * wo, bbase + 4 * bo, 1 - self.bf16
             a.rows, a.rows_p, a.K, a.Mp = n, rows_p, kp, mp
             a.lda, a.ldw, a.act, a.thr = lda, kp, act, thr
             if head:

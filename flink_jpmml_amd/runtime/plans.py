@@ -1784,15 +1784,16 @@ def compile_plan(compiled, device, **opts) -> DevicePlan:
         if impl == "gemm":
             return GemmMlpPlan(compiled, device, precision=prec)
         if impl == "wide":
-            return WideMlpPlan(compiled, device, precision="bf16")
+            return WideMlpPlan(compiled, device, precision=prec)
         try:
             return MlpPlan(compiled, device, precision=prec, **opts)
         except NotLowerable as e:
             if "fused kernel" not in str(e) or impl == "fused":
                 raise
-            if prec == "bf16":  # wide layers: one fused MFMA GEMM launch per layer (ops/csrc/gemm.hip)
+            try:  # wide layers: one fused MFMA GEMM launch per layer (ops/csrc/gemm.hip), bf16 or fp32
                 return WideMlpPlan(compiled, device, precision=prec)
-            return GemmMlpPlan(compiled, device, precision=prec)
+            except NotLowerable:  # > 32 outputs or > 512 inputs: library GEMMs
+                return GemmMlpPlan(compiled, device, precision=prec)
     if isinstance(ev, SvmEvaluator):
         from .nn_plans import SvmGemmPlan, SvmPlan, SvmWidePlan
 

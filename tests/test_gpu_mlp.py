@@ -61,17 +61,19 @@ def test_mlp_gathered_inputs_and_classification(gpu):
     assert (v == vref).all() and (s == ref).mean() > 0.9999
 
 
+@pytest.mark.parametrize("impl", ["auto", "gemm"])
 @pytest.mark.parametrize("hidden", [(1024,), (64,) * 9])
-def test_mlp_beyond_fused_kernel_runs_on_device(gpu, hidden):
-    """A 1024-unit layer and a 10-layer network exceed the fused kernel's registers / LDS: they
-    run as per-layer library GEMMs on the device (GemmMlpPlan), never on the host."""
+def test_mlp_beyond_fused_kernel_runs_on_device(gpu, hidden, impl):
+    """A 1024-unit layer and a 10-layer network exceed the fused kernel's registers / LDS: under
+    the default fp32 policy they run on the fused GEMM's exact-fp32 MFMA variant (WideMlpPlan);
+    ``mlp_impl="gemm"`` forces per-layer library GEMMs. Never on the host."""
     from flink_jpmml_amd.bench.synth import mlp_pmml, stream_matrix
     from flink_jpmml_amd.runtime.compiled import CompiledPmml
-    from flink_jpmml_amd.runtime.nn_plans import GemmMlpPlan
+    from flink_jpmml_amd.runtime.nn_plans import GemmMlpPlan, WideMlpPlan
 
     c = CompiledPmml.from_string(mlp_pmml(n_features=32, hidden=hidden, n_out=1, seed=7))
-    plan = c.plan(gpu)
-    assert isinstance(plan, GemmMlpPlan)
+    plan = c.plan(gpu, mlp_impl=impl)
+    assert isinstance(plan, WideMlpPlan if impl == "auto" else GemmMlpPlan) and plan.bf16 == 0
     X = stream_matrix(8192, 32, seed=3)
     X[3, 4] = np.nan
     s, v = _np(plan, X)

@@ -3,7 +3,8 @@
 CPU: the plan's packed operands (unit-major bf16 weights padded to the kernel tiles, fp32 biases,
 the input stage) run through a numpy model of the kernels' arithmetic — bf16 operands, fp32
 accumulation, bf16 activations between layers — and must reproduce the float64 oracle within bf16
-tolerance. GPU: the kernels against the same model (tight) and the oracle (bf16 tolerance)."""
+tolerance. The fp32 variant (default fp32 policy: exact-fp32 MFMA, fp32 activations) must match
+the oracle to fp32 rounding. GPU: the kernels against the same model (tight) and the oracle."""
 
 import numpy as np
 import pytest
@@ -35,14 +36,15 @@ def emulate_wide(plan, X):
     ok = ~np.isnan(z).any(axis=1)
     H = np.zeros((len(X), plan.k0), np.float32)
     H[:, : plan.n_in] = np.nan_to_num(z)
-    H = _bf16(H)
+    rnd = _bf16 if plan.bf16 else (lambda a: np.asarray(a, np.float32))
+    H = rnd(H)
     W = plan.wts.float().cpu().numpy()
     B = plan.bss.cpu().numpy()
     for li, (kp, mp, act, thr, wo, bo) in enumerate(plan.dims):
         Wt = W[wo: wo + mp * kp].reshape(mp, kp)
         Z = (H[:, :kp].astype(np.float64) @ Wt.T.astype(np.float64)).astype(np.float32) + B[bo: bo + mp]
         Z = _ACT[act](Z).astype(np.float32)
-        H = _bf16(Z) if li < len(plan.dims) - 1 else Z
+        H = rnd(Z) if li < len(plan.dims) - 1 else Z
     out = H[:, : plan.n_out]
     if plan.is_classification:
         P = np.exp(out - out.max(1, keepdims=True)) if plan.final_norm == 1 else out
@@ -77,34 +79,58 @@ def test_wide_plan_packing_matches_oracle(shape):
         assert np.abs(s[v] - ref[v]).max() < 3e-2 * scale
 
 
-def test_fp32_policy_keeps_library_gemm():
-    """fp32 precision policy: wide layers stay fp32 (library GEMM); bf16 operands are opt-in."""
+@pytest.mark.parametrize("shape", SHAPES, ids=lambda d: "x".join(map(str, d["hidden"])))
+def test_fp32_policy_runs_fp32_wide_gemm(shape):
+    """fp32 precision policy: wide layers stay fp32 — on the fused GEMM's exact-fp32 MFMA variant
+    (not a library GEMM); bf16 operands are opt-in. Packed fp32 operands reproduce the oracle."""
+    from flink_jpmml_amd.runtime.nn_plans import WideMlpPlan
+    from flink_jpmml_amd.runtime.plans import compile_plan, lowering_dry_run
+
+    c = CompiledPmml.from_string(mlp_pmml(seed=5, **shape))
+    with lowering_dry_run():
+        plan = compile_plan(c, torch.device("cpu"))
+    assert isinstance(plan, WideMlpPlan) and plan.bf16 == 0 and plan.wts.dtype == torch.float32
+    X = stream_matrix(2000, shape["n_features"], seed=2, missing_rate=0.01)
+    s, v = emulate_wide(plan, X)
+    ref, vref = c.score_matrix_oracle(X)
+    assert (v == vref).all()
+    if shape.get("classification"):
+        assert (s[v] == ref[v]).mean() > 0.999
+    else:
+        scale = max(1.0, float(np.abs(ref[v]).max()))
+        assert np.abs(s[v] - ref[v]).max() < 1e-4 * scale
+
+
+def test_library_gemm_beyond_wide_limits():
+    """More than 32 output neurons: the wide GEMM's output tile is 32 units — library GEMMs."""
     from flink_jpmml_amd.runtime.nn_plans import GemmMlpPlan
     from flink_jpmml_amd.runtime.plans import compile_plan, lowering_dry_run
 
-    c = CompiledPmml.from_string(mlp_pmml(n_features=32, hidden=(1024,), seed=1))
+    c = CompiledPmml.from_string(mlp_pmml(n_features=8, hidden=(300,), n_out=40, classification=True, seed=1))
     with lowering_dry_run():
         assert isinstance(compile_plan(c, torch.device("cpu")), GemmMlpPlan)
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("precision", ["bf16", "fp32"])
 @pytest.mark.parametrize("shape", SHAPES, ids=lambda d: "x".join(map(str, d["hidden"])))
-def test_wide_gemm_kernels_on_gpu(gpu, shape):
+def test_wide_gemm_kernels_on_gpu(gpu, shape, precision):
     from flink_jpmml_amd.runtime.nn_plans import WideMlpPlan
 
     c = CompiledPmml.from_string(mlp_pmml(seed=5, **shape))
-    plan = c.plan(gpu, precision="bf16")
-    assert isinstance(plan, WideMlpPlan)
+    plan = c.plan(gpu, precision=precision)
+    assert isinstance(plan, WideMlpPlan) and plan.bf16 == (precision == "bf16")
     X = stream_matrix(10_001, shape["n_features"], seed=3, missing_rate=0.01)  # not a multiple of 256
     s, v = plan.score(X)
     s, v = s.cpu().numpy(), v.cpu().numpy()
     es, ev = emulate_wide(plan, X)
     ref, vref = c.score_matrix_oracle(X)
     assert (v == ev).all() and (v == vref).all()
+    fp32 = precision == "fp32"
     if shape.get("classification"):
         assert (s[v] == es[v]).mean() > 0.995
-        assert (s[v] == ref[v]).mean() > 0.98
+        assert (s[v] == ref[v]).mean() > (0.999 if fp32 else 0.98)
     else:
         scale = max(1.0, float(np.abs(ref[v]).max()))
-        assert np.abs(s[v] - es[v]).max() < 5e-3 * scale  # same bf16 operands: summation order only
-        assert np.abs(s[v] - ref[v]).max() < 3e-2 * scale
+        assert np.abs(s[v] - es[v]).max() < (1e-4 if fp32 else 5e-3) * scale  # same operands: summation order
+        assert np.abs(s[v] - ref[v]).max() < (1e-4 if fp32 else 3e-2) * scale
