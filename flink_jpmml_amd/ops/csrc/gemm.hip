@@ -126,6 +126,12 @@ __device__ __forceinline__ void glds16(const void* g, void* lds) {
 // Stage one 128-byte-per-row slice of `nrows` rows of a matrix with row pitch `ldb` bytes,
 // starting at byte column `kb0`, into a swizzled LDS image.
 // Instruction q of the block covers 1 KiB = 8 rows; lane L lands at byte q*1024 + 16 L.
+// LDS chunk swizzle of row r: (r >> 1) & 7. Two 128-byte rows share one 256-byte bank row, so the
+// 16 rows a ds_read_b128 lane group reads need 16 distinct (row parity, chunk) slots — this is
+// conflict-free; r & 7 left rows r and r + 8 on one slot (2-way: SQ_LDS_BANK_CONFLICT 1.9e9 -> 0,
+// LDS busy -40 %, same wall time in this barrier-bound loop, profiles/r3ak).
+__device__ __forceinline__ int swz(int r) { return (r >> 1) & 7; }
+
 template <int NROWS>
 __device__ __forceinline__ void stage_slice(const unsigned char* src, size_t ldb, size_t kb0, unsigned char* img,
                                             int wave, int lane) {
@@ -137,7 +143,7 @@ __device__ __forceinline__ void stage_slice(const unsigned char* src, size_t ldb
     if (NINSTR % 8 == 0 || q < NINSTR) {
       const int p = q * 64 + lane;
       const int r = p >> 3;
-      const int c = (p & 7) ^ (r & 7);
+      const int c = (p & 7) ^ swz(r);
       glds16(src + (size_t)r * ldb + kb0 + 16 * c, img + q * 1024);
     }
   }
@@ -145,7 +151,7 @@ __device__ __forceinline__ void stage_slice(const unsigned char* src, size_t ldb
 
 template <typename V = bf16x8>
 __device__ __forceinline__ V frag(const unsigned char* img, int r, int c) {
-  return *reinterpret_cast<const V*>(img + r * SLICE_B + (((c ^ (r & 7)) & 7) << 4));
+  return *reinterpret_cast<const V*>(img + r * SLICE_B + (((c ^ swz(r)) & 7) << 4));
 }
 
 __device__ __noinline__ float activate_any(int act, float z, float thr) { return activate(act, z, thr); }
@@ -376,14 +382,15 @@ PMML_API int pmml_gemm_launch(hipStream_t stream, const GemmArgs* args, int head
   if (a.rows <= 0) return 0;
   const int BN = head ? 32 : 256;
   if (a.f32 != 0 && a.f32 != 1) return -4;
-  const int sk = a.f32 ? SLICE_B / 4 : SLICE_B / 2;
+  const int f32 = a.f32;
+  const int sk = f32 ? SLICE_B / 4 : SLICE_B / 2;
   if (a.rows_p % BM || a.rows_p < a.rows || a.K % sk || a.K <= 0 || a.Mp % BN || a.Mp <= 0) return -4;
   if ((a.lda & 7) || (a.ldw & 7) || a.lda < a.K || a.ldw < a.K) return -4;
   if ((reinterpret_cast<uintptr_t>(a.A) & 15) || (reinterpret_cast<uintptr_t>(a.Wt) & 15)) return -4;
   if (head && (a.n_out < 1 || a.n_out > 32 || a.Mp != 32 || !a.row_ok || !a.score || !a.valid)) return -4;
   if (!head && ((a.ldc & 7) || a.ldc < a.Mp || !a.C || (reinterpret_cast<uintptr_t>(a.C) & 15))) return -4;
-  const int rc = a.f32 ? (head ? launch<32, true, true>(stream, a) : launch<256, false, true>(stream, a))
-                       : (head ? launch<32, true, false>(stream, a) : launch<256, false, false>(stream, a));
+  const int rc = f32 ? (head ? launch<32, true, true>(stream, a) : launch<256, false, true>(stream, a))
+                     : (head ? launch<32, true, false>(stream, a) : launch<256, false, false>(stream, a));
   if (rc) return rc;
   return hipGetLastError() == hipSuccess ? 0 : -7;
 }

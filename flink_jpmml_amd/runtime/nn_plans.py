@@ -405,6 +405,8 @@ class WideMlpPlan(MlpPlan):
         self.bss = self._t(np.concatenate(bss))
         self.dims = dims
 
+    gemm_flags = 0  # experiment bits ORed into GemmArgs.f32 (scripts/gemm_ab.py); the kernel rejects unknown bits
+
     def _dtype(self):
         import torch
 
@@ -441,7 +443,7 @@ class WideMlpPlan(MlpPlan):
         for li, (kp, mp, act, thr, wo, bo) in enumerate(self.dims):
             head = li == len(self.dims) - 1
             a = GemmArgs()
-            a.A, a.Wt, a.bias, a.f32 = cur.data_ptr(), wbase + es * wo, bbase + 4 * bo, 1 - self.bf16
+            a.A, a.Wt, a.bias, a.f32 = cur.data_ptr(), wbase + es * wo, bbase + 4 * bo, (1 - self.bf16) | self.gemm_flags
             a.rows, a.rows_p, a.K, a.Mp = n, rows_p, kp, mp
             a.lda, a.ldw, a.act, a.thr = lda, kp, act, thr
             if head:
