@@ -342,6 +342,178 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Hidden layers, bf16, phase-interleaved (gemm8_kernel). Same 256 x 256 tile, BK = 64 slices, 8
+// waves with a 128 x 64 sub-tile each (4 x 2 accumulators of 32x32x16), but:
+//  * each slice is staged as four 16 KiB half-tiles — A0 / A1: the first / second 64 rows of
+//    each wave row-group's 128, B0 / B1: the first / second 32 units of each wave column's 64 —
+//    into two buffers of four slots;
+//  * a slice is consumed in four phases, one output quadrant each: P1 A0 x B0 (reads A0, B0),
+//    P2 A0 x B1 (reads B1), P3 A1 x B1 (reads A1), P4 A1 x B0 (no reads, B0 kept in registers);
+//    a phase = its fragment reads + one half-tile LDS-DMA, lgkmcnt(0), raw barrier, 8 MFMAs,
+//    raw barrier;
+//  * a slot is restaged one phase after the barrier that ends its last read: P1 stages A1 of
+//    slice t + 1 (into the other buffer), P2 / P3 / P4 stage A0 / B0 / B1 of slice t + 2 into
+//    the slots P1 / P1 / P2 freed, and ONE counted vmcnt(6) per slice (at P4, after its issue)
+//    retires everything of slice t + 1 while three half-tiles of t + 2 stay in flight across
+//    the barriers (__syncthreads() would add vmcnt(0));
+//  * the two wave row-groups run one barrier apart (group 1 passes one extra barrier first), so
+//    on every SIMD one wave's MFMAs overlap the other wave's fragment reads and staging.
+// Hazards, by barrier matching (group 1's n-th barrier is group 0's (n+1)-th): a wave reads a
+// slice only after a barrier that every wave reached after its vmcnt for that slice; a wave
+// restages a slot only after a barrier that every wave reached after lgkmcnt(0) on its reads of
+// the slot's previous contents.
+// ---------------------------------------------------------------------------------------------
+constexpr int HALF_B = 128 * SLICE_B;  // one half-tile slot: 128 rows x 128 B
+
+// Half-tile `half` of a slice: slot row j <- A row (j >> 6) * 128 + half * 64 + (j & 63), or
+// weight row (unit) (j >> 5) * 64 + half * 32 + (j & 31). Two 1 KiB LDS-DMA instructions per wave.
+template <bool IS_A>
+__device__ __forceinline__ void stage_half(const unsigned char* src, size_t ldb, size_t kb0, unsigned char* slot,
+                                           int half, int wave, int lane) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int q = wave * 2 + i;
+    const int p = q * 64 + lane;
+    const int j = p >> 3;
+    const int c = (p & 7) ^ swz(j);
+    const int r = IS_A ? ((j >> 6) * 128 + half * 64 + (j & 63)) : ((j >> 5) * 64 + half * 32 + (j & 31));
+    glds16(src + (size_t)r * ldb + kb0 + 16 * c, slot + q * 1024);
+  }
+}
+
+__device__ __forceinline__ void raw_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// A phase: reads issued -> mma_begin (lgkmcnt(0), barrier, high priority) -> MFMAs -> mma_end.
+__device__ __forceinline__ void mma_begin() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  raw_barrier();
+  __builtin_amdgcn_s_setprio(1);
+}
+__device__ __forceinline__ void mma_end() {
+  __builtin_amdgcn_s_setprio(0);
+  raw_barrier();
+}
+
+// acc[i0 + i][j] += a[i] . b over the slice's four k16 steps. The empty volatile asm on the
+// accumulators pins the MFMAs between the phase's two barriers (register-only instructions are
+// otherwise free to sink past them; sched_barrier alone did not keep them there).
+__device__ __forceinline__ void mma_quad(f32x16& c0, f32x16& c1, const bf16x8 (&a)[2][4], const bf16x8 (&b)[4]) {
+  asm volatile("" : "+v"(c0), "+v"(c1));
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][ks], b[ks], c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][ks], b[ks], c1, 0, 0, 0);
+  }
+  asm volatile("" : "+v"(c0), "+v"(c1));
+}
+
+__global__ __launch_bounds__(NT, 1) void gemm8_kernel(GemmArgs a) {
+  constexpr int TM = 4, TN = 2;  // acc[2 * a_half + tile][b_half]
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, l32 = lane & 31;
+  const int n_ct = a.Mp / 256;
+  const int total = (a.rows_p / BM) * n_ct;
+  int t = blockIdx.x;
+  if ((total & 7) == 0) t = (t & 7) * (total >> 3) + (t >> 3);  // XCD-contiguous tile ranges
+  const int row0 = (t / n_ct) * BM;
+  const int col0 = (t % n_ct) * 256;
+  const int wr = wave >> 2, wc = wave & 3;
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x16{};
+
+  const size_t lda_b = (size_t)a.lda * 2, ldw_b = (size_t)a.ldw * 2;
+  const unsigned char* Ab = static_cast<const unsigned char*>(a.A) + (size_t)row0 * lda_b;
+  const unsigned char* Bb = static_cast<const unsigned char*>(a.Wt) + (size_t)col0 * ldw_b;
+  const int KT = a.K / BK;
+  // slot s of buffer b: 0 A0, 1 A1, 2 B0, 3 B1
+#define SLOT(b, s) (smem + (b) * 4 * HALF_B + (s) * HALF_B)
+  stage_half<true>(Ab, lda_b, 0, SLOT(0, 0), 0, wave, lane);
+  stage_half<false>(Bb, ldw_b, 0, SLOT(0, 2), 0, wave, lane);
+  stage_half<false>(Bb, ldw_b, 0, SLOT(0, 3), 1, wave, lane);
+  stage_half<true>(Ab, lda_b, 0, SLOT(0, 1), 1, wave, lane);
+  if (KT > 1) {
+    stage_half<true>(Ab, lda_b, SLICE_B, SLOT(1, 0), 0, wave, lane);
+    stage_half<false>(Bb, ldw_b, SLICE_B, SLOT(1, 2), 0, wave, lane);
+    stage_half<false>(Bb, ldw_b, SLICE_B, SLOT(1, 3), 1, wave, lane);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  raw_barrier();
+  if (wr == 1) raw_barrier();  // group 1 runs one barrier behind group 0
+
+  const int ra = wr * 64 + l32, rb = wc * 32 + l32;  // slot rows of this lane's fragments
+  for (int kt = 0; kt < KT; ++kt) {
+    const int b = kt & 1;
+    const size_t k1 = (size_t)(kt + 1) * SLICE_B, k2 = (size_t)(kt + 2) * SLICE_B;
+    bf16x8 a0[2][4], a1[2][4], b0[4], b1[4];
+    // P1: A0 x B0
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) a0[i][ks] = frag(SLOT(b, 0), ra + 32 * i, 2 * ks + h);
+      b0[ks] = frag(SLOT(b, 2), rb, 2 * ks + h);
+    }
+    if (kt + 1 < KT) stage_half<true>(Ab, lda_b, k1, SLOT(b ^ 1, 1), 1, wave, lane);
+    mma_begin();
+    mma_quad(acc[0][0], acc[1][0], a0, b0);
+    mma_end();
+    // P2: A0 x B1
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) b1[ks] = frag(SLOT(b, 3), rb, 2 * ks + h);
+    if (kt + 2 < KT) stage_half<true>(Ab, lda_b, k2, SLOT(b, 0), 0, wave, lane);
+    mma_begin();
+    mma_quad(acc[0][1], acc[1][1], a0, b1);
+    mma_end();
+    // P3: A1 x B1
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) a1[i][ks] = frag(SLOT(b, 1), ra + 32 * i, 2 * ks + h);
+    if (kt + 2 < KT) stage_half<false>(Bb, ldw_b, k2, SLOT(b, 2), 0, wave, lane);
+    mma_begin();
+    mma_quad(acc[2][1], acc[3][1], a1, b1);
+    mma_end();
+    // P4: A1 x B0; slice kt + 1 retired (three half-tiles of kt + 2 may stay in flight)
+    if (kt + 2 < KT) stage_half<false>(Bb, ldw_b, k2, SLOT(b, 3), 1, wave, lane);
+    if (kt + 2 < KT) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if (kt + 1 < KT) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    mma_begin();
+    mma_quad(acc[2][0], acc[3][0], a1, b0);
+    mma_end();
+  }
+#undef SLOT
+  if (wr == 0) raw_barrier();  // balance group 1's extra barrier
+  switch (a.act) {
+    case A_IDENTITY: store_hidden<A_IDENTITY, TM, TN, false>(a, acc, row0, col0, wr, wc, lane); break;
+    case A_RELU: store_hidden<A_RELU, TM, TN, false>(a, acc, row0, col0, wr, wc, lane); break;
+    case A_LOGISTIC: store_hidden<A_LOGISTIC, TM, TN, false>(a, acc, row0, col0, wr, wc, lane); break;
+    case A_TANH: store_hidden<A_TANH, TM, TN, false>(a, acc, row0, col0, wr, wc, lane); break;
+    default: store_hidden<-1, TM, TN, false>(a, acc, row0, col0, wr, wc, lane); break;
+  }
+}
+
+int launch8(hipStream_t stream, const GemmArgs& a) {
+  const size_t lds = 8 * (size_t)HALF_B;
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm8_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)lds) != hipSuccess)
+    return -5;
+  hipLaunchKernelGGL(gemm8_kernel, dim3((a.rows_p / BM) * (a.Mp / 256)), dim3(NT), lds, stream, a);
+  return 0;
+}
+
 template <int BN, bool HEAD, bool F32>
 int launch(hipStream_t stream, const GemmArgs& a) {
   const size_t stage = 2 * (size_t)BM * SLICE_B + 2 * (size_t)BN * SLICE_B;
@@ -381,8 +553,11 @@ PMML_API int pmml_gemm_launch(hipStream_t stream, const GemmArgs* args, int head
   const GemmArgs a = *args;
   if (a.rows <= 0) return 0;
   const int BN = head ? 32 : 256;
-  if (a.f32 != 0 && a.f32 != 1) return -4;
-  const int f32 = a.f32;
+  if (a.f32 & ~0x81) return -4;
+  // bf16 hidden layers with K >= 512 run the phase-interleaved kernel (profiles/r3ao: 2048 x 2048
+  // 8.73 -> 8.36 ms, 1024 x 1024 2.62 -> 2.48 ms over 1M rows); below that the layer is bound by
+  // its output writes and the 2-buffer loop is faster (K = 64: 0.83 vs 0.92 ms). Bit 7 forces it.
+  const int f32 = a.f32 & 1, ph8 = !f32 && (((a.f32 >> 7) & 1) || a.K >= 512);
   const int sk = f32 ? SLICE_B / 4 : SLICE_B / 2;
   if (a.rows_p % BM || a.rows_p < a.rows || a.K % sk || a.K <= 0 || a.Mp % BN || a.Mp <= 0) return -4;
   if ((a.lda & 7) || (a.ldw & 7) || a.lda < a.K || a.ldw < a.K) return -4;
@@ -390,7 +565,8 @@ PMML_API int pmml_gemm_launch(hipStream_t stream, const GemmArgs* args, int head
   if (head && (a.n_out < 1 || a.n_out > 32 || a.Mp != 32 || !a.row_ok || !a.score || !a.valid)) return -4;
   if (!head && ((a.ldc & 7) || a.ldc < a.Mp || !a.C || (reinterpret_cast<uintptr_t>(a.C) & 15))) return -4;
   const int rc = f32 ? (head ? launch<32, true, true>(stream, a) : launch<256, false, true>(stream, a))
-                     : (head ? launch<32, true, false>(stream, a) : launch<256, false, false>(stream, a));
+                     : (head ? launch<32, true, false>(stream, a)
+                             : (ph8 ? launch8(stream, a) : launch<256, false, false>(stream, a)));
   if (rc) return rc;
   return hipGetLastError() == hipSuccess ? 0 : -7;
 }

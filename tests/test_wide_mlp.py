@@ -134,3 +134,28 @@ def test_wide_gemm_kernels_on_gpu(gpu, shape, precision):
         scale = max(1.0, float(np.abs(ref[v]).max()))
         assert np.abs(s[v] - es[v]).max() < (1e-4 if fp32 else 5e-3) * scale  # same operands: summation order
         assert np.abs(s[v] - ref[v]).max() < (1e-4 if fp32 else 3e-2) * scale
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [dict(n_features=100, hidden=(300,)), dict(n_features=150, hidden=(260, 300)),
+                                   dict(n_features=40, hidden=(1024, 512))],
+                         ids=["k128", "k192", "k1024"])
+def test_phase_interleaved_gemm_matches_two_buffer_loop(gpu, shape):
+    """The phase-interleaved bf16 hidden-layer kernel (gemm8_kernel: half-tile staging, counted
+    vmcnt across raw barriers, staggered wave groups) runs by default for K >= 512; forcing it on
+    every hidden layer (K = 128 / 192: 2 / 3 slices, the pipeline's edge cases) must give the same
+    bits as the 2-buffer loop — the same MFMAs in the same k order."""
+    c = CompiledPmml.from_string(mlp_pmml(seed=9, **shape))
+    plan = c.plan(gpu, precision="bf16", mlp_impl="wide")
+    X = stream_matrix(5000, shape["n_features"], seed=4, missing_rate=0.01)
+    s0, v0 = plan.score(X)
+    plan.gemm_flags = 0x80
+    try:
+        s1, v1 = plan.score(X)
+    finally:
+        plan.gemm_flags = 0
+    assert torch.equal(v0, v1) and torch.equal(s0[v0.bool()], s1[v1.bool()])
+    ref, vref = c.score_matrix_oracle(X)
+    s1, v1 = s1.cpu().numpy(), v1.cpu().numpy().astype(bool)
+    assert (v1 == vref).all()
+    assert np.abs(s1[v1] - ref[v1]).max() < 3e-2 * max(1.0, float(np.abs(ref[v1]).max()))
