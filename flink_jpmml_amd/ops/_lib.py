@@ -147,7 +147,7 @@ class GenTreeArgs(ctypes.Structure):
 
 
 class HybridArgs(ctypes.Structure):
-    _fields_ = [("t", TreeArgs), ("heads", c_void_p), ("head_words", c_int), ("pad", c_int)]
+    _fields_ = [("t", TreeArgs), ("heads", c_void_p), ("head_words", c_int), ("tail_format", c_int)]
 
 
 class ClusterArgs(ctypes.Structure):

@@ -9,7 +9,15 @@ namespace {
 // missing | bit 31 default right.
 // MASKED: finished walks skip their load (exec-masked) instead of re-loading node 0 — the vector
 // memory pipe then only processes the lanes still walking.
-template <bool GENERAL, bool FEAT_LDS, int PILP = 8, bool MASKED = false>
+// USKIP: a walk slot whose walks have ended in EVERY lane of the wave issues no load and no
+// compare (wave-uniform branch on a ballot): a lock-step group then costs the sum of its trees'
+// wave-level depths in gather instructions instead of PILP x the deepest one.
+// PEEL: the top two levels of every walk come from wave-uniform node loads (every lane of the
+// wave starts on the same root, and a root's two children are adjacent BFS nodes): scalar loads
+// through the constant cache plus a per-lane select, instead of two 64-lane vector gathers of
+// the same one or two nodes (the walk is bound by the vector memory pipe's per-instruction cost,
+// profiles/r3w).
+template <bool GENERAL, bool FEAT_LDS, int PILP = 8, bool MASKED = false, bool USKIP = false, bool PEEL = false>
 __global__ __launch_bounds__(TB, 2) void tree_pointer_kernel(TreeArgs a) {
   extern __shared__ __align__(16) uint32_t smem[];
   float* feat = reinterpret_cast<float*>(smem);
@@ -60,12 +68,56 @@ __global__ __launch_bounds__(TB, 2) void tree_pointer_kernel(TreeArgs a) {
       code[i] = i < nt ? a.roots[t0 + i] : -1;
       pz[i] = false;
     }
+    if (PEEL) {
+      // level 0: the root (uniform)
+      int rc[PILP];
+      uint4 n0[PILP];
+#pragma unroll
+      for (int i = 0; i < PILP; ++i) {
+        rc[i] = __builtin_amdgcn_readfirstlane(code[i]);
+        n0[i] = nodes[max(rc[i], 0)];
+      }
+      bool r0[PILP];
+#pragma unroll
+      for (int i = 0; i < PILP; ++i) {
+        const float x = *reinterpret_cast<const float*>(feat_lane + (n0[i].y & 0xFFFFu));
+        const bool isn = (x != x);
+        const bool nulled = rc[i] >= 0 && isn && ((n0[i].y >> 30) & 1u);
+        r0[i] = (x >= __uint_as_float(n0[i].x)) || (isn && (n0[i].y >> 31));
+        pz[i] = nulled;
+        code[i] = rc[i] < 0 ? rc[i] : (nulled ? -1 : (r0[i] ? (int)n0[i].w : (int)n0[i].z));
+      }
+      // level 1: both children of the root (uniform), selected per lane
+      uint4 nl[PILP], nr[PILP];
+#pragma unroll
+      for (int i = 0; i < PILP; ++i) {
+        nl[i] = nodes[max(__builtin_amdgcn_readfirstlane((int)n0[i].z), 0)];
+        nr[i] = nodes[max(__builtin_amdgcn_readfirstlane((int)n0[i].w), 0)];
+      }
+#pragma unroll
+      for (int i = 0; i < PILP; ++i) {
+        const uint4 nd = r0[i] ? nr[i] : nl[i];
+        const bool act = code[i] >= 0;
+        const float x = *reinterpret_cast<const float*>(feat_lane + (nd.y & 0xFFFFu));
+        const bool isn = (x != x);
+        const bool nulled = act && isn && ((nd.y >> 30) & 1u);
+        const bool right = (x >= __uint_as_float(nd.x)) || (isn && (nd.y >> 31));
+        pz[i] = pz[i] || nulled;
+        code[i] = act ? (nulled ? -1 : (right ? (int)nd.w : (int)nd.z)) : code[i];
+      }
+    }
     bool live = true;
     while (live) {
       uint4 nd[PILP];
+      bool any[PILP];
+#pragma unroll
+      for (int i = 0; i < PILP; ++i) any[i] = !USKIP || __builtin_amdgcn_ballot_w64(code[i] >= 0) != 0ull;
 #pragma unroll
       for (int i = 0; i < PILP; ++i) {
-        if (MASKED) {
+        if (USKIP) {
+          nd[i] = make_uint4(0u, 0u, 0u, 0u);
+          if (any[i]) nd[i] = nodes[max(code[i], 0)];
+        } else if (MASKED) {
           nd[i] = make_uint4(0u, 0u, 0u, 0u);
           if (code[i] >= 0) nd[i] = nodes[code[i]];
         } else {
@@ -75,6 +127,7 @@ __global__ __launch_bounds__(TB, 2) void tree_pointer_kernel(TreeArgs a) {
       live = false;
 #pragma unroll
       for (int i = 0; i < PILP; ++i) {  // branch-free: finished walks compute on node 0 and keep their leaf
+        if (USKIP && !any[i]) continue;
         const bool act = code[i] >= 0;
         float x;
         if (FEAT_LDS) {
@@ -651,7 +704,8 @@ PMML_API int pmml_tree_launch(hipStream_t stream, const TreeArgs* args, int layo
     }
   } else {
     if (a.variant != 0 && a.variant != VAR_POINTER_REFILL && a.variant != VAR_POINTER_COMPACT &&
-        a.variant != VAR_POINTER_MASKED && a.variant != VAR_POINTER_SUPER)
+        a.variant != VAR_POINTER_MASKED && a.variant != VAR_POINTER_SUPER && a.variant != VAR_POINTER_USKIP &&
+        a.variant != VAR_POINTER_PEEL)
       return -10;
     const bool feat_lds = a.n_feat <= 64;
     size_t lds = (feat_lds ? (size_t)a.n_feat * TB * 4 : 0) + TB * 4 + acc_lds;
@@ -701,6 +755,30 @@ PMML_API int pmml_tree_launch(hipStream_t stream, const TreeArgs* args, int layo
           if (!err) hipLaunchKernelGGL((tree_pointer_refill_kernel<false, false>), grid, dim3(TB), lds, stream, a);
         }
       }
+    } else if (a.variant == VAR_POINTER_PEEL && feat_lds) {
+      if (a.general) {
+        err = prepare_launch(tree_pointer_kernel<true, true, 8, false, false, true>, lds);
+        if (!err) hipLaunchKernelGGL((tree_pointer_kernel<true, true, 8, false, false, true>), grid, dim3(TB), lds, stream, a);
+      } else {
+        err = prepare_launch(tree_pointer_kernel<false, true, 8, false, false, true>, lds);
+        if (!err) hipLaunchKernelGGL((tree_pointer_kernel<false, true, 8, false, false, true>), grid, dim3(TB), lds, stream, a);
+      }
+    } else if (a.variant == VAR_POINTER_USKIP && feat_lds) {
+      if (a.general) {
+        err = prepare_launch(tree_pointer_kernel<true, true, 8, false, true>, lds);
+        if (!err) hipLaunchKernelGGL((tree_pointer_kernel<true, true, 8, false, true>), grid, dim3(TB), lds, stream, a);
+      } else if (a.pilp == 4) {
+        err = prepare_launch(tree_pointer_kernel<false, true, 4, false, true>, lds);
+        if (!err) hipLaunchKernelGGL((tree_pointer_kernel<false, true, 4, false, true>), grid, dim3(TB), lds, stream, a);
+      } else if (a.pilp == 16) {
+        err = prepare_launch(tree_pointer_kernel<false, true, 16, false, true>, lds);
+        if (!err) hipLaunchKernelGGL((tree_pointer_kernel<false, true, 16, false, true>), grid, dim3(TB), lds, stream, a);
+      } else {
+        err = prepare_launch(tree_pointer_kernel<false, true, 8, false, true>, lds);
+        if (!err) hipLaunchKernelGGL((tree_pointer_kernel<false, true, 8, false, true>), grid, dim3(TB), lds, stream, a);
+      }
+    } else if (a.variant == VAR_POINTER_USKIP || a.variant == VAR_POINTER_PEEL) {
+      return -4;  // features in LDS only
     } else if (a.general) {
       if (feat_lds && (a.variant & VAR_POINTER_MASKED)) {
         err = prepare_launch(tree_pointer_kernel<true, true, 8, true>, lds);

@@ -77,6 +77,8 @@ constexpr int VAR_POINTER_REFILL = 16;  // pointer layout: refill schedule (tree
 constexpr int VAR_POINTER_COMPACT = 32; // pointer layout: 8-byte BFS slots (tree.hip::tree_compact_kernel)
 constexpr int VAR_POINTER_MASKED = 64;  // pointer layout, lock-step sums: exec-masked loads of finished walks
 constexpr int VAR_POINTER_SUPER = 128;  // pointer layout: two levels per 16-byte slot (tree.hip::tree_super_kernel)
+constexpr int VAR_POINTER_USKIP = 256;  // pointer layout, lock-step: wave-uniform skip of finished walk slots
+constexpr int VAR_POINTER_PEEL = 512;   // pointer layout, lock-step: top two levels from uniform (scalar) loads
 
 // per-depth launchers (tree_d<D>.hip)
 #define PMML_TREE_DECL(D) int launch_perfect_d##D(hipStream_t st, const TreeArgs& a, dim3 grid, size_t lds);

@@ -33,7 +33,8 @@ namespace {
 struct HybridArgs {
   TreeArgs t;               // blob = tail nodes (uint4), leaves, rows, epilogue, outputs
   const uint32_t* heads;    // [n_trees][head_words]: (2^H - 1) uint2 nodes, then 2^H int exit codes
-  int head_words, pad;
+  int head_words;
+  int tail_format;          // 0: COMPACT depth-first uint2 tail, 1: 16-byte BFS POINTER tail, 2: same + USKIP
 };
 
 template <bool FEAT_LDS>
@@ -187,6 +188,150 @@ __global__ __launch_bounds__(TB, 2) void tree_hybrid_kernel(HybridArgs ha) {
   finish_row(a, acc, accl, blk.y, GENERAL, row, row_ok && !poisoned);
 }
 
+// HYBRID head + 16-byte POINTER tail (runtime/hybrid.py::pack_trees with H > 0): the head is the
+// kernel above; the exits are pointer codes (tail node index, or ~leaf) and the tail walk is the
+// lock-step BFS pointer walk (uint4 {T, meta, left code, right code}, siblings adjacent — the node
+// format the lanes of a wave share cache lines best in, profiles/r3w). The top H levels, where
+// every lane of the wave reads one of a handful of nodes, come from LDS (broadcast reads) instead
+// of costing one vector-memory gather per level each; a walk slot that has ended in every lane of
+// the wave issues no tail load (USKIP: wave-uniform ballot branch; otherwise finished walks re-load
+// node 0 like the pointer kernel). Leaves are read after the tail loop.
+template <bool GENERAL, bool FEAT_LDS, int H, bool USKIP>
+__global__ __launch_bounds__(TB, 2) void tree_hybrid_ptr_kernel(HybridArgs ha) {
+  const TreeArgs& a = ha.t;
+  constexpr int NI = (1 << H) - 1;
+  extern __shared__ __align__(16) uint32_t smem[];
+  float* feat = reinterpret_cast<float*>(smem);
+  int* bad = reinterpret_cast<int*>(smem + (FEAT_LDS ? a.n_feat * TB : 0));
+  float* accl = reinterpret_cast<float*>(bad + TB);
+  uint32_t* hbuf = reinterpret_cast<uint32_t*>(accl + (GENERAL ? a.C * TB : 0));
+  const int tid = threadIdx.x;
+  const int2 blk = tree_block(a);
+  const int row0 = blk.x * TB;
+  const int row = row0 + tid;
+  if (FEAT_LDS) {
+    stage_rows_T<TB>(a.X, a.n_rows, a.n_feat, a.ldx, a.prep, feat, bad, row0);
+  } else {
+    bad[tid] = 0;
+    __syncthreads();
+  }
+  bool row_ok = bad[tid] == 0;
+  const float* xrow = a.X + (size_t)min(row, a.n_rows - 1) * a.ldx;
+  if (!FEAT_LDS && a.prep && row < a.n_rows) {
+    for (int f = 0; f < a.n_feat; ++f) {
+      bool b = false;
+      (void)prep_value(xrow[f], a.prep[f], &b);
+      if (b) row_ok = false;
+    }
+  }
+  if (a.row_valid_in && row < a.n_rows) row_ok = row_ok && a.row_valid_in[row];
+  if (GENERAL) {
+    for (int c = 0; c < a.C; ++c) accl[c * TB + tid] = 0.f;
+  }
+  const uint4* nodes = reinterpret_cast<const uint4*>(a.blob);
+  const int tb = blk.y * a.trees_per_split;
+  const int te = min(a.n_trees, tb + a.trees_per_split);
+  const int rw = ha.head_words;
+  const int CT = a.chunk_trees;
+  const char* feat_lane = reinterpret_cast<const char*>(feat + tid);
+  float acc = 0.f;
+  bool poisoned = false;
+  constexpr int PILP = 8;
+  for (int c0 = tb; c0 < te; c0 += CT) {
+    const int nt = min(CT, te - c0);
+    __syncthreads();
+    {
+      const uint4* src = reinterpret_cast<const uint4*>(ha.heads + (size_t)c0 * rw);
+      uint4* dst = reinterpret_cast<uint4*>(hbuf);
+      const int n16 = (nt * rw) >> 2;
+      for (int i = tid; i < n16; i += TB) dst[i] = src[i];
+    }
+    __syncthreads();
+    for (int k = 0; k < nt; k += PILP) {
+      const int m = min(PILP, nt - k);
+      uint32_t j[PILP];
+      bool pz[PILP];
+      const uint32_t* rec[PILP];
+#pragma unroll
+      for (int i = 0; i < PILP; ++i) {
+        j[i] = 0u;
+        pz[i] = false;
+        rec[i] = hbuf + (size_t)(k + min(i, m - 1)) * rw;
+      }
+#pragma unroll
+      for (int d = 0; d < H; ++d) {
+#pragma unroll
+        for (int i = 0; i < PILP; ++i) {
+          const uint2 nd = reinterpret_cast<const uint2*>(rec[i])[j[i]];
+          const float x = hy_feature<FEAT_LDS>(a, feat_lane, xrow, nd.y);
+          const bool isn = x != x;
+          pz[i] = pz[i] || (isn && ((nd.y >> 30) & 1u));
+          const uint32_t right = ((x >= __uint_as_float(nd.x)) || (isn && (nd.y >> 31))) ? 1u : 0u;
+          j[i] = 2u * j[i] + 1u + right;
+        }
+      }
+      int code[PILP];
+      bool live = false;
+#pragma unroll
+      for (int i = 0; i < PILP; ++i) {
+        const int e = reinterpret_cast<const int*>(rec[i] + 2 * NI)[j[i] - NI];
+        code[i] = (pz[i] || i >= m) ? -1 : e;  // a poisoned / surplus walk carries no leaf
+        live = live || code[i] >= 0;
+      }
+      while (live) {
+        uint4 nd[PILP];
+        bool any[PILP];
+#pragma unroll
+        for (int i = 0; i < PILP; ++i) any[i] = !USKIP || __builtin_amdgcn_ballot_w64(code[i] >= 0) != 0ull;
+#pragma unroll
+        for (int i = 0; i < PILP; ++i) {
+          if (USKIP) {
+            nd[i] = make_uint4(0u, 0u, 0u, 0u);
+            if (any[i]) nd[i] = nodes[max(code[i], 0)];
+          } else {
+            nd[i] = nodes[max(code[i], 0)];
+          }
+        }
+        live = false;
+#pragma unroll
+        for (int i = 0; i < PILP; ++i) {
+          if (USKIP && !any[i]) continue;
+          const bool act = code[i] >= 0;
+          float x;
+          if (FEAT_LDS) {
+            x = *reinterpret_cast<const float*>(feat_lane + (nd[i].y & 0xFFFFu));
+          } else {
+            x = hy_feature<false>(a, feat_lane, xrow, nd[i].y & 0xFFFFu);
+          }
+          const bool isn = x != x;
+          const bool nulled = act && isn && ((nd[i].y >> 30) & 1u);
+          const bool right = (x >= __uint_as_float(nd[i].x)) || (isn && (nd[i].y >> 31));
+          const int nc = right ? (int)nd[i].w : (int)nd[i].z;
+          pz[i] = pz[i] || nulled;
+          code[i] = act ? (nulled ? -1 : nc) : code[i];
+          live = live || code[i] >= 0;
+        }
+      }
+      for (int i = 0; i < PILP; ++i) {
+        if (i >= m) break;
+        if (pz[i]) {
+          if (GENERAL) poisoned = true;
+          else acc += __builtin_nanf("");
+          continue;
+        }
+        const int leaf = ~code[i];
+        if (GENERAL) {
+          const int slot = a.tree_slot[c0 + k + i];
+          for (int p = 0; p < a.P; ++p) accl[(slot + p) * TB + tid] += a.leaves[(size_t)leaf * a.P + p];
+        } else {
+          acc += a.leaves[leaf];
+        }
+      }
+    }
+  }
+  finish_row(a, acc, accl, blk.y, GENERAL, row, row_ok && !poisoned);
+}
+
 // Split-mode reduction (same partial layout as the pointer kernel).
 __global__ __launch_bounds__(TB) void tree_hybrid_reduce_kernel(TreeArgs a, int splits) {
   const int row = blockIdx.x * TB + threadIdx.x;
@@ -206,6 +351,18 @@ __global__ __launch_bounds__(TB) void tree_hybrid_reduce_kernel(TreeArgs a, int 
 
 template <bool GENERAL, bool FEAT_LDS, int H>
 int launch_hybrid_t(hipStream_t stream, const HybridArgs& ha, dim3 grid, size_t lds) {
+  if (ha.tail_format == 1) {  // 16-byte pointer tail, clamped loads
+    int err = prepare_launch(tree_hybrid_ptr_kernel<GENERAL, FEAT_LDS, H, false>, lds);
+    if (err) return err;
+    hipLaunchKernelGGL((tree_hybrid_ptr_kernel<GENERAL, FEAT_LDS, H, false>), grid, dim3(TB), lds, stream, ha);
+    return 0;
+  }
+  if (ha.tail_format == 2) {  // 16-byte pointer tail, wave-uniform skip of finished slots
+    int err = prepare_launch(tree_hybrid_ptr_kernel<GENERAL, FEAT_LDS, H, true>, lds);
+    if (err) return err;
+    hipLaunchKernelGGL((tree_hybrid_ptr_kernel<GENERAL, FEAT_LDS, H, true>), grid, dim3(TB), lds, stream, ha);
+    return 0;
+  }
   int err = prepare_launch(tree_hybrid_kernel<GENERAL, FEAT_LDS, H>, lds);
   if (err) return err;
   hipLaunchKernelGGL((tree_hybrid_kernel<GENERAL, FEAT_LDS, H>), grid, dim3(TB), lds, stream, ha);
@@ -229,7 +386,7 @@ using namespace pmml_tree;
 
 PMML_API int pmml_tree_hybrid_args_size() { return (int)sizeof(HybridArgs); }
 
-// head_depth in {4, 6, 8, 10}; splits >= 1 (grid.y tree groups, > 1 needs t.partial).
+// head_depth in {2, 3, 4, 6, 8, 10} (2 and 3: pointer tail only); splits >= 1 (grid.y tree groups, > 1 needs t.partial).
 PMML_API int pmml_tree_hybrid_launch(hipStream_t stream, const HybridArgs* args, int head_depth, int splits) {
   HybridArgs ha = *args;
   TreeArgs& a = ha.t;
@@ -253,8 +410,12 @@ PMML_API int pmml_tree_hybrid_launch(hipStream_t stream, const HybridArgs* args,
   if (a.xcd_split > 0) a.xcd_split = splits;
   if (a.xcd_split > 0 && (long long)row_blocks * splits > 0x7FFFFFFFLL) return -11;
   dim3 grid = a.xcd_split > 0 ? dim3(row_blocks * splits) : dim3(row_blocks, splits);
+  if (ha.tail_format < 0 || ha.tail_format > 2) return -4;
+  if (head_depth < 4 && ha.tail_format == 0) return -6;
   int err;
   switch (head_depth) {
+    case 2: err = launch_hybrid_h<2>(stream, ha, grid, lds, a.general != 0, feat_lds); break;
+    case 3: err = launch_hybrid_h<3>(stream, ha, grid, lds, a.general != 0, feat_lds); break;
     case 4: err = launch_hybrid_h<4>(stream, ha, grid, lds, a.general != 0, feat_lds); break;
     case 6: err = launch_hybrid_h<6>(stream, ha, grid, lds, a.general != 0, feat_lds); break;
     case 8: err = launch_hybrid_h<8>(stream, ha, grid, lds, a.general != 0, feat_lds); break;

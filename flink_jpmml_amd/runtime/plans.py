@@ -1069,6 +1069,8 @@ def _perfect_pack_vec(trees, weights, P: int, D: int, stride: int, fmap, leaf_bi
 
 VAR_NAN_FAST, VAR_NAN_PLANES, VAR_POINTER_REFILL, VAR_POINTER_COMPACT, VAR_POINTER_MASKED = 4, 8, 16, 32, 64  # tree_common.h
 VAR_POINTER_SUPER = 128
+VAR_POINTER_USKIP = 256
+VAR_POINTER_PEEL = 512
 DYN_B, DYN_SLOTS = 8, 16  # csrc: MODE_SUM trees per claimed batch, batch slots per chunk
 
 
@@ -1210,7 +1212,8 @@ class TreePlan(DevicePlan):
                                   "blob", "leaves", "roots", "has_dr", "table", "slots", "splits", "epi_args",
                                   "variant", "children", "preds", "pool", "trees_tab", "max_steps", "blob_nan",
                                   "chunk_trees_nan", "full_epi", "labels", "mode", "tree_w", "acc_init", "feat_map",
-                                  "rows_wide", "n_stage", "heads", "head_depth", "pointer_ilp", "xcd_split")
+                                  "rows_wide", "n_stage", "heads", "head_depth", "pointer_ilp", "xcd_split",
+                                  "tail_format")
 
     WIDE_G = 4  # tree groups of the wide kernel (mirrors csrc)
 
@@ -1218,9 +1221,17 @@ class TreePlan(DevicePlan):
                  variant: str = "auto", precision: str = "fp32", nan_mode: str = "auto", max_chunk_trees: int = 0,
                  tree_shard: Optional[Tuple[int, int]] = None, head_depth: int = 0,
                  pointer_schedule: str = "lockstep", node_order: str = "bfs", node_format: str = "wide",
-                 pointer_ilp: int = 8, xcd_split: str = "off", pointer_load: str = "clamped"):
+                 pointer_ilp: int = 8, xcd_split: str = "off", pointer_load: str = "clamped",
+                 hybrid_tail: str = "compact"):
         """``pointer_load`` (pointer lock-step kernel, features in LDS): ``"clamped"`` (finished walks
-        re-load node 0, no branch) or ``"masked"`` (their loads are exec-masked off).
+        re-load node 0, no branch), ``"masked"`` (their loads are exec-masked off) or ``"uskip"``
+        (a walk slot finished in every lane of the wave issues no load at all: wave-uniform branch)
+        or ``"peel"`` (the top two levels from wave-uniform scalar loads + a per-lane select).
+
+        ``hybrid_tail`` (hybrid layout): ``"compact"`` (depth-first uint2 tail,
+        :func:`~flink_jpmml_amd.runtime.hybrid.pack_hybrid_compact`) or ``"wide"`` (the 16-byte BFS
+        pointer tail of :func:`~flink_jpmml_amd.runtime.hybrid.pack_trees`, clamped loads, or
+        the wave-uniform skip with ``pointer_load="uskip"``; head depths 2-10).
 
         ``xcd_split`` (pointer / hybrid layouts): ``"on"`` splits the forest into 8 tree slices
         scored by workgroups placed on the 8 XCDs (csrc ``tree_block``), so each XCD's 4 MiB L2
@@ -1258,8 +1269,11 @@ class TreePlan(DevicePlan):
         if pointer_schedule not in ("refill", "lockstep"):
             raise ValueError("pointer_schedule must be 'refill' or 'lockstep'")
         self.heads, self.head_depth = None, 0  # hybrid layout only
-        if pointer_load not in ("clamped", "masked"):
-            raise ValueError("pointer_load must be 'clamped' or 'masked'")
+        if pointer_load not in ("clamped", "masked", "uskip", "peel"):
+            raise ValueError("pointer_load must be 'clamped', 'masked', 'uskip' or 'peel'")
+        if hybrid_tail not in ("compact", "wide"):
+            raise ValueError("hybrid_tail must be 'compact' or 'wide'")
+        self.tail_format = 0
         if xcd_split not in ("on", "off"):
             raise ValueError("xcd_split must be 'on' or 'off'")
         self.xcd_split = 0
@@ -1444,8 +1458,8 @@ class TreePlan(DevicePlan):
                 # (tree_hybrid.hip); H = 4 measured best at depth 14 (profiles/r3c: larger heads
                 # pay more for the per-workgroup head copy and LDS bank conflicts than they save)
                 H = head_depth or 4
-                if H not in (4, 6, 8, 10):
-                    raise ValueError("head_depth must be 4, 6, 8 or 10")
+                if H not in ((2, 3, 4, 6, 8, 10) if hybrid_tail == "wide" else (4, 6, 8, 10)):
+                    raise ValueError("head_depth must be 4, 6, 8 or 10 (2 and 3 with the wide tail)")
                 fixed = (F * TB * 4 if feat_lds else 0) + TB * 4 + (self.C * TB * 4 if self.general else 0)
                 fit = (lds_budget - fixed) // (head_words(H) * 4)
                 if fit < 1:
@@ -1453,13 +1467,17 @@ class TreePlan(DevicePlan):
                 # small chunks: the head buffer must not cost occupancy (the tail walk hides L2 latency
                 # with waves; profiles/r3e: 234-tree chunks -> 2 workgroups per CU, 1.5x slower)
                 self.chunk_trees = int(min(fit, self.n_trees, max_chunk_trees or 32))
-                try:
-                    heads, nodes, leaves, has_dr = pack_hybrid_compact(spec.trees, spec.weights, spec.P, H, F)
-                    roots = np.zeros(self.n_trees, dtype=np.int32)
-                    if leaves is None:
-                        leaves = np.zeros((1, 1), np.float32)
-                except ValueError:
-                    self.layout, H, heads, self.chunk_trees = "pointer", 0, None, 0
+                if hybrid_tail == "wide":
+                    heads, nodes, leaves, roots, has_dr = pack_trees(spec.trees, spec.weights, spec.P, H, feat_lds)
+                    self.tail_format = 2 if pointer_load == "uskip" else 1
+                else:
+                    try:
+                        heads, nodes, leaves, has_dr = pack_hybrid_compact(spec.trees, spec.weights, spec.P, H, F)
+                        roots = np.zeros(self.n_trees, dtype=np.int32)
+                        if leaves is None:
+                            leaves = np.zeros((1, 1), np.float32)
+                    except ValueError:
+                        self.layout, H, heads, self.chunk_trees = "pointer", 0, None, 0
             else:
                 self.chunk_trees = 0
             compact = superl = False
@@ -1501,6 +1519,10 @@ class TreePlan(DevicePlan):
                 self.variant = VAR_POINTER_COMPACT
             elif pointer_load == "masked" and self.layout == "pointer" and self.variant == 0 and feat_lds:
                 self.variant = VAR_POINTER_MASKED  # finished walks skip their node load (exec mask)
+            elif pointer_load == "peel" and self.layout == "pointer" and self.variant == 0 and feat_lds:
+                self.variant = VAR_POINTER_PEEL  # top two levels from wave-uniform scalar loads
+            elif pointer_load == "uskip" and self.layout == "pointer" and self.variant == 0 and feat_lds:
+                self.variant = VAR_POINTER_USKIP  # slots finished in the whole wave issue no load
             self.blob = self._t(nodes.reshape(-1).view(np.int32))
             self.leaves = self._t(leaves.reshape(-1))
             self.roots = self._t(roots)
@@ -1663,6 +1685,7 @@ class TreePlan(DevicePlan):
             h = HybridArgs()
             h.t = a
             h.heads, h.head_words = ptr(self.heads), int(self.rec_words)
+            h.tail_format = int(getattr(self, "tail_format", 0))
             rc = self.lib.pmml_tree_hybrid_launch(stream_handle(stream), ctypes.byref(h), int(self.head_depth), s)
             check(rc, f"tree kernel (hybrid, head {self.head_depth}, depth {self.depth})")
             return

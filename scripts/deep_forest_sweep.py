@@ -31,6 +31,16 @@ CONFIGS = {
     "hybrid4": dict(layout="hybrid", head_depth=4, xcd_split="off"),
     "hybrid4+xcd": dict(layout="hybrid", head_depth=4, xcd_split="on"),
     "hybrid6+xcd": dict(layout="hybrid", head_depth=6, xcd_split="on"),
+    "pointer+uskip": dict(layout="pointer", pointer_load="uskip"),
+    "pointer4+uskip": dict(layout="pointer", pointer_load="uskip", pointer_ilp=4),
+    "pointer16+uskip": dict(layout="pointer", pointer_load="uskip", pointer_ilp=16),
+    "hybw2": dict(layout="hybrid", head_depth=2, hybrid_tail="wide"),
+    "hybw3": dict(layout="hybrid", head_depth=3, hybrid_tail="wide"),
+    "hybw4": dict(layout="hybrid", head_depth=4, hybrid_tail="wide"),
+    "hybw6": dict(layout="hybrid", head_depth=6, hybrid_tail="wide"),
+    "hybw3u": dict(layout="hybrid", head_depth=3, hybrid_tail="wide", pointer_load="uskip"),
+    "hybw4u": dict(layout="hybrid", head_depth=4, hybrid_tail="wide", pointer_load="uskip"),
+    "pointer+peel": dict(layout="pointer", pointer_load="peel"),
     "auto": dict(),
 }
 

@@ -1,0 +1,11 @@
+set -o pipefail
+# uniform-skip pointer walk + LDS-head/pointer-tail hybrid: GPU tests, then the deep-forest sweep.
+mkdir -p gpurun_out/r3aq
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+timeout -k 10 300 python -u -m pytest tests/test_gpu_hybrid.py -x -v --timeout 120 --timeout-method thread -k "uniform_skip" > gpurun_out/r3aq/pytest.log 2>&1 || { tail -40 gpurun_out/r3aq/pytest.log; exit 1; }
+tail -2 gpurun_out/r3aq/pytest.log
+CFG=pointer,pointer+uskip,pointer4+uskip,pointer16+uskip,hybw2,hybw3,hybw4,hybw6,hybrid4
+for m in gbdt rf; do
+  timeout -k 10 400 python -u scripts/deep_forest_sweep.py --model $m --configs $CFG >> gpurun_out/r3aq/sweep.jsonl 2>> gpurun_out/r3aq/sweep.err || { tail -20 gpurun_out/r3aq/sweep.err; exit 1; }
+done
+grep config gpurun_out/r3aq/sweep.jsonl | python -c "import sys,json; [print(d['model'],d['config'],round(d['ms'],3),d['valid_match'],d['max_abs_err']) for d in map(json.loads,sys.stdin)]"

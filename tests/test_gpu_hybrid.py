@@ -125,3 +125,44 @@ def test_super_layout_votes_on_gpu(gpu):
     ref, vref = c.score_matrix_oracle(X)
     assert (v == vref).all()
     np.testing.assert_array_equal(s[v], ref[v])
+
+
+@pytest.mark.parametrize("opts", [dict(layout="pointer", pointer_load="uskip"),
+                                  dict(layout="pointer", pointer_load="peel"),
+                                  dict(layout="pointer", pointer_load="uskip", pointer_ilp=4),
+                                  dict(layout="hybrid", hybrid_tail="wide", head_depth=2),
+                                  dict(layout="hybrid", hybrid_tail="wide", head_depth=4, pointer_load="uskip"),
+                                  dict(layout="hybrid", hybrid_tail="wide", head_depth=4),
+                                  dict(layout="hybrid", hybrid_tail="wide", head_depth=6)])
+@pytest.mark.parametrize("missing", ["defaultChild", "nullPrediction"])
+def test_uniform_skip_walks_on_gpu(gpu, opts, missing):
+    """Wave-uniform skip of finished walk slots (pointer walk and the LDS-head + 16-byte pointer
+    tail hybrid): against the fp64 oracle, and bit-identical to the clamped pointer walk (same
+    tree-order leaf sums)."""
+    txt = gbdt_pmml(n_trees=45, depth=14, n_features=24, seed=7, p_split=0.8, missing_strategy=missing)
+    c = CompiledPmml.from_string(txt)
+    plan = c.plan(gpu, **opts)
+    ptr = c.plan(gpu, layout="pointer")
+    assert plan.layout == opts["layout"]
+    X = stream_matrix(100_000, 24, seed=3, missing_rate=0.03)
+    s, v = _score(c, plan, X)
+    s0, v0 = _score(c, ptr, X)
+    ref, vref = c.score_matrix_oracle(X)
+    assert (v == vref).all()
+    np.testing.assert_allclose(s[v], ref[v], rtol=0, atol=5e-5)
+    assert (v == v0).all() and np.array_equal(s[v], s0[v0])
+
+
+@pytest.mark.parametrize("opts", [dict(layout="pointer", pointer_load="uskip"),
+                                  dict(layout="pointer", pointer_load="peel"),
+                                  dict(layout="hybrid", hybrid_tail="wide", head_depth=3)])
+def test_uniform_skip_votes_on_gpu(gpu, opts):
+    """Random-forest votes (P = 3 class slots in LDS) on the uniform-skip walks."""
+    txt = random_forest_pmml(n_trees=30, depth=16, n_features=16, n_classes=3, seed=5, p_split=0.8)
+    c = CompiledPmml.from_string(txt.encode())
+    plan = c.plan(gpu, **opts)
+    X = stream_matrix(50_000, 16, seed=8, missing_rate=0.02)
+    s, v = _score(c, plan, X)
+    ref, vref = c.score_matrix_oracle(X)
+    assert (v == vref).all()
+    np.testing.assert_array_equal(s[v], ref[v])

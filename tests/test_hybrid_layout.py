@@ -30,7 +30,8 @@ def emulate(plan, X):
     H = plan.head_depth
     if plan.variant == 32:
         return emulate_compact(plan, Xf)
-    tail = plan.blob.numpy().view(np.uint32).reshape(-1, 2 if H else 4)
+    compact_tail = bool(H) and getattr(plan, "tail_format", 0) == 0
+    tail = plan.blob.numpy().view(np.uint32).reshape(-1, 2 if compact_tail else 4)
     leaves = plan.leaves.numpy().reshape(-1, plan.P)[:, 0]
     NI = (1 << H) - 1
     acc = np.zeros(n)
@@ -51,7 +52,7 @@ def emulate(plan, X):
             code = rec[2 * NI + (j - NI)].view(np.int32).astype(np.int64)
         else:
             code = np.full(n, plan.roots.numpy()[t], np.int64)
-        if H:  # COMPACT depth-first tail: left child adjacent, right at +rel, stop at the leaf's parent
+        if compact_tail:  # COMPACT depth-first tail: left child adjacent, right at +rel, stop at the leaf's parent
             done = pz | (code < 0)
             code = np.where(code < 0, ~code, code)
             while (~done).any():
@@ -249,3 +250,31 @@ def test_super_layout_votes_and_limits():
 
     with pytest.raises(NotLowerable):  # 5-bit feature fields
         _plan(gbdt_pmml(n_trees=3, depth=6, n_features=40, seed=1), layout="pointer", node_format="super")
+
+
+@pytest.mark.parametrize("H", [2, 3, 4, 6])
+@pytest.mark.parametrize("missing", ["defaultChild", "nullPrediction"])
+def test_hybrid_wide_tail_emulation_matches_oracle(H, missing):
+    """LDS head + 16-byte BFS pointer tail (``tree_hybrid_ptr_kernel``): head exits are pointer
+    codes (tail node index or ~leaf) into :func:`pack_trees`' tail."""
+    txt = gbdt_pmml(n_trees=12, depth=12, n_features=20, seed=3, p_split=0.8, missing_strategy=missing)
+    c, plan = _plan(txt, layout="hybrid", hybrid_tail="wide", head_depth=H)
+    assert plan.layout == "hybrid" and plan.tail_format == 1 and plan.head_depth == H
+    with lowering_dry_run():
+        assert TreePlan(c, torch.device("cpu"), layout="hybrid", hybrid_tail="wide", head_depth=H,
+                        pointer_load="uskip").tail_format == 2
+    X = stream_matrix(3000, 20, seed=2, missing_rate=0.05)
+    ref, vref = c.score_matrix_oracle(X)
+    got = plan.epi_args.get("a", 1.0) * emulate(plan, X) + plan.epi_args.get("b", 0.0)
+    assert (np.isfinite(got) == vref).all()
+    np.testing.assert_allclose(got[vref], ref[vref], rtol=0, atol=2e-5)
+
+
+def test_hybrid_wide_tail_rejects_bad_head_depth():
+    txt = gbdt_pmml(n_trees=4, depth=8, n_features=8, seed=1)
+    with pytest.raises(ValueError):
+        _plan(txt, layout="hybrid", hybrid_tail="compact", head_depth=3)
+    with pytest.raises(ValueError):
+        _plan(txt, layout="hybrid", hybrid_tail="wide", head_depth=5)
+    with pytest.raises(ValueError):
+        _plan(txt, layout="pointer", pointer_load="bogus")
