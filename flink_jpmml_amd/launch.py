@@ -117,19 +117,18 @@ class Supervisor:
     def _run_attempt(self, attempt: Attempt) -> None:
         t0 = time.monotonic()
         procs = self._spawn(attempt)
-        failed = False
+        failed = True  # stays set if the supervisor itself is interrupted: the ranks are stopped
         try:
             while True:
                 codes = [p.poll() for p in procs]
                 bad = [c for c in codes if c not in (None, 0)]
                 if bad:
-                    failed = True
                     attempt.first_failure = bad[0]
                     break
                 if all(c == 0 for c in codes):
+                    failed = False
                     break
                 if self.attempt_timeout_s and time.monotonic() - t0 > self.attempt_timeout_s:
-                    failed = True
                     logger.error("attempt %d exceeded %.0f s", attempt.index, self.attempt_timeout_s)
                     break
                 time.sleep(0.05)
@@ -181,6 +180,11 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
     if not cmd:
         p.error("give the job command after --")
     logging.basicConfig(level=logging.INFO, format="[launch] %(message)s")
+
+    def _terminate(signum, frame):  # SIGTERM to the supervisor: stop the ranks' process groups too
+        raise SystemExit(128 + signum)
+
+    signal.signal(signal.SIGTERM, _terminate)
     sup = Supervisor(cmd, a.nproc, a.checkpoint_dir, a.max_restarts, a.restart_delay, a.grace,
                      attempt_timeout_s=a.attempt_timeout)
     return sup.run()

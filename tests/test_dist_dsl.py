@@ -400,3 +400,41 @@ def test_supervisor_gives_up_after_max_restarts(tmp_path):
     sup = Supervisor([sys.executable, "-c", "import sys; sys.exit(3)"], nproc=2, checkpoint_dir=str(tmp_path),
                      max_restarts=1, restart_delay_s=0.0, grace_s=0.5)
     assert sup.run() == 3 and len(sup.attempts) == 2
+
+
+def test_supervisor_sigterm_stops_its_ranks(tmp_path):
+    """SIGTERM to the launcher must not orphan the ranks (each runs in its own session)."""
+    import os
+    import signal
+    import subprocess
+    import sys
+    import time
+
+    pidfile = tmp_path / "pids"
+    child = (f"import os, time; open({str(pidfile)!r} + os.environ['RANK'], 'w').write(str(os.getpid())); "
+             "time.sleep(120)")
+    sup = subprocess.Popen([sys.executable, "-m", "flink_jpmml_amd.launch", "--nproc", "2", "--grace", "0.5", "--",
+                            sys.executable, "-c", child])
+    try:
+        deadline = time.monotonic() + 60
+        while time.monotonic() < deadline and not all((tmp_path / f"pids{r}").exists() and (tmp_path / f"pids{r}").stat().st_size
+                                                for r in range(2)):
+            time.sleep(0.05)
+        pids = [int((tmp_path / f"pids{r}").read_text()) for r in range(2)]
+        sup.send_signal(signal.SIGTERM)
+        assert sup.wait(timeout=30) != 0
+        deadline = time.monotonic() + 10
+        alive = pids
+        while time.monotonic() < deadline and alive:
+            alive = []
+            for p in pids:
+                try:
+                    os.kill(p, 0)
+                    alive.append(p)
+                except ProcessLookupError:
+                    pass
+            time.sleep(0.05)
+        assert not alive, f"ranks left running: {alive}"
+    finally:
+        if sup.poll() is None:
+            sup.kill()
