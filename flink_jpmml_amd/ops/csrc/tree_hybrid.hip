@@ -351,6 +351,9 @@ __global__ __launch_bounds__(TB) void tree_hybrid_reduce_kernel(TreeArgs a, int 
 
 template <bool GENERAL, bool FEAT_LDS, int H>
 int launch_hybrid_t(hipStream_t stream, const HybridArgs& ha, dim3 grid, size_t lds) {
+  if constexpr (H > 4) {
+    if (ha.tail_format != 0) return -6;  // pointer tails: heads of 2-4 levels (profiles/r3ar)
+  } else {
   if (ha.tail_format == 1) {  // 16-byte pointer tail, clamped loads
     int err = prepare_launch(tree_hybrid_ptr_kernel<GENERAL, FEAT_LDS, H, false>, lds);
     if (err) return err;
@@ -362,6 +365,7 @@ int launch_hybrid_t(hipStream_t stream, const HybridArgs& ha, dim3 grid, size_t 
     if (err) return err;
     hipLaunchKernelGGL((tree_hybrid_ptr_kernel<GENERAL, FEAT_LDS, H, true>), grid, dim3(TB), lds, stream, ha);
     return 0;
+  }
   }
   int err = prepare_launch(tree_hybrid_kernel<GENERAL, FEAT_LDS, H>, lds);
   if (err) return err;
@@ -386,7 +390,7 @@ using namespace pmml_tree;
 
 PMML_API int pmml_tree_hybrid_args_size() { return (int)sizeof(HybridArgs); }
 
-// head_depth in {2, 3, 4, 6, 8, 10} (2 and 3: pointer tail only); splits >= 1 (grid.y tree groups, > 1 needs t.partial).
+// head_depth in {2, 3, 4, 6, 8, 10} (2 and 3: pointer tail only, 6-10: compact tail only); splits >= 1 (grid.y tree groups, > 1 needs t.partial).
 PMML_API int pmml_tree_hybrid_launch(hipStream_t stream, const HybridArgs* args, int head_depth, int splits) {
   HybridArgs ha = *args;
   TreeArgs& a = ha.t;

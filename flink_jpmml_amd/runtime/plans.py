@@ -1231,7 +1231,8 @@ class TreePlan(DevicePlan):
         ``hybrid_tail`` (hybrid layout): ``"compact"`` (depth-first uint2 tail,
         :func:`~flink_jpmml_amd.runtime.hybrid.pack_hybrid_compact`) or ``"wide"`` (the 16-byte BFS
         pointer tail of :func:`~flink_jpmml_amd.runtime.hybrid.pack_trees`, clamped loads, or
-        the wave-uniform skip with ``pointer_load="uskip"``; head depths 2-10).
+        the wave-uniform skip with ``pointer_load="uskip"``; head depths 2-4). Measured slower than
+        the plain pointer walk (profiles/r3ar), kept as a tested option.
 
         ``xcd_split`` (pointer / hybrid layouts): ``"on"`` splits the forest into 8 tree slices
         scored by workgroups placed on the 8 XCDs (csrc ``tree_block``), so each XCD's 4 MiB L2
@@ -1458,8 +1459,8 @@ class TreePlan(DevicePlan):
                 # (tree_hybrid.hip); H = 4 measured best at depth 14 (profiles/r3c: larger heads
                 # pay more for the per-workgroup head copy and LDS bank conflicts than they save)
                 H = head_depth or 4
-                if H not in ((2, 3, 4, 6, 8, 10) if hybrid_tail == "wide" else (4, 6, 8, 10)):
-                    raise ValueError("head_depth must be 4, 6, 8 or 10 (2 and 3 with the wide tail)")
+                if H not in ((2, 3, 4) if hybrid_tail == "wide" else (4, 6, 8, 10)):
+                    raise ValueError("head_depth must be 4, 6, 8 or 10 (compact tail) or 2-4 (wide tail)")
                 fixed = (F * TB * 4 if feat_lds else 0) + TB * 4 + (self.C * TB * 4 if self.general else 0)
                 fit = (lds_budget - fixed) // (head_words(H) * 4)
                 if fit < 1:

@@ -37,7 +37,6 @@ CONFIGS = {
     "hybw2": dict(layout="hybrid", head_depth=2, hybrid_tail="wide"),
     "hybw3": dict(layout="hybrid", head_depth=3, hybrid_tail="wide"),
     "hybw4": dict(layout="hybrid", head_depth=4, hybrid_tail="wide"),
-    "hybw6": dict(layout="hybrid", head_depth=6, hybrid_tail="wide"),
     "hybw3u": dict(layout="hybrid", head_depth=3, hybrid_tail="wide", pointer_load="uskip"),
     "hybw4u": dict(layout="hybrid", head_depth=4, hybrid_tail="wide", pointer_load="uskip"),
     "pointer+peel": dict(layout="pointer", pointer_load="peel"),

@@ -133,7 +133,7 @@ def test_super_layout_votes_on_gpu(gpu):
                                   dict(layout="hybrid", hybrid_tail="wide", head_depth=2),
                                   dict(layout="hybrid", hybrid_tail="wide", head_depth=4, pointer_load="uskip"),
                                   dict(layout="hybrid", hybrid_tail="wide", head_depth=4),
-                                  dict(layout="hybrid", hybrid_tail="wide", head_depth=6)])
+                                  dict(layout="hybrid", hybrid_tail="wide", head_depth=3)])
 @pytest.mark.parametrize("missing", ["defaultChild", "nullPrediction"])
 def test_uniform_skip_walks_on_gpu(gpu, opts, missing):
     """Wave-uniform skip of finished walk slots (pointer walk and the LDS-head + 16-byte pointer

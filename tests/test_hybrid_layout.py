@@ -252,7 +252,7 @@ def test_super_layout_votes_and_limits():
         _plan(gbdt_pmml(n_trees=3, depth=6, n_features=40, seed=1), layout="pointer", node_format="super")
 
 
-@pytest.mark.parametrize("H", [2, 3, 4, 6])
+@pytest.mark.parametrize("H", [2, 3, 4])
 @pytest.mark.parametrize("missing", ["defaultChild", "nullPrediction"])
 def test_hybrid_wide_tail_emulation_matches_oracle(H, missing):
     """LDS head + 16-byte BFS pointer tail (``tree_hybrid_ptr_kernel``): head exits are pointer
