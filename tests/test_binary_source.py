@@ -61,3 +61,21 @@ def test_socket_binary_frames(fixtures_dir):
     srv.close()
     np.testing.assert_array_equal(np.concatenate([b.numpy() for _, b in out]), X)
     assert len(out) == 5
+
+
+def test_binary_file_parallel_reads_exact_and_truncation_detected(tmp_path):
+    """Positional reads by several threads land every row in place (odd row counts, batches that
+    do not divide the file, more threads than rows in a batch); a file cut short raises instead
+    of yielding a batch with unread rows."""
+    import pytest
+
+    X = np.random.default_rng(3).standard_normal((1003, 7)).astype(np.float32)
+    path = write_binary(str(tmp_path / "x.fjab"), X)
+    for threads, rows in ((1, 1003), (4, 100), (16, 5)):
+        src = BinaryBatchSource(path, batch_rows=rows, threads=threads, repeat=2)
+        got = np.concatenate([b.X.numpy() for b in src.iterate()])
+        np.testing.assert_array_equal(got, np.concatenate([X, X]))
+    with open(path, "r+b") as fh:
+        fh.truncate(64 + 500 * 7 * 4 + 3)
+    with pytest.raises(EOFError):
+        list(BinaryBatchSource(path, batch_rows=256, threads=4).iterate())
