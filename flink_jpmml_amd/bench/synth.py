@@ -609,11 +609,13 @@ def naive_bayes_pmml(n_features: int = 4, classes: int = 3, seed: int = 0, thres
 
 def knn_pmml(n_instances: int = 200, n_features: int = 4, k: int = 3, classification: bool = True, seed: int = 0,
              method: Optional[str] = None, metric: str = "euclidean", classes: int = 3,
-             measure: str = "distance", compare: Optional[str] = None, target: Optional[str] = None) -> str:
+             measure: str = "distance", compare: Optional[str] = None, target: Optional[str] = None,
+             threshold: float = 0.001, quantum: Optional[float] = None) -> str:
     """``NearestNeighborModel`` over ``n_instances`` inline training rows of ``f*`` (targets
     ``0..classes-1`` or real values). ``metric`` is the ComparisonMeasure element body (e.g.
     ``'minkowski p-parameter="3"'``), ``measure`` its kind, ``compare`` a compareFunction, ``target``
-    the attributes of a ``<Target field="y" .../>`` (regression rescale / clip / cast)."""
+    the attributes of a ``<Target field="y" .../>`` (regression rescale / clip / cast), ``threshold``
+    the weighting offset, ``quantum`` rounds the instances to multiples of it (exact in fp32)."""
     rng = np.random.default_rng(seed)
     out = io.StringIO()
     _header(out, f"synthetic {k}-NN")
@@ -622,7 +624,7 @@ def knn_pmml(n_instances: int = 200, n_features: int = 4, k: int = 3, classifica
     fn = "classification" if classification else "regression"
     meth = (f' categoricalScoringMethod="{method or "majorityVote"}"' if classification
             else f' continuousScoringMethod="{method or "average"}"')
-    out.write(f' <NearestNeighborModel functionName="{fn}" numberOfNeighbors="{k}"{meth} threshold="0.001">\n')
+    out.write(f' <NearestNeighborModel functionName="{fn}" numberOfNeighbors="{k}"{meth} threshold="{threshold!r}">\n')
     _mining_schema(out, n_features, "y", "  ")
     if target:
         out.write(f'  <Targets><Target field="y" {target}/></Targets>\n')
@@ -630,6 +632,8 @@ def knn_pmml(n_instances: int = 200, n_features: int = 4, k: int = 3, classifica
     out.write("".join(f'<InstanceField field="f{j}" column="c{j}"/>' for j in range(n_features)))
     out.write('<InstanceField field="y" column="target"/></InstanceFields>\n   <InlineTable>\n')
     X = rng.standard_normal((n_instances, n_features))
+    if quantum:
+        X = np.round(X / quantum) * quantum
     for i in range(n_instances):
         t = str(int(rng.integers(classes))) if classification else f"{rng.normal() * 3:.4f}"
         out.write("    <row>" + "".join(f"<c{j}>{X[i, j]:.5f}</c{j}>" for j in range(n_features))

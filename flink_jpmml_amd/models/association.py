@@ -73,7 +73,9 @@ class AssociationEvaluator(ModelEvaluator):
             a, c = self.sets[r.antecedent], self.sets[r.consequent]
             if not a <= basket:
                 continue
-            if algorithm == "exclusiveRecommendation" and (c & basket):
+            # PMML: the rule is excluded when its whole consequent is already in the basket
+            # (a consequent that only partly overlaps is still recommended)
+            if algorithm == "exclusiveRecommendation" and c <= basket:
                 continue
             if algorithm == "ruleAssociation" and not c <= basket:
                 continue

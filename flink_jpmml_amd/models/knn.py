@@ -89,7 +89,7 @@ class NearestNeighborEvaluator(ClusteringEvaluator):
             C = len(self.categories)
             votes = np.zeros((n, C))
             first = np.full((n, C), k, dtype=np.int64)
-            w = 1.0 / (np.abs(dist) + m.threshold) if m.categorical_method == "weightedMajorityVote" else np.ones_like(dist)
+            w = _weights(dist, m.threshold) if m.categorical_method == "weightedMajorityVote" else np.ones_like(dist)
             if m.categorical_method not in ("majorityVote", "weightedMajorityVote"):
                 raise UnsupportedFeatureException(f"categoricalScoringMethod {m.categorical_method!r}")
             rows = np.arange(n)
@@ -110,8 +110,23 @@ class NearestNeighborEvaluator(ClusteringEvaluator):
         elif meth == "median":
             v = np.median(y, axis=1)
         elif meth == "weightedAverage":
-            w = 1.0 / (np.abs(dist) + m.threshold)
-            v = (w * y).sum(axis=1) / w.sum(axis=1)
+            w = _weights(dist, m.threshold)
+            with np.errstate(invalid="ignore"):  # rows without neighbours (all fields missing): NaN
+                v = (w * y).sum(axis=1) / w.sum(axis=1)
         else:
             raise UnsupportedFeatureException(f"continuousScoringMethod {meth!r}")
         return ModelResult("regression", np.where(valid, v, NAN), valid & np.isfinite(v))
+
+
+def _weights(dist: np.ndarray, threshold: float) -> np.ndarray:
+    """Neighbour weights ``1 / (|d| + threshold)`` of the weighted scoring methods. A zero
+    denominator (an exact match with ``threshold = 0``) would make the weighted average inf / inf;
+    its limit as the distance goes to 0 is the exact matches alone, equally weighted — so a row
+    with any exact match weighs those 1 and the others 0 (the kernel applies the same rule)."""
+    with np.errstate(divide="ignore"):
+        w = 1.0 / (np.abs(dist) + threshold)
+    exact = ~np.isfinite(w) & ~np.isnan(w)
+    if exact.any():
+        rows = exact.any(axis=1)
+        w[rows] = exact[rows].astype(np.float64)
+    return w

@@ -59,6 +59,10 @@ PyObject *pack_dense(PyObject *, PyObject *args) {
     PyTypeObject *tp = reinterpret_cast<PyTypeObject *>(type_obj);
     PyArrayObject *out = reinterpret_cast<PyArrayObject *>(out_obj);
     const Py_ssize_t n = PyList_GET_SIZE(seq);
+    if (width < 0) {
+        PyErr_SetString(PyExc_ValueError, "pack_dense: negative width");
+        return nullptr;
+    }
     if (PyArray_TYPE(out) != NPY_DOUBLE || !PyArray_IS_C_CONTIGUOUS(out) || PyArray_SIZE(out) < n * width) {
         PyErr_SetString(PyExc_ValueError, "pack_dense: out must be a C-contiguous float64 array of n*width");
         return nullptr;

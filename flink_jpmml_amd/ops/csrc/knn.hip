@@ -146,12 +146,18 @@ __device__ __forceinline__ void knn_finish(const KnnArgs& a, const float (&key)[
     if (a.agg == AGG_MAJORITY || a.agg == AGG_WMAJORITY) {
       int cls[KMAX];
       float w[KMAX];
+      bool any_exact = false;
 #pragma unroll
       for (int j = 0; j < KMAX; ++j) {
         cls[j] = j < k ? a.inst_class[id[j]] : -1;
         w[j] = a.agg == AGG_WMAJORITY ? 1.0f / (fabsf(d[j]) + a.threshold) : 1.0f;
-        w[j] = __builtin_isfinite(w[j]) ? w[j] : 0.f;
+        any_exact = any_exact || (j < k && !__builtin_isfinite(w[j]));
       }
+      // an exact match (weight 1 / (0 + threshold 0)) dominates: the weighted vote's limit is the
+      // vote of the exact neighbours alone, each counting once (models/knn.py, same rule)
+#pragma unroll
+      for (int j = 0; j < KMAX; ++j)
+        if (any_exact) w[j] = __builtin_isfinite(w[j]) ? 0.f : 1.f;
       // votes of neighbour j's class, summed in rank order; the first rank reaching the maximum
       // names the winner (= the tied class whose best member ranks first)
       float best = -1.f;
@@ -182,16 +188,21 @@ __device__ __forceinline__ void knn_finish(const KnnArgs& a, const float (&key)[
           if (j < k) acc += y[j];
         s = acc / (float)k;
       } else if (a.agg == AGG_WAVERAGE) {
-        float num = 0.f, den = 0.f;
+        float num = 0.f, den = 0.f, num0 = 0.f, den0 = 0.f;
 #pragma unroll
         for (int j = 0; j < KMAX; ++j) {
           if (j < k) {
             const float w = 1.0f / (fabsf(d[j]) + a.threshold);
-            num = fmaf(w, y[j], num);
-            den += w;
+            if (__builtin_isfinite(w)) {
+              num = fmaf(w, y[j], num);
+              den += w;
+            } else {  // exact match: see the vote above
+              num0 += y[j];
+              den0 += 1.f;
+            }
           }
         }
-        s = num / den;
+        s = den0 > 0.f ? num0 / den0 : num / den;
       } else {  // median: odd-even transposition sort of the k values (+inf padding sorts last)
 #pragma unroll
         for (int pass = 0; pass < KMAX; ++pass) {

@@ -178,6 +178,18 @@ def all_reduce_max(x: int, ctx: DistContext, group=None) -> int:
     return int(t.item())
 
 
+def all_gather_ints(x: int, ctx: DistContext, group=None) -> List[int]:
+    """One integer per rank, in rank order (host tensors: use it on a gloo group such as ``ctrl``
+    so no device work or device sync is involved)."""
+    if not ctx.is_distributed:
+        return [int(x)]
+    dev = _obj_device(ctx, group) or torch.device("cpu")
+    t = torch.tensor([int(x)], dtype=torch.int64, device=dev)
+    out = [torch.zeros_like(t) for _ in range(ctx.world_size)]
+    dist.all_gather(out, t, group=group)
+    return [int(o.item()) for o in out]
+
+
 def broadcast_tensors(tensors: Optional[dict], spec: Optional[dict], ctx: DistContext, src: int = 0,
                       group=None) -> dict:
     """Broadcast a dict of tensors whose shapes/dtypes are given by ``spec`` (known on all ranks).

@@ -111,7 +111,7 @@ class GatherSink(SinkFunction):
         self._buf: List[Tuple[PredictionBatch, Optional[RecordBatch]]] = []
         self._parts: List[Tuple[np.ndarray, np.ndarray, np.ndarray]] = []
         self._comm = None
-        self._inflight: List[Any] = []  # (works, keepalive, gathered device tensors)
+        self._inflight: List[Any] = []  # (collective works, batches, deliver-on-retire closure)
         self._lock_rows: Optional[int] = None
         self._lock_path: Optional[bool] = None
         self._ring: List[Any] = []
@@ -153,15 +153,6 @@ class GatherSink(SinkFunction):
             return
         buf, self._buf = self._buf, []
         self._gather(buf)
-
-    def finish(self) -> None:
-        """Wait for outstanding asynchronous gathers and move kept results to the host."""
-        inflight, self._inflight = self._inflight, []
-        for works, _keep, dev in inflight:
-            for w in works:
-                w.wait()
-            if dev is not None and (self.keep or self.on_gathered is not None):
-                self._deliver(*(t.cpu().numpy() for t in dev))
 
     # ------------------------------------------------------------------ results
     def _deliver(self, s: np.ndarray, v: np.ndarray, o: np.ndarray) -> None:
@@ -248,23 +239,116 @@ class GatherSink(SinkFunction):
             for t in pb.device_out:
                 t.record_stream(comm)  # the allocator keeps them until the gather has read them
 
-    def _gather_device(self, items) -> None:
+    @staticmethod
+    def _h2d(a: np.ndarray, device, keep: list):
+        """Stream-ordered copy of a small host array (pinned staging, no host sync); the staging
+        tensor goes into ``keep`` so it outlives the copy."""
         import torch
 
-        comm = self._stream()
+        h = torch.from_numpy(np.ascontiguousarray(a)).pin_memory()
+        keep.append(h)
+        return h.to(device, non_blocking=True)
+
+    @classmethod
+    def _masked_mirrors(cls, pb: PredictionBatch, keep: list):
+        """The device ``(score, valid)`` mirrors with the per-record size validation applied
+        (rows whose vector had the wrong width are EmptyScore on every path, as in
+        ``PredictionBatch._finish``). Runs on the current (comm) stream."""
+        import torch
+
+        s, v = pb.device_out
+        ok = getattr(pb, "_row_ok", None)
+        if ok is None or ok.all():
+            return s, v
+        ok_t = cls._h2d(ok.astype(np.bool_), s.device, keep)
+        return torch.where(ok_t, s, torch.full_like(s, float("nan"))), v & ok_t.to(v.dtype)
+
+    def _retire(self, entry) -> None:
+        """Complete one in-flight gather: wait for its collective, deliver the rows, then run the
+        batches' completion hooks (latency observers) — the kernels finished before the gather."""
+        works, pbs, finish = entry
+        for w in works:
+            w.wait()
+        if finish is not None:
+            finish()
+        for pb in pbs:
+            pb.wait()
+
+    def finish(self) -> None:
+        """Wait for outstanding asynchronous gathers and move kept results to the host."""
+        inflight, self._inflight = self._inflight, []
+        for entry in inflight:
+            self._retire(entry)
+
+    def _bound_inflight(self, limit: int) -> None:
+        while len(self._inflight) >= limit:
+            self._retire(self._inflight.pop(0))
+
+    def _gather_device(self, items) -> None:
+        """Variable-length device gather without host syncs: the row counts travel on the gloo
+        ``ctrl`` group (host integers — the job thread knows them without touching the GPU), the
+        payload as one packed byte buffer per rank (scores | valid | source offsets) in a single
+        asynchronous RCCL collective on the comm stream. Delivery happens when the gather is
+        retired (next flush beyond the in-flight bound, ``finish``, ``close``)."""
+        import torch
+        import torch.distributed as dist
+
+        from .dist import all_gather_ints
+
+        ctx = self.dist
         pbs = [pb for pb, _ in items]
+        n = sum(len(pb) for pb in pbs)
+        sizes = all_gather_ints(n, ctx, group=ctx.group("ctrl"))
+        m = max(sizes) if sizes else 0
+        if m == 0:
+            return
+        W = ctx.world_size
+        row = 13  # float32 score + uint8 valid + int64 source offset
+        offs = np.zeros(m, dtype=np.int64)
+        if n:
+            offs[:n] = np.concatenate([_row_offsets(pb, b) for pb, b in items])
+        keep: list = []
+        offs_h = torch.from_numpy(offs).pin_memory()
+        self._bound_inflight(4)
+        comm = self._stream()
+        dev = ctx.device
         with torch.cuda.stream(comm):
             self._wait_inputs(comm, pbs)
-            s = torch.cat([pb.device_out[0] for pb in pbs])
-            v = torch.cat([pb.device_out[1] for pb in pbs])
-            o = torch.from_numpy(np.concatenate([_row_offsets(pb, b) for pb, b in items])).to(s.device)
-            dst = None if self.to == "all" else 0
-            gs = gather_varlen(s, self.dist, dst=dst)
-            gv = gather_varlen(v, self.dist, dst=dst)
-            go = gather_varlen(o, self.dist, dst=dst)
-        comm.synchronize()
-        if gs is not None:
-            self._deliver(gs.cpu().numpy(), gv.cpu().numpy(), go.cpu().numpy())
+            buf = torch.zeros(m * row, dtype=torch.uint8, device=dev)
+            sv = buf[: 4 * m].view(torch.float32)
+            vv = buf[4 * m: 5 * m]
+            ov = buf[5 * m:].view(torch.int64)
+            k = 0
+            for pb in pbs:
+                ms, mv = self._masked_mirrors(pb, keep)
+                sv[k: k + len(pb)].copy_(ms)
+                vv[k: k + len(pb)].copy_(mv.to(torch.uint8))
+                k += len(pb)
+            ov.copy_(offs_h, non_blocking=True)
+            root = self.to == "all" or ctx.rank == 0
+            out = torch.empty(W * m * row, dtype=torch.uint8, device=dev) if root else None
+            if self.to == "all":
+                work = dist.all_gather_into_tensor(out, buf, async_op=True)
+            else:
+                parts = list(out.chunk(W)) if root else None
+                work = dist.gather(buf, parts, dst=0, async_op=True)
+            host = torch.empty(W * m * row, dtype=torch.uint8, pin_memory=True) if root else None
+        METRICS.inc("dist.bytes_gathered", W * m * row)
+        keepalive = (buf, offs_h, out, keep)
+
+        def finish(out=out, host=host, sizes=sizes, m=m, keepalive=keepalive):
+            if out is None or not (self.keep or self.on_gathered is not None):
+                return
+            with torch.cuda.stream(comm):
+                host.copy_(out, non_blocking=True)
+            comm.synchronize()
+            a = host.numpy().reshape(W, m * row)
+            s = np.concatenate([a[r, : 4 * m].view(np.float32)[: sizes[r]] for r in range(W)])
+            v = np.concatenate([a[r, 4 * m: 5 * m][: sizes[r]] for r in range(W)]).astype(bool)
+            o = np.concatenate([a[r, 5 * m:].view(np.int64)[: sizes[r]] for r in range(W)])
+            self._deliver(s, v, o)
+
+        self._inflight.append(([work], pbs, finish))
 
     def _gather_lockstep_device(self, item) -> None:
         """Equal-size per-rank elements: asynchronous ``all_gather_into_tensor`` on the comm stream,
@@ -288,30 +372,30 @@ class GatherSink(SinkFunction):
                            torch.empty(n * W, dtype=torch.uint8, device=dev)) for _ in range(2)]
         elif n != self._lock_rows:
             raise ValueError("GatherSink(lockstep=True): element row count changed")
-        if len(self._inflight) >= len(self._ring):
-            works, _, dev_out = self._inflight.pop(0)
-            for w in works:
-                w.wait()
-            if dev_out is not None and (self.keep or self.on_gathered is not None):
-                self._deliver(*(t.cpu().numpy() for t in dev_out))
+        self._bound_inflight(len(self._ring))
         gs, gv = self._ring[self._ring_i]
         self._ring_i = (self._ring_i + 1) % len(self._ring)
         comm = self._stream()
+        keep: list = []
         with torch.cuda.stream(comm):
             self._wait_inputs(comm, [pb])
-            w1 = dist.all_gather_into_tensor(gs, pb.device_out[0], async_op=True)
-            w2 = dist.all_gather_into_tensor(gv, pb.device_out[1], async_op=True)
+            ms, mv = self._masked_mirrors(pb, keep)
+            w1 = dist.all_gather_into_tensor(gs, ms, async_op=True)
+            w2 = dist.all_gather_into_tensor(gv, mv.to(torch.uint8) if mv.dtype != torch.uint8 else mv,
+                                             async_op=True)
         METRICS.inc("dist.bytes_gathered", gs.numel() * 4 + gv.numel())
-        keep_dev = None
         if self.keep or self.on_gathered is not None:
-            o = torch.from_numpy(np.tile(_row_offsets(pb, batch), 1)).to(gs.device)
             go = torch.empty(n * self.dist.world_size, dtype=torch.int64, device=gs.device)
             with torch.cuda.stream(comm):
+                o = self._h2d(_row_offsets(pb, batch), gs.device, keep)
                 w3 = dist.all_gather_into_tensor(go, o, async_op=True)
-            keep_dev = (gs, gv, go)
-            self._inflight.append(([w1, w2, w3], pb, keep_dev))
+
+            def finish(gs=gs, gv=gv, go=go, keep=keep):
+                self._deliver(gs.cpu().numpy(), gv.cpu().numpy(), go.cpu().numpy())
+
+            self._inflight.append(([w1, w2, w3], [pb], finish))
         else:
-            self._inflight.append(([w1, w2], pb, None))
+            self._inflight.append(([w1, w2], [pb], lambda keep=keep: None))
 
 
 __all__ = ["GatherSink", "gather_varlen"]

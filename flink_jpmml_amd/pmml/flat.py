@@ -49,6 +49,8 @@ class FlatTree:
         self.n_children = counts.astype(np.int64)
         self._lock = threading.Lock()
         self._root: Optional[ir.Node] = None
+        # raw predicate spans parse now, so a malformed one fails the load like on the DOM path
+        self.raw_pred: Dict[int, ir.Predicate] = {k: _parse_raw(v) for k, v in raw.items()}
 
     # ------------------------------------------------------------------ helpers
     def s(self, k: int) -> Optional[str]:
@@ -87,14 +89,7 @@ class FlatTree:
             return ir.SimplePredicate(self.strings[int(a["pred_field"][k])], OP_NAMES[int(a["pred_op"][k])],
                                       self.s(int(a["pred_value_s"][k])))
         if kind == P_RAW:
-            import xml.etree.ElementTree as ET
-
-            from .parser import _parse_predicate
-
-            el = ET.fromstring(_with_ns(self.raw[k]))
-            if el.tag.rsplit("}", 1)[-1] == "FjaWrap":
-                el = el[0]
-            return _parse_predicate(el)
+            return self.raw_pred[k]
         from ..api.exceptions import PmmlParseError
 
         raise PmmlParseError("<Node> has no predicate")
@@ -131,6 +126,25 @@ class FlatTree:
             return self._root
 
 
+def _parse_raw(snippet: bytes) -> ir.Predicate:
+    import xml.etree.ElementTree as ET
+
+    from ..api.exceptions import PmmlParseError
+    from .parser import _parse_predicate
+
+    try:
+        el = ET.fromstring(_with_ns(snippet))
+        if el.tag.rsplit("}", 1)[-1] == "FjaWrap":
+            el = el[0]
+        return _parse_predicate(el)
+    except ET.ParseError as e:
+        raise PmmlParseError(f"malformed PMML XML in a tree predicate: {e}") from e
+    except (ValueError, TypeError) as e:
+        if isinstance(e, PmmlParseError):
+            raise
+        raise PmmlParseError(f"malformed PMML content in a tree predicate: {e}") from e
+
+
 def _with_ns(snippet: bytes) -> bytes:
     """A raw predicate cut out of the document: wrap it so namespace prefixes / the default
     namespace parse (the parser only looks at local names)."""
@@ -138,6 +152,13 @@ def _with_ns(snippet: bytes) -> bytes:
         prefix = snippet[1:snippet.index(b":")]
         return b"<FjaWrap xmlns:" + prefix + b'="http://www.dmg.org/PMML-4_4">' + snippet + b"</FjaWrap>"
     return snippet
+
+
+def _py_float(s: str) -> float:
+    try:
+        return float(s)
+    except ValueError:
+        return float("nan")
 
 
 def scan_document(data: bytes):
@@ -154,6 +175,21 @@ def scan_document(data: bytes):
     if res is None:
         return None
     skeleton, trees, strings = res
+    # the scanner reads numbers from ASCII strings only; Python's float() also takes Unicode digits
+    # and white space, so non-ASCII scores / split values are settled here (DOM path: float(s))
+    wide = [k for k, s in enumerate(strings) if not s.isascii()]
+    if wide:
+        num = np.full(len(strings) + 1, np.nan)
+        for k in wide:
+            num[k] = _py_float(strings[k])
+        wide_a = np.zeros(len(strings) + 1, dtype=bool)
+        wide_a[wide] = True
+        for arrays in trees:
+            for s_key, d_key in (("score_s", "score_d"), ("pred_value_s", "pred_value_d")):
+                sk = arrays[s_key]
+                m = wide_a[sk]  # index -1 (absent) hits the trailing False
+                if m.any():
+                    arrays[d_key][m] = num[sk[m]]
     flats = []
     for arrays in trees:
         raw = {}

@@ -390,7 +390,7 @@ def _parse_node(el: ET.Element) -> ir.Node:
             node.children.append(_parse_node(c))
         elif ln == "ScoreDistribution":
             node.distributions.append(
-                ir.ScoreDistribution(c.get("value"), float(c.get("recordCount", "0")), _f(c, "probability"),
+                ir.ScoreDistribution(c.get("value"), _f(c, "recordCount", 0.0), _f(c, "probability"),
                                      _f(c, "confidence"))
             )
         elif ln in ("Regression", "DecisionTree"):
@@ -574,7 +574,7 @@ def _parse_rules(el: ET.Element) -> List[object]:
     for c in el:
         ln = _local(c.tag)
         if ln == "SimpleRule":
-            dists = [ir.ScoreDistribution(d.get("value"), float(d.get("recordCount", "0")), _f(d, "probability"),
+            dists = [ir.ScoreDistribution(d.get("value"), _f(d, "recordCount", 0.0), _f(d, "probability"),
                                           _f(d, "confidence")) for d in _children(c, "ScoreDistribution")]
             out.append(ir.SimpleRule(c.get("id"), c.get("score"), _find_predicate(c), _f(c, "confidence", 1.0),
                                      _f(c, "weight", 1.0), dists))
@@ -720,6 +720,17 @@ _VERSION_RE = re.compile(r"PMML-(\d)_(\d)")
 
 
 def parse_element(root: ET.Element) -> ir.PMMLDocument:
+    """The IR of a parsed document. Malformed attribute values (``float("x")``, a missing
+    required number) raise :class:`PmmlParseError` like malformed markup does."""
+    try:
+        return _parse_document(root)
+    except (ValueError, TypeError) as e:
+        if isinstance(e, PmmlParseError):
+            raise
+        raise PmmlParseError(f"malformed PMML content: {e}") from e
+
+
+def _parse_document(root: ET.Element) -> ir.PMMLDocument:
     if _local(root.tag) != "PMML":
         raise PmmlParseError(f"root element is <{_local(root.tag)}>, expected <PMML>")
     version = root.get("version")
@@ -772,20 +783,21 @@ def parse_string(text) -> ir.PMMLDocument:
             skeleton, flats = scanned
             token = _FLATS.set(flats)
             try:
-                try:
-                    root = ET.fromstring(skeleton)
-                except ET.ParseError as e:
-                    raise PmmlParseError(f"malformed PMML XML: {e}") from e
-                return parse_element(root)
+                return parse_element(_xml_root(skeleton))
             finally:
                 _FLATS.reset(token)
-    if isinstance(text, bytes):
-        text = text.decode("utf-8")
+    if isinstance(text, (bytearray, memoryview)):
+        text = bytes(text)
+    return parse_element(_xml_root(text))
+
+
+def _xml_root(text) -> ET.Element:
+    """expat's verdict on the document (bytes honour their XML declaration's encoding); every
+    rejection — malformed markup, an unknown or unsupported encoding — is a PmmlParseError."""
     try:
-        root = ET.fromstring(text)
-    except ET.ParseError as e:
+        return ET.fromstring(text)
+    except (ET.ParseError, LookupError, ValueError) as e:
         raise PmmlParseError(f"malformed PMML XML: {e}") from e
-    return parse_element(root)
 
 
 def parse_file(path: str) -> ir.PMMLDocument:
@@ -798,7 +810,7 @@ def parse_file(path: str) -> ir.PMMLDocument:
             return parse_string(fh.read())
     try:
         tree = ET.parse(path)
-    except ET.ParseError as e:
+    except (ET.ParseError, LookupError, ValueError) as e:
         raise PmmlParseError(f"malformed PMML XML in {path}: {e}") from e
     return parse_element(tree.getroot())
 

@@ -218,53 +218,18 @@ def _score_calls(model: PmmlModel, calls: List[Tuple[Any, Optional[float]]]) -> 
     return out  # type: ignore[return-value]
 
 
-class _DeferredTarget(Target):
-    """``prediction.value`` of a not-yet-scored :class:`DeferredPrediction`: resolves (scoring the
-    pending micro-batch) only when its score is actually read."""
-
-    __slots__ = ("_dp",)
-
-    def __init__(self, dp: "DeferredPrediction"):
-        self._dp = dp
-
-    def _t(self) -> Target:
-        return self._dp._get().value
-
-    def get(self) -> float:
-        return self._t().get()
-
-    def get_or_else(self, default: float) -> float:
-        return self._t().get_or_else(default)
-
-    @property
-    def is_empty(self) -> bool:
-        return self._t().is_empty
-
-    @property
-    def value(self) -> float:
-        return self._t().value
-
-    def __eq__(self, other: object) -> bool:
-        return self._t() == (other._t() if isinstance(other, _DeferredTarget) else other)
-
-    def __hash__(self) -> int:
-        return hash(self._t())
-
-    def __repr__(self) -> str:
-        return repr(self._t())
-
-    def __reduce__(self):
-        return self._t().__reduce__()
-
-
 class DeferredPrediction(Prediction):
     """The :class:`Prediction` a per-record UDF gets from ``model.predict`` inside a micro-batch.
 
     The UDF runs **exactly once per event**, when the event arrives; its ``predict`` calls are
     collected and scored together (one RecordBatch per model) when the micro-batch flushes — on
     size, latency timer, control message, barrier or end of input. A UDF that reads the score
-    inside ``f`` (``.value.get_or_else(..)``) resolves the pending calls right there (a smaller
-    batch, never a second call of ``f``); ``prediction.value`` itself stays lazy."""
+    inside ``f`` — any access to ``prediction.value`` (``.value.get_or_else(..)``,
+    ``isinstance(p.value, Score)``, ``p.value is EmptyScore``) — resolves the pending calls right
+    there (a smaller batch, never a second call of ``f``), so it sees the real ``Score`` /
+    ``EmptyScore`` object, as with the reference's ``case Score(v) / case EmptyScore``. UDFs that
+    only return the prediction stay fully batched. The one check that cannot hold is object
+    identity of the prediction itself (``p is EMPTY_PREDICTION``): compare ``p.value`` instead."""
 
     __slots__ = ("_batcher", "_resolved")
 
@@ -281,8 +246,7 @@ class DeferredPrediction(Prediction):
 
     @property
     def value(self) -> Target:  # type: ignore[override]
-        r = self._resolved
-        return r.value if r is not None else _DeferredTarget(self)
+        return self._get().value
 
     @property
     def outputs(self):  # type: ignore[override]

@@ -356,13 +356,25 @@ class Executor:
             off = int(entry.get("offset", 0))
             ranks = entry.get("ranks")
             leader = None
+            cuts = None
             if ranks is not None and len(ranks) == self.world:
                 off = int(ranks[self.rank])  # per-rank cut of a time-based checkpoint
                 leader = int(min(ranks))
-            elif ranks is not None and n.dist_mode in ("parallel",):
-                raise RuntimeError(f"source {n.uid}: checkpoint was taken at world size {len(ranks)}, "
-                                   f"restoring at {self.world} needs the same rank-local splits")
-            self.readers[id(n)] = SourceReader(n, self.rank, self.world, self.clock, off, leader_offset=leader)
+            elif ranks is not None:
+                # rescaled restore of a time-based checkpoint: every rank stopped at its own cut
+                if n.dist_mode in ("parallel", "either"):
+                    raise RuntimeError(f"source {n.uid}: checkpoint was taken at world size {len(ranks)}, "
+                                       f"restoring at {self.world} needs the same rank-local splits")
+                off = int(min(ranks))
+                if n.dist_mode == "shard":
+                    # old rank j owned the global offsets g with g % old_world == j and processed
+                    # those below its cut: resume at the smallest cut, skip what its owner did
+                    cuts = [int(r) for r in ranks]
+                # replicate / all: every rank saw every element; replaying from the smallest cut
+                # re-applies control messages the union-restored state already holds (Add of a
+                # known id is ignored, Del of an absent one is a no-op: MetadataManager)
+            self.readers[id(n)] = SourceReader(n, self.rank, self.world, self.clock, off, leader_offset=leader,
+                                               owner_cuts=cuts)
             self.processed[id(n)] = off
         primaries = [n for n in sources if n.dist_mode != "replicate"] or sources
         self.primary = primaries[0] if primaries else None

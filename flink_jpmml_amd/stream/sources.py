@@ -541,8 +541,11 @@ class SourceReader:
     """
 
     def __init__(self, node, rank: int = 0, world: int = 1, clock: Optional[Clock] = None, offset: int = 0,
-                 leader_offset: Optional[int] = None):
+                 leader_offset: Optional[int] = None, owner_cuts: Optional[List[int]] = None):
         self.node = node
+        # restore of a shard-mode checkpoint taken at another world size: global offset g was owned
+        # by old rank g % len(cuts), which processed it iff g < cuts[owner]
+        self._cuts = list(owner_cuts) if owner_cuts else None
         self.rank = rank
         self.world = world
         self.mode = node.dist_mode if world > 1 else "all"
@@ -575,7 +578,7 @@ class SourceReader:
         (``read_chunks``), else ``None`` (iterate element-wise)."""
         src = self.node.source
         rc = getattr(src, "read_chunks", None)
-        if rc is None or self.mode not in ("all", "shard") or self._skip_until:
+        if rc is None or self.mode not in ("all", "shard") or self._skip_until or self._cuts:
             return None
         rank, world = (self.rank, self.world) if self.mode == "shard" else (0, 1)
 
@@ -590,9 +593,12 @@ class SourceReader:
         return gen()
 
     def __iter__(self) -> Iterator[Tuple[int, Any]]:
+        cuts = self._cuts
         if self._strided:  # (global offset, element) pairs of this rank only
             for g, x in self._it:
                 self.offset = g + 1
+                if cuts is not None and g < cuts[g % len(cuts)]:
+                    continue
                 yield g, x
             total = getattr(self.node.source, "global_length", None)
             if callable(total):
@@ -604,6 +610,8 @@ class SourceReader:
                 g = self.offset
                 self.offset += 1
                 if g < self._skip_until:
+                    continue
+                if cuts is not None and g < cuts[g % len(cuts)]:
                     continue
                 if self.mode == "shard" and g % self.world != self.rank:
                     foreign += 1

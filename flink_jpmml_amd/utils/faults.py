@@ -9,13 +9,16 @@ path is exercised deterministically:
   operators turn it into the reference's fatal :class:`ModelLoadingException`);
 * ``corrupt_pmml`` — the document read for a matching path is truncated (a torn / partial file:
   the parser must fail loudly, never score with half a model);
+* ``tear_pmml`` — a span of bytes is deleted from the middle of a matching document, at a node
+  boundary (``…"/>\n <Node id="7" …`` loses ``"/>\n <Node id=``): a torn write inside a large
+  ensemble, which the streaming tree scanner must refuse like the DOM parser does;
 * ``kill_rank`` — rank ``r`` dies (``os._exit``) when it reaches micro-batch ``n`` of the
   distributed serving loop; the survivors' next collective fails or times out and
   :class:`Watchdog` / :func:`guarded_collective` turn that into a :class:`RankFailure` so the job
   restarts from the last checkpoint manifest (`stream/state.py`).
 
 Environment form (read once by :func:`injector`): ``FJA_FAULTS="fail_load=bad.xml;
-corrupt_pmml=torn;kill_rank=1@3"`` (``;``-separated, ``kill_rank=<rank>@<batch>``).
+corrupt_pmml=torn;tear_pmml=gbdt;kill_rank=1@3"`` (``;``-separated, ``kill_rank=<rank>@<batch>``).
 ``FJA_FAULT_ATTEMPTS=k`` limits the faults to the first ``k`` attempts of a job run under the
 restart supervisor (``FJA_ATTEMPT``, :mod:`flink_jpmml_amd.launch`): the restarted job runs clean.
 """
@@ -42,6 +45,7 @@ class RankFailure(RuntimeError):
 class FaultInjector:
     fail_load: List[str] = field(default_factory=list)
     corrupt_pmml: List[str] = field(default_factory=list)
+    tear_pmml: List[str] = field(default_factory=list)
     kill_rank: Dict[int, int] = field(default_factory=dict)  # rank -> micro-batch index
 
     @staticmethod
@@ -53,6 +57,8 @@ class FaultInjector:
                 fi.fail_load.append(val)
             elif key == "corrupt_pmml":
                 fi.corrupt_pmml.append(val)
+            elif key == "tear_pmml":
+                fi.tear_pmml.append(val)
             elif key == "kill_rank":
                 r, _, n = val.partition("@")
                 fi.kill_rank[int(r)] = int(n or 0)
@@ -62,7 +68,7 @@ class FaultInjector:
 
     @property
     def active(self) -> bool:
-        return bool(self.fail_load or self.corrupt_pmml or self.kill_rank)
+        return bool(self.fail_load or self.corrupt_pmml or self.tear_pmml or self.kill_rank)
 
     # -- hooks
     def on_read(self, path: str, data: bytes) -> bytes:
@@ -72,6 +78,8 @@ class FaultInjector:
         if any(p in path for p in self.corrupt_pmml):
             logger.warning("fault injection: truncating %s", path)
             return data[: max(1, len(data) // 2)]
+        if any(p in path for p in self.tear_pmml):
+            return tear(data)
         return data
 
     def on_batch(self, rank: int, index: int) -> None:
@@ -81,6 +89,17 @@ class FaultInjector:
             logger.error("fault injection: killing rank %d at micro-batch %d", rank, index)
             logging.shutdown()
             os._exit(EXIT_KILLED_RANK)
+
+
+def tear(data: bytes, at: Optional[int] = None, span: int = 15) -> bytes:
+    """``data`` with ``span`` bytes deleted just before the first ``<Node`` at or after ``at``
+    (default: the middle), so the tear splices the end of one node into the next."""
+    mid = len(data) // 2 if at is None else at
+    p = data.find(b"<Node", mid)
+    p = mid if p < 0 else p
+    lo = max(0, p - 3)
+    logger.warning("fault injection: tearing %d bytes at offset %d", span, lo)
+    return data[:lo] + data[lo + span:]
 
 
 _INJECTOR: Optional[FaultInjector] = None

@@ -72,3 +72,17 @@ def test_no_matching_rule_is_missing(model):
     out = model.predict_with_outputs(DenseVector(2.0, 2.0, 2.0)).outputs  # basket {2}
     assert out["rec1"] is None and out["excl"] is None
     assert out["conf"] is None or math.isnan(out["conf"])
+
+
+def test_exclusive_recommendation_drops_only_contained_consequents():
+    """``exclusiveRecommendation`` drops a rule only when its whole consequent is already
+    in the basket (PMML; parity unpinned — no JPMML here). A two-item consequent {1, 3} against
+    the basket {2, 3} overlaps in one item and is still recommended."""
+    doc = DOC.replace('<AssociationRule id="r1" support="1.0" confidence="1.0" lift="1.0" antecedent="1" consequent="2"/>',
+                      '<AssociationRule id="r1" support="1.0" confidence="1.0" lift="1.0" antecedent="2" consequent="4"/>')
+    m = PmmlModel.from_string(doc)
+    out = m.predict_with_outputs(DenseVector(2.0, 3.0, float("nan"))).outputs  # basket {2, 3}
+    assert out["excl"] == "{1,3}", out
+    # and a fully contained consequent is excluded: basket {1, 2, 3} contains {1, 3}
+    out = m.predict_with_outputs(DenseVector(1.0, 2.0, 3.0)).outputs
+    assert out["excl"] == "4", out  # r1 excluded; r3 ({1,3} -> {4}) is next

@@ -280,7 +280,8 @@ def test_batched_udf_runs_exactly_once_per_event(fixtures_dir, chunked):
 
 def test_dynamic_batched_udf_exactly_once_with_lazy_value(fixtures_dir):
     """The reference's dynamic UDF returns ``prediction.value`` (E/DynamicEvaluateKmeans.scala:54-60):
-    the Target stays lazy, so events still batch; Add/Del boundaries keep their semantics."""
+    reading ``.value`` resolves the pending calls (the UDF sees a real Target), the UDF still runs
+    exactly once per event, and Add/Del boundaries keep their semantics."""
     seen = []
     seq = [("L", (N1, (1.0, 1.0, 1.0, 1.0))), ("R", AddMessage(N1, 1, fixtures_dir["kmeans"], 0))] + \
           [("L", (N1, (1.0 + i / 10, 2.0, 3.0, 1.0))) for i in range(20)] + [("R", DelMessage(N1, 1, 0))] + \
@@ -305,6 +306,29 @@ def test_dynamic_batched_udf_exactly_once_with_lazy_value(fixtures_dir):
     assert len(seen) == 2 * n  # once per event in each run
     assert [repr(t) for t in out] == [repr(t) for t in ref]
     assert repr(out[0]) == "EmptyScore" and repr(out[-1]) == "EmptyScore" and out[1] == Score(3.0)
+
+
+@pytest.mark.parametrize("bs", [None, 8])
+def test_batched_udf_sees_real_score_and_empty_score(fixtures_dir, bs):
+    """under ``batch_size`` a UDF that pattern-matches the Target inside ``f`` (the
+    reference's ``case Score(v) / case EmptyScore``) gets the real objects, not a lazy stand-in."""
+    from flink_jpmml_amd.domain import EmptyScore as EMPTY
+
+    vals = [(1.0, 1.0, 1.0, 1.0), (1.0, 2.0), (6.9, 3.1, 5.8, 2.1), (1.0,)] * 6
+
+    def udf(e, m):
+        p = m.predict(DenseVector(*e))
+        t = p.value
+        if isinstance(t, Score):
+            return ("score", t.value)
+        if t is EMPTY:
+            return ("empty", None)
+        return ("neither", repr(t))
+
+    env = StreamExecutionEnvironment()
+    out = env.from_collection(vals).evaluate(ModelReader(fixtures_dir["kmeans"]), udf, batch_size=bs).collect()
+    assert [k for k, _ in out] == ["score", "empty", "score", "empty"] * 6
+    assert out[0] == ("score", 3.0)
 
 
 def test_to_batches_adapter_matches_per_record(fixtures_dir):

@@ -15,8 +15,9 @@ def faults():
 
 
 def test_parse_env_spec():
-    fi = FaultInjector.parse("fail_load=bad.xml; corrupt_pmml=torn ;kill_rank=1@3")
+    fi = FaultInjector.parse("fail_load=bad.xml; corrupt_pmml=torn ;tear_pmml=gbdt;kill_rank=1@3")
     assert fi.fail_load == ["bad.xml"] and fi.corrupt_pmml == ["torn"] and fi.kill_rank == {1: 3}
+    assert fi.tear_pmml == ["gbdt"]
     assert not FaultInjector.parse("").active
     with pytest.raises(ValueError):
         FaultInjector.parse("explode=1")
@@ -43,6 +44,26 @@ def test_torn_pmml_never_scores(fixtures_dir, faults):
     faults(FaultInjector(corrupt_pmml=["kmeans"]))
     with pytest.raises(Exception):
         PmmlModel.from_reader(ModelReader(fixtures_dir["kmeans"]))
+
+
+def test_mid_document_tear_of_large_ensemble_fails_the_job(tmp_path, faults):
+    """A torn write inside a 1.3 MB GBDT (the production-size, native-scanner load path): the
+    static operator's ``open`` raises ModelLoadingException like the reference's JAXB load
+    (`S/api/functions/EvaluationFunction.scala:45-48`), and so does the dynamic operator."""
+    from flink_jpmml_amd.api.reader import ModelReader
+    from flink_jpmml_amd.bench import synth
+    from flink_jpmml_amd.pmml import flat
+    from flink_jpmml_amd.stream.operators import EvaluationFunction
+
+    path = tmp_path / "gbdt_big.pmml"
+    path.write_text(synth.gbdt_pmml(n_trees=100, depth=6, n_features=32, seed=3))
+    assert path.stat().st_size >= flat.SCAN_MIN_BYTES
+    fn = EvaluationFunction(ModelReader(str(path)), lambda e, m: None)
+    fn.open(None)  # intact: loads
+    faults(FaultInjector(tear_pmml=["gbdt_big"]))
+    fn = EvaluationFunction(ModelReader(str(path)), lambda e, m: None)
+    with pytest.raises(ModelLoadingException):
+        fn.open(None)
 
 
 def test_watchdog_fires_without_heartbeat():

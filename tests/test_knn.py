@@ -9,6 +9,15 @@ from flink_jpmml_amd.bench.synth import knn_pmml, stream_matrix
 from flink_jpmml_amd.runtime.compiled import CompiledPmml
 
 
+def _wts(d, thr):
+    """Weights of the weighted methods; exact matches (zero denominator) alone, equally weighted."""
+    d = np.abs(np.asarray(d, dtype=np.float64)) + thr
+    exact = d == 0
+    if exact.any():
+        return exact.astype(np.float64)
+    return 1.0 / d
+
+
 def _brute(c, x):
     m = c.model
     inst = np.array([[float(r[f"c{j}"]) for j in range(len(m.inputs))] for r in m.rows])
@@ -19,8 +28,10 @@ def _brute(c, x):
     order = sorted(range(len(d)), key=lambda i: (d[i], i))[: m.k]
     if m.function_name == "classification":
         votes, first = {}, {}
+        ws = _wts([d[i] for i in order], m.threshold) if m.categorical_method == "weightedMajorityVote" \
+            else np.ones(len(order))
         for rank, i in enumerate(order):
-            w = 1.0 / (d[i] + m.threshold) if m.categorical_method == "weightedMajorityVote" else 1.0
+            w = ws[rank]
             votes[tgt[i]] = votes.get(tgt[i], 0.0) + w
             first.setdefault(tgt[i], rank)
         best = max(votes.values())
@@ -29,7 +40,7 @@ def _brute(c, x):
     if m.continuous_method == "median":
         return float(np.median(y))
     if m.continuous_method == "weightedAverage":
-        w = np.array([1.0 / (d[i] + m.threshold) for i in order])
+        w = _wts([d[i] for i in order], m.threshold)
         return float((w * y).sum() / w.sum())
     return float(y.mean())
 
@@ -112,7 +123,7 @@ def _emulate_knn_kernel(plan, X):
     ok = np.isfinite(d).all(1) & (qp > 0)
     if plan.agg < 2:
         cls = plan.inst_class.numpy()[order]
-        wt = 1 / (np.abs(d) + plan.threshold) if plan.agg == 1 else np.ones_like(d)
+        wt = np.stack([_wts(r, plan.threshold) for r in d]) if plan.agg == 1 else np.ones_like(d)
         votes = np.stack([(wt * (cls == cls[:, [j]])).sum(1) for j in range(plan.k)], 1)
         win = cls[np.arange(n), np.argmax(votes, axis=1)]
         s = plan.class_table.numpy()[win].astype(np.float64)
@@ -123,8 +134,9 @@ def _emulate_knn_kernel(plan, X):
         elif plan.agg == 3:
             s = np.median(y, 1)
         else:
-            wt = 1 / (np.abs(d) + plan.threshold)
-            s = (wt * y).sum(1) / wt.sum(1)
+            wt = np.stack([_wts(r, plan.threshold) for r in d])
+            with np.errstate(invalid="ignore"):
+                s = (wt * y).sum(1) / wt.sum(1)
     import torch
 
     st, ot = apply_target_torch(torch.from_numpy(s), torch.from_numpy(ok & np.isfinite(s)), plan.tgt)
@@ -145,6 +157,27 @@ def test_knn_plan_lowering_and_kernel_model(case):
     ref, vref = c.score_matrix_oracle(X)
     assert (v == vref).all()
     np.testing.assert_allclose(s[v], ref[v], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("classification,method", [(False, "weightedAverage"), (True, "weightedMajorityVote")])
+def test_knn_zero_distance_with_zero_threshold_is_pinned(classification, method):
+    """``threshold="0"`` and a query equal to a training instance: ``1/(0 + 0)`` is infinite and
+    the weighted average would be inf / inf = NaN. Pinned semantics (parity unpinned, no JPMML):
+    the limit as the distance goes to 0 — the exact matches alone, equally weighted. A query
+    equal to instance i scores instance i's target (k = 1 behaviour), never NaN / EmptyScore."""
+    doc = knn_pmml(n_instances=60, n_features=4, k=5, classification=classification, method=method, seed=3,
+                   threshold=0.0, quantum=0.25)
+    c = CompiledPmml.from_string(doc)
+    m = c.model
+    inst = np.array([[float(r[f"c{j}"]) for j in range(4)] for r in m.rows])
+    tgt = np.array([float(r["target"]) for r in m.rows])
+    uniq = [i for i in range(len(inst)) if (inst == inst[i]).all(axis=1).sum() == 1]
+    X = inst[uniq]
+    s, v = c.score_matrix_oracle(X)
+    assert v.all()
+    np.testing.assert_array_equal(s, tgt[uniq])
+    for r in range(len(X)):
+        assert s[r] == _brute(c, X[r])
 
 
 def test_knn_targets_applied_by_oracle():
@@ -180,3 +213,31 @@ def test_knn_kernel_matches_oracle(gpu, case, variant):
     close = np.isclose(s[both], ref[both], rtol=1e-4, atol=1e-5)
     # fp32 distances may swap two neighbours the fp64 oracle ranks a hair apart
     assert close.mean() > 0.998, close.mean()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", ["valu", "mfma"])
+@pytest.mark.parametrize("classification,method", [(False, "weightedAverage"), (True, "weightedMajorityVote")])
+def test_knn_kernel_zero_distance_zero_threshold(gpu, variant, classification, method):
+    """The kernel applies the same pinned exact-match rule as the oracle (no NaN for d = 0)."""
+    from flink_jpmml_amd.runtime.plans import NotLowerable
+
+    doc = knn_pmml(n_instances=500, n_features=8, k=6, classification=classification, method=method, seed=4,
+                   threshold=0.0, quantum=0.25, metric="euclidean")
+    c = CompiledPmml.from_string(doc)
+    try:
+        plan = c.plan(gpu, knn_variant=variant)
+    except NotLowerable:
+        pytest.skip(f"{variant} does not lower this model")
+    m = c.model
+    inst = np.array([[float(r[f"c{j}"]) for j in range(8)] for r in m.rows], dtype=np.float32)
+    X = np.concatenate([inst, stream_matrix(2000, 8, seed=2)]).astype(np.float32)
+    s, v = plan.score(X)
+    s, v = s.cpu().numpy(), v.cpu().numpy()
+    ref, vref = c.score_matrix_oracle(X)
+    n0 = len(inst)
+    assert v[:n0].all() and vref[:n0].all()
+    np.testing.assert_allclose(s[:n0], ref[:n0], rtol=1e-5, atol=1e-6)  # the exact matches
+    both = v & vref
+    assert (v == vref).mean() > 0.999
+    assert np.isclose(s[both], ref[both], rtol=1e-4, atol=1e-5).mean() > 0.998
