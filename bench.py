@@ -86,6 +86,15 @@ def parse_args(argv=None):
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--no-numa", action="store_true", help="do not bind to the GPU's NUMA node")
     p.add_argument("--force-dist", action="store_true", help="form a 1-rank RCCL group at N=1 (exercise RCCL)")
+    p.add_argument("--models", type=int, default=1,
+                   help="> 1: dynamic serving of this many models (AddMessage control stream); every record "
+                        "names a random one (dictionary-encoded model_ids) and each pass is scored through "
+                        "ConnectedStreams.quick_evaluate's grouped device pass")
+    p.add_argument("--rehearse-cpu", action="store_true",
+                   help="run the exact DSL / sink / collective code on the CPU (host oracle scorer, gloo): a "
+                        "functional rehearsal of N ranks without GPUs -- its numbers are NOT a benchmark")
+    p.add_argument("--model-docs", type=int, default=8,
+                   help="--models mode: distinct synthetic PMML documents (seeds) the model ids cycle over")
     a = p.parse_args(argv)
     a.trees = a.trees or (500 if a.model == "rf" else 1000)
     a.depth = a.depth or (8 if a.model == "rf" else 6)
@@ -94,29 +103,32 @@ def parse_args(argv=None):
     return a
 
 
-def model_text(args) -> str:
+def model_text(args, seed=None) -> str:
     from flink_jpmml_amd.bench import synth
 
+    seed = args.seed if seed is None else seed
     if args.model == "gbdt":
-        return synth.gbdt_pmml(n_trees=args.trees, depth=args.depth, n_features=args.features, seed=args.seed)
+        return synth.gbdt_pmml(n_trees=args.trees, depth=args.depth, n_features=args.features, seed=seed)
     if args.model == "chain":
-        return synth.gbdt_pmml(n_trees=args.trees, depth=args.depth, n_features=args.features, seed=args.seed,
+        return synth.gbdt_pmml(n_trees=args.trees, depth=args.depth, n_features=args.features, seed=seed,
                                objective="binary")
     if args.model == "rf":
         return synth.random_forest_pmml(n_trees=args.trees, depth=args.depth, n_features=args.features,
-                                        n_classes=3, seed=args.seed)
-    return synth.mlp_pmml(n_features=args.features, hidden=(256, 256), n_out=1, seed=args.seed)
+                                        n_classes=3, seed=seed)
+    return synth.mlp_pmml(n_features=args.features, hidden=(256, 256), n_out=1, seed=seed)
 
 
 class _StepSource:
     """``--warmup + --steps`` RecordBatches (one per step) of this rank's pinned shard; calls
-    ``on_step(i)`` right before step i is handed to the pipeline (timer start hook)."""
+    ``on_step(i)`` right before step i is handed to the pipeline (timer start hook). ``model_ids``
+    (``--models`` mode): the per-row ``(codes, ids)`` column every batch carries."""
 
-    def __init__(self, X, n_steps, passes, on_step):
+    def __init__(self, X, n_steps, passes, on_step, model_ids=None):
         self.X = X
         self.n = n_steps
         self.passes = passes
         self.on_step = on_step
+        self.model_ids = model_ids
 
     def open_subtask(self, rank, world):  # parallel source: every rank scores its own shard
         pass
@@ -128,7 +140,7 @@ class _StepSource:
         for i in range(self.n):
             self.on_step(i)
             for p in range(self.passes):
-                yield RecordBatch(self.X, offset=(i * self.passes + p) * rows)
+                yield RecordBatch(self.X, model_ids=self.model_ids, offset=(i * self.passes + p) * rows)
 
 
 class _FileStepSource:
@@ -192,6 +204,27 @@ def _h2d_streams(pipe, args):
     return int(n) if n else (args.h2d_streams or None)
 
 
+def _kernel_ms(plan, Xh, device) -> float:
+    """Kernel-only time of one launch over the device-resident rows ``Xh`` (ms)."""
+    import torch
+
+    n_k = Xh.shape[0]
+    Xd = Xh.to(device)
+    sd = torch.empty(n_k, dtype=torch.float32, device=device)
+    vd = torch.empty(n_k, dtype=torch.uint8, device=device)
+    for _ in range(2):
+        plan.launch(Xd, sd, vd)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    kiters = 10
+    e0.record()
+    for _ in range(kiters):
+        plan.launch(Xd, sd, vd)
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / kiters
+
+
 def main(argv=None) -> int:
     args = parse_args(argv)
     import torch
@@ -206,11 +239,16 @@ def main(argv=None) -> int:
     from flink_jpmml_amd.runtime.loading import load_replicated
     from flink_jpmml_amd.utils.metrics import METRICS
 
-    if not torch.cuda.is_available():
+    cpu = bool(args.rehearse_cpu)
+    if not cpu and not torch.cuda.is_available():
         print(json.dumps({"metric": METRIC, "error": "no GPU visible"}))
         return 1
-    ctx = init_from_env(force=args.force_dist)
-    device = ctx.device
+    ctx = init_from_env(backend="gloo" if cpu else None, force=args.force_dist)
+    device = None if cpu else ctx.device
+
+    def sync():
+        if not cpu:
+            torch.cuda.synchronize()
     N = ctx.world_size
     if args.gpus != N and ctx.rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={N}; using {N}", file=sys.stderr)
@@ -226,12 +264,22 @@ def main(argv=None) -> int:
         with os.fdopen(fd, "w") as fh:
             fh.write(model_text(args))
     path = broadcast_object(path, ctx)
+    doc_paths = [path]
+    if args.models > 1:  # --models mode: more distinct documents (seeds) for the model ids to cycle over
+        extra = []
+        if ctx.rank == 0:
+            for k in range(1, max(1, min(args.model_docs, args.models))):
+                fd, pk = tempfile.mkstemp(suffix=".pmml", prefix=f"bench-{k}-")
+                with os.fdopen(fd, "w") as fh:
+                    fh.write(model_text(args, seed=args.seed + k))
+                extra.append(pk)
+        doc_paths += broadcast_object(extra, ctx)
     t_load = time.perf_counter()
     lm = load_replicated(path, ctx, device, cfg)
-    torch.cuda.synchronize()
+    sync()
     load_s = time.perf_counter() - t_load
     model = lm.model
-    plan = model.scorer.plan
+    plan = getattr(model.scorer, "plan", None)
 
     # ---- untimed correctness spot-check against the float64 oracle (rank 0)
     check = {}
@@ -249,17 +297,19 @@ def main(argv=None) -> int:
     # ---- this rank's synthetic record shard in pinned host memory, on the GPU's NUMA node
     from flink_jpmml_amd.utils.numa import bind_to_gpu_numa
 
-    numa_node = None if args.no_numa else bind_to_gpu_numa(device.index or 0)
-    X = torch.from_numpy(stream_matrix(args.rows, args.features, seed=1000 + ctx.rank)).pin_memory()
+    numa_node = None if args.no_numa or cpu else bind_to_gpu_numa(device.index or 0)
+    X = torch.from_numpy(stream_matrix(args.rows, args.features, seed=1000 + ctx.rank))
+    if not cpu:
+        X = X.pin_memory()
     # every distributed run all-gathers (a 1-rank RCCL group under --force-dist takes the same
     # device-mirror / RCCL path as N > 1)
     gather = ctx.is_distributed and not args.no_allgather
     timing = {}
 
     def barrier_sync():
-        torch.cuda.synchronize()
+        sync()
         ctx.barrier()
-        torch.cuda.synchronize()
+        sync()
 
     pipe = None
     job = {}
@@ -276,10 +326,21 @@ def main(argv=None) -> int:
         env = StreamExecutionEnvironment(config=cfg, dist_ctx=ctx if ctx.is_distributed else None)
         # the library F5 sink: waits for every scored batch; with N > 1 all-gathers the device
         # mirrors over RCCL on its comm stream, overlapping the next batch
-        sink = GatherSink(to="all", lockstep=True, keep=False) if gather or not ctx.is_distributed else _WaitSink()
+        sink = GatherSink(to="all", lockstep=True, keep=cpu) if gather or not ctx.is_distributed else _WaitSink()
         op_cfg = cfg.replace(device_mirror=gather)
+        model_ids = None
+        if args.models > 1:
+            if args.source != "synthetic":
+                raise SystemExit("--models needs --source synthetic")
+            uuids = [f"00000000-0000-4000-8000-{k:012d}" for k in range(args.models)]
+            rng = np.random.default_rng(2000 + ctx.rank)
+            codes = torch.from_numpy(rng.integers(0, args.models, args.rows).astype(
+                np.uint8 if args.models <= 256 else np.int16))
+            if not cpu:
+                codes = codes.pin_memory()
+            model_ids = (codes, [f"{u}_1" for u in uuids])
         if args.source == "synthetic":
-            src = _StepSource(X, args.warmup + args.steps, args.passes, on_step)
+            src = _StepSource(X, args.warmup + args.steps, args.passes, on_step, model_ids)
         else:
             from flink_jpmml_amd.stream.binary import BinaryBatchSource
             from flink_jpmml_amd.stream.sources import TextBatchSource
@@ -294,8 +355,18 @@ def main(argv=None) -> int:
                 make = lambda: TextBatchSource(src_path, text_model, batch_rows=args.micro_batch,  # noqa: E731
                                                threads=args.ingest_threads)
             src = _FileStepSource(make, args.warmup + args.steps, args.passes, on_step)
-        stream = env.add_source(src, mode="parallel")
-        scored = stream.quick_evaluate(ModelReader(path), config=op_cfg)
+        if args.models > 1:
+            from flink_jpmml_amd import AddMessage
+
+            # the control stream (replicated to every rank) registers the models; timestamps order
+            # it before the first batch in the deterministic input merge
+            adds = [AddMessage(u, 1, doc_paths[k % len(doc_paths)], 0) for k, u in enumerate(uuids)]
+            control = env.from_collection(adds, timestamp=lambda m: -1, uid="control")
+            stream = env.add_source(src, timestamp=lambda b: b.offset, mode="parallel")
+            scored = stream.with_support_stream(control).quick_evaluate(config=op_cfg, uid="serving")
+        else:
+            stream = env.add_source(src, mode="parallel")
+            scored = stream.quick_evaluate(ModelReader(path), config=op_cfg)
         scored.add_sink(sink)
         res = env.execute("bench")
         sink.finish()
@@ -304,9 +375,46 @@ def main(argv=None) -> int:
         job.update(records_in=res.records_in, elements_in=res.elements_in)
         seen = sink.rows_seen
         assert seen == (args.warmup + args.steps) * rows_per_step, (seen, rows_per_step)
-        assert res.records_in == seen
+        assert res.records_in == seen + (args.models if args.models > 1 else 0)  # + the AddMessages
+        if cpu and gather and args.models == 1:
+            # rehearsal: every rank checks every rank's gathered rows against that rank's oracle
+            from flink_jpmml_amd.parallel.dist import all_gather_object
+
+            compiled = CompiledPmml.from_string(open(path).read())
+            ok = True
+            gs, gv = sink.scores, sink.valid
+            n = args.rows
+            for r in range(N):
+                ref_s, ref_v = compiled.score_matrix_oracle(stream_matrix(args.rows, args.features, seed=1000 + r))
+                ref_s = ref_s.astype(np.float32)
+                for k in range(len(gs) // (N * n)):
+                    seg = slice(k * N * n + r * n, k * N * n + (r + 1) * n)
+                    ok = ok and bool((gv[seg] == ref_v).all()) and bool(np.array_equal(gs[seg][ref_v], ref_s[ref_v]))
+            job["rehearsal_gather_check"] = all_gather_object(bool(ok), ctx, group=ctx.group("ctrl"))
+            job["rehearsal_rows_gathered_per_rank"] = int(len(gs))
         op = scored.node.factory  # the operator instance this (single-subtask) rank ran
         pipe = getattr(getattr(op, "inner", op), "_pipeline", None)
+        if args.models > 1:
+            job["models_served"] = len(op.serving_models)
+            if ctx.rank == 0 and args.check_rows > 0:  # untimed: every model's rows vs its fp64 oracle
+                from flink_jpmml_amd.api.batch import RecordBatch as _RB
+
+                Xc = stream_matrix(args.check_rows, args.features, seed=99, missing_rate=0.02)
+                cc = np.random.default_rng(5).integers(0, args.models, args.check_rows)
+                pbm = op.score_mixed(_RB(Xc, model_ids=(cc.astype(np.int32), model_ids[1])))
+                oracles = [CompiledPmml.from_string(open(pth).read()) for pth in doc_paths]
+                errs, vm = [], True
+                for k in range(args.models):
+                    rows = np.flatnonzero(cc == k)
+                    if rows.size == 0:
+                        continue
+                    sr, vr = oracles[k % len(doc_paths)].score_matrix_oracle(Xc[rows])
+                    vm = vm and bool((pbm.valid[rows] == vr).all())
+                    both = vr & pbm.valid[rows]
+                    if both.any():
+                        errs.append(float(np.max(np.abs(pbm.scores[rows][both] - sr[both]))))
+                check["mixed_models"] = {"models": args.models, "rows": int(args.check_rows), "valid_match": vm,
+                                         "max_abs_err_vs_fp64": max(errs) if errs else None}
         if args.source != "synthetic":
             os.unlink(src_path)
     else:
@@ -326,7 +434,7 @@ def main(argv=None) -> int:
         barrier_sync()
         elapsed = time.perf_counter() - t0
     if ctx.is_distributed:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device if device is not None else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms_per_step = elapsed / args.steps * 1e3
@@ -334,25 +442,15 @@ def main(argv=None) -> int:
 
     # ---- device-resident kernel throughput (records already in HBM) — reported separately
     n_k = min(args.rows, 1 << 22)
-    Xd = X[:n_k].to(device)
-    sd = torch.empty(n_k, dtype=torch.float32, device=device)
-    vd = torch.empty(n_k, dtype=torch.uint8, device=device)
-    for _ in range(2):
-        plan.launch(Xd, sd, vd)
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    kiters = 10
-    e0.record()
-    for _ in range(kiters):
-        plan.launch(Xd, sd, vd)
-    e1.record()
-    torch.cuda.synchronize()
-    kernel_ms = e0.elapsed_time(e1) / kiters
+    kernel_ms = float("nan")
+    if not cpu:
+        kernel_ms = _kernel_ms(plan, X[:n_k], device)
 
     # ---- p50 latency: one small RecordBatch through model.predict (host records -> host scores)
     from flink_jpmml_amd.api.batch import RecordBatch
 
-    Xl = RecordBatch(torch.from_numpy(stream_matrix(args.latency_batch, args.features, seed=7)).pin_memory())
+    Xl = torch.from_numpy(stream_matrix(args.latency_batch, args.features, seed=7))
+    Xl = RecordBatch(Xl if cpu else Xl.pin_memory())
     lats = []
     for i in range(args.latency_iters + 5):
         t1 = time.perf_counter()
@@ -363,10 +461,15 @@ def main(argv=None) -> int:
     p99 = float(np.percentile(lats, 99))
 
     if ctx.rank == 0:
-        default = args.model == "gbdt" and args.source == "synthetic"
+        default = args.model == "gbdt" and args.source == "synthetic" and args.models == 1
         metric = METRIC if default else f"records/sec (whole node) on {MODELS[args.model][1]} PMML; p50 latency"
+        if args.models > 1:
+            metric = (f"records/sec (whole node), dynamic serving of {args.models} x {args.trees}-tree "
+                      f"{MODELS[args.model][1]} PMML models, every record names a random model")
         if args.source != "synthetic":
             metric += f" [source: {args.source} record file, end to end incl. ingest]"
+        if cpu:
+            metric = "[CPU REHEARSAL, not a benchmark] " + metric
         out = {
             "metric": metric,
             "value": records_per_s,
@@ -401,12 +504,14 @@ def main(argv=None) -> int:
                 "allgather_sink": gather,
                 "zero_copy_host_sink": bool(getattr(model.scorer, "direct", False)),
                 "numa_node": numa_node,
+                "models": args.models,
+                "model_docs": len(doc_paths),
             },
             "p50_latency_ms": p50,
             "p99_latency_ms": p99,
             "latency_batch_rows": args.latency_batch,
-            "kernel_only_records_per_s_per_gpu": n_k / (kernel_ms / 1e3),
-            "kernel_ms_per_1M_rows": kernel_ms * (1 << 20) / n_k,
+            "kernel_only_records_per_s_per_gpu": None if cpu else n_k / (kernel_ms / 1e3),
+            "kernel_ms_per_1M_rows": None if cpu else kernel_ms * (1 << 20) / n_k,
             "h2d_gbps_effective": rows_per_step * args.features * 4 * args.steps / elapsed / 1e9,
             "job": job,
             "model_load_broadcast_s": load_s,
@@ -414,13 +519,15 @@ def main(argv=None) -> int:
             "plan": {"layout": getattr(plan, "layout", None), "depth": getattr(plan, "depth", None),
                      "chunk_trees": getattr(plan, "chunk_trees", None), "kind": getattr(plan, "kind", None)},
             "check": check,
+            "rehearsal_cpu": cpu,
             "metrics": {k: v for k, v in METRICS.summary()["counters"].items() if not k.startswith("model_cache")},
         }
         print(json.dumps(out), flush=True)
-        try:
-            os.unlink(path)
-        except OSError:
-            pass
+        for pth in doc_paths:
+            try:
+                os.unlink(pth)
+            except OSError:
+                pass
     if ctx.is_distributed:
         dist.destroy_process_group()
     return 0

@@ -55,6 +55,11 @@ def _env(args) -> StreamExecutionEnvironment:
     return StreamExecutionEnvironment(args.parallelism, config=scoring_config(args))
 
 
+def _records(args) -> Optional[int]:
+    """``--records``: ``None`` (unbounded, the reference's default) for 0 or less."""
+    return args.records if args.records and args.records > 0 else None
+
+
 def _rate(args) -> Optional[float]:
     return args.rate if args.rate and args.rate > 0 else None
 
@@ -62,9 +67,10 @@ def _rate(args) -> Optional[float]:
 def quick_evaluate_kmeans(args) -> List:
     """X1 (`E/QuickEvaluateKmeans.scala:29-54`): Iris vectors → quick_evaluate → writeAsText."""
     env = _env(args)
-    vectors = env.add_source(IrisSource(None, n=args.records, rate=_rate(args), seed=args.seed)).map(
+    vectors = env.add_source(IrisSource(None, n=_records(args), rate=_rate(args), seed=args.seed)).map(
         lambda e: e.to_vector())
-    out = _sink(vectors.quick_evaluate(ModelReader(args.model), batch_size=args.batch_size, device=args.device), args)
+    out = _sink(vectors.quick_evaluate(ModelReader(args.model), batch_size=args.batch_size, device=args.device), args,
+                keep=_records(args) is not None)
     env.execute("Quick Evaluate Kmeans")
     return out
 
@@ -72,13 +78,14 @@ def quick_evaluate_kmeans(args) -> List:
 def evaluate_kmeans(args) -> List:
     """X2 (`E/EvaluateKmeans.scala:29-57`): full UDF with ``predict(vec, Some(0.0))``."""
     env = _env(args)
-    events = env.add_source(IrisSource(None, n=args.records, rate=_rate(args), seed=args.seed))
+    events = env.add_source(IrisSource(None, n=_records(args), rate=_rate(args), seed=args.seed))
 
     def udf(event, model):
         prediction = model.predict(event.to_vector(), 0.0)
         return event, prediction.value.get_or_else(-1.0)
 
-    out = _sink(events.evaluate(ModelReader(args.model), udf, batch_size=args.batch_size, device=args.device), args)
+    out = _sink(events.evaluate(ModelReader(args.model), udf, batch_size=args.batch_size, device=args.device), args,
+                keep=_records(args) is not None)
     env.execute("Evaluate Kmeans")
     return out
 
@@ -105,10 +112,10 @@ def dynamic_evaluate_kmeans(args) -> List:
     _enable_checkpointing(env, args)
     control = env.add_source(ControlSource(idp, args.gen_policy, n=args.control_messages,
                                            max_interval_ms=args.maxIntervalControlStream, seed=args.seed))
-    events = env.add_source(IrisSource(list(idp), n=args.records, rate=_rate(args), seed=args.seed))
+    events = env.add_source(IrisSource(list(idp), n=_records(args), rate=_rate(args), seed=args.seed))
     preds = events.with_support_stream(control).evaluate(_predict_udf, batch_size=args.batch_size,
                                                          device=args.device, uid="dynamic-kmeans")
-    out = _sink(preds, args, keep=args.records is not None)
+    out = _sink(preds, args, keep=_records(args) is not None)
     env.execute("Dynamic Clustering Example", restore=args.restore)
     return out
 
@@ -134,10 +141,10 @@ def checkpoint_evaluate(args) -> List:
         raise SystemExit("checkpoint: give --socket host:port or --control-file")
     control = lines.filter(lambda ln: bool(ln.strip())).map(
         lambda path: AddMessage(ids[rng.randrange(len(ids))], 1, path.strip(), now_ms()))
-    events = env.add_source(IrisSource(ids, n=args.records, rate=_rate(args), seed=args.seed))
+    events = env.add_source(IrisSource(ids, n=_records(args), rate=_rate(args), seed=args.seed))
     preds = events.with_support_stream(control).evaluate(_predict_udf, batch_size=args.batch_size,
                                                          device=args.device, uid="checkpoint-evaluate")
-    out = _sink(preds, args, keep=args.records is not None)
+    out = _sink(preds, args, keep=_records(args) is not None)
     env.execute("Checkpoint Evaluate Example", restore=args.restore)
     return out
 
@@ -148,7 +155,9 @@ def build_parser() -> argparse.ArgumentParser:
 
     def common(sp):
         sp.add_argument("--output", required=True)
-        sp.add_argument("--records", type=int, default=100)
+        sp.add_argument("--records", type=int, default=0,
+                        help="Iris records to emit; 0 (default) = unbounded, the job runs until cancelled like "
+                             "the reference's (IrisSource.scala:52)")
         sp.add_argument("--parallelism", type=int, default=1)
         sp.add_argument("--batch-size", type=int, default=None)
         sp.add_argument("--device", default=None)
@@ -174,7 +183,8 @@ def build_parser() -> argparse.ArgumentParser:
     sp.add_argument("--intervalCheckpoint", type=int, default=1000, help="checkpoint interval in ms (0 = off)")
     sp.add_argument("--maxIntervalControlStream", type=int, default=5000,
                     help="max random gap between control messages, ms (reference default 5000)")
-    sp.add_argument("--control-messages", type=int, default=None)
+    sp.add_argument("--control-messages", type=int, default=None,
+                    help="control messages to emit (default: unbounded; 10 when --records bounds the run)")
     sp.add_argument("--checkpoint-dir", default=None)
     sp.add_argument("--restore", default=None)
     common(sp)
@@ -192,8 +202,11 @@ def build_parser() -> argparse.ArgumentParser:
 
 def main(argv=None) -> int:
     args = build_parser().parse_args(argv)
-    if getattr(args, "cmd", None) == "dynamic" and args.gen_policy != "finite" and args.control_messages is None:
-        args.control_messages = 10  # bounded by default so the example terminates
+    if getattr(args, "cmd", None) == "dynamic" and args.gen_policy != "finite" and args.control_messages is None \
+            and _records(args) is not None:
+        # a bounded run (--records N) ends with its events: bound the loop / random control stream
+        # too. The default (unbounded events and control) runs until cancelled, like the reference.
+        args.control_messages = 10
     METRICS.reset()
     args.fn(args)
     if args.metrics_out:

@@ -23,7 +23,9 @@
 #define PY_ARRAY_UNIQUE_SYMBOL fja_fastpath_ARRAY_API
 #include <numpy/arrayobject.h>
 
+#include <cstdint>
 #include <cstring>
+#include <vector>
 
 PyObject *fja_scan_trees(PyObject *, PyObject *args);  // pmml_scan.cpp
 
@@ -133,7 +135,140 @@ PyObject *make_predictions(PyObject *, PyObject *args) {
     return list;
 }
 
+// group_ids(ids: list | ndarray[object]) -> (codes: int32[n], keys: list)
+// Dictionary-encodes a per-row model-id column in first-appearance order (the mixed-model batch of
+// the dynamic operator, `S/package.scala:111-114`, keyed by id string). Rows usually repeat a few
+// id objects: a 256-entry direct-mapped cache on the object pointer answers most rows without
+// hashing; misses fall back to a dict keyed by the (equal-comparing) id values.
+PyObject *group_ids(PyObject *, PyObject *args) {
+    PyObject *seq;
+    if (!PyArg_ParseTuple(args, "O", &seq)) return nullptr;
+    PyObject *fast = nullptr;
+    PyObject **items;
+    Py_ssize_t n;
+    if (PyArray_Check(seq)) {
+        PyArrayObject *a = reinterpret_cast<PyArrayObject *>(seq);
+        if (PyArray_TYPE(a) != NPY_OBJECT || PyArray_NDIM(a) != 1 || !PyArray_IS_C_CONTIGUOUS(a)) {
+            PyErr_SetString(PyExc_TypeError, "group_ids: a 1-D contiguous object array or a list");
+            return nullptr;
+        }
+        items = static_cast<PyObject **>(PyArray_DATA(a));
+        n = PyArray_DIM(a, 0);
+    } else {
+        fast = PySequence_Fast(seq, "group_ids: a sequence of ids");
+        if (!fast) return nullptr;
+        items = PySequence_Fast_ITEMS(fast);
+        n = PySequence_Fast_GET_SIZE(fast);
+    }
+    npy_intp dims[1] = {static_cast<npy_intp>(n)};
+    PyObject *codes_obj = PyArray_SimpleNew(1, dims, NPY_INT32);
+    PyObject *keys = PyList_New(0);
+    PyObject *index = PyDict_New();
+    if (!codes_obj || !keys || !index) {
+        Py_XDECREF(codes_obj);
+        Py_XDECREF(keys);
+        Py_XDECREF(index);
+        Py_XDECREF(fast);
+        return nullptr;
+    }
+    int32_t *codes = static_cast<int32_t *>(PyArray_DATA(reinterpret_cast<PyArrayObject *>(codes_obj)));
+    PyObject *cache_obj[256] = {nullptr};
+    int32_t cache_code[256];
+    bool ok = true;
+    for (Py_ssize_t i = 0; i < n; ++i) {
+        PyObject *o = items[i];
+        const size_t h = (reinterpret_cast<uintptr_t>(o) >> 4) & 255;
+        if (cache_obj[h] == o) {
+            codes[i] = cache_code[h];
+            continue;
+        }
+        PyObject *c = PyDict_GetItemWithError(index, o);  // borrowed
+        int32_t code;
+        if (c) {
+            code = static_cast<int32_t>(PyLong_AsLong(c));
+        } else {
+            if (PyErr_Occurred()) {
+                ok = false;
+                break;
+            }
+            code = static_cast<int32_t>(PyList_GET_SIZE(keys));
+            PyObject *v = PyLong_FromLong(code);
+            if (!v || PyDict_SetItem(index, o, v) < 0 || PyList_Append(keys, o) < 0) {
+                Py_XDECREF(v);
+                ok = false;
+                break;
+            }
+            Py_DECREF(v);
+        }
+        // the dict holds a reference to an equal key, and `items` keeps `o` alive for the loop
+        cache_obj[h] = o;
+        cache_code[h] = code;
+        codes[i] = code;
+    }
+    Py_DECREF(index);
+    Py_XDECREF(fast);
+    if (!ok) {
+        Py_DECREF(codes_obj);
+        Py_DECREF(keys);
+        return nullptr;
+    }
+    return Py_BuildValue("(NN)", codes_obj, keys);
+}
+
+// counting_sort(codes: int32[n], k: int) -> (perm: int32[n], counts: int64[k])
+// Stable grouping permutation: rows of code 0 first (in row order), then code 1, ... One pass to
+// count, one to place; the GIL is released. Codes outside [0, k) raise ValueError.
+PyObject *counting_sort(PyObject *, PyObject *args) {
+    PyObject *c_obj;
+    Py_ssize_t k;
+    if (!PyArg_ParseTuple(args, "On", &c_obj, &k)) return nullptr;
+    if (!PyArray_Check(c_obj)) {
+        PyErr_SetString(PyExc_TypeError, "counting_sort(int32 ndarray, int)");
+        return nullptr;
+    }
+    PyArrayObject *ca = reinterpret_cast<PyArrayObject *>(c_obj);
+    if (PyArray_TYPE(ca) != NPY_INT32 || PyArray_NDIM(ca) != 1 || !PyArray_IS_C_CONTIGUOUS(ca) || k < 0 ||
+        k > (1 << 24)) {
+        PyErr_SetString(PyExc_ValueError, "counting_sort: contiguous 1-D int32 codes and 0 <= k <= 2^24");
+        return nullptr;
+    }
+    const npy_intp n = PyArray_DIM(ca, 0);
+    npy_intp dn[1] = {n}, dk[1] = {static_cast<npy_intp>(k)};
+    PyObject *perm_obj = PyArray_SimpleNew(1, dn, NPY_INT32);
+    PyObject *cnt_obj = PyArray_ZEROS(1, dk, NPY_INT64, 0);
+    if (!perm_obj || !cnt_obj) {
+        Py_XDECREF(perm_obj);
+        Py_XDECREF(cnt_obj);
+        return nullptr;
+    }
+    const int32_t *codes = static_cast<const int32_t *>(PyArray_DATA(ca));
+    int32_t *perm = static_cast<int32_t *>(PyArray_DATA(reinterpret_cast<PyArrayObject *>(perm_obj)));
+    int64_t *cnt = static_cast<int64_t *>(PyArray_DATA(reinterpret_cast<PyArrayObject *>(cnt_obj)));
+    bool ok = n <= 0x7FFFFFFF;
+    Py_BEGIN_ALLOW_THREADS;
+    for (npy_intp i = 0; ok && i < n; ++i) {
+        const int32_t c = codes[i];
+        if (c < 0 || c >= k) ok = false;
+        else ++cnt[c];
+    }
+    if (ok) {
+        std::vector<int64_t> next(static_cast<size_t>(k) + 1, 0);
+        for (Py_ssize_t j = 0; j < k; ++j) next[j + 1] = next[j] + cnt[j];
+        for (npy_intp i = 0; i < n; ++i) perm[next[codes[i]]++] = static_cast<int32_t>(i);
+    }
+    Py_END_ALLOW_THREADS;
+    if (!ok) {
+        Py_DECREF(perm_obj);
+        Py_DECREF(cnt_obj);
+        PyErr_SetString(PyExc_ValueError, "counting_sort: code outside [0, k) or more than 2^31 rows");
+        return nullptr;
+    }
+    return Py_BuildValue("(NN)", perm_obj, cnt_obj);
+}
+
 PyMethodDef methods[] = {
+    {"group_ids", group_ids, METH_VARARGS, "Dictionary-encode a model-id column (first-appearance order)."},
+    {"counting_sort", counting_sort, METH_VARARGS, "Stable grouping permutation of int32 codes."},
     {"pack_dense", pack_dense, METH_VARARGS, "Pack a list of DenseVector objects into a float64 matrix."},
     {"make_predictions", make_predictions, METH_VARARGS, "Prediction objects for a scored batch."},
     {"scan_trees", fja_scan_trees, METH_VARARGS, "Streaming TreeModel reader: (skeleton, flat trees, strings)."},

@@ -141,6 +141,13 @@ class TreeArgs(ctypes.Structure):
                 ("prof", c_void_p)]
 
 
+class TextParseArgs(ctypes.Structure):
+    _fields_ = [("buf", c_void_p), ("n_bytes", ctypes.c_longlong), ("starts", c_void_p), ("n_rows", c_int),
+                ("n_cols", c_int), ("colmap", c_void_p), ("F", c_int), ("delim", ctypes.c_char), ("n_missing", c_int),
+                ("missing", c_void_p), ("X", c_void_p), ("flagged", c_void_p), ("max_flagged", c_int),
+                ("n_flagged", c_void_p)]
+
+
 class GenTreeArgs(ctypes.Structure):
     _fields_ = [("t", TreeArgs), ("nodes", c_void_p), ("children", c_void_p), ("preds", c_void_p),
                 ("pool", c_void_p), ("trees", c_void_p), ("max_steps", c_int), ("pad", c_int)]
@@ -220,6 +227,7 @@ class DeriveArgs(ctypes.Structure):
 
 
 _ABI = {
+    "pmml_textparse_args_size": TextParseArgs,
     "pmml_derive_args_size": DeriveArgs,
     "pmml_tree_args_size": TreeArgs,
     "pmml_tree_general_args_size": GenTreeArgs,
@@ -307,6 +315,20 @@ def load(auto_build: bool = True) -> ctypes.CDLL:
         lib.pmml_derive_launch.restype = c_int
         lib.pmml_mask_invalid.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int]
         lib.pmml_mask_invalid.restype = c_int
+        lib.pmml_tree_launch_many.argtypes = [c_void_p, c_void_p, c_void_p, c_int]
+        lib.pmml_tree_launch_many.restype = c_int
+        lib.pmml_text_rows_count.argtypes = [c_void_p, c_void_p, ctypes.c_longlong, c_void_p]
+        lib.pmml_text_rows_count.restype = c_int
+        lib.pmml_text_rows_write.argtypes = [c_void_p, c_void_p, ctypes.c_longlong, c_void_p, c_void_p]
+        lib.pmml_text_rows_write.restype = c_int
+        lib.pmml_text_parse.argtypes = [c_void_p, ctypes.POINTER(TextParseArgs)]
+        lib.pmml_text_parse.restype = c_int
+        lib.pmml_group_rows.argtypes = [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
+                                        c_void_p, c_void_p]
+        lib.pmml_group_rows.restype = c_int
+        lib.pmml_ungroup.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
+                                     c_void_p]
+        lib.pmml_ungroup.restype = c_int
         _lib = lib
         return lib
 

@@ -822,6 +822,18 @@ PMML_API int pmml_tree_launch(hipStream_t stream, const TreeArgs* args, int layo
   return 0;
 }
 
+// Many tree launches in one host call (mixed-model micro-batches, runtime/grouped.py): args[i] is a
+// complete argument block, meta[4 i ..] = {layout, depth, has_dr, splits}. Stops at the first
+// failing launch and returns (its index + 1) << 8 | (-its code).
+PMML_API int pmml_tree_launch_many(hipStream_t stream, const TreeArgs* args, const int* meta, int count) {
+  for (int i = 0; i < count; ++i) {
+    const int* m = meta + 4 * i;
+    const int rc = pmml_tree_launch(stream, args + i, m[0], m[1], m[2], m[3]);
+    if (rc != 0) return ((i + 1) << 8) | (-rc & 0xFF);
+  }
+  return 0;
+}
+
 PMML_API int pmml_tree_general_args_size() { return (int)sizeof(GenTreeArgs); }
 
 // GENERAL layout launch (one split; grid over rows only).

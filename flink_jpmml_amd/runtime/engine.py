@@ -140,7 +140,9 @@ class DevicePipeline:
 
         METRICS.observe("pipeline.h2d_calibration_gbps_1", mib * 1.048576e-3 / best[1])
         METRICS.observe("pipeline.h2d_calibration_gbps_2", mib * 1.048576e-3 / best[2])
-        METRICS.inc("pipeline.h2d_streams_chosen", choice)
+        # one observation per calibrated pipeline (a histogram, not a summed counter: the BENCH line
+        # reports the distribution, never "4 streams" from four pipelines choosing 1)
+        METRICS.observe("pipeline.h2d_streams_chosen", float(choice))
         return choice
 
     def host_dev_ptr(self, t):
@@ -398,8 +400,12 @@ class StreamingScorer:
                 if X.dtype != torch.float32 or not X.is_contiguous():
                     X = X.to(torch.float32).contiguous()
                 # device-resident input: the kernels on the compute stream must see the producer's
-                # writes (its current stream), and the allocator must not recycle X while they read
-                self.comp.wait_stream(torch.cuda.current_stream(self.device))
+                # writes (its ready event, else its current stream), and the allocator must not
+                # recycle X while they read
+                if getattr(batch, "ready", None) is not None:
+                    self.comp.wait_event(batch.ready)
+                else:
+                    self.comp.wait_stream(torch.cuda.current_stream(self.device))
                 X.record_stream(self.comp)
             elif not X.is_pinned() or X.dtype != torch.float32 or not X.is_contiguous():
                 X = _pin(X)

@@ -1695,6 +1695,33 @@ class TreePlan(DevicePlan):
         check(rc, f"tree kernel ({self.layout}, depth {self.depth})")
 
 
+    def batch_launch_args(self, x_ptr: int, n: int, n_feat: int, ldx: int, score_ptr: int, valid_ptr: int):
+        """``(TreeArgs, (layout, depth, has_dr, splits))`` of one launch over rows at ``x_ptr``,
+        for ``pmml_tree_launch_many`` (several models' launches from one host call), or ``None``
+        when this plan launches otherwise (hybrid / general layouts go through :meth:`launch`)."""
+        import torch
+
+        from ..ops._lib import TreeArgs, ptr
+
+        if self.layout not in ("perfect", "pointer") or n <= 0:
+            return None
+        s = self._auto_splits(n)
+        a = TreeArgs.from_buffer_copy(self._args_template(False))
+        a.X, a.n_rows, a.n_feat, a.ldx = x_ptr, n, n_feat, ldx
+        a.row_valid_in = None
+        a.score, a.valid, a.probs = score_ptr, valid_ptr, None
+        a.epi.score2, a.epi.valid2 = None, None
+        a.partial = None
+        a.xcd_split = 1 if getattr(self, "xcd_split", 0) and s > 1 else 0
+        if s > 1:
+            need = s * (self.C + 1) * n
+            if self._partial is None or self._partial.numel() < need:
+                if self._partial is not None:
+                    self.__dict__.setdefault("_retired", []).append(self._partial)
+                self._partial = torch.empty(max(need, 1 << 20), dtype=torch.float32, device=self.device)
+            a.partial = ptr(self._partial)
+        return a, (0 if self.layout == "perfect" else 1, int(self.depth), 1 if self.has_dr else 0, int(s))
+
     def _launch_general(self, X, score, valid, stream, probs, row_valid, score2, valid2) -> None:
         import ctypes
 

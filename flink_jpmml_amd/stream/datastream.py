@@ -604,6 +604,32 @@ class ConnectedStreams:
             out.node.uid = uid
         return out
 
+    def quick_evaluate(self, device: Any = None, cache_capacity: Optional[int] = None,
+                       plan_opts: Optional[dict] = None, uid: Optional[str] = None,
+                       config: Optional[ScoringConfig] = None) -> DataStream:
+        """Dynamic serving without a UDF — the multi-model counterpart of ``quickEvaluate``
+        (`S/package.scala:107-119,138-142`). Columnar events (RecordBatch with ``model_id`` or
+        per-row ``model_ids``) → ``(PredictionBatch, RecordBatch)`` with one prediction per row in
+        row order, however many models the batch mixes (grouped device pass,
+        :mod:`flink_jpmml_amd.runtime.grouped`); per-record events exposing ``to_vector()`` →
+        ``(Prediction, event)``."""
+        op = EvaluationCoFunction(_quick_event_udf, None, device, cache_capacity, plan_opts, config)
+        op.grouped = True
+        out = self.process(op, "quick_evaluate_co")
+        if uid:
+            out.node.uid = uid
+        return out
+
+    quickEvaluate = quick_evaluate  # noqa: N815
+
+
+def _quick_event_udf(event: Any, model: Any) -> Tuple[Any, Any]:
+    to_vector = getattr(event, "to_vector", None) or getattr(event, "toVector", None)
+    if to_vector is None:
+        raise TypeError(f"quick_evaluate on connected streams needs RecordBatch events or events with "
+                        f"to_vector(), got {type(event).__name__}")
+    return model.predict(to_vector()), event
+
 
 __all__ = ["CollectSink", "ConnectedStreams", "DataStream", "FileSink", "SimulatedFailure",
            "StreamExecutionEnvironment", "TextSink"]

@@ -599,6 +599,8 @@ class EvaluationCoFunction(CoProcessFunction, CheckpointedFunction, _ScoringMixi
         self._pending = collections.deque()
         self._restored_digests: Dict[ModelId, str] = {}
         self._by_str: Dict[str, PmmlModel] = {}
+        self.grouped = False  # quick mode: columnar batches -> (PredictionBatch, RecordBatch), any id mix
+        self._grouped_scorer = None
 
     @property
     def batch_size(self) -> Optional[int]:
@@ -701,7 +703,47 @@ class EvaluationCoFunction(CoProcessFunction, CheckpointedFunction, _ScoringMixi
         else:
             b.add_many(events, self._model_of_event, out)
 
+    def score_mixed(self, batch: RecordBatch) -> PredictionBatch:
+        """One row-order :class:`PredictionBatch` for a columnar batch whose rows may name different
+        models (``model_ids``): row ``i`` equals ``model_for(id_i).predict(batch.vector(i))``.
+        Device models are scored in one grouped pass (one H2D, device-side grouping, a launch per
+        model present: ``runtime/grouped.py``); anything else is split per model and merged."""
+        keep = self.config.device_mirror
+        if not batch.has_model_ids:
+            return self.model_for(batch.model_id).predict_records(batch, keep_device=keep)
+        codes, keys = batch.id_codes()
+        models = [self.model_for(k) for k in keys]  # WrongModelIdFormat fails the job (parity)
+        if len(models) == 1:
+            return models[0].predict_records(batch, keep_device=keep)
+        from ..runtime.engine import NullScorer
+        from ..runtime.grouped import GroupedScorer, NotGroupable, groupable
+
+        width = batch.n_features
+        scorers = [NullScorer(width) if m.is_empty or len(m.active_fields) != width else m.scorer for m in models]
+        pipe = self._pipe()
+        if pipe is not None and groupable(scorers, width) is None and \
+                all(getattr(sc, "pipe", pipe) is pipe for sc in scorers):
+            if self._grouped_scorer is None:
+                self._grouped_scorer = GroupedScorer(pipe, max_inflight=self.config.max_inflight)
+            try:
+                return self._grouped_scorer.submit(batch, codes, scorers, keep_device=keep)
+            except NotGroupable:  # pragma: no cover - groupable() checked the same conditions
+                pass
+        METRICS.inc("grouped.split_batches")
+        n = len(batch)
+        s = np.full(n, np.nan, dtype=np.float32)
+        v = np.zeros(n, dtype=bool)
+        for sub in batch.split_by_model():
+            pb = self.model_for(sub.model_id).predict_records(sub)
+            s[sub.row_index] = pb.scores
+            v[sub.row_index] = pb.valid
+        return PredictionBatch.from_arrays(s, v).masked(batch.size_ok())
+
     def process_element1(self, event: Any, ctx, out: Collector) -> None:
+        if isinstance(event, RecordBatch) and self.grouped:
+            with prange("evaluate.grouped"):
+                self._push((self.score_mixed(event), event), out)
+            return
         if isinstance(event, RecordBatch):
             for sub in event.split_by_model():
                 model = self.model_for(sub.model_id)

@@ -155,13 +155,24 @@ class TextBatchSource(SourceFunction):
     """Delimited text records → RecordBatches in pinned memory, parsed by the native multi-threaded
     C++ ingest (:class:`flink_jpmml_amd.native.RecordParser`) straight into the batch buffer.
     Columns are matched to the model's active fields by header name (``columns`` overrides the
-    header); categorical tokens get the model's PMML codes, missing tokens become NaN."""
+    header); categorical tokens get the model's PMML codes, missing tokens become NaN.
+
+    ``parse="device"`` (or ``"auto"`` on a GPU box, when every used field is numeric) moves the raw
+    bytes to the GPU and parses them there (:mod:`~flink_jpmml_amd.stream.device_text`): batches
+    are then device-resident, ``device_chunk_bytes`` of text each, bit-identical to the host
+    parser."""
 
     chunkable = False  # each batch is a large parse: hand it downstream as soon as it exists
 
     def __init__(self, path: str, model: Any, batch_rows: int = 1 << 16, delimiter: str = ",",
                  columns: Optional[Sequence[str]] = None, threads: int = 0, model_id: Optional[str] = None,
-                 chunk_bytes: int = 16 << 20, use_mmap: bool = True):
+                 chunk_bytes: int = 16 << 20, use_mmap: bool = True, parse: str = "auto", device: Any = None,
+                 device_chunk_bytes: int = 256 << 20):
+        if parse not in ("auto", "host", "device"):
+            raise ValueError(f"parse must be auto / host / device, not {parse!r}")
+        self.parse = parse
+        self.device = device
+        self.device_chunk_bytes = int(device_chunk_bytes)
         self.path = path
         self.model = model  # CompiledPmml, PmmlModel or ModelReader / path
         self.batch_rows = int(batch_rows)
@@ -192,6 +203,27 @@ class TextBatchSource(SourceFunction):
         rank, and no rank reads the others' lines."""
         self._rank, self._world = int(rank), int(world)
 
+    def _device_for_parse(self, compiled, cols):
+        """The GPU to parse on, or None (host parser)."""
+        if self.parse == "host":
+            return None
+        import torch
+
+        from .. import native
+        from .device_text import device_parse_supported
+
+        if not torch.cuda.is_available():
+            if self.parse == "device":
+                raise RuntimeError("TextBatchSource(parse='device') needs a GPU")
+            return None
+        why = device_parse_supported(compiled, cols, native.DEFAULT_MISSING)
+        if why is not None:
+            if self.parse == "device":
+                raise ValueError(f"TextBatchSource(parse='device'): {why}")
+            return None
+        dev = self.device if self.device is not None else f"cuda:{torch.cuda.current_device()}"
+        return torch.device(dev)
+
     def _line_start_at_or_after(self, fh, p: int, data_start: int) -> int:
         if p <= data_start:
             return data_start
@@ -213,10 +245,22 @@ class TextBatchSource(SourceFunction):
                 head = fh.readline()
                 data_start = len(head)
                 cols = [h.strip().strip('"') for h in head.decode(errors="replace").strip().split(self.delimiter)]
-            parser = native.RecordParser(compiled, cols, delimiter=self.delimiter, threads=self.threads)
             span = size - data_start
             lo = self._line_start_at_or_after(fh, data_start + span * self._rank // self._world, data_start)
             hi = self._line_start_at_or_after(fh, data_start + span * (self._rank + 1) // self._world, data_start)
+            dev = self._device_for_parse(compiled, cols)
+            if dev is not None:
+                from .device_text import DeviceTextReader
+
+                reader = DeviceTextReader(self.path, compiled, cols, lo, hi, dev, delimiter=self.delimiter,
+                                          chunk_bytes=self.device_chunk_bytes, threads=self.threads or 8,
+                                          model_id=self.model_id)
+                for b in reader:
+                    self.bytes_parsed = reader.bytes_read
+                    yield b
+                METRICS.inc("ingest.bytes_parsed", reader.bytes_read)
+                return
+            parser = native.RecordParser(compiled, cols, delimiter=self.delimiter, threads=self.threads)
             if hi > lo and self.use_mmap:
                 try:
                     mm = mmap.mmap(fh.fileno(), 0, access=mmap.ACCESS_READ)

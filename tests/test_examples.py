@@ -42,6 +42,8 @@ def test_reference_defaults():
     args = jobs.build_parser().parse_args(["dynamic", "--models", "a.xml", "--output", "-"])
     assert args.maxIntervalControlStream == 5000 and args.intervalCheckpoint == 1000 and args.rate == 1.0
     assert IrisSource(None, rate=1.0).live and ControlSource({}, "finite", max_interval_ms=5000).live
+    # unbounded by default: the jobs run until cancelled (`E/sources/IrisSource.scala:52`)
+    assert args.records == 0 and jobs._records(args) is None and args.control_messages is None
 
 
 def test_sources_policies():

@@ -258,7 +258,7 @@ assert batch.size_ok() is not None
 out = {}
 for lockstep in (False, True):
     sink = GatherSink(to="all", lockstep=lockstep).bind(ctx)
-    pbs = [model.predict(batch) for _ in range(3)]
+    pbs = [model.predict_records(batch, keep_device=True) for _ in range(3)]
     assert all(pb.device_out is not None for pb in pbs)
     # no host sync may happen while the device gather is issued
     calls = []
