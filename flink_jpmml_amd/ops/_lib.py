@@ -148,6 +148,16 @@ class TextParseArgs(ctypes.Structure):
                 ("n_flagged", c_void_p)]
 
 
+class SegArgs(ctypes.Structure):
+    _fields_ = [("X", c_void_p), ("n_rows", c_int), ("ldx", c_int), ("S", c_void_p), ("V", c_void_p),
+                ("P", c_void_p), ("coff", c_void_p), ("prog", c_void_p), ("pool", c_void_p), ("pc", c_void_p),
+                ("weights", c_void_p), ("remap", c_void_p), ("table", c_void_p), ("K", c_int), ("C", c_int),
+                ("method", c_int), ("classification", c_int), ("skip", c_int), ("tgt", c_int),
+                ("lo", ctypes.c_double), ("hi", ctypes.c_double), ("ta", ctypes.c_double), ("tb", ctypes.c_double),
+                ("dflt", ctypes.c_double), ("score", c_void_p), ("valid", c_void_p), ("score2", c_void_p),
+                ("valid2", c_void_p)]
+
+
 class GenTreeArgs(ctypes.Structure):
     _fields_ = [("t", TreeArgs), ("nodes", c_void_p), ("children", c_void_p), ("preds", c_void_p),
                 ("pool", c_void_p), ("trees", c_void_p), ("max_steps", c_int), ("pad", c_int)]
@@ -227,6 +237,7 @@ class DeriveArgs(ctypes.Structure):
 
 
 _ABI = {
+    "pmml_segment_args_size": SegArgs,
     "pmml_textparse_args_size": TextParseArgs,
     "pmml_derive_args_size": DeriveArgs,
     "pmml_tree_args_size": TreeArgs,
@@ -315,6 +326,8 @@ def load(auto_build: bool = True) -> ctypes.CDLL:
         lib.pmml_derive_launch.restype = c_int
         lib.pmml_mask_invalid.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int]
         lib.pmml_mask_invalid.restype = c_int
+        lib.pmml_segment_reduce.argtypes = [c_void_p, ctypes.POINTER(SegArgs)]
+        lib.pmml_segment_reduce.restype = c_int
         lib.pmml_tree_launch_many.argtypes = [c_void_p, c_void_p, c_void_p, c_int]
         lib.pmml_tree_launch_many.restype = c_int
         lib.pmml_text_rows_count.argtypes = [c_void_p, c_void_p, ctypes.c_longlong, c_void_p]

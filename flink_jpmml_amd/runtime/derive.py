@@ -569,6 +569,9 @@ def plan_field_layout(compiled, allow_alias: bool = True, allow_fold: bool = Fal
     if not defs:
         return FieldLayout(active, index, None)
     refs = referenced_fields(_model_of(compiled)) + list(members)
+    shadow = [r for r in refs if r in defs and r in index]
+    if shadow:  # a (local) derived field named like an input: the oracle's scope rules, not ours
+        raise NotLowerable(f"derived field(s) {shadow} shadow input fields")
     needed = [r for r in refs if r in defs and r not in index]
     if not needed:
         return FieldLayout(active, index, None)

@@ -69,11 +69,10 @@ def segmentable(ev, compiled) -> Optional[str]:
         return f"classification multipleModelMethod {method!r}"
     if ev.kind not in ("regression", "classification"):
         return f"{ev.kind} segmentation"
-    if ev.mm.local_transformations:
-        return "MiningModel LocalTransformations"
+    # MiningModel- and segment-level LocalTransformations are computed by the derive pass in front
+    # of this plan (runtime/derive.py::collect_derived walks the segments): the segment plans and
+    # predicates read them as columns of the augmented matrix
     for seg in ev.segments:
-        if seg.model.local_transformations:
-            return "segment LocalTransformations"
         why = _predicate_fields_ok(seg.predicate, compiled)
         if why:
             return why
@@ -207,6 +206,51 @@ def _index_outputs(plan) -> None:
         _index_outputs(inner)
 
 
+_SP = dict(END=0, TRUE=1, FALSE=2, CMP=3, ISMISS=4, NOTMISS=5, SET=6, AND=7, OR=8, XOR=9, SURR=10)
+_CMP = {"equal": 0, "notEqual": 1, "lessThan": 2, "lessOrEqual": 3, "greaterThan": 4, "greaterOrEqual": 5}
+_METHOD_CODE = {"selectFirst": 0, "sum": 1, "average": 2, "weightedAverage": 3, "max": 4, "min": 5, "median": 6,
+                "weightedMedian": 7, "majorityVote": 8, "weightedMajorityVote": 9}
+_PROB_CODE = {"average": 10, "weightedAverage": 11, "max": 12, "median": 13}
+SEG_MAXK = SEG_MAXC = 64  # ops/csrc/segment.hip
+
+
+def predicate_programs(progs) -> tuple:
+    """The compiled segment predicates as the reduction kernel's postfix programs:
+    ``(insns int32[m, 4], pool float64[p], starts int32[K])`` (``ops/csrc/segment.hip``)."""
+    insns: List[tuple] = []
+    pool: List[float] = []
+
+    def emit(prog) -> None:
+        tag = prog[0]
+        if tag == "T":
+            insns.append((_SP["TRUE"], 0, 0, 0))
+        elif tag == "F":
+            insns.append((_SP["FALSE"], 0, 0, 0))
+        elif tag == "M":
+            insns.append((_SP["ISMISS"] if prog[2] else _SP["NOTMISS"], prog[1], 0, 0))
+        elif tag == "S":
+            insns.append((_SP["CMP"] | (_CMP[prog[2]] << 8), prog[1], len(pool), 1))
+            pool.append(float(prog[3]))
+        elif tag == "I":
+            insns.append((_SP["SET"] | ((1 if prog[2] else 0) << 8), prog[1], len(pool), len(prog[3])))
+            pool.extend(float(v) for v in prog[3])
+        else:
+            if len(prog[2]) > 32:
+                raise NotLowerable("CompoundPredicate with more than 32 children")
+            for q in prog[2]:
+                emit(q)
+            insns.append(({"and": _SP["AND"], "or": _SP["OR"], "xor": _SP["XOR"], "surrogate": _SP["SURR"]}[prog[1]],
+                          len(prog[2]), 0, 0))
+
+    starts = []
+    for prog in progs:
+        starts.append(len(insns))
+        emit(prog)
+        insns.append((_SP["END"], 0, 0, 0))
+    return (np.array(insns, dtype=np.int32).reshape(-1, 4), np.array(pool or [0.0], dtype=np.float64),
+            np.array(starts, dtype=np.int32))
+
+
 class SegmentedPlan(DevicePlan):
     """Per-segment device plans + device predicates + tensor-op aggregation (module docstring)."""
 
@@ -261,6 +305,31 @@ class SegmentedPlan(DevicePlan):
         import torch
 
         self.remaps = [torch.tensor(r, dtype=torch.int64, device=self.device) for r in (self.remap_lists or [])]
+        # the fused reduction kernel's tables (ops/csrc/segment.hip); None -> tensor-op aggregation
+        self._red = None
+        probs = self.kind_ == "classification" and self.method in PROB_METHODS
+        code = _PROB_CODE[self.method] if probs else _METHOD_CODE.get(self.method)
+        if code is None or self.n_subs > SEG_MAXK or (self.categories and len(self.categories) > SEG_MAXC) or \
+                any(len(r) - 1 > SEG_MAXC for r in (self.remap_lists or [])):
+            return
+        try:
+            insns, pool, starts = predicate_programs(self.progs)
+        except NotLowerable:
+            return
+        rm = np.full((max(1, self.n_subs), SEG_MAXC + 1), -1, dtype=np.int32)
+        for i, r in enumerate(self.remap_lists or []):
+            rm[i, : len(r) - 1] = r[:-1]
+        widths = [len(r) - 1 for r in self.remap_lists] if probs else [0] * self.n_subs
+        coff = np.zeros(self.n_subs + 1, dtype=np.int64)
+        np.cumsum(widths, out=coff[1:])
+        dev = self.device
+        self._red = dict(code=code, probs=probs, widths=widths,
+                         prog=torch.from_numpy(insns.reshape(-1)).to(dev), pool=torch.from_numpy(pool).to(dev),
+                         pc=torch.from_numpy(starts).to(dev),
+                         weights=torch.tensor(self.weights, dtype=torch.float64, device=dev),
+                         remap=torch.from_numpy(rm.reshape(-1)).to(dev), coff=torch.from_numpy(coff).to(dev),
+                         coff_h=coff,
+                         table=self.table if self.table is not None else torch.zeros(1, device=dev))
 
     # replication: the container's scalars + every segment plan's state under "sub<i>/"
     def export_state(self):
@@ -288,6 +357,9 @@ class SegmentedPlan(DevicePlan):
     def launch(self, X, score, valid, stream=None, probs=None, score2=None, valid2=None, **kw) -> None:
         import torch
 
+        if self.device.type == "cuda" and getattr(self, "_red", None) is not None:
+            self._launch_fused(X, score, valid, stream, score2, valid2)
+            return
         n = X.shape[0]
         if self.device.type == "cuda":
             st = stream if stream is not None else torch.cuda.current_stream(self.device)
@@ -319,6 +391,51 @@ class SegmentedPlan(DevicePlan):
                 if so is not None and not isinstance(so, int):
                     so.copy_(s.to(so.dtype))
                     vo.copy_(v.to(torch.uint8))
+
+    def _launch_fused(self, X, score, valid, stream, score2, valid2) -> None:
+        """Segment plans, then ONE kernel for predicates + aggregation + target / label epilogue."""
+        import ctypes
+
+        import torch
+
+        from ..ops._lib import SegArgs, check, stream_handle
+        from .plans import _addr
+
+        n = X.shape[0]
+        if n == 0:
+            return
+        r = self._red
+        st = stream if stream is not None else torch.cuda.current_stream(self.device)
+        with torch.cuda.stream(st):
+            S = torch.empty((self.n_subs, n), dtype=torch.float32, device=self.device)
+            V = torch.empty((self.n_subs, n), dtype=torch.uint8, device=self.device)
+            P = torch.empty(max(1, int(r["coff_h"][-1]) * n), dtype=torch.float32, device=self.device) \
+                if r["probs"] else None
+            for i, plan in enumerate(self.subs):
+                kw = {}
+                if r["probs"]:
+                    a0, w = int(r["coff_h"][i]) * n, r["widths"][i]
+                    kw["probs"] = P[a0: a0 + n * w].view(n, w)
+                plan.launch(X, S[i], V[i], stream=st, **kw)
+            a = SegArgs()
+            a.X, a.n_rows, a.ldx = X.data_ptr(), n, X.stride(0)
+            a.S, a.V = S.data_ptr(), V.data_ptr()
+            a.P = P.data_ptr() if P is not None else None
+            a.coff, a.prog, a.pool, a.pc = (r["coff"].data_ptr(), r["prog"].data_ptr(), r["pool"].data_ptr(),
+                                            r["pc"].data_ptr())
+            a.weights, a.remap, a.table = r["weights"].data_ptr(), r["remap"].data_ptr(), r["table"].data_ptr()
+            a.K, a.C = self.n_subs, len(self.categories or [])
+            a.method, a.classification = r["code"], 1 if self.kind_ == "classification" else 0
+            a.skip = 1 if self.skip else 0
+            t = self.tgt
+            a.tgt = int(t["flags"]) if t else 0
+            if t:
+                a.lo, a.hi, a.ta, a.tb, a.dflt = t["lo"], t["hi"], t["ta"], t["tb"], t["dflt"]
+            else:
+                a.ta = 1.0
+            a.score, a.valid = _addr(score), _addr(valid)
+            a.score2, a.valid2 = _addr(score2), _addr(valid2)
+            check(self.lib.pmml_segment_reduce(stream_handle(st), ctypes.byref(a)), "segment reduce kernel")
 
     def _select(self, S, ok, T):
         import torch

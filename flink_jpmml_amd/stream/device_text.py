@@ -254,7 +254,8 @@ class DeviceTextReader:
                     if ring_ev[c.slot] is not None:
                         ring_ev[c.slot].synchronize()  # the H2D (and host patching) of its last use is over
                     c.pinned = ring[c.slot]
-                    self._read(fd, pool, lo, hi, c.pinned)
+                    with METRICS.timer("ingest.device_text_read_ms"):
+                        self._read(fd, pool, lo, hi, c.pinned)
                     n = hi - lo
                     if c.pinned[n - 1] != 10:  # the file's last line without a newline
                         c.pinned[n] = 10
@@ -266,10 +267,12 @@ class DeviceTextReader:
                     stage_b.append(c)
                 if stage_b and (len(stage_b) > 1 or i >= len(spans)):
                     c = stage_b.pop(0)
-                    self._submit_parse(c)
+                    with METRICS.timer("ingest.device_text_count_wait_ms"):
+                        self._submit_parse(c)
                     stage_c.append(c)
                 if stage_c and (len(stage_c) > 1 or i >= len(spans)):
-                    c = self._finish(stage_c.pop(0))
+                    with METRICS.timer("ingest.device_text_parse_wait_ms"):
+                        c = self._finish(stage_c.pop(0))
                     ring_ev[c.slot] = c.ev_parse
                     if c.rows:
                         rb = RecordBatch(c.X, model_id=self.model_id, offset=row)

@@ -45,3 +45,26 @@ def test_linear_segment_median_on_gpu(gpu):
                                                      linear_segment=True), missing=0.0)
     assert (v == vref).all() and v.all()
     np.testing.assert_allclose(s, ref, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("method", ["selectFirst", "max", "average", "median"])
+def test_local_transformations_segmented_on_gpu(gpu, method):
+    """MiningModel- and segment-level LocalTransformations: derive pass + SegmentedPlan on the GPU
+    against the oracle, ``fallback="error"``."""
+    from test_segmented import local_transform_segmented
+
+    from flink_jpmml_amd.bench.synth import stream_matrix
+    from flink_jpmml_amd.config import ScoringConfig
+    from flink_jpmml_amd.runtime.compiled import CompiledPmml
+    from flink_jpmml_amd.runtime.derive import DerivedPlan
+    from flink_jpmml_amd.runtime.segmented import SegmentedPlan
+
+    c = CompiledPmml.from_string(local_transform_segmented(method, seed=9))
+    plan = c.plan(gpu, **ScoringConfig(device=gpu, fallback="error").lowering_opts())
+    assert isinstance(plan, DerivedPlan) and isinstance(plan.inner, SegmentedPlan)
+    X = stream_matrix(50_000, c.n_features, seed=4, missing_rate=0.05)
+    s, v = plan.score(X)
+    s, v = s.cpu().numpy(), v.cpu().numpy().astype(bool)
+    ref, vref = c.score_matrix_oracle(X)
+    assert (v == vref).all() and v.any()
+    np.testing.assert_allclose(s[v], ref[v], rtol=1e-5, atol=1e-5)

@@ -98,3 +98,107 @@ def test_segmented_state_roundtrip():
         q = DevicePlan.from_state(meta, {k: t.clone() for k, t in tensors.items()}, torch.device("cpu"))
     assert isinstance(q, SegmentedPlan) and q.n_subs == plan.n_subs and q.progs == plan.progs
     assert [type(a).__name__ for a in q.subs] == [type(b).__name__ for b in plan.subs]
+
+
+def local_transform_segmented(method="selectFirst", classification=False, seed=7):
+    """A segmented MiningModel whose MiningModel-level LocalTransformations feed a segment
+    predicate and whose second segment computes its own split field."""
+    txt = segmented_pmml(method, classification, n_segments=4, seed=seed, predicates=True)
+    mm_local = ('<LocalTransformations><DerivedField name="d_scaled" optype="continuous" dataType="double">'
+                '<Apply function="+"><Apply function="*"><FieldRef field="f0"/><Constant>2.0</Constant></Apply>'
+                '<Constant>0.25</Constant></Apply></DerivedField></LocalTransformations>\n')
+    head, tail = txt.split("  <Segmentation", 1)
+    txt = head + "  " + mm_local + "  <Segmentation" + tail
+    # segment 1 selects on the MiningModel-level derived field
+    i = txt.index('<Segment id="1"')
+    j = txt.index(">", i) + 1
+    k = txt.index("\n", j)
+    txt = txt[:j] + '<SimplePredicate field="d_scaled" operator="lessThan" value="0.3"/>' + txt[k:]
+    # segment 2's tree splits on |f1| through its own LocalTransformations
+    i = txt.index('<Segment id="2"')
+    e = txt.index("</Segment>", i)
+    seg = txt[i:e]
+    tm = seg.index("<TreeModel")
+    ms_end = seg.index("</MiningSchema>", tm) + len("</MiningSchema>")
+    seg_local = ('<LocalTransformations><DerivedField name="s2_abs" optype="continuous" dataType="double">'
+                 '<Apply function="abs"><FieldRef field="f1"/></Apply></DerivedField></LocalTransformations>')
+    seg = seg[:ms_end] + seg_local + seg[ms_end:].replace('field="f1"', 'field="s2_abs"')
+    return txt[:i] + seg + txt[e:]
+
+
+@pytest.mark.parametrize("method", ["selectFirst", "max", "average"])
+def test_local_transformations_lower_to_derived_segmented_plan(method):
+    """Segment- and MiningModel-level LocalTransformations no longer force the host oracle: the
+    derive pass computes them and the SegmentedPlan reads them as columns."""
+    from flink_jpmml_amd.runtime.derive import DerivedPlan
+
+    c = CompiledPmml.from_string(local_transform_segmented(method))
+    with lowering_dry_run():
+        plan = compile_plan(c, torch.device("cpu"))
+    assert isinstance(plan, DerivedPlan) and isinstance(plan.inner, SegmentedPlan)
+    assert {"d_scaled", "s2_abs"} <= set(plan.program.derived)
+
+
+def _run_program(insns, pool, pc, X):
+    """numpy twin of segment.hip::seg_predicate (TRUE 1 / FALSE 0 / UNKNOWN 2 stack)."""
+    out = np.zeros(len(X), dtype=np.int64)
+    for r, x in enumerate(X.astype(np.float64)):
+        st = []
+        k = pc
+        while True:
+            op, a, b, c = insns[k]
+            code, arg = op & 0xFF, op >> 8
+            k += 1
+            if code == 0:
+                out[r] = st[-1]
+                break
+            if code >= 7:
+                vals = [st.pop() for _ in range(a)][::-1]
+                if code == 7:
+                    v = 0 if 0 in vals else (2 if 2 in vals else 1)
+                elif code == 8:
+                    v = 1 if 1 in vals else (2 if 2 in vals else 0)
+                elif code == 9:
+                    v = 2 if 2 in vals else sum(1 for q in vals if q == 1) % 2
+                else:
+                    known = [q for q in vals if q != 2]
+                    v = known[0] if known else 2
+            elif code == 1:
+                v = 1
+            elif code == 2:
+                v = 0
+            else:
+                xv = x[a]
+                miss = np.isnan(xv)
+                if code == 4:
+                    v = 1 if miss else 0
+                elif code == 5:
+                    v = 0 if miss else 1
+                elif miss:
+                    v = 2
+                elif code == 3:
+                    t = pool[b]
+                    v = int([xv == t, xv != t, xv < t, xv <= t, xv > t, xv >= t][arg])
+                else:
+                    inside = any(pool[b + i] == xv for i in range(c))
+                    v = int(inside == bool(arg))
+            st.append(v)
+    return out
+
+
+@pytest.mark.parametrize("seed", [7, 11, 21])
+def test_reduction_kernel_predicate_programs_match_device_predicates(seed):
+    """The fused reduction kernel's postfix predicate programs (three-valued logic) agree with the
+    tensor evaluation the CPU path uses, on every segment predicate shape the generator emits."""
+    from flink_jpmml_amd.runtime.segmented import compile_predicate, eval_predicate_device, predicate_programs
+
+    c = CompiledPmml.from_string(segmented_pmml("selectFirst", False, n_segments=10, seed=seed))
+    progs = [compile_predicate(s.predicate, c) for s in c.evaluator.segments]
+    insns, pool, starts = predicate_programs(progs)
+    X = stream_matrix(600, c.n_features, seed=seed, missing_rate=0.2).astype(np.float32)
+    Xt = torch.from_numpy(X)
+    for prog, pc in zip(progs, starts):
+        t, u = eval_predicate_device(prog, Xt)
+        want = np.where(u.numpy(), 2, t.numpy().astype(np.int64))
+        got = _run_program(insns.tolist(), pool, int(pc), X)
+        assert (got == want).all()
