@@ -326,6 +326,10 @@ def load(auto_build: bool = True) -> ctypes.CDLL:
         lib.pmml_derive_launch.restype = c_int
         lib.pmml_mask_invalid.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int]
         lib.pmml_mask_invalid.restype = c_int
+        lib.pmml_host_register.argtypes = [c_void_p, ctypes.c_size_t, ctypes.c_uint]
+        lib.pmml_host_register.restype = c_int
+        lib.pmml_host_unregister.argtypes = [c_void_p]
+        lib.pmml_host_unregister.restype = c_int
         lib.pmml_segment_reduce.argtypes = [c_void_p, ctypes.POINTER(SegArgs)]
         lib.pmml_segment_reduce.restype = c_int
         lib.pmml_tree_launch_many.argtypes = [c_void_p, c_void_p, c_void_p, c_int]

@@ -12,6 +12,15 @@ PMML_API int pmml_memcpy_async(void* dst, const void* src, size_t bytes, int kin
   return (int)hipMemcpyAsync(dst, src, bytes, (hipMemcpyKind)kind, stream);
 }
 
+// Page-lock an existing host range (e.g. a memory-mapped file in the page cache) so copy engines
+// DMA straight from it: flags = hipHostRegister* (ReadOnly for PROT_READ mappings). Returns a
+// hipError_t.
+PMML_API int pmml_host_register(void* p, size_t bytes, unsigned flags) {
+  return (int)hipHostRegister(p, bytes, flags);
+}
+
+PMML_API int pmml_host_unregister(void* p) { return (int)hipHostUnregister(p); }
+
 PMML_API int pmml_device_count() {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;

@@ -18,6 +18,8 @@
 //     those few lines with the exact host parser and patches the rows, so results are
 //     bit-identical to ingest.cpp for every input.
 
+#include <algorithm>
+
 #include "common.h"
 
 namespace {
@@ -200,47 +202,121 @@ __device__ bool fast_token(const uint8_t* p, const uint8_t* e, float* out) {
   return true;
 }
 
-__global__ __launch_bounds__(TP_TB) void parse_rows(TextParseArgs a) {
-  const int r = blockIdx.x * TP_TB + threadIdx.x;
-  if (r >= a.n_rows) return;
-  float* row = a.X + (size_t)r * a.F;
-  const float nan = __builtin_nanf("");
-  for (int c = 0; c < a.F; ++c) row[c] = nan;
-  const uint8_t* b = a.buf;
-  const uint8_t* p = b + a.starts[r];
-  const uint8_t* bend = b + a.n_bytes;
+// One record: the line starting at p (it ends at the next '\n' before bend). Field values land in
+// out[oc] (out pre-filled with NaN); returns true when a token needs the host parser. colmap and
+// missing may live in LDS or global memory, as may the line itself.
+__device__ __forceinline__ bool parse_record(const uint8_t* p, const uint8_t* bend, int n_cols, const int* colmap,
+                                             char delim, int n_missing, const char* missing, float* out) {
   // line end: the next '\n' (the chunk ends with one)
   const uint8_t* le = p;
   while (le < bend && *le != '\n') ++le;
   bool bad = false;
-  for (int c = 0; c < a.n_cols && p <= le; ++c) {
+  for (int c = 0; c < n_cols && p <= le; ++c) {
     const uint8_t* te = p;
-    while (te < le && *te != (uint8_t)a.delim) ++te;
-    const int oc = a.colmap[c];
+    while (te < le && *te != (uint8_t)delim) ++te;
+    const int oc = colmap[c];
     if (oc >= 0) {
       const uint8_t* s = p;
       const uint8_t* e = te;
       while (s < e && is_space(*s)) ++s;
       while (e > s && (is_space(e[-1]) || e[-1] == '\r')) --e;
-      bool missing = s == e;
-      for (int m = 0; !missing && m < a.n_missing; ++m) {
-        const char* tok = a.missing + m * TP_MISSING_LEN;
+      bool miss = s == e;
+      for (int m = 0; !miss && m < n_missing; ++m) {
+        const char* tok = missing + m * TP_MISSING_LEN;
         int k = 0;
         while (k < TP_MISSING_LEN && tok[k] && s + k < e && s[k] == (uint8_t)tok[k]) ++k;
-        missing = (k == TP_MISSING_LEN || !tok[k]) && s + k == e;
+        miss = (k == TP_MISSING_LEN || !tok[k]) && s + k == e;
       }
-      if (!missing) {
+      if (!miss) {
         float v;
-        if (fast_token(s, e, &v)) row[oc] = v;
+        if (fast_token(s, e, &v)) out[oc] = v;
         else bad = true;
       }
     }
     if (te >= le) break;
     p = te + 1;
   }
-  if (bad) {
-    const int k = atomicAdd(a.n_flagged, 1);
-    if (k < a.max_flagged) a.flagged[k] = r;
+  return bad;
+}
+
+__device__ __forceinline__ void flag_row(const TextParseArgs& a, int r) {
+  const int k = atomicAdd(a.n_flagged, 1);
+  if (k < a.max_flagged) a.flagged[k] = r;
+}
+
+// Global-memory variant: one lane per record reading its line byte by byte from HBM (every load
+// instruction touches 64 different lines). Kept for workgroups whose byte span exceeds the LDS
+// staging capacity of parse_rows_lds (very long lines).
+__global__ __launch_bounds__(TP_TB) void parse_rows(TextParseArgs a) {
+  const int r = blockIdx.x * TP_TB + threadIdx.x;
+  if (r >= a.n_rows) return;
+  float* row = a.X + (size_t)r * a.F;
+  const float nan = __builtin_nanf("");
+  for (int c = 0; c < a.F; ++c) row[c] = nan;
+  if (parse_record(a.buf + a.starts[r], a.buf + a.n_bytes, a.n_cols, a.colmap, a.delim, a.n_missing, a.missing, row))
+    flag_row(a, r);
+}
+
+// LDS-staged variant. The records of a workgroup are one contiguous byte span of the chunk
+// [starts[r0], starts[r0 + PR_TB]): the workgroup copies it into LDS with coalesced 16-byte loads,
+// every lane then parses its record out of LDS (byte reads at LDS latency, no per-byte TA
+// traffic), and the [PR_TB, F] result tile — contiguous in X — leaves with coalesced stores.
+// Output rows are padded to F + 1 floats in LDS so the per-lane column writes do not collide in
+// one bank. A span beyond `cap` bytes (lines much longer than the chunk's average) takes the
+// global-memory path for that workgroup.
+constexpr int PR_TB = 128;
+constexpr int PR_MAX_COLS = 256;
+
+__global__ __launch_bounds__(PR_TB) void parse_rows_lds(TextParseArgs a, int cap) {
+  extern __shared__ __align__(16) uint8_t lds[];
+  __shared__ int colmap_l[PR_MAX_COLS];
+  __shared__ char missing_l[TP_MAX_MISSING * TP_MISSING_LEN];
+  const int tid = threadIdx.x;
+  const int F = a.F, FP = a.F + 1;
+  float* out = reinterpret_cast<float*>(lds);
+  uint8_t* text = lds + (size_t)PR_TB * FP * 4;
+  const int r0 = blockIdx.x * PR_TB;
+  const int nr = min(PR_TB, a.n_rows - r0);
+  const long long s_lo = a.starts[r0];
+  const long long s_hi = r0 + nr < a.n_rows ? a.starts[r0 + nr] : a.n_bytes;
+  const long long a_lo = s_lo & ~15ll;
+  const long long span = s_hi - a_lo;
+  const float nan = __builtin_nanf("");
+  if (span > cap) {  // global-memory path for this workgroup
+    if (tid < nr) {
+      const int r = r0 + tid;
+      float* row = a.X + (size_t)r * F;
+      for (int c = 0; c < F; ++c) row[c] = nan;
+      if (parse_record(a.buf + a.starts[r], a.buf + a.n_bytes, a.n_cols, a.colmap, a.delim, a.n_missing, a.missing,
+                       row))
+        flag_row(a, r);
+    }
+    return;
+  }
+  for (int c = tid; c < a.n_cols; c += PR_TB) colmap_l[c] = a.colmap[c];
+  for (int i = tid; i < a.n_missing * TP_MISSING_LEN; i += PR_TB) missing_l[i] = a.missing[i];
+  for (int i = tid; i < PR_TB * FP; i += PR_TB) out[i] = nan;
+  // stage [a_lo, s_hi): whole 16-byte words inside the chunk, the tail byte by byte
+  const long long full_end = min(s_hi + 15, a.n_bytes) & ~15ll;  // 16-byte words fully inside the chunk
+  const int n16 = (int)((full_end - a_lo) >> 4);
+  const uint4* src = reinterpret_cast<const uint4*>(a.buf + a_lo);
+  uint4* dst = reinterpret_cast<uint4*>(text);
+  for (int i = tid; i < n16; i += PR_TB) dst[i] = src[i];
+  for (long long p = full_end + tid; p < s_hi; p += PR_TB) text[p - a_lo] = a.buf[p];
+  __syncthreads();
+  if (tid < nr) {
+    const int r = r0 + tid;
+    if (parse_record(text + (a.starts[r] - a_lo), text + span, a.n_cols, colmap_l, a.delim, a.n_missing, missing_l,
+                     out + tid * FP))
+      flag_row(a, r);
+  }
+  __syncthreads();
+  // the tile is X[r0 : r0 + nr] — one contiguous run of nr * F floats
+  float* xo = a.X + (size_t)r0 * F;
+  const int total = nr * F;
+  for (int i = tid; i < total; i += PR_TB) {
+    const int rr = i / F;
+    xo[i] = out[rr * FP + (i - rr * F)];
   }
 }
 
@@ -273,6 +349,26 @@ PMML_API int pmml_text_parse(hipStream_t stream, const TextParseArgs* args) {
   const TextParseArgs& a = *args;
   if (a.n_rows <= 0) return 0;
   if (a.F < 1 || a.n_cols < 1 || a.n_missing < 0 || a.n_missing > TP_MAX_MISSING) return -2;
-  hipLaunchKernelGGL(parse_rows, dim3((a.n_rows + TP_TB - 1) / TP_TB), dim3(TP_TB), 0, stream, a);
+  // LDS staging capacity: 1.25x the chunk's average bytes per workgroup (so two workgroups share a
+  // CU for 32-field rows); a workgroup over it parses from global memory.
+  const long long avg = a.n_bytes / a.n_rows + 1;
+  const long long out_bytes = (long long)PR_TB * (a.F + 1) * 4;
+  long long cap = ((avg * PR_TB * 5 / 4 + 256) + 15) & ~15ll;
+  cap = std::max(cap, 4096ll);
+  const long long lds_max = 160 * 1024 - 2048;  // minus the static tables
+  const bool lds_ok = a.n_cols <= PR_MAX_COLS && ((reinterpret_cast<uintptr_t>(a.buf) & 15) == 0) &&
+                      out_bytes + 4096 + 16 <= lds_max;
+  if (!lds_ok) {
+    hipLaunchKernelGGL(parse_rows, dim3((a.n_rows + TP_TB - 1) / TP_TB), dim3(TP_TB), 0, stream, a);
+    return hipGetLastError() == hipSuccess ? 0 : -7;
+  }
+  cap = std::min(cap, lds_max - out_bytes - 16);
+  const size_t lds = (size_t)(out_bytes + cap + 16);
+  if (lds > 65536) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(parse_rows_lds),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return (int)e;
+  }
+  hipLaunchKernelGGL(parse_rows_lds, dim3((a.n_rows + PR_TB - 1) / PR_TB), dim3(PR_TB), lds, stream, a, (int)cap);
   return hipGetLastError() == hipSuccess ? 0 : -7;
 }

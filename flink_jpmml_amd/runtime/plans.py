@@ -1747,8 +1747,14 @@ def _segmented_plan(compiled, device, fused_error: Exception, opts: dict) -> Dev
     """A MiningModel the fused ensemble kernels refuse: per-segment plans + device predicates
     (runtime/segmented.py), behind a prepare-only derive pass when the inputs need MiningField
     treatment (segment plans and predicates read prepared columns, as the oracle's do)."""
-    from .segmented import SegmentedPlan, segmentable
+    from .segmented import ChainPlan, SegmentedPlan, segmentable
 
+    ev = compiled.evaluator
+    if getattr(ev, "method", None) == "modelChain":  # general chains: segment outputs feed later segments
+        try:
+            return _with_prepared_inputs(compiled, device, lambda c: ChainPlan(c, device, **opts), opts)
+        except NotLowerable as e:
+            raise NotLowerable(f"{fused_error}; modelChain: {e}") from e
     why = segmentable(compiled.evaluator, compiled)
     if why:
         raise NotLowerable(f"{fused_error}; segmentation: {why}") from fused_error

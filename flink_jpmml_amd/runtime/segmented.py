@@ -549,6 +549,141 @@ class SegmentedPlan(DevicePlan):
         return s, v & ~torch.isnan(s)
 
 
+class ChainView(SubView):
+    """A chain segment's model over its own MiningSchema's active fields, which may include the
+    Output fields of earlier segments (columns of the chain's augmented matrix)."""
+
+    def __init__(self, parent, evaluator, columns: List[str]):
+        super().__init__(parent, evaluator)
+        self.active_fields = list(columns)
+        self.field_index = {c: j for j, c in enumerate(columns)}
+
+    @property
+    def n_features(self) -> int:
+        return len(self.active_fields)
+
+
+_CHAIN_OUT = ("predictedValue", "transformedValue", "probability")
+
+
+class ChainPlan(DevicePlan):
+    """``multipleModelMethod="modelChain"`` beyond the fused tree → calibrator form: the segments
+    run in document order on an augmented device matrix ``[inputs | chain outputs]``; each
+    segment's Output fields (predictedValue, transformedValue without an expression, probability
+    of a class) are written into their columns where its predicate is TRUE (NaN elsewhere, as the
+    oracle hides them), later segments read them like inputs, and every row takes the result of
+    the LAST segment whose predicate is TRUE (`models/mining.py::MiningEvaluator._select`)."""
+
+    kind = "chain"
+    supports_direct = False
+
+    def __init__(self, compiled, device, **opts):
+        from .plans import compile_plan
+
+        super().__init__(compiled, device)
+        ev = compiled.evaluator
+        if not isinstance(ev, MiningEvaluator) or ev.method != "modelChain":
+            raise NotLowerable("not a modelChain")
+        if self.prep is not None:
+            raise NotLowerable("chain plans read prepared inputs (compile_plan adds the prepare pass)")
+        base = list(compiled.active_fields)
+        self.n_base = len(base)
+        self.outs = []  # (segment, column, feature, class position or -1)
+        names = list(base)
+        for i, (seg, sub) in enumerate(zip(ev.segments, ev.sub)):
+            for of in sub.model.output:
+                if of.feature not in _CHAIN_OUT or (of.feature == "transformedValue" and of.expression is not None):
+                    raise NotLowerable(f"chain output {of.name!r}: feature {of.feature!r} is host-only")
+                if of.name in names:
+                    raise NotLowerable(f"chain output {of.name!r} shadows a field")
+                pos = -1
+                if of.feature == "probability":
+                    cats = getattr(sub, "categories", None) or []
+                    if of.value is None or of.value not in cats:
+                        raise NotLowerable(f"chain output {of.name!r}: probability of an unknown class")
+                    pos = cats.index(of.value)
+                elif sub.kind == "classification" and compiled.schema.is_string(of.name):
+                    raise NotLowerable(f"chain output {of.name!r}: string-typed predicted label")
+                self.outs.append((i, len(names), of.feature, pos))
+                names.append(of.name)
+        self.columns = names
+        col = {c: j for j, c in enumerate(names)}
+        self.progs = [compile_predicate(s.predicate, _Cols(compiled, col)) for s in ev.segments]
+        self.subs, self.cols, self.need_probs = [], [], []
+        for i, (seg, sub) in enumerate(zip(ev.segments, ev.sub)):
+            used = [f.name for f in sub.model.mining_schema.active]
+            missing = [f for f in used if f not in col]
+            if missing:
+                raise NotLowerable(f"chain segment {seg.id!r} reads unknown fields {missing}")
+            try:
+                plan = compile_plan(ChainView(compiled, sub, used), device, **dict(opts))
+            except NotLowerable as e:
+                raise NotLowerable(f"chain segment {seg.id!r}: {e}") from e
+            want = any(o[0] == i and o[2] == "probability" for o in self.outs)
+            if want and probs_width(plan) != len(sub.categories):
+                raise NotLowerable(f"chain segment {seg.id!r}: {type(plan).__name__} does not expose probabilities")
+            self.subs.append(plan)
+            self.cols.append([col[f] for f in used])
+            self.need_probs.append(len(sub.categories) if want else 0)
+        self.kind_ = ev.kind
+        final = ev.sub[-1]
+        self.tgt = target_post(ev.target, force=True) if ev.kind == "regression" and ev.target is not None else None
+        self.final_labels = None
+        if ev.kind == "classification":
+            self.final_labels = self._t(_label_table(list(final.categories)))
+        self._col_idx = [self._t(np.array(c, dtype=np.int64)) for c in self.cols]
+
+    def launch(self, X, score, valid, stream=None, probs=None, score2=None, valid2=None, **kw) -> None:
+        import torch
+
+        n = X.shape[0]
+        if n == 0:
+            return
+        st = stream if stream is not None and self.device.type == "cuda" else None
+        ctx = torch.cuda.stream(st) if st is not None else contextlib.nullcontext()
+        with ctx:
+            Xa = torch.full((n, len(self.columns)), float("nan"), dtype=torch.float32, device=self.device)
+            Xa[:, : self.n_base] = X[:, : self.n_base]
+            best_s = torch.full((n,), float("nan"), dtype=torch.float64, device=self.device)
+            best_v = torch.zeros(n, dtype=torch.bool, device=self.device)
+            for i, plan in enumerate(self.subs):
+                Xi = Xa.index_select(1, self._col_idx[i]).contiguous()
+                s = torch.empty(n, dtype=torch.float32, device=self.device)
+                v = torch.empty(n, dtype=torch.uint8, device=self.device)
+                pr = None
+                if self.need_probs[i]:
+                    pr = torch.full((n, self.need_probs[i]), float("nan"), dtype=torch.float32, device=self.device)
+                plan.launch(Xi, s, v, stream=st, **({"probs": pr} if pr is not None else {}))
+                t = eval_predicate_device(self.progs[i], Xa)[0]
+                ok = v.bool() & ~torch.isnan(s)
+                for seg, c, feat, pos in self.outs:
+                    if seg != i:
+                        continue
+                    val = pr[:, pos] if feat == "probability" else s
+                    Xa[:, c] = torch.where(t & ok, val, torch.full_like(val, float("nan")))
+                best_s = torch.where(t, s.double(), best_s)  # the last applicable segment wins
+                best_v = torch.where(t, ok, best_v)
+            if self.kind_ == "classification":
+                best_v = best_v & torch.isin(best_s.float(), self.final_labels)
+            else:
+                best_v = best_v & torch.isfinite(best_s)
+                best_s, best_v = apply_target_torch(best_s, best_v, self.tgt)
+            out = torch.where(best_v, best_s, torch.full_like(best_s, float("nan")))
+            for so, vo in ((score, valid), (score2, valid2)):
+                if so is not None and not isinstance(so, int):
+                    so.copy_(out.to(so.dtype))
+                    vo.copy_(best_v.to(torch.uint8))
+
+
+class _Cols:
+    """compile_predicate's view of the chain's augmented columns."""
+
+    def __init__(self, compiled, index):
+        self.field_index = index
+        self.active_fields = list(index)
+        self.schema = compiled.schema
+
+
 def _median0(A):
     """``numpy.nanmedian`` along dim 0 (mean of the two middle values; NaN where nothing is left)."""
     import torch
@@ -561,4 +696,4 @@ def _median0(A):
     return torch.where(cnt > 0, (lo + hi) / 2, torch.full_like(lo, float("nan")))
 
 
-__all__ = ["SegmentedPlan", "SubView", "probs_width", "segmentable"]
+__all__ = ["ChainPlan", "ChainView", "SegmentedPlan", "SubView", "probs_width", "segmentable"]

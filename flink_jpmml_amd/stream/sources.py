@@ -167,7 +167,7 @@ class TextBatchSource(SourceFunction):
     def __init__(self, path: str, model: Any, batch_rows: int = 1 << 16, delimiter: str = ",",
                  columns: Optional[Sequence[str]] = None, threads: int = 0, model_id: Optional[str] = None,
                  chunk_bytes: int = 16 << 20, use_mmap: bool = True, parse: str = "auto", device: Any = None,
-                 device_chunk_bytes: int = 256 << 20):
+                 device_chunk_bytes: int = 64 << 20):
         if parse not in ("auto", "host", "device"):
             raise ValueError(f"parse must be auto / host / device, not {parse!r}")
         self.parse = parse

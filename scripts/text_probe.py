@@ -34,21 +34,26 @@ def main():
     with open(path, "rb") as fh:
         lo = len(fh.readline())
     out = {"bytes": size, "rows": rows}
-    for threads in (8, 16):
-        for chunk in (64 << 20, 256 << 20):
-            r = DeviceTextReader(path, model, cols, lo, size, torch.device("cuda"), chunk_bytes=chunk, threads=threads)
-            for rep in range(2):
-                torch.cuda.synchronize()
-                t0 = time.perf_counter()
-                n = 0
-                for b in r:
-                    n += len(b)
-                torch.cuda.synchronize()
-                dt = time.perf_counter() - t0
-            out[f"t{threads}_c{chunk >> 20}M"] = {"rows": n, "s": dt, "rows_per_s": n / dt, "GBps": (size - lo) / dt / 1e9,
-                                                   "timers": {k: v for k, v in METRICS.summary().get("histograms", {}).items()
-                                                              if k.startswith("ingest.")}}
-            METRICS.reset()
+    configs = [(16, 64 << 20, False), (16, 256 << 20, False), (8, 64 << 20, True), (8, 128 << 20, True),
+               (8, 256 << 20, True)]
+    for threads, chunk, zc in configs:
+        r = DeviceTextReader(path, model, cols, lo, size, torch.device("cuda"), chunk_bytes=chunk, threads=threads,
+                             zero_copy=zc)
+        first = None
+        for rep in range(3):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            n = 0
+            for b in r:
+                n += len(b)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            first = dt if first is None else first
+        out[f"t{threads}_c{chunk >> 20}M_zc{int(zc)}"] = {
+            "rows": n, "s": dt, "first_s": first, "zero_copy_active": getattr(r, "zero_copy_active", False),
+            "rows_per_s": n / dt, "GBps": (size - lo) / dt / 1e9,
+            "timers": {k: v for k, v in METRICS.summary().get("histograms", {}).items() if k.startswith("ingest.")}}
+        METRICS.reset()
     # host read alone (pinned), 16 threads
     from concurrent.futures import ThreadPoolExecutor
 

@@ -68,3 +68,24 @@ def test_local_transformations_segmented_on_gpu(gpu, method):
     ref, vref = c.score_matrix_oracle(X)
     assert (v == vref).all() and v.any()
     np.testing.assert_allclose(s[v], ref[v], rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("classification", [False, True])
+def test_general_model_chain_on_gpu(gpu, classification):
+    """modelChain with segment outputs (predictedValue / class probability) feeding later segments
+    under segment predicates: ChainPlan on the GPU against the oracle, ``fallback="error"``."""
+    from test_segmented import general_chain_pmml
+
+    from flink_jpmml_amd.bench.synth import stream_matrix
+    from flink_jpmml_amd.config import ScoringConfig
+    from flink_jpmml_amd.runtime.compiled import CompiledPmml
+
+    c = CompiledPmml.from_string(general_chain_pmml(classification))
+    plan = c.plan(gpu, **ScoringConfig(device=gpu, fallback="error").lowering_opts())
+    assert type(plan).__name__ in ("ChainPlan", "DerivedPlan")
+    X = stream_matrix(40_000, 4, seed=6, missing_rate=0.05)
+    s, v = plan.score(X)
+    s, v = s.cpu().numpy(), v.cpu().numpy().astype(bool)
+    ref, vref = c.score_matrix_oracle(X)
+    assert (v == vref).all() and v.any()
+    np.testing.assert_allclose(s[v], ref[v], rtol=1e-5, atol=1e-5)

@@ -113,3 +113,32 @@ def test_device_text_scores_like_host_text(gpu, tmp_path):
         out[mode] = (np.concatenate([p.scores for p, _ in res]), np.concatenate([p.valid for p, _ in res]))
     assert (out["host"][1] == out["device"][1]).all()
     np.testing.assert_array_equal(out["host"][0][out["host"][1]], out["device"][0][out["device"][1]])
+
+
+@pytest.mark.parametrize("chunk", [1 << 14, 1 << 26])
+def test_zero_copy_mapping_equals_staged_reads(gpu, tmp_path, chunk):
+    """The registered-mapping path (DMA straight from the page cache) yields the same batches as
+    positional reads into the pinned ring, including the last line without a newline."""
+    import torch
+
+    from flink_jpmml_amd.stream.device_text import DeviceTextReader, _mapped, release_mapped
+
+    rng = np.random.default_rng(7)
+    path = _write_csv(tmp_path / "zc.csv", rng)
+    model = CompiledPmml.from_string(synth.gbdt_pmml(n_trees=4, depth=3, n_features=4, seed=1))
+    cols = path.read_bytes().split(b"\n", 1)[0].decode().split(",")
+    lo = len(path.read_bytes().split(b"\n", 1)[0]) + 1
+    size = path.stat().st_size
+    got = {}
+    for zc in (False, True):
+        r = DeviceTextReader(str(path), model, cols, lo, size, gpu, chunk_bytes=chunk, zero_copy=zc)
+        mats = [b.X for b in r]
+        torch.cuda.synchronize()
+        got[zc] = torch.cat(mats).cpu().numpy()
+        if zc:
+            assert r.zero_copy_active == (_mapped(str(path), r.lib) is not None)
+    release_mapped()
+    a, b = got[False], got[True]
+    assert a.shape == b.shape and a.shape[0] > 4000
+    assert np.array_equal(np.isnan(a), np.isnan(b))
+    assert np.array_equal(a[~np.isnan(a)].view(np.uint32), b[~np.isnan(b)].view(np.uint32))

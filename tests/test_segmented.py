@@ -202,3 +202,76 @@ def test_reduction_kernel_predicate_programs_match_device_predicates(seed):
         want = np.where(u.numpy(), 2, t.numpy().astype(np.int64))
         got = _run_program(insns.tolist(), pool, int(pc), X)
         assert (got == want).all()
+
+
+NS44 = "http://www.dmg.org/PMML-4_4"
+
+
+def general_chain_pmml(classification: bool = False) -> str:
+    """modelChain beyond tree -> calibrator: a tree whose predictedValue (or class probability)
+    feeds a linear model under a segment predicate, whose output a final tree splits on."""
+    fields = "".join(f'<DataField name="f{j}" optype="continuous" dataType="double"/>' for j in range(4))
+    tgt = ('<DataField name="y" optype="categorical" dataType="string"><Value value="1"/><Value value="2"/>'
+           '<Value value="3"/></DataField>') if classification else \
+        '<DataField name="y" optype="continuous" dataType="double"/>'
+    ms = '<MiningSchema><MiningField name="y" usageType="target"/>' + \
+        "".join(f'<MiningField name="f{j}"/>' for j in range(4)) + "</MiningSchema>"
+
+    def node(i, f, t, a, b):
+        return (f'<Node id="{i}"><True/><Node id="{i}a" score="{a}"><SimplePredicate field="{f}" operator="lessThan" '
+                f'value="{t}"/></Node><Node id="{i}b" score="{b}"><SimplePredicate field="{f}" '
+                f'operator="greaterOrEqual" value="{t}"/></Node></Node>')
+
+    if classification:
+        seg1 = ('<Segment id="1"><True/><TreeModel functionName="classification" splitCharacteristic="binarySplit">'
+                + ms + '<Output><OutputField name="p_a" optype="continuous" dataType="double" feature="probability" '
+                'value="1"/></Output><Node id="r"><True/><Node id="l" score="1"><SimplePredicate field="f0" '
+                'operator="lessThan" value="0.1"/><ScoreDistribution value="1" recordCount="7"/>'
+                '<ScoreDistribution value="2" recordCount="3"/></Node><Node id="g" score="2"><SimplePredicate '
+                'field="f0" operator="greaterOrEqual" value="0.1"/><ScoreDistribution value="1" recordCount="2"/>'
+                '<ScoreDistribution value="2" recordCount="8"/></Node></Node></TreeModel></Segment>')
+        feed = "p_a"
+    else:
+        seg1 = ('<Segment id="1"><True/><TreeModel functionName="regression" splitCharacteristic="binarySplit">'
+                + ms + '<Output><OutputField name="t1" optype="continuous" dataType="double" feature="predictedValue"/>'
+                '</Output>' + node("n", "f0", "0.2", "-1.5", "2.25") + '</TreeModel></Segment>')
+        feed = "t1"
+    ms2 = f'<MiningSchema><MiningField name="{feed}"/><MiningField name="f3"/></MiningSchema>'
+    seg2 = ('<Segment id="2"><SimplePredicate field="f2" operator="greaterThan" value="-0.5"/>'
+            '<RegressionModel functionName="regression">' + ms2 +
+            '<Output><OutputField name="t2" optype="continuous" dataType="double" feature="predictedValue"/></Output>'
+            f'<RegressionTable intercept="0.1"><NumericPredictor name="{feed}" coefficient="0.5"/>'
+            '<NumericPredictor name="f3" coefficient="-0.3"/></RegressionTable></RegressionModel></Segment>')
+    ms3 = ('<MiningSchema><MiningField name="t2"/><MiningField name="f1"/></MiningSchema>')
+    if classification:
+        seg3 = ('<Segment id="3"><True/><TreeModel functionName="classification" missingValueStrategy="lastPrediction" '
+                'splitCharacteristic="binarySplit">' + ms3 + '<Node id="r" score="3"><True/><Node id="x" score="1">'
+                '<SimplePredicate field="t2" operator="lessThan" value="0.0"/></Node><Node id="y" score="2">'
+                '<SimplePredicate field="t2" operator="greaterOrEqual" value="0.0"/></Node></Node></TreeModel></Segment>')
+    else:
+        seg3 = ('<Segment id="3"><True/><TreeModel functionName="regression" missingValueStrategy="lastPrediction" '
+                'splitCharacteristic="binarySplit">' + ms3 + '<Node id="r" score="0.5"><True/>'
+                '<Node id="x" score="-4"><SimplePredicate field="t2" operator="lessThan" value="0.3"/></Node>'
+                '<Node id="y" score="6"><SimplePredicate field="t2" operator="greaterOrEqual" value="0.3"/></Node>'
+                '</Node></TreeModel></Segment>')
+    fn = "classification" if classification else "regression"
+    return (f'<PMML version="4.4" xmlns="{NS44}"><DataDictionary>{fields}{tgt}</DataDictionary>'
+            f'<MiningModel functionName="{fn}">{ms}<Segmentation multipleModelMethod="modelChain">'
+            f'{seg1}{seg2}{seg3}</Segmentation></MiningModel></PMML>')
+
+
+@pytest.mark.parametrize("classification", [False, True])
+def test_general_model_chain_lowers_to_chain_plan(classification):
+    """a modelChain whose segment outputs feed later segments (not the fused
+    tree -> calibrator form) lowers to ChainPlan; on the CPU dry run its segment plans are stand-ins,
+    so the oracle parity check runs on the GPU (tests/test_gpu_segmented.py)."""
+    from flink_jpmml_amd.runtime.segmented import ChainPlan
+
+    c = CompiledPmml.from_string(general_chain_pmml(classification))
+    X = stream_matrix(500, 4, seed=2, missing_rate=0.05)
+    s, v = c.score_matrix_oracle(X)
+    assert v.any()
+    with lowering_dry_run():
+        plan = compile_plan(c, torch.device("cpu"))
+    assert isinstance(plan, ChainPlan)
+    assert plan.columns[4:] == (["p_a", "t2"] if classification else ["t1", "t2"])
