@@ -208,6 +208,37 @@ __device__ __forceinline__ void store_hidden(const GemmArgs& a, const f32x16 (&a
   }
 }
 
+// Output-layer decode of one row from its n_out activated output units z[]: the regression
+// affine + Target epilogue, or softmax / simplemax, probabilities, argmax and the label table.
+__device__ __forceinline__ void decode_row(const GemmArgs& a, int row, const float* z) {
+  const bool bad = !a.row_ok[row];
+  if (a.final_norm == 0 && a.n_out == 1) {
+    apply_epilogue(a.epi, [&](int) { return z[0]; }, !bad, row, a.rows, a.score, a.valid, a.probs);
+    return;
+  }
+  float mx = -__builtin_inff();
+  for (int u = 0; u < a.n_out; ++u) mx = fmaxf(mx, z[u]);
+  float sum = 0.f;
+  for (int u = 0; u < a.n_out; ++u) sum += (a.final_norm == 1) ? __expf(z[u] - mx) : z[u];
+  float best = -__builtin_inff();
+  int best_u = 1 << 30;
+  for (int u = 0; u < a.n_out; ++u) {
+    float p = (a.final_norm == 1) ? __expf(z[u] - mx) : z[u];
+    if (a.final_norm != 0) p /= sum;
+    if (p > best || (p == best && u < best_u)) { best = p; best_u = u; }
+    if (a.probs) a.probs[(size_t)row * a.n_out + u] = p;
+  }
+  bool ok = !bad && best == best && best_u < a.n_out;
+  float sc = ok ? (a.epi.has_table ? a.epi.table[best_u] : (float)best_u) : __builtin_nanf("");
+  ok = ok && (sc == sc);
+  a.score[row] = ok ? sc : __builtin_nanf("");
+  a.valid[row] = ok ? 1 : 0;
+  if (a.epi.score2) {
+    a.epi.score2[row] = ok ? sc : __builtin_nanf("");
+    a.epi.valid2[row] = ok ? 1 : 0;
+  }
+}
+
 template <int BN, bool HEAD, bool F32>
 __global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmArgs a) {
   constexpr int WM = BN == 256 ? 2 : 8;  // waves along rows
@@ -309,35 +340,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmArgs a) {
     __syncthreads();
     if (tid < BM) {
       const int row = row0 + tid;
-      if (row < a.rows) {
-        const float* z = zt + tid * HEAD_LD;
-        const bool bad = !a.row_ok[row];
-        if (a.final_norm == 0 && a.n_out == 1) {
-          apply_epilogue(a.epi, [&](int) { return z[0]; }, !bad, row, a.rows, a.score, a.valid, a.probs);
-        } else {
-          float mx = -__builtin_inff();
-          for (int u = 0; u < a.n_out; ++u) mx = fmaxf(mx, z[u]);
-          float sum = 0.f;
-          for (int u = 0; u < a.n_out; ++u) sum += (a.final_norm == 1) ? __expf(z[u] - mx) : z[u];
-          float best = -__builtin_inff();
-          int best_u = 1 << 30;
-          for (int u = 0; u < a.n_out; ++u) {
-            float p = (a.final_norm == 1) ? __expf(z[u] - mx) : z[u];
-            if (a.final_norm != 0) p /= sum;
-            if (p > best || (p == best && u < best_u)) { best = p; best_u = u; }
-            if (a.probs) a.probs[(size_t)row * a.n_out + u] = p;
-          }
-          bool ok = !bad && best == best && best_u < a.n_out;
-          float sc = ok ? (a.epi.has_table ? a.epi.table[best_u] : (float)best_u) : __builtin_nanf("");
-          ok = ok && (sc == sc);
-          a.score[row] = ok ? sc : __builtin_nanf("");
-          a.valid[row] = ok ? 1 : 0;
-          if (a.epi.score2) {
-            a.epi.score2[row] = ok ? sc : __builtin_nanf("");
-            a.epi.valid2[row] = ok ? 1 : 0;
-          }
-        }
-      }
+      if (row < a.rows) decode_row(a, row, zt + tid * HEAD_LD);
     }
   }
 }
@@ -404,17 +407,84 @@ __device__ __forceinline__ void mma_end() {
 // acc[i0 + i][j] += a[i] . b over the slice's four k16 steps. The empty volatile asm on the
 // accumulators pins the MFMAs between the phase's two barriers (register-only instructions are
 // otherwise free to sink past them; sched_barrier alone did not keep them there).
+// SWAP: the transposed product (weights as the A operand): the accumulator tile is [unit][row],
+// a row per lane and the units in the registers — the layout a following MFMA takes as its B
+// operand with no lane movement (the fused output layer of gemm8_kernel<true>).
+template <bool SWAP = false>
 __device__ __forceinline__ void mma_quad(f32x16& c0, f32x16& c1, const bf16x8 (&a)[2][4], const bf16x8 (&b)[4]) {
   asm volatile("" : "+v"(c0), "+v"(c1));
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) {
-    c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][ks], b[ks], c0, 0, 0, 0);
-    c1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][ks], b[ks], c1, 0, 0, 0);
+    if constexpr (SWAP) {
+      c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[ks], a[0][ks], c0, 0, 0, 0);
+      c1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[ks], a[1][ks], c1, 0, 0, 0);
+    } else {
+      c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][ks], b[ks], c0, 0, 0, 0);
+      c1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][ks], b[ks], c1, 0, 0, 0);
+    }
   }
   asm volatile("" : "+v"(c0), "+v"(c1));
 }
 
-__global__ __launch_bounds__(NT, 1) void gemm8_kernel(GemmArgs a) {
+struct HeadFuse {
+  const __bf16* wh;  // [32][ldw] output-layer weights, k permuted within 32-unit groups (fuse_head_perm)
+  float* part;       // [Mp / 256][rows_p][n_out] per-column-tile partial output sums
+  int ldw, n_out;
+};
+
+// Fused output layer (gemm8_kernel<true>, the last hidden layer): the accumulators hold the
+// transposed tile [unit][row] (mma_quad<true>), so bias + activation + bf16 of 8 consecutive
+// registers IS an MFMA B fragment [k = unit][col = row] — with the output-layer weights' k order
+// permuted the same way on the host (fuse_head_perm), Z[out][row] = Wh · H accumulates with no
+// lane movement, no LDS round trip and no store of the hidden layer. The four column waves of a
+// row group leave their Z in LDS and the block writes the in-order sum, its [256, n_out] partial,
+// to hf.part[column tile] (deterministic); nn_head_decode_kernel sums the column tiles in order
+// and decodes.
+template <int ACT>
+__device__ __forceinline__ void head_partial(const GemmArgs& a, const HeadFuse& hf, const f32x16 (&acc)[4][2], int row0,
+                                             int col0, int wr, int wc, int lane, int tid, unsigned char* smem) {
+  const int h = lane >> 5, l32 = lane & 31;
+  const int no = hf.n_out;
+  float* zp = reinterpret_cast<float*>(smem);  // [4 column waves][BM][n_out] (the staging buffers are drained)
+  bf16x8 wf[2][2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+      wf[j][s] = *reinterpret_cast<const bf16x8*>(hf.wh + (size_t)l32 * hf.ldw + col0 + wc * 64 + 32 * j + 16 * s + 8 * h);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f32x16 z = f32x16{};
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const float* bias = a.bias + col0 + wc * 64 + 32 * j + 4 * h;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 hb;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int r = 8 * s + e;
+          hb[e] = (__bf16)act_of<ACT>(acc[i][j][r] + bias[(r & 3) + 8 * (r >> 2)], a.act, a.thr);
+        }
+        z = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[j][s], hb, z, 0, 0, 0);
+      }
+    }
+    // z[r]: output unit o = (r & 3) + 8 (r >> 2) + 4 h of block row wr * 128 + 32 i + l32
+    float* dst = zp + ((size_t)wc * BM + wr * 128 + 32 * i + l32) * no;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int o = (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (o < no) dst[o] = z[r];
+    }
+  }
+  __syncthreads();
+  float* out = hf.part + ((size_t)(col0 >> 8) * a.rows_p + row0) * no;
+  const size_t plane = (size_t)BM * no;
+  for (int e = tid; e < BM * no; e += NT) out[e] = ((zp[e] + zp[plane + e]) + zp[2 * plane + e]) + zp[3 * plane + e];
+}
+
+template <bool HEADF>
+__global__ __launch_bounds__(NT, 1) void gemm8_kernel(GemmArgs a, HeadFuse hf) {
   constexpr int TM = 4, TN = 2;  // acc[2 * a_half + tile][b_half]
   extern __shared__ __align__(16) unsigned char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -468,14 +538,14 @@ __global__ __launch_bounds__(NT, 1) void gemm8_kernel(GemmArgs a) {
     }
     if (kt + 1 < KT) stage_half<true>(Ab, lda_b, k1, SLOT(b ^ 1, 1), 1, wave, lane);
     mma_begin();
-    mma_quad(acc[0][0], acc[1][0], a0, b0);
+    mma_quad<HEADF>(acc[0][0], acc[1][0], a0, b0);
     mma_end();
     // P2: A0 x B1
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) b1[ks] = frag(SLOT(b, 3), rb, 2 * ks + h);
     if (kt + 2 < KT) stage_half<true>(Ab, lda_b, k2, SLOT(b, 0), 0, wave, lane);
     mma_begin();
-    mma_quad(acc[0][1], acc[1][1], a0, b1);
+    mma_quad<HEADF>(acc[0][1], acc[1][1], a0, b1);
     mma_end();
     // P3: A1 x B1
 #pragma unroll
@@ -484,34 +554,60 @@ __global__ __launch_bounds__(NT, 1) void gemm8_kernel(GemmArgs a) {
       for (int i = 0; i < 2; ++i) a1[i][ks] = frag(SLOT(b, 1), ra + 32 * i, 2 * ks + h);
     if (kt + 2 < KT) stage_half<false>(Bb, ldw_b, k2, SLOT(b, 2), 0, wave, lane);
     mma_begin();
-    mma_quad(acc[2][1], acc[3][1], a1, b1);
+    mma_quad<HEADF>(acc[2][1], acc[3][1], a1, b1);
     mma_end();
     // P4: A1 x B0; slice kt + 1 retired (three half-tiles of kt + 2 may stay in flight)
     if (kt + 2 < KT) stage_half<false>(Bb, ldw_b, k2, SLOT(b, 3), 1, wave, lane);
     if (kt + 2 < KT) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     else if (kt + 1 < KT) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     mma_begin();
-    mma_quad(acc[2][0], acc[3][0], a1, b0);
+    mma_quad<HEADF>(acc[2][0], acc[3][0], a1, b0);
     mma_end();
   }
 #undef SLOT
   if (wr == 0) raw_barrier();  // balance group 1's extra barrier
-  switch (a.act) {
-    case A_IDENTITY: store_hidden<A_IDENTITY, TM, TN, false>(a, acc, row0, col0, wr, wc, lane); break;
-    case A_RELU: store_hidden<A_RELU, TM, TN, false>(a, acc, row0, col0, wr, wc, lane); break;
-    case A_LOGISTIC: store_hidden<A_LOGISTIC, TM, TN, false>(a, acc, row0, col0, wr, wc, lane); break;
-    case A_TANH: store_hidden<A_TANH, TM, TN, false>(a, acc, row0, col0, wr, wc, lane); break;
-    default: store_hidden<-1, TM, TN, false>(a, acc, row0, col0, wr, wc, lane); break;
+  if constexpr (HEADF) {
+    switch (a.act) {
+      case A_IDENTITY: head_partial<A_IDENTITY>(a, hf, acc, row0, col0, wr, wc, lane, tid, smem); break;
+      case A_RELU: head_partial<A_RELU>(a, hf, acc, row0, col0, wr, wc, lane, tid, smem); break;
+      case A_LOGISTIC: head_partial<A_LOGISTIC>(a, hf, acc, row0, col0, wr, wc, lane, tid, smem); break;
+      case A_TANH: head_partial<A_TANH>(a, hf, acc, row0, col0, wr, wc, lane, tid, smem); break;
+      default: head_partial<-1>(a, hf, acc, row0, col0, wr, wc, lane, tid, smem); break;
+    }
+    return;
+  } else {
+    switch (a.act) {
+      case A_IDENTITY: store_hidden<A_IDENTITY, TM, TN, false>(a, acc, row0, col0, wr, wc, lane); break;
+      case A_RELU: store_hidden<A_RELU, TM, TN, false>(a, acc, row0, col0, wr, wc, lane); break;
+      case A_LOGISTIC: store_hidden<A_LOGISTIC, TM, TN, false>(a, acc, row0, col0, wr, wc, lane); break;
+      case A_TANH: store_hidden<A_TANH, TM, TN, false>(a, acc, row0, col0, wr, wc, lane); break;
+      default: store_hidden<-1, TM, TN, false>(a, acc, row0, col0, wr, wc, lane); break;
+    }
   }
 }
 
-int launch8(hipStream_t stream, const GemmArgs& a) {
+template <bool HEADF>
+int launch8(hipStream_t stream, const GemmArgs& a, const HeadFuse& hf) {
   const size_t lds = 8 * (size_t)HALF_B;
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm8_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)lds) != hipSuccess)
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm8_kernel<HEADF>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return -5;
-  hipLaunchKernelGGL(gemm8_kernel, dim3((a.rows_p / BM) * (a.Mp / 256)), dim3(NT), lds, stream, a);
+  hipLaunchKernelGGL((gemm8_kernel<HEADF>), dim3((a.rows_p / BM) * (a.Mp / 256)), dim3(NT), lds, stream, a, hf);
   return 0;
+}
+
+// The fused output layer's second half: one thread per row sums the column tiles' partials in
+// order, + bias, output activation, decode.
+__global__ __launch_bounds__(256) void nn_head_decode_kernel(GemmArgs a, const float* __restrict__ part, int n_ct) {
+  const int row = blockIdx.x * 256 + threadIdx.x;
+  if (row >= a.rows) return;
+  float z[32];
+  for (int o = 0; o < a.n_out; ++o) {
+    float s = 0.f;
+    for (int c = 0; c < n_ct; ++c) s += part[((size_t)c * a.rows_p + row) * a.n_out + o];
+    z[o] = activate(a.act, s + a.bias[o], a.thr);
+  }
+  decode_row(a, row, z);
 }
 
 template <int BN, bool HEAD, bool F32>
@@ -566,7 +662,29 @@ PMML_API int pmml_gemm_launch(hipStream_t stream, const GemmArgs* args, int head
   if (!head && ((a.ldc & 7) || a.ldc < a.Mp || !a.C || (reinterpret_cast<uintptr_t>(a.C) & 15))) return -4;
   const int rc = f32 ? (head ? launch<32, true, true>(stream, a) : launch<256, false, true>(stream, a))
                      : (head ? launch<32, true, false>(stream, a)
-                             : (ph8 ? launch8(stream, a) : launch<256, false, false>(stream, a)));
+                             : (ph8 ? launch8<false>(stream, a, HeadFuse{}) : launch<256, false, false>(stream, a)));
   if (rc) return rc;
+  return hipGetLastError() == hipSuccess ? 0 : -7;
+}
+
+// The last hidden layer and the output layer in one GEMM launch + one decode launch
+// (gemm8_kernel<true>): the hidden activations never reach HBM. hidden: a bf16 hidden layer (K a
+// multiple of 64, Mp of 256); head: the output layer's args (Wt unused: wh_perm holds its weights
+// [32][hidden.Mp], k permuted by fuse_head_perm); part: (hidden.Mp / 256) * rows_p * n_out floats.
+PMML_API int pmml_gemm_fused_head_launch(hipStream_t stream, const GemmArgs* hidden, const GemmArgs* head,
+                                         const void* wh_perm, float* part) {
+  const GemmArgs a = *hidden;
+  const GemmArgs o = *head;
+  if (a.rows <= 0) return 0;
+  if ((a.f32 & 1) || (o.f32 & 1)) return -4;  // bf16 only (bit 7, the gemm8 force flag, is moot here)
+  if (a.rows_p % BM || a.rows_p < a.rows || a.K % BK || a.K <= 0 || a.Mp % 256 || a.Mp <= 0) return -4;
+  if ((a.lda & 7) || (a.ldw & 7) || a.lda < a.K || a.ldw < a.K) return -4;
+  if ((reinterpret_cast<uintptr_t>(a.A) & 15) || (reinterpret_cast<uintptr_t>(a.Wt) & 15)) return -4;
+  if (o.n_out < 1 || o.n_out > 32 || o.K != a.Mp || o.rows != a.rows || o.rows_p != a.rows_p) return -4;
+  if (!o.row_ok || !o.score || !o.valid || !part || !wh_perm || (reinterpret_cast<uintptr_t>(wh_perm) & 15)) return -4;
+  HeadFuse hf{static_cast<const __bf16*>(wh_perm), part, a.Mp, o.n_out};
+  int rc = launch8<true>(stream, a, hf);
+  if (rc) return rc;
+  hipLaunchKernelGGL(nn_head_decode_kernel, dim3((a.rows + 255) / 256), dim3(256), 0, stream, o, part, a.Mp / 256);
   return hipGetLastError() == hipSuccess ? 0 : -7;
 }

@@ -352,6 +352,15 @@ def _ceil(x: int, m: int) -> int:
     return -(-x // m) * m
 
 
+def fused_head_perm(K: int) -> np.ndarray:
+    """Source unit of every storage position of the fused output layer's weight rows (K a multiple
+    of 32): position g + 16 s + 8 h + e <- unit g + 16 s + 8 (e >> 2) + 4 h + (e & 3)."""
+    q = np.arange(K)
+    g, t = q - q % 32, q % 32
+    s, h, e = t // 16, (t % 16) // 8, t % 8
+    return (g + 16 * s + 8 * (e >> 2) + 4 * h + (e & 3)).astype(np.int64)
+
+
 class WideMlpPlan(MlpPlan):
     """NeuralNetworks beyond the fused kernel (layers wider than 256 units, more than 8 layers or
     256 inputs) on ``gemm.hip``: an input-stage kernel (gather, NormContinuous, missing values,
@@ -406,6 +415,26 @@ class WideMlpPlan(MlpPlan):
         self.dims = dims
 
     gemm_flags = 0  # experiment bits ORed into GemmArgs.f32 (scripts/gemm_ab.py); the kernel rejects unknown bits
+    # bf16: the last hidden layer and the output layer in one GEMM launch (gemm8_kernel<true>) — the
+    # last hidden activations never reach HBM (profiles/r4f)
+    fuse_head = True
+
+    def _fused_head(self) -> bool:
+        return bool(self.fuse_head) and self.bf16 == 1 and len(self.dims) >= 2 and self.dims[-2][0] % 64 == 0
+
+    def _head_weights(self):
+        """The output layer's weights [32, K] with k permuted inside every 32-unit group as the
+        fused epilogue consumes them: storage position 16 s + 8 h + e of a group holds unit
+        16 s + 8 (e >> 2) + 4 h + (e & 3) — the unit an MFMA accumulator register (8 s + e) of lane
+        half h carries (csrc/gemm.hip head_partial)."""
+        w = getattr(self, "_whp", None)
+        if w is None:
+            import torch
+
+            kp, mp, _, _, wo, _ = self.dims[-1]
+            w = self._whp = self.wts[wo: wo + mp * kp].view(mp, kp)[:, torch.from_numpy(
+                fused_head_perm(kp)).to(self.device)].contiguous()
+        return w
 
     def _dtype(self):
         import torch
@@ -439,7 +468,10 @@ class WideMlpPlan(MlpPlan):
         p.f32 = 1 - self.bf16
         check(self.lib.pmml_nn_prep_launch(h, ctypes.byref(p)), "nn input stage")
         wbase, bbase, es = self.wts.data_ptr(), self.bss.data_ptr(), 2 if self.bf16 else 4
+        fused = self._fused_head()
+        extra = []
         cur, lda = H0, self.k0
+        pending = None
         for li, (kp, mp, act, thr, wo, bo) in enumerate(self.dims):
             head = li == len(self.dims) - 1
             a = GemmArgs()
@@ -451,13 +483,25 @@ class WideMlpPlan(MlpPlan):
                 a.epi = _epilogue(mode=EPI_AFFINE, a=self.out_a, b=self.out_b, table=self.table, tgt=self.target_stage)
                 a.epi.score2, a.epi.valid2 = _addr(score2), _addr(valid2)
                 a.score, a.valid, a.probs = _addr(score), _addr(valid), ptr(probs)
-                check(self.lib.pmml_gemm_launch(h, ctypes.byref(a), 1), "nn output-layer gemm")
+                if pending is not None:  # last hidden layer + this one: one fused GEMM + the decode
+                    whp = self._head_weights()
+                    with torch.cuda.stream(st):
+                        part = torch.empty((pending.Mp // 256) * rows_p * self.n_out, dtype=torch.float32,
+                                           device=self.device)
+                    extra.append(part)
+                    check(self.lib.pmml_gemm_fused_head_launch(h, ctypes.byref(pending), ctypes.byref(a),
+                                                               whp.data_ptr(), part.data_ptr()),
+                          "nn fused last-hidden + output-layer gemm")
+                else:
+                    check(self.lib.pmml_gemm_launch(h, ctypes.byref(a), 1), "nn output-layer gemm")
+            elif fused and li == len(self.dims) - 2:
+                pending = a  # its activations go straight into the output layer's MFMAs
             else:
                 out = bufs[li & 1]
                 a.C, a.ldc = out.data_ptr(), out.stride(0)
                 check(self.lib.pmml_gemm_launch(h, ctypes.byref(a), 0), "nn layer gemm")
                 cur, lda = out, out.stride(0)
-        for t in [H0, ok] + bufs:  # freed by the caching allocator only after this stream's work
+        for t in [H0, ok] + bufs + extra:  # freed by the caching allocator only after this stream's work
             t.record_stream(st)
 
 

@@ -147,6 +147,7 @@ def test_phase_interleaved_gemm_matches_two_buffer_loop(gpu, shape):
     bits as the 2-buffer loop — the same MFMAs in the same k order."""
     c = CompiledPmml.from_string(mlp_pmml(seed=9, **shape))
     plan = c.plan(gpu, precision="bf16", mlp_impl="wide")
+    plan.fuse_head = False  # every hidden layer through pmml_gemm_launch
     X = stream_matrix(5000, shape["n_features"], seed=4, missing_rate=0.01)
     s0, v0 = plan.score(X)
     plan.gemm_flags = 0x80
@@ -159,3 +160,57 @@ def test_phase_interleaved_gemm_matches_two_buffer_loop(gpu, shape):
     s1, v1 = s1.cpu().numpy(), v1.cpu().numpy().astype(bool)
     assert (v1 == vref).all()
     assert np.abs(s1[v1] - ref[v1]).max() < 3e-2 * max(1.0, float(np.abs(ref[v1]).max()))
+
+
+def test_fused_head_permutation_matches_accumulator_layout():
+    """gemm8_kernel<true> feeds the last hidden layer's accumulators (a row per lane, units in the
+    16 registers: unit (r & 3) + 8 (r >> 2) + 4 h for lane half h) straight into the output-layer
+    MFMA as B fragments (k-step s = registers 8 s .. 8 s + 7, MFMA k = 8 h + e). The host-permuted
+    weights must put, at the A-fragment position a lane reads (16 s + 8 h + e), the weight of the
+    very unit that register carries."""
+    from flink_jpmml_amd.runtime.nn_plans import fused_head_perm
+
+    K = 1024
+    perm = fused_head_perm(K)
+    assert sorted(perm.tolist()) == list(range(K))  # a permutation inside every 32-unit group
+    assert (perm // 32 == np.arange(K) // 32).all()
+    for g in range(0, K, 32):
+        for h in (0, 1):
+            for s in (0, 1):
+                for e in range(8):
+                    r = 8 * s + e
+                    unit = g + (r & 3) + 8 * (r >> 2) + 4 * h  # what accumulator register r carries
+                    assert perm[g + 16 * s + 8 * h + e] == unit
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [dict(n_features=32, hidden=(1024, 1024), n_out=1, activation="rectifier"),
+                                   dict(n_features=21, hidden=(512,), n_out=5, activation="tanh",
+                                        classification=True),
+                                   dict(n_features=40, hidden=(300, 1024), n_out=3, activation="logistic",
+                                        classification=True)],
+                         ids=["reg1024x2", "cls512", "cls300x1024"])
+def test_fused_output_layer_matches_separate_launch(gpu, shape):
+    """The last hidden layer + output layer as one GEMM (the hidden activations never stored) give
+    the unfused result up to fp32 summation order, and the oracle within bf16 tolerance."""
+    c = CompiledPmml.from_string(mlp_pmml(seed=11, **shape))
+    plan = c.plan(gpu, precision="bf16", mlp_impl="wide")
+    assert plan._fused_head()
+    X = stream_matrix(20_001, shape["n_features"], seed=5, missing_rate=0.01)
+    s1, v1 = plan.score(X)
+    plan.fuse_head = False
+    try:
+        s0, v0 = plan.score(X)
+    finally:
+        plan.fuse_head = True
+    assert torch.equal(v0, v1)
+    s0, s1, v = s0.cpu().numpy(), s1.cpu().numpy(), v1.cpu().numpy().astype(bool)
+    ref, vref = c.score_matrix_oracle(X)
+    assert (v == vref).all()
+    if shape.get("classification"):
+        assert (s0[v] == s1[v]).mean() > 0.999
+        assert (s1[v] == ref[v]).mean() > 0.98
+    else:
+        scale = max(1.0, float(np.abs(ref[v]).max()))
+        assert np.abs(s1[v] - s0[v]).max() < 1e-4 * scale
+        assert np.abs(s1[v] - ref[v]).max() < 3e-2 * scale
