@@ -148,6 +148,13 @@ class TextParseArgs(ctypes.Structure):
                 ("n_flagged", c_void_p)]
 
 
+class MultiTreeArgs(ctypes.Structure):
+    """tree.hip MultiTreeArgs: several pointer-layout ensembles (segments) over the same rows."""
+    _fields_ = [("segs", c_void_p), ("X", c_void_p), ("S", c_void_p), ("V", c_void_p), ("P", c_void_p),
+                ("poff", c_void_p), ("sidx", c_void_p), ("n_rows", c_int), ("n_feat", c_int), ("ldx", c_int),
+                ("count", c_int)]
+
+
 class SegArgs(ctypes.Structure):
     _fields_ = [("X", c_void_p), ("n_rows", c_int), ("ldx", c_int), ("S", c_void_p), ("V", c_void_p),
                 ("P", c_void_p), ("coff", c_void_p), ("prog", c_void_p), ("pool", c_void_p), ("pc", c_void_p),
@@ -241,6 +248,7 @@ _ABI = {
     "pmml_textparse_args_size": TextParseArgs,
     "pmml_derive_args_size": DeriveArgs,
     "pmml_tree_args_size": TreeArgs,
+    "pmml_tree_multi_args_size": MultiTreeArgs,
     "pmml_tree_general_args_size": GenTreeArgs,
     "pmml_tree_hybrid_args_size": HybridArgs,
     "pmml_cluster_args_size": ClusterArgs,
@@ -334,6 +342,8 @@ def load(auto_build: bool = True) -> ctypes.CDLL:
         lib.pmml_host_unregister.argtypes = [c_void_p]
         lib.pmml_host_unregister.restype = c_int
         lib.pmml_segment_reduce.argtypes = [c_void_p, ctypes.POINTER(SegArgs)]
+        lib.pmml_tree_pointer_multi.argtypes = [c_void_p, ctypes.POINTER(MultiTreeArgs), c_int, c_int]
+        lib.pmml_tree_pointer_multi.restype = c_int
         lib.pmml_segment_reduce.restype = c_int
         lib.pmml_tree_launch_many.argtypes = [c_void_p, c_void_p, c_void_p, c_int]
         lib.pmml_tree_launch_many.restype = c_int

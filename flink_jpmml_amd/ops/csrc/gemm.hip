@@ -239,6 +239,51 @@ __device__ __forceinline__ void decode_row(const GemmArgs& a, int row, const flo
   }
 }
 
+// Hidden-layer epilogue through LDS (bf16, 256 x 256 tile): the tile is assembled in LDS (rows
+// padded to 528 B so the two lane halves' rows land on different banks), then every thread stores
+// whole 16-byte chunks of contiguous rows — 16 store instructions per thread instead of 128
+// two-unit stores. Pays off when the layer is store-bound (K <= 128: the first hidden layer over
+// a narrow input); for K = 1024 the direct stores drain behind the MFMAs of other waves (r3l).
+constexpr int EPI_LD = 528;  // bytes per staged row
+constexpr size_t EPI_LDS = (size_t)BM * EPI_LD;
+
+template <int ACT>
+__device__ __forceinline__ void store_hidden_lds(const GemmArgs& a, const f32x16 (&acc)[4][2], int row0, int col0,
+                                                 int wm, int wn, int lane, int tid, unsigned char* smem) {
+  constexpr int TM = 4, TN = 2;
+  const int h = lane >> 5, l32 = lane & 31;
+  __syncthreads();  // every wave is done reading the staging buffers
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int ul = (wn * TN + j) * 32 + l32;  // unit within the tile
+    const float b = a.bias[col0 + ul];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int rb = (wm * TM + i) * 32 + 4 * h;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float v = act_of<ACT>(acc[i][j][r] + b, a.act, a.thr);
+        const float o = __shfl_xor(v, 1);
+        if ((lane & 1) == 0) {
+          const uint32_t lo = __builtin_bit_cast(uint16_t, (__bf16)v);
+          const uint32_t hi = __builtin_bit_cast(uint16_t, (__bf16)o);
+          const int row = rb + (r & 3) + 8 * (r >> 2);
+          *reinterpret_cast<uint32_t*>(smem + row * EPI_LD + 2 * ul) = lo | (hi << 16);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  // 256 rows x 32 chunks of 16 B; thread t: chunk t & 31 of rows (t >> 5) + 16 q
+  const int c = tid & 31;
+#pragma unroll 4
+  for (int q = 0; q < BM / (NT / 32); ++q) {
+    const int row = (tid >> 5) + (NT / 32) * q;
+    const uint4 v = *reinterpret_cast<const uint4*>(smem + row * EPI_LD + 16 * c);
+    *reinterpret_cast<uint4*>(static_cast<__bf16*>(a.C) + (size_t)(row0 + row) * a.ldc + col0 + 8 * c) = v;
+  }
+}
+
 template <int BN, bool HEAD, bool F32>
 __global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmArgs a) {
   constexpr int WM = BN == 256 ? 2 : 8;  // waves along rows
@@ -320,6 +365,18 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmArgs a) {
     __syncthreads();                // ... for every wave before anyone reads / overwrites it
   }
 
+  if constexpr (!HEAD && !F32 && BN == 256) {
+    if (KT <= 2) {  // a store-bound layer (small K, e.g. the first hidden layer): LDS-staged stores
+      switch (a.act) {
+        case A_IDENTITY: store_hidden_lds<A_IDENTITY>(a, acc, row0, col0, wm, wn, lane, tid, smem); break;
+        case A_RELU: store_hidden_lds<A_RELU>(a, acc, row0, col0, wm, wn, lane, tid, smem); break;
+        case A_LOGISTIC: store_hidden_lds<A_LOGISTIC>(a, acc, row0, col0, wm, wn, lane, tid, smem); break;
+        case A_TANH: store_hidden_lds<A_TANH>(a, acc, row0, col0, wm, wn, lane, tid, smem); break;
+        default: store_hidden_lds<-1>(a, acc, row0, col0, wm, wn, lane, tid, smem); break;
+      }
+      return;
+    }
+  }
   if constexpr (!HEAD) {
     switch (a.act) {  // uniform: one unrolled epilogue per common activation
       case A_IDENTITY: store_hidden<A_IDENTITY, TM, TN, F32>(a, acc, row0, col0, wm, wn, lane); break;
@@ -613,7 +670,8 @@ __global__ __launch_bounds__(256) void nn_head_decode_kernel(GemmArgs a, const f
 template <int BN, bool HEAD, bool F32>
 int launch(hipStream_t stream, const GemmArgs& a) {
   const size_t stage = 2 * (size_t)BM * SLICE_B + 2 * (size_t)BN * SLICE_B;
-  const size_t head = HEAD ? (size_t)BM * HEAD_LD * 4 : 0;
+  size_t head = HEAD ? (size_t)BM * HEAD_LD * 4 : 0;
+  if (!HEAD && !F32 && BN == 256 && a.K <= 2 * (SLICE_B / 2)) head = EPI_LDS;  // store_hidden_lds
   const size_t lds = stage > head ? stage : head;
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_kernel<BN, HEAD, F32>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)

@@ -18,7 +18,7 @@ namespace {
 // the same one or two nodes (the walk is bound by the vector memory pipe's per-instruction cost,
 // profiles/r3w).
 template <bool GENERAL, bool FEAT_LDS, int PILP = 8, bool MASKED = false, bool USKIP = false, bool PEEL = false>
-__global__ __launch_bounds__(TB, 2) void tree_pointer_kernel(TreeArgs a) {
+__device__ __forceinline__ void pointer_walk(const TreeArgs& a) {
   extern __shared__ __align__(16) uint32_t smem[];
   float* feat = reinterpret_cast<float*>(smem);
   int* bad = reinterpret_cast<int*>(smem + (FEAT_LDS ? a.n_feat * TB : 0));
@@ -164,6 +164,48 @@ __global__ __launch_bounds__(TB, 2) void tree_pointer_kernel(TreeArgs a) {
     }
   }
   finish_row(a, acc, accl, split, GENERAL, row, row_ok && !poisoned);
+}
+
+template <bool GENERAL, bool FEAT_LDS, int PILP = 8, bool MASKED = false, bool USKIP = false, bool PEEL = false>
+__global__ __launch_bounds__(TB, 2) void tree_pointer_kernel(TreeArgs a) {
+  pointer_walk<GENERAL, FEAT_LDS, PILP, MASKED, USKIP, PEEL>(a);
+}
+
+// Several pointer-layout ensembles over the SAME rows in one launch — the segments of a segmented
+// MiningModel (runtime/segmented.py: K segment walks + the fused reduction = 2 launches instead of
+// K + 1). grid.z selects the segment; its static argument block (nodes, leaves, epilogue) lives in
+// a device array built once per plan, the per-launch fields come from the kernel argument:
+// member z scores into S[sidx[z]] / V[sidx[z]] (and probabilities at P + poff[z] * n_rows).
+struct MultiTreeArgs {
+  const TreeArgs* segs;
+  const float* X;
+  float* S;
+  uint8_t* V;
+  float* P;
+  const long long* poff;  // nullable: per member, probability column offset (in rows of n_rows)
+  const int* sidx;        // per member: its segment index (row of S / V)
+  int n_rows, n_feat, ldx, count;
+};
+
+template <bool GENERAL>
+__global__ __launch_bounds__(TB, 2) void tree_pointer_multi_kernel(MultiTreeArgs m) {
+  const int z = blockIdx.z;
+  TreeArgs a = m.segs[z];
+  a.X = m.X;
+  a.n_rows = m.n_rows;
+  a.n_feat = m.n_feat;
+  a.ldx = m.ldx;
+  a.row_valid_in = nullptr;
+  a.partial = nullptr;
+  a.xcd_split = 0;
+  a.trees_per_split = a.n_trees;
+  const int seg = m.sidx[z];
+  a.score = m.S + (size_t)seg * m.n_rows;
+  a.valid = m.V + (size_t)seg * m.n_rows;
+  a.probs = (m.P && m.poff) ? m.P + (size_t)m.poff[z] * m.n_rows : nullptr;
+  a.epi.score2 = nullptr;
+  a.epi.valid2 = nullptr;
+  pointer_walk<GENERAL, true>(a);
 }
 
 // Compact pointer layout (runtime/hybrid.py::pack_compact_bfs): 8-byte slots {T | leaf value,
@@ -865,6 +907,29 @@ PMML_API int pmml_tree_general_launch(hipStream_t stream, const GenTreeArgs* arg
       err = prepare_launch(tree_general_kernel<false, false>, lds);
       if (!err) hipLaunchKernelGGL((tree_general_kernel<false, false>), grid, dim3(TB), lds, stream, ga);
     }
+  }
+  if (err) return err;
+  return hipGetLastError() == hipSuccess ? 0 : -7;
+}
+
+PMML_API int pmml_tree_multi_args_size() { return (int)sizeof(MultiTreeArgs); }
+
+// One launch of tree_pointer_multi_kernel over m->count segments (features staged in LDS: n_feat
+// <= 64; general: the multi-slot accumulator variant, max_C the largest slot count).
+PMML_API int pmml_tree_pointer_multi(hipStream_t stream, const MultiTreeArgs* args, int general, int max_C) {
+  const MultiTreeArgs m = *args;
+  if (m.n_rows <= 0 || m.count <= 0) return 0;
+  if (m.n_feat < 1 || m.n_feat > 64 || m.count > 65535 || max_C < 0 || max_C > 16 || !m.segs || !m.S || !m.V || !m.sidx)
+    return -4;
+  const size_t lds = (size_t)m.n_feat * TB * 4 + TB * 4 + (general ? (size_t)max_C * TB * 4 : 0);
+  const dim3 grid((m.n_rows + TB - 1) / TB, 1, m.count);
+  int err;
+  if (general) {
+    err = prepare_launch(tree_pointer_multi_kernel<true>, lds);
+    if (!err) hipLaunchKernelGGL((tree_pointer_multi_kernel<true>), grid, dim3(TB), lds, stream, m);
+  } else {
+    err = prepare_launch(tree_pointer_multi_kernel<false>, lds);
+    if (!err) hipLaunchKernelGGL((tree_pointer_multi_kernel<false>), grid, dim3(TB), lds, stream, m);
   }
   if (err) return err;
   return hipGetLastError() == hipSuccess ? 0 : -7;

@@ -34,7 +34,8 @@ import numpy as np
 
 from ..models.mining import MiningEvaluator
 from ..pmml import ir
-from .plans import DevicePlan, NotLowerable, _label_table, apply_target_torch, target_post
+from .plans import (VAR_POINTER_COMPACT, VAR_POINTER_REFILL, VAR_POINTER_SUPER, DevicePlan, NotLowerable, _label_table,
+                    apply_target_torch, target_post)
 
 REGRESSION_METHODS = ("sum", "average", "weightedAverage", "max", "min", "median", "weightedMedian", "selectFirst")
 PROB_METHODS = ("average", "weightedAverage", "max", "median")  # classification over segment probabilities
@@ -212,6 +213,7 @@ _METHOD_CODE = {"selectFirst": 0, "sum": 1, "average": 2, "weightedAverage": 3, 
                 "weightedMedian": 7, "majorityVote": 8, "weightedMajorityVote": 9}
 _PROB_CODE = {"average": 10, "weightedAverage": 11, "max": 12, "median": 13}
 SEG_MAXK = SEG_MAXC = 64  # ops/csrc/segment.hip
+MULTI_MAX_TREES = 64  # tree segments this small share one pointer-layout launch (tree_pointer_multi_kernel)
 
 
 def predicate_programs(progs) -> tuple:
@@ -290,6 +292,7 @@ class SegmentedPlan(DevicePlan):
                 _index_outputs(plan)
             self.subs.append(plan)
         self.n_subs = len(self.subs)
+        self._pointer_segments(compiled, ev, device, opts)
         self.table, self.tgt, self.categories, self.remap_lists = None, None, None, None
         if self.kind_ == "classification":
             cats = list(ev.sub[0].categories) if self.method == "selectFirst" else list(ev.categories)
@@ -301,10 +304,63 @@ class SegmentedPlan(DevicePlan):
             self.tgt = target_post(ev.target, force=True)
         self._post_build()
 
+    def _pointer_segments(self, compiled, ev, device, opts) -> None:
+        """Small tree segments (<= MULTI_MAX_TREES trees in all) are re-lowered on the pointer
+        layout, whose walk does not depend on the depth: they then score in ONE launch
+        (``tree_pointer_multi_kernel``, grid.z = segment) instead of one launch each."""
+        from .plans import TreePlan, compile_plan
+
+        if "layout" in opts or self.n_subs < 2:
+            return
+        trees = [p for p in self.subs if isinstance(p, TreePlan)]
+        if len(trees) < 2 or sum(p.n_trees for p in trees) > MULTI_MAX_TREES:
+            return
+        for i, (sub, plan) in enumerate(zip(ev.sub, self.subs)):
+            if not isinstance(plan, TreePlan) or plan.layout == "pointer":
+                continue
+            try:
+                new = compile_plan(SubView(compiled, sub), device, **dict(opts, layout="pointer"))
+            except NotLowerable:
+                continue
+            if not isinstance(new, TreePlan) or new.layout != "pointer":
+                continue
+            if self.kind_ == "classification":
+                if self.method in PROB_METHODS and probs_width(new) != probs_width(plan):
+                    continue
+                _index_outputs(new)
+            self.subs[i] = new
+
+    def _build_multi(self, probs: bool, coff) -> None:
+        """Device argument blocks of the pointer-layout tree segments, one group per accumulator
+        kind (single value / multi-slot), for pmml_tree_pointer_multi."""
+        import torch
+
+        from .plans import TreePlan
+
+        self._multi = []
+        # 16-byte BFS nodes only (the refill / compact / super formats have kernels of their own;
+        # the clamped, masked, uskip and peel loads of the same nodes are bit-identical walks)
+        members = [i for i, p in enumerate(self.subs)
+                   if isinstance(p, TreePlan) and p.layout == "pointer" and p.C <= 16 and
+                   (int(p.variant) & (VAR_POINTER_REFILL | VAR_POINTER_COMPACT | VAR_POINTER_SUPER)) == 0]
+        if len(members) < 2:
+            return
+        for general in (0, 1):
+            idx = [i for i in members if int(self.subs[i].general) == general]
+            if not idx:
+                continue
+            blob = b"".join(bytes(self.subs[i]._args_template(probs)) for i in idx)
+            segs = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(self.device)
+            sidx = torch.tensor(idx, dtype=torch.int32, device=self.device)
+            poff = torch.tensor([int(coff[i]) for i in idx], dtype=torch.int64, device=self.device) if probs else None
+            self._multi.append(dict(general=general, idx=idx, segs=segs, sidx=sidx, poff=poff,
+                                    max_c=max(int(self.subs[i].C) for i in idx)))
+
     def _post_build(self) -> None:
         import torch
 
         self.remaps = [torch.tensor(r, dtype=torch.int64, device=self.device) for r in (self.remap_lists or [])]
+        self._multi = None  # built lazily by the first fused launch (the segments' args templates)
         # the fused reduction kernel's tables (ops/csrc/segment.hip); None -> tensor-op aggregation
         self._red = None
         probs = self.kind_ == "classification" and self.method in PROB_METHODS
@@ -398,7 +454,7 @@ class SegmentedPlan(DevicePlan):
 
         import torch
 
-        from ..ops._lib import SegArgs, check, stream_handle
+        from ..ops._lib import MultiTreeArgs, SegArgs, check, stream_handle
         from .plans import _addr
 
         n = X.shape[0]
@@ -411,7 +467,23 @@ class SegmentedPlan(DevicePlan):
             V = torch.empty((self.n_subs, n), dtype=torch.uint8, device=self.device)
             P = torch.empty(max(1, int(r["coff_h"][-1]) * n), dtype=torch.float32, device=self.device) \
                 if r["probs"] else None
+            done = set()
+            if n and X.shape[1] <= 64 and X.stride(1) == 1 and X.dtype == torch.float32:
+                if self._multi is None:
+                    self._build_multi(r["probs"], r["coff_h"])
+                for g in self._multi:
+                    m = MultiTreeArgs()
+                    m.segs, m.X, m.S, m.V = g["segs"].data_ptr(), X.data_ptr(), S.data_ptr(), V.data_ptr()
+                    m.P = P.data_ptr() if P is not None else None
+                    m.poff = g["poff"].data_ptr() if g["poff"] is not None else None
+                    m.sidx = g["sidx"].data_ptr()
+                    m.n_rows, m.n_feat, m.ldx, m.count = n, X.shape[1], X.stride(0), len(g["idx"])
+                    check(self.lib.pmml_tree_pointer_multi(stream_handle(st), ctypes.byref(m), g["general"],
+                                                           g["max_c"]), "multi-segment tree launch")
+                    done.update(g["idx"])
             for i, plan in enumerate(self.subs):
+                if i in done:
+                    continue
                 kw = {}
                 if r["probs"]:
                     a0, w = int(r["coff_h"][i]) * n, r["widths"][i]

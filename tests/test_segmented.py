@@ -275,3 +275,42 @@ def test_general_model_chain_lowers_to_chain_plan(classification):
         plan = compile_plan(c, torch.device("cpu"))
     assert isinstance(plan, ChainPlan)
     assert plan.columns[4:] == (["p_a", "t2"] if classification else ["t1", "t2"])
+
+
+@pytest.mark.parametrize("classification", [False, True])
+def test_small_tree_segments_share_one_pointer_launch(classification):
+    """Tree segments (few trees in all) are re-lowered on the depth-independent pointer layout and
+    grouped into ONE tree_pointer_multi_kernel launch (grid.z = segment): with the fused reduction
+    a segmented batch is 2 launches, not K + 1."""
+    import ctypes
+
+    from flink_jpmml_amd.ops._lib import TreeArgs
+    from flink_jpmml_amd.runtime.plans import TreePlan
+
+    c = CompiledPmml.from_string(segmented_pmml("max" if classification else "selectFirst", classification,
+                                                n_segments=5, n_classes=3, seed=4))
+    with lowering_dry_run():
+        plan = compile_plan(c, torch.device("cpu"))
+    assert isinstance(plan, SegmentedPlan) and plan.n_subs == 5
+    assert all(isinstance(p, TreePlan) and p.layout == "pointer" for p in plan.subs)
+    coff = np.arange(6) * 3
+    plan._build_multi(classification, coff)
+    assert sum(len(g["idx"]) for g in plan._multi) == 5
+    for g in plan._multi:
+        assert g["segs"].numel() == len(g["idx"]) * ctypes.sizeof(TreeArgs)
+        assert g["sidx"].tolist() == g["idx"]
+        if classification:
+            assert g["poff"].tolist() == [int(coff[i]) for i in g["idx"]]
+
+
+def test_large_tree_segments_keep_their_own_layout(monkeypatch):
+    """Segments with more trees in all than MULTI_MAX_TREES keep their per-segment (perfect /
+    wide) launches."""
+    from flink_jpmml_amd.runtime import segmented
+
+    monkeypatch.setattr(segmented, "MULTI_MAX_TREES", 3)
+    c = CompiledPmml.from_string(segmented_pmml("selectFirst", False, n_segments=5, seed=4))
+    with lowering_dry_run():
+        plan = compile_plan(c, torch.device("cpu"))
+    assert isinstance(plan, SegmentedPlan)
+    assert not any(getattr(p, "layout", None) == "pointer" for p in plan.subs)
