@@ -132,15 +132,15 @@ __device__ __forceinline__ void glds16(const void* g, void* lds) {
 // LDS busy -40 %, same wall time in this barrier-bound loop, profiles/r3ak).
 __device__ __forceinline__ int swz(int r) { return (r >> 1) & 7; }
 
-template <int NROWS>
+template <int NROWS, int NW = 8>
 __device__ __forceinline__ void stage_slice(const unsigned char* src, size_t ldb, size_t kb0, unsigned char* img,
                                             int wave, int lane) {
   constexpr int NINSTR = NROWS / 8;
-  constexpr int PER_WAVE = (NINSTR + 7) / 8;
+  constexpr int PER_WAVE = (NINSTR + NW - 1) / NW;
 #pragma unroll
   for (int i = 0; i < PER_WAVE; ++i) {
     const int q = wave * PER_WAVE + i;
-    if (NINSTR % 8 == 0 || q < NINSTR) {
+    if (NINSTR % NW == 0 || q < NINSTR) {
       const int p = q * 64 + lane;
       const int r = p >> 3;
       const int c = (p & 7) ^ swz(r);
@@ -239,51 +239,6 @@ __device__ __forceinline__ void decode_row(const GemmArgs& a, int row, const flo
   }
 }
 
-// Hidden-layer epilogue through LDS (bf16, 256 x 256 tile): the tile is assembled in LDS (rows
-// padded to 528 B so the two lane halves' rows land on different banks), then every thread stores
-// whole 16-byte chunks of contiguous rows — 16 store instructions per thread instead of 128
-// two-unit stores. Pays off when the layer is store-bound (K <= 128: the first hidden layer over
-// a narrow input); for K = 1024 the direct stores drain behind the MFMAs of other waves (r3l).
-constexpr int EPI_LD = 528;  // bytes per staged row
-constexpr size_t EPI_LDS = (size_t)BM * EPI_LD;
-
-template <int ACT>
-__device__ __forceinline__ void store_hidden_lds(const GemmArgs& a, const f32x16 (&acc)[4][2], int row0, int col0,
-                                                 int wm, int wn, int lane, int tid, unsigned char* smem) {
-  constexpr int TM = 4, TN = 2;
-  const int h = lane >> 5, l32 = lane & 31;
-  __syncthreads();  // every wave is done reading the staging buffers
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int ul = (wn * TN + j) * 32 + l32;  // unit within the tile
-    const float b = a.bias[col0 + ul];
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int rb = (wm * TM + i) * 32 + 4 * h;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float v = act_of<ACT>(acc[i][j][r] + b, a.act, a.thr);
-        const float o = __shfl_xor(v, 1);
-        if ((lane & 1) == 0) {
-          const uint32_t lo = __builtin_bit_cast(uint16_t, (__bf16)v);
-          const uint32_t hi = __builtin_bit_cast(uint16_t, (__bf16)o);
-          const int row = rb + (r & 3) + 8 * (r >> 2);
-          *reinterpret_cast<uint32_t*>(smem + row * EPI_LD + 2 * ul) = lo | (hi << 16);
-        }
-      }
-    }
-  }
-  __syncthreads();
-  // 256 rows x 32 chunks of 16 B; thread t: chunk t & 31 of rows (t >> 5) + 16 q
-  const int c = tid & 31;
-#pragma unroll 4
-  for (int q = 0; q < BM / (NT / 32); ++q) {
-    const int row = (tid >> 5) + (NT / 32) * q;
-    const uint4 v = *reinterpret_cast<const uint4*>(smem + row * EPI_LD + 16 * c);
-    *reinterpret_cast<uint4*>(static_cast<__bf16*>(a.C) + (size_t)(row0 + row) * a.ldc + col0 + 8 * c) = v;
-  }
-}
-
 template <int BN, bool HEAD, bool F32>
 __global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmArgs a) {
   constexpr int WM = BN == 256 ? 2 : 8;  // waves along rows
@@ -365,18 +320,6 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmArgs a) {
     __syncthreads();                // ... for every wave before anyone reads / overwrites it
   }
 
-  if constexpr (!HEAD && !F32 && BN == 256) {
-    if (KT <= 2) {  // a store-bound layer (small K, e.g. the first hidden layer): LDS-staged stores
-      switch (a.act) {
-        case A_IDENTITY: store_hidden_lds<A_IDENTITY>(a, acc, row0, col0, wm, wn, lane, tid, smem); break;
-        case A_RELU: store_hidden_lds<A_RELU>(a, acc, row0, col0, wm, wn, lane, tid, smem); break;
-        case A_LOGISTIC: store_hidden_lds<A_LOGISTIC>(a, acc, row0, col0, wm, wn, lane, tid, smem); break;
-        case A_TANH: store_hidden_lds<A_TANH>(a, acc, row0, col0, wm, wn, lane, tid, smem); break;
-        default: store_hidden_lds<-1>(a, acc, row0, col0, wm, wn, lane, tid, smem); break;
-      }
-      return;
-    }
-  }
   if constexpr (!HEAD) {
     switch (a.act) {  // uniform: one unrolled epilogue per common activation
       case A_IDENTITY: store_hidden<A_IDENTITY, TM, TN, F32>(a, acc, row0, col0, wm, wn, lane); break;
@@ -399,6 +342,60 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmArgs a) {
       const int row = row0 + tid;
       if (row < a.rows) decode_row(a, row, zt + tid * HEAD_LD);
     }
+  }
+}
+
+// First hidden layer over a narrow input (bf16, K = 64: one slice). The layer is bound by its
+// output (2 bytes per unit, ~2 GB for 1M rows x 1024 units), not by its 16 MFMAs per wave: the
+// 256 x 256 / 8-wave tile of gemm_kernel holds a whole CU (128 KiB LDS), so every tile's load
+// latency, MFMAs and stores run back to back. Here a 128 x 256 tile on 4 waves (48 KiB LDS,
+// 2 x 4 accumulators per wave) lets three workgroups share a CU — one drains its stores while
+// the others load and multiply.
+constexpr int K64_BM = 128, K64_NT = 256;
+
+__global__ __launch_bounds__(K64_NT, 3) void gemm_k64_kernel(GemmArgs a) {
+  constexpr int TM = 2, TN = 4;  // 2 x 2 waves, 64 rows x 128 units each
+  extern __shared__ __align__(16) unsigned char smem[];
+  unsigned char* As = smem;
+  unsigned char* Bs = smem + K64_BM * SLICE_B;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, l32 = lane & 31;
+  const int n_ct = a.Mp / 256;
+  const int total = (a.rows_p / K64_BM) * n_ct;
+  int t = blockIdx.x;
+  if ((total & 7) == 0) t = (t & 7) * (total >> 3) + (t >> 3);  // XCD-contiguous tile ranges
+  const int row0 = (t / n_ct) * K64_BM;
+  const int col0 = (t % n_ct) * 256;
+  const int wm = wave >> 1, wn = wave & 1;
+  const size_t lda_b = (size_t)a.lda * 2, ldw_b = (size_t)a.ldw * 2;
+  stage_slice<K64_BM, 4>(static_cast<const unsigned char*>(a.A) + (size_t)row0 * lda_b, lda_b, 0, As, wave, lane);
+  stage_slice<256, 4>(static_cast<const unsigned char*>(a.Wt) + (size_t)col0 * ldw_b, ldw_b, 0, Bs, wave, lane);
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x16{};
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+#pragma unroll
+  for (int ks = 0; ks < BK / 16; ++ks) {
+    bf16x8 af[TM], bfr[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) af[i] = frag(As, (wm * TM + i) * 32 + l32, 2 * ks + h);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bfr[j] = frag(Bs, (wn * TN + j) * 32 + l32, 2 * ks + h);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+  }
+  switch (a.act) {
+    case A_IDENTITY: store_hidden<A_IDENTITY, TM, TN, false>(a, acc, row0, col0, wm, wn, lane); break;
+    case A_RELU: store_hidden<A_RELU, TM, TN, false>(a, acc, row0, col0, wm, wn, lane); break;
+    case A_LOGISTIC: store_hidden<A_LOGISTIC, TM, TN, false>(a, acc, row0, col0, wm, wn, lane); break;
+    case A_TANH: store_hidden<A_TANH, TM, TN, false>(a, acc, row0, col0, wm, wn, lane); break;
+    default: store_hidden<-1, TM, TN, false>(a, acc, row0, col0, wm, wn, lane); break;
   }
 }
 
@@ -670,8 +667,7 @@ __global__ __launch_bounds__(256) void nn_head_decode_kernel(GemmArgs a, const f
 template <int BN, bool HEAD, bool F32>
 int launch(hipStream_t stream, const GemmArgs& a) {
   const size_t stage = 2 * (size_t)BM * SLICE_B + 2 * (size_t)BN * SLICE_B;
-  size_t head = HEAD ? (size_t)BM * HEAD_LD * 4 : 0;
-  if (!HEAD && !F32 && BN == 256 && a.K <= 2 * (SLICE_B / 2)) head = EPI_LDS;  // store_hidden_lds
+  const size_t head = HEAD ? (size_t)BM * HEAD_LD * 4 : 0;
   const size_t lds = stage > head ? stage : head;
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_kernel<BN, HEAD, F32>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
@@ -707,7 +703,7 @@ PMML_API int pmml_gemm_launch(hipStream_t stream, const GemmArgs* args, int head
   const GemmArgs a = *args;
   if (a.rows <= 0) return 0;
   const int BN = head ? 32 : 256;
-  if (a.f32 & ~0x81) return -4;
+  if (a.f32 & ~0xC1) return -4;
   // bf16 hidden layers with K >= 512 run the phase-interleaved kernel (profiles/r3ao: 2048 x 2048
   // 8.73 -> 8.36 ms, 1024 x 1024 2.62 -> 2.48 ms over 1M rows); below that the layer is bound by
   // its output writes and the 2-buffer loop is faster (K = 64: 0.83 vs 0.92 ms). Bit 7 forces it.
@@ -718,6 +714,11 @@ PMML_API int pmml_gemm_launch(hipStream_t stream, const GemmArgs* args, int head
   if ((reinterpret_cast<uintptr_t>(a.A) & 15) || (reinterpret_cast<uintptr_t>(a.Wt) & 15)) return -4;
   if (head && (a.n_out < 1 || a.n_out > 32 || a.Mp != 32 || !a.row_ok || !a.score || !a.valid)) return -4;
   if (!head && ((a.ldc & 7) || a.ldc < a.Mp || !a.C || (reinterpret_cast<uintptr_t>(a.C) & 15))) return -4;
+  if (!head && !f32 && a.K == 64 && !((a.f32 >> 6) & 1)) {  // bit 6 forces the 256 x 256 tile
+    hipLaunchKernelGGL(gemm_k64_kernel, dim3((a.rows_p / K64_BM) * (a.Mp / 256)), dim3(K64_NT),
+                       (size_t)(K64_BM + 256) * SLICE_B, stream, a);
+    return hipGetLastError() == hipSuccess ? 0 : -7;
+  }
   const int rc = f32 ? (head ? launch<32, true, true>(stream, a) : launch<256, false, true>(stream, a))
                      : (head ? launch<32, true, false>(stream, a)
                              : (ph8 ? launch8<false>(stream, a, HeadFuse{}) : launch<256, false, false>(stream, a)));

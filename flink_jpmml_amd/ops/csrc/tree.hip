@@ -393,6 +393,113 @@ __global__ __launch_bounds__(TB, 2) void tree_super_kernel(TreeArgs a) {
   finish_row(a, acc, accl, split, GENERAL, row, row_ok && !poisoned);
 }
 
+// RANK3 pointer layout (runtime/hybrid.py::pack_rank3): THREE tree levels per 16-byte record.
+// Split thresholds are replaced by their rank among the feature's sorted unique thresholds: with
+// t_0 < t_1 < ... and rank(x) = #{t_k <= x}, "x >= t_k" <=> "rank(x) >= k + 1" — exact, NaN kept
+// as its own rank (RK_NAN, routed by the node's default-direction bit). A row's ranks are computed
+// once per workgroup (a branchless binary search per feature) into LDS; then a record holds a
+// 3-level subtree (7 nodes: 8-bit rank, 5-bit feature, default-right bit each) plus its exit
+// block, so one 16-byte gather serves three levels (the deep-forest walk is bound by gather
+// instructions / L1 line accesses per visited level, profiles/r3w). Record bits: lo = x | y << 32:
+// rank of node n at 8 n, live-exit mask at 56; hi = z | w << 32: feature of node n at 5 n,
+// default-right at 35 + n, exit block offset (from the tree's base slot) at 42 (21 bits), bit
+// 63 = leaf slot (x = the weighted leaf value, or the leaf row for P > 1). Nodes: 0 the root,
+// 1 / 2 its children, 3..6 the grandchildren; exit e = 4 b0 + 2 b1 + b2 lives at block +
+// popcount(mask below e) (only live exits are stored; a block stays within one 128-byte line).
+// Leaves above the third level are padded with never-right nodes (rank 255). Lock-step walks,
+// leaves accumulated in tree order (bit-identical to tree_pointer_kernel).
+constexpr uint32_t RK_NAN = 255;
+
+template <bool GENERAL, int PILP = 8>
+__global__ __launch_bounds__(TB, 2) void tree_rank3_kernel(TreeArgs a) {
+  extern __shared__ __align__(16) uint32_t smem[];
+  float* feat = reinterpret_cast<float*>(smem);
+  int* bad = reinterpret_cast<int*>(smem + a.n_feat * TB);
+  float* accl = reinterpret_cast<float*>(bad + TB);
+  uint16_t* rk = reinterpret_cast<uint16_t*>(accl + (GENERAL ? a.C * TB : 0));  // [F][TB]
+  const int tid = threadIdx.x;
+  const int2 blk = tree_block(a);
+  const int row0 = blk.x * TB;
+  const int split = blk.y;
+  const int row = row0 + tid;
+  stage_rows_T<TB>(a.X, a.n_rows, a.n_feat, a.ldx, a.prep, feat, bad, row0);
+  bool row_ok = bad[tid] == 0;
+  if (a.row_valid_in && row < a.n_rows) row_ok = row_ok && a.row_valid_in[row];
+  // ranks of this lane's row (only this lane reads them back: no barrier)
+  for (int f = 0; f < a.n_feat; ++f) {
+    const float x = feat[f * TB + tid];
+    const int cnt = a.rank_cnt[f];
+    const float* t = a.rank_thr + (size_t)f * a.rank_stride;
+    int pos = 0;  // #{t_k <= x}
+    for (int step = 128; step > 0; step >>= 1)
+      if (pos + step <= cnt && t[pos + step - 1] <= x) pos += step;
+    rk[f * TB + tid] = (uint16_t)(x != x ? RK_NAN : (uint32_t)pos);
+  }
+  const uint16_t* rk_lane = rk + tid;
+  const uint4* nodes = reinterpret_cast<const uint4*>(a.blob);
+  const uint32_t* roots = reinterpret_cast<const uint32_t*>(a.roots);
+  const int tb = split * a.trees_per_split;
+  const int te = min(a.n_trees, tb + a.trees_per_split);
+  if (GENERAL) {
+    for (int c = 0; c < a.C; ++c) accl[c * TB + tid] = 0.f;
+  }
+  float acc = 0.f;
+  for (int t0 = tb; t0 < te; t0 += PILP) {
+    const int nt = min(PILP, te - t0);
+    int pos[PILP], base[PILP];
+    uint32_t leafv[PILP];
+    bool act[PILP];
+#pragma unroll
+    for (int i = 0; i < PILP; ++i) {
+      base[i] = i < nt ? (int)roots[t0 + i] : 0;
+      pos[i] = base[i];
+      act[i] = i < nt;
+      leafv[i] = 0u;
+    }
+    bool live = nt > 0;
+    while (live) {
+      uint4 nd[PILP];
+#pragma unroll
+      for (int i = 0; i < PILP; ++i) nd[i] = nodes[act[i] ? pos[i] : 0];
+      live = false;
+#pragma unroll
+      for (int i = 0; i < PILP; ++i) {
+        const uint64_t lo = (uint64_t)nd[i].x | ((uint64_t)nd[i].y << 32);
+        const uint64_t hi = (uint64_t)nd[i].z | ((uint64_t)nd[i].w << 32);
+        const bool leaf = (nd[i].w >> 31) != 0u;
+        auto go_right = [&](int n) -> int {
+          const uint32_t f = (uint32_t)(hi >> (5 * n)) & 31u;
+          const uint32_t r = (uint32_t)(lo >> (8 * n)) & 255u;
+          const uint32_t d = (uint32_t)(hi >> (35 + n)) & 1u;
+          const uint32_t k = rk_lane[f * TB];
+          return (int)(k == RK_NAN ? d : (uint32_t)(k >= r));
+        };
+        const int b0 = go_right(0);
+        const int b1 = go_right(1 + b0);
+        const int b2 = go_right(3 + 2 * b0 + b1);
+        const int e = 4 * b0 + 2 * b1 + b2;
+        const uint32_t below = (nd[i].y >> 24) & ((1u << e) - 1u);  // live exits before e
+        const int nxt = base[i] + (int)((hi >> 42) & 0x1FFFFFu) + __popc(below);
+        leafv[i] = (act[i] && leaf) ? nd[i].x : leafv[i];
+        pos[i] = (act[i] && !leaf) ? nxt : pos[i];
+        act[i] = act[i] && !leaf;
+        live = live || act[i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < PILP; ++i) {
+      if (i >= nt) break;
+      if (GENERAL) {
+        const int slot = a.tree_slot[t0 + i];
+        for (int p = 0; p < a.P; ++p) accl[(slot + p) * TB + tid] += a.leaves[(size_t)leafv[i] * a.P + p];
+      } else {
+        acc += __uint_as_float(leafv[i]);
+      }
+    }
+  }
+  finish_row(a, acc, accl, split, GENERAL, row, row_ok);
+}
+
 // Pointer layout, refill schedule. The lock-step kernel above runs each group of PILP walks until
 // the deepest of its 64 x PILP walks ends: at depth 14 with ~6-level average paths most lanes idle
 // through half of every group. Here each of a lane's PILP slots is a work queue over the tree
@@ -747,11 +854,27 @@ PMML_API int pmml_tree_launch(hipStream_t stream, const TreeArgs* args, int layo
   } else {
     if (a.variant != 0 && a.variant != VAR_POINTER_REFILL && a.variant != VAR_POINTER_COMPACT &&
         a.variant != VAR_POINTER_MASKED && a.variant != VAR_POINTER_SUPER && a.variant != VAR_POINTER_USKIP &&
-        a.variant != VAR_POINTER_PEEL)
+        a.variant != VAR_POINTER_PEEL && a.variant != VAR_POINTER_RANK3)
       return -10;
     const bool feat_lds = a.n_feat <= 64;
     size_t lds = (feat_lds ? (size_t)a.n_feat * TB * 4 : 0) + TB * 4 + acc_lds;
-    if (a.variant == VAR_POINTER_SUPER) {
+    if (a.variant == VAR_POINTER_RANK3) {
+      if (a.n_feat > 32 || !a.rank_thr || !a.rank_cnt || a.rank_stride < 1 || a.rank_stride > 254) return -4;
+      lds += (size_t)a.n_feat * TB * 2;  // rank planes
+      if (a.general) {
+        err = prepare_launch(tree_rank3_kernel<true>, lds);
+        if (!err) hipLaunchKernelGGL((tree_rank3_kernel<true>), grid, dim3(TB), lds, stream, a);
+      } else if (a.pilp == 16) {
+        err = prepare_launch(tree_rank3_kernel<false, 16>, lds);
+        if (!err) hipLaunchKernelGGL((tree_rank3_kernel<false, 16>), grid, dim3(TB), lds, stream, a);
+      } else if (a.pilp == 4) {
+        err = prepare_launch(tree_rank3_kernel<false, 4>, lds);
+        if (!err) hipLaunchKernelGGL((tree_rank3_kernel<false, 4>), grid, dim3(TB), lds, stream, a);
+      } else {
+        err = prepare_launch(tree_rank3_kernel<false>, lds);
+        if (!err) hipLaunchKernelGGL((tree_rank3_kernel<false>), grid, dim3(TB), lds, stream, a);
+      }
+    } else if (a.variant == VAR_POINTER_SUPER) {
       if (a.n_feat > 32) return -4;  // 5-bit feature fields
       if (a.general) {
         err = prepare_launch(tree_super_kernel<true>, lds);

@@ -70,6 +70,9 @@ struct TreeArgs {
   int rows_wide, mode;          // wide kernel: rows per workgroup (256/128/64), accumulation mode
   int n_stage, pilp;            // wide kernel: staged feature columns; pointer kernel: walks per lane (4/8/16)
   unsigned long long* prof;     // nullable: per-wave phase ticks of one workgroup ([16][4], s_memtime)
+  const float* rank_thr;        // RANK3 pointer layout: per feature, its sorted unique split thresholds
+  const int* rank_cnt;          // ... and their count (<= 254); row f of rank_thr starts at f * rank_stride
+  int rank_stride, pad1;
 };
 constexpr int VAR_NAN_FAST = 4;    // wide kernel: take the fast path even on tiles with missing values
 constexpr int VAR_NAN_PLANES = 8;  // ... via blob_nan + a second feature plane (NaN -> +inf)
@@ -79,6 +82,7 @@ constexpr int VAR_POINTER_MASKED = 64;  // pointer layout, lock-step sums: exec-
 constexpr int VAR_POINTER_SUPER = 128;  // pointer layout: two levels per 16-byte slot (tree.hip::tree_super_kernel)
 constexpr int VAR_POINTER_USKIP = 256;  // pointer layout, lock-step: wave-uniform skip of finished walk slots
 constexpr int VAR_POINTER_PEEL = 512;   // pointer layout, lock-step: top two levels from uniform (scalar) loads
+constexpr int VAR_POINTER_RANK3 = 1024; // pointer layout: three levels per 16-byte record on threshold ranks (tree.hip)
 
 // per-depth launchers (tree_d<D>.hip)
 #define PMML_TREE_DECL(D) int launch_perfect_d##D(hipStream_t st, const TreeArgs& a, dim3 grid, size_t lds);

@@ -471,3 +471,160 @@ def pack_super(trees, weights: List[float], P: int):
 
 
 __all__ += ["pack_compact_bfs", "pack_super"]
+
+
+# ------------------------------------------------------------------------------------------------
+# RANK3: three tree levels per 16-byte record on per-feature threshold ranks (tree.hip
+# tree_rank3_kernel). Record bits — lo = words 0-1: rank of node n (8 bits) at 8 n, live-exit mask
+# at 56 (8 bits); hi = words 2-3: feature of node n (5 bits) at 5 n, default-right of node n at
+# 35 + n, exit block offset from the tree's base slot at 42 (21 bits), bit 63 = leaf slot (word 0
+# = weighted value / leaf row). Only the live exits of a record are stored: exit e sits at
+# block + popcount(mask & ((1 << e) - 1)); a block never straddles a 128-byte line.
+RK_NAN = 255        # a missing value's rank (csrc RK_NAN)
+RK_NEVER = 255      # a padding node's rank: never "right" (ranks of values are <= 254)
+RK_MAX_UNIQUE = 254
+RK_LINE = 8         # 16-byte slots per 128-byte line
+RK_OFF_BITS = 21
+
+
+def rank_tables(trees, n_features: int):
+    """Per feature: the sorted unique canonical (fp32, "go right iff x >= T") thresholds of every
+    split. Returns ``(uniq list, thr [F, stride] f32, cnt [F] i32)``; ``ValueError`` beyond
+    RK_MAX_UNIQUE thresholds on a feature (XGBoost / LightGBM histogram models have <= 255 bins)."""
+    from .plans import _canonical_vec
+
+    per = [[] for _ in range(n_features)]
+    for t in trees:
+        feat = np.asarray(t.feature, dtype=np.int64)
+        internal = feat >= 0
+        if not internal.any():
+            continue
+        T, _ = _canonical_vec(np.asarray(t.op)[internal], np.asarray(t.threshold, dtype=np.float64)[internal])
+        for f in np.unique(feat[internal]):
+            per[int(f)].append(T[feat[internal] == f])
+    uniq = [np.unique(np.concatenate(p)).astype(np.float32) if p else np.zeros(0, np.float32) for p in per]
+    cnt = np.array([u.size for u in uniq], dtype=np.int32)
+    if cnt.size and cnt.max() > RK_MAX_UNIQUE:
+        raise ValueError(f"rank3 layout: {int(cnt.max())} unique thresholds on one feature (max {RK_MAX_UNIQUE})")
+    stride = max(1, int(cnt.max()) if cnt.size else 1)
+    thr = np.full((n_features, stride), np.inf, dtype=np.float32)
+    for f, u in enumerate(uniq):
+        thr[f, : u.size] = u
+    return uniq, thr, cnt
+
+
+def pack_rank3(trees, weights: List[float], P: int, n_features: int):
+    """RANK3 records of every tree: per tree, slot 0 is the root record (or the root leaf slot),
+    then the exit blocks in breadth-first order; a record's block holds its live exits (the next
+    records and leaf slots) and never straddles a 128-byte line.
+
+    Returns ``(nodes [n, 4] u32, leaves [n_leaves, P] f32 or None, roots [n_trees] i32 (base slot of
+    each tree), thr [F, stride] f32, cnt [F] i32, has_dr)``; ``ValueError`` when a feature index
+    is >= 32, a feature has more than 254 unique thresholds, a tree is null-on-missing or needs
+    more than 2^21 slots."""
+    from .plans import _canonical_vec
+
+    if n_features > 32:
+        raise ValueError("rank3 layout: more than 32 features")
+    if any(t.null_missing for t in trees):
+        raise ValueError("rank3 layout: null-on-missing trees")
+    uniq, thr, cnt = rank_tables(trees, n_features)
+    slots_all: List[np.ndarray] = []
+    leaves_all: List[np.ndarray] = []
+    roots = np.zeros(len(trees), dtype=np.int32)
+    total = n_leaf = 0
+    has_dr = False
+    for ti, (t, w) in enumerate(zip(trees, weights)):
+        feat = np.asarray(t.feature, dtype=np.int64)
+        internal = feat >= 0
+        T, swap = _canonical_vec(np.asarray(t.op), np.asarray(t.threshold, dtype=np.float64))
+        left, right = np.asarray(t.left, dtype=np.int64), np.asarray(t.right, dtype=np.int64)
+        lc = np.where(swap, right, left)
+        rc = np.where(swap, left, right)
+        dr = np.where(swap, np.asarray(t.default_left, bool), ~np.asarray(t.default_left, bool)) & internal
+        has_dr = has_dr or bool(dr.any())
+        rank = np.zeros(feat.shape[0], dtype=np.uint64)
+        for k in np.nonzero(internal)[0]:
+            rank[k] = int(np.searchsorted(uniq[int(feat[k])], T[k])) + 1
+        n_slots = 1  # slot 0: the root
+        slots = {}
+
+        def leaf_slot(k: int) -> np.ndarray:
+            nonlocal n_leaf
+            s = np.zeros(4, dtype=np.uint32)
+            if P == 1:
+                s[0] = np.float32(float(t.leaf_value[k]) * w).view(np.uint32)
+            else:
+                s[0] = n_leaf
+                leaves_all.append(np.asarray(t.leaf_probs[k], dtype=np.float64)[:P] * w)
+                n_leaf += 1
+            s[3] = np.uint32(1 << 31)
+            return s
+
+        queue = [(0, 0)]  # (node, slot)
+        while queue:
+            k, s = queue.pop(0)
+            if not internal[k]:
+                slots[s] = leaf_slot(k)
+                continue
+            # the 7 nodes of this record: ("n", node) a real split, ("p", leaf) a never-right pad
+            # carrying a leaf down its left side, ("x", -1) a pad nobody reaches
+            def below(entries):
+                out = []
+                for kind, v in entries:
+                    if kind == "n":
+                        out += [("n", int(c)) if internal[c] else ("p", int(c)) for c in (lc[v], rc[v])]
+                    elif kind == "p":
+                        out += [("p", v), ("x", -1)]
+                    else:
+                        out += [("x", -1), ("x", -1)]
+                return out
+
+            lvl1 = below([("n", k)])
+            lvl2 = below(lvl1)
+            nodes7 = [("n", k)] + lvl1 + lvl2
+            exits = []
+            for kind, v in lvl2:  # exit e = 2 * (third-level entry) + right
+                if kind == "n":
+                    exits += [int(lc[v]), int(rc[v])]
+                elif kind == "p":
+                    exits += [v, -1]
+                else:
+                    exits += [-1, -1]
+            live = [c for c in exits if c >= 0]
+            mask = sum(1 << e for e, c in enumerate(exits) if c >= 0)
+            if n_slots % RK_LINE + len(live) > RK_LINE:  # keep the block inside one line
+                n_slots += RK_LINE - n_slots % RK_LINE
+            base = n_slots
+            n_slots += len(live)
+            if base >= (1 << RK_OFF_BITS):
+                raise ValueError("rank3 layout: tree needs more than 2^21 slots")
+            lo = mask << 56
+            hi = 0
+            for n, (kind, v) in enumerate(nodes7):
+                if kind == "n":
+                    lo |= int(rank[v]) << (8 * n)
+                    hi |= int(feat[v]) << (5 * n)
+                    hi |= int(dr[v]) << (35 + n)
+                else:
+                    lo |= RK_NEVER << (8 * n)
+            hi |= base << 42
+            rec = np.array([lo & 0xFFFFFFFF, lo >> 32, hi & 0xFFFFFFFF, hi >> 32], dtype=np.uint64).astype(np.uint32)
+            slots[s] = rec
+            for j, c in enumerate(live):
+                queue.append((c, base + j))
+        n_slots += (-n_slots) % RK_LINE  # the next tree starts on a line
+        arr = np.zeros((n_slots, 4), dtype=np.uint32)
+        for s, v in slots.items():
+            arr[s] = v
+        roots[ti] = total
+        total += n_slots
+        if total >= (1 << 31):
+            raise ValueError("rank3 layout: more than 2^31 slots")
+        slots_all.append(arr)
+    nodes = np.concatenate(slots_all) if slots_all else np.zeros((1, 4), np.uint32)
+    leaves = np.stack(leaves_all).astype(np.float32) if leaves_all else None
+    return nodes, leaves, roots, thr, cnt, has_dr
+
+
+__all__ += ["pack_rank3", "rank_tables"]

@@ -1071,6 +1071,7 @@ VAR_NAN_FAST, VAR_NAN_PLANES, VAR_POINTER_REFILL, VAR_POINTER_COMPACT, VAR_POINT
 VAR_POINTER_SUPER = 128
 VAR_POINTER_USKIP = 256
 VAR_POINTER_PEEL = 512
+VAR_POINTER_RANK3 = 1024
 DYN_B, DYN_SLOTS = 8, 16  # csrc: MODE_SUM trees per claimed batch, batch slots per chunk
 
 
@@ -1213,7 +1214,7 @@ class TreePlan(DevicePlan):
                                   "variant", "children", "preds", "pool", "trees_tab", "max_steps", "blob_nan",
                                   "chunk_trees_nan", "full_epi", "labels", "mode", "tree_w", "acc_init", "feat_map",
                                   "rows_wide", "n_stage", "heads", "head_depth", "pointer_ilp", "xcd_split",
-                                  "tail_format")
+                                  "tail_format", "rank_thr", "rank_cnt", "rank_stride")
 
     WIDE_G = 4  # tree groups of the wide kernel (mirrors csrc)
 
@@ -1270,6 +1271,7 @@ class TreePlan(DevicePlan):
         if pointer_schedule not in ("refill", "lockstep"):
             raise ValueError("pointer_schedule must be 'refill' or 'lockstep'")
         self.heads, self.head_depth = None, 0  # hybrid layout only
+        self.rank_thr, self.rank_cnt, self.rank_stride = None, None, 0  # rank3 node format only
         if pointer_load not in ("clamped", "masked", "uskip", "peel"):
             raise ValueError("pointer_load must be 'clamped', 'masked', 'uskip' or 'peel'")
         if hybrid_tail not in ("compact", "wide"):
@@ -1481,8 +1483,22 @@ class TreePlan(DevicePlan):
                         self.layout, H, heads, self.chunk_trees = "pointer", 0, None, 0
             else:
                 self.chunk_trees = 0
-            compact = superl = False
-            if node_format == "super":
+            compact = superl = rank3 = False
+            if node_format == "rank3":
+                if heads is not None or not feat_lds or pointer_schedule != "lockstep" or F > 32:
+                    raise NotLowerable("rank3 pointer layout needs <= 32 features in LDS and the lock-step walk")
+                from .hybrid import pack_rank3
+
+                try:
+                    nodes, leaves, roots, rthr, rcnt, has_dr = pack_rank3(spec.trees, spec.weights, spec.P, F)
+                except ValueError as e:
+                    raise NotLowerable(f"rank3 pointer layout: {e}") from e
+                rank3 = True
+                self.rank_thr, self.rank_cnt = self._t(rthr.reshape(-1)), self._t(rcnt)
+                self.rank_stride = int(rthr.shape[1])
+                if leaves is None:
+                    leaves = np.zeros((1, 1), np.float32)
+            elif node_format == "super":
                 if heads is not None or not feat_lds or pointer_schedule != "lockstep" or F > 32:
                     raise NotLowerable("super pointer layout needs <= 32 features in LDS and the lock-step walk")
                 try:
@@ -1505,7 +1521,7 @@ class TreePlan(DevicePlan):
                         raise NotLowerable("compact pointer layout does not apply")
             elif node_format == "compact":
                 raise NotLowerable("compact pointer layout needs features in LDS, lock-step, bfs")
-            if heads is None and not compact and not superl:
+            if heads is None and not compact and not superl and not rank3:
                 _, nodes, leaves, roots, has_dr = pack_trees(spec.trees, spec.weights, spec.P, 0, feat_lds,
                                                              order=node_order)
             self.blob_nan, self.chunk_trees_nan = None, 0
@@ -1514,7 +1530,9 @@ class TreePlan(DevicePlan):
             # pointer walks: refill schedule (each PILP slot restarts on the next tree as soon as
             # its walk ends) unless pinned to the lock-step kernel's tree-order sums
             self.variant = VAR_POINTER_REFILL if (self.layout == "pointer" and pointer_schedule == "refill") else 0
-            if superl:
+            if rank3:
+                self.variant = VAR_POINTER_RANK3
+            elif superl:
                 self.variant = VAR_POINTER_SUPER
             elif compact:
                 self.variant = VAR_POINTER_COMPACT
@@ -1619,6 +1637,8 @@ class TreePlan(DevicePlan):
             a.n_stage = getattr(self, "n_stage", self.n_features)
             a.pilp = getattr(self, "pointer_ilp", 8)
             a.prof = ptr(getattr(self, "prof", None))  # kbench --tree-prof phase timers (nullable)
+            a.rank_thr, a.rank_cnt = ptr(getattr(self, "rank_thr", None)), ptr(getattr(self, "rank_cnt", None))
+            a.rank_stride = int(getattr(self, "rank_stride", 0) or 0)
             a.epi = _epilogue(table=self.table, write_probs=with_probs, **self.epi_args)
             cache[with_probs] = a
         # one mutable copy per thread, reused across launches: the C launcher copies the struct

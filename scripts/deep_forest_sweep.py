@@ -17,6 +17,9 @@ CONFIGS = {
     "pointer+xcd": dict(layout="pointer", xcd_split="on"),
     "pointer+masked": dict(layout="pointer", pointer_load="masked"),
     "super": dict(layout="pointer", node_format="super"),
+    "rank3": dict(layout="pointer", node_format="rank3"),
+    "rank3_4": dict(layout="pointer", node_format="rank3", pointer_ilp=4),
+    "rank3_16": dict(layout="pointer", node_format="rank3", pointer_ilp=16),
     "super+xcd": dict(layout="pointer", node_format="super", xcd_split="on"),
     "super16": dict(layout="pointer", node_format="super", pointer_ilp=16),
     "super4": dict(layout="pointer", node_format="super", pointer_ilp=4),

@@ -214,3 +214,21 @@ def test_fused_output_layer_matches_separate_launch(gpu, shape):
         scale = max(1.0, float(np.abs(ref[v]).max()))
         assert np.abs(s1[v] - s0[v]).max() < 1e-4 * scale
         assert np.abs(s1[v] - ref[v]).max() < 3e-2 * scale
+
+
+@pytest.mark.gpu
+def test_k64_first_layer_kernel_matches_256_tile(gpu):
+    """The 128 x 256 / 4-wave first-layer kernel (gemm_k64_kernel, 3 workgroups per CU) runs the
+    same MFMAs in the same k order as the 256 x 256 tile: identical bits (flag bit 6 forces the
+    latter)."""
+    c = CompiledPmml.from_string(mlp_pmml(n_features=32, hidden=(1024, 512), seed=13))
+    plan = c.plan(gpu, precision="bf16", mlp_impl="wide")
+    assert plan.dims[0][0] == 64
+    X = stream_matrix(9000, 32, seed=6, missing_rate=0.01)
+    s0, v0 = plan.score(X)
+    plan.gemm_flags = 0x40
+    try:
+        s1, v1 = plan.score(X)
+    finally:
+        plan.gemm_flags = 0
+    assert torch.equal(v0, v1) and torch.equal(s0[v0.bool()], s1[v1.bool()])
