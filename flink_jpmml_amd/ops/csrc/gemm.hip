@@ -351,9 +351,13 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmArgs a) {
 // latency, MFMAs and stores run back to back. Here a 128 x 256 tile on 4 waves (48 KiB LDS,
 // 2 x 4 accumulators per wave) lets three workgroups share a CU — one drains its stores while
 // the others load and multiply.
+// PREP: the input stage fused in (nn_prep_kernel's gather, NormContinuous, missing values, bf16 and
+// row validity): the A tile is built from the raw records straight into the swizzled LDS image
+// (no [rows, 64] bf16 round trip through HBM, no separate launch); column tile 0 writes row_ok.
 constexpr int K64_BM = 128, K64_NT = 256;
 
-__global__ __launch_bounds__(K64_NT, 3) void gemm_k64_kernel(GemmArgs a) {
+template <bool PREP>
+__global__ __launch_bounds__(K64_NT, PREP ? 2 : 3) void gemm_k64_kernel(GemmArgs a, PrepArgs p) {
   constexpr int TM = 2, TN = 4;  // 2 x 2 waves, 64 rows x 128 units each
   extern __shared__ __align__(16) unsigned char smem[];
   unsigned char* As = smem;
@@ -368,8 +372,37 @@ __global__ __launch_bounds__(K64_NT, 3) void gemm_k64_kernel(GemmArgs a) {
   const int col0 = (t % n_ct) * 256;
   const int wm = wave >> 1, wn = wave & 1;
   const size_t lda_b = (size_t)a.lda * 2, ldw_b = (size_t)a.ldw * 2;
-  stage_slice<K64_BM, 4>(static_cast<const unsigned char*>(a.A) + (size_t)row0 * lda_b, lda_b, 0, As, wave, lane);
   stage_slice<256, 4>(static_cast<const unsigned char*>(a.Wt) + (size_t)col0 * ldw_b, ldw_b, 0, Bs, wave, lane);
+  if constexpr (PREP) {
+    // item it = row r (of the tile) x 8-input chunk c; a row's 8 chunks are 8 consecutive lanes
+#pragma unroll 1
+    for (int q = 0; q < K64_BM * 8 / K64_NT; ++q) {
+      const int it = tid + K64_NT * q;
+      const int r = it >> 3, c = it & 7;
+      const int row = row0 + r;
+      const bool live = row < p.n_rows;
+      const float* x = p.X + (size_t)(live ? row : 0) * p.ldx;
+      bool bad = false;
+      bf16x8 b;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = 8 * c + j;
+        float z = 0.f;
+        if (live && k < p.n_in) {
+          const float xv = x[p.in_index[k]];
+          z = xv == xv ? fmaf(xv, p.in_scale[k], p.in_shift[k]) : p.in_missing[k];
+          bad = bad || (z != z);
+          z = z == z ? z : 0.f;
+        }
+        b[j] = (__bf16)z;
+      }
+      *reinterpret_cast<bf16x8*>(As + r * SLICE_B + (((c ^ swz(r)) & 7) << 4)) = b;
+      const unsigned long long m = __ballot(bad);
+      if (col0 == 0 && c == 0) p.row_ok[row] = (live && ((m >> (lane & ~7)) & 0xFFull) == 0) ? 1 : 0;
+    }
+  } else {
+    stage_slice<K64_BM, 4>(static_cast<const unsigned char*>(a.A) + (size_t)row0 * lda_b, lda_b, 0, As, wave, lane);
+  }
   f32x16 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -715,8 +748,8 @@ PMML_API int pmml_gemm_launch(hipStream_t stream, const GemmArgs* args, int head
   if (head && (a.n_out < 1 || a.n_out > 32 || a.Mp != 32 || !a.row_ok || !a.score || !a.valid)) return -4;
   if (!head && ((a.ldc & 7) || a.ldc < a.Mp || !a.C || (reinterpret_cast<uintptr_t>(a.C) & 15))) return -4;
   if (!head && !f32 && a.K == 64 && !((a.f32 >> 6) & 1)) {  // bit 6 forces the 256 x 256 tile
-    hipLaunchKernelGGL(gemm_k64_kernel, dim3((a.rows_p / K64_BM) * (a.Mp / 256)), dim3(K64_NT),
-                       (size_t)(K64_BM + 256) * SLICE_B, stream, a);
+    hipLaunchKernelGGL((gemm_k64_kernel<false>), dim3((a.rows_p / K64_BM) * (a.Mp / 256)), dim3(K64_NT),
+                       (size_t)(K64_BM + 256) * SLICE_B, stream, a, PrepArgs{});
     return hipGetLastError() == hipSuccess ? 0 : -7;
   }
   const int rc = f32 ? (head ? launch<32, true, true>(stream, a) : launch<256, false, true>(stream, a))
@@ -745,5 +778,21 @@ PMML_API int pmml_gemm_fused_head_launch(hipStream_t stream, const GemmArgs* hid
   int rc = launch8<true>(stream, a, hf);
   if (rc) return rc;
   hipLaunchKernelGGL(nn_head_decode_kernel, dim3((a.rows + 255) / 256), dim3(256), 0, stream, o, part, a.Mp / 256);
+  return hipGetLastError() == hipSuccess ? 0 : -7;
+}
+
+// Input stage + first hidden layer in one launch (gemm_k64_kernel<true>): bf16, K = k0 = 64 (at
+// most 64 network inputs), hidden-layer output C; p->row_ok receives the row validity as
+// pmml_nn_prep_launch would (p->H is not written).
+PMML_API int pmml_nn_first_layer_launch(hipStream_t stream, const GemmArgs* args, const PrepArgs* prep) {
+  const GemmArgs a = *args;
+  const PrepArgs p = *prep;
+  if (a.rows <= 0) return 0;
+  if ((a.f32 & 1) || p.f32 != 0 || a.K != 64 || p.k0 != 64 || p.n_in > 64 || p.n_in < 0) return -4;
+  if (a.rows_p % 256 || a.rows_p < a.rows || p.rows_p != a.rows_p || p.n_rows != a.rows) return -4;
+  if (a.Mp % 256 || a.Mp <= 0 || (a.ldw & 7) || a.ldw < a.K || (reinterpret_cast<uintptr_t>(a.Wt) & 15)) return -4;
+  if ((a.ldc & 7) || a.ldc < a.Mp || !a.C || (reinterpret_cast<uintptr_t>(a.C) & 15) || !p.row_ok || !p.X) return -4;
+  hipLaunchKernelGGL((gemm_k64_kernel<true>), dim3((a.rows_p / K64_BM) * (a.Mp / 256)), dim3(K64_NT),
+                     (size_t)(K64_BM + 256) * SLICE_B, stream, a, p);
   return hipGetLastError() == hipSuccess ? 0 : -7;
 }

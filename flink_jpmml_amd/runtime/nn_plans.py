@@ -422,6 +422,15 @@ class WideMlpPlan(MlpPlan):
     def _fused_head(self) -> bool:
         return bool(self.fuse_head) and self.bf16 == 1 and len(self.dims) >= 2 and self.dims[-2][0] % 64 == 0
 
+    # bf16, <= 64 network inputs: the input stage runs inside the first layer's GEMM (gemm_k64_kernel<true>)
+    fuse_input = True
+
+    def _fused_input(self, fused_head: bool) -> bool:
+        """The first layer is a hidden layer launched on its own (not the fused last hidden layer)."""
+        n_hidden = len(self.dims) - 1
+        return (bool(self.fuse_input) and self.bf16 == 1 and self.k0 == 64 and self.gemm_flags == 0 and
+                n_hidden >= 1 and not (fused_head and n_hidden == 1))
+
     def _head_weights(self):
         """The output layer's weights [32, K] with k permuted inside every 32-unit group as the
         fused epilogue consumes them: storage position 16 s + 8 h + e of a group holds unit
@@ -466,9 +475,11 @@ class WideMlpPlan(MlpPlan):
         p.in_index, p.in_scale, p.in_shift = ptr(self.in_index), ptr(self.in_scale), ptr(self.in_shift)
         p.in_missing, p.H, p.ldh, p.k0, p.row_ok = ptr(self.in_missing), H0.data_ptr(), self.k0, self.k0, ok.data_ptr()
         p.f32 = 1 - self.bf16
-        check(self.lib.pmml_nn_prep_launch(h, ctypes.byref(p)), "nn input stage")
-        wbase, bbase, es = self.wts.data_ptr(), self.bss.data_ptr(), 2 if self.bf16 else 4
         fused = self._fused_head()
+        first = self._fused_input(fused)
+        if not first:
+            check(self.lib.pmml_nn_prep_launch(h, ctypes.byref(p)), "nn input stage")
+        wbase, bbase, es = self.wts.data_ptr(), self.bss.data_ptr(), 2 if self.bf16 else 4
         extra = []
         cur, lda = H0, self.k0
         pending = None
@@ -478,6 +489,13 @@ class WideMlpPlan(MlpPlan):
             a.A, a.Wt, a.bias, a.f32 = cur.data_ptr(), wbase + es * wo, bbase + 4 * bo, (1 - self.bf16) | self.gemm_flags
             a.rows, a.rows_p, a.K, a.Mp = n, rows_p, kp, mp
             a.lda, a.ldw, a.act, a.thr = lda, kp, act, thr
+            if li == 0 and first:  # input stage + first hidden layer: one launch, no [rows, 64] round trip
+                out = bufs[0]
+                a.C, a.ldc = out.data_ptr(), out.stride(0)
+                check(self.lib.pmml_nn_first_layer_launch(h, ctypes.byref(a), ctypes.byref(p)),
+                      "nn input stage + first layer gemm")
+                cur, lda = out, out.stride(0)
+                continue
             if head:
                 a.n_out, a.final_norm, a.row_ok = self.n_out, self.final_norm, ok.data_ptr()
                 a.epi = _epilogue(mode=EPI_AFFINE, a=self.out_a, b=self.out_b, table=self.table, tgt=self.target_stage)

@@ -89,3 +89,21 @@ def test_general_model_chain_on_gpu(gpu, classification):
     ref, vref = c.score_matrix_oracle(X)
     assert (v == vref).all() and v.any()
     np.testing.assert_allclose(s[v], ref[v], rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("method,classification", [("selectFirst", False), ("max", True), ("median", False)])
+def test_tree_segments_score_in_one_multi_launch(gpu, method, classification):
+    """Every tree segment scores in one tree_pointer_multi_kernel launch (grid.z = segment) and the
+    fused reduction kernel combines them: 2 launches per batch, results equal to the oracle."""
+    from flink_jpmml_amd.bench.synth import segmented_pmml
+
+    plan, s, v, ref, vref = _run(gpu, segmented_pmml(method, classification, n_segments=8, n_classes=3, seed=21),
+                                 n=70_000)
+    assert type(plan).__name__ == "SegmentedPlan"
+    assert sum(len(g["idx"]) for g in plan._multi) == plan.n_subs == 8
+    v = v.astype(bool)
+    assert (v == vref).all() and v.any()
+    if classification:
+        assert (s[v] == ref[v]).all()
+    else:
+        np.testing.assert_allclose(s[v], ref[v], rtol=1e-5, atol=1e-5)

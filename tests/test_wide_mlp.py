@@ -232,3 +232,26 @@ def test_k64_first_layer_kernel_matches_256_tile(gpu):
     finally:
         plan.gemm_flags = 0
     assert torch.equal(v0, v1) and torch.equal(s0[v0.bool()], s1[v1.bool()])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [dict(n_features=32, hidden=(1024, 1024, 1024)),
+                                   dict(n_features=60, hidden=(512, 256), n_out=4, classification=True),
+                                   dict(n_features=20, hidden=(300, 1024))],
+                         ids=["1024x3", "cls512x256", "300x1024"])
+def test_fused_input_stage_matches_separate_prep(gpu, shape):
+    """Input stage fused into the first layer's GEMM (gemm_k64_kernel<true>: gather, NormContinuous,
+    missing values, bf16 A tile built in LDS, row validity) gives the separate prep + GEMM bits."""
+    c = CompiledPmml.from_string(mlp_pmml(seed=17, **shape))
+    plan = c.plan(gpu, precision="bf16", mlp_impl="wide")
+    assert plan._fused_input(plan._fused_head())
+    X = stream_matrix(12_345, shape["n_features"], seed=9, missing_rate=0.03)
+    s1, v1 = plan.score(X)
+    plan.fuse_input = False
+    try:
+        s0, v0 = plan.score(X)
+    finally:
+        plan.fuse_input = True
+    assert torch.equal(v0, v1) and torch.equal(s0[v0.bool()], s1[v1.bool()])
+    ref, vref = c.score_matrix_oracle(X)
+    assert (v1.cpu().numpy().astype(bool) == vref).all()
