@@ -103,7 +103,10 @@ class _ScoringMixin:
 
     def _emit_one(self, out: Collector) -> None:
         res, _, _ = self._pending.popleft()
-        out.collect(res)
+        if type(res) is _RecordRows:  # a per-record micro-batch: its (Prediction, vector) pairs, in order
+            out.collect_many(list(zip(res.pb.predictions(), res.rows)))
+        else:
+            out.collect(res)
 
     def _emit_ready(self, out: Collector) -> None:
         while self._pending and all(f.ready for f in self._pending[0][1]):
@@ -132,7 +135,19 @@ class _ScoringMixin:
         rctx.register_timer(max(t_first + lat / 1e3, self._now()), fire)
 
 
+class _RecordRows:
+    """A submitted per-record micro-batch awaiting emission (QuickEvaluationFunction): the scoring
+    runs while the next batch is packed; the pairs go out in arrival order once it is ready."""
+
+    __slots__ = ("pb", "rows")
+
+    def __init__(self, pb: PredictionBatch, rows: List[Any]):
+        self.pb, self.rows = pb, rows
+
+
 def _futures_of(res: Any) -> List[PredictionBatch]:
+    if type(res) is _RecordRows:
+        return [res.pb]
     if isinstance(res, PredictionBatch):
         return [res]
     if isinstance(res, (tuple, list)) and len(res) <= 8:
@@ -949,8 +964,9 @@ class QuickEvaluationFunction(FlatMapFunction, _ScoringMixin):
         model = self.inner.evaluator
         with prange("quick_evaluate.flush"):
             batch = RecordBatch.from_vectors(buf, len(model.active_fields))
-            preds = model.predict_records(batch).predictions()
-        out.collect_many(list(zip(preds, buf)))
+            # submitted, not awaited: the pairs go out when the kernel is done (or at the latency
+            # bound / barrier / end of input), so the next batch packs while this one scores
+            self._push(_RecordRows(model.predict_records(batch), buf), out)
 
     def end_of_input(self, out: Collector) -> None:
         self._flush(out)
