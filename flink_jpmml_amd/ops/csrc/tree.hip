@@ -406,8 +406,9 @@ __global__ __launch_bounds__(TB, 2) void tree_super_kernel(TreeArgs a) {
 // 63 = leaf slot (x = the weighted leaf value, or the leaf row for P > 1). Nodes: 0 the root,
 // 1 / 2 its children, 3..6 the grandchildren; exit e = 4 b0 + 2 b1 + b2 lives at block +
 // popcount(mask below e) (only live exits are stored; a block stays within one 128-byte line).
-// Leaves above the third level are padded with never-right nodes (rank 255). Lock-step walks,
-// leaves accumulated in tree order (bit-identical to tree_pointer_kernel).
+// Leaves above the third level are padded with never-right nodes (rank 255). The root record is
+// read with a wave-uniform (scalar) load. Lock-step walks, leaves accumulated in tree order
+// (bit-identical to tree_pointer_kernel).
 constexpr uint32_t RK_NAN = 255;
 
 template <bool GENERAL, int PILP = 8>
@@ -456,7 +457,38 @@ __global__ __launch_bounds__(TB, 2) void tree_rank3_kernel(TreeArgs a) {
       act[i] = i < nt;
       leafv[i] = 0u;
     }
-    bool live = nt > 0;
+    // the root record: every lane of the wave starts on it — one uniform (scalar) load per tree
+    // instead of a 64-lane gather
+    {
+      uint4 rt[PILP];
+#pragma unroll
+      for (int i = 0; i < PILP; ++i) rt[i] = nodes[__builtin_amdgcn_readfirstlane(base[i])];
+#pragma unroll
+      for (int i = 0; i < PILP; ++i) {
+        const uint64_t lo = (uint64_t)rt[i].x | ((uint64_t)rt[i].y << 32);
+        const uint64_t hi = (uint64_t)rt[i].z | ((uint64_t)rt[i].w << 32);
+        const bool leaf = (rt[i].w >> 31) != 0u;
+        auto go_right = [&](int n) -> int {
+          const uint32_t f = (uint32_t)(hi >> (5 * n)) & 31u;
+          const uint32_t r = (uint32_t)(lo >> (8 * n)) & 255u;
+          const uint32_t d = (uint32_t)(hi >> (35 + n)) & 1u;
+          const uint32_t k = rk_lane[f * TB];
+          return (int)(k == RK_NAN ? d : (uint32_t)(k >= r));
+        };
+        const int b0 = go_right(0);
+        const int b1 = go_right(1 + b0);
+        const int b2 = go_right(3 + 2 * b0 + b1);
+        const int e = 4 * b0 + 2 * b1 + b2;
+        const uint32_t below = (rt[i].y >> 24) & ((1u << e) - 1u);
+        const int nxt = base[i] + (int)((hi >> 42) & 0x1FFFFFu) + __popc(below);
+        leafv[i] = (act[i] && leaf) ? rt[i].x : leafv[i];
+        pos[i] = (act[i] && !leaf) ? nxt : pos[i];
+        act[i] = act[i] && !leaf;
+      }
+    }
+    bool live = false;
+#pragma unroll
+    for (int i = 0; i < PILP; ++i) live = live || act[i];
     while (live) {
       uint4 nd[PILP];
 #pragma unroll
