@@ -12,4 +12,6 @@ timeout -k 10 600 python -u scripts/deep_forest_sweep.py --model rf --configs po
 cut -c1-220 $O/sweep_rf.jsonl; [ $rc -eq 0 ] || exit $rc
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_mlp -o mlp -- python3 scripts/mlp_prof.py > $O/prof_mlp.log 2>&1; rc=$?
-grep '^{' $O/prof_mlp.log | tail -1; exit $rc
+grep "^{" $O/prof_mlp.log | tail -1; [ $rc -eq 0 ] || exit $rc
+timeout -s KILL 120 rocprofv3 --kernel-trace --stats --output-format csv --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE -d $O/pmc_mlp -o pmc -- python3 scripts/mlp_prof.py > $O/pmc_mlp.log 2>&1; rc=$?
+grep '^{' $O/pmc_mlp.log | tail -1; exit $rc
