@@ -513,7 +513,104 @@ def rank_tables(trees, n_features: int):
     return uniq, thr, cnt
 
 
-def pack_rank3(trees, weights: List[float], P: int, n_features: int):
+_K_N, _K_P, _K_X = 0, 1, 2  # record entries: a real split, a pad carrying a leaf left, a dead pad
+
+
+def _rank3_tree(feat, internal, lc, rc, dr, rank, t, w, P, leaf0):
+    """One tree's RANK3 slots, a breadth-first level of records at a time (numpy over the level;
+    only the line-padded block allocation is a scalar loop). Same slots, same leaf-row order as
+    the reference builder of :func:`pack_rank3`. Returns ``(slots [n, 4] u32, leaf rows or None)``."""
+    leafvals = []
+
+    def leaf_words(nodes):
+        nodes = np.asarray(nodes, dtype=np.int64)
+        wv = np.zeros(nodes.size, dtype=np.uint32)
+        if P == 1:
+            wv[:] = (np.asarray(t.leaf_value, dtype=np.float64)[nodes] * w).astype(np.float32).view(np.uint32)
+        else:
+            base = leaf0 + sum(v.shape[0] for v in leafvals)
+            wv[:] = base + np.arange(nodes.size, dtype=np.uint32)
+            leafvals.append(np.asarray(t.leaf_probs, dtype=np.float64)[nodes, :P] * w)
+        return wv
+
+    chunks = []  # (slot indices, [k, 4] words)
+    if not internal[0]:
+        s0 = np.zeros((1, 4), np.uint32)
+        s0[0, 0] = leaf_words([0])[0]
+        s0[0, 3] = np.uint32(1 << 31)
+        arr = np.zeros((RK_LINE, 4), np.uint32)
+        arr[0] = s0[0]
+        return arr, (np.concatenate(leafvals) if leafvals else None)
+    n_slots = 1
+    fj = np.array([0], dtype=np.int64)    # record roots of this level
+    fs = np.array([0], dtype=np.int64)    # their slots
+
+    def below(k, v):
+        """children entries of entries (k, v): ([..., 2] kinds, [..., 2] values)."""
+        isn = k == _K_N
+        vv = np.where(isn, v, 0)
+        cl, cr = lc[vv], rc[vv]
+        kl = np.where(isn, np.where(internal[cl], _K_N, _K_P), np.where(k == _K_P, _K_P, _K_X))
+        kr = np.where(isn, np.where(internal[cr], _K_N, _K_P), _K_X)
+        vl = np.where(isn, cl, np.where(k == _K_P, v, -1))
+        vr = np.where(isn, cr, -1)
+        return np.stack([kl, kr], -1), np.stack([vl, vr], -1)
+
+    while fj.size:
+        K = fj.size
+        k0 = np.full((K, 1), _K_N)
+        v0 = fj[:, None]
+        k1, v1 = below(k0[:, 0], v0[:, 0])                              # [K, 2]
+        k2, v2 = below(k1.reshape(-1), v1.reshape(-1))                  # [2K, 2]
+        k2, v2 = k2.reshape(K, 4), v2.reshape(K, 4)
+        kind = np.concatenate([k0, k1, k2], 1)                          # [K, 7]
+        val = np.concatenate([v0, v1, v2], 1)
+        vv = np.where(k2 == _K_N, v2, 0)
+        ex = np.stack([np.where(k2 == _K_N, lc[vv], np.where(k2 == _K_P, v2, -1)),
+                       np.where(k2 == _K_N, rc[vv], -1)], -1).reshape(K, 8)
+        live = ex >= 0
+        nl = live.sum(1)
+        bases = np.empty(K, dtype=np.int64)
+        pos = n_slots
+        for i in range(K):  # a block never straddles a line
+            if pos % RK_LINE + nl[i] > RK_LINE:
+                pos += RK_LINE - pos % RK_LINE
+            bases[i] = pos
+            pos += nl[i]
+        n_slots = pos
+        if n_slots >= (1 << RK_OFF_BITS):
+            raise ValueError("rank3 layout: tree needs more than 2^21 slots")
+        isn = kind == _K_N
+        vn = np.where(isn, val, 0)
+        r = np.where(isn, rank[vn], np.uint64(RK_NEVER)).astype(np.uint64)
+        f = np.where(isn, feat[vn], 0).astype(np.uint64)
+        d = np.where(isn, dr[vn], False).astype(np.uint64)
+        sh = np.arange(7, dtype=np.uint64)
+        mask = (live.astype(np.uint64) << np.arange(8, dtype=np.uint64)).sum(1)
+        lo = (r << (np.uint64(8) * sh)).sum(1) | (mask << np.uint64(56))
+        hi = (f << (np.uint64(5) * sh)).sum(1) | (d << (np.uint64(35) + sh)).sum(1) | \
+            (bases.astype(np.uint64) << np.uint64(42))
+        rec = np.stack([lo & np.uint64(0xFFFFFFFF), lo >> np.uint64(32), hi & np.uint64(0xFFFFFFFF),
+                        hi >> np.uint64(32)], 1).astype(np.uint32)
+        chunks.append((fs, rec))
+        # exits, row-major (the reference builder's queue order): records -> next level, leaves -> slots
+        es = bases[:, None] + np.cumsum(live, 1) - 1
+        child, cslot = ex[live], es[live]
+        isr = internal[child]
+        if (~isr).any():
+            lw = np.zeros((int((~isr).sum()), 4), np.uint32)
+            lw[:, 0] = leaf_words(child[~isr])
+            lw[:, 3] = np.uint32(1 << 31)
+            chunks.append((cslot[~isr], lw))
+        fj, fs = child[isr], cslot[isr]
+    n_slots += (-n_slots) % RK_LINE
+    arr = np.zeros((n_slots, 4), dtype=np.uint32)
+    for sl, words in chunks:
+        arr[sl] = words
+    return arr, (np.concatenate(leafvals) if leafvals else None)
+
+
+def pack_rank3(trees, weights: List[float], P: int, n_features: int, vectorized: bool = True):
     """RANK3 records of every tree: per tree, slot 0 is the root record (or the root leaf slot),
     then the exit blocks in breadth-first order; a record's block holds its live exits (the next
     records and leaf slots) and never straddles a 128-byte line.
@@ -521,7 +618,8 @@ def pack_rank3(trees, weights: List[float], P: int, n_features: int):
     Returns ``(nodes [n, 4] u32, leaves [n_leaves, P] f32 or None, roots [n_trees] i32 (base slot of
     each tree), thr [F, stride] f32, cnt [F] i32, has_dr)``; ``ValueError`` when a feature index
     is >= 32, a feature has more than 254 unique thresholds, a tree is null-on-missing or needs
-    more than 2^21 slots."""
+    more than 2^21 slots. ``vectorized=False``: the record-by-record reference builder (the same
+    arrays, tests/test_rank3.py)."""
     from .plans import _canonical_vec
 
     if n_features > 32:
@@ -544,8 +642,20 @@ def pack_rank3(trees, weights: List[float], P: int, n_features: int):
         dr = np.where(swap, np.asarray(t.default_left, bool), ~np.asarray(t.default_left, bool)) & internal
         has_dr = has_dr or bool(dr.any())
         rank = np.zeros(feat.shape[0], dtype=np.uint64)
-        for k in np.nonzero(internal)[0]:
-            rank[k] = int(np.searchsorted(uniq[int(feat[k])], T[k])) + 1
+        for f in np.unique(feat[internal]):
+            m = feat == f
+            rank[m] = (np.searchsorted(uniq[int(f)], T[m]) + 1).astype(np.uint64)
+        if vectorized:
+            arr, lv = _rank3_tree(feat, internal, lc, rc, dr, rank, t, w, P, n_leaf)
+            if lv is not None:
+                leaves_all.append(lv)
+                n_leaf += lv.shape[0]
+            roots[ti] = total
+            total += arr.shape[0]
+            if total >= (1 << 31):
+                raise ValueError("rank3 layout: more than 2^31 slots")
+            slots_all.append(arr)
+            continue
         n_slots = 1  # slot 0: the root
         slots = {}
 

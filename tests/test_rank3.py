@@ -163,3 +163,15 @@ def test_rank3_kernel_bit_identical_to_pointer_walk(gpu, model, ilp):
     assert torch.equal(s0[m].view(torch.int32), s1[m].view(torch.int32))
     ref, vref = c.score_matrix_oracle(X)
     assert (v1.cpu().numpy().astype(bool) == vref).all()
+
+
+@pytest.mark.parametrize("depth,p_split,seed", [(12, 0.85, 1), (3, 1.0, 2), (9, 0.7, 3)])
+def test_vectorized_packer_matches_reference_builder(depth, p_split, seed):
+    """The level-at-a-time numpy packer (default) emits exactly the record-by-record builder's
+    slots, leaves, roots and rank tables."""
+    c = CompiledPmml.from_string(gbdt_pmml(n_trees=10, depth=depth, n_features=24, seed=seed, p_split=p_split))
+    spec = ensemble_spec(c)
+    a = pack_rank3(spec.trees, spec.weights, spec.P, c.n_features, vectorized=False)
+    b = pack_rank3(spec.trees, spec.weights, spec.P, c.n_features, vectorized=True)
+    for x, y in zip(a, b):
+        assert (x is None and y is None) or np.array_equal(x, y)
