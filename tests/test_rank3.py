@@ -175,3 +175,21 @@ def test_vectorized_packer_matches_reference_builder(depth, p_split, seed):
     b = pack_rank3(spec.trees, spec.weights, spec.P, c.n_features, vectorized=True)
     for x, y in zip(a, b):
         assert (x is None and y is None) or np.array_equal(x, y)
+
+
+def test_vectorized_packer_multislot_leaves():
+    """P > 1 leaf rows (the pointer layout's vote / probability forests): identical leaf tables."""
+    from flink_jpmml_amd.runtime.plans import TreePlan, lowering_dry_run
+
+    c = CompiledPmml.from_string(random_forest_pmml(n_trees=12, depth=9, n_features=20, n_classes=3, seed=5))
+    with lowering_dry_run():
+        plan = TreePlan(c, torch.device("cpu"), layout="pointer", node_format="rank3")
+    spec = plan.spec
+    a = pack_rank3(spec.trees, spec.weights, spec.P, c.n_features, vectorized=False)
+    b = pack_rank3(spec.trees, spec.weights, spec.P, c.n_features, vectorized=True)
+    assert spec.P > 1 and a[1].shape[1] == spec.P
+    for x, y in zip(a, b):
+        assert (x is None and y is None) or np.array_equal(x, y)
+    X = stream_matrix(2000, c.n_features, seed=3, missing_rate=0.05).astype(np.float32)
+    np.testing.assert_allclose(walk_rank3(b[0], b[2], b[3], b[4], X, spec.P, b[1]), walk_direct(spec, X),
+                               rtol=0, atol=1e-5)
