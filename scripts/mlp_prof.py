@@ -21,6 +21,9 @@ def main():
     iters = int(os.environ.get("ITERS", 10))
     c = CompiledPmml.from_string(mlp_pmml(n_features=32, hidden=hidden, seed=4))
     plan = c.plan("cuda:0", precision=prec, mlp_impl="wide")
+    plan.fuse_input = os.environ.get("FUSE_INPUT", "1") == "1"
+    plan.fuse_head = os.environ.get("FUSE_HEAD", "1") == "1"
+    plan.gemm_flags = int(os.environ.get("GEMM_FLAGS", "0"), 0)
     X = torch.from_numpy(stream_matrix(rows, 32, seed=1)).cuda()
     s, v = plan.alloc_outputs(rows)
     plan.launch(X, s, v)
@@ -30,7 +33,8 @@ def main():
         plan.launch(X, s, v)
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) / iters * 1e3
-    print(json.dumps({"hidden": hidden, "precision": prec, "rows": rows, "ms": ms, "plan": type(plan).__name__}))
+    print(json.dumps({"hidden": hidden, "precision": prec, "rows": rows, "ms": ms, "plan": type(plan).__name__,
+                      "fuse_input": plan.fuse_input, "fuse_head": plan.fuse_head, "gemm_flags": plan.gemm_flags}))
 
 
 if __name__ == "__main__":
