@@ -239,6 +239,61 @@ __device__ __forceinline__ void decode_row(const GemmArgs& a, int row, const flo
   }
 }
 
+// Hidden-layer epilogue through a wave-private LDS scratch (bf16): each 32 x 32 accumulator tile
+// (a unit per lane, 16 rows in the registers) is written to the wave's own 2.5 KiB of LDS as bf16
+// pairs and read back as 16-byte row chunks, so the tile leaves in 2 full-width 16-byte global
+// stores per lane instead of 16 two-unit stores by half the lanes — the store instruction count,
+// not the bytes, bounds a store-heavy epilogue. No block barrier: a wave's LDS operations complete
+// in order. Rows padded to 80 B so the two lane halves' rows (r, r + 4) use different banks.
+constexpr int WEPI_RP = 80;                    // bytes per scratch row
+constexpr int WEPI_BYTES = 32 * WEPI_RP;       // per wave
+
+template <int ACT, int TM, int TN>
+__device__ __forceinline__ void store_hidden_wave(const GemmArgs& a, const f32x16 (&acc)[TM][TN], int row0, int col0,
+                                                  int wm, int wn, int lane, unsigned char* scratch) {
+  const int h = lane >> 5, l32 = lane & 31;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int u0 = col0 + (wn * TN + j) * 32;
+    const float b = a.bias[u0 + l32];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int rb = row0 + (wm * TM + i) * 32;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float v = act_of<ACT>(acc[i][j][r] + b, a.act, a.thr);
+        const float o = __shfl_xor(v, 1);
+        if ((lane & 1) == 0) {
+          const uint32_t lo = __builtin_bit_cast(uint16_t, (__bf16)v);
+          const uint32_t hi = __builtin_bit_cast(uint16_t, (__bf16)o);
+          const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+          *reinterpret_cast<uint32_t*>(scratch + row * WEPI_RP + 2 * l32) = lo | (hi << 16);
+        }
+      }
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {  // chunk c = lane + 64 q: row c >> 2, 16-byte part c & 3
+        const int c = lane + 64 * q;
+        const uint4 v = *reinterpret_cast<const uint4*>(scratch + (c >> 2) * WEPI_RP + 16 * (c & 3));
+        *reinterpret_cast<uint4*>(static_cast<__bf16*>(a.C) + (size_t)(rb + (c >> 2)) * a.ldc + u0 + 8 * (c & 3)) = v;
+      }
+      asm volatile("" ::: "memory");
+    }
+  }
+}
+
+template <int TM, int TN>
+__device__ __forceinline__ void store_hidden_wave_any(const GemmArgs& a, const f32x16 (&acc)[TM][TN], int row0,
+                                                      int col0, int wm, int wn, int lane, unsigned char* scratch) {
+  switch (a.act) {
+    case A_IDENTITY: store_hidden_wave<A_IDENTITY, TM, TN>(a, acc, row0, col0, wm, wn, lane, scratch); break;
+    case A_RELU: store_hidden_wave<A_RELU, TM, TN>(a, acc, row0, col0, wm, wn, lane, scratch); break;
+    case A_LOGISTIC: store_hidden_wave<A_LOGISTIC, TM, TN>(a, acc, row0, col0, wm, wn, lane, scratch); break;
+    case A_TANH: store_hidden_wave<A_TANH, TM, TN>(a, acc, row0, col0, wm, wn, lane, scratch); break;
+    default: store_hidden_wave<-1, TM, TN>(a, acc, row0, col0, wm, wn, lane, scratch); break;
+  }
+}
+
 template <int BN, bool HEAD, bool F32>
 __global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmArgs a) {
   constexpr int WM = BN == 256 ? 2 : 8;  // waves along rows
@@ -357,7 +412,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmArgs a) {
 constexpr int K64_BM = 128, K64_NT = 256;
 
 template <bool PREP>
-__global__ __launch_bounds__(K64_NT, PREP ? 2 : 3) void gemm_k64_kernel(GemmArgs a, PrepArgs p) {
+__global__ __launch_bounds__(K64_NT, 2) void gemm_k64_kernel(GemmArgs a, PrepArgs p) {
   constexpr int TM = 2, TN = 4;  // 2 x 2 waves, 64 rows x 128 units each
   extern __shared__ __align__(16) unsigned char smem[];
   unsigned char* As = smem;
@@ -422,6 +477,11 @@ __global__ __launch_bounds__(K64_NT, PREP ? 2 : 3) void gemm_k64_kernel(GemmArgs
 #pragma unroll
       for (int j = 0; j < TN; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+  }
+  if (!((a.f32 >> 5) & 1)) {  // bit 5: the direct two-unit stores
+    __syncthreads();  // every wave is done reading the staged tiles: their LDS becomes scratch
+    store_hidden_wave_any<TM, TN>(a, acc, row0, col0, wm, wn, lane, smem + wave * WEPI_BYTES);
+    return;
   }
   switch (a.act) {
     case A_IDENTITY: store_hidden<A_IDENTITY, TM, TN, false>(a, acc, row0, col0, wm, wn, lane); break;
@@ -663,6 +723,11 @@ __global__ __launch_bounds__(NT, 1) void gemm8_kernel(GemmArgs a, HeadFuse hf) {
     }
     return;
   } else {
+    if (!((a.f32 >> 5) & 1)) {  // bit 5: the direct two-unit stores
+      // every wave is past its last LDS read of the staged slices (the balancing barrier above)
+      store_hidden_wave_any<TM, TN>(a, acc, row0, col0, wr, wc, lane, smem + wave * WEPI_BYTES);
+      return;
+    }
     switch (a.act) {
       case A_IDENTITY: store_hidden<A_IDENTITY, TM, TN, false>(a, acc, row0, col0, wr, wc, lane); break;
       case A_RELU: store_hidden<A_RELU, TM, TN, false>(a, acc, row0, col0, wr, wc, lane); break;
@@ -736,7 +801,7 @@ PMML_API int pmml_gemm_launch(hipStream_t stream, const GemmArgs* args, int head
   const GemmArgs a = *args;
   if (a.rows <= 0) return 0;
   const int BN = head ? 32 : 256;
-  if (a.f32 & ~0xC1) return -4;
+  if (a.f32 & ~0xE1) return -4;
   // bf16 hidden layers with K >= 512 run the phase-interleaved kernel (profiles/r3ao: 2048 x 2048
   // 8.73 -> 8.36 ms, 1024 x 1024 2.62 -> 2.48 ms over 1M rows); below that the layer is bound by
   // its output writes and the 2-buffer loop is faster (K = 64: 0.83 vs 0.92 ms). Bit 7 forces it.

@@ -426,15 +426,37 @@ __global__ __launch_bounds__(TB, 2) void tree_rank3_kernel(TreeArgs a) {
   stage_rows_T<TB>(a.X, a.n_rows, a.n_feat, a.ldx, a.prep, feat, bad, row0);
   bool row_ok = bad[tid] == 0;
   if (a.row_valid_in && row < a.n_rows) row_ok = row_ok && a.row_valid_in[row];
-  // ranks of this lane's row (only this lane reads them back: no barrier)
-  for (int f = 0; f < a.n_feat; ++f) {
-    const float x = feat[f * TB + tid];
-    const int cnt = a.rank_cnt[f];
-    const float* t = a.rank_thr + (size_t)f * a.rank_stride;
-    int pos = 0;  // #{t_k <= x}
-    for (int step = 128; step > 0; step >>= 1)
-      if (pos + step <= cnt && t[pos + step - 1] <= x) pos += step;
-    rk[f * TB + tid] = (uint16_t)(x != x ? RK_NAN : (uint32_t)pos);
+  // ranks of this lane's row: the threshold tables staged in LDS, then 8 features' branchless
+  // binary searches advanced together (8 independent LDS reads in flight per step; a dependent
+  // global-memory search per feature left every workgroup idle for tens of microseconds before
+  // its first tree). Only this lane reads its ranks back: no barrier after.
+  float* thr_l = reinterpret_cast<float*>(rk + a.n_feat * TB);  // [F][rank_stride]
+  const int stride = a.rank_stride;
+  for (int e = tid; e < a.n_feat * stride; e += TB) thr_l[e] = a.rank_thr[e];
+  __syncthreads();
+  for (int f0 = 0; f0 < a.n_feat; f0 += 8) {
+    float x[8];
+    int pos[8], cnt[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const bool on = f0 + k < a.n_feat;
+      x[k] = on ? feat[(f0 + k) * TB + tid] : 0.f;
+      cnt[k] = on ? a.rank_cnt[f0 + k] : 0;
+      pos[k] = 0;  // #{t <= x}
+    }
+#pragma unroll
+    for (int step = 128; step > 0; step >>= 1) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int q = pos[k] + step;
+        const int at = max(min(q, cnt[k]) - 1, 0);
+        const float t = thr_l[(f0 + k) * stride + at];
+        pos[k] = (q <= cnt[k] && t <= x[k]) ? q : pos[k];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (f0 + k < a.n_feat) rk[(f0 + k) * TB + tid] = (uint16_t)(x[k] != x[k] ? RK_NAN : (uint32_t)pos[k]);
   }
   const uint16_t* rk_lane = rk + tid;
   const uint4* nodes = reinterpret_cast<const uint4*>(a.blob);
@@ -468,16 +490,18 @@ __global__ __launch_bounds__(TB, 2) void tree_rank3_kernel(TreeArgs a) {
         const uint64_t lo = (uint64_t)rt[i].x | ((uint64_t)rt[i].y << 32);
         const uint64_t hi = (uint64_t)rt[i].z | ((uint64_t)rt[i].w << 32);
         const bool leaf = (rt[i].w >> 31) != 0u;
-        auto go_right = [&](int n) -> int {
-          const uint32_t f = (uint32_t)(hi >> (5 * n)) & 31u;
+        // the root's and both children's ranks in one round of LDS reads, then the grandchild's
+        auto rank_of = [&](int n) -> uint32_t { return rk_lane[((uint32_t)(hi >> (5 * n)) & 31u) * TB]; };
+        auto right = [&](uint32_t k, int n) -> int {
           const uint32_t r = (uint32_t)(lo >> (8 * n)) & 255u;
           const uint32_t d = (uint32_t)(hi >> (35 + n)) & 1u;
-          const uint32_t k = rk_lane[f * TB];
           return (int)(k == RK_NAN ? d : (uint32_t)(k >= r));
         };
-        const int b0 = go_right(0);
-        const int b1 = go_right(1 + b0);
-        const int b2 = go_right(3 + 2 * b0 + b1);
+        const uint32_t k0 = rank_of(0), k1 = rank_of(1), k2 = rank_of(2);
+        const int b0 = right(k0, 0);
+        const int b1 = right(b0 ? k2 : k1, 1 + b0);
+        const int n2 = 3 + 2 * b0 + b1;
+        const int b2 = right(rank_of(n2), n2);
         const int e = 4 * b0 + 2 * b1 + b2;
         const uint32_t below = (rt[i].y >> 24) & ((1u << e) - 1u);
         const int nxt = base[i] + (int)((hi >> 42) & 0x1FFFFFu) + __popc(below);
@@ -499,16 +523,18 @@ __global__ __launch_bounds__(TB, 2) void tree_rank3_kernel(TreeArgs a) {
         const uint64_t lo = (uint64_t)nd[i].x | ((uint64_t)nd[i].y << 32);
         const uint64_t hi = (uint64_t)nd[i].z | ((uint64_t)nd[i].w << 32);
         const bool leaf = (nd[i].w >> 31) != 0u;
-        auto go_right = [&](int n) -> int {
-          const uint32_t f = (uint32_t)(hi >> (5 * n)) & 31u;
+        // the root's and both children's ranks in one round of LDS reads, then the grandchild's
+        auto rank_of = [&](int n) -> uint32_t { return rk_lane[((uint32_t)(hi >> (5 * n)) & 31u) * TB]; };
+        auto right = [&](uint32_t k, int n) -> int {
           const uint32_t r = (uint32_t)(lo >> (8 * n)) & 255u;
           const uint32_t d = (uint32_t)(hi >> (35 + n)) & 1u;
-          const uint32_t k = rk_lane[f * TB];
           return (int)(k == RK_NAN ? d : (uint32_t)(k >= r));
         };
-        const int b0 = go_right(0);
-        const int b1 = go_right(1 + b0);
-        const int b2 = go_right(3 + 2 * b0 + b1);
+        const uint32_t k0 = rank_of(0), k1 = rank_of(1), k2 = rank_of(2);
+        const int b0 = right(k0, 0);
+        const int b1 = right(b0 ? k2 : k1, 1 + b0);
+        const int n2 = 3 + 2 * b0 + b1;
+        const int b2 = right(rank_of(n2), n2);
         const int e = 4 * b0 + 2 * b1 + b2;
         const uint32_t below = (nd[i].y >> 24) & ((1u << e) - 1u);  // live exits before e
         const int nxt = base[i] + (int)((hi >> 42) & 0x1FFFFFu) + __popc(below);
@@ -892,7 +918,8 @@ PMML_API int pmml_tree_launch(hipStream_t stream, const TreeArgs* args, int layo
     size_t lds = (feat_lds ? (size_t)a.n_feat * TB * 4 : 0) + TB * 4 + acc_lds;
     if (a.variant == VAR_POINTER_RANK3) {
       if (a.n_feat > 32 || !a.rank_thr || !a.rank_cnt || a.rank_stride < 1 || a.rank_stride > 254) return -4;
-      lds += (size_t)a.n_feat * TB * 2;  // rank planes
+      lds += (size_t)a.n_feat * TB * 2 + (size_t)a.n_feat * a.rank_stride * 4;  // rank planes + threshold tables
+      if (lds > 160 * 1024) return -5;
       if (a.general) {
         err = prepare_launch(tree_rank3_kernel<true>, lds);
         if (!err) hipLaunchKernelGGL((tree_rank3_kernel<true>), grid, dim3(TB), lds, stream, a);

@@ -423,7 +423,7 @@ class WideMlpPlan(MlpPlan):
         return bool(self.fuse_head) and self.bf16 == 1 and len(self.dims) >= 2 and self.dims[-2][0] % 64 == 0
 
     # bf16, <= 64 network inputs: the input stage runs inside the first layer's GEMM (gemm_k64_kernel<true>)
-    fuse_input = True
+    fuse_input = False  # measured slower (profiles/r4j: the gather in the GEMM prologue, 1.43 vs 0.18 + 0.82 ms)
 
     def _fused_input(self, fused_head: bool) -> bool:
         """The first layer is a hidden layer launched on its own (not the fused last hidden layer)."""

@@ -244,14 +244,31 @@ def test_fused_input_stage_matches_separate_prep(gpu, shape):
     missing values, bf16 A tile built in LDS, row validity) gives the separate prep + GEMM bits."""
     c = CompiledPmml.from_string(mlp_pmml(seed=17, **shape))
     plan = c.plan(gpu, precision="bf16", mlp_impl="wide")
+    plan.fuse_input = True  # opt-in (measured slower than the separate input stage)
     assert plan._fused_input(plan._fused_head())
     X = stream_matrix(12_345, shape["n_features"], seed=9, missing_rate=0.03)
     s1, v1 = plan.score(X)
     plan.fuse_input = False
-    try:
-        s0, v0 = plan.score(X)
-    finally:
-        plan.fuse_input = True
+    s0, v0 = plan.score(X)
     assert torch.equal(v0, v1) and torch.equal(s0[v0.bool()], s1[v1.bool()])
     ref, vref = c.score_matrix_oracle(X)
     assert (v1.cpu().numpy().astype(bool) == vref).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [dict(n_features=32, hidden=(1024, 1024, 512)), dict(n_features=40, hidden=(300, 260))],
+                         ids=["1024x1024x512", "300x260"])
+def test_wave_lds_epilogue_matches_direct_stores(gpu, shape):
+    """Hidden-layer tiles leaving through the wave-private LDS scratch (16-byte stores) equal the
+    direct two-unit stores bit for bit (flag bit 5 forces the latter)."""
+    c = CompiledPmml.from_string(mlp_pmml(seed=19, **shape))
+    plan = c.plan(gpu, precision="bf16", mlp_impl="wide")
+    plan.fuse_head = False  # every hidden layer stores its activations
+    X = stream_matrix(7000, shape["n_features"], seed=2, missing_rate=0.01)
+    s0, v0 = plan.score(X)
+    plan.gemm_flags = 0x20
+    try:
+        s1, v1 = plan.score(X)
+    finally:
+        plan.gemm_flags = 0
+    assert torch.equal(v0, v1) and torch.equal(s0[v0.bool()], s1[v1.bool()])
