@@ -239,7 +239,9 @@ __device__ __forceinline__ void decode_row(const GemmArgs& a, int row, const flo
   }
 }
 
-// Hidden-layer epilogue through a wave-private LDS scratch (bf16): each 32 x 32 accumulator tile
+// Hidden-layer epilogue through a wave-private LDS scratch (bf16; opt-in, flag bit 5 — measured
+// slower than the direct stores: 2.70 vs 2.60 ms for a 1024 x 1024 layer, 0.99 vs 0.84 ms for the
+// K = 64 layer, profiles/r4k). Each 32 x 32 accumulator tile
 // (a unit per lane, 16 rows in the registers) is written to the wave's own 2.5 KiB of LDS as bf16
 // pairs and read back as 16-byte row chunks, so the tile leaves in 2 full-width 16-byte global
 // stores per lane instead of 16 two-unit stores by half the lanes — the store instruction count,
@@ -478,7 +480,7 @@ __global__ __launch_bounds__(K64_NT, 2) void gemm_k64_kernel(GemmArgs a, PrepArg
       for (int j = 0; j < TN; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
   }
-  if (!((a.f32 >> 5) & 1)) {  // bit 5: the direct two-unit stores
+  if ((a.f32 >> 5) & 1) {  // bit 5: the wave-private LDS epilogue (measured slower, profiles/r4k)
     __syncthreads();  // every wave is done reading the staged tiles: their LDS becomes scratch
     store_hidden_wave_any<TM, TN>(a, acc, row0, col0, wm, wn, lane, smem + wave * WEPI_BYTES);
     return;
@@ -723,7 +725,7 @@ __global__ __launch_bounds__(NT, 1) void gemm8_kernel(GemmArgs a, HeadFuse hf) {
     }
     return;
   } else {
-    if (!((a.f32 >> 5) & 1)) {  // bit 5: the direct two-unit stores
+    if ((a.f32 >> 5) & 1) {  // bit 5: the wave-private LDS epilogue (measured slower, profiles/r4k)
       // every wave is past its last LDS read of the staged slices (the balancing barrier above)
       store_hidden_wave_any<TM, TN>(a, acc, row0, col0, wr, wc, lane, smem + wave * WEPI_BYTES);
       return;

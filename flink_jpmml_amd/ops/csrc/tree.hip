@@ -417,7 +417,10 @@ __global__ __launch_bounds__(TB, 2) void tree_rank3_kernel(TreeArgs a) {
   float* feat = reinterpret_cast<float*>(smem);
   int* bad = reinterpret_cast<int*>(smem + a.n_feat * TB);
   float* accl = reinterpret_cast<float*>(bad + TB);
-  uint16_t* rk = reinterpret_cast<uint16_t*>(accl + (GENERAL ? a.C * TB : 0));  // [F][TB]
+  // ranks overwrite the feature planes in place (a lane only ever reads its own row): 32-bit
+  // entries keep every lane on its own bank whatever feature it reads (16-bit planes put two
+  // lanes on one bank: 2-way conflicts on every rank read of the walk)
+  uint32_t* rk = reinterpret_cast<uint32_t*>(feat);  // [F][TB]
   const int tid = threadIdx.x;
   const int2 blk = tree_block(a);
   const int row0 = blk.x * TB;
@@ -430,7 +433,7 @@ __global__ __launch_bounds__(TB, 2) void tree_rank3_kernel(TreeArgs a) {
   // binary searches advanced together (8 independent LDS reads in flight per step; a dependent
   // global-memory search per feature left every workgroup idle for tens of microseconds before
   // its first tree). Only this lane reads its ranks back: no barrier after.
-  float* thr_l = reinterpret_cast<float*>(rk + a.n_feat * TB);  // [F][rank_stride]
+  float* thr_l = accl + (GENERAL ? a.C * TB : 0);  // [F][rank_stride]
   const int stride = a.rank_stride;
   for (int e = tid; e < a.n_feat * stride; e += TB) thr_l[e] = a.rank_thr[e];
   __syncthreads();
@@ -456,9 +459,9 @@ __global__ __launch_bounds__(TB, 2) void tree_rank3_kernel(TreeArgs a) {
     }
 #pragma unroll
     for (int k = 0; k < 8; ++k)
-      if (f0 + k < a.n_feat) rk[(f0 + k) * TB + tid] = (uint16_t)(x[k] != x[k] ? RK_NAN : (uint32_t)pos[k]);
+      if (f0 + k < a.n_feat) rk[(f0 + k) * TB + tid] = x[k] != x[k] ? RK_NAN : (uint32_t)pos[k];
   }
-  const uint16_t* rk_lane = rk + tid;
+  const uint32_t* rk_lane = rk + tid;
   const uint4* nodes = reinterpret_cast<const uint4*>(a.blob);
   const uint32_t* roots = reinterpret_cast<const uint32_t*>(a.roots);
   const int tb = split * a.trees_per_split;
@@ -490,16 +493,14 @@ __global__ __launch_bounds__(TB, 2) void tree_rank3_kernel(TreeArgs a) {
         const uint64_t lo = (uint64_t)rt[i].x | ((uint64_t)rt[i].y << 32);
         const uint64_t hi = (uint64_t)rt[i].z | ((uint64_t)rt[i].w << 32);
         const bool leaf = (rt[i].w >> 31) != 0u;
-        // the root's and both children's ranks in one round of LDS reads, then the grandchild's
         auto rank_of = [&](int n) -> uint32_t { return rk_lane[((uint32_t)(hi >> (5 * n)) & 31u) * TB]; };
         auto right = [&](uint32_t k, int n) -> int {
           const uint32_t r = (uint32_t)(lo >> (8 * n)) & 255u;
           const uint32_t d = (uint32_t)(hi >> (35 + n)) & 1u;
           return (int)(k == RK_NAN ? d : (uint32_t)(k >= r));
         };
-        const uint32_t k0 = rank_of(0), k1 = rank_of(1), k2 = rank_of(2);
-        const int b0 = right(k0, 0);
-        const int b1 = right(b0 ? k2 : k1, 1 + b0);
+        const int b0 = right(rank_of(0), 0);
+        const int b1 = right(rank_of(1 + b0), 1 + b0);
         const int n2 = 3 + 2 * b0 + b1;
         const int b2 = right(rank_of(n2), n2);
         const int e = 4 * b0 + 2 * b1 + b2;
@@ -523,16 +524,14 @@ __global__ __launch_bounds__(TB, 2) void tree_rank3_kernel(TreeArgs a) {
         const uint64_t lo = (uint64_t)nd[i].x | ((uint64_t)nd[i].y << 32);
         const uint64_t hi = (uint64_t)nd[i].z | ((uint64_t)nd[i].w << 32);
         const bool leaf = (nd[i].w >> 31) != 0u;
-        // the root's and both children's ranks in one round of LDS reads, then the grandchild's
         auto rank_of = [&](int n) -> uint32_t { return rk_lane[((uint32_t)(hi >> (5 * n)) & 31u) * TB]; };
         auto right = [&](uint32_t k, int n) -> int {
           const uint32_t r = (uint32_t)(lo >> (8 * n)) & 255u;
           const uint32_t d = (uint32_t)(hi >> (35 + n)) & 1u;
           return (int)(k == RK_NAN ? d : (uint32_t)(k >= r));
         };
-        const uint32_t k0 = rank_of(0), k1 = rank_of(1), k2 = rank_of(2);
-        const int b0 = right(k0, 0);
-        const int b1 = right(b0 ? k2 : k1, 1 + b0);
+        const int b0 = right(rank_of(0), 0);
+        const int b1 = right(rank_of(1 + b0), 1 + b0);
         const int n2 = 3 + 2 * b0 + b1;
         const int b2 = right(rank_of(n2), n2);
         const int e = 4 * b0 + 2 * b1 + b2;
@@ -918,7 +917,7 @@ PMML_API int pmml_tree_launch(hipStream_t stream, const TreeArgs* args, int layo
     size_t lds = (feat_lds ? (size_t)a.n_feat * TB * 4 : 0) + TB * 4 + acc_lds;
     if (a.variant == VAR_POINTER_RANK3) {
       if (a.n_feat > 32 || !a.rank_thr || !a.rank_cnt || a.rank_stride < 1 || a.rank_stride > 254) return -4;
-      lds += (size_t)a.n_feat * TB * 2 + (size_t)a.n_feat * a.rank_stride * 4;  // rank planes + threshold tables
+      lds += (size_t)a.n_feat * a.rank_stride * 4;  // threshold tables (ranks replace the feature planes)
       if (lds > 160 * 1024) return -5;
       if (a.general) {
         err = prepare_launch(tree_rank3_kernel<true>, lds);

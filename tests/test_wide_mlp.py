@@ -259,8 +259,8 @@ def test_fused_input_stage_matches_separate_prep(gpu, shape):
 @pytest.mark.parametrize("shape", [dict(n_features=32, hidden=(1024, 1024, 512)), dict(n_features=40, hidden=(300, 260))],
                          ids=["1024x1024x512", "300x260"])
 def test_wave_lds_epilogue_matches_direct_stores(gpu, shape):
-    """Hidden-layer tiles leaving through the wave-private LDS scratch (16-byte stores) equal the
-    direct two-unit stores bit for bit (flag bit 5 forces the latter)."""
+    """Hidden-layer tiles leaving through the wave-private LDS scratch (16-byte stores, flag bit 5)
+    equal the direct two-unit stores bit for bit."""
     c = CompiledPmml.from_string(mlp_pmml(seed=19, **shape))
     plan = c.plan(gpu, precision="bf16", mlp_impl="wide")
     plan.fuse_head = False  # every hidden layer stores its activations
