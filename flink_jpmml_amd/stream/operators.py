@@ -94,8 +94,10 @@ class _ScoringMixin:
         return rctx.now() if rctx is not None else __import__("time").monotonic()
 
     # -- ordered, non-blocking emission of columnar results
-    def _push(self, result: Any, out: Collector) -> None:
-        self._pending.append((result, _futures_of(result), self._now()))
+    def _push(self, result: Any, out: Collector, t0: Optional[float] = None) -> None:
+        """Queue a submitted result; it goes out once scored, or at ``t0`` (default: now) plus
+        the latency bound, in submission order."""
+        self._pending.append((result, _futures_of(result), self._now() if t0 is None else t0))
         self._emit_ready(out)
         while len(self._pending) > self.config.max_inflight:
             self._emit_one(out)
@@ -953,6 +955,7 @@ class QuickEvaluationFunction(FlatMapFunction, _ScoringMixin):
             if self._buf and now >= self._first_ts + lat / 1e3:
                 METRICS.inc("batcher.latency_flushes")
                 self._flush(out)
+                self._drain_pending(out)  # the latency bound is due: out now, waiting for the kernel
             self._arm(out)
 
         rctx.register_timer(self._first_ts + lat / 1e3, fire)
@@ -966,7 +969,7 @@ class QuickEvaluationFunction(FlatMapFunction, _ScoringMixin):
             batch = RecordBatch.from_vectors(buf, len(model.active_fields))
             # submitted, not awaited: the pairs go out when the kernel is done (or at the latency
             # bound / barrier / end of input), so the next batch packs while this one scores
-            self._push(_RecordRows(model.predict_records(batch), buf), out)
+            self._push(_RecordRows(model.predict_records(batch), buf), out, t0=self._first_ts)
 
     def end_of_input(self, out: Collector) -> None:
         self._flush(out)
