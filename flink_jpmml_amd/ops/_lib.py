@@ -314,6 +314,8 @@ def load(auto_build: bool = True) -> ctypes.CDLL:
                                                  ctypes.c_int, ctypes.c_int]
         lib.pmml_gemm_launch.restype = ctypes.c_int
         lib.pmml_gemm_launch.argtypes = [c_void_p, ctypes.POINTER(GemmArgs), ctypes.c_int]
+        lib.pmml_nn_decode_wide.restype = ctypes.c_int
+        lib.pmml_nn_decode_wide.argtypes = [c_void_p, ctypes.POINTER(GemmArgs), c_void_p, c_int]
         lib.pmml_nn_first_layer_launch.restype = ctypes.c_int
         lib.pmml_nn_first_layer_launch.argtypes = [c_void_p, ctypes.POINTER(GemmArgs), ctypes.POINTER(NnPrepArgs)]
         lib.pmml_gemm_fused_head_launch.restype = ctypes.c_int

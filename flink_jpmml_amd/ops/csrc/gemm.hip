@@ -41,6 +41,7 @@ constexpr int BK = 64;   // bf16 k per LDS slice (128 B per row); fp32: 32
 constexpr int SLICE_B = 128;  // bytes of one row in one LDS slice
 constexpr int NT = 512;  // threads (8 waves)
 constexpr int HEAD_LD = 33;
+constexpr int NN_MAX_INPUTS = 16384;  // network inputs of the wide-layer input stage (padded to 64)
 
 struct GemmArgs {
   const void* A;          // [rows_p][lda] activations (bf16 or fp32), rows_p = rows rounded up to BM
@@ -72,21 +73,21 @@ struct PrepArgs {
   int f32, pad;
 };
 
-// Input layer: gather the network inputs, normalise, replace missing, bf16. One thread per
-// (row, 8-input chunk) — a row's chunks are GP consecutive lanes (GP = chunks rounded up to a
-// power of two <= 64), so its reads and its 16-byte stores are contiguous, and the row's validity
-// is the AND over its lane group (one wave ballot).
+// Input layer: gather the network inputs, normalise, replace missing, bf16. A row's 8-input
+// chunks are spread over GP consecutive lanes (GP = chunks rounded up to a power of two, at most
+// 64: beyond 512 inputs a lane takes every 64th chunk), so its reads and its 16-byte stores are
+// contiguous, and the row's validity is the AND over its lane group (one wave ballot).
 template <bool F32>
 __global__ __launch_bounds__(256) void nn_prep_kernel(PrepArgs a, int gp_log2) {
   const int GP = 1 << gp_log2;
   const int t = blockIdx.x * 256 + threadIdx.x;
   const int row = t >> gp_log2;
-  const int chunk = t & (GP - 1);
+  const int lc = t & (GP - 1);
   const int nchunk = a.k0 >> 3;
   const bool live_row = row < a.n_rows;
-  const bool active = row < a.rows_p && chunk < nchunk;
+  const bool active = row < a.rows_p;
   bool bad = false;
-  if (active) {
+  for (int chunk = lc; active && chunk < nchunk; chunk += GP) {
     const float* x = a.X + (size_t)(live_row ? row : 0) * a.ldx;
     float v[8];
 #pragma unroll
@@ -116,7 +117,7 @@ __global__ __launch_bounds__(256) void nn_prep_kernel(PrepArgs a, int gp_log2) {
   const int lane = threadIdx.x & 63;
   const int g0 = lane & ~(GP - 1);
   const unsigned long long grp = GP == 64 ? ~0ull : ((1ull << GP) - 1) << g0;
-  if (active && chunk == 0) a.row_ok[row] = (live_row && (m & grp) == 0) ? 1 : 0;
+  if (active && lc == 0) a.row_ok[row] = (live_row && (m & grp) == 0) ? 1 : 0;
 }
 
 __device__ __forceinline__ void glds16(const void* g, void* lds) {
@@ -397,8 +398,46 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmArgs a) {
     __syncthreads();
     if (tid < BM) {
       const int row = row0 + tid;
-      if (row < a.rows) decode_row(a, row, zt + tid * HEAD_LD);
+      if (row < a.rows) {
+        if (a.C) {  // one 32-output group of a wider output layer: its activated outputs (fp32)
+          float* zo = static_cast<float*>(a.C) + (size_t)row * a.ldc;
+          for (int u = 0; u < a.n_out; ++u) zo[u] = zt[tid * HEAD_LD + u];
+        } else {
+          decode_row(a, row, zt + tid * HEAD_LD);
+        }
+      }
     }
+  }
+}
+
+// Decode of an output layer wider than one 32-unit tile: Z holds every row's activated outputs
+// (fp32, row pitch ldz), written group by group by the output-layer GEMM. Streaming passes (max,
+// normaliser, probabilities + argmax) — no per-row array, any n_out.
+__global__ __launch_bounds__(256) void nn_decode_wide_kernel(GemmArgs a, const float* __restrict__ Z, int ldz) {
+  const int row = blockIdx.x * 256 + threadIdx.x;
+  if (row >= a.rows) return;
+  const float* z = Z + (size_t)row * ldz;
+  const bool bad = !a.row_ok[row];
+  float mx = -__builtin_inff();
+  for (int u = 0; u < a.n_out; ++u) mx = fmaxf(mx, z[u]);
+  float sum = 0.f;
+  for (int u = 0; u < a.n_out; ++u) sum += (a.final_norm == 1) ? __expf(z[u] - mx) : z[u];
+  float best = -__builtin_inff();
+  int best_u = 1 << 30;
+  for (int u = 0; u < a.n_out; ++u) {
+    float p = (a.final_norm == 1) ? __expf(z[u] - mx) : z[u];
+    if (a.final_norm != 0) p /= sum;
+    if (p > best || (p == best && u < best_u)) { best = p; best_u = u; }
+    if (a.probs) a.probs[(size_t)row * a.n_out + u] = p;
+  }
+  bool ok = !bad && best == best && best_u < a.n_out;
+  float sc = ok ? (a.epi.has_table ? a.epi.table[best_u] : (float)best_u) : __builtin_nanf("");
+  ok = ok && (sc == sc);
+  a.score[row] = ok ? sc : __builtin_nanf("");
+  a.valid[row] = ok ? 1 : 0;
+  if (a.epi.score2) {
+    a.epi.score2[row] = ok ? sc : __builtin_nanf("");
+    a.epi.valid2[row] = ok ? 1 : 0;
   }
 }
 
@@ -785,11 +824,11 @@ PMML_API int pmml_nn_prep_args_size() { return (int)sizeof(PrepArgs); }
 PMML_API int pmml_nn_prep_launch(hipStream_t stream, const PrepArgs* args) {
   const PrepArgs a = *args;
   if (a.rows_p <= 0) return 0;
-  if ((a.k0 & 7) || a.k0 < a.n_in || a.k0 > 512 || (a.ldh & 7) || (reinterpret_cast<uintptr_t>(a.H) & 15))
+  if ((a.k0 & 7) || a.k0 < a.n_in || a.k0 > NN_MAX_INPUTS || (a.ldh & 7) || (reinterpret_cast<uintptr_t>(a.H) & 15))
     return -4;
   if (a.f32 != 0 && a.f32 != 1) return -4;
   int g = 0;
-  while ((1 << g) < (a.k0 >> 3)) ++g;  // lanes per row: chunks rounded up to a power of two (<= 64)
+  while ((1 << g) < (a.k0 >> 3) && g < 6) ++g;  // lanes per row: chunks rounded up to a power of two, <= 64
   const long long threads = (long long)a.rows_p << g;
   const dim3 grid((unsigned)((threads + 255) / 256));
   if (a.f32) hipLaunchKernelGGL(nn_prep_kernel<true>, grid, dim3(256), 0, stream, a, g);
@@ -812,7 +851,8 @@ PMML_API int pmml_gemm_launch(hipStream_t stream, const GemmArgs* args, int head
   if (a.rows_p % BM || a.rows_p < a.rows || a.K % sk || a.K <= 0 || a.Mp % BN || a.Mp <= 0) return -4;
   if ((a.lda & 7) || (a.ldw & 7) || a.lda < a.K || a.ldw < a.K) return -4;
   if ((reinterpret_cast<uintptr_t>(a.A) & 15) || (reinterpret_cast<uintptr_t>(a.Wt) & 15)) return -4;
-  if (head && (a.n_out < 1 || a.n_out > 32 || a.Mp != 32 || !a.row_ok || !a.score || !a.valid)) return -4;
+  if (head && (a.n_out < 1 || a.n_out > 32 || a.Mp != 32 || (!a.C && (!a.row_ok || !a.score || !a.valid)))) return -4;
+  if (head && a.C && (a.ldc < a.n_out || (reinterpret_cast<uintptr_t>(a.C) & 3))) return -4;
   if (!head && ((a.ldc & 7) || a.ldc < a.Mp || !a.C || (reinterpret_cast<uintptr_t>(a.C) & 15))) return -4;
   if (!head && !f32 && a.K == 64 && !((a.f32 >> 6) & 1)) {  // bit 6 forces the 256 x 256 tile
     hipLaunchKernelGGL((gemm_k64_kernel<false>), dim3((a.rows_p / K64_BM) * (a.Mp / 256)), dim3(K64_NT),
@@ -861,5 +901,14 @@ PMML_API int pmml_nn_first_layer_launch(hipStream_t stream, const GemmArgs* args
   if ((a.ldc & 7) || a.ldc < a.Mp || !a.C || (reinterpret_cast<uintptr_t>(a.C) & 15) || !p.row_ok || !p.X) return -4;
   hipLaunchKernelGGL((gemm_k64_kernel<true>), dim3((a.rows_p / K64_BM) * (a.Mp / 256)), dim3(K64_NT),
                      (size_t)(K64_BM + 256) * SLICE_B, stream, a, p);
+  return hipGetLastError() == hipSuccess ? 0 : -7;
+}
+
+// Decode of a wide output layer (n_out > 32) from its activated outputs Z [rows][ldz] fp32.
+PMML_API int pmml_nn_decode_wide(hipStream_t stream, const GemmArgs* args, const float* Z, int ldz) {
+  const GemmArgs a = *args;
+  if (a.rows <= 0) return 0;
+  if (a.n_out < 1 || ldz < a.n_out || !Z || !a.row_ok || !a.score || !a.valid) return -4;
+  hipLaunchKernelGGL(nn_decode_wide_kernel, dim3((a.rows + 255) / 256), dim3(256), 0, stream, a, Z, ldz);
   return hipGetLastError() == hipSuccess ? 0 : -7;
 }

@@ -388,18 +388,18 @@ class WideMlpPlan(MlpPlan):
             raise ValueError("precision must be bf16 or fp32")
         self.bf16 = 1 if precision == "bf16" else 0
         layers, _ = self._io(compiled, ev)
-        if self.n_out > 32:
-            raise NotLowerable("more than 32 output neurons")
+        if self.n_out > 1024:
+            raise NotLowerable("more than 1024 output neurons")
         self.k0 = _ceil(max(self.n_in, 1), 64)
-        if self.k0 > 512:
-            raise NotLowerable("more than 512 network inputs (wide-layer input stage)")
+        if self.k0 > 16384:
+            raise NotLowerable("more than 16384 network inputs (wide-layer input stage)")
         wts, bss, dims = [], [], []
         wo = bo = 0
         kp = self.k0
         for li, (W, b, act, thr, _) in enumerate(layers):
             k, m = W.shape
             head = li == len(layers) - 1
-            mp = 32 if head else _ceil(m, 256)
+            mp = _ceil(m, 32) if head else _ceil(m, 256)  # output layer: 32-unit groups
             Wt = np.zeros((mp, kp), dtype=np.float32)
             Wt[:m, :k] = np.asarray(W, np.float32).T
             bias = np.zeros(mp, dtype=np.float32)
@@ -420,7 +420,8 @@ class WideMlpPlan(MlpPlan):
     fuse_head = True
 
     def _fused_head(self) -> bool:
-        return bool(self.fuse_head) and self.bf16 == 1 and len(self.dims) >= 2 and self.dims[-2][0] % 64 == 0
+        return (bool(self.fuse_head) and self.bf16 == 1 and len(self.dims) >= 2 and self.dims[-2][0] % 64 == 0
+                and self.n_out <= 32)
 
     # bf16, <= 64 network inputs: the input stage runs inside the first layer's GEMM (gemm_k64_kernel<true>)
     fuse_input = False  # measured slower (profiles/r4j: the gather in the GEMM prologue, 1.43 vs 0.18 + 0.82 ms)
@@ -510,8 +511,19 @@ class WideMlpPlan(MlpPlan):
                     check(self.lib.pmml_gemm_fused_head_launch(h, ctypes.byref(pending), ctypes.byref(a),
                                                                whp.data_ptr(), part.data_ptr()),
                           "nn fused last-hidden + output-layer gemm")
-                else:
+                elif mp <= 32:
                     check(self.lib.pmml_gemm_launch(h, ctypes.byref(a), 1), "nn output-layer gemm")
+                else:  # > 32 outputs: one 32-unit group per launch into Z, then the wide decode
+                    with torch.cuda.stream(st):
+                        Z = torch.empty((rows_p, mp), dtype=torch.float32, device=self.device)
+                    extra.append(Z)
+                    for g in range(mp // 32):
+                        ag = GemmArgs.from_buffer_copy(a)
+                        ag.Wt, ag.bias = wbase + es * (wo + g * 32 * kp), bbase + 4 * (bo + 32 * g)
+                        ag.Mp, ag.n_out = 32, min(32, self.n_out - 32 * g)
+                        ag.C, ag.ldc = Z.data_ptr() + 4 * 32 * g, mp
+                        check(self.lib.pmml_gemm_launch(h, ctypes.byref(ag), 1), "nn output-layer gemm (group)")
+                    check(self.lib.pmml_nn_decode_wide(h, ctypes.byref(a), Z.data_ptr(), mp), "nn wide decode")
             elif fused and li == len(self.dims) - 2:
                 pending = a  # its activations go straight into the output layer's MFMAs
             else:

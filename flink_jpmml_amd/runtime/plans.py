@@ -1869,7 +1869,7 @@ def compile_plan(compiled, device, **opts) -> DevicePlan:
                 raise
             try:  # wide layers: one fused MFMA GEMM launch per layer (ops/csrc/gemm.hip), bf16 or fp32
                 return WideMlpPlan(compiled, device, precision=prec)
-            except NotLowerable:  # > 32 outputs or > 512 inputs: library GEMMs
+            except NotLowerable:  # > 32 outputs or > 16384 inputs: library GEMMs
                 return GemmMlpPlan(compiled, device, precision=prec)
     if isinstance(ev, SvmEvaluator):
         from .nn_plans import SvmGemmPlan, SvmPlan, SvmWidePlan

@@ -15,6 +15,7 @@ from flink_jpmml_amd.runtime.compiled import CompiledPmml
 
 SHAPES = [
     dict(n_features=32, hidden=(1024,), n_out=1, activation="rectifier"),
+    dict(n_features=600, hidden=(300,), n_out=40, activation="tanh", classification=True),
     dict(n_features=40, hidden=(300, 1024), n_out=1, activation="logistic"),
     dict(n_features=21, hidden=(512,), n_out=5, activation="tanh", classification=True),
     dict(n_features=16, hidden=(64,) * 9, n_out=1, activation="rectifier"),
@@ -101,12 +102,22 @@ def test_fp32_policy_runs_fp32_wide_gemm(shape):
         assert np.abs(s[v] - ref[v]).max() < 1e-4 * scale
 
 
-def test_library_gemm_beyond_wide_limits():
-    """More than 32 output neurons: the wide GEMM's output tile is 32 units — library GEMMs."""
-    from flink_jpmml_amd.runtime.nn_plans import GemmMlpPlan
+def test_wide_plan_covers_many_outputs_and_inputs():
+    """More than 32 output neurons (32-unit output groups + the streaming wide decode) and more
+    than 512 inputs (the input stage spreads a row's chunks over a wave) stay on the hand-written
+    GEMM; only past 1024 outputs do library GEMMs take over."""
+    from flink_jpmml_amd.runtime.nn_plans import GemmMlpPlan, WideMlpPlan
     from flink_jpmml_amd.runtime.plans import compile_plan, lowering_dry_run
 
     c = CompiledPmml.from_string(mlp_pmml(n_features=8, hidden=(300,), n_out=40, classification=True, seed=1))
+    with lowering_dry_run():
+        plan = compile_plan(c, torch.device("cpu"))
+    assert isinstance(plan, WideMlpPlan) and plan.dims[-1][1] == 64 and not plan._fused_head()
+    c = CompiledPmml.from_string(mlp_pmml(n_features=700, hidden=(300,), n_out=1, seed=1))
+    with lowering_dry_run():
+        plan = compile_plan(c, torch.device("cpu"))
+    assert isinstance(plan, WideMlpPlan) and plan.k0 == 704
+    c = CompiledPmml.from_string(mlp_pmml(n_features=4, hidden=(8,), n_out=1030, classification=True, seed=1))
     with lowering_dry_run():
         assert isinstance(compile_plan(c, torch.device("cpu")), GemmMlpPlan)
 
