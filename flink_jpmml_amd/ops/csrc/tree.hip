@@ -400,16 +400,36 @@ __global__ __launch_bounds__(TB, 2) void tree_super_kernel(TreeArgs a) {
 // once per workgroup (a branchless binary search per feature) into LDS; then a record holds a
 // 3-level subtree (7 nodes: 8-bit rank, 5-bit feature, default-right bit each) plus its exit
 // block, so one 16-byte gather serves three levels (the deep-forest walk is bound by gather
-// instructions / L1 line accesses per visited level, profiles/r3w). Record bits: lo = x | y << 32:
-// rank of node n at 8 n, live-exit mask at 56; hi = z | w << 32: feature of node n at 5 n,
-// default-right at 35 + n, exit block offset (from the tree's base slot) at 42 (21 bits), bit
-// 63 = leaf slot (x = the weighted leaf value, or the leaf row for P > 1). Nodes: 0 the root,
+// instructions / L1 line accesses per visited level, profiles/r3w). Record words: rank3_step; a
+// leaf slot has bit 31 of w set and x = the weighted leaf value (or the leaf row for P > 1).
+// Nodes: 0 the root,
 // 1 / 2 its children, 3..6 the grandchildren; exit e = 4 b0 + 2 b1 + b2 lives at block +
 // popcount(mask below e) (only live exits are stored; a block stays within one 128-byte line).
 // Leaves above the third level are padded with never-right nodes (rank 255). The root record is
 // read with a wave-uniform (scalar) load. Lock-step walks, leaves accumulated in tree order
 // (bit-identical to tree_pointer_kernel).
 constexpr uint32_t RK_NAN = 255;
+
+// One record step: the three levels' decisions, then the exit's slot offset from the tree base.
+// Every field sits inside one 32-bit word (runtime/hybrid.py record layout): x = ranks 0-3,
+// y = ranks 4-6 | live-exit mask << 24, z = features 0-5 | default-right 0 / 1 << 30 / 31,
+// w = feature 6 | default-right 2-6 << 5.. | block offset << 10 | leaf << 31.
+__device__ __forceinline__ int rank3_step(const uint4 rec, const uint32_t* rk_lane) {
+  auto decide = [](uint32_t k, uint32_t r, uint32_t d) -> uint32_t { return k == RK_NAN ? d : (uint32_t)(k >= r); };
+  // level 0: node 0
+  const uint32_t b0 = decide(rk_lane[(rec.z & 31u) * TB], rec.x & 255u, (rec.z >> 30) & 1u);
+  // level 1: node 1 + b0 (features / ranks in z / x; default-right bit 31 of z or bit 5 of w)
+  const uint32_t n1 = 1u + b0;
+  const uint32_t b1 = decide(rk_lane[((rec.z >> (5u * n1)) & 31u) * TB], (rec.x >> (8u * n1)) & 255u,
+                             b0 ? ((rec.w >> 5) & 1u) : (rec.z >> 31));
+  // level 2: node 3 + 2 b0 + b1 (3 .. 6)
+  const uint32_t n2 = 3u + 2u * b0 + b1;
+  const uint32_t f2 = n2 == 6u ? (rec.w & 31u) : ((rec.z >> (5u * n2)) & 31u);
+  const uint32_t r2 = n2 == 3u ? (rec.x >> 24) : ((rec.y >> (8u * (n2 - 4u))) & 255u);
+  const uint32_t b2 = decide(rk_lane[f2 * TB], r2, (rec.w >> (n2 + 3u)) & 1u);
+  const uint32_t e = 4u * b0 + 2u * b1 + b2;
+  return (int)((rec.w >> 10) & 0x1FFFFFu) + __popc((rec.y >> 24) & ((1u << e) - 1u));
+}
 
 template <bool GENERAL, int PILP = 8>
 __global__ __launch_bounds__(TB, 2) void tree_rank3_kernel(TreeArgs a) {
@@ -490,22 +510,8 @@ __global__ __launch_bounds__(TB, 2) void tree_rank3_kernel(TreeArgs a) {
       for (int i = 0; i < PILP; ++i) rt[i] = nodes[__builtin_amdgcn_readfirstlane(base[i])];
 #pragma unroll
       for (int i = 0; i < PILP; ++i) {
-        const uint64_t lo = (uint64_t)rt[i].x | ((uint64_t)rt[i].y << 32);
-        const uint64_t hi = (uint64_t)rt[i].z | ((uint64_t)rt[i].w << 32);
         const bool leaf = (rt[i].w >> 31) != 0u;
-        auto rank_of = [&](int n) -> uint32_t { return rk_lane[((uint32_t)(hi >> (5 * n)) & 31u) * TB]; };
-        auto right = [&](uint32_t k, int n) -> int {
-          const uint32_t r = (uint32_t)(lo >> (8 * n)) & 255u;
-          const uint32_t d = (uint32_t)(hi >> (35 + n)) & 1u;
-          return (int)(k == RK_NAN ? d : (uint32_t)(k >= r));
-        };
-        const int b0 = right(rank_of(0), 0);
-        const int b1 = right(rank_of(1 + b0), 1 + b0);
-        const int n2 = 3 + 2 * b0 + b1;
-        const int b2 = right(rank_of(n2), n2);
-        const int e = 4 * b0 + 2 * b1 + b2;
-        const uint32_t below = (rt[i].y >> 24) & ((1u << e) - 1u);
-        const int nxt = base[i] + (int)((hi >> 42) & 0x1FFFFFu) + __popc(below);
+        const int nxt = base[i] + rank3_step(rt[i], rk_lane);
         leafv[i] = (act[i] && leaf) ? rt[i].x : leafv[i];
         pos[i] = (act[i] && !leaf) ? nxt : pos[i];
         act[i] = act[i] && !leaf;
@@ -521,22 +527,8 @@ __global__ __launch_bounds__(TB, 2) void tree_rank3_kernel(TreeArgs a) {
       live = false;
 #pragma unroll
       for (int i = 0; i < PILP; ++i) {
-        const uint64_t lo = (uint64_t)nd[i].x | ((uint64_t)nd[i].y << 32);
-        const uint64_t hi = (uint64_t)nd[i].z | ((uint64_t)nd[i].w << 32);
         const bool leaf = (nd[i].w >> 31) != 0u;
-        auto rank_of = [&](int n) -> uint32_t { return rk_lane[((uint32_t)(hi >> (5 * n)) & 31u) * TB]; };
-        auto right = [&](uint32_t k, int n) -> int {
-          const uint32_t r = (uint32_t)(lo >> (8 * n)) & 255u;
-          const uint32_t d = (uint32_t)(hi >> (35 + n)) & 1u;
-          return (int)(k == RK_NAN ? d : (uint32_t)(k >= r));
-        };
-        const int b0 = right(rank_of(0), 0);
-        const int b1 = right(rank_of(1 + b0), 1 + b0);
-        const int n2 = 3 + 2 * b0 + b1;
-        const int b2 = right(rank_of(n2), n2);
-        const int e = 4 * b0 + 2 * b1 + b2;
-        const uint32_t below = (nd[i].y >> 24) & ((1u << e) - 1u);  // live exits before e
-        const int nxt = base[i] + (int)((hi >> 42) & 0x1FFFFFu) + __popc(below);
+        const int nxt = base[i] + rank3_step(nd[i], rk_lane);
         leafv[i] = (act[i] && leaf) ? nd[i].x : leafv[i];
         pos[i] = (act[i] && !leaf) ? nxt : pos[i];
         act[i] = act[i] && !leaf;

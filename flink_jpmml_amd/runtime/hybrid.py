@@ -475,16 +475,20 @@ __all__ += ["pack_compact_bfs", "pack_super"]
 
 # ------------------------------------------------------------------------------------------------
 # RANK3: three tree levels per 16-byte record on per-feature threshold ranks (tree.hip
-# tree_rank3_kernel). Record bits — lo = words 0-1: rank of node n (8 bits) at 8 n, live-exit mask
-# at 56 (8 bits); hi = words 2-3: feature of node n (5 bits) at 5 n, default-right of node n at
-# 35 + n, exit block offset from the tree's base slot at 42 (21 bits), bit 63 = leaf slot (word 0
-# = weighted value / leaf row). Only the live exits of a record are stored: exit e sits at
+# tree_rank3_kernel). Words (every field inside one 32-bit word, so the walk extracts it with one
+# shift-and-mask): x = ranks of nodes 0-3 (8 bits each); y = ranks of nodes 4-6 | live-exit mask
+# << 24; z = features of nodes 0-5 (5 bits each) | default-right of nodes 0 / 1 at bits 30 / 31;
+# w = feature of node 6 | default-right of nodes 2-6 at bits 5-9 | exit block offset from the
+# tree's base slot << 10 (21 bits) | leaf slot << 31 (a leaf slot's x = weighted value / leaf row). Only the live exits of a record are stored: exit e sits at
 # block + popcount(mask & ((1 << e) - 1)); a block never straddles a 128-byte line.
 RK_NAN = 255        # a missing value's rank (csrc RK_NAN)
 RK_NEVER = 255      # a padding node's rank: never "right" (ranks of values are <= 254)
 RK_MAX_UNIQUE = 254
 RK_LINE = 8         # 16-byte slots per 128-byte line
 RK_OFF_BITS = 21
+# bit of node n's feature / default-right flag in hi = words 2-3 (every field inside one 32-bit word)
+_RK_FSHIFT = np.array([0, 5, 10, 15, 20, 25, 32], dtype=np.uint64)
+_RK_DSHIFT = np.array([30, 31, 37, 38, 39, 40, 41], dtype=np.uint64)
 
 
 def rank_tables(trees, n_features: int):
@@ -588,8 +592,7 @@ def _rank3_tree(feat, internal, lc, rc, dr, rank, t, w, P, leaf0):
         sh = np.arange(7, dtype=np.uint64)
         mask = (live.astype(np.uint64) << np.arange(8, dtype=np.uint64)).sum(1)
         lo = (r << (np.uint64(8) * sh)).sum(1) | (mask << np.uint64(56))
-        hi = (f << (np.uint64(5) * sh)).sum(1) | (d << (np.uint64(35) + sh)).sum(1) | \
-            (bases.astype(np.uint64) << np.uint64(42))
+        hi = (f << _RK_FSHIFT).sum(1) | (d << _RK_DSHIFT).sum(1) | (bases.astype(np.uint64) << np.uint64(42))
         rec = np.stack([lo & np.uint64(0xFFFFFFFF), lo >> np.uint64(32), hi & np.uint64(0xFFFFFFFF),
                         hi >> np.uint64(32)], 1).astype(np.uint32)
         chunks.append((fs, rec))
@@ -714,8 +717,8 @@ def pack_rank3(trees, weights: List[float], P: int, n_features: int, vectorized:
             for n, (kind, v) in enumerate(nodes7):
                 if kind == "n":
                     lo |= int(rank[v]) << (8 * n)
-                    hi |= int(feat[v]) << (5 * n)
-                    hi |= int(dr[v]) << (35 + n)
+                    hi |= int(feat[v]) << int(_RK_FSHIFT[n])
+                    hi |= int(dr[v]) << int(_RK_DSHIFT[n])
                 else:
                     lo |= RK_NEVER << (8 * n)
             hi |= base << 42

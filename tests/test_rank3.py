@@ -35,11 +35,13 @@ def walk_rank3(nodes, roots, thr, cnt, X, P=1, leaves=None):
             done = act & leaf
             leafv[done] = nodes[pos[done], 0]
 
+            fsh = np.array([0, 5, 10, 15, 20, 25, 32], dtype=np.uint64)
+            dsh = np.array([30, 31, 37, 38, 39, 40, 41], dtype=np.uint64)
+
             def right(nn):
-                nn = nn.astype(np.uint64)
-                f = ((h_ >> (np.uint64(5) * nn)) & np.uint64(31)).astype(np.int64)
-                r = ((l_ >> (np.uint64(8) * nn)) & np.uint64(255)).astype(np.int64)
-                d = ((h_ >> (np.uint64(35) + nn)) & np.uint64(1)).astype(np.int64)
+                f = ((h_ >> fsh[nn]) & np.uint64(31)).astype(np.int64)
+                r = ((l_ >> (np.uint64(8) * nn.astype(np.uint64))) & np.uint64(255)).astype(np.int64)
+                d = ((h_ >> dsh[nn]) & np.uint64(1)).astype(np.int64)
                 k = rk[rows, f]
                 return np.where(k == RK_NAN, d, (k >= r).astype(np.int64))
 
