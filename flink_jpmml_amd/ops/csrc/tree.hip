@@ -412,31 +412,35 @@ constexpr uint32_t RK_NAN = 255;
 
 // One record step: the three levels' decisions, then the exit's slot offset from the tree base.
 // Every field sits inside one 32-bit word (runtime/hybrid.py record layout): x = ranks 0-3,
-// y = ranks 4-6 | live-exit mask << 24, z = plane indices 0-4 (6 bits: feature | default-right
-// << 5), w = planes 5 / 6 | block offset << 12 | leaf << 31. A level is one LDS read and one
-// compare: the plane of a default-right node ranks missing values 255 (right), the other 0 (left).
+// y = ranks 4-6 | live-exit mask << 24, z = features 0-5 | default-right 0 / 1 << 30 / 31,
+// w = feature 6 | default-right 2-6 << 5.. | block offset << 10 | leaf << 31.
 __device__ __forceinline__ int rank3_step(const uint4 rec, const uint32_t* rk_lane) {
-  const uint32_t b0 = rk_lane[(rec.z & 63u) * TB] >= (rec.x & 255u);
+  auto decide = [](uint32_t k, uint32_t r, uint32_t d) -> uint32_t { return k == RK_NAN ? d : (uint32_t)(k >= r); };
+  // level 0: node 0
+  const uint32_t b0 = decide(rk_lane[(rec.z & 31u) * TB], rec.x & 255u, (rec.z >> 30) & 1u);
+  // level 1: node 1 + b0 (features / ranks in z / x; default-right bit 31 of z or bit 5 of w)
   const uint32_t n1 = 1u + b0;
-  const uint32_t b1 = rk_lane[((rec.z >> (6u * n1)) & 63u) * TB] >= ((rec.x >> (8u * n1)) & 255u);
-  const uint32_t n2 = 3u + 2u * b0 + b1;  // 3 .. 6
-  const uint32_t p2 = n2 <= 4u ? ((rec.z >> (6u * n2)) & 63u) : ((rec.w >> (6u * (n2 - 5u))) & 63u);
+  const uint32_t b1 = decide(rk_lane[((rec.z >> (5u * n1)) & 31u) * TB], (rec.x >> (8u * n1)) & 255u,
+                             b0 ? ((rec.w >> 5) & 1u) : (rec.z >> 31));
+  // level 2: node 3 + 2 b0 + b1 (3 .. 6)
+  const uint32_t n2 = 3u + 2u * b0 + b1;
+  const uint32_t f2 = n2 == 6u ? (rec.w & 31u) : ((rec.z >> (5u * n2)) & 31u);
   const uint32_t r2 = n2 == 3u ? (rec.x >> 24) : ((rec.y >> (8u * (n2 - 4u))) & 255u);
-  const uint32_t b2 = rk_lane[p2 * TB] >= r2;
+  const uint32_t b2 = decide(rk_lane[f2 * TB], r2, (rec.w >> (n2 + 3u)) & 1u);
   const uint32_t e = 4u * b0 + 2u * b1 + b2;
-  return (int)((rec.w >> 12) & 0x7FFFFu) + __popc((rec.y >> 24) & ((1u << e) - 1u));
+  return (int)((rec.w >> 10) & 0x1FFFFFu) + __popc((rec.y >> 24) & ((1u << e) - 1u));
 }
 
 template <bool GENERAL, int PILP = 8>
 __global__ __launch_bounds__(TB, 2) void tree_rank3_kernel(TreeArgs a) {
   extern __shared__ __align__(16) uint32_t smem[];
-  // [64 rank planes][bad][class slots][threshold tables]; the features are staged in the first
-  // F planes and their ranks overwrite them in place (a lane only ever reads its own row); 32-bit
-  // entries keep every lane on its own bank whatever plane it reads
   float* feat = reinterpret_cast<float*>(smem);
-  int* bad = reinterpret_cast<int*>(smem + 64 * TB);
+  int* bad = reinterpret_cast<int*>(smem + a.n_feat * TB);
   float* accl = reinterpret_cast<float*>(bad + TB);
-  uint32_t* rk = smem;  // plane f: missing -> 0; plane 32 + f: missing -> RK_NAN
+  // ranks overwrite the feature planes in place (a lane only ever reads its own row): 32-bit
+  // entries keep every lane on its own bank whatever feature it reads (16-bit planes put two
+  // lanes on one bank: 2-way conflicts on every rank read of the walk)
+  uint32_t* rk = reinterpret_cast<uint32_t*>(feat);  // [F][TB]
   const int tid = threadIdx.x;
   const int2 blk = tree_block(a);
   const int row0 = blk.x * TB;
@@ -475,11 +479,7 @@ __global__ __launch_bounds__(TB, 2) void tree_rank3_kernel(TreeArgs a) {
     }
 #pragma unroll
     for (int k = 0; k < 8; ++k)
-      if (f0 + k < a.n_feat) {
-        const bool miss = x[k] != x[k];
-        rk[(f0 + k) * TB + tid] = miss ? 0u : (uint32_t)pos[k];
-        rk[(32 + f0 + k) * TB + tid] = miss ? RK_NAN : (uint32_t)pos[k];
-      }
+      if (f0 + k < a.n_feat) rk[(f0 + k) * TB + tid] = x[k] != x[k] ? RK_NAN : (uint32_t)pos[k];
   }
   const uint32_t* rk_lane = rk + tid;
   const uint4* nodes = reinterpret_cast<const uint4*>(a.blob);
@@ -909,7 +909,7 @@ PMML_API int pmml_tree_launch(hipStream_t stream, const TreeArgs* args, int layo
     size_t lds = (feat_lds ? (size_t)a.n_feat * TB * 4 : 0) + TB * 4 + acc_lds;
     if (a.variant == VAR_POINTER_RANK3) {
       if (a.n_feat > 32 || !a.rank_thr || !a.rank_cnt || a.rank_stride < 1 || a.rank_stride > 254) return -4;
-      lds += (size_t)(64 - a.n_feat) * TB * 4 + (size_t)a.n_feat * a.rank_stride * 4;  // 64 rank planes + thresholds
+      lds += (size_t)a.n_feat * a.rank_stride * 4;  // threshold tables (ranks replace the feature planes)
       if (lds > 160 * 1024) return -5;
       if (a.general) {
         err = prepare_launch(tree_rank3_kernel<true>, lds);

@@ -475,21 +475,20 @@ __all__ += ["pack_compact_bfs", "pack_super"]
 
 # ------------------------------------------------------------------------------------------------
 # RANK3: three tree levels per 16-byte record on per-feature threshold ranks (tree.hip
-# tree_rank3_kernel). Each node carries an 8-bit rank r and a 6-bit plane index p = feature |
-# default-right << 5: the kernel keeps two rank planes per feature, missing values ranked 0 in the
-# first (never >= r: left) and 255 in the second (always >= r: right), so a level is one LDS read
-# and one compare. Words (every field inside one 32-bit word): x = ranks of nodes 0-3; y = ranks
-# of nodes 4-6 | live-exit mask << 24; z = planes of nodes 0-4 (6 bits each); w = planes of nodes
-# 5 / 6 | exit block offset from the tree's base slot << 12 (19 bits) | leaf slot << 31 (a leaf
-# slot's x = weighted value / leaf row).
-RK_NAN = 255        # a missing value's rank in the default-right planes (0 in the others)
+# tree_rank3_kernel). Words (every field inside one 32-bit word, so the walk extracts it with one
+# shift-and-mask): x = ranks of nodes 0-3 (8 bits each); y = ranks of nodes 4-6 | live-exit mask
+# << 24; z = features of nodes 0-5 (5 bits each) | default-right of nodes 0 / 1 at bits 30 / 31;
+# w = feature of node 6 | default-right of nodes 2-6 at bits 5-9 | exit block offset from the
+# tree's base slot << 10 (21 bits) | leaf slot << 31 (a leaf slot's x = weighted value / leaf row). Only the live exits of a record are stored: exit e sits at
+# block + popcount(mask & ((1 << e) - 1)); a block never straddles a 128-byte line.
+RK_NAN = 255        # a missing value's rank (csrc RK_NAN)
 RK_NEVER = 255      # a padding node's rank: never "right" (ranks of values are <= 254)
 RK_MAX_UNIQUE = 254
 RK_LINE = 8         # 16-byte slots per 128-byte line
-RK_OFF_BITS = 19
-# bit of node n's plane index (6 bits) in hi = words 2-3
-_RK_PSHIFT = np.array([0, 6, 12, 18, 24, 32, 38], dtype=np.uint64)
-_RK_OFF_SHIFT = np.uint64(44)
+RK_OFF_BITS = 21
+# bit of node n's feature / default-right flag in hi = words 2-3 (every field inside one 32-bit word)
+_RK_FSHIFT = np.array([0, 5, 10, 15, 20, 25, 32], dtype=np.uint64)
+_RK_DSHIFT = np.array([30, 31, 37, 38, 39, 40, 41], dtype=np.uint64)
 
 
 def rank_tables(trees, n_features: int):
@@ -584,7 +583,7 @@ def _rank3_tree(feat, internal, lc, rc, dr, rank, t, w, P, leaf0):
             pos += nl[i]
         n_slots = pos
         if n_slots >= (1 << RK_OFF_BITS):
-            raise ValueError("rank3 layout: tree needs more than 2^19 slots")
+            raise ValueError("rank3 layout: tree needs more than 2^21 slots")
         isn = kind == _K_N
         vn = np.where(isn, val, 0)
         r = np.where(isn, rank[vn], np.uint64(RK_NEVER)).astype(np.uint64)
@@ -593,7 +592,7 @@ def _rank3_tree(feat, internal, lc, rc, dr, rank, t, w, P, leaf0):
         sh = np.arange(7, dtype=np.uint64)
         mask = (live.astype(np.uint64) << np.arange(8, dtype=np.uint64)).sum(1)
         lo = (r << (np.uint64(8) * sh)).sum(1) | (mask << np.uint64(56))
-        hi = ((f | (d << np.uint64(5))) << _RK_PSHIFT).sum(1) | (bases.astype(np.uint64) << _RK_OFF_SHIFT)
+        hi = (f << _RK_FSHIFT).sum(1) | (d << _RK_DSHIFT).sum(1) | (bases.astype(np.uint64) << np.uint64(42))
         rec = np.stack([lo & np.uint64(0xFFFFFFFF), lo >> np.uint64(32), hi & np.uint64(0xFFFFFFFF),
                         hi >> np.uint64(32)], 1).astype(np.uint32)
         chunks.append((fs, rec))
@@ -622,7 +621,7 @@ def pack_rank3(trees, weights: List[float], P: int, n_features: int, vectorized:
     Returns ``(nodes [n, 4] u32, leaves [n_leaves, P] f32 or None, roots [n_trees] i32 (base slot of
     each tree), thr [F, stride] f32, cnt [F] i32, has_dr)``; ``ValueError`` when a feature index
     is >= 32, a feature has more than 254 unique thresholds, a tree is null-on-missing or needs
-    more than 2^19 slots. ``vectorized=False``: the record-by-record reference builder (the same
+    more than 2^21 slots. ``vectorized=False``: the record-by-record reference builder (the same
     arrays, tests/test_rank3.py)."""
     from .plans import _canonical_vec
 
@@ -712,16 +711,17 @@ def pack_rank3(trees, weights: List[float], P: int, n_features: int, vectorized:
             base = n_slots
             n_slots += len(live)
             if base >= (1 << RK_OFF_BITS):
-                raise ValueError("rank3 layout: tree needs more than 2^19 slots")
+                raise ValueError("rank3 layout: tree needs more than 2^21 slots")
             lo = mask << 56
             hi = 0
             for n, (kind, v) in enumerate(nodes7):
                 if kind == "n":
                     lo |= int(rank[v]) << (8 * n)
-                    hi |= (int(feat[v]) | int(dr[v]) << 5) << int(_RK_PSHIFT[n])
+                    hi |= int(feat[v]) << int(_RK_FSHIFT[n])
+                    hi |= int(dr[v]) << int(_RK_DSHIFT[n])
                 else:
                     lo |= RK_NEVER << (8 * n)
-            hi |= base << int(_RK_OFF_SHIFT)
+            hi |= base << 42
             rec = np.array([lo & 0xFFFFFFFF, lo >> 32, hi & 0xFFFFFFFF, hi >> 32], dtype=np.uint64).astype(np.uint32)
             slots[s] = rec
             for j, c in enumerate(live):

@@ -16,18 +16,15 @@ from flink_jpmml_amd.runtime.plans import _canonical_vec, ensemble_spec
 def walk_rank3(nodes, roots, thr, cnt, X, P=1, leaves=None):
     """numpy model of tree_rank3_kernel: per row, ranks by upper_bound, then record walks."""
     n, F = X.shape
-    rk = np.zeros((n, 64), dtype=np.int64)  # planes f (missing -> 0) and 32 + f (missing -> 255)
+    rk = np.full((n, F), RK_NAN, dtype=np.int64)
     for f in range(F):
         t = thr[f, : cnt[f]]
         ok = ~np.isnan(X[:, f])
-        r = np.searchsorted(t, np.where(ok, X[:, f], 0), side="right")
-        rk[:, f] = np.where(ok, r, 0)
-        rk[:, 32 + f] = np.where(ok, r, RK_NAN)
+        rk[ok, f] = np.searchsorted(t, X[ok, f], side="right")
     lo = nodes[:, 0].astype(np.uint64) | (nodes[:, 1].astype(np.uint64) << np.uint64(32))
     hi = nodes[:, 2].astype(np.uint64) | (nodes[:, 3].astype(np.uint64) << np.uint64(32))
     out = np.zeros((n, P), dtype=np.float32)
     rows = np.arange(n)
-    psh = np.array([0, 6, 12, 18, 24, 32, 38], dtype=np.uint64)
     for base in roots.astype(np.int64):
         pos = np.full(n, base, dtype=np.int64)
         act = np.ones(n, dtype=bool)
@@ -38,10 +35,15 @@ def walk_rank3(nodes, roots, thr, cnt, X, P=1, leaves=None):
             done = act & leaf
             leafv[done] = nodes[pos[done], 0]
 
+            fsh = np.array([0, 5, 10, 15, 20, 25, 32], dtype=np.uint64)
+            dsh = np.array([30, 31, 37, 38, 39, 40, 41], dtype=np.uint64)
+
             def right(nn):
-                p = ((h_ >> psh[nn]) & np.uint64(63)).astype(np.int64)
+                f = ((h_ >> fsh[nn]) & np.uint64(31)).astype(np.int64)
                 r = ((l_ >> (np.uint64(8) * nn.astype(np.uint64))) & np.uint64(255)).astype(np.int64)
-                return (rk[rows, p] >= r).astype(np.int64)
+                d = ((h_ >> dsh[nn]) & np.uint64(1)).astype(np.int64)
+                k = rk[rows, f]
+                return np.where(k == RK_NAN, d, (k >= r).astype(np.int64))
 
             b0 = right(np.zeros(n, np.int64))
             b1 = right(1 + b0)
@@ -49,7 +51,7 @@ def walk_rank3(nodes, roots, thr, cnt, X, P=1, leaves=None):
             e = 4 * b0 + 2 * b1 + b2
             mask = ((l_ >> np.uint64(56)) & np.uint64(255)).astype(np.int64) & ((1 << e) - 1)
             below = np.array([bin(m).count("1") for m in mask], dtype=np.int64)
-            nxt = base + ((h_ >> np.uint64(44)) & np.uint64(0x7FFFF)).astype(np.int64) + below
+            nxt = base + ((h_ >> np.uint64(42)) & np.uint64(0x1FFFFF)).astype(np.int64) + below
             go = act & ~leaf
             pos = np.where(go, nxt, pos)
             act = go
