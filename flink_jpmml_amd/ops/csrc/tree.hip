@@ -449,14 +449,13 @@ __global__ __launch_bounds__(TB, 2) void tree_rank3_kernel(TreeArgs a) {
   stage_rows_T<TB>(a.X, a.n_rows, a.n_feat, a.ldx, a.prep, feat, bad, row0);
   bool row_ok = bad[tid] == 0;
   if (a.row_valid_in && row < a.n_rows) row_ok = row_ok && a.row_valid_in[row];
-  // ranks of this lane's row: the threshold tables staged in LDS, then 8 features' branchless
-  // binary searches advanced together (8 independent LDS reads in flight per step; a dependent
-  // global-memory search per feature left every workgroup idle for tens of microseconds before
-  // its first tree). Only this lane reads its ranks back: no barrier after.
-  float* thr_l = accl + (GENERAL ? a.C * TB : 0);  // [F][rank_stride]
+  // ranks of this lane's row: 8 features' branchless binary searches advanced together (8
+  // independent cached reads in flight per step; a dependent search per feature left every
+  // workgroup idle for tens of microseconds before its first tree). The tables stay in global
+  // memory (L1-resident; staging them in LDS cost a workgroup per CU, profiles/r4q). Only this
+  // lane reads its ranks back: no barrier after.
+  const float* thr_l = a.rank_thr;  // [F][rank_stride]
   const int stride = a.rank_stride;
-  for (int e = tid; e < a.n_feat * stride; e += TB) thr_l[e] = a.rank_thr[e];
-  __syncthreads();
   for (int f0 = 0; f0 < a.n_feat; f0 += 8) {
     float x[8];
     int pos[8], cnt[8];
@@ -909,7 +908,7 @@ PMML_API int pmml_tree_launch(hipStream_t stream, const TreeArgs* args, int layo
     size_t lds = (feat_lds ? (size_t)a.n_feat * TB * 4 : 0) + TB * 4 + acc_lds;
     if (a.variant == VAR_POINTER_RANK3) {
       if (a.n_feat > 32 || !a.rank_thr || !a.rank_cnt || a.rank_stride < 1 || a.rank_stride > 254) return -4;
-      lds += (size_t)a.n_feat * a.rank_stride * 4;  // threshold tables (ranks replace the feature planes)
+      // (ranks replace the feature planes; the threshold tables are read from global memory)
       if (lds > 160 * 1024) return -5;
       if (a.general) {
         err = prepare_launch(tree_rank3_kernel<true>, lds);
