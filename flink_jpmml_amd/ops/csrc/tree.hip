@@ -414,20 +414,19 @@ constexpr uint32_t RK_NAN = 255;
 // Every field sits inside one 32-bit word (runtime/hybrid.py record layout): x = ranks 0-3,
 // y = ranks 4-6 | live-exit mask << 24, z = features 0-5 | default-right 0 / 1 << 30 / 31,
 // w = feature 6 | default-right 2-6 << 5.. | block offset << 10 | leaf << 31.
-__device__ __forceinline__ int rank3_step(const uint4 rec, const uint32_t* rk_lane, uint32_t hsh) {
+__device__ __forceinline__ int rank3_step(const uint4 rec, const uint32_t* rk_lane) {
   auto decide = [](uint32_t k, uint32_t r, uint32_t d) -> uint32_t { return k == RK_NAN ? d : (uint32_t)(k >= r); };
   // level 0: node 0
-  auto rank = [&](uint32_t f) -> uint32_t { return (rk_lane[f * (TB / 2)] >> hsh) & 0xFFFFu; };
-  const uint32_t b0 = decide(rank(rec.z & 31u), rec.x & 255u, (rec.z >> 30) & 1u);
+  const uint32_t b0 = decide(rk_lane[(rec.z & 31u) * TB], rec.x & 255u, (rec.z >> 30) & 1u);
   // level 1: node 1 + b0 (features / ranks in z / x; default-right bit 31 of z or bit 5 of w)
   const uint32_t n1 = 1u + b0;
-  const uint32_t b1 = decide(rank((rec.z >> (5u * n1)) & 31u), (rec.x >> (8u * n1)) & 255u,
+  const uint32_t b1 = decide(rk_lane[((rec.z >> (5u * n1)) & 31u) * TB], (rec.x >> (8u * n1)) & 255u,
                              b0 ? ((rec.w >> 5) & 1u) : (rec.z >> 31));
   // level 2: node 3 + 2 b0 + b1 (3 .. 6)
   const uint32_t n2 = 3u + 2u * b0 + b1;
   const uint32_t f2 = n2 == 6u ? (rec.w & 31u) : ((rec.z >> (5u * n2)) & 31u);
   const uint32_t r2 = n2 == 3u ? (rec.x >> 24) : ((rec.y >> (8u * (n2 - 4u))) & 255u);
-  const uint32_t b2 = decide(rank(f2), r2, (rec.w >> (n2 + 3u)) & 1u);
+  const uint32_t b2 = decide(rk_lane[f2 * TB], r2, (rec.w >> (n2 + 3u)) & 1u);
   const uint32_t e = 4u * b0 + 2u * b1 + b2;
   return (int)((rec.w >> 10) & 0x1FFFFFu) + __popc((rec.y >> 24) & ((1u << e) - 1u));
 }
@@ -435,27 +434,26 @@ __device__ __forceinline__ int rank3_step(const uint4 rec, const uint32_t* rk_la
 template <bool GENERAL, int PILP = 8>
 __global__ __launch_bounds__(TB, 2) void tree_rank3_kernel(TreeArgs a) {
   extern __shared__ __align__(16) uint32_t smem[];
-  // [F x 128 rank dwords][bad TB][class slots]: 16-bit ranks, two rows per dword — rows r and
-  // r + 64 of the workgroup share one (waves 0 / 1 and 2 / 3 take the low / high halves), so the
-  // 64 lanes of a wave read 64 distinct dwords on 64 banks whatever feature each reads: conflict
-  // free at half the LDS of 32-bit planes (17 KiB for 32 features: more workgroups per CU hide
-  // the walk's latency, profiles/r4r)
-  uint32_t* rk = smem;
-  int* bad = reinterpret_cast<int*>(smem + a.n_feat * (TB / 2));
+  float* feat = reinterpret_cast<float*>(smem);
+  int* bad = reinterpret_cast<int*>(smem + a.n_feat * TB);
   float* accl = reinterpret_cast<float*>(bad + TB);
+  // ranks overwrite the feature planes in place (a lane only ever reads its own row): 32-bit
+  // entries keep every lane on its own bank whatever feature it reads (16-bit planes put two
+  // lanes on one bank: 2-way conflicts on every rank read of the walk)
+  uint32_t* rk = reinterpret_cast<uint32_t*>(feat);  // [F][TB]
   const int tid = threadIdx.x;
   const int2 blk = tree_block(a);
   const int row0 = blk.x * TB;
   const int split = blk.y;
   const int row = row0 + tid;
-  const int lane_dw = (tid & 63) + 64 * (tid >> 7);
-  const uint32_t hsh = 16u * ((uint32_t)(tid >> 6) & 1u);
-  uint16_t* rk16 = reinterpret_cast<uint16_t*>(rk);
-  // lane = row: read the row, prepare it, rank every feature (8 features' branchless binary
-  // searches over the L1-resident threshold tables advanced together)
-  const bool live = row < a.n_rows;
-  const float* xr = a.X + (size_t)(live ? row : 0) * a.ldx;
-  bool bad_row = false;
+  stage_rows_T<TB>(a.X, a.n_rows, a.n_feat, a.ldx, a.prep, feat, bad, row0);
+  bool row_ok = bad[tid] == 0;
+  if (a.row_valid_in && row < a.n_rows) row_ok = row_ok && a.row_valid_in[row];
+  // ranks of this lane's row: 8 features' branchless binary searches advanced together (8
+  // independent cached reads in flight per step; a dependent search per feature left every
+  // workgroup idle for tens of microseconds before its first tree). The tables stay in global
+  // memory (L1-resident; staging them in LDS cost a workgroup per CU, profiles/r4q). Only this
+  // lane reads its ranks back: no barrier after.
   const float* thr_l = a.rank_thr;  // [F][rank_stride]
   const int stride = a.rank_stride;
   for (int f0 = 0; f0 < a.n_feat; f0 += 8) {
@@ -463,15 +461,9 @@ __global__ __launch_bounds__(TB, 2) void tree_rank3_kernel(TreeArgs a) {
     int pos[8], cnt[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      const int f = f0 + k;
-      const bool on = f < a.n_feat;
-      float v = __builtin_nanf("");
-      if (on && live) {
-        v = xr[f];
-        if (a.prep) v = prep_value(v, a.prep[f], &bad_row);
-      }
-      x[k] = v;
-      cnt[k] = on ? a.rank_cnt[f] : 0;
+      const bool on = f0 + k < a.n_feat;
+      x[k] = on ? feat[(f0 + k) * TB + tid] : 0.f;
+      cnt[k] = on ? a.rank_cnt[f0 + k] : 0;
       pos[k] = 0;  // #{t <= x}
     }
 #pragma unroll
@@ -486,13 +478,9 @@ __global__ __launch_bounds__(TB, 2) void tree_rank3_kernel(TreeArgs a) {
     }
 #pragma unroll
     for (int k = 0; k < 8; ++k)
-      if (f0 + k < a.n_feat)
-        rk16[2 * ((f0 + k) * (TB / 2) + lane_dw) + (hsh >> 4)] = (uint16_t)(x[k] != x[k] ? RK_NAN : (uint32_t)pos[k]);
+      if (f0 + k < a.n_feat) rk[(f0 + k) * TB + tid] = x[k] != x[k] ? RK_NAN : (uint32_t)pos[k];
   }
-  bad[tid] = bad_row ? 1 : 0;
-  bool row_ok = !bad_row;
-  if (a.row_valid_in && live) row_ok = row_ok && a.row_valid_in[row];
-  const uint32_t* rk_lane = rk + lane_dw;
+  const uint32_t* rk_lane = rk + tid;
   const uint4* nodes = reinterpret_cast<const uint4*>(a.blob);
   const uint32_t* roots = reinterpret_cast<const uint32_t*>(a.roots);
   const int tb = split * a.trees_per_split;
@@ -522,7 +510,7 @@ __global__ __launch_bounds__(TB, 2) void tree_rank3_kernel(TreeArgs a) {
 #pragma unroll
       for (int i = 0; i < PILP; ++i) {
         const bool leaf = (rt[i].w >> 31) != 0u;
-        const int nxt = base[i] + rank3_step(rt[i], rk_lane, hsh);
+        const int nxt = base[i] + rank3_step(rt[i], rk_lane);
         leafv[i] = (act[i] && leaf) ? rt[i].x : leafv[i];
         pos[i] = (act[i] && !leaf) ? nxt : pos[i];
         act[i] = act[i] && !leaf;
@@ -539,7 +527,7 @@ __global__ __launch_bounds__(TB, 2) void tree_rank3_kernel(TreeArgs a) {
 #pragma unroll
       for (int i = 0; i < PILP; ++i) {
         const bool leaf = (nd[i].w >> 31) != 0u;
-        const int nxt = base[i] + rank3_step(nd[i], rk_lane, hsh);
+        const int nxt = base[i] + rank3_step(nd[i], rk_lane);
         leafv[i] = (act[i] && leaf) ? nd[i].x : leafv[i];
         pos[i] = (act[i] && !leaf) ? nxt : pos[i];
         act[i] = act[i] && !leaf;
@@ -920,7 +908,7 @@ PMML_API int pmml_tree_launch(hipStream_t stream, const TreeArgs* args, int layo
     size_t lds = (feat_lds ? (size_t)a.n_feat * TB * 4 : 0) + TB * 4 + acc_lds;
     if (a.variant == VAR_POINTER_RANK3) {
       if (a.n_feat > 32 || !a.rank_thr || !a.rank_cnt || a.rank_stride < 1 || a.rank_stride > 254) return -4;
-      lds = (size_t)a.n_feat * (TB / 2) * 4 + TB * 4 + acc_lds;  // 16-bit rank planes, no feature planes
+      // (ranks replace the feature planes; the threshold tables are read from global memory)
       if (lds > 160 * 1024) return -5;
       if (a.general) {
         err = prepare_launch(tree_rank3_kernel<true>, lds);
