@@ -450,12 +450,14 @@ PMML_API int pmml_svm_launch(hipStream_t stream, const SvmArgs* args, int fmax, 
 PMML_API int pmml_svm_wide_args_size() { return (int)sizeof(SvmWideArgs); }
 
 // fmax in {16, 32, 64, 128} (vector fields padded), mt in {1, 2, 4} (machine tiles per group);
-// intercept / thr / tgt / alt hold n_groups * mt * 32 entries; n_classes <= 64.
+// intercept / thr / tgt / alt hold n_groups * mt * 32 entries; n_classes <= 256 (votes: TB x 128
+// packed u16 counters = 128 KiB of LDS at most), at most 65535 machines per classifier.
 PMML_API int pmml_svm_wide_launch(hipStream_t stream, const SvmWideArgs* args, int fmax, int mt) {
   const SvmWideArgs w = *args;
   const SvmArgs& a = w.s;
   if (a.n_rows <= 0) return 0;
-  if (a.n_in > fmax || a.n_classes > 64 || (a.classification && a.n_classes < 1)) return -4;
+  if (a.n_in > fmax || a.n_classes > 256) return -4;
+  if (a.classification && (a.n_classes < 1 || a.n_machines > 0xFFFF)) return -4;
   if (w.n_tiles < 1 || w.n_groups < 1 || w.n_mtiles != w.n_groups * mt || a.n_machines > w.n_mtiles * 32) return -4;
   if (!a.classification && a.n_machines != 1) return -4;
   if (a.kernel < 0 || a.kernel > 3) return -4;

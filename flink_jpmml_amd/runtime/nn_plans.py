@@ -642,9 +642,9 @@ def _pperm(i, h):
 
 
 class SvmWidePlan(DevicePlan):
-    """SupportVectorMachineModel beyond the fused kernel's limits — one-against-one over up to 64
-    classes (any number of machines), up to 128 vector fields, any number of support vectors — on
-    ``svm_wide_kernel`` (``ops/csrc/svm.hip``): the decision function as two chained exact-fp32
+    """SupportVectorMachineModel beyond the fused kernel's limits — one-against-one over up to 256
+    classes (up to 65535 machines: packed u16 vote counters), up to 128 vector fields, any number
+    of support vectors — on ``svm_wide_kernel`` (``ops/csrc/svm.hip``): the decision function as two chained exact-fp32
     MFMA products (``G = S·xᵀ`` → kernel function on the accumulators → ``D = Aᵀ·K``) fused in
     one pass, votes in LDS; the [rows x support vectors] kernel matrix never leaves the registers.
 
@@ -657,7 +657,7 @@ class SvmWidePlan(DevicePlan):
     kind = "svm_wide"
     supports_direct = True
     FMAXES = (16, 32, 64, 128)
-    CMAX = 64
+    CMAX = 256  # packed u16 vote counters: TB x 128 dwords = 128 KiB of LDS
     _KERNELS = SvmPlan._KERNELS
     _STATE = DevicePlan._STATE + ("in_index", "svA", "coefA", "svnP", "intercept", "thr", "tgt", "alt", "n_in",
                                   "n_sv", "n_machines", "kernel_code", "classification", "gamma", "coef0", "degree",
@@ -730,6 +730,8 @@ class SvmWidePlan(DevicePlan):
             cats = ev.categories
             if len(cats) > self.CMAX:
                 raise NotLowerable(f"more than {self.CMAX} SVM classes (wide kernel vote counters)")
+            if M > 0xFFFF:
+                raise NotLowerable("more than 65535 SVM machines (u16 vote counters)")
             for m, mach in enumerate(sm.machines):
                 thr[m] = mach.threshold if mach.threshold is not None else sm.threshold
                 tgt[m] = cats.index(mach.target_category)

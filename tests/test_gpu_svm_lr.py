@@ -90,3 +90,23 @@ def test_wide_regression_svm_on_gpu(gpu):
     ref, vref = c.score_matrix_oracle(X)
     assert (v == vref).all()
     np.testing.assert_allclose(s[v], ref[v], rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("n_classes,n_rows", [(100, 5_000), (256, 600)])
+def test_wide_svm_hundreds_of_classes_on_gpu(gpu, n_classes, n_rows):
+    """4950 / 32640 one-against-one machines (39 / 255 groups of 128) voting into packed u16
+    counters of up to 128 KiB of LDS, against the fp64 oracle and the library-GEMM plan."""
+    from flink_jpmml_amd.bench.synth import stream_matrix, svm_pmml
+    from flink_jpmml_amd.runtime.compiled import CompiledPmml
+
+    c = CompiledPmml.from_string(svm_pmml(n_features=10, n_sv=64, seed=9, n_classes=n_classes, gamma=0.3))
+    plan = c.plan(gpu)
+    assert type(plan).__name__ == "SvmWidePlan" and plan.n_classes == n_classes
+    X = stream_matrix(n_rows, 10, seed=4, missing_rate=0.01)
+    s, v = plan.score(X)
+    s, v = s.cpu().numpy(), v.cpu().numpy().astype(bool)
+    ref, vref = c.score_matrix_oracle(X)
+    assert (v == vref).all()
+    assert (s[v] == ref[v]).mean() > 0.99
+    sg, _ = c.plan(gpu, svm_impl="gemm").score(X)
+    assert (s[v] == sg.cpu().numpy()[v]).mean() > 0.99

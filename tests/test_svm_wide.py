@@ -120,3 +120,21 @@ def test_wide_svm_routing():
     assert isinstance(_plan(huge), SvmGemmPlan)  # > 128 fields: library GEMMs
     with pytest.raises(ValueError):
         _plan(small, svm_impl="nope")
+
+
+def test_wide_svm_hundreds_of_classes():
+    """100 classes = 4950 one-against-one machines in 39 groups of 128: the packed u16 vote
+    counters cover up to 256 classes (128 KiB of LDS per 256-row tile); 257 classes go to the
+    library-GEMM plan."""
+    c = CompiledPmml.from_string(svm_pmml(n_features=6, n_sv=40, seed=3, n_classes=100, gamma=0.3))
+    plan = _plan(c)
+    assert isinstance(plan, SvmWidePlan) and plan.n_classes == 100
+    assert plan.n_machines == 4950 and plan.mt == 4 and plan.n_groups == 39
+    X = stream_matrix(150, 6, seed=7, missing_rate=0.01)
+    D, bad = emulate(plan, X)
+    s, v = finish(plan, D, bad)
+    ref, vref = c.score_matrix_oracle(X)
+    assert (v == vref).all()
+    assert (s[v] == ref[v]).mean() > 0.99
+    over = CompiledPmml.from_string(svm_pmml(n_features=4, n_sv=8, seed=3, n_classes=SvmWidePlan.CMAX + 1))
+    assert isinstance(_plan(over), SvmGemmPlan)
