@@ -209,6 +209,63 @@ __device__ __forceinline__ void store_hidden(const GemmArgs& a, const f32x16 (&a
   }
 }
 
+// Hidden-layer epilogue for TRANSPOSED accumulators (the operands swapped, mma_quad<true>: the
+// tile is [unit][row] — a row per lane, units (r & 3) + 8 (r >> 2) + 4 h in the registers). After
+// bias, activation and bf16 a lane holds four 8-byte unit runs of its row; one v_permlane32_swap per
+// dword pair trades runs between the lane halves so that every lane owns two whole 16-byte runs
+// (units 0-7 and 16-23 in the low half, 8-15 and 24-31 in the high half) and stores them straight
+// from the registers: 2 full-width stores per lane per 32 x 32 tile instead of 16 two-unit stores
+// by half the lanes, no LDS, no barrier. Default for the bf16 hidden kernels; flag bit 8 (0x100)
+// selects store_hidden.
+template <int ACT, int TM, int TN>
+__device__ __forceinline__ void store_hidden_t(const GemmArgs& a, const f32x16 (&acc)[TM][TN], int row0, int col0,
+                                               int wm, int wn, int lane) {
+  const int h = lane >> 5, l32 = lane & 31;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int u0 = col0 + (wn * TN + j) * 32;
+    float b[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) b[r] = a.bias[u0 + (r & 3) + 8 * (r >> 2) + 4 * h];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      uint32_t p[8];  // p[2q], p[2q + 1]: units 8q + 4h + 0..3 as bf16 pairs
+#pragma unroll
+      for (int w = 0; w < 8; ++w) {
+        const float v0 = act_of<ACT>(acc[i][j][2 * w] + b[2 * w], a.act, a.thr);
+        const float v1 = act_of<ACT>(acc[i][j][2 * w + 1] + b[2 * w + 1], a.act, a.thr);
+        p[w] = (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)v0) |
+               ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)v1) << 16);
+      }
+      // swap(X, Y): X keeps the low half's own X and takes the low half's Y into the high half;
+      // Y takes the high half's X into the low half — runs (q, q + 1) become the 16-byte run 2q + h
+      uint4 c[2];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const auto x0 = __builtin_amdgcn_permlane32_swap(p[4 * s + 0], p[4 * s + 2], false, false);
+        const auto x1 = __builtin_amdgcn_permlane32_swap(p[4 * s + 1], p[4 * s + 3], false, false);
+        c[s] = make_uint4(x0[0], x1[0], x0[1], x1[1]);
+      }
+      const size_t row = (size_t)(row0 + (wm * TM + i) * 32 + l32);
+      __bf16* dst = static_cast<__bf16*>(a.C) + row * a.ldc + u0 + 8 * h;
+      *reinterpret_cast<uint4*>(dst) = c[0];
+      *reinterpret_cast<uint4*>(dst + 16) = c[1];
+    }
+  }
+}
+
+template <int TM, int TN>
+__device__ __forceinline__ void store_hidden_t_any(const GemmArgs& a, const f32x16 (&acc)[TM][TN], int row0, int col0,
+                                                   int wm, int wn, int lane) {
+  switch (a.act) {
+    case A_IDENTITY: store_hidden_t<A_IDENTITY, TM, TN>(a, acc, row0, col0, wm, wn, lane); break;
+    case A_RELU: store_hidden_t<A_RELU, TM, TN>(a, acc, row0, col0, wm, wn, lane); break;
+    case A_LOGISTIC: store_hidden_t<A_LOGISTIC, TM, TN>(a, acc, row0, col0, wm, wn, lane); break;
+    case A_TANH: store_hidden_t<A_TANH, TM, TN>(a, acc, row0, col0, wm, wn, lane); break;
+    default: store_hidden_t<-1, TM, TN>(a, acc, row0, col0, wm, wn, lane); break;
+  }
+}
+
 // Output-layer decode of one row from its n_out activated output units z[]: the regression
 // affine + Target epilogue, or softmax / simplemax, probabilities, argmax and the label table.
 __device__ __forceinline__ void decode_row(const GemmArgs& a, int row, const float* z) {
@@ -452,7 +509,7 @@ __global__ __launch_bounds__(256) void nn_decode_wide_kernel(GemmArgs a, const f
 // (no [rows, 64] bf16 round trip through HBM, no separate launch); column tile 0 writes row_ok.
 constexpr int K64_BM = 128, K64_NT = 256;
 
-template <bool PREP>
+template <bool PREP, bool TST>
 __global__ __launch_bounds__(K64_NT, 2) void gemm_k64_kernel(GemmArgs a, PrepArgs p) {
   constexpr int TM = 2, TN = 4;  // 2 x 2 waves, 64 rows x 128 units each
   extern __shared__ __align__(16) unsigned char smem[];
@@ -517,7 +574,12 @@ __global__ __launch_bounds__(K64_NT, 2) void gemm_k64_kernel(GemmArgs a, PrepArg
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = TST ? __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0)
+                        : __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+  }
+  if constexpr (TST) {
+    store_hidden_t_any<TM, TN>(a, acc, row0, col0, wm, wn, lane);
+    return;
   }
   if ((a.f32 >> 5) & 1) {  // bit 5: the wave-private LDS epilogue (measured slower, profiles/r4k)
     __syncthreads();  // every wave is done reading the staged tiles: their LDS becomes scratch
@@ -671,8 +733,9 @@ __device__ __forceinline__ void head_partial(const GemmArgs& a, const HeadFuse& 
   for (int e = tid; e < BM * no; e += NT) out[e] = ((zp[e] + zp[plane + e]) + zp[2 * plane + e]) + zp[3 * plane + e];
 }
 
-template <bool HEADF>
+template <bool HEADF, bool TST>
 __global__ __launch_bounds__(NT, 1) void gemm8_kernel(GemmArgs a, HeadFuse hf) {
+  constexpr bool SWAP = HEADF || TST;  // transposed accumulator tiles
   constexpr int TM = 4, TN = 2;  // acc[2 * a_half + tile][b_half]
   extern __shared__ __align__(16) unsigned char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -726,14 +789,14 @@ __global__ __launch_bounds__(NT, 1) void gemm8_kernel(GemmArgs a, HeadFuse hf) {
     }
     if (kt + 1 < KT) stage_half<true>(Ab, lda_b, k1, SLOT(b ^ 1, 1), 1, wave, lane);
     mma_begin();
-    mma_quad<HEADF>(acc[0][0], acc[1][0], a0, b0);
+    mma_quad<SWAP>(acc[0][0], acc[1][0], a0, b0);
     mma_end();
     // P2: A0 x B1
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) b1[ks] = frag(SLOT(b, 3), rb, 2 * ks + h);
     if (kt + 2 < KT) stage_half<true>(Ab, lda_b, k2, SLOT(b, 0), 0, wave, lane);
     mma_begin();
-    mma_quad<HEADF>(acc[0][1], acc[1][1], a0, b1);
+    mma_quad<SWAP>(acc[0][1], acc[1][1], a0, b1);
     mma_end();
     // P3: A1 x B1
 #pragma unroll
@@ -742,14 +805,14 @@ __global__ __launch_bounds__(NT, 1) void gemm8_kernel(GemmArgs a, HeadFuse hf) {
       for (int i = 0; i < 2; ++i) a1[i][ks] = frag(SLOT(b, 1), ra + 32 * i, 2 * ks + h);
     if (kt + 2 < KT) stage_half<false>(Bb, ldw_b, k2, SLOT(b, 2), 0, wave, lane);
     mma_begin();
-    mma_quad<HEADF>(acc[2][1], acc[3][1], a1, b1);
+    mma_quad<SWAP>(acc[2][1], acc[3][1], a1, b1);
     mma_end();
     // P4: A1 x B0; slice kt + 1 retired (three half-tiles of kt + 2 may stay in flight)
     if (kt + 2 < KT) stage_half<false>(Bb, ldw_b, k2, SLOT(b, 3), 1, wave, lane);
     if (kt + 2 < KT) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     else if (kt + 1 < KT) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     mma_begin();
-    mma_quad<HEADF>(acc[2][0], acc[3][0], a1, b0);
+    mma_quad<SWAP>(acc[2][0], acc[3][0], a1, b0);
     mma_end();
   }
 #undef SLOT
@@ -763,6 +826,8 @@ __global__ __launch_bounds__(NT, 1) void gemm8_kernel(GemmArgs a, HeadFuse hf) {
       default: head_partial<-1>(a, hf, acc, row0, col0, wr, wc, lane, tid, smem); break;
     }
     return;
+  } else if constexpr (TST) {
+    store_hidden_t_any<TM, TN>(a, acc, row0, col0, wr, wc, lane);
   } else {
     if ((a.f32 >> 5) & 1) {  // bit 5: the wave-private LDS epilogue (measured slower, profiles/r4k)
       // every wave is past its last LDS read of the staged slices (the balancing barrier above)
@@ -779,13 +844,13 @@ __global__ __launch_bounds__(NT, 1) void gemm8_kernel(GemmArgs a, HeadFuse hf) {
   }
 }
 
-template <bool HEADF>
+template <bool HEADF, bool TST = false>
 int launch8(hipStream_t stream, const GemmArgs& a, const HeadFuse& hf) {
   const size_t lds = 8 * (size_t)HALF_B;
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm8_kernel<HEADF>),
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm8_kernel<HEADF, TST>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return -5;
-  hipLaunchKernelGGL((gemm8_kernel<HEADF>), dim3((a.rows_p / BM) * (a.Mp / 256)), dim3(NT), lds, stream, a, hf);
+  hipLaunchKernelGGL((gemm8_kernel<HEADF, TST>), dim3((a.rows_p / BM) * (a.Mp / 256)), dim3(NT), lds, stream, a, hf);
   return 0;
 }
 
@@ -842,7 +907,7 @@ PMML_API int pmml_gemm_launch(hipStream_t stream, const GemmArgs* args, int head
   const GemmArgs a = *args;
   if (a.rows <= 0) return 0;
   const int BN = head ? 32 : 256;
-  if (a.f32 & ~0xE1) return -4;
+  if (a.f32 & ~0x1E1) return -4;
   // bf16 hidden layers with K >= 512 run the phase-interleaved kernel (profiles/r3ao: 2048 x 2048
   // 8.73 -> 8.36 ms, 1024 x 1024 2.62 -> 2.48 ms over 1M rows); below that the layer is bound by
   // its output writes and the 2-buffer loop is faster (K = 64: 0.83 vs 0.92 ms). Bit 7 forces it.
@@ -854,14 +919,19 @@ PMML_API int pmml_gemm_launch(hipStream_t stream, const GemmArgs* args, int head
   if (head && (a.n_out < 1 || a.n_out > 32 || a.Mp != 32 || (!a.C && (!a.row_ok || !a.score || !a.valid)))) return -4;
   if (head && a.C && (a.ldc < a.n_out || (reinterpret_cast<uintptr_t>(a.C) & 3))) return -4;
   if (!head && ((a.ldc & 7) || a.ldc < a.Mp || !a.C || (reinterpret_cast<uintptr_t>(a.C) & 15))) return -4;
+  // transposed-accumulator stores (store_hidden_t) unless bit 8 or the bit-5 LDS epilogue asks otherwise
+  const bool tst = !((a.f32 >> 8) & 1) && !((a.f32 >> 5) & 1);
   if (!head && !f32 && a.K == 64 && !((a.f32 >> 6) & 1)) {  // bit 6 forces the 256 x 256 tile
-    hipLaunchKernelGGL((gemm_k64_kernel<false>), dim3((a.rows_p / K64_BM) * (a.Mp / 256)), dim3(K64_NT),
-                       (size_t)(K64_BM + 256) * SLICE_B, stream, a, PrepArgs{});
+    const dim3 grid((a.rows_p / K64_BM) * (a.Mp / 256));
+    const size_t lds = (size_t)(K64_BM + 256) * SLICE_B;
+    if (tst) hipLaunchKernelGGL((gemm_k64_kernel<false, true>), grid, dim3(K64_NT), lds, stream, a, PrepArgs{});
+    else hipLaunchKernelGGL((gemm_k64_kernel<false, false>), grid, dim3(K64_NT), lds, stream, a, PrepArgs{});
     return hipGetLastError() == hipSuccess ? 0 : -7;
   }
   const int rc = f32 ? (head ? launch<32, true, true>(stream, a) : launch<256, false, true>(stream, a))
                      : (head ? launch<32, true, false>(stream, a)
-                             : (ph8 ? launch8<false>(stream, a, HeadFuse{}) : launch<256, false, false>(stream, a)));
+                             : (ph8 ? (tst ? launch8<false, true>(stream, a, HeadFuse{}) : launch8<false, false>(stream, a, HeadFuse{}))
+                                   : launch<256, false, false>(stream, a)));
   if (rc) return rc;
   return hipGetLastError() == hipSuccess ? 0 : -7;
 }
@@ -882,7 +952,7 @@ PMML_API int pmml_gemm_fused_head_launch(hipStream_t stream, const GemmArgs* hid
   if (o.n_out < 1 || o.n_out > 32 || o.K != a.Mp || o.rows != a.rows || o.rows_p != a.rows_p) return -4;
   if (!o.row_ok || !o.score || !o.valid || !part || !wh_perm || (reinterpret_cast<uintptr_t>(wh_perm) & 15)) return -4;
   HeadFuse hf{static_cast<const __bf16*>(wh_perm), part, a.Mp, o.n_out};
-  int rc = launch8<true>(stream, a, hf);
+  int rc = launch8<true, false>(stream, a, hf);
   if (rc) return rc;
   hipLaunchKernelGGL(nn_head_decode_kernel, dim3((a.rows + 255) / 256), dim3(256), 0, stream, o, part, a.Mp / 256);
   return hipGetLastError() == hipSuccess ? 0 : -7;
@@ -899,8 +969,12 @@ PMML_API int pmml_nn_first_layer_launch(hipStream_t stream, const GemmArgs* args
   if (a.rows_p % 256 || a.rows_p < a.rows || p.rows_p != a.rows_p || p.n_rows != a.rows) return -4;
   if (a.Mp % 256 || a.Mp <= 0 || (a.ldw & 7) || a.ldw < a.K || (reinterpret_cast<uintptr_t>(a.Wt) & 15)) return -4;
   if ((a.ldc & 7) || a.ldc < a.Mp || !a.C || (reinterpret_cast<uintptr_t>(a.C) & 15) || !p.row_ok || !p.X) return -4;
-  hipLaunchKernelGGL((gemm_k64_kernel<true>), dim3((a.rows_p / K64_BM) * (a.Mp / 256)), dim3(K64_NT),
-                     (size_t)(K64_BM + 256) * SLICE_B, stream, a, p);
+  const dim3 grid((a.rows_p / K64_BM) * (a.Mp / 256));
+  const size_t lds = (size_t)(K64_BM + 256) * SLICE_B;
+  if (!((a.f32 >> 8) & 1) && !((a.f32 >> 5) & 1))
+    hipLaunchKernelGGL((gemm_k64_kernel<true, true>), grid, dim3(K64_NT), lds, stream, a, p);
+  else
+    hipLaunchKernelGGL((gemm_k64_kernel<true, false>), grid, dim3(K64_NT), lds, stream, a, p);
   return hipGetLastError() == hipSuccess ? 0 : -7;
 }
 

@@ -283,3 +283,36 @@ def test_wave_lds_epilogue_matches_direct_stores(gpu, shape):
     finally:
         plan.gemm_flags = 0
     assert torch.equal(v0, v1) and torch.equal(s0[v0.bool()], s1[v1.bool()])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [dict(n_features=32, hidden=(1024, 1024, 512)),
+                                   dict(n_features=40, hidden=(300, 260), activation="tanh"),
+                                   dict(n_features=24, hidden=(512, 768), activation="logistic", n_out=3,
+                                        classification=True)],
+                         ids=["1024x1024x512", "300x260-tanh", "512x768-logistic"])
+def test_transposed_accumulator_stores_match_direct_stores(gpu, shape):
+    """The default bf16 hidden-layer epilogue (operands swapped so the accumulator tile is
+    [unit][row]; v_permlane32_swap pairs the lane halves' unit runs into two 16-byte stores per lane,
+    store_hidden_t) equals the direct two-unit stores of the [row][unit] tile (flag bit 8) bit for
+    bit, on the K = 64 first-layer kernel and the phase-interleaved kernel, with and without the
+    fused input stage."""
+    c = CompiledPmml.from_string(mlp_pmml(seed=23, **shape))
+    plan = c.plan(gpu, precision="bf16", mlp_impl="wide")
+    plan.fuse_head = False  # every hidden layer stores its activations
+    X = stream_matrix(7000, shape["n_features"], seed=4, missing_rate=0.01)
+    s0, v0 = plan.score(X)
+    plan.gemm_flags = 0x100
+    try:
+        s1, v1 = plan.score(X)
+    finally:
+        plan.gemm_flags = 0
+    assert torch.equal(v0, v1) and torch.equal(s0[v0.bool()], s1[v1.bool()])
+    plan.fuse_input = True
+    try:
+        s2, v2 = plan.score(X)
+    finally:
+        plan.fuse_input = False
+    assert torch.equal(v0, v2) and torch.equal(s0[v0.bool()], s2[v2.bool()])
+    ref, vref = c.score_matrix_oracle(X)
+    assert (v0.cpu().numpy().astype(bool) == vref).all()
