@@ -217,16 +217,25 @@ __device__ __forceinline__ void store_hidden(const GemmArgs& a, const f32x16 (&a
 // from the registers: 2 full-width stores per lane per 32 x 32 tile instead of 16 two-unit stores
 // by half the lanes, no LDS, no barrier. Default for the bf16 hidden kernels; flag bit 8 (0x100)
 // selects store_hidden.
-template <int ACT, int TM, int TN>
+// LB: bl holds the column tile's 256 biases in LDS (16-byte reads) instead of a.bias.
+template <int ACT, int TM, int TN, bool LB>
 __device__ __forceinline__ void store_hidden_t(const GemmArgs& a, const f32x16 (&acc)[TM][TN], int row0, int col0,
-                                               int wm, int wn, int lane) {
+                                               int wm, int wn, int lane, const float* bl) {
   const int h = lane >> 5, l32 = lane & 31;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int u0 = col0 + (wn * TN + j) * 32;
     float b[16];
+    if constexpr (LB) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) b[r] = a.bias[u0 + (r & 3) + 8 * (r >> 2) + 4 * h];
+      for (int q = 0; q < 4; ++q) {
+        const float4 v = *reinterpret_cast<const float4*>(bl + (wn * TN + j) * 32 + 8 * q + 4 * h);
+        b[4 * q] = v.x, b[4 * q + 1] = v.y, b[4 * q + 2] = v.z, b[4 * q + 3] = v.w;
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) b[r] = a.bias[u0 + (r & 3) + 8 * (r >> 2) + 4 * h];
+    }
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       uint32_t p[8];  // p[2q], p[2q + 1]: units 8q + 4h + 0..3 as bf16 pairs
@@ -254,15 +263,15 @@ __device__ __forceinline__ void store_hidden_t(const GemmArgs& a, const f32x16 (
   }
 }
 
-template <int TM, int TN>
+template <int TM, int TN, bool LB = false>
 __device__ __forceinline__ void store_hidden_t_any(const GemmArgs& a, const f32x16 (&acc)[TM][TN], int row0, int col0,
-                                                   int wm, int wn, int lane) {
+                                                   int wm, int wn, int lane, const float* bl = nullptr) {
   switch (a.act) {
-    case A_IDENTITY: store_hidden_t<A_IDENTITY, TM, TN>(a, acc, row0, col0, wm, wn, lane); break;
-    case A_RELU: store_hidden_t<A_RELU, TM, TN>(a, acc, row0, col0, wm, wn, lane); break;
-    case A_LOGISTIC: store_hidden_t<A_LOGISTIC, TM, TN>(a, acc, row0, col0, wm, wn, lane); break;
-    case A_TANH: store_hidden_t<A_TANH, TM, TN>(a, acc, row0, col0, wm, wn, lane); break;
-    default: store_hidden_t<-1, TM, TN>(a, acc, row0, col0, wm, wn, lane); break;
+    case A_IDENTITY: store_hidden_t<A_IDENTITY, TM, TN, LB>(a, acc, row0, col0, wm, wn, lane, bl); break;
+    case A_RELU: store_hidden_t<A_RELU, TM, TN, LB>(a, acc, row0, col0, wm, wn, lane, bl); break;
+    case A_LOGISTIC: store_hidden_t<A_LOGISTIC, TM, TN, LB>(a, acc, row0, col0, wm, wn, lane, bl); break;
+    case A_TANH: store_hidden_t<A_TANH, TM, TN, LB>(a, acc, row0, col0, wm, wn, lane, bl); break;
+    default: store_hidden_t<-1, TM, TN, LB>(a, acc, row0, col0, wm, wn, lane, bl); break;
   }
 }
 
@@ -844,6 +853,86 @@ __global__ __launch_bounds__(NT, 1) void gemm8_kernel(GemmArgs a, HeadFuse hf) {
   }
 }
 
+// Persistent K = 64 hidden layer (bf16, the input stage separate): a workgroup owns one 256-unit
+// column tile — its weight slice (32 KiB) and biases staged in LDS ONCE — and walks row tiles of
+// 128 rows, the next tile's A slice (16 KiB, LDS-DMA) in flight while the current one multiplies
+// and leaves through the transposed-accumulator stores (store_hidden_t). The wait for a tile's A is
+// a COUNTED vmcnt: the only younger vector-memory operations are the previous tile's 16 stores
+// (loads, stores and LDS-DMA retire in issue order), so the stores drain behind the next tile's
+// work instead of at a workgroup exit. Workgroups are laid out XCD-major: blockIdx & 7 is the XCD,
+// and the n_ct column-tile owners of a row group share it, so a row tile's A is fetched from HBM
+// once and hit in that XCD's L2 by the other column tiles. Two workgroups per CU (65 KiB of LDS each).
+constexpr int K64P_STORES = 16;  // store_hidden_t<2, 4>: 2 x 4 tiles x 2 stores per lane
+__global__ __launch_bounds__(K64_NT, 2) void gemm_k64p_kernel(GemmArgs a, int rg) {
+  constexpr int TM = 2, TN = 4;
+  constexpr int A_B = K64_BM * SLICE_B;
+  extern __shared__ __align__(16) unsigned char smem[];
+  unsigned char* Bs = smem;                          // 256 units x 128 B
+  unsigned char* As = smem + 256 * SLICE_B;          // two 128-row A buffers
+  float* bl = reinterpret_cast<float*>(As + 2 * A_B);  // 256 biases
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, l32 = lane & 31;
+  const int n_ct = a.Mp / 256, n_rt = a.rows_p / K64_BM;
+  const int local = blockIdx.x >> 3;
+  const int ct = local % n_ct;
+  const int g = (local / n_ct) * 8 + (blockIdx.x & 7);  // row group: XCD-major
+  const int stride = 8 * rg;
+  if (g >= n_rt) return;
+  const int col0 = ct * 256;
+  const int wm = wave >> 1, wn = wave & 1;
+  const size_t lda_b = (size_t)a.lda * 2, ldw_b = (size_t)a.ldw * 2;
+  const unsigned char* A = static_cast<const unsigned char*>(a.A);
+  stage_slice<256, 4>(static_cast<const unsigned char*>(a.Wt) + (size_t)col0 * ldw_b, ldw_b, 0, Bs, wave, lane);
+  stage_slice<K64_BM, 4>(A + (size_t)g * K64_BM * lda_b, lda_b, 0, As, wave, lane);
+  bl[tid] = a.bias[col0 + tid];  // K64_NT == 256
+  int it = 0;
+  for (int rt = g; rt < n_rt; rt += stride, ++it) {
+    const unsigned char* Ac = As + (it & 1) * A_B;
+    if (it == 0) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(K64P_STORES) : "memory");
+    raw_barrier();  // every wave's part of A(rt) landed; every wave's reads of the other buffer done
+    if (rt + stride < n_rt)
+      stage_slice<K64_BM, 4>(A + (size_t)(rt + stride) * K64_BM * lda_b, lda_b, 0, As + ((it + 1) & 1) * A_B, wave,
+                             lane);
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = f32x16{};
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = frag(Ac, (wm * TM + i) * 32 + l32, 2 * ks + h);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j] = frag(Bs, (wn * TN + j) * 32 + l32, 2 * ks + h);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+    }
+    store_hidden_t_any<TM, TN, true>(a, acc, rt * K64_BM, col0, wm, wn, lane, bl);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+int launch_k64p(hipStream_t stream, const GemmArgs& a) {
+  static int n_cu = 0;
+  if (n_cu == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
+      n_cu = 256;
+  }
+  const int n_ct = a.Mp / 256;
+  const int rg = std::max(1, (2 * n_cu / 8) / n_ct);  // row groups per XCD: ~2 workgroups per CU
+  const size_t lds = (size_t)(256 + 2 * K64_BM) * SLICE_B + 256 * 4;
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_k64p_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)lds) != hipSuccess)
+    return -5;
+  hipLaunchKernelGGL(gemm_k64p_kernel, dim3(8 * n_ct * rg), dim3(K64_NT), lds, stream, a, rg);
+  return 0;
+}
+
 template <bool HEADF, bool TST = false>
 int launch8(hipStream_t stream, const GemmArgs& a, const HeadFuse& hf) {
   const size_t lds = 8 * (size_t)HALF_B;
@@ -907,7 +996,7 @@ PMML_API int pmml_gemm_launch(hipStream_t stream, const GemmArgs* args, int head
   const GemmArgs a = *args;
   if (a.rows <= 0) return 0;
   const int BN = head ? 32 : 256;
-  if (a.f32 & ~0x1E1) return -4;
+  if (a.f32 & ~0x3E1) return -4;
   // bf16 hidden layers with K >= 512 run the phase-interleaved kernel (profiles/r3ao: 2048 x 2048
   // 8.73 -> 8.36 ms, 1024 x 1024 2.62 -> 2.48 ms over 1M rows); below that the layer is bound by
   // its output writes and the 2-buffer loop is faster (K = 64: 0.83 vs 0.92 ms). Bit 7 forces it.
@@ -924,8 +1013,14 @@ PMML_API int pmml_gemm_launch(hipStream_t stream, const GemmArgs* args, int head
   if (!head && !f32 && a.K == 64 && !((a.f32 >> 6) & 1)) {  // bit 6 forces the 256 x 256 tile
     const dim3 grid((a.rows_p / K64_BM) * (a.Mp / 256));
     const size_t lds = (size_t)(K64_BM + 256) * SLICE_B;
-    if (tst) hipLaunchKernelGGL((gemm_k64_kernel<false, true>), grid, dim3(K64_NT), lds, stream, a, PrepArgs{});
-    else hipLaunchKernelGGL((gemm_k64_kernel<false, false>), grid, dim3(K64_NT), lds, stream, a, PrepArgs{});
+    if (tst && !((a.f32 >> 9) & 1)) {  // bit 9: the one-tile-per-workgroup kernel
+      const int rc = launch_k64p(stream, a);
+      if (rc) return rc;
+    } else if (tst) {
+      hipLaunchKernelGGL((gemm_k64_kernel<false, true>), grid, dim3(K64_NT), lds, stream, a, PrepArgs{});
+    } else {
+      hipLaunchKernelGGL((gemm_k64_kernel<false, false>), grid, dim3(K64_NT), lds, stream, a, PrepArgs{});
+    }
     return hipGetLastError() == hipSuccess ? 0 : -7;
   }
   const int rc = f32 ? (head ? launch<32, true, true>(stream, a) : launch<256, false, true>(stream, a))

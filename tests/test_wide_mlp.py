@@ -296,11 +296,12 @@ def test_transposed_accumulator_stores_match_direct_stores(gpu, shape):
     [unit][row]; v_permlane32_swap pairs the lane halves' unit runs into two 16-byte stores per lane,
     store_hidden_t) equals the direct two-unit stores of the [row][unit] tile (flag bit 8) bit for
     bit, on the K = 64 first-layer kernel and the phase-interleaved kernel, with and without the
-    fused input stage."""
+    fused input stage; 41000 rows = 322 row tiles of the persistent K = 64 kernel (several per
+    workgroup, a ragged last one)."""
     c = CompiledPmml.from_string(mlp_pmml(seed=23, **shape))
     plan = c.plan(gpu, precision="bf16", mlp_impl="wide")
     plan.fuse_head = False  # every hidden layer stores its activations
-    X = stream_matrix(7000, shape["n_features"], seed=4, missing_rate=0.01)
+    X = stream_matrix(41_000, shape["n_features"], seed=4, missing_rate=0.01)
     s0, v0 = plan.score(X)
     plan.gemm_flags = 0x100
     try:
@@ -308,6 +309,12 @@ def test_transposed_accumulator_stores_match_direct_stores(gpu, shape):
     finally:
         plan.gemm_flags = 0
     assert torch.equal(v0, v1) and torch.equal(s0[v0.bool()], s1[v1.bool()])
+    plan.gemm_flags = 0x200  # K = 64 layer: one tile per workgroup instead of the persistent kernel
+    try:
+        s3, v3 = plan.score(X)
+    finally:
+        plan.gemm_flags = 0
+    assert torch.equal(v0, v3) and torch.equal(s0[v0.bool()], s3[v3.bool()])
     plan.fuse_input = True
     try:
         s2, v2 = plan.score(X)
