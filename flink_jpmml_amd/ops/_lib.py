@@ -204,7 +204,7 @@ class NnPrepArgs(ctypes.Structure):
     _fields_ = [("X", c_void_p), ("n_rows", c_int), ("rows_p", c_int), ("ldx", c_int), ("n_in", c_int),
                 ("in_index", c_void_p), ("in_scale", c_void_p), ("in_shift", c_void_p), ("in_missing", c_void_p),
                 ("H", c_void_p), ("ldh", c_int), ("k0", c_int), ("row_ok", c_void_p), ("f32", c_int),
-                ("pad", c_int)]
+                ("contig", c_int)]
 
 
 class LinearArgs(ctypes.Structure):

@@ -70,15 +70,21 @@ struct PrepArgs {
   void* H;                 // [rows_p][ldh] bf16 or fp32
   int ldh, k0;             // k0: padded width (zero columns past n_in)
   uint8_t* row_ok;         // [rows_p]
-  int f32, pad;
+  int f32;
+  int contig;              // in_index[k] == in_index[0] + k, in_index[0] % 4 == 0 (host); X 16-byte rows (launch)
 };
 
 // Input layer: gather the network inputs, normalise, replace missing, bf16. A row's 8-input
 // chunks are spread over GP consecutive lanes (GP = chunks rounded up to a power of two, at most
 // 64: beyond 512 inputs a lane takes every 64th chunk), so its reads and its 16-byte stores are
-// contiguous, and the row's validity is the AND over its lane group (one wave ballot).
+// contiguous, and the row's validity is the AND over its lane group (one wave ballot). The affine
+// / missing-value tables of the first NN_PREP_LDS inputs are staged in LDS (16-byte reads instead
+// of three 4-byte vector loads per input), and a contiguous, aligned input map reads a chunk's 8
+// inputs as two 16-byte loads.
+constexpr int NN_PREP_LDS = 1024;
 template <bool F32>
 __global__ __launch_bounds__(256) void nn_prep_kernel(PrepArgs a, int gp_log2) {
+  __shared__ __align__(16) float tb[3][NN_PREP_LDS];  // scale, shift, missing (zero past n_in)
   const int GP = 1 << gp_log2;
   const int t = blockIdx.x * 256 + threadIdx.x;
   const int row = t >> gp_log2;
@@ -86,21 +92,62 @@ __global__ __launch_bounds__(256) void nn_prep_kernel(PrepArgs a, int gp_log2) {
   const int nchunk = a.k0 >> 3;
   const bool live_row = row < a.n_rows;
   const bool active = row < a.rows_p;
+  const bool lds_tab = a.k0 <= NN_PREP_LDS;
+  if (lds_tab) {
+    for (int k = threadIdx.x; k < a.k0; k += 256) {
+      const bool in = k < a.n_in;
+      tb[0][k] = in ? a.in_scale[k] : 0.f;
+      tb[1][k] = in ? a.in_shift[k] : 0.f;
+      tb[2][k] = in ? a.in_missing[k] : 0.f;
+    }
+    __syncthreads();
+  }
+  const int c0 = a.contig ? a.in_index[0] : 0;
   bool bad = false;
   for (int chunk = lc; active && chunk < nchunk; chunk += GP) {
     const float* x = a.X + (size_t)(live_row ? row : 0) * a.ldx;
     float v[8];
+    if (lds_tab && a.contig && chunk * 8 + 8 <= a.n_in) {  // a full chunk: vector loads
+      const float4 x0 = *reinterpret_cast<const float4*>(x + c0 + chunk * 8);
+      const float4 x1 = *reinterpret_cast<const float4*>(x + c0 + chunk * 8 + 4);
+      const float xs[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+      float sc[8], sh[8], ms[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int k = chunk * 8 + j;
-      float z = 0.f;
-      if (live_row && k < a.n_in) {
-        const float xv = x[a.in_index[k]];
-        z = xv == xv ? fmaf(xv, a.in_scale[k], a.in_shift[k]) : a.in_missing[k];
-        bad = bad || (z != z);
-        z = z == z ? z : 0.f;
+      for (int q = 0; q < 2; ++q) {
+        const float4 s4 = *reinterpret_cast<const float4*>(&tb[0][chunk * 8 + 4 * q]);
+        const float4 h4 = *reinterpret_cast<const float4*>(&tb[1][chunk * 8 + 4 * q]);
+        const float4 m4 = *reinterpret_cast<const float4*>(&tb[2][chunk * 8 + 4 * q]);
+        sc[4 * q] = s4.x, sc[4 * q + 1] = s4.y, sc[4 * q + 2] = s4.z, sc[4 * q + 3] = s4.w;
+        sh[4 * q] = h4.x, sh[4 * q + 1] = h4.y, sh[4 * q + 2] = h4.z, sh[4 * q + 3] = h4.w;
+        ms[4 * q] = m4.x, ms[4 * q + 1] = m4.y, ms[4 * q + 2] = m4.z, ms[4 * q + 3] = m4.w;
       }
-      v[j] = z;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float z = 0.f;
+        if (live_row) {
+          const float xv = xs[j];
+          z = xv == xv ? fmaf(xv, sc[j], sh[j]) : ms[j];
+          bad = bad || (z != z);
+          z = z == z ? z : 0.f;
+        }
+        v[j] = z;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = chunk * 8 + j;
+        float z = 0.f;
+        if (live_row && k < a.n_in) {
+          const float xv = x[a.in_index[k]];
+          const float scale = lds_tab ? tb[0][k] : a.in_scale[k];
+          const float shift = lds_tab ? tb[1][k] : a.in_shift[k];
+          const float miss = lds_tab ? tb[2][k] : a.in_missing[k];
+          z = xv == xv ? fmaf(xv, scale, shift) : miss;
+          bad = bad || (z != z);
+          z = z == z ? z : 0.f;
+        }
+        v[j] = z;
+      }
     }
     if constexpr (F32) {
       f32x4* o = reinterpret_cast<f32x4*>(static_cast<float*>(a.H) + (size_t)row * a.ldh + chunk * 8);
@@ -976,11 +1023,13 @@ PMML_API int pmml_gemm_args_size() { return (int)sizeof(GemmArgs); }
 PMML_API int pmml_nn_prep_args_size() { return (int)sizeof(PrepArgs); }
 
 PMML_API int pmml_nn_prep_launch(hipStream_t stream, const PrepArgs* args) {
-  const PrepArgs a = *args;
+  PrepArgs a = *args;
   if (a.rows_p <= 0) return 0;
   if ((a.k0 & 7) || a.k0 < a.n_in || a.k0 > NN_MAX_INPUTS || (a.ldh & 7) || (reinterpret_cast<uintptr_t>(a.H) & 15))
     return -4;
   if (a.f32 != 0 && a.f32 != 1) return -4;
+  // the vector path needs every row's first input 16-byte aligned
+  if (a.contig && ((reinterpret_cast<uintptr_t>(a.X) & 15) || (a.ldx & 3))) a.contig = 0;
   int g = 0;
   while ((1 << g) < (a.k0 >> 3) && g < 6) ++g;  // lanes per row: chunks rounded up to a power of two, <= 64
   const long long threads = (long long)a.rows_p << g;

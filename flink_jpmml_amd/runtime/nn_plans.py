@@ -376,7 +376,7 @@ class WideMlpPlan(MlpPlan):
     supports_direct = True
     _STATE = DevicePlan._STATE + ("in_scale", "in_shift", "in_missing", "in_index", "n_in", "out_a", "out_b",
                                   "final_norm", "n_out", "table", "is_classification", "target_stage", "wts", "bss",
-                                  "dims", "k0", "bf16")
+                                  "dims", "k0", "bf16", "in_contig")
     ROWS = 256  # GEMM block rows (mirrors csrc/gemm.hip BM)
 
     def __init__(self, compiled, device, precision: str = "bf16"):
@@ -388,6 +388,9 @@ class WideMlpPlan(MlpPlan):
             raise ValueError("precision must be bf16 or fp32")
         self.bf16 = 1 if precision == "bf16" else 0
         layers, _ = self._io(compiled, ev)
+        idx = self.in_index.cpu().numpy()
+        # the input stage reads a contiguous, 16-byte aligned input map as two 16-byte loads per 8 inputs
+        self.in_contig = int(len(idx) > 0 and idx[0] % 4 == 0 and bool((np.diff(idx) == 1).all()))
         if self.n_out > 1024:
             raise NotLowerable("more than 1024 output neurons")
         self.k0 = _ceil(max(self.n_in, 1), 64)
@@ -476,6 +479,7 @@ class WideMlpPlan(MlpPlan):
         p.in_index, p.in_scale, p.in_shift = ptr(self.in_index), ptr(self.in_scale), ptr(self.in_shift)
         p.in_missing, p.H, p.ldh, p.k0, p.row_ok = ptr(self.in_missing), H0.data_ptr(), self.k0, self.k0, ok.data_ptr()
         p.f32 = 1 - self.bf16
+        p.contig = getattr(self, "in_contig", 0)
         fused = self._fused_head()
         first = self._fused_input(fused)
         if not first:

@@ -1,7 +1,7 @@
 set -o pipefail
 # persistent K = 64 first-layer kernel (gemm_k64p_kernel): GPU bit-identity tests, then 1024^3 bf16
 # MLP kernel stats, default vs flag 0x200 (one tile per workgroup); input stage with LDS tables
-O=gpurun_out/r4w
+O=gpurun_out/r4x
 mkdir -p $O
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 timeout -k 10 300 python -u -m pytest tests/test_wide_mlp.py -m gpu -x -q --timeout 180 --timeout-method thread -rf -k "transposed or k64 or fused_input or wide_gemm_kernels" > $O/pytest_mlp.log 2>&1 || { tail -30 $O/pytest_mlp.log; exit 1; }

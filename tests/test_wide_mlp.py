@@ -262,6 +262,13 @@ def test_fused_input_stage_matches_separate_prep(gpu, shape):
     plan.fuse_input = False
     s0, v0 = plan.score(X)
     assert torch.equal(v0, v1) and torch.equal(s0[v0.bool()], s1[v1.bool()])
+    assert plan.in_contig == 1  # identity input map: the input stage's 16-byte gather
+    plan.in_contig = 0
+    try:
+        s2, v2 = plan.score(X)  # the per-input gather
+    finally:
+        plan.in_contig = 1
+    assert torch.equal(v0, v2) and torch.equal(s0[v0.bool()], s2[v2.bool()])
     ref, vref = c.score_matrix_oracle(X)
     assert (v1.cpu().numpy().astype(bool) == vref).all()
 
