@@ -410,8 +410,9 @@ __device__ __forceinline__ void store_hidden_wave_any(const GemmArgs& a, const f
   }
 }
 
-template <int BN, bool HEAD, bool F32>
+template <int BN, bool HEAD, bool F32, bool TST = false>
 __global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmArgs a) {
+  static_assert(!TST || (!HEAD && !F32), "transposed stores: bf16 hidden layers");
   constexpr int WM = BN == 256 ? 2 : 8;  // waves along rows
   constexpr int WN = 8 / WM;             // waves along units
   constexpr int TM = BM / WM / 32;       // 32-row accumulator tiles per wave
@@ -484,14 +485,17 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmArgs a) {
         for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = TST ? __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0)
+                            : __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
       }
     }
     __builtin_amdgcn_s_waitcnt(0);  // the slice in flight has landed (LDS-DMA retires on vmcnt)
     __syncthreads();                // ... for every wave before anyone reads / overwrites it
   }
 
-  if constexpr (!HEAD) {
+  if constexpr (TST) {
+    store_hidden_t_any<TM, TN>(a, acc, row0, col0, wm, wn, lane);
+  } else if constexpr (!HEAD) {
     switch (a.act) {  // uniform: one unrolled epilogue per common activation
       case A_IDENTITY: store_hidden<A_IDENTITY, TM, TN, F32>(a, acc, row0, col0, wm, wn, lane); break;
       case A_RELU: store_hidden<A_RELU, TM, TN, F32>(a, acc, row0, col0, wm, wn, lane); break;
@@ -1004,16 +1008,16 @@ __global__ __launch_bounds__(256) void nn_head_decode_kernel(GemmArgs a, const f
   decode_row(a, row, z);
 }
 
-template <int BN, bool HEAD, bool F32>
+template <int BN, bool HEAD, bool F32, bool TST = false>
 int launch(hipStream_t stream, const GemmArgs& a) {
   const size_t stage = 2 * (size_t)BM * SLICE_B + 2 * (size_t)BN * SLICE_B;
   const size_t head = HEAD ? (size_t)BM * HEAD_LD * 4 : 0;
   const size_t lds = stage > head ? stage : head;
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_kernel<BN, HEAD, F32>),
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_kernel<BN, HEAD, F32, TST>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return -5;
   dim3 grid((a.rows_p / BM) * (a.Mp / BN));
-  hipLaunchKernelGGL((gemm_kernel<BN, HEAD, F32>), grid, dim3(NT), lds, stream, a);
+  hipLaunchKernelGGL((gemm_kernel<BN, HEAD, F32, TST>), grid, dim3(NT), lds, stream, a);
   return 0;
 }
 
@@ -1075,7 +1079,7 @@ PMML_API int pmml_gemm_launch(hipStream_t stream, const GemmArgs* args, int head
   const int rc = f32 ? (head ? launch<32, true, true>(stream, a) : launch<256, false, true>(stream, a))
                      : (head ? launch<32, true, false>(stream, a)
                              : (ph8 ? (tst ? launch8<false, true>(stream, a, HeadFuse{}) : launch8<false, false>(stream, a, HeadFuse{}))
-                                   : launch<256, false, false>(stream, a)));
+                                   : (tst ? launch<256, false, false, true>(stream, a) : launch<256, false, false>(stream, a))));
   if (rc) return rc;
   return hipGetLastError() == hipSuccess ? 0 : -7;
 }

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Wide MLP kernel-only run for rocprofv3 (per-kernel times of the layer GEMMs): HIDDEN layers
-(default 1024,1024,1024), 1M device-resident rows, PREC precision, ITERS launches."""
+(default 1024,1024,1024), N_FEATURES inputs (32), 1M device-resident rows, PREC precision, ITERS launches."""
 import json
 import os
 import sys
@@ -19,12 +19,13 @@ def main():
     hidden = tuple(int(h) for h in os.environ.get("HIDDEN", "1024,1024,1024").split(","))
     prec = os.environ.get("PREC", "bf16")
     iters = int(os.environ.get("ITERS", 10))
-    c = CompiledPmml.from_string(mlp_pmml(n_features=32, hidden=hidden, seed=4))
+    nf = int(os.environ.get("N_FEATURES", 32))
+    c = CompiledPmml.from_string(mlp_pmml(n_features=nf, hidden=hidden, seed=4))
     plan = c.plan("cuda:0", precision=prec, mlp_impl="wide")
     plan.fuse_input = os.environ.get("FUSE_INPUT", "1") == "1"
     plan.fuse_head = os.environ.get("FUSE_HEAD", "1") == "1"
     plan.gemm_flags = int(os.environ.get("GEMM_FLAGS", "0"), 0)
-    X = torch.from_numpy(stream_matrix(rows, 32, seed=1)).cuda()
+    X = torch.from_numpy(stream_matrix(rows, nf, seed=1)).cuda()
     s, v = plan.alloc_outputs(rows)
     plan.launch(X, s, v)
     torch.cuda.synchronize()

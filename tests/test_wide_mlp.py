@@ -296,14 +296,15 @@ def test_wave_lds_epilogue_matches_direct_stores(gpu, shape):
 @pytest.mark.parametrize("shape", [dict(n_features=32, hidden=(1024, 1024, 512)),
                                    dict(n_features=40, hidden=(300, 260), activation="tanh"),
                                    dict(n_features=24, hidden=(512, 768), activation="logistic", n_out=3,
-                                        classification=True)],
-                         ids=["1024x1024x512", "300x260-tanh", "512x768-logistic"])
+                                        classification=True),
+                                   dict(n_features=100, hidden=(512, 300))],
+                         ids=["1024x1024x512", "300x260-tanh", "512x768-logistic", "k128-512x300"])
 def test_transposed_accumulator_stores_match_direct_stores(gpu, shape):
     """The default bf16 hidden-layer epilogue (operands swapped so the accumulator tile is
     [unit][row]; v_permlane32_swap pairs the lane halves' unit runs into two 16-byte stores per lane,
     store_hidden_t) equals the direct two-unit stores of the [row][unit] tile (flag bit 8) bit for
-    bit, on the K = 64 first-layer kernel and the phase-interleaved kernel, with and without the
-    fused input stage; 41000 rows = 322 row tiles of the persistent K = 64 kernel (several per
+    bit, on the K = 64 first-layer kernel, the two-buffer kernel (K = 128) and the phase-interleaved
+    kernel, with and without the fused input stage; 41000 rows = 322 row tiles of the persistent K = 64 kernel (several per
     workgroup, a ragged last one)."""
     c = CompiledPmml.from_string(mlp_pmml(seed=23, **shape))
     plan = c.plan(gpu, precision="bf16", mlp_impl="wide")
