@@ -52,7 +52,10 @@ struct GemmArgs {
   int lda, ldw, ldc, act;
   float thr;              // threshold activation parameter
   int n_out, final_norm;  // output layer: real units, 0 none / 1 softmax / 2 simplemax
-  int f32;                // operand / activation type: 0 bf16, 1 fp32
+  int f32;                // bit 0: operand / activation type (0 bf16, 1 fp32); experiment bits (A/B tests,
+                          // WideMlpPlan.gemm_flags): 5 wave-private LDS epilogue, 6 K = 64 on the 256 x 256
+                          // tile, 7 force the phase-interleaved kernel, 8 direct [row][unit] stores instead of
+                          // store_hidden_t, 9 one K = 64 tile per workgroup instead of gemm_k64p_kernel
   const uint8_t* row_ok;  // [rows] input-stage validity (output layer)
   Epilogue epi;           // output layer decode (affine + Target, or label table)
   float* score;
