@@ -427,7 +427,7 @@ class WideMlpPlan(MlpPlan):
                 and self.n_out <= 32)
 
     # bf16, <= 64 network inputs: the input stage runs inside the first layer's GEMM (gemm_k64_kernel<true>)
-    fuse_input = False  # measured slower (profiles/r4j: the gather in the GEMM prologue, 1.43 vs 0.18 + 0.82 ms)
+    fuse_input = False  # measured slower (the gather in the GEMM prologue: 1.41 vs 0.06 + 0.57 ms, profiles/r4v, r4y)
 
     def _fused_input(self, fused_head: bool) -> bool:
         """The first layer is a hidden layer launched on its own (not the fused last hidden layer)."""
