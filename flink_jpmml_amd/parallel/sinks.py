@@ -140,6 +140,9 @@ class GatherSink(SinkFunction):
 
     def pre_commit(self, cid: int) -> None:  # checkpoint barrier / end of input: all ranks meet
         self.flush()
+        # retire every in-flight gather before the barrier commits source offsets past its rows:
+        # a failure after the commit must not lose rows that were never delivered
+        self.finish()
 
     def commit(self, cid: int) -> None:
         if cid < 0:

@@ -68,6 +68,7 @@ def _parse_array(el: ET.Element) -> List[str]:
     """``<Array type="real|int|string">`` (and the legacy ``REAL-ARRAY``/``NUM-ARRAY``/``INT-ARRAY``)."""
     text = (el.text or "").strip()
     if not text:
+        _check_n(el, 0)
         return []
     atype = el.get("type", "real")
     if atype == "string" or '"' in text:
@@ -75,8 +76,24 @@ def _parse_array(el: ET.Element) -> List[str]:
         lex.whitespace_split = True
         lex.escapedquotes = '"\\'
         lex.quotes = '"'
-        return list(lex)
-    return text.split()
+        out = list(lex)
+    else:
+        out = text.split()
+    _check_n(el, len(out))
+    return out
+
+
+def _check_n(el: ET.Element, count: int) -> None:
+    """``n`` is the number of entries (JPMML's ArrayUtil rejects an array that disagrees)."""
+    n = el.get("n")
+    if n is None:
+        return
+    try:
+        want = int(n.strip())
+    except ValueError as e:
+        raise PmmlParseError(f"<{_local(el.tag)}> n={n!r} is not an integer") from e
+    if want != count:
+        raise PmmlParseError(f"<{_local(el.tag)}> n={want} but it holds {count} entries")
 
 
 def _parse_sparse(el: ET.Element) -> List[float]:

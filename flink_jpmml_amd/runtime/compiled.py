@@ -25,6 +25,7 @@ from ..models import ModelResult, make_evaluator, result_scores
 from ..pmml import ir
 from ..pmml.fields import Columns, FieldSchema
 from ..pmml.parser import parse_string
+from ..pmml.validate import validate_literals
 
 logger = logging.getLogger(__name__)
 
@@ -35,6 +36,7 @@ class CompiledPmml:
         self.source = source
         self.schema = FieldSchema(doc)
         self.evaluator = make_evaluator(doc.model, self.schema)
+        validate_literals(doc, self.schema)  # junk literals on numeric fields fail the load
         self.model = doc.model
         self.active_fields: List[str] = list(self.evaluator.active_fields)
         self.mining_fields: Dict[str, ir.MiningField] = dict(self.evaluator.mining_fields)

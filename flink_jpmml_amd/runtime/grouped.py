@@ -183,11 +183,12 @@ class GroupedScorer:
             for s in range(0, n, S):
                 e = min(n, s + S)
                 m = e - s
-                counts = np.bincount(codes_np[s:e], minlength=K)
-                if len(counts) > K:
-                    raise ValueError(f"model code {len(counts) - 1} out of range [0, {K})")
-                starts = np.zeros(K + 1, dtype=np.int64)
-                np.cumsum(counts, out=starts[1:])
+                with prange("grouped.count"):
+                    counts = np.bincount(codes_np[s:e], minlength=K)
+                    if len(counts) > K:
+                        raise ValueError(f"model code {len(counts) - 1} out of range [0, {K})")
+                    starts = np.zeros(K + 1, dtype=np.int64)
+                    np.cumsum(counts, out=starts[1:])
                 # ---- H2D of the rows and the codes into the next ring slot
                 slot = self._ring[self._next]
                 self._next = (self._next + 1) % len(self._ring)
@@ -200,7 +201,8 @@ class GroupedScorer:
                       "group cursor H2D")
                 check(lib.pmml_group_rows(p.comp.cuda_stream, xs_ptr, ldx, F, m, cs_ptr, code_bytes, K,
                                           cursor.data_ptr(), Xg.data_ptr(), inv.data_ptr()), "group_rows kernel")
-                self._launch_models(scorers, counts, starts, Xg, sg, vg, F, keep)
+                with prange("grouped.launch"):
+                    self._launch_models(scorers, counts, starts, Xg, sg, vg, F, keep)
                 os_ = hs + 4 * s if hs is not None else dev_out[0][s:e].data_ptr()
                 ov_ = hv + s if hv is not None else dev_out[1][s:e].data_ptr()
                 s2 = dev_out[0][s:e].data_ptr() if (dev_out is not None and hs is not None) else None

@@ -213,6 +213,7 @@ _METHOD_CODE = {"selectFirst": 0, "sum": 1, "average": 2, "weightedAverage": 3, 
                 "weightedMedian": 7, "majorityVote": 8, "weightedMajorityVote": 9}
 _PROB_CODE = {"average": 10, "weightedAverage": 11, "max": 12, "median": 13}
 SEG_MAXK = SEG_MAXC = 64  # ops/csrc/segment.hip
+SEG_STACK = 32  # seg_predicate's postfix stack: 2-bit entries of one uint64 (ops/csrc/segment.hip)
 MULTI_MAX_TREES = 64  # tree segments this small share one pointer-layout launch (tree_pointer_multi_kernel)
 
 
@@ -221,9 +222,16 @@ def predicate_programs(progs) -> tuple:
     ``(insns int32[m, 4], pool float64[p], starts int32[K])`` (``ops/csrc/segment.hip``)."""
     insns: List[tuple] = []
     pool: List[float] = []
+    depth = [0, 0]  # running postfix stack depth, its maximum over the program
+
+    def push(pops: int) -> None:
+        depth[0] += 1 - pops
+        depth[1] = max(depth[1], depth[0])
 
     def emit(prog) -> None:
         tag = prog[0]
+        if tag != "C":
+            push(0)
         if tag == "T":
             insns.append((_SP["TRUE"], 0, 0, 0))
         elif tag == "F":
@@ -239,15 +247,23 @@ def predicate_programs(progs) -> tuple:
         else:
             if len(prog[2]) > 32:
                 raise NotLowerable("CompoundPredicate with more than 32 children")
+            if not prog[2]:
+                raise NotLowerable("CompoundPredicate without children")
             for q in prog[2]:
                 emit(q)
+            push(len(prog[2]))
             insns.append(({"and": _SP["AND"], "or": _SP["OR"], "xor": _SP["XOR"], "surrogate": _SP["SURR"]}[prog[1]],
                           len(prog[2]), 0, 0))
 
     starts = []
     for prog in progs:
         starts.append(len(insns))
+        depth[0] = depth[1] = 0
         emit(prog)
+        # seg_predicate keeps its three-valued stack as 2-bit entries of one uint64: a program whose
+        # postfix stack ever holds more than SEG_STACK entries would shift the oldest ones out
+        if depth[1] > SEG_STACK:
+            raise NotLowerable(f"segment predicate needs a {depth[1]}-entry stack > {SEG_STACK}")
         insns.append((_SP["END"], 0, 0, 0))
     return (np.array(insns, dtype=np.int32).reshape(-1, 4), np.array(pool or [0.0], dtype=np.float64),
             np.array(starts, dtype=np.int32))

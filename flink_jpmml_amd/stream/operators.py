@@ -746,12 +746,18 @@ class EvaluationCoFunction(CoProcessFunction, CheckpointedFunction, _ScoringMixi
                 return self._grouped_scorer.submit(batch, codes, scorers, keep_device=keep)
             except NotGroupable:  # pragma: no cover - groupable() checked the same conditions
                 pass
+        # split path: per-model predict + merge. Rows of an empty model or of one whose active
+        # fields differ from the batch width are EmptyScore, as on the grouped path (NullScorer).
+        # The merged batch has no device mirrors: a device GatherSink takes its host path for it.
         METRICS.inc("grouped.split_batches")
         n = len(batch)
         s = np.full(n, np.nan, dtype=np.float32)
         v = np.zeros(n, dtype=bool)
         for sub in batch.split_by_model():
-            pb = self.model_for(sub.model_id).predict_records(sub)
+            m = self.model_for(sub.model_id)
+            if m.is_empty or len(m.active_fields) != width:
+                continue
+            pb = m.predict_records(sub)
             s[sub.row_index] = pb.scores
             v[sub.row_index] = pb.valid
         return PredictionBatch.from_arrays(s, v).masked(batch.size_ok())

@@ -356,7 +356,8 @@ class Executor:
             off = int(entry.get("offset", 0))
             ranks = entry.get("ranks")
             leader = None
-            cuts = None
+            # earlier rescales' owner cuts still in force when that checkpoint was taken
+            cuts = [[int(c) for c in lay] for lay in entry.get("skip_layers", [])] or None
             if ranks is not None and len(ranks) == self.world:
                 off = int(ranks[self.rank])  # per-rank cut of a time-based checkpoint
                 leader = int(min(ranks))
@@ -369,7 +370,7 @@ class Executor:
                 if n.dist_mode == "shard":
                     # old rank j owned the global offsets g with g % old_world == j and processed
                     # those below its cut: resume at the smallest cut, skip what its owner did
-                    cuts = [int(r) for r in ranks]
+                    cuts = (cuts or []) + [[int(r) for r in ranks]]
                 # replicate / all: every rank saw every element; replaying from the smallest cut
                 # re-applies control messages the union-restored state already holds (Add of a
                 # known id is ignored, Del of an absent one is a no-op: MetadataManager)
@@ -485,13 +486,15 @@ class Executor:
                                 e = merged_ops.setdefault(uid, {}).setdefault(name, {"mode": s["mode"],
                                                                                      "subtasks": []})
                                 e["subtasks"].extend(s["subtasks"])
-                    sources = {uid: {"offset": off, "ranks": [p[2][uid] for p in parts]}
-                               for uid, off in local_src.items()}
+                    sources = {}
+                    for uid, off in local_src.items():
+                        ranks = [p[2][uid] for p in parts]
+                        sources[uid] = self._skip_layers(uid, {"offset": off, "ranks": ranks}, ranks)
                     path = self._write_manifest(cid, merged_ops, sources, models)
                 path = guarded_collective(broadcast_object, path, self.dist, group=g,
                                           what=f"checkpoint {cid} commit")
             else:
-                sources = {uid: {"offset": off} for uid, off in local_src.items()}
+                sources = {uid: self._skip_layers(uid, {"offset": off}, [off]) for uid, off in local_src.items()}
                 path = self._write_manifest(cid, operators, sources, models)
             for sk in sinks:
                 if hasattr(sk, "commit"):
@@ -499,6 +502,18 @@ class Executor:
             self.checkpoint_paths.append(path)
             METRICS.inc("checkpoint.completed")
             METRICS.observe("checkpoint.duration_ms", (time.perf_counter() - t0) * 1e3)
+
+    def _skip_layers(self, uid: str, entry: dict, ranks: List[int]) -> dict:
+        """Carry a rescaled restore's owner cuts into the next checkpoint while some reader is still
+        inside their skip window: a cut list stays until ``min(ranks)`` has passed its
+        largest cut, since a restore from this checkpoint resumes at ``min(ranks)`` and must not
+        re-score what the old owners had already processed."""
+        rd = next((r for r in self.readers.values() if r.node.uid == uid), None)
+        lo = min(ranks) if ranks else 0
+        live = [lay for lay in (getattr(rd, "skip_layers", None) or []) if max(lay) > lo]
+        if live:
+            entry["skip_layers"] = live
+        return entry
 
     def _write_manifest(self, cid: int, operators, sources, models) -> str:
         payload = {"operators": operators, "sources": sources, "models": models, "records_in": self.records_in,

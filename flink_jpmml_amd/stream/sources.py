@@ -588,8 +588,13 @@ class SourceReader:
                  leader_offset: Optional[int] = None, owner_cuts: Optional[List[int]] = None):
         self.node = node
         # restore of a shard-mode checkpoint taken at another world size: global offset g was owned
-        # by old rank g % len(cuts), which processed it iff g < cuts[owner]
-        self._cuts = list(owner_cuts) if owner_cuts else None
+        # by old rank g % len(cuts), which processed it iff g < cuts[owner]. ``owner_cuts`` is one
+        # such cut list or several *layers* of them (a rescale of a rescale: each earlier world's
+        # cuts stay in force until every reader has passed them, runtime.py::_skip_layers)
+        if owner_cuts and not isinstance(owner_cuts[0], (list, tuple)):
+            owner_cuts = [owner_cuts]
+        self.skip_layers: List[List[int]] = [[int(c) for c in lay] for lay in (owner_cuts or []) if lay]
+        self._cuts = self.skip_layers or None
         self.rank = rank
         self.world = world
         self.mode = node.dist_mode if world > 1 else "all"
@@ -636,12 +641,19 @@ class SourceReader:
 
         return gen()
 
+    def _done_before(self, g: int) -> bool:
+        """Global element ``g`` was processed before the restore (by its owner in some layer)."""
+        for lay in self._cuts:
+            if g < lay[g % len(lay)]:
+                return True
+        return False
+
     def __iter__(self) -> Iterator[Tuple[int, Any]]:
         cuts = self._cuts
         if self._strided:  # (global offset, element) pairs of this rank only
             for g, x in self._it:
                 self.offset = g + 1
-                if cuts is not None and g < cuts[g % len(cuts)]:
+                if cuts is not None and self._done_before(g):
                     continue
                 yield g, x
             total = getattr(self.node.source, "global_length", None)
@@ -655,7 +667,7 @@ class SourceReader:
                 self.offset += 1
                 if g < self._skip_until:
                     continue
-                if cuts is not None and g < cuts[g % len(cuts)]:
+                if cuts is not None and self._done_before(g):
                     continue
                 if self.mode == "shard" and g % self.world != self.rank:
                     foreign += 1

@@ -280,9 +280,13 @@ for lockstep in (False, True):
         for pb in trapped:
             sink.invoke((pb, batch))
         if not lockstep:
-            sink.pre_commit(1)
+            sink.flush()  # issues the gather: still no host sync
     finally:
         torch.Tensor.item, torch.cuda.synchronize, torch.cuda.Stream.synchronize, torch.cuda.Event.synchronize = saved
+    delivered_at_commit = None
+    if not lockstep:
+        sink.pre_commit(1)  # the barrier retires every in-flight gather (ADVICE r4: exactly-once)
+        delivered_at_commit = sink.rows_gathered
     for pb in pbs[len(trapped):]:
         sink.invoke((pb, batch))
     sink.finish()
@@ -290,7 +294,8 @@ for lockstep in (False, True):
     out[str(lockstep)] = {"calls": calls, "rows": int(len(sink.valid)),
                           "valid_eq": bool((sink.valid == ref_v).all()),
                           "scores_eq": bool(np.array_equal(sink.scores[ref_v], ref_s[ref_v])),
-                          "invalid": int((~sink.valid).sum()), "ref_invalid": int((~ref_v).sum())}
+                          "invalid": int((~sink.valid).sum()), "ref_invalid": int((~ref_v).sum()),
+                          "delivered_at_commit": delivered_at_commit}
 print(json.dumps(out))
 """
 
@@ -314,3 +319,4 @@ def test_device_gather_issues_without_host_sync_and_masks_invalid_rows(gpu, tmp_
         assert got["calls"] == [], got
         assert got["rows"] == 15000 and got["valid_eq"] and got["scores_eq"], got
         assert got["invalid"] == got["ref_invalid"] > 0
+    assert res["False"]["delivered_at_commit"] == 15000  # nothing left in flight past pre_commit

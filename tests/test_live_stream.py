@@ -341,3 +341,17 @@ def test_manifest_is_json(tmp_path):
     with open(res.checkpoints[0]) as fh:
         doc = json.load(fh)
     assert doc["trigger"] == "count" and doc["checkpoint_id"] == 1
+
+
+def test_gather_sink_pre_commit_retires_inflight_gathers():
+    """the asynchronous device gather leaves collectives in flight after ``flush``; the
+    checkpoint barrier (``pre_commit``) must retire them so no committed offset runs past rows the
+    sink never delivered."""
+    from flink_jpmml_amd.parallel.sinks import GatherSink
+
+    sink = GatherSink(to="all")
+    delivered = []
+    for i in range(3):
+        sink._inflight.append(([], [], lambda i=i: delivered.append(i)))
+    sink.pre_commit(1)
+    assert delivered == [0, 1, 2] and not sink._inflight

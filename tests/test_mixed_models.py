@@ -88,6 +88,29 @@ def test_dynamic_quick_evaluate_mixed_batch_matches_per_model(tmp_path, encoded)
     assert not out[1][0].valid.any()  # deleted model: EmptyScore
 
 
+def test_mixed_batch_with_wrong_width_model_is_empty_score(tmp_path):
+    """on the split path a served model whose active-field count differs from the
+    batch width scores EmptyScore rows (as the grouped path's NullScorer does), never raises."""
+    paths = _models(tmp_path, k=2)
+    narrow = tmp_path / "narrow.pmml"
+    narrow.write_text(synth.gbdt_pmml(n_trees=4, depth=3, n_features=4, seed=9))
+    n = 600
+    X = synth.stream_matrix(n, 8, seed=1, missing_rate=0.0)
+    code = np.arange(n) % 3
+    ids = [f"{UUIDS[i]}_1" for i in range(3)]
+    seq = [("R", AddMessage(UUIDS[0], 1, paths[0], 0)), ("R", AddMessage(UUIDS[1], 1, paths[1], 0)),
+           ("R", AddMessage(UUIDS[2], 1, str(narrow), 0)),
+           ("L", RecordBatch(X, model_ids=np.array(ids, dtype=object)[code]))]
+    env = StreamExecutionEnvironment()
+    ev, ctrl = env.from_either(seq)
+    (pb, _), = ev.with_support_stream(ctrl).quick_evaluate().collect()
+    assert not pb.valid[code == 2].any()
+    for i in range(2):
+        rows = np.flatnonzero(code == i)
+        ref = PmmlModel.from_path(paths[i]).predict(X[rows])
+        assert (pb.valid[rows] == ref.valid).all() and ref.valid.any()
+
+
 def test_dynamic_quick_evaluate_per_record_events(tmp_path):
     from tests.test_stream import DynamicInput
 

@@ -78,3 +78,51 @@ def test_either_split_refuses_rescale(tmp_path):
     s.map(lambda x: [x]).add_sink(FileSink(str(tmp_path / "out")))
     with pytest.raises(RuntimeError, match="world size 2"):
         env.execute("either", restore=manifest)
+
+
+def test_checkpoint_inside_skip_window_keeps_owner_cuts(tmp_path):
+    """restore a world-2 manifest at world 1, take a checkpoint while the reader is still
+    inside the old owners' skip window (offset 12 < max cut 20), fail, restore from THAT checkpoint:
+    the old cuts must travel in the manifest (``skip_layers``) so elements 12..19 the old rank 0 had
+    processed are not scored a second time."""
+    from flink_jpmml_amd.stream import FileSink, StreamExecutionEnvironment
+    from flink_jpmml_amd.stream.state import CheckpointStorage
+
+    store = CheckpointStorage(str(tmp_path / "ck0"))
+    first = store.write(3, {"trigger": "time", "operators": {},
+                            "sources": {"events": {"offset": CUTS[0], "ranks": CUTS}}})
+
+    def job(restore, fail_after=None):
+        env = StreamExecutionEnvironment()
+        env.enable_checkpointing(every_n_records=12, directory=str(tmp_path / "ck"))
+        if fail_after is not None:
+            env.inject_failure(fail_after)
+        env.from_collection(list(range(N)), uid="events").map(lambda x: [x]) \
+            .add_sink(FileSink(str(tmp_path / "out")))
+        return env.execute("rescaled-twice", restore=restore)
+
+    with pytest.raises(Exception):
+        job(first, fail_after=5)
+    ck = CheckpointStorage(str(tmp_path / "ck"))
+    doc = CheckpointStorage.read(ck.latest())
+    assert doc["sources"]["events"]["offset"] == 12
+    assert doc["sources"]["events"]["skip_layers"] == [CUTS]
+    job(ck.latest())
+    got = [r[0] for r in FileSink.read(str(tmp_path / "out"))]
+    assert sorted(got) == _unprocessed() and len(got) == len(set(got))
+    # past the window the layers are dropped from later manifests
+    last = CheckpointStorage.read(CheckpointStorage(str(tmp_path / "ck")).latest())
+    assert "skip_layers" not in last["sources"]["events"]
+
+
+def test_skip_layers_compose():
+    """Two rescales: world 2 cuts [20, 9], then world 3 cuts [24, 13, 30] recorded while the first
+    window was open. A world-2 restore skips what either layer marks processed."""
+    items = list(range(N))
+    layers = [CUTS, [24, 13, 30]]
+    got = []
+    for r in range(2):
+        node = SimpleNamespace(source=CollectionSource(items), dist_mode="shard")
+        got.extend(g for g, _ in SourceReader(node, r, 2, None, 13, owner_cuts=layers))
+    want = [g for g in range(13, N) if not any(g < lay[g % len(lay)] for lay in layers)]
+    assert sorted(got) == want and len(got) == len(set(got))
