@@ -166,6 +166,13 @@ class SegArgs(ctypes.Structure):
                 ("valid2", c_void_p)]
 
 
+class GroupedTreeArgs(ctypes.Structure):
+    """tree_common.h GroupedTreeArgs: one wide-kernel launch over a mixed-model slice."""
+    _fields_ = [("models", c_void_p), ("model_code", c_void_p), ("row_start", c_void_p), ("tile_start", c_void_p),
+                ("Xg", c_void_p), ("perm", c_void_p), ("out_s", c_void_p), ("out_v", c_void_p), ("n_models", c_int),
+                ("F", c_int)]
+
+
 class GenTreeArgs(ctypes.Structure):
     _fields_ = [("t", TreeArgs), ("nodes", c_void_p), ("children", c_void_p), ("preds", c_void_p),
                 ("pool", c_void_p), ("trees", c_void_p), ("max_steps", c_int), ("pad", c_int)]
@@ -251,6 +258,7 @@ _ABI = {
     "pmml_tree_args_size": TreeArgs,
     "pmml_tree_multi_args_size": MultiTreeArgs,
     "pmml_tree_general_args_size": GenTreeArgs,
+    "pmml_tree_grouped_args_size": GroupedTreeArgs,
     "pmml_tree_hybrid_args_size": HybridArgs,
     "pmml_cluster_args_size": ClusterArgs,
     "pmml_knn_args_size": KnnArgs,
@@ -364,6 +372,13 @@ def load(auto_build: bool = True) -> ctypes.CDLL:
         lib.pmml_ungroup.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
                                      c_void_p]
         lib.pmml_ungroup.restype = c_int
+        lib.pmml_group_slice.argtypes = [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
+                                         c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                         c_void_p, c_void_p, c_void_p, c_void_p]
+        lib.pmml_group_slice.restype = c_int
+        lib.pmml_tree_launch_grouped.argtypes = [c_void_p, c_void_p, c_int, ctypes.POINTER(GroupedTreeArgs), c_int,
+                                                 c_int]
+        lib.pmml_tree_launch_grouped.restype = c_int
         _lib = lib
         return lib
 

@@ -1048,6 +1048,61 @@ PMML_API int pmml_tree_launch_many(hipStream_t stream, const TreeArgs* args, con
   return 0;
 }
 
+PMML_API int pmml_tree_grouped_args_size() { return (int)sizeof(GroupedTreeArgs); }
+
+// ONE wide-kernel launch over a mixed-model slice (tree_grouped_wide_kernel). host_models: the
+// host copies of the n entries' args (the kernel reads the device copies, g->models); they must
+// share depth, leaf format, tile rows and accumulation mode. tiles: grid upper bound
+// (ceil(rows / tile rows) + n). Returns 0 or a negative code (-20: entries disagree).
+PMML_API int pmml_tree_launch_grouped(hipStream_t stream, const TreeArgs* host_models, int n,
+                                      const GroupedTreeArgs* g, int depth, int tiles) {
+  if (n <= 0 || tiles <= 0) return 0;
+  if (g->n_models != n || g->F < 1) return -2;
+  const TreeArgs& a0 = host_models[0];
+  size_t lds = 0;
+  for (int i = 0; i < n; ++i) {
+    const TreeArgs& a = host_models[i];
+    if ((a.variant & 3) == 0 || (a.variant & 3) != (a0.variant & 3) || a.rows_wide != a0.rows_wide ||
+        a.mode != a0.mode)
+      return -20;
+    if (a.n_stage < 1 || a.n_stage > g->F || a.n_stage > (64 * 256) / a.rows_wide) return -4;
+    if (a.C > 16) return -3;
+    size_t need = 0;
+    int chk = 0;
+    switch (depth) {
+      case 1: chk = wide_check<1>(a, need); break;
+      case 2: chk = wide_check<2>(a, need); break;
+      case 3: chk = wide_check<3>(a, need); break;
+      case 4: chk = wide_check<4>(a, need); break;
+      case 5: chk = wide_check<5>(a, need); break;
+      case 6: chk = wide_check<6>(a, need); break;
+      case 7: chk = wide_check<7>(a, need); break;
+      case 8: chk = wide_check<8>(a, need); break;
+      case 9: chk = wide_check<9>(a, need); break;
+      case 10: chk = wide_check<10>(a, need); break;
+      default: return -6;
+    }
+    if (chk) return chk;
+    lds = need > lds ? need : lds;
+  }
+  int err = 0;
+  switch (depth) {
+    case 1: err = launch_grouped_d1(stream, a0, *g, tiles, lds); break;
+    case 2: err = launch_grouped_d2(stream, a0, *g, tiles, lds); break;
+    case 3: err = launch_grouped_d3(stream, a0, *g, tiles, lds); break;
+    case 4: err = launch_grouped_d4(stream, a0, *g, tiles, lds); break;
+    case 5: err = launch_grouped_d5(stream, a0, *g, tiles, lds); break;
+    case 6: err = launch_grouped_d6(stream, a0, *g, tiles, lds); break;
+    case 7: err = launch_grouped_d7(stream, a0, *g, tiles, lds); break;
+    case 8: err = launch_grouped_d8(stream, a0, *g, tiles, lds); break;
+    case 9: err = launch_grouped_d9(stream, a0, *g, tiles, lds); break;
+    case 10: err = launch_grouped_d10(stream, a0, *g, tiles, lds); break;
+    default: return -6;
+  }
+  if (err) return err;
+  return hipGetLastError() == hipSuccess ? 0 : -7;
+}
+
 PMML_API int pmml_tree_general_args_size() { return (int)sizeof(GenTreeArgs); }
 
 // GENERAL layout launch (one split; grid over rows only).

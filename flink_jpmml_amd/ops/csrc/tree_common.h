@@ -74,6 +74,18 @@ struct TreeArgs {
   const int* rank_cnt;          // ... and their count (<= 254); row f of rank_thr starts at f * rank_stride
   int rank_stride, pad1;
 };
+// One grouped launch of the wide kernel over a mixed-model slice (tree_grouped_wide_kernel).
+struct GroupedTreeArgs {
+  const TreeArgs* models;   // [n_models] device copies of the entries' launch args (row fields unset)
+  const int* model_code;    // [n_models] the entry's model code (index into row_start)
+  const int* row_start;     // [K + 1] grouped-row range of every code in this slice (device)
+  const int* tile_start;    // [n_models + 1] first tile of every entry, prefix over all entries (device)
+  const float* Xg;          // grouped rows [m][F]
+  const int* perm;          // grouped row -> arrival-order row of the slice
+  float* out_s;             // arrival-order outputs of the slice
+  uint8_t* out_v;
+  int n_models, F;
+};
 constexpr int VAR_NAN_FAST = 4;    // wide kernel: take the fast path even on tiles with missing values
 constexpr int VAR_NAN_PLANES = 8;  // ... via blob_nan + a second feature plane (NaN -> +inf)
 constexpr int VAR_POINTER_REFILL = 16;  // pointer layout: refill schedule (tree.hip)
@@ -85,7 +97,8 @@ constexpr int VAR_POINTER_PEEL = 512;   // pointer layout, lock-step: top two le
 constexpr int VAR_POINTER_RANK3 = 1024; // pointer layout: three levels per 16-byte record on threshold ranks (tree.hip)
 
 // per-depth launchers (tree_d<D>.hip)
-#define PMML_TREE_DECL(D) int launch_perfect_d##D(hipStream_t st, const TreeArgs& a, dim3 grid, size_t lds);
+#define PMML_TREE_DECL(D) int launch_perfect_d##D(hipStream_t st, const TreeArgs& a, dim3 grid, size_t lds); \
+  int launch_grouped_d##D(hipStream_t st, const TreeArgs& a, const GroupedTreeArgs& g, int tiles, size_t lds);
 PMML_TREE_DECL(1) PMML_TREE_DECL(2) PMML_TREE_DECL(3) PMML_TREE_DECL(4) PMML_TREE_DECL(5)
 PMML_TREE_DECL(6) PMML_TREE_DECL(7) PMML_TREE_DECL(8) PMML_TREE_DECL(9) PMML_TREE_DECL(10)
 #undef PMML_TREE_DECL
@@ -648,8 +661,12 @@ __device__ __forceinline__ void traverse_fast_g(const TreeArgs& a, const uint32_
   if (m < mt) fast_batch_acc<DEPTH, 1, G, LEAF8, MODE>(a, lds0, g, m, t0, feat_lane, acc);
 }
 
+// The wide kernel's work on one ROWS-row tile starting at row0 of a (tree split `split`).
+// out_row (nullable): the epilogue writes row r's outputs at out_row[r] instead of r (the grouped
+// mixed-model launch scatters its model-contiguous rows back to arrival order, grouped.hip).
 template <int DEPTH, int ILP, int ROWS, bool LEAF8, int MODE>
-__global__ __launch_bounds__(WIDE_T, 1) void tree_perfect_wide_kernel(TreeArgs a) {
+__device__ __forceinline__ void wide_tile(const TreeArgs& a, const int row0, const int split,
+                                          const int* __restrict__ out_row, const bool prof_on) {
   using WG = WideGeom<ROWS>;
   constexpr int G = WG::G, RS = WG::RS, PS = WG::PS, T = WIDE_T;
   extern __shared__ __align__(16) uint32_t smem[];
@@ -674,14 +691,11 @@ __global__ __launch_bounds__(WIDE_T, 1) void tree_perfect_wide_kernel(TreeArgs a
   const int hw = (tid >> 6) * 2 + (lane >> 5);
   const int r_local = 32 * (hw % RS) + (lane & 31);
   const int g = __builtin_amdgcn_readfirstlane(hw / RS);  // both halves of a wave: same group
-  const int row0 = blockIdx.x * ROWS;
-  const int split = blockIdx.y;
   const int tb = split * a.trees_per_split;
   const int te = min(a.n_trees, tb + a.trees_per_split);
 
   // optional per-wave phase timers of one workgroup (kbench --tree-prof): staging, traversal,
   // chunk store + barrier, total
-  const bool prof_on = a.prof != nullptr && blockIdx.x == gridDim.x / 2 && blockIdx.y == 0;
   const unsigned long long tstart = prof_on ? __builtin_amdgcn_s_memtime() : 0ull;
   PF4_DECL
   int n16 = (tb < te) ? (min(a.chunk_trees, te - tb) * rw) >> 2 : 0;
@@ -880,7 +894,8 @@ __global__ __launch_bounds__(WIDE_T, 1) void tree_perfect_wide_kernel(TreeArgs a
           pbase[row] = sum;
           pbase[stride + row] = row_ok ? 0.f : 1.f;
         } else {
-          apply_epilogue(a.epi, [&](int) { return sum; }, row_ok, row, a.n_rows, a.score, a.valid, a.probs);
+          const int orow = out_row ? out_row[row] : row;
+          apply_epilogue(a.epi, [&](int) { return sum; }, row_ok, orow, a.n_rows, a.score, a.valid, a.probs);
         }
       }
     }
@@ -927,9 +942,48 @@ __global__ __launch_bounds__(WIDE_T, 1) void tree_perfect_wide_kernel(TreeArgs a
         for (int k = 1; k < CMAX; ++k) r = (cls == k) ? tot[k] : r;
         return r;
       };
-      apply_epilogue(a.epi, sel, row_ok, row, a.n_rows, a.score, a.valid, a.probs);
+      apply_epilogue(a.epi, sel, row_ok, out_row ? out_row[row] : row, a.n_rows, a.score, a.valid, a.probs);
     }
   }
+}
+
+template <int DEPTH, int ILP, int ROWS, bool LEAF8, int MODE>
+__global__ __launch_bounds__(WIDE_T, 1) void tree_perfect_wide_kernel(TreeArgs a) {
+  const bool prof_on = a.prof != nullptr && blockIdx.x == gridDim.x / 2 && blockIdx.y == 0;
+  wide_tile<DEPTH, ILP, ROWS, LEAF8, MODE>(a, blockIdx.x * ROWS, blockIdx.y, nullptr, prof_on);
+}
+
+// ONE launch over the model-contiguous rows of a mixed-model slice (runtime/grouped.py): the
+// entries' tiles are numbered model after model (tile_start, computed on the device by
+// grouped.hip::group_count_kernel), workgroup L takes tile tile_start[0] + L, finds its entry by
+// binary search, and runs that model's wide tile with its own forest, prepare and epilogue; the
+// epilogue scatters each row back to arrival order (perm). Workgroups past the slice's last tile
+// (the grid is sized from the row count before the counts exist) exit at once.
+template <int DEPTH, int ILP, int ROWS, bool LEAF8, int MODE>
+__global__ __launch_bounds__(WIDE_T, 1) void tree_grouped_wide_kernel(GroupedTreeArgs ga) {
+  const int t = ga.tile_start[0] + (int)blockIdx.x;
+  if (t >= ga.tile_start[ga.n_models]) return;
+  int lo = 0, hi = ga.n_models - 1;  // the last entry whose first tile is <= t (empty ones skipped)
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (ga.tile_start[mid] <= t) lo = mid;
+    else hi = mid - 1;
+  }
+  const int e = __builtin_amdgcn_readfirstlane(lo);
+  TreeArgs a = ga.models[e];
+  const int code = ga.model_code[e];
+  const int rs = ga.row_start[code];
+  a.X = ga.Xg + (size_t)rs * ga.F;
+  a.ldx = ga.F;
+  a.n_feat = ga.F;
+  a.n_rows = ga.row_start[code + 1] - rs;
+  a.score = ga.out_s;
+  a.valid = ga.out_v;
+  a.row_valid_in = nullptr;
+  a.partial = nullptr;
+  a.prof = nullptr;
+  a.trees_per_split = a.n_trees;
+  wide_tile<DEPTH, ILP, ROWS, LEAF8, MODE>(a, (t - ga.tile_start[e]) * ROWS, 0, ga.perm + rs, false);
 }
 
 template <typename K>
@@ -955,6 +1009,65 @@ int launch_wide(hipStream_t st, const TreeArgs& a, size_t lds_w) {
   return err;
 }
 
+// Validation + dynamic LDS bytes of one wide-kernel launch (0 or a negative error code).
+template <int D>
+int wide_check(const TreeArgs& a, size_t& lds_w) {
+  const bool leaf8 = (a.variant & 3) == 2;
+  const int rows = a.rows_wide;
+  if (!(rows == 256 || rows == 128 || rows == 64)) return -12;
+  const int G = WIDE_T / rows;
+  const bool dyn = a.mode == MODE_SUM && rows == 256;  // kernel's DYN / NPART
+  const int npart = dyn ? DYN_SLOTS : G;
+  const size_t head = (size_t)(rows + 4 + 8) * 4 + (size_t)npart * rows * 4;
+  if (dyn && (a.chunk_trees > DYN_B * DYN_SLOTS || (a.blob_nan && a.chunk_trees_nan > DYN_B * DYN_SLOTS)))
+    return -14;  // more batches per chunk than slots
+  const size_t plane = (size_t)a.n_stage * rows * 4;
+  lds_w = head + plane + 2 * (size_t)a.chunk_trees * a.rec_words * 4;
+  if ((size_t)a.chunk_trees * a.rec_words > (size_t)WIDE_T * 4 * 4) return -9;
+  if (a.blob_nan) {
+    if (a.chunk_trees_nan < 1 || (size_t)a.chunk_trees_nan * a.rec_words > (size_t)WIDE_T * 4 * 4) return -9;
+    lds_w = max(lds_w, head + 2 * plane + 2 * (size_t)a.chunk_trees_nan * a.rec_words * 4);
+  }
+  if (lds_w > 160 * 1024) return -5;
+  if (a.P != 1 || a.rec_words != (leaf8 ? perfect_rec_words8(D) : perfect_rec_words(D, 1))) return -10;
+  if (a.mode != MODE_SUM && (a.partial || a.C > CMAX || (a.mode == MODE_VOTE8 && a.C > 4) ||
+                             (leaf8 && a.mode != MODE_VOTE8)))
+    return -11;  // leaf pairs in the metas: fp8 sums or VOTE8 class codes
+  if (a.mode == MODE_SLOT && !a.tree_slot) return -11;
+  return 0;
+}
+
+// Grouped launch: `a` is a representative entry (kernel selection), lds the largest entry's need.
+template <int D>
+int launch_grouped(hipStream_t st, const TreeArgs& a, const GroupedTreeArgs& g, int tiles, size_t lds) {
+  const bool leaf8 = (a.variant & 3) == 2;
+#define PMML_GROUPED(R, L8, M)                                                       \
+  {                                                                                  \
+    auto k = tree_grouped_wide_kernel<D, 8, R, L8, M>;                               \
+    int err = prepare_launch(k, lds);                                                \
+    if (!err) hipLaunchKernelGGL(k, dim3(tiles), dim3(WIDE_T), lds, st, g);          \
+    return err;                                                                      \
+  }
+#define PMML_GROUPED_ROWS(R)                                                         \
+  if (a.rows_wide == R) {                                                            \
+    switch (a.mode) {                                                                \
+      case MODE_SUM:                                                                 \
+        if (leaf8) PMML_GROUPED(R, true, MODE_SUM) else PMML_GROUPED(R, false, MODE_SUM)       \
+      case MODE_SLOT: PMML_GROUPED(R, false, MODE_SLOT)                              \
+      case MODE_CLASS: PMML_GROUPED(R, false, MODE_CLASS)                            \
+      case MODE_VOTE8:                                                               \
+        if (leaf8) PMML_GROUPED(R, true, MODE_VOTE8) else PMML_GROUPED(R, false, MODE_VOTE8)   \
+      default: return -11;                                                           \
+    }                                                                                \
+  }
+  PMML_GROUPED_ROWS(256)
+  PMML_GROUPED_ROWS(128)
+  PMML_GROUPED_ROWS(64)
+#undef PMML_GROUPED_ROWS
+#undef PMML_GROUPED
+  return -12;
+}
+
 template <int D>
 int launch_perfect(hipStream_t st, const TreeArgs& a, dim3 grid, size_t lds) {
   int err = 0;
@@ -962,26 +1075,9 @@ int launch_perfect(hipStream_t st, const TreeArgs& a, dim3 grid, size_t lds) {
   if (base == 1 || base == 2) {
     const bool leaf8 = base == 2;
     const int rows = a.rows_wide;
-    const int G = WIDE_T / rows;
-    const bool dyn = a.mode == MODE_SUM && rows == 256;  // kernel's DYN / NPART
-    const int npart = dyn ? DYN_SLOTS : G;
-    const size_t head = (size_t)(rows + 4 + 8) * 4 + (size_t)npart * rows * 4;
-    if (dyn &&
-        (a.chunk_trees > DYN_B * DYN_SLOTS || (a.blob_nan && a.chunk_trees_nan > DYN_B * DYN_SLOTS)))
-      return -14;  // more batches per chunk than slots
-    const size_t plane = (size_t)a.n_stage * rows * 4;
-    size_t lds_w = head + plane + 2 * (size_t)a.chunk_trees * a.rec_words * 4;
-    if ((size_t)a.chunk_trees * a.rec_words > (size_t)WIDE_T * 4 * 4) return -9;
-    if (a.blob_nan) {
-      if (a.chunk_trees_nan < 1 || (size_t)a.chunk_trees_nan * a.rec_words > (size_t)WIDE_T * 4 * 4) return -9;
-      lds_w = max(lds_w, head + 2 * plane + 2 * (size_t)a.chunk_trees_nan * a.rec_words * 4);
-    }
-    if (lds_w > 160 * 1024) return -5;
-    if (a.P != 1 || a.rec_words != (leaf8 ? perfect_rec_words8(D) : perfect_rec_words(D, 1))) return -10;
-    if (a.mode != MODE_SUM && (a.partial || a.C > CMAX || (a.mode == MODE_VOTE8 && a.C > 4) ||
-                               (leaf8 && a.mode != MODE_VOTE8)))
-      return -11;  // leaf pairs in the metas: fp8 sums or VOTE8 class codes
-    if (a.mode == MODE_SLOT && !a.tree_slot) return -11;
+    size_t lds_w = 0;
+    const int chk = wide_check<D>(a, lds_w);
+    if (chk) return chk;
     (void)grid;
     (void)lds;
 #define PMML_WIDE_ROWS(R)                                                                     \

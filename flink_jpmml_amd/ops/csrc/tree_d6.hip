@@ -5,4 +5,9 @@ namespace pmml_tree {
 int launch_perfect_d6(hipStream_t st, const TreeArgs& a, dim3 grid, size_t lds) {
   return launch_perfect<6>(st, a, grid, lds);
 }
+int launch_grouped_d6(hipStream_t st, const TreeArgs& a, const GroupedTreeArgs& g, int tiles, size_t lds) {
+  size_t need = 0;
+  const int chk = wide_check<6>(a, need);
+  return chk ? chk : launch_grouped<6>(st, a, g, tiles, lds);
+}
 }  // namespace pmml_tree

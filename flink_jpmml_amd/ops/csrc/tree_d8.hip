@@ -5,4 +5,9 @@ namespace pmml_tree {
 int launch_perfect_d8(hipStream_t st, const TreeArgs& a, dim3 grid, size_t lds) {
   return launch_perfect<8>(st, a, grid, lds);
 }
+int launch_grouped_d8(hipStream_t st, const TreeArgs& a, const GroupedTreeArgs& g, int tiles, size_t lds) {
+  size_t need = 0;
+  const int chk = wide_check<8>(a, need);
+  return chk ? chk : launch_grouped<8>(st, a, g, tiles, lds);
+}
 }  // namespace pmml_tree

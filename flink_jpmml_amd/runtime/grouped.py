@@ -17,6 +17,19 @@ HBM (``ops/csrc/grouped.hip``)::
 The host's per-row work is one pass over the codes (the per-model row counts size the launches);
 everything else is O(models) per micro-batch. The result is ONE :class:`PredictionBatch` in row
 order — row ``i`` equals ``model_for(id_i).predict(batch.vector(i))``.
+
+**Device-counted path** (every model a wide-kernel tree ensemble — the common serving case): the
+host does no per-row work at all and issues THREE kernels per slice whatever the number of models::
+
+    group_count_kernel   per-model counts + prefixes on the device (row ranges, tile numbering)
+    group_place_kernel   rows -> model-contiguous Xg, perm[pos] = arrival row, EmptyScore rows
+    tree_grouped_wide_kernel   ONE launch: workgroup -> (model, tile) through the device tile
+                         table, each model's own forest / prepare / epilogue, outputs scattered
+                         back to arrival order in HBM (then one D2H copy of the slice's scores)
+
+(one tree launch per distinct kernel configuration — depth, leaf format, tile rows, accumulation
+mode — so a fleet of same-shaped models is one launch). Models on other kernels take the
+host-counted path above.
 """
 
 from __future__ import annotations
@@ -89,6 +102,8 @@ class GroupedScorer:
         self._next = 0
         self._inflight: "collections.deque" = collections.deque()
         self.rows_submitted = 0
+        self._dg: Optional[dict] = None  # device-counted grouping tables of the current scorer set
+        self.device_grouping = True
 
     # ------------------------------------------------------------------ buffers
     def slice_rows(self, n_models: int) -> int:
@@ -172,6 +187,9 @@ class GroupedScorer:
         Xg, inv, sg, vg = self._work
         score_h = torch.empty(n, dtype=torch.float32, pin_memory=True)
         valid_h = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+        dg = self._device_tables(scorers, F) if self.device_grouping else None
+        if dg is not None:
+            return self._submit_device(batch, X, codes_t, code_bytes, n, F, S, dg, score_h, valid_h, keep_device)
         hs, hv = p.host_dev_ptr(score_h), p.host_dev_ptr(valid_h)
         dev_out = None
         if keep_device or hs is None:
@@ -232,6 +250,118 @@ class GroupedScorer:
         METRICS.inc("grouped.batches")
         return PredictionBatch(n, score_h, valid_h, done, owner=(X, codes_t, dev_out, keep),
                                on_done=_observe_latency, device_out=dev_out, row_ok=batch.size_ok())
+
+    # ------------------------------------------------------------------ device-counted path
+    def _device_tables(self, scorers, F: int) -> Optional[dict]:
+        """Launch tables of the device-counted path for this scorer set (cached while the set is
+        unchanged), or ``None`` when some model does not score with the wide tree kernel."""
+        import ctypes
+
+        import torch
+
+        from ..ops._lib import TreeArgs
+
+        key = (tuple(id(sc) for sc in scorers), F)
+        if self._dg is not None and self._dg["key"] == key:
+            return self._dg
+        K = len(scorers)
+        tile_rows = np.zeros(K, dtype=np.int32)
+        groups: dict = {}
+        for k, sc in enumerate(scorers):
+            if isinstance(sc, NullScorer):
+                continue
+            fn = getattr(getattr(sc, "plan", None), "grouped_args", None)
+            got = fn(F) if fn is not None else None
+            if got is None:
+                return None
+            a, depth, gkey, rows = got
+            tile_rows[k] = rows
+            groups.setdefault(gkey, []).append((k, a))
+        order, launches, args = [], [], []
+        for gkey in sorted(groups):
+            ents = groups[gkey]
+            launches.append(dict(gs=len(order), n=len(ents), depth=gkey[0], rows=gkey[2]))
+            order.extend(k for k, _ in ents)
+            args.extend(a for _, a in ents)
+        dev = self.device
+        n_ent = len(order)
+        host_arr = (TreeArgs * max(1, n_ent))(*args)
+        raw = torch.frombuffer(bytearray(ctypes.string_at(ctypes.addressof(host_arr), ctypes.sizeof(host_arr))),
+                               dtype=torch.uint8)
+        i32 = dict(dtype=torch.int32, device=dev)
+        dg = dict(key=key, scorers=list(scorers), K=K, n_entries=n_ent, launches=launches, host_arr=host_arr,
+                  models=raw.to(dev), order=torch.tensor(order or [0], **i32),
+                  tile_rows=torch.from_numpy(tile_rows).to(dev), counts=torch.zeros(K, **i32),
+                  ticket=torch.zeros(1, **i32), cursor=torch.empty(K, **i32), row_start=torch.empty(K + 1, **i32),
+                  tile_start=torch.empty(n_ent + 1, **i32), arg_size=ctypes.sizeof(TreeArgs))
+        if self._dg is not None:  # queued kernels may still read the old tables
+            for t in (self._dg["models"], self._dg["order"], self._dg["tile_rows"], self._dg["counts"],
+                      self._dg["ticket"], self._dg["cursor"], self._dg["row_start"], self._dg["tile_start"]):
+                t.record_stream(self.pipe.comp)
+        self._dg = dg
+        return dg
+
+    def _submit_device(self, batch, X, codes_t, code_bytes: int, n: int, F: int, S: int, dg: dict, score_h, valid_h,
+                       keep_device: bool) -> PredictionBatch:
+        import ctypes
+
+        import torch
+
+        from ..ops._lib import GroupedTreeArgs, check
+
+        p, lib = self.pipe, self._lib
+        Xg, perm = self._work[0], self._work[1]
+        with torch.cuda.stream(p.comp):
+            dev_out = (torch.empty(n, dtype=torch.float32, device=self.device),
+                       torch.empty(n, dtype=torch.uint8, device=self.device))
+        K, n_ent = dg["K"], dg["n_entries"]
+        cs = p.comp.cuda_stream
+        with prange("grouped.enqueue"):
+            for s in range(0, n, S):
+                e = min(n, s + S)
+                m = e - s
+                slot = self._ring[self._next]
+                self._next = (self._next + 1) % len(self._ring)
+                xs_ptr, ldx, cs_ptr = self._stage(X, codes_t, s, m, F, code_bytes, slot)
+                out_s, out_v = dev_out[0][s:e].data_ptr(), dev_out[1][s:e].data_ptr()
+                check(lib.pmml_group_slice(cs, xs_ptr, ldx, F, m, cs_ptr, code_bytes, K, dg["tile_rows"].data_ptr(),
+                                           dg["order"].data_ptr(), n_ent, dg["counts"].data_ptr(),
+                                           dg["ticket"].data_ptr(), dg["cursor"].data_ptr(),
+                                           dg["row_start"].data_ptr(), dg["tile_start"].data_ptr(), Xg.data_ptr(),
+                                           perm.data_ptr(), out_s, out_v), "group count / place kernels")
+                for ln in dg["launches"]:
+                    gs, cnt = ln["gs"], ln["n"]
+                    ga = GroupedTreeArgs(models=dg["models"].data_ptr() + gs * dg["arg_size"],
+                                         model_code=dg["order"].data_ptr() + 4 * gs,
+                                         row_start=dg["row_start"].data_ptr(),
+                                         tile_start=dg["tile_start"].data_ptr() + 4 * gs, Xg=Xg.data_ptr(),
+                                         perm=perm.data_ptr(), out_s=out_s, out_v=out_v, n_models=cnt, F=F)
+                    tiles = -(-m // ln["rows"]) + cnt
+                    rc = lib.pmml_tree_launch_grouped(cs, ctypes.addressof(dg["host_arr"]) + gs * dg["arg_size"], cnt,
+                                                      ctypes.byref(ga), ln["depth"], tiles)
+                    check(rc, "grouped tree launch")
+                slot["ev_comp"].record(p.comp)
+                slot["used"] = True
+                # this slice's scores back to the host while the next slice is grouped and scored
+                with torch.cuda.stream(p.d2h):
+                    p.d2h.wait_event(slot["ev_comp"])
+                    score_h[s:e].copy_(dev_out[0][s:e], non_blocking=True)
+                    valid_h[s:e].copy_(dev_out[1][s:e], non_blocking=True)
+                METRICS.inc("grouped.tree_launches", len(dg["launches"]))
+                METRICS.inc("grouped.slices")
+            for t in dev_out:
+                t.record_stream(p.d2h)
+            done = torch.cuda.Event()
+            done.record(p.d2h)
+        keep = [dg["host_arr"]]
+        self._inflight.append((done, X, codes_t, keep))
+        self.rows_submitted += n
+        METRICS.inc("grouped.rows", n)
+        METRICS.inc("grouped.batches")
+        METRICS.inc("grouped.device_counted_batches")
+        return PredictionBatch(n, score_h, valid_h, done, owner=(X, codes_t, dev_out, keep, dg),
+                               on_done=_observe_latency, device_out=dev_out if keep_device else None,
+                               row_ok=batch.size_ok())
 
     def _stage(self, X, codes_t, s: int, m: int, F: int, code_bytes: int, slot: dict):
         """Rows ``[s, s + m)`` and their codes on the device (copied into ``slot`` unless already

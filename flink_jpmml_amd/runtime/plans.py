@@ -1742,6 +1742,24 @@ class TreePlan(DevicePlan):
             a.partial = ptr(self._partial)
         return a, (0 if self.layout == "perfect" else 1, int(self.depth), 1 if self.has_dr else 0, int(s))
 
+    def grouped_args(self, n_feat: int):
+        """``(TreeArgs, depth, key, tile_rows)`` of this plan as one entry of a grouped mixed-model
+        launch (``pmml_tree_launch_grouped``: one wide-kernel launch over many models' rows,
+        ``runtime/grouped.py``), or ``None`` when it does not score with the wide perfect kernel.
+        Entries with equal ``key`` share one launch; the row fields are set on the device."""
+        from ..ops._lib import TreeArgs
+
+        if self.layout != "perfect" or not (self.variant & 3) or self.P != 1 or \
+                getattr(self, "n_stage", self.n_features) > n_feat:
+            return None
+        a = TreeArgs.from_buffer_copy(self._args_template(False))
+        a.X, a.n_rows, a.n_feat, a.ldx = None, 0, n_feat, n_feat
+        a.row_valid_in, a.score, a.valid, a.probs, a.partial, a.prof = None, None, None, None, None, None
+        a.epi.score2, a.epi.valid2 = None, None
+        a.xcd_split, a.trees_per_split = 0, self.n_trees
+        rows = int(a.rows_wide)
+        return a, int(self.depth), (int(self.depth), int(self.variant & 3), rows, int(a.mode)), rows
+
     def _launch_general(self, X, score, valid, stream, probs, row_valid, score2, valid2) -> None:
         import ctypes
 

@@ -166,3 +166,54 @@ def test_grouped_device_pass_matches_oracle(gpu, tmp_path, n_models):
         ref, vref = oracles[i % kinds].score_matrix_oracle(X[rows])
         assert (pb.valid[rows] == vref).all(), i
         np.testing.assert_allclose(pb.scores[rows][vref], ref[vref], atol=2e-5, rtol=0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_models", [5, 64])
+def test_device_counted_grouped_pass(gpu, tmp_path, n_models):
+    """when every served model scores with the wide tree kernel the grouped pass
+    counts on the device and issues ONE tree launch per kernel configuration per slice (here:
+    depths 4 / 6 / 7 GBDTs + a fp32 random forest vote -> a handful of launches, not one per
+    model). Every model's rows equal its fp64 oracle; unknown ids are EmptyScore."""
+    from flink_jpmml_amd.runtime.compiled import CompiledPmml
+    from flink_jpmml_amd.utils.metrics import METRICS
+
+    F = 16
+    docs = [synth.gbdt_pmml(n_trees=80, depth=6, n_features=F, seed=1),
+            synth.gbdt_pmml(n_trees=96, depth=4, n_features=F, seed=2),
+            synth.gbdt_pmml(n_trees=64, depth=7, n_features=F, seed=3),
+            synth.gbdt_pmml(n_trees=70, depth=6, n_features=F, seed=4, objective="binary"),
+            synth.random_forest_pmml(n_trees=64, depth=6, n_features=F, n_classes=3, seed=5)]
+    paths = []
+    for i, d in enumerate(docs):
+        p = tmp_path / f"d{i}.pmml"
+        p.write_text(d)
+        paths.append(str(p))
+    uuids = [f"a1b2c3d4-0000-4000-8000-{k:012d}" for k in range(n_models)]
+    rng = np.random.default_rng(7 + n_models)
+    n = 700_001
+    X = synth.stream_matrix(n, F, seed=8, missing_rate=0.03).astype(np.float32)
+    code = rng.integers(0, n_models + 1, n)
+    ids = [f"{u}_1" for u in uuids] + ["ffffffff-0000-4000-8000-000000000000_1"]
+    seq = [("R", AddMessage(uuids[i], 1, paths[i % len(docs)], 0)) for i in range(n_models)]
+    seq += [("L", RecordBatch(X, model_ids=(code, ids)))]
+    cfg = ScoringConfig(device=gpu, fallback="error", micro_batch=1 << 17)
+    before = METRICS.counters.get("grouped.device_counted_batches", 0)
+    launches = METRICS.counters.get("grouped.tree_launches", 0)
+    slices = METRICS.counters.get("grouped.slices", 0)
+    env = StreamExecutionEnvironment(config=cfg)
+    ev, ctrl = env.from_either(seq)
+    (pb, _), = ev.with_support_stream(ctrl).quick_evaluate(config=cfg).collect()
+    assert METRICS.counters.get("grouped.device_counted_batches", 0) == before + 1
+    n_slices = METRICS.counters.get("grouped.slices", 0) - slices
+    per_slice = (METRICS.counters.get("grouped.tree_launches", 0) - launches) / n_slices
+    assert per_slice <= len(docs)  # one launch per kernel configuration, whatever n_models
+    oracles = [CompiledPmml.from_string(d) for d in docs]
+    for i in range(n_models + 1):
+        rows = np.flatnonzero(code == i)
+        if i == n_models:
+            assert not pb.valid[rows].any()
+            continue
+        ref, vref = oracles[i % len(docs)].score_matrix_oracle(X[rows])
+        assert (pb.valid[rows] == vref).all(), i
+        np.testing.assert_allclose(pb.scores[rows][vref], ref[vref], atol=2e-5, rtol=0)
