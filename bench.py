@@ -225,6 +225,55 @@ def _kernel_ms(plan, Xh, device) -> float:
     return e0.elapsed_time(e1) / kiters
 
 
+def _rehearsal_reference(args, rank, doc_paths):
+    """``(scores, valid)`` this rank's records must score to (CPU rehearsal): the fp64 oracle of the
+    model each record names over the records this rank's source produced."""
+    from flink_jpmml_amd.bench.synth import stream_matrix
+    from flink_jpmml_amd.runtime.compiled import CompiledPmml
+
+    X = stream_matrix(args.rows, args.features, seed=1000 + rank)
+    if args.source == "text":  # what the CSV the rank wrote holds (%.7g), parsed back
+        import io
+
+        buf = io.StringIO()
+        np.savetxt(buf, X, fmt="%.7g", delimiter=",")
+        X = np.loadtxt(io.StringIO(buf.getvalue()), delimiter=",", dtype=np.float64).reshape(X.shape)
+    X = X.astype(np.float32)
+    docs = [CompiledPmml.from_string(open(p).read()) for p in doc_paths]
+    if args.models <= 1:
+        return docs[0].score_matrix_oracle(X)
+    codes = np.random.default_rng(2000 + rank).integers(0, args.models, args.rows)
+    s = np.full(args.rows, np.nan)
+    v = np.zeros(args.rows, dtype=bool)
+    for k in np.unique(codes).tolist():
+        rows = np.flatnonzero(codes == k)
+        s[rows], v[rows] = docs[k % len(docs)].score_matrix_oracle(X[rows])
+    return s, v
+
+
+def _rehearsal_check(args, sink, ctx, doc_paths):
+    """Every gathered element holds the N ranks' equal-size chunks in rank order; this rank's chunk
+    must be its records in source order (consecutive offsets) scoring like its reference."""
+    ref_s, ref_v = _rehearsal_reference(args, ctx.rank, doc_paths)
+    ref_s = ref_s.astype(np.float32)
+    N, me = ctx.world_size, ctx.rank
+    ok, checked, expect_off = True, 0, 0
+    tol = 1e-5 if args.source == "text" else 0.0  # CSV: decimal -> float32 rounding may differ per parser
+    for s, v, o in sink._parts:
+        if len(s) % N:
+            return False, checked
+        m = len(s) // N
+        cs, cv, co = s[me * m:(me + 1) * m], v[me * m:(me + 1) * m], o[me * m:(me + 1) * m]
+        ok = ok and bool((co == expect_off + np.arange(m)).all())  # nothing lost / reordered / duplicated
+        expect_off += m
+        idx = co % args.rows
+        ok = ok and bool((cv == ref_v[idx]).all())
+        both = cv & ref_v[idx]
+        ok = ok and bool(np.all(np.abs(cs[both] - ref_s[idx][both]) <= tol))
+        checked += m
+    return ok and checked == (args.warmup + args.steps) * args.passes * args.rows, checked
+
+
 def main(argv=None) -> int:
     args = parse_args(argv)
     import torch
@@ -376,22 +425,15 @@ def main(argv=None) -> int:
         seen = sink.rows_seen
         assert seen == (args.warmup + args.steps) * rows_per_step, (seen, rows_per_step)
         assert res.records_in == seen + (args.models if args.models > 1 else 0)  # + the AddMessages
-        if cpu and gather and args.models == 1:
-            # rehearsal: every rank checks every rank's gathered rows against that rank's oracle
+        if cpu and gather:
+            # rehearsal: every rank checks ITS rows inside every gathered element against its own
+            # oracle (row order via the source offsets), then the verdicts are all-gathered
             from flink_jpmml_amd.parallel.dist import all_gather_object
 
-            compiled = CompiledPmml.from_string(open(path).read())
-            ok = True
-            gs, gv = sink.scores, sink.valid
-            n = args.rows
-            for r in range(N):
-                ref_s, ref_v = compiled.score_matrix_oracle(stream_matrix(args.rows, args.features, seed=1000 + r))
-                ref_s = ref_s.astype(np.float32)
-                for k in range(len(gs) // (N * n)):
-                    seg = slice(k * N * n + r * n, k * N * n + (r + 1) * n)
-                    ok = ok and bool((gv[seg] == ref_v).all()) and bool(np.array_equal(gs[seg][ref_v], ref_s[ref_v]))
+            ok, n_rows = _rehearsal_check(args, sink, ctx, doc_paths)
             job["rehearsal_gather_check"] = all_gather_object(bool(ok), ctx, group=ctx.group("ctrl"))
-            job["rehearsal_rows_gathered_per_rank"] = int(len(gs))
+            job["rehearsal_rows_checked_per_rank"] = all_gather_object(int(n_rows), ctx, group=ctx.group("ctrl"))
+            job["rehearsal_rows_gathered_per_rank"] = int(len(sink.scores))
         op = scored.node.factory  # the operator instance this (single-subtask) rank ran
         pipe = getattr(getattr(op, "inner", op), "_pipeline", None)
         if args.models > 1:

@@ -3,13 +3,21 @@
 ``python -m torch.distributed.run --nproc-per-node N ... bench.py --rehearse-cpu`` runs the exact
 DSL job, GatherSink (lockstep all-gather, host path over gloo) and collective code of the timed
 region with the host oracle scorer; every rank then checks every rank's gathered rows against
-that rank's oracle scores. The committed 8-rank run is ``profiles/r4_rehearsal/``."""
+that rank's oracle scores. The committed 8-rank run is ``profiles/r4_rehearsal/``.
+
+Round 5: the check is per rank, over every gathered element, with the row
+order taken from the source offsets — so it covers every bench mode: ``--models N`` (mixed-model
+rows, each against its own model's oracle), ``--source binary`` (memory-mapped record files,
+micro-batch elements) and ``--source text`` (CSV through the native parser), at world 8
+(``profiles/r5_rehearsal/``)."""
 
 import json
 import os
 import socket
 import subprocess
 import sys
+
+import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -20,6 +28,59 @@ def _port():
     p = s.getsockname()[1]
     s.close()
     return p
+
+
+def _rehearse(tmp_path, world, *extra):
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"), "--gpus",
+           str(world), "--rehearse-cpu", "--rows", "512", "--passes", "2", "--steps", "1", "--warmup", "1",
+           "--trees", "12", "--check-rows", "128", "--latency-iters", "2", "--ingest-threads", "1", *extra]
+    r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+@pytest.mark.parametrize("mode", [("--models", "16"), ("--source", "binary", "--micro-batch", "200"),
+                                  ("--source", "text", "--micro-batch", "200")])
+def test_bench_eight_rank_rehearsal_every_mode(tmp_path, mode):
+    out = _rehearse(tmp_path, 8, *mode)
+    assert out["n_gpus"] == 8 and out["rehearsal_cpu"]
+    assert out["job"]["rehearsal_gather_check"] == [True] * 8
+    assert out["job"]["rehearsal_rows_checked_per_rank"] == [512 * 2 * 2] * 8  # rows x passes x steps
+    assert out["job"]["rehearsal_rows_gathered_per_rank"] == 8 * 512 * 2 * 2
+
+
+def test_rehearsal_check_catches_misplaced_rows():
+    """The per-rank check fails when two ranks' chunks are swapped inside a gathered element."""
+    from types import SimpleNamespace
+
+    import numpy as np
+
+    sys.path.insert(0, ROOT)
+    import bench
+
+    args = SimpleNamespace(rows=64, features=4, source="synthetic", models=1, warmup=0, steps=1, passes=1)
+    from flink_jpmml_amd.bench import synth
+
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_reh_model.pmml")
+    with open(path, "w") as fh:
+        fh.write(synth.gbdt_pmml(n_trees=5, depth=3, n_features=4, seed=3))
+    try:
+        parts = []
+        for r in range(2):
+            s, v = bench._rehearsal_reference(args, r, [path])
+            parts.append((s.astype(np.float32), v, np.arange(64)))
+        good = tuple(np.concatenate([p[i] for p in parts]) for i in range(3))
+        swapped = tuple(np.concatenate([p[i] for p in parts[::-1]]) for i in range(3))
+        for me in range(2):
+            ctx = SimpleNamespace(world_size=2, rank=me)
+            assert bench._rehearsal_check(args, SimpleNamespace(_parts=[good]), ctx, [path])[0]
+            assert not bench._rehearsal_check(args, SimpleNamespace(_parts=[swapped]), ctx, [path])[0]
+    finally:
+        os.unlink(path)
 
 
 def test_bench_two_rank_cpu_rehearsal(tmp_path):
