@@ -173,6 +173,12 @@ class GroupedTreeArgs(ctypes.Structure):
                 ("F", c_int)]
 
 
+class LdsTreeArgs(ctypes.Structure):
+    """tree_lds.hip LdsTreeArgs: the LDS-resident deep-forest walk."""
+    _fields_ = [("t", TreeArgs), ("chunks", c_void_p), ("slice_chunk", c_void_p), ("n_slices", c_int),
+                ("chunk_u4", c_int), ("rows", c_int), ("pad", c_int)]
+
+
 class GenTreeArgs(ctypes.Structure):
     _fields_ = [("t", TreeArgs), ("nodes", c_void_p), ("children", c_void_p), ("preds", c_void_p),
                 ("pool", c_void_p), ("trees", c_void_p), ("max_steps", c_int), ("pad", c_int)]
@@ -259,6 +265,7 @@ _ABI = {
     "pmml_tree_multi_args_size": MultiTreeArgs,
     "pmml_tree_general_args_size": GenTreeArgs,
     "pmml_tree_grouped_args_size": GroupedTreeArgs,
+    "pmml_tree_lds_args_size": LdsTreeArgs,
     "pmml_tree_hybrid_args_size": HybridArgs,
     "pmml_cluster_args_size": ClusterArgs,
     "pmml_knn_args_size": KnnArgs,
@@ -379,6 +386,10 @@ def load(auto_build: bool = True) -> ctypes.CDLL:
         lib.pmml_tree_launch_grouped.argtypes = [c_void_p, c_void_p, c_int, ctypes.POINTER(GroupedTreeArgs), c_int,
                                                  c_int]
         lib.pmml_tree_launch_grouped.restype = c_int
+        lib.pmml_tree_lds_launch.argtypes = [c_void_p, ctypes.POINTER(LdsTreeArgs)]
+        lib.pmml_tree_lds_launch.restype = c_int
+        lib.pmml_tree_lds_bytes.argtypes = [c_int, c_int, c_int, c_int, c_int]
+        lib.pmml_tree_lds_bytes.restype = ctypes.c_longlong
         _lib = lib
         return lib
 

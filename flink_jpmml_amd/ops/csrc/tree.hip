@@ -1050,6 +1050,17 @@ PMML_API int pmml_tree_launch_many(hipStream_t stream, const TreeArgs* args, con
 
 PMML_API int pmml_tree_grouped_args_size() { return (int)sizeof(GroupedTreeArgs); }
 
+// Split reduction alone (partial[splits][C + 1][n_rows] -> epilogue), for kernels outside this
+// translation unit (tree_lds.hip).
+PMML_API int pmml_tree_reduce(hipStream_t stream, const TreeArgs* args, int splits) {
+  const TreeArgs& a = *args;
+  if (a.n_rows <= 0) return 0;
+  if (a.C > 16 || splits < 1) return -3;
+  dim3 g2((a.n_rows + TB - 1) / TB);
+  hipLaunchKernelGGL(tree_reduce_kernel, g2, dim3(TB), 0, stream, a, splits);
+  return hipGetLastError() == hipSuccess ? 0 : -8;
+}
+
 // ONE wide-kernel launch over a mixed-model slice (tree_grouped_wide_kernel). host_models: the
 // host copies of the n entries' args (the kernel reads the device copies, g->models); they must
 // share depth, leaf format, tile rows and accumulation mode. tiles: grid upper bound

@@ -354,6 +354,44 @@ def pack_compact_bfs(trees, weights: List[float], P: int):
     return nodes, leaves, roots, has_dr
 
 
+def pack_lds_chunks(n_slots: int, roots: np.ndarray, chunk_u4: int, n_slices: int = 8):
+    """Chunk table of the LDS-resident walk (``tree_lds.hip``) over a :func:`pack_compact_bfs`
+    forest: trees in order, cut into ``n_slices`` contiguous slices of about equal slots (one per
+    XCD) and every slice into chunks of whole trees whose slots — copied from an even start, as
+    16-byte words — fit ``chunk_u4`` uint4 of LDS.
+
+    Returns ``(chunks int32[n, 4] {even slot start, uint4 count, tree begin, tree end},
+    slice_chunk int32[S + 1])``; ``ValueError`` when one tree alone exceeds the buffer."""
+    roots = np.asarray(roots, dtype=np.int64)
+    T = roots.size
+    start = np.where(roots >= 0, roots, ~roots)
+    end = np.append(start[1:], n_slots)
+    sizes = end - start
+
+    def u4(a: int, b: int) -> int:  # uint4 words covering slots [a, b) copied from an even start
+        return (b - (a & ~1) + 1) // 2
+
+    if T and max(u4(int(a), int(b)) for a, b in zip(start, end)) > chunk_u4:
+        raise ValueError("a tree exceeds the LDS chunk buffer")
+    # slices first (contiguous tree ranges of ~equal slots), then greedy chunks inside each
+    S = int(max(1, min(n_slices, T)))
+    cum = np.cumsum(sizes)
+    cuts = [0] + [int(np.searchsorted(cum, cum[-1] * k / S, side="left")) + 1 for k in range(1, S)] + [T]
+    cuts = sorted(set(min(max(c, 0), T) for c in cuts))
+    chunks: List[tuple] = []
+    slice_chunk = [0]
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        t = a
+        while t < b:
+            e = t + 1
+            while e < b and u4(int(start[t]), int(end[e])) <= chunk_u4:
+                e += 1
+            chunks.append((int(start[t]) & ~1, u4(int(start[t]), int(end[e - 1])), t, e))
+            t = e
+        slice_chunk.append(len(chunks))
+    return np.asarray(chunks, dtype=np.int32).reshape(-1, 4), np.asarray(slice_chunk, dtype=np.int32)
+
+
 # --------------------------------------------------------------------------- SUPER pointer layout
 # Two tree levels per 16-byte load (``tree.hip::tree_super_kernel``). The deep-forest walk is bound
 # by the vector memory pipe's cost per load INSTRUCTION (profiles/r3u: ~20 TA cycles per 64-lane

@@ -1072,6 +1072,7 @@ VAR_POINTER_SUPER = 128
 VAR_POINTER_USKIP = 256
 VAR_POINTER_PEEL = 512
 VAR_POINTER_RANK3 = 1024
+VAR_POINTER_LDS = 2048  # compact slots walked out of LDS chunks (tree_lds.hip); host-side flag only
 DYN_B, DYN_SLOTS = 8, 16  # csrc: MODE_SUM trees per claimed batch, batch slots per chunk
 
 
@@ -1214,7 +1215,8 @@ class TreePlan(DevicePlan):
                                   "variant", "children", "preds", "pool", "trees_tab", "max_steps", "blob_nan",
                                   "chunk_trees_nan", "full_epi", "labels", "mode", "tree_w", "acc_init", "feat_map",
                                   "rows_wide", "n_stage", "heads", "head_depth", "pointer_ilp", "xcd_split",
-                                  "tail_format", "rank_thr", "rank_cnt", "rank_stride")
+                                  "tail_format", "rank_thr", "rank_cnt", "rank_stride", "lds_chunks", "lds_slices",
+                                  "lds_rows", "lds_chunk_u4", "lds_n_slices")
 
     WIDE_G = 4  # tree groups of the wide kernel (mirrors csrc)
 
@@ -1271,6 +1273,8 @@ class TreePlan(DevicePlan):
         if pointer_schedule not in ("refill", "lockstep"):
             raise ValueError("pointer_schedule must be 'refill' or 'lockstep'")
         self.heads, self.head_depth = None, 0  # hybrid layout only
+        self.lds_chunks = self.lds_slices = None  # lds node format only
+        self.lds_rows = self.lds_chunk_u4 = self.lds_n_slices = 0
         self.rank_thr, self.rank_cnt, self.rank_stride = None, None, 0  # rank3 node format only
         if pointer_load not in ("clamped", "masked", "uskip", "peel"):
             raise ValueError("pointer_load must be 'clamped', 'masked', 'uskip' or 'peel'")
@@ -1517,8 +1521,10 @@ class TreePlan(DevicePlan):
                     if leaves is None:
                         leaves = np.zeros((1, 1), np.float32)
                 except ValueError:
-                    if node_format == "compact":
-                        raise NotLowerable("compact pointer layout does not apply")
+                    if node_format in ("compact", "lds"):
+                        raise NotLowerable(f"{node_format} pointer layout does not apply")
+                if compact and node_format == "lds":
+                    self._lds_chunks(nodes, roots, F, spec)
             elif node_format == "compact":
                 raise NotLowerable("compact pointer layout needs features in LDS, lock-step, bfs")
             if heads is None and not compact and not superl and not rank3:
@@ -1534,6 +1540,8 @@ class TreePlan(DevicePlan):
                 self.variant = VAR_POINTER_RANK3
             elif superl:
                 self.variant = VAR_POINTER_SUPER
+            elif compact and getattr(self, "lds_chunks", None) is not None:
+                self.variant = VAR_POINTER_LDS
             elif compact:
                 self.variant = VAR_POINTER_COMPACT
             elif pointer_load == "masked" and self.layout == "pointer" and self.variant == 0 and feat_lds:
@@ -1559,6 +1567,60 @@ class TreePlan(DevicePlan):
             self.slots = None
         self.splits = 1 if self.mode else splits
         self._partial = None
+
+    LDS_SLICES = 8  # XCD slices of the LDS-resident walk (one per XCD: tree_lds.hip)
+
+    def _lds_chunks(self, nodes, roots, F: int, spec) -> None:
+        """Chunk tables of ``node_format="lds"`` (``tree_lds.hip``): 512-row tiles (256 when the
+        feature planes leave too little room), the rest of the 160 KiB LDS one chunk buffer."""
+        from .hybrid import pack_lds_chunks
+
+        general = spec.P > 1 or (spec.mode == "sum" and spec.slots is not None)
+        CA = spec.C if general else 1
+        if general and (spec.C > 8 or spec.P > 8):
+            raise NotLowerable("lds pointer layout: at most 8 class slots")
+        last = None
+        for rows in (512, 256):
+            G = 1024 // rows
+            head = F * rows * 4 + rows * 4 + ((G * CA * rows + 3) & ~3) * 4
+            chunk_u4 = (160 * 1024 - head) // 16
+            if chunk_u4 < 1024:
+                continue
+            try:
+                chunks, slices = pack_lds_chunks(nodes.shape[0], roots, chunk_u4, self.LDS_SLICES)
+            except ValueError as e:
+                last = e
+                continue
+            self.lds_rows, self.lds_chunk_u4 = rows, int(chunk_u4)
+            self.lds_chunks = self._t(chunks.reshape(-1))
+            self.lds_slices = self._t(slices)
+            self.lds_n_slices = int(slices.size - 1)
+            return
+        raise NotLowerable(f"lds pointer layout: {last or 'no room for a chunk buffer'}")
+
+    def _launch_lds(self, a, n: int, stream) -> None:
+        import ctypes
+
+        import torch
+
+        from ..ops._lib import LdsTreeArgs, check, ptr, stream_handle
+
+        S = int(self.lds_n_slices)
+        a.partial = None
+        if S > 1:
+            CA = self.C if self.general else 1
+            need = S * (CA + 1) * n
+            if self._partial is None or self._partial.numel() < need:
+                if self._partial is not None:
+                    self.__dict__.setdefault("_retired", []).append(self._partial)
+                self._partial = torch.empty(max(need, 1 << 20), dtype=torch.float32, device=self.device)
+            a.partial = ptr(self._partial)
+        la = LdsTreeArgs()
+        la.t = a
+        la.chunks, la.slice_chunk = ptr(self.lds_chunks), ptr(self.lds_slices)
+        la.n_slices, la.chunk_u4, la.rows = S, int(self.lds_chunk_u4), int(self.lds_rows)
+        check(self.lib.pmml_tree_lds_launch(stream_handle(stream), ctypes.byref(la)),
+              f"tree kernel (lds, depth {self.depth})")
 
     @staticmethod
     def _stage_columns(compiled, trees) -> List[int]:
@@ -1700,6 +1762,9 @@ class TreePlan(DevicePlan):
                     self.__dict__.setdefault("_retired", []).append(self._partial)
                 self._partial = torch.empty(max(need, 1 << 20), dtype=torch.float32, device=self.device)
             a.partial = ptr(self._partial)
+        if self.variant & VAR_POINTER_LDS:
+            self._launch_lds(a, n, stream)
+            return
         if self.layout == "hybrid":
             from ..ops._lib import HybridArgs
 
@@ -1723,7 +1788,7 @@ class TreePlan(DevicePlan):
 
         from ..ops._lib import TreeArgs, ptr
 
-        if self.layout not in ("perfect", "pointer") or n <= 0:
+        if self.layout not in ("perfect", "pointer") or n <= 0 or self.variant & VAR_POINTER_LDS:
             return None
         s = self._auto_splits(n)
         a = TreeArgs.from_buffer_copy(self._args_template(False))
