@@ -11,7 +11,10 @@
 //    that fit the LDS chunk buffer (compact 8-byte BFS slots, tree.hip::tree_compact_kernel format);
 //  * a workgroup (1024 threads) owns a ROWS-row tile: the rows' prepared features sit in LDS as
 //    [F][ROWS] planes (a lane's read feat[f][lane] is conflict free whatever f), the thread groups
-//    G = 1024 / ROWS split every chunk's trees round-robin, 8 lock-step walks per lane;
+//    G = 1024 / ROWS split every chunk's trees round-robin; a lane walks its trees one after
+//    another, starting the next the step the last one ends (LDS has no shared-line benefit that
+//    would favour lock-step walks; profiles/r5d: lock-step batches over a chunk's 2-3 trees were
+//    VALU bound, 7x the pointer walk's instructions);
 //  * chunks stream global -> VGPRs -> LDS: the next chunk's first 8 KiB per thread group is loaded
 //    into registers while the current chunk is walked (its L2 latency overlaps the walk);
 //  * each (tile, slice) workgroup writes the slice's partial row sums (+ an invalid flag) in the
@@ -35,9 +38,9 @@ struct LdsTreeArgs {
 };
 
 constexpr int LT = 1024;
-constexpr int LPILP = 8;
 constexpr int LCMAX = 8;
 constexpr int LPREF = 4;  // uint4 per thread prefetched into registers during a walk
+constexpr int LROOTS = 256;  // trees per chunk (host-enforced): their chunk-local roots in LDS
 
 template <bool GENERAL, int ROWS>
 __global__ __launch_bounds__(LT, 1) void tree_lds_kernel(LdsTreeArgs la) {
@@ -49,7 +52,8 @@ __global__ __launch_bounds__(LT, 1) void tree_lds_kernel(LdsTreeArgs la) {
   float* feat = reinterpret_cast<float*>(smem);           // [F][ROWS]
   int* bad = reinterpret_cast<int*>(feat + F * ROWS);     // [ROWS]
   float* part = reinterpret_cast<float*>(bad + ROWS);     // [G][CA][ROWS]
-  uint4* cbuf = reinterpret_cast<uint4*>(part + ((G * CA * ROWS + 3) & ~3));
+  int* roots_l = reinterpret_cast<int*>(part + G * CA * ROWS);    // [LROOTS] chunk-local roots
+  uint4* cbuf = reinterpret_cast<uint4*>(roots_l + LROOTS);
   const uint2* nodes = reinterpret_cast<const uint2*>(cbuf);
   const int tid = threadIdx.x;
   const int S = la.n_slices;
@@ -127,6 +131,10 @@ __global__ __launch_bounds__(LT, 1) void tree_lds_kernel(LdsTreeArgs la) {
     __syncthreads();  // the previous chunk's walks are done (and, first time, the feature planes)
     {
       const uint4* src = reinterpret_cast<const uint4*>(a.blob) + (ch.x >> 1);
+      if (tid < ch.w - ch.z) {  // chunk-local root codes (~slot: single-leaf tree)
+        const int rc = a.roots[ch.z + tid];
+        roots_l[tid] = rc >= 0 ? rc - ch.x : ~((~rc) - ch.x);
+      }
       if (tid < ch.y) cbuf[tid] = pf0;
       if (tid + LT < ch.y) cbuf[tid + LT] = pf1;
       if (tid + 2 * LT < ch.y) cbuf[tid + 2 * LT] = pf2;
@@ -144,7 +152,6 @@ __global__ __launch_bounds__(LT, 1) void tree_lds_kernel(LdsTreeArgs la) {
       }
     }
     __syncthreads();
-    const int base = ch.x;
     const int tb = ch.z, te = ch.w;
     // ---- next chunk's head into registers: its loads overlap this chunk's walks
     int4 nch = make_int4(0, 0, 0, 0);
@@ -152,59 +159,57 @@ __global__ __launch_bounds__(LT, 1) void tree_lds_kernel(LdsTreeArgs la) {
       nch = la.chunks[c + 1];
       LDS_PREFETCH(nch)
     }
-    // ---- walk this group's trees of the chunk: trees tb + g, tb + g + G, ... in lock-step batches
-    for (int t0 = tb + g; t0 < te; t0 += G * LPILP) {
-      int pos[LPILP];
-      bool act[LPILP], pz[LPILP];
-#pragma unroll
-      for (int i = 0; i < LPILP; ++i) {
-        const int t = t0 + G * i;
-        const int rc = t < te ? a.roots[t] : ~base;
-        pos[i] = (rc >= 0 ? rc : ~rc) - base;
-        act[i] = rc >= 0;  // a single-leaf tree starts on its leaf
-        pz[i] = false;
+    // ---- walk this group's trees of the chunk (tb + g, tb + g + G, ...) one after another per
+    // lane: a lane whose walk ends adds its leaf and starts its next tree at once (the chunk's
+    // roots sit in LDS), so a wave iterates about the SUM of its lanes' path lengths rather than
+    // the deepest walk of every lock-step batch; leaves still add in tree order per lane.
+    {
+      int t = tb + g;
+      int pos = 0;
+      bool act = false, pz = false;
+      if (t < te) {
+        const int rc = roots_l[t - tb];
+        pos = rc >= 0 ? rc : ~rc;
+        act = rc >= 0;  // a single-leaf tree starts on its leaf
       }
-      bool live = true;
-      while (live) {
-        uint2 nd[LPILP];
-#pragma unroll
-        for (int i = 0; i < LPILP; ++i) nd[i] = nodes[act[i] ? pos[i] : 0];
-        live = false;
-#pragma unroll
-        for (int i = 0; i < LPILP; ++i) {
-          const uint32_t m = nd[i].y;
+      while (t < te) {
+        if (act) {
+          const uint2 nd = nodes[pos];
+          const uint32_t m = nd.y;
           const float x = *reinterpret_cast<const float*>(feat_lane + (m & 63u) * (ROWS * 4));
           const bool isn = (x != x);
-          const bool nulled = act[i] && isn && ((m >> 30) & 1u);
-          const bool right = (x >= __uint_as_float(nd[i].x)) || (isn && (m >> 31));
-          const int child = pos[i] + (int)((m >> 8) & 0x3FFFFFu) + (right ? 1 : 0);
+          const bool nulled = isn && ((m >> 30) & 1u);
+          const bool right = (x >= __uint_as_float(nd.x)) || (isn && (m >> 31));
+          const int child = pos + (int)((m >> 8) & 0x3FFFFFu) + (right ? 1 : 0);
           const bool leaf = right ? ((m >> 7) & 1u) : ((m >> 6) & 1u);
-          pz[i] = pz[i] || nulled;
-          pos[i] = act[i] && !nulled ? child : pos[i];
-          act[i] = act[i] && !nulled && !leaf;
-          live = live || act[i];
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < LPILP; ++i) {
-        const int t = t0 + G * i;
-        if (t >= te) break;
-        if (pz[i]) {
-          if (GENERAL) poisoned = true;
-          else acc += __builtin_nanf("");
-          continue;
-        }
-        const uint32_t lv = nodes[pos[i]].x;
-        if (GENERAL) {
-          const int slot = a.tree_slot[t];
-          const float* lp = a.leaves + (size_t)lv * a.P;
-#pragma unroll
-          for (int k = 0; k < LCMAX; ++k) {
-            const int p = k - slot;
-            if (p >= 0 && p < a.P) accv[k] += lp[p];
-          }
+          pz = pz || nulled;
+          pos = nulled ? pos : child;
+          act = !nulled && !leaf;
         } else {
-          acc += __uint_as_float(lv);
+          if (pz) {
+            if (GENERAL) poisoned = true;
+            else acc += __builtin_nanf("");
+          } else {
+            const uint32_t lv = nodes[pos].x;
+            if (GENERAL) {
+              const int slot = a.tree_slot[t];
+              const float* lp = a.leaves + (size_t)lv * a.P;
+#pragma unroll
+              for (int k = 0; k < LCMAX; ++k) {
+                const int p = k - slot;
+                if (p >= 0 && p < a.P) accv[k] += lp[p];
+              }
+            } else {
+              acc += __uint_as_float(lv);
+            }
+          }
+          t += G;
+          pz = false;
+          if (t < te) {
+            const int rc = roots_l[t - tb];
+            pos = rc >= 0 ? rc : ~rc;
+            act = rc >= 0;
+          }
         }
       }
     }
@@ -278,7 +283,7 @@ PMML_API int pmml_tree_lds_args_size() { return (int)sizeof(LdsTreeArgs); }
 PMML_API long long pmml_tree_lds_bytes(int n_feat, int rows, int C, int general, int chunk_u4) {
   const int G = LT / rows;
   const int CA = general ? C : 1;
-  const long long head = (long long)n_feat * rows * 4 + rows * 4 + (((long long)G * CA * rows + 3) & ~3LL) * 4;
+  const long long head = (long long)n_feat * rows * 4 + rows * 4 + (long long)G * CA * rows * 4 + LROOTS * 4;
   const long long total = head + (long long)chunk_u4 * 16;
   return total <= 160 * 1024 ? total : 0;
 }

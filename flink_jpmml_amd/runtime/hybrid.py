@@ -354,11 +354,12 @@ def pack_compact_bfs(trees, weights: List[float], P: int):
     return nodes, leaves, roots, has_dr
 
 
-def pack_lds_chunks(n_slots: int, roots: np.ndarray, chunk_u4: int, n_slices: int = 8):
+def pack_lds_chunks(n_slots: int, roots: np.ndarray, chunk_u4: int, n_slices: int = 8, max_trees: int = 256):
     """Chunk table of the LDS-resident walk (``tree_lds.hip``) over a :func:`pack_compact_bfs`
     forest: trees in order, cut into ``n_slices`` contiguous slices of about equal slots (one per
     XCD) and every slice into chunks of whole trees whose slots — copied from an even start, as
-    16-byte words — fit ``chunk_u4`` uint4 of LDS.
+    16-byte words — fit ``chunk_u4`` uint4 of LDS (and at most ``max_trees`` trees: their roots are
+    staged in LDS too).
 
     Returns ``(chunks int32[n, 4] {even slot start, uint4 count, tree begin, tree end},
     slice_chunk int32[S + 1])``; ``ValueError`` when one tree alone exceeds the buffer."""
@@ -384,7 +385,7 @@ def pack_lds_chunks(n_slots: int, roots: np.ndarray, chunk_u4: int, n_slices: in
         t = a
         while t < b:
             e = t + 1
-            while e < b and u4(int(start[t]), int(end[e])) <= chunk_u4:
+            while e < b and e - t < max_trees and u4(int(start[t]), int(end[e])) <= chunk_u4:
                 e += 1
             chunks.append((int(start[t]) & ~1, u4(int(start[t]), int(end[e - 1])), t, e))
             t = e

@@ -1582,7 +1582,7 @@ class TreePlan(DevicePlan):
         last = None
         for rows in (512, 256):
             G = 1024 // rows
-            head = F * rows * 4 + rows * 4 + ((G * CA * rows + 3) & ~3) * 4
+            head = F * rows * 4 + rows * 4 + G * CA * rows * 4 + 256 * 4  # + the chunk's roots (csrc LROOTS)
             chunk_u4 = (160 * 1024 - head) // 16
             if chunk_u4 < 1024:
                 continue
