@@ -15,8 +15,10 @@
 //    another, starting the next the step the last one ends (LDS has no shared-line benefit that
 //    would favour lock-step walks; profiles/r5d: lock-step batches over a chunk's 2-3 trees were
 //    VALU bound, 7x the pointer walk's instructions);
-//  * chunks stream global -> VGPRs -> LDS: the next chunk's first 8 KiB per thread group is loaded
-//    into registers while the current chunk is walked (its L2 latency overlaps the walk);
+//  * chunks stream global -> VGPRs -> LDS: the whole next chunk (<= 96 KiB, 6 x 16 B per thread)
+//    and its roots are loaded into registers while the current chunk is walked, so a chunk switch
+//    costs two barriers and the LDS stores, not an L2 round trip (profiles/r5e: the synchronous
+//    remainder of each chunk copy was most of the time);
 //  * each (tile, slice) workgroup writes the slice's partial row sums (+ an invalid flag) in the
 //    split layout [S][C + 1][n], and tree_reduce_kernel (tree.hip) applies the epilogue.
 //
@@ -39,7 +41,8 @@ struct LdsTreeArgs {
 
 constexpr int LT = 1024;
 constexpr int LCMAX = 8;
-constexpr int LPREF = 4;  // uint4 per thread prefetched into registers during a walk
+constexpr int LPREF = 6;  // uint4 per thread: the WHOLE next chunk is prefetched into registers
+                          // during a walk (chunk_u4 <= LPREF * LT, host-enforced)
 constexpr int LROOTS = 256;  // trees per chunk (host-enforced): their chunk-local roots in LDS
 
 template <bool GENERAL, int ROWS>
@@ -113,8 +116,9 @@ __global__ __launch_bounds__(LT, 1) void tree_lds_kernel(LdsTreeArgs la) {
   bool poisoned = false;
 
   const int c0 = la.slice_chunk[slice], c1 = la.slice_chunk[slice + 1];
-  // four named registers (an array here was put in scratch by the compiler)
-  uint4 pf0, pf1, pf2, pf3;
+  // named registers (an array here was put in scratch by the compiler); rtp: the chunk's root
+  uint4 pf0, pf1, pf2, pf3, pf4, pf5;
+  int rtp = 0;
 #define LDS_PREFETCH(CH)                                                                      \
   {                                                                                           \
     const uint4* src_ = reinterpret_cast<const uint4*>(a.blob) + ((CH).x >> 1);             \
@@ -123,33 +127,24 @@ __global__ __launch_bounds__(LT, 1) void tree_lds_kernel(LdsTreeArgs la) {
     pf1 = src_[min(tid + LT, last_)];                                                         \
     pf2 = src_[min(tid + 2 * LT, last_)];                                                     \
     pf3 = src_[min(tid + 3 * LT, last_)];                                                     \
+    pf4 = src_[min(tid + 4 * LT, last_)];                                                     \
+    pf5 = src_[min(tid + 5 * LT, last_)];                                                     \
+    rtp = a.roots[min((CH).z + tid, max((CH).w - 1, 0))];                                    \
   }
   int4 ch = c0 < c1 ? la.chunks[c0] : make_int4(0, 0, 0, 0);
-  LDS_PREFETCH(ch)  // first chunk's head (consumed below like every later chunk's)
+  LDS_PREFETCH(ch)  // first chunk (consumed below like every later chunk)
   for (int c = c0; c < c1; ++c) {
     // ---- chunk c into LDS: the prefetched head from registers, the rest straight through
     __syncthreads();  // the previous chunk's walks are done (and, first time, the feature planes)
     {
-      const uint4* src = reinterpret_cast<const uint4*>(a.blob) + (ch.x >> 1);
-      if (tid < ch.w - ch.z) {  // chunk-local root codes (~slot: single-leaf tree)
-        const int rc = a.roots[ch.z + tid];
-        roots_l[tid] = rc >= 0 ? rc - ch.x : ~((~rc) - ch.x);
-      }
+      if (tid < ch.w - ch.z)  // chunk-local root codes (~slot: single-leaf tree)
+        roots_l[tid] = rtp >= 0 ? rtp - ch.x : ~((~rtp) - ch.x);
       if (tid < ch.y) cbuf[tid] = pf0;
       if (tid + LT < ch.y) cbuf[tid + LT] = pf1;
       if (tid + 2 * LT < ch.y) cbuf[tid + 2 * LT] = pf2;
       if (tid + 3 * LT < ch.y) cbuf[tid + 3 * LT] = pf3;
-      for (int i = tid + LPREF * LT; i < ch.y; i += 4 * LT) {
-        uint4 t0 = src[i], t1, t2, t3;
-        const int i1 = i + LT, i2 = i + 2 * LT, i3 = i + 3 * LT;
-        if (i1 < ch.y) t1 = src[i1];
-        if (i2 < ch.y) t2 = src[i2];
-        if (i3 < ch.y) t3 = src[i3];
-        cbuf[i] = t0;
-        if (i1 < ch.y) cbuf[i1] = t1;
-        if (i2 < ch.y) cbuf[i2] = t2;
-        if (i3 < ch.y) cbuf[i3] = t3;
-      }
+      if (tid + 4 * LT < ch.y) cbuf[tid + 4 * LT] = pf4;
+      if (tid + 5 * LT < ch.y) cbuf[tid + 5 * LT] = pf5;
     }
     __syncthreads();
     const int tb = ch.z, te = ch.w;
@@ -294,7 +289,7 @@ PMML_API int pmml_tree_lds_launch(hipStream_t stream, const LdsTreeArgs* args) {
   LdsTreeArgs la = *args;
   TreeArgs& a = la.t;
   if (a.n_rows <= 0) return 0;
-  if (la.n_slices < 1 || la.chunk_u4 < 1) return -2;
+  if (la.n_slices < 1 || la.chunk_u4 < 1 || la.chunk_u4 > LPREF * LT) return -2;
   if (!(la.rows == 512 || la.rows == 256)) return -4;
   if (a.n_feat < 1 || a.n_feat > 64) return -4;
   if (a.general && (a.C > LCMAX || a.P > LCMAX)) return -3;

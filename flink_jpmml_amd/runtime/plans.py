@@ -1583,7 +1583,7 @@ class TreePlan(DevicePlan):
         for rows in (512, 256):
             G = 1024 // rows
             head = F * rows * 4 + rows * 4 + G * CA * rows * 4 + 256 * 4  # + the chunk's roots (csrc LROOTS)
-            chunk_u4 = (160 * 1024 - head) // 16
+            chunk_u4 = min((160 * 1024 - head) // 16, 6 * 1024)  # csrc: LPREF x 1024 uint4 prefetched
             if chunk_u4 < 1024:
                 continue
             try:
