@@ -313,6 +313,93 @@ __device__ __forceinline__ void store_hidden_t(const GemmArgs& a, const f32x16 (
   }
 }
 
+// 128-byte ROW-SEGMENT stores of the transposed accumulators (K = 64 persistent kernel, VERDICT r4
+// item 4). store_hidden_t leaves a 32 x 32 tile as 16-byte stores whose 64 lanes sit on 32 rows —
+// every store instruction touches 32 cache lines, and the K = 64 layer, which writes 2 GB per 1M
+// rows, is bound by the address unit (TA 78 % busy, profiles/r4ad). Here a pair of 32-unit tiles
+// (one 128-byte segment of a row) is packed to bf16 per tile, the pair's rows pass through a
+// 2 KiB wave-private LDS scratch 16 rows at a time (16-byte chunks XOR-swizzled by row & 7: both
+// the staging writes and the segment reads are conflict free), and each global store instruction
+// covers 8 whole 128-byte row segments (8 lines). Same store count (4 per tile pair and 32 rows),
+// same values; only the wave's own lanes touch its scratch, so no barrier.
+template <int ACT, int TM, int TN>
+__device__ __forceinline__ void store_hidden_seg(const GemmArgs& a, const f32x16 (&acc)[TM][TN], int row0, int col0,
+                                                 int wm, int wn, int lane, const float* bl, unsigned char* ws) {
+  static_assert(TN % 2 == 0, "tile pairs");
+  const int h = lane >> 5, l32 = lane & 31;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int jp = 0; jp < TN / 2; ++jp) {
+      uint4 c[2][2];  // [tile of the pair][run]: runs at chunks h, 2 + h of the tile's 64 bytes
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const int j = 2 * jp + jj;
+        float b[16];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float4 v = *reinterpret_cast<const float4*>(bl + (wn * TN + j) * 32 + 8 * q + 4 * h);
+          b[4 * q] = v.x, b[4 * q + 1] = v.y, b[4 * q + 2] = v.z, b[4 * q + 3] = v.w;
+        }
+        uint32_t p[8];
+#pragma unroll
+        for (int w = 0; w < 8; ++w) {
+          const float v0 = act_of<ACT>(acc[i][j][2 * w] + b[2 * w], a.act, a.thr);
+          const float v1 = act_of<ACT>(acc[i][j][2 * w + 1] + b[2 * w + 1], a.act, a.thr);
+          p[w] = (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)v0) |
+                 ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)v1) << 16);
+        }
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const auto x0 = __builtin_amdgcn_permlane32_swap(p[4 * s + 0], p[4 * s + 2], false, false);
+          const auto x1 = __builtin_amdgcn_permlane32_swap(p[4 * s + 1], p[4 * s + 3], false, false);
+          c[jj][s] = make_uint4(x0[0], x1[0], x0[1], x1[1]);
+        }
+      }
+      const int u0 = col0 + (wn * TN + 2 * jp) * 32;  // first unit of the pair's 128-byte segment
+      const size_t rb = (size_t)(row0 + (wm * TM + i) * 32);
+#pragma unroll
+      for (int ph = 0; ph < 2; ++ph) {
+        if ((l32 >> 4) == ph) {  // rows 16 ph .. 16 ph + 15 stage their 4 x 16 bytes per lane
+          const int r = l32 & 15;
+          unsigned char* rowp = ws + r * 128;
+          const int sw = r & 7;
+          *reinterpret_cast<uint4*>(rowp + (((0 + h) ^ sw) << 4)) = c[0][0];
+          *reinterpret_cast<uint4*>(rowp + (((2 + h) ^ sw) << 4)) = c[0][1];
+          *reinterpret_cast<uint4*>(rowp + (((4 + h) ^ sw) << 4)) = c[1][0];
+          *reinterpret_cast<uint4*>(rowp + (((6 + h) ^ sw) << 4)) = c[1][1];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // lane L: chunk L & 7 of rows L >> 3 and 8 + (L >> 3) (LDS hands a wave's ops back in order)
+        const int rr = lane >> 3, k = lane & 7;
+        const uint4 v0 = *reinterpret_cast<const uint4*>(ws + rr * 128 + ((k ^ (rr & 7)) << 4));
+        const uint4 v1 = *reinterpret_cast<const uint4*>(ws + (rr + 8) * 128 + ((k ^ ((rr + 8) & 7)) << 4));
+        __bf16* d0 = static_cast<__bf16*>(a.C) + (rb + 16 * ph + rr) * a.ldc + u0 + 8 * k;
+        *reinterpret_cast<uint4*>(d0) = v0;
+        *reinterpret_cast<uint4*>(d0 + 8 * (size_t)a.ldc) = v1;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
+    }
+  }
+}
+
+template <int TM, int TN>
+__device__ __forceinline__ void store_hidden_seg_any(const GemmArgs& a, const f32x16 (&acc)[TM][TN], int row0,
+                                                     int col0, int wm, int wn, int lane, const float* bl,
+                                                     unsigned char* ws) {
+  switch (a.act) {
+    case A_IDENTITY: store_hidden_seg<A_IDENTITY, TM, TN>(a, acc, row0, col0, wm, wn, lane, bl, ws); break;
+    case A_RELU: store_hidden_seg<A_RELU, TM, TN>(a, acc, row0, col0, wm, wn, lane, bl, ws); break;
+    case A_LOGISTIC: store_hidden_seg<A_LOGISTIC, TM, TN>(a, acc, row0, col0, wm, wn, lane, bl, ws); break;
+    case A_TANH: store_hidden_seg<A_TANH, TM, TN>(a, acc, row0, col0, wm, wn, lane, bl, ws); break;
+    default: store_hidden_seg<-1, TM, TN>(a, acc, row0, col0, wm, wn, lane, bl, ws); break;
+  }
+}
+
 template <int TM, int TN, bool LB = false>
 __device__ __forceinline__ void store_hidden_t_any(const GemmArgs& a, const f32x16 (&acc)[TM][TN], int row0, int col0,
                                                    int wm, int wn, int lane, const float* bl = nullptr) {
@@ -917,6 +1004,7 @@ __global__ __launch_bounds__(NT, 1) void gemm8_kernel(GemmArgs a, HeadFuse hf) {
 // and the n_ct column-tile owners of a row group share it, so a row tile's A is fetched from HBM
 // once and hit in that XCD's L2 by the other column tiles. Two workgroups per CU (65 KiB of LDS each).
 constexpr int K64P_STORES = 16;  // store_hidden_t<2, 4>: 2 x 4 tiles x 2 stores per lane
+template <bool SEG>
 __global__ __launch_bounds__(K64_NT, 2) void gemm_k64p_kernel(GemmArgs a, int rg) {
   constexpr int TM = 2, TN = 4;
   constexpr int A_B = K64_BM * SLICE_B;
@@ -925,6 +1013,7 @@ __global__ __launch_bounds__(K64_NT, 2) void gemm_k64p_kernel(GemmArgs a, int rg
   unsigned char* As = smem + 256 * SLICE_B;          // two 128-row A buffers
   float* bl = reinterpret_cast<float*>(As + 2 * A_B);  // 256 biases
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  unsigned char* ws = reinterpret_cast<unsigned char*>(bl + 256) + wave * 2048;  // SEG: wave scratch
   const int h = lane >> 5, l32 = lane & 31;
   const int n_ct = a.Mp / 256, n_rt = a.rows_p / K64_BM;
   const int local = blockIdx.x >> 3;
@@ -965,7 +1054,8 @@ __global__ __launch_bounds__(K64_NT, 2) void gemm_k64p_kernel(GemmArgs a, int rg
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
     }
-    store_hidden_t_any<TM, TN, true>(a, acc, rt * K64_BM, col0, wm, wn, lane, bl);
+    if constexpr (SEG) store_hidden_seg_any<TM, TN>(a, acc, rt * K64_BM, col0, wm, wn, lane, bl, ws);
+    else store_hidden_t_any<TM, TN, true>(a, acc, rt * K64_BM, col0, wm, wn, lane, bl);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
@@ -979,11 +1069,16 @@ int launch_k64p(hipStream_t stream, const GemmArgs& a) {
   }
   const int n_ct = a.Mp / 256;
   const int rg = std::max(1, (2 * n_cu / 8) / n_ct);  // row groups per XCD: ~2 workgroups per CU
-  const size_t lds = (size_t)(256 + 2 * K64_BM) * SLICE_B + 256 * 4;
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_k64p_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)lds) != hipSuccess)
-    return -5;
-  hipLaunchKernelGGL(gemm_k64p_kernel, dim3(8 * n_ct * rg), dim3(K64_NT), lds, stream, a, rg);
+  // bit 10: 128-byte row-segment stores through a 2 KiB wave scratch (store_hidden_seg)
+  const bool seg = (a.f32 >> 10) & 1;
+  const size_t lds = (size_t)(256 + 2 * K64_BM) * SLICE_B + 256 * 4 + (seg ? 4 * 2048 : 0);
+  const void* kp = seg ? reinterpret_cast<const void*>(&gemm_k64p_kernel<true>)
+                       : reinterpret_cast<const void*>(&gemm_k64p_kernel<false>);
+  if (hipFuncSetAttribute(kp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return -5;
+  if (seg)
+    hipLaunchKernelGGL(gemm_k64p_kernel<true>, dim3(8 * n_ct * rg), dim3(K64_NT), lds, stream, a, rg);
+  else
+    hipLaunchKernelGGL(gemm_k64p_kernel<false>, dim3(8 * n_ct * rg), dim3(K64_NT), lds, stream, a, rg);
   return 0;
 }
 
@@ -1052,7 +1147,7 @@ PMML_API int pmml_gemm_launch(hipStream_t stream, const GemmArgs* args, int head
   const GemmArgs a = *args;
   if (a.rows <= 0) return 0;
   const int BN = head ? 32 : 256;
-  if (a.f32 & ~0x3E1) return -4;
+  if (a.f32 & ~0x7E1) return -4;
   // bf16 hidden layers with K >= 512 run the phase-interleaved kernel (profiles/r3ao: 2048 x 2048
   // 8.73 -> 8.36 ms, 1024 x 1024 2.62 -> 2.48 ms over 1M rows); below that the layer is bound by
   // its output writes and the 2-buffer loop is faster (K = 64: 0.83 vs 0.92 ms). Bit 7 forces it.

@@ -331,3 +331,26 @@ def test_transposed_accumulator_stores_match_direct_stores(gpu, shape):
     assert torch.equal(v0, v2) and torch.equal(s0[v0.bool()], s2[v2.bool()])
     ref, vref = c.score_matrix_oracle(X[:3000])  # the oracle walks connections in Python
     assert (v0[:3000].cpu().numpy().astype(bool) == vref).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [dict(n_features=32, hidden=(1024, 1024, 512)),
+                                   dict(n_features=40, hidden=(300, 260), activation="tanh"),
+                                   dict(n_features=24, hidden=(512, 768), activation="logistic", n_out=3,
+                                        classification=True)],
+                         ids=["1024x1024x512", "300x260-tanh", "512x768-logistic"])
+def test_row_segment_stores_match_transposed_stores(gpu, shape):
+    """K = 64 persistent layer, 128-byte row-segment stores through the wave LDS scratch (flag bit
+    10, store_hidden_seg) equal the default store_hidden_t bits; 41000 rows =
+    a ragged last row tile."""
+    c = CompiledPmml.from_string(mlp_pmml(seed=29, **shape))
+    plan = c.plan(gpu, precision="bf16", mlp_impl="wide")
+    plan.fuse_head = False
+    X = stream_matrix(41_000, shape["n_features"], seed=8, missing_rate=0.01)
+    s0, v0 = plan.score(X)
+    plan.gemm_flags = 0x400
+    try:
+        s1, v1 = plan.score(X)
+    finally:
+        plan.gemm_flags = 0
+    assert torch.equal(v0, v1) and torch.equal(s0[v0.bool()], s1[v1.bool()])
