@@ -55,7 +55,9 @@ struct GemmArgs {
   int f32;                // bit 0: operand / activation type (0 bf16, 1 fp32); experiment bits (A/B tests,
                           // WideMlpPlan.gemm_flags): 5 wave-private LDS epilogue, 6 K = 64 on the 256 x 256
                           // tile, 7 force the phase-interleaved kernel, 8 direct [row][unit] stores instead of
-                          // store_hidden_t, 9 one K = 64 tile per workgroup instead of gemm_k64p_kernel
+                          // store_hidden_t, 9 one K = 64 tile per workgroup instead of gemm_k64p_kernel,
+                          // 10 gemm_k64p_kernel with store_hidden_t instead of the row-segment stores,
+                          // 11 the same for gemm8_kernel<false, true>
   const uint8_t* row_ok;  // [rows] input-stage validity (output layer)
   Epilogue epi;           // output layer decode (affine + Target, or label table)
   float* score;
@@ -322,7 +324,7 @@ __device__ __forceinline__ void store_hidden_t(const GemmArgs& a, const f32x16 (
 // the staging writes and the segment reads are conflict free), and each global store instruction
 // covers 8 whole 128-byte row segments (8 lines). Same store count (4 per tile pair and 32 rows),
 // same values; only the wave's own lanes touch its scratch, so no barrier.
-template <int ACT, int TM, int TN>
+template <int ACT, int TM, int TN, bool LB = true>
 __device__ __forceinline__ void store_hidden_seg(const GemmArgs& a, const f32x16 (&acc)[TM][TN], int row0, int col0,
                                                  int wm, int wn, int lane, const float* bl, unsigned char* ws) {
   static_assert(TN % 2 == 0, "tile pairs");
@@ -336,10 +338,16 @@ __device__ __forceinline__ void store_hidden_seg(const GemmArgs& a, const f32x16
       for (int jj = 0; jj < 2; ++jj) {
         const int j = 2 * jp + jj;
         float b[16];
+        if constexpr (LB) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float4 v = *reinterpret_cast<const float4*>(bl + (wn * TN + j) * 32 + 8 * q + 4 * h);
-          b[4 * q] = v.x, b[4 * q + 1] = v.y, b[4 * q + 2] = v.z, b[4 * q + 3] = v.w;
+          for (int q = 0; q < 4; ++q) {
+            const float4 v = *reinterpret_cast<const float4*>(bl + (wn * TN + j) * 32 + 8 * q + 4 * h);
+            b[4 * q] = v.x, b[4 * q + 1] = v.y, b[4 * q + 2] = v.z, b[4 * q + 3] = v.w;
+          }
+        } else {
+          const int ub = col0 + (wn * TN + j) * 32;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) b[r] = a.bias[ub + (r & 3) + 8 * (r >> 2) + 4 * h];
         }
         uint32_t p[8];
 #pragma unroll
@@ -387,16 +395,16 @@ __device__ __forceinline__ void store_hidden_seg(const GemmArgs& a, const f32x16
   }
 }
 
-template <int TM, int TN>
+template <int TM, int TN, bool LB = true>
 __device__ __forceinline__ void store_hidden_seg_any(const GemmArgs& a, const f32x16 (&acc)[TM][TN], int row0,
                                                      int col0, int wm, int wn, int lane, const float* bl,
                                                      unsigned char* ws) {
   switch (a.act) {
-    case A_IDENTITY: store_hidden_seg<A_IDENTITY, TM, TN>(a, acc, row0, col0, wm, wn, lane, bl, ws); break;
-    case A_RELU: store_hidden_seg<A_RELU, TM, TN>(a, acc, row0, col0, wm, wn, lane, bl, ws); break;
-    case A_LOGISTIC: store_hidden_seg<A_LOGISTIC, TM, TN>(a, acc, row0, col0, wm, wn, lane, bl, ws); break;
-    case A_TANH: store_hidden_seg<A_TANH, TM, TN>(a, acc, row0, col0, wm, wn, lane, bl, ws); break;
-    default: store_hidden_seg<-1, TM, TN>(a, acc, row0, col0, wm, wn, lane, bl, ws); break;
+    case A_IDENTITY: store_hidden_seg<A_IDENTITY, TM, TN, LB>(a, acc, row0, col0, wm, wn, lane, bl, ws); break;
+    case A_RELU: store_hidden_seg<A_RELU, TM, TN, LB>(a, acc, row0, col0, wm, wn, lane, bl, ws); break;
+    case A_LOGISTIC: store_hidden_seg<A_LOGISTIC, TM, TN, LB>(a, acc, row0, col0, wm, wn, lane, bl, ws); break;
+    case A_TANH: store_hidden_seg<A_TANH, TM, TN, LB>(a, acc, row0, col0, wm, wn, lane, bl, ws); break;
+    default: store_hidden_seg<-1, TM, TN, LB>(a, acc, row0, col0, wm, wn, lane, bl, ws); break;
   }
 }
 
@@ -977,7 +985,13 @@ __global__ __launch_bounds__(NT, 1) void gemm8_kernel(GemmArgs a, HeadFuse hf) {
     }
     return;
   } else if constexpr (TST) {
-    store_hidden_t_any<TM, TN>(a, acc, row0, col0, wr, wc, lane);
+    if (!((a.f32 >> 11) & 1)) {
+      // 128-byte row-segment stores through a 2 KiB wave scratch (the staging slots are drained:
+      // every wave is past the balancing barrier above); bit 11: store_hidden_t
+      store_hidden_seg_any<TM, TN, false>(a, acc, row0, col0, wr, wc, lane, nullptr, smem + wave * 2048);
+    } else {
+      store_hidden_t_any<TM, TN>(a, acc, row0, col0, wr, wc, lane);
+    }
   } else {
     if ((a.f32 >> 5) & 1) {  // bit 5: the wave-private LDS epilogue (measured slower, profiles/r4k)
       // every wave is past its last LDS read of the staged slices (the balancing barrier above)
@@ -1069,8 +1083,9 @@ int launch_k64p(hipStream_t stream, const GemmArgs& a) {
   }
   const int n_ct = a.Mp / 256;
   const int rg = std::max(1, (2 * n_cu / 8) / n_ct);  // row groups per XCD: ~2 workgroups per CU
-  // bit 10: 128-byte row-segment stores through a 2 KiB wave scratch (store_hidden_seg)
-  const bool seg = (a.f32 >> 10) & 1;
+  // 128-byte row-segment stores through a 2 KiB wave scratch (store_hidden_seg, default: 0.565 ->
+  // 0.438 ms for 1M rows x 1024 units, TA busy 78 -> 52 %, profiles/r5f); bit 10: store_hidden_t
+  const bool seg = !((a.f32 >> 10) & 1);
   const size_t lds = (size_t)(256 + 2 * K64_BM) * SLICE_B + 256 * 4 + (seg ? 4 * 2048 : 0);
   const void* kp = seg ? reinterpret_cast<const void*>(&gemm_k64p_kernel<true>)
                        : reinterpret_cast<const void*>(&gemm_k64p_kernel<false>);
@@ -1147,7 +1162,7 @@ PMML_API int pmml_gemm_launch(hipStream_t stream, const GemmArgs* args, int head
   const GemmArgs a = *args;
   if (a.rows <= 0) return 0;
   const int BN = head ? 32 : 256;
-  if (a.f32 & ~0x7E1) return -4;
+  if (a.f32 & ~0xFE1) return -4;
   // bf16 hidden layers with K >= 512 run the phase-interleaved kernel (profiles/r3ao: 2048 x 2048
   // 8.73 -> 8.36 ms, 1024 x 1024 2.62 -> 2.48 ms over 1M rows); below that the layer is bound by
   // its output writes and the 2-buffer loop is faster (K = 64: 0.83 vs 0.92 ms). Bit 7 forces it.

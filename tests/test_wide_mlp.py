@@ -337,20 +337,22 @@ def test_transposed_accumulator_stores_match_direct_stores(gpu, shape):
 @pytest.mark.parametrize("shape", [dict(n_features=32, hidden=(1024, 1024, 512)),
                                    dict(n_features=40, hidden=(300, 260), activation="tanh"),
                                    dict(n_features=24, hidden=(512, 768), activation="logistic", n_out=3,
-                                        classification=True)],
-                         ids=["1024x1024x512", "300x260-tanh", "512x768-logistic"])
+                                        classification=True),
+                                   dict(n_features=32, hidden=(1024, 1024, 1024, 512))],
+                         ids=["1024x1024x512", "300x260-tanh", "512x768-logistic", "1024x3-512"])
 def test_row_segment_stores_match_transposed_stores(gpu, shape):
-    """K = 64 persistent layer, 128-byte row-segment stores through the wave LDS scratch (flag bit
-    10, store_hidden_seg) equal the default store_hidden_t bits; 41000 rows =
-    a ragged last row tile."""
+    """The default 128-byte row-segment stores through a wave LDS scratch (store_hidden_seg) on the
+    K = 64 persistent layer and on the phase-interleaved hidden kernel equal the store_hidden_t
+    bits (flag bits 10 / 11); 41000 rows = a ragged last row tile."""
     c = CompiledPmml.from_string(mlp_pmml(seed=29, **shape))
     plan = c.plan(gpu, precision="bf16", mlp_impl="wide")
     plan.fuse_head = False
     X = stream_matrix(41_000, shape["n_features"], seed=8, missing_rate=0.01)
     s0, v0 = plan.score(X)
-    plan.gemm_flags = 0x400
-    try:
-        s1, v1 = plan.score(X)
-    finally:
-        plan.gemm_flags = 0
-    assert torch.equal(v0, v1) and torch.equal(s0[v0.bool()], s1[v1.bool()])
+    for flags in (0x400, 0x800, 0xC00):  # store_hidden_t on the K = 64 layer / on gemm8 / on both
+        plan.gemm_flags = flags
+        try:
+            s1, v1 = plan.score(X)
+        finally:
+            plan.gemm_flags = 0
+        assert torch.equal(v0, v1) and torch.equal(s0[v0.bool()], s1[v1.bool()]), hex(flags)
