@@ -651,16 +651,24 @@ class ChainView(SubView):
         return len(self.active_fields)
 
 
-_CHAIN_OUT = ("predictedValue", "transformedValue", "probability")
+_CHAIN_OUT = ("predictedValue", "transformedValue", "probability", "decision")
 
 
 class ChainPlan(DevicePlan):
     """``multipleModelMethod="modelChain"`` beyond the fused tree → calibrator form: the segments
     run in document order on an augmented device matrix ``[inputs | chain outputs]``; each
-    segment's Output fields (predictedValue, transformedValue without an expression, probability
-    of a class) are written into their columns where its predicate is TRUE (NaN elsewhere, as the
-    oracle hides them), later segments read them like inputs, and every row takes the result of
-    the LAST segment whose predicate is TRUE (`models/mining.py::MiningEvaluator._select`)."""
+    segment's Output fields are written into their columns where its predicate is TRUE (NaN
+    elsewhere, as the oracle hides them), later segments read them like inputs, and every row takes
+    the result of the LAST segment whose predicate is TRUE (`models/mining.py::MiningEvaluator._select`).
+
+    Output fields: predictedValue (classification segments score class INDICES here; a per-output
+    table maps them to the field's encoding, so string-typed labels feed later segments as their
+    vocabulary codes, as in the oracle), probability of a class, transformedValue / decision
+    without an expression (the segment value), and transformedValue / decision WITH an expression:
+    those are compiled into one derive program per segment (``ops/csrc/derive.hip``, the postfix
+    fp64 VM of the DerivedField pass) over the augmented columns — they may read inputs, earlier
+    segments' outputs and this segment's own outputs, in document order like
+    ``ModelEvaluator.compute_outputs``."""
 
     kind = "chain"
     supports_direct = False
@@ -674,30 +682,46 @@ class ChainPlan(DevicePlan):
             raise NotLowerable("not a modelChain")
         if self.prep is not None:
             raise NotLowerable("chain plans read prepared inputs (compile_plan adds the prepare pass)")
+        schema = compiled.schema
         base = list(compiled.active_fields)
         self.n_base = len(base)
-        self.outs = []  # (segment, column, feature, class position or -1)
+        # (segment, column, feature, class position or -1, value table index or -1, expression or None)
+        self.outs = []
+        self.tables: List[np.ndarray] = []
         names = list(base)
         for i, (seg, sub) in enumerate(zip(ev.segments, ev.sub)):
+            cats = list(getattr(sub, "categories", None) or []) if sub.kind == "classification" else []
             for of in sub.model.output:
-                if of.feature not in _CHAIN_OUT or (of.feature == "transformedValue" and of.expression is not None):
+                if of.feature not in _CHAIN_OUT:
                     raise NotLowerable(f"chain output {of.name!r}: feature {of.feature!r} is host-only")
                 if of.name in names:
                     raise NotLowerable(f"chain output {of.name!r} shadows a field")
-                pos = -1
+                pos, tab, ex = -1, -1, None
                 if of.feature == "probability":
-                    cats = getattr(sub, "categories", None) or []
                     if of.value is None or of.value not in cats:
                         raise NotLowerable(f"chain output {of.name!r}: probability of an unknown class")
                     pos = cats.index(of.value)
-                elif sub.kind == "classification" and compiled.schema.is_string(of.name):
-                    raise NotLowerable(f"chain output {of.name!r}: string-typed predicted label")
-                self.outs.append((i, len(names), of.feature, pos))
+                elif of.feature in ("transformedValue", "decision") and of.expression is not None:
+                    ex = of.expression
+                elif of.feature == "decision":
+                    raise NotLowerable(f"chain output {of.name!r}: decision without an expression")
+                elif of.feature == "transformedValue":
+                    pos = -2 if sub.kind == "classification" else -1  # -2: the oracle's NaN column
+                elif sub.kind == "classification":
+                    # class index -> the output field's encoding of the label (a vocabulary code for a
+                    # string-typed field, the label's number otherwise)
+                    tab = len(self.tables)
+                    self.tables.append(np.array([schema.lookup(of.name, c) for c in cats] + [np.nan]))
+                elif sub.kind == "regression":
+                    pass
+                else:
+                    raise NotLowerable(f"chain output {of.name!r}: {sub.kind} predictedValue is host-only")
+                self.outs.append((i, len(names), of.feature, pos, tab, ex))
                 names.append(of.name)
         self.columns = names
         col = {c: j for j, c in enumerate(names)}
         self.progs = [compile_predicate(s.predicate, _Cols(compiled, col)) for s in ev.segments]
-        self.subs, self.cols, self.need_probs = [], [], []
+        self.subs, self.cols, self.need_probs, self.label_tabs = [], [], [], []
         for i, (seg, sub) in enumerate(zip(ev.segments, ev.sub)):
             used = [f.name for f in sub.model.mining_schema.active]
             missing = [f for f in used if f not in col]
@@ -710,9 +734,16 @@ class ChainPlan(DevicePlan):
             want = any(o[0] == i and o[2] == "probability" for o in self.outs)
             if want and probs_width(plan) != len(sub.categories):
                 raise NotLowerable(f"chain segment {seg.id!r}: {type(plan).__name__} does not expose probabilities")
+            if sub.kind == "classification":
+                _index_outputs(plan)  # class indices; labels through label_tabs / output tables
+                self.label_tabs.append(self._t(np.append(_label_table(list(sub.categories)), np.float32(np.nan))))
+            else:
+                self.label_tabs.append(None)
             self.subs.append(plan)
             self.cols.append([col[f] for f in used])
             self.need_probs.append(len(sub.categories) if want else 0)
+        # expression outputs: one derive program per segment over every augmented column
+        self.expr_progs = [self._expr_program(compiled, col, i) for i in range(len(self.subs))]
         self.kind_ = ev.kind
         final = ev.sub[-1]
         self.tgt = target_post(ev.target, force=True) if ev.kind == "regression" and ev.target is not None else None
@@ -720,6 +751,59 @@ class ChainPlan(DevicePlan):
         if ev.kind == "classification":
             self.final_labels = self._t(_label_table(list(final.categories)))
         self._col_idx = [self._t(np.array(c, dtype=np.int64)) for c in self.cols]
+        self._tabs = [self._t(t) for t in self.tables]
+
+    def _expr_program(self, compiled, col: dict, seg: int):
+        """``(DerivedProgram, insns, pool, out_cols, [augmented column of each output])`` computing
+        segment ``seg``'s expression outputs in document order, or None."""
+        from .derive import INSN_DTYPE, OP_STORE, STACK_DEPTH, DerivedProgram, _Emitter
+
+        exprs = [(c, ex) for s_, c, _, _, _, ex in self.outs if s_ == seg and ex is not None]
+        if not exprs:
+            return None
+        n_in = len(self.columns)
+        if n_in + len(exprs) > 256:
+            raise NotLowerable("chain expression outputs: more than 256 augmented columns")
+        col_of = dict(col)
+        em = _Emitter(compiled.schema, col_of)
+        derived = []
+        for j, (c, ex) in enumerate(exprs):
+            name = self.columns[c]
+            em.expr(ex, name)
+            dt = compiled.schema.types.get(name)
+            em.emit(OP_STORE, a=n_in + j, c=2 if dt == "integer" else 0, pops=1)
+            col_of[name] = n_in + j  # later expressions read the fresh value
+            derived.append(name)
+        if em.max_sp > STACK_DEPTH:
+            raise NotLowerable(f"chain expression output needs a stack of {em.max_sp} > {STACK_DEPTH}")
+        insns = np.array(em.insns, dtype=INSN_DTYPE)
+        prog = DerivedProgram(list(self.columns), derived, derived, insns, np.array(em.pool or [0.0]), em.max_sp)
+        return (prog, self._t(insns.view(np.int32).reshape(-1)), self._t(prog.pool), self._t(prog.out_cols),
+                [c for c, _ in exprs])
+
+    def _run_expr(self, ep, Xa, st):
+        """The derive program over the augmented matrix -> ``[n, outputs]`` fp32."""
+        import ctypes
+
+        import torch
+
+        from ..ops._lib import DeriveArgs, check, ptr, stream_handle
+        from .derive import emulate
+
+        prog, insns, pool, out_cols, _ = ep
+        n = Xa.shape[0]
+        if self.device.type != "cuda":  # lowering dry run (CPU tests): the kernel's numpy twin
+            return torch.from_numpy(emulate(prog, Xa.double().numpy()))
+        out = torch.empty((n, len(prog.selected)), dtype=torch.float32, device=self.device)
+        ok = torch.empty(n, dtype=torch.uint8, device=self.device)
+        a = DeriveArgs()
+        a.X = Xa.data_ptr()
+        a.n_rows, a.n_in, a.ldx, a.n_tile = n, Xa.shape[1], Xa.stride(0), prog.n_tile
+        a.prep, a.prog, a.pool, a.out_cols = None, ptr(insns), ptr(pool), ptr(out_cols)
+        a.n_insn, a.n_sel = len(prog.insns), len(prog.selected)
+        a.out, a.row_ok = ptr(out), ptr(ok)
+        check(self.lib.pmml_derive_launch(stream_handle(st), ctypes.byref(a)), "chain output derive kernel")
+        return out
 
     def launch(self, X, score, valid, stream=None, probs=None, score2=None, valid2=None, **kw) -> None:
         import torch
@@ -729,10 +813,11 @@ class ChainPlan(DevicePlan):
             return
         st = stream if stream is not None and self.device.type == "cuda" else None
         ctx = torch.cuda.stream(st) if st is not None else contextlib.nullcontext()
+        nan = float("nan")
         with ctx:
-            Xa = torch.full((n, len(self.columns)), float("nan"), dtype=torch.float32, device=self.device)
+            Xa = torch.full((n, len(self.columns)), nan, dtype=torch.float32, device=self.device)
             Xa[:, : self.n_base] = X[:, : self.n_base]
-            best_s = torch.full((n,), float("nan"), dtype=torch.float64, device=self.device)
+            best_s = torch.full((n,), nan, dtype=torch.float64, device=self.device)
             best_v = torch.zeros(n, dtype=torch.bool, device=self.device)
             for i, plan in enumerate(self.subs):
                 Xi = Xa.index_select(1, self._col_idx[i]).contiguous()
@@ -740,23 +825,48 @@ class ChainPlan(DevicePlan):
                 v = torch.empty(n, dtype=torch.uint8, device=self.device)
                 pr = None
                 if self.need_probs[i]:
-                    pr = torch.full((n, self.need_probs[i]), float("nan"), dtype=torch.float32, device=self.device)
+                    pr = torch.full((n, self.need_probs[i]), nan, dtype=torch.float32, device=self.device)
                 plan.launch(Xi, s, v, stream=st, **({"probs": pr} if pr is not None else {}))
                 t = eval_predicate_device(self.progs[i], Xa)[0]
-                ok = v.bool() & ~torch.isnan(s)
-                for seg, c, feat, pos in self.outs:
-                    if seg != i:
+                ok = v.bool() & ~torch.isnan(s)  # the segment predicted (its outputs exist)
+                idx = None
+                lab_ok = ok
+                if self.label_tabs[i] is not None:  # class index -> label (NaN: not a number)
+                    k = self.label_tabs[i].numel() - 1
+                    idx = torch.where(ok, s, torch.full_like(s, float(k))).long().clamp(0, k)
+                    s = self.label_tabs[i][idx]
+                    lab_ok = ok & ~torch.isnan(s)
+                mine = []
+                for seg, c, feat, pos, tab, ex in self.outs:  # the values, unmasked by the predicate
+                    if seg != i or ex is not None:
                         continue
-                    val = pr[:, pos] if feat == "probability" else s
-                    Xa[:, c] = torch.where(t & ok, val, torch.full_like(val, float("nan")))
+                    if feat == "probability":
+                        val = pr[:, pos]
+                    elif tab >= 0:
+                        val = self._tabs[tab][idx].float()
+                    elif pos == -2:
+                        val = torch.full_like(s, nan)
+                    else:
+                        val = s
+                    Xa[:, c] = torch.where(ok, val, torch.full_like(val, nan))
+                    mine.append(c)
+                ep = self.expr_progs[i]
+                if ep is not None:  # expression outputs see this segment's own outputs (document order)
+                    out = self._run_expr(ep, Xa, st)
+                    for j, c in enumerate(ep[4]):
+                        Xa[:, c] = out[:, j].to(Xa.dtype)
+                        mine.append(c)
+                if mine:  # rows the segment does not apply to do not see its outputs
+                    cols = torch.tensor(mine, dtype=torch.int64, device=self.device)
+                    Xa[:, cols] = torch.where(t[:, None], Xa[:, cols], torch.full_like(Xa[:, cols], nan))
                 best_s = torch.where(t, s.double(), best_s)  # the last applicable segment wins
-                best_v = torch.where(t, ok, best_v)
+                best_v = torch.where(t, lab_ok, best_v)
             if self.kind_ == "classification":
                 best_v = best_v & torch.isin(best_s.float(), self.final_labels)
             else:
                 best_v = best_v & torch.isfinite(best_s)
                 best_s, best_v = apply_target_torch(best_s, best_v, self.tgt)
-            out = torch.where(best_v, best_s, torch.full_like(best_s, float("nan")))
+            out = torch.where(best_v, best_s, torch.full_like(best_s, nan))
             for so, vo in ((score, valid), (score2, valid2)):
                 if so is not None and not isinstance(so, int):
                     so.copy_(out.to(so.dtype))
