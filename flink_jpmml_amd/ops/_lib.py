@@ -163,7 +163,7 @@ class SegArgs(ctypes.Structure):
                 ("method", c_int), ("classification", c_int), ("skip", c_int), ("tgt", c_int),
                 ("lo", ctypes.c_double), ("hi", ctypes.c_double), ("ta", ctypes.c_double), ("tb", ctypes.c_double),
                 ("dflt", ctypes.c_double), ("score", c_void_p), ("valid", c_void_p), ("score2", c_void_p),
-                ("valid2", c_void_p)]
+                ("valid2", c_void_p), ("remap_stride", c_int), ("pad", c_int)]
 
 
 class GroupedTreeArgs(ctypes.Structure):

@@ -13,15 +13,15 @@
 //     median of the probability vectors (classification), missingPredictionTreatment;
 //   * the regression Target stage (clip, rescale, castInteger, defaultValue) and the label table.
 //
-// One lane per row, every per-row array in registers / scratch (K, C <= 64).
+// One lane per row, every per-row array in registers / scratch: the <64, 64> instantiation for
+// K, C <= 64 segments / classes, the <256, 256> one (bitmask words, scratch arrays) up to 256.
 
 #include "common.h"
 
 namespace {
 
 constexpr int SEG_TB = 256;
-constexpr int SEG_MAXK = 64;
-constexpr int SEG_MAXC = 64;
+constexpr int SEG_WIDE = 256;  // segments / classes of the wide instantiation
 
 enum : int {
   SP_END = 0, SP_TRUE, SP_FALSE, SP_CMP, SP_ISMISS, SP_NOTMISS, SP_SET, SP_AND, SP_OR, SP_XOR, SP_SURR,
@@ -54,6 +54,7 @@ struct SegArgs {
   uint8_t* valid;
   float* score2;           // optional device mirrors
   uint8_t* valid2;
+  int remap_stride, pad;   // remap row length: (max classes of the instantiation) + 1
 };
 
 __device__ uint32_t seg_predicate(const SegArgs& a, int pc, const float* xrow) {
@@ -130,7 +131,7 @@ __device__ __forceinline__ double seg_target(const SegArgs& a, double v) {
 
 // numpy-style median of the first m values of w (sorted in place): mean of the two middle values
 __device__ double seg_median(double* w, int m) {
-  for (int i = 1; i < m; ++i) {  // insertion sort, m <= 64
+  for (int i = 1; i < m; ++i) {  // insertion sort, m <= 256
     const double x = w[i];
     int j = i - 1;
     while (j >= 0 && w[j] > x) {
@@ -143,30 +144,58 @@ __device__ double seg_median(double* w, int m) {
   return (w[(m - 1) / 2] + w[m / 2]) * 0.5;
 }
 
+template <int MK>
+struct SegMask {  // one bit per segment, MK / 64 words
+  uint64_t w[MK / 64];
+  __device__ __forceinline__ SegMask() {
+#pragma unroll
+    for (int i = 0; i < MK / 64; ++i) w[i] = 0ull;
+  }
+  __device__ __forceinline__ void set(int k) { w[k >> 6] |= 1ull << (k & 63); }
+  __device__ __forceinline__ bool get(int k) const { return (w[k >> 6] >> (k & 63)) & 1ull; }
+  __device__ __forceinline__ bool any() const {
+    uint64_t o = 0ull;
+#pragma unroll
+    for (int i = 0; i < MK / 64; ++i) o |= w[i];
+    return o != 0ull;
+  }
+  __device__ __forceinline__ int first() const {  // lowest set bit, -1 if none
+#pragma unroll
+    for (int i = 0; i < MK / 64; ++i)
+      if (w[i]) return 64 * i + __ffsll((unsigned long long)w[i]) - 1;
+    return -1;
+  }
+};
+
+template <int MK, int MC>
 __global__ __launch_bounds__(SEG_TB) void segment_reduce_kernel(SegArgs a) {
   const int row = blockIdx.x * SEG_TB + threadIdx.x;
   if (row >= a.n_rows) return;
   const size_t n = (size_t)a.n_rows;
   const float* xrow = a.X + (size_t)row * a.ldx;
   const int K = a.K;
-  uint64_t tmask = 0, okmask = 0;
+  const int RS = a.remap_stride;
+  SegMask<MK> tmask, okmask, use;
+  bool anymiss = false;
   for (int i = 0; i < K; ++i) {
-    if (seg_predicate(a, a.pc[i], xrow) == SV_T) tmask |= 1ull << i;
+    const bool t = seg_predicate(a, a.pc[i], xrow) == SV_T;
     const float s = a.S[i * n + row];
-    if (a.V[i * n + row] && s == s) okmask |= 1ull << i;
+    const bool okk = a.V[i * n + row] && s == s;
+    if (t) tmask.set(i);
+    if (okk) okmask.set(i);
+    if (t && okk) use.set(i);
+    anymiss = anymiss || (t && !okk);
   }
-  const uint64_t use = tmask & okmask;
-  const bool anymiss = (tmask & ~okmask) != 0;
   double out = __builtin_nan("");
   bool ok = false;
   const int m = a.method;
   if (m == SM_SELECT) {
-    const int f = tmask ? __ffsll((unsigned long long)tmask) - 1 : -1;
+    const int f = tmask.first();
     if (f >= 0) {
-      ok = (okmask >> f) & 1;
+      ok = okmask.get(f);
       const float s = a.S[f * n + row];
       if (a.classification) {
-        const int lab = s == s ? a.remap[f * (SEG_MAXC + 1) + (int)s] : -1;
+        const int lab = s == s ? a.remap[f * RS + (int)s] : -1;
         ok = ok && lab >= 0;
         out = lab >= 0 ? (double)a.table[lab] : __builtin_nan("");
         ok = ok && out == out;
@@ -183,12 +212,12 @@ __global__ __launch_bounds__(SEG_TB) void segment_reduce_kernel(SegArgs a) {
       ok = true;
     }
   } else if (!a.classification) {
-    double w[SEG_MAXK];
+    double w[MK];
     int cnt = 0;
     double acc = 0.0, wsum = 0.0;
     double best = m == SM_MAX ? -__builtin_inf() : __builtin_inf();
     for (int i = 0; i < K; ++i) {
-      if (!((use >> i) & 1)) continue;
+      if (!use.get(i)) continue;
       const double s = (double)a.S[i * n + row];
       ++cnt;
       if (m == SM_SUM || m == SM_AVG) acc += s;
@@ -205,11 +234,11 @@ __global__ __launch_bounds__(SEG_TB) void segment_reduce_kernel(SegArgs a) {
     else if (m == SM_MAX || m == SM_MIN) out = best;
     else if (m == SM_MEDIAN) out = seg_median(w, cnt);
     else {  // weightedMedian: first value (stable ascending order) whose cumulative weight reaches half
-      int idx[SEG_MAXK];
+      int idx[MK];
       int c2 = 0;
       double total = 0.0;
       for (int i = 0; i < K; ++i)
-        if ((use >> i) & 1) {
+        if (use.get(i)) {
           idx[c2++] = i;
           total += a.weights[i];
         }
@@ -241,24 +270,24 @@ __global__ __launch_bounds__(SEG_TB) void segment_reduce_kernel(SegArgs a) {
     }
   } else {
     const int C = a.C;
-    double acc[SEG_MAXC];
+    double acc[MC];
     for (int c = 0; c < C; ++c) acc[c] = 0.0;
     if (m == SM_VOTE || m == SM_WVOTE) {
       for (int i = 0; i < K; ++i) {
-        if (!((use >> i) & 1)) continue;
-        const int lab = a.remap[i * (SEG_MAXC + 1) + (int)a.S[i * n + row]];
+        if (!use.get(i)) continue;
+        const int lab = a.remap[i * RS + (int)a.S[i * n + row]];
         if (lab >= 0) acc[lab] += m == SM_WVOTE ? a.weights[i] : 1.0;
       }
     } else if (m == SM_PAVG || m == SM_PWAVG) {
       double wu = 0.0;
       for (int i = 0; i < K; ++i) {
-        if (!((use >> i) & 1)) continue;
+        if (!use.get(i)) continue;
         const double wi = m == SM_PWAVG ? a.weights[i] : 1.0;
         wu += wi;
         const int Ci = (int)(a.coff[i + 1] - a.coff[i]);
         const float* pr = a.P + a.coff[i] * n + (size_t)row * Ci;
         for (int j = 0; j < Ci; ++j) {
-          const int c = a.remap[i * (SEG_MAXC + 1) + j];
+          const int c = a.remap[i * RS + j];
           const float p = pr[j];
           if (c >= 0) acc[c] += (p == p ? (double)p : 0.0) * wi;
         }
@@ -266,11 +295,11 @@ __global__ __launch_bounds__(SEG_TB) void segment_reduce_kernel(SegArgs a) {
       for (int c = 0; c < C; ++c) acc[c] /= wu;
     } else if (m == SM_PMAX) {
       for (int i = 0; i < K; ++i) {
-        if (!((use >> i) & 1)) continue;
+        if (!use.get(i)) continue;
         const int Ci = (int)(a.coff[i + 1] - a.coff[i]);
         const float* pr = a.P + a.coff[i] * n + (size_t)row * Ci;
         for (int j = 0; j < Ci; ++j) {
-          const int c = a.remap[i * (SEG_MAXC + 1) + j];
+          const int c = a.remap[i * RS + j];
           const float p = pr[j];
           if (c >= 0) {
             const double v = p == p ? (double)p : 0.0;
@@ -280,14 +309,14 @@ __global__ __launch_bounds__(SEG_TB) void segment_reduce_kernel(SegArgs a) {
       }
     } else {  // SM_PMEDIAN: per class, the median over the using segments (NaN entries dropped)
       for (int c = 0; c < C; ++c) {
-        double w[SEG_MAXK];
+        double w[MK];
         int cnt = 0;
         for (int i = 0; i < K; ++i) {
-          if (!((use >> i) & 1)) continue;
+          if (!use.get(i)) continue;
           const int Ci = (int)(a.coff[i + 1] - a.coff[i]);
           const float* pr = a.P + a.coff[i] * n + (size_t)row * Ci;
           for (int j = 0; j < Ci; ++j)
-            if (a.remap[i * (SEG_MAXC + 1) + j] == c && pr[j] == pr[j]) w[cnt++] = (double)pr[j];
+            if (a.remap[i * RS + j] == c && pr[j] == pr[j]) w[cnt++] = (double)pr[j];
         }
         acc[c] = seg_median(w, cnt);
       }
@@ -301,7 +330,7 @@ __global__ __launch_bounds__(SEG_TB) void segment_reduce_kernel(SegArgs a) {
         lab = c;
       }
     }
-    ok = use != 0 && (a.skip || !anymiss);
+    ok = use.any() && (a.skip || !anymiss);
     out = (double)a.table[lab];
     ok = ok && out == out;
   }
@@ -316,10 +345,20 @@ __global__ __launch_bounds__(SEG_TB) void segment_reduce_kernel(SegArgs a) {
 
 PMML_API int pmml_segment_args_size() { return (int)sizeof(SegArgs); }
 
+// remap_stride selects the instantiation: 65 -> <64, 64> (K, C <= 64), 257 -> <256, 256>.
 PMML_API int pmml_segment_reduce(hipStream_t stream, const SegArgs* args) {
   const SegArgs& a = *args;
   if (a.n_rows <= 0) return 0;
-  if (a.K < 1 || a.K > SEG_MAXK || a.C > SEG_MAXC || a.method < SM_SELECT || a.method > SM_PMEDIAN) return -2;
-  hipLaunchKernelGGL(segment_reduce_kernel, dim3((a.n_rows + SEG_TB - 1) / SEG_TB), dim3(SEG_TB), 0, stream, a);
+  if (a.method < SM_SELECT || a.method > SM_PMEDIAN || a.K < 1) return -2;
+  const dim3 grid((a.n_rows + SEG_TB - 1) / SEG_TB);
+  if (a.remap_stride == 64 + 1) {
+    if (a.K > 64 || a.C > 64) return -2;
+    hipLaunchKernelGGL((segment_reduce_kernel<64, 64>), grid, dim3(SEG_TB), 0, stream, a);
+  } else if (a.remap_stride == SEG_WIDE + 1) {
+    if (a.K > SEG_WIDE || a.C > SEG_WIDE) return -2;
+    hipLaunchKernelGGL((segment_reduce_kernel<SEG_WIDE, SEG_WIDE>), grid, dim3(SEG_TB), 0, stream, a);
+  } else {
+    return -2;
+  }
   return hipGetLastError() == hipSuccess ? 0 : -7;
 }

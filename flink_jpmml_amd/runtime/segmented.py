@@ -212,7 +212,7 @@ _CMP = {"equal": 0, "notEqual": 1, "lessThan": 2, "lessOrEqual": 3, "greaterThan
 _METHOD_CODE = {"selectFirst": 0, "sum": 1, "average": 2, "weightedAverage": 3, "max": 4, "min": 5, "median": 6,
                 "weightedMedian": 7, "majorityVote": 8, "weightedMajorityVote": 9}
 _PROB_CODE = {"average": 10, "weightedAverage": 11, "max": 12, "median": 13}
-SEG_MAXK = SEG_MAXC = 64  # ops/csrc/segment.hip
+SEG_MAXK = SEG_MAXC = 256  # ops/csrc/segment.hip: <64, 64> instantiation up to 64, <256, 256> beyond
 SEG_STACK = 32  # seg_predicate's postfix stack: 2-bit entries of one uint64 (ops/csrc/segment.hip)
 MULTI_MAX_TREES = 64  # tree segments this small share one pointer-layout launch (tree_pointer_multi_kernel)
 
@@ -388,14 +388,16 @@ class SegmentedPlan(DevicePlan):
             insns, pool, starts = predicate_programs(self.progs)
         except NotLowerable:
             return
-        rm = np.full((max(1, self.n_subs), SEG_MAXC + 1), -1, dtype=np.int32)
+        widest = max([self.n_subs, len(self.categories or [])] + [len(r) - 1 for r in (self.remap_lists or [])])
+        stride = (64 if widest <= 64 else SEG_MAXC) + 1  # the kernel instantiation (remap row length)
+        rm = np.full((max(1, self.n_subs), stride), -1, dtype=np.int32)
         for i, r in enumerate(self.remap_lists or []):
             rm[i, : len(r) - 1] = r[:-1]
         widths = [len(r) - 1 for r in self.remap_lists] if probs else [0] * self.n_subs
         coff = np.zeros(self.n_subs + 1, dtype=np.int64)
         np.cumsum(widths, out=coff[1:])
         dev = self.device
-        self._red = dict(code=code, probs=probs, widths=widths,
+        self._red = dict(code=code, probs=probs, widths=widths, stride=stride,
                          prog=torch.from_numpy(insns.reshape(-1)).to(dev), pool=torch.from_numpy(pool).to(dev),
                          pc=torch.from_numpy(starts).to(dev),
                          weights=torch.tensor(self.weights, dtype=torch.float64, device=dev),
@@ -523,6 +525,7 @@ class SegmentedPlan(DevicePlan):
                 a.ta = 1.0
             a.score, a.valid = _addr(score), _addr(valid)
             a.score2, a.valid2 = _addr(score2), _addr(valid2)
+            a.remap_stride = int(r["stride"])
             check(self.lib.pmml_segment_reduce(stream_handle(st), ctypes.byref(a)), "segment reduce kernel")
 
     def _select(self, S, ok, T):
