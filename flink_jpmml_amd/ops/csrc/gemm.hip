@@ -57,7 +57,10 @@ struct GemmArgs {
                           // tile, 7 force the phase-interleaved kernel, 8 direct [row][unit] stores instead of
                           // store_hidden_t, 9 one K = 64 tile per workgroup instead of gemm_k64p_kernel,
                           // 10 gemm_k64p_kernel with store_hidden_t instead of the row-segment stores,
-                          // 11 the same for gemm8_kernel<false, true>
+                          // 11 the same for gemm8_kernel<false, true>, 12 one tile per workgroup
+                          // (gemm8_kernel) instead of the persistent gemm8p_kernel, 13 gemm8p_kernel
+                          // without its epilogue stores (timing only: the layer output is not written),
+                          // 14 gemm_k64p_kernel with ordinary instead of non-temporal stores
   const uint8_t* row_ok;  // [rows] input-stage validity (output layer)
   Epilogue epi;           // output layer decode (affine + Target, or label table)
   float* score;
@@ -324,7 +327,9 @@ __device__ __forceinline__ void store_hidden_t(const GemmArgs& a, const f32x16 (
 // the staging writes and the segment reads are conflict free), and each global store instruction
 // covers 8 whole 128-byte row segments (8 lines). Same store count (4 per tile pair and 32 rows),
 // same values; only the wave's own lanes touch its scratch, so no barrier.
-template <int ACT, int TM, int TN, bool LB = true>
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+// NTS: non-temporal stores (the nt bit: streamed past the caches' retention; gemm_k64p_kernel)
+template <int ACT, int TM, int TN, bool LB = true, bool NTS = false>
 __device__ __forceinline__ void store_hidden_seg(const GemmArgs& a, const f32x16 (&acc)[TM][TN], int row0, int col0,
                                                  int wm, int wn, int lane, const float* bl, unsigned char* ws) {
   static_assert(TN % 2 == 0, "tile pairs");
@@ -385,8 +390,13 @@ __device__ __forceinline__ void store_hidden_seg(const GemmArgs& a, const f32x16
         const uint4 v0 = *reinterpret_cast<const uint4*>(ws + rr * 128 + ((k ^ (rr & 7)) << 4));
         const uint4 v1 = *reinterpret_cast<const uint4*>(ws + (rr + 8) * 128 + ((k ^ ((rr + 8) & 7)) << 4));
         __bf16* d0 = static_cast<__bf16*>(a.C) + (rb + 16 * ph + rr) * a.ldc + u0 + 8 * k;
-        *reinterpret_cast<uint4*>(d0) = v0;
-        *reinterpret_cast<uint4*>(d0 + 8 * (size_t)a.ldc) = v1;
+        if constexpr (NTS) {
+          __builtin_nontemporal_store(u32x4{v0.x, v0.y, v0.z, v0.w}, reinterpret_cast<u32x4*>(d0));
+          __builtin_nontemporal_store(u32x4{v1.x, v1.y, v1.z, v1.w}, reinterpret_cast<u32x4*>(d0 + 8 * (size_t)a.ldc));
+        } else {
+          *reinterpret_cast<uint4*>(d0) = v0;
+          *reinterpret_cast<uint4*>(d0 + 8 * (size_t)a.ldc) = v1;
+        }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -395,16 +405,16 @@ __device__ __forceinline__ void store_hidden_seg(const GemmArgs& a, const f32x16
   }
 }
 
-template <int TM, int TN, bool LB = true>
+template <int TM, int TN, bool LB = true, bool NTS = false>
 __device__ __forceinline__ void store_hidden_seg_any(const GemmArgs& a, const f32x16 (&acc)[TM][TN], int row0,
                                                      int col0, int wm, int wn, int lane, const float* bl,
                                                      unsigned char* ws) {
   switch (a.act) {
-    case A_IDENTITY: store_hidden_seg<A_IDENTITY, TM, TN, LB>(a, acc, row0, col0, wm, wn, lane, bl, ws); break;
-    case A_RELU: store_hidden_seg<A_RELU, TM, TN, LB>(a, acc, row0, col0, wm, wn, lane, bl, ws); break;
-    case A_LOGISTIC: store_hidden_seg<A_LOGISTIC, TM, TN, LB>(a, acc, row0, col0, wm, wn, lane, bl, ws); break;
-    case A_TANH: store_hidden_seg<A_TANH, TM, TN, LB>(a, acc, row0, col0, wm, wn, lane, bl, ws); break;
-    default: store_hidden_seg<-1, TM, TN, LB>(a, acc, row0, col0, wm, wn, lane, bl, ws); break;
+    case A_IDENTITY: store_hidden_seg<A_IDENTITY, TM, TN, LB, NTS>(a, acc, row0, col0, wm, wn, lane, bl, ws); break;
+    case A_RELU: store_hidden_seg<A_RELU, TM, TN, LB, NTS>(a, acc, row0, col0, wm, wn, lane, bl, ws); break;
+    case A_LOGISTIC: store_hidden_seg<A_LOGISTIC, TM, TN, LB, NTS>(a, acc, row0, col0, wm, wn, lane, bl, ws); break;
+    case A_TANH: store_hidden_seg<A_TANH, TM, TN, LB, NTS>(a, acc, row0, col0, wm, wn, lane, bl, ws); break;
+    default: store_hidden_seg<-1, TM, TN, LB, NTS>(a, acc, row0, col0, wm, wn, lane, bl, ws); break;
   }
 }
 
@@ -793,6 +803,32 @@ __device__ __forceinline__ void stage_half(const unsigned char* src, size_t ldb,
   }
 }
 
+// stage_half as inline-asm LDS-DMA in the SADDR form: 64-bit wave-uniform base (the tile's first
+// row + the slice's byte column) in SGPRs, a 32-bit per-lane offset in one VGPR, the LDS
+// destination in M0. For the persistent kernel, whose register budget is exhausted: hipcc keeps
+// the builtin's per-lane 64-bit addresses (16 VGPRs) loop-invariant and spilled them, with a
+// vmcnt(0) per reload in the loop. Invisible to hipcc's wait-count pass, which is what the kernel
+// wants: every wait on these loads is an explicit counted vmcnt already, and hipcc no longer
+// drains them before the epilogue's LDS accesses. ldb * 256 rows must fit 32 bits (launcher).
+__device__ __forceinline__ void glds16s(const unsigned char* sbase, uint32_t voff, const unsigned char* lds) {
+  const uint32_t m = __builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uintptr_t>(lds));
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(m), "v"(voff), "s"(sbase)
+               : "memory", "m0");
+}
+template <bool IS_A>
+__device__ __forceinline__ void stage_half_s(const unsigned char* src, uint32_t ldb, unsigned char* slot, int half,
+                                             int wave, int lane) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int q = wave * 2 + i;
+    const int p = q * 64 + lane;
+    const int j = p >> 3;
+    const int c = (p & 7) ^ swz(j);
+    const int r = IS_A ? ((j >> 6) * 128 + half * 64 + (j & 63)) : ((j >> 5) * 64 + half * 32 + (j & 31));
+    glds16s(src, (uint32_t)r * ldb + 16u * (uint32_t)c, slot + q * 1024);
+  }
+}
+
 __device__ __forceinline__ void raw_barrier() {
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("" ::: "memory");
@@ -848,24 +884,33 @@ struct HeadFuse {
 // row group leave their Z in LDS and the block writes the in-order sum, its [256, n_out] partial,
 // to hf.part[column tile] (deterministic); nn_head_decode_kernel sums the column tiles in order
 // and decodes.
-template <int ACT>
+// LW (the persistent kernel): the output-layer weights' first n_out rows come from an LDS copy
+// whl [n_out][Mp] (rows >= n_out are zero in hf.wh) and the partial-sum exchange uses a raw barrier
+// — no global load and no fence in the epilogue, so nothing makes hipcc wait for vector memory
+// (the next tile's LDS-DMA loads are in flight).
+template <int ACT, bool LW = false>
 __device__ __forceinline__ void head_partial(const GemmArgs& a, const HeadFuse& hf, const f32x16 (&acc)[4][2], int row0,
-                                             int col0, int wr, int wc, int lane, int tid, unsigned char* smem) {
+                                             int col0, int wr, int wc, int lane, int tid, unsigned char* smem,
+                                             const float* btile, const __bf16* whl = nullptr) {
   const int h = lane >> 5, l32 = lane & 31;
   const int no = hf.n_out;
-  float* zp = reinterpret_cast<float*>(smem);  // [4 column waves][BM][n_out] (the staging buffers are drained)
+  float* zp = reinterpret_cast<float*>(smem);  // [4 column waves][BM][n_out] (staging buffers drained / scratch)
   bf16x8 wf[2][2];
 #pragma unroll
   for (int j = 0; j < 2; ++j)
 #pragma unroll
     for (int s = 0; s < 2; ++s)
-      wf[j][s] = *reinterpret_cast<const bf16x8*>(hf.wh + (size_t)l32 * hf.ldw + col0 + wc * 64 + 32 * j + 16 * s + 8 * h);
+      if constexpr (LW)
+        wf[j][s] = l32 < no ? *reinterpret_cast<const bf16x8*>(whl + l32 * a.Mp + col0 + wc * 64 + 32 * j + 16 * s + 8 * h)
+                            : bf16x8{};
+      else
+        wf[j][s] = *reinterpret_cast<const bf16x8*>(hf.wh + (size_t)l32 * hf.ldw + col0 + wc * 64 + 32 * j + 16 * s + 8 * h);
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     f32x16 z = f32x16{};
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const float* bias = a.bias + col0 + wc * 64 + 32 * j + 4 * h;
+      const float* bias = btile + wc * 64 + 32 * j + 4 * h;  // btile: the column tile's biases
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         bf16x8 hb;
@@ -885,7 +930,12 @@ __device__ __forceinline__ void head_partial(const GemmArgs& a, const HeadFuse& 
       if (o < no) dst[o] = z[r];
     }
   }
-  __syncthreads();
+  if constexpr (LW) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    raw_barrier();
+  } else {
+    __syncthreads();
+  }
   float* out = hf.part + ((size_t)(col0 >> 8) * a.rows_p + row0) * no;
   const size_t plane = (size_t)BM * no;
   for (int e = tid; e < BM * no; e += NT) out[e] = ((zp[e] + zp[plane + e]) + zp[2 * plane + e]) + zp[3 * plane + e];
@@ -977,11 +1027,11 @@ __global__ __launch_bounds__(NT, 1) void gemm8_kernel(GemmArgs a, HeadFuse hf) {
   if (wr == 0) raw_barrier();  // balance group 1's extra barrier
   if constexpr (HEADF) {
     switch (a.act) {
-      case A_IDENTITY: head_partial<A_IDENTITY>(a, hf, acc, row0, col0, wr, wc, lane, tid, smem); break;
-      case A_RELU: head_partial<A_RELU>(a, hf, acc, row0, col0, wr, wc, lane, tid, smem); break;
-      case A_LOGISTIC: head_partial<A_LOGISTIC>(a, hf, acc, row0, col0, wr, wc, lane, tid, smem); break;
-      case A_TANH: head_partial<A_TANH>(a, hf, acc, row0, col0, wr, wc, lane, tid, smem); break;
-      default: head_partial<-1>(a, hf, acc, row0, col0, wr, wc, lane, tid, smem); break;
+      case A_IDENTITY: head_partial<A_IDENTITY>(a, hf, acc, row0, col0, wr, wc, lane, tid, smem, a.bias + col0); break;
+      case A_RELU: head_partial<A_RELU>(a, hf, acc, row0, col0, wr, wc, lane, tid, smem, a.bias + col0); break;
+      case A_LOGISTIC: head_partial<A_LOGISTIC>(a, hf, acc, row0, col0, wr, wc, lane, tid, smem, a.bias + col0); break;
+      case A_TANH: head_partial<A_TANH>(a, hf, acc, row0, col0, wr, wc, lane, tid, smem, a.bias + col0); break;
+      default: head_partial<-1>(a, hf, acc, row0, col0, wr, wc, lane, tid, smem, a.bias + col0); break;
     }
     return;
   } else if constexpr (TST) {
@@ -1008,6 +1058,196 @@ __global__ __launch_bounds__(NT, 1) void gemm8_kernel(GemmArgs a, HeadFuse hf) {
   }
 }
 
+// Persistent phase-interleaved hidden layer (gemm8p_kernel; bf16, 512 <= K <= 1024: the default
+// of the transposed-store path and of the fused output layer; flag bit 12 selects gemm8_kernel).
+// gemm8_kernel runs ONE 256 x 256 tile per workgroup; at one workgroup per CU the matrix cores
+// idle while a fresh workgroup fills its first slices and while the last one drains its
+// epilogue. Here a grid of one workgroup per CU walks a list of tiles and the slice stream of
+// gemm8_kernel continues across tile boundaries: global slice g = j * KT + kt of the workgroup's
+// j-th tile, buffer g & 1, the same four phases, restaging points and counted vmcnt(6) — the
+// first slices of tile j + 1 are staged by the last phases of tile j, and tile j's epilogue runs
+// between two phases while they are in flight:
+//  * hidden layer: bias from LDS, activation, 128-byte row-segment stores through the wave's own
+//    scratch (store_hidden_seg), no barrier. The stores are older than the next slices' loads, so
+//    the counted wait of the next tile's first slice retires them too (vector-memory operations
+//    retire in issue order);
+//  * fused output layer (HEADF, n_out <= 4): head_partial with the biases from LDS and its
+//    partial sums in the scratch region, the two wave groups re-aligned around its barrier.
+// The LDS-DMA is issued as inline asm (stage_half_s): hipcc kept the builtin's 64-bit per-lane
+// addresses live and spilled them (a vmcnt(0) per reload inside the loop) and drained the loads
+// in flight before the epilogue's first LDS access; neither happens to loads it cannot see.
+// LDS: the 128 KiB of staging slots, 16 KiB of wave scratch / head partials, the Mp biases.
+// Tile list: the XCD-contiguous order of gemm8_kernel — XCD x (blockIdx & 7) owns tiles
+// [x T / 8, (x + 1) T / 8) and its G / 8 workgroups take every (G / 8)-th of them, so the column
+// tiles of a row block run together on one XCD and its A rows come from HBM once.
+// Measured (profiles/r5n, 1M rows x 1024 x 1024, one process, interleaved): 2.04 vs 2.23 ms for
+// gemm8_kernel<false, true>; without any stores (bit 13, timing only) 1.85 ms. A K = 4096 layer is
+// slower persistent (profiles/r5m: 7.71 vs 7.37 ms, and 7.64 without stores), hence the K <= 1024
+// routing. Measured and dropped (profiles/r5m, r5n): staging the next tile's A1 before the
+// epilogue with the stores left in flight one slice longer (+9 %), half of the next slice's A0
+// fragments read in the otherwise read-free P4 (12/4/8/0 -> 8/4/8/4 reads per phase: +8 %),
+// XCDs 4-7 started half a tile late to split the chip-wide store burst (no change).
+constexpr int P8_SCR = 8 * 2048;
+constexpr int P8_MAX_MP = (160 * 1024 - 8 * HALF_B - P8_SCR) / 4;
+constexpr int P8_HEAD_MAX_OUT = P8_SCR / (4 * BM * 4);  // head partials [4 column waves][BM][n_out] fp32
+constexpr int P8_HEAD_MAX_MP = (160 * 1024 - 8 * HALF_B - P8_SCR) / (4 + 2 * P8_HEAD_MAX_OUT);  // biases + whl
+
+// NOSTORE (flag bit 13, timing only): the hidden epilogue writes nothing — the cost of the stores.
+// (Non-temporal stores, which take 10 % off gemm_k64p_kernel, measured no change here: profiles/r5p.)
+template <bool HEADF, bool NOSTORE>
+__global__ __launch_bounds__(NT, 1) void gemm8p_kernel(GemmArgs a, HeadFuse hf) {
+  constexpr int TM = 4, TN = 2;
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, l32 = lane & 31;
+  const int n_ct = a.Mp / 256;
+  const int total = (a.rows_p / BM) * n_ct;
+  const int G = gridDim.x;
+  int base, step, n_my;
+  if ((total & 7) == 0 && (G & 7) == 0) {
+    const int T8 = total >> 3, G8 = G >> 3, s = blockIdx.x >> 3;
+    base = (blockIdx.x & 7) * T8 + s;
+    step = G8;
+    n_my = s < T8 ? (T8 - s + G8 - 1) / G8 : 0;
+  } else {
+    base = blockIdx.x;
+    step = G;
+    n_my = (int)blockIdx.x < total ? (total - (int)blockIdx.x + G - 1) / G : 0;
+  }
+  if (n_my <= 0) return;  // workgroup-uniform, before any barrier
+  unsigned char* scr = smem + 8 * HALF_B;  // wave scratch (hidden) / head partials (HEADF)
+  float* bl = reinterpret_cast<float*>(smem + 8 * HALF_B + P8_SCR);
+  __bf16* whl = reinterpret_cast<__bf16*>(bl + a.Mp);  // HEADF: [n_out][Mp] output-layer weights
+  for (int u = tid; u < a.Mp; u += NT) bl[u] = a.bias[u];
+  if constexpr (HEADF)
+    for (int e = tid; e < hf.n_out * a.Mp; e += NT) whl[e] = hf.wh[(size_t)(e / a.Mp) * hf.ldw + e % a.Mp];
+  __syncthreads();
+
+  const int wr = wave >> 2, wc = wave & 3;
+  const size_t lda_b = (size_t)a.lda * 2, ldw_b = (size_t)a.ldw * 2;
+  const uint32_t lda32 = (uint32_t)lda_b, ldw32 = (uint32_t)ldw_b;
+  const unsigned char* A0p = static_cast<const unsigned char*>(a.A);
+  const unsigned char* B0p = static_cast<const unsigned char*>(a.Wt);
+  const int KT = a.K / BK;
+  const int NS = n_my * KT;
+  // the sources of slices g + 1 (s1) and g + 2 (s2): tile pointers + slice offset
+  struct Src {
+    const unsigned char* A;
+    const unsigned char* B;
+    int j, k;
+  };
+  auto at_tile = [&](int j, int k) -> Src {
+    const int t = base + j * step;
+    return Src{A0p + (size_t)((t / n_ct) * BM) * lda_b, B0p + (size_t)((t % n_ct) * 256) * ldw_b, j, k};
+  };
+  auto advance = [&](const Src& s) -> Src {
+    return s.k + 1 < KT ? Src{s.A, s.B, s.j, s.k + 1} : (s.j + 1 < n_my ? at_tile(s.j + 1, 0) : Src{s.A, s.B, s.j + 1, 0});
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x16{};
+
+#define SLOT(b, s) (smem + (b) * 4 * HALF_B + (s) * HALF_B)
+  const Src s0 = at_tile(0, 0);
+  Src s1 = advance(s0);
+  Src s2 = advance(s1);
+  stage_half_s<true>(s0.A, lda32, SLOT(0, 0), 0, wave, lane);
+  stage_half_s<false>(s0.B, ldw32, SLOT(0, 2), 0, wave, lane);
+  stage_half_s<false>(s0.B, ldw32, SLOT(0, 3), 1, wave, lane);
+  stage_half_s<true>(s0.A, lda32, SLOT(0, 1), 1, wave, lane);
+  if (NS > 1) {
+    const size_t kb = (size_t)s1.k * SLICE_B;
+    stage_half_s<true>(s1.A + kb, lda32, SLOT(1, 0), 0, wave, lane);
+    stage_half_s<false>(s1.B + kb, ldw32, SLOT(1, 2), 0, wave, lane);
+    stage_half_s<false>(s1.B + kb, ldw32, SLOT(1, 3), 1, wave, lane);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  raw_barrier();
+  if (wr == 1) raw_barrier();  // group 1 runs one barrier behind group 0
+
+  const int ra = wr * 64 + l32, rb = wc * 32 + l32;
+  int row0 = (base / n_ct) * BM, col0 = (base % n_ct) * 256;
+  for (int g = 0, kt = 0, j = 0; g < NS; ++g) {
+    const int b = g & 1;
+    const bool n1 = g + 1 < NS, n2 = g + 2 < NS;
+    const size_t k1 = (size_t)s1.k * SLICE_B, k2 = (size_t)s2.k * SLICE_B;
+    bf16x8 a0[2][4], a1[2][4], b0[4], b1[4];
+    // P1: A0 x B0
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) a0[i][ks] = frag(SLOT(b, 0), ra + 32 * i, 2 * ks + h);
+      b0[ks] = frag(SLOT(b, 2), rb, 2 * ks + h);
+    }
+    if (n1) stage_half_s<true>(s1.A + k1, lda32, SLOT(b ^ 1, 1), 1, wave, lane);
+    mma_begin();
+    mma_quad<true>(acc[0][0], acc[1][0], a0, b0);
+    mma_end();
+    // P2: A0 x B1
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) b1[ks] = frag(SLOT(b, 3), rb, 2 * ks + h);
+    if (n2) stage_half_s<true>(s2.A + k2, lda32, SLOT(b, 0), 0, wave, lane);
+    mma_begin();
+    mma_quad<true>(acc[0][1], acc[1][1], a0, b1);
+    mma_end();
+    // P3: A1 x B1
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) a1[i][ks] = frag(SLOT(b, 1), ra + 32 * i, 2 * ks + h);
+    if (n2) stage_half_s<false>(s2.B + k2, ldw32, SLOT(b, 2), 0, wave, lane);
+    mma_begin();
+    mma_quad<true>(acc[2][1], acc[3][1], a1, b1);
+    mma_end();
+    // P4: A1 x B0; slice g + 1 retired (three half-tiles of g + 2 may stay in flight — and, on a
+    // tile's first slice, the previous epilogue's stores, which are older, retired with it)
+    if (n2) stage_half_s<false>(s2.B + k2, ldw32, SLOT(b, 3), 1, wave, lane);
+    if (n2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if (n1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    mma_begin();
+    mma_quad<true>(acc[2][0], acc[3][0], a1, b0);
+    mma_end();
+    s1 = s2;
+    s2 = advance(s2);
+    if (++kt == KT) {  // tile j done: epilogue between two phases, the next tile's slices in flight
+      if constexpr (HEADF) {
+        if (wr == 0) raw_barrier();  // align the groups for head_partial's barrier
+        switch (a.act) {
+          case A_IDENTITY: head_partial<A_IDENTITY, true>(a, hf, acc, row0, col0, wr, wc, lane, tid, scr, bl + col0, whl); break;
+          case A_RELU: head_partial<A_RELU, true>(a, hf, acc, row0, col0, wr, wc, lane, tid, scr, bl + col0, whl); break;
+          case A_LOGISTIC: head_partial<A_LOGISTIC, true>(a, hf, acc, row0, col0, wr, wc, lane, tid, scr, bl + col0, whl); break;
+          case A_TANH: head_partial<A_TANH, true>(a, hf, acc, row0, col0, wr, wc, lane, tid, scr, bl + col0, whl); break;
+          default: head_partial<-1, true>(a, hf, acc, row0, col0, wr, wc, lane, tid, scr, bl + col0, whl); break;
+        }
+        if (wr == 1) raw_barrier();  // group 1 one barrier behind again
+      } else if constexpr (NOSTORE) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) asm volatile("" ::"v"(acc[i][0]), "v"(acc[i][1]));
+      } else {
+        store_hidden_seg_any<TM, TN, true>(a, acc, row0, col0, wr, wc, lane, bl + col0, scr + wave * 2048);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int q = 0; q < TN; ++q) acc[i][q] = f32x16{};
+      kt = 0;
+      if (++j < n_my) {
+        const int t = base + j * step;
+        row0 = (t / n_ct) * BM;
+        col0 = (t % n_ct) * 256;
+      }
+    }
+  }
+#undef SLOT
+  if (wr == 0) raw_barrier();  // balance group 1's extra barrier
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // Persistent K = 64 hidden layer (bf16, the input stage separate): a workgroup owns one 256-unit
 // column tile — its weight slice (32 KiB) and biases staged in LDS ONCE — and walks row tiles of
 // 128 rows, the next tile's A slice (16 KiB, LDS-DMA) in flight while the current one multiplies
@@ -1018,7 +1258,7 @@ __global__ __launch_bounds__(NT, 1) void gemm8_kernel(GemmArgs a, HeadFuse hf) {
 // and the n_ct column-tile owners of a row group share it, so a row tile's A is fetched from HBM
 // once and hit in that XCD's L2 by the other column tiles. Two workgroups per CU (65 KiB of LDS each).
 constexpr int K64P_STORES = 16;  // store_hidden_t<2, 4>: 2 x 4 tiles x 2 stores per lane
-template <bool SEG>
+template <bool SEG, bool NTS = false>
 __global__ __launch_bounds__(K64_NT, 2) void gemm_k64p_kernel(GemmArgs a, int rg) {
   constexpr int TM = 2, TN = 4;
   constexpr int A_B = K64_BM * SLICE_B;
@@ -1068,7 +1308,7 @@ __global__ __launch_bounds__(K64_NT, 2) void gemm_k64p_kernel(GemmArgs a, int rg
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
     }
-    if constexpr (SEG) store_hidden_seg_any<TM, TN>(a, acc, rt * K64_BM, col0, wm, wn, lane, bl, ws);
+    if constexpr (SEG) store_hidden_seg_any<TM, TN, true, NTS>(a, acc, rt * K64_BM, col0, wm, wn, lane, bl, ws);
     else store_hidden_t_any<TM, TN, true>(a, acc, rt * K64_BM, col0, wm, wn, lane, bl);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1087,10 +1327,16 @@ int launch_k64p(hipStream_t stream, const GemmArgs& a) {
   // 0.438 ms for 1M rows x 1024 units, TA busy 78 -> 52 %, profiles/r5f); bit 10: store_hidden_t
   const bool seg = !((a.f32 >> 10) & 1);
   const size_t lds = (size_t)(256 + 2 * K64_BM) * SLICE_B + 256 * 4 + (seg ? 4 * 2048 : 0);
-  const void* kp = seg ? reinterpret_cast<const void*>(&gemm_k64p_kernel<true>)
+  // non-temporal row-segment stores (the layer streams 2 GB of output per 1M rows and reads
+  // little): 0.435 -> 0.391 ms, profiles/r5p; bit 14: ordinary stores
+  const bool nts = seg && !((a.f32 >> 14) & 1);
+  const void* kp = nts ? reinterpret_cast<const void*>(&gemm_k64p_kernel<true, true>)
+                 : seg ? reinterpret_cast<const void*>(&gemm_k64p_kernel<true>)
                        : reinterpret_cast<const void*>(&gemm_k64p_kernel<false>);
   if (hipFuncSetAttribute(kp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return -5;
-  if (seg)
+  if (nts)
+    hipLaunchKernelGGL((gemm_k64p_kernel<true, true>), dim3(8 * n_ct * rg), dim3(K64_NT), lds, stream, a, rg);
+  else if (seg)
     hipLaunchKernelGGL(gemm_k64p_kernel<true>, dim3(8 * n_ct * rg), dim3(K64_NT), lds, stream, a, rg);
   else
     hipLaunchKernelGGL(gemm_k64p_kernel<false>, dim3(8 * n_ct * rg), dim3(K64_NT), lds, stream, a, rg);
@@ -1105,6 +1351,38 @@ int launch8(hipStream_t stream, const GemmArgs& a, const HeadFuse& hf) {
     return -5;
   hipLaunchKernelGGL((gemm8_kernel<HEADF, TST>), dim3((a.rows_p / BM) * (a.Mp / 256)), dim3(NT), lds, stream, a, hf);
   return 0;
+}
+
+int cu_count() {
+  static int n_cu = 0;
+  if (n_cu == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
+      n_cu = 256;
+  }
+  return n_cu;
+}
+
+template <bool HEADF>
+int launch8p(hipStream_t stream, const GemmArgs& a, const HeadFuse& hf) {
+  const size_t lds = 8 * (size_t)HALF_B + P8_SCR + 4 * (size_t)a.Mp + (HEADF ? 2 * (size_t)hf.n_out * a.Mp : 0);
+  const bool nostore = !HEADF && ((a.f32 >> 13) & 1);
+  const void* kp = HEADF ? reinterpret_cast<const void*>(&gemm8p_kernel<true, false>)
+                 : nostore ? reinterpret_cast<const void*>(&gemm8p_kernel<false, true>)
+                           : reinterpret_cast<const void*>(&gemm8p_kernel<false, false>);
+  if (hipFuncSetAttribute(kp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return -5;
+  const int total = (a.rows_p / BM) * (a.Mp / 256);
+  const int grid = std::min(total, cu_count());
+  if (HEADF) hipLaunchKernelGGL((gemm8p_kernel<true, false>), dim3(grid), dim3(NT), lds, stream, a, hf);
+  else if (nostore) hipLaunchKernelGGL((gemm8p_kernel<false, true>), dim3(grid), dim3(NT), lds, stream, a, hf);
+  else hipLaunchKernelGGL((gemm8p_kernel<false, false>), dim3(grid), dim3(NT), lds, stream, a, hf);
+  return 0;
+}
+
+// whether the persistent kernel takes a layer (a: the hidden layer's args; flag bit 12 opts out)
+bool use8p(const GemmArgs& a) {
+  return !((a.f32 >> 12) & 1) && a.Mp <= P8_MAX_MP && a.K <= 1024 && (size_t)a.lda * 2 * BM < (1ull << 31) &&
+         (size_t)a.ldw * 2 * 256 < (1ull << 31);
 }
 
 // The fused output layer's second half: one thread per row sums the column tiles' partials in
@@ -1162,7 +1440,7 @@ PMML_API int pmml_gemm_launch(hipStream_t stream, const GemmArgs* args, int head
   const GemmArgs a = *args;
   if (a.rows <= 0) return 0;
   const int BN = head ? 32 : 256;
-  if (a.f32 & ~0xFE1) return -4;
+  if (a.f32 & ~0x7FE1) return -4;
   // bf16 hidden layers with K >= 512 run the phase-interleaved kernel (profiles/r3ao: 2048 x 2048
   // 8.73 -> 8.36 ms, 1024 x 1024 2.62 -> 2.48 ms over 1M rows); below that the layer is bound by
   // its output writes and the 2-buffer loop is faster (K = 64: 0.83 vs 0.92 ms). Bit 7 forces it.
@@ -1189,9 +1467,14 @@ PMML_API int pmml_gemm_launch(hipStream_t stream, const GemmArgs* args, int head
     }
     return hipGetLastError() == hipSuccess ? 0 : -7;
   }
+  // persistent tile walk (gemm8p_kernel) for the transposed-store phase-interleaved layers with the
+  // row-segment stores and K <= 1024, unless bit 12 (one tile per workgroup) or bit 11
+  // (store_hidden_t) is set
+  const bool p8 = ph8 && tst && !head && !((a.f32 >> 11) & 1) && (use8p(a) || ((a.f32 >> 13) & 1));
   const int rc = f32 ? (head ? launch<32, true, true>(stream, a) : launch<256, false, true>(stream, a))
                      : (head ? launch<32, true, false>(stream, a)
-                             : (ph8 ? (tst ? launch8<false, true>(stream, a, HeadFuse{}) : launch8<false, false>(stream, a, HeadFuse{}))
+                             : (p8 ? launch8p<false>(stream, a, HeadFuse{})
+                                   : ph8 ? (tst ? launch8<false, true>(stream, a, HeadFuse{}) : launch8<false, false>(stream, a, HeadFuse{}))
                                    : (tst ? launch<256, false, false, true>(stream, a) : launch<256, false, false>(stream, a))));
   if (rc) return rc;
   return hipGetLastError() == hipSuccess ? 0 : -7;
@@ -1213,7 +1496,8 @@ PMML_API int pmml_gemm_fused_head_launch(hipStream_t stream, const GemmArgs* hid
   if (o.n_out < 1 || o.n_out > 32 || o.K != a.Mp || o.rows != a.rows || o.rows_p != a.rows_p) return -4;
   if (!o.row_ok || !o.score || !o.valid || !part || !wh_perm || (reinterpret_cast<uintptr_t>(wh_perm) & 15)) return -4;
   HeadFuse hf{static_cast<const __bf16*>(wh_perm), part, a.Mp, o.n_out};
-  int rc = launch8<true, false>(stream, a, hf);
+  const bool p8 = use8p(a) && o.n_out <= P8_HEAD_MAX_OUT && a.Mp <= P8_HEAD_MAX_MP;
+  int rc = p8 ? launch8p<true>(stream, a, hf) : launch8<true, false>(stream, a, hf);
   if (rc) return rc;
   hipLaunchKernelGGL(nn_head_decode_kernel, dim3((a.rows + 255) / 256), dim3(256), 0, stream, o, part, a.Mp / 256);
   return hipGetLastError() == hipSuccess ? 0 : -7;

@@ -1,0 +1,12 @@
+set -o pipefail
+# r5p: non-temporal row-segment stores (bit 14) on gemm8p / k64p: tests + interleaved A/B
+O=gpurun_out/r5p
+mkdir -p $O
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+timeout -k 10 300 python -u -m pytest tests/test_wide_mlp.py -m gpu -k "persistent" -x -q --timeout 200 --timeout-method thread -rf > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
+tail -2 $O/pytest.log
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+HIDDEN=1024,1024,1024,1024 FLAGS=0x1000,0,0x4000,0x5000 ROUNDS=5 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/ab -o k -- python3 scripts/gemm8p_ab.py > $O/ab.log 2>&1 || { tail -20 $O/ab.log; exit 1; }
+grep hidden $O/ab.log
+python3 scripts/gemm8p_ab_parse.py $O/ab/k_kernel_trace.csv 3 > $O/ab_summary.json
+echo done

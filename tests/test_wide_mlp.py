@@ -349,10 +349,77 @@ def test_row_segment_stores_match_transposed_stores(gpu, shape):
     plan.fuse_head = False
     X = stream_matrix(41_000, shape["n_features"], seed=8, missing_rate=0.01)
     s0, v0 = plan.score(X)
-    for flags in (0x400, 0x800, 0xC00):  # store_hidden_t on the K = 64 layer / on gemm8 / on both
+    for flags in (0x400, 0x800, 0xC00, 0x4000):  # store_hidden_t on the K = 64 layer / on gemm8 / on both;
+        # 0x4000: the K = 64 layer's row segments with ordinary instead of non-temporal stores
         plan.gemm_flags = flags
         try:
             s1, v1 = plan.score(X)
         finally:
             plan.gemm_flags = 0
         assert torch.equal(v0, v1) and torch.equal(s0[v0.bool()], s1[v1.bool()]), hex(flags)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape,rows,force", [(dict(n_features=32, hidden=(1024, 1024, 512)), 41_000, 0),
+                                              (dict(n_features=32, hidden=(1024, 1024, 512)), 300_000, 0),
+                                              (dict(n_features=24, hidden=(512, 768, 640), activation="tanh"), 70_000, 0),
+                                              (dict(n_features=16, hidden=(512, 512), activation="logistic"), 3_000, 0),
+                                              (dict(n_features=300, hidden=(260, 200), activation="tanh"), 50_000, 0x80),
+                                              (dict(n_features=16, hidden=(512, 256)), 30_000, 0xC0)],
+                         ids=["41k", "300k", "768-odd-tiles", "tiny-grid", "k320-odd-slices", "k64-one-slice"])
+def test_persistent_phase_kernel_matches_one_tile_per_workgroup(gpu, shape, rows, force):
+    """The persistent tile walk of the phase-interleaved hidden layers (gemm8p_kernel: the slice
+    stream continues across tile boundaries, the epilogue runs while the next tile's slices are in
+    flight, its stores counted in the next slice's vmcnt) equals gemm8_kernel (flag bit 12, one tile
+    per workgroup) bit for bit: more tiles than workgroups (300k rows: 1172 row tiles x 4), a tile
+    count that is not a multiple of 8 (the plain round-robin tile list; 768 units = 3 column
+    tiles), fewer tiles than CUs (3000 rows), and — the phase kernel forced (bit 7) — an odd slice
+    count per tile (300 inputs: K = 320, KT = 5, the buffer parity flips across tile boundaries)
+    and one slice per tile (bit 6 + 7 on the K = 64 first layer: KT = 1, every slice is a tile's
+    first and last)."""
+    c = CompiledPmml.from_string(mlp_pmml(seed=31, **shape))
+    plan = c.plan(gpu, precision="bf16", mlp_impl="wide")
+    plan.fuse_head = False
+    X = stream_matrix(rows, shape["n_features"], seed=9, missing_rate=0.01)
+    plan.gemm_flags = force
+    try:
+        s0, v0 = plan.score(X)
+        plan.gemm_flags = force | 0x1000
+        s1, v1 = plan.score(X)
+    finally:
+        plan.gemm_flags = 0
+    assert torch.equal(v0, v1) and torch.equal(s0[v0.bool()], s1[v1.bool()])
+    n = min(rows, 4000)
+    ref, _ = emulate_wide(plan, X[:n])
+    got = s0[:n].cpu().numpy().astype(np.float64)
+    ok = v0[:n].cpu().numpy().astype(bool)
+    np.testing.assert_allclose(got[ok], ref[ok], rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape,rows", [(dict(n_features=32, hidden=(1024, 1024)), 300_000),
+                                        (dict(n_features=40, hidden=(300, 1024), n_out=3, activation="logistic",
+                                              classification=True), 41_000),
+                                        (dict(n_features=24, hidden=(512, 768), n_out=4, activation="tanh",
+                                              classification=True), 70_000)],
+                         ids=["reg-300k", "cls3-41k", "cls4-768-odd-tiles"])
+def test_persistent_fused_head_matches_one_tile_per_workgroup(gpu, shape, rows):
+    """The fused output layer on the persistent tile walk (gemm8p_kernel<true>: head weights and
+    biases from LDS, the partial sums in the scratch region, the wave groups re-aligned around the
+    exchange barrier) equals gemm8_kernel<true> (flag bit 12) bit for bit — per tile the same
+    products in the same order — for n_out 1, 3 and 4 (the persistent limit), with a tile count
+    that is not a multiple of 8 (768 units = 3 column tiles)."""
+    c = CompiledPmml.from_string(mlp_pmml(seed=37, **shape))
+    plan = c.plan(gpu, precision="bf16", mlp_impl="wide")
+    assert plan._fused_head()
+    X = stream_matrix(rows, shape["n_features"], seed=10, missing_rate=0.01)
+    s0, v0 = plan.score(X)
+    plan.gemm_flags = 0x1000
+    try:
+        s1, v1 = plan.score(X)
+    finally:
+        plan.gemm_flags = 0
+    assert torch.equal(v0, v1) and torch.equal(s0[v0.bool()], s1[v1.bool()])
+    ref, vref = c.score_matrix_oracle(X[:3000])
+    v = v0[:3000].cpu().numpy().astype(bool)
+    assert (v == vref).all()
