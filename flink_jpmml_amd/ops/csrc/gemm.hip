@@ -60,7 +60,8 @@ struct GemmArgs {
                           // 11 the same for gemm8_kernel<false, true>, 12 one tile per workgroup
                           // (gemm8_kernel) instead of the persistent gemm8p_kernel, 13 gemm8p_kernel
                           // without its epilogue stores (timing only: the layer output is not written),
-                          // 14 gemm_k64p_kernel with ordinary instead of non-temporal stores
+                          // 14 gemm_k64p_kernel with ordinary instead of non-temporal stores, 15
+                          // gemm8p_kernel storing each tile in two halves (deferred, measured slower)
   const uint8_t* row_ok;  // [rows] input-stage validity (output layer)
   Epilogue epi;           // output layer decode (affine + Target, or label table)
   float* score;
@@ -329,13 +330,14 @@ __device__ __forceinline__ void store_hidden_t(const GemmArgs& a, const f32x16 (
 // same values; only the wave's own lanes touch its scratch, so no barrier.
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 // NTS: non-temporal stores (the nt bit: streamed past the caches' retention; gemm_k64p_kernel)
-template <int ACT, int TM, int TN, bool LB = true, bool NTS = false>
+// IB / IE: only the accumulator rows i in [IB, IE) (the persistent kernel stores a tile in halves)
+template <int ACT, int TM, int TN, bool LB = true, bool NTS = false, int IB = 0, int IE = TM>
 __device__ __forceinline__ void store_hidden_seg(const GemmArgs& a, const f32x16 (&acc)[TM][TN], int row0, int col0,
                                                  int wm, int wn, int lane, const float* bl, unsigned char* ws) {
   static_assert(TN % 2 == 0, "tile pairs");
   const int h = lane >> 5, l32 = lane & 31;
 #pragma unroll
-  for (int i = 0; i < TM; ++i) {
+  for (int i = IB; i < IE; ++i) {
 #pragma unroll
     for (int jp = 0; jp < TN / 2; ++jp) {
       uint4 c[2][2];  // [tile of the pair][run]: runs at chunks h, 2 + h of the tile's 64 bytes
@@ -405,16 +407,16 @@ __device__ __forceinline__ void store_hidden_seg(const GemmArgs& a, const f32x16
   }
 }
 
-template <int TM, int TN, bool LB = true, bool NTS = false>
+template <int TM, int TN, bool LB = true, bool NTS = false, int IB = 0, int IE = TM>
 __device__ __forceinline__ void store_hidden_seg_any(const GemmArgs& a, const f32x16 (&acc)[TM][TN], int row0,
                                                      int col0, int wm, int wn, int lane, const float* bl,
                                                      unsigned char* ws) {
   switch (a.act) {
-    case A_IDENTITY: store_hidden_seg<A_IDENTITY, TM, TN, LB, NTS>(a, acc, row0, col0, wm, wn, lane, bl, ws); break;
-    case A_RELU: store_hidden_seg<A_RELU, TM, TN, LB, NTS>(a, acc, row0, col0, wm, wn, lane, bl, ws); break;
-    case A_LOGISTIC: store_hidden_seg<A_LOGISTIC, TM, TN, LB, NTS>(a, acc, row0, col0, wm, wn, lane, bl, ws); break;
-    case A_TANH: store_hidden_seg<A_TANH, TM, TN, LB, NTS>(a, acc, row0, col0, wm, wn, lane, bl, ws); break;
-    default: store_hidden_seg<-1, TM, TN, LB, NTS>(a, acc, row0, col0, wm, wn, lane, bl, ws); break;
+    case A_IDENTITY: store_hidden_seg<A_IDENTITY, TM, TN, LB, NTS, IB, IE>(a, acc, row0, col0, wm, wn, lane, bl, ws); break;
+    case A_RELU: store_hidden_seg<A_RELU, TM, TN, LB, NTS, IB, IE>(a, acc, row0, col0, wm, wn, lane, bl, ws); break;
+    case A_LOGISTIC: store_hidden_seg<A_LOGISTIC, TM, TN, LB, NTS, IB, IE>(a, acc, row0, col0, wm, wn, lane, bl, ws); break;
+    case A_TANH: store_hidden_seg<A_TANH, TM, TN, LB, NTS, IB, IE>(a, acc, row0, col0, wm, wn, lane, bl, ws); break;
+    default: store_hidden_seg<-1, TM, TN, LB, NTS, IB, IE>(a, acc, row0, col0, wm, wn, lane, bl, ws); break;
   }
 }
 
@@ -1094,8 +1096,16 @@ constexpr int P8_HEAD_MAX_MP = (160 * 1024 - 8 * HALF_B - P8_SCR) / (4 + 2 * P8_
 
 // NOSTORE (flag bit 13, timing only): the hidden epilogue writes nothing — the cost of the stores.
 // (Non-temporal stores, which take 10 % off gemm_k64p_kernel, measured no change here: profiles/r5p.)
-template <bool HEADF, bool NOSTORE>
+// DEFER (flag bit 15, measured slower, profiles/r5r: 2.17-2.22 vs 2.10-2.14 ms): a tile is stored
+// in two halves. Accumulator rows 0-1 are read by the next tile's P1 / P2, rows 2-3 only from its
+// P3 on — so rows 0-1 leave at the tile boundary and rows 2-3 after the next tile's P2, half of the
+// stores overlapping two phases of MFMAs. P4 of a tile's first slice then retires slice g + 1 with
+// the 8 deferred stores still in flight: everything younger than A1 of g + 1 is A0 of g + 2, the
+// 8 stores, B0 / B1 of g + 2 = 14 instructions.
+constexpr int P8_HALF_STORES = 8;  // global stores of store_hidden_seg rows [2, 4) per lane (all lanes)
+template <bool HEADF, bool NOSTORE, bool DEFER = false>
 __global__ __launch_bounds__(NT, 1) void gemm8p_kernel(GemmArgs a, HeadFuse hf) {
+  constexpr bool DF = DEFER && !HEADF && !NOSTORE;
   constexpr int TM = 4, TN = 2;
   extern __shared__ __align__(16) unsigned char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1172,9 +1182,11 @@ __global__ __launch_bounds__(NT, 1) void gemm8p_kernel(GemmArgs a, HeadFuse hf) 
 
   const int ra = wr * 64 + l32, rb = wc * 32 + l32;
   int row0 = (base / n_ct) * BM, col0 = (base % n_ct) * 256;
+  int prow0 = 0, pcol0 = 0;  // DF: the previous tile, whose rows 2-3 are still in acc[2], acc[3]
   for (int g = 0, kt = 0, j = 0; g < NS; ++g) {
     const int b = g & 1;
     const bool n1 = g + 1 < NS, n2 = g + 2 < NS;
+    const bool first = DF && kt == 0 && g > 0;
     const size_t k1 = (size_t)s1.k * SLICE_B, k2 = (size_t)s2.k * SLICE_B;
     bf16x8 a0[2][4], a1[2][4], b0[4], b1[4];
     // P1: A0 x B0
@@ -1195,6 +1207,18 @@ __global__ __launch_bounds__(NT, 1) void gemm8p_kernel(GemmArgs a, HeadFuse hf) 
     mma_begin();
     mma_quad<true>(acc[0][1], acc[1][1], a0, b1);
     mma_end();
+    if constexpr (DF) {
+      if (first) {  // the previous tile's rows 2-3, before this tile's P3 accumulates into them
+        store_hidden_seg_any<TM, TN, true, false, 2, 4>(a, acc, prow0, pcol0, wr, wc, lane, bl + pcol0, scr + wave * 2048);
+#pragma unroll
+        for (int i = 2; i < TM; ++i)
+#pragma unroll
+          for (int q = 0; q < TN; ++q) acc[i][q] = f32x16{};
+        // B1 re-read rather than held through the epilogue (its slot is restaged only in P4)
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) b1[ks] = frag(SLOT(b, 3), rb, 2 * ks + h);
+      }
+    }
     // P3: A1 x B1
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks)
@@ -1207,8 +1231,13 @@ __global__ __launch_bounds__(NT, 1) void gemm8p_kernel(GemmArgs a, HeadFuse hf) 
     // P4: A1 x B0; slice g + 1 retired (three half-tiles of g + 2 may stay in flight — and, on a
     // tile's first slice, the previous epilogue's stores, which are older, retired with it)
     if (n2) stage_half_s<false>(s2.B + k2, ldw32, SLOT(b, 3), 1, wave, lane);
-    if (n2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    else if (n1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (n2) {
+      if (first) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(6 + P8_HALF_STORES) : "memory");
+      else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else if (n1) {
+      if (first) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(P8_HALF_STORES) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     mma_begin();
     mma_quad<true>(acc[2][0], acc[3][0], a1, b0);
     mma_end();
@@ -1228,11 +1257,15 @@ __global__ __launch_bounds__(NT, 1) void gemm8p_kernel(GemmArgs a, HeadFuse hf) 
       } else if constexpr (NOSTORE) {
 #pragma unroll
         for (int i = 0; i < TM; ++i) asm volatile("" ::"v"(acc[i][0]), "v"(acc[i][1]));
+      } else if constexpr (DF) {
+        store_hidden_seg_any<TM, TN, true, false, 0, 2>(a, acc, row0, col0, wr, wc, lane, bl + col0, scr + wave * 2048);
+        prow0 = row0;
+        pcol0 = col0;
       } else {
         store_hidden_seg_any<TM, TN, true>(a, acc, row0, col0, wr, wc, lane, bl + col0, scr + wave * 2048);
       }
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+      for (int i = 0; i < (DF ? 2 : TM); ++i)
 #pragma unroll
         for (int q = 0; q < TN; ++q) acc[i][q] = f32x16{};
       kt = 0;
@@ -1244,6 +1277,8 @@ __global__ __launch_bounds__(NT, 1) void gemm8p_kernel(GemmArgs a, HeadFuse hf) 
     }
   }
 #undef SLOT
+  if constexpr (DF)  // the last tile's rows 2-3
+    store_hidden_seg_any<TM, TN, true, false, 2, 4>(a, acc, prow0, pcol0, wr, wc, lane, bl + pcol0, scr + wave * 2048);
   if (wr == 0) raw_barrier();  // balance group 1's extra barrier
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
@@ -1366,15 +1401,17 @@ int cu_count() {
 template <bool HEADF>
 int launch8p(hipStream_t stream, const GemmArgs& a, const HeadFuse& hf) {
   const size_t lds = 8 * (size_t)HALF_B + P8_SCR + 4 * (size_t)a.Mp + (HEADF ? 2 * (size_t)hf.n_out * a.Mp : 0);
-  const bool nostore = !HEADF && ((a.f32 >> 13) & 1);
+  const bool nostore = !HEADF && ((a.f32 >> 13) & 1), defer = !HEADF && !nostore && ((a.f32 >> 15) & 1);
   const void* kp = HEADF ? reinterpret_cast<const void*>(&gemm8p_kernel<true, false>)
                  : nostore ? reinterpret_cast<const void*>(&gemm8p_kernel<false, true>)
-                           : reinterpret_cast<const void*>(&gemm8p_kernel<false, false>);
+                 : defer ? reinterpret_cast<const void*>(&gemm8p_kernel<false, false, true>)
+                         : reinterpret_cast<const void*>(&gemm8p_kernel<false, false>);
   if (hipFuncSetAttribute(kp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return -5;
   const int total = (a.rows_p / BM) * (a.Mp / 256);
   const int grid = std::min(total, cu_count());
   if (HEADF) hipLaunchKernelGGL((gemm8p_kernel<true, false>), dim3(grid), dim3(NT), lds, stream, a, hf);
   else if (nostore) hipLaunchKernelGGL((gemm8p_kernel<false, true>), dim3(grid), dim3(NT), lds, stream, a, hf);
+  else if (defer) hipLaunchKernelGGL((gemm8p_kernel<false, false, true>), dim3(grid), dim3(NT), lds, stream, a, hf);
   else hipLaunchKernelGGL((gemm8p_kernel<false, false>), dim3(grid), dim3(NT), lds, stream, a, hf);
   return 0;
 }
@@ -1440,7 +1477,7 @@ PMML_API int pmml_gemm_launch(hipStream_t stream, const GemmArgs* args, int head
   const GemmArgs a = *args;
   if (a.rows <= 0) return 0;
   const int BN = head ? 32 : 256;
-  if (a.f32 & ~0x7FE1) return -4;
+  if (a.f32 & ~0xFFE1) return -4;
   // bf16 hidden layers with K >= 512 run the phase-interleaved kernel (profiles/r3ao: 2048 x 2048
   // 8.73 -> 8.36 ms, 1024 x 1024 2.62 -> 2.48 ms over 1M rows); below that the layer is bound by
   // its output writes and the 2-buffer loop is faster (K = 64: 0.83 vs 0.92 ms). Bit 7 forces it.
