@@ -812,6 +812,8 @@ __device__ __forceinline__ void stage_half(const unsigned char* src, size_t ldb,
 // vmcnt(0) per reload in the loop. Invisible to hipcc's wait-count pass, which is what the kernel
 // wants: every wait on these loads is an explicit counted vmcnt already, and hipcc no longer
 // drains them before the epilogue's LDS accesses. ldb * 256 rows must fit 32 bits (launcher).
+// M0 is clobbered (hipcc notes it cannot preserve a reserved register): none of the gemm8p_kernel
+// instantiations uses M0 outside these statements (checked in the generated .s).
 __device__ __forceinline__ void glds16s(const unsigned char* sbase, uint32_t voff, const unsigned char* lds) {
   const uint32_t m = __builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uintptr_t>(lds));
   asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(m), "v"(voff), "s"(sbase)
