@@ -61,7 +61,8 @@ struct GemmArgs {
                           // (gemm8_kernel) instead of the persistent gemm8p_kernel, 13 gemm8p_kernel
                           // without its epilogue stores (timing only: the layer output is not written),
                           // 14 gemm_k64p_kernel with ordinary instead of non-temporal stores, 15
-                          // gemm8p_kernel storing each tile in two halves (deferred, measured slower)
+                          // gemm8p_kernel storing each tile in two halves (deferred, measured slower),
+                          // 16 gemm8p_kernel also above K = 1024 (experiment)
   const uint8_t* row_ok;  // [rows] input-stage validity (output layer)
   Epilogue epi;           // output layer decode (affine + Target, or label table)
   float* score;
@@ -1479,7 +1480,7 @@ PMML_API int pmml_gemm_launch(hipStream_t stream, const GemmArgs* args, int head
   const GemmArgs a = *args;
   if (a.rows <= 0) return 0;
   const int BN = head ? 32 : 256;
-  if (a.f32 & ~0xFFE1) return -4;
+  if (a.f32 & ~0x1FFE1) return -4;
   // bf16 hidden layers with K >= 512 run the phase-interleaved kernel (profiles/r3ao: 2048 x 2048
   // 8.73 -> 8.36 ms, 1024 x 1024 2.62 -> 2.48 ms over 1M rows); below that the layer is bound by
   // its output writes and the 2-buffer loop is faster (K = 64: 0.83 vs 0.92 ms). Bit 7 forces it.
@@ -1509,7 +1510,7 @@ PMML_API int pmml_gemm_launch(hipStream_t stream, const GemmArgs* args, int head
   // persistent tile walk (gemm8p_kernel) for the transposed-store phase-interleaved layers with the
   // row-segment stores and K <= 1024, unless bit 12 (one tile per workgroup) or bit 11
   // (store_hidden_t) is set
-  const bool p8 = ph8 && tst && !head && !((a.f32 >> 11) & 1) && (use8p(a) || ((a.f32 >> 13) & 1));
+  const bool p8 = ph8 && tst && !head && !((a.f32 >> 11) & 1) && (use8p(a) || ((a.f32 >> 13) & 1) || ((a.f32 >> 16) & 1));
   const int rc = f32 ? (head ? launch<32, true, true>(stream, a) : launch<256, false, true>(stream, a))
                      : (head ? launch<32, true, false>(stream, a)
                              : (p8 ? launch8p<false>(stream, a, HeadFuse{})
