@@ -1352,13 +1352,18 @@ __global__ __launch_bounds__(K64_NT, 2) void gemm_k64p_kernel(GemmArgs a, int rg
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-int launch_k64p(hipStream_t stream, const GemmArgs& a) {
+int cu_count() {
   static int n_cu = 0;
   if (n_cu == 0) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
       n_cu = 256;
   }
+  return n_cu;
+}
+
+int launch_k64p(hipStream_t stream, const GemmArgs& a) {
+  const int n_cu = cu_count();
   const int n_ct = a.Mp / 256;
   const int rg = std::max(1, (2 * n_cu / 8) / n_ct);  // row groups per XCD: ~2 workgroups per CU
   // 128-byte row-segment stores through a 2 KiB wave scratch (store_hidden_seg, default: 0.565 ->
@@ -1389,16 +1394,6 @@ int launch8(hipStream_t stream, const GemmArgs& a, const HeadFuse& hf) {
     return -5;
   hipLaunchKernelGGL((gemm8_kernel<HEADF, TST>), dim3((a.rows_p / BM) * (a.Mp / 256)), dim3(NT), lds, stream, a, hf);
   return 0;
-}
-
-int cu_count() {
-  static int n_cu = 0;
-  if (n_cu == 0) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
-      n_cu = 256;
-  }
-  return n_cu;
 }
 
 template <bool HEADF>
