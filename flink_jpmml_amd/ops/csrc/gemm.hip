@@ -1063,8 +1063,9 @@ __global__ __launch_bounds__(NT, 1) void gemm8_kernel(GemmArgs a, HeadFuse hf) {
   }
 }
 
-// Persistent phase-interleaved hidden layer (gemm8p_kernel; bf16, 512 <= K <= 1024: the default
-// of the transposed-store path and of the fused output layer; flag bit 12 selects gemm8_kernel).
+// Persistent phase-interleaved hidden layer (gemm8p_kernel; bf16, K >= 128: the default of the
+// transposed-store path and of the fused output layer; flag bit 12 selects gemm8_kernel / the
+// 2-buffer loop).
 // gemm8_kernel runs ONE 256 x 256 tile per workgroup; at one workgroup per CU the matrix cores
 // idle while a fresh workgroup fills its first slices and while the last one drains its
 // epilogue. Here a grid of one workgroup per CU walks a list of tiles and the slice stream of
@@ -1085,10 +1086,11 @@ __global__ __launch_bounds__(NT, 1) void gemm8_kernel(GemmArgs a, HeadFuse hf) {
 // Tile list: the XCD-contiguous order of gemm8_kernel — XCD x (blockIdx & 7) owns tiles
 // [x T / 8, (x + 1) T / 8) and its G / 8 workgroups take every (G / 8)-th of them, so the column
 // tiles of a row block run together on one XCD and its A rows come from HBM once.
-// Measured (profiles/r5n, 1M rows x 1024 x 1024, one process, interleaved): 2.04 vs 2.23 ms for
-// gemm8_kernel<false, true>; without any stores (bit 13, timing only) 1.85 ms. A K = 4096 layer is
-// slower persistent (profiles/r5m: 7.71 vs 7.37 ms, and 7.64 without stores), hence the K <= 1024
-// routing. Measured and dropped (profiles/r5m, r5n): staging the next tile's A1 before the
+// Measured (profiles/r5n, r5t; 1M rows, one process, interleaved): 1024 x 1024 2.04 vs 2.23 ms for
+// gemm8_kernel<false, true> (without any stores, bit 13, timing only: 1.63 ms); K = 4096 6.92 vs
+// 7.42 ms; K = 256 0.25 / 0.47 vs 0.32 / 0.60 ms for the 2-buffer loop (256 / 512 units). (With the
+// builtin LDS-DMA the K = 4096 layer was slower persistent, profiles/r5m: 7.71 vs 7.37 ms.)
+// Measured and dropped (profiles/r5m, r5n): staging the next tile's A1 before the
 // epilogue with the stores left in flight one slice longer (+9 %), half of the next slice's A0
 // fragments read in the otherwise read-free P4 (12/4/8/0 -> 8/4/8/4 reads per phase: +8 %),
 // XCDs 4-7 started half a tile late to split the chip-wide store burst (no change).
@@ -1416,7 +1418,7 @@ int launch8p(hipStream_t stream, const GemmArgs& a, const HeadFuse& hf) {
 
 // whether the persistent kernel takes a layer (a: the hidden layer's args; flag bit 12 opts out)
 bool use8p(const GemmArgs& a) {
-  return !((a.f32 >> 12) & 1) && a.Mp <= P8_MAX_MP && a.K <= 1024 && (size_t)a.lda * 2 * BM < (1ull << 31) &&
+  return !((a.f32 >> 12) & 1) && a.Mp <= P8_MAX_MP && (size_t)a.lda * 2 * BM < (1ull << 31) &&
          (size_t)a.ldw * 2 * 256 < (1ull << 31);
 }
 
@@ -1505,7 +1507,11 @@ PMML_API int pmml_gemm_launch(hipStream_t stream, const GemmArgs* args, int head
   // persistent tile walk (gemm8p_kernel) for the transposed-store phase-interleaved layers with the
   // row-segment stores and K <= 1024, unless bit 12 (one tile per workgroup) or bit 11
   // (store_hidden_t) is set
-  const bool p8 = ph8 && tst && !head && !((a.f32 >> 11) & 1) && (use8p(a) || ((a.f32 >> 13) & 1) || ((a.f32 >> 16) & 1));
+  // bf16 hidden layers with K >= 128 (bit 7: also K = 64) on the transposed-store path run the
+  // persistent kernel (profiles/r5t: K = 256 layers 0.25 / 0.47 vs 0.32 / 0.60 ms on the 2-buffer
+  // loop, K = 4096 6.92 vs 7.42 ms on gemm8_kernel)
+  const bool p8 = !f32 && tst && !head && !((a.f32 >> 11) & 1) && (a.K >= 128 || ((a.f32 >> 7) & 1)) &&
+                  (use8p(a) || ((a.f32 >> 13) & 1) || ((a.f32 >> 16) & 1));
   const int rc = f32 ? (head ? launch<32, true, true>(stream, a) : launch<256, false, true>(stream, a))
                      : (head ? launch<32, true, false>(stream, a)
                              : (p8 ? launch8p<false>(stream, a, HeadFuse{})

@@ -152,21 +152,23 @@ def test_wide_gemm_kernels_on_gpu(gpu, shape, precision):
                                    dict(n_features=40, hidden=(1024, 512))],
                          ids=["k128", "k192", "k1024"])
 def test_phase_interleaved_gemm_matches_two_buffer_loop(gpu, shape):
-    """The phase-interleaved bf16 hidden-layer kernel (gemm8_kernel: half-tile staging, counted
-    vmcnt across raw barriers, staggered wave groups) runs by default for K >= 512; forcing it on
-    every hidden layer (K = 128 / 192: 2 / 3 slices, the pipeline's edge cases) must give the same
-    bits as the 2-buffer loop — the same MFMAs in the same k order."""
+    """The phase-interleaved bf16 hidden-layer kernels — the persistent gemm8p_kernel (default for
+    K >= 128) and the one-tile gemm8_kernel (bit 12, K >= 512, or forced by bit 7): half-tile
+    staging, counted vmcnt across raw barriers, staggered wave groups — must give the same bits as
+    the 2-buffer loop (bit 12 at K < 512) on every hidden layer, including K = 128 / 192 (2 / 3
+    slices, the pipeline's edge cases): the same MFMAs in the same k order."""
     c = CompiledPmml.from_string(mlp_pmml(seed=9, **shape))
     plan = c.plan(gpu, precision="bf16", mlp_impl="wide")
     plan.fuse_head = False  # every hidden layer through pmml_gemm_launch
     X = stream_matrix(5000, shape["n_features"], seed=4, missing_rate=0.01)
     s0, v0 = plan.score(X)
-    plan.gemm_flags = 0x80
-    try:
-        s1, v1 = plan.score(X)
-    finally:
-        plan.gemm_flags = 0
-    assert torch.equal(v0, v1) and torch.equal(s0[v0.bool()], s1[v1.bool()])
+    for flags in (0x1000, 0x1080):  # one tile per workgroup: 2-buffer loop below K = 512 / gemm8_kernel forced
+        plan.gemm_flags = flags
+        try:
+            s1, v1 = plan.score(X)
+        finally:
+            plan.gemm_flags = 0
+        assert torch.equal(v0, v1) and torch.equal(s0[v0.bool()], s1[v1.bool()]), hex(flags)
     ref, vref = c.score_matrix_oracle(X)
     s1, v1 = s1.cpu().numpy(), v1.cpu().numpy().astype(bool)
     assert (v1 == vref).all()
@@ -216,15 +218,17 @@ def test_fused_output_layer_matches_separate_launch(gpu, shape):
         plan.fuse_head = True
     assert torch.equal(v0, v1)
     s0, s1, v = s0.cpu().numpy(), s1.cpu().numpy(), v1.cpu().numpy().astype(bool)
-    ref, vref = c.score_matrix_oracle(X)
-    assert (v == vref).all()
+    n = 4000  # the oracle walks connections in Python: its rows are a prefix
+    ref, vref = c.score_matrix_oracle(X[:n])
+    assert (v[:n] == vref).all()
+    vo = v[:n]
     if shape.get("classification"):
         assert (s0[v] == s1[v]).mean() > 0.999
-        assert (s1[v] == ref[v]).mean() > 0.98
+        assert (s1[:n][vo] == ref[vo]).mean() > 0.98
     else:
-        scale = max(1.0, float(np.abs(ref[v]).max()))
+        scale = max(1.0, float(np.abs(ref[vo]).max()))
         assert np.abs(s1[v] - s0[v]).max() < 1e-4 * scale
-        assert np.abs(s1[v] - ref[v]).max() < 3e-2 * scale
+        assert np.abs(s1[:n][vo] - ref[vo]).max() < 3e-2 * scale
 
 
 @pytest.mark.gpu
@@ -269,8 +273,8 @@ def test_fused_input_stage_matches_separate_prep(gpu, shape):
     finally:
         plan.in_contig = 1
     assert torch.equal(v0, v2) and torch.equal(s0[v0.bool()], s2[v2.bool()])
-    ref, vref = c.score_matrix_oracle(X)
-    assert (v1.cpu().numpy().astype(bool) == vref).all()
+    ref, vref = c.score_matrix_oracle(X[:3000])  # the oracle walks connections in Python
+    assert (v1[:3000].cpu().numpy().astype(bool) == vref).all()
 
 
 @pytest.mark.gpu
@@ -401,14 +405,16 @@ def test_persistent_phase_kernel_matches_one_tile_per_workgroup(gpu, shape, rows
                                         (dict(n_features=40, hidden=(300, 1024), n_out=3, activation="logistic",
                                               classification=True), 41_000),
                                         (dict(n_features=24, hidden=(512, 768), n_out=4, activation="tanh",
-                                              classification=True), 70_000)],
-                         ids=["reg-300k", "cls3-41k", "cls4-768-odd-tiles"])
+                                              classification=True), 70_000),
+                                        (dict(n_features=32, hidden=(512,), n_out=2, classification=True), 50_000)],
+                         ids=["reg-300k", "cls3-41k", "cls4-768-odd-tiles", "k64-one-slice"])
 def test_persistent_fused_head_matches_one_tile_per_workgroup(gpu, shape, rows):
     """The fused output layer on the persistent tile walk (gemm8p_kernel<true>: head weights and
     biases from LDS, the partial sums in the scratch region, the wave groups re-aligned around the
     exchange barrier) equals gemm8_kernel<true> (flag bit 12) bit for bit — per tile the same
-    products in the same order — for n_out 1, 3 and 4 (the persistent limit), with a tile count
-    that is not a multiple of 8 (768 units = 3 column tiles)."""
+    products in the same order — for n_out 1 to 4 (4: the persistent limit), with a tile count
+    that is not a multiple of 8 (768 units = 3 column tiles), and on a K = 64 layer (one slice per
+    tile: every slice ends in the head epilogue)."""
     c = CompiledPmml.from_string(mlp_pmml(seed=37, **shape))
     plan = c.plan(gpu, precision="bf16", mlp_impl="wide")
     assert plan._fused_head()
