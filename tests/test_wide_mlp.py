@@ -429,3 +429,47 @@ def test_persistent_fused_head_matches_one_tile_per_workgroup(gpu, shape, rows):
     ref, vref = c.score_matrix_oracle(X[:3000])
     v = v0[:3000].cpu().numpy().astype(bool)
     assert (v == vref).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(6))
+def test_persistent_kernels_random_shapes(gpu, seed):
+    """Random wide-MLP shapes through the persistent kernels (hidden widths 64-1600, inputs 3-700,
+    1-5 outputs, any activation, 1 to 70k rows incl. sub-tile batches), fused head on and off:
+    bit-identical to one tile per workgroup (flag bit 12) and within bf16 tolerance of the numpy
+    model of the kernels."""
+    rng = np.random.default_rng(1000 + seed)
+    n_layers = int(rng.integers(1, 4))
+    hidden = tuple(int(rng.integers(1, 26)) * 64 for _ in range(n_layers))
+    n_out = int(rng.integers(1, 6))
+    act = ["rectifier", "tanh", "logistic", "identity"][int(rng.integers(0, 4))]
+    n_features = int(rng.integers(3, 700))
+    rows = int(rng.choice([1, 255, 257, 3000, 70_000]))
+    shape = dict(n_features=n_features, hidden=hidden, n_out=n_out, activation=act,
+                 classification=bool(n_out > 1))
+    c = CompiledPmml.from_string(mlp_pmml(seed=50 + seed, **shape))
+    plan = c.plan(gpu, precision="bf16", mlp_impl="wide")
+    X = stream_matrix(rows, n_features, seed=seed, missing_rate=0.2 / n_features)  # ~80 % complete rows
+    for fuse in (True, False):
+        plan.fuse_head = fuse
+        try:
+            s0, v0 = plan.score(X)
+            plan.gemm_flags = 0x1000
+            s1, v1 = plan.score(X)
+        finally:
+            plan.gemm_flags = 0
+            plan.fuse_head = True
+        assert torch.equal(v0, v1) and torch.equal(s0[v0.bool()], s1[v1.bool()]), (shape, rows, fuse)
+    n = min(rows, 2000)
+    ref, ok_ref = emulate_wide(plan, X[:n])
+    ok = v0[:n].cpu().numpy().astype(bool)
+    assert (ok == ok_ref).all()
+    assert ok.any() or n < 10
+    got = s0[:n].cpu().numpy().astype(np.float64)
+    if not ok.any():
+        return
+    if shape["classification"]:
+        assert (got[ok] == ref[ok]).mean() > 0.97
+    else:
+        scale = max(1.0, float(np.abs(ref[ok]).max()))
+        np.testing.assert_allclose(got[ok], ref[ok], rtol=0, atol=3e-2 * scale)
