@@ -214,6 +214,14 @@ __device__ __forceinline__ V frag(const unsigned char* img, int r, int c) {
 
 __device__ __noinline__ float activate_any(int act, float z, float thr) { return activate(act, z, thr); }
 
+// Two floats -> one word of two bf16 (round to nearest even, lo = a): ONE v_cvt_pk_bf16_f32
+// (scalar (__bf16) casts cost a conversion per value plus an SDWA or to merge them).
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2{a, b}), bf16x2));
+}
+
 template <int ACT>
 __device__ __forceinline__ float act_of(float z, int act, float thr) {
   if constexpr (ACT == A_IDENTITY) return z;
@@ -300,8 +308,7 @@ __device__ __forceinline__ void store_hidden_t(const GemmArgs& a, const f32x16 (
       for (int w = 0; w < 8; ++w) {
         const float v0 = act_of<ACT>(acc[i][j][2 * w] + b[2 * w], a.act, a.thr);
         const float v1 = act_of<ACT>(acc[i][j][2 * w + 1] + b[2 * w + 1], a.act, a.thr);
-        p[w] = (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)v0) |
-               ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)v1) << 16);
+        p[w] = pack_bf16x2(v0, v1);
       }
       // swap(X, Y): X keeps the low half's own X and takes the low half's Y into the high half;
       // Y takes the high half's X into the low half — runs (q, q + 1) become the 16-byte run 2q + h
@@ -362,8 +369,7 @@ __device__ __forceinline__ void store_hidden_seg(const GemmArgs& a, const f32x16
         for (int w = 0; w < 8; ++w) {
           const float v0 = act_of<ACT>(acc[i][j][2 * w] + b[2 * w], a.act, a.thr);
           const float v1 = act_of<ACT>(acc[i][j][2 * w + 1] + b[2 * w + 1], a.act, a.thr);
-          p[w] = (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)v0) |
-                 ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)v1) << 16);
+          p[w] = pack_bf16x2(v0, v1);
         }
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
