@@ -1114,6 +1114,9 @@ constexpr int P8_HEAD_MAX_MP = (160 * 1024 - 8 * HALF_B - P8_SCR) / (4 + 2 * P8_
 // the 8 deferred stores still in flight: everything younger than A1 of g + 1 is A0 of g + 2, the
 // 8 stores, B0 / B1 of g + 2 = 14 instructions.
 constexpr int P8_HALF_STORES = 8;  // global stores of store_hidden_seg rows [2, 4) per lane (all lanes)
+// (Also measured and dropped, profiles/r5z: the last slice of a tile staging A1 of slice g + 2 in
+// its P4 so that the next tile's first slice can retire g + 2 with the epilogue's stores still in
+// flight — 2.09-2.14 vs 1.99-2.08 ms with the asm staging, as it was with the builtin one.)
 template <bool HEADF, bool NOSTORE, bool DEFER = false>
 __global__ __launch_bounds__(NT, 1) void gemm8p_kernel(GemmArgs a, HeadFuse hf) {
   constexpr bool DF = DEFER && !HEADF && !NOSTORE;

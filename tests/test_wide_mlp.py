@@ -388,11 +388,12 @@ def test_persistent_phase_kernel_matches_one_tile_per_workgroup(gpu, shape, rows
     plan.gemm_flags = force
     try:
         s0, v0 = plan.score(X)
-        plan.gemm_flags = force | 0x1000
-        s1, v1 = plan.score(X)
+        for extra in (0x1000,):  # one tile per workgroup
+            plan.gemm_flags = force | extra
+            s1, v1 = plan.score(X)
+            assert torch.equal(v0, v1) and torch.equal(s0[v0.bool()], s1[v1.bool()]), hex(extra)
     finally:
         plan.gemm_flags = 0
-    assert torch.equal(v0, v1) and torch.equal(s0[v0.bool()], s1[v1.bool()])
     n = min(rows, 4000)
     ref, _ = emulate_wide(plan, X[:n])
     got = s0[:n].cpu().numpy().astype(np.float64)
