@@ -27,6 +27,18 @@
 //   Epilogue (output layer): + bias into an LDS row tile, then one thread per row applies the
 //   output activation, softmax / simplemax, label table or regression affine + Target stage and
 //   writes score / valid / probabilities (the zero-copy sink pointers of the pipeline).
+//
+// Which kernel takes a layer (pmml_gemm_launch / pmml_gemm_fused_head_launch):
+//   bf16 hidden, K = 64          gemm_k64p_kernel  persistent over row tiles, weights staged once,
+//                                                   non-temporal 128-byte row-segment stores
+//   bf16 hidden, K >= 128        gemm8p_kernel     persistent 256 x 256 phase-interleaved walk
+//                                                   (LDS-DMA slice stream across tiles, SADDR asm)
+//   last hidden + output layer   gemm8p_kernel<true> (n_out <= 4) / gemm8_kernel<true>: the output
+//                                                   layer folded into the accumulators, no H store
+//   output layer / fp32 / flags  gemm_kernel       the 2-buffer loop described above
+//   bit 12 (A/B reference)       gemm8_kernel / gemm_kernel, one tile per workgroup
+// Every alternative path stays selectable by a flag bit of GemmArgs.f32 and is pinned bit for bit
+// against the default by tests/test_wide_mlp.py.
 #include "epilogue.h"
 #include "nn_act.h"
 
