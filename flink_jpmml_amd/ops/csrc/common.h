@@ -73,6 +73,8 @@ enum : int {
   EPI_ARGMAX = 2,       // label = argmax_c acc_c (ties -> lowest c); probs = acc * a
   EPI_SOFTMAX = 3,      // probs = softmax(acc); label = argmax
   EPI_CUMULATIVE = 4,   // ordinal: cum_c = link(acc_c) (c < C-1), cum_{C-1} = 1; p_c = cum_c - cum_{c-1}
+  EPI_LINKMAX = 5,      // > 2 tables, element-wise link: p_c = link(acc_c); label = first argmax; any
+                        // non-finite p_c voids the row (models/regression.py finish)
 };
 
 struct Epilogue {

@@ -41,6 +41,15 @@ __device__ __forceinline__ void apply_epilogue(const Epilogue& e, Acc acc, bool 
       probs[(size_t)row * 2 + 1] = 1.0f - p0;
     }
     ok = ok && (p0 == p0);
+  } else if (e.mode == EPI_LINKMAX) {
+    const int C = e.n_classes;
+    float best = -__builtin_inff();
+    for (int c = 0; c < C; ++c) {
+      const float pv = apply_link(e.link, acc(c));
+      if (pv > best) { best = pv; label = c; }  // NaN never wins (the oracle's nan -> -inf)
+      ok = ok && __builtin_isfinite(pv);
+      if (e.write_probs && probs) probs[(size_t)row * C + c] = pv;
+    }
   } else if (e.mode == EPI_CUMULATIVE) {
     const int C = e.n_classes;
     float best = -__builtin_inff();

@@ -50,7 +50,7 @@ FP_INTEGER = 1 << 9
 FP_CODE_RANGE = 1 << 10
 FP_ROW_INVALID = 1 << 11
 
-EPI_AFFINE, EPI_LOGISTIC2, EPI_ARGMAX, EPI_SOFTMAX, EPI_CUMULATIVE = 0, 1, 2, 3, 4
+EPI_AFFINE, EPI_LOGISTIC2, EPI_ARGMAX, EPI_SOFTMAX, EPI_CUMULATIVE, EPI_LINKMAX = 0, 1, 2, 3, 4, 5
 LINKS = {"none": 0, None: 0, "logit": 1, "exp": 2, "probit": 3, "cloglog": 4, "loglog": 5, "cauchit": 6}
 
 
@@ -625,8 +625,10 @@ class LinearPlan(DevicePlan):
                     raise NotLowerable(f"normalizationMethod {norm!r}")
                 # p0 = link(y0); the second table is ignored (PMML binary rule)
                 self.epi_args = dict(mode=EPI_LOGISTIC2, C=2, link=LINKS[norm])
-            else:
-                raise NotLowerable("multi-table element-wise link is host-only")
+            else:  # > 2 tables: every class its own link value, first argmax (models/regression.py)
+                if norm not in LINKS:
+                    raise NotLowerable(f"normalizationMethod {norm!r}")
+                self.epi_args = dict(mode=EPI_LINKMAX, C=self.K, link=LINKS[norm])
         else:
             self.table = None
             if norm not in LINKS:

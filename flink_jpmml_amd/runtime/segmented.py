@@ -182,14 +182,14 @@ def eval_predicate_device(prog, X):
 def probs_width(plan) -> Optional[int]:
     """Number of probability columns a classification plan writes through ``launch(probs=...)``
     (the oracle's ``ModelResult.probs`` of that model), or None when it cannot."""
-    from .plans import EPI_ARGMAX, EPI_CUMULATIVE, EPI_LOGISTIC2, EPI_SOFTMAX, LinearPlan, TreePlan
+    from .plans import EPI_ARGMAX, EPI_CUMULATIVE, EPI_LINKMAX, EPI_LOGISTIC2, EPI_SOFTMAX, LinearPlan, TreePlan
 
     inner = getattr(plan, "inner", None)
     if inner is not None:
         return probs_width(inner)
     if isinstance(plan, (LinearPlan, TreePlan)):
         e = getattr(plan, "epi_args", {})
-        if e.get("mode") in (EPI_ARGMAX, EPI_SOFTMAX, EPI_CUMULATIVE, EPI_LOGISTIC2):
+        if e.get("mode") in (EPI_ARGMAX, EPI_SOFTMAX, EPI_CUMULATIVE, EPI_LOGISTIC2, EPI_LINKMAX):
             if isinstance(plan, TreePlan) and getattr(plan, "sharded", False):
                 return None
             return 2 if e["mode"] == EPI_LOGISTIC2 else int(e.get("C", 0)) or None

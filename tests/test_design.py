@@ -17,6 +17,12 @@ CASES = {
     "reg-logit": lambda: regression_design_pmml(normalization="logit"),
     "reg-softmax": lambda: regression_design_pmml(classes=3, normalization="softmax"),
     "reg-binary": lambda: regression_design_pmml(classes=2, normalization="logit"),
+    # > 2 tables with an element-wise link (one-vs-rest logistic exports): p_k = link(y_k), argmax
+    "reg-ovr-logit": lambda: regression_design_pmml(classes=3, normalization="logit"),
+    "reg-ovr-none": lambda: regression_design_pmml(classes=4, normalization="none", seed=2),
+    "reg-ovr-probit": lambda: regression_design_pmml(classes=3, normalization="probit", seed=3),
+    "reg-ovr-cloglog": lambda: regression_design_pmml(classes=5, normalization="cloglog", seed=4),
+    "reg-ovr-exp": lambda: regression_design_pmml(classes=3, normalization="exp", seed=5),
     "glm-log": lambda: glm_pmml(link="log"),
     "glm-logit": lambda: glm_pmml(link="logit"),
     "glm-identity": lambda: glm_pmml(link="identity"),
