@@ -184,6 +184,8 @@ class MlpPlan(DevicePlan):
     def _io(self, compiled, ev):
         """Inputs (NormContinuous affine maps, missing replacements, active-field index), the
         dense layers, output normalisation and the target decode. Returns ``(layers, index)``."""
+        if self.prep is not None:  # the input stages read raw columns: compile_plan adds the prepare pass
+            raise NotLowerable("network plans read prepared inputs (MiningField / DataField treatment present)")
         nn = ev.nn
         scales, shifts, misses, index = [], [], [], []
         for inp in nn.inputs:

@@ -1943,19 +1943,27 @@ def compile_plan(compiled, device, **opts) -> DevicePlan:
         impl = opts.pop("mlp_impl", "auto")  # auto | fused | wide | gemm
         if impl not in ("auto", "fused", "wide", "gemm"):
             raise ValueError("mlp_impl must be auto, fused, wide or gemm")
-        if impl == "gemm":
-            return GemmMlpPlan(compiled, device, precision=prec)
-        if impl == "wide":
-            return WideMlpPlan(compiled, device, precision=prec)
-        try:
-            return MlpPlan(compiled, device, precision=prec, **opts)
-        except NotLowerable as e:
-            if "fused kernel" not in str(e) or impl == "fused":
-                raise
-            try:  # wide layers: one fused MFMA GEMM launch per layer (ops/csrc/gemm.hip), bf16 or fp32
-                return WideMlpPlan(compiled, device, precision=prec)
-            except NotLowerable:  # > 32 outputs or > 16384 inputs: library GEMMs
-                return GemmMlpPlan(compiled, device, precision=prec)
+
+        def build(c):
+            if impl == "gemm":
+                return GemmMlpPlan(c, device, precision=prec)
+            if impl == "wide":
+                return WideMlpPlan(c, device, precision=prec)
+            try:
+                return MlpPlan(c, device, precision=prec, **opts)
+            except NotLowerable as e:
+                if "fused kernel" not in str(e) or impl == "fused":
+                    raise
+                try:  # wide layers: one fused MFMA GEMM launch per layer (ops/csrc/gemm.hip), bf16 or fp32
+                    return WideMlpPlan(c, device, precision=prec)
+                except NotLowerable:  # > 32 outputs or > 16384 inputs: library GEMMs
+                    return GemmMlpPlan(c, device, precision=prec)
+
+        # the network kernels read the raw input columns (NormContinuous / mapMissingTo fused into
+        # their input stage): a MiningField / DataField treatment that is not the identity
+        # (missing replacement, validity intervals, outliers, invalid treatment) runs as a
+        # prepare-only derive pass first — the kernels never see unprepared values
+        return _with_prepared_inputs(compiled, device, build, dict(opts, precision=policy, mlp_impl=impl))
     if isinstance(ev, SvmEvaluator):
         from .nn_plans import SvmGemmPlan, SvmPlan, SvmWidePlan
 
