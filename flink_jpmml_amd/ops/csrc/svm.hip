@@ -64,6 +64,13 @@ __device__ __forceinline__ void svm_finish(const SvmArgs& a, int row, const floa
     sc = a.epi.table[best];
   }
   ok = ok && (sc == sc);
+  if (!a.classification && a.epi.tgt) {  // PMML Target of a regression SVM (epilogue.h order)
+    sc = apply_target(a.epi, sc);
+    if (!ok && (a.epi.tgt & TGT_DEFAULT)) {
+      sc = a.epi.dflt;
+      ok = true;
+    }
+  }
   const float so = ok ? sc : __builtin_nanf("");
   a.score[row] = so;
   a.valid[row] = ok ? 1 : 0;
@@ -387,7 +394,14 @@ __global__ __launch_bounds__(WTB) void svm_wide_kernel(SvmWideArgs w) {
   } else {
     sc = reg;
   }
-  const bool ok = !bad && (sc == sc);
+  bool ok = !bad && (sc == sc);
+  if (!a.classification && a.epi.tgt) {  // PMML Target of a regression SVM (epilogue.h order)
+    sc = apply_target(a.epi, sc);
+    if (!ok && (a.epi.tgt & TGT_DEFAULT)) {
+      sc = a.epi.dflt;
+      ok = true;
+    }
+  }
   const float so = ok ? sc : __builtin_nanf("");
   a.score[row] = so;
   a.valid[row] = ok ? 1 : 0;

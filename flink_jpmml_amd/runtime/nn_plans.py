@@ -548,7 +548,7 @@ class SvmPlan(DevicePlan):
     supports_direct = True
     MMAX = 8
     _KERNELS = {"linear": 0, "polynomial": 1, "radialBasis": 2, "sigmoid": 3}
-    _STATE = DevicePlan._STATE + ("in_index", "sv", "sv_norm", "coef", "intercept", "thr", "tgt", "alt", "n_in",
+    _STATE = DevicePlan._STATE + ("target_stage", "in_index", "sv", "sv_norm", "coef", "intercept", "thr", "tgt", "alt", "n_in",
                                   "n_sv", "n_machines", "kernel_code", "classification", "gamma", "coef0", "degree",
                                   "max_wins", "n_classes", "table", "fmax", "n_svp")
 
@@ -602,6 +602,8 @@ class SvmPlan(DevicePlan):
         tgt = np.zeros(self.MMAX, np.int32)
         alt = np.full(self.MMAX, -1, np.int32)
         self.classification = 1 if ev.kind == "classification" else 0
+        # PMML Target of a regression SVM (the oracle applies it to every regression model)
+        self.target_stage = target_post(ev.target, force=True) if not self.classification else None
         if self.classification:
             cats = ev.categories
             if len(cats) > 16:
@@ -635,7 +637,7 @@ class SvmPlan(DevicePlan):
             self.classification
         a.gamma, a.coef0, a.degree = self.gamma, self.coef0, self.degree
         a.max_wins, a.n_classes = self.max_wins, self.n_classes
-        a.epi = _epilogue(mode=EPI_AFFINE, table=self.table)
+        a.epi = _epilogue(mode=EPI_AFFINE, table=self.table, tgt=self.target_stage)
         a.epi.score2, a.epi.valid2 = _addr(score2), _addr(valid2)
         a.score, a.valid, a.decision = _addr(score), _addr(valid), ptr(decision)
         check(self.lib.pmml_svm_launch(stream_handle(stream), ctypes.byref(a), self.fmax,
@@ -665,7 +667,7 @@ class SvmWidePlan(DevicePlan):
     FMAXES = (16, 32, 64, 128)
     CMAX = 256  # packed u16 vote counters: TB x 128 dwords = 128 KiB of LDS
     _KERNELS = SvmPlan._KERNELS
-    _STATE = DevicePlan._STATE + ("in_index", "svA", "coefA", "svnP", "intercept", "thr", "tgt", "alt", "n_in",
+    _STATE = DevicePlan._STATE + ("target_stage", "in_index", "svA", "coefA", "svnP", "intercept", "thr", "tgt", "alt", "n_in",
                                   "n_sv", "n_machines", "kernel_code", "classification", "gamma", "coef0", "degree",
                                   "max_wins", "n_classes", "table", "fmax", "mt", "n_tiles", "n_groups")
 
@@ -691,6 +693,8 @@ class SvmWidePlan(DevicePlan):
         if kind not in self._KERNELS:
             raise NotLowerable(f"SVM kernel {kind!r}")
         self.classification = 1 if ev.kind == "classification" else 0
+        # PMML Target of a regression SVM (the oracle applies it to every regression model)
+        self.target_stage = target_post(ev.target, force=True) if not self.classification else None
         if not self.classification and M != 1:
             raise NotLowerable("regression SVM must have one machine")
         nsv = S.shape[0]
@@ -765,7 +769,7 @@ class SvmWidePlan(DevicePlan):
             self.classification
         a.gamma, a.coef0, a.degree = self.gamma, self.coef0, self.degree
         a.max_wins, a.n_classes = self.max_wins, self.n_classes
-        a.epi = _epilogue(mode=EPI_AFFINE, table=self.table)
+        a.epi = _epilogue(mode=EPI_AFFINE, table=self.table, tgt=self.target_stage)
         a.epi.score2, a.epi.valid2 = _addr(score2), _addr(valid2)
         a.score, a.valid, a.decision = _addr(score), _addr(valid), ptr(decision)
         w.svA, w.coefA, w.svnP = ptr(self.svA), ptr(self.coefA), ptr(self.svnP)
@@ -788,7 +792,7 @@ class SvmGemmPlan(DevicePlan):
     kind = "svm_gemm"
     supports_direct = False
     ROW_CHUNK = 1 << 18  # bounds the [rows, n_sv] kernel matrix
-    _STATE = DevicePlan._STATE + ("in_index", "S", "s_norm", "A", "b", "W_lin", "thr", "vote_t", "vote_a",
+    _STATE = DevicePlan._STATE + ("target_stage", "in_index", "S", "s_norm", "A", "b", "W_lin", "thr", "vote_t", "vote_a",
                                   "kernel_kind", "gamma", "coef0", "degree", "max_wins", "classification",
                                   "table", "coefficients")
 
@@ -821,6 +825,8 @@ class SvmGemmPlan(DevicePlan):
         self.b = self._t(ev.b.astype(np.float32))
         self.max_wins = 1 if sm.max_wins else 0
         self.classification = 1 if ev.kind == "classification" else 0
+        # PMML Target of a regression SVM (the oracle applies it to every regression model)
+        self.target_stage = target_post(ev.target, force=True) if not self.classification else None
         self.table = self.thr = self.vote_t = self.vote_a = None
         if self.classification:
             cats = ev.categories
@@ -881,6 +887,8 @@ class SvmGemmPlan(DevicePlan):
                 else:
                     s = D[:, 0]
                 s = torch.where(ok, s, torch.full_like(s, float("nan")))
+                if not self.classification:
+                    s, ok = apply_target_torch(s, ok, self.target_stage)
                 for so, vo in ((score, valid), (score2, valid2)):
                     if so is not None and not isinstance(so, int):
                         so[lo:hi].copy_(s)

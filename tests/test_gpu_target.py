@@ -70,3 +70,18 @@ def test_mlp_target(gpu, kind):
     plan, agree, _, _ = _cmp(gpu, txt, 8, **opts)
     assert plan.kind == ("mlp" if kind == "fused" else "mlp_gemm")
     assert agree > 0.999
+
+
+@pytest.mark.parametrize("impl", ["fused", "wide", "gemm"])
+@pytest.mark.parametrize("kw", [dict(min=-0.5, max=0.5, factor=10.0, cast="floor"),
+                                dict(factor=3.0, constant=-1.0),
+                                dict(default=7.0, cast="round")], ids=["clip-cast", "rescale", "default"])
+def test_svm_regression_target(gpu, impl, kw):
+    """A regression SVM's Target (clip, rescale, castInteger, TargetValue defaultValue for rows
+    without a prediction) on all three SVM plans — the kernels used to write the raw decision
+    value (the oracle applies the Target to every regression model)."""
+    from flink_jpmml_amd.bench.synth import set_target, svm_pmml
+
+    txt = set_target(svm_pmml(n_features=12, n_sv=64, seed=5, classification=False), **kw)
+    plan, agree, s, ref = _cmp(gpu, txt, 12, missing=0.05, svm_impl=impl)
+    assert agree > 0.999
