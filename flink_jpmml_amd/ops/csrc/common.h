@@ -24,6 +24,7 @@ enum : uint32_t {
   FP_INTEGER = 1u << 9,            // non-integral value is invalid
   FP_CODE_RANGE = 1u << 10,        // categorical codes: valid iff 0 <= x < hi (string vocabularies)
   FP_ROW_INVALID = 1u << 11,       // field definition rejects every value (e.g. Interval on categorical)
+  FP_MISSING_VALUE = 1u << 12,     // x == pad is a missing value (DataField <Value property="missing">)
 };
 
 struct FieldPrep {
@@ -32,7 +33,7 @@ struct FieldPrep {
   float missing_repl;
   float invalid_repl;
   float out_lo, out_hi;  // outlier bounds
-  float pad;
+  float pad;             // FP_MISSING_VALUE: the field's explicit missing value
 };
 static_assert(sizeof(FieldPrep) == 32, "FieldPrep must stay 32 bytes (host mirror in ops/_lib.py)");
 
@@ -41,7 +42,7 @@ __device__ __forceinline__ float prep_value(float x, const FieldPrep& p, bool* b
   const uint32_t fl = p.flags;
   if (fl == 0u) return x;
   if (fl & FP_ROW_INVALID) { *bad = true; return x; }
-  bool miss = (x != x);
+  bool miss = (x != x) || ((fl & FP_MISSING_VALUE) && x == p.pad);
   if (!miss) {
     bool invalid = false;
     if (fl & FP_HAS_INTERVAL) {

@@ -49,6 +49,7 @@ FP_OUTLIER_AS_EXTREME = 1 << 8
 FP_INTEGER = 1 << 9
 FP_CODE_RANGE = 1 << 10
 FP_ROW_INVALID = 1 << 11
+FP_MISSING_VALUE = 1 << 12
 
 EPI_AFFINE, EPI_LOGISTIC2, EPI_ARGMAX, EPI_SOFTMAX, EPI_CUMULATIVE, EPI_LINKMAX = 0, 1, 2, 3, 4, 5
 LINKS = {"none": 0, None: 0, "logit": 1, "exp": 2, "probit": 3, "cloglog": 4, "loglog": 5, "cauchit": 6}
@@ -115,13 +116,23 @@ def build_field_prep(compiled, fields: List[str]) -> Tuple[np.ndarray, bool]:
         out_lo, out_hi = -np.inf, np.inf
         mrepl = math.nan
         irepl = math.nan
+        mval = 0.0
         optype = (mf.optype if mf is not None and mf.optype else None) or (df.optype if df else "continuous")
         constrained = False
         if df is not None:
             if optype != "continuous" and df.intervals:
                 fl |= FP_ROW_INVALID
-            if df.missing_values or df.invalid_values:
-                raise NotLowerable(f"field {name!r}: explicit missing/invalid value lists are host-only")
+            if df.invalid_values or len(df.missing_values) > 1 or (df.missing_values and df.is_string):
+                raise NotLowerable(f"field {name!r}: explicit invalid values / several missing values are host-only")
+            if df.missing_values:  # one numeric missing-value sentinel (e.g. -999): compared in fp32
+                try:
+                    mv = float(df.missing_values[0])
+                except ValueError:
+                    raise NotLowerable(f"field {name!r}: non-numeric missing value") from None
+                if not math.isfinite(mv) or float(np.float32(mv)) != mv:
+                    raise NotLowerable(f"field {name!r}: missing value {mv!r} is not an fp32 number")
+                fl |= FP_MISSING_VALUE
+                mval = mv
             if optype == "continuous" and df.intervals:
                 if len(df.intervals) != 1:
                     raise NotLowerable(f"field {name!r}: multiple validity intervals are host-only")
@@ -176,7 +187,7 @@ def build_field_prep(compiled, fields: List[str]) -> Tuple[np.ndarray, bool]:
         elif constrained:
             fl |= FP_INVALID_RETURN
         flags[j] = fl
-        table[j, 1:7] = [lo, hi, mrepl, irepl, out_lo, out_hi]
+        table[j, 1:8] = [lo, hi, mrepl, irepl, out_lo, out_hi, mval]
         any_prep = any_prep or fl != 0
     raw = table.view(np.uint32).copy()
     raw[:, 0] = flags

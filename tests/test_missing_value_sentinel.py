@@ -1,0 +1,135 @@
+"""A DataField's explicit missing value (``<Value value="-999" property="missing"/>``, the usual
+sentinel of exported numeric columns) on the device: ``build_field_prep`` lowers ONE numeric,
+fp32-exact sentinel into the FieldPrep record (``FP_MISSING_VALUE``, compared in ``prep_value``
+before every other treatment, as ``pmml/fields.py::prepare_matrix`` does); several sentinels, string
+sentinels and invalid-value lists stay host-only (``NotLowerable``, never a plan that ignores them).
+CPU: the lowering decisions; GPU: trees, regression, SVM, k-means and networks (through their
+prepare pass) vs the float64 oracle on inputs that carry the sentinel, with and without a
+missingValueReplacement."""
+
+import re
+
+import numpy as np
+import pytest
+
+from flink_jpmml_amd.runtime.compiled import CompiledPmml
+
+SENT = -999.0
+
+
+def _with_sentinel(txt: str, field: str = "f1", values=("-999",), prop: str = "missing") -> str:
+    child = "".join(f'<Value value="{v}" property="{prop}"/>' for v in values)
+    out, n = re.subn(rf'(<DataField name="{field}"[^>]*?)\s*/>', rf'\1>{child}</DataField>', txt, count=1)
+    assert n == 1
+    return out
+
+
+def _with_replacement(txt: str, field: str = "f1", value: str = "0.3") -> str:
+    out = txt.replace(f'<MiningField name="{field}"/>',
+                      f'<MiningField name="{field}" missingValueReplacement="{value}"/>', 1)
+    assert out != txt
+    return out
+
+
+def _models():
+    from flink_jpmml_amd.bench.synth import (gbdt_pmml, kmeans_pmml, mlp_pmml, random_forest_pmml,
+                                             regression_design_pmml, svm_pmml)
+
+    return {
+        "gbdt": (gbdt_pmml(n_trees=20, depth=5, n_features=6, seed=1), {}),
+        "rf": (random_forest_pmml(n_trees=12, depth=5, n_features=6, n_classes=3, seed=2), {}),
+        "regression": (regression_design_pmml(n_features=6, seed=3), {}),  # + categorical "color" column
+        "svm": (svm_pmml(n_features=6, n_sv=40, seed=4), {}),
+        "kmeans": (kmeans_pmml(n_clusters=9, n_features=6, seed=5), {}),
+        "mlp": (mlp_pmml(n_features=6, hidden=(16,), seed=6), dict(precision="fp32")),
+    }
+
+
+MODELS = _models()
+
+
+def test_sentinel_lowers_into_field_prep():
+    from flink_jpmml_amd.runtime.plans import FP_HAS_MISSING_REPL, FP_MISSING_VALUE, build_field_prep
+
+    txt = _with_replacement(_with_sentinel(MODELS["gbdt"][0]))
+    c = CompiledPmml.from_string(txt)
+    names = [f"f{j}" for j in range(6)]
+    raw, any_prep = build_field_prep(c, names)
+    assert any_prep
+    assert raw[1, 0] & FP_MISSING_VALUE and raw[1, 0] & FP_HAS_MISSING_REPL
+    assert raw[1:2, 7].view(np.float32)[0] == np.float32(SENT)
+    assert not any(raw[j, 0] & FP_MISSING_VALUE for j in (0, 2, 3, 4, 5))
+
+
+@pytest.mark.parametrize("kind", ["two-sentinels", "invalid-list", "not-fp32", "non-numeric"])
+def test_other_value_lists_stay_host_only(kind):
+    from flink_jpmml_amd.runtime.plans import NotLowerable, build_field_prep
+
+    base = MODELS["gbdt"][0]
+    txt = {"two-sentinels": _with_sentinel(base, values=("-999", "-1")),
+           "invalid-list": _with_sentinel(base, values=("7",), prop="invalid"),
+           "not-fp32": _with_sentinel(base, values=("0.1",)),
+           "non-numeric": _with_sentinel(base, values=("NA",))}[kind]
+    c = CompiledPmml.from_string(txt)
+    with pytest.raises(NotLowerable):
+        build_field_prep(c, [f"f{j}" for j in range(6)])
+
+
+@pytest.mark.parametrize("name", list(MODELS))
+def test_every_family_lowers_with_a_sentinel(name):
+    from flink_jpmml_amd.runtime.plans import lowering_dry_run
+
+    txt, opts = MODELS[name]
+    c = CompiledPmml.from_string(_with_sentinel(txt))
+    with lowering_dry_run():
+        plan = c.plan("cpu", **opts)
+    preps = [getattr(plan, "prep", None), getattr(getattr(plan, "inner", None), "prep", None)]
+    assert any(p is not None for p in preps), type(plan).__name__
+
+
+def test_oracle_treats_the_sentinel_as_missing():
+    base = MODELS["gbdt"][0]
+    c0, c1 = CompiledPmml.from_string(base), CompiledPmml.from_string(_with_sentinel(base))
+    X = _inputs(500)
+    Xn = X.copy()
+    Xn[Xn[:, 1] == SENT, 1] = np.nan
+    s1, v1 = c1.score_matrix_oracle(X)
+    s0, v0 = c0.score_matrix_oracle(Xn)
+    assert (v1 == v0).all()
+    np.testing.assert_array_equal(s1[v1], s0[v0])
+
+
+def _inputs(n: int, codes: bool = False) -> np.ndarray:
+    from flink_jpmml_amd.bench.synth import stream_matrix
+
+    X = stream_matrix(n, 6, seed=11, missing_rate=0.02)
+    rng = np.random.default_rng(12)
+    X[rng.random(n) < 0.25, 1] = SENT
+    if codes:  # the regression model's string field, as category codes
+        X = np.concatenate([X, rng.integers(0, 3, (n, 1)).astype(X.dtype)], axis=1)
+    return X
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("repl", [False, True], ids=["missing", "replaced"])
+@pytest.mark.parametrize("name", list(MODELS))
+def test_sentinel_on_gpu(gpu, name, repl):
+    txt, opts = MODELS[name]
+    txt = _with_sentinel(txt)
+    if repl:
+        txt = _with_replacement(txt)
+    c = CompiledPmml.from_string(txt)
+    plan = c.plan(gpu, **opts)
+    preps = [getattr(plan, "prep", None), getattr(getattr(plan, "inner", None), "prep", None)]
+    assert any(p is not None for p in preps), f"{type(plan).__name__} lowered without a FieldPrep table"
+    X = _inputs(5000, codes=name == "regression")
+    s, v = plan.score(X)
+    s, v = s.cpu().numpy().astype(np.float64), v.cpu().numpy().astype(bool)
+    ref, vref = c.score_matrix_oracle(X)
+    assert (v == vref).all()
+    assert v.any()
+    if name in ("rf", "kmeans"):
+        assert (s[v] == ref[v]).mean() >= 0.995
+    else:
+        scale = max(1.0, float(np.abs(ref[v]).max()))
+        np.testing.assert_allclose(s[v], ref[v], rtol=0, atol=2e-4 * scale)
