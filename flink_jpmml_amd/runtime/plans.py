@@ -122,13 +122,21 @@ def build_field_prep(compiled, fields: List[str]) -> Tuple[np.ndarray, bool]:
         if df is not None:
             if optype != "continuous" and df.intervals:
                 fl |= FP_ROW_INVALID
-            if df.invalid_values or len(df.missing_values) > 1 or (df.missing_values and df.is_string):
-                raise NotLowerable(f"field {name!r}: explicit invalid values / several missing values are host-only")
-            if df.missing_values:  # one numeric missing-value sentinel (e.g. -999): compared in fp32
+            if df.invalid_values or (df.missing_values and df.is_string):
+                raise NotLowerable(f"field {name!r}: explicit invalid values / string missing values are host-only")
+            # numeric missing-value sentinels (e.g. -999), compared in fp32; non-numeric ones ("NA")
+            # never reach a numeric matrix (the text parsers read them as missing already, as
+            # pmml/fields.py::prepare_matrix skips them)
+            sentinels = []
+            for txt in df.missing_values:
                 try:
-                    mv = float(df.missing_values[0])
+                    sentinels.append(float(txt))
                 except ValueError:
-                    raise NotLowerable(f"field {name!r}: non-numeric missing value") from None
+                    continue
+            if len(sentinels) > 1:
+                raise NotLowerable(f"field {name!r}: several numeric missing values are host-only")
+            if sentinels:
+                mv = sentinels[0]
                 if not math.isfinite(mv) or float(np.float32(mv)) != mv:
                     raise NotLowerable(f"field {name!r}: missing value {mv!r} is not an fp32 number")
                 fl |= FP_MISSING_VALUE

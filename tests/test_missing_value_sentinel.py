@@ -61,18 +61,34 @@ def test_sentinel_lowers_into_field_prep():
     assert not any(raw[j, 0] & FP_MISSING_VALUE for j in (0, 2, 3, 4, 5))
 
 
-@pytest.mark.parametrize("kind", ["two-sentinels", "invalid-list", "not-fp32", "non-numeric"])
+@pytest.mark.parametrize("kind", ["two-sentinels", "invalid-list", "not-fp32"])
 def test_other_value_lists_stay_host_only(kind):
     from flink_jpmml_amd.runtime.plans import NotLowerable, build_field_prep
 
     base = MODELS["gbdt"][0]
     txt = {"two-sentinels": _with_sentinel(base, values=("-999", "-1")),
            "invalid-list": _with_sentinel(base, values=("7",), prop="invalid"),
-           "not-fp32": _with_sentinel(base, values=("0.1",)),
-           "non-numeric": _with_sentinel(base, values=("NA",))}[kind]
+           "not-fp32": _with_sentinel(base, values=("0.1",))}[kind]
     c = CompiledPmml.from_string(txt)
     with pytest.raises(NotLowerable):
         build_field_prep(c, [f"f{j}" for j in range(6)])
+
+
+@pytest.mark.parametrize("values,flagged", [(("NA",), False), (("NA", "-999", "?"), True)])
+def test_non_numeric_missing_values_are_ignored_on_numeric_fields(values, flagged):
+    """A numeric matrix cannot hold "NA": like the oracle's prepare_matrix, only the numeric
+    sentinel takes part."""
+    from flink_jpmml_amd.runtime.plans import FP_MISSING_VALUE, build_field_prep
+
+    c = CompiledPmml.from_string(_with_sentinel(MODELS["gbdt"][0], values=values))
+    raw, _ = build_field_prep(c, [f"f{j}" for j in range(6)])
+    assert bool(raw[1, 0] & FP_MISSING_VALUE) == flagged
+    X = _inputs(400)
+    ref, vref = c.score_matrix_oracle(X)
+    c0 = CompiledPmml.from_string(_with_sentinel(MODELS["gbdt"][0], values=("-999",) if flagged else ()))
+    ref0, vref0 = c0.score_matrix_oracle(X)
+    assert (vref == vref0).all()
+    np.testing.assert_array_equal(ref[vref], ref0[vref0])
 
 
 @pytest.mark.parametrize("name", list(MODELS))
