@@ -168,8 +168,21 @@ def build_field_prep(compiled, fields: List[str]) -> Tuple[np.ndarray, bool]:
                 fl |= FP_CODE_RANGE
                 hi = float(len(df.values))
                 constrained = True
+            elif df.values and optype != "continuous":
+                # label-encoded numeric categories: a contiguous run of integers is "integral and
+                # inside [min, max]" (the oracle's set test); other sets stay host-only
+                try:
+                    vals = sorted({float(v) for v in df.values})
+                except ValueError:
+                    raise NotLowerable(f"field {name!r}: non-numeric valid value on a numeric field") from None
+                if not all(v == math.floor(v) and abs(v) < 2 ** 24 for v in vals) or \
+                        vals[-1] - vals[0] != len(vals) - 1:
+                    raise NotLowerable(f"field {name!r}: numeric valid values are not a contiguous integer run")
+                fl |= FP_HAS_INTERVAL | FP_INTEGER
+                lo, hi = vals[0], vals[-1]
+                constrained = True
             elif df.values:
-                raise NotLowerable(f"field {name!r}: numeric valid-value lists are host-only")
+                raise NotLowerable(f"field {name!r}: numeric valid-value lists on a continuous field are host-only")
             if df.data_type == "integer":
                 fl |= FP_INTEGER
                 constrained = True

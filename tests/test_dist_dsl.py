@@ -235,7 +235,7 @@ def job_timed_exactly_once(kmeans, out_dir, ck_dir, restore):
     ev = [DynamicInput(f"{N1}_1", (1.0 + (i % 7) / 3, 2.0, 3.0, 1.0), occurred_on=i) for i in range(60)]
     env = StreamExecutionEnvironment.get_execution_environment()
     env.enable_checkpointing(interval_ms=40, directory=ck_dir)
-    events = env.add_source(PacedShardSource(ev, 0.004), uid="events")
+    events = env.add_source(PacedShardSource(ev, 0.008), uid="events")  # kill at 20 ≈ 160 ms: several 40 ms checkpoints even on a loaded host
     control = env.from_collection([AddMessage(N1, 1, kmeans, 0)], uid="control")
     events.with_support_stream(control).evaluate(
         lambda e, m: [e.occurred_on, m.predict(e.to_vector()).value.get_or_else(-1.0)], uid="scorer"

@@ -5,7 +5,9 @@ before every other treatment, as ``pmml/fields.py::prepare_matrix`` does); sever
 sentinels and invalid-value lists stay host-only (``NotLowerable``, never a plan that ignores them).
 CPU: the lowering decisions; GPU: trees, regression, SVM, k-means and networks (through their
 prepare pass) vs the float64 oracle on inputs that carry the sentinel, with and without a
-missingValueReplacement."""
+missingValueReplacement. Also numeric categorical valid-value lists (label-encoded categories):
+a contiguous integer run lowers to "integral and inside [min, max]" under every
+invalidValueTreatment; other sets stay host-only."""
 
 import re
 
@@ -149,3 +151,54 @@ def test_sentinel_on_gpu(gpu, name, repl):
     else:
         scale = max(1.0, float(np.abs(ref[v]).max()))
         np.testing.assert_allclose(s[v], ref[v], rtol=0, atol=2e-4 * scale)
+
+
+def _categorical(txt: str, values=("0", "1", "2", "3"), treat: str = "returnInvalid") -> str:
+    child = "".join(f'<Value value="{v}"/>' for v in values)
+    out, n = re.subn(r'<DataField name="f1"[^>]*/>',
+                     f'<DataField name="f1" optype="categorical" dataType="integer">{child}</DataField>', txt, count=1)
+    assert n == 1
+    extra = ' invalidValueReplacement="2"' if treat == "asValue" else ""
+    return out.replace('<MiningField name="f1"/>', f'<MiningField name="f1" invalidValueTreatment="{treat}"{extra}/>', 1)
+
+
+def _categorical_inputs(n: int, codes: bool = False) -> np.ndarray:
+    X = _inputs(n, codes)
+    X[:, 1] = np.random.default_rng(13).choice([0, 1, 2, 3, 4, -1, 1.5, np.nan], n)
+    return X
+
+
+def test_integer_category_run_lowers_to_interval_and_integer():
+    from flink_jpmml_amd.runtime.plans import FP_HAS_INTERVAL, FP_INTEGER, FP_INVALID_AS_MISSING, build_field_prep
+
+    c = CompiledPmml.from_string(_categorical(MODELS["gbdt"][0], values=("3", "1", "2", "0"), treat="asMissing"))
+    raw, _ = build_field_prep(c, [f"f{j}" for j in range(6)])
+    assert raw[1, 0] & (FP_HAS_INTERVAL | FP_INTEGER | FP_INVALID_AS_MISSING) == \
+        FP_HAS_INTERVAL | FP_INTEGER | FP_INVALID_AS_MISSING
+    assert list(raw[1:2, 1:3].view(np.float32)[0]) == [0.0, 3.0]
+
+
+@pytest.mark.parametrize("values", [("0", "2", "5"), ("0.5", "1.5"), ("a", "1")])
+def test_other_numeric_category_sets_stay_host_only(values):
+    from flink_jpmml_amd.runtime.plans import NotLowerable, build_field_prep
+
+    c = CompiledPmml.from_string(_categorical(MODELS["gbdt"][0], values=values))
+    with pytest.raises(NotLowerable):
+        build_field_prep(c, [f"f{j}" for j in range(6)])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("treat", ["returnInvalid", "asMissing", "asIs", "asValue"])
+@pytest.mark.parametrize("name", ["gbdt", "svm", "mlp"])
+def test_integer_categories_on_gpu(gpu, name, treat):
+    txt, opts = MODELS[name]
+    c = CompiledPmml.from_string(_categorical(txt, treat=treat))
+    plan = c.plan(gpu, **opts)
+    X = _categorical_inputs(4000)
+    s, v = plan.score(X)
+    s, v = s.cpu().numpy().astype(np.float64), v.cpu().numpy().astype(bool)
+    ref, vref = c.score_matrix_oracle(X)
+    assert (v == vref).all()
+    assert v.any()
+    scale = max(1.0, float(np.abs(ref[v]).max()))
+    np.testing.assert_allclose(s[v], ref[v], rtol=0, atol=2e-4 * scale)

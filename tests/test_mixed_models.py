@@ -7,6 +7,7 @@ time (native dictionary encoding + counting sort) and, on a GPU, scored in one g
 (``runtime/grouped.py``, GPU tests below). Every row must equal the per-record prediction of its
 own model."""
 
+import math
 import time
 
 import numpy as np
@@ -39,10 +40,12 @@ def test_group_rows_is_linear_and_exact():
     ids = [f"{u}_1" for u in UUIDS]
     n = 1 << 20
     col = np.array(ids, dtype=object)[rng.integers(0, len(ids), n)]
-    b = RecordBatch(np.zeros((n, 2), np.float32), model_ids=col)
-    t = time.perf_counter()
-    keys, perm, starts = b.group_rows()
-    dt = time.perf_counter() - t
+    dt = math.inf
+    for _ in range(3):  # best of 3 (fresh batches: id codes are cached): a loaded host must not fail the rate check
+        b = RecordBatch(np.zeros((n, 2), np.float32), model_ids=col)
+        t = time.perf_counter()
+        keys, perm, starts = b.group_rows()
+        dt = min(dt, time.perf_counter() - t)
     assert sorted(keys) == sorted(ids) and starts[-1] == n
     for k, key in enumerate(keys):
         rows = perm[starts[k]:starts[k + 1]]
