@@ -25,6 +25,8 @@ enum : uint32_t {
   FP_CODE_RANGE = 1u << 10,        // categorical codes: valid iff 0 <= x < hi (string vocabularies)
   FP_ROW_INVALID = 1u << 11,       // field definition rejects every value (e.g. Interval on categorical)
   FP_MISSING_VALUE = 1u << 12,     // x == pad is a missing value (DataField <Value property="missing">)
+  FP_VALUE_MASK = 1u << 13,        // numeric categories: valid iff x integral, lo <= x < lo + 64 and
+                                   // bit (x - lo) of the 64-bit mask in the out_lo / out_hi words
 };
 
 struct FieldPrep {
@@ -32,7 +34,7 @@ struct FieldPrep {
   float lo, hi;          // validity interval (or code range in hi)
   float missing_repl;
   float invalid_repl;
-  float out_lo, out_hi;  // outlier bounds
+  float out_lo, out_hi;  // outlier bounds (continuous) / FP_VALUE_MASK bits 0-31, 32-63 (categorical)
   float pad;             // FP_MISSING_VALUE: the field's explicit missing value
 };
 static_assert(sizeof(FieldPrep) == 32, "FieldPrep must stay 32 bytes (host mirror in ops/_lib.py)");
@@ -52,6 +54,15 @@ __device__ __forceinline__ float prep_value(float x, const FieldPrep& p, bool* b
     }
     if (fl & FP_CODE_RANGE) invalid = invalid || !(x >= 0.f && x < p.hi);
     if (fl & FP_INTEGER) invalid = invalid || (floorf(x) != x);
+    if (fl & FP_VALUE_MASK) {
+      const float d = x - p.lo;
+      bool in = d >= 0.f && d < 64.f && floorf(x) == x;
+      if (in) {
+        const int k = (int)d;
+        in = (__float_as_uint(k < 32 ? p.out_lo : p.out_hi) >> (k & 31)) & 1u;
+      }
+      invalid = invalid || !in;
+    }
     if (invalid) {
       if (fl & FP_INVALID_RETURN) *bad = true;
       else if (fl & FP_INVALID_AS_MISSING) miss = true;

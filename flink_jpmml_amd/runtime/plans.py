@@ -50,6 +50,7 @@ FP_INTEGER = 1 << 9
 FP_CODE_RANGE = 1 << 10
 FP_ROW_INVALID = 1 << 11
 FP_MISSING_VALUE = 1 << 12
+FP_VALUE_MASK = 1 << 13
 
 EPI_AFFINE, EPI_LOGISTIC2, EPI_ARGMAX, EPI_SOFTMAX, EPI_CUMULATIVE, EPI_LINKMAX = 0, 1, 2, 3, 4, 5
 LINKS = {"none": 0, None: 0, "logit": 1, "exp": 2, "probit": 3, "cloglog": 4, "loglog": 5, "cauchit": 6}
@@ -108,6 +109,7 @@ def build_field_prep(compiled, fields: List[str]) -> Tuple[np.ndarray, bool]:
     table = np.zeros((len(fields), 8), dtype=np.float32)
     flags = np.zeros(len(fields), dtype=np.uint32)
     any_prep = False
+    masks = {}  # field -> (bits 0-31, bits 32-63) of an FP_VALUE_MASK set, written as raw words
     for j, name in enumerate(fields):
         df = schema.data_fields.get(name)
         mf = compiled.mining_fields.get(name)
@@ -175,11 +177,18 @@ def build_field_prep(compiled, fields: List[str]) -> Tuple[np.ndarray, bool]:
                     vals = sorted({float(v) for v in df.values})
                 except ValueError:
                     raise NotLowerable(f"field {name!r}: non-numeric valid value on a numeric field") from None
-                if not all(v == math.floor(v) and abs(v) < 2 ** 24 for v in vals) or \
-                        vals[-1] - vals[0] != len(vals) - 1:
-                    raise NotLowerable(f"field {name!r}: numeric valid values are not a contiguous integer run")
-                fl |= FP_HAS_INTERVAL | FP_INTEGER
-                lo, hi = vals[0], vals[-1]
+                if not all(v == math.floor(v) and abs(v) < 2 ** 24 for v in vals):
+                    raise NotLowerable(f"field {name!r}: non-integral numeric valid values are host-only")
+                if vals[-1] - vals[0] == len(vals) - 1:
+                    fl |= FP_HAS_INTERVAL | FP_INTEGER
+                    lo, hi = vals[0], vals[-1]
+                elif vals[-1] - vals[0] < 64:  # a sparse set within 64 consecutive integers: bit mask
+                    fl |= FP_VALUE_MASK
+                    lo = vals[0]
+                    bits = sum(1 << int(v - lo) for v in vals)
+                    masks[j] = (bits & 0xFFFFFFFF, bits >> 32)
+                else:
+                    raise NotLowerable(f"field {name!r}: numeric valid values span more than 64 integers")
                 constrained = True
             elif df.values:
                 raise NotLowerable(f"field {name!r}: numeric valid-value lists on a continuous field are host-only")
@@ -212,6 +221,8 @@ def build_field_prep(compiled, fields: List[str]) -> Tuple[np.ndarray, bool]:
         any_prep = any_prep or fl != 0
     raw = table.view(np.uint32).copy()
     raw[:, 0] = flags
+    for j, (w0, w1) in masks.items():
+        raw[j, 5], raw[j, 6] = w0, w1
     return raw, any_prep
 
 
@@ -1666,7 +1677,7 @@ class TreePlan(DevicePlan):
         prep, _ = build_field_prep(compiled, compiled.active_fields) if compiled.active_fields else (None, False)
         if prep is not None:
             for j in range(len(compiled.active_fields)):
-                if prep[j, 0] & (FP_INVALID_RETURN | FP_ROW_INVALID | FP_INTEGER | FP_CODE_RANGE | FP_HAS_INTERVAL):
+                if prep[j, 0] & (FP_INVALID_RETURN | FP_ROW_INVALID | FP_INTEGER | FP_CODE_RANGE | FP_HAS_INTERVAL | FP_VALUE_MASK):
                     used.add(j)
         return sorted(used) if used else [0]
 

@@ -1,6 +1,6 @@
 set -o pipefail
-# r5ai: label-encoded integer categories (contiguous runs, 64-wide bit masks) + sentinels on the device
-O=gpurun_out/r5ai
+# r5aj: label-encoded integer categories (contiguous runs, 64-wide bit masks) + sentinels on the device
+O=gpurun_out/r5aj
 mkdir -p $O
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 timeout -k 10 400 python -u -m pytest tests/test_field_value_lists.py tests/test_nn_field_prep.py tests/test_design.py -m gpu -x -q --timeout 200 --timeout-method thread -rf > $O/pytest.log 2>&1 || { tail -60 $O/pytest.log; exit 1; }

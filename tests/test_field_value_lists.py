@@ -6,8 +6,9 @@ sentinels and invalid-value lists stay host-only (``NotLowerable``, never a plan
 CPU: the lowering decisions; GPU: trees, regression, SVM, k-means and networks (through their
 prepare pass) vs the float64 oracle on inputs that carry the sentinel, with and without a
 missingValueReplacement. Also numeric categorical valid-value lists (label-encoded categories):
-a contiguous integer run lowers to "integral and inside [min, max]" under every
-invalidValueTreatment; other sets stay host-only."""
+a contiguous integer run lowers to "integral and inside [min, max]", a sparse set within 64
+consecutive integers to a bit mask (``FP_VALUE_MASK``), under every invalidValueTreatment; other
+sets stay host-only."""
 
 import re
 
@@ -164,7 +165,7 @@ def _categorical(txt: str, values=("0", "1", "2", "3"), treat: str = "returnInva
 
 def _categorical_inputs(n: int, codes: bool = False) -> np.ndarray:
     X = _inputs(n, codes)
-    X[:, 1] = np.random.default_rng(13).choice([0, 1, 2, 3, 4, -1, 1.5, np.nan], n)
+    X[:, 1] = np.random.default_rng(13).choice([0, 1, 2, 3, 4, -1, 1.5, 50, 51, -2, np.nan], n)
     return X
 
 
@@ -178,7 +179,40 @@ def test_integer_category_run_lowers_to_interval_and_integer():
     assert list(raw[1:2, 1:3].view(np.float32)[0]) == [0.0, 3.0]
 
 
-@pytest.mark.parametrize("values", [("0", "2", "5"), ("0.5", "1.5"), ("a", "1")])
+def test_sparse_integer_category_set_lowers_to_a_bit_mask():
+    from flink_jpmml_amd.runtime.plans import FP_VALUE_MASK, build_field_prep
+
+    c = CompiledPmml.from_string(_categorical(MODELS["gbdt"][0], values=("-3", "0", "2", "40", "60")))
+    raw, _ = build_field_prep(c, [f"f{j}" for j in range(6)])
+    assert raw[1, 0] & FP_VALUE_MASK
+    assert raw[1:2, 1].view(np.float32)[0] == -3.0
+    bits = int(raw[1, 5]) | (int(raw[1, 6]) << 32)
+    assert bits == sum(1 << (v + 3) for v in (-3, 0, 2, 40, 60))
+
+
+def _mask_model_valid(x: np.ndarray, lo: float, bits: int) -> np.ndarray:
+    """Line-for-line model of prep_value's FP_VALUE_MASK test (fp32)."""
+    x = x.astype(np.float32)
+    d = x - np.float32(lo)
+    ok = (d >= 0) & (d < 64) & (np.floor(x) == x)
+    k = np.where(ok, d, 0).astype(np.uint64)
+    return ok & (((np.uint64(bits) >> k) & np.uint64(1)) == 1)
+
+
+def test_value_mask_model_matches_the_oracle_validity():
+    values = ("-3", "0", "2", "40", "60")
+    c = CompiledPmml.from_string(_categorical(MODELS["gbdt"][0], values=values))
+    X = _inputs(3000)
+    X[:, 1] = np.random.default_rng(5).choice([-4, -3, -2.5, 0, 1, 2, 39, 40, 60, 61, 70, np.nan], 3000)
+    _, vref = c.score_matrix_oracle(X)
+    bits = sum(1 << (int(v) + 3) for v in values)
+    miss_elsewhere = np.isnan(X).any(axis=1) & ~np.isnan(X[:, 1])
+    model = _mask_model_valid(X[:, 1], -3.0, bits) | np.isnan(X[:, 1])
+    # the GBDT scores rows with other missing features too; only f1's validity decides here
+    assert (vref[~miss_elsewhere] == model[~miss_elsewhere]).all()
+
+
+@pytest.mark.parametrize("values", [("0", "100"), ("0.5", "1.5"), ("a", "1")])
 def test_other_numeric_category_sets_stay_host_only(values):
     from flink_jpmml_amd.runtime.plans import NotLowerable, build_field_prep
 
@@ -188,11 +222,12 @@ def test_other_numeric_category_sets_stay_host_only(values):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("values", [("0", "1", "2", "3"), ("-1", "1", "3", "50")], ids=["run", "mask"])
 @pytest.mark.parametrize("treat", ["returnInvalid", "asMissing", "asIs", "asValue"])
 @pytest.mark.parametrize("name", ["gbdt", "svm", "mlp"])
-def test_integer_categories_on_gpu(gpu, name, treat):
+def test_integer_categories_on_gpu(gpu, name, treat, values):
     txt, opts = MODELS[name]
-    c = CompiledPmml.from_string(_categorical(txt, treat=treat))
+    c = CompiledPmml.from_string(_categorical(txt, values=values, treat=treat))
     plan = c.plan(gpu, **opts)
     X = _categorical_inputs(4000)
     s, v = plan.score(X)
