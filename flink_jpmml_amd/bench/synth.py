@@ -445,23 +445,30 @@ def regression_design_pmml(n_features: int = 4, classes: int = 0, normalization:
 
 
 def glm_pmml(model_type: str = "generalizedLinear", link: str = "log", n_features: int = 3, seed: int = 0,
-             classes: int = 3) -> str:
+             classes: int = 3, binomial: Optional[str] = None, event_cells: bool = True) -> str:
     """``GeneralRegressionModel`` (PPMatrix / ParamMatrix) with covariates ``f*`` (one squared),
     factor ``color`` and a covariate x factor interaction. ``multinomialLogistic`` gets
     ``classes`` categories, the last one the reference; ``ordinalMultinomial`` gets ``classes``
     ordered categories, one increasing cut point (``p0``) per category but the last, the other
-    parameters shared, and ``link`` as its ``cumulativeLink``."""
+    parameters shared, and ``link`` as its ``cumulativeLink``. ``binomial`` ("first" / "last" /
+    "default"): a classification ``generalizedLinear`` over categories "0" / "1" whose reference "0"
+    is listed first, last, or left to the default (no attribute); ``event_cells`` puts the event's
+    targetCategory on the PCells (else the cells carry none)."""
     rng = np.random.default_rng(seed)
     out = io.StringIO()
     _header(out, f"synthetic GLM {model_type} {link}")
     ordinal = model_type == "ordinalMultinomial"
     multi = model_type == "multinomialLogistic" or ordinal
     cats = [str(c) for c in range(classes)] if multi else None
+    if binomial:
+        cats = ["0", "1"] if binomial == "first" else ["1", "0"]  # reference "0" (numeric labels: Score values)
     _mixed_dictionary(out, n_features, "y", cats)
-    fn = "classification" if multi else "regression"
+    fn = "classification" if multi or binomial else "regression"
     attrs = f' targetReferenceCategory="{classes - 1}"' if multi else f' linkFunction="{link}"'
     if ordinal:
         attrs = f' cumulativeLink="{link}"'
+    if binomial in ("first", "last"):
+        attrs += ' targetReferenceCategory="0"'
     if link == "power" and not multi:
         attrs += ' linkParameter="0"'
     out.write(f' <GeneralRegressionModel functionName="{fn}" modelType="{model_type}"{attrs} '
@@ -487,7 +494,7 @@ def glm_pmml(model_type: str = "generalizedLinear", link: str = "log", n_feature
             out.write(f'   <PCell parameterName="p0" targetCategory="{c}" beta="{cut:.6g}"/>\n')
         for p in params[1:]:
             out.write(f'   <PCell parameterName="{p}" beta="{rng.normal() * 0.5:.6g}"/>\n')
-    for c in ([] if ordinal else cats[:-1] if multi else [None]):
+    for c in ([] if ordinal else cats[:-1] if multi else ["1" if event_cells else None] if binomial else [None]):
         tc = f' targetCategory="{c}"' if c is not None else ""
         for p in params:
             out.write(f'   <PCell parameterName="{p}"{tc} beta="{rng.normal() * 0.3:.6g}"/>\n')

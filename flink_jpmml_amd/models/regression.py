@@ -175,7 +175,8 @@ class RegressionEvaluator(ModelEvaluator):
 
 class GeneralRegressionEvaluator(ModelEvaluator):
     """GeneralRegressionModel for ``regression``, ``generalLinear``, ``generalizedLinear``
-    (identity/log/logit/probit/cloglog/power links), ``multinomialLogistic`` and
+    (identity/log/logit/probit/cloglog/loglog/power links; as a binomial classifier too),
+    ``multinomialLogistic`` and
     ``ordinalMultinomial`` (cumulative logit/probit/cloglog/loglog/cauchit). Parity unpinned (no
     JPMML here): follows the PMML 4.4 GeneralRegression text."""
 
@@ -240,8 +241,8 @@ class GeneralRegressionEvaluator(ModelEvaluator):
                 y = 1.0 / (1.0 + np.exp(-eta))
             elif lf == "probit":
                 y = link("probit", eta)
-            elif lf == "cloglog":
-                y = link("cloglog", eta)
+            elif lf in ("cloglog", "loglog"):
+                y = link(lf, eta)
             elif lf == "power":
                 p = gm.link_power if gm.link_power is not None else 1.0
                 y = np.exp(eta) if p == 0 else np.power(eta, 1.0 / p)
@@ -252,6 +253,8 @@ class GeneralRegressionEvaluator(ModelEvaluator):
         n = cols.n
         if gm.model_type == "ordinalMultinomial":
             return self._ordinal(cols)
+        if gm.model_type == "generalizedLinear":
+            return self._binomial(cols)
         etas = np.zeros((n, len(cats)))
         miss = np.zeros(n, dtype=bool)
         for k, c in enumerate(cats):
@@ -268,6 +271,41 @@ class GeneralRegressionEvaluator(ModelEvaluator):
             raise UnsupportedFeatureException(f"classification GeneralRegressionModel {gm.model_type!r}")
         lab = np.argmax(P, axis=1).astype(np.float64)
         ok = ~miss
+        return ModelResult("classification", np.where(ok, lab, NAN), ok, categories=cats,
+                           probs=np.where(ok[:, None], P, NAN))
+
+    def binomial_roles(self) -> tuple:
+        """``(reference, event)`` categories of a classification ``generalizedLinear`` model: exactly
+        two categories; the reference is ``targetReferenceCategory`` (default: the last one)."""
+        cats = self.categories
+        if len(cats) != 2:
+            raise UnsupportedFeatureException(f"classification generalizedLinear needs 2 categories, got {len(cats)}")
+        ref = self.gm.target_reference_category if self.gm.target_reference_category is not None else cats[-1]
+        if ref not in cats:
+            raise UnsupportedFeatureException(f"targetReferenceCategory {ref!r} is not a target category")
+        return ref, cats[1] if cats[0] == ref else cats[0]
+
+    def _binomial(self, cols: Columns) -> ModelResult:
+        """Classification ``generalizedLinear`` (binomial GLM): ``P(event) = F(η)`` with F the
+        inverse ``linkFunction`` and η over the event category's PCells plus the cells without a
+        targetCategory (exports use one or the other); the reference category takes ``1 − P``."""
+        gm = self.gm
+        cats = self.categories
+        ref, event = self.binomial_roles()
+        lf = gm.link_function or "logit"
+        names = {"logit": "logit", "probit": "probit", "cloglog": "cloglog", "loglog": "loglog", "identity": "none"}
+        if lf not in names:
+            raise UnsupportedFeatureException(f"classification generalizedLinear linkFunction {lf!r}")
+        eta, miss = self._linear(cols, event)
+        if any(tc is None for _, tc, _ in gm.p_cells):
+            e0, m0 = self._linear(cols, None)
+            eta, miss = eta + e0 - gm.offset_value, miss | m0  # offset counted once
+        p = link(names[lf], eta)
+        P = np.empty((cols.n, 2))
+        P[:, cats.index(event)] = p
+        P[:, cats.index(ref)] = 1.0 - p
+        lab = np.argmax(np.nan_to_num(P, nan=-np.inf), axis=1).astype(np.float64)
+        ok = ~miss & np.isfinite(P).all(axis=1)
         return ModelResult("classification", np.where(ok, lab, NAN), ok, categories=cats,
                            probs=np.where(ok[:, None], P, NAN))
 

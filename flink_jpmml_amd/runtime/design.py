@@ -31,7 +31,9 @@ from ..pmml import ir
 from .plans import NotLowerable
 
 _GLM_LINKS = {None: "none", "identity": "none", "log": "exp", "logit": "logit", "probit": "probit",
-              "cloglog": "cloglog"}
+              "cloglog": "cloglog", "loglog": "loglog"}
+# binomial GLM with the reference category FIRST: P(ref) = 1 - F(η) = F'(-η)
+_MIRRORED = {"logit": "logit", "probit": "probit", "cloglog": "loglog", "loglog": "cloglog"}
 
 
 class _Design:
@@ -147,6 +149,31 @@ def _glm_tables(ev: GeneralRegressionEvaluator, d: _Design) -> Tuple[List[ir.Reg
                                            [ir.NumericPredictor(n, w) for n, w in coef.items()]))
         tabs.append(ir.RegressionTable(0.0, ev.categories[-1], []))
         return tabs, f"cumulative:{gm.cumulative_link or 'logit'}"
+    if gm.model_type == "generalizedLinear":
+        # binomial: the PMML two-table rule p0 = F(y0), p1 = 1 - p0 (LinearPlan's EPI_LOGISTIC2)
+        # with the tables in category order; a reference category listed first gets y0 = -η
+        # through the mirrored link (identity: y0 = 1 - η)
+        ref, event = ev.binomial_roles()
+        lf = gm.link_function or "logit"
+        if lf not in _MIRRORED and lf != "identity":
+            raise NotLowerable(f"classification generalizedLinear linkFunction {lf!r} is host-only")
+        own, shared = table(event), table(None)
+        coef: Dict[str, float] = {}
+        for p in own.numeric + shared.numeric:
+            coef[p.name] = coef.get(p.name, 0.0) + p.coefficient
+        icpt = own.intercept + (shared.intercept - gm.offset_value if any(tc is None for _, tc, _ in gm.p_cells)
+                                else 0.0)
+        if ev.categories[0] == event:
+            first = ir.RegressionTable(icpt, event, [ir.NumericPredictor(n, w) for n, w in coef.items()])
+            norm = _GLM_LINKS[lf]
+        elif lf == "identity":
+            first = ir.RegressionTable(1.0 - icpt, ref, [ir.NumericPredictor(n, -w) for n, w in coef.items()])
+            norm = "none"
+        else:
+            first = ir.RegressionTable(-icpt, ref, [ir.NumericPredictor(n, -w) for n, w in coef.items()])
+            norm = _MIRRORED[lf]
+        second = ir.RegressionTable(0.0, ev.categories[1], [])
+        return [first, second], norm
     if gm.model_type != "multinomialLogistic":
         raise NotLowerable(f"classification GeneralRegressionModel {gm.model_type!r} is host-only")
     tabs = []

@@ -34,6 +34,14 @@ CASES = {
     "glm-ordinal-cloglog": lambda: glm_pmml(model_type="ordinalMultinomial", link="cloglog", classes=5, seed=3),
     "glm-ordinal-loglog": lambda: glm_pmml(model_type="ordinalMultinomial", link="loglog", seed=4),
     "glm-ordinal-cauchit": lambda: glm_pmml(model_type="ordinalMultinomial", link="cauchit", seed=5),
+    # binomial GLM (classification generalizedLinear): P(event) = F(η), the reference 1 - P;
+    # reference listed first (mirrored link in the lowering), last, or by default
+    "glm-binomial-logit-first": lambda: glm_pmml(link="logit", binomial="first", seed=6),
+    "glm-binomial-probit-last": lambda: glm_pmml(link="probit", binomial="last", seed=7),
+    "glm-binomial-cloglog-first": lambda: glm_pmml(link="cloglog", binomial="first", seed=8, event_cells=False),
+    "glm-binomial-loglog-default": lambda: glm_pmml(link="loglog", binomial="default", seed=9),
+    "glm-binomial-loglog-first": lambda: glm_pmml(link="loglog", binomial="first", seed=10),
+    "glm-binomial-identity-first": lambda: glm_pmml(link="identity", binomial="first", seed=11),
     "naive-bayes": lambda: naive_bayes_pmml(),
     "naive-bayes-2": lambda: naive_bayes_pmml(classes=2, seed=3),
 }
@@ -61,10 +69,43 @@ def test_design_program_matches_oracle(name):
     res = dense.finish(D @ W + b, ok & ~np.isnan(D).any(axis=1))
     ref, vref = c.score_matrix_oracle(X)
     assert (res.valid == vref).all()
-    if res.kind == "classification":  # categories are "0".."K-1": the index is the label
-        assert (res.value[vref] == ref[vref]).mean() > 0.999
+    if res.kind == "classification":  # numeric category labels: the score is the label's value
+        labels = np.array([float(k) for k in res.categories])
+        assert (labels[res.value[vref].astype(int)] == ref[vref]).mean() > 0.999
+        full = c.result(X)  # class probabilities in category order (mirrored binomial tables too)
+        assert list(full.categories) == list(res.categories)
+        np.testing.assert_allclose(res.probs[vref], full.probs[vref], rtol=1e-5, atol=1e-6)  # fp32 design columns
     else:
         assert np.allclose(res.value[vref], ref[vref], rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("ref", ["first", "last", "default"])
+@pytest.mark.parametrize("event_cells", [True, False])
+def test_binomial_glm_oracle_by_hand(ref, event_cells):
+    """P("1") = logistic(offset + Σ β·design), P("0") (the reference) = 1 − P("1"); the label is
+    the larger one."""
+    c = CompiledPmml.from_string(glm_pmml(link="logit", binomial=ref, event_cells=event_cells, seed=3))
+    ev = c.evaluator
+    assert ev.binomial_roles() == ("0", "1")
+    gm = ev.gm
+    beta = {p: b for p, _, b in gm.p_cells}
+    _, X = mixed_records(40, 3, seed=12, missing_rate=0.1)
+    res = c.result(X)
+    cats = ev.categories
+    levels = c.schema.data_fields["color"].values
+    for r in range(len(X)):
+        f0, f1, f2, code = X[r]
+        if np.isnan([f0, f1, f2]).any():
+            assert not res.valid[r]
+            continue
+        color = levels[int(code)] if not np.isnan(code) else None
+        eta = gm.offset_value + beta["p0"] + beta["p1"] * f0 + beta["p2"] * f1 ** 2 + beta["p3"] * f2
+        eta += beta["pc1"] * (color == "red") + beta["pc2"] * (color == "green") + beta["px"] * (color == "blue") * f0
+        p_yes = 1.0 / (1.0 + np.exp(-eta))
+        assert res.valid[r]
+        assert np.isclose(res.probs[r, cats.index("1")], p_yes, rtol=1e-12)
+        assert np.isclose(res.probs[r, cats.index("0")], 1.0 - p_yes, rtol=1e-12)
+        assert res.value[r] == (cats.index("1") if p_yes > 0.5 else cats.index("0"))
 
 
 def test_ordinal_glm_oracle_by_hand():
