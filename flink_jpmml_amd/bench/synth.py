@@ -581,9 +581,12 @@ def ruleset_pmml(n_features: int = 4, n_rules: int = 12, criterion: str = "first
     return out.getvalue()
 
 
-def naive_bayes_pmml(n_features: int = 4, classes: int = 3, seed: int = 0, threshold: float = 0.001) -> str:
+def naive_bayes_pmml(n_features: int = 4, classes: int = 3, seed: int = 0, threshold: float = 0.001,
+                     discretized: Optional[str] = None) -> str:
     """``NaiveBayesModel``: Gaussian ``f*`` inputs and the categorical ``color`` (one level never
-    seen with class 0: exercises the threshold)."""
+    seen with class 0: exercises the threshold). ``discretized``: the last ``f`` input becomes
+    three Discretize bins with PairCounts — ``"inline"`` as the BayesInput's own DerivedField,
+    ``"local"`` as a LocalTransformations field ``fbin`` the BayesInput names."""
     rng = np.random.default_rng(seed)
     out = io.StringIO()
     _header(out, "synthetic naive Bayes")
@@ -591,9 +594,28 @@ def naive_bayes_pmml(n_features: int = 4, classes: int = 3, seed: int = 0, thres
     _mixed_dictionary(out, n_features, "y", cats)
     out.write(f' <NaiveBayesModel functionName="classification" threshold="{threshold}">\n')
     _mixed_schema(out, n_features, "y")
+    last = n_features - 1
+    disc = (f'<Discretize field="f{last}"><DiscretizeBin binValue="low"><Interval closure="openOpen" '
+            'rightMargin="-0.5"/></DiscretizeBin><DiscretizeBin binValue="mid"><Interval closure="closedOpen" '
+            'leftMargin="-0.5" rightMargin="0.5"/></DiscretizeBin><DiscretizeBin binValue="high"><Interval '
+            'closure="closedOpen" leftMargin="0.5"/></DiscretizeBin></Discretize>')
+    if discretized == "local":
+        out.write(f'  <LocalTransformations><DerivedField name="fbin" optype="categorical" dataType="string">'
+                  f'{disc}</DerivedField></LocalTransformations>\n')
     counts = rng.integers(50, 200, classes)
     out.write('  <BayesInputs>\n')
     for j in range(n_features):
+        if discretized and j == last:
+            name = "fbin" if discretized == "local" else f"f{j}"
+            inner = ("" if discretized == "local"
+                     else f'<DerivedField optype="categorical" dataType="string">{disc}</DerivedField>')
+            out.write(f'   <BayesInput fieldName="{name}">{inner}')
+            for b in ("low", "mid", "high"):
+                out.write(f'<PairCounts value="{b}"><TargetValueCounts>'
+                          + "".join(f'<TargetValueCount value="{cats[k]}" count="{int(rng.integers(5, 60))}"/>'
+                                    for k in range(classes)) + '</TargetValueCounts></PairCounts>')
+            out.write('</BayesInput>\n')
+            continue
         out.write(f'   <BayesInput fieldName="f{j}"><TargetValueStats>')
         for k in range(classes):
             out.write(f'<TargetValueStat value="{cats[k]}"><GaussianDistribution mean="{rng.normal() * 0.7:.4f}" '

@@ -20,7 +20,7 @@ def _registry() -> Dict[type, Callable[..., ModelEvaluator]]:
     from .neural import NeuralEvaluator
     from .regression import GeneralRegressionEvaluator, RegressionEvaluator
     from .svm import SvmEvaluator
-    from .scorecard import ScorecardEvaluator, make_ruleset_evaluator
+    from .scorecard import make_ruleset_evaluator, make_scorecard_evaluator
     from .tree import TreeEvaluator
 
     return {
@@ -31,7 +31,7 @@ def _registry() -> Dict[type, Callable[..., ModelEvaluator]]:
         ir.GeneralRegressionModel: GeneralRegressionEvaluator,
         ir.NeuralNetwork: NeuralEvaluator,
         ir.SupportVectorMachineModel: SvmEvaluator,
-        ir.Scorecard: ScorecardEvaluator,
+        ir.Scorecard: make_scorecard_evaluator,
         ir.RuleSetModel: make_ruleset_evaluator,
         ir.NaiveBayesModel: NaiveBayesEvaluator,
         ir.NearestNeighborModel: NearestNeighborEvaluator,

@@ -10,7 +10,10 @@ kernels are the existing ones:
   UNKNOWN predicate (missing input) does not match (``missingValueStrategy="none"``); a
   characteristic without a matching attribute has no partial score, which makes the whole score
   missing (``returnNullPrediction`` + ``sum``'s missing rule) → ``EmptyScore``. Multiway trees lower
-  to the GENERAL tree layout (``tree.hip::tree_general_kernel``). Reason codes
+  to the GENERAL tree layout (``tree.hip::tree_general_kernel``). An Attribute with a
+  ``ComplexPartialScore`` (an expression over the record, taking precedence over ``partialScore``)
+  has no constant leaf: such scorecards are evaluated directly (:class:`ComplexScorecardEvaluator`,
+  host only — same first-TRUE-attribute rule; a missing expression value voids the score). Reason codes
   (``useReasonCodes``, ``pointsBelow`` / ``pointsAbove``) are host outputs.
 * **RuleSetModel** ``firstHit`` = a one-level ``TreeModel``: the (flattened) rules are the root's
   children in document order, a ``CompoundRule``'s predicate AND-ed into its rules; the
@@ -30,7 +33,7 @@ import numpy as np
 
 from ..api.exceptions import UnsupportedFeatureException
 from ..pmml import ir
-from ..pmml.fields import NAN, Columns, FieldSchema, eval_predicate
+from ..pmml.fields import NAN, Columns, FieldSchema, eval_expression, eval_predicate
 from .base import ModelEvaluator, ModelResult
 from .mining import MiningEvaluator
 from .tree import TreeEvaluator
@@ -66,18 +69,33 @@ def scorecard_as_mining(sc: ir.Scorecard) -> ir.MiningModel:
                           segments=segs, missing_prediction_treatment="returnMissing")
 
 
-class ScorecardEvaluator(MiningEvaluator):
-    def __init__(self, model: ir.Scorecard, schema: FieldSchema):
-        if model.function_name not in ("regression", ""):
-            raise UnsupportedFeatureException(f"Scorecard functionName {model.function_name!r}")
-        self.scorecard = model
-        super().__init__(scorecard_as_mining(model), schema)
+def _picks(sc: ir.Scorecard, cols: Columns) -> List[Tuple[np.ndarray, np.ndarray]]:
+    """Per characteristic: the first attribute whose predicate is TRUE (-1: none) and its partial
+    score per row (NaN without a match; a ComplexPartialScore evaluated on the record)."""
+    n = cols.n
+    out = []
+    for ch in sc.characteristics:
+        pick = np.full(n, -1)
+        for j, a in enumerate(ch.attributes):
+            t, _ = eval_predicate(a.predicate, cols)
+            pick = np.where((pick < 0) & t, j, pick)
+        partial = np.full(n, NAN)
+        for j, a in enumerate(ch.attributes):
+            sel = pick == j
+            if not sel.any():
+                continue
+            if a.complex_score is not None:
+                partial[sel] = eval_expression(a.complex_score, cols)[sel]
+            elif a.partial_score is not None:
+                partial[sel] = a.partial_score
+            else:
+                raise UnsupportedFeatureException("Scorecard Attribute without partialScore")
+        out.append((pick, partial))
+    return out
 
-    def _evaluate(self, cols: Columns) -> ModelResult:
-        res = super()._evaluate(cols)
-        if self.scorecard.use_reason_codes and any(of.feature == "reasonCode" for of in self.model.output):
-            res.extra["reason_codes"] = self._reason_codes(cols)
-        return res
+
+class _ReasonCodes:
+    """Reason-code outputs shared by both scorecard evaluators."""
 
     def _reason_codes(self, cols: Columns) -> List[List[str]]:
         """Per row: reason codes ranked by their summed point difference to the baseline
@@ -86,15 +104,10 @@ class ScorecardEvaluator(MiningEvaluator):
         sc = self.scorecard
         n = cols.n
         diffs: List[Tuple[np.ndarray, np.ndarray, List[Optional[str]]]] = []
-        for ch in sc.characteristics:
-            pick = np.full(n, -1)
-            for j, a in enumerate(ch.attributes):
-                t, _ = eval_predicate(a.predicate, cols)
-                pick = np.where((pick < 0) & t, j, pick)
+        for ch, (pick, partial) in zip(sc.characteristics, _picks(sc, cols)):
             base = ch.baseline_score if ch.baseline_score is not None else sc.baseline_score
             if base is None:
                 raise UnsupportedFeatureException("reason codes need a baselineScore")
-            partial = np.array([a.partial_score for a in ch.attributes] + [NAN])[pick]
             d = (base - partial) if sc.reason_code_algorithm == "pointsBelow" else (partial - base)
             codes = [a.reason_code or ch.reason_code for a in ch.attributes]
             diffs.append((pick, d, codes))
@@ -115,6 +128,47 @@ class ScorecardEvaluator(MiningEvaluator):
             k = max(1, int(of.rank)) - 1
             return self._encode_label(of.name, [r[k] if len(r) > k and v else None for r, v in zip(rc, res.valid)])
         return super()._output_column(of, cols, res, n)
+
+    def _with_reason_codes(self, res: ModelResult, cols: Columns) -> ModelResult:
+        if self.scorecard.use_reason_codes and any(of.feature == "reasonCode" for of in self.model.output):
+            res.extra["reason_codes"] = self._reason_codes(cols)
+        return res
+
+
+class ScorecardEvaluator(_ReasonCodes, MiningEvaluator):
+    def __init__(self, model: ir.Scorecard, schema: FieldSchema):
+        if model.function_name not in ("regression", ""):
+            raise UnsupportedFeatureException(f"Scorecard functionName {model.function_name!r}")
+        self.scorecard = model
+        super().__init__(scorecard_as_mining(model), schema)
+
+    def _evaluate(self, cols: Columns) -> ModelResult:
+        return self._with_reason_codes(super()._evaluate(cols), cols)
+
+
+class ComplexScorecardEvaluator(_ReasonCodes, ModelEvaluator):
+    """Scorecards with ``ComplexPartialScore`` attributes: ``initialScore + Σ partial`` evaluated
+    directly (no constant-leaf tree form, so no device plan: ``compile_plan`` falls back to host)."""
+
+    def __init__(self, model: ir.Scorecard, schema: FieldSchema):
+        if model.function_name not in ("regression", ""):
+            raise UnsupportedFeatureException(f"Scorecard functionName {model.function_name!r}")
+        super().__init__(model, schema)
+        self.scorecard = model
+        self.categories = None
+
+    def _evaluate(self, cols: Columns) -> ModelResult:
+        total = np.full(cols.n, float(self.scorecard.initial_score))
+        for _, partial in _picks(self.scorecard, cols):
+            total = total + partial  # no matching attribute / missing expression value -> NaN
+        ok = np.isfinite(total)
+        return self._with_reason_codes(ModelResult("regression", np.where(ok, total, NAN), ok), cols)
+
+
+def make_scorecard_evaluator(model: ir.Scorecard, schema: FieldSchema) -> ModelEvaluator:
+    if any(a.complex_score is not None for ch in model.characteristics for a in ch.attributes):
+        return ComplexScorecardEvaluator(model, schema)
+    return ScorecardEvaluator(model, schema)
 
 
 # --------------------------------------------------------------------------- rule sets

@@ -533,6 +533,7 @@ class ScorecardAttribute:
     predicate: Predicate
     partial_score: Optional[float]
     reason_code: Optional[str] = None
+    complex_score: Optional["Expression"] = None  # ComplexPartialScore: evaluated per record
 
 
 @dataclass

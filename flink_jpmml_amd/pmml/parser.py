@@ -579,9 +579,15 @@ def _parse_scorecard(el: ET.Element) -> ir.Scorecard:
     for c in _children(chars, "Characteristic"):
         ch = ir.Characteristic(c.get("name"), reason_code=c.get("reasonCode"), baseline_score=_f(c, "baselineScore"))
         for a in _children(c, "Attribute"):
-            if _child(a, "ComplexPartialScore") is not None:
-                raise UnsupportedFeatureException("Scorecard ComplexPartialScore is not supported")
-            ch.attributes.append(ir.ScorecardAttribute(_find_predicate(a), _f(a, "partialScore"), a.get("reasonCode")))
+            cps = _child(a, "ComplexPartialScore")
+            expr = None
+            if cps is not None:
+                ex = _find_expression(cps)
+                if ex is None:
+                    raise PmmlParseError("ComplexPartialScore without an expression")
+                expr = _parse_expression(ex)
+            ch.attributes.append(ir.ScorecardAttribute(_find_predicate(a), _f(a, "partialScore"), a.get("reasonCode"),
+                                                       complex_score=expr))
         m.characteristics.append(ch)
     return m
 
@@ -626,11 +632,23 @@ def _parse_naive_bayes(el: ET.Element) -> ir.NaiveBayesModel:
     m.threshold = _f(el, "threshold", 0.0)
     bis = _child(el, "BayesInputs")
     for bi in _children(bis, "BayesInput") if bis is not None else []:
-        if _child(bi, "DerivedField") is not None:
-            raise UnsupportedFeatureException("BayesInput with a DerivedField (discretisation) is not supported")
         inp = ir.BayesInput(bi.get("fieldName"))
         for pc in _children(bi, "PairCounts"):
             inp.pair_counts[pc.get("value")] = _target_value_counts(_child(pc, "TargetValueCounts"))
+        dfe = _child(bi, "DerivedField")
+        if dfe is not None:
+            # a discretised input (e.g. Discretize bins of a continuous field): the PairCounts are
+            # keyed by the derived values, so the BayesInput reads a model-local derived field —
+            # the oracle and the device derive pass then treat it like any LocalTransformation
+            ex = _find_expression(dfe)
+            if ex is None:
+                raise PmmlParseError(f"BayesInput {inp.field!r}: DerivedField without an expression")
+            name = f"__bayes_{inp.field}"
+            values = list(inp.pair_counts) + [v.get("value") for v in _children(dfe, "Value")]
+            m.local_transformations.append(ir.DerivedField(name, dfe.get("optype", "categorical"),
+                                                           dfe.get("dataType", "string"), _parse_expression(ex),
+                                                           list(dict.fromkeys(values))))
+            inp.field = name
         tvs = _child(bi, "TargetValueStats")
         for st in _children(tvs, "TargetValueStat") if tvs is not None else []:
             g = _child(st, "GaussianDistribution")

@@ -44,6 +44,10 @@ CASES = {
     "glm-binomial-identity-first": lambda: glm_pmml(link="identity", binomial="first", seed=11),
     "naive-bayes": lambda: naive_bayes_pmml(),
     "naive-bayes-2": lambda: naive_bayes_pmml(classes=2, seed=3),
+    # BayesInput with its own DerivedField (Discretize bins keyed PairCounts) / the same bins as a
+    # LocalTransformations field
+    "naive-bayes-discretized": lambda: naive_bayes_pmml(seed=4, discretized="inline"),
+    "naive-bayes-local-bins": lambda: naive_bayes_pmml(seed=4, discretized="local"),
 }
 
 
@@ -190,3 +194,27 @@ def test_design_plan_on_gpu(gpu, name):
         assert (s[v] == ref[v]).mean() > 0.999
     else:
         assert np.allclose(s[v], ref[v], rtol=1e-4, atol=1e-4)
+
+
+def test_naive_bayes_inline_discretization():
+    """A BayesInput's own DerivedField scores exactly like the same bins as a LocalTransformations
+    field, and the bin edges follow the Interval closures (-0.5 is "mid", just below is "low")."""
+    inline = CompiledPmml.from_string(naive_bayes_pmml(seed=4, discretized="inline"))
+    local = CompiledPmml.from_string(naive_bayes_pmml(seed=4, discretized="local"))
+    _, X = mixed_records(3000, 4, seed=6, missing_rate=0.05)
+    ra, rb = inline.result(X), local.result(X)
+    assert (ra.valid == rb.valid).all() and ra.valid.any()
+    np.testing.assert_array_equal(ra.probs[ra.valid], rb.probs[rb.valid])
+    row = X[:1].copy()
+    row[0, :3] = 0.1
+    row[0, 4] = 0.0
+
+    def probs(v):
+        r = row.copy()
+        r[0, 3] = v
+        return inline.result(r).probs[0]
+
+    np.testing.assert_array_equal(probs(-0.5), probs(0.49))       # both "mid"
+    np.testing.assert_array_equal(probs(-0.6), probs(-3.0))       # both "low"
+    assert not np.array_equal(probs(-0.5), probs(np.nextafter(-0.5, -1.0)))  # mid | low edge
+    assert not np.array_equal(probs(0.5), probs(0.49))            # high | mid edge

@@ -180,3 +180,42 @@ def test_general_layout_emulation(kind):
     else:
         lab = np.array([float(x) for x in spec.labels])[np.argmax(acc[ok], axis=1)]
         assert (lab == ref[ok]).all()
+
+
+def _with_complex_score(txt: str) -> tuple:
+    """ch1's first attribute (f1 < t) scores the expression 2 * f1 + 3 instead of its constant."""
+    import re
+
+    m = re.search(r'<Attribute partialScore="([^"]+)">(<SimplePredicate field="f1" operator="lessThan" '
+                  r'value="([^"]+)"/>)</Attribute>', txt)
+    assert m is not None
+    cps = ('<ComplexPartialScore><Apply function="+"><Apply function="*"><FieldRef field="f1"/>'
+           '<Constant>2</Constant></Apply><Constant>3</Constant></Apply></ComplexPartialScore>')
+    out = txt[:m.start()] + f'<Attribute partialScore="{m.group(1)}">{m.group(2)}{cps}</Attribute>' + txt[m.end():]
+    return out, float(m.group(1)), float(m.group(3))
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_complex_partial_score(seed):
+    """ComplexPartialScore (precedence over partialScore): the attribute's points are the expression
+    on the record; everything else equals the constant scorecard. Host-only (no tree form)."""
+    from flink_jpmml_amd.models.scorecard import ComplexScorecardEvaluator
+    from flink_jpmml_amd.runtime.plans import NotLowerable, compile_plan, lowering_dry_run
+
+    base = scorecard_pmml(seed=seed)
+    txt, const, thr = _with_complex_score(base)
+    c0, c1 = CompiledPmml.from_string(base), CompiledPmml.from_string(txt)
+    assert isinstance(c1.evaluator, ComplexScorecardEvaluator)
+    _, X = mixed_records(800, 4, seed=seed + 5, missing_rate=0.08)
+    s0, v0 = c0.score_matrix_oracle(X)
+    s1, v1 = c1.score_matrix_oracle(X)
+    assert (v0 == v1).all() and v1.any()
+    hit = X[:, 1] < thr
+    assert hit[v1].any() and (~hit[v1]).any()
+    np.testing.assert_allclose(s1[v1 & ~hit], s0[v1 & ~hit], rtol=0, atol=1e-9)
+    np.testing.assert_allclose(s1[v1 & hit], (s0 - const + 2 * X[:, 1] + 3)[v1 & hit], rtol=0, atol=1e-9)
+    # reason codes use the expression's points too
+    res = c1.result(X[:50])
+    assert len(res.extra["reason_codes"]) == 50
+    with lowering_dry_run(), pytest.raises(NotLowerable):
+        compile_plan(c1, "cpu")
