@@ -7,7 +7,13 @@ whose predicate is TRUE is followed. A predicate that is UNKNOWN (missing input)
 * ``none`` — UNKNOWN counts as FALSE;
 * ``lastPrediction`` — stop and return the current node's score;
 * ``nullPrediction`` — no prediction (→ ``EmptyScore``);
-* ``defaultChild`` — continue at the node's ``defaultChild``.
+* ``defaultChild`` — continue at the node's ``defaultChild``;
+* ``weightedConfidence`` / ``aggregateNodes`` (classification) — at the first UNKNOWN child, the
+  row is scored down that child and every sibling whose predicate is not FALSE (recursively);
+  ``weightedConfidence`` sums the siblings' class confidences weighted by ``recordCount`` relative
+  to the parent's, ``aggregateNodes`` sums the reached leaves' ScoreDistribution record counts; the
+  winner is the largest class (probabilities: the normalised sum). Host-only (the device lowerings
+  reject both strategies); parity unpinned — the PMML 4.4 text, no JPMML here.
 
 When no child is TRUE, ``noTrueChildStrategy`` decides: ``returnNullPrediction`` (default) or
 ``returnLastPrediction``.
@@ -51,8 +57,10 @@ class TreeEvaluator(ModelEvaluator):
     def __init__(self, model: ir.TreeModel, schema: FieldSchema):
         super().__init__(model, schema)
         self.tree = model
-        if model.missing_value_strategy in ("weightedConfidence", "aggregateNodes"):
-            raise UnsupportedFeatureException(f"missingValueStrategy {model.missing_value_strategy!r}")
+        if model.missing_value_strategy in ("weightedConfidence", "aggregateNodes") and \
+                model.function_name != "classification":
+            raise UnsupportedFeatureException(f"missingValueStrategy {model.missing_value_strategy!r} "
+                                              "needs a classification TreeModel")
         self._nodes: Optional[List[ir.Node]] = None
         self._index_map: Optional[Dict[int, int]] = None
         if model.flat is not None:
@@ -200,6 +208,76 @@ class TreeEvaluator(ModelEvaluator):
                 out[remaining] = me
         return out
 
+    def _node_mass(self, i: int) -> np.ndarray:
+        """Per-class mass a node contributes: ScoreDistribution record counts (aggregateNodes) or
+        its class confidences (weightedConfidence)."""
+        nd = self.nodes[i]
+        if self.tree.missing_value_strategy == "aggregateNodes":
+            v = np.zeros(len(self.categories))
+            for d in nd.distributions:
+                v[self.categories.index(d.value)] += d.record_count
+            if not nd.distributions and nd.score is not None:
+                v[self.categories.index(nd.score)] = nd.record_count if nd.record_count else 1.0
+            return v
+        return self.node_probs[i]
+
+    def _mixture(self, node: ir.Node, cols, rows: np.ndarray) -> np.ndarray:
+        """``[len(rows), C]`` class mass of the rows that reached ``node`` (NaN row: no prediction)."""
+        C = len(self.categories)
+        me = self._index[id(node)]
+        out = np.full((rows.size, C), NAN)
+        if rows.size == 0:
+            return out
+        if not node.children:
+            out[:] = self._node_mass(me)
+            return out
+        view = _RowView(cols, rows)
+        evals = [eval_predicate(c.predicate, view) for c in node.children]
+        todo = np.ones(rows.size, dtype=bool)
+        for k, child in enumerate(node.children):
+            t, u = evals[k]
+            go = todo & t & ~u
+            if go.any():  # TRUE before any UNKNOWN: the ordinary walk
+                out[go] = self._mixture(child, cols, rows[go])
+            unk = todo & u
+            if unk.any():  # first UNKNOWN: this child and every later sibling not FALSE
+                acc = np.zeros((int(unk.sum()), C))
+                parent_n = node.record_count
+                for j in range(k, len(node.children)):
+                    tj, uj = evals[j]
+                    sel = (tj | uj)[unk]
+                    if not sel.any():
+                        continue
+                    sub = self._mixture(node.children[j], cols, rows[unk][sel])
+                    w = 1.0
+                    if self.tree.missing_value_strategy == "weightedConfidence":
+                        cn = node.children[j].record_count
+                        w = (cn / parent_n) if cn is not None and parent_n else 1.0
+                    acc[sel] += np.nan_to_num(sub, nan=0.0) * w
+                out[unk] = acc
+            todo &= ~(t | u)
+        if todo.any() and self.tree.no_true_child_strategy == "returnLastPrediction":
+            out[todo] = self._node_mass(me)
+        return out
+
+    def _mix_rows(self, res: ModelResult, cols: Columns, leaf: np.ndarray) -> ModelResult:
+        """Rows the ordinary walk left without a node (an UNKNOWN on the way, or no TRUE child):
+        the recursive sibling mixture; rows that never met an UNKNOWN keep their leaf's result."""
+        root_t, _ = eval_predicate(self.tree.root.predicate, cols)
+        rows = np.nonzero(root_t & (leaf < 0))[0]
+        if rows.size == 0:
+            return res
+        mass = self._mixture(self.tree.root, cols, rows)
+        tot = mass.sum(axis=1)
+        ok = np.isfinite(tot) & (tot > 0)
+        with np.errstate(invalid="ignore", divide="ignore"):
+            probs = np.where(ok[:, None], mass / np.where(ok, tot, 1.0)[:, None], NAN)
+        lab = np.where(ok, np.argmax(np.nan_to_num(mass, nan=-np.inf), axis=1), 0).astype(np.float64)
+        res.value[rows] = np.where(ok, lab, NAN)
+        res.valid[rows] = ok
+        res.probs[rows] = probs
+        return res
+
     def _evaluate(self, cols: Columns) -> ModelResult:
         leaf = self.leaf_index(cols)
         ok = leaf >= 0
@@ -211,6 +289,8 @@ class TreeEvaluator(ModelEvaluator):
             ok = ok & ~np.isnan(lab)
             probs = np.where(ok[:, None], self.node_probs[safe], NAN)
             res = ModelResult("classification", np.where(ok, lab, NAN), ok, categories=self.categories, probs=probs)
+            if self.tree.missing_value_strategy in ("weightedConfidence", "aggregateNodes"):
+                res = self._mix_rows(res, cols, leaf)
         else:
             val = np.where(ok, self.node_value[safe], NAN)
             ok = ok & ~np.isnan(val)
