@@ -129,10 +129,12 @@ class MiningEvaluator(ModelEvaluator):
         method = self.method
         with np.errstate(invalid="ignore", divide="ignore"):
             Vz = np.where(use, V, 0.0)
-            if is_float(self.mm) and method in ("sum", "average", "weightedAverage"):
+            if is_float(self.mm) and method in ("sum", "weightedSum", "average", "weightedAverage"):
                 out = _float_aggregate(method, Vz, W, use)
             elif method == "sum":
                 out = np.sum(Vz, axis=1)
+            elif method == "weightedSum":  # PMML 4.4: Σ weight · value over the used segments
+                out = np.sum(Vz * W, axis=1)
             elif method == "average":
                 out = np.sum(Vz, axis=1) / np.sum(use, axis=1)
             elif method == "weightedAverage":
@@ -216,10 +218,11 @@ def _float_aggregate(method: str, Vz: np.ndarray, W: np.ndarray, use: np.ndarray
     wsum = np.zeros(Vz.shape[0], dtype=np.float32)
     for j in range(Vz.shape[1]):
         v = Vz[:, j].astype(np.float32)
-        w = W[:, j].astype(np.float32) if method == "weightedAverage" else np.float32(1.0)
-        acc = acc + (w * v if method == "weightedAverage" else v)
+        weighted = method in ("weightedAverage", "weightedSum")
+        w = W[:, j].astype(np.float32) if weighted else np.float32(1.0)
+        acc = acc + (w * v if weighted else v)
         wsum = wsum + np.where(use[:, j], w, np.float32(0.0))
-    if method == "sum":
+    if method in ("sum", "weightedSum"):
         return acc.astype(np.float64)
     return (acc / wsum).astype(np.float64)
 

@@ -782,7 +782,7 @@ def _regression_ensemble(ev, field_index, lower=lower_binary_tree,
         if not _segments_all_true(mm):
             raise NotLowerable("segment predicates other than True are host-only")
         method = mm.multiple_model_method
-        if method not in ("sum", "average", "weightedAverage"):
+        if method not in ("sum", "weightedSum", "average", "weightedAverage"):
             raise NotLowerable(f"multipleModelMethod {method!r} is host-only for regression ensembles")
         trees: List[BinaryTree] = []
         weights: List[float] = []
@@ -790,7 +790,7 @@ def _regression_ensemble(ev, field_index, lower=lower_binary_tree,
             st, sw, sa, sb = _regression_ensemble(sub, field_index, lower)
             if sb != 0.0:
                 raise NotLowerable("nested Target rescaleConstant inside an ensemble is host-only")
-            w = seg.weight if method == "weightedAverage" else 1.0
+            w = seg.weight if method in ("weightedAverage", "weightedSum") else 1.0
             trees.extend(st)
             weights.extend([x * w * sa for x in sw])
         _check_null_trees(mm, trees)
