@@ -46,10 +46,11 @@ enum : int {
 
 // Apply function ids (mirror of runtime/derive.py::APPLY_FN)
 enum : int {
-  F_ADD = 0, F_SUB, F_MUL, F_DIV, F_POW, F_MOD,                        // binary arithmetic
+  F_ADD = 0, F_SUB, F_MUL, F_DIV, F_POW, F_MOD, F_HYPOT, F_ATAN2,      // binary arithmetic
   F_EQ = 10, F_NE, F_LT, F_LE, F_GT, F_GE, F_THRESHOLD,                 // comparisons -> 0/1
   F_LOG10 = 20, F_LN, F_SQRT, F_ABS, F_EXP, F_FLOOR, F_CEIL, F_ROUND, F_RINT, F_SIN, F_COS, F_TAN, F_ASIN,
   F_ACOS, F_ATAN, F_SINH, F_COSH, F_TANH, F_EXPM1, F_LN1P, F_NOT,      // unary
+  F_ERF, F_SNCDF, F_SNPDF, F_SNIDF,                                    // unary, PMML 4.4 (41-44)
   F_MIN = 50, F_MAX, F_SUM, F_AVG, F_PRODUCT, F_MEDIAN, F_AND, F_OR,   // n-ary
   F_ISMISSING = 60, F_ISNOTMISSING, F_IF,                              // no mapMissingTo / defaultValue
 };
@@ -79,6 +80,10 @@ __device__ __forceinline__ double unary(int fn, double v) {
     case F_EXPM1: return expm1(v);
     case F_LN1P: return log1p(v);
     case F_NOT: return v == 0.0 ? 1.0 : 0.0;
+    case F_ERF: return erf(v);
+    case F_SNCDF: return normcdf(v);
+    case F_SNPDF: return exp(-0.5 * v * v) * 0.3989422804014327;  // 1 / sqrt(2 pi)
+    case F_SNIDF: return normcdfinv(v);
     default: return __builtin_nan("");
   }
 }
@@ -95,6 +100,8 @@ __device__ __forceinline__ double binary(int fn, double a, double b) {
       if (r != 0.0 && ((r < 0.0) != (b < 0.0))) r += b;
       return r;
     }
+    case F_HYPOT: return hypot(a, b);
+    case F_ATAN2: return atan2(a, b);
     case F_EQ: return a == b ? 1.0 : 0.0;
     case F_NE: return a != b ? 1.0 : 0.0;
     case F_LT: return a < b ? 1.0 : 0.0;

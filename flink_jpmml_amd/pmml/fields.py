@@ -504,15 +504,39 @@ def denorm_continuous(ex: ir.NormContinuous, y: np.ndarray) -> np.ndarray:
     return x0 + (y - y0) * (x1 - x0) / (y1 - y0)
 
 
+def _erf(a):
+    from scipy.special import erf
+
+    return erf(a)
+
+
+def _ndtri(a):
+    from scipy.special import ndtri
+
+    return ndtri(a)
+
+
+_SQRT2 = math.sqrt(2.0)
+_SQRT2PI = math.sqrt(2.0 * math.pi)
+
 _BINARY_NUM: Dict[str, Callable] = {
     "+": np.add, "-": np.subtract, "*": np.multiply, "/": np.divide, "pow": np.power,
-    "min": np.fmin, "max": np.fmax, "modulo": np.mod,
+    "min": np.fmin, "max": np.fmax, "modulo": np.mod, "hypot": np.hypot, "atan2": np.arctan2,
+}
+# PMML 4.4 distribution functions: f(x, mean, stdev)
+_TERNARY_NUM: Dict[str, Callable] = {
+    "normalCDF": lambda x, m, s: 0.5 * (1.0 + _erf((x - m) / (s * _SQRT2))),
+    "normalPDF": lambda x, m, s: np.exp(-0.5 * ((x - m) / s) ** 2) / (s * _SQRT2PI),
+    "normalIDF": lambda p, m, s: m + s * _ndtri(p),
 }
 _UNARY_NUM: Dict[str, Callable] = {
     "log10": np.log10, "ln": np.log, "sqrt": np.sqrt, "abs": np.abs, "exp": np.exp, "floor": np.floor,
     "ceil": np.ceil, "round": lambda a: np.floor(a + 0.5), "rint": np.rint, "sin": np.sin, "cos": np.cos,
     "tan": np.tan, "asin": np.arcsin, "acos": np.arccos, "atan": np.arctan, "sinh": np.sinh, "cosh": np.cosh,
-    "tanh": np.tanh, "expm1": np.expm1, "ln1p": np.log1p,
+    "tanh": np.tanh, "expm1": np.expm1, "ln1p": np.log1p, "erf": _erf,
+    "stdNormalCDF": lambda a: 0.5 * (1.0 + _erf(a / _SQRT2)),
+    "stdNormalPDF": lambda a: np.exp(-0.5 * a * a) / _SQRT2PI,
+    "stdNormalIDF": _ndtri,
 }
 
 
@@ -658,8 +682,17 @@ def _eval_apply(ex: ir.Apply, cols: Columns, out_field: Optional[str]) -> np.nda
             miss |= np.isnan(a)
         if fn in _UNARY_NUM and len(args) == 1:
             res = _UNARY_NUM[fn](args[0])
-        elif fn in ("+", "-", "*", "/", "pow", "modulo") and len(args) == 2:
+        elif fn in ("+", "-", "*", "/", "pow", "modulo", "hypot", "atan2") and len(args) == 2:
             res = _BINARY_NUM[fn](args[0], args[1])
+        elif fn in _TERNARY_NUM and len(args) == 3:
+            res = _TERNARY_NUM[fn](args[0], args[1], args[2])
+        elif fn == "stdev" and args:  # sample standard deviation of the present arguments
+            stack = np.vstack(args)
+            cnt = np.sum(~np.isnan(stack), axis=0)
+            mean = np.nansum(stack, axis=0) / np.maximum(cnt, 1)
+            ss = np.nansum((stack - mean) ** 2, axis=0)
+            res = np.where(cnt >= 2, np.sqrt(ss / np.maximum(cnt - 1, 1)), NAN)
+            miss = cnt == 0
         elif fn in ("min", "max", "sum", "avg", "product", "median") and args:
             stack = np.vstack(args)
             res = {"min": np.nanmin, "max": np.nanmax, "sum": np.nansum, "avg": np.nanmean, "product": np.nanprod,

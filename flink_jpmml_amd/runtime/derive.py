@@ -48,18 +48,19 @@ OP_LOAD, OP_CONST, OP_MAPMISS, OP_REMAP, OP_NORMCONT, OP_NORMDISC, OP_DISCRETIZE
     OP_STORE = range(10)
 
 APPLY_FN: Dict[str, int] = {
-    "+": 0, "-": 1, "*": 2, "/": 3, "pow": 4, "modulo": 5,
+    "+": 0, "-": 1, "*": 2, "/": 3, "pow": 4, "modulo": 5, "hypot": 6, "atan2": 7,
     "equal": 10, "notEqual": 11, "lessThan": 12, "lessOrEqual": 13, "greaterThan": 14, "greaterOrEqual": 15,
     "threshold": 16,
     "log10": 20, "ln": 21, "sqrt": 22, "abs": 23, "exp": 24, "floor": 25, "ceil": 26, "round": 27, "rint": 28,
     "sin": 29, "cos": 30, "tan": 31, "asin": 32, "acos": 33, "atan": 34, "sinh": 35, "cosh": 36, "tanh": 37,
     "expm1": 38, "ln1p": 39, "not": 40, "x-exp": 24,
+    "erf": 41, "stdNormalCDF": 42, "stdNormalPDF": 43, "stdNormalIDF": 44,
     "min": 50, "max": 51, "sum": 52, "avg": 53, "product": 54, "median": 55, "and": 56, "or": 57,
     "isMissing": 60, "isNotMissing": 61, "if": 62,
 }
-_BINARY_ARITH = range(0, 6)
+_BINARY_ARITH = range(0, 8)
 _COMPARE = range(10, 17)
-_UNARY = range(20, 41)
+_UNARY = range(20, 45)
 _OUTLIERS = {"asIs": 0, "asMissingValues": 1, "asExtremeValues": 2}
 
 INSN_DTYPE = np.dtype([("op", "<i4"), ("a", "<i4"), ("b", "<i4"), ("c", "<i4"), ("x", "<f8"), ("y", "<f8")])
@@ -724,11 +725,20 @@ def emulate(prog: DerivedProgram, X: np.ndarray) -> np.ndarray:
     return tile[:, prog.out_cols]
 
 
+def _scipy(name: str):
+    import scipy.special
+
+    return getattr(scipy.special, name)
+
+
 _NP_UNARY = {20: np.log10, 21: np.log, 22: np.sqrt, 23: np.abs, 24: np.exp, 25: np.floor, 26: np.ceil,
              27: lambda v: np.floor(v + 0.5), 28: np.rint, 29: np.sin, 30: np.cos, 31: np.tan, 32: np.arcsin,
              33: np.arccos, 34: np.arctan, 35: np.sinh, 36: np.cosh, 37: np.tanh, 38: np.expm1, 39: np.log1p,
-             40: lambda v: (v == 0).astype(np.float64)}
-_NP_BINARY = {0: np.add, 1: np.subtract, 2: np.multiply, 3: np.divide, 4: np.power, 5: np.mod,
+             40: lambda v: (v == 0).astype(np.float64), 41: _scipy("erf"),
+             42: lambda v: _scipy("ndtr")(v), 43: lambda v: np.exp(-0.5 * v * v) / np.sqrt(2.0 * np.pi),
+             44: lambda v: _scipy("ndtri")(v)}
+_NP_BINARY = {0: np.add, 1: np.subtract, 2: np.multiply, 3: np.divide, 4: np.power, 5: np.mod, 6: np.hypot,
+              7: np.arctan2,
               10: np.equal, 11: np.not_equal, 12: np.less, 13: np.less_equal, 14: np.greater,
               15: np.greater_equal, 16: np.greater}
 _NP_NARY = {50: np.nanmin, 51: np.nanmax, 52: np.nansum, 53: np.nanmean, 54: np.nanprod, 55: np.nanmedian}

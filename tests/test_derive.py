@@ -36,11 +36,17 @@ DICT = """
   <DerivedField name="fa" optype="continuous" dataType="float"><FieldRef field="a"/></DerivedField>
   <DerivedField name="in_c" optype="continuous" dataType="double"><Apply function="isIn"><FieldRef field="c"/><Constant>red</Constant><Constant>blue</Constant></Apply></DerivedField>
   <DerivedField name="notin_a" optype="continuous" dataType="double"><Apply function="isNotIn" mapMissingTo="5"><FieldRef field="a"/><Constant>0</Constant><Constant>1.5</Constant></Apply></DerivedField>
+  <DerivedField name="erf_b" optype="continuous" dataType="double"><Apply function="erf"><FieldRef field="b"/></Apply></DerivedField>
+  <DerivedField name="ncdf_a" optype="continuous" dataType="double"><Apply function="stdNormalCDF"><FieldRef field="a"/></Apply></DerivedField>
+  <DerivedField name="npdf_b" optype="continuous" dataType="double"><Apply function="stdNormalPDF"><FieldRef field="b"/></Apply></DerivedField>
+  <DerivedField name="nidf_a" optype="continuous" dataType="double"><Apply function="stdNormalIDF"><Apply function="/"><Apply function="+"><FieldRef field="a"/><Constant>2.01</Constant></Apply><Constant>5.1</Constant></Apply></Apply></DerivedField>
+  <DerivedField name="hyp" optype="continuous" dataType="double"><Apply function="hypot"><FieldRef field="a"/><FieldRef field="b"/></Apply></DerivedField>
+  <DerivedField name="at2" optype="continuous" dataType="double"><Apply function="atan2"><FieldRef field="b"/><FieldRef field="a"/></Apply></DerivedField>
  </TransformationDictionary>
 """
 
 DERIVED = ["log_a", "ab", "nb", "is_red", "bin_a", "code_c", "mx", "md", "cond", "miss_b", "modv", "fa", "in_c",
-           "notin_a"]
+           "notin_a", "erf_b", "ncdf_a", "npdf_b", "nidf_a", "hyp", "at2"]  # last six: PMML 4.4 functions
 
 
 def regression_doc() -> str:
