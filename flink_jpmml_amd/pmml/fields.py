@@ -136,7 +136,7 @@ class FieldSchema:
             # An Interval only makes sense on a continuous field (JPMML rejects the field).
             raise InputPreparationException(f"field {name!r}: Interval is not allowed on a {optype} field")
         is_missing = raw is None or (isinstance(raw, float) and math.isnan(raw))
-        if not is_missing and df is not None and df.missing_values and _as_text(raw) in df.missing_values:
+        if not is_missing and df is not None and df.missing_values and _in_value_list(df, raw, df.missing_values):
             is_missing = True
         value = NAN
         if not is_missing:
@@ -200,7 +200,7 @@ class FieldSchema:
     def _is_valid(self, df: Optional[ir.DataField], optype: str, raw: Any, value: float) -> bool:
         if df is None:
             return True
-        if df.invalid_values and _as_text(raw) in df.invalid_values:
+        if df.invalid_values and _in_value_list(df, raw, df.invalid_values):
             return False
         if optype == "continuous":
             if df.intervals and not any(iv.contains(value) for iv in df.intervals):
@@ -270,16 +270,19 @@ class FieldSchema:
                 elif treat != "asIs":
                     valid &= ~bad
             if mf is not None and optype == "continuous":
+                # outlier treatment belongs to the VALID-value treatment (as in prepare_value and
+                # JPMML): invalid values kept asIs or replaced asValue are not clamped / voided
+                ok_vals = present & ~bad
                 if mf.outliers == "asMissingValues":
                     if mf.low_value is not None:
-                        miss |= col < mf.low_value
+                        miss |= ok_vals & (col < mf.low_value)
                     if mf.high_value is not None:
-                        miss |= col > mf.high_value
+                        miss |= ok_vals & (col > mf.high_value)
                 elif mf.outliers == "asExtremeValues":
                     if mf.low_value is not None:
-                        col[col < mf.low_value] = mf.low_value
+                        col[ok_vals & (col < mf.low_value)] = mf.low_value
                     if mf.high_value is not None:
-                        col[col > mf.high_value] = mf.high_value
+                        col[ok_vals & (col > mf.high_value)] = mf.high_value
             col[miss] = NAN
             if mf is not None and mf.missing_value_replacement is not None:
                 col[miss] = self.lookup(name, mf.missing_value_replacement)
@@ -288,6 +291,27 @@ class FieldSchema:
             else:
                 X[:, j] = col
         return X, valid
+
+
+def _in_value_list(df: ir.DataField, raw: Any, values: List[str]) -> bool:
+    """Membership of a raw input in a DataField's missing / invalid Value list: by text, and for
+    numeric fields by value too (-999.0 matches "-999", as the typed comparison of JPMML and the
+    matrix path ``prepare_matrix`` do)."""
+    if _as_text(raw) in values:
+        return True
+    if df.is_string:
+        return False
+    try:
+        x = float(raw)
+    except (TypeError, ValueError):
+        return False
+    for v in values:
+        try:
+            if float(v) == x:
+                return True
+        except ValueError:
+            continue
+    return False
 
 
 def _as_text(raw: Any) -> str:
