@@ -95,9 +95,11 @@ __device__ __forceinline__ double binary(int fn, double a, double b) {
     case F_MUL: return a * b;
     case F_DIV: return a / b;
     case F_POW: return pow(a, b);
-    case F_MOD: {  // numpy.mod: the result takes the sign of the divisor
+    case F_MOD: {  // numpy.mod: the result takes the sign of the divisor (a zero result too: -0.0
+                   // for b < 0, which atan2 / a division downstream can see)
       double r = fmod(a, b);
-      if (r != 0.0 && ((r < 0.0) != (b < 0.0))) r += b;
+      if (r == 0.0) return copysign(0.0, b);
+      if ((r < 0.0) != (b < 0.0)) r += b;
       return r;
     }
     case F_HYPOT: return hypot(a, b);
