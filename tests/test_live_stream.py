@@ -81,8 +81,9 @@ def test_idle_control_source_does_not_stall_events(fixtures_dir):
     assert res.input_mode == "live"
     assert sorted(emitted) == list(range(15))
     lat = {i: emitted[i] - log[i] for i in emitted}
-    # events of the first ~0.1 s can race the Add (EmptyScore) but are never held back
-    assert max(lat.values()) < 0.020 + 0.25, lat
+    # events of the first ~0.1 s can race the Add (EmptyScore) but are never held back until the
+    # idle control source yields (the round-2 bug: 1.4 s); the bound leaves room for a loaded host
+    assert max(lat.values()) < 0.020 + 0.9, lat
     # the job ends when the idle control source finishes (2 s), not earlier
     assert time.monotonic() - t0 >= 1.9
 
