@@ -1787,6 +1787,11 @@ class TreePlan(DevicePlan):
         from ..ops._lib import TreeArgs, check, ptr, stream_handle
 
         n = X.shape[0]
+        if X.shape[1] == 0:
+            # feature-less trees (single leaves, e.g. a chain segment with an empty MiningSchema):
+            # the kernels still stage one column, so hand them a real one instead of a 0-wide
+            # tensor whose data pointer owns no bytes
+            X = torch.zeros((n, 1), dtype=torch.float32, device=X.device)
         if self.layout == "general":
             self._launch_general(X, score, valid, stream, probs, row_valid, score2, valid2)
             return

@@ -824,6 +824,8 @@ class ChainPlan(DevicePlan):
             best_v = torch.zeros(n, dtype=torch.bool, device=self.device)
             for i, plan in enumerate(self.subs):
                 Xi = Xa.index_select(1, self._col_idx[i]).contiguous()
+                if Xi.shape[1] == 0:  # a segment without inputs: never hand a kernel a 0-wide matrix
+                    Xi = torch.zeros((n, 1), dtype=torch.float32, device=self.device)
                 s = torch.empty(n, dtype=torch.float32, device=self.device)
                 v = torch.empty(n, dtype=torch.uint8, device=self.device)
                 pr = None

@@ -1,0 +1,130 @@
+"""Randomized regression ``modelChain`` MiningModels on the device (ChainPlan) vs the float64 oracle:
+2-5 segments, each a small regression tree or RegressionModel over the inputs AND the outputs of
+earlier segments (predictedValue, optionally a transformedValue expression), under a True or a
+SimplePredicate segment predicate on an input or an earlier output (so later segments can be
+skipped and earlier outputs can be missing). Validity equal to the oracle, scores within fp32."""
+
+import numpy as np
+import pytest
+
+from flink_jpmml_amd.runtime.compiled import CompiledPmml
+
+NS = "http://www.dmg.org/PMML-4_4"
+F = 4
+
+
+def _tree(rng, fields, depth) -> str:
+    def node(d, nid):
+        if d == depth or rng.random() < 0.2:
+            return None
+        f = str(rng.choice(fields))
+        t = round(float(rng.normal() * 0.8), 3)
+        left, right = node(d + 1, nid + "l"), node(d + 1, nid + "r")
+        sl = f'{rng.normal():.3f}'
+        sr = f'{rng.normal():.3f}'
+        lbody = left if left else ""
+        rbody = right if right else ""
+        return (f'<Node id="{nid}l" score="{sl}"><SimplePredicate field="{f}" operator="lessThan" value="{t}"/>'
+                f'{lbody}</Node><Node id="{nid}r" score="{sr}"><SimplePredicate field="{f}" '
+                f'operator="greaterOrEqual" value="{t}"/>{rbody}</Node>')
+
+    body = node(0, "n") or ""
+    strat = str(rng.choice(["defaultChild", "lastPrediction", "nullPrediction", "none"]))
+    dc = ' defaultChild="nl"' if strat == "defaultChild" and body else ""
+    ntc = ' noTrueChildStrategy="returnLastPrediction"'
+    if strat == "defaultChild":
+        body = body.replace('<Node id="', '<Node defaultChild="PLACEHOLDER" id="')  # fixed below
+        body = _default_children(body)
+    return (f'<TreeModel functionName="regression" missingValueStrategy="{strat}"{ntc} splitCharacteristic="binarySplit">'
+            f'{{ms}}{{out}}<Node id="n" score="{rng.normal():.3f}"{dc}><True/>{body}</Node></TreeModel>')
+
+
+def _default_children(body: str) -> str:
+    """Every node that has children gets defaultChild = its left child (ids are positional)."""
+    import re
+
+    def fix(m):
+        nid = m.group(1)
+        return f'<Node defaultChild="{nid}l" id="{nid}"' if f'id="{nid}l"' in body else f'<Node id="{nid}"'
+
+    return re.sub(r'<Node defaultChild="PLACEHOLDER" id="([a-z]+)"', fix, body)
+
+
+def _linear(rng, fields) -> str:
+    preds = "".join(f'<NumericPredictor name="{f}" coefficient="{rng.normal() * 0.5:.3f}"/>'
+                    for f in rng.permutation(fields)[: int(rng.integers(1, min(4, len(fields)) + 1))])
+    return ('<RegressionModel functionName="regression">{ms}{out}'
+            f'<RegressionTable intercept="{rng.normal() * 0.3:.3f}">{preds}</RegressionTable></RegressionModel>')
+
+
+def _doc(seed: int) -> str:
+    rng = np.random.default_rng(2200 + seed)
+    inputs = [f"f{j}" for j in range(F)]
+    avail = list(inputs)
+    segs = []
+    n_seg = int(rng.integers(2, 6))
+    for k in range(n_seg):
+        model = _tree(rng, avail, int(rng.integers(1, 4))) if rng.random() < 0.6 else _linear(rng, avail)
+        used = sorted({f for f in avail if f'"{f}"' in model})
+        ms = "<MiningSchema>" + "".join(f'<MiningField name="{f}"/>' for f in used) + "</MiningSchema>"
+        out = ""
+        new = []
+        if k < n_seg - 1:
+            out = f'<OutputField name="t{k}" optype="continuous" dataType="double" feature="predictedValue"/>'
+            new.append(f"t{k}")
+            if rng.random() < 0.4:
+                out += (f'<OutputField name="u{k}" optype="continuous" dataType="double" feature="transformedValue">'
+                        f'<Apply function="*"><FieldRef field="t{k}"/><Constant>{rng.normal():.2f}</Constant></Apply>'
+                        '</OutputField>')
+                new.append(f"u{k}")
+            out = f"<Output>{out}</Output>"
+        if k == 0 or rng.random() < 0.5:
+            pred = "<True/>"
+        else:
+            f = str(rng.choice(avail))
+            op = str(rng.choice(["lessThan", "greaterThan", "greaterOrEqual"]))
+            pred = f'<SimplePredicate field="{f}" operator="{op}" value="{rng.normal() * 0.5:.3f}"/>'
+        segs.append(f'<Segment id="{k + 1}">{pred}{model.replace("{ms}", ms).replace("{out}", out)}</Segment>')
+        avail += new
+    fields = "".join(f'<DataField name="{f}" optype="continuous" dataType="double"/>' for f in inputs)
+    ms = '<MiningSchema><MiningField name="y" usageType="target"/>' + \
+        "".join(f'<MiningField name="{f}"/>' for f in inputs) + "</MiningSchema>"
+    return (f'<PMML version="4.4" xmlns="{NS}"><DataDictionary>{fields}'
+            '<DataField name="y" optype="continuous" dataType="double"/></DataDictionary>'
+            f'<MiningModel functionName="regression">{ms}<Segmentation multipleModelMethod="modelChain">'
+            f'{"".join(segs)}</Segmentation></MiningModel></PMML>')
+
+
+def _inputs(n, seed):
+    from flink_jpmml_amd.bench.synth import stream_matrix
+
+    return stream_matrix(n, F, seed=seed, missing_rate=0.05)
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_random_chains_load_and_lower(seed):
+    from flink_jpmml_amd.runtime.plans import lowering_dry_run
+    from flink_jpmml_amd.runtime.segmented import ChainPlan
+
+    c = CompiledPmml.from_string(_doc(seed))
+    _, v = c.score_matrix_oracle(_inputs(500, seed))
+    assert v.any()
+    with lowering_dry_run():
+        assert isinstance(c.plan("cpu"), ChainPlan)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(40))
+def test_random_chains_on_gpu(gpu, seed):
+    c = CompiledPmml.from_string(_doc(seed))
+    plan = c.plan(gpu)
+    X = _inputs(8000, seed)
+    s, v = plan.score(X)
+    s, v = s.cpu().numpy().astype(np.float64), v.cpu().numpy().astype(bool)
+    ref, vref = c.score_matrix_oracle(X)
+    assert (v == vref).all(), (seed, type(plan).__name__, int((v != vref).sum()))
+    if v.any():
+        scale = np.maximum(1.0, np.abs(ref[v]))
+        # a chained tree splits on an earlier segment's fp32 output: a row within fp32 of a
+        # threshold may take the other branch
+        assert (np.abs(s[v] - ref[v]) <= 2e-4 * scale).mean() >= 0.998, (seed, type(plan).__name__)
