@@ -985,10 +985,18 @@ def _perfect_pack_loop(trees, weights, P: int, D: int, stride: int, fmap, leaf_b
         nodes_meta = np.zeros(NI, dtype=np.uint32)
         leaves = np.zeros((NL, P), dtype=np.float32)
         dr_bits = np.zeros(ndr * 32, dtype=np.uint32)
-        stack = [(0, 0, 0)]  # (node k, level-order index p, depth)
+        stack = [(0, 0, 0, None)]  # (node k, level-order index p, depth, parent split's meta)
         while stack:
-            k, p, d = stack.pop()
+            k, p, d, pm = stack.pop()
             if t.feature[k] < 0:
+                # the padded nodes below a leaf above depth D read the parent split's column: the
+                # walk visited it already, so a NaN there cannot newly null a nullPrediction tree
+                # (column 0 could be missing when the path never touched it)
+                if pm is not None:
+                    q, cnt = p, 1
+                    while q < NI:
+                        nodes_meta[q: min(q + cnt, NI)] = pm
+                        q, cnt = 2 * q + 1, 2 * cnt
                 if leaf_bits == "vote8":
                     val = np.array([np.uint32(1 << (8 * int(t.leaf_value[k]))).view(np.float32)])
                 else:
@@ -1019,9 +1027,9 @@ def _perfect_pack_loop(trees, weights, P: int, D: int, stride: int, fmap, leaf_b
             if dr:
                 dr_bits[p] = 1
                 has_dr = True
-            stack.append((left_child, 2 * p + 1, d + 1))
-            stack.append((right_child, 2 * p + 2, d + 1))
-        if t.null_missing:
+            stack.append((left_child, 2 * p + 1, d + 1, nodes_meta[p]))
+            stack.append((right_child, 2 * p + 2, d + 1, nodes_meta[p]))
+        if t.null_missing and t.feature[0] >= 0:
             dr_bits[NI] = 1  # tree-level null-on-missing flag (node index NI does not exist)
         blob[ti, 0: 2 * NI: 2] = nodes_T.view(np.uint32)
         blob[ti, 1: 2 * NI: 2] = nodes_meta
@@ -1076,18 +1084,23 @@ def _perfect_pack_vec(trees, weights, P: int, D: int, stride: int, fmap, leaf_bi
     nodes_meta = np.zeros((n, NI), np.uint32)
     dr_bits = np.zeros((n, ndr * 32), np.uint32)
     cur = off.copy()[:, None]  # [n, 1] node at each heap position of the current level
+    pm = np.full((n, 1), -1, np.int64)  # meta of the deepest real split above (-1: none)
     for d in range(D):
         split = feat[cur] >= 0
         p0 = (1 << d) - 1
         sl = slice(p0, p0 + (1 << d))
         nodes_T[:, sl] = np.where(split, T[cur], 0.0)
-        nodes_meta[:, sl] = np.where(split, (col[cur] * stride * 4).astype(np.uint32), 0)
+        # padded nodes (below a leaf above depth D) read the parent split's column, which the walk
+        # visited already: a NaN in a column the path never touched must not null the tree
+        meta = np.where(split, col[cur] * stride * 4, np.maximum(pm, 0))
+        nodes_meta[:, sl] = meta.astype(np.uint32)
         dr_bits[:, sl] = np.where(split, dr[cur], False)
         # a leaf above depth D covers its whole padded subtree: both "children" are itself
         nxt = np.empty((n, 2 << d), np.int64)
         nxt[:, 0::2] = np.where(split, lc[cur], cur)
         nxt[:, 1::2] = np.where(split, rc[cur], cur)
         cur = nxt
+        pm = np.repeat(np.where(split, meta, pm), 2, axis=1)
     if (feat[cur] >= 0).any():
         raise NotLowerable("tree deeper than the PERFECT depth")
     if leaf_bits == "vote8":
@@ -1101,7 +1114,7 @@ def _perfect_pack_vec(trees, weights, P: int, D: int, stride: int, fmap, leaf_bi
         leaves = (lv[cur] * w_node[cur]).astype(np.float32)[..., None]
     has_dr = bool(dr_bits.any())
     for ti, t in enumerate(trees):
-        if t.null_missing:
+        if t.null_missing and t.feature[0] >= 0:  # a single-leaf tree never visits a split
             dr_bits[ti, NI] = 1
     blob = np.zeros((n, rec), dtype=np.uint32)
     blob[:, 0:2 * NI:2] = nodes_T.view(np.uint32)

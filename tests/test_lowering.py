@@ -326,3 +326,31 @@ def test_vectorised_perfect_pack_is_bit_identical():
             a = _perfect_pack_loop(spec.trees, spec.weights, spec.P, D, stride, fmap, leaf_bits, rec)
             b = _perfect_pack_vec(spec.trees, spec.weights, spec.P, D, stride, fmap, leaf_bits, rec)
             assert np.array_equal(a[0], b[0]) and a[1:] == b[1:], (leaf_bits, general, stride)
+
+
+def test_null_prediction_padding_reads_a_visited_column():
+    """An unbalanced nullPrediction tree: a leaf above the PERFECT depth is padded down to depth D,
+    and the padded nodes must read a column the walk already visited (their parent split's), not
+    column 0 — a row whose path never touches the missing column 0 keeps its prediction (the
+    r5av chain-fuzz failure: 1-2.5 % of rows wrongly EmptyScore on the device)."""
+    ns = "http://www.dmg.org/PMML-4_4"
+    doc = (f'<PMML version="4.4" xmlns="{ns}"><DataDictionary>'
+           '<DataField name="f0" optype="continuous" dataType="double"/>'
+           '<DataField name="f1" optype="continuous" dataType="double"/>'
+           '<DataField name="y" optype="continuous" dataType="double"/></DataDictionary>'
+           '<TreeModel functionName="regression" missingValueStrategy="nullPrediction" splitCharacteristic="binarySplit">'
+           '<MiningSchema><MiningField name="y" usageType="target"/><MiningField name="f0"/><MiningField name="f1"/>'
+           '</MiningSchema><Node id="r" score="0"><True/>'
+           '<Node id="a" score="1.5"><SimplePredicate field="f1" operator="lessThan" value="0.2"/></Node>'
+           '<Node id="b" score="2"><SimplePredicate field="f1" operator="greaterOrEqual" value="0.2"/>'
+           '<Node id="c" score="-1"><SimplePredicate field="f0" operator="lessThan" value="0"/></Node>'
+           '<Node id="d" score="4"><SimplePredicate field="f0" operator="greaterOrEqual" value="0"/></Node>'
+           '</Node></Node></TreeModel></PMML>')
+    c = CompiledPmml.from_string(doc)
+    X = np.array([[np.nan, -1.0], [np.nan, 1.0], [0.5, np.nan], [-0.5, 1.0], [np.nan, 0.1]])
+    ref, vref = c.score_matrix_oracle(X)
+    assert list(vref) == [True, False, False, True, True]
+    spec, acc = emulate_perfect(c, X)
+    out = _scores(spec, acc)
+    assert (np.isfinite(out) == vref).all()
+    assert np.allclose(out[vref], ref[vref])
