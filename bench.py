@@ -25,8 +25,9 @@ Under ``torchrun`` the model is parsed once on rank 0 and its compiled tensors a
 RCCL-broadcast to every rank (F2). Rank 0 prints ONE JSON line.
 
     python bench.py                                # 1 GPU, defaults
+    python bench.py --gpus 8 --steps 20 --warmup 3   # spawns the 8 ranks itself (launch_ranks)
     python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \\
-        --master-port 29500 bench.py --gpus 8 --steps 20 --warmup 3
+        --master-port 29500 bench.py --gpus 8 --steps 20 --warmup 3   # same job, external launcher
     python bench.py --model rf|chain|mlp           # BASELINE configs 3 / 5 / 4
 """
 
@@ -274,8 +275,79 @@ def _rehearsal_check(args, sink, ctx, doc_paths):
     return ok and checked == (args.warmup + args.steps) * args.passes * args.rows, checked
 
 
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _needs_launch(args) -> bool:
+    """``--gpus N > 1`` without a launcher (no ``WORLD_SIZE`` in the environment): this process
+    only spawns the N ranks (SURVEY §2.6 F3 — one process per GPU)."""
+    return args.gpus > 1 and "WORLD_SIZE" not in os.environ and not os.environ.get("FJA_BENCH_CHILD")
+
+
+def launch_ranks(args, argv) -> int:
+    """Spawn ``--gpus N`` fresh rank processes through ``torch.distributed.run`` and relay rank 0's
+    JSON line; returns the launcher's exit status (non-zero if any rank failed — the elastic agent
+    then terminates the surviving siblings). Called BEFORE this process makes any GPU call: the
+    parent never touches the GPU (no ``torch.cuda.is_available()``), and it never ``exec``s — the
+    ranks are children, the parent exits with their status.
+
+    With the RCCL backend every rank needs its own GPU, so N must not exceed the visible device
+    count (``torch.cuda.device_count()`` does not initialise the GPU on this image);
+    ``FJA_DIST_BACKEND=gloo`` (or ``--rehearse-cpu``) lets N ranks share fewer GPUs / run on CPUs."""
+    import signal
+    import subprocess
+
+    n = args.gpus
+    if not args.rehearse_cpu and os.environ.get("FJA_DIST_BACKEND", "nccl") != "gloo":
+        import torch
+
+        have = torch.cuda.device_count()
+        if have < n:
+            print(json.dumps({"metric": METRIC, "error": f"--gpus {n} but {have} GPU(s) visible "
+                              "(set FJA_DIST_BACKEND=gloo to share GPUs between ranks)"}), flush=True)
+            return 1
+    env = dict(os.environ, FJA_BENCH_CHILD="1")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", str(max(1, (os.cpu_count() or n) // n)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__), *argv]
+    proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True, start_new_session=True)
+    last_json = None
+    try:
+        for line in proc.stdout:  # rank 0 is the only rank that prints to stdout
+            sys.stdout.write(line)
+            sys.stdout.flush()
+            if line.lstrip().startswith("{"):
+                last_json = line
+        rc = proc.wait()
+    except BaseException:
+        try:
+            os.killpg(proc.pid, signal.SIGTERM)
+            proc.wait(timeout=30)
+        except Exception:  # noqa: BLE001 - the group is gone or will not die: SIGKILL it
+            try:
+                os.killpg(proc.pid, signal.SIGKILL)
+            except OSError:
+                pass
+        raise
+    if rc == 0 and last_json is None:
+        print("error: the ranks exited without rank 0's JSON line", file=sys.stderr)
+        return 1
+    return rc
+
+
 def main(argv=None) -> int:
-    args = parse_args(argv)
+    raw_argv = list(sys.argv[1:] if argv is None else argv)
+    args = parse_args(raw_argv)
+    if _needs_launch(args):
+        return launch_ranks(args, raw_argv)
     import torch
     import torch.distributed as dist
 

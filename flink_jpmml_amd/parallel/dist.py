@@ -38,6 +38,8 @@ class DistContext:
     """Run the collective code path even at world size 1 (a 1-rank RCCL group: lets a single-GPU
     box execute every broadcast / all-gather / all-reduce on real RCCL)."""
     groups: dict = field(default_factory=dict)
+    group_backends: dict = field(default_factory=dict)
+    """Backend each named group was created with (``"gloo"`` or the data backend)."""
 
     @property
     def is_distributed(self) -> bool:
@@ -49,7 +51,11 @@ class DistContext:
 
         * ``"ctrl"`` (gloo) — the job thread: checkpoint state gathers, manifest broadcast, sink
           gathers of host objects;
-        * ``"model"`` (the data backend) — the model-loader thread: parse-once replication;
+        * ``"model_ctrl"`` (gloo) — the model-loader thread's host handshake: the parsed header,
+          errors and plan metadata, so ranks 1..N-1 wait for rank 0's parse on the HOST, not in a
+          device collective spinning on the GPU;
+        * ``"model"`` (the data backend) — the model-loader thread: the compiled tensor payload of
+          parse-once replication, issued only after the handshake said every rank is ready;
         * ``"replicate"`` (gloo) — the leader-read source pump thread (control streams, sockets);
         * ``"ckpt"`` (gloo) — the checkpoint-coordinator thread (time-based triggers).
 
@@ -101,10 +107,11 @@ def init_from_env(backend: Optional[str] = None, timeout_s: Optional[float] = No
         dist.init_process_group(**kw)
     if ctx.is_distributed:
         to = datetime.timedelta(seconds=timeout_s)
-        ctx.groups["ctrl"] = dist.new_group(backend="gloo", timeout=to)
-        ctx.groups["model"] = dist.new_group(backend=backend, timeout=to)
-        ctx.groups["replicate"] = dist.new_group(backend="gloo", timeout=to)
-        ctx.groups["ckpt"] = dist.new_group(backend="gloo", timeout=to)
+        # creation order is part of the protocol: every rank creates the same groups in this order
+        for name, be in (("ctrl", "gloo"), ("model", backend), ("replicate", "gloo"), ("ckpt", "gloo"),
+                         ("model_ctrl", "gloo")):
+            ctx.groups[name] = dist.new_group(backend=be, timeout=to)
+            ctx.group_backends[name] = be
     return ctx
 
 
@@ -133,15 +140,19 @@ def shard_range(n: int, rank: int, world: int) -> Tuple[int, int]:
 # --------------------------------------------------------------------------- replication
 
 
+def group_backend(ctx: DistContext, group) -> Optional[str]:
+    """Backend of ``group`` (``None`` = the default group, created with ``ctx.backend``)."""
+    if group is None:
+        return ctx.backend
+    for name, g in ctx.groups.items():
+        if g is group:
+            return ctx.group_backends.get(name, ctx.backend)
+    return ctx.backend
+
+
 def _obj_device(ctx: DistContext, group):
-    """Device for object collectives: CPU on gloo groups, the GPU on the RCCL default group."""
-    if group is not None and group is ctx.groups.get("ctrl"):
-        return None
-    if group is None and ctx.backend == "nccl":
-        return ctx.device
-    if group is not None and group is ctx.groups.get("model") and ctx.backend == "nccl":
-        return ctx.device
-    return None
+    """Device for object collectives: CPU on gloo groups, the GPU on RCCL groups."""
+    return ctx.device if group_backend(ctx, group) == "nccl" else None
 
 
 def broadcast_object(obj, ctx: DistContext, src: int = 0, group=None):

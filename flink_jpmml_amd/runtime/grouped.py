@@ -181,6 +181,12 @@ class GroupedScorer:
                 codes_t = torch.empty(n, dtype=cdt, pin_memory=True)
                 codes_t.numpy()[:] = c_np
             codes_np = codes_t.cpu().numpy() if codes_t.is_cuda else codes_t.numpy()
+            if codes_t is codes:  # pinned / device codes: the same range check as the host path
+                # (the device-counted kernels would otherwise answer EmptyScore silently
+                # where the host-counted path raises)
+                if len(codes_np) != n or (n and not (K >= 256 and cdt == torch.uint8) and (
+                        int(codes_np.max()) >= K or (cdt != torch.uint8 and int(codes_np.min()) < 0))):
+                    raise ValueError(f"model codes must be {n} values in [0, {K})")
         S = self.slice_rows(K)
         self._ensure(S, F)
         self._throttle()
@@ -289,11 +295,15 @@ class GroupedScorer:
         raw = torch.frombuffer(bytearray(ctypes.string_at(ctypes.addressof(host_arr), ctypes.sizeof(host_arr))),
                                dtype=torch.uint8)
         i32 = dict(dtype=torch.int32, device=dev)
-        dg = dict(key=key, scorers=list(scorers), K=K, n_entries=n_ent, launches=launches, host_arr=host_arr,
-                  models=raw.to(dev), order=torch.tensor(order or [0], **i32),
-                  tile_rows=torch.from_numpy(tile_rows).to(dev), counts=torch.zeros(K, **i32),
-                  ticket=torch.zeros(1, **i32), cursor=torch.empty(K, **i32), row_start=torch.empty(K + 1, **i32),
-                  tile_start=torch.empty(n_ent + 1, **i32), arg_size=ctypes.sizeof(TreeArgs))
+        # the zero-fills of ``counts`` / ``ticket`` (the last-workgroup ticket
+        # scheme needs both zero) and the table uploads are enqueued on the compute stream the
+        # group kernels run on, so stream order guarantees they land first
+        with torch.cuda.stream(self.pipe.comp):
+            dg = dict(key=key, scorers=list(scorers), K=K, n_entries=n_ent, launches=launches, host_arr=host_arr,
+                      models=raw.to(dev), order=torch.tensor(order or [0], **i32),
+                      tile_rows=torch.from_numpy(tile_rows).to(dev), counts=torch.zeros(K, **i32),
+                      ticket=torch.zeros(1, **i32), cursor=torch.empty(K, **i32), row_start=torch.empty(K + 1, **i32),
+                      tile_start=torch.empty(n_ent + 1, **i32), arg_size=ctypes.sizeof(TreeArgs))
         if self._dg is not None:  # queued kernels may still read the old tables
             for t in (self._dg["models"], self._dg["order"], self._dg["tile_rows"], self._dg["counts"],
                       self._dg["ticket"], self._dg["cursor"], self._dg["row_start"], self._dg["tile_start"]):

@@ -136,6 +136,11 @@ def load_replicated(path: str, ctx, device: Any = None, config: Any = None, pipe
 
     cfg = config or ScoringConfig()
     g = ctx.group("model")
+    # F2 ordering rule: the header / error / plan-metadata handshake runs on the
+    # loader thread's own GLOO group, so ranks 1..N-1 block on the host while rank 0 reads, parses
+    # and lowers (seconds for a large document) -- no device collective spins on the GPU meanwhile.
+    # The RCCL payload broadcast on ``model`` is issued only after it, when every rank is ready.
+    gh = ctx.groups.get("model_ctrl") or ctx.group("ctrl")
     t0 = time.perf_counter()
     compiled = plan = None
     head: dict = {}
@@ -157,7 +162,7 @@ def load_replicated(path: str, ctx, device: Any = None, config: Any = None, pipe
                     # broadcast until the timeout): all ranks then fall back or fail alike
                     plan = None
                     head["lower_error"] = f"{type(e).__name__}: {e}"
-        head = broadcast_object(head, ctx, group=g)
+        head = broadcast_object(head, ctx, group=gh)
         if "err" in head:
             raise ModelLoadingException(f"model at {path}: {head['err']}")
         meta = head.get("plan_meta")

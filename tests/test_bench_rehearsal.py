@@ -83,6 +83,38 @@ def test_rehearsal_check_catches_misplaced_rows():
         os.unlink(path)
 
 
+def test_bench_spawns_its_own_ranks_without_a_launcher(tmp_path):
+    """the driver's bare ``bench.py --gpus N`` (no torchrun, no WORLD_SIZE) must
+    run N ranks — the parent spawns them and relays rank 0's JSON line."""
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT", "MASTER_ADDR", "FJA_BENCH_CHILD"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--rehearse-cpu", "--rows", "512",
+           "--passes", "2", "--steps", "1", "--warmup", "1", "--trees", "12", "--check-rows", "128",
+           "--latency-iters", "2"]
+    r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.lstrip().startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]  # exactly one JSON line: rank 0's
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 4 and out["config"]["parallelism"] == "dp4"
+    assert out["job"]["rehearsal_gather_check"] == [True] * 4
+
+
+def test_bench_launcher_fails_when_a_rank_fails(tmp_path):
+    """A rank that dies makes the launcher exit non-zero (the siblings are torn down)."""
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT", "MASTER_ADDR", "FJA_BENCH_CHILD"):
+        env.pop(k, None)
+    # --models with a file source is refused inside every rank (SystemExit) after the group formed
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--rehearse-cpu", "--rows", "256",
+           "--passes", "1", "--steps", "1", "--warmup", "1", "--trees", "4", "--check-rows", "0",
+           "--models", "2", "--source", "binary"]
+    r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode != 0
+    assert not any(ln.lstrip().startswith("{") for ln in r.stdout.splitlines())
+
+
 def test_bench_two_rank_cpu_rehearsal(tmp_path):
     env = dict(os.environ, PYTHONPATH=ROOT)
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT"):

@@ -136,6 +136,50 @@ def job_exactly_once(kmeans, out_dir, ck_dir, restore):
     return "done"
 
 
+def job_midstream_adds_with_gather(kmeans, n_batches, rows):
+    """Add messages arrive mid-stream while the library GatherSink all-gathers scored batches; every
+    object collective of the loader thread is recorded with the process group it used."""
+    import threading
+
+    import numpy as np
+
+    from flink_jpmml_amd import AddMessage
+    from flink_jpmml_amd.api.batch import RecordBatch
+    from flink_jpmml_amd.parallel import dist as D
+    from flink_jpmml_amd.parallel.sinks import GatherSink
+    from flink_jpmml_amd.stream import StreamExecutionEnvironment
+
+    calls = []
+    orig = D.broadcast_object
+
+    def spy(obj, ctx, src=0, group=None):
+        name = next((k for k, g in ctx.groups.items() if g is group), None)
+        calls.append((threading.current_thread().name, name))
+        return orig(obj, ctx, src, group)
+
+    D.broadcast_object = spy
+    N3 = "a1b2c3d4-0000-4000-8000-000000000003"
+    rng = np.random.default_rng(3)
+    seq = [("R", AddMessage(N1, 1, kmeans, 0))]
+    for i in range(n_batches):
+        X = rng.uniform(0.2, 7.0, size=(rows, 4))
+        ids = [N1, N2, N3][i % 3] if i >= 6 else N1
+        seq.append(("L", RecordBatch(X, model_id=f"{ids}_1", offset=i * rows)))
+        if i == 3:
+            seq.append(("R", AddMessage(N2, 1, kmeans, 0)))  # mid-stream, while gathers are in flight
+        if i == 5:
+            seq.append(("R", AddMessage(N3, 1, kmeans, 0)))
+    env = StreamExecutionEnvironment.get_execution_environment()
+    events, control = env.from_either(seq)
+    sink = GatherSink(to="all")
+    events.with_support_stream(control).quick_evaluate().add_sink(sink)
+    env.execute("midstream-adds")
+    sink.finish()
+    loader = [(t, g) for t, g in calls if t.startswith("model-loader")]
+    order = np.argsort(sink.offsets)
+    return loader, sink.scores[order].tolist(), sink.valid[order].tolist(), sink.offsets[order].tolist()
+
+
 # ------------------------------------------------------------------ tests
 
 
@@ -444,3 +488,26 @@ def test_supervisor_sigterm_stops_its_ranks(tmp_path):
     finally:
         if sup.poll() is None:
             sup.kill()
+
+
+def test_replicated_loads_handshake_on_gloo_while_gathers_run(fixtures_dir):
+    """with Add messages arriving mid-stream while GatherSink all-gathers run
+    on the job thread, the loader thread's object handshake (header / errors / plan metadata) uses
+    its own gloo group (``model_ctrl``) -- never the data-backend ``model`` group, which is RCCL on
+    GPUs -- and every rank gathers the same, correct scores."""
+    from flink_jpmml_amd.api.pmml_model import PmmlModel
+
+    world, n_batches, rows = 4, 12, 50
+    res, codes = _spawn(world, job_midstream_adds_with_gather, (fixtures_dir["kmeans"], n_batches, rows),
+                        timeout=300)
+    assert codes == [0] * world, res
+    rng = np.random.default_rng(3)
+    X = np.concatenate([rng.uniform(0.2, 7.0, size=(rows, 4)) for _ in range(n_batches)])
+    ref = PmmlModel.from_path(fixtures_dir["kmeans"]).predict(X).values(-1.0)
+    for r in range(world):
+        loader, scores, valid, offs = res[r]
+        assert len(loader) == 3, loader  # one handshake per Add, on the loader thread
+        assert {g for _, g in loader} == {"model_ctrl"}, loader
+        assert offs == list(range(n_batches * rows))
+        assert all(valid)
+        np.testing.assert_allclose(scores, ref, rtol=0, atol=1e-9)

@@ -220,3 +220,68 @@ def test_device_counted_grouped_pass(gpu, tmp_path, n_models):
         ref, vref = oracles[i % len(docs)].score_matrix_oracle(X[rows])
         assert (pb.valid[rows] == vref).all(), i
         np.testing.assert_allclose(pb.scores[rows][vref], ref[vref], atol=2e-5, rtol=0)
+
+
+@pytest.mark.gpu
+def test_device_tables_built_while_default_stream_busy(gpu, tmp_path):
+    """the device-counted tables (zeroed ``counts`` / ``ticket``) must be ready
+    on the compute stream even when the default stream is still busy when they are created."""
+    import torch
+
+    from flink_jpmml_amd.runtime.compiled import CompiledPmml
+    from flink_jpmml_amd.runtime.engine import DevicePipeline
+    from flink_jpmml_amd.runtime.grouped import GroupedScorer
+    from flink_jpmml_amd.runtime.loading import load_local
+
+    F = 16
+    docs = [synth.gbdt_pmml(n_trees=40, depth=6, n_features=F, seed=s) for s in (11, 12, 13)]
+    cfg = ScoringConfig(device=gpu, fallback="error", micro_batch=1 << 16)
+    pipe = DevicePipeline(gpu, micro_batch=1 << 16)
+    models = []
+    for i, d in enumerate(docs):
+        p = tmp_path / f"s{i}.pmml"
+        p.write_text(d)
+        models.append(load_local(str(p), gpu, cfg, pipe).model)
+    n = 200_003
+    X = synth.stream_matrix(n, F, seed=3, missing_rate=0.02).astype(np.float32)
+    code = np.random.default_rng(1).integers(0, 3, n).astype(np.uint8)
+    gs = GroupedScorer(pipe)
+    # poison the allocator's next int32 blocks, then keep the default stream busy while the tables
+    # are created: a zero-fill enqueued there would land after the count kernel ran
+    junk = torch.full((1 << 20,), 12345, dtype=torch.int32, device=gpu)
+    del junk
+    torch.cuda._sleep(200_000_000)
+    pb = gs.submit(RecordBatch(X), torch.from_numpy(code).pin_memory(), [m.scorer for m in models])
+    pb.wait()
+    torch.cuda.synchronize()
+    for k, d in enumerate(docs):
+        rows = np.flatnonzero(code == k)
+        ref, vref = CompiledPmml.from_string(d).score_matrix_oracle(X[rows])
+        assert (pb.valid[rows] == vref).all(), k
+        np.testing.assert_allclose(pb.scores[rows][vref], ref[vref], atol=2e-5, rtol=0)
+
+
+@pytest.mark.gpu
+def test_out_of_range_pinned_codes_raise_like_host_codes(gpu, tmp_path):
+    """pinned codes outside [0, K) raise ValueError on the device-counted path too."""
+    import torch
+
+    from flink_jpmml_amd.runtime.engine import DevicePipeline
+    from flink_jpmml_amd.runtime.grouped import GroupedScorer
+    from flink_jpmml_amd.runtime.loading import load_local
+
+    F = 8
+    pipe = DevicePipeline(gpu, micro_batch=1 << 14)
+    cfg = ScoringConfig(device=gpu, fallback="error", micro_batch=1 << 14)
+    scorers = []
+    for s in (1, 2):
+        p = tmp_path / f"o{s}.pmml"
+        p.write_text(synth.gbdt_pmml(n_trees=8, depth=4, n_features=F, seed=s))
+        scorers.append(load_local(str(p), gpu, cfg, pipe).model.scorer)
+    X = synth.stream_matrix(1000, F, seed=2).astype(np.float32)
+    codes = torch.zeros(1000, dtype=torch.uint8).pin_memory()
+    codes[17] = 5
+    with pytest.raises(ValueError):
+        GroupedScorer(pipe).submit(RecordBatch(X), codes, scorers)
+    with pytest.raises(ValueError):
+        GroupedScorer(pipe).submit(RecordBatch(X), codes.numpy().copy(), scorers)
