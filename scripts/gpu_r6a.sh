@@ -10,6 +10,6 @@ FJA_DIST_BACKEND=gloo timeout -k 10 300 python3 bench.py --gpus 2 --steps 5 --wa
 tail -c 600 $O/bench_gloo2.json
 timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench1.json 2> $O/bench1.err || { tail -30 $O/bench1.err; exit 1; }
 python3 -c "import json; d=json.loads(open('$O/bench1.json').read().strip().splitlines()[-1]); print(d['value'], d['n_gpus'], d['check'])"
-timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread --durations=0 -rf > $O/pytest_full.log 2>&1 || { tail -40 $O/pytest_full.log; exit 1; }
+timeout -k 10 820 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread --durations=0 -rf > $O/pytest_full.log 2>&1 || { tail -40 $O/pytest_full.log; exit 1; }
 tail -3 $O/pytest_full.log
 echo done
