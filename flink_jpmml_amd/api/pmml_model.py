@@ -5,8 +5,10 @@ Per-record API (reference parity)::
     prediction = model.predict(DenseVector(1, 1, 1, 1), replace_nan=None)   # Prediction(Score(3.0))
 
 runs ``validate → prepare → evaluate → extract`` under a Try and never raises for a bad record
-(`S/api/PmmlModel.scala:109-119`). The per-record path evaluates on the host in float64 — it is
-the semantic reference.
+(`S/api/PmmlModel.scala:109-119`). On a model bound to a device (the operators bind every model
+to the rank's GPU; ``ScoringConfig.device="auto"`` is the default) a conforming vector is scored
+as a 1-row batch by the device plan; unbound models, and vectors that fail validation, run the
+host float64 pipeline — the semantic reference (its tree walks in C++: ``models/native_tree.py``).
 
 Batch API (the MI355X path)::
 
@@ -116,6 +118,10 @@ class PmmlModel(Pipeline):
         batch = as_record_batch(input_vector)
         if batch is not None:
             return self.predict_records(batch, replace_nan)
+        if self.on_device:
+            pred = self._predict_one_device(input_vector, replace_nan)
+            if pred is not None:
+                return pred
 
         def run() -> float:
             validated = self.validate_input(input_vector)
@@ -124,6 +130,27 @@ class PmmlModel(Pipeline):
             return self.extract_target(result)
 
         return Prediction.extract_prediction(run)
+
+    def _predict_one_device(self, input_vector: Any, replace_nan: Optional[float]) -> Optional[Prediction]:
+        """The reference's per-record call (`S/package.scala:76-82,111-114`) on the bound device
+        plan: the vector is a 1-row batch through the same kernels as a columnar batch (whose row
+        ``i`` equals ``predict(batch.vector(i))``). Returns None — the caller then runs the host
+        pipeline, which produces the reference's exception / EmptyScore handling — for anything
+        that is not a conforming numeric vector."""
+        try:
+            vec = as_vector(input_vector)
+        except Exception:  # noqa: BLE001 - the host path reports the validation failure
+            return None
+        width = len(self.evaluator.model.active_fields)
+        if not isinstance(vec, Vector) or vec.size != width:
+            return None
+        X, absent, ok = pack_vectors_masked([vec], width)
+        if ok is not None and not ok[0]:
+            return None
+        pb = self._scorer.submit_batch(RecordBatch(X, absent=absent), replace_nan)
+        if not bool(pb.valid[0]):
+            return Prediction(EmptyScore)
+        return Prediction(Score(float(pb.scores[0])))
 
     def validate_input(self, v: Any) -> PmmlInput:
         """Size check against the active fields, then vector → map (`S/api/PmmlModel.scala:127-134`)."""

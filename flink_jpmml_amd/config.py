@@ -39,9 +39,10 @@ class ScoringConfig:
     trigger). ``None`` = size, control message, checkpoint barrier or end of input only."""
 
     # -- device placement and precision
-    device: Any = None
-    """HIP device for model kernels (``"cuda"``, ``"cuda:3"``); ``None`` = host float64 oracle.
-    Under ``torchrun`` every rank uses its own GPU (``cuda:LOCAL_RANK``) when this is ``"cuda"``."""
+    device: Any = "auto"
+    """HIP device for model kernels (``"cuda"``, ``"cuda:3"``); ``"auto"`` (default) = the rank's
+    GPU when one is visible, else the host; ``None`` / ``"cpu"`` = host float64 oracle. Under
+    ``torchrun`` every rank uses its own GPU (``cuda:LOCAL_RANK``) for ``"cuda"`` / ``"auto"``."""
     device_ids: Optional[Sequence[int]] = None
     """Explicit GPU per rank (``device_ids[local_rank]``), overrides the ``LOCAL_RANK`` default."""
     precision: str = "fp32"
@@ -122,7 +123,12 @@ class ScoringConfig:
             return None
         import torch
 
-        dev = torch.device(self.device) if not isinstance(self.device, torch.device) else self.device
+        if isinstance(self.device, str) and self.device == "auto":
+            if not torch.cuda.is_available():
+                return None
+            dev = torch.device("cuda")
+        else:
+            dev = torch.device(self.device) if not isinstance(self.device, torch.device) else self.device
         if dev.type != "cuda":
             return None if dev.type == "cpu" else dev
         if self.device_ids is not None:

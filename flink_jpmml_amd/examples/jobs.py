@@ -160,7 +160,7 @@ def build_parser() -> argparse.ArgumentParser:
                              "the reference's (IrisSource.scala:52)")
         sp.add_argument("--parallelism", type=int, default=1)
         sp.add_argument("--batch-size", type=int, default=None)
-        sp.add_argument("--device", default=None)
+        sp.add_argument("--device", default="auto", help="auto (GPU when visible, default), cuda[:i] or cpu")
         sp.add_argument("--seed", type=int, default=0)
         sp.add_argument("--rate", type=float, default=1.0,
                         help="Iris records per second (reference: 1, IrisSource.scala:52); 0 = unthrottled")

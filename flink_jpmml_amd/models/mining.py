@@ -48,9 +48,55 @@ class MiningEvaluator(ModelEvaluator):
         else:
             self.categories = None
 
+    # ------------------------------------------------------------------ native forest pass
+    _REGRESS_METHODS = ("sum", "weightedSum", "average", "weightedAverage", "max", "min", "median",
+                        "weightedMedian")
+
+    def native_forest(self):
+        """One :class:`~flink_jpmml_amd.models.native_tree.ForestProgram` over every segment when
+        this is a regression ensemble of plain trees (True segment predicates, regression trees
+        without outputs / local transformations / targets): the whole segment loop is then one
+        native call producing the ``[rows, segments]`` value matrix ``_regress`` aggregates.
+        None otherwise (built once)."""
+        prog = getattr(self, "_native", False)
+        if prog is False:
+            prog = None
+            from .tree import TreeEvaluator
+
+            if self.kind == "regression" and self.method in self._REGRESS_METHODS and self.sub and all(
+                    isinstance(seg.predicate, ir.TruePredicate) and type(ev) is TreeEvaluator
+                    and ev.kind == "regression" and not ev.model.output and not ev.model.local_transformations
+                    and ev.target is None for seg, ev in zip(self.segments, self.sub)):
+                from .native_tree import forest_program
+
+                prog = forest_program(self.sub, [ev.node_value for ev in self.sub])
+            self._native = prog
+        return prog
+
     def _evaluate(self, cols: Columns) -> ModelResult:
         n = cols.n
         method = self.method
+        prog = self.native_forest() if n else None
+        if prog is not None:
+            try:
+                X = prog.matrix(cols)
+            except Exception:  # noqa: BLE001 - a field the segments reference cannot be prepared
+                X = None
+            if X is not None:
+                if method in ("sum", "weightedSum", "average", "weightedAverage") and not is_float(self.mm) \
+                        and self.mm.missing_prediction_treatment != "skipSegment":
+                    # every segment applies: a row is valid iff no tree is null, and the value is
+                    # _regress's np.sum over the row (the native sum reproduces its pairwise order)
+                    weighted = method in ("weightedSum", "weightedAverage")
+                    out = prog.sums(X, self.weights if weighted else None)
+                    with np.errstate(invalid="ignore", divide="ignore"):
+                        if method == "average":
+                            out = out / len(self.sub)
+                        elif method == "weightedAverage":
+                            out = out / np.sum(self.weights)
+                    return ModelResult("regression", out, np.isfinite(out))
+                V = prog.values(X)
+                return self._regress_matrix(V, np.ones(V.shape, dtype=bool))
         results: List[ModelResult] = []
         applies: List[np.ndarray] = []
         chain = method == "modelChain"
@@ -122,6 +168,11 @@ class MiningEvaluator(ModelEvaluator):
     def _regress(self, results: List[ModelResult], applies: List[np.ndarray]) -> ModelResult:
         V = np.stack([np.where(r.valid, r.value, NAN) for r in results], axis=1)
         A = np.stack(applies, axis=1)
+        return self._regress_matrix(V, A)
+
+    def _regress_matrix(self, V: np.ndarray, A: np.ndarray) -> ModelResult:
+        """Aggregate the ``[rows, segments]`` values ``V`` (NaN = no prediction) of the segments
+        that apply (``A``)."""
         W = np.broadcast_to(self.weights[None, :], V.shape)
         miss = np.isnan(V) & A
         skip = self.mm.missing_prediction_treatment == "skipSegment"

@@ -29,6 +29,7 @@ produces the (feature, threshold, op, default-direction, leaf) arrays of
 
 from __future__ import annotations
 
+from collections.abc import Sequence
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Tuple
 
@@ -51,6 +52,32 @@ class _RowView:
 
     def get(self, name: str) -> np.ndarray:
         return self.cols.get(name)[self.rows]
+
+
+class EntityLabels(Sequence):
+    """Per-row ``entityId`` of the scoring node (None for a null prediction), materialised only
+    when an output asks for it (a list comprehension per tree and batch otherwise dominated the
+    host scoring of large ensembles)."""
+
+    def __init__(self, ev: "TreeEvaluator", leaf: np.ndarray):
+        self._ev = ev
+        self._leaf = leaf
+        self._list: Optional[List[Optional[str]]] = None
+
+    def _materialise(self) -> List[Optional[str]]:
+        if self._list is None:
+            ids = [nd.id for nd in self._ev.nodes]
+            self._list = [ids[i] if i >= 0 else None for i in self._leaf.tolist()]
+        return self._list
+
+    def __len__(self) -> int:
+        return int(self._leaf.shape[0])
+
+    def __getitem__(self, i):
+        return self._materialise()[i]
+
+    def __iter__(self):
+        return iter(self._materialise())
 
 
 class TreeEvaluator(ModelEvaluator):
@@ -164,8 +191,32 @@ class TreeEvaluator(ModelEvaluator):
             probs[dn, code[a["dist_value_s"]]] = p
         self.node_probs = probs
 
+    def native_program(self):
+        """This tree's :class:`~flink_jpmml_amd.models.native_tree.ForestProgram` (built once), or
+        None when the tree keeps the numpy walk."""
+        prog = getattr(self, "_native", False)
+        if prog is False:
+            from .native_tree import tree_program
+
+            prog = self._native = tree_program(self)
+        return prog
+
     def leaf_index(self, cols: Columns) -> np.ndarray:
-        """Index (into ``self.nodes``) of the scoring node per row; -1 = null prediction."""
+        """Index (into ``self.nodes``) of the scoring node per row; -1 = null prediction. Runs the
+        native walker (``models/native_tree.py``, the same decisions in C++) when the tree has a
+        program and every field it references can be prepared, else the numpy walk below."""
+        prog = self.native_program()
+        if prog is not None and cols.n:
+            try:
+                X = prog.matrix(cols)
+            except Exception:  # noqa: BLE001 - e.g. a field only unreachable nodes reference
+                X = None
+            if X is not None:
+                return prog.leaves(X)[0].astype(np.int64)
+        return self.leaf_index_numpy(cols)
+
+    def leaf_index_numpy(self, cols: Columns) -> np.ndarray:
+        """The numpy-mask walk (the semantic reference of the native walker)."""
         n = cols.n
         out = np.full(n, -1, dtype=np.int64)
         strat = self.tree.missing_value_strategy
@@ -282,8 +333,7 @@ class TreeEvaluator(ModelEvaluator):
         leaf = self.leaf_index(cols)
         ok = leaf >= 0
         safe = np.where(ok, leaf, 0)
-        ids = [nd.id for nd in self.nodes]
-        ent = [ids[i] if o else None for i, o in zip(safe, ok)]
+        ent = EntityLabels(self, leaf)
         if self.kind == "classification":
             lab = np.where(ok, self.node_label[safe], NAN)
             ok = ok & ~np.isnan(lab)

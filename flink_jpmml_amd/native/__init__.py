@@ -44,7 +44,7 @@ def build(force: bool = False) -> str:
 
 
 FAST_SRC = os.path.join(HERE, "csrc", "fastpath.cpp")
-FAST_SRCS = [FAST_SRC, os.path.join(HERE, "csrc", "pmml_scan.cpp")]
+FAST_SRCS = [FAST_SRC, os.path.join(HERE, "csrc", "pmml_scan.cpp"), os.path.join(HERE, "csrc", "tree_walk.cpp")]
 _fast = None
 
 

@@ -357,3 +357,14 @@ def test_to_batches_dynamic_ids_and_latency(fixtures_dir):
     for mid, vals in out:
         got.setdefault(mid, []).extend(vals)
     assert got[f"{N1}_1"] == [3.0] * 5 and got[f"{N2}_1"] == [-1.0] * 5
+
+
+def test_device_auto_is_the_default_and_resolves_to_the_host_without_a_gpu():
+    import torch
+
+    cfg = ScoringConfig()
+    assert cfg.device == "auto"
+    if not torch.cuda.is_available():
+        assert cfg.resolve_device() is None
+    assert ScoringConfig(device="cpu").resolve_device() is None
+    assert ScoringConfig(device=None).resolve_device() is None
