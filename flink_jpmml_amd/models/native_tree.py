@@ -235,6 +235,20 @@ class ForestProgram:
                             i32(self.roots), i32(self.modes), lv)
         return self._arrays
 
+    def compiled(self):
+        """The walker's fixed-depth / perfect tables of this program, built once (a capsule tied
+        to the :meth:`arrays` buffers) so per-record calls do not rebuild them."""
+        cap = getattr(self, "_capsule", None)
+        if cap is None or cap[0] is not self._arrays:
+            from ..native import fastpath
+
+            arrs = self.arrays()
+            ni, nd, kids, pi, pd, ai, ad, roots, modes, _ = arrs
+            cap = (arrs, fastpath().forest_compile(ni, nd, kids, pi, pd, ai, ad, roots, modes,
+                                                   max(1, len(self.fields))))
+            self._capsule = cap
+        return cap[1]
+
     @property
     def n_trees(self) -> int:
         return len(self.roots)
@@ -258,7 +272,7 @@ class ForestProgram:
         X = np.ascontiguousarray(X, dtype=np.float64)
         ni, nd, kids, pi, pd, ai, ad, roots, modes, _ = self.arrays()
         out = np.empty((self.n_trees, X.shape[0]), dtype=np.int32)
-        fp.forest_leaves(ni, nd, kids, pi, pd, ai, ad, roots, modes, X, X.shape[1], out)
+        fp.forest_leaves(ni, nd, kids, pi, pd, ai, ad, roots, modes, X, X.shape[1], out, self.compiled())
         return out
 
     def values(self, X: np.ndarray) -> np.ndarray:
@@ -271,7 +285,7 @@ class ForestProgram:
         if lv.shape[0] != nd.shape[0]:
             raise ValueError("values() needs a leaf value for every node of every tree")
         out = np.empty((X.shape[0], self.n_trees), dtype=np.float64)
-        fp.forest_values(ni, nd, kids, pi, pd, ai, ad, roots, modes, X, X.shape[1], lv, out)
+        fp.forest_values(ni, nd, kids, pi, pd, ai, ad, roots, modes, X, X.shape[1], lv, out, self.compiled())
         return out
 
 
@@ -288,7 +302,7 @@ class ForestProgram:
             raise ValueError("sums() needs a leaf value for every node of every tree")
         w = None if weights is None else np.ascontiguousarray(weights, dtype=np.float64)
         out = np.empty(X.shape[0], dtype=np.float64)
-        fp.forest_sums(ni, nd, kids, pi, pd, ai, ad, roots, modes, X, X.shape[1], lv, w, out)
+        fp.forest_sums(ni, nd, kids, pi, pd, ai, ad, roots, modes, X, X.shape[1], lv, w, out, self.compiled())
         return out
 
 

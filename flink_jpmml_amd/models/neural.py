@@ -123,11 +123,56 @@ class NeuralEvaluator(ModelEvaluator):
         return np.stack(mats, axis=1)
 
     # ------------------------------------------------------------------ oracle
+    def _native_layers(self) -> List[Optional[Tuple[np.ndarray, np.ndarray, np.ndarray]]]:
+        """Per layer ``(order, W, b)`` for the native ``seq_affine`` when every neuron reads the
+        previous layer's neurons (or the inputs) in one shared connection order, else None."""
+        cached = getattr(self, "_native", None)
+        if cached is not None:
+            return cached
+        from ..native import fastpath
+
+        fp = fastpath()
+        out: List[Optional[Tuple[np.ndarray, np.ndarray, np.ndarray]]] = []
+        prev_ids = [inp.id for inp in self.nn.inputs]
+        for layer in self.nn.layers:
+            act, _, _ = self._layer_params(layer)
+            idx = {nid: i for i, nid in enumerate(prev_ids)}
+            entry = None
+            if fp is not None and hasattr(fp, "seq_affine") and act != "radialBasis" and layer.neurons:
+                srcs = [s for s, _ in layer.neurons[0].connections]
+                if all(src in idx for src in srcs) and all(
+                        len(neu.connections) == len(srcs) and all(c[0] == s for c, s in zip(neu.connections, srcs))
+                        for neu in layer.neurons):
+                    W = np.array([[w for _, w in neu.connections] for neu in layer.neurons],
+                                 dtype=np.float64).T.copy() if srcs else np.zeros((0, len(layer.neurons)))
+                    entry = (np.array([idx[s] for s in srcs], dtype=np.int32), np.ascontiguousarray(W),
+                             np.array([neu.bias for neu in layer.neurons], dtype=np.float64))
+            out.append(entry)
+            prev_ids = [n.id for n in layer.neurons]
+        self._native = out
+        return out
+
     def forward(self, A0: np.ndarray) -> Dict[str, np.ndarray]:
         vals: Dict[str, np.ndarray] = {inp.id: A0[:, i] for i, inp in enumerate(self.nn.inputs)}
         n = A0.shape[0]
-        for layer in self.nn.layers:
+        native = self._native_layers()
+        prev = [inp.id for inp in self.nn.inputs]
+        for li, layer in enumerate(self.nn.layers):
             act, thr, norm = self._layer_params(layer)
+            if native[li] is not None and n:
+                from ..native import fastpath
+
+                order, W, b = native[li]
+                Ap = np.ascontiguousarray(np.stack([vals[i] for i in prev], axis=1), dtype=np.float64)
+                Z = np.empty((n, len(layer.neurons)))
+                fastpath().seq_affine(Ap, Ap.shape[1], order, W, b, Z)
+                A = activate(act, Z, thr)
+                A = normalize_layer(norm, A)
+                for j, neu in enumerate(layer.neurons):
+                    vals[neu.id] = A[:, j]
+                prev = [neu.id for neu in layer.neurons]
+                continue
+            prev = [neu.id for neu in layer.neurons]
             Z = np.zeros((n, len(layer.neurons)))
             for j, neu in enumerate(layer.neurons):
                 if act == "radialBasis":

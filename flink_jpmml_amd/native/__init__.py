@@ -44,7 +44,8 @@ def build(force: bool = False) -> str:
 
 
 FAST_SRC = os.path.join(HERE, "csrc", "fastpath.cpp")
-FAST_SRCS = [FAST_SRC, os.path.join(HERE, "csrc", "pmml_scan.cpp"), os.path.join(HERE, "csrc", "tree_walk.cpp")]
+FAST_SRCS = [FAST_SRC, os.path.join(HERE, "csrc", "pmml_scan.cpp"), os.path.join(HERE, "csrc", "tree_walk.cpp"),
+             os.path.join(HERE, "csrc", "nn_host.cpp")]
 _fast = None
 
 
@@ -62,7 +63,8 @@ def build_fastpath(force: bool = False) -> str:
     if not force and os.path.exists(out) and all(os.path.getmtime(out) >= os.path.getmtime(s) for s in FAST_SRCS):
         return out
     tmp = out + ".tmp"
-    cmd = ["g++", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall", "-fvisibility=hidden",
+    # -ffp-contract=off: the oracle's sums round every product and every partial sum (no FMA)
+    cmd = ["g++", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared", "-Wall", "-fvisibility=hidden",
            "-I" + sysconfig.get_paths()["include"], "-I" + np.get_include(), *FAST_SRCS, "-o", tmp]
     r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
     if r.returncode != 0:

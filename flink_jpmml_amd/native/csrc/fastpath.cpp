@@ -12,7 +12,8 @@
 //                       EmptyScore prediction. Objects are allocated with tp_alloc and their slots
 //                       filled directly (the Python __init__s only assign those same slots).
 //   * scan_trees      — the streaming TreeModel reader of large PMML documents (pmml_scan.cpp).
-//   * forest_leaves / forest_values — the float64 oracle's tree walk in C++ (tree_walk.cpp).
+//   * forest_leaves / forest_values / forest_sums — the float64 oracle's tree walk in C++ (tree_walk.cpp).
+//   * seq_affine      — the oracle's NeuralNetwork layer sums in connection order (nn_host.cpp).
 //
 // Both return None / -1 when an input does not have the exact expected shape; the Python caller
 // then takes its general (slower, element-wise) path — results are identical either way.
@@ -29,9 +30,11 @@
 #include <vector>
 
 PyObject *fja_scan_trees(PyObject *, PyObject *args);     // pmml_scan.cpp
+PyObject *fja_forest_compile(PyObject *, PyObject *args); // tree_walk.cpp
 PyObject *fja_forest_leaves(PyObject *, PyObject *args);  // tree_walk.cpp
 PyObject *fja_forest_values(PyObject *, PyObject *args);  // tree_walk.cpp
 PyObject *fja_forest_sums(PyObject *, PyObject *args);    // tree_walk.cpp
+PyObject *fja_seq_affine(PyObject *, PyObject *args);     // nn_host.cpp
 
 namespace {
 
@@ -276,9 +279,11 @@ PyMethodDef methods[] = {
     {"pack_dense", pack_dense, METH_VARARGS, "Pack a list of DenseVector objects into a float64 matrix."},
     {"make_predictions", make_predictions, METH_VARARGS, "Prediction objects for a scored batch."},
     {"scan_trees", fja_scan_trees, METH_VARARGS, "Streaming TreeModel reader: (skeleton, flat trees, strings)."},
+    {"forest_compile", fja_forest_compile, METH_VARARGS, "Oracle tree walk: compile a program once (capsule)."},
     {"forest_leaves", fja_forest_leaves, METH_VARARGS, "Oracle tree walk: scoring node per tree and row."},
     {"forest_values", fja_forest_values, METH_VARARGS, "Oracle tree walk: leaf value per row and tree."},
     {"forest_sums", fja_forest_sums, METH_VARARGS, "Oracle tree walk: numpy-pairwise ensemble sum per row."},
+    {"seq_affine", fja_seq_affine, METH_VARARGS, "Oracle NeuralNetwork layer: bias + sum in connection order."},
     {nullptr, nullptr, 0, nullptr},
 };
 

@@ -358,18 +358,20 @@ struct Call {
     Py_ssize_t T = 0, n = 0, k = 0;
     bool has_weights = false;
 
+    PyObject *cache = Py_None;  // forest_compile's capsule of this program, or None
+
     bool parse(PyObject *args, Kind kind) {
         PyObject *o[14] = {};
         bool okp;
         if (kind == Kind::LEAVES)
-            okp = PyArg_ParseTuple(args, "OOOOOOOOOOnO", &o[0], &o[1], &o[2], &o[3], &o[4], &o[5], &o[6], &o[7], &o[8],
-                                   &o[9], &k, &o[11]);
+            okp = PyArg_ParseTuple(args, "OOOOOOOOOOnO|O", &o[0], &o[1], &o[2], &o[3], &o[4], &o[5], &o[6], &o[7],
+                                   &o[8], &o[9], &k, &o[11], &cache);
         else if (kind == Kind::VALUES)
-            okp = PyArg_ParseTuple(args, "OOOOOOOOOOnOO", &o[0], &o[1], &o[2], &o[3], &o[4], &o[5], &o[6], &o[7],
-                                   &o[8], &o[9], &k, &o[11], &o[12]);
+            okp = PyArg_ParseTuple(args, "OOOOOOOOOOnOO|O", &o[0], &o[1], &o[2], &o[3], &o[4], &o[5], &o[6], &o[7],
+                                   &o[8], &o[9], &k, &o[11], &o[12], &cache);
         else
-            okp = PyArg_ParseTuple(args, "OOOOOOOOOOnOOO", &o[0], &o[1], &o[2], &o[3], &o[4], &o[5], &o[6], &o[7],
-                                   &o[8], &o[9], &k, &o[11], &o[12], &o[13]);
+            okp = PyArg_ParseTuple(args, "OOOOOOOOOOnOOO|O", &o[0], &o[1], &o[2], &o[3], &o[4], &o[5], &o[6], &o[7],
+                                   &o[8], &o[9], &k, &o[11], &o[12], &o[13], &cache);
         if (!okp) return false;
         if (!ni.get(o[0], "i", 4, false, "nodes_i") || !nd.get(o[1], "d", 8, false, "nodes_d") ||
             !kids.get(o[2], "i", 4, false, "kids") || !pi.get(o[3], "i", 4, false, "preds_i") ||
@@ -542,6 +544,27 @@ void compile_all(const Call &c, Fixed &f) {
     }
 }
 
+// A compiled program kept across calls (forest_compile): the fixed-depth / perfect tables of a
+// 1000-tree ensemble take milliseconds to build, so per-record scoring must not rebuild them.
+// The fingerprint ties the tables to the exact program buffers they were built from.
+struct Cached {
+    Fixed f;
+    const void *ni, *kids, *pi, *roots;
+    Py_ssize_t n_nodes, T, k;
+};
+constexpr const char *CAPSULE = "fja.forest_program";
+
+void drop_cached(PyObject *cap) { delete static_cast<Cached *>(PyCapsule_GetPointer(cap, CAPSULE)); }
+
+const Fixed *cached_fixed(const Call &c) {
+    if (c.cache == nullptr || c.cache == Py_None || !PyCapsule_IsValid(c.cache, CAPSULE)) return nullptr;
+    const Cached *h = static_cast<const Cached *>(PyCapsule_GetPointer(c.cache, CAPSULE));
+    if (h == nullptr || h->ni != c.ni.b.buf || h->kids != c.kids.b.buf || h->pi != c.pi.b.buf ||
+        h->roots != c.roots.b.buf || h->n_nodes != c.prog.n_nodes || h->T != c.T || h->k != c.k)
+        return nullptr;  // not this program: the caller compiles afresh
+    return &h->f;
+}
+
 constexpr int G = 16;
 
 // G rows through one perfect tree (scalar, interleaved). Writes the scoring node (or -1).
@@ -706,9 +729,11 @@ PyObject *forest_leaves(PyObject *, PyObject *args) {
     int32_t *out = static_cast<int32_t *>(c.out.b.buf);
     const Py_ssize_t n = c.n;
     const bool avx = use_avx512(c);
+    const Fixed *fc = cached_fixed(c);
     Py_BEGIN_ALLOW_THREADS
-    Fixed f;
-    compile_all(c, f);
+    Fixed local;
+    if (fc == nullptr) compile_all(c, local);
+    const Fixed &f = fc ? *fc : local;
     for (Py_ssize_t r0 = 0; r0 < n; r0 += ROW_BLOCK) {
         const Py_ssize_t r1 = r0 + ROW_BLOCK < n ? r0 + ROW_BLOCK : n;
         run_block(c, f, X, r0, r1, avx, [&](Py_ssize_t t, Py_ssize_t r, int32_t g) {
@@ -727,9 +752,11 @@ PyObject *forest_values(PyObject *, PyObject *args) {
     double *out = static_cast<double *>(c.out.b.buf);
     const Py_ssize_t n = c.n, T = c.T;
     const bool avx = use_avx512(c);
+    const Fixed *fc = cached_fixed(c);
     Py_BEGIN_ALLOW_THREADS
-    Fixed f;
-    compile_all(c, f);
+    Fixed local;
+    if (fc == nullptr) compile_all(c, local);
+    const Fixed &f = fc ? *fc : local;
     for (Py_ssize_t r0 = 0; r0 < n; r0 += ROW_BLOCK) {
         const Py_ssize_t r1 = r0 + ROW_BLOCK < n ? r0 + ROW_BLOCK : n;
         run_block(c, f, X, r0, r1, avx, [&](Py_ssize_t t, Py_ssize_t r, int32_t g) {
@@ -757,9 +784,11 @@ PyObject *forest_sums(PyObject *, PyObject *args) {
     } catch (const std::bad_alloc &) {
         return PyErr_NoMemory();
     }
+    const Fixed *fc = cached_fixed(c);
     Py_BEGIN_ALLOW_THREADS
-    Fixed f;
-    compile_all(c, f);
+    Fixed local;
+    if (fc == nullptr) compile_all(c, local);
+    const Fixed &f = fc ? *fc : local;
     for (Py_ssize_t r0 = 0; r0 < n; r0 += ROW_BLOCK) {
         const Py_ssize_t r1 = r0 + ROW_BLOCK < n ? r0 + ROW_BLOCK : n;
         double *bb = buf.data();
@@ -773,8 +802,47 @@ PyObject *forest_sums(PyObject *, PyObject *args) {
     Py_RETURN_NONE;
 }
 
+// forest_compile(nodes_i, nodes_d, kids, preds_i, preds_d, aux_i, aux_d, roots, modes, k) -> capsule
+PyObject *forest_compile(PyObject *, PyObject *args) {
+    PyObject *o[9];
+    Call c;
+    if (!PyArg_ParseTuple(args, "OOOOOOOOOn", &o[0], &o[1], &o[2], &o[3], &o[4], &o[5], &o[6], &o[7], &o[8], &c.k))
+        return nullptr;
+    if (!c.ni.get(o[0], "i", 4, false, "nodes_i") || !c.nd.get(o[1], "d", 8, false, "nodes_d") ||
+        !c.kids.get(o[2], "i", 4, false, "kids") || !c.pi.get(o[3], "i", 4, false, "preds_i") ||
+        !c.pd.get(o[4], "d", 8, false, "preds_d") || !c.ai.get(o[5], "i", 4, false, "aux_i") ||
+        !c.ad.get(o[6], "d", 8, false, "aux_d") || !c.roots.get(o[7], "i", 4, false, "roots") ||
+        !c.modes.get(o[8], "i", 4, false, "modes"))
+        return nullptr;
+    c.prog = Program{static_cast<const int32_t *>(c.ni.b.buf),  static_cast<const double *>(c.nd.b.buf),
+                     static_cast<const int32_t *>(c.kids.b.buf), static_cast<const int32_t *>(c.pi.b.buf),
+                     static_cast<const double *>(c.pd.b.buf),   static_cast<const int32_t *>(c.ai.b.buf),
+                     static_cast<const double *>(c.ad.b.buf),   c.ni.n() / 8, c.kids.n(), c.pi.n() / 4, c.ai.n(),
+                     c.ad.n()};
+    c.T = c.roots.n();
+    if (c.modes.n() != c.T || c.nd.n() != c.prog.n_nodes || c.pd.n() != c.prog.n_preds || c.k < 1) {
+        PyErr_SetString(PyExc_ValueError, "tree walk: inconsistent program shapes");
+        return nullptr;
+    }
+    if (!c.validate()) return nullptr;
+    Cached *h = new (std::nothrow) Cached();
+    if (h == nullptr) return PyErr_NoMemory();
+    compile_all(c, h->f);
+    h->ni = c.ni.b.buf;
+    h->kids = c.kids.b.buf;
+    h->pi = c.pi.b.buf;
+    h->roots = c.roots.b.buf;
+    h->n_nodes = c.prog.n_nodes;
+    h->T = c.T;
+    h->k = c.k;
+    PyObject *cap = PyCapsule_New(h, CAPSULE, drop_cached);
+    if (cap == nullptr) delete h;
+    return cap;
+}
+
 }  // namespace
 
+PyObject *fja_forest_compile(PyObject *self, PyObject *args) { return forest_compile(self, args); }
 PyObject *fja_forest_leaves(PyObject *self, PyObject *args) { return forest_leaves(self, args); }
 PyObject *fja_forest_values(PyObject *self, PyObject *args) { return forest_values(self, args); }
 PyObject *fja_forest_sums(PyObject *self, PyObject *args) { return forest_sums(self, args); }

@@ -27,6 +27,9 @@ enum : uint32_t {
   FP_MISSING_VALUE = 1u << 12,     // x == pad is a missing value (DataField <Value property="missing">)
   FP_VALUE_MASK = 1u << 13,        // numeric categories: valid iff x integral, lo <= x < lo + 64 and
                                    // bit (x - lo) of the 64-bit mask in the out_lo / out_hi words
+  FP_VALUE_LIST = 1u << 14,        // DataField <Value property="missing"/"invalid"> lists: the pad word
+                                   // holds {offset 16 | n_missing 8 | n_invalid 8}; the values are
+                                   // fp32 words `offset` floats past this record (same buffer)
 };
 
 struct FieldPrep {
@@ -35,7 +38,8 @@ struct FieldPrep {
   float missing_repl;
   float invalid_repl;
   float out_lo, out_hi;  // outlier bounds (continuous) / FP_VALUE_MASK bits 0-31, 32-63 (categorical)
-  float pad;             // FP_MISSING_VALUE: the field's explicit missing value
+  float pad;             // FP_MISSING_VALUE: the field's explicit missing value;
+                         // FP_VALUE_LIST: {offset, n_missing, n_invalid} of its value lists
 };
 static_assert(sizeof(FieldPrep) == 32, "FieldPrep must stay 32 bytes (host mirror in ops/_lib.py)");
 
@@ -45,8 +49,18 @@ __device__ __forceinline__ float prep_value(float x, const FieldPrep& p, bool* b
   if (fl == 0u) return x;
   if (fl & FP_ROW_INVALID) { *bad = true; return x; }
   bool miss = (x != x) || ((fl & FP_MISSING_VALUE) && x == p.pad);
+  const float* vlist = nullptr;
+  uint32_t n_miss = 0u, n_inv = 0u;
+  if (fl & FP_VALUE_LIST) {
+    const uint32_t w = __float_as_uint(p.pad);
+    vlist = reinterpret_cast<const float*>(&p) + (w & 0xFFFFu);
+    n_miss = (w >> 16) & 0xFFu;
+    n_inv = w >> 24;
+    for (uint32_t i = 0; i < n_miss; ++i) miss = miss || (x == vlist[i]);
+  }
   if (!miss) {
     bool invalid = false;
+    for (uint32_t i = 0; i < n_inv; ++i) invalid = invalid || (x == vlist[n_miss + i]);
     if (fl & FP_HAS_INTERVAL) {
       bool lo_ok = (fl & FP_LO_OPEN) ? (x > p.lo) : (x >= p.lo);
       bool hi_ok = (fl & FP_HI_OPEN) ? (x < p.hi) : (x <= p.hi);

@@ -19,12 +19,17 @@ Checked, on fields whose data type is numeric (``integer`` / ``float`` / ``doubl
 over the whole document: transformation dictionary, every model's local transformations, tree
 nodes (object trees and the scanner's flat arrays, ``pmml/flat.py``), segment, rule and scorecard
 predicates. ``Array n=`` disagreeing with the number of entries is rejected by the parser
-(``pmml/parser.py::_parse_array``).
+(``pmml/parser.py::_parse_array``). Numbers follow Java's ``Double.parseDouble`` grammar
+(:func:`java_double_ok`): ``inf``, ``nan`` or ``1_000`` are not numbers to JPMML either.
+
+Deviation (documented in ``docs/PARITY.md``): the reference fails only the records whose
+evaluation reaches the bad literal (lazily, per record); here the whole document fails to load.
 """
 
 from __future__ import annotations
 
 import dataclasses
+import re
 from typing import Optional
 
 import numpy as np
@@ -36,6 +41,21 @@ _NUMERIC = ("integer", "float", "double")
 _COMPARE = ("equal", "notEqual", "lessThan", "lessOrEqual", "greaterThan", "greaterOrEqual")
 
 
+# java.lang.Double.parseDouble's decimal grammar (after its trim of characters <= U+0020):
+# optional sign, then NaN / Infinity (exact case) or digits with an optional fraction and
+# exponent. Python's float() also accepts "inf", "nan", "infinity" in any case and "1_000", which
+# Java rejects; Java's type suffixes (1.5f, 2d) and hex floats (0x1p3) are not accepted here either
+# (float() cannot read them, and no exporter writes them): such documents fail closed.
+_JAVA_DOUBLE = re.compile(r"[+-]?(NaN|Infinity|(\d+\.?\d*|\.\d+)([eE][+-]?\d+)?)")
+
+
+def java_double_ok(value: str) -> bool:
+    """Whether ``value`` parses as a Java double (the JPMML number grammar) and as a Python float
+    with the same value."""
+    v = value.strip(" \t\n\r\x0b\x0c\x00")
+    return bool(_JAVA_DOUBLE.fullmatch(v))
+
+
 def literal_ok(data_type: Optional[str], value: Optional[str]) -> bool:
     """Whether ``value`` is a literal of a field typed ``data_type`` (untyped / string: any)."""
     if data_type not in _NUMERIC and data_type != "boolean":
@@ -44,6 +64,8 @@ def literal_ok(data_type: Optional[str], value: Optional[str]) -> bool:
         return False
     if data_type == "boolean" and value.strip().lower() in ("true", "false"):
         return True
+    if not java_double_ok(value):
+        return False
     try:
         float(value)
     except ValueError:

@@ -51,6 +51,8 @@ FP_CODE_RANGE = 1 << 10
 FP_ROW_INVALID = 1 << 11
 FP_MISSING_VALUE = 1 << 12
 FP_VALUE_MASK = 1 << 13
+FP_VALUE_LIST = 1 << 14
+MAX_VALUE_LIST = 255  # per list (8-bit counts in the FieldPrep pad word)
 
 EPI_AFFINE, EPI_LOGISTIC2, EPI_ARGMAX, EPI_SOFTMAX, EPI_CUMULATIVE, EPI_LINKMAX = 0, 1, 2, 3, 4, 5
 LINKS = {"none": 0, None: 0, "logit": 1, "exp": 2, "probit": 3, "cloglog": 4, "loglog": 5, "cauchit": 6}
@@ -102,14 +104,36 @@ def canonical_threshold(op: int, t: float) -> Tuple[float, bool]:
 # --------------------------------------------------------------------------- field preparation
 
 
+def _fp32_values(name: str, texts, what: str) -> List[float]:
+    """The numeric members of a DataField Value list as fp32-exact numbers (non-numeric entries
+    never reach a numeric matrix: the text parsers read them as missing, as ``prepare_matrix``
+    skips them); a member fp32 cannot hold exactly is host-only."""
+    out = []
+    for txt in texts:
+        try:
+            v = float(txt)
+        except ValueError:
+            continue
+        if not math.isfinite(v) or float(np.float32(v)) != v:
+            raise NotLowerable(f"field {name!r}: {what} value {v!r} is not an fp32 number")
+        out.append(v)
+    if len(out) > MAX_VALUE_LIST:
+        raise NotLowerable(f"field {name!r}: more than {MAX_VALUE_LIST} {what} values")
+    return sorted(set(out), key=out.index)
+
+
 def build_field_prep(compiled, fields: List[str]) -> Tuple[np.ndarray, bool]:
-    """FieldPrep table (``[F, 8]`` as raw 32-bit words) for the active fields; second value tells
-    whether any field needs preparation at all."""
+    """FieldPrep table for the active fields: ``[F, 8]`` raw 32-bit words (one 32-byte record per
+    field), followed by the fp32 value lists of ``FP_VALUE_LIST`` fields (several missing-value
+    sentinels, invalid-value lists) in extra 8-word rows of the same buffer — a record finds its
+    lists through the relative offset in its pad word. Second value: whether any field needs
+    preparation at all."""
     schema = compiled.schema
     table = np.zeros((len(fields), 8), dtype=np.float32)
     flags = np.zeros(len(fields), dtype=np.uint32)
     any_prep = False
     masks = {}  # field -> (bits 0-31, bits 32-63) of an FP_VALUE_MASK set, written as raw words
+    lists = {}  # field -> (missing values, invalid values) of an FP_VALUE_LIST field
     for j, name in enumerate(fields):
         df = schema.data_fields.get(name)
         mf = compiled.mining_fields.get(name)
@@ -124,25 +148,20 @@ def build_field_prep(compiled, fields: List[str]) -> Tuple[np.ndarray, bool]:
         if df is not None:
             if optype != "continuous" and df.intervals:
                 fl |= FP_ROW_INVALID
-            if df.invalid_values or (df.missing_values and df.is_string):
-                raise NotLowerable(f"field {name!r}: explicit invalid values / string missing values are host-only")
-            # numeric missing-value sentinels (e.g. -999), compared in fp32; non-numeric ones ("NA")
-            # never reach a numeric matrix (the text parsers read them as missing already, as
-            # pmml/fields.py::prepare_matrix skips them)
-            sentinels = []
-            for txt in df.missing_values:
-                try:
-                    sentinels.append(float(txt))
-                except ValueError:
-                    continue
-            if len(sentinels) > 1:
-                raise NotLowerable(f"field {name!r}: several numeric missing values are host-only")
-            if sentinels:
-                mv = sentinels[0]
-                if not math.isfinite(mv) or float(np.float32(mv)) != mv:
-                    raise NotLowerable(f"field {name!r}: missing value {mv!r} is not an fp32 number")
+            if (df.invalid_values or df.missing_values) and df.is_string:
+                raise NotLowerable(f"field {name!r}: missing / invalid value lists on a string field are host-only")
+            # numeric missing-value sentinels (e.g. -999) and invalid-value lists, compared in fp32
+            # (prepare_matrix's order: a missing value first, then an invalid one)
+            sentinels = _fp32_values(name, df.missing_values, "missing")
+            invalids = _fp32_values(name, df.invalid_values, "invalid")
+            if len(sentinels) == 1 and not invalids:
                 fl |= FP_MISSING_VALUE
-                mval = mv
+                mval = sentinels[0]
+            elif sentinels or invalids:
+                fl |= FP_VALUE_LIST
+                lists[j] = (sentinels, invalids)
+                if invalids:
+                    constrained = True
             if optype == "continuous" and df.intervals:
                 if len(df.intervals) != 1:
                     raise NotLowerable(f"field {name!r}: multiple validity intervals are host-only")
@@ -223,6 +242,19 @@ def build_field_prep(compiled, fields: List[str]) -> Tuple[np.ndarray, bool]:
     raw[:, 0] = flags
     for j, (w0, w1) in masks.items():
         raw[j, 5], raw[j, 6] = w0, w1
+    if lists:
+        pool: List[float] = []
+        for j, (miss_v, inv_v) in lists.items():
+            start = len(fields) * 8 + len(pool)  # in words from the start of the buffer
+            off = start - j * 8  # relative to field j's record
+            if off >= 1 << 16:
+                raise NotLowerable("FieldPrep value lists too large")
+            raw[j, 7] = off | (len(miss_v) << 16) | (len(inv_v) << 24)
+            pool.extend(miss_v)
+            pool.extend(inv_v)
+        pad = np.zeros(-(-len(pool) // 8) * 8, dtype=np.float32)
+        pad[: len(pool)] = pool
+        raw = np.concatenate([raw, pad.view(np.uint32).reshape(-1, 8)], axis=0)
     return raw, any_prep
 
 

@@ -10,6 +10,8 @@ import re
 import numpy as np
 import pytest
 
+from tests._suite import gpu_seeds
+
 from flink_jpmml_amd.runtime.compiled import CompiledPmml
 
 METRICS = ["squaredEuclidean", "euclidean", "cityBlock", "chebychev", 'minkowski p-parameter="3"']
@@ -54,7 +56,7 @@ def test_random_clusterings_lower(seed):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("seed", range(30))
+@pytest.mark.parametrize("seed", gpu_seeds(30, 10))
 def test_random_clusterings_on_gpu(gpu, seed):
     txt, F, mixed = _case(seed)
     c = CompiledPmml.from_string(txt)

@@ -8,6 +8,8 @@ the float64 oracle; GPU: the DerivedPlan (derive kernel → linear kernel) vs th
 import numpy as np
 import pytest
 
+from tests._suite import gpu_seeds
+
 from flink_jpmml_amd.bench.synth import mixed_records
 from flink_jpmml_amd.runtime.compiled import CompiledPmml
 
@@ -101,7 +103,7 @@ def test_design_twin_matches_oracle(seed):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("seed", range(40))
+@pytest.mark.parametrize("seed", gpu_seeds(40, 12))
 def test_design_plans_on_gpu(gpu, seed):
     doc, classes, norm = _doc(seed)
     c = CompiledPmml.from_string(doc)

@@ -8,6 +8,8 @@ twin, column for column (so a kernel bug cannot hide behind a model's aggregatio
 import numpy as np
 import pytest
 
+from tests._suite import gpu_seeds
+
 from flink_jpmml_amd.runtime.compiled import CompiledPmml
 
 NS = "http://www.dmg.org/PMML-4_4"
@@ -162,7 +164,7 @@ def test_program_twin_matches_oracle(seed):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("seed", range(60))
+@pytest.mark.parametrize("seed", gpu_seeds(60, 16))
 def test_derive_kernel_matches_twin(gpu, seed):
     import torch
 

@@ -1,8 +1,10 @@
 """A DataField's explicit missing value (``<Value value="-999" property="missing"/>``, the usual
 sentinel of exported numeric columns) on the device: ``build_field_prep`` lowers ONE numeric,
 fp32-exact sentinel into the FieldPrep record (``FP_MISSING_VALUE``, compared in ``prep_value``
-before every other treatment, as ``pmml/fields.py::prepare_matrix`` does); several sentinels, string
-sentinels and invalid-value lists stay host-only (``NotLowerable``, never a plan that ignores them).
+before every other treatment, as ``pmml/fields.py::prepare_matrix`` does); several sentinels and
+invalid-value lists (``property="invalid"``) go into a per-field value table appended to the
+FieldPrep buffer (``FP_VALUE_LIST``, round 6); string-field lists and members fp32 cannot hold
+stay host-only (``NotLowerable``, never a plan that ignores them).
 CPU: the lowering decisions; GPU: trees, regression, SVM, k-means and networks (through their
 prepare pass) vs the float64 oracle on inputs that carry the sentinel, with and without a
 missingValueReplacement. Also numeric categorical valid-value lists (label-encoded categories):
@@ -64,17 +66,73 @@ def test_sentinel_lowers_into_field_prep():
     assert not any(raw[j, 0] & FP_MISSING_VALUE for j in (0, 2, 3, 4, 5))
 
 
-@pytest.mark.parametrize("kind", ["two-sentinels", "invalid-list", "not-fp32"])
-def test_other_value_lists_stay_host_only(kind):
+@pytest.mark.parametrize("kind", ["not-fp32", "invalid-not-fp32"])
+def test_value_lists_fp32_cannot_hold_stay_host_only(kind):
     from flink_jpmml_amd.runtime.plans import NotLowerable, build_field_prep
 
     base = MODELS["gbdt"][0]
-    txt = {"two-sentinels": _with_sentinel(base, values=("-999", "-1")),
-           "invalid-list": _with_sentinel(base, values=("7",), prop="invalid"),
-           "not-fp32": _with_sentinel(base, values=("0.1",))}[kind]
+    txt = {"not-fp32": _with_sentinel(base, values=("0.1",)),
+           "invalid-not-fp32": _with_sentinel(base, values=("-999", "0.1"), prop="invalid")}[kind]
     c = CompiledPmml.from_string(txt)
     with pytest.raises(NotLowerable):
         build_field_prep(c, [f"f{j}" for j in range(6)])
+
+
+def _with_lists(txt: str, field: str = "f1", missing=("-999", "-1"), invalid=("7", "0.5")) -> str:
+    child = "".join(f'<Value value="{v}" property="missing"/>' for v in missing) + \
+        "".join(f'<Value value="{v}" property="invalid"/>' for v in invalid)
+    out, n = re.subn(rf'(<DataField name="{field}"[^>]*?)\s*/>', rf'\1>{child}</DataField>', txt, count=1)
+    assert n == 1
+    return out
+
+
+@pytest.mark.parametrize("treat", ["returnInvalid", "asMissing", "asIs", "asValue"])
+def test_value_lists_lower_into_a_field_table(treat):
+    """Several sentinels and an invalid list: FP_VALUE_LIST with the values in a table after the
+    records, found through the pad word's relative offset; a line-for-line model of prep_value
+    over that buffer equals the oracle's prepare on every value."""
+    from flink_jpmml_amd.runtime.plans import FP_VALUE_LIST, build_field_prep
+
+    txt = _with_lists(MODELS["gbdt"][0])
+    extra = ' invalidValueReplacement="0.25"' if treat == "asValue" else ""
+    txt = txt.replace('<MiningField name="f1"/>', f'<MiningField name="f1" invalidValueTreatment="{treat}"{extra}/>', 1)
+    c = CompiledPmml.from_string(txt)
+    names = [f"f{j}" for j in range(6)]
+    raw, any_prep = build_field_prep(c, names)
+    assert any_prep and raw.shape[0] > 6 and raw[1, 0] & FP_VALUE_LIST
+    w = int(raw[1, 7])
+    off, nm, ni = w & 0xFFFF, (w >> 16) & 0xFF, w >> 24
+    flat = raw.reshape(-1).view(np.float32)
+    vals = flat[1 * 8 + off: 1 * 8 + off + nm + ni]
+    assert list(vals[:nm]) == [-999.0, -1.0] and list(vals[nm:]) == [7.0, 0.5]
+    x = np.array([-999.0, -1.0, 7.0, 0.5, 3.0, np.nan, 0.75])
+    X = np.zeros((len(x), 6))
+    X[:, 1] = x
+    P, ok = c.prepare(X)
+    for i, xv in enumerate(x.astype(np.float32)):
+        miss = bool(np.isnan(xv)) or bool(np.any(vals[:nm] == xv))
+        inv = (not miss) and bool(np.any(vals[nm:] == xv))
+        if inv and treat == "returnInvalid":
+            assert not ok[i]
+        elif inv and treat == "asMissing" or miss:
+            assert np.isnan(P[i, 1]) and ok[i]
+        elif inv and treat == "asValue":
+            assert P[i, 1] == 0.25
+        else:
+            assert P[i, 1] == x[i] and ok[i]
+
+
+def test_string_field_lists_stay_host_only():
+    from flink_jpmml_amd.runtime.plans import NotLowerable, build_field_prep
+
+    txt = MODELS["regression"][0]
+    m = re.search(r'<DataField name="(\w+)" optype="categorical" dataType="string">', txt)
+    assert m
+    name = m.group(1)
+    txt = txt.replace(m.group(0), m.group(0) + '<Value value="NA" property="missing"/>', 1)
+    c = CompiledPmml.from_string(txt)
+    with pytest.raises(NotLowerable):
+        build_field_prep(c, c.active_fields)
 
 
 @pytest.mark.parametrize("values,flagged", [(("NA",), False), (("NA", "-999", "?"), True)])
@@ -237,3 +295,52 @@ def test_integer_categories_on_gpu(gpu, name, treat, values):
     assert v.any()
     scale = max(1.0, float(np.abs(ref[v]).max()))
     np.testing.assert_allclose(s[v], ref[v], rtol=0, atol=2e-4 * scale)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("treat", ["returnInvalid", "asMissing", "asValue"])
+@pytest.mark.parametrize("name", ["gbdt", "rf", "regression", "svm", "kmeans", "mlp"])
+def test_value_lists_on_gpu(gpu, name, treat):
+    """Several sentinels + an invalid-value list lowered into the FieldPrep value table: validity
+    and scores equal the oracle with ``fallback="error"`` semantics (the plan must exist)."""
+    txt, opts = MODELS[name]
+    txt = _with_lists(txt, missing=("-999", "-1", "4"), invalid=("7", "0.5", "-2"))
+    extra = ' invalidValueReplacement="0.25"' if treat == "asValue" else ""
+    txt = txt.replace('<MiningField name="f1"/>', f'<MiningField name="f1" invalidValueTreatment="{treat}"{extra}/>', 1)
+    c = CompiledPmml.from_string(txt)
+    plan = c.plan(gpu, **opts)
+    X = _inputs(6000, codes=name == "regression")
+    rng = np.random.default_rng(21)
+    X[:, 1] = np.where(rng.random(len(X)) < 0.5, rng.choice([-999.0, -1.0, 4.0, 7.0, 0.5, -2.0], len(X)), X[:, 1])
+    s, v = plan.score(X)
+    s, v = s.cpu().numpy().astype(np.float64), v.cpu().numpy().astype(bool)
+    ref, vref = c.score_matrix_oracle(X)
+    assert (v == vref).all()
+    assert v.any()
+    if name in ("rf", "kmeans"):
+        assert (s[v] == ref[v]).mean() >= 0.995
+    else:
+        scale = max(1.0, float(np.abs(ref[v]).max()))
+        np.testing.assert_allclose(s[v], ref[v], rtol=0, atol=2e-4 * scale)
+
+
+@pytest.mark.gpu
+def test_near_sentinel_input_is_missing_on_the_device_only(gpu):
+    """ADVICE r5 (low), documented in docs/PARITY.md "Deliberate deviations": a float64 input within
+    half an fp32 ulp of the sentinel rounds onto it in the fp32 row the kernels read, so the device
+    treats it as missing while the float64 oracle keeps the value."""
+    txt = _with_replacement(_with_sentinel(MODELS["gbdt"][0]))
+    c = CompiledPmml.from_string(txt)
+    plan = c.plan(gpu)
+    near = -999.00003  # |near - (-999)| < half an fp32 ulp (3.05e-5) at 999
+    assert np.float32(near) == np.float32(SENT) and near != SENT
+    X = _inputs(64)
+    X[:, 1] = near
+    Xs = X.copy()
+    Xs[:, 1] = SENT
+    s_near, _ = plan.score(X)
+    s_sent, _ = plan.score(Xs)
+    np.testing.assert_array_equal(s_near.cpu().numpy(), s_sent.cpu().numpy())  # device: missing
+    ref_near, _ = c.score_matrix_oracle(X)
+    ref_sent, _ = c.score_matrix_oracle(Xs)
+    assert not np.array_equal(ref_near, ref_sent)  # oracle: -999.00003 is a value, not the sentinel

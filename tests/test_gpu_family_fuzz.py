@@ -9,6 +9,8 @@ scores within fp32 of it (labels: near-boundary rows may flip). The plan must lo
 import numpy as np
 import pytest
 
+from tests._suite import gpu_seeds
+
 pytestmark = pytest.mark.gpu
 
 
@@ -26,7 +28,7 @@ def _check(c, plan, X, label: bool, rtol=1e-4, agree=0.99):
         np.testing.assert_allclose(s[v], ref[v], rtol=0, atol=rtol * scale)
 
 
-@pytest.mark.parametrize("seed", range(24))
+@pytest.mark.parametrize("seed", gpu_seeds(24, 8))
 def test_random_svms(gpu, seed):
     from flink_jpmml_amd.bench.synth import stream_matrix, svm_pmml
     from flink_jpmml_amd.runtime.compiled import CompiledPmml
@@ -45,7 +47,7 @@ def test_random_svms(gpu, seed):
     _check(c, plan, X, label=classes > 0, rtol=2e-4, agree=0.98)
 
 
-@pytest.mark.parametrize("seed", range(20))
+@pytest.mark.parametrize("seed", gpu_seeds(20, 6))
 def test_random_kmeans(gpu, seed):
     from flink_jpmml_amd.bench.synth import kmeans_pmml, stream_matrix
     from flink_jpmml_amd.runtime.compiled import CompiledPmml
@@ -61,7 +63,7 @@ def test_random_kmeans(gpu, seed):
     _check(c, plan, X, label=True, agree=0.995)
 
 
-@pytest.mark.parametrize("seed", range(16))
+@pytest.mark.parametrize("seed", gpu_seeds(16, 6))
 def test_random_knn(gpu, seed):
     from flink_jpmml_amd.bench.synth import knn_pmml, stream_matrix
     from flink_jpmml_amd.runtime.compiled import CompiledPmml
@@ -82,7 +84,7 @@ _REG = ["selectFirst", "max", "min", "median", "sum", "average", "weightedAverag
 _CLS = ["majorityVote", "weightedMajorityVote", "selectFirst", "average", "weightedAverage", "max", "median"]
 
 
-@pytest.mark.parametrize("seed", range(24))
+@pytest.mark.parametrize("seed", gpu_seeds(24, 8))
 def test_random_segmentations(gpu, seed):
     from flink_jpmml_amd.bench.synth import segmented_pmml, stream_matrix
     from flink_jpmml_amd.runtime.compiled import CompiledPmml

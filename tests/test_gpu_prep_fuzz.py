@@ -13,6 +13,8 @@ import re
 import numpy as np
 import pytest
 
+from tests._suite import gpu_seeds
+
 from flink_jpmml_amd.runtime.compiled import CompiledPmml
 
 F = 6
@@ -134,7 +136,7 @@ def test_random_treatments_lower(seed):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("seed", range(40))
+@pytest.mark.parametrize("seed", gpu_seeds(40, 12))
 def test_random_treatments_on_gpu(gpu, seed):
     kind, txt, opts, label, sentinel, integer = _case(seed)
     c = CompiledPmml.from_string(txt)

@@ -8,6 +8,8 @@ kernels that the hand-written cases do not pin."""
 import numpy as np
 import pytest
 
+from tests._suite import gpu_seeds
+
 pytestmark = pytest.mark.gpu
 
 
@@ -24,7 +26,7 @@ def _shape(seed):
     return kind, depth, n_trees, F, missing, strategy, rows, p_split, int(rng.integers(0, 1 << 30))
 
 
-@pytest.mark.parametrize("seed", range(32))
+@pytest.mark.parametrize("seed", gpu_seeds(32, 10))
 def test_random_tree_ensembles_match_oracle(gpu, seed):
     from flink_jpmml_amd.bench.synth import gbdt_pmml, random_forest_pmml, stream_matrix
     from flink_jpmml_amd.runtime.compiled import CompiledPmml

@@ -258,3 +258,23 @@ def test_host_gbdt_throughput():
     rate = len(X) / (time.perf_counter() - t)
     print(f"host 1000-tree GBDT: {rate:.0f} records/s")
     assert rate > 20_000
+
+
+@pytest.mark.parametrize("shape", [dict(n_features=12, hidden=(40, 17)), dict(n_features=5, hidden=(8,), n_out=3,
+                                                                             classification=True),
+                                   dict(n_features=30, hidden=(64, 64, 32), activation="tanh")])
+def test_native_neural_layers_are_bit_identical_to_the_connection_loop(shape):
+    """nn_host.cpp::seq_affine: bias + products summed in connection order, one rounding each (no
+    FMA) -- the numpy per-connection loop's exact bits."""
+    from flink_jpmml_amd.bench.synth import mlp_pmml, stream_matrix
+
+    doc = mlp_pmml(seed=3, **shape)
+    X = stream_matrix(700, shape["n_features"], seed=4, missing_rate=0.02)
+    c1 = CompiledPmml.from_string(doc)
+    assert all(e is not None for e in c1.evaluator._native_layers())
+    s1, v1 = c1.score_matrix_oracle(X)
+    c2 = CompiledPmml.from_string(doc)
+    c2.evaluator._native = [None] * len(c2.evaluator.nn.layers)
+    s2, v2 = c2.score_matrix_oracle(X)
+    np.testing.assert_array_equal(v1, v2)
+    assert np.array_equal(s1[v1], s2[v2])

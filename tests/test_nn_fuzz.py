@@ -9,6 +9,8 @@ lowering decision of every drawn network (no ``NotLowerable``)."""
 import numpy as np
 import pytest
 
+from tests._suite import gpu_seeds
+
 from flink_jpmml_amd.runtime.compiled import CompiledPmml
 
 ACTS = ["identity", "logistic", "tanh", "rectifier", "Gauss", "sine", "cosine", "Elliott", "arctan", "threshold"]
@@ -41,7 +43,7 @@ def test_random_networks_lower(seed):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("seed", range(36))
+@pytest.mark.parametrize("seed", gpu_seeds(36, 10))
 def test_random_networks_on_gpu(gpu, seed):
     from flink_jpmml_amd.bench.synth import stream_matrix
 

@@ -9,6 +9,8 @@ the fp32 value."""
 import numpy as np
 import pytest
 
+from tests._suite import gpu_seeds
+
 from flink_jpmml_amd.runtime.compiled import CompiledPmml
 
 
@@ -72,7 +74,7 @@ def test_random_targets_lower(seed):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("seed", range(42))
+@pytest.mark.parametrize("seed", gpu_seeds(42, 12))
 def test_random_targets_on_gpu(gpu, seed):
     kind, txt, F, kw = _case(seed)
     c = CompiledPmml.from_string(txt)
