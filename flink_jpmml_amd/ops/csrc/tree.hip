@@ -682,8 +682,9 @@ __global__ __launch_bounds__(TB) void tree_reduce_kernel(TreeArgs a, int splits)
 enum : int {
   P_END = 0, P_TRUE, P_FALSE, P_GE, P_EQ, P_ISMISS, P_NOTMISS, P_SET, P_AND, P_OR, P_XOR, P_SURR,
 };
-enum : int { S_NONE = 0, S_LAST = 1, S_NULL = 2, S_DEFAULT = 3 };
+enum : int { S_NONE = 0, S_LAST = 1, S_NULL = 2, S_DEFAULT = 3, S_WCONF = 4, S_AGG = 5 };
 constexpr uint32_t V_F = 0u, V_T = 1u, V_U = 2u;
+constexpr int MIX_STACK = 64;  // host-checked: 1 + sum over any path of (children - 1)
 
 struct GenTreeArgs {
   TreeArgs t;                  // rows, prep, epilogue, payload (t.leaves [nodes][P]), slots, outputs
@@ -691,8 +692,13 @@ struct GenTreeArgs {
   const int* children;         // child node indices
   const int4* preds;           // {op | neg << 8, field or n, pool offset / count, T bits}
   const float* pool;           // SimpleSetPredicate values
-  const int2* trees;           // {root node, strategy | returnLastPrediction << 2}
+  const int2* trees;           // {root node, strategy (3 bits) | returnLastPrediction << 3}
   int max_steps, pad;
+  // weightedConfidence / aggregateNodes trees (null when the ensemble has none):
+  const float* mix_mass;       // [nodes][P] class mass of each node, tree category order
+  const float* mix_w;          // [nodes] weight of a node as a mixture child
+  const int4* mix_tab;         // [trees] {segment weight bits, vote, tree categories, remap offset}
+  const int* remap;            // tree category -> accumulator slot
 };
 
 template <bool FEAT_LDS>
@@ -762,12 +768,13 @@ __device__ uint32_t gen_eval(const GenTreeArgs& a, int pc, const char* feat_lane
   }
 }
 
-// Returns the scoring node of tree t for this lane's row, or -1 (null prediction).
+// Returns the scoring node of tree t for this lane's row, -1 (null prediction), or -2: a
+// weightedConfidence / aggregateNodes tree met an UNKNOWN child (the caller runs gen_mixture).
 template <bool FEAT_LDS>
 __device__ int gen_walk(const GenTreeArgs& a, int t, const char* feat_lane, const float* xrow) {
   const int2 tr = a.trees[t];
-  const int strat = tr.y & 3;
-  const bool ret_last = ((tr.y >> 2) & 1) != 0;
+  const int strat = tr.y & 7;
+  const bool ret_last = ((tr.y >> 3) & 1) != 0;
   int node = tr.x;
   if (gen_eval<FEAT_LDS>(a, a.nodes[node].z, feat_lane, xrow) != V_T) return -1;
   for (int step = 0; step < a.max_steps; ++step) {
@@ -778,6 +785,7 @@ __device__ int gen_walk(const GenTreeArgs& a, int t, const char* feat_lane, cons
     for (int c = 0; c < nc; ++c) {
       const int ch = a.children[nd.x + c];
       const uint32_t v = gen_eval<FEAT_LDS>(a, a.nodes[ch].z, feat_lane, xrow);
+      if (v == V_U && strat >= S_WCONF) return -2;
       if (v == V_U && strat != S_NONE) {
         if (strat == S_LAST) return node;
         if (strat == S_NULL) return -1;
@@ -794,6 +802,100 @@ __device__ int gen_walk(const GenTreeArgs& a, int t, const char* feat_lane, cons
     node = next;
   }
   return -1;
+}
+
+// weightedConfidence / aggregateNodes (models/tree.py::_mixture): the row restarts at the root
+// as a depth-first walk over (node, weight, inside-a-mixture) entries. A TRUE child continues the
+// path; at the first UNKNOWN child the path forks into that child and every later sibling that is
+// not FALSE, each weighted by its mix_w; a leaf adds weight x its class mass. A node without a
+// true child adds its own mass under returnLastPrediction, else voids the row on a pure TRUE path
+// (the oracle's NaN) or contributes nothing inside a mixture (nan_to_num). Then the tree adds its
+// normalised mass (or a vote for its first argmax) to the class slots. Returns false: no prediction.
+template <bool FEAT_LDS>
+__device__ bool gen_mixture(const GenTreeArgs& a, int t, const char* feat_lane, const float* xrow, float* accl,
+                            int tid) {
+  const int2 tr = a.trees[t];
+  const bool ret_last = ((tr.y >> 3) & 1) != 0;
+  const int4 mt = a.mix_tab[t];
+  const int P = a.t.P;
+  const int Ct = mt.z;
+  float mass[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) mass[c] = 0.f;
+  int st_node[MIX_STACK];
+  float st_w[MIX_STACK];
+  uint64_t st_in = 0;  // bit i: entry i is inside a mixture
+  int sp = 0;
+  st_node[0] = tr.x;
+  st_w[0] = 1.f;
+  sp = 1;
+  int guard = 0;
+  while (sp > 0 && guard < (1 << 20)) {
+    ++guard;
+    --sp;
+    const int node = st_node[sp];
+    const float w = st_w[sp];
+    const bool inside = (st_in >> sp) & 1ull;
+    st_in &= ~(1ull << sp);
+    const int4 nd = a.nodes[node];
+    const int nc = nd.y & 0xFFFF;
+    if (nc == 0) {
+      for (int c = 0; c < Ct; ++c) mass[c] += w * a.mix_mass[(size_t)node * P + c];
+      continue;
+    }
+    int k = -1;
+    uint32_t vk = V_F;
+    for (int c = 0; c < nc; ++c) {
+      vk = gen_eval<FEAT_LDS>(a, a.nodes[a.children[nd.x + c]].z, feat_lane, xrow);
+      if (vk != V_F) {
+        k = c;
+        break;
+      }
+    }
+    if (k < 0) {
+      if (ret_last) {
+        for (int c = 0; c < Ct; ++c) mass[c] += w * a.mix_mass[(size_t)node * P + c];
+      } else if (!inside) {
+        return false;
+      }
+      continue;
+    }
+    if (vk == V_T) {
+      if (sp >= MIX_STACK) return false;  // host-checked bound; never reached
+      st_node[sp] = a.children[nd.x + k];
+      st_w[sp] = w;
+      if (inside) st_in |= 1ull << sp;
+      ++sp;
+      continue;
+    }
+    // first UNKNOWN at child k: k and every later sibling that is not FALSE, pushed last-first
+    // so child k is expanded first (the oracle's summation order)
+    for (int c = nc - 1; c >= k; --c) {
+      const int ch = a.children[nd.x + c];
+      const uint32_t v = c == k ? V_U : gen_eval<FEAT_LDS>(a, a.nodes[ch].z, feat_lane, xrow);
+      if (v == V_F) continue;
+      if (sp >= MIX_STACK) return false;
+      st_node[sp] = ch;
+      st_w[sp] = w * a.mix_w[ch];
+      st_in |= 1ull << sp;
+      ++sp;
+    }
+  }
+  float tot = 0.f;
+  for (int c = 0; c < Ct; ++c) tot += mass[c];
+  if (!(tot > 0.f) || !isfinite(tot)) return false;
+  const float wt = __int_as_float(mt.x);
+  const int* rm = a.remap + mt.w;
+  if (mt.y) {
+    int best = 0;
+    for (int c = 1; c < Ct; ++c)
+      if (mass[c] > mass[best]) best = c;
+    accl[rm[best] * TB + tid] += wt;
+  } else {
+    const float inv = 1.f / tot;
+    for (int c = 0; c < Ct; ++c) accl[rm[c] * TB + tid] += (mass[c] * inv) * wt;
+  }
+  return true;
 }
 
 template <bool GENERAL, bool FEAT_LDS>
@@ -831,6 +933,10 @@ __global__ __launch_bounds__(TB, 2) void tree_general_kernel(GenTreeArgs ga) {
   if (row < a.n_rows) {
     for (int t = 0; t < a.n_trees; ++t) {
       const int node = gen_walk<FEAT_LDS>(ga, t, feat_lane, xrow);
+      if (GENERAL && node == -2) {  // sibling mixture (weightedConfidence / aggregateNodes)
+        if (!gen_mixture<FEAT_LDS>(ga, t, feat_lane, xrow, accl, tid)) poisoned = true;
+        continue;
+      }
       if (node < 0 || ((ga.nodes[node].y >> 16) & 1) == 0) {  // null prediction
         if (GENERAL) poisoned = true;
         else acc += __builtin_nanf("");

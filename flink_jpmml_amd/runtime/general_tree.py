@@ -27,8 +27,11 @@ from .plans import NotLowerable, _ceil32, _floor32, _next_up32
 
 P_END, P_TRUE, P_FALSE, P_GE, P_EQ, P_ISMISS, P_NOTMISS, P_SET, P_AND, P_OR, P_XOR, P_SURR = range(12)
 _COMPOUND = {"and": P_AND, "or": P_OR, "xor": P_XOR, "surrogate": P_SURR}
-STRATEGY = {"none": 0, "lastPrediction": 1, "nullPrediction": 2, "defaultChild": 3}
+STRATEGY = {"none": 0, "lastPrediction": 1, "nullPrediction": 2, "defaultChild": 3, "weightedConfidence": 4,
+            "aggregateNodes": 5}
+MIX_STRATEGIES = ("weightedConfidence", "aggregateNodes")
 MAX_STACK = 32  # 2-bit entries in the kernel's 64-bit stack
+MIX_STACK = 64  # the mixture walk's explicit DFS stack (tree.hip::gen_mixture)
 
 
 @dataclass
@@ -43,6 +46,14 @@ class GeneralTree:
     has_score: np.ndarray
     depth: int
     null_missing: bool = True  # may yield no prediction (checked against skipSegment)
+    # weightedConfidence / aggregateNodes: the sibling mixture a row takes at its first UNKNOWN
+    # child (models/tree.py::_mixture) -- per node its class mass (tree category order) and its
+    # weight as a child (recordCount / parent recordCount, or 1)
+    mix_mass: Optional[np.ndarray] = None
+    mix_w: Optional[np.ndarray] = None
+    mix_vote: bool = False  # set by the ensemble lowering: this tree votes (majority) ...
+    mix_weight: float = 1.0  # ... or averages its probabilities, with this segment weight
+    mix_remap: Optional[np.ndarray] = None  # tree category -> accumulator slot
 
 
 def lower_general_tree(ev: TreeEvaluator, field_index: Dict[str, int]) -> GeneralTree:
@@ -55,12 +66,31 @@ def lower_general_tree(ev: TreeEvaluator, field_index: Dict[str, int]) -> Genera
     value = ev.node_label.copy() if classification else ev.node_value.copy()
     probs = ev.node_probs.copy() if classification else None
     depth = 0
-    stack = [(tm.root, 0)]
+    bound = 0  # worst-case DFS stack of the mixture walk: 1 + sum over a path of (children - 1)
+    stack = [(tm.root, 0, 1)]
     while stack:
-        nd, d = stack.pop()
+        nd, d, b = stack.pop()
         depth = max(depth, d)
-        stack.extend((c, d + 1) for c in nd.children)
-    return GeneralTree(ev, field_index, value, probs, ~np.isnan(value), depth)
+        bound = max(bound, b)
+        stack.extend((c, d + 1, b + max(0, len(nd.children) - 1)) for c in nd.children)
+    gt = GeneralTree(ev, field_index, value, probs, ~np.isnan(value), depth)
+    if tm.missing_value_strategy in MIX_STRATEGIES:
+        if not classification:  # pragma: no cover - TreeEvaluator refuses it at load
+            raise NotLowerable("weightedConfidence / aggregateNodes need a classification tree")
+        if bound > MIX_STACK:
+            raise NotLowerable(f"sibling mixture needs a {bound}-entry stack > {MIX_STACK}")
+        nodes = ev.nodes
+        gt.mix_mass = np.stack([ev._node_mass(i) for i in range(len(nodes))]).astype(np.float64)
+        w = np.ones(len(nodes))
+        if tm.missing_value_strategy == "weightedConfidence":
+            index = ev._index
+            for nd in nodes:
+                pn = nd.record_count
+                for c in nd.children:
+                    cn = c.record_count
+                    w[index[id(c)]] = (cn / pn) if cn is not None and pn else 1.0
+        gt.mix_w = w
+    return gt
 
 
 class _PredCompiler:
@@ -147,6 +177,11 @@ def pack_general(trees: List[GeneralTree], weights: List[float], P: int, schema)
     children: List[int] = []
     payload: List[np.ndarray] = []
     tree_tab: List[tuple] = []
+    mix_tab: List[tuple] = []  # per tree {weight bits, vote, n classes, remap offset}
+    mix_mass: List[np.ndarray] = []
+    mix_w: List[np.ndarray] = []
+    remap: List[int] = []
+    any_mix = any(getattr(t, "mix_mass", None) is not None for t in trees)
     pc: Optional[_PredCompiler] = None
     max_depth = 0
     for t, w in zip(trees, weights):
@@ -176,9 +211,27 @@ def pack_general(trees: List[GeneralTree], weights: List[float], P: int, schema)
                 row = np.array([t.leaf_value[i] if has else 0.0]) * w
             payload.append(row)
         flags = STRATEGY[ev.tree.missing_value_strategy] | (
-            (1 << 2) if ev.tree.no_true_child_strategy == "returnLastPrediction" else 0)
+            (1 << 3) if ev.tree.no_true_child_strategy == "returnLastPrediction" else 0)
         tree_tab.append((base, flags))
         max_depth = max(max_depth, t.depth)
+        if any_mix:
+            mm = getattr(t, "mix_mass", None)
+            n = len(ev.nodes)
+            if mm is None:
+                mix_mass.append(np.zeros((n, P)))
+                mix_w.append(np.ones(n))
+                mix_tab.append((0, 0, 0, len(remap)))
+            else:
+                Ct = mm.shape[1]
+                if Ct > P:
+                    raise NotLowerable("tree has more categories than the ensemble's class slots")
+                pad = np.zeros((n, P))
+                pad[:, :Ct] = mm
+                mix_mass.append(pad)
+                mix_w.append(t.mix_w)
+                rm = t.mix_remap if t.mix_remap is not None else np.arange(Ct)
+                mix_tab.append((_bits(float(t.mix_weight)), int(bool(t.mix_vote)), Ct, len(remap)))
+                remap.extend(int(x) for x in rm)
     return {
         "nodes": np.array(nodes, dtype=np.int64).astype(np.int32).reshape(-1, 4),
         "children": np.array(children or [0], dtype=np.int32),
@@ -187,6 +240,10 @@ def pack_general(trees: List[GeneralTree], weights: List[float], P: int, schema)
         "trees": np.array(tree_tab, dtype=np.int32).reshape(-1, 2),
         "payload": np.stack(payload).astype(np.float32).reshape(len(nodes), -1),
         "max_steps": int(max_depth + 2),
+        "mix_mass": np.concatenate(mix_mass).astype(np.float32).reshape(len(nodes), P) if any_mix else None,
+        "mix_w": np.concatenate(mix_w).astype(np.float32) if any_mix else None,
+        "mix_tab": np.array(mix_tab, dtype=np.int64).astype(np.int32).reshape(-1, 4) if any_mix else None,
+        "remap": np.array(remap or [0], dtype=np.int32) if any_mix else None,
     }
 
 
@@ -244,10 +301,15 @@ def emulate_general(packed: dict, X: np.ndarray, P: int, n_trees: int) -> np.nda
         x = Xf[r]
         for t in range(n_trees):
             root, flags = (int(v) for v in packed["trees"][t])
-            strat, ret_last = flags & 3, (flags >> 2) & 1
+            strat, ret_last = flags & 7, (flags >> 3) & 1
             node = root
             res = -1
-            if ev(int(nodes[node, 2]), x) == 1:
+            root_true = ev(int(nodes[node, 2]), x) == 1
+            if root_true and strat >= 4:  # weightedConfidence / aggregateNodes
+                res = _emulate_mixture(packed, ev, x, t, root, ret_last, P, out, r)
+                if res is None:
+                    continue
+            if root_true:
                 for _ in range(packed["max_steps"]):
                     off, nc, _, dflt = (int(v) for v in nodes[node])
                     nc &= 0xFFFF
@@ -258,6 +320,9 @@ def emulate_general(packed: dict, X: np.ndarray, P: int, n_trees: int) -> np.nda
                     for c in range(nc):
                         ch = int(children[off + c])
                         v = ev(int(nodes[ch, 2]), x)
+                        if v == 2 and strat >= 4:  # pragma: no cover - mixture trees walk above
+                            res, stop = -1, True
+                            break
                         if v == 2 and strat != 0:
                             if strat == 1:
                                 res, stop = node, True
@@ -282,3 +347,79 @@ def emulate_general(packed: dict, X: np.ndarray, P: int, n_trees: int) -> np.nda
             else:
                 out[r] += packed["payload"][res]
     return out
+
+
+def _emulate_mixture(packed: dict, ev, x, t: int, root: int, ret_last: int, P: int, out: np.ndarray, r: int):
+    """Twin of tree.hip::gen_walk + gen_mixture for a weightedConfidence / aggregateNodes tree: the
+    ordinary walk while no predicate is UNKNOWN; at the first UNKNOWN the whole row restarts as the
+    DFS sibling mixture. Adds the tree's payload to ``out[r]`` and returns None, or returns the
+    scoring node / -1 of an ordinary walk for the caller to finish."""
+    nodes, children = packed["nodes"], packed["children"]
+    node = root
+    for _ in range(packed["max_steps"]):
+        off, nc, _, _ = (int(v) for v in nodes[node])
+        nc &= 0xFFFF
+        if nc == 0:
+            return node
+        nxt = -1
+        unknown = False
+        for c in range(nc):
+            ch = int(children[off + c])
+            v = ev(int(nodes[ch, 2]), x)
+            if v == 2:
+                unknown = True
+                break
+            if v == 1:
+                nxt = ch
+                break
+        if unknown:
+            break
+        if nxt < 0:
+            return node if ret_last else -1
+        node = nxt
+    else:  # pragma: no cover - max_steps bounds the depth
+        return -1
+    mm, mw, tab, remap = packed["mix_mass"], packed["mix_w"], packed["mix_tab"], packed["remap"]
+    wbits, vote, Ct, roff = (int(v) for v in tab[t])
+    w_tree = float(np.array([wbits], dtype=np.int32).view(np.float32)[0])
+    mass = np.zeros(P, dtype=np.float32)
+    stack = [(root, np.float32(1.0), False)]
+    while stack:
+        node, w, inside = stack.pop()
+        off, nc, _, _ = (int(v) for v in nodes[node])
+        nc &= 0xFFFF
+        if nc == 0:
+            mass += w * mm[node]
+            continue
+        k, vk = -1, 0
+        vals = []
+        for c in range(nc):
+            ch = int(children[off + c])
+            v = ev(int(nodes[ch, 2]), x)
+            vals.append((ch, v))
+            if k < 0 and v != 0:
+                k, vk = c, v
+        if k < 0:
+            if ret_last:
+                mass += w * mm[node]
+            elif not inside:
+                out[r] = np.nan
+                return None
+            continue
+        if vk == 1:
+            stack.append((vals[k][0], w, inside))
+            continue
+        for ch, v in reversed(vals[k:]):  # DFS order: child k first
+            if v != 0:
+                stack.append((ch, np.float32(w * mw[ch]), True))
+    tot = float(mass[:Ct].sum())
+    if not (np.isfinite(tot) and tot > 0):
+        out[r] = np.nan
+        return None
+    if vote:
+        lab = int(np.argmax(mass[:Ct]))
+        out[r, remap[roff + lab]] += w_tree
+    else:
+        for c in range(Ct):
+            out[r, remap[roff + c]] += np.float32(mass[c] / tot) * w_tree
+    return None

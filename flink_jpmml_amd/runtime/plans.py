@@ -1306,7 +1306,8 @@ class TreePlan(DevicePlan):
                                   "chunk_trees_nan", "full_epi", "labels", "mode", "tree_w", "acc_init", "feat_map",
                                   "rows_wide", "n_stage", "heads", "head_depth", "pointer_ilp", "xcd_split",
                                   "tail_format", "rank_thr", "rank_cnt", "rank_stride", "lds_chunks", "lds_slices",
-                                  "lds_rows", "lds_chunk_u4", "lds_n_slices")
+                                  "lds_rows", "lds_chunk_u4", "lds_n_slices", "mix_mass", "mix_w", "mix_tab",
+                                  "mix_remap")
 
     WIDE_G = 4  # tree groups of the wide kernel (mirrors csrc)
 
@@ -1422,6 +1423,11 @@ class TreePlan(DevicePlan):
             self.pool = self._t(g["pool"])
             self.trees_tab = self._t(g["trees"].reshape(-1))
             self.leaves = self._t(g["payload"].reshape(-1))
+            mix = g["mix_mass"] is not None
+            self.mix_mass = self._t(g["mix_mass"].reshape(-1)) if mix else None
+            self.mix_w = self._t(g["mix_w"]) if mix else None
+            self.mix_tab = self._t(g["mix_tab"].reshape(-1)) if mix else None
+            self.mix_remap = self._t(g["remap"]) if mix else None
             self.roots = None
             self.max_steps = g["max_steps"]
             self.has_dr = False
@@ -1758,6 +1764,23 @@ class TreePlan(DevicePlan):
             spec = ensemble_spec(compiled, lower=lower_general_tree)
             if spec.mode == "slot" and any(b != 0.0 for b in (spec.acc_init or [])):
                 raise NotLowerable("K-class chains with intercepts over non-binary trees are host-only")
+            # sibling-mixture trees (weightedConfidence / aggregateNodes) add their normalised
+            # mixture (or its argmax vote) themselves: they need their segment weight, vote mode
+            # and category slots before to_general folds them into the leaf payloads
+            for i, t in enumerate(spec.trees):
+                if getattr(t, "mix_mass", None) is None:
+                    continue
+                if spec.mode == "class":
+                    t.mix_vote, t.mix_weight = True, float((spec.tree_w or [1.0] * len(spec.trees))[i])
+                elif spec.mode == "sum" and spec.P > 1 and spec.slots is None:
+                    t.mix_vote, t.mix_weight = False, float(spec.weights[i])
+                else:
+                    raise NotLowerable("sibling mixture trees inside this ensemble form are host-only")
+                cats = list(spec.labels or [])
+                tc = list(t.ev.categories)
+                if any(c not in cats for c in tc):
+                    raise NotLowerable("tree category outside the ensemble's classes")
+                t.mix_remap = np.array([cats.index(c) for c in tc], dtype=np.int32)
             return to_general(spec)  # the predicate VM accumulates P = C payloads in LDS
         except NotBinary as e:  # pragma: no cover - the general lowering never raises NotBinary
             raise NotLowerable(str(e)) from e
@@ -1935,6 +1958,8 @@ class TreePlan(DevicePlan):
         g.t.partial = None
         g.nodes, g.children, g.preds = ptr(self.blob), ptr(self.children), ptr(self.preds)
         g.pool, g.trees, g.max_steps = ptr(self.pool), ptr(self.trees_tab), int(self.max_steps)
+        g.mix_mass, g.mix_w = ptr(getattr(self, "mix_mass", None)), ptr(getattr(self, "mix_w", None))
+        g.mix_tab, g.remap = ptr(getattr(self, "mix_tab", None)), ptr(getattr(self, "mix_remap", None))
         check(self.lib.pmml_tree_general_launch(stream_handle(stream), ctypes.byref(g)), "general tree kernel")
 
 

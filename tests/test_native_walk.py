@@ -50,7 +50,10 @@ def _pred(rng: random.Random, depth: int) -> str:
         _pred(rng, depth - 1) for _ in range(rng.randrange(2, 4))) + "</CompoundPredicate>"
 
 
-def _node(rng: random.Random, depth: int, ids: list, classification: bool, pred: str) -> str:
+def _node(rng: random.Random, depth: int, ids: list, classification: bool, pred: str,
+          consistent: bool = False) -> str:
+    """``consistent``: a classification node's score is its distribution's first argmax (what
+    exporters write; the device label is the argmax of the class probabilities)."""
     nid = f"n{len(ids)}"
     ids.append(nid)
     cats = ["a", "b", "c"]
@@ -58,6 +61,8 @@ def _node(rng: random.Random, depth: int, ids: list, classification: bool, pred:
     dist = ""
     if classification:
         cnts = [rng.randrange(1, 9) for _ in cats]
+        if consistent:
+            score = cats[int(np.argmax(cnts))]
         dist = "".join(f'<ScoreDistribution value="{c}" recordCount="{n}"/>' for c, n in zip(cats, cnts))
     rc = f' recordCount="{rng.randrange(1, 50)}"'
     if depth == 0 or rng.random() < 0.2:
@@ -76,7 +81,7 @@ def _node(rng: random.Random, depth: int, ids: list, classification: bool, pred:
         preds = [_pred(rng, 2) for _ in range(nch)]
     first_kid = len(ids)
     for p in preds:
-        kids.append(_node(rng, depth - 1, ids, classification, p))
+        kids.append(_node(rng, depth - 1, ids, classification, p, consistent))
     dflt = ""
     if rng.random() < 0.8:
         dflt = f' defaultChild="{ids[first_kid] if rng.random() < 0.6 else ids[-1]}"'

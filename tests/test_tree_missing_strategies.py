@@ -2,8 +2,9 @@
 at the first UNKNOWN child the row is scored down that child and every sibling not FALSE,
 recursively; weightedConfidence weights the siblings' confidences by recordCount / parent's,
 aggregateNodes sums the reached leaves' record counts. Parity unpinned (no JPMML here): the expected
-values are computed by hand from the PMML 4.4 text. Host-only: the device lowerings reject both
-strategies (checked below)."""
+values are computed by hand from the PMML 4.4 text. Device: the GENERAL tree layout runs the same
+mixture (``tree.hip::gen_mixture``; its numpy twin is checked here, the kernel in
+``tests/test_mixture_gpu.py``)."""
 
 import math
 
@@ -85,10 +86,30 @@ def test_regression_trees_reject_the_strategies():
         CompiledPmml.from_string(doc).result(ROWS)
 
 
-@pytest.mark.parametrize("strategy", ["weightedConfidence", "aggregateNodes"])
-def test_device_lowering_refuses(strategy):
-    from flink_jpmml_amd.runtime.plans import NotLowerable, compile_plan, lowering_dry_run
+def _emulate(c, X):
+    """(labels, probs, valid) of the GENERAL layout's numpy twin (tree.hip gen_walk + gen_mixture)."""
+    from flink_jpmml_amd.runtime.general_tree import emulate_general, pack_general
+    from flink_jpmml_amd.runtime.plans import TreePlan
 
-    c = CompiledPmml.from_string(_doc(strategy))
-    with lowering_dry_run(), pytest.raises(NotLowerable):
-        compile_plan(c, "cpu")
+    spec = TreePlan._general_spec(c)
+    packed = pack_general(spec.trees, spec.weights, spec.P, c.schema)
+    acc = emulate_general(packed, X, spec.P, len(spec.trees))
+    valid = ~np.isnan(acc).any(axis=1)
+    a = spec.epi.get("a", 1.0)
+    return np.argmax(np.nan_to_num(acc), axis=1), acc * a, valid
+
+
+@pytest.mark.parametrize("strategy,expected", [("weightedConfidence", WEIGHTED), ("aggregateNodes", AGGREGATE)])
+@pytest.mark.parametrize("no_true", ["returnNullPrediction", "returnLastPrediction"])
+def test_device_lowering_mixes_siblings(strategy, expected, no_true):
+    """Round 6: both strategies lower to the GENERAL layout's sibling mixture
+    (tree.hip::gen_mixture); its numpy twin reproduces the hand-computed probabilities."""
+    from flink_jpmml_amd.runtime.plans import TreePlan, compile_plan, lowering_dry_run
+
+    c = CompiledPmml.from_string(_doc(strategy, no_true))
+    with lowering_dry_run():
+        plan = compile_plan(c, "cpu")
+    assert isinstance(plan, TreePlan) and plan.layout == "general" and plan.mix_mass is not None
+    lab, probs, valid = _emulate(c, ROWS.astype(np.float32).astype(np.float64))
+    assert valid.all()
+    np.testing.assert_allclose(probs[:, 0], expected, rtol=0, atol=1e-6)
