@@ -147,10 +147,16 @@ class PmmlModel(Pipeline):
         X, absent, ok = pack_vectors_masked([vec], width)
         if ok is not None and not ok[0]:
             return None
-        pb = self._scorer.submit_batch(RecordBatch(X, absent=absent), replace_nan)
-        if not bool(pb.valid[0]):
-            return Prediction(EmptyScore)
-        return Prediction(Score(float(pb.scores[0])))
+        row = X[0]
+        if absent is not None and absent.any():  # sparse-absent entries: replace_nan, else missing
+            row = np.where(absent[0], np.nan if replace_nan is None else replace_nan, row)
+        score_row = getattr(self._scorer, "score_row", None)
+        if score_row is not None:
+            s, v = score_row(row)
+        else:
+            pb = self._scorer.submit_batch(RecordBatch(row[None, :]), None)
+            s, v = float(pb.scores[0]), bool(pb.valid[0])
+        return Prediction(Score(s)) if v else Prediction(EmptyScore)
 
     def validate_input(self, v: Any) -> PmmlInput:
         """Size check against the active fields, then vector → map (`S/api/PmmlModel.scala:127-134`)."""

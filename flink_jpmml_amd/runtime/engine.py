@@ -34,7 +34,7 @@ import collections
 import logging
 import time
 from dataclasses import dataclass
-from typing import List, Optional
+from typing import Tuple, List, Optional
 
 import numpy as np
 
@@ -199,6 +199,7 @@ class StreamingScorer:
         self.max_inflight = int(max_inflight)
         self._inflight: "collections.deque" = collections.deque()
         self.rows_submitted = 0
+        self._row_state = None  # score_row's persistent buffers
         from ..ops import _lib
 
         self._lib = _lib.load()
@@ -449,6 +450,52 @@ class StreamingScorer:
         METRICS.inc("scoring.batches_device")
         return PredictionBatch(n, score_h, valid_h, done, owner=(X, dev_out), on_done=_observe_latency,
                                device_out=dev_out, row_ok=batch.size_ok())
+
+    def score_row(self, x: np.ndarray) -> Tuple[float, bool]:
+        """One record (``[F]`` values, NaN = missing) through the plan, synchronously: the
+        reference's per-record call pattern (`S/package.scala:76-82`) on the device. Persistent
+        pinned staging and output buffers, one H2D copy, one launch on the compute stream (after
+        whatever batches are queued there), the scores written straight into host-mapped memory
+        when the plan's epilogue can (else one D2H copy), one stream sync — no per-call tensor
+        allocation. Same kernels and row semantics as a 1-row :meth:`submit_batch`."""
+        import torch
+
+        from ..ops._lib import check
+
+        st = self._row_state
+        if st is None:
+            F = max(1, self.F)
+            xh = torch.empty(F, dtype=torch.float32, pin_memory=True)
+            oh = torch.empty(8, dtype=torch.float32, pin_memory=True)  # [score, valid bytes...]
+            xd = torch.empty((1, F), dtype=torch.float32, device=self.device)
+            sd = torch.empty(1, dtype=torch.float32, device=self.device)
+            vd = torch.empty(1, dtype=torch.uint8, device=self.device)
+            hs = hv = None
+            if self.direct:
+                base = self.pipe.host_dev_ptr(oh)
+                if base is not None:
+                    hs, hv = base, base + 4
+            st = self._row_state = dict(xh=xh, xh_np=xh.numpy(), oh=oh, oh_np=oh.numpy(), xd=xd, sd=sd, vd=vd,
+                                        hs=hs, hv=hv)
+        st["xh_np"][: self.F] = x
+        cs = self.comp.cuda_stream
+        check(self._lib.pmml_memcpy_async(st["xd"].data_ptr(), st["xh"].data_ptr(), self.F * 4, 1, cs), "row H2D")
+        g = self._graphs
+        if st["hs"] is not None:
+            self.plan.launch(st["xd"], st["hs"], st["hv"], stream=self.comp)
+        else:
+            if g is not None and g.applies(1, {}):
+                g.launch(st["xd"], st["sd"], st["vd"], stream=self.comp)
+            else:
+                self.plan.launch(st["xd"], st["sd"], st["vd"], stream=self.comp)
+            oh = st["oh"].data_ptr()
+            check(self._lib.pmml_memcpy_async(oh, st["sd"].data_ptr(), 4, 2, cs), "row D2H")
+            check(self._lib.pmml_memcpy_async(oh + 4, st["vd"].data_ptr(), 1, 2, cs), "row D2H")
+        self.comp.synchronize()
+        o = st["oh_np"]
+        valid = bool(o[1:2].view(np.uint8)[0])
+        METRICS.inc("scoring.rows_device")
+        return float(o[0]), valid
 
     def score_numpy(self, X: np.ndarray) -> tuple:
         """Blocking convenience: score a host numpy matrix, return numpy ``(score, valid)``."""
