@@ -66,7 +66,8 @@ class MiningEvaluator(ModelEvaluator):
             if self.kind == "regression" and self.method in self._REGRESS_METHODS and self.sub and all(
                     isinstance(seg.predicate, ir.TruePredicate) and type(ev) is TreeEvaluator
                     and ev.kind == "regression" and not ev.model.output and not ev.model.local_transformations
-                    and ev.target is None for seg, ev in zip(self.segments, self.sub)):
+                    and ev.target is None and not getattr(ev, "value_fields", None)
+                    for seg, ev in zip(self.segments, self.sub)):
                 from .native_tree import forest_program
 
                 prog = forest_program(self.sub, [ev.node_value for ev in self.sub])

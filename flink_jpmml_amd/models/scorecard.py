@@ -12,8 +12,11 @@ kernels are the existing ones:
   missing (``returnNullPrediction`` + ``sum``'s missing rule) → ``EmptyScore``. Multiway trees lower
   to the GENERAL tree layout (``tree.hip::tree_general_kernel``). An Attribute with a
   ``ComplexPartialScore`` (an expression over the record, taking precedence over ``partialScore``)
-  has no constant leaf: such scorecards are evaluated directly (:class:`ComplexScorecardEvaluator`,
-  host only — same first-TRUE-attribute rule; a missing expression value voids the score). Reason codes
+  becomes a leaf that reads its value per record from a synthetic DerivedField (``__cps_<i>_<j>``,
+  the expression, in the rewrite's LocalTransformations): the device's derive pass computes the
+  column and the GENERAL tree kernel adds it (``tree.hip`` ``vcol``); a missing expression value
+  voids the score. :class:`ComplexScorecardEvaluator` is the direct formulation kept for the
+  tests. Reason codes
   (``useReasonCodes``, ``pointsBelow`` / ``pointsAbove``) are host outputs.
 * **RuleSetModel** ``firstHit`` = a one-level ``TreeModel``: the (flattened) rules are the root's
   children in document order, a ``CompoundRule``'s predicate AND-ed into its rules; the
@@ -53,20 +56,37 @@ def _segment_tree(sc: ir.Model, root: ir.Node, **kw) -> ir.TreeModel:
                                   local_transformations=[]), root=root, **kw)
 
 
+def complex_field(i: int, j: int) -> str:
+    """Name of the synthetic DerivedField holding characteristic i / attribute j's
+    ComplexPartialScore expression."""
+    return f"__cps_{i}_{j}"
+
+
 def scorecard_as_mining(sc: ir.Scorecard) -> ir.MiningModel:
     segs = [ir.Segment("initialScore", 1.0, ir.TruePredicate(),
                        _segment_tree(sc, ir.Node("initialScore", repr(float(sc.initial_score)), ir.TruePredicate())))]
+    extra: List[ir.DerivedField] = []
     for i, ch in enumerate(sc.characteristics):
         kids = []
         for j, a in enumerate(ch.attributes):
+            if a.complex_score is not None:
+                # a ComplexPartialScore: the leaf reads its value per record from a synthetic
+                # DerivedField of the scorecard's scope (a missing value voids the score)
+                name = complex_field(i, j)
+                extra.append(ir.DerivedField(name, "continuous", "double", a.complex_score))
+                kids.append(ir.Node(f"c{i}a{j}", "0", a.predicate, value_field=name))
+                continue
             if a.partial_score is None:
                 raise UnsupportedFeatureException("Scorecard Attribute without partialScore")
             kids.append(ir.Node(f"c{i}a{j}", repr(float(a.partial_score)), a.predicate))
         root = ir.Node(f"c{i}", None, ir.TruePredicate(), children=kids)
         tree = _segment_tree(sc, root, missing_value_strategy="none", no_true_child_strategy="returnNullPrediction")
         segs.append(ir.Segment(ch.name or f"c{i}", 1.0, ir.TruePredicate(), tree))
-    return ir.MiningModel(**_common(sc, "MiningModel", function_name="regression"), multiple_model_method="sum",
-                          segments=segs, missing_prediction_treatment="returnMissing")
+    common = _common(sc, "MiningModel", function_name="regression")
+    if extra:
+        common["local_transformations"] = list(common["local_transformations"] or []) + extra
+    return ir.MiningModel(**common, multiple_model_method="sum", segments=segs,
+                          missing_prediction_treatment="returnMissing")
 
 
 def _picks(sc: ir.Scorecard, cols: Columns) -> List[Tuple[np.ndarray, np.ndarray]]:
@@ -166,8 +186,9 @@ class ComplexScorecardEvaluator(_ReasonCodes, ModelEvaluator):
 
 
 def make_scorecard_evaluator(model: ir.Scorecard, schema: FieldSchema) -> ModelEvaluator:
-    if any(a.complex_score is not None for ch in model.characteristics for a in ch.attributes):
-        return ComplexScorecardEvaluator(model, schema)
+    """Every scorecard — ComplexPartialScore attributes included (leaves reading a synthetic
+    derived field, so the device lowers them too) — runs as its MiningModel rewrite;
+    :class:`ComplexScorecardEvaluator` stays the direct formulation the tests check it against."""
     return ScorecardEvaluator(model, schema)
 
 

@@ -119,6 +119,8 @@ class TreeEvaluator(ModelEvaluator):
         else:
             self.categories = None
             self.node_value = np.array([_num(nd.score) for nd in self.nodes], dtype=np.float64)
+        # leaves whose score is read per record from a field (complex scorecards)
+        self.value_fields = {i: nd.value_field for i, nd in enumerate(self.nodes) if nd.value_field is not None}
 
     # -- node list (preorder, first child first): built from the IR, or materialised lazily from a
     #    flat body (pmml/flat.py) only when an object-level consumer needs it
@@ -343,6 +345,10 @@ class TreeEvaluator(ModelEvaluator):
                 res = self._mix_rows(res, cols, leaf)
         else:
             val = np.where(ok, self.node_value[safe], NAN)
+            for i, name in getattr(self, "value_fields", {}).items():
+                m = leaf == i
+                if m.any():
+                    val[m] = cols.get(name)[m]
             ok = ok & ~np.isnan(val)
             res = ModelResult("regression", val, ok)
         res.extra["entity_labels"] = ent

@@ -182,7 +182,8 @@ class LdsTreeArgs(ctypes.Structure):
 class GenTreeArgs(ctypes.Structure):
     _fields_ = [("t", TreeArgs), ("nodes", c_void_p), ("children", c_void_p), ("preds", c_void_p),
                 ("pool", c_void_p), ("trees", c_void_p), ("max_steps", c_int), ("pad", c_int),
-                ("mix_mass", c_void_p), ("mix_w", c_void_p), ("mix_tab", c_void_p), ("remap", c_void_p)]
+                ("mix_mass", c_void_p), ("mix_w", c_void_p), ("mix_tab", c_void_p), ("remap", c_void_p),
+                ("vcol", c_void_p)]
 
 
 class HybridArgs(ctypes.Structure):

@@ -699,6 +699,7 @@ struct GenTreeArgs {
   const float* mix_w;          // [nodes] weight of a node as a mixture child
   const int4* mix_tab;         // [trees] {segment weight bits, vote, tree categories, remap offset}
   const int* remap;            // tree category -> accumulator slot
+  const int* vcol;             // [nodes] input column added to the leaf value (complex scorecards), -1: none; nullable
 };
 
 template <bool FEAT_LDS>
@@ -947,6 +948,10 @@ __global__ __launch_bounds__(TB, 2) void tree_general_kernel(GenTreeArgs ga) {
         for (int p = 0; p < a.P; ++p) accl[(slot + p) * TB + tid] += a.leaves[(size_t)node * a.P + p];
       } else {
         acc += a.leaves[node];
+        if (ga.vcol) {  // a leaf scored per record from an input column (NaN -> no prediction)
+          const int vc = ga.vcol[node];
+          if (vc >= 0) acc += gen_feature<FEAT_LDS>(ga, feat_lane, xrow, vc);
+        }
       }
     }
   }

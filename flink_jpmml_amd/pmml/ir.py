@@ -320,6 +320,7 @@ class Node:
     record_count: Optional[float] = None
     default_child: Optional[str] = None
     distributions: List[ScoreDistribution] = field(default_factory=list)
+    value_field: Optional[str] = None  # leaf score read per record from this field (complex scorecards)
 
 
 @dataclass

@@ -140,6 +140,7 @@ def referenced_fields(model: ir.Model) -> List[str]:
             while stack:
                 nd = stack.pop()
                 _pred_fields(nd.predicate, add)
+                add(nd.value_field)
                 stack.extend(reversed(nd.children))
         elif isinstance(m, ir.MiningModel):
             for s in m.segments:

@@ -54,6 +54,7 @@ class GeneralTree:
     mix_vote: bool = False  # set by the ensemble lowering: this tree votes (majority) ...
     mix_weight: float = 1.0  # ... or averages its probabilities, with this segment weight
     mix_remap: Optional[np.ndarray] = None  # tree category -> accumulator slot
+    value_col: Optional[np.ndarray] = None  # per node: kernel input column added to the leaf (or -1)
 
 
 def lower_general_tree(ev: TreeEvaluator, field_index: Dict[str, int]) -> GeneralTree:
@@ -74,6 +75,16 @@ def lower_general_tree(ev: TreeEvaluator, field_index: Dict[str, int]) -> Genera
         bound = max(bound, b)
         stack.extend((c, d + 1, b + max(0, len(nd.children) - 1)) for c in nd.children)
     gt = GeneralTree(ev, field_index, value, probs, ~np.isnan(value), depth)
+    vf = getattr(ev, "value_fields", None)
+    if vf:  # complex scorecard leaves: the score is a (derived) input column of the kernel
+        if classification:  # pragma: no cover - only the regression scorecard rewrite sets them
+            raise NotLowerable("per-record leaf values on a classification tree")
+        col = np.full(len(ev.nodes), -1, dtype=np.int32)
+        for i, name in vf.items():
+            if name not in field_index:
+                raise NotLowerable(f"leaf value field {name!r} is not a kernel input")
+            col[i] = field_index[name]
+        gt.value_col = col
     if tm.missing_value_strategy in MIX_STRATEGIES:
         if not classification:  # pragma: no cover - TreeEvaluator refuses it at load
             raise NotLowerable("weightedConfidence / aggregateNodes need a classification tree")
@@ -182,6 +193,8 @@ def pack_general(trees: List[GeneralTree], weights: List[float], P: int, schema)
     mix_w: List[np.ndarray] = []
     remap: List[int] = []
     any_mix = any(getattr(t, "mix_mass", None) is not None for t in trees)
+    vcol: List[np.ndarray] = []
+    any_vcol = any(getattr(t, "value_col", None) is not None for t in trees)
     pc: Optional[_PredCompiler] = None
     max_depth = 0
     for t, w in zip(trees, weights):
@@ -214,6 +227,9 @@ def pack_general(trees: List[GeneralTree], weights: List[float], P: int, schema)
             (1 << 3) if ev.tree.no_true_child_strategy == "returnLastPrediction" else 0)
         tree_tab.append((base, flags))
         max_depth = max(max_depth, t.depth)
+        if any_vcol:
+            vc = getattr(t, "value_col", None)
+            vcol.append(vc if vc is not None else np.full(len(ev.nodes), -1, dtype=np.int32))
         if any_mix:
             mm = getattr(t, "mix_mass", None)
             n = len(ev.nodes)
@@ -244,6 +260,7 @@ def pack_general(trees: List[GeneralTree], weights: List[float], P: int, schema)
         "mix_w": np.concatenate(mix_w).astype(np.float32) if any_mix else None,
         "mix_tab": np.array(mix_tab, dtype=np.int64).astype(np.int32).reshape(-1, 4) if any_mix else None,
         "remap": np.array(remap or [0], dtype=np.int32) if any_mix else None,
+        "vcol": np.concatenate(vcol).astype(np.int32) if any_vcol else None,
     }
 
 
@@ -346,6 +363,9 @@ def emulate_general(packed: dict, X: np.ndarray, P: int, n_trees: int) -> np.nda
                 out[r] = np.nan
             else:
                 out[r] += packed["payload"][res]
+                vc = packed.get("vcol")
+                if vc is not None and int(vc[res]) >= 0:
+                    out[r] += np.float32(x[int(vc[res])])
     return out
 
 

@@ -1307,7 +1307,10 @@ class TreePlan(DevicePlan):
                                   "rows_wide", "n_stage", "heads", "head_depth", "pointer_ilp", "xcd_split",
                                   "tail_format", "rank_thr", "rank_cnt", "rank_stride", "lds_chunks", "lds_slices",
                                   "lds_rows", "lds_chunk_u4", "lds_n_slices", "mix_mass", "mix_w", "mix_tab",
-                                  "mix_remap")
+                                  "mix_remap", "vcol")
+
+    # GENERAL-layout extras (sibling mixtures, per-record leaf columns); None on every other layout
+    mix_mass = mix_w = mix_tab = mix_remap = vcol = None
 
     WIDE_G = 4  # tree groups of the wide kernel (mirrors csrc)
 
@@ -1428,6 +1431,7 @@ class TreePlan(DevicePlan):
             self.mix_w = self._t(g["mix_w"]) if mix else None
             self.mix_tab = self._t(g["mix_tab"].reshape(-1)) if mix else None
             self.mix_remap = self._t(g["remap"]) if mix else None
+            self.vcol = self._t(g["vcol"]) if g["vcol"] is not None else None
             self.roots = None
             self.max_steps = g["max_steps"]
             self.has_dr = False
@@ -1960,6 +1964,7 @@ class TreePlan(DevicePlan):
         g.pool, g.trees, g.max_steps = ptr(self.pool), ptr(self.trees_tab), int(self.max_steps)
         g.mix_mass, g.mix_w = ptr(getattr(self, "mix_mass", None)), ptr(getattr(self, "mix_w", None))
         g.mix_tab, g.remap = ptr(getattr(self, "mix_tab", None)), ptr(getattr(self, "mix_remap", None))
+        g.vcol = ptr(getattr(self, "vcol", None))
         check(self.lib.pmml_tree_general_launch(stream_handle(stream), ctypes.byref(g)), "general tree kernel")
 
 

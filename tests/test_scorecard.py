@@ -198,14 +198,14 @@ def _with_complex_score(txt: str) -> tuple:
 @pytest.mark.parametrize("seed", [0, 1])
 def test_complex_partial_score(seed):
     """ComplexPartialScore (precedence over partialScore): the attribute's points are the expression
-    on the record; everything else equals the constant scorecard. Host-only (no tree form)."""
-    from flink_jpmml_amd.models.scorecard import ComplexScorecardEvaluator
-    from flink_jpmml_amd.runtime.plans import NotLowerable, compile_plan, lowering_dry_run
+    on the record; everything else equals the constant scorecard. The MiningModel rewrite (a leaf
+    reading a synthetic derived field) equals the direct formulation bit for bit."""
+    from flink_jpmml_amd.models.scorecard import ComplexScorecardEvaluator, ScorecardEvaluator
 
     base = scorecard_pmml(seed=seed)
     txt, const, thr = _with_complex_score(base)
     c0, c1 = CompiledPmml.from_string(base), CompiledPmml.from_string(txt)
-    assert isinstance(c1.evaluator, ComplexScorecardEvaluator)
+    assert isinstance(c1.evaluator, ScorecardEvaluator)
     _, X = mixed_records(800, 4, seed=seed + 5, missing_rate=0.08)
     s0, v0 = c0.score_matrix_oracle(X)
     s1, v1 = c1.score_matrix_oracle(X)
@@ -214,8 +214,64 @@ def test_complex_partial_score(seed):
     assert hit[v1].any() and (~hit[v1]).any()
     np.testing.assert_allclose(s1[v1 & ~hit], s0[v1 & ~hit], rtol=0, atol=1e-9)
     np.testing.assert_allclose(s1[v1 & hit], (s0 - const + 2 * X[:, 1] + 3)[v1 & hit], rtol=0, atol=1e-9)
+    # the direct formulation
+    direct = ComplexScorecardEvaluator(c1.evaluator.scorecard, c1.schema)
+    P, ok = c1.prepare(X)
+    rd = direct.evaluate(c1.columns(P))
+    np.testing.assert_array_equal(rd.valid & ok, v1)
+    np.testing.assert_allclose(rd.value[v1], s1[v1], rtol=0, atol=1e-9)
     # reason codes use the expression's points too
     res = c1.result(X[:50])
     assert len(res.extra["reason_codes"]) == 50
-    with lowering_dry_run(), pytest.raises(NotLowerable):
-        compile_plan(c1, "cpu")
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_complex_partial_score_lowers_to_the_general_layout(seed):
+    """Round 6: the synthetic derived field is a derive-pass column and the
+    GENERAL kernel adds it to the leaf (``vcol``); the CPU twin equals the oracle."""
+    from flink_jpmml_amd.runtime.derive import FieldView, plan_field_layout
+    from flink_jpmml_amd.runtime.general_tree import emulate_general, lower_general_tree, pack_general
+    from flink_jpmml_amd.runtime.plans import compile_plan, ensemble_spec, lowering_dry_run
+
+    txt, _, _ = _with_complex_score(scorecard_pmml(seed=seed))
+    c = CompiledPmml.from_string(txt)
+    with lowering_dry_run():
+        plan = compile_plan(c, "cpu")
+    assert type(plan).__name__ == "DerivedPlan"
+    layout = plan_field_layout(c, allow_alias=True)
+    assert layout.program is not None
+    view = FieldView(c, layout, prepared=True)
+    spec = ensemble_spec(view, lower=lower_general_tree)
+    packed = pack_general(spec.trees, spec.weights, spec.P, c.schema)
+    assert packed["vcol"] is not None and (packed["vcol"] >= 0).sum() == 1
+    _, X = mixed_records(600, 4, seed=seed + 9, missing_rate=0.08)
+    P, _ = c.prepare(X)
+    # the derive pass's columns: the active inputs, then the derived fields the layout computes
+    cols = c.columns(P)
+    model = c.evaluator.model
+    child = cols.child(model.local_transformations)
+    Xk = np.stack([child.get(name) for name in layout.columns], axis=1)
+    acc = emulate_general(packed, Xk.astype(np.float32), spec.P, len(spec.trees))
+    ref, vref = c.score_matrix_oracle(X)
+    ok = ~np.isnan(acc).any(axis=1)
+    assert (ok == vref).all()
+    e = spec.epi
+    assert np.allclose(e["a"] * acc[ok, 0] + e["b"], ref[ok], atol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [0, 1])
+def test_complex_partial_score_on_gpu(gpu, seed):
+    """ComplexPartialScore scorecards on the device (derive pass + GENERAL kernel leaf column)."""
+    from flink_jpmml_amd.runtime.plans import TreePlan
+
+    txt, _, _ = _with_complex_score(scorecard_pmml(seed=seed))
+    c = CompiledPmml.from_string(txt)
+    plan = c.plan(gpu)
+    assert isinstance(getattr(plan, "inner", plan), TreePlan)
+    _, X = mixed_records(20_000, 4, seed=seed + 3, missing_rate=0.08)
+    s, v = plan.score(X)
+    s, v = s.cpu().numpy(), v.cpu().numpy().astype(bool)
+    ref, vref = c.score_matrix_oracle(X)
+    assert (v == vref).all() and v.any()
+    assert np.allclose(s[v], ref[v], rtol=1e-5, atol=1e-4)
