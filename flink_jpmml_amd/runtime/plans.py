@@ -148,12 +148,12 @@ def build_field_prep(compiled, fields: List[str]) -> Tuple[np.ndarray, bool]:
         if df is not None:
             if optype != "continuous" and df.intervals:
                 fl |= FP_ROW_INVALID
-            if (df.invalid_values or df.missing_values) and df.is_string:
-                raise NotLowerable(f"field {name!r}: missing / invalid value lists on a string field are host-only")
             # numeric missing-value sentinels (e.g. -999) and invalid-value lists, compared in fp32
-            # (prepare_matrix's order: a missing value first, then an invalid one)
-            sentinels = _fp32_values(name, df.missing_values, "missing")
-            invalids = _fp32_values(name, df.invalid_values, "invalid")
+            # (prepare_matrix's order: a missing value first, then an invalid one). A string field's
+            # lists are text: its matrix column holds vocabulary codes, and the text ingest already
+            # read a listed missing token as missing -- prepare_matrix ignores them, and so does this
+            sentinels = [] if df.is_string else _fp32_values(name, df.missing_values, "missing")
+            invalids = [] if df.is_string else _fp32_values(name, df.invalid_values, "invalid")
             if len(sentinels) == 1 and not invalids:
                 fl |= FP_MISSING_VALUE
                 mval = sentinels[0]

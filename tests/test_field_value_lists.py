@@ -122,17 +122,26 @@ def test_value_lists_lower_into_a_field_table(treat):
             assert P[i, 1] == x[i] and ok[i]
 
 
-def test_string_field_lists_stay_host_only():
-    from flink_jpmml_amd.runtime.plans import NotLowerable, build_field_prep
+def test_string_field_lists_are_text_level_like_the_matrix_oracle():
+    """A string field's missing / invalid Value lists are matched as text by the ingest; on the
+    numeric (vocabulary-code) matrix the oracle's prepare_matrix ignores them — so does the
+    FieldPrep table (no flag), and the device and oracle agree."""
+    from flink_jpmml_amd.runtime.plans import FP_VALUE_LIST, build_field_prep
 
     txt = MODELS["regression"][0]
     m = re.search(r'<DataField name="(\w+)" optype="categorical" dataType="string">', txt)
     assert m
-    name = m.group(1)
-    txt = txt.replace(m.group(0), m.group(0) + '<Value value="NA" property="missing"/>', 1)
-    c = CompiledPmml.from_string(txt)
-    with pytest.raises(NotLowerable):
-        build_field_prep(c, c.active_fields)
+    txt2 = txt.replace(m.group(0), m.group(0) + '<Value value="NA" property="missing"/>'
+                       '<Value value="zzz" property="invalid"/>', 1)
+    c, c2 = CompiledPmml.from_string(txt), CompiledPmml.from_string(txt2)
+    raw, _ = build_field_prep(c2, c2.active_fields)
+    j = c2.active_fields.index(m.group(1))
+    assert not raw[j, 0] & FP_VALUE_LIST
+    X = _inputs(300, codes=True)
+    s1, v1 = c.score_matrix_oracle(X)
+    s2, v2 = c2.score_matrix_oracle(X)
+    assert (v1 == v2).all()
+    np.testing.assert_array_equal(s1[v1], s2[v2])
 
 
 @pytest.mark.parametrize("values,flagged", [(("NA",), False), (("NA", "-999", "?"), True)])
