@@ -54,6 +54,10 @@ class ScoringConfig:
     oracle (batched, vectorised) and count ``scoring.host_fallback``; ``warn`` — the same plus one
     WARNING per model; ``error`` — fail the model load (strict production setting)."""
 
+    host_threads: int = 0
+    """Worker threads of the native host tree walk (``fallback="host"`` models, CPU-only ranks,
+    direct CPU ``predict_batch``); 0 = ``FJA_HOST_THREADS`` or 1. Results do not depend on it."""
+
     # -- columnar (RecordBatch) pipeline
     micro_batch: int = 1 << 19
     """Rows per device kernel launch when a RecordBatch is split (H2D / kernel overlap)."""
@@ -148,7 +152,8 @@ class ScoringConfig:
                   device=get("DEVICE", str), precision=get("PRECISION", str), fallback=get("FALLBACK", str),
                   micro_batch=get("MICRO_BATCH", int), cache_capacity=get("CACHE_CAPACITY", int),
                   checkpoint_dir=get("CHECKPOINT_DIR", str), watchdog_s=get("WATCHDOG_S", float),
-                  graph_max_rows=get("GRAPH_MAX_ROWS", int), metrics_port=get("METRICS_PORT", int))
+                  graph_max_rows=get("GRAPH_MAX_ROWS", int), metrics_port=get("METRICS_PORT", int),
+                  host_threads=get("HOST_THREADS", int))
         kw = {k: v for k, v in kw.items() if v is not None}
         kw.update({k: v for k, v in overrides.items() if v is not None})
         return ScoringConfig(**kw)

@@ -64,7 +64,7 @@ def build_fastpath(force: bool = False) -> str:
         return out
     tmp = out + ".tmp"
     # -ffp-contract=off: the oracle's sums round every product and every partial sum (no FMA)
-    cmd = ["g++", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared", "-Wall", "-fvisibility=hidden",
+    cmd = ["g++", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared", "-pthread", "-Wall", "-fvisibility=hidden",
            "-I" + sysconfig.get_paths()["include"], "-I" + np.get_include(), *FAST_SRCS, "-o", tmp]
     r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
     if r.returncode != 0:

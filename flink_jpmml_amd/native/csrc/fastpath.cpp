@@ -31,6 +31,7 @@
 
 PyObject *fja_scan_trees(PyObject *, PyObject *args);     // pmml_scan.cpp
 PyObject *fja_forest_compile(PyObject *, PyObject *args); // tree_walk.cpp
+PyObject *fja_set_walk_threads(PyObject *, PyObject *args); // tree_walk.cpp
 PyObject *fja_forest_leaves(PyObject *, PyObject *args);  // tree_walk.cpp
 PyObject *fja_forest_values(PyObject *, PyObject *args);  // tree_walk.cpp
 PyObject *fja_forest_sums(PyObject *, PyObject *args);    // tree_walk.cpp
@@ -279,6 +280,7 @@ PyMethodDef methods[] = {
     {"pack_dense", pack_dense, METH_VARARGS, "Pack a list of DenseVector objects into a float64 matrix."},
     {"make_predictions", make_predictions, METH_VARARGS, "Prediction objects for a scored batch."},
     {"scan_trees", fja_scan_trees, METH_VARARGS, "Streaming TreeModel reader: (skeleton, flat trees, strings)."},
+    {"set_walk_threads", fja_set_walk_threads, METH_VARARGS, "Worker threads of the host tree walk (default 1)."},
     {"forest_compile", fja_forest_compile, METH_VARARGS, "Oracle tree walk: compile a program once (capsule)."},
     {"forest_leaves", fja_forest_leaves, METH_VARARGS, "Oracle tree walk: scoring node per tree and row."},
     {"forest_values", fja_forest_values, METH_VARARGS, "Oracle tree walk: leaf value per row and tree."},

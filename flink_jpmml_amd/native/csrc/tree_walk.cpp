@@ -37,7 +37,10 @@
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
 
+#include <algorithm>
+#include <atomic>
 #include <cmath>
+#include <thread>
 #include <new>
 #if defined(__x86_64__)
 #include <immintrin.h>
@@ -721,6 +724,53 @@ double pairwise_sum(const double *a, Py_ssize_t n) {
     return pairwise_sum(a, n2) + pairwise_sum(a + n2, n - n2);
 }
 
+// Row blocks over worker threads (set_walk_threads / FJA_HOST_THREADS, default 1: the
+// reference's one-record-at-a-time subtask is single-threaded). fn(r0, r1, worker); every block
+// writes only its own rows, so the result does not depend on the thread count.
+std::atomic<int> g_walk_threads{-1};
+
+int walk_threads() {
+    int t = g_walk_threads.load(std::memory_order_relaxed);
+    if (t < 0) {
+        const char *e = std::getenv("FJA_HOST_THREADS");
+        t = e ? std::atoi(e) : 1;
+        t = t < 1 ? 1 : (t > 256 ? 256 : t);
+        g_walk_threads.store(t, std::memory_order_relaxed);
+    }
+    return t;
+}
+
+template <class Fn>
+void for_blocks(Py_ssize_t n, Fn &&fn) {
+    const Py_ssize_t nb = (n + ROW_BLOCK - 1) / ROW_BLOCK;
+    Py_ssize_t threads = walk_threads();
+    const Py_ssize_t by_size = nb / 16;  // >= 16 blocks (4096 rows) per extra thread
+    if (threads > by_size) threads = by_size;
+    if (threads <= 1) {
+        for (Py_ssize_t b = 0; b < nb; ++b) fn(b * ROW_BLOCK, std::min(n, (b + 1) * ROW_BLOCK), 0);
+        return;
+    }
+    std::atomic<Py_ssize_t> next{0};
+    std::vector<std::thread> pool;
+    pool.reserve(static_cast<size_t>(threads));
+    for (Py_ssize_t w = 0; w < threads; ++w)
+        pool.emplace_back([&, w] {
+            for (;;) {
+                const Py_ssize_t b = next.fetch_add(1);
+                if (b >= nb) break;
+                fn(b * ROW_BLOCK, std::min(n, (b + 1) * ROW_BLOCK), static_cast<int>(w));
+            }
+        });
+    for (auto &t : pool) t.join();
+}
+
+PyObject *set_walk_threads(PyObject *, PyObject *args) {
+    int t;
+    if (!PyArg_ParseTuple(args, "i", &t)) return nullptr;
+    g_walk_threads.store(t < 1 ? 1 : (t > 256 ? 256 : t));
+    Py_RETURN_NONE;
+}
+
 PyObject *forest_leaves(PyObject *, PyObject *args) {
     Call c;
     if (!c.parse(args, Kind::LEAVES)) return nullptr;
@@ -734,12 +784,11 @@ PyObject *forest_leaves(PyObject *, PyObject *args) {
     Fixed local;
     if (fc == nullptr) compile_all(c, local);
     const Fixed &f = fc ? *fc : local;
-    for (Py_ssize_t r0 = 0; r0 < n; r0 += ROW_BLOCK) {
-        const Py_ssize_t r1 = r0 + ROW_BLOCK < n ? r0 + ROW_BLOCK : n;
+    for_blocks(n, [&](Py_ssize_t r0, Py_ssize_t r1, int) {
         run_block(c, f, X, r0, r1, avx, [&](Py_ssize_t t, Py_ssize_t r, int32_t g) {
             out[t * n + r] = g < 0 ? -1 : g - roots[t];
         });
-    }
+    });
     Py_END_ALLOW_THREADS
     Py_RETURN_NONE;
 }
@@ -757,12 +806,11 @@ PyObject *forest_values(PyObject *, PyObject *args) {
     Fixed local;
     if (fc == nullptr) compile_all(c, local);
     const Fixed &f = fc ? *fc : local;
-    for (Py_ssize_t r0 = 0; r0 < n; r0 += ROW_BLOCK) {
-        const Py_ssize_t r1 = r0 + ROW_BLOCK < n ? r0 + ROW_BLOCK : n;
+    for_blocks(n, [&](Py_ssize_t r0, Py_ssize_t r1, int) {
         run_block(c, f, X, r0, r1, avx, [&](Py_ssize_t t, Py_ssize_t r, int32_t g) {
             out[r * T + t] = g < 0 ? NAN : lv[g];
         });
-    }
+    });
     Py_END_ALLOW_THREADS
     Py_RETURN_NONE;
 }
@@ -778,9 +826,9 @@ PyObject *forest_sums(PyObject *, PyObject *args) {
     double *out = static_cast<double *>(c.out.b.buf);
     const Py_ssize_t n = c.n, T = c.T;
     const bool avx = use_avx512(c);
-    std::vector<double> buf;
+    std::vector<double> buf;  // one ROW_BLOCK x T slab per worker
     try {
-        buf.resize(static_cast<size_t>(ROW_BLOCK) * static_cast<size_t>(T));
+        buf.resize(static_cast<size_t>(ROW_BLOCK) * static_cast<size_t>(T) * static_cast<size_t>(walk_threads()));
     } catch (const std::bad_alloc &) {
         return PyErr_NoMemory();
     }
@@ -789,15 +837,14 @@ PyObject *forest_sums(PyObject *, PyObject *args) {
     Fixed local;
     if (fc == nullptr) compile_all(c, local);
     const Fixed &f = fc ? *fc : local;
-    for (Py_ssize_t r0 = 0; r0 < n; r0 += ROW_BLOCK) {
-        const Py_ssize_t r1 = r0 + ROW_BLOCK < n ? r0 + ROW_BLOCK : n;
-        double *bb = buf.data();
+    for_blocks(n, [&](Py_ssize_t r0, Py_ssize_t r1, int worker) {
+        double *bb = buf.data() + static_cast<size_t>(worker) * ROW_BLOCK * static_cast<size_t>(T);
         run_block(c, f, X, r0, r1, avx, [&](Py_ssize_t t, Py_ssize_t r, int32_t g) {
             const double v = g < 0 ? NAN : lv[g];
             bb[(r - r0) * T + t] = w ? v * w[t] : v;
         });
         for (Py_ssize_t r = r0; r < r1; ++r) out[r] = pairwise_sum(bb + (r - r0) * T, T);
-    }
+    });
     Py_END_ALLOW_THREADS
     Py_RETURN_NONE;
 }
@@ -843,6 +890,7 @@ PyObject *forest_compile(PyObject *, PyObject *args) {
 }  // namespace
 
 PyObject *fja_forest_compile(PyObject *self, PyObject *args) { return forest_compile(self, args); }
+PyObject *fja_set_walk_threads(PyObject *self, PyObject *args) { return set_walk_threads(self, args); }
 PyObject *fja_forest_leaves(PyObject *self, PyObject *args) { return forest_leaves(self, args); }
 PyObject *fja_forest_values(PyObject *self, PyObject *args) { return forest_values(self, args); }
 PyObject *fja_forest_sums(PyObject *self, PyObject *args) { return forest_sums(self, args); }

@@ -564,6 +564,15 @@ class NullScorer:
         pass
 
 
+def _set_host_threads(n: int) -> None:
+    """Worker threads of the native host tree walk (process-wide)."""
+    from ..native import fastpath
+
+    fp = fastpath()
+    if fp is not None and hasattr(fp, "set_walk_threads"):
+        fp.set_walk_threads(int(n))
+
+
 def make_scorer(compiled, device, config=None, pipeline: Optional[DevicePipeline] = None, plan=None,
                 lower_error: Optional[str] = None):
     """The scorer for ``compiled`` on ``device`` under ``config``'s fallback policy.
@@ -579,6 +588,8 @@ def make_scorer(compiled, device, config=None, pipeline: Optional[DevicePipeline
     cfg = config or ScoringConfig()
     if not compiled.target_fields:
         return NullScorer(compiled.n_features)
+    if cfg.host_threads:
+        _set_host_threads(cfg.host_threads)
     if device is None:
         return HostScorer(compiled)
     if plan is None:

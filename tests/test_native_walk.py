@@ -283,3 +283,23 @@ def test_native_neural_layers_are_bit_identical_to_the_connection_loop(shape):
     s2, v2 = c2.score_matrix_oracle(X)
     np.testing.assert_array_equal(v1, v2)
     assert np.array_equal(s1[v1], s2[v2])
+
+
+def test_thread_count_does_not_change_results():
+    """set_walk_threads / FJA_HOST_THREADS: blocks of rows on worker threads, every block writing
+    only its own rows -- bit-identical results for any thread count."""
+    from flink_jpmml_amd.bench import synth
+    from flink_jpmml_amd.native import fastpath
+
+    c = CompiledPmml.from_string(_gbdt_doc(5, n_trees=64))
+    prog = c.evaluator.native_forest()
+    X = np.ascontiguousarray(synth.stream_matrix(50_000, 8, seed=2, missing_rate=0.05), dtype=np.float64)
+    try:
+        fastpath().set_walk_threads(1)
+        one = (prog.leaves(X), prog.values(X), prog.sums(X))
+        fastpath().set_walk_threads(6)
+        six = (prog.leaves(X), prog.values(X), prog.sums(X))
+    finally:
+        fastpath().set_walk_threads(1)
+    for a, b in zip(one, six):
+        np.testing.assert_array_equal(a, b)
