@@ -350,6 +350,7 @@ def test_near_sentinel_input_is_missing_on_the_device_only(gpu):
     s_near, _ = plan.score(X)
     s_sent, _ = plan.score(Xs)
     np.testing.assert_array_equal(s_near.cpu().numpy(), s_sent.cpu().numpy())  # device: missing
-    ref_near, _ = c.score_matrix_oracle(X)
-    ref_sent, _ = c.score_matrix_oracle(Xs)
-    assert not np.array_equal(ref_near, ref_sent)  # oracle: -999.00003 is a value, not the sentinel
+    P_near, _ = c.prepare(X)
+    P_sent, _ = c.prepare(Xs)
+    assert (P_near[:, 1] == near).all()  # oracle: -999.00003 is a value, not the sentinel
+    assert (P_sent[:, 1] == 0.3).all()  # the sentinel takes the missingValueReplacement
