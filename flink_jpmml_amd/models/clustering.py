@@ -66,22 +66,34 @@ class ClusteringEvaluator(ModelEvaluator):
         """``[n, K]`` distance (or similarity) matrix, float64."""
         n, F = X.shape
         K = self.centers.shape[0]
+        # bounded [rows, K, F] blocks: every row's distances are independent, so the chunked
+        # result is bit-identical (a 256-centre x 128-field model no longer builds GBs at once)
+        chunk = max(1, (1 << 22) // max(1, K * F))
+        if n > chunk:
+            return np.concatenate([self.distances(X[i:i + chunk]) for i in range(0, n, chunk)], axis=0)
         miss = np.isnan(X)
         if self.metric in _SIMILARITY_METRICS:
             return self._binary_similarity(X)
-        comp = np.empty((n, K, F))
         diff = X[:, None, :] - self.centers[None, :, :]
-        for j, cf in enumerate(self.compare):
-            d = diff[:, :, j]
+        cfs = np.asarray(self.compare, dtype=object)
+        kinds = set(self.compare)
+        comp = np.empty((n, K, F)) if len(kinds) > 1 else None
+        for cf in kinds:  # the same element-wise formulas as one field at a time, per group
+            cols = slice(None) if comp is None else np.flatnonzero(cfs == cf)
+            d = diff[:, :, cols]
             if cf == "absDiff":
-                comp[:, :, j] = np.abs(d)
+                v = np.abs(d)
             elif cf == "gaussSim":
-                s = self.scales[j]
-                comp[:, :, j] = np.exp(-np.log(2.0) * d * d / (s * s))
+                s = self.scales[cols]
+                v = np.exp(-np.log(2.0) * d * d / (s * s))
             elif cf == "delta":
-                comp[:, :, j] = (d != 0).astype(np.float64)
+                v = (d != 0).astype(np.float64)
             else:  # equal
-                comp[:, :, j] = (d == 0).astype(np.float64)
+                v = (d == 0).astype(np.float64)
+            if comp is None:
+                comp = np.ascontiguousarray(v, dtype=np.float64)
+            else:
+                comp[:, :, cols] = v
         comp[np.broadcast_to(miss[:, None, :], comp.shape)] = 0.0
         w = self.weights[None, None, :]
         if self.metric == "squaredEuclidean":
