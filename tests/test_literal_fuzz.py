@@ -182,3 +182,15 @@ def test_array_count_and_content(arr, ok):
     else:
         with pytest.raises(PmmlParseError):
             CompiledPmml.from_string(text)
+
+
+@pytest.mark.parametrize("value,ok", [("1", True), ("-1.5", True), ("+.5", True), ("2.", True), ("1e-3", True),
+                                      ("6.02E+23", True), ("NaN", True), ("-Infinity", True), (" 7 ", True),
+                                      ("inf", False), ("nan", False), ("infinity", False), ("1_000", False),
+                                      ("0x1p3", False), ("1.5f", False), ("", False), ("1,5", False)])
+def test_literals_follow_java_double_grammar(value, ok):
+    """JPMML parses numbers with Double.parseDouble -- Python-only spellings are not
+    numbers (Java's type suffixes / hex floats are refused too: no exporter writes them)."""
+    from flink_jpmml_amd.pmml.validate import literal_ok
+
+    assert literal_ok("double", value) is ok
