@@ -12,3 +12,5 @@ rc=$?; echo "suite rc=$rc"; tail -3 $O/pytest.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench1.json 2> $O/bench1.err || { tail -30 $O/bench1.err; exit 1; }
 python3 -c "import json; d=json.loads(open('$O/bench1.json').read().strip().splitlines()[-1]); print(d['value'], d['n_gpus'], d['check'])"
+timeout -k 10 200 python3 scripts/probe_blaslt.py > $O/blaslt.jsonl 2> $O/blaslt.err || { tail -20 $O/blaslt.err; exit 1; }
+cat $O/blaslt.jsonl
