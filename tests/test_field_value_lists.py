@@ -338,12 +338,15 @@ def test_near_sentinel_input_is_missing_on_the_device_only(gpu):
     """ADVICE r5 (low), documented in docs/PARITY.md "Deliberate deviations": a float64 input within
     half an fp32 ulp of the sentinel rounds onto it in the fp32 row the kernels read, so the device
     treats it as missing while the float64 oracle keeps the value."""
-    txt = _with_replacement(_with_sentinel(MODELS["gbdt"][0]))
+    base = MODELS["gbdt"][0].replace('<DataField name="f1" optype="continuous" dataType="float"/>',
+                                     '<DataField name="f1" optype="continuous" dataType="double"/>')
+    assert 'name="f1" optype="continuous" dataType="double"' in base  # float fields round first (no deviation)
+    txt = _with_replacement(_with_sentinel(base))
     c = CompiledPmml.from_string(txt)
     plan = c.plan(gpu)
     near = -999.00003  # |near - (-999)| < half an fp32 ulp (3.05e-5) at 999
     assert np.float32(near) == np.float32(SENT) and near != SENT
-    X = _inputs(64)
+    X = _inputs(64).astype(np.float64)  # float64 records: -999.00003 is representable
     X[:, 1] = near
     Xs = X.copy()
     Xs[:, 1] = SENT
