@@ -17,7 +17,12 @@ namespace {
 // through the constant cache plus a per-lane select, instead of two 64-lane vector gathers of
 // the same one or two nodes (the walk is bound by the vector memory pipe's per-instruction cost,
 // profiles/r3w).
-template <bool GENERAL, bool FEAT_LDS, int PILP = 8, bool MASKED = false, bool USKIP = false, bool PEEL = false>
+// INL (VAR_POINTER_INLINE): a leaf child's payload sits in its parent's child field (meta bit 29:
+// the left child is a leaf, bit 28: the right one) -- the leaf value's fp32 bits for a sum
+// ensemble, the class index for an unweighted vote (GENERAL, one increment). The walk ends at the
+// parent with the payload in hand: no leaf gather (one per tree and row; P of them for votes).
+template <bool GENERAL, bool FEAT_LDS, int PILP = 8, bool MASKED = false, bool USKIP = false, bool PEEL = false,
+          bool INL = false>
 __device__ __forceinline__ void pointer_walk(const TreeArgs& a) {
   extern __shared__ __align__(16) uint32_t smem[];
   float* feat = reinterpret_cast<float*>(smem);
@@ -63,10 +68,14 @@ __device__ __forceinline__ void pointer_walk(const TreeArgs& a) {
     const int nt = min(PILP, te - t0);
     int code[PILP];
     bool pz[PILP];
+    bool inl[PILP];       // INL: the walk ended on an inline leaf payload (lpay)
+    uint32_t lpay[PILP];
 #pragma unroll
     for (int i = 0; i < PILP; ++i) {
       code[i] = i < nt ? a.roots[t0 + i] : -1;
       pz[i] = false;
+      inl[i] = false;
+      lpay[i] = 0u;
     }
     if (PEEL) {
       // level 0: the root (uniform)
@@ -142,7 +151,14 @@ __device__ __forceinline__ void pointer_walk(const TreeArgs& a) {
         const bool right = (x >= __uint_as_float(nd[i].x)) || (isn && (nd[i].y >> 31));
         const int nc = right ? (int)nd[i].w : (int)nd[i].z;
         pz[i] = pz[i] || nulled;
-        code[i] = act ? (nulled ? -1 : nc) : code[i];
+        if (INL) {
+          const bool to_leaf = act && !nulled && ((nd[i].y >> (right ? 28 : 29)) & 1u);
+          inl[i] = inl[i] || to_leaf;
+          lpay[i] = to_leaf ? (uint32_t)nc : lpay[i];
+          code[i] = act ? ((nulled || to_leaf) ? -1 : nc) : code[i];
+        } else {
+          code[i] = act ? (nulled ? -1 : nc) : code[i];
+        }
         live = live || code[i] >= 0;
       }
     }
@@ -152,6 +168,11 @@ __device__ __forceinline__ void pointer_walk(const TreeArgs& a) {
       if (pz[i]) {
         if (GENERAL) poisoned = true;
         else acc += __builtin_nanf("");
+        continue;
+      }
+      if (INL && inl[i]) {
+        if (GENERAL) accl[(a.tree_slot[t0 + i] + (int)lpay[i]) * TB + tid] += 1.f;
+        else acc += __uint_as_float(lpay[i]);
         continue;
       }
       const int leaf = ~code[i];
@@ -166,9 +187,10 @@ __device__ __forceinline__ void pointer_walk(const TreeArgs& a) {
   finish_row(a, acc, accl, split, GENERAL, row, row_ok && !poisoned);
 }
 
-template <bool GENERAL, bool FEAT_LDS, int PILP = 8, bool MASKED = false, bool USKIP = false, bool PEEL = false>
+template <bool GENERAL, bool FEAT_LDS, int PILP = 8, bool MASKED = false, bool USKIP = false, bool PEEL = false,
+          bool INL = false>
 __global__ __launch_bounds__(TB, 2) void tree_pointer_kernel(TreeArgs a) {
-  pointer_walk<GENERAL, FEAT_LDS, PILP, MASKED, USKIP, PEEL>(a);
+  pointer_walk<GENERAL, FEAT_LDS, PILP, MASKED, USKIP, PEEL, INL>(a);
 }
 
 // Several pointer-layout ensembles over the SAME rows in one launch — the segments of a segmented
@@ -1101,6 +1123,24 @@ PMML_API int pmml_tree_launch(hipStream_t stream, const TreeArgs* args, int layo
       } else {
         err = prepare_launch(tree_pointer_kernel<false, true, 8, false, true>, lds);
         if (!err) hipLaunchKernelGGL((tree_pointer_kernel<false, true, 8, false, true>), grid, dim3(TB), lds, stream, a);
+      }
+    } else if (a.variant == VAR_POINTER_INLINE) {
+      if (feat_lds && a.general) {
+        err = prepare_launch(tree_pointer_kernel<true, true, 8, false, false, false, true>, lds);
+        if (!err)
+          hipLaunchKernelGGL((tree_pointer_kernel<true, true, 8, false, false, false, true>), grid, dim3(TB), lds, stream, a);
+      } else if (feat_lds) {
+        err = prepare_launch(tree_pointer_kernel<false, true, 8, false, false, false, true>, lds);
+        if (!err)
+          hipLaunchKernelGGL((tree_pointer_kernel<false, true, 8, false, false, false, true>), grid, dim3(TB), lds, stream, a);
+      } else if (a.general) {
+        err = prepare_launch(tree_pointer_kernel<true, false, 8, false, false, false, true>, lds);
+        if (!err)
+          hipLaunchKernelGGL((tree_pointer_kernel<true, false, 8, false, false, false, true>), grid, dim3(TB), lds, stream, a);
+      } else {
+        err = prepare_launch(tree_pointer_kernel<false, false, 8, false, false, false, true>, lds);
+        if (!err)
+          hipLaunchKernelGGL((tree_pointer_kernel<false, false, 8, false, false, false, true>), grid, dim3(TB), lds, stream, a);
       }
     } else if (a.variant == VAR_POINTER_USKIP || a.variant == VAR_POINTER_PEEL) {
       return -4;  // features in LDS only

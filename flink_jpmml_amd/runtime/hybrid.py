@@ -30,8 +30,11 @@ def head_words(H: int) -> int:
     return (w + 3) // 4 * 4
 
 
-def pack_trees(trees, weights: List[float], P: int, H: int, feat_lds: bool, order: str = "bfs"
-               ) -> Tuple[Optional[np.ndarray], np.ndarray, np.ndarray, np.ndarray, bool]:
+INLINE_LEFT_BIT, INLINE_RIGHT_BIT = 29, 28  # tree.hip pointer_walk<..., INL>
+
+
+def pack_trees(trees, weights: List[float], P: int, H: int, feat_lds: bool, order: str = "bfs",
+               inline_leaves: bool = False) -> Tuple[Optional[np.ndarray], np.ndarray, np.ndarray, np.ndarray, bool]:
     """``(heads [n_trees, head_words] u32 or None when H == 0, tail nodes [n, 4] u32,
     leaves [n_leaves, P] f32, root codes [n_trees] i32, has_default_right)``.
 
@@ -39,7 +42,12 @@ def pack_trees(trees, weights: List[float], P: int, H: int, feat_lds: bool, orde
     with the two children of every node adjacent: the lock-step walk moves all lanes of a wave
     through the same level of the same tree together, so their loads share cache lines (the
     top levels of a tree sit in a few lines; a node's two children always share one). ``"dfs"``:
-    the lowered tree's own (preorder) order."""
+    the lowered tree's own (preorder) order.
+
+    ``inline_leaves`` (pointer layout, ``VAR_POINTER_INLINE``): a leaf child's payload is stored
+    in its parent's child field with meta bit 29 (left) / 28 (right) set -- the fp32 bits of the
+    weighted leaf value (``P == 1``), or the class index of a unit one-hot vote (``P > 1``); other
+    leaves keep their ``~leaf`` code into the leaf table."""
     if order not in ("bfs", "dfs"):
         raise ValueError("order must be 'bfs' or 'dfs'")
     from .plans import _canonical_vec
@@ -117,6 +125,20 @@ def pack_trees(trees, weights: List[float], P: int, H: int, feat_lds: bool, orde
             nd[:, 1] = meta[tk]
             nd[:, 2] = code[lc[tk]].astype(np.int32).view(np.uint32)
             nd[:, 3] = code[rc[tk]].astype(np.int32).view(np.uint32)
+            if inline_leaves and H == 0:
+                pay = np.zeros(n, dtype=np.uint32)
+                ok = np.zeros(n, dtype=bool)
+                if P == 1:
+                    pay[lk] = vals[:, 0].astype(np.float32).view(np.uint32)
+                    ok[lk] = True
+                else:  # unit one-hot votes: the class index
+                    one = (np.count_nonzero(vals, axis=1) == 1) & (vals.max(axis=1) == 1.0)
+                    pay[lk[one]] = np.argmax(vals[one], axis=1).astype(np.uint32)
+                    ok[lk[one]] = True
+                for col, child, bit in ((2, lc[tk], INLINE_LEFT_BIT), (3, rc[tk], INLINE_RIGHT_BIT)):
+                    m = ok[child]
+                    nd[m, col] = pay[child[m]]
+                    nd[m, 1] |= np.uint32(1 << bit)
             tails.append(nd)
         roots[ti] = code[0]  # POINTER layout entry (the HYBRID walk starts in the head)
         if H:

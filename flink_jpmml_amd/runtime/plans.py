@@ -1163,6 +1163,7 @@ VAR_POINTER_USKIP = 256
 VAR_POINTER_PEEL = 512
 VAR_POINTER_RANK3 = 1024
 VAR_POINTER_LDS = 2048  # compact slots walked out of LDS chunks (tree_lds.hip); host-side flag only
+VAR_POINTER_INLINE = 4096  # lock-step pointer walk, leaf payloads inline in the parent nodes
 DYN_B, DYN_SLOTS = 8, 16  # csrc: MODE_SUM trees per claimed batch, batch slots per chunk
 
 
@@ -1319,8 +1320,12 @@ class TreePlan(DevicePlan):
                  tree_shard: Optional[Tuple[int, int]] = None, head_depth: int = 0,
                  pointer_schedule: str = "lockstep", node_order: str = "bfs", node_format: str = "wide",
                  pointer_ilp: int = 8, xcd_split: str = "off", pointer_load: str = "clamped",
-                 hybrid_tail: str = "compact"):
-        """``pointer_load`` (pointer lock-step kernel, features in LDS): ``"clamped"`` (finished walks
+                 hybrid_tail: str = "compact", pointer_leaf: str = "table"):
+        """``pointer_leaf`` (lock-step pointer walk): ``"table"`` (a walk ends on a ``~leaf`` code and
+        gathers the leaf payload) or ``"inline"`` (leaf payloads of sum ensembles and unit votes sit
+        in the parent node's child field: no leaf gather, ``VAR_POINTER_INLINE``).
+
+        ``pointer_load`` (pointer lock-step kernel, features in LDS): ``"clamped"`` (finished walks
         re-load node 0, no branch), ``"masked"`` (their loads are exec-masked off) or ``"uskip"``
         (a walk slot finished in every lane of the wave issues no load at all: wave-uniform branch)
         or ``"peel"`` (the top two levels from wave-uniform scalar loads + a per-lane select).
@@ -1374,6 +1379,8 @@ class TreePlan(DevicePlan):
             raise ValueError("pointer_load must be 'clamped', 'masked', 'uskip' or 'peel'")
         if hybrid_tail not in ("compact", "wide"):
             raise ValueError("hybrid_tail must be 'compact' or 'wide'")
+        if pointer_leaf not in ("table", "inline"):
+            raise ValueError("pointer_leaf must be 'table' or 'inline'")
         self.tail_format = 0
         if xcd_split not in ("on", "off"):
             raise ValueError("xcd_split must be 'on' or 'off'")
@@ -1627,9 +1634,15 @@ class TreePlan(DevicePlan):
                     self._lds_chunks(nodes, roots, F, spec)
             elif node_format == "compact":
                 raise NotLowerable("compact pointer layout needs features in LDS, lock-step, bfs")
+            inline = False
             if heads is None and not compact and not superl and not rank3:
+                # inline leaf payloads on the default lock-step walk (sums, or unit votes) unless
+                # asked for the leaf table (pointer_leaf="table")
+                inline = (pointer_leaf == "inline" and self.layout == "pointer" and pointer_schedule == "lockstep"
+                          and pointer_load == "clamped" and pointer_ilp == 8
+                          and ((spec.P == 1 and spec.slots is None) or spec.P > 1))
                 _, nodes, leaves, roots, has_dr = pack_trees(spec.trees, spec.weights, spec.P, 0, feat_lds,
-                                                             order=node_order)
+                                                             order=node_order, inline_leaves=inline)
             self.blob_nan, self.chunk_trees_nan = None, 0
             self.head_depth = H
             self.rec_words = head_words(H) if H else 0
@@ -1650,6 +1663,8 @@ class TreePlan(DevicePlan):
                 self.variant = VAR_POINTER_PEEL  # top two levels from wave-uniform scalar loads
             elif pointer_load == "uskip" and self.layout == "pointer" and self.variant == 0 and feat_lds:
                 self.variant = VAR_POINTER_USKIP  # slots finished in the whole wave issue no load
+            elif inline and self.variant == 0:
+                self.variant = VAR_POINTER_INLINE  # leaf payloads inline: no leaf gather
             self.blob = self._t(nodes.reshape(-1).view(np.int32))
             self.leaves = self._t(leaves.reshape(-1))
             self.roots = self._t(roots)

@@ -14,6 +14,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 CONFIGS = {
     "pointer": dict(layout="pointer", xcd_split="off"),
+    "pointer_inline": dict(layout="pointer", xcd_split="off", pointer_leaf="inline"),
+    "pointer_inline+xcd": dict(layout="pointer", xcd_split="on", pointer_leaf="inline"),
     "pointer+xcd": dict(layout="pointer", xcd_split="on"),
     "pointer+masked": dict(layout="pointer", pointer_load="masked"),
     "super": dict(layout="pointer", node_format="super"),
