@@ -410,8 +410,12 @@ struct Call {
             PyErr_SetString(PyExc_ValueError, "tree walk: output / leaf-value / weight shape mismatch");
             return false;
         }
-        return validate();
+        // a program compiled by forest_compile was validated then (same buffers, same k): the
+        // per-call check of every node would cost more than scoring one row
+        return cache_matches() || validate();
     }
+
+    bool cache_matches() const;
 
     // Every index the walk can follow stays inside its array (a malformed program raises here
     // instead of reading out of bounds).
@@ -552,8 +556,8 @@ void compile_all(const Call &c, Fixed &f) {
 // The fingerprint ties the tables to the exact program buffers they were built from.
 struct Cached {
     Fixed f;
-    const void *ni, *kids, *pi, *roots;
-    Py_ssize_t n_nodes, T, k;
+    const void *ni, *kids, *pi, *roots, *modes, *nd, *pd, *ai, *ad;
+    Py_ssize_t n_nodes, T, k, n_kids, n_preds, n_ai, n_ad;
 };
 constexpr const char *CAPSULE = "fja.forest_program";
 
@@ -563,10 +567,15 @@ const Fixed *cached_fixed(const Call &c) {
     if (c.cache == nullptr || c.cache == Py_None || !PyCapsule_IsValid(c.cache, CAPSULE)) return nullptr;
     const Cached *h = static_cast<const Cached *>(PyCapsule_GetPointer(c.cache, CAPSULE));
     if (h == nullptr || h->ni != c.ni.b.buf || h->kids != c.kids.b.buf || h->pi != c.pi.b.buf ||
-        h->roots != c.roots.b.buf || h->n_nodes != c.prog.n_nodes || h->T != c.T || h->k != c.k)
-        return nullptr;  // not this program: the caller compiles afresh
+        h->roots != c.roots.b.buf || h->n_nodes != c.prog.n_nodes || h->T != c.T || h->k != c.k ||
+        h->n_kids != c.prog.n_kids || h->n_preds != c.prog.n_preds || h->n_ai != c.prog.n_ai ||
+        h->n_ad != c.prog.n_ad || h->modes != c.modes.b.buf || h->nd != c.nd.b.buf || h->pd != c.pd.b.buf ||
+        h->ai != c.ai.b.buf || h->ad != c.ad.b.buf)
+        return nullptr;  // not this program: the caller validates and compiles afresh
     return &h->f;
 }
+
+bool Call::cache_matches() const { return cached_fixed(*this) != nullptr; }
 
 constexpr int G = 16;
 
@@ -676,6 +685,10 @@ void run_block(const Call &c, const Fixed &f, const double *X, Py_ssize_t r0, Py
             for (; r + G <= r1; r += G) {
                 walk_perfect<G>(pt, pm, pl, f.depth[t], X, k, r, node);
                 for (int j = 0; j < G; ++j) emit(t, r + j, node[j]);
+            }
+            for (; r < r1; ++r) {  // the block's tail (and single-record calls): one row at a time
+                walk_perfect<1>(pt, pm, pl, f.depth[t], X, k, r, node);
+                emit(t, r, node[0]);
             }
         } else if (f.depth[t] >= 0) {
             for (; r + G <= r1; r += G) {
@@ -826,9 +839,10 @@ PyObject *forest_sums(PyObject *, PyObject *args) {
     double *out = static_cast<double *>(c.out.b.buf);
     const Py_ssize_t n = c.n, T = c.T;
     const bool avx = use_avx512(c);
-    std::vector<double> buf;  // one ROW_BLOCK x T slab per worker
+    std::vector<double> buf;  // one ROW_BLOCK x T slab per worker (rows of one block at most)
+    const size_t slab_rows = static_cast<size_t>(n < ROW_BLOCK ? (n > 0 ? n : 1) : ROW_BLOCK);
     try {
-        buf.resize(static_cast<size_t>(ROW_BLOCK) * static_cast<size_t>(T) * static_cast<size_t>(walk_threads()));
+        buf.resize(slab_rows * static_cast<size_t>(T) * static_cast<size_t>(walk_threads()));
     } catch (const std::bad_alloc &) {
         return PyErr_NoMemory();
     }
@@ -838,7 +852,7 @@ PyObject *forest_sums(PyObject *, PyObject *args) {
     if (fc == nullptr) compile_all(c, local);
     const Fixed &f = fc ? *fc : local;
     for_blocks(n, [&](Py_ssize_t r0, Py_ssize_t r1, int worker) {
-        double *bb = buf.data() + static_cast<size_t>(worker) * ROW_BLOCK * static_cast<size_t>(T);
+        double *bb = buf.data() + static_cast<size_t>(worker) * slab_rows * static_cast<size_t>(T);
         run_block(c, f, X, r0, r1, avx, [&](Py_ssize_t t, Py_ssize_t r, int32_t g) {
             const double v = g < 0 ? NAN : lv[g];
             bb[(r - r0) * T + t] = w ? v * w[t] : v;
@@ -879,9 +893,18 @@ PyObject *forest_compile(PyObject *, PyObject *args) {
     h->kids = c.kids.b.buf;
     h->pi = c.pi.b.buf;
     h->roots = c.roots.b.buf;
+    h->modes = c.modes.b.buf;
+    h->nd = c.nd.b.buf;
+    h->pd = c.pd.b.buf;
+    h->ai = c.ai.b.buf;
+    h->ad = c.ad.b.buf;
     h->n_nodes = c.prog.n_nodes;
     h->T = c.T;
     h->k = c.k;
+    h->n_kids = c.prog.n_kids;
+    h->n_preds = c.prog.n_preds;
+    h->n_ai = c.prog.n_ai;
+    h->n_ad = c.prog.n_ad;
     PyObject *cap = PyCapsule_New(h, CAPSULE, drop_cached);
     if (cap == nullptr) delete h;
     return cap;
