@@ -224,7 +224,11 @@ class FieldSchema:
         """
         X = np.array(X, dtype=np.float64, copy=True)
         valid = np.ones(X.shape[0], dtype=bool)
-        for j, name in enumerate(names):
+        float_cols, general = self._prep_plan(names, mfs)
+        if len(float_cols):
+            # fields with no preparation besides the float data type's rounding, in one op
+            X[:, float_cols] = X[:, float_cols].astype(np.float32).astype(np.float64)
+        for j, name in general:
             col = X[:, j]
             mf = mfs.get(name)
             df = self.data_fields.get(name)
@@ -291,6 +295,34 @@ class FieldSchema:
             else:
                 X[:, j] = col
         return X, valid
+
+    def _prep_plan(self, names: List[str], mfs: Dict[str, ir.MiningField]) -> tuple:
+        """Split ``names`` into the columns :meth:`prepare_matrix` leaves as they are (at most a
+        float32 rounding) and the ones that need the per-field treatment; cached per name list
+        and MiningField map, so per-record calls skip the per-field checks."""
+        cache = self.__dict__.setdefault("_prep_plans", {})
+        key = tuple(names)
+        hit = cache.get(key)
+        if hit is not None and hit[0] is mfs:
+            return hit[1], hit[2]
+        float_cols, general = [], []
+        for j, name in enumerate(names):
+            mf = mfs.get(name)
+            df = self.data_fields.get(name)
+            optype = (mf.optype if mf is not None and mf.optype else None) or (df.optype if df else "continuous")
+            trivial = (
+                (mf is None or (mf.missing_value_replacement is None
+                                and (optype != "continuous" or mf.outliers not in ("asMissingValues", "asExtremeValues"))))
+                and (df is None or (not df.missing_values and not df.invalid_values and not df.intervals
+                                    and not (df.values and optype != "continuous")
+                                    and df.data_type != "integer")))
+            if not trivial:
+                general.append((j, name))
+            elif df is not None and df.data_type == "float":
+                float_cols.append(j)
+        plan = (np.asarray(float_cols, dtype=np.intp), general)
+        cache[key] = (mfs,) + plan
+        return plan
 
 
 def _in_value_list(df: ir.DataField, raw: Any, values: List[str]) -> bool:
