@@ -631,9 +631,43 @@ __attribute__((target("avx512f,avx512vl"))) void walk_perfect_avx512(const doubl
     }
     const double *Xb = X + r0 * k;
     for (int d = 0; d < D; ++d) {
+        // Levels of at most 32 nodes live in registers: every lane's node is a permute of the
+        // level's thresholds / metadata (no gather); deeper levels gather from the tables.
+        const int W = 1 << d, base = W - 1;
+        const bool regs = W <= 32;
+        __m512d T0 = _mm512_setzero_pd(), T1 = T0, T2 = T0, T3 = T0;
+        __m512i M0 = _mm512_setzero_si512(), M1 = M0;
+        if (regs) {
+            T0 = _mm512_maskz_loadu_pd(static_cast<__mmask8>(W >= 8 ? 0xFF : (1u << W) - 1), pt + base);
+            M0 = _mm512_maskz_loadu_epi32(static_cast<__mmask16>(W >= 16 ? 0xFFFF : (1u << W) - 1), pm + base);
+            if (W >= 16) T1 = _mm512_loadu_pd(pt + base + 8);
+            if (W == 32) {
+                T2 = _mm512_loadu_pd(pt + base + 16);
+                T3 = _mm512_loadu_pd(pt + base + 24);
+                M1 = _mm512_loadu_si512(pm + base + 16);
+            }
+        }
+        const __m256i vbase = _mm256_set1_epi32(base);
         for (int v = 0; v < V; ++v) {
-            const __m256i m = _mm256_i32gather_epi32(pm, s[v], 4);
-            const __m512d t = _mm512_i32gather_pd(s[v], pt, 8);
+            __m256i m;
+            __m512d t;
+            if (regs) {
+                const __m256i li = _mm256_sub_epi32(s[v], vbase);  // index within the level
+                const __m512i li512 = _mm512_castsi256_si512(li);
+                const __m512i li64 = _mm512_cvtepi32_epi64(li);
+                if (W <= 16) {
+                    m = _mm512_castsi512_si256(_mm512_permutexvar_epi32(li512, M0));
+                    t = W <= 8 ? _mm512_permutexvar_pd(li64, T0) : _mm512_permutex2var_pd(T0, li64, T1);
+                } else {
+                    m = _mm512_castsi512_si256(_mm512_permutex2var_epi32(M0, li512, M1));
+                    const __mmask8 hi = _mm256_test_epi32_mask(li, _mm256_set1_epi32(16));
+                    t = _mm512_mask_blend_pd(hi, _mm512_permutex2var_pd(T0, li64, T1),
+                                             _mm512_permutex2var_pd(T2, li64, T3));
+                }
+            } else {
+                m = _mm256_i32gather_epi32(pm, s[v], 4);
+                t = _mm512_i32gather_pd(s[v], pt, 8);
+            }
             const __m256i xi = _mm256_add_epi32(rowoff[v], _mm256_and_si256(m, fmask));
             const __m512d x = _mm512_i32gather_pd(xi, Xb, 8);
             const __mmask8 lt = _mm512_cmp_pd_mask(x, t, _CMP_LT_OQ);

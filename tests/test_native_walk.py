@@ -179,10 +179,11 @@ def test_forest_aggregate_is_bit_identical_to_numpy(method, seed):
     assert np.array_equal(s1[v1], s2[v2])  # bit-identical, not approximately equal
 
 
-def test_scalar_and_avx512_walks_agree(monkeypatch):
+@pytest.mark.parametrize("seed", [0, 2, 4])  # depths 3, 5, 7: register levels (<= 32 nodes) and gathers
+def test_scalar_and_avx512_walks_agree(monkeypatch, seed):
     from flink_jpmml_amd.bench import synth
 
-    c = CompiledPmml.from_string(_gbdt_doc(4, n_trees=64))
+    c = CompiledPmml.from_string(_gbdt_doc(seed, n_trees=64))
     prog = c.evaluator.native_forest()
     X = np.ascontiguousarray(synth.stream_matrix(3001, 8, seed=9, missing_rate=0.1))
     fast = prog.leaves(X)
