@@ -1035,7 +1035,8 @@ PMML_API int pmml_tree_launch(hipStream_t stream, const TreeArgs* args, int layo
   } else {
     if (a.variant != 0 && a.variant != VAR_POINTER_REFILL && a.variant != VAR_POINTER_COMPACT &&
         a.variant != VAR_POINTER_MASKED && a.variant != VAR_POINTER_SUPER && a.variant != VAR_POINTER_USKIP &&
-        a.variant != VAR_POINTER_PEEL && a.variant != VAR_POINTER_RANK3)
+        a.variant != VAR_POINTER_PEEL && a.variant != VAR_POINTER_RANK3 &&
+        a.variant != VAR_POINTER_INLINE)
       return -10;
     const bool feat_lds = a.n_feat <= 64;
     size_t lds = (feat_lds ? (size_t)a.n_feat * TB * 4 : 0) + TB * 4 + acc_lds;
