@@ -17,10 +17,14 @@ t = time.perf_counter()
 c.score_matrix_oracle(X)
 batch = len(X) / (time.perf_counter() - t)
 m = PmmlModel.from_string(doc)
+m.predict_batch(X[:64])
+t = time.perf_counter()
+m.predict_batch(X)
+pbatch = len(X) / (time.perf_counter() - t)
 vecs = [DenseVector(r) for r in X[:300]]
 m.predict(vecs[0])
 t = time.perf_counter()
 for v in vecs:
     m.predict(v)
 rec = len(vecs) / (time.perf_counter() - t)
-print(json.dumps({"host_batch_records_per_s": batch, "host_per_record_predict_per_s": rec, "trees": 1000, "depth": 6}))
+print(json.dumps({"host_batch_records_per_s": batch, "host_per_record_predict_per_s": rec, "host_predict_batch_per_s": pbatch, "trees": 1000, "depth": 6}))
