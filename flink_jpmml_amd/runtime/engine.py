@@ -32,6 +32,7 @@ from __future__ import annotations
 
 import collections
 import logging
+import threading
 import time
 from dataclasses import dataclass
 from typing import Tuple, List, Optional
@@ -200,6 +201,7 @@ class StreamingScorer:
         self._inflight: "collections.deque" = collections.deque()
         self.rows_submitted = 0
         self._row_state = None  # score_row's persistent buffers
+        self._row_lock = threading.Lock()  # ...shared by every caller of score_row
         from ..ops import _lib
 
         self._lib = _lib.load()
@@ -458,6 +460,10 @@ class StreamingScorer:
         whatever batches are queued there), the scores written straight into host-mapped memory
         when the plan's epilogue can (else one D2H copy), one stream sync — no per-call tensor
         allocation. Same kernels and row semantics as a 1-row :meth:`submit_batch`."""
+        with self._row_lock:  # one set of staging buffers: concurrent callers take turns
+            return self._score_row(x)
+
+    def _score_row(self, x: np.ndarray) -> Tuple[float, bool]:
         import torch
 
         from ..ops._lib import check

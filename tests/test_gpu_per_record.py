@@ -83,3 +83,23 @@ def test_per_record_device_predict_matches_host_contract(gpu, fixtures_dir):
                     assert abs(a.value.value - b.value.value) <= 1e-4 * max(1.0, abs(a.value.value)), (name, v)
         checked += 1
     assert checked >= 3
+
+
+def test_per_record_device_predict_from_several_threads(gpu, tmp_path):
+    """``score_row`` keeps one set of staging buffers per scorer; callers on several threads take
+    turns, so every thread gets its own record's score."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from flink_jpmml_amd import DenseVector
+    from flink_jpmml_amd.api.pmml_model import PmmlModel
+    from flink_jpmml_amd.bench.synth import gbdt_pmml, stream_matrix
+    from flink_jpmml_amd.config import ScoringConfig
+
+    doc = gbdt_pmml(n_trees=50, depth=5, n_features=16, seed=3)
+    m = PmmlModel.from_string(doc).bind(gpu, ScoringConfig(device=gpu, fallback="error"))
+    assert m.on_device
+    X = stream_matrix(400, 16, seed=8, missing_rate=0.05).astype(np.float64)
+    seq = [m.predict(DenseVector(r)).value.get_or_else(float("nan")) for r in X]
+    with ThreadPoolExecutor(4) as ex:
+        par = list(ex.map(lambda r: m.predict(DenseVector(r)).value.get_or_else(float("nan")), X))
+    np.testing.assert_array_equal(np.array(par), np.array(seq))
