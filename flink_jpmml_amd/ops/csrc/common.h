@@ -195,3 +195,44 @@ __device__ __forceinline__ void stage_rows_T(const float* __restrict__ X, int n_
   }
   __syncthreads();
 }
+
+// stage_rows_T where thread t stages ITS OWN row t (same loads and values as stage_rows_T's
+// aligned path; unaligned rows are read a column at a time) and returns the row's rejected flag in
+// a register: no bad[TB] array, so a kernel's LDS is the feature planes alone — 32 features x 256
+// rows = exactly 32 KiB, five workgroups per CU instead of four. Ends with a barrier.
+template <int TB>
+__device__ __forceinline__ bool stage_rows_own(const float* __restrict__ X, int n_rows, int F, int ldx,
+                                               const FieldPrep* __restrict__ prep, float* __restrict__ feat, int row0) {
+  const int r = threadIdx.x;
+  const int row = row0 + r;
+  const bool in = row < n_rows;
+  bool b = false;
+  if ((ldx & 3) == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0) {
+    const int F4 = (F + 3) >> 2;
+    for (int fq = 0; fq < F4; ++fq) {
+      float4 v = make_float4(__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""));
+      if (in) v = *reinterpret_cast<const float4*>(X + (size_t)row * ldx + 4 * fq);
+      const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int f = 4 * fq + k;
+        if (f < F) {
+          float x = vv[k];
+          if (in && prep) x = prep_value(x, prep[f], &b);
+          feat[f * TB + r] = x;
+        }
+      }
+    }
+  } else {
+    for (int f = 0; f < F; ++f) {
+      float x = __builtin_nanf("");
+      if (in) {
+        x = X[(size_t)row * ldx + f];
+        if (prep) x = prep_value(x, prep[f], &b);
+      }
+      feat[f * TB + r] = x;
+    }
+  }
+  __syncthreads();
+  return b;
+}

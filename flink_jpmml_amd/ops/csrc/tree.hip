@@ -24,22 +24,18 @@ namespace {
 template <bool GENERAL, bool FEAT_LDS, int PILP = 8, bool MASKED = false, bool USKIP = false, bool PEEL = false,
           bool INL = false>
 __device__ __forceinline__ void pointer_walk(const TreeArgs& a) {
+  // LDS: the feature planes, then (GENERAL) the class accumulators — no bad[] array: each thread
+  // stages its own row and keeps the row's verdict in a register (POINTER_LDS_BYTES)
   extern __shared__ __align__(16) uint32_t smem[];
   float* feat = reinterpret_cast<float*>(smem);
-  int* bad = reinterpret_cast<int*>(smem + (FEAT_LDS ? a.n_feat * TB : 0));
-  float* accl = reinterpret_cast<float*>(bad + TB);
+  float* accl = reinterpret_cast<float*>(smem + (FEAT_LDS ? a.n_feat * TB : 0));
   const int tid = threadIdx.x;
   const int2 blk = tree_block(a);
   const int row0 = blk.x * TB;
   const int split = blk.y;
   const int row = row0 + tid;
-  if (FEAT_LDS) {
-    stage_rows_T<TB>(a.X, a.n_rows, a.n_feat, a.ldx, a.prep, feat, bad, row0);
-  } else {
-    bad[tid] = 0;
-    __syncthreads();
-  }
-  bool row_ok = bad[tid] == 0;
+  bool row_ok = true;
+  if (FEAT_LDS) row_ok = !stage_rows_own<TB>(a.X, a.n_rows, a.n_feat, a.ldx, a.prep, feat, row0);
   // global-feature mode: apply preparation lazily per read
   const float* xrow = a.X + (size_t)min(row, a.n_rows - 1) * a.ldx;
   if (!FEAT_LDS && a.prep && row < a.n_rows) {
@@ -1040,6 +1036,8 @@ PMML_API int pmml_tree_launch(hipStream_t stream, const TreeArgs* args, int layo
       return -10;
     const bool feat_lds = a.n_feat <= 64;
     size_t lds = (feat_lds ? (size_t)a.n_feat * TB * 4 : 0) + TB * 4 + acc_lds;
+    // pointer_walk kernels (PEEL / USKIP / INLINE / default): feature planes + accumulators only
+    const size_t lds_pw = (feat_lds ? (size_t)a.n_feat * TB * 4 : 0) + acc_lds;
     if (a.variant == VAR_POINTER_RANK3) {
       if (a.n_feat > 32 || !a.rank_thr || !a.rank_cnt || a.rank_stride < 1 || a.rank_stride > 254) return -4;
       // (ranks replace the feature planes; the threshold tables are read from global memory)
@@ -1105,76 +1103,76 @@ PMML_API int pmml_tree_launch(hipStream_t stream, const TreeArgs* args, int layo
       }
     } else if (a.variant == VAR_POINTER_PEEL && feat_lds) {
       if (a.general) {
-        err = prepare_launch(tree_pointer_kernel<true, true, 8, false, false, true>, lds);
-        if (!err) hipLaunchKernelGGL((tree_pointer_kernel<true, true, 8, false, false, true>), grid, dim3(TB), lds, stream, a);
+        err = prepare_launch(tree_pointer_kernel<true, true, 8, false, false, true>, lds_pw);
+        if (!err) hipLaunchKernelGGL((tree_pointer_kernel<true, true, 8, false, false, true>), grid, dim3(TB), lds_pw, stream, a);
       } else {
-        err = prepare_launch(tree_pointer_kernel<false, true, 8, false, false, true>, lds);
-        if (!err) hipLaunchKernelGGL((tree_pointer_kernel<false, true, 8, false, false, true>), grid, dim3(TB), lds, stream, a);
+        err = prepare_launch(tree_pointer_kernel<false, true, 8, false, false, true>, lds_pw);
+        if (!err) hipLaunchKernelGGL((tree_pointer_kernel<false, true, 8, false, false, true>), grid, dim3(TB), lds_pw, stream, a);
       }
     } else if (a.variant == VAR_POINTER_USKIP && feat_lds) {
       if (a.general) {
-        err = prepare_launch(tree_pointer_kernel<true, true, 8, false, true>, lds);
-        if (!err) hipLaunchKernelGGL((tree_pointer_kernel<true, true, 8, false, true>), grid, dim3(TB), lds, stream, a);
+        err = prepare_launch(tree_pointer_kernel<true, true, 8, false, true>, lds_pw);
+        if (!err) hipLaunchKernelGGL((tree_pointer_kernel<true, true, 8, false, true>), grid, dim3(TB), lds_pw, stream, a);
       } else if (a.pilp == 4) {
-        err = prepare_launch(tree_pointer_kernel<false, true, 4, false, true>, lds);
-        if (!err) hipLaunchKernelGGL((tree_pointer_kernel<false, true, 4, false, true>), grid, dim3(TB), lds, stream, a);
+        err = prepare_launch(tree_pointer_kernel<false, true, 4, false, true>, lds_pw);
+        if (!err) hipLaunchKernelGGL((tree_pointer_kernel<false, true, 4, false, true>), grid, dim3(TB), lds_pw, stream, a);
       } else if (a.pilp == 16) {
-        err = prepare_launch(tree_pointer_kernel<false, true, 16, false, true>, lds);
-        if (!err) hipLaunchKernelGGL((tree_pointer_kernel<false, true, 16, false, true>), grid, dim3(TB), lds, stream, a);
+        err = prepare_launch(tree_pointer_kernel<false, true, 16, false, true>, lds_pw);
+        if (!err) hipLaunchKernelGGL((tree_pointer_kernel<false, true, 16, false, true>), grid, dim3(TB), lds_pw, stream, a);
       } else {
-        err = prepare_launch(tree_pointer_kernel<false, true, 8, false, true>, lds);
-        if (!err) hipLaunchKernelGGL((tree_pointer_kernel<false, true, 8, false, true>), grid, dim3(TB), lds, stream, a);
+        err = prepare_launch(tree_pointer_kernel<false, true, 8, false, true>, lds_pw);
+        if (!err) hipLaunchKernelGGL((tree_pointer_kernel<false, true, 8, false, true>), grid, dim3(TB), lds_pw, stream, a);
       }
     } else if (a.variant == VAR_POINTER_INLINE) {
       if (feat_lds && a.general) {
-        err = prepare_launch(tree_pointer_kernel<true, true, 8, false, false, false, true>, lds);
+        err = prepare_launch(tree_pointer_kernel<true, true, 8, false, false, false, true>, lds_pw);
         if (!err)
-          hipLaunchKernelGGL((tree_pointer_kernel<true, true, 8, false, false, false, true>), grid, dim3(TB), lds, stream, a);
+          hipLaunchKernelGGL((tree_pointer_kernel<true, true, 8, false, false, false, true>), grid, dim3(TB), lds_pw, stream, a);
       } else if (feat_lds) {
-        err = prepare_launch(tree_pointer_kernel<false, true, 8, false, false, false, true>, lds);
+        err = prepare_launch(tree_pointer_kernel<false, true, 8, false, false, false, true>, lds_pw);
         if (!err)
-          hipLaunchKernelGGL((tree_pointer_kernel<false, true, 8, false, false, false, true>), grid, dim3(TB), lds, stream, a);
+          hipLaunchKernelGGL((tree_pointer_kernel<false, true, 8, false, false, false, true>), grid, dim3(TB), lds_pw, stream, a);
       } else if (a.general) {
-        err = prepare_launch(tree_pointer_kernel<true, false, 8, false, false, false, true>, lds);
+        err = prepare_launch(tree_pointer_kernel<true, false, 8, false, false, false, true>, lds_pw);
         if (!err)
-          hipLaunchKernelGGL((tree_pointer_kernel<true, false, 8, false, false, false, true>), grid, dim3(TB), lds, stream, a);
+          hipLaunchKernelGGL((tree_pointer_kernel<true, false, 8, false, false, false, true>), grid, dim3(TB), lds_pw, stream, a);
       } else {
-        err = prepare_launch(tree_pointer_kernel<false, false, 8, false, false, false, true>, lds);
+        err = prepare_launch(tree_pointer_kernel<false, false, 8, false, false, false, true>, lds_pw);
         if (!err)
-          hipLaunchKernelGGL((tree_pointer_kernel<false, false, 8, false, false, false, true>), grid, dim3(TB), lds, stream, a);
+          hipLaunchKernelGGL((tree_pointer_kernel<false, false, 8, false, false, false, true>), grid, dim3(TB), lds_pw, stream, a);
       }
     } else if (a.variant == VAR_POINTER_USKIP || a.variant == VAR_POINTER_PEEL) {
       return -4;  // features in LDS only
     } else if (a.general) {
       if (feat_lds && (a.variant & VAR_POINTER_MASKED)) {
-        err = prepare_launch(tree_pointer_kernel<true, true, 8, true>, lds);
-        if (!err) hipLaunchKernelGGL((tree_pointer_kernel<true, true, 8, true>), grid, dim3(TB), lds, stream, a);
+        err = prepare_launch(tree_pointer_kernel<true, true, 8, true>, lds_pw);
+        if (!err) hipLaunchKernelGGL((tree_pointer_kernel<true, true, 8, true>), grid, dim3(TB), lds_pw, stream, a);
       } else if (feat_lds) {
-        err = prepare_launch(tree_pointer_kernel<true, true>, lds);
-        if (!err) hipLaunchKernelGGL((tree_pointer_kernel<true, true>), grid, dim3(TB), lds, stream, a);
+        err = prepare_launch(tree_pointer_kernel<true, true>, lds_pw);
+        if (!err) hipLaunchKernelGGL((tree_pointer_kernel<true, true>), grid, dim3(TB), lds_pw, stream, a);
       } else {
-        err = prepare_launch(tree_pointer_kernel<true, false>, lds);
-        if (!err) hipLaunchKernelGGL((tree_pointer_kernel<true, false>), grid, dim3(TB), lds, stream, a);
+        err = prepare_launch(tree_pointer_kernel<true, false>, lds_pw);
+        if (!err) hipLaunchKernelGGL((tree_pointer_kernel<true, false>), grid, dim3(TB), lds_pw, stream, a);
       }
     } else {
       if (feat_lds && a.pilp == 2) {
-        err = prepare_launch(tree_pointer_kernel<false, true, 2>, lds);
-        if (!err) hipLaunchKernelGGL((tree_pointer_kernel<false, true, 2>), grid, dim3(TB), lds, stream, a);
+        err = prepare_launch(tree_pointer_kernel<false, true, 2>, lds_pw);
+        if (!err) hipLaunchKernelGGL((tree_pointer_kernel<false, true, 2>), grid, dim3(TB), lds_pw, stream, a);
       } else if (feat_lds && (a.variant & VAR_POINTER_MASKED)) {
-        err = prepare_launch(tree_pointer_kernel<false, true, 8, true>, lds);
-        if (!err) hipLaunchKernelGGL((tree_pointer_kernel<false, true, 8, true>), grid, dim3(TB), lds, stream, a);
+        err = prepare_launch(tree_pointer_kernel<false, true, 8, true>, lds_pw);
+        if (!err) hipLaunchKernelGGL((tree_pointer_kernel<false, true, 8, true>), grid, dim3(TB), lds_pw, stream, a);
       } else if (feat_lds && a.pilp == 16) {
-        err = prepare_launch(tree_pointer_kernel<false, true, 16>, lds);
-        if (!err) hipLaunchKernelGGL((tree_pointer_kernel<false, true, 16>), grid, dim3(TB), lds, stream, a);
+        err = prepare_launch(tree_pointer_kernel<false, true, 16>, lds_pw);
+        if (!err) hipLaunchKernelGGL((tree_pointer_kernel<false, true, 16>), grid, dim3(TB), lds_pw, stream, a);
       } else if (feat_lds && a.pilp == 4) {
-        err = prepare_launch(tree_pointer_kernel<false, true, 4>, lds);
-        if (!err) hipLaunchKernelGGL((tree_pointer_kernel<false, true, 4>), grid, dim3(TB), lds, stream, a);
+        err = prepare_launch(tree_pointer_kernel<false, true, 4>, lds_pw);
+        if (!err) hipLaunchKernelGGL((tree_pointer_kernel<false, true, 4>), grid, dim3(TB), lds_pw, stream, a);
       } else if (feat_lds) {
-        err = prepare_launch(tree_pointer_kernel<false, true>, lds);
-        if (!err) hipLaunchKernelGGL((tree_pointer_kernel<false, true>), grid, dim3(TB), lds, stream, a);
+        err = prepare_launch(tree_pointer_kernel<false, true>, lds_pw);
+        if (!err) hipLaunchKernelGGL((tree_pointer_kernel<false, true>), grid, dim3(TB), lds_pw, stream, a);
       } else {
-        err = prepare_launch(tree_pointer_kernel<false, false>, lds);
-        if (!err) hipLaunchKernelGGL((tree_pointer_kernel<false, false>), grid, dim3(TB), lds, stream, a);
+        err = prepare_launch(tree_pointer_kernel<false, false>, lds_pw);
+        if (!err) hipLaunchKernelGGL((tree_pointer_kernel<false, false>), grid, dim3(TB), lds_pw, stream, a);
       }
     }
   }

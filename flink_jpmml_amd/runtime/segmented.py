@@ -34,7 +34,8 @@ import numpy as np
 
 from ..models.mining import MiningEvaluator
 from ..pmml import ir
-from .plans import (VAR_POINTER_COMPACT, VAR_POINTER_REFILL, VAR_POINTER_SUPER, DevicePlan, NotLowerable, _label_table,
+from .plans import (VAR_POINTER_COMPACT, VAR_POINTER_INLINE, VAR_POINTER_LDS, VAR_POINTER_RANK3, VAR_POINTER_REFILL,
+                    VAR_POINTER_SUPER, DevicePlan, NotLowerable, _label_table,
                     apply_target_torch, target_post)
 
 REGRESSION_METHODS = ("sum", "average", "weightedAverage", "max", "min", "median", "weightedMedian", "selectFirst")
@@ -354,11 +355,13 @@ class SegmentedPlan(DevicePlan):
         from .plans import TreePlan
 
         self._multi = []
-        # 16-byte BFS nodes only (the refill / compact / super formats have kernels of their own;
-        # the clamped, masked, uskip and peel loads of the same nodes are bit-identical walks)
+        # 16-byte BFS nodes only (the refill / compact / super / rank3 / LDS formats have kernels of
+        # their own and inline-leaf nodes a different child encoding; the clamped, masked, uskip and
+        # peel loads of the same nodes are bit-identical walks)
+        own = (VAR_POINTER_REFILL | VAR_POINTER_COMPACT | VAR_POINTER_SUPER | VAR_POINTER_RANK3 | VAR_POINTER_LDS
+               | VAR_POINTER_INLINE)
         members = [i for i, p in enumerate(self.subs)
-                   if isinstance(p, TreePlan) and p.layout == "pointer" and p.C <= 16 and
-                   (int(p.variant) & (VAR_POINTER_REFILL | VAR_POINTER_COMPACT | VAR_POINTER_SUPER)) == 0]
+                   if isinstance(p, TreePlan) and p.layout == "pointer" and p.C <= 16 and (int(p.variant) & own) == 0]
         if len(members) < 2:
             return
         for general in (0, 1):

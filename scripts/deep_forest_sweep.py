@@ -14,6 +14,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 CONFIGS = {
     "pointer": dict(layout="pointer", xcd_split="off"),
+    "pointer_clamped": dict(layout="pointer", xcd_split="off", pointer_load="clamped"),
     "pointer_inline": dict(layout="pointer", xcd_split="off", pointer_leaf="inline"),
     "pointer_inline+xcd": dict(layout="pointer", xcd_split="on", pointer_leaf="inline"),
     "pointer+xcd": dict(layout="pointer", xcd_split="on"),
