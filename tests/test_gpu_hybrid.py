@@ -152,6 +152,7 @@ def test_super_layout_votes_on_gpu(gpu):
 
 @pytest.mark.parametrize("opts", [dict(layout="pointer", pointer_load="uskip"),
                                   dict(layout="pointer", pointer_load="peel"),
+                                  dict(layout="pointer", pointer_load="peel3"),
                                   dict(layout="pointer", pointer_load="uskip", pointer_ilp=4),
                                   dict(layout="hybrid", hybrid_tail="wide", head_depth=2),
                                   dict(layout="hybrid", hybrid_tail="wide", head_depth=4, pointer_load="uskip"),
@@ -164,7 +165,7 @@ def test_uniform_skip_walks_on_gpu(gpu, opts, missing):
     tree-order leaf sums)."""
     c = _model("gbdt", n_trees=45, depth=14, n_features=24, seed=7, p_split=0.8, missing_strategy=missing)
     plan = c.plan(gpu, **opts)
-    ptr = c.plan(gpu, layout="pointer")
+    ptr = c.plan(gpu, layout="pointer", pointer_load="clamped")
     assert plan.layout == opts["layout"]
     X = _inputs(100_000, 24, 3, 0.03)
     s, v = _score(c, plan, X)
@@ -177,6 +178,7 @@ def test_uniform_skip_walks_on_gpu(gpu, opts, missing):
 
 @pytest.mark.parametrize("opts", [dict(layout="pointer", pointer_load="uskip"),
                                   dict(layout="pointer", pointer_load="peel"),
+                                  dict(layout="pointer", pointer_load="peel3"),
                                   dict(layout="hybrid", hybrid_tail="wide", head_depth=3)])
 def test_uniform_skip_votes_on_gpu(gpu, opts):
     """Random-forest votes (P = 3 class slots in LDS) on the uniform-skip walks."""
@@ -187,3 +189,20 @@ def test_uniform_skip_votes_on_gpu(gpu, opts):
     ref, vref = _oracle(c, X)
     assert (v == vref).all()
     np.testing.assert_array_equal(s[v], ref[v])
+
+
+@pytest.mark.parametrize("load", ["peel", "peel3"])
+@pytest.mark.parametrize("p_split", [0.35, 0.6])
+def test_peeled_walks_with_shallow_leaves_on_gpu(gpu, load, p_split):
+    """The peeled top levels when leaves sit at levels 0-2 (stumps, a leaf child of the root, fewer
+    than four level-2 nodes): bit-identical to the clamped walk, exact validity vs the oracle."""
+    c = _model("gbdt", n_trees=64, depth=12, n_features=16, seed=11, p_split=p_split,
+               missing_strategy="nullPrediction")
+    plan = c.plan(gpu, layout="pointer", pointer_load=load)
+    ptr = c.plan(gpu, layout="pointer", pointer_load="clamped")
+    X = _inputs(60_000, 16, 4, 0.03)
+    s, v = _score(c, plan, X)
+    s0, v0 = _score(c, ptr, X)
+    ref, vref = _oracle(c, X)
+    assert (v == vref).all()
+    assert (v == v0).all() and np.array_equal(s[v], s0[v0])
