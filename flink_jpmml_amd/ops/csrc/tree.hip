@@ -21,7 +21,7 @@ namespace {
 // the left child is a leaf, bit 28: the right one) -- the leaf value's fp32 bits for a sum
 // ensemble, the class index for an unweighted vote (GENERAL, one increment). The walk ends at the
 // parent with the payload in hand: no leaf gather (one per tree and row; P of them for votes).
-template <bool GENERAL, bool FEAT_LDS, int PILP = 8, bool MASKED = false, bool USKIP = false, int PEEL = 0,
+template <bool GENERAL, bool FEAT_LDS, int PILP = 8, bool MASKED = false, bool USKIP = false, bool PEEL = false,
           bool INL = false>
 __device__ __forceinline__ void pointer_walk(const TreeArgs& a) {
   // LDS: the feature planes, then (GENERAL) the class accumulators — no bad[] array: each thread
@@ -110,28 +110,6 @@ __device__ __forceinline__ void pointer_walk(const TreeArgs& a) {
         pz[i] = pz[i] || nulled;
         code[i] = act ? (nulled ? -1 : (right ? (int)nd.w : (int)nd.z)) : code[i];
       }
-      if (PEEL >= 3) {
-        // level 2: the (at most four) children of the two level-1 nodes, uniform loads; a lane's
-        // node is the one whose code it holds (equal codes are the same node)
-#pragma unroll
-        for (int i = 0; i < PILP; ++i) {
-          const int g[4] = {(int)nl[i].z, (int)nl[i].w, (int)nr[i].z, (int)nr[i].w};
-          uint4 ng[4];
-#pragma unroll
-          for (int k = 0; k < 4; ++k) ng[k] = nodes[max(__builtin_amdgcn_readfirstlane(g[k]), 0)];
-          uint4 nd = ng[3];
-          nd = code[i] == g[2] ? ng[2] : nd;
-          nd = code[i] == g[1] ? ng[1] : nd;
-          nd = code[i] == g[0] ? ng[0] : nd;
-          const bool act = code[i] >= 0;
-          const float x = *reinterpret_cast<const float*>(feat_lane + (nd.y & 0xFFFFu));
-          const bool isn = (x != x);
-          const bool nulled = act && isn && ((nd.y >> 30) & 1u);
-          const bool right = (x >= __uint_as_float(nd.x)) || (isn && (nd.y >> 31));
-          pz[i] = pz[i] || nulled;
-          code[i] = act ? (nulled ? -1 : (right ? (int)nd.w : (int)nd.z)) : code[i];
-        }
-      }
     }
     bool live = true;
     while (live) {
@@ -205,7 +183,7 @@ __device__ __forceinline__ void pointer_walk(const TreeArgs& a) {
   finish_row(a, acc, accl, split, GENERAL, row, row_ok && !poisoned);
 }
 
-template <bool GENERAL, bool FEAT_LDS, int PILP = 8, bool MASKED = false, bool USKIP = false, int PEEL = 0,
+template <bool GENERAL, bool FEAT_LDS, int PILP = 8, bool MASKED = false, bool USKIP = false, bool PEEL = false,
           bool INL = false>
 __global__ __launch_bounds__(TB, 2) void tree_pointer_kernel(TreeArgs a) {
   pointer_walk<GENERAL, FEAT_LDS, PILP, MASKED, USKIP, PEEL, INL>(a);
@@ -1054,7 +1032,7 @@ PMML_API int pmml_tree_launch(hipStream_t stream, const TreeArgs* args, int layo
     if (a.variant != 0 && a.variant != VAR_POINTER_REFILL && a.variant != VAR_POINTER_COMPACT &&
         a.variant != VAR_POINTER_MASKED && a.variant != VAR_POINTER_SUPER && a.variant != VAR_POINTER_USKIP &&
         a.variant != VAR_POINTER_PEEL && a.variant != VAR_POINTER_RANK3 &&
-        a.variant != VAR_POINTER_INLINE && a.variant != VAR_POINTER_PEEL3)
+        a.variant != VAR_POINTER_INLINE)
       return -10;
     const bool feat_lds = a.n_feat <= 64;
     size_t lds = (feat_lds ? (size_t)a.n_feat * TB * 4 : 0) + TB * 4 + acc_lds;
@@ -1123,14 +1101,6 @@ PMML_API int pmml_tree_launch(hipStream_t stream, const TreeArgs* args, int layo
           if (!err) hipLaunchKernelGGL((tree_pointer_refill_kernel<false, false>), grid, dim3(TB), lds, stream, a);
         }
       }
-    } else if (a.variant == VAR_POINTER_PEEL3 && feat_lds) {
-      if (a.general) {
-        err = prepare_launch(tree_pointer_kernel<true, true, 8, false, false, 3>, lds_pw);
-        if (!err) hipLaunchKernelGGL((tree_pointer_kernel<true, true, 8, false, false, 3>), grid, dim3(TB), lds_pw, stream, a);
-      } else {
-        err = prepare_launch(tree_pointer_kernel<false, true, 8, false, false, 3>, lds_pw);
-        if (!err) hipLaunchKernelGGL((tree_pointer_kernel<false, true, 8, false, false, 3>), grid, dim3(TB), lds_pw, stream, a);
-      }
     } else if (a.variant == VAR_POINTER_PEEL && feat_lds) {
       if (a.general) {
         err = prepare_launch(tree_pointer_kernel<true, true, 8, false, false, true>, lds_pw);
@@ -1171,7 +1141,7 @@ PMML_API int pmml_tree_launch(hipStream_t stream, const TreeArgs* args, int layo
         if (!err)
           hipLaunchKernelGGL((tree_pointer_kernel<false, false, 8, false, false, false, true>), grid, dim3(TB), lds_pw, stream, a);
       }
-    } else if (a.variant == VAR_POINTER_USKIP || a.variant == VAR_POINTER_PEEL || a.variant == VAR_POINTER_PEEL3) {
+    } else if (a.variant == VAR_POINTER_USKIP || a.variant == VAR_POINTER_PEEL) {
       return -4;  // features in LDS only
     } else if (a.general) {
       if (feat_lds && (a.variant & VAR_POINTER_MASKED)) {

@@ -1164,7 +1164,6 @@ VAR_POINTER_PEEL = 512
 VAR_POINTER_RANK3 = 1024
 VAR_POINTER_LDS = 2048  # compact slots walked out of LDS chunks (tree_lds.hip); host-side flag only
 VAR_POINTER_INLINE = 4096  # lock-step pointer walk, leaf payloads inline in the parent nodes
-VAR_POINTER_PEEL3 = 8192  # lock-step pointer walk, top three levels from wave-uniform loads
 DYN_B, DYN_SLOTS = 8, 16  # csrc: MODE_SUM trees per claimed batch, batch slots per chunk
 
 
@@ -1329,8 +1328,7 @@ class TreePlan(DevicePlan):
         ``pointer_load`` (pointer lock-step kernel, features in LDS): ``"clamped"`` (finished walks
         re-load node 0, no branch), ``"masked"`` (their loads are exec-masked off) or ``"uskip"``
         (a walk slot finished in every lane of the wave issues no load at all: wave-uniform branch)
-        or ``"peel"`` (the top two levels from wave-uniform scalar loads + a per-lane select),
-        ``"peel3"`` (the top three levels: the level-2 node is picked among at most four), or
+        or ``"peel"`` (the top two levels from wave-uniform scalar loads + a per-lane select), or
         ``"auto"`` (default): peel for the 8-walk lock-step kernel with table leaves, else clamped.
         Measured (profiles/r6h, 300 trees x depth 14, 1M rows, kernels with a 32 KiB feature-plane
         LDS): GBDT 2.555 vs 2.768 ms, RF 3.48 vs 3.53 ms (bit-identical walks).
@@ -1380,8 +1378,8 @@ class TreePlan(DevicePlan):
         self.lds_chunks = self.lds_slices = None  # lds node format only
         self.lds_rows = self.lds_chunk_u4 = self.lds_n_slices = 0
         self.rank_thr, self.rank_cnt, self.rank_stride = None, None, 0  # rank3 node format only
-        if pointer_load not in ("auto", "clamped", "masked", "uskip", "peel", "peel3"):
-            raise ValueError("pointer_load must be 'auto', 'clamped', 'masked', 'uskip', 'peel' or 'peel3'")
+        if pointer_load not in ("auto", "clamped", "masked", "uskip", "peel"):
+            raise ValueError("pointer_load must be 'auto', 'clamped', 'masked', 'uskip' or 'peel'")
         if pointer_load == "auto":
             pointer_load = "peel" if (pointer_ilp == 8 and pointer_leaf == "table") else "clamped"
         if hybrid_tail not in ("compact", "wide"):
@@ -1668,8 +1666,6 @@ class TreePlan(DevicePlan):
                 self.variant = VAR_POINTER_MASKED  # finished walks skip their node load (exec mask)
             elif pointer_load == "peel" and self.layout == "pointer" and self.variant == 0 and feat_lds:
                 self.variant = VAR_POINTER_PEEL  # top two levels from wave-uniform scalar loads
-            elif pointer_load == "peel3" and self.layout == "pointer" and self.variant == 0 and feat_lds:
-                self.variant = VAR_POINTER_PEEL3  # ... and the third (at most four nodes) too
             elif pointer_load == "uskip" and self.layout == "pointer" and self.variant == 0 and feat_lds:
                 self.variant = VAR_POINTER_USKIP  # slots finished in the whole wave issue no load
             elif inline and self.variant == 0:

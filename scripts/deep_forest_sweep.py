@@ -46,7 +46,6 @@ CONFIGS = {
     "hybw3u": dict(layout="hybrid", head_depth=3, hybrid_tail="wide", pointer_load="uskip"),
     "hybw4u": dict(layout="hybrid", head_depth=4, hybrid_tail="wide", pointer_load="uskip"),
     "pointer+peel": dict(layout="pointer", pointer_load="peel"),
-    "pointer+peel3": dict(layout="pointer", pointer_load="peel3"),
     "lds": dict(layout="pointer", node_format="lds"),
     "auto": dict(),
 }

@@ -152,7 +152,6 @@ def test_super_layout_votes_on_gpu(gpu):
 
 @pytest.mark.parametrize("opts", [dict(layout="pointer", pointer_load="uskip"),
                                   dict(layout="pointer", pointer_load="peel"),
-                                  dict(layout="pointer", pointer_load="peel3"),
                                   dict(layout="pointer", pointer_load="uskip", pointer_ilp=4),
                                   dict(layout="hybrid", hybrid_tail="wide", head_depth=2),
                                   dict(layout="hybrid", hybrid_tail="wide", head_depth=4, pointer_load="uskip"),
@@ -178,7 +177,6 @@ def test_uniform_skip_walks_on_gpu(gpu, opts, missing):
 
 @pytest.mark.parametrize("opts", [dict(layout="pointer", pointer_load="uskip"),
                                   dict(layout="pointer", pointer_load="peel"),
-                                  dict(layout="pointer", pointer_load="peel3"),
                                   dict(layout="hybrid", hybrid_tail="wide", head_depth=3)])
 def test_uniform_skip_votes_on_gpu(gpu, opts):
     """Random-forest votes (P = 3 class slots in LDS) on the uniform-skip walks."""
@@ -191,11 +189,11 @@ def test_uniform_skip_votes_on_gpu(gpu, opts):
     np.testing.assert_array_equal(s[v], ref[v])
 
 
-@pytest.mark.parametrize("load", ["peel", "peel3"])
+@pytest.mark.parametrize("load", ["peel", "auto"])
 @pytest.mark.parametrize("p_split", [0.35, 0.6])
 def test_peeled_walks_with_shallow_leaves_on_gpu(gpu, load, p_split):
-    """The peeled top levels when leaves sit at levels 0-2 (stumps, a leaf child of the root, fewer
-    than four level-2 nodes): bit-identical to the clamped walk, exact validity vs the oracle."""
+    """The peeled top levels when leaves sit at levels 1-2 (a leaf child of the root in most
+    trees): bit-identical to the clamped walk, exact validity vs the oracle."""
     c = _model("gbdt", n_trees=64, depth=12, n_features=16, seed=11, p_split=p_split,
                missing_strategy="nullPrediction")
     plan = c.plan(gpu, layout="pointer", pointer_load=load)
