@@ -21,8 +21,15 @@ namespace {
 // the left child is a leaf, bit 28: the right one) -- the leaf value's fp32 bits for a sum
 // ensemble, the class index for an unweighted vote (GENERAL, one increment). The walk ends at the
 // parent with the payload in hand: no leaf gather (one per tree and row; P of them for votes).
+// LTOP (VAR_POINTER_LTOP, BFS node order): the first 2^LTOP - 1 nodes of the PILP trees of a
+// lock-step group -- every internal node of their levels 0 .. LTOP-1 -- are staged in LDS (the
+// next group's nodes are loaded into registers while this group walks and written after it:
+// NBUF 1 = one buffer, two barriers per group; NBUF 2 = double buffered, one barrier), and the walk
+// reads those levels with ds_read_b128 instead of 64-lane global gathers (each ~20 TA cycles
+// whatever the lanes hit, profiles/r3w). The host pads the blob with 2^LTOP - 1 zero nodes so the
+// staging reads stay in bounds.
 template <bool GENERAL, bool FEAT_LDS, int PILP = 8, bool MASKED = false, bool USKIP = false, bool PEEL = false,
-          bool INL = false>
+          bool INL = false, int LTOP = 0, int NBUF = 2>
 __device__ __forceinline__ void pointer_walk(const TreeArgs& a) {
   // LDS: the feature planes, then (GENERAL) the class accumulators — no bad[] array: each thread
   // stages its own row and keeps the row's verdict in a register (POINTER_LDS_BYTES)
@@ -55,13 +62,39 @@ __device__ __forceinline__ void pointer_walk(const TreeArgs& a) {
   float acc = 0.f;
   bool poisoned = false;
   const char* feat_lane = reinterpret_cast<const char*>(feat + tid);
+  constexpr int NTOP = LTOP ? (1 << LTOP) - 1 : 1;
+  constexpr int TOPN = PILP * NTOP;          // staged nodes per group
+  constexpr int TOPK = (TOPN + TB - 1) / TB;  // ... per thread
+  uint4* topl = reinterpret_cast<uint4*>(accl + (GENERAL ? a.C * TB : 0));  // [NBUF][PILP][NTOP]
+  auto top_node = [&](int t0s, int e) -> uint4 {  // staged node e of the group at t0s
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (e < TOPN) {
+      const int t = t0s + e / NTOP;
+      const int r = t < te ? a.roots[t] : -1;
+      if (r >= 0) v = nodes[r + e % NTOP];
+    }
+    return v;
+  };
+  if (LTOP) {
+#pragma unroll
+    for (int k = 0; k < TOPK; ++k)
+      if (tid + k * TB < TOPN) topl[tid + k * TB] = top_node(tb, tid + k * TB);
+    __syncthreads();
+  }
+  int grp = 0;
   // PILP trees walked in lock-step per lane: every level issues the PILP node loads (L2 gathers)
   // together, so one L2 round trip serves PILP walks instead of one — the walk is latency-bound
   // (dependent loads, divergent depths). Finished walks keep re-loading node 0 (clamped index,
   // no branch around the loads) and are masked out; leaves are accumulated in tree order, so the
   // sums are bit-identical to a serial walk.
-  for (int t0 = tb; t0 < te; t0 += PILP) {
+  for (int t0 = tb; t0 < te; t0 += PILP, ++grp) {
     const int nt = min(PILP, te - t0);
+    const uint4* topg = topl + (NBUF == 2 ? (grp & 1) * TOPN : 0);
+    uint4 pre[TOPK];  // the next group's staged nodes, in flight during this group's walk
+#pragma unroll
+    for (int k = 0; k < TOPK; ++k)
+      pre[k] = (LTOP && t0 + PILP < te) ? top_node(t0 + PILP, tid + k * TB) : make_uint4(0u, 0u, 0u, 0u);
+    int rootc[PILP];
     int code[PILP];
     bool pz[PILP];
     bool inl[PILP];       // INL: the walk ended on an inline leaf payload (lpay)
@@ -69,6 +102,7 @@ __device__ __forceinline__ void pointer_walk(const TreeArgs& a) {
 #pragma unroll
     for (int i = 0; i < PILP; ++i) {
       code[i] = i < nt ? a.roots[t0 + i] : -1;
+      rootc[i] = code[i];
       pz[i] = false;
       inl[i] = false;
       lpay[i] = 0u;
@@ -112,14 +146,20 @@ __device__ __forceinline__ void pointer_walk(const TreeArgs& a) {
       }
     }
     bool live = true;
+    int lvl = 0;
     while (live) {
       uint4 nd[PILP];
       bool any[PILP];
 #pragma unroll
       for (int i = 0; i < PILP; ++i) any[i] = !USKIP || __builtin_amdgcn_ballot_w64(code[i] >= 0) != 0ull;
+      const bool from_lds = LTOP && lvl < LTOP;  // wave-uniform: every walk of the group is on level lvl
+      ++lvl;
 #pragma unroll
       for (int i = 0; i < PILP; ++i) {
-        if (USKIP) {
+        if (from_lds) {
+          // a live walk's level-lvl node is one of its tree's first NTOP (BFS); finished -> entry 0
+          nd[i] = topg[i * NTOP + min(max(code[i] - rootc[i], 0), NTOP - 1)];
+        } else if (USKIP) {
           nd[i] = make_uint4(0u, 0u, 0u, 0u);
           if (any[i]) nd[i] = nodes[max(code[i], 0)];
         } else if (MASKED) {
@@ -179,14 +219,23 @@ __device__ __forceinline__ void pointer_walk(const TreeArgs& a) {
         acc += a.leaves[leaf];
       }
     }
+    if (LTOP) {
+      // NBUF 2: the other buffer was last read by group grp - 1, which every wave finished before
+      // the previous barrier; NBUF 1: wait until every wave is done with this group's nodes
+      if (NBUF == 1) __syncthreads();
+#pragma unroll
+      for (int k = 0; k < TOPK; ++k)
+        if (tid + k * TB < TOPN) topl[(NBUF == 2 ? ((grp + 1) & 1) * TOPN : 0) + tid + k * TB] = pre[k];
+      __syncthreads();
+    }
   }
   finish_row(a, acc, accl, split, GENERAL, row, row_ok && !poisoned);
 }
 
 template <bool GENERAL, bool FEAT_LDS, int PILP = 8, bool MASKED = false, bool USKIP = false, bool PEEL = false,
-          bool INL = false>
+          bool INL = false, int LTOP = 0, int NBUF = 2>
 __global__ __launch_bounds__(TB, 2) void tree_pointer_kernel(TreeArgs a) {
-  pointer_walk<GENERAL, FEAT_LDS, PILP, MASKED, USKIP, PEEL, INL>(a);
+  pointer_walk<GENERAL, FEAT_LDS, PILP, MASKED, USKIP, PEEL, INL, LTOP, NBUF>(a);
 }
 
 // Several pointer-layout ensembles over the SAME rows in one launch — the segments of a segmented
@@ -1032,7 +1081,7 @@ PMML_API int pmml_tree_launch(hipStream_t stream, const TreeArgs* args, int layo
     if (a.variant != 0 && a.variant != VAR_POINTER_REFILL && a.variant != VAR_POINTER_COMPACT &&
         a.variant != VAR_POINTER_MASKED && a.variant != VAR_POINTER_SUPER && a.variant != VAR_POINTER_USKIP &&
         a.variant != VAR_POINTER_PEEL && a.variant != VAR_POINTER_RANK3 &&
-        a.variant != VAR_POINTER_INLINE)
+        a.variant != VAR_POINTER_INLINE && a.variant != VAR_POINTER_LTOP)
       return -10;
     const bool feat_lds = a.n_feat <= 64;
     size_t lds = (feat_lds ? (size_t)a.n_feat * TB * 4 : 0) + TB * 4 + acc_lds;
@@ -1101,6 +1150,21 @@ PMML_API int pmml_tree_launch(hipStream_t stream, const TreeArgs* args, int layo
           if (!err) hipLaunchKernelGGL((tree_pointer_refill_kernel<false, false>), grid, dim3(TB), lds, stream, a);
         }
       }
+    } else if (a.variant == VAR_POINTER_LTOP && feat_lds) {
+      // levels 0-4 (31 nodes a tree), one LDS buffer (profiles/r6l: two buffers or a sixth level
+      // cost a workgroup per CU and measured no faster for sums, 16-20 % slower for votes)
+      const size_t lt = lds_pw + (size_t)8 * 31 * 16;
+      if (a.general) {
+        err = prepare_launch(tree_pointer_kernel<true, true, 8, false, false, false, false, 5, 1>, lt);
+        if (!err)
+          hipLaunchKernelGGL((tree_pointer_kernel<true, true, 8, false, false, false, false, 5, 1>), grid, dim3(TB), lt,
+                             stream, a);
+      } else {
+        err = prepare_launch(tree_pointer_kernel<false, true, 8, false, false, false, false, 5, 1>, lt);
+        if (!err)
+          hipLaunchKernelGGL((tree_pointer_kernel<false, true, 8, false, false, false, false, 5, 1>), grid, dim3(TB), lt,
+                             stream, a);
+      }
     } else if (a.variant == VAR_POINTER_PEEL && feat_lds) {
       if (a.general) {
         err = prepare_launch(tree_pointer_kernel<true, true, 8, false, false, true>, lds_pw);
@@ -1141,7 +1205,7 @@ PMML_API int pmml_tree_launch(hipStream_t stream, const TreeArgs* args, int layo
         if (!err)
           hipLaunchKernelGGL((tree_pointer_kernel<false, false, 8, false, false, false, true>), grid, dim3(TB), lds_pw, stream, a);
       }
-    } else if (a.variant == VAR_POINTER_USKIP || a.variant == VAR_POINTER_PEEL) {
+    } else if (a.variant == VAR_POINTER_USKIP || a.variant == VAR_POINTER_PEEL || a.variant == VAR_POINTER_LTOP) {
       return -4;  // features in LDS only
     } else if (a.general) {
       if (feat_lds && (a.variant & VAR_POINTER_MASKED)) {

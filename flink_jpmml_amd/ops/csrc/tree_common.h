@@ -96,6 +96,7 @@ constexpr int VAR_POINTER_USKIP = 256;  // pointer layout, lock-step: wave-unifo
 constexpr int VAR_POINTER_PEEL = 512;   // pointer layout, lock-step: top two levels from uniform (scalar) loads
 constexpr int VAR_POINTER_RANK3 = 1024; // pointer layout: three levels per 16-byte record on threshold ranks (tree.hip)
 constexpr int VAR_POINTER_INLINE = 4096; // pointer layout, lock-step: leaf payloads inline in the parent (tree.hip)
+constexpr int VAR_POINTER_LTOP = 8192;   // pointer layout, lock-step, BFS: top levels of each group's trees from LDS
 
 // per-depth launchers (tree_d<D>.hip)
 #define PMML_TREE_DECL(D) int launch_perfect_d##D(hipStream_t st, const TreeArgs& a, dim3 grid, size_t lds); \

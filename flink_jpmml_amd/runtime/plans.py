@@ -1164,6 +1164,8 @@ VAR_POINTER_PEEL = 512
 VAR_POINTER_RANK3 = 1024
 VAR_POINTER_LDS = 2048  # compact slots walked out of LDS chunks (tree_lds.hip); host-side flag only
 VAR_POINTER_INLINE = 4096  # lock-step pointer walk, leaf payloads inline in the parent nodes
+VAR_POINTER_LTOP = 8192  # lock-step pointer walk, BFS: levels 0-4 of each group's trees staged in LDS
+POINTER_LTOP_NODES = 31  # ... 2^5 - 1 nodes a tree (tree.hip launcher: LTOP 5)
 DYN_B, DYN_SLOTS = 8, 16  # csrc: MODE_SUM trees per claimed batch, batch slots per chunk
 
 
@@ -1328,10 +1330,11 @@ class TreePlan(DevicePlan):
         ``pointer_load`` (pointer lock-step kernel, features in LDS): ``"clamped"`` (finished walks
         re-load node 0, no branch), ``"masked"`` (their loads are exec-masked off) or ``"uskip"``
         (a walk slot finished in every lane of the wave issues no load at all: wave-uniform branch)
-        or ``"peel"`` (the top two levels from wave-uniform scalar loads + a per-lane select), or
-        ``"auto"`` (default): peel for the 8-walk lock-step kernel with table leaves, else clamped.
-        Measured (profiles/r6h, 300 trees x depth 14, 1M rows, kernels with a 32 KiB feature-plane
-        LDS): GBDT 2.555 vs 2.768 ms, RF 3.48 vs 3.53 ms (bit-identical walks).
+        or ``"peel"`` (the top two levels from wave-uniform scalar loads + a per-lane select),
+        ``"ltop"`` (BFS order: levels 0-4 of each lock-step group's trees staged in LDS), or
+        ``"auto"`` (default): ltop (BFS) / peel (DFS order) for the 8-walk lock-step kernel with
+        table leaves, else clamped. Measured (profiles/r6l, 300 trees x depth 14, 1M rows,
+        bit-identical walks): GBDT ltop 2.415 / peel 2.57 / clamped 2.79 ms, RF 3.11 / 3.48 / 3.52.
 
         ``hybrid_tail`` (hybrid layout): ``"compact"`` (depth-first uint2 tail,
         :func:`~flink_jpmml_amd.runtime.hybrid.pack_hybrid_compact`) or ``"wide"`` (the 16-byte BFS
@@ -1378,10 +1381,11 @@ class TreePlan(DevicePlan):
         self.lds_chunks = self.lds_slices = None  # lds node format only
         self.lds_rows = self.lds_chunk_u4 = self.lds_n_slices = 0
         self.rank_thr, self.rank_cnt, self.rank_stride = None, None, 0  # rank3 node format only
-        if pointer_load not in ("auto", "clamped", "masked", "uskip", "peel"):
-            raise ValueError("pointer_load must be 'auto', 'clamped', 'masked', 'uskip' or 'peel'")
+        if pointer_load not in ("auto", "clamped", "masked", "uskip", "peel", "ltop"):
+            raise ValueError("pointer_load must be 'auto', 'clamped', 'masked', 'uskip', 'peel' or 'ltop'")
         if pointer_load == "auto":
-            pointer_load = "peel" if (pointer_ilp == 8 and pointer_leaf == "table") else "clamped"
+            pointer_load = (("ltop" if node_order == "bfs" else "peel") if (pointer_ilp == 8 and pointer_leaf == "table")
+                            else "clamped")
         if hybrid_tail not in ("compact", "wide"):
             raise ValueError("hybrid_tail must be 'compact' or 'wide'")
         if pointer_leaf not in ("table", "inline"):
@@ -1666,6 +1670,11 @@ class TreePlan(DevicePlan):
                 self.variant = VAR_POINTER_MASKED  # finished walks skip their node load (exec mask)
             elif pointer_load == "peel" and self.layout == "pointer" and self.variant == 0 and feat_lds:
                 self.variant = VAR_POINTER_PEEL  # top two levels from wave-uniform scalar loads
+            elif (pointer_load == "ltop" and self.layout == "pointer" and self.variant == 0 and feat_lds
+                  and node_order == "bfs" and pointer_ilp == 8):
+                self.variant = VAR_POINTER_LTOP  # levels 0-4 of each lock-step group from LDS
+                # staging reads root + 0 .. 30 of every tree: pad so the last tree's stay in bounds
+                nodes = np.concatenate([nodes, np.zeros((POINTER_LTOP_NODES, 4), dtype=nodes.dtype)])
             elif pointer_load == "uskip" and self.layout == "pointer" and self.variant == 0 and feat_lds:
                 self.variant = VAR_POINTER_USKIP  # slots finished in the whole wave issue no load
             elif inline and self.variant == 0:

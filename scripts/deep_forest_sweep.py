@@ -46,6 +46,7 @@ CONFIGS = {
     "hybw3u": dict(layout="hybrid", head_depth=3, hybrid_tail="wide", pointer_load="uskip"),
     "hybw4u": dict(layout="hybrid", head_depth=4, hybrid_tail="wide", pointer_load="uskip"),
     "pointer+peel": dict(layout="pointer", pointer_load="peel"),
+    "pointer+ltop": dict(layout="pointer", pointer_load="ltop"),
     "lds": dict(layout="pointer", node_format="lds"),
     "auto": dict(),
 }

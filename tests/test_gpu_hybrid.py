@@ -152,6 +152,7 @@ def test_super_layout_votes_on_gpu(gpu):
 
 @pytest.mark.parametrize("opts", [dict(layout="pointer", pointer_load="uskip"),
                                   dict(layout="pointer", pointer_load="peel"),
+                                  dict(layout="pointer", pointer_load="ltop"),
                                   dict(layout="pointer", pointer_load="uskip", pointer_ilp=4),
                                   dict(layout="hybrid", hybrid_tail="wide", head_depth=2),
                                   dict(layout="hybrid", hybrid_tail="wide", head_depth=4, pointer_load="uskip"),
@@ -177,6 +178,7 @@ def test_uniform_skip_walks_on_gpu(gpu, opts, missing):
 
 @pytest.mark.parametrize("opts", [dict(layout="pointer", pointer_load="uskip"),
                                   dict(layout="pointer", pointer_load="peel"),
+                                  dict(layout="pointer", pointer_load="ltop"),
                                   dict(layout="hybrid", hybrid_tail="wide", head_depth=3)])
 def test_uniform_skip_votes_on_gpu(gpu, opts):
     """Random-forest votes (P = 3 class slots in LDS) on the uniform-skip walks."""
@@ -189,7 +191,7 @@ def test_uniform_skip_votes_on_gpu(gpu, opts):
     np.testing.assert_array_equal(s[v], ref[v])
 
 
-@pytest.mark.parametrize("load", ["peel", "auto"])
+@pytest.mark.parametrize("load", ["peel", "ltop", "auto"])
 @pytest.mark.parametrize("p_split", [0.35, 0.6])
 def test_peeled_walks_with_shallow_leaves_on_gpu(gpu, load, p_split):
     """The peeled top levels when leaves sit at levels 1-2 (a leaf child of the root in most

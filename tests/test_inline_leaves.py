@@ -94,7 +94,7 @@ def test_inline_leaves_on_gpu(gpu, kind):
     c = CompiledPmml.from_string(txt)
     inl = c.plan(gpu, layout="pointer", pointer_leaf="inline")
     tab = c.plan(gpu, layout="pointer", pointer_leaf="table")
-    assert inl.variant == 4096 and tab.variant == 512  # table leaves: the default PEEL walk
+    assert inl.variant == 4096 and tab.variant == 8192  # table leaves: the default LTOP walk
     X = stream_matrix(100_000, F, seed=3, missing_rate=0.03)
     Xd = torch.from_numpy(X).cuda()
     outs = []
