@@ -214,7 +214,21 @@ __device__ __forceinline__ void pointer_walk(const TreeArgs& a) {
       const int leaf = ~code[i];
       if (GENERAL) {
         const int slot = a.tree_slot[t0 + i];
-        for (int p = 0; p < a.P; ++p) accl[(slot + p) * TB + tid] += a.leaves[(size_t)leaf * a.P + p];
+        const float* lp = a.leaves + (size_t)leaf * a.P;
+        if (a.P == 3) {
+          // the row's three payloads as ONE multi-dword gather (a loop over a runtime P issues
+          // one 64-lane gather per class); per-slot sums keep the tree order
+          const float v0 = lp[0], v1 = lp[1], v2 = lp[2];
+          accl[slot * TB + tid] += v0;
+          accl[(slot + 1) * TB + tid] += v1;
+          accl[(slot + 2) * TB + tid] += v2;
+        } else if (a.P == 2) {
+          const float v0 = lp[0], v1 = lp[1];
+          accl[slot * TB + tid] += v0;
+          accl[(slot + 1) * TB + tid] += v1;
+        } else {
+          for (int p = 0; p < a.P; ++p) accl[(slot + p) * TB + tid] += lp[p];
+        }
       } else {
         acc += a.leaves[leaf];
       }
