@@ -1095,7 +1095,8 @@ PMML_API int pmml_tree_launch(hipStream_t stream, const TreeArgs* args, int layo
     if (a.variant != 0 && a.variant != VAR_POINTER_REFILL && a.variant != VAR_POINTER_COMPACT &&
         a.variant != VAR_POINTER_MASKED && a.variant != VAR_POINTER_SUPER && a.variant != VAR_POINTER_USKIP &&
         a.variant != VAR_POINTER_PEEL && a.variant != VAR_POINTER_RANK3 &&
-        a.variant != VAR_POINTER_INLINE && a.variant != VAR_POINTER_LTOP)
+        a.variant != VAR_POINTER_INLINE && a.variant != VAR_POINTER_LTOP &&
+        a.variant != (VAR_POINTER_LTOP | VAR_POINTER_INLINE))
       return -10;
     const bool feat_lds = a.n_feat <= 64;
     size_t lds = (feat_lds ? (size_t)a.n_feat * TB * 4 : 0) + TB * 4 + acc_lds;
@@ -1163,6 +1164,19 @@ PMML_API int pmml_tree_launch(hipStream_t stream, const TreeArgs* args, int layo
           err = prepare_launch(tree_pointer_refill_kernel<false, false>, lds);
           if (!err) hipLaunchKernelGGL((tree_pointer_refill_kernel<false, false>), grid, dim3(TB), lds, stream, a);
         }
+      }
+    } else if (a.variant == (VAR_POINTER_LTOP | VAR_POINTER_INLINE) && feat_lds) {
+      const size_t lt = lds_pw + (size_t)8 * 31 * 16;
+      if (a.general) {
+        err = prepare_launch(tree_pointer_kernel<true, true, 8, false, false, false, true, 5, 1>, lt);
+        if (!err)
+          hipLaunchKernelGGL((tree_pointer_kernel<true, true, 8, false, false, false, true, 5, 1>), grid, dim3(TB), lt,
+                             stream, a);
+      } else {
+        err = prepare_launch(tree_pointer_kernel<false, true, 8, false, false, false, true, 5, 1>, lt);
+        if (!err)
+          hipLaunchKernelGGL((tree_pointer_kernel<false, true, 8, false, false, false, true, 5, 1>), grid, dim3(TB), lt,
+                             stream, a);
       }
     } else if (a.variant == VAR_POINTER_LTOP && feat_lds) {
       // levels 0-4 (31 nodes a tree), one LDS buffer (profiles/r6l: two buffers or a sixth level

@@ -1648,7 +1648,7 @@ class TreePlan(DevicePlan):
                 # inline leaf payloads on the default lock-step walk (sums, or unit votes) unless
                 # asked for the leaf table (pointer_leaf="table")
                 inline = (pointer_leaf == "inline" and self.layout == "pointer" and pointer_schedule == "lockstep"
-                          and pointer_load == "clamped" and pointer_ilp == 8
+                          and pointer_load in ("clamped", "ltop") and pointer_ilp == 8
                           and ((spec.P == 1 and spec.slots is None) or spec.P > 1))
                 _, nodes, leaves, roots, has_dr = pack_trees(spec.trees, spec.weights, spec.P, 0, feat_lds,
                                                              order=node_order, inline_leaves=inline)
@@ -1672,7 +1672,7 @@ class TreePlan(DevicePlan):
                 self.variant = VAR_POINTER_PEEL  # top two levels from wave-uniform scalar loads
             elif (pointer_load == "ltop" and self.layout == "pointer" and self.variant == 0 and feat_lds
                   and node_order == "bfs" and pointer_ilp == 8):
-                self.variant = VAR_POINTER_LTOP  # levels 0-4 of each lock-step group from LDS
+                self.variant = VAR_POINTER_LTOP | (VAR_POINTER_INLINE if inline else 0)  # levels 0-4 from LDS
                 # staging reads root + 0 .. 30 of every tree: pad so the last tree's stay in bounds
                 nodes = np.concatenate([nodes, np.zeros((POINTER_LTOP_NODES, 4), dtype=nodes.dtype)])
             elif pointer_load == "uskip" and self.layout == "pointer" and self.variant == 0 and feat_lds:

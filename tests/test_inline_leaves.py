@@ -81,8 +81,9 @@ def test_inline_twin_equals_table_and_oracle(kind, missing):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("load", ["auto", "ltop"])
 @pytest.mark.parametrize("kind", ["gbdt", "rf"])
-def test_inline_leaves_on_gpu(gpu, kind):
+def test_inline_leaves_on_gpu(gpu, kind, load):
     import torch
 
     if kind == "gbdt":
@@ -92,9 +93,10 @@ def test_inline_leaves_on_gpu(gpu, kind):
         txt = random_forest_pmml(n_trees=40, depth=14, n_features=16, n_classes=3, seed=5, p_split=0.8)
         F = 16
     c = CompiledPmml.from_string(txt)
-    inl = c.plan(gpu, layout="pointer", pointer_leaf="inline")
+    inl = c.plan(gpu, layout="pointer", pointer_leaf="inline", pointer_load=load)
     tab = c.plan(gpu, layout="pointer", pointer_leaf="table")
-    assert inl.variant == 4096 and tab.variant == 8192  # table leaves: the default LTOP walk
+    # inline leaves: the clamped walk (auto), or with the LDS-staged top levels; table leaves: LTOP
+    assert inl.variant == (4096 if load == "auto" else 4096 | 8192) and tab.variant == 8192
     X = stream_matrix(100_000, F, seed=3, missing_rate=0.03)
     Xd = torch.from_numpy(X).cuda()
     outs = []
