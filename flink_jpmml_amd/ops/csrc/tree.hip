@@ -1181,8 +1181,20 @@ PMML_API int pmml_tree_launch(hipStream_t stream, const TreeArgs* args, int layo
     } else if (a.variant == VAR_POINTER_LTOP && feat_lds) {
       // levels 0-4 (31 nodes a tree), one LDS buffer (profiles/r6l: two buffers or a sixth level
       // cost a workgroup per CU and measured no faster for sums, 16-20 % slower for votes)
-      const size_t lt = lds_pw + (size_t)8 * 31 * 16;
-      if (a.general) {
+      const size_t lt = lds_pw + (size_t)(a.pilp == 6 ? 6 : 8) * 31 * 16;
+      if (a.pilp == 6) {
+        if (a.general) {
+          err = prepare_launch(tree_pointer_kernel<true, true, 6, false, false, false, false, 5, 1>, lt);
+          if (!err)
+            hipLaunchKernelGGL((tree_pointer_kernel<true, true, 6, false, false, false, false, 5, 1>), grid, dim3(TB),
+                               lt, stream, a);
+        } else {
+          err = prepare_launch(tree_pointer_kernel<false, true, 6, false, false, false, false, 5, 1>, lt);
+          if (!err)
+            hipLaunchKernelGGL((tree_pointer_kernel<false, true, 6, false, false, false, false, 5, 1>), grid, dim3(TB),
+                               lt, stream, a);
+        }
+      } else if (a.general) {
         err = prepare_launch(tree_pointer_kernel<true, true, 8, false, false, false, false, 5, 1>, lt);
         if (!err)
           hipLaunchKernelGGL((tree_pointer_kernel<true, true, 8, false, false, false, false, 5, 1>), grid, dim3(TB), lt,

@@ -1372,8 +1372,8 @@ class TreePlan(DevicePlan):
         super().__init__(compiled, device)
         if nan_mode not in ("auto", "off"):
             raise ValueError("nan_mode must be 'auto' or 'off'")
-        if pointer_ilp not in (2, 4, 8, 16):
-            raise ValueError("pointer_ilp must be 2, 4, 8 or 16")
+        if pointer_ilp not in (2, 4, 6, 8, 16):
+            raise ValueError("pointer_ilp must be 2, 4, 6 (LTOP only), 8 or 16")
         self.pointer_ilp = int(pointer_ilp)
         if pointer_schedule not in ("refill", "lockstep"):
             raise ValueError("pointer_schedule must be 'refill' or 'lockstep'")
@@ -1671,7 +1671,7 @@ class TreePlan(DevicePlan):
             elif pointer_load == "peel" and self.layout == "pointer" and self.variant == 0 and feat_lds:
                 self.variant = VAR_POINTER_PEEL  # top two levels from wave-uniform scalar loads
             elif (pointer_load == "ltop" and self.layout == "pointer" and self.variant == 0 and feat_lds
-                  and node_order == "bfs" and pointer_ilp == 8):
+                  and node_order == "bfs" and pointer_ilp in (6, 8)):
                 self.variant = VAR_POINTER_LTOP | (VAR_POINTER_INLINE if inline else 0)  # levels 0-4 from LDS
                 # staging reads root + 0 .. 30 of every tree: pad so the last tree's stay in bounds
                 nodes = np.concatenate([nodes, np.zeros((POINTER_LTOP_NODES, 4), dtype=nodes.dtype)])

@@ -47,6 +47,7 @@ CONFIGS = {
     "hybw4u": dict(layout="hybrid", head_depth=4, hybrid_tail="wide", pointer_load="uskip"),
     "pointer+peel": dict(layout="pointer", pointer_load="peel"),
     "pointer+ltop": dict(layout="pointer", pointer_load="ltop"),
+    "ltop6": dict(layout="pointer", pointer_load="ltop", pointer_ilp=6),
     "ltop_inline": dict(layout="pointer", pointer_load="ltop", pointer_leaf="inline"),
     "lds": dict(layout="pointer", node_format="lds"),
     "auto": dict(),
