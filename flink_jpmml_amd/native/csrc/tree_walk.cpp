@@ -694,6 +694,46 @@ __attribute__((target("avx512f,avx512vl"))) void walk_perfect_avx512(const doubl
 }
 #endif
 
+#if defined(__x86_64__)
+// ONE row through 8 perfect trees of equal depth D (a lane per tree: the single-record call, where
+// row-parallel lanes have nothing to work on). Same arithmetic as walk_perfect; pb / lb: the 8
+// trees' offsets into the concatenated perfect tables.
+__attribute__((target("avx512f,avx512vl"))) void walk_trees8_avx512(const double *pt, const int32_t *pm,
+                                                                    const int32_t *pl, const int32_t *pb,
+                                                                    const int32_t *lb, int D, const double *xr,
+                                                                    int32_t *res) {
+    const __m256i base = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(pb));
+    const __m256i one = _mm256_set1_epi32(1), fmask = _mm256_set1_epi32(0xFFFF), three = _mm256_set1_epi32(3);
+    const __m256i two = _mm256_set1_epi32(2);
+    __m256i s = _mm256_setzero_si256();
+    __mmask8 poison = 0;
+    for (int d = 0; d < D; ++d) {
+        const __m256i idx = _mm256_add_epi32(base, s);
+        const __m256i m = _mm256_i32gather_epi32(pm, idx, 4);
+        const __m512d t = _mm512_i32gather_pd(idx, pt, 8);
+        const __m512d x = _mm512_i32gather_pd(_mm256_and_si256(m, fmask), xr, 8);
+        const __mmask8 lt = _mm512_cmp_pd_mask(x, t, _CMP_LT_OQ);
+        const __mmask8 eq = _mm512_cmp_pd_mask(x, t, _CMP_EQ_OQ);
+        const __mmask8 un = _mm512_cmp_pd_mask(x, x, _CMP_UNORD_Q);
+        const __mmask8 incl = _mm256_test_epi32_mask(m, _mm256_set1_epi32(1 << 16));
+        const __mmask8 neg = _mm256_test_epi32_mask(m, _mm256_set1_epi32(1 << 17));
+        const __m256i miss = _mm256_and_si256(_mm256_srli_epi32(m, 18), three);
+        const __mmask8 mright = _mm256_cmpeq_epi32_mask(miss, one);
+        const __mmask8 mnull = _mm256_cmpeq_epi32_mask(miss, two);
+        const __mmask8 pred = (lt | (eq & incl)) ^ neg;
+        const __mmask8 right = static_cast<__mmask8>((~pred & ~un) | (un & mright));
+        poison |= un & mnull;
+        const __m256i s2 = _mm256_add_epi32(_mm256_add_epi32(s, s), one);
+        s = _mm256_mask_add_epi32(s2, right, s2, one);
+    }
+    const __m256i NI = _mm256_set1_epi32((int32_t(1) << D) - 1);
+    const __m256i lidx = _mm256_add_epi32(_mm256_loadu_si256(reinterpret_cast<const __m256i *>(lb)), _mm256_sub_epi32(s, NI));
+    __m256i leaf = _mm256_i32gather_epi32(pl, lidx, 4);
+    leaf = _mm256_mask_mov_epi32(leaf, poison, _mm256_set1_epi32(-1));
+    _mm256_storeu_si256(reinterpret_cast<__m256i *>(res), leaf);
+}
+#endif
+
 // Runs every tree over rows [r0, r1) and hands (tree, row, global node or -1) to `emit`.
 template <class Emit>
 void run_block(const Call &c, const Fixed &f, const double *X, Py_ssize_t r0, Py_ssize_t r1, bool avx512,
@@ -703,6 +743,29 @@ void run_block(const Call &c, const Fixed &f, const double *X, Py_ssize_t r0, Py
     const Py_ssize_t k = c.k;
     int32_t node[32];
     for (Py_ssize_t t = 0; t < c.T; ++t) {
+#if defined(__x86_64__)
+        // fewer rows than one row-parallel call: 8 trees at a time per row (perfect, equal depth,
+        // table offsets within int32)
+        if (avx512 && r1 - r0 < 32 && t + 8 <= c.T && f.pt.size() < (size_t(1) << 31) &&
+            f.pleaf.size() < (size_t(1) << 31)) {
+            bool same = true;
+            for (int j = 0; j < 8 && same; ++j)
+                same = f.pbase[t + j] >= 0 && f.depth[t + j] == f.depth[t];
+            if (same) {
+                int32_t pb[8], lb[8];
+                for (int j = 0; j < 8; ++j) {
+                    pb[j] = static_cast<int32_t>(f.pbase[t + j]);
+                    lb[j] = static_cast<int32_t>(f.plbase[t + j]);
+                }
+                for (Py_ssize_t r = r0; r < r1; ++r) {
+                    walk_trees8_avx512(f.pt.data(), f.pmeta.data(), f.pleaf.data(), pb, lb, f.depth[t], X + r * k, node);
+                    for (int j = 0; j < 8; ++j) emit(t + j, r, node[j]);
+                }
+                t += 7;
+                continue;
+            }
+        }
+#endif
         Py_ssize_t r = r0;
         if (f.pbase[t] >= 0) {
             const double *pt = f.pt.data() + f.pbase[t];

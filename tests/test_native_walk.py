@@ -194,6 +194,10 @@ def test_scalar_and_avx512_walks_agree(monkeypatch, seed):
     # whenever a block is shorter than the interleave width
     one = prog.leaves(np.ascontiguousarray(X[:7]))
     np.testing.assert_array_equal(one, fast[:, :7])
+    monkeypatch.delenv("FJA_WALK_SCALAR")
+    # single records on the AVX-512 path: 8 trees per vector instead of 32 rows
+    for i in (0, 5, 17):
+        np.testing.assert_array_equal(prog.leaves(np.ascontiguousarray(X[i:i + 1])), fast[:, i:i + 1])
 
 
 def test_pairwise_sum_matches_numpy_for_every_width():
