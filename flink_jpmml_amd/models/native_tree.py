@@ -257,6 +257,14 @@ class ForestProgram:
         """The walker's input: the prepared float64 column of every referenced field, row-major.
         Raises whatever ``cols.get`` raises (the caller then keeps the numpy walk)."""
         n, k = cols.n, max(1, len(self.fields))
+        M, mindex = getattr(cols, "matrix", None), getattr(cols, "mindex", None)
+        if M is not None and self.fields:
+            hit = getattr(self, "_midx", None)
+            if hit is None or hit[0] is not mindex:
+                idx = [mindex.get(f) for f in self.fields]
+                hit = self._midx = (mindex, None if None in idx else np.asarray(idx, dtype=np.intp))
+            if hit[1] is not None:
+                return M[:, hit[1]]  # every referenced field is an input column: one gather
         X = np.empty((n, k), dtype=np.float64)
         if not self.fields:
             X[:] = 0.0

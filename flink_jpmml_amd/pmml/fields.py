@@ -401,6 +401,11 @@ class Columns:
         if derived:
             self.derived.update(derived)
         self._busy: set = set()
+        # the [n, k] matrix the base columns are views of, and name -> column (CompiledPmml.columns);
+        # lets a consumer of many base columns take them in one gather (None once a base column is
+        # replaced through set())
+        self.matrix: Optional[np.ndarray] = None
+        self.mindex: Optional[Dict[str, int]] = None
 
     def child(self, extra_derived: Iterable[ir.DerivedField], rows: Optional[np.ndarray] = None) -> "Columns":
         """A context for a nested model; shares computed columns (optionally row-subset)."""
@@ -437,6 +442,8 @@ class Columns:
         return col
 
     def set(self, name: str, col: np.ndarray) -> None:
+        if self.mindex is not None and name in self.mindex:
+            self.matrix = None
         self.data[name] = col
 
 

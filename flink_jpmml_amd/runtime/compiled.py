@@ -72,7 +72,12 @@ class CompiledPmml:
     def columns(self, X: np.ndarray) -> Columns:
         X = np.asarray(X, dtype=np.float64)
         base = {name: X[:, j] for j, name in enumerate(self.active_fields)}
-        return Columns(self.schema, X.shape[0], base)
+        cols = Columns(self.schema, X.shape[0], base)
+        mindex = self.__dict__.get("_mindex")
+        if mindex is None:
+            mindex = self._mindex = {name: j for j, name in enumerate(self.active_fields)}
+        cols.matrix, cols.mindex = X, mindex
+        return cols
 
     def evaluate_prepared(self, X: np.ndarray) -> tuple:
         """Oracle over a *prepared* matrix. Returns ``(ModelResult, outputs dict)``."""
