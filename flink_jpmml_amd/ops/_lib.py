@@ -139,7 +139,7 @@ class TreeArgs(ctypes.Structure):
                 ("chunk_trees_nan", c_int), ("xcd_split", c_int), ("tree_w", c_void_p), ("acc_init", c_void_p),
                 ("feat_map", c_void_p), ("rows_wide", c_int), ("mode", c_int), ("n_stage", c_int), ("pilp", c_int),
                 ("prof", c_void_p), ("rank_thr", c_void_p), ("rank_cnt", c_void_p), ("rank_stride", c_int),
-                ("pad1", c_int)]
+                ("leaf_onehot", c_int)]
 
 
 class TextParseArgs(ctypes.Structure):

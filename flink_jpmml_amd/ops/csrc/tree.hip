@@ -215,7 +215,12 @@ __device__ __forceinline__ void pointer_walk(const TreeArgs& a) {
       if (GENERAL) {
         const int slot = a.tree_slot[t0 + i];
         const float* lp = a.leaves + (size_t)leaf * a.P;
-        if (a.P == 3) {
+        if (a.leaf_onehot) {
+          // a one-hot vote {class, weight}: one 8-byte gather and one slot update (the other
+          // slots' += 0 of the dense form change nothing: the accumulators are never -0)
+          const int2 lv = reinterpret_cast<const int2*>(a.leaves)[leaf];
+          accl[(slot + lv.x) * TB + tid] += __int_as_float(lv.y);
+        } else if (a.P == 3) {
           // the row's three payloads as ONE multi-dword gather (a loop over a runtime P issues
           // one 64-lane gather per class); per-slot sums keep the tree order
           const float v0 = lp[0], v1 = lp[1], v2 = lp[2];

@@ -72,7 +72,8 @@ struct TreeArgs {
   unsigned long long* prof;     // nullable: per-wave phase ticks of one workgroup ([16][4], s_memtime)
   const float* rank_thr;        // RANK3 pointer layout: per feature, its sorted unique split thresholds
   const int* rank_cnt;          // ... and their count (<= 254); row f of rank_thr starts at f * rank_stride
-  int rank_stride, pad1;
+  int rank_stride;
+  int leaf_onehot;               // pointer_walk GENERAL: leaves are {class, weight bits} int pairs (one-hot votes)
 };
 // One grouped launch of the wide kernel over a mixed-model slice (tree_grouped_wide_kernel).
 struct GroupedTreeArgs {

@@ -1310,10 +1310,11 @@ class TreePlan(DevicePlan):
                                   "rows_wide", "n_stage", "heads", "head_depth", "pointer_ilp", "xcd_split",
                                   "tail_format", "rank_thr", "rank_cnt", "rank_stride", "lds_chunks", "lds_slices",
                                   "lds_rows", "lds_chunk_u4", "lds_n_slices", "mix_mass", "mix_w", "mix_tab",
-                                  "mix_remap", "vcol")
+                                  "mix_remap", "vcol", "leaf_onehot")
 
     # GENERAL-layout extras (sibling mixtures, per-record leaf columns); None on every other layout
     mix_mass = mix_w = mix_tab = mix_remap = vcol = None
+    leaf_onehot = 0  # pointer walks of one-hot votes: leaves as {class, weight} pairs
 
     WIDE_G = 4  # tree groups of the wide kernel (mirrors csrc)
 
@@ -1680,6 +1681,18 @@ class TreePlan(DevicePlan):
             elif inline and self.variant == 0:
                 self.variant = VAR_POINTER_INLINE  # leaf payloads inline: no leaf gather
             self.blob = self._t(nodes.reshape(-1).view(np.int32))
+            self.leaf_onehot = 0
+            if (self.general and self.P > 1 and leaves.size and self.layout == "pointer"
+                    and (self.variant in (0, VAR_POINTER_MASKED, VAR_POINTER_USKIP, VAR_POINTER_PEEL, VAR_POINTER_LTOP))):
+                # votes: every leaf row has at most one non-zero payload -> {class, weight} pairs
+                # (pointer_walk reads one 8-byte pair and updates one slot instead of P)
+                L = np.asarray(leaves, dtype=np.float32).reshape(len(leaves), -1)
+                nz = L != 0
+                if (nz.sum(axis=1) <= 1).all():
+                    cls = np.where(nz.any(axis=1), nz.argmax(axis=1), 0).astype(np.int32)
+                    w = L[np.arange(len(L)), cls].astype(np.float32)
+                    leaves = np.stack([cls, w.view(np.int32)], axis=1).view(np.float32)
+                    self.leaf_onehot = 1
             self.leaves = self._t(leaves.reshape(-1))
             self.roots = self._t(roots)
             self.heads = self._t(heads.reshape(-1).view(np.int32)) if heads is not None else None
@@ -1847,6 +1860,7 @@ class TreePlan(DevicePlan):
             a.prof = ptr(getattr(self, "prof", None))  # kbench --tree-prof phase timers (nullable)
             a.rank_thr, a.rank_cnt = ptr(getattr(self, "rank_thr", None)), ptr(getattr(self, "rank_cnt", None))
             a.rank_stride = int(getattr(self, "rank_stride", 0) or 0)
+            a.leaf_onehot = int(getattr(self, "leaf_onehot", 0) or 0)
             a.epi = _epilogue(table=self.table, write_probs=with_probs, **self.epi_args)
             cache[with_probs] = a
         # one mutable copy per thread, reused across launches: the C launcher copies the struct
