@@ -74,9 +74,67 @@ class MiningEvaluator(ModelEvaluator):
             self._native = prog
         return prog
 
+    def native_vote(self):
+        """``(ForestProgram, class table, node offsets, weights)`` when this is a (weighted)
+        majority vote over plain classification trees (True segment predicates, no outputs / local
+        transformations, no mixture missing strategies): the whole vote is then one native leaf
+        walk plus a bincount, instead of one Python tree evaluation per segment. None otherwise."""
+        vote = getattr(self, "_native_vote", False)
+        if vote is False:
+            vote = None
+            from .tree import TreeEvaluator
+
+            if self.kind == "classification" and self.method in ("majorityVote", "weightedMajorityVote") and self.sub \
+                    and all(isinstance(seg.predicate, ir.TruePredicate) and type(ev) is TreeEvaluator
+                            and ev.kind == "classification" and not ev.model.output
+                            and not ev.model.local_transformations and not getattr(ev, "value_fields", None)
+                            and ev.tree.missing_value_strategy not in ("weightedConfidence", "aggregateNodes")
+                            for seg, ev in zip(self.segments, self.sub)):
+                from .native_tree import forest_program
+
+                cats = self.categories
+                tabs, offs, off = [], [], 0
+                for ev in self.sub:
+                    idx_map = np.array([cats.index(c) for c in ev.categories], dtype=np.int64)
+                    lab = np.asarray(ev.node_label, dtype=np.float64)
+                    ok = ~np.isnan(lab)
+                    tabs.append(np.where(ok, idx_map[np.where(ok, lab, 0).astype(np.int64)], -1))
+                    offs.append(off)
+                    off += len(lab)
+                prog = forest_program(self.sub, [np.zeros(len(ev.node_label)) for ev in self.sub])
+                if prog is not None:
+                    vote = (prog, np.concatenate(tabs).astype(np.int64), np.asarray(offs, dtype=np.int64),
+                            np.asarray(self.weights, dtype=np.float64))
+            self._native_vote = vote
+        return vote
+
+    def _vote_native(self, L: np.ndarray, glab: np.ndarray, offs: np.ndarray, w: np.ndarray) -> ModelResult:
+        """``_classify`` for a (weighted) majority vote from the ``[T, n]`` leaf matrix: the same
+        per-(row, class) additions in tree order (bincount over the tree-major entries), so the
+        vote shares are bit-identical to the per-segment loop."""
+        T, n = L.shape
+        C = len(self.categories)
+        G = np.where(L >= 0, L + offs[:, None], -1)
+        lab = np.where(G >= 0, glab[np.maximum(G, 0)], -1)
+        use = lab >= 0
+        ww = w if self.method == "weightedMajorityVote" else np.ones(T)
+        rows = np.broadcast_to(np.arange(n, dtype=np.int64), (T, n))
+        wts = np.broadcast_to(ww[:, None], (T, n))[use]
+        acc = np.bincount((rows * C + lab)[use], weights=wts, minlength=n * C).reshape(n, C)
+        wsum = np.bincount(rows[use], weights=wts, minlength=n)
+        return self._class_result(acc, wsum, use.sum(axis=0), ~use.all(axis=0))
+
     def _evaluate(self, cols: Columns) -> ModelResult:
         n = cols.n
         method = self.method
+        vote = self.native_vote() if n else None
+        if vote is not None:
+            try:
+                X = vote[0].matrix(cols)
+            except Exception:  # noqa: BLE001 - a field the segments reference cannot be prepared
+                X = None
+            if X is not None:
+                return self._vote_native(vote[0].leaves(X), *vote[1:])
         prog = self.native_forest() if n else None
         if prog is not None:
             try:
@@ -251,6 +309,10 @@ class MiningEvaluator(ModelEvaluator):
                 P[~(a & r.valid)] = NAN
                 stack.append(P)
             acc = np.nanmedian(np.stack(stack, axis=0), axis=0)
+        return self._class_result(acc, wsum, count, anymiss)
+
+    def _class_result(self, acc: np.ndarray, wsum: np.ndarray, count: np.ndarray, anymiss: np.ndarray) -> ModelResult:
+        method, cats = self.method, self.categories
         with np.errstate(invalid="ignore", divide="ignore"):
             if method in ("majorityVote", "weightedMajorityVote", "average", "weightedAverage"):
                 probs = acc / wsum[:, None]

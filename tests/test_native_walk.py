@@ -308,3 +308,36 @@ def test_thread_count_does_not_change_results():
         fastpath().set_walk_threads(1)
     for a, b in zip(one, six):
         np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("missing", ["defaultChild", "nullPrediction", "lastPrediction"])
+@pytest.mark.parametrize("weighted", [False, True])
+def test_native_majority_vote_equals_segment_loop(missing, weighted):
+    """The native vote (one leaf walk + tree-order bincount) gives the per-segment ``_classify``
+    loop's labels, validity and vote shares bit for bit."""
+    from flink_jpmml_amd.bench import synth
+
+    doc = synth.random_forest_pmml(n_trees=40, depth=7, n_features=10, n_classes=4, seed=3,
+                                   missing_strategy=missing if missing != "lastPrediction" else "defaultChild")
+    if missing == "lastPrediction":
+        doc = doc.replace('missingValueStrategy="defaultChild"', 'missingValueStrategy="lastPrediction"')
+    if weighted:
+        doc = doc.replace('multipleModelMethod="majorityVote"', 'multipleModelMethod="weightedMajorityVote"')
+        k = [0]
+
+        def _w(m):
+            k[0] += 1
+            return f'<Segment id="{m.group(1)}" weight="{0.25 + (k[0] % 7) * 0.375}"'
+        import re
+        doc = re.sub(r'<Segment id="([^"]+)"', _w, doc)
+    c = CompiledPmml.from_string(doc)
+    ev = c.evaluator
+    assert ev.native_vote() is not None
+    X = synth.stream_matrix(3000, 10, seed=4, missing_rate=0.15)
+    res_native = ev.evaluate(c.columns(c.prepare(X)[0]))
+    ev._native_vote = None  # the per-segment loop
+    res_loop = ev.evaluate(c.columns(c.prepare(X)[0]))
+    np.testing.assert_array_equal(res_native.valid, res_loop.valid)
+    np.testing.assert_array_equal(res_native.value, res_loop.value)
+    np.testing.assert_array_equal(res_native.probs, res_loop.probs)
+    assert res_native.valid.any() and (not res_native.valid.all() or missing == "defaultChild")
