@@ -103,8 +103,13 @@ class MiningEvaluator(ModelEvaluator):
                     off += len(lab)
                 prog = forest_program(self.sub, [np.zeros(len(ev.node_label)) for ev in self.sub])
                 if prog is not None:
+                    # the class of every node in the program's global numbering (tree t at roots[t])
+                    roots = np.asarray(prog.roots, dtype=np.int64)
+                    gcls = np.full(int(sum(len(t) for t in tabs)), -1, dtype=np.int32)
+                    for t, tab in enumerate(tabs):
+                        gcls[roots[t]:roots[t] + len(tab)] = tab
                     vote = (prog, np.concatenate(tabs).astype(np.int64), np.asarray(offs, dtype=np.int64),
-                            np.asarray(self.weights, dtype=np.float64))
+                            np.asarray(self.weights, dtype=np.float64), gcls)
             self._native_vote = vote
         return vote
 
@@ -134,7 +139,14 @@ class MiningEvaluator(ModelEvaluator):
             except Exception:  # noqa: BLE001 - a field the segments reference cannot be prepared
                 X = None
             if X is not None:
-                return self._vote_native(vote[0].leaves(X), *vote[1:])
+                prog, glab, offs, w, gcls = vote
+                ww = w if method == "weightedMajorityVote" else np.ones(len(w))
+                from ..native import fastpath
+
+                if hasattr(fastpath(), "forest_votes"):
+                    acc, wsum, count, anymiss = prog.votes(X, gcls, ww, len(self.categories))
+                    return self._class_result(acc, wsum, count, anymiss)
+                return self._vote_native(prog.leaves(X), glab, offs, w)  # (an older _fastpath build)
         prog = self.native_forest() if n else None
         if prog is not None:
             try:

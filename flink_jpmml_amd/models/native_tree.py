@@ -314,6 +314,26 @@ class ForestProgram:
         return out
 
 
+    def votes(self, X: np.ndarray, cls: np.ndarray, weights: np.ndarray, C: int):
+        """A (weighted) majority vote in one native call: ``(acc [n, C], wsum [n], count [n],
+        anymiss [n])`` -- ``acc[r, cls[node]] += weights[t]`` for every tree whose scoring node has
+        a class (``cls`` indexed by the program's global node ids, -1 = none), in tree order."""
+        from ..native import fastpath
+
+        fp = fastpath()
+        X = np.ascontiguousarray(X, dtype=np.float64)
+        ni, nd, kids, pi, pd, ai, ad, roots, modes, _ = self.arrays()
+        n = X.shape[0]
+        acc = np.empty((n, C), dtype=np.float64)
+        wsum = np.empty(n, dtype=np.float64)
+        count = np.empty(n, dtype=np.int32)
+        miss = np.empty(n, dtype=np.uint8)
+        fp.forest_votes(ni, nd, kids, pi, pd, ai, ad, roots, modes, X, X.shape[1],
+                        np.ascontiguousarray(cls, dtype=np.int32), np.ascontiguousarray(weights, dtype=np.float64),
+                        int(C), acc, wsum, count, miss, self.compiled())
+        return acc, wsum, count, miss.astype(bool)
+
+
 def native_available() -> bool:
     from ..native import fastpath
 

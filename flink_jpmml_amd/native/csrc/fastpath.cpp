@@ -12,7 +12,8 @@
 //                       EmptyScore prediction. Objects are allocated with tp_alloc and their slots
 //                       filled directly (the Python __init__s only assign those same slots).
 //   * scan_trees      — the streaming TreeModel reader of large PMML documents (pmml_scan.cpp).
-//   * forest_leaves / forest_values / forest_sums — the float64 oracle's tree walk in C++ (tree_walk.cpp).
+//   * forest_leaves / forest_values / forest_sums / forest_votes — the float64 oracle's tree walk in C++
+//     (tree_walk.cpp).
 //   * seq_affine      — the oracle's NeuralNetwork layer sums in connection order (nn_host.cpp).
 //
 // Both return None / -1 when an input does not have the exact expected shape; the Python caller
@@ -35,6 +36,7 @@ PyObject *fja_set_walk_threads(PyObject *, PyObject *args); // tree_walk.cpp
 PyObject *fja_forest_leaves(PyObject *, PyObject *args);  // tree_walk.cpp
 PyObject *fja_forest_values(PyObject *, PyObject *args);  // tree_walk.cpp
 PyObject *fja_forest_sums(PyObject *, PyObject *args);    // tree_walk.cpp
+PyObject *fja_forest_votes(PyObject *, PyObject *args);   // tree_walk.cpp
 PyObject *fja_seq_affine(PyObject *, PyObject *args);     // nn_host.cpp
 
 namespace {
@@ -285,6 +287,7 @@ PyMethodDef methods[] = {
     {"forest_leaves", fja_forest_leaves, METH_VARARGS, "Oracle tree walk: scoring node per tree and row."},
     {"forest_values", fja_forest_values, METH_VARARGS, "Oracle tree walk: leaf value per row and tree."},
     {"forest_sums", fja_forest_sums, METH_VARARGS, "Oracle tree walk: numpy-pairwise ensemble sum per row."},
+    {"forest_votes", fja_forest_votes, METH_VARARGS, "Oracle tree walk: (weighted) majority vote shares per row."},
     {"seq_affine", fja_seq_affine, METH_VARARGS, "Oracle NeuralNetwork layer: bias + sum in connection order."},
     {nullptr, nullptr, 0, nullptr},
 };

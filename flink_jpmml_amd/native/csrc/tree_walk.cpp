@@ -352,21 +352,26 @@ struct Buf {
 
 constexpr Py_ssize_t ROW_BLOCK = 256;
 
-enum class Kind { LEAVES, VALUES, SUMS };
+enum class Kind { LEAVES, VALUES, SUMS, VOTES };
 
 // Common front half of the entry points: parse + validate the program and the input matrix.
 struct Call {
     Buf ni, nd, kids, pi, pd, ai, ad, roots, modes, X, out, leafval, weights;
+    Buf cls, wsum, cnt, miss;  // VOTES: node -> class table and the per-row outputs
     Program prog{};
-    Py_ssize_t T = 0, n = 0, k = 0;
+    Py_ssize_t T = 0, n = 0, k = 0, C = 0;
     bool has_weights = false;
 
     PyObject *cache = Py_None;  // forest_compile's capsule of this program, or None
 
     bool parse(PyObject *args, Kind kind) {
-        PyObject *o[14] = {};
+        PyObject *o[18] = {};
         bool okp;
-        if (kind == Kind::LEAVES)
+        if (kind == Kind::VOTES)
+            okp = PyArg_ParseTuple(args, "OOOOOOOOOOnOOnOOOO|O", &o[0], &o[1], &o[2], &o[3], &o[4], &o[5], &o[6],
+                                   &o[7], &o[8], &o[9], &k, &o[11], &o[12], &C, &o[13], &o[14], &o[15], &o[16],
+                                   &cache);
+        else if (kind == Kind::LEAVES)
             okp = PyArg_ParseTuple(args, "OOOOOOOOOOnO|O", &o[0], &o[1], &o[2], &o[3], &o[4], &o[5], &o[6], &o[7],
                                    &o[8], &o[9], &k, &o[11], &cache);
         else if (kind == Kind::VALUES)
@@ -382,7 +387,13 @@ struct Call {
             !ad.get(o[6], "d", 8, false, "aux_d") || !roots.get(o[7], "i", 4, false, "roots") ||
             !modes.get(o[8], "i", 4, false, "modes") || !X.get(o[9], "d", 8, false, "X"))
             return false;
-        if (kind == Kind::LEAVES) {
+        if (kind == Kind::VOTES) {
+            if (!cls.get(o[11], "i", 4, false, "cls") || !weights.get(o[12], "d", 8, false, "weights") ||
+                !out.get(o[13], "d", 8, true, "acc") || !wsum.get(o[14], "d", 8, true, "wsum") ||
+                !cnt.get(o[15], "i", 4, true, "count") || !miss.get(o[16], "B", 1, true, "anymiss"))
+                return false;
+            has_weights = true;
+        } else if (kind == Kind::LEAVES) {
             if (!out.get(o[11], "i", 4, true, "out")) return false;
         } else if (kind == Kind::VALUES) {
             if (!leafval.get(o[11], "d", 8, false, "leafval") || !out.get(o[12], "d", 8, true, "out")) return false;
@@ -404,6 +415,20 @@ struct Call {
             return false;
         }
         n = X.n() / k;
+        if (kind == Kind::VOTES) {
+            if (C < 1 || cls.n() != prog.n_nodes || weights.n() != T || out.n() != n * C || wsum.n() != n ||
+                cnt.n() != n || miss.n() != n) {
+                PyErr_SetString(PyExc_ValueError, "tree walk: vote table / output shape mismatch");
+                return false;
+            }
+            const int32_t *ct = static_cast<const int32_t *>(cls.b.buf);
+            for (Py_ssize_t i = 0; i < prog.n_nodes; ++i)
+                if (ct[i] < -1 || ct[i] >= C) {
+                    PyErr_SetString(PyExc_ValueError, "tree walk: vote class out of range");
+                    return false;
+                }
+            return cache_matches() || validate();
+        }
         const Py_ssize_t want = kind == Kind::SUMS ? n : T * n;
         if (out.n() != want || (kind != Kind::LEAVES && leafval.n() != prog.n_nodes) ||
             (has_weights && weights.n() != T)) {
@@ -960,6 +985,50 @@ PyObject *forest_sums(PyObject *, PyObject *args) {
     Py_RETURN_NONE;
 }
 
+// forest_votes(..., X, k, cls int32 [n_nodes] (class of a scoring node, -1 = no score), weights f64 [T],
+// C, acc f64 [n, C], wsum f64 [n], count int32 [n], anymiss u8 [n]): a (weighted) majority vote --
+// acc[r, cls] += w[t] and wsum[r] += w[t] for every tree with a class, in tree order per row (the
+// additions of MiningEvaluator._classify / _vote_native), count = such trees, anymiss = some tree
+// without one. Outputs are overwritten.
+PyObject *forest_votes(PyObject *, PyObject *args) {
+    Call c;
+    if (!c.parse(args, Kind::VOTES)) return nullptr;
+    const double *X = static_cast<const double *>(c.X.b.buf);
+    const int32_t *ct = static_cast<const int32_t *>(c.cls.b.buf);
+    const double *w = static_cast<const double *>(c.weights.b.buf);
+    double *acc = static_cast<double *>(c.out.b.buf);
+    double *ws = static_cast<double *>(c.wsum.b.buf);
+    int32_t *cnt = static_cast<int32_t *>(c.cnt.b.buf);
+    uint8_t *miss = static_cast<uint8_t *>(c.miss.b.buf);
+    const Py_ssize_t n = c.n, C = c.C;
+    const bool avx = use_avx512(c);
+    const Fixed *fc = cached_fixed(c);
+    Py_BEGIN_ALLOW_THREADS
+    Fixed local;
+    if (fc == nullptr) compile_all(c, local);
+    const Fixed &f = fc ? *fc : local;
+    for_blocks(n, [&](Py_ssize_t r0, Py_ssize_t r1, int) {
+        for (Py_ssize_t r = r0; r < r1; ++r) {
+            for (Py_ssize_t j = 0; j < C; ++j) acc[r * C + j] = 0.0;
+            ws[r] = 0.0;
+            cnt[r] = 0;
+            miss[r] = 0;
+        }
+        run_block(c, f, X, r0, r1, avx, [&](Py_ssize_t t, Py_ssize_t r, int32_t g) {
+            const int32_t k = g < 0 ? -1 : ct[g];
+            if (k < 0) {
+                miss[r] = 1;
+                return;
+            }
+            acc[r * C + k] += w[t];
+            ws[r] += w[t];
+            ++cnt[r];
+        });
+    });
+    Py_END_ALLOW_THREADS
+    Py_RETURN_NONE;
+}
+
 // forest_compile(nodes_i, nodes_d, kids, preds_i, preds_d, aux_i, aux_d, roots, modes, k) -> capsule
 PyObject *forest_compile(PyObject *, PyObject *args) {
     PyObject *o[9];
@@ -1014,3 +1083,4 @@ PyObject *fja_set_walk_threads(PyObject *self, PyObject *args) { return set_walk
 PyObject *fja_forest_leaves(PyObject *self, PyObject *args) { return forest_leaves(self, args); }
 PyObject *fja_forest_values(PyObject *self, PyObject *args) { return forest_values(self, args); }
 PyObject *fja_forest_sums(PyObject *self, PyObject *args) { return forest_sums(self, args); }
+PyObject *fja_forest_votes(PyObject *self, PyObject *args) { return forest_votes(self, args); }

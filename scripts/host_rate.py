@@ -27,4 +27,12 @@ t = time.perf_counter()
 for v in vecs:
     m.predict(v)
 rec = len(vecs) / (time.perf_counter() - t)
-print(json.dumps({"host_batch_records_per_s": batch, "host_per_record_predict_per_s": rec, "host_predict_batch_per_s": pbatch, "trees": 1000, "depth": 6}))
+from flink_jpmml_amd.bench.synth import random_forest_pmml  # noqa: E402
+
+rf = CompiledPmml.from_string(random_forest_pmml(n_trees=500, depth=8, n_features=32, n_classes=3, seed=0))
+rf.score_matrix_oracle(X[:64])
+t = time.perf_counter()
+rf.score_matrix_oracle(X)
+rf_batch = len(X) / (time.perf_counter() - t)
+print(json.dumps({"host_batch_records_per_s": batch, "host_per_record_predict_per_s": rec, "host_predict_batch_per_s": pbatch, "trees": 1000, "depth": 6,
+                  "rf500x8_host_batch_records_per_s": rf_batch}))

@@ -335,9 +335,16 @@ def test_native_majority_vote_equals_segment_loop(missing, weighted):
     assert ev.native_vote() is not None
     X = synth.stream_matrix(3000, 10, seed=4, missing_rate=0.15)
     res_native = ev.evaluate(c.columns(c.prepare(X)[0]))
+    prog, glab, offs, w, _ = ev.native_vote()
+    L = prog.leaves(prog.matrix(c.columns(c.prepare(X)[0])))
+    res_np = ev._vote_native(L, glab, offs, w)  # the numpy form of the same vote
     ev._native_vote = None  # the per-segment loop
     res_loop = ev.evaluate(c.columns(c.prepare(X)[0]))
     np.testing.assert_array_equal(res_native.valid, res_loop.valid)
     np.testing.assert_array_equal(res_native.value, res_loop.value)
     np.testing.assert_array_equal(res_native.probs, res_loop.probs)
+    for r in (res_np,):
+        np.testing.assert_array_equal(r.valid, res_loop.valid)
+        np.testing.assert_array_equal(r.value, res_loop.value)
+        np.testing.assert_array_equal(r.probs, res_loop.probs)
     assert res_native.valid.any() and (not res_native.valid.all() or missing == "defaultChild")
