@@ -1,6 +1,5 @@
 set -o pipefail
 # r6aa: final validation after the one-hot leaf pairs and the native vote oracle: host rates (GBDT + RF), default GPU suite, smoke, bench N=1.
-# single-record walk); default GPU suite; smoke; bench N=1.
 O=gpurun_out/r6aa
 mkdir -p $O
 export HSA_ENABLE_IPC_MODE_LEGACY=0
