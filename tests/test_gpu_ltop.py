@@ -60,3 +60,26 @@ def test_ltop_walk_equals_clamped_walk_and_oracle(gpu, case):
         np.testing.assert_allclose(s[v], ref[v], rtol=0, atol=5e-5)
     else:
         np.testing.assert_array_equal(s[v], ref[v])
+
+
+@pytest.mark.parametrize("opts", [dict(xcd_split="on"), dict(splits=3)], ids=["xcd", "splits3"])
+@pytest.mark.parametrize("kind", ["gbdt", "rf"])
+def test_ltop_walk_with_tree_splits(gpu, opts, kind):
+    """Tree slices per workgroup (XCD-aware slices, grid.y splits + the split reduction): every
+    slice stages its own groups' top levels."""
+    from flink_jpmml_amd.runtime.plans import VAR_POINTER_LTOP
+
+    if kind == "gbdt":
+        doc = gbdt_pmml(n_trees=70, depth=13, n_features=20, seed=5, p_split=0.8)
+    else:
+        doc = random_forest_pmml(n_trees=45, depth=13, n_features=20, n_classes=3, seed=5, p_split=0.8)
+    c = CompiledPmml.from_string(doc)
+    plan = c.plan(gpu, layout="pointer", **opts)
+    ref_plan = c.plan(gpu, layout="pointer", pointer_load="clamped", **opts)
+    assert plan.variant == VAR_POINTER_LTOP
+    X = stream_matrix(12_345, 20, seed=6, missing_rate=0.03)
+    s, v = _scores(plan, X)
+    s0, v0 = _scores(ref_plan, X)
+    assert (v == v0).all() and np.array_equal(s[v], s0[v0])
+    ref, vref = c.score_matrix_oracle(X)
+    assert (v == vref).all()
