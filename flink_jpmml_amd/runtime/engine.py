@@ -487,7 +487,13 @@ class StreamingScorer:
         cs = self.comp.cuda_stream
         check(self._lib.pmml_memcpy_async(st["xd"].data_ptr(), st["xh"].data_ptr(), self.F * 4, 1, cs), "row H2D")
         g = self._graphs
-        if st["hs"] is not None:
+        run = st.get("run", False)
+        if run is False:  # the plan's prepared launch over these fixed buffers, when it has one
+            rl = getattr(self.plan, "row_launcher", None)
+            run = st["run"] = rl(st["xd"], st["hs"], st["hv"]) if (rl is not None and st["hs"] is not None) else None
+        if run is not None:
+            run(self.comp)
+        elif st["hs"] is not None:
             self.plan.launch(st["xd"], st["hs"], st["hv"], stream=self.comp)
         else:
             if g is not None and g.applies(1, {}):

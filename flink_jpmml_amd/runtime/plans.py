@@ -1945,6 +1945,44 @@ class TreePlan(DevicePlan):
         check(rc, f"tree kernel ({self.layout}, depth {self.depth})")
 
 
+    def row_launcher(self, X, score, valid):
+        """A launch of this plan over FIXED buffers (``StreamingScorer.score_row``'s persistent
+        row): the argument block (and the split partials) are built once, and each call only hands
+        the block to the C launcher -- the per-call Python of :meth:`launch` was a third of a
+        per-record predict. None for the layouts with launchers of their own."""
+        if self.layout not in ("perfect", "pointer") or self.variant & VAR_POINTER_LDS or X.shape[1] == 0:
+            return None
+        import ctypes
+
+        import torch
+
+        from ..ops._lib import TreeArgs, check, stream_handle
+
+        n = X.shape[0]
+        s = self._auto_splits(n)
+        a = TreeArgs()
+        ctypes.memmove(ctypes.byref(a), ctypes.byref(self._args_template(False)), ctypes.sizeof(TreeArgs))
+        a.X = X.data_ptr()
+        a.n_rows, a.n_feat, a.ldx = n, X.shape[1], X.stride(0)
+        a.row_valid_in = None
+        a.score, a.valid, a.probs = _addr(score), _addr(valid), None
+        a.epi.score2, a.epi.valid2 = None, None
+        a.partial = None
+        a.xcd_split = 1 if getattr(self, "xcd_split", 0) and s > 1 else 0
+        partial = None
+        if s > 1:
+            partial = torch.empty(max(s * (self.C + 1) * n, 1), dtype=torch.float32, device=self.device)
+            a.partial = partial.data_ptr()
+        lib, layout = self.lib, 0 if self.layout == "perfect" else 1
+        depth, dr = self.depth, 1 if self.has_dr else 0
+
+        def run(stream) -> None:
+            check(lib.pmml_tree_launch(stream_handle(stream), ctypes.byref(a), layout, depth, dr, s),
+                  f"tree kernel ({self.layout}, depth {depth}, row)")
+
+        run.keep = (a, partial, X)  # the block and the buffers it points at live as long as run
+        return run
+
     def batch_launch_args(self, x_ptr: int, n: int, n_feat: int, ldx: int, score_ptr: int, valid_ptr: int):
         """``(TreeArgs, (layout, depth, has_dr, splits))`` of one launch over rows at ``x_ptr``,
         for ``pmml_tree_launch_many`` (several models' launches from one host call), or ``None``
